@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""
+tests/golden/gen_golden.py -- regenerates the committed golden vectors.
+
+Runs ONLY in the dev container (needs /root/reference); the vectors it writes
+(tests/golden/*.json) are data: inputs and the outputs the reference code
+itself produced for them.  Sections:
+
+  gotoh    every _gotoh2.align call made by the reference's own KATs
+           (micall/alignment/tests/test.py) plus seeded random pairs, all
+           answered by the reference extension built from its source.
+  pileup   every remap.sam_to_conseqs call made by micall/tests/remap_test.py
+           (recorded around the real function, so the expected value is what
+           the code returns, not the test's stale expectation -- see
+           SURVEY.md 4, testSeedsConvergedWithConfusingGap) plus synthetic
+           SAMs produced by the oracle mapper on synthetic reads.
+  sam2aln  every apply_cigar / merge_pairs / merge_inserts call made by
+           micall/tests/sam2aln_test.py.
+
+usage: python tests/golden/gen_golden.py [gotoh] [pileup] [sam2aln]
+"""
+import io
+import json
+import os
+import random
+import sys
+import unittest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(REPO, 'oracle'))
+sys.path.insert(0, os.path.join(REPO, 'micall-lite_amd'))
+
+import refharness  # noqa: E402
+
+
+def _run_suite(module):
+    suite = unittest.defaultTestLoader.loadTestsFromModule(module)
+    unittest.TextTestRunner(stream=io.StringIO(), verbosity=0).run(suite)
+
+
+def gen_gotoh():
+    refmod = refharness.setup()
+    records = []
+    real_align = refmod.align
+
+    class Recorder:
+        @staticmethod
+        def align(s1, s2, gop, gep, is_global, alphabet, matrix):
+            matrix = list(matrix)
+            rec = dict(seq1=s1, seq2=s2, gop=gop, gep=gep, is_global=is_global,
+                       alphabet=alphabet, matrix=matrix)
+            try:
+                a1, a2, score = real_align(s1, s2, gop, gep, is_global, alphabet, matrix)
+                rec.update(aligned1=a1, aligned2=a2, score=score, error=None)
+            except RuntimeError as ex:
+                rec.update(error=str(ex))
+                records.append(rec)
+                raise
+            records.append(rec)
+            return a1, a2, score
+
+    import micall.alignment.gotoh2 as g2
+    g2._gotoh2 = Recorder
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        'ref_alignment_kats', os.path.join(refharness.REF, 'micall', 'alignment', 'tests', 'test.py'))
+    kat = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(kat)
+    _run_suite(kat)
+    n_kat = len(records)
+
+    # seeded random pairs: nucleotide (HYPHY_NUC, global gop15/gep3 as in
+    # remap.py:33 and ends-free) and amino (EmpHIV25 gop40/gep10 ends-free as
+    # in aln2counts), including mutated copies so alignments are non-trivial.
+    rng = random.Random(20261015)
+    nuc = g2.Aligner(gop=15, gep=3, is_global=True, model='HYPHY_NUC')
+    amino = g2.Aligner(gop=40, gep=10, is_global=False, model='EmpHIV25')
+
+    def mutate(s, alpha, rate):
+        out = []
+        for c in s:
+            r = rng.random()
+            if r < rate:
+                out.append(rng.choice(alpha))
+            elif r < rate * 1.4:
+                continue
+            elif r < rate * 1.8:
+                out.append(c + ''.join(rng.choice(alpha) for _ in range(rng.choice([1, 3]))))
+            else:
+                out.append(c)
+        return ''.join(out) or alpha[0]
+
+    for k in range(160):
+        n = rng.choice([1, 2, 5, 17, 40, 97, 150, 300])
+        a = ''.join(rng.choice('ACGT') for _ in range(n))
+        b = mutate(a, 'ACGTN', rng.choice([0.05, 0.15, 0.3]))
+        if rng.random() < 0.3:
+            b = b[rng.randrange(len(b)):] or b
+        nuc.is_global = (k % 2 == 0)
+        nuc.gap_open_penalty = rng.choice([15, 10, 5])
+        nuc.gap_extend_penalty = rng.choice([3, 1])
+        try:
+            nuc.align(a, b)
+        except RuntimeError:
+            pass
+    for k in range(40):
+        n = rng.choice([3, 10, 33, 80])
+        a = ''.join(rng.choice('ARNDCQEGHILKMFPSTWYV') for _ in range(n))
+        b = mutate(a, 'ARNDCQEGHILKMFPSTWYV*', 0.2)
+        amino.is_global = (k % 3 == 0)
+        try:
+            amino.align(a, b)
+        except RuntimeError:
+            pass
+    out = dict(source='reference _gotoh2.c built by oracle/Makefile; KATs from '
+                      'micall/alignment/tests/test.py then seeded random pairs',
+               n_kat=n_kat, cases=records)
+    with open(os.path.join(HERE, 'gotoh_golden.json'), 'w') as f:
+        json.dump(out, f, indent=0)
+    print('gotoh: {} cases ({} from KATs)'.format(len(records), n_kat))
+
+
+def _synthetic_sams():
+    """SAM texts made by the oracle mapper on synthetic pol reads (local and
+    end-to-end), so the pileup vectors exercise soft clips, indels and
+    insertions the way the product sees them."""
+    import oracle
+    from micall_amd import synth, projects
+    seeds = projects.load_default().seed_sequences()
+    pol = seeds['HIV1B-pol-seed']
+    texts = []
+    for mode, n_pairs, seed in ((oracle.LOCAL, 300, 1), (oracle.E2E, 300, 2), (oracle.LOCAL, 60, 3)):
+        pairs = synth.make_pairs(n_pairs, genome_seed=seed, read_seed=seed + 100,
+                                 genomes={'HIV1B-pol-seed': pol}, indel_rate=0.01)
+        names, seqs, quals = synth.interleave(pairs)
+        refnames = ['HIV1B-pol-seed']
+        ix = oracle.Index([pol], oracle.seed_len(mode))
+        alns = oracle.map_reads(ix, oracle.params(mode), seqs, quals, True)
+        lines = ['@HD\tVN:1.0\tSO:unsorted\n', '@SQ\tSN:HIV1B-pol-seed\tLN:%d\n' % len(pol)]
+        for i in range(len(seqs)):
+            lines.append('\t'.join(oracle.sam_fields(alns[i], oracle.qname_of(names[i], True),
+                                                     seqs[i], quals[i], refnames)) + '\n')
+        texts.append((''.join(lines), {'seeds': {'HIV1B-pol-seed': pol}}))
+    return texts
+
+
+def gen_pileup():
+    refharness.setup()
+    from micall.core import remap
+    records = []
+    real = remap.sam_to_conseqs
+
+    def recorder(samfile, quality_cutoff=0, debug_reports=None, seeds=None, is_filtered=False,
+                 worker_pool=None, filter_coverage=1, distance_report=None):
+        text = samfile.getvalue() if hasattr(samfile, 'getvalue') else samfile.read()
+        result = real(io.StringIO(text), quality_cutoff, debug_reports, seeds, is_filtered,
+                      None, filter_coverage, distance_report)
+        if debug_reports is None:
+            records.append(dict(sam=text, quality_cutoff=quality_cutoff, seeds=seeds,
+                                is_filtered=is_filtered, filter_coverage=filter_coverage,
+                                conseqs=result,
+                                distance_report=distance_report))
+        return result
+
+    remap.sam_to_conseqs = recorder
+    import micall.tests.remap_test as rt
+    _run_suite(rt)
+    n_tests = len(records)
+    for text, extra in _synthetic_sams():
+        for q in (20, 0):
+            recorder(io.StringIO(text), quality_cutoff=q, seeds=extra['seeds'])
+        recorder(io.StringIO(text), quality_cutoff=20)
+    remap.sam_to_conseqs = real
+    out = dict(source='reference remap.sam_to_conseqs; remap_test.py calls then oracle-mapped '
+                      'synthetic SAMs', n_tests=n_tests, cases=records)
+    with open(os.path.join(HERE, 'pileup_golden.json'), 'w') as f:
+        json.dump(out, f, indent=0)
+    print('pileup: {} cases ({} from remap_test)'.format(len(records), n_tests))
+
+
+def gen_sam2aln():
+    refharness.setup()
+    from micall.core import sam2aln
+    records = []
+    originals = {}
+
+    def wrap(name):
+        fn = getattr(sam2aln, name)
+        originals[name] = fn
+
+        def recorder(*args, **kwargs):
+            rec = dict(fn=name, args=list(args), kwargs=kwargs)
+            try:
+                res = fn(*args, **kwargs)
+            except RuntimeError as ex:
+                rec['error'] = str(ex)
+                records.append(rec)
+                raise
+            rec['result'] = res
+            records.append(rec)
+            return res
+        setattr(sam2aln, name, recorder)
+
+    for name in ('apply_cigar', 'merge_pairs', 'merge_inserts'):
+        wrap(name)
+    import micall.tests.sam2aln_test as st
+    _run_suite(st)
+    for name, fn in originals.items():
+        setattr(sam2aln, name, fn)
+
+    def enc(x):
+        if isinstance(x, dict):
+            return {'__dict__': [[enc(k), enc(v)] for k, v in x.items()]}
+        if isinstance(x, (list, tuple)):
+            return [enc(v) for v in x]
+        return x
+    out = dict(source='reference sam2aln helpers as called by micall/tests/sam2aln_test.py',
+               cases=[enc(r) for r in records])
+    with open(os.path.join(HERE, 'sam2aln_golden.json'), 'w') as f:
+        json.dump(out, f, indent=0)
+    print('sam2aln: {} calls'.format(len(records)))
+
+
+if __name__ == '__main__':
+    which = sys.argv[1:] or ['gotoh', 'pileup', 'sam2aln']
+    for w in which:
+        globals()['gen_' + w]()
