@@ -1,0 +1,171 @@
+/*
+ * micall_hip.h -- C-ABI of libmicall_hip.so, the MI355X (gfx950) drop-in for
+ * MiCall-Lite's iterative remap hot path.
+ *
+ * The reference crosses two boundaries on this path; every entry point below
+ * replaces one of them (file:line into the reference):
+ *
+ *   1. the bowtie2 / bowtie2-build process boundary, reached through
+ *      micall/utils/externals.py:106-125 (CommandWrapper.yield_output) and
+ *      :185-203 (Bowtie2Build.build):
+ *        bowtie2-build-s ... -f <fasta> <template>   prelim_map.py:106,
+ *                                                    remap.py:695
+ *          -> mh_index_build
+ *        bowtie2 ... -1 R1 -2 R2 | -U R [--local]    prelim_map.py:134,
+ *                                                    remap.py:734
+ *          -> mh_reads_load / mh_reads_load_fastq (FASTQ ingest, once),
+ *             mh_map (one mapping pass), mh_alns_fetch / mh_format_rows
+ *             (the SAM lines bowtie2 would print), mh_map_counts (the
+ *             per-line tallies remap.py:743-755 and :485-515 make);
+ *   2. the pileup the reference runs in Python on the SAM text,
+ *      remap.py:141-306 (sam_to_conseqs -> merge_reads -> apply_cigar /
+ *      merge_pairs / merge_inserts -> update_counts)
+ *          -> mh_rows_load (SAM rows read back from prelim.csv),
+ *             mh_pileup, mh_pileup_fetch / mh_pileup_events,
+ *             mh_pileup_export / mh_pileup_import (RCCL all-reduce between
+ *             ranks, done by the caller on device buffers);
+ *   3. the _gotoh2 C-extension boundary, micall/alignment/src/_gotoh2.c:544-607
+ *      (align_wrapper, "ssiiisO")
+ *          -> mh_gotoh_align.
+ *
+ * Conventions: every function returns 0 on success, -1 on traceback failure
+ * (mh_gotoh_align only), -2 on out-of-memory, -3 on a bad argument, -4 on a
+ * HIP runtime error, -5 when the HIP device or kernels are unavailable.
+ * mh_last_error() describes the last failure of the calling thread.  No C++
+ * exception and no exit() crosses this boundary.  All host buffers are owned
+ * by the caller; device buffers are owned by the context.  One context per
+ * device; calls on one context are not thread-safe, calls on different
+ * contexts are independent (ctypes releases the GIL around each call).
+ */
+#ifndef MICALL_HIP_H
+#define MICALL_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MH_MAXOPS 128
+
+enum { MH_E2E = 0, MH_LOCAL = 1 };          /* bowtie2 default / --local */
+enum { MH_OP_M = 0, MH_OP_I = 1, MH_OP_D = 2, MH_OP_S = 4 };
+
+/* Scoring knobs MiCall passes to bowtie2 (prelim_map.py:27-30,114-131). */
+typedef struct {
+    int mode;                 /* MH_E2E (prelim_map) or MH_LOCAL (remap) */
+    int rdg_open, rdg_ext;    /* --rdg 10,3 */
+    int rfg_open, rfg_ext;    /* --rfg 10,3 */
+    int maxins;               /* -X 1200 */
+} mh_params;
+
+/* One SAM record of one read, fields as bowtie2 prints them.  Layout is
+ * identical to oracle/og_mapper.h og_aln. */
+typedef struct {
+    int32_t ref, pos, rev, score, secbest, flag, mapq, rnext, pnext, tlen;
+    int32_t sam_ref, sam_pos, xm, xo, xg, nm, ys, yt, yf, n_cigar;
+    uint32_t cigar[MH_MAXOPS];   /* (len << 4) | op */
+} mh_aln;
+
+typedef struct mh_ctx mh_ctx;
+
+int mh_version(void);
+int mh_last_error(char *buf, size_t cap);
+int mh_device_count(int *n);
+
+int mh_ctx_create(int device, mh_ctx **out);
+int mh_ctx_destroy(mh_ctx *ctx);
+int mh_ctx_sync(mh_ctx *ctx);
+/* the hipStream_t the context launches on (as an opaque handle) */
+int mh_ctx_stream(mh_ctx *ctx, void **stream);
+
+/* ---- reference set: replaces bowtie2-build ---------------------------- */
+int mh_index_build(mh_ctx *ctx, int n_refs, const char *const *seqs, int seedlen);
+
+/* ---- reads: replaces bowtie2's FASTQ input (-1/-2/-U) ------------------ */
+/* Reads back to back; paired: reads 2p and 2p+1 are mates 1 and 2.  Kept
+ * resident on the device (2-bit bases + N mask + qualities) across passes. */
+int mh_reads_load(mh_ctx *ctx, int64_t n_reads, int paired, const uint8_t *seq,
+                  const uint8_t *qual, const int64_t *offsets, const int32_t *lens);
+/* Parse (gzip or plain) FASTQ files and load them; path2 may be NULL.
+ * Keeps the read names (bowtie2 QNAME rules) for mh_format_rows. */
+int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64_t *n_reads);
+int mh_reads_count(mh_ctx *ctx, int64_t *n_reads, int *paired);
+
+/* ---- one mapping pass: replaces `bowtie2 [--local] ...` ---------------- */
+int mh_map(mh_ctx *ctx, const mh_params *par);
+int mh_alns_fetch(mh_ctx *ctx, int64_t first, int64_t n, mh_aln *out);
+/* Per-reference tallies of the last pass (n_refs entries each):
+ *   lines[r]     SAM lines with RNAME r           (prelim count, remap.py:494)
+ *   filtered[r]  mapped lines with a >50-base M run (remap.py:500-506)
+ *   mapped[r]    mapped lines with RNAME r        (new_counts, remap.py:755)
+ *   first_row[r] first line index with RNAME r, -1 if none
+ *   first_mapped[r] first mapped line with RNAME r (Counter order), -1 if none
+ * and *unmapped = unmapped lines (remap.py:743-753); star_lines = RNAME '*'. */
+int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mapped,
+                  int64_t *first_row, int64_t *first_mapped, int64_t *unmapped,
+                  int64_t *star_lines);
+/* The 20 int32 header fields of mh_aln (no CIGAR) for reads [first, first+n). */
+int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20);
+/* SAM text for reads order[first .. first+n) (order NULL: reads first ..
+ * first+n-1): style 0 = tab-separated SAM with
+ * optional tags, style 1 = the 11 CSV columns prelim.csv / remap.csv hold
+ * (csv.QUOTE_MINIMAL).  Needs names from mh_reads_load_fastq or
+ * mh_reads_set_names.  *used = bytes written; -2 if cap is too small. */
+int mh_reads_set_names(mh_ctx *ctx, int64_t n, const char *const *names);
+int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
+                   const char *const *refnames, char *buf, size_t cap, size_t *used);
+
+/* ---- pileup: replaces sam_to_conseqs' counting (remap.py:141-306) ------ */
+/* External SAM rows (e.g. prelim.csv read back, remap.py:474-498).
+ * units: n_units pairs of row indices as matchmaker (remap.py:853-889)
+ * yields them, -1 for a missing mate.  seq/qual as printed in SAM. */
+int mh_rows_load(mh_ctx *ctx, int64_t n_rows, const int32_t *flag, const int32_t *ref,
+                 const int32_t *pos, const int32_t *cigar_off, const int32_t *n_cigar,
+                 const uint32_t *cigar, const uint8_t *seq, const uint8_t *qual,
+                 const int64_t *offsets, const int32_t *lens, int64_t n_units,
+                 const int64_t *unit_rows);
+/* source 0 = alignments of the last mh_map (units = pairs / reads),
+ * source 1 = rows from mh_rows_load.  n_refs/ref_lens size the dense
+ * counters (positions 1..ref_lens[r] + MH_PILEUP_SLACK). */
+#define MH_PILEUP_SLACK 2048
+int mh_pileup(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *ref_lens);
+/* dense: n_refs x cap x 4 int32 counts of A,C,G,T at positions 1..cap;
+ * nflag/dflag: n_refs x cap bytes ('N' seen -> count -1, '-' seen -> -2);
+ * read_counts: merged pairs per ref; first_unit: first merged unit index
+ * per ref (-1 if none); max_pos: largest position touched per ref. */
+int mh_pileup_dims(mh_ctx *ctx, int *n_refs, int32_t *cap, int64_t *n_events,
+                   int64_t *event_bytes);
+int mh_pileup_fetch(mh_ctx *ctx, int32_t *dense, uint8_t *nflag, uint8_t *dflag,
+                    int64_t *read_counts, int64_t *first_unit, int32_t *max_pos);
+/* sparse tokens (base + insertion with len % 3 == 0): per event ref, pos
+ * and the token bytes at tok_off[e] .. tok_off[e] + tok_len[e] of pool. */
+int mh_pileup_events(mh_ctx *ctx, int32_t *ref, int32_t *pos, int32_t *tok_off,
+                     int32_t *tok_len, char *pool);
+/* Multi-GPU: copy the device counters to / from a caller-owned device
+ * buffer of `bytes` (>= mh_pileup_packed_bytes) so the caller can all-reduce
+ * them with RCCL (int32 sum; flags are 0/1 and are OR-ed by max-reduce of
+ * the second segment).  Layout: [dense | read_counts(int32)] summed, then
+ * [nflag|dflag as int32 | max_pos | -first_unit] max-reduced. */
+int mh_pileup_packed_bytes(mh_ctx *ctx, int64_t *sum_bytes, int64_t *max_bytes);
+int mh_pileup_export(mh_ctx *ctx, void *dev_sum, void *dev_max);
+/* as mh_pileup_export, with this rank's first unit index added to
+ * first_unit so the max-reduce yields the global refmap order */
+int mh_pileup_export_base(mh_ctx *ctx, int64_t unit_base, void *dev_sum, void *dev_max);
+int mh_pileup_import(mh_ctx *ctx, const void *dev_sum, const void *dev_max);
+
+/* ---- Gotoh: replaces _gotoh2.align (_gotoh2.c:544-607) ---------------- */
+/* seq1/seq2 already cleaned (gotoh2.py:70-72).  out1/out2 need
+ * strlen(seq1)+strlen(seq2)+1 bytes (cap). */
+int mh_gotoh_align(mh_ctx *ctx, const char *seq1, const char *seq2, int gop, int gep,
+                   int is_global, const char *alphabet, const int *matrix, char *out1,
+                   char *out2, int cap, int *score);
+
+/* Unit-cost edit distance (Levenshtein.distance, remap.py:250). */
+int mh_levenshtein(const char *a, const char *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,881 @@
+// mh_api.cpp -- host side of libmicall_hip.so: the extern "C" entry points of
+// include/micall_hip.h, context and device-memory management, the seed index
+// build (bowtie2-build's job), FASTQ ingest and SAM/CSV text emission.
+#include <zlib.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "mh_internal.h"
+
+namespace mh {
+
+static thread_local char g_err[1024];
+
+void set_error(const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int hip_fail(hipError_t e, const char *what)
+{
+    set_error("HIP error %d (%s) in %s", (int)e, hipGetErrorString(e), what);
+    return -4;
+}
+
+// ---- per-length tables, same formulas as oracle/og_mapper.c --------------
+static int seed_interval(int mode, int len)
+{
+    const double f = mode == MH_LOCAL ? 0.75 : 1.15;
+    int iv = (int)(1.0 + f * std::sqrt((double)len) + 0.5);
+    return iv < 1 ? 1 : iv;
+}
+
+static int min_score(int mode, int len)
+{
+    if (mode == MH_LOCAL) {
+        double v = 20.0 + 8.0 * std::log((double)(len > 0 ? len : 1));
+        long s = (long)v;
+        return (int)(s < 0 ? 0 : s);
+    }
+    long s = (long)(-0.6 + -0.6 * (double)len);
+    return (int)(s > 0 ? 0 : s);
+}
+
+static int n_ceil(int len) { return (int)(0.0 + 0.15 * (double)len); }
+
+static int prepare_len_tab(Ctx &c, int mode)
+{
+    if (c.len_tab && c.len_tab_mode == mode) return 0;
+    std::vector<int32_t> t(3 * (MAXLEN + 1));
+    for (int l = 0; l <= MAXLEN; ++l) {
+        t[l] = seed_interval(mode, l);
+        t[(MAXLEN + 1) + l] = min_score(mode, l);
+        t[2 * (MAXLEN + 1) + l] = n_ceil(l);
+    }
+    if (!c.len_tab) MH_HIP(hipMalloc(&c.len_tab, sizeof(int32_t) * t.size()));
+    MH_HIP(hipMemcpy(c.len_tab, t.data(), sizeof(int32_t) * t.size(), hipMemcpyHostToDevice));
+    c.len_tab_mode = mode;
+    return 0;
+}
+
+// ---- host copies of the reads (SAM SEQ/QUAL text) ------------------------
+struct HostReads {
+    std::vector<uint8_t> seq, qual;
+    std::vector<int64_t> off;
+    std::vector<int32_t> len;
+};
+
+struct CtxEx : Ctx {
+    HostReads host;
+    // index cache: large (fixed seed-set) indexes are kept by content signature
+    std::vector<DevIndex> cache;
+    std::vector<Rec> rec_cache;
+};
+
+static void free_index(DevIndex &ix)
+{
+    hipFree(ix.codes); hipFree(ix.ref_off); hipFree(ix.ref_len); hipFree(ix.hkey);
+    hipFree(ix.hstart); hipFree(ix.hcount); hipFree(ix.hits);
+    ix = DevIndex{};
+}
+
+static void free_reads(DevReads &r)
+{
+    hipFree(r.seq2); hipFree(r.nmask); hipFree(r.qual); hipFree(r.off); hipFree(r.len);
+    r = DevReads{};
+}
+
+static uint8_t code_of(char ch)
+{
+    switch (ch) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return 4;
+    }
+}
+
+static uint64_t signature(int n, const char *const *seqs, int seedlen)
+{
+    uint64_t h = 1469598103934665603ull ^ (uint64_t)seedlen;
+    for (int r = 0; r < n; ++r) {
+        for (const char *p = seqs[r]; *p; ++p) { h ^= (uint8_t)*p; h *= 1099511628211ull; }
+        h ^= 0xff; h *= 1099511628211ull;
+    }
+    return h ^ (uint64_t)n;
+}
+
+static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int seedlen)
+{
+    struct E { uint64_t key; int32_t ref, pos; };
+    std::vector<uint8_t> codes;
+    std::vector<int64_t> ref_off(n_refs);
+    std::vector<int32_t> ref_len(n_refs);
+    std::vector<E> ent;
+    for (int r = 0; r < n_refs; ++r) {
+        const int L = (int)std::strlen(seqs[r]);
+        ref_off[r] = (int64_t)codes.size();
+        ref_len[r] = L;
+        uint64_t key = 0;
+        int last_n = -1;
+        for (int p = 0; p < L; ++p) {
+            const uint8_t c = code_of(seqs[r][p]);
+            codes.push_back(c);
+            if (c > 3) last_n = p;
+            // little-endian 2-bit packing: base x of the window at bits 2x+1:2x
+            key = (key >> 2) | ((uint64_t)(c & 3) << (2 * (seedlen - 1)));
+            if (p >= seedlen - 1 && last_n <= p - seedlen) ent.push_back({key, r, p - seedlen + 1});
+        }
+    }
+    std::sort(ent.begin(), ent.end(), [](const E &a, const E &b) {
+        if (a.key != b.key) return a.key < b.key;
+        if (a.ref != b.ref) return a.ref < b.ref;
+        return a.pos < b.pos;
+    });
+    size_t nkeys = 0;
+    for (size_t i = 0; i < ent.size(); ++i) if (i == 0 || ent[i].key != ent[i - 1].key) ++nkeys;
+    uint64_t cap = 1024;
+    while (cap < 2 * nkeys) cap <<= 1;
+    std::vector<uint64_t> hkey(cap, HEMPTY);
+    std::vector<uint32_t> hstart(cap, 0), hcount(cap, 0);
+    std::vector<int2> hits(ent.size() ? ent.size() : 1);
+    for (size_t i = 0; i < ent.size();) {
+        size_t j = i + 1;
+        while (j < ent.size() && ent[j].key == ent[i].key) ++j;
+        uint64_t h = hash_key(ent[i].key) & (cap - 1);
+        while (hkey[h] != HEMPTY) h = (h + 1) & (cap - 1);
+        hkey[h] = ent[i].key;
+        hstart[h] = (uint32_t)i;
+        hcount[h] = (uint32_t)(j - i);
+        i = j;
+    }
+    for (size_t i = 0; i < ent.size(); ++i) hits[i] = make_int2(ent[i].ref, ent[i].pos);
+    ix.n_refs = n_refs;
+    ix.seedlen = seedlen;
+    ix.total = (int64_t)codes.size();
+    ix.hmask = cap - 1;
+    codes.resize(codes.size() + 64, 4);
+    MH_HIP(hipMalloc(&ix.codes, codes.size()));
+    MH_HIP(hipMalloc(&ix.ref_off, sizeof(int64_t) * (n_refs > 0 ? n_refs : 1)));
+    MH_HIP(hipMalloc(&ix.ref_len, sizeof(int32_t) * (n_refs > 0 ? n_refs : 1)));
+    MH_HIP(hipMalloc(&ix.hkey, sizeof(uint64_t) * cap));
+    MH_HIP(hipMalloc(&ix.hstart, sizeof(uint32_t) * cap));
+    MH_HIP(hipMalloc(&ix.hcount, sizeof(uint32_t) * cap));
+    MH_HIP(hipMalloc(&ix.hits, sizeof(int2) * hits.size()));
+    MH_HIP(hipMemcpy(ix.codes, codes.data(), codes.size(), hipMemcpyHostToDevice));
+    if (n_refs > 0) {
+        MH_HIP(hipMemcpy(ix.ref_off, ref_off.data(), sizeof(int64_t) * n_refs, hipMemcpyHostToDevice));
+        MH_HIP(hipMemcpy(ix.ref_len, ref_len.data(), sizeof(int32_t) * n_refs, hipMemcpyHostToDevice));
+    }
+    MH_HIP(hipMemcpy(ix.hkey, hkey.data(), sizeof(uint64_t) * cap, hipMemcpyHostToDevice));
+    MH_HIP(hipMemcpy(ix.hstart, hstart.data(), sizeof(uint32_t) * cap, hipMemcpyHostToDevice));
+    MH_HIP(hipMemcpy(ix.hcount, hcount.data(), sizeof(uint32_t) * cap, hipMemcpyHostToDevice));
+    MH_HIP(hipMemcpy(ix.hits, hits.data(), sizeof(int2) * hits.size(), hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int load_reads(CtxEx &c, DevReads &dst, HostReads &host, int64_t n, int paired,
+                      const uint8_t *seq, const uint8_t *qual, const int64_t *offsets,
+                      const int32_t *lens, bool keep_host)
+{
+    if (n < 0 || (paired && (n & 1))) { set_error("reads: bad count"); return -3; }
+    int max_len = 0;
+    int64_t src_total = 0;
+    for (int64_t r = 0; r < n; ++r) {
+        if (lens[r] < 0 || lens[r] > MAXLEN) {
+            set_error("reads: read %lld has length %d (max %d)", (long long)r, lens[r], MAXLEN);
+            return -3;
+        }
+        max_len = std::max(max_len, (int)lens[r]);
+        src_total = std::max(src_total, offsets[r] + lens[r]);
+    }
+    std::vector<int64_t> off(n > 0 ? n : 1);
+    int64_t total = 0;
+    for (int64_t r = 0; r < n; ++r) {
+        off[r] = total;
+        total += ((int64_t)lens[r] + 31) / 32 * 32;
+    }
+    free_reads(dst);
+    dst.n = n;
+    dst.paired = paired;
+    dst.max_len = max_len;
+    dst.total_bases = total;
+    MH_HIP(hipMalloc(&dst.seq2, sizeof(uint32_t) * (total / 16 + 8)));
+    MH_HIP(hipMalloc(&dst.nmask, sizeof(uint32_t) * (total / 32 + 8)));
+    MH_HIP(hipMalloc(&dst.qual, total + 64));
+    MH_HIP(hipMalloc(&dst.off, sizeof(int64_t) * (n > 0 ? n : 1)));
+    MH_HIP(hipMalloc(&dst.len, sizeof(int32_t) * (n > 0 ? n : 1)));
+    MH_HIP(hipMemsetAsync(dst.seq2, 0, sizeof(uint32_t) * (total / 16 + 8), c.stream));
+    MH_HIP(hipMemsetAsync(dst.nmask, 0, sizeof(uint32_t) * (total / 32 + 8), c.stream));
+    if (n > 0) {
+        MH_HIP(hipMemcpyAsync(dst.off, off.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, c.stream));
+        MH_HIP(hipMemcpyAsync(dst.len, lens, sizeof(int32_t) * n, hipMemcpyHostToDevice, c.stream));
+        uint8_t *dseq = nullptr, *dqual = nullptr;
+        int64_t *doff = nullptr;
+        MH_HIP(hipMalloc(&dseq, src_total + 1));
+        MH_HIP(hipMalloc(&dqual, src_total + 1));
+        MH_HIP(hipMalloc(&doff, sizeof(int64_t) * n));
+        MH_HIP(hipMemcpyAsync(dseq, seq, src_total, hipMemcpyHostToDevice, c.stream));
+        MH_HIP(hipMemcpyAsync(dqual, qual, src_total, hipMemcpyHostToDevice, c.stream));
+        MH_HIP(hipMemcpyAsync(doff, offsets, sizeof(int64_t) * n, hipMemcpyHostToDevice, c.stream));
+        MH_HIP(launch_pack_reads(dst, dseq, dqual, doff, c.stream));
+        MH_HIP(hipStreamSynchronize(c.stream));
+        hipFree(dseq); hipFree(dqual); hipFree(doff);
+    }
+    if (keep_host) {
+        host.seq.assign(seq, seq + src_total);
+        host.qual.assign(qual, qual + src_total);
+        host.off.assign(offsets, offsets + n);
+        host.len.assign(lens, lens + n);
+    }
+    return 0;
+}
+
+// bowtie2 read name: header up to the first whitespace, /1 or /2 dropped for mates
+static std::string qname_of(const char *h, size_t n, bool paired)
+{
+    size_t a = (n && h[0] == '@') ? 1 : 0;
+    while (a < n && (h[a] == ' ' || h[a] == '\t')) ++a;
+    size_t b = a;
+    while (b < n && h[b] != ' ' && h[b] != '\t' && h[b] != '\r') ++b;
+    std::string s(h + a, b - a);
+    if (paired && s.size() > 2 && s[s.size() - 2] == '/' && (s.back() == '1' || s.back() == '2'))
+        s.resize(s.size() - 2);
+    return s;
+}
+
+struct Fastq {
+    std::vector<std::string> names;
+    std::vector<uint8_t> seq, qual;
+    std::vector<int32_t> len;
+};
+
+static int read_fastq(const char *path, Fastq &fq, bool paired)
+{
+    gzFile f = gzopen(path, "rb");
+    if (!f) { set_error("cannot open FASTQ %s", path); return -3; }
+    gzbuffer(f, 1 << 20);
+    std::string data;
+    std::vector<char> buf(1 << 22);
+    int got;
+    while ((got = gzread(f, buf.data(), (unsigned)buf.size())) > 0) data.append(buf.data(), got);
+    const bool err = got < 0;
+    gzclose(f);
+    if (err) { set_error("gzip error reading %s", path); return -3; }
+    size_t p = 0, n = data.size();
+    auto line = [&](size_t &a, size_t &b) -> bool {
+        if (p >= n) return false;
+        a = p;
+        const void *nl = memchr(data.data() + p, '\n', n - p);
+        b = nl ? (size_t)((const char *)nl - data.data()) : n;
+        p = b + 1;
+        size_t e = b;
+        if (e > a && data[e - 1] == '\r') --e;
+        b = e;
+        return true;
+    };
+    size_t h0, h1, s0, s1, x0, x1, q0, q1;
+    while (line(h0, h1)) {
+        if (h1 == h0) continue;
+        if (!line(s0, s1) || !line(x0, x1) || !line(q0, q1)) {
+            set_error("truncated FASTQ record in %s", path);
+            return -3;
+        }
+        if (s1 - s0 > (size_t)MAXLEN) { set_error("read longer than %d in %s", MAXLEN, path); return -3; }
+        fq.names.push_back(qname_of(data.data() + h0, h1 - h0, paired));
+        fq.seq.insert(fq.seq.end(), data.begin() + s0, data.begin() + s1);
+        std::string q(data.begin() + q0, data.begin() + q1);
+        q.resize(s1 - s0, 'I');
+        fq.qual.insert(fq.qual.end(), q.begin(), q.end());
+        fq.len.push_back((int32_t)(s1 - s0));
+    }
+    return 0;
+}
+
+static void csv_field(std::string &out, const char *s, size_t n)
+{
+    bool quote = false;
+    for (size_t i = 0; i < n; ++i)
+        if (s[i] == ',' || s[i] == '"' || s[i] == '\n' || s[i] == '\r') { quote = true; break; }
+    if (!quote) { out.append(s, n); return; }
+    out.push_back('"');
+    for (size_t i = 0; i < n; ++i) {
+        if (s[i] == '"') out.push_back('"');
+        out.push_back(s[i]);
+    }
+    out.push_back('"');
+}
+
+}  // namespace mh
+
+using namespace mh;
+
+static CtxEx *X(mh_ctx *c) { return reinterpret_cast<CtxEx *>(c); }
+
+extern "C" {
+
+int mh_version(void) { return 1; }
+
+int mh_last_error(char *buf, size_t cap)
+{
+    if (!buf || cap == 0) return -3;
+    snprintf(buf, cap, "%s", g_err);
+    return 0;
+}
+
+int mh_device_count(int *n)
+{
+    int k = 0;
+    hipError_t e = hipGetDeviceCount(&k);
+    if (e != hipSuccess) { *n = 0; return hip_fail(e, "hipGetDeviceCount") == -4 ? -5 : -5; }
+    *n = k;
+    return 0;
+}
+
+int mh_ctx_create(int device, mh_ctx **out)
+{
+    if (!out) return -3;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        set_error("no HIP device available (the MI355X path has no CPU fallback)");
+        return -5;
+    }
+    if (device < 0 || device >= n) { set_error("bad device %d", device); return -3; }
+    MH_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    MH_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error("device %d is %s, libmicall_hip is built for gfx950 only", device, prop.gcnArchName);
+        return -5;
+    }
+    CtxEx *c = new (std::nothrow) CtxEx();
+    if (!c) return -2;
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete c; return hip_fail(e, "hipStreamCreate"); }
+    *out = reinterpret_cast<mh_ctx *>(c);
+    return 0;
+}
+
+int mh_ctx_destroy(mh_ctx *ctx)
+{
+    if (!ctx) return 0;
+    CtxEx *c = X(ctx);
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    free_reads(c->reads);
+    free_reads(c->rows.reads);
+    for (auto &ix : c->cache) if (ix.hkey != c->index.hkey) free_index(ix);
+    free_index(c->index);
+    MapState &M = c->map;
+    hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work); hipFree(M.slot);
+    hipFree(M.pool); hipFree(M.rec); hipFree(M.counters); hipFree(M.ref_stats);
+    RowState &R = c->rows;
+    hipFree(R.flag); hipFree(R.ref); hipFree(R.pos); hipFree(R.cig_off); hipFree(R.n_cigar);
+    hipFree(R.cigar); hipFree(R.units);
+    PileState &P = c->pile;
+    hipFree(P.dense); hipFree(P.nflag); hipFree(P.dflag); hipFree(P.read_counts);
+    hipFree(P.first_unit); hipFree(P.max_pos); hipFree(P.ev); hipFree(P.ev_pool);
+    hipFree(P.ev_counters);
+    hipFree(c->len_tab);
+    hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int mh_ctx_sync(mh_ctx *ctx)
+{
+    if (!ctx) return -3;
+    MH_HIP(hipSetDevice(X(ctx)->device));
+    MH_HIP(hipStreamSynchronize(X(ctx)->stream));
+    return 0;
+}
+
+int mh_ctx_stream(mh_ctx *ctx, void **stream)
+{
+    if (!ctx || !stream) return -3;
+    *stream = (void *)X(ctx)->stream;
+    return 0;
+}
+
+int mh_index_build(mh_ctx *ctx, int n_refs, const char *const *seqs, int seedlen)
+{
+    if (!ctx || n_refs < 0 || (n_refs > 0 && !seqs) || seedlen < 8 || seedlen > 32) {
+        set_error("mh_index_build: bad arguments");
+        return -3;
+    }
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    MH_HIP(hipStreamSynchronize(c->stream));
+    int64_t total = 0;
+    for (int r = 0; r < n_refs; ++r) total += (int64_t)std::strlen(seqs[r]);
+    const uint64_t sig = signature(n_refs, seqs, seedlen);
+    const bool cacheable = total > 65536;
+    // current index is not cached: drop it unless it lives in the cache
+    bool cur_cached = false;
+    for (auto &ix : c->cache) cur_cached |= ix.hkey == c->index.hkey;
+    if (!cur_cached) free_index(c->index);
+    c->index = DevIndex{};
+    for (auto &ix : c->cache) {
+        if (ix.sig == sig && ix.n_refs == n_refs && ix.seedlen == seedlen) {
+            c->index = ix;
+            return 0;
+        }
+    }
+    DevIndex ix;
+    if (int st = build_index(ix, n_refs, seqs, seedlen)) { free_index(ix); return st; }
+    ix.sig = sig;
+    if (cacheable) {
+        if (c->cache.size() >= 2) { free_index(c->cache.front()); c->cache.erase(c->cache.begin()); }
+        c->cache.push_back(ix);
+    }
+    c->index = ix;
+    return 0;
+}
+
+int mh_reads_load(mh_ctx *ctx, int64_t n_reads, int paired, const uint8_t *seq,
+                  const uint8_t *qual, const int64_t *offsets, const int32_t *lens)
+{
+    if (!ctx || (n_reads > 0 && (!seq || !qual || !offsets || !lens))) return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    c->names.clear();
+    c->map.valid = false;
+    return load_reads(*c, c->reads, c->host, n_reads, paired, seq, qual, offsets, lens, true);
+}
+
+int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64_t *n_reads)
+{
+    if (!ctx || !path1) return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    const bool paired = path2 != nullptr;
+    Fastq a, b;
+    if (int st = read_fastq(path1, a, paired)) return st;
+    std::vector<std::string> names;
+    std::vector<uint8_t> seq, qual;
+    std::vector<int64_t> off;
+    std::vector<int32_t> len;
+    if (paired) {
+        if (int st = read_fastq(path2, b, paired)) return st;
+        if (a.len.size() != b.len.size()) {
+            set_error("paired FASTQ files hold %zu and %zu reads", a.len.size(), b.len.size());
+            return -3;
+        }
+        int64_t pa = 0, pb = 0;
+        for (size_t i = 0; i < a.len.size(); ++i) {
+            off.push_back((int64_t)seq.size());
+            len.push_back(a.len[i]);
+            seq.insert(seq.end(), a.seq.begin() + pa, a.seq.begin() + pa + a.len[i]);
+            qual.insert(qual.end(), a.qual.begin() + pa, a.qual.begin() + pa + a.len[i]);
+            pa += a.len[i];
+            off.push_back((int64_t)seq.size());
+            len.push_back(b.len[i]);
+            seq.insert(seq.end(), b.seq.begin() + pb, b.seq.begin() + pb + b.len[i]);
+            qual.insert(qual.end(), b.qual.begin() + pb, b.qual.begin() + pb + b.len[i]);
+            pb += b.len[i];
+            names.push_back(a.names[i]);
+            names.push_back(b.names[i]);
+        }
+    } else {
+        int64_t pa = 0;
+        for (size_t i = 0; i < a.len.size(); ++i) {
+            off.push_back(pa);
+            len.push_back(a.len[i]);
+            pa += a.len[i];
+        }
+        seq.swap(a.seq);
+        qual.swap(a.qual);
+        names.swap(a.names);
+    }
+    const int64_t n = (int64_t)len.size();
+    int st = load_reads(*c, c->reads, c->host, n, paired, seq.data(), qual.data(), off.data(),
+                        len.data(), true);
+    if (st) return st;
+    c->names.swap(names);
+    c->map.valid = false;
+    if (n_reads) *n_reads = n;
+    return 0;
+}
+
+int mh_reads_count(mh_ctx *ctx, int64_t *n_reads, int *paired)
+{
+    if (!ctx) return -3;
+    if (n_reads) *n_reads = X(ctx)->reads.n;
+    if (paired) *paired = X(ctx)->reads.paired;
+    return 0;
+}
+
+int mh_reads_set_names(mh_ctx *ctx, int64_t n, const char *const *names)
+{
+    if (!ctx || n != X(ctx)->reads.n) { set_error("mh_reads_set_names: count mismatch"); return -3; }
+    CtxEx *c = X(ctx);
+    c->names.assign(names, names + n);
+    return 0;
+}
+
+int mh_map(mh_ctx *ctx, const mh_params *par)
+{
+    if (!ctx || !par) return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    if (int st = prepare_len_tab(*c, par->mode)) return st;
+    int st = run_map(*c, *par);
+    if (st == 0) MH_HIP(hipStreamSynchronize(c->stream));
+    c->rec_cache.clear();
+    return st;
+}
+
+static int fetch_recs(CtxEx *c, int64_t first, int64_t n, std::vector<Rec> &rec,
+                      std::vector<uint32_t> &pool)
+{
+    MapState &M = c->map;
+    if (!M.valid) { set_error("no mapping results (call mh_map)"); return -3; }
+    if (first < 0 || n < 0 || first + n > M.n_reads) { set_error("record range out of bounds"); return -3; }
+    rec.resize(n > 0 ? n : 1);
+    if (n > 0)
+        MH_HIP(hipMemcpy(rec.data(), M.rec + first, sizeof(Rec) * n, hipMemcpyDeviceToHost));
+    int32_t used = 0;
+    MH_HIP(hipMemcpy(&used, M.counters + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+    pool.resize(used > 0 ? used : 1);
+    if (used > 0)
+        MH_HIP(hipMemcpy(pool.data(), M.pool, sizeof(uint32_t) * used, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int mh_alns_fetch(mh_ctx *ctx, int64_t first, int64_t n, mh_aln *out)
+{
+    if (!ctx || (n > 0 && !out)) return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    std::vector<Rec> rec;
+    std::vector<uint32_t> pool;
+    if (int st = fetch_recs(c, first, n, rec, pool)) return st;
+    for (int64_t i = 0; i < n; ++i) {
+        const Rec &r = rec[i];
+        mh_aln &o = out[i];
+        std::memcpy(&o, &r, sizeof(int32_t) * 20);
+        std::memset(o.cigar, 0, sizeof(o.cigar));
+        for (int k = 0; k < r.n_cigar && k < MH_MAXOPS; ++k) o.cigar[k] = pool[r.cig_off + k];
+    }
+    return 0;
+}
+
+int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mapped,
+                  int64_t *first_row, int64_t *first_mapped, int64_t *unmapped,
+                  int64_t *star_lines)
+{
+    if (!ctx) return -3;
+    CtxEx *c = X(ctx);
+    MapState &M = c->map;
+    if (!M.valid) { set_error("no mapping results (call mh_map)"); return -3; }
+    MH_HIP(hipSetDevice(c->device));
+    const int n = M.n_refs;
+    std::vector<int64_t> s(5 * n + 2);
+    MH_HIP(hipMemcpy(s.data(), M.ref_stats, sizeof(int64_t) * s.size(), hipMemcpyDeviceToHost));
+    if (lines) std::memcpy(lines, s.data(), sizeof(int64_t) * n);
+    if (filtered) std::memcpy(filtered, s.data() + n, sizeof(int64_t) * n);
+    if (mapped) std::memcpy(mapped, s.data() + 2 * n, sizeof(int64_t) * n);
+    if (first_row) std::memcpy(first_row, s.data() + 3 * n, sizeof(int64_t) * n);
+    if (first_mapped) std::memcpy(first_mapped, s.data() + 4 * n, sizeof(int64_t) * n);
+    if (unmapped) *unmapped = s[5 * n];
+    if (star_lines) *star_lines = s[5 * n + 1];
+    return 0;
+}
+
+int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20)
+{
+    if (!ctx || (n > 0 && !out20)) return -3;
+    CtxEx *c = X(ctx);
+    MapState &M = c->map;
+    if (!M.valid) { set_error("no mapping results (call mh_map)"); return -3; }
+    if (first < 0 || n < 0 || first + n > M.n_reads) { set_error("record range out of bounds"); return -3; }
+    MH_HIP(hipSetDevice(c->device));
+    if (n == 0) return 0;
+    // Rec is 22 int32; copy with a 2D memcpy that keeps the first 20 of each
+    MH_HIP(hipMemcpy2D(out20, sizeof(int32_t) * 20, M.rec + first, sizeof(Rec), sizeof(int32_t) * 20,
+                       (size_t)n, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
+                   const char *const *refnames, char *buf, size_t cap, size_t *used)
+{
+    if (!ctx || !refnames || (style != 0 && style != 1)) return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    if ((int64_t)c->names.size() != c->reads.n) { set_error("no read names loaded"); return -3; }
+    std::vector<Rec> rec;
+    std::vector<uint32_t> pool;
+    if (order) {
+        if (int st = fetch_recs(c, 0, c->map.n_reads, rec, pool)) return st;
+        for (int64_t k = 0; k < n; ++k)
+            if (order[first + k] < 0 || order[first + k] >= c->map.n_reads) {
+                set_error("format order index out of range");
+                return -3;
+            }
+    } else if (int st = fetch_recs(c, first, n, rec, pool)) {
+        return st;
+    }
+    static const char comp[256] = {};
+    (void)comp;
+    static const char *ytn[4] = {"CP", "DP", "UP", "UU"};
+    static const char *yfn[3] = {"", "NS", "LN"};
+    std::string out;
+    out.reserve((size_t)n * 700);
+    std::string seq, qual, cig, tmp;
+    char nb[64];
+    const char sep = style == 0 ? '\t' : ',';
+    for (int64_t k = 0; k < n; ++k) {
+        const int64_t r = order ? order[first + k] : first + k;
+        const Rec &a = order ? rec[r] : rec[k];
+        const int L = c->host.len[r];
+        const uint8_t *s = c->host.seq.data() + c->host.off[r];
+        const uint8_t *q = c->host.qual.data() + c->host.off[r];
+        seq.resize(L);
+        qual.resize(L);
+        const bool rev = a.ref >= 0 && a.rev;
+        for (int x = 0; x < L; ++x) {
+            const uint8_t cd = code_of((char)s[x]);
+            const char b = "ACGTN"[cd];
+            if (rev) {
+                seq[L - 1 - x] = "TGCAN"[cd];
+                qual[L - 1 - x] = (char)q[x];
+            } else {
+                seq[x] = b;
+                qual[x] = (char)q[x];
+            }
+        }
+        cig.clear();
+        if (a.ref < 0) {
+            cig = "*";
+        } else {
+            for (int z = 0; z < a.n_cigar; ++z) {
+                const uint32_t op = pool[a.cig_off + z];
+                snprintf(nb, sizeof(nb), "%u%c", op >> 4, "MIDxS"[op & 7]);
+                cig += nb;
+            }
+        }
+        const std::string &qn = c->names[r];
+        auto put = [&](const char *p, size_t len) {
+            if (style == 1) csv_field(out, p, len); else out.append(p, len);
+        };
+        put(qn.data(), qn.size());
+        out.push_back(sep);
+        out += std::to_string(a.flag);
+        out.push_back(sep);
+        const char *rn = a.sam_ref >= 0 ? refnames[a.sam_ref] : "*";
+        put(rn, std::strlen(rn));
+        out.push_back(sep);
+        out += std::to_string(a.sam_pos);
+        out.push_back(sep);
+        out += std::to_string(a.mapq);
+        out.push_back(sep);
+        out += cig;
+        out.push_back(sep);
+        if (a.rnext == -2) out += "*";
+        else if (a.rnext == -1) out += "=";
+        else put(refnames[a.rnext], std::strlen(refnames[a.rnext]));
+        out.push_back(sep);
+        out += std::to_string(a.pnext);
+        out.push_back(sep);
+        out += std::to_string(a.tlen);
+        out.push_back(sep);
+        if (L == 0) out += "*"; else put(seq.data(), seq.size());
+        out.push_back(sep);
+        if (L == 0) out += "*"; else put(qual.data(), qual.size());
+        if (style == 0) {
+            if (a.ref >= 0) {
+                out += "\tAS:i:" + std::to_string(a.score);
+                if (a.secbest != I32MIN) out += "\tXS:i:" + std::to_string(a.secbest);
+                out += "\tXN:i:0\tXM:i:" + std::to_string(a.xm) + "\tXO:i:" + std::to_string(a.xo) +
+                       "\tXG:i:" + std::to_string(a.xg) + "\tNM:i:" + std::to_string(a.nm);
+                if (a.ys != I32MIN) out += "\tYS:i:" + std::to_string(a.ys);
+            } else {
+                if (a.ys != I32MIN) out += "\tYS:i:" + std::to_string(a.ys);
+                if (a.yf) { out += "\tYF:Z:"; out += yfn[a.yf]; }
+            }
+            out += "\tYT:Z:";
+            out += ytn[a.yt & 3];
+        }
+        out.push_back('\n');
+    }
+    if (used) *used = out.size();
+    if (out.size() > cap || !buf) { set_error("format buffer too small (%zu needed)", out.size()); return -2; }
+    std::memcpy(buf, out.data(), out.size());
+    return 0;
+}
+
+int mh_rows_load(mh_ctx *ctx, int64_t n_rows, const int32_t *flag, const int32_t *ref,
+                 const int32_t *pos, const int32_t *cigar_off, const int32_t *n_cigar,
+                 const uint32_t *cigar, const uint8_t *seq, const uint8_t *qual,
+                 const int64_t *offsets, const int32_t *lens, int64_t n_units,
+                 const int64_t *unit_rows)
+{
+    if (!ctx || n_rows < 0 || n_units < 0) return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    RowState &R = c->rows;
+    hipFree(R.flag); hipFree(R.ref); hipFree(R.pos); hipFree(R.cig_off); hipFree(R.n_cigar);
+    hipFree(R.cigar); hipFree(R.units);
+    R = RowState{};
+    int64_t ncig = 0;
+    for (int64_t i = 0; i < n_rows; ++i) {
+        if (n_cigar[i] < 0 || n_cigar[i] > MH_MAXOPS || cigar_off[i] < 0) {
+            set_error("rows: bad cigar in row %lld", (long long)i);
+            return -3;
+        }
+        ncig = std::max<int64_t>(ncig, (int64_t)cigar_off[i] + n_cigar[i]);
+        for (int k = 0; k < n_cigar[i]; ++k) {
+            const uint32_t op = cigar[cigar_off[i] + k] & 15;
+            if (op != MH_OP_M && op != MH_OP_I && op != MH_OP_D && op != MH_OP_S) {
+                set_error("Unsupported CIGAR token in row %lld", (long long)i);
+                return -3;
+            }
+        }
+        for (int x = 0; x < lens[i]; ++x) {
+            const char ch = (char)seq[offsets[i] + x];
+            if (ch != 'A' && ch != 'C' && ch != 'G' && ch != 'T' && ch != 'N' && !(flag[i] & 4)) {
+                set_error("row %lld: base letter '%c' (only ACGTN as bowtie2 prints)", (long long)i, ch);
+                return -3;
+            }
+        }
+    }
+    const int64_t nr = n_rows > 0 ? n_rows : 1;
+    MH_HIP(hipMalloc(&R.flag, sizeof(int32_t) * nr));
+    MH_HIP(hipMalloc(&R.ref, sizeof(int32_t) * nr));
+    MH_HIP(hipMalloc(&R.pos, sizeof(int32_t) * nr));
+    MH_HIP(hipMalloc(&R.cig_off, sizeof(int32_t) * nr));
+    MH_HIP(hipMalloc(&R.n_cigar, sizeof(int32_t) * nr));
+    MH_HIP(hipMalloc(&R.cigar, sizeof(uint32_t) * (ncig > 0 ? ncig : 1)));
+    MH_HIP(hipMalloc(&R.units, sizeof(int64_t) * 2 * (n_units > 0 ? n_units : 1)));
+    if (n_rows > 0) {
+        MH_HIP(hipMemcpy(R.flag, flag, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
+        MH_HIP(hipMemcpy(R.ref, ref, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
+        MH_HIP(hipMemcpy(R.pos, pos, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
+        MH_HIP(hipMemcpy(R.cig_off, cigar_off, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
+        MH_HIP(hipMemcpy(R.n_cigar, n_cigar, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
+    }
+    if (ncig > 0) MH_HIP(hipMemcpy(R.cigar, cigar, sizeof(uint32_t) * ncig, hipMemcpyHostToDevice));
+    if (n_units > 0)
+        MH_HIP(hipMemcpy(R.units, unit_rows, sizeof(int64_t) * 2 * n_units, hipMemcpyHostToDevice));
+    R.n_rows = n_rows;
+    R.n_units = n_units;
+    HostReads dummy;
+    return load_reads(*c, R.reads, dummy, n_rows, 0, seq, qual, offsets, lens, false);
+}
+
+int mh_pileup(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *ref_lens)
+{
+    if (!ctx || n_refs < 0 || (n_refs > 0 && !ref_lens) || (source != 0 && source != 1)) return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    int32_t cap = 1;
+    for (int r = 0; r < n_refs; ++r) cap = std::max(cap, ref_lens[r] + MH_PILEUP_SLACK);
+    c->pile.n_refs = n_refs;
+    c->pile.cap = cap;
+    int st = run_pileup(*c, source, q_cutoff);
+    if (st == 0) MH_HIP(hipStreamSynchronize(c->stream));
+    return st;
+}
+
+int mh_pileup_dims(mh_ctx *ctx, int *n_refs, int32_t *cap, int64_t *n_events, int64_t *event_bytes)
+{
+    if (!ctx) return -3;
+    CtxEx *c = X(ctx);
+    PileState &P = c->pile;
+    if (n_refs) *n_refs = P.n_refs;
+    if (cap) *cap = P.cap;
+    int64_t ctr[4] = {0, 0, 0, 0};
+    if (P.ev_counters) {
+        MH_HIP(hipSetDevice(c->device));
+        MH_HIP(hipMemcpy(ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
+    }
+    if (n_events) *n_events = ctr[0];
+    if (event_bytes) *event_bytes = ctr[1];
+    return 0;
+}
+
+int mh_pileup_fetch(mh_ctx *ctx, int32_t *dense, uint8_t *nflag, uint8_t *dflag,
+                    int64_t *read_counts, int64_t *first_unit, int32_t *max_pos)
+{
+    if (!ctx) return -3;
+    CtxEx *c = X(ctx);
+    PileState &P = c->pile;
+    if (!P.dense) { set_error("no pileup (call mh_pileup)"); return -3; }
+    MH_HIP(hipSetDevice(c->device));
+    const int64_t cells = (int64_t)P.n_refs * P.cap;
+    if (dense) MH_HIP(hipMemcpy(dense, P.dense, sizeof(int32_t) * 4 * cells, hipMemcpyDeviceToHost));
+    if (nflag) MH_HIP(hipMemcpy(nflag, P.nflag, cells, hipMemcpyDeviceToHost));
+    if (dflag) MH_HIP(hipMemcpy(dflag, P.dflag, cells, hipMemcpyDeviceToHost));
+    if (read_counts) MH_HIP(hipMemcpy(read_counts, P.read_counts, sizeof(int64_t) * P.n_refs, hipMemcpyDeviceToHost));
+    if (first_unit) MH_HIP(hipMemcpy(first_unit, P.first_unit, sizeof(int64_t) * P.n_refs, hipMemcpyDeviceToHost));
+    if (max_pos) MH_HIP(hipMemcpy(max_pos, P.max_pos, sizeof(int32_t) * P.n_refs, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int mh_pileup_events(mh_ctx *ctx, int32_t *ref, int32_t *pos, int32_t *tok_off, int32_t *tok_len,
+                     char *pool)
+{
+    if (!ctx) return -3;
+    CtxEx *c = X(ctx);
+    PileState &P = c->pile;
+    MH_HIP(hipSetDevice(c->device));
+    int64_t ctr[4] = {0, 0, 0, 0};
+    if (P.ev_counters) MH_HIP(hipMemcpy(ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
+    const int64_t ne = ctr[0];
+    std::vector<int32_t> ev(4 * (ne > 0 ? ne : 1));
+    if (ne > 0) MH_HIP(hipMemcpy(ev.data(), P.ev, sizeof(int32_t) * 4 * ne, hipMemcpyDeviceToHost));
+    for (int64_t e = 0; e < ne; ++e) {
+        if (ref) ref[e] = ev[4 * e];
+        if (pos) pos[e] = ev[4 * e + 1];
+        if (tok_off) tok_off[e] = ev[4 * e + 2];
+        if (tok_len) tok_len[e] = ev[4 * e + 3];
+    }
+    if (pool && ctr[1] > 0) MH_HIP(hipMemcpy(pool, P.ev_pool, ctr[1], hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int mh_gotoh_align(mh_ctx *ctx, const char *seq1, const char *seq2, int gop, int gep,
+                   int is_global, const char *alphabet, const int *matrix, char *out1, char *out2,
+                   int cap, int *score)
+{
+    if (!ctx || !seq1 || !seq2 || !alphabet || !matrix || !out1 || !out2 || !score) return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    return run_gotoh(*c, seq1, seq2, gop, gep, is_global, alphabet, matrix, out1, out2, cap, score);
+}
+
+int mh_levenshtein(const char *a, const char *b)
+{
+    if (!a || !b) return -3;
+    const size_t m = std::strlen(a), n = std::strlen(b);
+    std::vector<int> row(n + 1);
+    for (size_t j = 0; j <= n; ++j) row[j] = (int)j;
+    for (size_t i = 1; i <= m; ++i) {
+        int diag = row[0];
+        row[0] = (int)i;
+        for (size_t j = 1; j <= n; ++j) {
+            const int up = row[j];
+            row[j] = std::min({diag + (a[i - 1] != b[j - 1]), up + 1, row[j - 1] + 1});
+            diag = up;
+        }
+    }
+    return row[n];
+}
+
+}  // extern "C"

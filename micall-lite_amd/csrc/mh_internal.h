@@ -1,0 +1,169 @@
+// mh_internal.h -- device-side data layout shared by the HIP translation
+// units of libmicall_hip.so (gfx950 only).  See DESIGN.md "Data layout".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "micall_hip.h"
+
+namespace mh {
+
+// Mapper constants (the specification lives in oracle/og_mapper.c, which the
+// kernels reproduce bit for bit).
+constexpr int BAND = 64;            // diagonals per band = lanes of one wave64
+constexpr int HALF = 32;            // band = [center - 32, center + 31]
+constexpr int MAXCAND = 4;          // extension candidates per mate
+constexpr int MAXHITS_SEED = 64;    // seeds with more exact hits are skipped
+constexpr int MAXHITS_MATE = 512;   // hit budget per mate, in seed order
+constexpr int CLUSTER_GAP = 8;      // diagonal gap that splits clusters
+constexpr int MAXSEEDS = 32;        // seeds per strand
+constexpr int MAXLEN = 1024;        // longest read accepted
+constexpr int GBAR = 4;             // --gbar 4
+constexpr int NPEN = 1;             // --np 1
+constexpr int NEG = -(1 << 29);     // minus infinity of the DP
+constexpr int32_t I32MIN = INT32_MIN;
+
+// Reads resident in HBM: each read starts on a 32-base boundary.
+//   seq2 : 2-bit codes, 16 bases per u32, base b at bits 2*(b%16)
+//   nmask: 1 bit per base (ambiguous -> code 0 in seq2 and bit set here)
+//   qual : Phred+33 bytes
+struct DevReads {
+    int64_t n = 0;
+    int paired = 0;
+    int max_len = 0;
+    int64_t total_bases = 0;  // padded
+    uint32_t *seq2 = nullptr;
+    uint32_t *nmask = nullptr;
+    uint8_t *qual = nullptr;
+    int64_t *off = nullptr;   // padded base offset (multiple of 32)
+    int32_t *len = nullptr;
+};
+
+// Reference set + exact-seed hash index (replaces the .bt2 files).
+struct DevIndex {
+    int n_refs = 0;
+    int seedlen = 0;
+    int64_t total = 0;
+    uint8_t *codes = nullptr;      // 0..3, 4 = ambiguous; refs back to back
+    int64_t *ref_off = nullptr;
+    int32_t *ref_len = nullptr;
+    uint64_t *hkey = nullptr;      // open addressing, EMPTY = ~0
+    uint32_t *hstart = nullptr;
+    uint32_t *hcount = nullptr;
+    uint64_t hmask = 0;
+    int2 *hits = nullptr;          // (ref, pos) sorted per key
+    uint64_t sig = 0;              // content signature (cache key)
+};
+
+constexpr uint64_t HEMPTY = ~0ull;
+
+__host__ __device__ inline uint64_t hash_key(uint64_t k)
+{
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+struct Cand {
+    int32_t strand, ref, center, support;
+};
+
+// Result of one banded extension (one candidate of one read).
+struct Slot {
+    int32_t valid, strand, ref, pos, end, score, xm, xo, xg, nm, n_cigar, cig_off;
+};
+
+// Final per-read SAM record (mh_aln without the inline CIGAR).
+struct Rec {
+    int32_t ref, pos, rev, score, secbest, flag, mapq, rnext, pnext, tlen;
+    int32_t sam_ref, sam_pos, xm, xo, xg, nm, ys, yt, yf, n_cigar;
+    int32_t cig_off, maxm;   // cigar offset in the pool; longest M run
+};
+
+struct MapState {
+    int64_t n_reads = 0;
+    int n_refs = 0;
+    mh_params par{};
+    Cand *cand = nullptr;        // n_reads * MAXCAND
+    int32_t *n_cand = nullptr;   // n_reads
+    int32_t *yf = nullptr;       // n_reads
+    int32_t *work = nullptr;     // slot ids to extend
+    Slot *slot = nullptr;        // n_reads * MAXCAND
+    uint32_t *pool = nullptr;    // CIGAR ops of all slots
+    int64_t pool_cap = 0;
+    Rec *rec = nullptr;          // n_reads
+    int32_t *counters = nullptr; // [work_n, pool_used, pool_overflow, pad]
+    int64_t *ref_stats = nullptr;// per ref: lines, filtered, mapped, first_row, first_mapped; + unmapped, star
+    int64_t cap_reads = 0;
+    int cap_refs = 0;
+    bool valid = false;
+};
+
+// External SAM rows for the pileup (prelim.csv read back).
+struct RowState {
+    int64_t n_rows = 0, n_units = 0;
+    int32_t *flag = nullptr, *ref = nullptr, *pos = nullptr, *cig_off = nullptr,
+            *n_cigar = nullptr;
+    uint32_t *cigar = nullptr;
+    int64_t *units = nullptr;
+    DevReads reads;
+};
+
+struct PileState {
+    int n_refs = 0;
+    int32_t cap = 0;
+    int32_t *dense = nullptr;       // n_refs * cap * 4
+    uint8_t *nflag = nullptr;       // n_refs * cap
+    uint8_t *dflag = nullptr;
+    int64_t *read_counts = nullptr; // n_refs
+    int64_t *first_unit = nullptr;  // n_refs
+    int32_t *max_pos = nullptr;     // n_refs
+    int32_t *ev = nullptr;          // events: 4 int32 (ref, pos, tok_off, tok_len)
+    char *ev_pool = nullptr;
+    int64_t ev_cap = 0, pool_cap = 0;
+    int64_t *ev_counters = nullptr; // [n_events, pool_used, overflow, error]
+    int64_t alloc_cells = 0;
+    int alloc_refs = 0;
+};
+
+// ---- kernels' host-side launchers (defined in the .hip files) ----------
+hipError_t launch_pack_reads(DevReads &r, const uint8_t *d_seq, const uint8_t *d_qual,
+                             const int64_t *d_src_off, hipStream_t s);
+int run_map(struct Ctx &c, const mh_params &par);
+int run_pileup(struct Ctx &c, int source, int q_cutoff);
+int run_gotoh(struct Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_global,
+              const char *alphabet, const int *matrix, char *out1, char *out2, int cap,
+              int *score);
+
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevReads reads;
+    std::vector<std::string> names;  // QNAMEs for SAM text
+    std::vector<std::string> host_seq, host_qual; // kept only when names are
+    DevIndex index;
+    MapState map;
+    RowState rows;
+    PileState pile;
+    // per-length tables (host-computed, uploaded): seed interval, min score, n ceil
+    int32_t *len_tab = nullptr;      // [3][MAXLEN + 1]
+    int len_tab_mode = -1;
+};
+
+void set_error(const char *fmt, ...);
+int hip_fail(hipError_t e, const char *what);
+
+}  // namespace mh
+
+#define MH_HIP(call)                                                  \
+    do {                                                              \
+        hipError_t e_ = (call);                                       \
+        if (e_ != hipSuccess) return ::mh::hip_fail(e_, #call);       \
+    } while (0)

@@ -1,0 +1,928 @@
+// mh_map.hip -- the read mapper that replaces bowtie2 on MiCall-Lite's remap
+// path (prelim_map.py:114-140 end-to-end, remap.py:701-755 --local), written
+// for gfx950.  Bit-for-bit specification: oracle/og_mapper.c.
+//
+// Kernels, in launch order for one mapping pass:
+//   k_pack_reads  ASCII reads -> 2-bit bases + N mask + qualities (ingest only)
+//   k_seed        one wave64 per read: 2x32 exact seeds (one lane each),
+//                 hash lookups, hit sort (LDS bitonic), diagonal clustering,
+//                 top-4 candidates + work list
+//   k_dp          one wave64 per candidate: banded affine-gap DP, lane k =
+//                 diagonal center-32+k, rows = read bases; vertical moves by a
+//                 DPP wave shift, horizontal gaps by a DPP prefix-max scan;
+//                 4 traceback bits per cell in LDS; lane-0 traceback -> CIGAR
+//   k_pair        one thread per pair: concordance, flags, MAPQ, SAM fields,
+//                 per-reference line tallies
+#include "mh_internal.h"
+
+namespace mh {
+
+// ---------------------------------------------------------------------------
+// small wave helpers
+// ---------------------------------------------------------------------------
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ int dpp(int old, int v)
+{
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xF, false);
+}
+constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114,
+              DPP_ROW_SHR8 = 0x118, DPP_WAVE_SHL1 = 0x130, DPP_WAVE_SHR1 = 0x138,
+              DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143;
+
+__device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int wave_sum(int v)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ int wave_excl_scan(int v, int lane)
+{
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+
+__device__ __forceinline__ long long wave_max64(long long v)
+{
+    for (int o = 32; o > 0; o >>= 1) {
+        long long y = __shfl_xor(v, o, 64);
+        v = y > v ? y : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+
+// ---------------------------------------------------------------------------
+// k_pack_reads: one wave per read, one lane per 32-base chunk
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t base_code(uint8_t c, uint32_t &isn)
+{
+    switch (c) {
+    case 'A': case 'a': isn = 0; return 0;
+    case 'C': case 'c': isn = 0; return 1;
+    case 'G': case 'g': isn = 0; return 2;
+    case 'T': case 't': isn = 0; return 3;
+    default: isn = 1; return 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pack_reads(DevReads R, const uint8_t *__restrict__ seq,
+                                                    const uint8_t *__restrict__ qual,
+                                                    const int64_t *__restrict__ src_off)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    for (int64_t r = wave; r < R.n; r += nwaves) {
+        const int m = R.len[r];
+        const int64_t so = src_off[r], dofs = R.off[r];
+        const int chunks = (m + 31) >> 5;
+        if (lane < chunks) {
+            uint32_t w0 = 0, w1 = 0, nm = 0;
+            for (int x = 0; x < 32; ++x) {
+                const int b = lane * 32 + x;
+                if (b >= m) break;
+                uint32_t isn;
+                const uint32_t c = base_code(seq[so + b], isn);
+                if (x < 16) w0 |= c << (2 * x); else w1 |= c << (2 * (x - 16));
+                nm |= isn << x;
+                R.qual[dofs + b] = qual[so + b];
+            }
+            R.seq2[(dofs >> 4) + 2 * lane] = w0;
+            R.seq2[(dofs >> 4) + 2 * lane + 1] = w1;
+            R.nmask[(dofs >> 5) + lane] = nm;
+        }
+    }
+}
+
+hipError_t launch_pack_reads(DevReads &r, const uint8_t *d_seq, const uint8_t *d_qual,
+                             const int64_t *d_src_off, hipStream_t s)
+{
+    if (r.n == 0) return hipSuccess;
+    int64_t blocks = (r.n + 3) / 4;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_pack_reads, dim3((unsigned)blocks), dim3(256), 0, s, r, d_seq, d_qual,
+                       d_src_off);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// read access helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t read_code(const DevReads &R, int64_t off, int b)
+{
+    const int64_t g = off + b;
+    if ((R.nmask[g >> 5] >> (g & 31)) & 1) return 4;
+    return (R.seq2[g >> 4] >> (2 * (g & 15))) & 3;
+}
+
+// SL (<= 32) consecutive 2-bit codes starting at absolute base g, base x at
+// bits 2x+1:2x; and the N-mask bits of the same window.
+__device__ __forceinline__ uint64_t window_key(const DevReads &R, int64_t g, int SL)
+{
+    const int64_t w = g >> 4;
+    const int sh = 2 * (int)(g & 15);
+    const uint64_t lo = (uint64_t)R.seq2[w] | ((uint64_t)R.seq2[w + 1] << 32);
+    const uint64_t hi = R.seq2[w + 2];
+    uint64_t k = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    return SL >= 32 ? k : (k & ((1ull << (2 * SL)) - 1));
+}
+
+__device__ __forceinline__ uint32_t window_nmask(const DevReads &R, int64_t g, int SL)
+{
+    const int64_t w = g >> 5;
+    const int sh = (int)(g & 31);
+    const uint64_t v = ((uint64_t)R.nmask[w] | ((uint64_t)R.nmask[w + 1] << 32)) >> sh;
+    return (uint32_t)(v & ((1ull << SL) - 1));
+}
+
+__device__ __forceinline__ uint64_t revcomp_key(uint64_t k, int SL)
+{
+    uint64_t x = ~k;
+    x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
+    x = ((x >> 8) & 0x00FF00FF00FF00FFull) | ((x & 0x00FF00FF00FF00FFull) << 8);
+    x = ((x >> 16) & 0x0000FFFF0000FFFFull) | ((x & 0x0000FFFF0000FFFFull) << 16);
+    x = (x >> 32) | (x << 32);
+    return x >> (64 - 2 * SL);
+}
+
+// ---------------------------------------------------------------------------
+// k_seed
+// ---------------------------------------------------------------------------
+struct SeedArgs {
+    DevReads R;
+    DevIndex I;
+    int mode;
+    const int32_t *len_tab;  // [0]: seed interval, [1]: min score, [2]: n ceil
+    Cand *cand;
+    int32_t *n_cand;
+    int32_t *yf;
+    int32_t *work;
+    int32_t *counters;
+};
+
+__device__ __forceinline__ bool cand_before(const Cand &x, const Cand &y)
+{
+    if (x.support != y.support) return x.support > y.support;
+    if (x.strand != y.strand) return x.strand < y.strand;
+    if (x.ref != y.ref) return x.ref < y.ref;
+    return x.center < y.center;
+}
+
+__global__ __launch_bounds__(256) void k_seed(SeedArgs A)
+{
+    __shared__ uint64_t sh_hits[4][MAXHITS_MATE];
+    const int lane = threadIdx.x & 63;
+    const int wv = wave_uniform(threadIdx.x >> 6);
+    uint64_t *hits = sh_hits[wv];
+    const int SL = A.I.seedlen;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + wv; r < A.R.n; r += (int64_t)gridDim.x * 4) {
+        const int m = A.R.len[r];
+        const int64_t off = A.R.off[r];
+        if (m == 0) {
+            if (lane == 0) { A.n_cand[r] = 0; A.yf[r] = 2; }
+            continue;
+        }
+        int nn = 0;
+        for (int w = lane; w * 32 < m; w += 64) {
+            uint32_t bits = A.R.nmask[(off >> 5) + w];
+            const int rem = m - w * 32;
+            if (rem < 32) bits &= (1u << rem) - 1;
+            nn += __popc(bits);
+        }
+        nn = wave_sum(nn);
+        if (nn > A.len_tab[2 * (MAXLEN + 1) + m]) {
+            if (lane == 0) { A.n_cand[r] = 0; A.yf[r] = 1; }
+            continue;
+        }
+        if (lane == 0) A.yf[r] = 0;
+        if (m < SL) {
+            if (lane == 0) A.n_cand[r] = 0;
+            continue;
+        }
+        const int iv = A.len_tab[m];
+        int ns = 1 + (m - SL) / iv;
+        if (ns > MAXSEEDS) ns = MAXSEEDS;
+        const int s = lane >> 5, t = lane & 31;
+        const int o = t * iv;
+        int cnt = 0;
+        uint32_t start = 0;
+        if (t < ns) {
+            const int p = s == 0 ? o : m - o - SL;
+            if (window_nmask(A.R, off + p, SL) == 0) {
+                uint64_t key = window_key(A.R, off + p, SL);
+                if (s) key = revcomp_key(key, SL);
+                uint64_t h = hash_key(key) & A.I.hmask;
+                for (;;) {
+                    const uint64_t k = A.I.hkey[h];
+                    if (k == HEMPTY) break;
+                    if (k == key) {
+                        start = A.I.hstart[h];
+                        cnt = (int)A.I.hcount[h];
+                        break;
+                    }
+                    h = (h + 1) & A.I.hmask;
+                }
+                if (cnt > MAXHITS_SEED) cnt = 0;
+            }
+        }
+        const int pre = wave_excl_scan(cnt, lane);
+        int total = wave_sum(cnt);
+        if (total > MAXHITS_MATE) total = MAXHITS_MATE;
+        for (int e = 0; e < cnt && pre + e < MAXHITS_MATE; ++e) {
+            const int2 h = A.I.hits[start + e];
+            const int diag = h.y - o;
+            hits[pre + e] = ((uint64_t)s << 62) | ((uint64_t)h.x << 32) |
+                            (uint64_t)(uint32_t)(diag + (1 << 30));
+        }
+        if (total == 0) {
+            if (lane == 0) A.n_cand[r] = 0;
+            continue;
+        }
+        int N = 1;
+        while (N < total) N <<= 1;
+        for (int x = total + lane; x < N; x += 64) hits[x] = ~0ull;
+        wave_sync();
+        // bitonic sort, ascending
+        for (int k = 2; k <= N; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int tt = lane; tt < (N >> 1); tt += 64) {
+                    const int i = 2 * j * (tt / j) + (tt % j);
+                    const int q = i + j;
+                    const uint64_t a = hits[i], b = hits[q];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) { hits[i] = b; hits[q] = a; }
+                }
+                wave_sync();
+            }
+        }
+        if (lane == 0) {
+            Cand best[MAXCAND];
+            int nc = 0;
+            int h0 = 0;
+            while (h0 < total) {
+                const uint64_t k0 = hits[h0];
+                const int st = (int)(k0 >> 62), rf = (int)((k0 >> 32) & 0x3fffffff);
+                int h1 = h0 + 1;
+                int prev = (int)(uint32_t)k0 - (1 << 30);
+                while (h1 < total) {
+                    const uint64_t k1 = hits[h1];
+                    const int d1 = (int)(uint32_t)k1 - (1 << 30);
+                    if ((k1 >> 32) != (k0 >> 32) || d1 - prev > CLUSTER_GAP) break;
+                    prev = d1;
+                    ++h1;
+                }
+                int center = (int)(uint32_t)k0 - (1 << 30), center_n = 0;
+                for (int a = h0; a < h1;) {
+                    int b = a + 1;
+                    while (b < h1 && hits[b] == hits[a]) ++b;
+                    if (b - a > center_n) {
+                        center_n = b - a;
+                        center = (int)(uint32_t)hits[a] - (1 << 30);
+                    }
+                    a = b;
+                }
+                Cand c{st, rf, center, h1 - h0};
+                int at = nc;
+                while (at > 0 && cand_before(c, best[at - 1])) --at;
+                if (at < MAXCAND) {
+                    const int last = nc < MAXCAND ? nc : MAXCAND - 1;
+                    for (int z = last; z > at; --z) best[z] = best[z - 1];
+                    best[at] = c;
+                    if (nc < MAXCAND) ++nc;
+                }
+                h0 = h1;
+            }
+            for (int c = 0; c < nc; ++c) A.cand[r * MAXCAND + c] = best[c];
+            A.n_cand[r] = nc;
+            const int base = atomicAdd(&A.counters[0], nc);
+            for (int c = 0; c < nc; ++c) A.work[base + c] = (int32_t)(r * MAXCAND + c);
+        }
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_dp: banded affine-gap DP, one wave64 per candidate
+// ---------------------------------------------------------------------------
+struct DpArgs {
+    DevReads R;
+    DevIndex I;
+    const int32_t *len_tab;
+    const Cand *cand;
+    const int32_t *work;
+    const int32_t *counters;  // [0] = number of work items
+    Slot *slot;
+    uint32_t *pool;
+    int32_t *pool_ctr;        // [0] used, [1] overflow
+    int64_t pool_cap;
+    int rows_pad;             // per-wave LDS row capacity (multiple of 8)
+    int wave_lds;             // bytes of LDS per wave
+    int oeI, exI, oeD, exD;
+};
+
+__device__ __forceinline__ int mm_pen(int qchar)
+{
+    int q = qchar - 33;
+    q = q < 0 ? 0 : (q > 40 ? 40 : q);
+    return 2 + q / 10;
+}
+
+template <int LOCAL>
+__global__ __launch_bounds__(256) void k_dp(DpArgs A)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wv = wave_uniform(threadIdx.x >> 6);
+    const int wpb = blockDim.x >> 6;
+    unsigned char *wbase = smem + (size_t)wv * A.wave_lds;
+    uint32_t *bits = (uint32_t *)wbase;                       // rows_pad/8 * 64
+    uint32_t *tab = bits + (A.rows_pad >> 3) * 64;            // rows_pad
+    uint8_t *refw = (uint8_t *)(tab + A.rows_pad);            // rows_pad + 64 (code*4)
+    uint8_t *rdc = refw + A.rows_pad + 64;                    // rows_pad
+    uint8_t *ops = rdc + A.rows_pad;                          // 2*rows_pad + 128
+    const int ma = LOCAL ? 2 : 0;
+    const int n_work = A.counters[0];
+    const int xD = lane * A.exD;                  // X = H1 + exD*lane
+    const int cF = -(A.oeD - A.exD) - A.exD * lane;
+
+    for (int w = blockIdx.x * wpb + wv; w < n_work; w += gridDim.x * wpb) {
+        const int sid = A.work[w];
+        const int64_t r = sid / MAXCAND;
+        const Cand cd = A.cand[sid];
+        const int m = A.R.len[r];
+        const int64_t roff = A.R.off[r];
+        const int reflen = A.I.ref_len[cd.ref];
+        const int64_t gref = A.I.ref_off[cd.ref];
+        const int d0 = cd.center - HALF;
+        const int strand = cd.strand;
+
+        // ---- stage per-row score tables, read codes and the ref window ----
+        for (int i = lane; i < m; i += 64) {
+            const int b = strand ? m - 1 - i : i;
+            uint32_t c = read_code(A.R, roff, b);
+            if (strand && c < 4) c = 3 - c;
+            const int pen = mm_pen(A.R.qual[roff + b]);
+            uint32_t tb = 0;
+            for (int g = 0; g < 5; ++g) {
+                const int sc = (c > 3 || g > 3) ? -NPEN : (c == (uint32_t)g ? ma : -pen);
+                tb |= (uint32_t)(sc + 8) << (4 * g);
+            }
+            tab[i] = tb;
+            rdc[i] = (uint8_t)c;
+        }
+        for (int x = lane; x < m + 64; x += 64) {
+            const int j = d0 + x;
+            const int g = (j >= 0 && j < reflen) ? A.I.codes[gref + j] : 4;
+            refw[x] = (uint8_t)(g * 4);
+        }
+        wave_sync();
+
+        // ---- DP over rows ----
+        int Hp = 0, Ep = NEG;
+        int bestH = NEG, bestI = 0;
+        uint32_t acc = 0;
+        for (int i = 0; i < m; ++i) {
+            const bool gap_ok = i >= GBAR && i < m - GBAR;
+            const int rc4 = refw[i + lane];
+            const uint32_t tb = tab[i];
+            const int s = (int)((tb >> rc4) & 15u) - 8;
+            const int Hd = Hp + s;
+            int E = NEG, eb = 0, H, fb = 0;
+            if (gap_ok) {
+                const int eu = dpp<DPP_WAVE_SHL1>(NEG, Ep) - A.exI;
+                const int hu = dpp<DPP_WAVE_SHL1>(NEG, Hp) - A.oeI;
+                E = imax(eu, hu);
+                eb = eu > hu;
+            }
+            int H1 = imax(Hd, E);
+            if (LOCAL) H1 = imax(H1, 0);
+            if (gap_ok) {
+                const int X = H1 + xD;
+                int P = X;
+                P = imax(P, dpp<DPP_ROW_SHR1>(NEG, P));
+                P = imax(P, dpp<DPP_ROW_SHR2>(NEG, P));
+                P = imax(P, dpp<DPP_ROW_SHR4>(NEG, P));
+                P = imax(P, dpp<DPP_ROW_SHR8>(NEG, P));
+                P = imax(P, dpp<DPP_ROW_BCAST15, 0xA>(NEG, P));
+                P = imax(P, dpp<DPP_ROW_BCAST31, 0xC>(NEG, P));
+                const int gt = P > X;
+                fb = dpp<DPP_WAVE_SHR1>(0, gt);
+                const int F = dpp<DPP_WAVE_SHR1>(NEG, P) + cF;
+                H = imax(H1, F);
+            } else {
+                H = H1;
+            }
+            const int src = (LOCAL && H == 0) ? 0 : (H == Hd ? 1 : (H == E ? 2 : 3));
+            acc |= (uint32_t)(src | (eb << 2) | (fb << 3)) << (4 * (i & 7));
+            if ((i & 7) == 7 || i == m - 1) {
+                bits[(i >> 3) * 64 + lane] = acc;
+                acc = 0;
+            }
+            if (LOCAL) {
+                if (H > bestH) { bestH = H; bestI = i; }
+            } else if (i == m - 1) {
+                bestH = H;
+                bestI = i;
+            }
+            Hp = H;
+            Ep = E;
+        }
+        // best cell: max score, then smallest row, then smallest lane
+        const long long key = (long long)bestH * 1048576ll + (long long)((1023 - bestI) << 6) +
+                              (long long)(63 - lane);
+        const long long bk = wave_max64(key);
+        const int best = (int)(bk >> 20);
+        const int bi = 1023 - (int)((bk >> 6) & 1023);
+        const int bl = 63 - (int)(bk & 63);
+        wave_sync();
+
+        Slot out{};
+        out.valid = 0;
+        out.strand = strand;
+        out.ref = cd.ref;
+        if (lane == 0) {
+            const int minsc = A.len_tab[(MAXLEN + 1) + m];
+            bool ok = !(LOCAL && best <= 0) && best >= minsc;
+            int nops = 0, first_j = 0, start_i = 0;
+            const int last_j = bi + d0 + bl;
+            if (ok) {
+                int i = bi, k = bl, state = 0;
+                for (;;) {
+                    const uint32_t nib = (bits[(i >> 3) * 64 + k] >> (4 * (i & 7))) & 15u;
+                    if (state == 0) {
+                        const int src = nib & 3;
+                        if (src == 0) break;
+                        if (src == 1) {
+                            ops[nops++] = MH_OP_M;
+                            first_j = i + d0 + k;
+                            if (--i < 0) break;
+                        } else {
+                            state = src == 2 ? 1 : 2;
+                        }
+                    } else if (state == 1) {
+                        ops[nops++] = MH_OP_I;
+                        state = (nib >> 2) & 1 ? 1 : 0;
+                        --i; ++k;
+                        if (i < 0 || k >= BAND) { ok = false; break; }
+                    } else {
+                        ops[nops++] = MH_OP_D;
+                        state = (nib >> 3) & 1 ? 2 : 0;
+                        --k;
+                        if (k < 0) { ok = false; break; }
+                    }
+                }
+                start_i = i + 1;
+            }
+            if (ok) {
+                for (int a = 0, z = nops - 1; a < z; ++a, --z) {
+                    const uint8_t t = ops[a]; ops[a] = ops[z]; ops[z] = t;
+                }
+                int nn = 0, ri = start_i, rj = first_j;
+                for (int o = 0; o < nops; ++o) {
+                    if (ops[o] == MH_OP_M) {
+                        const int g = refw[rj - d0] >> 2;
+                        if (rdc[ri] > 3 || g > 3) ++nn;
+                        ++ri; ++rj;
+                    } else if (ops[o] == MH_OP_I) {
+                        ++ri;
+                    } else {
+                        ++rj;
+                    }
+                }
+                if (nn > A.len_tab[2 * (MAXLEN + 1) + m]) ok = false;
+            }
+            int lo = 0, hi = nops, clipL = start_i, clipR = m - 1 - bi, jL = first_j, jR = last_j;
+            if (ok) {
+                while (lo < hi && !(ops[lo] == MH_OP_M && jL >= 0)) {
+                    if (ops[lo] == MH_OP_M) { ++clipL; ++jL; }
+                    else if (ops[lo] == MH_OP_I) ++clipL;
+                    else ++jL;
+                    ++lo;
+                }
+                while (hi > lo && !(ops[hi - 1] == MH_OP_M && jR < reflen)) {
+                    if (ops[hi - 1] == MH_OP_M) { ++clipR; --jR; }
+                    else if (ops[hi - 1] == MH_OP_I) ++clipR;
+                    else --jR;
+                    --hi;
+                }
+                if (lo >= hi) ok = false;
+            }
+            if (ok) {
+                // count runs first so the pool slice is allocated once
+                int nc = (clipL > 0) + (clipR > 0);
+                for (int o = lo; o < hi;) {
+                    int p = o + 1;
+                    while (p < hi && ops[p] == ops[o]) ++p;
+                    ++nc;
+                    o = p;
+                }
+                if (nc > MH_MAXOPS - 1) ok = false;
+                if (ok) {
+                    const int64_t base = atomicAdd(&A.pool_ctr[0], nc);
+                    if (base + nc > A.pool_cap) {
+                        atomicExch(&A.pool_ctr[1], 1);
+                        ok = false;
+                    } else {
+                        uint32_t *cg = A.pool + base;
+                        int n = 0, xm = 0, xo = 0, xg = 0;
+                        int ri = clipL, rj = jL;
+                        if (clipL) cg[n++] = ((uint32_t)clipL << 4) | MH_OP_S;
+                        for (int o = lo; o < hi;) {
+                            int p = o + 1;
+                            while (p < hi && ops[p] == ops[o]) ++p;
+                            const int len = p - o;
+                            cg[n++] = ((uint32_t)len << 4) | ops[o];
+                            if (ops[o] == MH_OP_M) {
+                                for (int x = 0; x < len; ++x, ++ri, ++rj) {
+                                    const int g = refw[rj - d0] >> 2;
+                                    const int rb = rdc[ri];
+                                    if (rb > 3 || g > 3 || rb != g) ++xm;
+                                }
+                            } else {
+                                ++xo;
+                                xg += len;
+                                if (ops[o] == MH_OP_I) ri += len; else rj += len;
+                            }
+                            o = p;
+                        }
+                        if (clipR) cg[n++] = ((uint32_t)clipR << 4) | MH_OP_S;
+                        out.valid = 1;
+                        out.pos = jL;
+                        out.end = jR + 1;
+                        out.score = best;
+                        out.xm = xm; out.xo = xo; out.xg = xg; out.nm = xm + xg;
+                        out.n_cigar = n;
+                        out.cig_off = (int32_t)base;
+                    }
+                }
+            }
+            A.slot[sid] = out;
+        }
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_pair: pairing, flags, MAPQ (unpinned V2-style table, see og_mapq)
+// ---------------------------------------------------------------------------
+__device__ int mapq_v2(int local, int perfect, int minsc, int best, int has_sec, int sec)
+{
+    int diff = perfect - minsc;
+    if (diff < 1) diff = 1;
+    const int over = best - minsc;
+#define GE(x, f10) (10ll * (long long)(x) >= (long long)(f10) * diff)
+    if (!has_sec) {
+        if (GE(over, 8)) return local ? 44 : 42;
+        if (GE(over, 7)) return 40;
+        if (GE(over, 6)) return 24;
+        if (GE(over, 5)) return 23;
+        if (GE(over, 4)) return 8;
+        if (GE(over, 3)) return 3;
+        return 0;
+    }
+    int bd = best - sec;
+    if (bd < 0) bd = -bd;
+    const int top = over == diff;
+    if (GE(bd, 10)) return top ? 39 : 33;
+    if (GE(bd, 9)) return top ? 38 : 27;
+    if (GE(bd, 8)) return top ? 37 : 26;
+    if (GE(bd, 7)) return top ? 36 : 25;
+    if (GE(bd, 6)) return top ? 35 : 21;
+    if (GE(bd, 5)) return top ? 34 : GE(over, 8) ? 25 : GE(over, 7) ? 16 : 5;
+    if (GE(bd, 4)) return top ? 33 : GE(over, 8) ? 21 : GE(over, 7) ? 14 : 4;
+    if (GE(bd, 3)) return top ? 32 : GE(over, 8) ? 18 : GE(over, 7) ? 10 : 3;
+    if (GE(bd, 2)) return top ? 31 : GE(over, 8) ? 16 : GE(over, 7) ? 9 : 2;
+    if (GE(bd, 1)) return top ? 30 : GE(over, 8) ? 12 : GE(over, 7) ? 7 : 1;
+    if (bd > 0) return GE(over, 6) ? 2 : 1;
+    return GE(over, 6) ? 1 : 0;
+#undef GE
+}
+
+struct PairArgs {
+    DevReads R;
+    const int32_t *len_tab;
+    const Slot *slot;
+    const int32_t *n_cand;
+    const int32_t *yf;
+    const uint32_t *pool;
+    Rec *rec;
+    int64_t *ref_stats;  // [5][n_refs] lines, filtered, mapped, first_row, first_mapped; unmapped, star
+    int n_refs;
+    int local;
+    int maxins;
+    int paired;
+};
+
+struct MateView {
+    int n;
+    int best;
+    Slot s[MAXCAND];
+};
+
+__device__ __forceinline__ void load_mate(const PairArgs &A, int64_t r, MateView &mv)
+{
+    mv.n = A.n_cand[r];
+    mv.best = -1;
+    for (int c = 0; c < mv.n; ++c) {
+        mv.s[c] = A.slot[r * MAXCAND + c];
+        if (mv.s[c].valid && (mv.best < 0 || mv.s[c].score > mv.s[mv.best].score)) mv.best = c;
+    }
+}
+
+__device__ __forceinline__ bool same_place(const Slot &x, const Slot &y)
+{
+    return x.strand == y.strand && x.ref == y.ref && x.pos == y.pos;
+}
+
+__device__ void clear_rec(Rec &o)
+{
+    o.ref = -1; o.pos = 0; o.rev = 0; o.score = 0; o.secbest = I32MIN; o.flag = 0; o.mapq = 0;
+    o.rnext = -2; o.pnext = 0; o.tlen = 0; o.sam_ref = -1; o.sam_pos = 0; o.xm = 0; o.xo = 0;
+    o.xg = 0; o.nm = 0; o.ys = I32MIN; o.yt = 0; o.yf = 0; o.n_cigar = 0; o.cig_off = 0;
+    o.maxm = 0;
+}
+
+__device__ void fill_aligned(const PairArgs &A, Rec &o, const MateView &mv, int chosen, int m)
+{
+    const Slot &a = mv.s[chosen];
+    o.ref = a.ref; o.pos = a.pos; o.rev = a.strand; o.score = a.score;
+    int sec = 0, has = 0;
+    for (int c = 0; c < mv.n; ++c) {
+        if (c == chosen || !mv.s[c].valid || same_place(mv.s[c], a)) continue;
+        if (!has || mv.s[c].score > sec) { sec = mv.s[c].score; has = 1; }
+    }
+    o.secbest = has ? sec : I32MIN;
+    o.mapq = mapq_v2(A.local, A.local ? 2 * m : 0, A.len_tab[(MAXLEN + 1) + m], a.score, has, sec);
+    o.xm = a.xm; o.xo = a.xo; o.xg = a.xg; o.nm = a.nm;
+    o.n_cigar = a.n_cigar;
+    o.cig_off = a.cig_off;
+    int mx = 0;
+    for (int k = 0; k < a.n_cigar; ++k) {
+        const uint32_t op = A.pool[a.cig_off + k];
+        if ((op & 15) == MH_OP_M && (int)(op >> 4) > mx) mx = (int)(op >> 4);
+    }
+    o.maxm = mx;
+    o.sam_ref = a.ref;
+    o.sam_pos = a.pos + 1;
+}
+
+__device__ __forceinline__ bool concordant(const Slot &x, const Slot &y, int maxins)
+{
+    if (x.ref != y.ref || x.strand == y.strand) return false;
+    const Slot &fw = x.strand == 0 ? x : y;
+    const Slot &rv = x.strand == 0 ? y : x;
+    const int lo = fw.pos < rv.pos ? fw.pos : rv.pos;
+    const int hi = fw.end > rv.end ? fw.end : rv.end;
+    if (hi - lo > maxins) return false;
+    if (rv.pos < fw.pos && rv.end < fw.end) return false;
+    return true;
+}
+
+__device__ void tally(const PairArgs &A, const Rec &o, int64_t row)
+{
+    const int n = A.n_refs;
+    if (o.sam_ref >= 0) {
+        atomicAdd((unsigned long long *)&A.ref_stats[o.sam_ref], 1ull);
+        if (!(o.flag & 4)) {
+            if (o.maxm > 50) atomicAdd((unsigned long long *)&A.ref_stats[n + o.sam_ref], 1ull);
+            atomicAdd((unsigned long long *)&A.ref_stats[2 * n + o.sam_ref], 1ull);
+        }
+        atomicMin((long long *)&A.ref_stats[3 * n + o.sam_ref], (long long)row);
+        if (!(o.flag & 4)) atomicMin((long long *)&A.ref_stats[4 * n + o.sam_ref], (long long)row);
+    } else {
+        atomicAdd((unsigned long long *)&A.ref_stats[5 * n + 1], 1ull);
+    }
+    if (o.flag & 4) atomicAdd((unsigned long long *)&A.ref_stats[5 * n], 1ull);
+}
+
+__global__ __launch_bounds__(256) void k_pair(PairArgs A)
+{
+    const int64_t units = A.paired ? A.R.n / 2 : A.R.n;
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        if (!A.paired) {
+            MateView mv;
+            load_mate(A, u, mv);
+            Rec o;
+            clear_rec(o);
+            o.yf = A.yf[u];
+            o.yt = 3;
+            if (mv.best >= 0) {
+                fill_aligned(A, o, mv, mv.best, A.R.len[u]);
+                o.flag = o.rev ? 0x10 : 0;
+            } else {
+                o.flag = 0x4;
+            }
+            A.rec[u] = o;
+            tally(A, o, u);
+            continue;
+        }
+        const int64_t r1 = 2 * u, r2 = 2 * u + 1;
+        MateView m1, m2;
+        load_mate(A, r1, m1);
+        load_mate(A, r2, m2);
+        Rec o1, o2;
+        clear_rec(o1);
+        clear_rec(o2);
+        o1.yf = A.yf[r1];
+        o2.yf = A.yf[r2];
+        int c1 = m1.best, c2 = m2.best, conc = 0;
+        long long best_sum = -9223372036854775807ll - 1;
+        for (int x = 0; x < m1.n; ++x) {
+            if (!m1.s[x].valid) continue;
+            for (int y = 0; y < m2.n; ++y) {
+                if (!m2.s[y].valid) continue;
+                if (!concordant(m1.s[x], m2.s[y], A.maxins)) continue;
+                const long long s = (long long)m1.s[x].score + m2.s[y].score;
+                if (s > best_sum) { best_sum = s; c1 = x; c2 = y; conc = 1; }
+            }
+        }
+        const int al1 = c1 >= 0, al2 = c2 >= 0;
+        if (al1) fill_aligned(A, o1, m1, c1, A.R.len[r1]);
+        if (al2) fill_aligned(A, o2, m2, c2, A.R.len[r2]);
+        int f1 = 0x1 | 0x40, f2 = 0x1 | 0x80;
+        if (conc) { f1 |= 0x2; f2 |= 0x2; }
+        if (!al1) { f1 |= 0x4; f2 |= 0x8; }
+        if (!al2) { f2 |= 0x4; f1 |= 0x8; }
+        if (al1 && o1.rev) { f1 |= 0x10; f2 |= 0x20; }
+        if (al2 && o2.rev) { f2 |= 0x10; f1 |= 0x20; }
+        o1.flag = f1;
+        o2.flag = f2;
+        const int yt = conc ? 0 : (al1 && al2) ? 1 : 2;
+        o1.yt = o2.yt = yt;
+        if (al1 && al2) {
+            o1.ys = o2.score;
+            o2.ys = o1.score;
+            if (o1.ref == o2.ref) {
+                o1.rnext = o2.rnext = -1;
+                const Slot &a = m1.s[c1], &b = m2.s[c2];
+                const int lo = a.pos < b.pos ? a.pos : b.pos;
+                const int hi = a.end > b.end ? a.end : b.end;
+                const int t = hi - lo;
+                const bool first1 = a.pos <= b.pos;
+                o1.tlen = first1 ? t : -t;
+                o2.tlen = first1 ? -t : t;
+            } else {
+                o1.rnext = o2.ref;
+                o2.rnext = o1.ref;
+            }
+            o1.pnext = o2.sam_pos;
+            o2.pnext = o1.sam_pos;
+        } else if (al1 || al2) {
+            Rec &Al = al1 ? o1 : o2;
+            Rec &Un = al1 ? o2 : o1;
+            Un.sam_ref = Al.sam_ref;
+            Un.sam_pos = Al.sam_pos;
+            Al.rnext = Un.rnext = -1;
+            Al.pnext = Al.sam_pos;
+            Un.pnext = Al.sam_pos;
+            Un.ys = Al.score;
+        }
+        A.rec[r1] = o1;
+        A.rec[r2] = o2;
+        tally(A, o1, r1);
+        tally(A, o2, r2);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host driver of one mapping pass
+// ---------------------------------------------------------------------------
+static int ensure_map_buffers(Ctx &c)
+{
+    MapState &M = c.map;
+    const int64_t n = c.reads.n;
+    if (M.cap_reads < n || M.cand == nullptr) {
+        hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work);
+        hipFree(M.slot); hipFree(M.rec);
+        const int64_t cap = n > 0 ? n : 1;
+        MH_HIP(hipMalloc(&M.cand, sizeof(Cand) * cap * MAXCAND));
+        MH_HIP(hipMalloc(&M.n_cand, sizeof(int32_t) * cap));
+        MH_HIP(hipMalloc(&M.yf, sizeof(int32_t) * cap));
+        MH_HIP(hipMalloc(&M.work, sizeof(int32_t) * cap * MAXCAND));
+        MH_HIP(hipMalloc(&M.slot, sizeof(Slot) * cap * MAXCAND));
+        MH_HIP(hipMalloc(&M.rec, sizeof(Rec) * cap));
+        M.cap_reads = cap;
+    }
+    if (M.counters == nullptr) MH_HIP(hipMalloc(&M.counters, sizeof(int32_t) * 4));
+    if (M.cap_refs < c.index.n_refs || M.ref_stats == nullptr) {
+        hipFree(M.ref_stats);
+        const int cr = c.index.n_refs > 0 ? c.index.n_refs : 1;
+        MH_HIP(hipMalloc(&M.ref_stats, sizeof(int64_t) * (5 * cr + 2)));
+        M.cap_refs = cr;
+    }
+    if (M.pool == nullptr) {
+        M.pool_cap = (n > 0 ? n : 1) * 8 + 4096;
+        MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * M.pool_cap));
+    }
+    return 0;
+}
+
+__global__ void k_init_stats(int64_t *s, int n_refs)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 5 * n_refs + 2; i += gridDim.x * blockDim.x)
+        s[i] = (i >= 3 * n_refs && i < 5 * n_refs) ? INT64_MAX : 0;
+}
+
+__global__ void k_fix_first(int64_t *s, int n_refs)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * n_refs; i += gridDim.x * blockDim.x)
+        if (s[3 * n_refs + i] == INT64_MAX) s[3 * n_refs + i] = -1;
+}
+
+int run_map(Ctx &c, const mh_params &par)
+{
+    if (c.index.n_refs <= 0 || c.index.hkey == nullptr) {
+        set_error("mh_map: no reference index (call mh_index_build first)");
+        return -3;
+    }
+    if (par.mode != MH_E2E && par.mode != MH_LOCAL) { set_error("mh_map: bad mode"); return -3; }
+    const int SL = par.mode == MH_LOCAL ? 20 : 22;
+    if (c.index.seedlen != SL) {
+        set_error("mh_map: index seed length %d does not match mode (%d)", c.index.seedlen, SL);
+        return -3;
+    }
+    if (c.len_tab == nullptr || c.len_tab_mode != par.mode) {
+        set_error("mh_map: length tables not prepared");
+        return -3;
+    }
+    if (int st = ensure_map_buffers(c)) return st;
+    MapState &M = c.map;
+    const int64_t n = c.reads.n;
+    M.n_reads = n;
+    M.n_refs = c.index.n_refs;
+    M.par = par;
+    hipStream_t s = c.stream;
+    MH_HIP(hipMemsetAsync(M.counters, 0, sizeof(int32_t) * 4, s));
+    hipLaunchKernelGGL(k_init_stats, dim3(64), dim3(256), 0, s, M.ref_stats, M.n_refs);
+    if (n > 0) {
+        SeedArgs sa{c.reads, c.index, par.mode, c.len_tab, M.cand, M.n_cand, M.yf, M.work, M.counters};
+        int64_t blocks = (n + 3) / 4;
+        if (blocks > 1 << 16) blocks = 1 << 16;
+        hipLaunchKernelGGL(k_seed, dim3((unsigned)blocks), dim3(256), 0, s, sa);
+        MH_HIP(hipGetLastError());
+
+        const int rows_pad = ((c.reads.max_len + 7) / 8) * 8;
+        const int wave_lds = ((rows_pad * 40 + 192) + 15) & ~15;
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            MH_HIP(hipMemsetAsync(M.counters + 1, 0, sizeof(int32_t) * 2, s));
+            DpArgs da{c.reads, c.index, c.len_tab, M.cand, M.work, M.counters, M.slot, M.pool,
+                      M.counters + 1, M.pool_cap, rows_pad, wave_lds,
+                      par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext,
+                      par.rdg_ext};
+            int wpb = (160 * 1024) / wave_lds;
+            if (wpb > 4) wpb = 4;
+            if (wpb < 1) { set_error("mh_map: reads too long for LDS"); return -3; }
+            int64_t dblocks = (n * 2 + wpb - 1) / wpb;
+            if (dblocks > 256 * 48) dblocks = 256 * 48;
+            if (par.mode == MH_LOCAL) {
+                MH_HIP(hipFuncSetAttribute((const void *)k_dp<1>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, wpb * wave_lds));
+                hipLaunchKernelGGL(k_dp<1>, dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
+            } else {
+                MH_HIP(hipFuncSetAttribute((const void *)k_dp<0>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, wpb * wave_lds));
+                hipLaunchKernelGGL(k_dp<0>, dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
+            }
+            MH_HIP(hipGetLastError());
+            int32_t ctr[3];
+            MH_HIP(hipMemcpyAsync(ctr, M.counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
+            MH_HIP(hipStreamSynchronize(s));
+            if (!ctr[2]) break;
+            // CIGAR pool overflow: grow to what was asked for and redo the extensions
+            hipFree(M.pool);
+            M.pool_cap = (int64_t)ctr[1] * 2 + 4096;
+            MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * M.pool_cap));
+            if (attempt == 1) { set_error("mh_map: CIGAR pool overflow"); return -2; }
+        }
+        PairArgs pa{c.reads, c.len_tab, M.slot, M.n_cand, M.yf, M.pool, M.rec, M.ref_stats,
+                    M.n_refs, par.mode == MH_LOCAL, par.maxins, c.reads.paired};
+        const int64_t units = c.reads.paired ? n / 2 : n;
+        int64_t pblocks = (units + 255) / 256;
+        if (pblocks > 1 << 16) pblocks = 1 << 16;
+        if (pblocks < 1) pblocks = 1;
+        hipLaunchKernelGGL(k_pair, dim3((unsigned)pblocks), dim3(256), 0, s, pa);
+        MH_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_fix_first, dim3(8), dim3(256), 0, s, M.ref_stats, M.n_refs);
+    MH_HIP(hipGetLastError());
+    M.valid = true;
+    return 0;
+}
+
+}  // namespace mh

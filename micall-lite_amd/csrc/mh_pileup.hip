@@ -1,0 +1,598 @@
+// mh_pileup.hip -- consensus pileup on gfx950: the counting half of
+// remap.sam_to_conseqs (micall/core/remap.py:141-306), one wave64 per read
+// pair (matchmaker unit):
+//   merge_reads    remap.py:86-126    which mates count, the rname check
+//   apply_cigar    sam2aln.py:84-153  each mate in reference coordinates
+//   merge_pairs    sam2aln.py:156-237 per-position merge, lane-parallel
+//   merge_inserts  sam2aln.py:240-273 (lane 0; rare)
+//   update_counts  remap.py:271-306   int32 atomics into dense A/C/G/T
+//                                     counters, 'N'/'-' flags, sparse events
+// The refmap of the reference is order-independent except for its key
+// order, which is recovered from first_unit (atomicMin), so results are
+// deterministic.  Bit-for-bit specification: oracle/og_pileup.c.
+#include "mh_internal.h"
+
+namespace mh {
+
+constexpr int PU_MAXREF = 2048;   // reference span per mate staged in LDS
+constexpr int PU_INSBUF = 2048;   // merged insertion bytes per unit
+
+struct RowV {
+    int present, flag, ref, pos, n_cigar, rev, m;
+    const uint32_t *cig;
+    int64_t roff;
+};
+
+struct PileArgs {
+    // source 0: mapped records
+    const Rec *rec;
+    const uint32_t *pool;
+    DevReads R;           // reads of source 0, or rows' reads for source 1
+    int paired;
+    // source 1: rows
+    const int32_t *flag, *ref, *pos, *cig_off, *n_cigar;
+    const uint32_t *cigar;
+    const int64_t *units;
+    int64_t n_units;
+    // outputs
+    int n_refs;
+    int32_t cap;
+    int32_t *dense;
+    uint8_t *nflag, *dflag;
+    unsigned long long *read_counts;
+    long long *first_unit;
+    int32_t *max_pos;
+    int32_t *ev;
+    char *ev_pool;
+    long long ev_cap, pool_cap;
+    unsigned long long *ev_ctr;  // [0] events, [1] pool bytes, [2] overflow, [3] error
+    int q_cutoff;
+};
+
+template <int SRC>
+__device__ __forceinline__ void load_row(const PileArgs &A, int64_t row, RowV &v)
+{
+    v.present = 0;
+    if (row < 0) return;
+    if (SRC == 0) {
+        const Rec &r = A.rec[row];
+        if (r.sam_ref < 0) return;      // RNAME '*' is not in @SQ (matchmaker)
+        v.present = 1;
+        v.flag = r.flag;
+        v.ref = r.sam_ref;
+        v.pos = r.sam_pos;
+        v.n_cigar = (r.flag & 4) ? 0 : r.n_cigar;
+        v.cig = A.pool + r.cig_off;
+        v.rev = (r.flag & 4) ? 0 : r.rev;
+    } else {
+        v.present = 1;
+        v.flag = A.flag[row];
+        v.ref = A.ref[row];
+        v.pos = A.pos[row];
+        v.n_cigar = A.n_cigar[row];
+        v.cig = A.cigar + A.cig_off[row];
+        v.rev = 0;
+    }
+    v.m = A.R.len[row];
+    v.roff = A.R.off[row];
+}
+
+__device__ __forceinline__ void sam_base(const DevReads &R, const RowV &v, int x, char &c, char &q)
+{
+    const int b = v.rev ? v.m - 1 - x : x;
+    const int64_t g = v.roff + b;
+    uint32_t code = ((R.nmask[g >> 5] >> (g & 31)) & 1) ? 4 : (R.seq2[g >> 4] >> (2 * (g & 15))) & 3;
+    if (v.rev && code < 4) code = 3 - code;
+    c = "ACGTN"[code];
+    q = (char)R.qual[g];
+}
+
+struct MateLds {
+    char c[PU_MAXREF];
+    char q[PU_MAXREF];
+    int32_t opref[MH_MAXOPS + 1];   // reference offset at the start of each op
+    int32_t opread[MH_MAXOPS + 1];  // read offset at the start of each op
+};
+
+struct UnitLds {
+    MateLds mate[2];
+    int32_t ins_key[2 * MH_MAXOPS];
+    int32_t ins_off[2 * MH_MAXOPS];   // into insbuf
+    int32_t ins_len[2 * MH_MAXOPS];
+    char insbuf[PU_INSBUF];
+    int32_t n_ins;
+    int32_t misc[8];
+};
+
+// merge_pairs on two short strings without '-' (insertions), sam2aln.py:156-237
+__device__ int merge_ins_strings(const char *s1, const char *q1, int l1, const char *s2,
+                                 const char *q2, int l2, int q_cutoff, char *out)
+{
+    if (l1 > l2) {
+        const char *t = s1; s1 = s2; s2 = t;
+        t = q1; q1 = q2; q2 = t;
+        int x = l1; l1 = l2; l2 = x;
+    }
+    const unsigned char cut = (unsigned char)(q_cutoff + 33);
+    for (int i = 0; i < l2; ++i) {
+        const char c2 = s2[i];
+        const unsigned char b = (unsigned char)q2[i];
+        if (i < l1) {
+            const char c1 = s1[i];
+            const unsigned char a = (unsigned char)q1[i];
+            if (c1 == c2) {
+                out[i] = (a > cut || b > cut) ? c1 : 'N';
+            } else {
+                const int dq = (int)b - (int)a;
+                if ((dq < 0 ? -dq : dq) >= 5) {
+                    const unsigned char m2 = b > cut ? b : cut, m1 = a > cut ? a : cut;
+                    out[i] = a > m2 ? c1 : (b > m1 ? c2 : 'N');
+                } else {
+                    out[i] = 'N';
+                }
+            }
+        } else {
+            out[i] = b > cut ? c2 : 'N';
+        }
+    }
+    return l2;
+}
+
+template <int SRC>
+__global__ __launch_bounds__(256) void k_pileup(PileArgs A)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wpb = blockDim.x >> 6;
+    UnitLds &L = *reinterpret_cast<UnitLds *>(smem + (size_t)wv * sizeof(UnitLds));
+    const unsigned char cut = (unsigned char)(A.q_cutoff + 33);
+
+    for (int64_t u = (int64_t)blockIdx.x * wpb + wv; u < A.n_units; u += (int64_t)gridDim.x * wpb) {
+        int64_t row1, row2;
+        if (SRC == 0) {
+            row1 = A.paired ? 2 * u : u;
+            row2 = A.paired ? 2 * u + 1 : -1;
+        } else {
+            row1 = A.units[2 * u];
+            row2 = A.units[2 * u + 1];
+        }
+        RowV r1, r2;
+        load_row<SRC>(A, row1, r1);
+        load_row<SRC>(A, row2, r2);
+        if (SRC == 0 && !r1.present && r2.present) { r1 = r2; r2.present = 0; }  // unpaired view
+        if (!r1.present) continue;
+        if (r2.present && r1.ref != r2.ref) continue;           // remap.py:96-98
+        RowV mp[2];
+        int nm = 0;
+        if (!(r1.flag & 4)) mp[nm++] = r1;
+        if (r2.present && !(r2.flag & 4)) mp[nm++] = r2;
+        if (nm == 0) continue;                                 // remap.py:111-112
+        const int ref = r1.ref;
+        if (ref < 0 || ref >= A.n_refs) {
+            if (lane == 0) atomicExch(&A.ev_ctr[3], 1ull);
+            continue;
+        }
+
+        // ---- apply_cigar: op offsets (lane 0), then expand lane-parallel ----
+        int pad[2], len[2], bad = 0;
+        for (int k = 0; k < nm; ++k) {
+            int rf = 0, rd = 0;
+            for (int o = 0; o < mp[k].n_cigar; ++o) {
+                const uint32_t op = mp[k].cig[o];
+                const int n = (int)(op >> 4), t = (int)(op & 15);
+                if (lane == 0 && o < MH_MAXOPS) { L.mate[k].opref[o] = rf; L.mate[k].opread[o] = rd; }
+                if (t == MH_OP_M) { rf += n; rd += n; }
+                else if (t == MH_OP_D) rf += n;
+                else if (t == MH_OP_I || t == MH_OP_S) rd += n;
+                else bad = 1;
+                if (rd > mp[k].m) bad = 1;
+            }
+            if (lane == 0 && mp[k].n_cigar <= MH_MAXOPS) { L.mate[k].opref[mp[k].n_cigar] = rf; L.mate[k].opread[mp[k].n_cigar] = rd; }
+            if (rd != mp[k].m || rf > PU_MAXREF || mp[k].pos < 1 || mp[k].n_cigar > MH_MAXOPS) bad = 1;
+            pad[k] = mp[k].pos - 1;
+            len[k] = pad[k] + rf;
+        }
+        if (bad) {
+            if (lane == 0) atomicExch(&A.ev_ctr[3], 1ull);
+            continue;
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int k = 0; k < nm; ++k) {
+            const int span = len[k] - pad[k];
+            for (int t = lane; t < span; t += 64) {
+                int o = 0;
+                while (L.mate[k].opref[o + 1] <= t ||
+                       ((mp[k].cig[o] & 15) != MH_OP_M && (mp[k].cig[o] & 15) != MH_OP_D))
+                    ++o;
+                const uint32_t op = mp[k].cig[o];
+                char c = '-', q = ' ';
+                if ((op & 15) == MH_OP_M) sam_base(A.R, mp[k], L.mate[k].opread[o] + (t - L.mate[k].opref[o]), c, q);
+                L.mate[k].c[t] = c;
+                L.mate[k].q[t] = q;
+            }
+        }
+        // ---- merge_inserts (lane 0): keys left + pad, sam2aln.py:133-135 ----
+        if (lane == 0) {
+            int n = 0, used = 0;
+            // ins1 entries passing quality
+            for (int pass = 0; pass < nm; ++pass) {
+                const RowV &v = mp[pass];
+                for (int o = 0; o < v.n_cigar; ++o) {
+                    if ((v.cig[o] & 15) != MH_OP_I) continue;
+                    const int il = (int)(v.cig[o] >> 4);
+                    const int key = L.mate[pass].opread[o] + pad[pass];
+                    char tc[1], tq[1];
+                    unsigned char mn = 255;
+                    for (int x = 0; x < il; ++x) {
+                        sam_base(A.R, v, L.mate[pass].opread[o] + x, tc[0], tq[0]);
+                        if ((unsigned char)tq[0] < mn) mn = (unsigned char)tq[0];
+                    }
+                    if (!(mn > cut)) continue;
+                    if (used + 2 * il + 2 > PU_INSBUF) { atomicExch(&A.ev_ctr[3], 1ull); continue; }
+                    // locate an existing entry with the same key (ins1 vs ins2)
+                    int at = -1;
+                    for (int z = 0; z < n; ++z) if (L.ins_key[z] == key) at = z;
+                    char *dst = L.insbuf + used;
+                    int outlen;
+                    if (pass == 0) {
+                        for (int x = 0; x < il; ++x) sam_base(A.R, v, L.mate[pass].opread[o] + x, dst[x], tc[0]);
+                        outlen = il;
+                    } else {
+                        // ins1 at this key (even if it failed quality) merges with ins2
+                        char s1[PU_INSBUF / 8], q1[PU_INSBUF / 8], s2[PU_INSBUF / 8], q2[PU_INSBUF / 8];
+                        int l1 = 0;
+                        const RowV &w = mp[0];
+                        for (int o1 = 0; o1 < w.n_cigar; ++o1) {
+                            if ((w.cig[o1] & 15) != MH_OP_I) continue;
+                            if (L.mate[0].opread[o1] + pad[0] != key) continue;
+                            l1 = (int)(w.cig[o1] >> 4);
+                            if (l1 > PU_INSBUF / 8) l1 = PU_INSBUF / 8;
+                            for (int x = 0; x < l1; ++x) sam_base(A.R, w, L.mate[0].opread[o1] + x, s1[x], q1[x]);
+                        }
+                        const int l2 = il > PU_INSBUF / 8 ? PU_INSBUF / 8 : il;
+                        for (int x = 0; x < l2; ++x) sam_base(A.R, v, L.mate[pass].opread[o] + x, s2[x], q2[x]);
+                        outlen = merge_ins_strings(s1, q1, l1, s2, q2, l2, A.q_cutoff, dst);
+                    }
+                    if (at < 0) at = n++;
+                    L.ins_key[at] = key;
+                    L.ins_off[at] = used;
+                    L.ins_len[at] = outlen;
+                    used += outlen;
+                }
+            }
+            L.n_ins = n;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+
+        // ---- merge_pairs positions: seq1 = shorter padded read ----
+        int a = 0, b = 1;             // mate indices of seq1 / seq2
+        int len1, len2, pad1, pad2;
+        if (nm == 1) {
+            a = -1; b = 0;
+            len1 = 0; pad1 = 0;
+        } else if (len[0] > len[1]) {
+            a = 1; b = 0;
+        }
+        if (a >= 0) { len1 = len[a]; pad1 = pad[a]; }
+        len2 = len[b];
+        pad2 = pad[b];
+        auto ch1 = [&](int i, char &c, char &q) {
+            if (i < pad1) { c = '-'; q = '!'; } else { c = L.mate[a].c[i - pad1]; q = L.mate[a].q[i - pad1]; }
+        };
+        auto ch2 = [&](int i, char &c, char &q) {
+            if (i < pad2) { c = '-'; q = '!'; } else { c = L.mate[b].c[i - pad2]; q = L.mate[b].q[i - pad2]; }
+        };
+        const int lo = a >= 0 ? (pad1 < pad2 ? pad1 : pad2) : pad2;
+        // first index where seq2 is not '-' (is_reverse_started) and where the
+        // forward read starts (first i < len1 not both '-')
+        int rev_start = 1 << 30, fwd_start = 1 << 30;
+        for (int i0 = lo; i0 < len2; i0 += 64) {
+            const int i = i0 + lane;
+            int rs = 1 << 30, fs = 1 << 30;
+            if (i < len2) {
+                char c2, q2;
+                ch2(i, c2, q2);
+                if (c2 != '-') rs = i;
+                if (a >= 0 && i < len1) {
+                    char c1, q1;
+                    ch1(i, c1, q1);
+                    if (!(c1 == '-' && c2 == '-')) fs = i;
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                rs = min(rs, __shfl_xor(rs, o, 64));
+                fs = min(fs, __shfl_xor(fs, o, 64));
+            }
+            rev_start = min(rev_start, rs);
+            fwd_start = min(fwd_start, fs);
+            if (rev_start < (1 << 30) && (a < 0 || fwd_start < (1 << 30) || i0 + 64 >= len1)) break;
+        }
+        const bool fwd = a >= 0 && fwd_start < len1;
+        // mseq = seq1[:i] + ... when the forward read starts, else only the
+        // part past len1 is appended (sam2aln.py:192-199, :220-230)
+        const int shift = fwd ? 0 : len1;
+        // The first mseq character that is not '-' starts update_counts
+        // (remap.py:286-289): the merged base at fwd_start (never '-', a gap's
+        // quality ' '/'!' cannot win), else the first index >= len1 (a base or
+        // 'n').  From there on every position counts, so the loop starts at
+        // fwd_start, or at rev_start skipping the 'n' interval before it.
+        const int begin = fwd ? fwd_start : rev_start;
+
+        // ---- update_counts over mseq (remap.py:284-301) ----
+        int mxp = 0;
+        int err = 0;
+        const int n_ins = L.n_ins;
+        for (int i0 = begin; i0 < len2; i0 += 64) {
+            const int i = i0 + lane;
+            if (i >= len2) break;
+            char mc;
+            char c2, q2;
+            ch2(i, c2, q2);
+            if (i < len1) {
+                char c1, q1;
+                ch1(i, c1, q1);
+                const unsigned char qa = (unsigned char)q1, qb = (unsigned char)q2;
+                if (c1 == '-' && c2 == '-') mc = '-';
+                else if (c1 == c2) mc = (qa > cut || qb > cut) ? c1 : 'N';
+                else {
+                    const int dq = (int)qb - (int)qa;
+                    if ((dq < 0 ? -dq : dq) >= 5) {
+                        const unsigned char m2 = qb > cut ? qb : cut, m1 = qa > cut ? qa : cut;
+                        mc = qa > m2 ? c1 : (qb > m1 ? c2 : 'N');
+                    } else {
+                        mc = 'N';
+                    }
+                }
+            } else {
+                if (c2 == '-') mc = i >= rev_start ? '-' : 'n';
+                else mc = (unsigned char)q2 > cut ? c2 : 'N';
+            }
+            if (mc == 'n') continue;
+            const int P = i - shift + 1;
+            if (P > A.cap) { err = 1; continue; }
+            mxp = P > mxp ? P : mxp;
+            const int64_t cell = (int64_t)ref * A.cap + (P - 1);
+            if (mc == 'N') { A.nflag[cell] = 1; continue; }
+            if (mc == '-') { A.dflag[cell] = 1; continue; }
+            int hit = -1;
+            for (int z = 0; z < n_ins; ++z)
+                if (L.ins_key[z] == P) hit = z;
+            if (hit >= 0 && L.ins_len[hit] > 0 && L.ins_len[hit] % 3 == 0) {
+                const int tl = 1 + L.ins_len[hit];
+                const unsigned long long e = atomicAdd(&A.ev_ctr[0], 1ull);
+                const unsigned long long p = atomicAdd(&A.ev_ctr[1], (unsigned long long)tl);
+                if ((long long)e < A.ev_cap && (long long)(p + tl) <= A.pool_cap) {
+                    A.ev[4 * e] = ref;
+                    A.ev[4 * e + 1] = P;
+                    A.ev[4 * e + 2] = (int32_t)p;
+                    A.ev[4 * e + 3] = tl;
+                    A.ev_pool[p] = mc;
+                    for (int x = 0; x < tl - 1; ++x) A.ev_pool[p + 1 + x] = L.insbuf[L.ins_off[hit] + x];
+                } else {
+                    atomicExch(&A.ev_ctr[2], 1ull);
+                }
+            } else {
+                const int code = mc == 'A' ? 0 : mc == 'C' ? 1 : mc == 'G' ? 2 : 3;
+                atomicAdd(&A.dense[cell * 4 + code], 1);
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            mxp = max(mxp, __shfl_xor(mxp, o, 64));
+            err |= __shfl_xor(err, o, 64);
+        }
+        if (lane == 0) {
+            atomicAdd(&A.read_counts[ref], 1ull);
+            atomicMin(&A.first_unit[ref], (long long)u);
+            if (mxp > 0) atomicMax(&A.max_pos[ref], mxp);
+            if (err) atomicExch(&A.ev_ctr[3], 1ull);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+__global__ void k_pile_init(long long *first_unit, int32_t *max_pos, int n)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        first_unit[i] = INT64_MAX;
+        max_pos[i] = 0;
+    }
+}
+
+__global__ void k_pile_fix(long long *first_unit, int n)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        if (first_unit[i] == INT64_MAX) first_unit[i] = -1;
+}
+
+static int ensure_pile(Ctx &c)
+{
+    PileState &P = c.pile;
+    const int64_t cells = (int64_t)(P.n_refs > 0 ? P.n_refs : 1) * P.cap;
+    if (P.alloc_cells < cells) {
+        hipFree(P.dense); hipFree(P.nflag); hipFree(P.dflag);
+        MH_HIP(hipMalloc(&P.dense, sizeof(int32_t) * 4 * cells));
+        MH_HIP(hipMalloc(&P.nflag, cells));
+        MH_HIP(hipMalloc(&P.dflag, cells));
+        P.alloc_cells = cells;
+    }
+    if (P.alloc_refs < (P.n_refs > 0 ? P.n_refs : 1)) {
+        hipFree(P.read_counts); hipFree(P.first_unit); hipFree(P.max_pos);
+        const int nr = P.n_refs > 0 ? P.n_refs : 1;
+        MH_HIP(hipMalloc(&P.read_counts, sizeof(int64_t) * nr));
+        MH_HIP(hipMalloc(&P.first_unit, sizeof(int64_t) * nr));
+        MH_HIP(hipMalloc(&P.max_pos, sizeof(int32_t) * nr));
+        P.alloc_refs = nr;
+    }
+    if (!P.ev_counters) MH_HIP(hipMalloc(&P.ev_counters, sizeof(int64_t) * 4));
+    if (!P.ev) {
+        P.ev_cap = 1 << 16;
+        P.pool_cap = 1 << 20;
+        MH_HIP(hipMalloc(&P.ev, sizeof(int32_t) * 4 * P.ev_cap));
+        MH_HIP(hipMalloc(&P.ev_pool, P.pool_cap));
+    }
+    return 0;
+}
+
+int run_pileup(Ctx &c, int source, int q_cutoff)
+{
+    PileState &P = c.pile;
+    int64_t n_units;
+    const DevReads *R;
+    if (source == 0) {
+        if (!c.map.valid) { set_error("mh_pileup: no mapping results"); return -3; }
+        R = &c.reads;
+        n_units = c.reads.paired ? c.reads.n / 2 : c.reads.n;
+    } else {
+        R = &c.rows.reads;
+        n_units = c.rows.n_units;
+    }
+    if (int st = ensure_pile(c)) return st;
+    hipStream_t s = c.stream;
+    const int64_t cells = (int64_t)P.n_refs * P.cap;
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        MH_HIP(hipMemsetAsync(P.dense, 0, sizeof(int32_t) * 4 * (cells > 0 ? cells : 1), s));
+        MH_HIP(hipMemsetAsync(P.nflag, 0, cells > 0 ? cells : 1, s));
+        MH_HIP(hipMemsetAsync(P.dflag, 0, cells > 0 ? cells : 1, s));
+        MH_HIP(hipMemsetAsync(P.read_counts, 0, sizeof(int64_t) * (P.n_refs > 0 ? P.n_refs : 1), s));
+        MH_HIP(hipMemsetAsync(P.ev_counters, 0, sizeof(int64_t) * 4, s));
+        hipLaunchKernelGGL(k_pile_init, dim3(8), dim3(256), 0, s, (long long *)P.first_unit,
+                           P.max_pos, P.n_refs);
+        PileArgs A{};
+        A.rec = c.map.rec;
+        A.pool = c.map.pool;
+        A.R = *R;
+        A.paired = source == 0 ? c.reads.paired : 0;
+        A.flag = c.rows.flag; A.ref = c.rows.ref; A.pos = c.rows.pos; A.cig_off = c.rows.cig_off;
+        A.n_cigar = c.rows.n_cigar; A.cigar = c.rows.cigar; A.units = c.rows.units;
+        A.n_units = n_units;
+        A.n_refs = P.n_refs;
+        A.cap = P.cap;
+        A.dense = P.dense; A.nflag = P.nflag; A.dflag = P.dflag;
+        A.read_counts = (unsigned long long *)P.read_counts;
+        A.first_unit = (long long *)P.first_unit;
+        A.max_pos = P.max_pos;
+        A.ev = P.ev; A.ev_pool = P.ev_pool; A.ev_cap = P.ev_cap; A.pool_cap = P.pool_cap;
+        A.ev_ctr = (unsigned long long *)P.ev_counters;
+        A.q_cutoff = q_cutoff;
+        if (n_units > 0) {
+            const int wpb = 2;
+            const size_t lds = sizeof(UnitLds) * wpb;
+            int64_t blocks = (n_units + wpb - 1) / wpb;
+            if (blocks > 256 * 32) blocks = 256 * 32;
+            if (source == 0) {
+                MH_HIP(hipFuncSetAttribute((const void *)k_pileup<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                hipLaunchKernelGGL(k_pileup<0>, dim3((unsigned)blocks), dim3(64 * wpb), lds, s, A);
+            } else {
+                MH_HIP(hipFuncSetAttribute((const void *)k_pileup<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                hipLaunchKernelGGL(k_pileup<1>, dim3((unsigned)blocks), dim3(64 * wpb), lds, s, A);
+            }
+            MH_HIP(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_pile_fix, dim3(8), dim3(256), 0, s, (long long *)P.first_unit, P.n_refs);
+        int64_t ctr[4];
+        MH_HIP(hipMemcpyAsync(ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
+        MH_HIP(hipStreamSynchronize(s));
+        if (ctr[3]) { set_error("mh_pileup: malformed alignment row (CIGAR/position)"); return -3; }
+        if (!ctr[2]) return 0;
+        hipFree(P.ev); hipFree(P.ev_pool);
+        P.ev_cap = ctr[0] * 2 + 1024;
+        P.pool_cap = ctr[1] * 2 + 4096;
+        MH_HIP(hipMalloc(&P.ev, sizeof(int32_t) * 4 * P.ev_cap));
+        MH_HIP(hipMalloc(&P.ev_pool, P.pool_cap));
+    }
+    set_error("mh_pileup: event buffer overflow");
+    return -2;
+}
+
+// ---- multi-GPU exchange layout ---------------------------------------------
+__global__ void k_pile_export(const int32_t *dense, const uint8_t *nflag, const uint8_t *dflag,
+                              const int64_t *read_counts, const int64_t *first_unit,
+                              const int32_t *max_pos, int64_t cells, int n_refs, int64_t unit_base,
+                              int32_t *sum, int32_t *mx)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 4 * cells; i += stride)
+        sum[i] = dense[i];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_refs; i += stride)
+        sum[4 * cells + i] = (int32_t)read_counts[i];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += stride) {
+        mx[i] = nflag[i];
+        mx[cells + i] = dflag[i];
+    }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_refs; i += stride) {
+        mx[2 * cells + i] = max_pos[i];
+        mx[2 * cells + n_refs + i] = first_unit[i] < 0 ? INT32_MIN : (int32_t)(-(first_unit[i] + unit_base));
+    }
+}
+
+__global__ void k_pile_import(int32_t *dense, uint8_t *nflag, uint8_t *dflag, int64_t *read_counts,
+                              int64_t *first_unit, int32_t *max_pos, int64_t cells, int n_refs,
+                              const int32_t *sum, const int32_t *mx)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 4 * cells; i += stride)
+        dense[i] = sum[i];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_refs; i += stride) {
+        read_counts[i] = sum[4 * cells + i];
+        max_pos[i] = mx[2 * cells + i];
+        const int32_t f = mx[2 * cells + n_refs + i];
+        first_unit[i] = f == INT32_MIN ? -1 : -(int64_t)f;
+    }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += stride) {
+        nflag[i] = (uint8_t)mx[i];
+        dflag[i] = (uint8_t)mx[cells + i];
+    }
+}
+
+}  // namespace mh
+
+using namespace mh;
+
+extern "C" int mh_pileup_packed_bytes(mh_ctx *ctx, int64_t *sum_bytes, int64_t *max_bytes)
+{
+    if (!ctx) return -3;
+    Ctx &c = *reinterpret_cast<Ctx *>(ctx);
+    const int64_t cells = (int64_t)c.pile.n_refs * c.pile.cap;
+    if (sum_bytes) *sum_bytes = sizeof(int32_t) * (4 * cells + c.pile.n_refs);
+    if (max_bytes) *max_bytes = sizeof(int32_t) * (2 * cells + 2 * c.pile.n_refs);
+    return 0;
+}
+
+extern "C" int mh_pileup_export_base(mh_ctx *ctx, int64_t unit_base, void *dev_sum, void *dev_max)
+{
+    if (!ctx || !dev_sum || !dev_max) return -3;
+    Ctx &c = *reinterpret_cast<Ctx *>(ctx);
+    PileState &P = c.pile;
+    if (!P.dense) { set_error("no pileup to export"); return -3; }
+    MH_HIP(hipSetDevice(c.device));
+    const int64_t cells = (int64_t)P.n_refs * P.cap;
+    hipLaunchKernelGGL(k_pile_export, dim3(1024), dim3(256), 0, c.stream, P.dense, P.nflag, P.dflag,
+                       P.read_counts, P.first_unit, P.max_pos, cells, P.n_refs, unit_base,
+                       (int32_t *)dev_sum, (int32_t *)dev_max);
+    MH_HIP(hipGetLastError());
+    MH_HIP(hipStreamSynchronize(c.stream));
+    return 0;
+}
+
+extern "C" int mh_pileup_export(mh_ctx *ctx, void *dev_sum, void *dev_max)
+{
+    return mh_pileup_export_base(ctx, 0, dev_sum, dev_max);
+}
+
+extern "C" int mh_pileup_import(mh_ctx *ctx, const void *dev_sum, const void *dev_max)
+{
+    if (!ctx || !dev_sum || !dev_max) return -3;
+    Ctx &c = *reinterpret_cast<Ctx *>(ctx);
+    PileState &P = c.pile;
+    if (!P.dense) { set_error("no pileup to import into"); return -3; }
+    MH_HIP(hipSetDevice(c.device));
+    const int64_t cells = (int64_t)P.n_refs * P.cap;
+    hipLaunchKernelGGL(k_pile_import, dim3(1024), dim3(256), 0, c.stream, P.dense, P.nflag, P.dflag,
+                       P.read_counts, P.first_unit, P.max_pos, cells, P.n_refs,
+                       (const int32_t *)dev_sum, (const int32_t *)dev_max);
+    MH_HIP(hipGetLastError());
+    MH_HIP(hipStreamSynchronize(c.stream));
+    return 0;
+}

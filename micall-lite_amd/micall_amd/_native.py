@@ -1,0 +1,357 @@
+"""
+ctypes binding of libmicall_hip.so (include/micall_hip.h).
+
+This is the only way the host package reaches the GPU path.  There is no CPU
+fallback: if the library is missing, or no gfx950 device is visible,
+constructing a Context raises NativeUnavailable.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('MICALL_HIP_LIB', os.path.join(HERE, 'libmicall_hip.so'))
+
+E2E, LOCAL = 0, 1
+MAXOPS = 128
+INT32_MIN = -2 ** 31
+OP_CHARS = 'MIDxS'
+PILEUP_SLACK = 2048
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class Params(ctypes.Structure):
+    _fields_ = [('mode', ctypes.c_int), ('rdg_open', ctypes.c_int), ('rdg_ext', ctypes.c_int),
+                ('rfg_open', ctypes.c_int), ('rfg_ext', ctypes.c_int), ('maxins', ctypes.c_int)]
+
+
+ALN_FIELDS = ('ref', 'pos', 'rev', 'score', 'secbest', 'flag', 'mapq', 'rnext', 'pnext', 'tlen',
+              'sam_ref', 'sam_pos', 'xm', 'xo', 'xg', 'nm', 'ys', 'yt', 'yf', 'n_cigar')
+
+
+class Aln(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_int32) for name in ALN_FIELDS] + [('cigar', ctypes.c_uint32 * MAXOPS)]
+
+
+ALN_DTYPE = np.dtype([(name, np.int32) for name in ALN_FIELDS] + [('cigar', np.uint32, MAXOPS)])
+assert ALN_DTYPE.itemsize == ctypes.sizeof(Aln)
+
+_lib = None
+
+_P = ctypes.c_void_p
+_I64P = ctypes.POINTER(ctypes.c_int64)
+_I32P = ctypes.POINTER(ctypes.c_int32)
+
+
+def _declare(L):
+    sig = {
+        'mh_version': ([], ctypes.c_int),
+        'mh_last_error': ([ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+        'mh_device_count': ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        'mh_ctx_create': ([ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
+        'mh_ctx_destroy': ([_P], ctypes.c_int),
+        'mh_ctx_sync': ([_P], ctypes.c_int),
+        'mh_ctx_stream': ([_P, ctypes.POINTER(_P)], ctypes.c_int),
+        'mh_index_build': ([_P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int], ctypes.c_int),
+        'mh_reads_load': ([_P, ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P], ctypes.c_int),
+        'mh_reads_load_fastq': ([_P, ctypes.c_char_p, ctypes.c_char_p, _I64P], ctypes.c_int),
+        'mh_reads_count': ([_P, _I64P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        'mh_reads_set_names': ([_P, ctypes.c_int64, ctypes.POINTER(ctypes.c_char_p)], ctypes.c_int),
+        'mh_map': ([_P, ctypes.POINTER(Params)], ctypes.c_int),
+        'mh_alns_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
+        'mh_map_counts': ([_P, _P, _P, _P, _P, _P, _I64P, _I64P], ctypes.c_int),
+        'mh_recs_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
+        'mh_format_rows': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.c_int64,
+                            ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_size_t,
+                            ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        'mh_rows_load': ([_P, ctypes.c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                          ctypes.c_int64, _P], ctypes.c_int),
+        'mh_pileup': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),
+        'mh_pileup_dims': ([_P, ctypes.POINTER(ctypes.c_int), _I32P, _I64P, _I64P], ctypes.c_int),
+        'mh_pileup_fetch': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+        'mh_pileup_events': ([_P, _P, _P, _P, _P, _P], ctypes.c_int),
+        'mh_pileup_packed_bytes': ([_P, _I64P, _I64P], ctypes.c_int),
+        'mh_pileup_export': ([_P, _P, _P], ctypes.c_int),
+        'mh_pileup_export_base': ([_P, ctypes.c_int64, _P, _P], ctypes.c_int),
+        'mh_pileup_import': ([_P, _P, _P], ctypes.c_int),
+        'mh_gotoh_align': ([_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                            ctypes.c_int, ctypes.c_char_p, _P, ctypes.c_char_p, ctypes.c_char_p,
+                            ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        'mh_levenshtein': ([ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    return sig
+
+
+EXPORTED = None
+
+
+def lib():
+    """The loaded library (raises NativeUnavailable if it was not built)."""
+    global _lib, EXPORTED
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeUnavailable('libmicall_hip.so not built at {} (run __graft_entry__.build() '
+                                    'or make -C micall-lite_amd/csrc)'.format(LIB_PATH))
+        _lib = ctypes.CDLL(LIB_PATH)
+        EXPORTED = sorted(_declare(_lib))
+    return _lib
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(1024)
+    lib().mh_last_error(buf, len(buf))
+    return buf.value.decode(errors='replace')
+
+
+def check(status, what):
+    if status == 0:
+        return
+    msg = last_error()
+    if status == -5:
+        raise NativeUnavailable('{}: {}'.format(what, msg))
+    if status == -1:
+        raise RuntimeError(msg or 'Traceback failed, try local alignment')
+    raise NativeError('{} failed ({}): {}'.format(what, status, msg))
+
+
+def device_count():
+    n = ctypes.c_int()
+    if lib().mh_device_count(ctypes.byref(n)) != 0:
+        return 0
+    return n.value
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def params(mode, rdg=(10, 3), rfg=(10, 3), maxins=1200):
+    return Params(mode, rdg[0], rdg[1], rfg[0], rfg[1], maxins)
+
+
+class Context:
+    """One device context (HIP stream, resident reads, index, results)."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = ctypes.c_void_p()
+        check(L.mh_ctx_create(device, ctypes.byref(h)), 'mh_ctx_create')
+        self.h = h
+        self.device = device
+        self.n_refs = 0
+        self.refnames = []
+        self.reflens = []
+
+    def close(self):
+        if getattr(self, 'h', None):
+            lib().mh_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(lib().mh_ctx_sync(self.h), 'mh_ctx_sync')
+
+    # ---- reference set --------------------------------------------------
+    def index_build(self, names, seqs, seedlen):
+        arr = (ctypes.c_char_p * max(len(seqs), 1))(*[s.encode() for s in seqs])
+        check(lib().mh_index_build(self.h, len(seqs), arr, seedlen), 'mh_index_build')
+        self.refnames = list(names)
+        self.reflens = [len(s) for s in seqs]
+        self.n_refs = len(seqs)
+
+    # ---- reads ----------------------------------------------------------
+    def reads_load_arrays(self, seq, qual, offsets, lens, paired):
+        """seq/qual: uint8 buffers; offsets int64, lens int32 per read."""
+        seq = np.ascontiguousarray(seq, dtype=np.uint8)
+        qual = np.ascontiguousarray(qual, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        check(lib().mh_reads_load(self.h, len(lens), int(paired), _ptr(seq), _ptr(qual),
+                                  _ptr(offsets), _ptr(lens)), 'mh_reads_load')
+
+    def reads_load(self, seqs, quals, paired, names=None):
+        lens = np.array([len(s) for s in seqs], dtype=np.int32)
+        offsets = np.zeros(len(seqs), dtype=np.int64)
+        if len(seqs):
+            offsets[1:] = np.cumsum(lens[:-1])
+        seq = np.frombuffer(''.join(seqs).encode(), dtype=np.uint8)
+        qual = np.frombuffer(''.join(quals).encode(), dtype=np.uint8)
+        self.reads_load_arrays(seq, qual, offsets, lens, paired)
+        if names is not None:
+            self.set_names(names)
+
+    def reads_load_fixed(self, reads, quals, paired):
+        """reads/quals: (n, L) uint8 arrays (mates interleaved when paired)."""
+        n, L = reads.shape
+        lens = np.full(n, L, dtype=np.int32)
+        offsets = np.arange(n, dtype=np.int64) * L
+        self.reads_load_arrays(reads.reshape(-1), quals.reshape(-1), offsets, lens, paired)
+
+    def reads_load_fastq(self, path1, path2=None):
+        n = ctypes.c_int64()
+        check(lib().mh_reads_load_fastq(self.h, path1.encode(), path2.encode() if path2 else None,
+                                        ctypes.byref(n)), 'mh_reads_load_fastq')
+        return n.value
+
+    def reads_count(self):
+        n = ctypes.c_int64()
+        p = ctypes.c_int()
+        check(lib().mh_reads_count(self.h, ctypes.byref(n), ctypes.byref(p)), 'mh_reads_count')
+        return n.value, bool(p.value)
+
+    def set_names(self, names):
+        arr = (ctypes.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+        check(lib().mh_reads_set_names(self.h, len(names), arr), 'mh_reads_set_names')
+
+    # ---- mapping --------------------------------------------------------
+    def map(self, par):
+        check(lib().mh_map(self.h, ctypes.byref(par)), 'mh_map')
+
+    def fetch(self, first=0, n=None):
+        if n is None:
+            n = self.reads_count()[0] - first
+        out = np.zeros(max(n, 1), dtype=ALN_DTYPE)
+        check(lib().mh_alns_fetch(self.h, first, n, _ptr(out)), 'mh_alns_fetch')
+        return out[:n]
+
+    def map_counts(self):
+        k = max(self.n_refs, 1)
+        lines, filt, mapped, first, firstm = (np.zeros(k, dtype=np.int64) for _ in range(5))
+        unm = ctypes.c_int64()
+        star = ctypes.c_int64()
+        check(lib().mh_map_counts(self.h, _ptr(lines), _ptr(filt), _ptr(mapped), _ptr(first),
+                                  _ptr(firstm), ctypes.byref(unm), ctypes.byref(star)),
+              'mh_map_counts')
+        n = self.n_refs
+        return dict(lines=lines[:n], filtered=filt[:n], mapped=mapped[:n], first_row=first[:n],
+                    first_mapped=firstm[:n], unmapped=unm.value, star=star.value)
+
+    def recs(self, first=0, n=None):
+        """(n, 20) int32 SAM header fields (ALN_FIELDS order) without CIGARs."""
+        if n is None:
+            n = self.reads_count()[0] - first
+        out = np.zeros((max(n, 1), 20), dtype=np.int32)
+        check(lib().mh_recs_fetch(self.h, first, n, _ptr(out)), 'mh_recs_fetch')
+        return out[:n]
+
+    def format_rows(self, style, first=0, n=None, order=None):
+        """SAM (style 0) or CSV (style 1) text of reads [first, first+n), or
+        of reads order[first:first+n] when an order is given."""
+        if order is not None:
+            order = np.ascontiguousarray(order, dtype=np.int64)
+            if n is None:
+                n = len(order) - first
+        elif n is None:
+            n = self.reads_count()[0] - first
+        names = (ctypes.c_char_p * max(self.n_refs, 1))(*[r.encode() for r in self.refnames])
+        used = ctypes.c_size_t()
+        cap = max(n, 1) * 900 + 4096
+        for _ in range(2):
+            buf = ctypes.create_string_buffer(cap)
+            st = lib().mh_format_rows(self.h, style, None if order is None else _ptr(order), first,
+                                      n, names, buf, cap, ctypes.byref(used))
+            if st == -2 and used.value > cap:
+                cap = used.value + 16
+                continue
+            check(st, 'mh_format_rows')
+            return buf.raw[:used.value].decode()
+        raise NativeError('mh_format_rows: buffer sizing failed')
+
+    # ---- pileup ---------------------------------------------------------
+    def rows_load(self, flag, ref, pos, cig_off, n_cigar, cigar, seq, qual, offsets, lens, units):
+        arrs = [np.ascontiguousarray(a, dtype=t) for a, t in (
+            (flag, np.int32), (ref, np.int32), (pos, np.int32), (cig_off, np.int32),
+            (n_cigar, np.int32), (cigar, np.uint32), (seq, np.uint8), (qual, np.uint8),
+            (offsets, np.int64), (lens, np.int32), (units, np.int64))]
+        self._rows_keep = arrs
+        n_units = len(arrs[10]) // 2
+        check(lib().mh_rows_load(self.h, len(arrs[0]), *[_ptr(a) for a in arrs[:10]], n_units,
+                                 _ptr(arrs[10])), 'mh_rows_load')
+
+    def pileup(self, source, q_cutoff, ref_lens):
+        rl = np.ascontiguousarray(ref_lens, dtype=np.int32)
+        check(lib().mh_pileup(self.h, source, q_cutoff, len(rl), _ptr(rl)), 'mh_pileup')
+
+    def pileup_fetch(self):
+        n = ctypes.c_int()
+        cap = ctypes.c_int32()
+        ne = ctypes.c_int64()
+        nb = ctypes.c_int64()
+        check(lib().mh_pileup_dims(self.h, ctypes.byref(n), ctypes.byref(cap), ctypes.byref(ne),
+                                   ctypes.byref(nb)), 'mh_pileup_dims')
+        n, cap, ne, nb = n.value, cap.value, ne.value, nb.value
+        dense = np.zeros((max(n, 1), cap, 4), dtype=np.int32)
+        nflag = np.zeros((max(n, 1), cap), dtype=np.uint8)
+        dflag = np.zeros((max(n, 1), cap), dtype=np.uint8)
+        rc = np.zeros(max(n, 1), dtype=np.int64)
+        fu = np.zeros(max(n, 1), dtype=np.int64)
+        mp = np.zeros(max(n, 1), dtype=np.int32)
+        check(lib().mh_pileup_fetch(self.h, _ptr(dense), _ptr(nflag), _ptr(dflag), _ptr(rc),
+                                    _ptr(fu), _ptr(mp)), 'mh_pileup_fetch')
+        eref = np.zeros(max(ne, 1), dtype=np.int32)
+        epos = np.zeros(max(ne, 1), dtype=np.int32)
+        eoff = np.zeros(max(ne, 1), dtype=np.int32)
+        elen = np.zeros(max(ne, 1), dtype=np.int32)
+        pool = ctypes.create_string_buffer(max(nb, 1))
+        check(lib().mh_pileup_events(self.h, _ptr(eref), _ptr(epos), _ptr(eoff), _ptr(elen), pool),
+              'mh_pileup_events')
+        raw = pool.raw
+        events = [(int(eref[e]), int(epos[e]), raw[eoff[e]:eoff[e] + elen[e]].decode())
+                  for e in range(ne)]
+        return dict(dense=dense[:n], nflag=nflag[:n], dflag=dflag[:n], read_counts=rc[:n],
+                    first_unit=fu[:n], max_pos=mp[:n], events=events, cap=cap)
+
+    def pileup_packed_bytes(self):
+        s = ctypes.c_int64()
+        m = ctypes.c_int64()
+        check(lib().mh_pileup_packed_bytes(self.h, ctypes.byref(s), ctypes.byref(m)),
+              'mh_pileup_packed_bytes')
+        return s.value, m.value
+
+    def pileup_export(self, dev_sum_ptr, dev_max_ptr, unit_base=0):
+        check(lib().mh_pileup_export_base(self.h, unit_base, ctypes.c_void_p(dev_sum_ptr),
+                                          ctypes.c_void_p(dev_max_ptr)), 'mh_pileup_export')
+
+    def pileup_import(self, dev_sum_ptr, dev_max_ptr):
+        check(lib().mh_pileup_import(self.h, ctypes.c_void_p(dev_sum_ptr),
+                                     ctypes.c_void_p(dev_max_ptr)), 'mh_pileup_import')
+
+    # ---- gotoh ----------------------------------------------------------
+    def gotoh_align(self, seq1, seq2, gop, gep, is_global, alphabet, matrix):
+        cap = len(seq1) + len(seq2) + 1
+        o1 = ctypes.create_string_buffer(cap)
+        o2 = ctypes.create_string_buffer(cap)
+        score = ctypes.c_int()
+        mat = np.ascontiguousarray(matrix, dtype=np.int32)
+        check(lib().mh_gotoh_align(self.h, seq1.encode(), seq2.encode(), gop, gep, int(is_global),
+                                   alphabet.encode(), _ptr(mat), o1, o2, cap, ctypes.byref(score)),
+              'mh_gotoh_align')
+        return o1.value.decode(), o2.value.decode(), score.value
+
+
+def levenshtein(a, b):
+    return lib().mh_levenshtein(a.encode(), b.encode())
+
+
+def cigar_text(aln):
+    if aln['ref'] < 0:
+        return '*'
+    return ''.join('{}{}'.format(int(c) >> 4, OP_CHARS[int(c) & 7])
+                   for c in aln['cigar'][:aln['n_cigar']])

@@ -1,0 +1,219 @@
+"""GPU parity: the HIP path through the C-ABI against the CPU oracle on the
+same seeded inputs (bit-exact: every SAM field and CIGAR op, every pileup
+counter), and against the reference-generated golden vectors."""
+import json
+import os
+from collections import Counter
+
+import numpy as np
+import pytest
+
+import oracle
+from micall_amd import _native, projects, synth
+
+pytestmark = pytest.mark.gpu
+
+SEEDS = projects.load_default().seed_sequences()
+POL = SEEDS['HIV1B-pol-seed']
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    c = _native.Context(0)
+    yield c
+    c.close()
+
+
+def _oracle_alns(refseqs, mode, seqs, quals, paired):
+    ix = oracle.Index(refseqs, oracle.seed_len(mode))
+    out = oracle.map_reads(ix, oracle.params(mode), seqs, quals, paired)
+    return np.frombuffer(bytes(out), dtype=_native.ALN_DTYPE)[:len(seqs)]
+
+
+def _gpu_alns(ctx, names, refseqs, mode, seqs, quals, paired):
+    ctx.index_build(names, refseqs, oracle.seed_len(mode))
+    ctx.reads_load(seqs, quals, paired)
+    ctx.map(_native.params(mode))
+    return ctx.fetch()
+
+
+def _assert_same(gpu, ref, seqs):
+    assert gpu.shape == ref.shape
+    for i in range(len(ref)):
+        g, r = gpu[i], ref[i]
+        for f in _native.ALN_FIELDS:
+            assert g[f] == r[f], (i, f, g[f], r[f], seqs[i][:60])
+        n = r['n_cigar']
+        assert np.array_equal(g['cigar'][:n], r['cigar'][:n]), (i, _native.cigar_text(g),
+                                                                 _native.cigar_text(r))
+
+
+def _reads(n_pairs, seed, genomes=None, **kw):
+    pairs = synth.make_pairs(n_pairs, genomes=genomes or {'HIV1B-pol-seed': POL},
+                             genome_seed=seed, read_seed=seed + 1000, **kw)
+    return synth.interleave(pairs)
+
+
+@pytest.mark.parametrize('mode', [oracle.E2E, oracle.LOCAL])
+def test_map_pol_vs_oracle(ctx, mode):
+    names, seqs, quals = _reads(1500, 7, indel_rate=0.01)
+    ref = _oracle_alns([POL], mode, seqs, quals, True)
+    gpu = _gpu_alns(ctx, ['HIV1B-pol-seed'], [POL], mode, seqs, quals, True)
+    _assert_same(gpu, ref, seqs)
+    assert (ref["flag"] & 4 == 0).mean() > 0.25  # the test exercises real alignments
+
+
+def test_map_all_seeds_e2e_vs_oracle(ctx):
+    """prelim_map's pass: every seed of projects.json, reads from 3 HIV genes."""
+    genomes = {k: SEEDS[k] for k in ('HIV1B-pol-seed', 'HIV1B-env-seed', 'HIV1B-gag-seed')}
+    names, seqs, quals = _reads(1500, 11, genomes=genomes)
+    refnames = list(SEEDS)
+    refseqs = [SEEDS[k] for k in refnames]
+    ref = _oracle_alns(refseqs, oracle.E2E, seqs, quals, True)
+    gpu = _gpu_alns(ctx, refnames, refseqs, oracle.E2E, seqs, quals, True)
+    _assert_same(gpu, ref, seqs)
+
+
+def test_map_unpaired_long_and_edge_reads(ctx):
+    """Unpaired 1x300, reads with Ns, short, empty and overhanging reads."""
+    rng = np.random.default_rng(5)
+    names, seqs, quals = _reads(400, 13, read_len=300, paired=False)
+    seqs = list(seqs)
+    quals = list(quals)
+    extra = ['', 'ACGT', POL[:30], POL[-120:] + 'ACGTACGTAC' * 10, 'N' * 60 + POL[500:700],
+             POL[1000:1250].replace('A', 'N', 30), POL[2000:2251].lower(), 'ACGTRYKM' + POL[10:200]]
+    for s in extra:
+        seqs.append(s)
+        quals.append(''.join(chr(33 + int(q)) for q in rng.integers(2, 41, size=len(s))))
+    for mode in (oracle.E2E, oracle.LOCAL):
+        ref = _oracle_alns([POL, SEEDS['HIV1B-gag-seed']], mode, seqs, quals, False)
+        gpu = _gpu_alns(ctx, ['pol', 'gag'], [POL, SEEDS['HIV1B-gag-seed']], mode, seqs, quals,
+                        False)
+        _assert_same(gpu, ref, seqs)
+
+
+def _sam_lines(alns, names, seqs, quals, refnames, paired):
+    lines = ['@HD\tVN:1.0\tSO:unsorted\n'] + ['@SQ\tSN:{}\tLN:0\n'.format(r) for r in refnames]
+    for i in range(len(seqs)):
+        a = oracle.OgAln.from_buffer_copy(alns[i].tobytes())
+        lines.append('\t'.join(oracle.sam_fields(a, oracle.qname_of(names[i], paired), seqs[i],
+                                                 quals[i], refnames)) + '\n')
+    return lines
+
+
+def test_format_rows_matches_oracle_text(ctx):
+    names, seqs, quals = _reads(300, 17, indel_rate=0.01)
+    ctx.index_build(['HIV1B-pol-seed'], [POL], 20)
+    ctx.reads_load(seqs, quals, True, names=[oracle.qname_of(n, True) for n in names])
+    ctx.map(_native.params(oracle.LOCAL))
+    gpu_text = ctx.format_rows(0)
+    ref = _oracle_alns([POL], oracle.LOCAL, seqs, quals, True)
+    want = ''.join(_sam_lines(ref, names, seqs, quals, ['HIV1B-pol-seed'], True)[2:])
+    assert gpu_text == want
+
+
+def _gpu_pileup_as_refmap(ctx, refnames, reflens, q_cutoff, source=0):
+    ctx.pileup(source, q_cutoff, reflens)
+    p = ctx.pileup_fetch()
+    events = {}
+    for r, pos, tok in p['events']:
+        events.setdefault((r, pos), Counter())[tok] += 1
+    refmap, counts = {}, Counter()
+    order = sorted((p['first_unit'][r], r) for r in range(len(refnames)) if p['first_unit'][r] >= 0)
+    for _, r in order:
+        counts[refnames[r]] = int(p['read_counts'][r])
+        pos_nucs = {}
+        for pos in range(1, int(p['max_pos'][r]) + 1):
+            c = Counter()
+            for k, tok in enumerate('ACGT'):
+                if p['dense'][r, pos - 1, k]:
+                    c[tok] = int(p['dense'][r, pos - 1, k])
+            if p['nflag'][r, pos - 1]:
+                c['N'] = -1
+            if p['dflag'][r, pos - 1]:
+                c['-'] = -2
+            c.update(events.get((r, pos), {}))
+            if c:
+                pos_nucs[pos] = c
+        refmap[refnames[r]] = (pos_nucs, int(p['max_pos'][r]))
+    return refmap, counts
+
+
+@pytest.mark.parametrize('mode,q', [(oracle.LOCAL, 20), (oracle.E2E, 20), (oracle.LOCAL, 0)])
+def test_pileup_vs_oracle(ctx, mode, q):
+    names, seqs, quals = _reads(2000, 23, indel_rate=0.01)
+    refnames = ['HIV1B-pol-seed', 'HIV1B-gag-seed']
+    refseqs = [POL, SEEDS['HIV1B-gag-seed']]
+    gpu = _gpu_alns(ctx, refnames, refseqs, mode, seqs, quals, True)
+    lines = _sam_lines(gpu, names, seqs, quals, refnames, True)
+    want_refmap, want_counts = oracle.pileup(*oracle.matchmaker(lines), q)
+    got_refmap, got_counts = _gpu_pileup_as_refmap(ctx, refnames, [len(s) for s in refseqs], q)
+    assert list(got_refmap) == list(want_refmap)
+    assert got_counts == want_counts
+    for name in want_refmap:
+        assert got_refmap[name] == want_refmap[name], name
+
+
+def test_pileup_rows_vs_golden_sams(ctx, golden_dir):
+    """Source 1 (rows read back from text) on every golden SAM case."""
+    with open(os.path.join(golden_dir, 'pileup_golden.json')) as f:
+        cases = json.load(f)['cases']
+    for c in cases:
+        ref_names, pairs = oracle.matchmaker(c['sam'].splitlines(True))
+        want_refmap, want_counts = oracle.pileup(ref_names, pairs, c['quality_cutoff'])
+        rows, units = [], []
+        for r1, r2 in pairs:
+            ids = []
+            for r in (r1, r2):
+                if r is None:
+                    ids.append(-1)
+                else:
+                    ids.append(len(rows))
+                    rows.append(r)
+            units += ids
+        flag = [int(r[1]) for r in rows]
+        ref = [ref_names.index(r[2]) for r in rows]
+        pos = [int(r[3]) for r in rows]
+        cig, cig_off, n_cig = [], [], []
+        for r, f in zip(rows, flag):
+            ops = oracle.parse_cigar(r[5]) if not (f & 4) else []
+            cig_off.append(len(cig))
+            n_cig.append(len(ops))
+            cig += ops
+        seq = ''.join(r[9] for r in rows).encode()
+        qual = ''.join(r[10][:len(r[9])].ljust(len(r[9]), 'J') for r in rows).encode()
+        lens = [len(r[9]) for r in rows]
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]) if rows else []
+        ctx.rows_load(flag, ref, pos, cig_off, n_cig, cig or [0], np.frombuffer(seq, np.uint8),
+                      np.frombuffer(qual, np.uint8), offs, lens, units)
+        cap_lens = [max([int(r[3]) + len(r[9]) for p in pairs for r in p if r] + [8])
+                    for _ in ref_names]
+        got_refmap, got_counts = _gpu_pileup_as_refmap(ctx, ref_names, cap_lens,
+                                                       c['quality_cutoff'], source=1)
+        assert list(got_refmap) == list(want_refmap)
+        assert got_counts == want_counts
+        for name in want_refmap:
+            assert got_refmap[name][0] == want_refmap[name][0], (name, c['sam'][:200])
+
+
+def test_gotoh_vs_golden(ctx, golden_dir):
+    with open(os.path.join(golden_dir, 'gotoh_golden.json')) as f:
+        cases = json.load(f)['cases']
+    for c in cases:
+        args = (c['seq1'], c['seq2'], c['gop'], c['gep'], c['is_global'], c['alphabet'], c['matrix'])
+        want = oracle.gotoh_align(*args) if not c['error'] else None
+        if c['error']:
+            with pytest.raises(RuntimeError):
+                ctx.gotoh_align(*args)
+            continue
+        assert ctx.gotoh_align(*args) == want, c
+
+
+def test_gotoh_pol_sized(ctx):
+    """A 3,039 x ~2,900 global alignment (the remap filter's size) vs oracle."""
+    rng = np.random.default_rng(3)
+    conseq = synth.sample_genome(POL, rng, 0.1, 0.004).tobytes().decode()[100:3000]
+    mat, alpha = [5, -4, -4, -4, 0, -4, 5, -4, -4, 0, -4, -4, 5, -4, 0, -4, -4, -4, 5, 0,
+                  0, 0, 0, 0, 0], 'ACGT?'
+    want = oracle.gotoh_align(POL, conseq, 15, 3, True, alpha, mat)
+    assert ctx.gotoh_align(POL, conseq, 15, 3, True, alpha, mat) == want
