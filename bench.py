@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""
+bench.py -- MiCall-Lite iterative-remap hot path on MI355X.
+
+One step = one pass of the hot path over one batch of synthetic input already
+resident in HBM (BASELINE.json configs[1], "C2"): prelim_map's end-to-end
+mapping of every read pair against all 74 seed references, seed selection,
+the prelim consensus (device pileup), ONE remap iteration (--local mapping
+against the consensus, device pileup, consensus + distance filter).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P]
+
+N > 1 is launched by torch.distributed.run, one rank per GPU; every rank holds
+its own block of P pairs (weak scaling), per-reference tallies and the dense
+pileup counters are all-reduced over RCCL between passes.  Rank 0 prints one
+JSON line.  value = reads/s over the whole job (2 reads per pair).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(REPO, 'micall-lite_amd'), os.path.join(REPO, 'oracle')):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+METRIC = 'paired 2×251 nt reads/sec mapped+realigned; fraction of HBM roofline'
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SEED = 20261015
+READ_LEN = 251
+
+
+def algo_bytes_per_pair(L=READ_LEN):
+    """2-bit bases + N mask + qualities for both mates + two
+    32-byte alignment records, per pair per mapping pass (756 B at L=251)."""
+    return 2 * -(-L // 4) + 2 * -(-L // 8) + 2 * L + 64
+
+
+def make_reads(pairs, block):
+    from micall_amd import projects, synth
+    pol = projects.load_default().seed_sequences()['HIV1B-pol-seed']
+    d = synth.make_pairs(pairs, genomes={'HIV1B-pol-seed': pol}, genome_seed=SEED,
+                         read_seed=SEED, block=block, read_len=READ_LEN)
+    reads = np.stack([d['r1'], d['r2']], axis=1).reshape(2 * pairs, READ_LEN)
+    quals = np.stack([d['q1'], d['q2']], axis=1).reshape(2 * pairs, READ_LEN)
+    return reads, quals
+
+
+def cpu_baseline(sample_pairs):
+    """The CPU oracle (C restatement, OpenMP over pairs) on a bounded sample
+    of the same workload, on this host's cores."""
+    import cpu_pipeline
+    from micall_amd import projects
+    cfg = projects.load_default()
+    seed_set = cfg.seed_sequences()
+    groups = {k: cfg.getSeedGroup(k) for k in seed_set}
+    reads, quals = make_reads(sample_pairs, block=0)
+    seqs = [r.tobytes().decode() for r in reads]
+    qs = [q.tobytes().decode() for q in quals]
+    threads = min(16, os.cpu_count() or 1)
+    _, secs = cpu_pipeline.run_step(seed_set, cfg.all_region_sequences(), groups, seqs, qs,
+                                    True, threads)
+    return {'value': round(2 * sample_pairs / secs, 1), 'unit': 'reads/s', 'cores': threads,
+            'kind': 'port',
+            'sample': '{} synthetic pairs (first block of the bench input): prelim e2e pass over '
+                      '74 seeds + 1 local remap pass + 2 pileups/consensus, oracle C restatement '
+                      'with OpenMP over pairs, {:.1f} s'.format(sample_pairs, secs)}
+
+
+def read_pmc_traffic(kernel, pairs):
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC
+    summary (separate --pmc pass, FETCH_SIZE doubled per the gfx950 rule),
+    when it was measured on the same per-GPU pair count."""
+    path = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d['kernels'][kernel]
+        if int(d.get('pairs', -1)) != pairs:
+            return None
+        return k['hbm_bytes_per_launch']
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split('\n\n')[0])
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--pairs', type=int, default=1000000, help='read pairs per GPU')
+    ap.add_argument('--cpu-sample', type=int, default=100000)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from micall_amd import _native
+    from micall_amd.pipeline import RemapPipeline, Shard
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        print('warning: --gpus {} but WORLD_SIZE {}'.format(args.gpus, world), file=sys.stderr)
+    device = torch.device('cuda', local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=device)
+
+    ctx = _native.Context(local)
+    reads, quals = make_reads(args.pairs, block=rank)
+    ctx.reads_load_fixed(reads, quals, True)
+    del reads, quals
+    shard = Shard(rank, world, read_base=rank * 2 * args.pairs, device=device) if world > 1 else None
+    pipe = RemapPipeline(ctx, shard=shard)
+    raw_count = 2.0 * args.pairs * world     # lines(R1) / 2, remap.py:457
+
+    def step():
+        return pipe.run(raw_count, max_iterations=1)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        conseqs, new_counts, _unm = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kernels = {k: ctx.profile_get(k) for k in ('k_seed', 'k_dp', 'k_pair', 'k_pileup')}
+    dom = max(kernels, key=lambda k: kernels[k][0])
+    dom_ms, dom_n = kernels[dom]
+    # every launch of a mapping / pileup kernel processes this rank's pairs once
+    bytes_per_launch = algo_bytes_per_pair() * args.pairs
+    avg_s = dom_ms / 1e3 / max(dom_n, 1)
+    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    total_pairs = args.pairs * world * args.steps
+    value = 2 * total_pairs / elapsed
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_sample)
+        out = {
+            'metric': METRIC, 'value': round(value, 1), 'unit': 'reads/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': round(1e3 * elapsed / args.steps, 3), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'int32', 'data': 'synthetic',
+            'config': {'workload': 'C2: synthetic 2x251 nt HIV-1 pol read pairs (10% divergent '
+                                   'sample genome, 0.5% errors), prelim_map end-to-end vs 74 seeds '
+                                   '+ 1 remap iteration (--local vs consensus) + 2 pileups, '
+                                   'default projects.json',
+                       'pairs_per_gpu': args.pairs, 'read_len': READ_LEN,
+                       'parallelism': 'dp{} (read-pair shards, RCCL all-reduce of pileup '
+                                      'counters)'.format(world)},
+            'roofline': {'kernel': dom, 'bound': 'hbm', 'achieved': round(achieved, 3),
+                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(achieved / HBM_PEAK_GBS, 6),
+                         'traffic': read_pmc_traffic(dom, args.pairs),
+                         'algo_bytes_per_launch': bytes_per_launch,
+                         'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': dom_n},
+            'kernels_ms_per_step': {k: round(v[0] / args.steps, 3) for k, v in kernels.items()},
+            'cpu_baseline': cpu,
+            'result': {'conseqs': {k: len(v) for k, v in conseqs.items()},
+                       'mapped_lines': dict(new_counts)},
+        }
+        print(json.dumps(out))
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

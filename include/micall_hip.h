@@ -102,10 +102,11 @@ int mh_alns_fetch(mh_ctx *ctx, int64_t first, int64_t n, mh_aln *out);
  *   mapped[r]    mapped lines with RNAME r        (new_counts, remap.py:755)
  *   first_row[r] first line index with RNAME r, -1 if none
  *   first_mapped[r] first mapped line with RNAME r (Counter order), -1 if none
- * and *unmapped = unmapped lines (remap.py:743-753); star_lines = RNAME '*'. */
+ * and *unmapped = unmapped lines (remap.py:743-753); star_lines / star_first =
+ * number of / first line with RNAME '*'. */
 int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mapped,
                   int64_t *first_row, int64_t *first_mapped, int64_t *unmapped,
-                  int64_t *star_lines);
+                  int64_t *star_lines, int64_t *star_first);
 /* The 20 int32 header fields of mh_aln (no CIGAR) for reads [first, first+n). */
 int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20);
 /* SAM text for reads order[first .. first+n) (order NULL: reads first ..
@@ -161,6 +162,11 @@ int mh_pileup_import(mh_ctx *ctx, const void *dev_sum, const void *dev_max);
 int mh_gotoh_align(mh_ctx *ctx, const char *seq1, const char *seq2, int gop, int gep,
                    int is_global, const char *alphabet, const int *matrix, char *out1,
                    char *out2, int cap, int *score);
+
+/* Per-kernel device time measured with HIP events on the context's stream
+ * (k_seed, k_dp, k_pair, k_pileup).  mh_profile(ctx, 1) enables and resets. */
+int mh_profile(mh_ctx *ctx, int enable);
+int mh_profile_get(mh_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 
 /* Unit-cost edit distance (Levenshtein.distance, remap.py:250). */
 int mh_levenshtein(const char *a, const char *b);

@@ -34,6 +34,37 @@ int hip_fail(hipError_t e, const char *what)
     return -4;
 }
 
+int prof_begin(Ctx &c, const char *name)
+{
+    if (!c.prof) return -1;
+    ProfPending p{name, nullptr, nullptr};
+    if (hipEventCreate(&p.a) != hipSuccess || hipEventCreate(&p.b) != hipSuccess) return -1;
+    hipEventRecord(p.a, c.stream);
+    c.prof_pending.push_back(p);
+    return (int)c.prof_pending.size() - 1;
+}
+
+void prof_end(Ctx &c, int slot)
+{
+    if (slot < 0 || slot >= (int)c.prof_pending.size()) return;
+    hipEventRecord(c.prof_pending[slot].b, c.stream);
+}
+
+void prof_flush(Ctx &c)
+{
+    for (auto &p : c.prof_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            ProfEntry &e = c.prof_acc[p.name];
+            e.ms += ms;
+            e.launches += 1;
+        }
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    c.prof_pending.clear();
+}
+
 // ---- per-length tables, same formulas as oracle/og_mapper.c --------------
 static int seed_interval(int mode, int len)
 {
@@ -536,8 +567,29 @@ int mh_map(mh_ctx *ctx, const mh_params *par)
     if (int st = prepare_len_tab(*c, par->mode)) return st;
     int st = run_map(*c, *par);
     if (st == 0) MH_HIP(hipStreamSynchronize(c->stream));
+    prof_flush(*c);
     c->rec_cache.clear();
     return st;
+}
+
+int mh_profile(mh_ctx *ctx, int enable)
+{
+    if (!ctx) return -3;
+    CtxEx *c = X(ctx);
+    c->prof = enable != 0;
+    c->prof_acc.clear();
+    return 0;
+}
+
+int mh_profile_get(mh_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches)
+{
+    if (!ctx || !kernel) return -3;
+    CtxEx *c = X(ctx);
+    prof_flush(*c);
+    auto it = c->prof_acc.find(kernel);
+    if (total_ms) *total_ms = it == c->prof_acc.end() ? 0.0 : it->second.ms;
+    if (launches) *launches = it == c->prof_acc.end() ? 0 : it->second.launches;
+    return 0;
 }
 
 static int fetch_recs(CtxEx *c, int64_t first, int64_t n, std::vector<Rec> &rec,
@@ -577,7 +629,7 @@ int mh_alns_fetch(mh_ctx *ctx, int64_t first, int64_t n, mh_aln *out)
 
 int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mapped,
                   int64_t *first_row, int64_t *first_mapped, int64_t *unmapped,
-                  int64_t *star_lines)
+                  int64_t *star_lines, int64_t *star_first)
 {
     if (!ctx) return -3;
     CtxEx *c = X(ctx);
@@ -585,7 +637,7 @@ int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mappe
     if (!M.valid) { set_error("no mapping results (call mh_map)"); return -3; }
     MH_HIP(hipSetDevice(c->device));
     const int n = M.n_refs;
-    std::vector<int64_t> s(5 * n + 2);
+    std::vector<int64_t> s(5 * n + 3);
     MH_HIP(hipMemcpy(s.data(), M.ref_stats, sizeof(int64_t) * s.size(), hipMemcpyDeviceToHost));
     if (lines) std::memcpy(lines, s.data(), sizeof(int64_t) * n);
     if (filtered) std::memcpy(filtered, s.data() + n, sizeof(int64_t) * n);
@@ -594,6 +646,7 @@ int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mappe
     if (first_mapped) std::memcpy(first_mapped, s.data() + 4 * n, sizeof(int64_t) * n);
     if (unmapped) *unmapped = s[5 * n];
     if (star_lines) *star_lines = s[5 * n + 1];
+    if (star_first) *star_first = s[5 * n + 2];
     return 0;
 }
 
@@ -790,6 +843,7 @@ int mh_pileup(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *
     c->pile.cap = cap;
     int st = run_pileup(*c, source, q_cutoff);
     if (st == 0) MH_HIP(hipStreamSynchronize(c->stream));
+    prof_flush(*c);
     return st;
 }
 

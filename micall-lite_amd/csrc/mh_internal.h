@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <map>
 #include <string>
 #include <vector>
 
@@ -142,8 +143,22 @@ int run_gotoh(struct Ctx &c, const char *s1, const char *s2, int gop, int gep, i
               const char *alphabet, const int *matrix, char *out1, char *out2, int cap,
               int *score);
 
+struct ProfEntry {
+    double ms = 0.0;
+    int64_t launches = 0;
+};
+
+struct ProfPending {
+    const char *name;
+    hipEvent_t a, b;
+};
+
 struct Ctx {
     int device = 0;
+    // per-kernel timing with HIP events on `stream` (mh_profile)
+    bool prof = false;
+    std::map<std::string, ProfEntry> prof_acc;
+    std::vector<ProfPending> prof_pending;
     hipStream_t stream = nullptr;
     DevReads reads;
     std::vector<std::string> names;  // QNAMEs for SAM text
@@ -158,6 +173,10 @@ struct Ctx {
 };
 
 void set_error(const char *fmt, ...);
+// bracket one kernel launch on c.stream when profiling is on
+int prof_begin(Ctx &c, const char *name);
+void prof_end(Ctx &c, int slot);
+void prof_flush(Ctx &c);   // after a stream sync: fold pending events
 int hip_fail(hipError_t e, const char *what);
 
 }  // namespace mh

@@ -186,9 +186,11 @@ __device__ __forceinline__ bool cand_before(const Cand &x, const Cand &y)
 __global__ __launch_bounds__(256) void k_seed(SeedArgs A)
 {
     __shared__ uint64_t sh_hits[4][MAXHITS_MATE];
+    __shared__ Cand sh_best[4][MAXCAND];
     const int lane = threadIdx.x & 63;
     const int wv = wave_uniform(threadIdx.x >> 6);
     uint64_t *hits = sh_hits[wv];
+    Cand *best = sh_best[wv];
     const int SL = A.I.seedlen;
     for (int64_t r = (int64_t)blockIdx.x * 4 + wv; r < A.R.n; r += (int64_t)gridDim.x * 4) {
         const int m = A.R.len[r];
@@ -271,7 +273,6 @@ __global__ __launch_bounds__(256) void k_seed(SeedArgs A)
             }
         }
         if (lane == 0) {
-            Cand best[MAXCAND];
             int nc = 0;
             int h0 = 0;
             while (h0 < total) {
@@ -629,18 +630,20 @@ struct PairArgs {
 };
 
 struct MateView {
+    const Slot *s;   // this read's MAXCAND slots in global memory (L2-hot after k_dp)
     int n;
     int best;
-    Slot s[MAXCAND];
 };
 
 __device__ __forceinline__ void load_mate(const PairArgs &A, int64_t r, MateView &mv)
 {
+    mv.s = A.slot + r * MAXCAND;
     mv.n = A.n_cand[r];
     mv.best = -1;
+    int bs = 0;
     for (int c = 0; c < mv.n; ++c) {
-        mv.s[c] = A.slot[r * MAXCAND + c];
-        if (mv.s[c].valid && (mv.best < 0 || mv.s[c].score > mv.s[mv.best].score)) mv.best = c;
+        const int v = mv.s[c].valid, sc = mv.s[c].score;
+        if (v && (mv.best < 0 || sc > bs)) { mv.best = c; bs = sc; }
     }
 }
 
@@ -659,12 +662,14 @@ __device__ void clear_rec(Rec &o)
 
 __device__ void fill_aligned(const PairArgs &A, Rec &o, const MateView &mv, int chosen, int m)
 {
-    const Slot &a = mv.s[chosen];
+    const Slot a = mv.s[chosen];
     o.ref = a.ref; o.pos = a.pos; o.rev = a.strand; o.score = a.score;
     int sec = 0, has = 0;
     for (int c = 0; c < mv.n; ++c) {
-        if (c == chosen || !mv.s[c].valid || same_place(mv.s[c], a)) continue;
-        if (!has || mv.s[c].score > sec) { sec = mv.s[c].score; has = 1; }
+        if (c == chosen) continue;
+        const Slot b = mv.s[c];
+        if (!b.valid || same_place(b, a)) continue;
+        if (!has || b.score > sec) { sec = b.score; has = 1; }
     }
     o.secbest = has ? sec : I32MIN;
     o.mapq = mapq_v2(A.local, A.local ? 2 * m : 0, A.len_tab[(MAXLEN + 1) + m], a.score, has, sec);
@@ -706,6 +711,7 @@ __device__ void tally(const PairArgs &A, const Rec &o, int64_t row)
         if (!(o.flag & 4)) atomicMin((long long *)&A.ref_stats[4 * n + o.sam_ref], (long long)row);
     } else {
         atomicAdd((unsigned long long *)&A.ref_stats[5 * n + 1], 1ull);
+        atomicMin((long long *)&A.ref_stats[5 * n + 2], (long long)row);
     }
     if (o.flag & 4) atomicAdd((unsigned long long *)&A.ref_stats[5 * n], 1ull);
 }
@@ -744,11 +750,13 @@ __global__ __launch_bounds__(256) void k_pair(PairArgs A)
         int c1 = m1.best, c2 = m2.best, conc = 0;
         long long best_sum = -9223372036854775807ll - 1;
         for (int x = 0; x < m1.n; ++x) {
-            if (!m1.s[x].valid) continue;
+            const Slot sx = m1.s[x];
+            if (!sx.valid) continue;
             for (int y = 0; y < m2.n; ++y) {
-                if (!m2.s[y].valid) continue;
-                if (!concordant(m1.s[x], m2.s[y], A.maxins)) continue;
-                const long long s = (long long)m1.s[x].score + m2.s[y].score;
+                const Slot sy = m2.s[y];
+                if (!sy.valid) continue;
+                if (!concordant(sx, sy, A.maxins)) continue;
+                const long long s = (long long)sx.score + sy.score;
                 if (s > best_sum) { best_sum = s; c1 = x; c2 = y; conc = 1; }
             }
         }
@@ -770,7 +778,7 @@ __global__ __launch_bounds__(256) void k_pair(PairArgs A)
             o2.ys = o1.score;
             if (o1.ref == o2.ref) {
                 o1.rnext = o2.rnext = -1;
-                const Slot &a = m1.s[c1], &b = m2.s[c2];
+                const Slot a = m1.s[c1], b = m2.s[c2];
                 const int lo = a.pos < b.pos ? a.pos : b.pos;
                 const int hi = a.end > b.end ? a.end : b.end;
                 const int t = hi - lo;
@@ -823,7 +831,7 @@ static int ensure_map_buffers(Ctx &c)
     if (M.cap_refs < c.index.n_refs || M.ref_stats == nullptr) {
         hipFree(M.ref_stats);
         const int cr = c.index.n_refs > 0 ? c.index.n_refs : 1;
-        MH_HIP(hipMalloc(&M.ref_stats, sizeof(int64_t) * (5 * cr + 2)));
+        MH_HIP(hipMalloc(&M.ref_stats, sizeof(int64_t) * (5 * cr + 3)));
         M.cap_refs = cr;
     }
     if (M.pool == nullptr) {
@@ -835,14 +843,15 @@ static int ensure_map_buffers(Ctx &c)
 
 __global__ void k_init_stats(int64_t *s, int n_refs)
 {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 5 * n_refs + 2; i += gridDim.x * blockDim.x)
-        s[i] = (i >= 3 * n_refs && i < 5 * n_refs) ? INT64_MAX : 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 5 * n_refs + 3; i += gridDim.x * blockDim.x)
+        s[i] = ((i >= 3 * n_refs && i < 5 * n_refs) || i == 5 * n_refs + 2) ? INT64_MAX : 0;
 }
 
 __global__ void k_fix_first(int64_t *s, int n_refs)
 {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * n_refs; i += gridDim.x * blockDim.x)
         if (s[3 * n_refs + i] == INT64_MAX) s[3 * n_refs + i] = -1;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && s[5 * n_refs + 2] == INT64_MAX) s[5 * n_refs + 2] = -1;
 }
 
 int run_map(Ctx &c, const mh_params &par)
@@ -874,7 +883,9 @@ int run_map(Ctx &c, const mh_params &par)
         SeedArgs sa{c.reads, c.index, par.mode, c.len_tab, M.cand, M.n_cand, M.yf, M.work, M.counters};
         int64_t blocks = (n + 3) / 4;
         if (blocks > 1 << 16) blocks = 1 << 16;
+        const int pk = prof_begin(c, "k_seed");
         hipLaunchKernelGGL(k_seed, dim3((unsigned)blocks), dim3(256), 0, s, sa);
+        prof_end(c, pk);
         MH_HIP(hipGetLastError());
 
         const int rows_pad = ((c.reads.max_len + 7) / 8) * 8;
@@ -890,6 +901,7 @@ int run_map(Ctx &c, const mh_params &par)
             if (wpb < 1) { set_error("mh_map: reads too long for LDS"); return -3; }
             int64_t dblocks = (n * 2 + wpb - 1) / wpb;
             if (dblocks > 256 * 48) dblocks = 256 * 48;
+            const int pd = prof_begin(c, "k_dp");
             if (par.mode == MH_LOCAL) {
                 MH_HIP(hipFuncSetAttribute((const void *)k_dp<1>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, wpb * wave_lds));
@@ -899,6 +911,7 @@ int run_map(Ctx &c, const mh_params &par)
                                            hipFuncAttributeMaxDynamicSharedMemorySize, wpb * wave_lds));
                 hipLaunchKernelGGL(k_dp<0>, dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
             }
+            prof_end(c, pd);
             MH_HIP(hipGetLastError());
             int32_t ctr[3];
             MH_HIP(hipMemcpyAsync(ctr, M.counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
@@ -916,7 +929,9 @@ int run_map(Ctx &c, const mh_params &par)
         int64_t pblocks = (units + 255) / 256;
         if (pblocks > 1 << 16) pblocks = 1 << 16;
         if (pblocks < 1) pblocks = 1;
+        const int pp = prof_begin(c, "k_pair");
         hipLaunchKernelGGL(k_pair, dim3((unsigned)pblocks), dim3(256), 0, s, pa);
+        prof_end(c, pp);
         MH_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(k_fix_first, dim3(8), dim3(256), 0, s, M.ref_stats, M.n_refs);

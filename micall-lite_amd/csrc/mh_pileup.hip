@@ -481,6 +481,7 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
             const size_t lds = sizeof(UnitLds) * wpb;
             int64_t blocks = (n_units + wpb - 1) / wpb;
             if (blocks > 256 * 32) blocks = 256 * 32;
+            const int pk = prof_begin(c, "k_pileup");
             if (source == 0) {
                 MH_HIP(hipFuncSetAttribute((const void *)k_pileup<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 hipLaunchKernelGGL(k_pileup<0>, dim3((unsigned)blocks), dim3(64 * wpb), lds, s, A);
@@ -488,6 +489,7 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
                 MH_HIP(hipFuncSetAttribute((const void *)k_pileup<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 hipLaunchKernelGGL(k_pileup<1>, dim3((unsigned)blocks), dim3(64 * wpb), lds, s, A);
             }
+            prof_end(c, pk);
             MH_HIP(hipGetLastError());
         }
         hipLaunchKernelGGL(k_pile_fix, dim3(8), dim3(256), 0, s, (long long *)P.first_unit, P.n_refs);

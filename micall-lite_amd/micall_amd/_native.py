@@ -67,7 +67,7 @@ def _declare(L):
         'mh_reads_set_names': ([_P, ctypes.c_int64, ctypes.POINTER(ctypes.c_char_p)], ctypes.c_int),
         'mh_map': ([_P, ctypes.POINTER(Params)], ctypes.c_int),
         'mh_alns_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
-        'mh_map_counts': ([_P, _P, _P, _P, _P, _P, _I64P, _I64P], ctypes.c_int),
+        'mh_map_counts': ([_P, _P, _P, _P, _P, _P, _I64P, _I64P, _I64P], ctypes.c_int),
         'mh_recs_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
         'mh_format_rows': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.c_int64,
                             ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_size_t,
@@ -86,6 +86,9 @@ def _declare(L):
                             ctypes.c_int, ctypes.c_char_p, _P, ctypes.c_char_p, ctypes.c_char_p,
                             ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         'mh_levenshtein': ([ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
+        'mh_profile': ([_P, ctypes.c_int], ctypes.c_int),
+        'mh_profile_get': ([_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _I64P],
+                           ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -236,12 +239,14 @@ class Context:
         lines, filt, mapped, first, firstm = (np.zeros(k, dtype=np.int64) for _ in range(5))
         unm = ctypes.c_int64()
         star = ctypes.c_int64()
+        star_first = ctypes.c_int64()
         check(lib().mh_map_counts(self.h, _ptr(lines), _ptr(filt), _ptr(mapped), _ptr(first),
-                                  _ptr(firstm), ctypes.byref(unm), ctypes.byref(star)),
-              'mh_map_counts')
+                                  _ptr(firstm), ctypes.byref(unm), ctypes.byref(star),
+                                  ctypes.byref(star_first)), 'mh_map_counts')
         n = self.n_refs
         return dict(lines=lines[:n], filtered=filt[:n], mapped=mapped[:n], first_row=first[:n],
-                    first_mapped=firstm[:n], unmapped=unm.value, star=star.value)
+                    first_mapped=firstm[:n], unmapped=unm.value, star=star.value,
+                    star_first=star_first.value)
 
     def recs(self, first=0, n=None):
         """(n, 20) int32 SAM header fields (ALN_FIELDS order) without CIGARs."""
@@ -332,6 +337,17 @@ class Context:
     def pileup_import(self, dev_sum_ptr, dev_max_ptr):
         check(lib().mh_pileup_import(self.h, ctypes.c_void_p(dev_sum_ptr),
                                      ctypes.c_void_p(dev_max_ptr)), 'mh_pileup_import')
+
+    # ---- kernel timing ---------------------------------------------------
+    def profile(self, enable=True):
+        check(lib().mh_profile(self.h, int(enable)), 'mh_profile')
+
+    def profile_get(self, kernel):
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        check(lib().mh_profile_get(self.h, kernel.encode(), ctypes.byref(ms), ctypes.byref(n)),
+              'mh_profile_get')
+        return ms.value, n.value
 
     # ---- gotoh ----------------------------------------------------------
     def gotoh_align(self, seq1, seq2, gop, gep, is_global, alphabet, matrix):

@@ -1,0 +1,216 @@
+"""
+Consensus from a device pileup: the host half of remap.sam_to_conseqs.
+
+  counts_to_conseqs  micall/core/remap.py:309-333 (with the seed prefill of
+                     :195-197: every seed position holds the seed base at
+                     count 0)
+  find_top_token     remap.py:892-902 (highest count, ties to the
+                     lexicographically smallest token)
+  filter_conseqs     remap.py:228-268 (consensus-distance filter: Gotoh
+                     global alignment of every seed against the covered part
+                     of each consensus, then edit distance)
+
+The per-read work (merge_reads / update_counts) ran on the GPU
+(mh_pileup); what arrives here is the dense A/C/G/T counters, the 'N' and
+'-' flags and the few sparse insertion tokens, O(reference length).
+"""
+import re
+from collections import Counter
+
+import numpy as np
+
+BASES = np.array(list('ACGT'))
+
+# micall/alignment/models/HYPHY_NUC.csv, the model of remap.py:33
+HYPHY_NUC_ALPHABET = 'ACGT?'
+HYPHY_NUC = [5, -4, -4, -4, 0,
+             -4, 5, -4, -4, 0,
+             -4, -4, 5, -4, 0,
+             -4, -4, -4, 5, 0,
+             0, 0, 0, 0, 0]
+FILTER_GOP, FILTER_GEP = 15, 3   # remap.py:33 Aligner(gop=15, gep=3, is_global=True)
+
+
+class Pileup:
+    """Host view of one pileup (Context.pileup_fetch) over refs `refnames`."""
+
+    def __init__(self, fetched, refnames):
+        self.refnames = list(refnames)
+        self.dense = fetched['dense']
+        self.nflag = fetched['nflag']
+        self.dflag = fetched['dflag']
+        self.read_counts = fetched['read_counts']
+        self.first_unit = fetched['first_unit']
+        self.max_pos = fetched['max_pos']
+        self.cap = fetched['cap']
+        self.events = {}
+        for r, pos, tok in fetched['events']:
+            self.events.setdefault(r, {}).setdefault(pos, Counter())[tok] += 1
+
+    def refs_with_reads(self, rank=None):
+        """Reference indices that received a merged pair, in refmap order:
+        by `rank` (e.g. first line of the rname group for the prelim SAM) or
+        by the first merged unit (remap.py:192-194)."""
+        present = [r for r in range(len(self.refnames)) if self.first_unit[r] >= 0]
+        key = self.first_unit if rank is None else rank
+        return sorted(present, key=lambda r: (key[r], r))
+
+    def read_count_items(self, order):
+        """read_counts Counter in insertion order (remap.py:186-191)."""
+        c = Counter()
+        for r in order:
+            c[self.refnames[r]] = int(self.read_counts[r])
+        return c
+
+    def _slice(self, r, length):
+        """dense, nflag, dflag for positions 1..length (zero past cap)."""
+        n = min(length, self.cap)
+        d = np.zeros((length, 4), dtype=np.int64)
+        nf = np.zeros(length, dtype=bool)
+        df = np.zeros(length, dtype=bool)
+        d[:n] = self.dense[r, :n]
+        nf[:n] = self.nflag[r, :n] != 0
+        df[:n] = self.dflag[r, :n] != 0
+        return d, nf, df
+
+    def counter_at(self, r, pos, seed):
+        """The reference's pos_nucs[pos] Counter (for positions with events)."""
+        c = Counter()
+        if seed and pos <= len(seed):
+            c[seed[pos - 1]] = 0
+        if pos <= self.cap:
+            for k, tok in enumerate('ACGT'):
+                v = int(self.dense[r, pos - 1, k])
+                if v:
+                    c[tok] += v
+            if self.nflag[r, pos - 1]:
+                c['N'] = -1
+            if self.dflag[r, pos - 1]:
+                c['-'] = -2
+        c.update(self.events.get(r, {}).get(pos, {}))
+        return c
+
+    def has_positive(self, r):
+        return bool(self.dense[r].max() > 0) or bool(self.events.get(r))
+
+    def tokens(self, r, seed):
+        """Top token per position 1..end-1 (remap.py:318-321)."""
+        end = max(int(self.max_pos[r]), len(seed) if seed else 0) + 1
+        length = end - 1
+        d, nf, df = self._slice(r, length)
+        tok = np.full(length, None, dtype=object)
+        if length:
+            cmax = d.max(axis=1)
+            positive = cmax > 0
+            # a positive count wins; ties go to the first of A<C<G<T
+            tok[positive] = BASES[d.argmax(axis=1)[positive]]
+            # otherwise: seed prefill (0) > 'N' (-1) > '-' (-2) > nothing
+            fill = np.full(length, None, dtype=object)
+            fill[df] = '-'
+            fill[nf] = 'N'
+            if seed:
+                k = min(len(seed), length)
+                fill[:k] = np.array(list(seed[:k]), dtype=object)
+            tok[~positive] = fill[~positive]
+        for pos in self.events.get(r, {}):
+            if pos <= length:
+                tok[pos - 1] = find_top_token(self.counter_at(r, pos, seed))
+        return tok
+
+    def position_sums(self, r, seed, length):
+        """sum(counts[pos].values()) for pos 1..length (remap.py:236-238)."""
+        d, nf, df = self._slice(r, length)
+        s = d.sum(axis=1) - nf.astype(np.int64) - 2 * df.astype(np.int64)
+        for pos, c in self.events.get(r, {}).items():
+            if pos <= length:
+                s[pos - 1] += sum(c.values())
+        return s
+
+
+def find_top_token(base_counts):
+    """remap.find_top_token (remap.py:892-902)."""
+    top_count = top_token = None
+    for token, count in base_counts.items():
+        if top_count is None or count > top_count or (count == top_count and token < top_token):
+            top_token, top_count = token, count
+    return top_token
+
+
+def _assemble(tokens):
+    """The deletion-run rule of counts_to_conseqs (remap.py:322-332): a '-'
+    run is kept only when its length is not a multiple of 3; a trailing run
+    is dropped; no token -> 'N'."""
+    out = []
+    deletion = 0
+    for t in tokens:
+        if t is None:
+            out.append('N')
+        elif t == '-':
+            deletion += 1
+        else:
+            if deletion:
+                if deletion % 3 != 0:
+                    out.append('-' * deletion)
+                deletion = 0
+            out.append(t)
+    return ''.join(out)
+
+
+def counts_to_conseqs(pile, order, seeds=None):
+    """{rname: consensus} in refmap order (remap.py:309-333)."""
+    conseqs = {}
+    for r in order:
+        name = pile.refnames[r]
+        seed = seeds.get(name) if seeds else None
+        if not pile.has_positive(r):
+            continue
+        conseqs[name] = _assemble(pile.tokens(r, seed))
+    return conseqs
+
+
+def extract_relevant_seed(aligned_conseq, aligned_seed):
+    """remap.extract_relevant_seed (remap.py:129-138)."""
+    match = re.match('-*([^-](.*[^-])?)', aligned_conseq)
+    return aligned_seed[match.start(1):match.end(1)].replace('-', '')
+
+
+def clean_sequence(seq, alphabet=HYPHY_NUC_ALPHABET):
+    """gotoh2.Aligner.clean_sequence (gotoh2.py:70-72)."""
+    return re.sub('[^%s]' % (alphabet,), '?', seq.upper())
+
+
+def filter_conseqs(ctx, pile, order, new_conseqs, seeds, filter_coverage, distance_report=None):
+    """The consensus-distance filter of remap.sam_to_conseqs (:228-268).
+    Alignments run on the GPU (mh_gotoh_align)."""
+    from . import _native
+    if not seeds or len(new_conseqs) < 2:
+        return new_conseqs
+    index = {pile.refnames[r]: r for r in order}
+    filtered = {}
+    for name in sorted(new_conseqs):
+        conseq = new_conseqs[name]
+        r = index[name]
+        sums = pile.position_sums(r, seeds.get(name), len(conseq))
+        keep = sums >= filter_coverage
+        relevant = ''.join(c for c, k in zip(conseq, keep) if k)
+        if not relevant:
+            continue
+        other_seed = other_dist = seed_dist = None
+        for seed_name in sorted(new_conseqs):
+            a_seed, a_conseq, _ = ctx.gotoh_align(clean_sequence(seeds[seed_name]),
+                                                  clean_sequence(relevant), FILTER_GOP, FILTER_GEP,
+                                                  True, HYPHY_NUC_ALPHABET, HYPHY_NUC)
+            d = _native.levenshtein(extract_relevant_seed(a_conseq, a_seed), relevant)
+            if seed_name == name:
+                seed_dist = d
+            elif other_dist is None or d < other_dist:
+                other_seed, other_dist = seed_name, d
+        if seed_dist <= other_dist:
+            filtered[name] = conseq
+        if distance_report is not None:
+            distance_report[name] = dict(seed_dist=seed_dist, other_dist=other_dist,
+                                         other_seed=other_seed)
+    if not filtered:
+        best_ref = pile.read_count_items(order).most_common(1)[0][0]
+        filtered[best_ref] = new_conseqs[best_ref]
+    return filtered

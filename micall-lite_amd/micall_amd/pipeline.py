@@ -1,0 +1,280 @@
+"""
+Device-resident prelim_map -> remap loop.
+
+The reference runs bowtie2 on the FASTQ files once for prelim_map and once per
+remap iteration, parsing SAM text in Python each time (prelim_map.py:114-151,
+remap.py:474-606, :661-761).  Here the reads are ingested once into HBM and
+every pass is a device call:
+
+    prelim pass     mh_map(end-to-end) over every seed        (prelim_map.py:134)
+    seed selection  per-rname line tallies (mh_map_counts)    (remap.py:482-528)
+    prelim conseqs  mh_pileup + counts_to_conseqs (host)      (remap.py:531-541)
+    remap loop      mh_map(--local) over the consensus set,   (remap.py:548-606)
+                    mh_pileup, consensus-distance filter
+                    (mh_gotoh_align), the three stopping rules
+
+The control flow and every dict order mirror remap() so the consensus
+sequences, counts and the final SAM records are the ones the reference would
+compute from the same alignments.  With a `Shard`, each rank holds a
+contiguous block of read pairs; per-reference tallies and the dense pileup
+counters are all-reduced over RCCL between passes and every rank then takes
+the same decisions.
+"""
+from collections import Counter
+
+import numpy as np
+
+from . import _native
+from .consensus import Pileup, counts_to_conseqs, filter_conseqs
+from .projects import ProjectConfig
+
+CONSENSUS_Q_CUTOFF = 20       # remap.py:35
+MIN_MAPPING_EFFICIENCY = 0.95  # remap.py:36
+MAX_REMAPS = 3                # remap.py:37
+READ_GAP_EXTEND = REF_GAP_EXTEND = 3   # prelim_map.py:27-30
+MAXINS = 1200                 # -X 1200
+E2E_SEEDLEN, LOCAL_SEEDLEN = 22, 20
+
+
+def write_remap_counts(remap_counts_writer, counts, title, distance_report=None):
+    """remap.write_remap_counts (remap.py:373-378)."""
+    distance_report = distance_report or {}
+    for refname in sorted(counts.keys()):
+        row = distance_report.get(refname, {})
+        row.update(type=title + ' ' + refname, count=counts[refname])
+        remap_counts_writer.writerow(row)
+
+
+class Shard:
+    """Multi-GPU view: this rank's first read index and the collectives used
+    between passes (torch.distributed over RCCL; gloo works for tests)."""
+
+    def __init__(self, rank, world, read_base, device=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.rank, self.world, self.read_base = rank, world, read_base
+        self.device = device if device is not None else torch.device('cpu')
+
+    def sum_i64(self, arr):
+        t = self.torch.as_tensor(np.ascontiguousarray(arr, dtype=np.int64), device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t.cpu().numpy()
+
+    def min_i64(self, arr):
+        """min over ranks, -1 meaning 'none'."""
+        a = np.where(np.asarray(arr) < 0, np.iinfo(np.int64).max, arr).astype(np.int64)
+        t = self.torch.as_tensor(a, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        out = t.cpu().numpy()
+        return np.where(out == np.iinfo(np.int64).max, -1, out)
+
+    def pileup(self, ctx, unit_base):
+        """All-reduce the device counters in place (sum, and max for flags /
+        max_pos / first unit) and gather the sparse events."""
+        torch = self.torch
+        sum_b, max_b = ctx.pileup_packed_bytes()
+        dev = self.device
+        s = torch.empty(sum_b // 4, dtype=torch.int32, device=dev)
+        m = torch.empty(max_b // 4, dtype=torch.int32, device=dev)
+        if dev.type == 'cuda':
+            ctx.pileup_export(s.data_ptr(), m.data_ptr(), unit_base)
+            self.dist.all_reduce(s, op=self.dist.ReduceOp.SUM)
+            self.dist.all_reduce(m, op=self.dist.ReduceOp.MAX)
+            torch.cuda.synchronize(dev)
+            ctx.pileup_import(s.data_ptr(), m.data_ptr())
+            fetched = ctx.pileup_fetch()
+        else:  # CPU collective (tests): go through host copies
+            fetched = ctx.pileup_fetch()
+            fetched = reduce_fetched_host(self, fetched, unit_base)
+        events = [None] * self.world
+        self.dist.all_gather_object(events, fetched['events'])
+        fetched['events'] = [e for part in events for e in part]
+        return fetched
+
+
+def reduce_fetched_host(shard, f, unit_base):
+    """Host-side equivalent of the device export/all-reduce/import."""
+    torch, dist = shard.torch, shard.dist
+    out = dict(f)
+    for key, op in (('dense', 'SUM'), ('read_counts', 'SUM'), ('max_pos', 'MAX')):
+        t = torch.as_tensor(np.ascontiguousarray(f[key]).astype(np.int64))
+        dist.all_reduce(t, op=getattr(dist.ReduceOp, op))
+        out[key] = t.numpy().astype(f[key].dtype)
+    for key in ('nflag', 'dflag'):
+        t = torch.as_tensor(np.ascontiguousarray(f[key]).astype(np.int64))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out[key] = t.numpy().astype(np.uint8)
+    fu = np.where(f['first_unit'] < 0, np.iinfo(np.int64).max, f['first_unit'] + unit_base)
+    t = torch.as_tensor(fu.astype(np.int64))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    fu = t.numpy()
+    out['first_unit'] = np.where(fu == np.iinfo(np.int64).max, -1, fu)
+    return out
+
+
+class RemapPipeline:
+    def __init__(self, ctx, config=None, count_threshold=10, rdgopen=10, rfgopen=10,
+                 shard=None, callback=None):
+        self.ctx = ctx
+        self.config = config or ProjectConfig.loadDefault()
+        self.seeds = self.config.all_region_sequences()      # remap.py:450-454
+        self.seed_set = self.config.seed_sequences()         # prelim_map.py:102-106
+        self.count_threshold = count_threshold
+        self.rdgopen, self.rfgopen = rdgopen, rfgopen
+        self.shard = shard
+        self.callback = callback
+        self.raw_count = None
+        self.log = []
+
+    # ---- plumbing --------------------------------------------------------
+    def _params(self, mode):
+        return _native.params(mode, rdg=(self.rdgopen, READ_GAP_EXTEND),
+                              rfg=(self.rfgopen, REF_GAP_EXTEND), maxins=MAXINS)
+
+    def _counts(self):
+        c = self.ctx.map_counts()
+        if self.shard is not None:
+            sh = self.shard
+            for key in ('lines', 'filtered', 'mapped'):
+                c[key] = sh.sum_i64(c[key])
+            for key in ('first_row', 'first_mapped'):
+                c[key] = sh.min_i64(np.where(c[key] >= 0, c[key] + sh.read_base, -1))
+            sf = c['star_first']
+            c['star_first'] = int(sh.min_i64([sf + sh.read_base if sf >= 0 else -1])[0])
+            c['unmapped'], c['star'] = (int(x) for x in sh.sum_i64([c['unmapped'], c['star']]))
+        return c
+
+    def _pileup(self, ref_lens):
+        self.ctx.pileup(0, CONSENSUS_Q_CUTOFF, ref_lens)
+        if self.shard is not None:
+            unit_base = self.shard.read_base // 2 if self.ctx.reads_count()[1] else self.shard.read_base
+            return self.shard.pileup(self.ctx, unit_base)
+        return self.ctx.pileup_fetch()
+
+    # ---- prelim_map ------------------------------------------------------
+    def prelim(self):
+        """End-to-end pass over every seed (prelim_map.py:96-140)."""
+        names = list(self.seed_set)
+        self.ctx.index_build(names, [self.seed_set[n] for n in names], E2E_SEEDLEN)
+        self.ctx.map(self._params(_native.E2E))
+        self.prelim_names = names
+        self.prelim_stats = self._counts()
+        return self.prelim_stats
+
+    def prelim_groups(self):
+        """(rname, count, filtered_count) per rname group of prelim.csv, in
+        file order ('*' included) -- remap.py:485-515."""
+        st = self.prelim_stats
+        groups = [(int(st['first_row'][r]), self.prelim_names[r], int(st['lines'][r]),
+                   int(st['filtered'][r])) for r in range(len(self.prelim_names))
+                  if st['lines'][r] > 0]
+        if st['star']:
+            groups.append((int(st['star_first']), '*', int(st['star']), 0))
+        groups.sort()
+        return [(name, count, filt) for _, name, count, filt in groups]
+
+    def select_seeds(self, groups):
+        """Best rname per seed group above the count threshold
+        (remap.py:517-528)."""
+        refgroups = {}
+        for refname, count, filtered in groups:
+            if refname == '*':
+                continue
+            refgroup = self.config.getSeedGroup(refname)
+            threshold = 1 if refname == 'HIV1B-env-seed' else self.count_threshold
+            _best, best_count = refgroups.get(refgroup, (None, threshold - 1))
+            if filtered > best_count:
+                refgroups[refgroup] = (refname, filtered)
+        return {best_ref: best_count for best_ref, best_count in refgroups.values()}
+
+    def prelim_conseqs(self, seed_counts):
+        """build_conseqs on the prelim alignments, then keep the seed-group
+        winners (remap.py:531-541)."""
+        names = self.prelim_names
+        fetched = self._pileup([len(self.seed_set[n]) for n in names])
+        pile = Pileup(fetched, names)
+        rank = self.prelim_stats['first_row']
+        order = pile.refs_with_reads(rank=np.where(rank < 0, np.iinfo(np.int64).max, rank))
+        conseqs = counts_to_conseqs(pile, order, seeds=self.seeds)
+        new_conseqs, map_counts = {}, {}
+        for rname, conseq in conseqs.items():
+            count = seed_counts.get(rname)
+            if count is not None:
+                map_counts[rname] = count
+                new_conseqs[rname] = conseq
+        return new_conseqs, map_counts
+
+    # ---- remap loop ------------------------------------------------------
+    def map_to_reference(self, refseqs):
+        """One --local pass (remap.py:661-761): returns (new_counts,
+        unmapped_count) with new_counts in first-mapped-line order."""
+        names = list(refseqs)
+        self.ctx.index_build(names, [refseqs[n] for n in names], LOCAL_SEEDLEN)
+        self.ctx.map(self._params(_native.LOCAL))
+        st = self._counts()
+        new_counts = Counter()
+        for r in sorted((r for r in range(len(names)) if st['mapped'][r] > 0),
+                        key=lambda r: st['first_mapped'][r]):
+            new_counts[names[r]] = int(st['mapped'][r])
+        self.last_names = names
+        self.last_refseqs = dict(refseqs)
+        return new_counts, int(st['unmapped'])
+
+    def build_conseqs_filtered(self, refseqs, distance_report=None):
+        """build_conseqs(..., is_filtered=True, filter_coverage=threshold/2)
+        on the last pass (remap.py:576-581)."""
+        names = list(refseqs)
+        fetched = self._pileup([len(refseqs[n]) for n in names])
+        pile = Pileup(fetched, names)
+        order = pile.refs_with_reads()
+        new = counts_to_conseqs(pile, order, seeds=self.seeds)
+        return filter_conseqs(self.ctx, pile, order, new, self.seeds, self.count_threshold / 2,
+                              distance_report)
+
+    def run(self, raw_count, max_iterations=None, remap_counts_writer=None):
+        """The whole of remap()'s loop.  max_iterations caps the number of
+        mapping passes (benchmark configs); None = the reference's rules."""
+        self.raw_count = raw_count
+        self.prelim()
+        groups = self.prelim_groups()
+        if remap_counts_writer is not None:
+            for refname, count, filt in groups:
+                remap_counts_writer.writerow(dict(type='prelim %s' % refname, count=count,
+                                                  filtered_count=filt))
+        seed_counts = self.select_seeds(groups)
+        conseqs, map_counts = self.prelim_conseqs(seed_counts)
+        n_remaps = 0
+        new_counts = Counter()
+        unmapped_count = raw_count
+        while conseqs:
+            if self.callback:
+                self.callback(message='... remap iteration %d' % n_remaps, progress=0)
+            mapped_to = conseqs
+            new_counts, unmapped_count = self.map_to_reference(conseqs)
+            old_seed_names = set(conseqs.keys())
+            distance_report = {}
+            conseqs = self.build_conseqs_filtered(mapped_to, distance_report)
+            new_seed_names = set(conseqs.keys())
+            n_remaps += 1
+            self.log.append(dict(iteration=n_remaps, mapped=dict(new_counts),
+                                 conseqs={k: len(v) for k, v in conseqs.items()}))
+            if remap_counts_writer is not None:
+                write_remap_counts(remap_counts_writer, new_counts, 'remap-{}'.format(n_remaps),
+                                   distance_report)
+            if max_iterations is not None and n_remaps >= max_iterations:
+                break
+            if new_seed_names == old_seed_names:
+                if all((count <= map_counts[refname]) for refname, count in new_counts.items()):
+                    break
+                mapping_efficiency = sum(new_counts.values()) / float(raw_count)
+                if mapping_efficiency > MIN_MAPPING_EFFICIENCY:
+                    break
+                if n_remaps >= MAX_REMAPS:
+                    break
+            map_counts = dict(new_counts)
+        self.conseqs = conseqs
+        self.new_counts = new_counts
+        self.unmapped_count = unmapped_count
+        self.n_remaps = n_remaps
+        return conseqs, new_counts, unmapped_count

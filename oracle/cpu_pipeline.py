@@ -1,0 +1,131 @@
+"""
+oracle/cpu_pipeline.py -- TEST INFRASTRUCTURE ONLY (bench.py's cpu_baseline
+leg and tests).
+
+The same step as bench.py's GPU step -- prelim pass (end-to-end over every
+seed), seed selection, prelim consensus, one --local remap pass over the
+consensus, pileup and consensus again -- run by the CPU oracle: the C
+restatement (og_map with OpenMP over read pairs, og_pileup) plus the Python
+consensus code of oracle.py.
+"""
+import ctypes
+import time
+from collections import Counter
+
+import oracle
+
+
+def _rows_from_alns(alns, seqs, quals, n_reads):
+    """OgRow per read in SAM orientation (what temp.sam would hold)."""
+    comp = str.maketrans('ACGTN', 'TGCAN')
+    rows, keep = [], []
+    for i in range(n_reads):
+        a = alns[i]
+        s = oracle.decode_seq(seqs[i])
+        q = quals[i]
+        if a.ref >= 0 and a.rev:
+            s = s.translate(comp)[::-1]
+            q = q[::-1]
+        sb, qb = s.encode(), q.encode()
+        n = a.n_cigar if a.ref >= 0 and not (a.flag & 4) else 0
+        arr = (ctypes.c_uint32 * max(n, 1))(*a.cigar[:n])
+        keep.append((sb, qb, arr))
+        rows.append(oracle.OgRow(a.flag, a.sam_ref, a.sam_pos, n, arr, len(sb), sb, qb))
+    return rows, keep
+
+
+def _pileup(alns, seqs, quals, n_refs, ref_lens, paired, q=20):
+    n = len(seqs)
+    rows, keep = _rows_from_alns(alns, seqs, quals, n)
+    units = []
+    if paired:
+        for u in range(n // 2):
+            a, b = 2 * u, 2 * u + 1
+            pa, pb = alns[a].sam_ref >= 0, alns[b].sam_ref >= 0
+            if pa and pb:
+                units += [a, b]
+    else:
+        for u in range(n):
+            if alns[u].sam_ref >= 0:
+                units += [u, -1]
+    cap = max(ref_lens) + 2048
+    row_arr = (oracle.OgRow * max(n, 1))(*rows)
+    unit_arr = (ctypes.c_int64 * max(len(units), 1))(*units)
+    dense = (ctypes.c_int32 * (n_refs * cap * 6))()
+    rc = (ctypes.c_int64 * n_refs)()
+    fu = (ctypes.c_int64 * n_refs)(*([-1] * n_refs))
+    mp = (ctypes.c_int32 * n_refs)()
+    ev_cap = n * 256 + 16
+    ev = (oracle.OgEvent * ev_cap)()
+    pool = ctypes.create_string_buffer(ev_cap * 4)
+    ne, used = ctypes.c_int64(), ctypes.c_int64()
+    st = oracle.lib().og_pileup(n_refs, cap, row_arr, len(units) // 2, unit_arr, q, dense, rc, fu, mp,
+                                ev, ev_cap, ctypes.byref(ne), pool, len(pool), ctypes.byref(used))
+    if st:
+        raise RuntimeError('og_pileup status %d' % st)
+    return dense, rc, fu, mp, ev, ne.value, pool.raw, cap
+
+
+def _conseqs(names, seeds, pile, order):
+    dense, rc, fu, mp, ev, ne, pool, cap = pile
+    events = {}
+    for e in ev[:ne]:
+        events.setdefault((e.ref, e.pos), Counter())[pool[e.tok_off:e.tok_off + e.tok_len].decode()] += 1
+    refmap = {}
+    for r in order:
+        pos_nucs = {}
+        for pos in range(1, mp[r] + 1):
+            base = (r * cap + pos - 1) * 6
+            c = Counter()
+            for k, tok in enumerate('ACGT'):
+                if dense[base + k]:
+                    c[tok] = dense[base + k]
+            if dense[base + 4]:
+                c['N'] = -1
+            if dense[base + 5]:
+                c['-'] = -2
+            c.update(events.get((r, pos), {}))
+            if c:
+                pos_nucs[pos] = c
+        refmap[names[r]] = (pos_nucs, mp[r])
+    return oracle.counts_to_conseqs(refmap, seeds)[0]
+
+
+def run_step(seed_set, all_seeds, seed_groups, seqs, quals, paired=True, nthreads=0,
+             count_threshold=10):
+    """prelim + one remap iteration on the CPU oracle; returns (conseqs, seconds)."""
+    t0 = time.perf_counter()
+    names = list(seed_set)
+    ix = oracle.Index([seed_set[n] for n in names], 22)
+    alns = oracle.map_reads(ix, oracle.params(oracle.E2E), seqs, quals, paired, nthreads)
+    n = len(seqs)
+    lines, filt, first = Counter(), Counter(), {}
+    for i in range(n):
+        a = alns[i]
+        if a.sam_ref < 0:
+            continue
+        name = names[a.sam_ref]
+        lines[name] += 1
+        first.setdefault(name, i)
+        if not (a.flag & 4):
+            mx = max([c >> 4 for c in a.cigar[:a.n_cigar] if (c & 15) == 0] or [0])
+            if mx > 50:
+                filt[name] += 1
+    refgroups = {}
+    for name in sorted(first, key=first.get):
+        thr = 1 if name == 'HIV1B-env-seed' else count_threshold
+        _b, best = refgroups.get(seed_groups[name], (None, thr - 1))
+        if filt[name] > best:
+            refgroups[seed_groups[name]] = (name, filt[name])
+    seed_counts = {r: c for r, c in refgroups.values()}
+    pile = _pileup(alns, seqs, quals, len(names), [len(seed_set[k]) for k in names], paired)
+    order = sorted((r for r in range(len(names)) if pile[2][r] >= 0), key=lambda r: first[names[r]])
+    conseqs = {k: v for k, v in _conseqs(names, all_seeds, pile, order).items() if k in seed_counts}
+    if conseqs:
+        cn = list(conseqs)
+        ix2 = oracle.Index([conseqs[k] for k in cn], 20)
+        alns2 = oracle.map_reads(ix2, oracle.params(oracle.LOCAL), seqs, quals, paired, nthreads)
+        pile2 = _pileup(alns2, seqs, quals, len(cn), [len(conseqs[k]) for k in cn], paired)
+        order2 = sorted((r for r in range(len(cn)) if pile2[2][r] >= 0), key=lambda r: pile2[2][r])
+        conseqs = _conseqs(cn, all_seeds, pile2, order2)
+    return conseqs, time.perf_counter() - t0

@@ -186,8 +186,13 @@ def cigar_string(aln):
 _COMP = str.maketrans('ACGTN', 'TGCAN')
 
 
+_DECODE = {i: 'N' for i in range(256)}
+_DECODE.update({ord(c): c.upper() for c in 'ACGTacgt'})
+
+
 def decode_seq(seq):
-    return ''.join(c if c in 'ACGT' else 'N' for c in seq.upper())
+    """bowtie2 prints reads as upper-case ACGT with every other letter N."""
+    return seq.translate(_DECODE)
 
 
 def sam_fields(aln, qname, seq, qual, refnames):
