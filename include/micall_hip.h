@@ -92,6 +92,9 @@ int mh_reads_load(mh_ctx *ctx, int64_t n_reads, int paired, const uint8_t *seq,
  * Keeps the read names (bowtie2 QNAME rules) for mh_format_rows. */
 int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64_t *n_reads);
 int mh_reads_count(mh_ctx *ctx, int64_t *n_reads, int *paired);
+/* newlines in FASTQ 1 of the last mh_reads_load_fastq (the `gunzip -c | wc
+ * -l` of LineCounter, externals.py:206-231; raw_count = lines / 2). */
+int mh_reads_fastq_lines(mh_ctx *ctx, int64_t *lines1);
 
 /* ---- one mapping pass: replaces `bowtie2 [--local] ...` ---------------- */
 int mh_map(mh_ctx *ctx, const mh_params *par);
@@ -127,6 +130,17 @@ int mh_rows_load(mh_ctx *ctx, int64_t n_rows, const int32_t *flag, const int32_t
                  const uint32_t *cigar, const uint8_t *seq, const uint8_t *qual,
                  const int64_t *offsets, const int32_t *lens, int64_t n_units,
                  const int64_t *unit_rows);
+/* prelim.csv text (prelim_map.py:142-151) read back as remap() does
+ * (remap.py:474-498): csv quoting, rname -> index into refnames (the @SQ
+ * set), matchmaker pairing by qname, upload as rows.  mh_rows_info then
+ * gives per row: name id (>= 0 index into refnames, < 0 other names such
+ * as '*'), flag, longest M run (is_short_read, remap.py:70-83), ref index. */
+int mh_rows_load_csv(mh_ctx *ctx, const char *text, int64_t len, int n_refs,
+                     const char *const *refnames, int64_t *n_rows, int64_t *n_units,
+                     int32_t *n_present);
+/* out4 per row: name id, flag, longest M run, compact ref id; present[k] =
+ * @SQ index of compact ref k; unknown = '\n'-joined names outside @SQ. */
+int mh_rows_info(mh_ctx *ctx, int32_t *out4, int32_t *present, char *unknown, size_t cap);
 /* source 0 = alignments of the last mh_map (units = pairs / reads),
  * source 1 = rows from mh_rows_load.  n_refs/ref_lens size the dense
  * counters (positions 1..ref_lens[r] + MH_PILEUP_SLACK). */

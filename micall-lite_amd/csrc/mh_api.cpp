@@ -113,6 +113,10 @@ struct CtxEx : Ctx {
     // index cache: large (fixed seed-set) indexes are kept by content signature
     std::vector<DevIndex> cache;
     std::vector<Rec> rec_cache;
+    std::vector<int32_t> csv_rows_info;   // per prelim.csv row: name id, flag, max M run, ref
+    std::vector<int32_t> csv_present;     // compact ref id -> index into the @SQ list
+    std::vector<std::string> csv_unknown; // names outside @SQ, by -1 - name id
+    int64_t fastq_lines1 = -1;            // newlines in FASTQ 1 (LineCounter, externals.py:206)
 };
 
 static void free_index(DevIndex &ix)
@@ -294,7 +298,7 @@ struct Fastq {
     std::vector<int32_t> len;
 };
 
-static int read_fastq(const char *path, Fastq &fq, bool paired)
+static int read_fastq(const char *path, Fastq &fq, bool paired, int64_t *newlines = nullptr)
 {
     gzFile f = gzopen(path, "rb");
     if (!f) { set_error("cannot open FASTQ %s", path); return -3; }
@@ -306,6 +310,7 @@ static int read_fastq(const char *path, Fastq &fq, bool paired)
     const bool err = got < 0;
     gzclose(f);
     if (err) { set_error("gzip error reading %s", path); return -3; }
+    if (newlines) *newlines = (int64_t)std::count(data.begin(), data.end(), '\n');
     size_t p = 0, n = data.size();
     auto line = [&](size_t &a, size_t &b) -> bool {
         if (p >= n) return false;
@@ -496,7 +501,8 @@ int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64
     MH_HIP(hipSetDevice(c->device));
     const bool paired = path2 != nullptr;
     Fastq a, b;
-    if (int st = read_fastq(path1, a, paired)) return st;
+    int64_t lines1 = 0;
+    if (int st = read_fastq(path1, a, paired, &lines1)) return st;
     std::vector<std::string> names;
     std::vector<uint8_t> seq, qual;
     std::vector<int64_t> off;
@@ -539,6 +545,7 @@ int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64
     if (st) return st;
     c->names.swap(names);
     c->map.valid = false;
+    c->fastq_lines1 = lines1;
     if (n_reads) *n_reads = n;
     return 0;
 }
@@ -795,7 +802,7 @@ int mh_rows_load(mh_ctx *ctx, int64_t n_rows, const int32_t *flag, const int32_t
         ncig = std::max<int64_t>(ncig, (int64_t)cigar_off[i] + n_cigar[i]);
         for (int k = 0; k < n_cigar[i]; ++k) {
             const uint32_t op = cigar[cigar_off[i] + k] & 15;
-            if (op != MH_OP_M && op != MH_OP_I && op != MH_OP_D && op != MH_OP_S) {
+            if (op != MH_OP_M && op != MH_OP_I && op != MH_OP_D && op != MH_OP_S && op != 3) {
                 set_error("Unsupported CIGAR token in row %lld", (long long)i);
                 return -3;
             }
@@ -830,6 +837,211 @@ int mh_rows_load(mh_ctx *ctx, int64_t n_rows, const int32_t *flag, const int32_t
     R.n_units = n_units;
     HostReads dummy;
     return load_reads(*c, R.reads, dummy, n_rows, 0, seq, qual, offsets, lens, false);
+}
+
+// ---- prelim.csv reader ------------------------------------------------------
+// csv.DictReader semantics for the 11 SAM columns prelim_map writes
+// (prelim_map.py:142-151), then remap.matchmaker (remap.py:853-889) over the
+// rows whose rname is in the @SQ set, then the rows go to the device.
+namespace mh {
+struct CsvRows {
+    std::vector<int32_t> flag, ref, pos, cig_off, n_cigar, maxm, name_id;
+    std::vector<uint32_t> cigar;
+    std::vector<uint8_t> seq, qual;
+    std::vector<int64_t> off;
+    std::vector<int32_t> len;
+    std::vector<int64_t> units;
+};
+
+static bool csv_record(const char *&p, const char *end, std::vector<std::string> &f)
+{
+    f.clear();
+    if (p >= end) return false;
+    std::string cur;
+    bool any = false;
+    for (;;) {
+        cur.clear();
+        if (p < end && *p == '"') {
+            ++p;
+            while (p < end) {
+                if (*p == '"') {
+                    if (p + 1 < end && p[1] == '"') { cur.push_back('"'); p += 2; continue; }
+                    ++p;
+                    break;
+                }
+                cur.push_back(*p++);
+            }
+            while (p < end && *p != ',' && *p != '\n' && *p != '\r') cur.push_back(*p++);
+        } else {
+            while (p < end && *p != ',' && *p != '\n' && *p != '\r') cur.push_back(*p++);
+        }
+        f.push_back(cur);
+        any = true;
+        if (p < end && *p == ',') { ++p; continue; }
+        if (p < end && *p == '\r') ++p;
+        if (p < end && *p == '\n') ++p;
+        break;
+    }
+    return any;
+}
+
+static bool parse_cigar_ops(const std::string &c, std::vector<uint32_t> &ops, int &maxm)
+{
+    // ^((\d+)([MIDNSHPX=]))*$ ; only M/I/D/S are usable (sam2aln.py:113-142)
+    ops.clear();
+    maxm = 0;
+    size_t i = 0;
+    bool ok = true;
+    while (i < c.size()) {
+        size_t j = i;
+        uint64_t n = 0;
+        while (j < c.size() && c[j] >= '0' && c[j] <= '9') { n = n * 10 + (c[j] - '0'); ++j; }
+        if (j == i || j >= c.size()) return false;
+        const char op = c[j];
+        uint32_t code;
+        switch (op) {
+        case 'M': code = MH_OP_M; if ((int)n > maxm) maxm = (int)n; break;
+        case 'I': code = MH_OP_I; break;
+        case 'D': code = MH_OP_D; break;
+        case 'S': code = MH_OP_S; break;
+        case 'N': case 'H': case 'P': case 'X': case '=': code = 3; ok = false; break;  // unsupported
+        default: return false;
+        }
+        ops.push_back(((uint32_t)n << 4) | code);
+        i = j + 1;
+    }
+    (void)ok;
+    return true;
+}
+}  // namespace mh
+
+extern "C" int mh_rows_load_csv(mh_ctx *ctx, const char *text, int64_t len, int n_refs,
+                                const char *const *refnames, int64_t *n_rows, int64_t *n_units,
+                                int32_t *n_present)
+{
+    if (!ctx || !text || len < 0 || n_refs < 0) return -3;
+    CtxEx *c = X(ctx);
+    std::unordered_map<std::string, int> refidx;
+    for (int r = 0; r < n_refs; ++r) refidx.emplace(refnames[r], r);
+    const char *p = text, *end = text + len;
+    std::vector<std::string> f;
+    if (!csv_record(p, end, f)) { set_error("prelim csv: empty"); return -3; }
+    const char *want[11] = {"qname", "flag", "rname", "pos", "mapq", "cigar", "rnext", "pnext",
+                            "tlen", "seq", "qual"};
+    int col[11];
+    for (int k = 0; k < 11; ++k) {
+        col[k] = -1;
+        for (size_t z = 0; z < f.size(); ++z) if (f[z] == want[k]) col[k] = (int)z;
+        if (col[k] < 0) { set_error("prelim csv: missing column %s", want[k]); return -3; }
+    }
+    CsvRows R;
+    std::unordered_map<std::string, int64_t> pending;   // qname -> slot in order
+    std::vector<std::pair<int64_t, bool>> order;         // (row, alive) insertion order
+    std::vector<uint32_t> ops;
+    std::unordered_map<std::string, int> unknown;
+    while (csv_record(p, end, f)) {
+        if (f.size() == 1 && f[0].empty()) continue;
+        if ((int)f.size() < 11) { set_error("prelim csv: short row"); return -3; }
+        const int64_t row = (int64_t)R.flag.size();
+        const std::string &qname = f[col[0]], &rname = f[col[2]], &seqs = f[col[9]], &quals = f[col[10]];
+        const int flag = std::atoi(f[col[1]].c_str());
+        auto it = refidx.find(rname);
+        int ref = it == refidx.end() ? -1 : it->second;
+        int nid = ref;
+        if (ref < 0) {
+            auto u = unknown.emplace(rname, (int)unknown.size());
+            nid = -1 - u.first->second;   // '*' and other names outside @SQ
+        }
+        int maxm = 0;
+        R.cig_off.push_back((int32_t)R.cigar.size());
+        if (!(flag & 4)) {
+            if (!parse_cigar_ops(f[col[5]], ops, maxm)) ops.assign(1, 3u);  // invalid: fails if used
+            if (ops.size() > MH_MAXOPS) ops.assign(1, 3u);
+        } else {
+            ops.clear();
+        }
+        R.cigar.insert(R.cigar.end(), ops.begin(), ops.end());
+        R.n_cigar.push_back((int32_t)ops.size());
+        R.flag.push_back(flag);
+        R.ref.push_back(ref);
+        R.name_id.push_back(nid);
+        R.pos.push_back(std::atoi(f[col[3]].c_str()));
+        R.maxm.push_back(maxm);
+        R.off.push_back((int64_t)R.seq.size());
+        R.len.push_back((int32_t)seqs.size());
+        R.seq.insert(R.seq.end(), seqs.begin(), seqs.end());
+        std::string q = quals;
+        q.resize(seqs.size(), 'J');
+        R.qual.insert(R.qual.end(), q.begin(), q.end());
+        if (ref >= 0) {
+            auto pit = pending.find(qname);
+            if (pit == pending.end()) {
+                pending.emplace(qname, (int64_t)order.size());
+                order.push_back({row, true});
+            } else {
+                order[pit->second].second = false;
+                R.units.push_back(order[pit->second].first);
+                R.units.push_back(row);
+                pending.erase(pit);
+            }
+        }
+    }
+    for (auto &o : order) if (o.second) { R.units.push_back(o.first); R.units.push_back(-1); }
+    const int64_t nr = (int64_t)R.flag.size();
+    const int64_t nu = (int64_t)R.units.size() / 2;
+    // compact reference ids: only references some unit row names, in @SQ
+    // order (keeps the dense counters small); rows outside @SQ are never
+    // paired and get compact id 0 (unused)
+    std::vector<int32_t> used(n_refs > 0 ? n_refs : 1, 0);
+    for (int64_t k = 0; k < 2 * nu; ++k) if (R.units[k] >= 0) used[R.ref[R.units[k]]] = 1;
+    std::vector<int32_t> compact(n_refs > 0 ? n_refs : 1, -1);
+    c->csv_present.clear();
+    for (int r = 0; r < n_refs; ++r)
+        if (used[r]) { compact[r] = (int32_t)c->csv_present.size(); c->csv_present.push_back(r); }
+    std::vector<int32_t> dref(R.ref);
+    for (auto &x : dref) x = (x >= 0 && compact[x] >= 0) ? compact[x] : 0;
+    c->csv_unknown.assign(unknown.size(), std::string());
+    for (auto &kv : unknown) c->csv_unknown[kv.second] = kv.first;
+    int st = mh_rows_load(ctx, nr, R.flag.data(), dref.data(), R.pos.data(), R.cig_off.data(),
+                          R.n_cigar.data(), R.cigar.empty() ? nullptr : R.cigar.data(),
+                          R.seq.data(), R.qual.data(), R.off.data(), R.len.data(), nu,
+                          R.units.data());
+    if (st) return st;
+    c->csv_rows_info.clear();
+    c->csv_rows_info.reserve(nr * 4);
+    for (int64_t i = 0; i < nr; ++i) {
+        c->csv_rows_info.push_back(R.name_id[i]);
+        c->csv_rows_info.push_back(R.flag[i]);
+        c->csv_rows_info.push_back(R.maxm[i]);
+        c->csv_rows_info.push_back(dref[i]);
+    }
+    if (n_rows) *n_rows = nr;
+    if (n_units) *n_units = nu;
+    if (n_present) *n_present = (int32_t)c->csv_present.size();
+    return 0;
+}
+
+extern "C" int mh_rows_info(mh_ctx *ctx, int32_t *out4, int32_t *present, char *unknown,
+                            size_t cap)
+{
+    if (!ctx) return -3;
+    CtxEx *c = X(ctx);
+    if (out4) std::memcpy(out4, c->csv_rows_info.data(), sizeof(int32_t) * c->csv_rows_info.size());
+    if (present) std::memcpy(present, c->csv_present.data(), sizeof(int32_t) * c->csv_present.size());
+    if (unknown) {
+        std::string all;
+        for (auto &u : c->csv_unknown) { all += u; all.push_back('\n'); }
+        if (all.size() + 1 > cap) { set_error("mh_rows_info: name buffer too small"); return -2; }
+        std::memcpy(unknown, all.c_str(), all.size() + 1);
+    }
+    return 0;
+}
+
+extern "C" int mh_reads_fastq_lines(mh_ctx *ctx, int64_t *lines1)
+{
+    if (!ctx || !lines1) return -3;
+    *lines1 = X(ctx)->fastq_lines1;
+    return 0;
 }
 
 int mh_pileup(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *ref_lens)

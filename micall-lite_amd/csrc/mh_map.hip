@@ -351,11 +351,12 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     const int wv = wave_uniform(threadIdx.x >> 6);
     const int wpb = blockDim.x >> 6;
     unsigned char *wbase = smem + (size_t)wv * A.wave_lds;
-    uint32_t *bits = (uint32_t *)wbase;                       // rows_pad/8 * 64
-    uint32_t *tab = bits + (A.rows_pad >> 3) * 64;            // rows_pad
-    uint8_t *refw = (uint8_t *)(tab + A.rows_pad);            // rows_pad + 64 (code*4)
-    uint8_t *rdc = refw + A.rows_pad + 64;                    // rows_pad
-    uint8_t *ops = rdc + A.rows_pad;                          // 2*rows_pad + 128
+    uint32_t *bits = (uint32_t *)wbase;                       // rows_pad/8 * 64: 4 bits/cell
+    uint32_t *tab = bits + (A.rows_pad >> 3) * 64;            // rows_pad: score nibbles per row
+    uint32_t *runs = tab + A.rows_pad;                        // rows_pad + 128: CIGAR runs (reversed)
+    uint8_t *refw = (uint8_t *)(runs + A.rows_pad + 128);     // rows_pad + 64: ref code * 4
+    uint8_t *rdc = refw + A.rows_pad + 64;                    // rows_pad: read codes
+    uint8_t *rowk = rdc + A.rows_pad;                         // rows_pad: lane of the M cell, 255 none
     const int ma = LOCAL ? 2 : 0;
     const int n_work = A.counters[0];
     const int xD = lane * A.exD;                  // X = H1 + exD*lane
@@ -373,75 +374,87 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         const int strand = cd.strand;
 
         // ---- stage per-row score tables, read codes and the ref window ----
-        for (int i = lane; i < m; i += 64) {
-            const int b = strand ? m - 1 - i : i;
-            uint32_t c = read_code(A.R, roff, b);
-            if (strand && c < 4) c = 3 - c;
-            const int pen = mm_pen(A.R.qual[roff + b]);
-            uint32_t tb = 0;
-            for (int g = 0; g < 5; ++g) {
-                const int sc = (c > 3 || g > 3) ? -NPEN : (c == (uint32_t)g ? ma : -pen);
-                tb |= (uint32_t)(sc + 8) << (4 * g);
+        for (int i = lane; i < A.rows_pad; i += 64) {
+            uint32_t tb = 0x88888u, c = 4;
+            if (i < m) {
+                const int b = strand ? m - 1 - i : i;
+                c = read_code(A.R, roff, b);
+                if (strand && c < 4) c = 3 - c;
+                const int pen = mm_pen(A.R.qual[roff + b]);
+                tb = 0;
+                for (int g = 0; g < 5; ++g) {
+                    const int sc = (c > 3 || g > 3) ? -NPEN : (c == (uint32_t)g ? ma : -pen);
+                    tb |= (uint32_t)(sc + 8) << (4 * g);
+                }
             }
             tab[i] = tb;
             rdc[i] = (uint8_t)c;
+            rowk[i] = 255;
         }
-        for (int x = lane; x < m + 64; x += 64) {
+        for (int x = lane; x < A.rows_pad + 64; x += 64) {
             const int j = d0 + x;
             const int g = (j >= 0 && j < reflen) ? A.I.codes[gref + j] : 4;
             refw[x] = (uint8_t)(g * 4);
         }
         wave_sync();
 
-        // ---- DP over rows ----
+        // ---- DP over rows, 8 rows per group: the group's LDS loads first ----
         int Hp = 0, Ep = NEG;
         int bestH = NEG, bestI = 0;
-        uint32_t acc = 0;
-        for (int i = 0; i < m; ++i) {
-            const bool gap_ok = i >= GBAR && i < m - GBAR;
-            const int rc4 = refw[i + lane];
-            const uint32_t tb = tab[i];
-            const int s = (int)((tb >> rc4) & 15u) - 8;
-            const int Hd = Hp + s;
-            int E = NEG, eb = 0, H, fb = 0;
-            if (gap_ok) {
-                const int eu = dpp<DPP_WAVE_SHL1>(NEG, Ep) - A.exI;
-                const int hu = dpp<DPP_WAVE_SHL1>(NEG, Hp) - A.oeI;
-                E = imax(eu, hu);
-                eb = eu > hu;
+        for (int i0 = 0; i0 < m; i0 += 8) {
+            uint32_t tbv[8];
+            int rcv[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                tbv[t] = tab[i0 + t];
+                rcv[t] = refw[i0 + t + lane];
             }
-            int H1 = imax(Hd, E);
-            if (LOCAL) H1 = imax(H1, 0);
-            if (gap_ok) {
-                const int X = H1 + xD;
-                int P = X;
-                P = imax(P, dpp<DPP_ROW_SHR1>(NEG, P));
-                P = imax(P, dpp<DPP_ROW_SHR2>(NEG, P));
-                P = imax(P, dpp<DPP_ROW_SHR4>(NEG, P));
-                P = imax(P, dpp<DPP_ROW_SHR8>(NEG, P));
-                P = imax(P, dpp<DPP_ROW_BCAST15, 0xA>(NEG, P));
-                P = imax(P, dpp<DPP_ROW_BCAST31, 0xC>(NEG, P));
-                const int gt = P > X;
-                fb = dpp<DPP_WAVE_SHR1>(0, gt);
-                const int F = dpp<DPP_WAVE_SHR1>(NEG, P) + cF;
-                H = imax(H1, F);
-            } else {
-                H = H1;
+            uint32_t acc = 0;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int i = i0 + t;
+                if (i < m) {
+                    const bool gap_ok = i >= GBAR && i < m - GBAR;
+                    const int s = (int)((tbv[t] >> rcv[t]) & 15u) - 8;
+                    const int Hd = Hp + s;
+                    int E = NEG, eb = 0, H, fb = 0;
+                    if (gap_ok) {
+                        const int eu = dpp<DPP_WAVE_SHL1>(NEG, Ep) - A.exI;
+                        const int hu = dpp<DPP_WAVE_SHL1>(NEG, Hp) - A.oeI;
+                        E = imax(eu, hu);
+                        eb = eu > hu;
+                    }
+                    int H1 = imax(Hd, E);
+                    if (LOCAL) H1 = imax(H1, 0);
+                    if (gap_ok) {
+                        const int X = H1 + xD;
+                        int P = X;
+                        P = imax(P, dpp<DPP_ROW_SHR1>(NEG, P));
+                        P = imax(P, dpp<DPP_ROW_SHR2>(NEG, P));
+                        P = imax(P, dpp<DPP_ROW_SHR4>(NEG, P));
+                        P = imax(P, dpp<DPP_ROW_SHR8>(NEG, P));
+                        P = imax(P, dpp<DPP_ROW_BCAST15, 0xA>(NEG, P));
+                        P = imax(P, dpp<DPP_ROW_BCAST31, 0xC>(NEG, P));
+                        const int gt = P > X;
+                        fb = dpp<DPP_WAVE_SHR1>(0, gt);
+                        const int F = dpp<DPP_WAVE_SHR1>(NEG, P) + cF;
+                        H = imax(H1, F);
+                    } else {
+                        H = H1;
+                    }
+                    const int src = (LOCAL && H == 0) ? 0 : (H == Hd ? 1 : (H == E ? 2 : 3));
+                    acc |= (uint32_t)(src | (eb << 2) | (fb << 3)) << (4 * t);
+                    if (LOCAL) {
+                        if (H > bestH) { bestH = H; bestI = i; }
+                    } else if (i == m - 1) {
+                        bestH = H;
+                        bestI = i;
+                    }
+                    Hp = H;
+                    Ep = E;
+                }
             }
-            const int src = (LOCAL && H == 0) ? 0 : (H == Hd ? 1 : (H == E ? 2 : 3));
-            acc |= (uint32_t)(src | (eb << 2) | (fb << 3)) << (4 * (i & 7));
-            if ((i & 7) == 7 || i == m - 1) {
-                bits[(i >> 3) * 64 + lane] = acc;
-                acc = 0;
-            }
-            if (LOCAL) {
-                if (H > bestH) { bestH = H; bestI = i; }
-            } else if (i == m - 1) {
-                bestH = H;
-                bestI = i;
-            }
-            Hp = H;
-            Ep = E;
+            bits[(i0 >> 3) * 64 + lane] = acc;
         }
         // best cell: max score, then smallest row, then smallest lane
         const long long key = (long long)bestH * 1048576ll + (long long)((1023 - bestI) << 6) +
@@ -450,130 +463,159 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         const int best = (int)(bk >> 20);
         const int bi = 1023 - (int)((bk >> 6) & 1023);
         const int bl = 63 - (int)(bk & 63);
+        const int minsc = A.len_tab[(MAXLEN + 1) + m];
         wave_sync();
+
+        // ---- traceback (lane 0): CIGAR runs, back to front, and the lane of
+        // every M row (rowk) for the lane-parallel statistics below ----
+        int tb_ok = 0, t_start = 0, t_first = 0, t_nrun = 0;
+#ifndef MH_ABLATE_NOTB
+        if (lane == 0 && !(LOCAL && best <= 0) && best >= minsc) {
+            int i = bi, k = bl, state = 0, ok = 1;
+            int wr = -1, wk = -1;
+            uint32_t word = 0;
+            int rop = -1, rlen = 0, nrun = 0, first_j = 0;
+            for (;;) {
+                const int g = i >> 3;
+                if (g != wr || k != wk) { word = bits[g * 64 + k]; wr = g; wk = k; }
+                const uint32_t nib = (word >> (4 * (i & 7))) & 15u;
+                int op;
+                if (state == 0) {
+                    const int src = nib & 3;
+                    if (src == 0) break;
+                    if (src != 1) { state = src == 2 ? 1 : 2; continue; }
+                    op = MH_OP_M;
+                } else {
+                    op = state == 1 ? MH_OP_I : MH_OP_D;
+                }
+                if (op == rop) ++rlen;
+                else {
+                    if (rlen) runs[nrun++] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                    rop = op;
+                    rlen = 1;
+                }
+                if (op == MH_OP_M) {
+                    rowk[i] = (uint8_t)k;
+                    first_j = i + d0 + k;
+                    if (--i < 0) break;
+                } else if (op == MH_OP_I) {
+                    state = (nib >> 2) & 1 ? 1 : 0;
+                    --i; ++k;
+                    if (i < 0 || k >= BAND) { ok = 0; break; }
+                } else {
+                    state = (nib >> 3) & 1 ? 2 : 0;
+                    --k;
+                    if (k < 0) { ok = 0; break; }
+                }
+            }
+            if (rlen) runs[nrun++] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+            tb_ok = ok;
+            t_start = i + 1;
+            t_first = first_j;
+            t_nrun = nrun;
+        }
+#endif
+        wave_sync();
+        tb_ok = __builtin_amdgcn_readfirstlane(tb_ok);
+        t_start = __builtin_amdgcn_readfirstlane(t_start);
+        t_first = __builtin_amdgcn_readfirstlane(t_first);
+        t_nrun = __builtin_amdgcn_readfirstlane(t_nrun);
 
         Slot out{};
         out.valid = 0;
         out.strand = strand;
         out.ref = cd.ref;
-        if (lane == 0) {
-            const int minsc = A.len_tab[(MAXLEN + 1) + m];
-            bool ok = !(LOCAL && best <= 0) && best >= minsc;
-            int nops = 0, first_j = 0, start_i = 0;
-            const int last_j = bi + d0 + bl;
-            if (ok) {
-                int i = bi, k = bl, state = 0;
-                for (;;) {
-                    const uint32_t nib = (bits[(i >> 3) * 64 + k] >> (4 * (i & 7))) & 15u;
-                    if (state == 0) {
-                        const int src = nib & 3;
-                        if (src == 0) break;
-                        if (src == 1) {
-                            ops[nops++] = MH_OP_M;
-                            first_j = i + d0 + k;
-                            if (--i < 0) break;
-                        } else {
-                            state = src == 2 ? 1 : 2;
-                        }
-                    } else if (state == 1) {
-                        ops[nops++] = MH_OP_I;
-                        state = (nib >> 2) & 1 ? 1 : 0;
-                        --i; ++k;
-                        if (i < 0 || k >= BAND) { ok = false; break; }
-                    } else {
-                        ops[nops++] = MH_OP_D;
-                        state = (nib >> 3) & 1 ? 2 : 0;
-                        --k;
-                        if (k < 0) { ok = false; break; }
-                    }
-                }
-                start_i = i + 1;
+        if (tb_ok) {
+            // ambiguous positions over the untrimmed alignment (--n-ceil)
+            int nn = 0;
+            for (int i = t_start + lane; i <= bi; i += 64) {
+                const int k = rowk[i];
+                if (k != 255 && (rdc[i] > 3 || refw[i + k] > 12)) ++nn;
             }
-            if (ok) {
-                for (int a = 0, z = nops - 1; a < z; ++a, --z) {
-                    const uint8_t t = ops[a]; ops[a] = ops[z]; ops[z] = t;
-                }
-                int nn = 0, ri = start_i, rj = first_j;
-                for (int o = 0; o < nops; ++o) {
-                    if (ops[o] == MH_OP_M) {
-                        const int g = refw[rj - d0] >> 2;
-                        if (rdc[ri] > 3 || g > 3) ++nn;
-                        ++ri; ++rj;
-                    } else if (ops[o] == MH_OP_I) {
-                        ++ri;
-                    } else {
-                        ++rj;
-                    }
-                }
-                if (nn > A.len_tab[2 * (MAXLEN + 1) + m]) ok = false;
-            }
-            int lo = 0, hi = nops, clipL = start_i, clipR = m - 1 - bi, jL = first_j, jR = last_j;
-            if (ok) {
-                while (lo < hi && !(ops[lo] == MH_OP_M && jL >= 0)) {
-                    if (ops[lo] == MH_OP_M) { ++clipL; ++jL; }
-                    else if (ops[lo] == MH_OP_I) ++clipL;
-                    else ++jL;
-                    ++lo;
-                }
-                while (hi > lo && !(ops[hi - 1] == MH_OP_M && jR < reflen)) {
-                    if (ops[hi - 1] == MH_OP_M) { ++clipR; --jR; }
-                    else if (ops[hi - 1] == MH_OP_I) ++clipR;
-                    else --jR;
-                    --hi;
-                }
-                if (lo >= hi) ok = false;
-            }
-            if (ok) {
-                // count runs first so the pool slice is allocated once
-                int nc = (clipL > 0) + (clipR > 0);
-                for (int o = lo; o < hi;) {
-                    int p = o + 1;
-                    while (p < hi && ops[p] == ops[o]) ++p;
-                    ++nc;
-                    o = p;
-                }
-                if (nc > MH_MAXOPS - 1) ok = false;
-                if (ok) {
-                    const int64_t base = atomicAdd(&A.pool_ctr[0], nc);
-                    if (base + nc > A.pool_cap) {
-                        atomicExch(&A.pool_ctr[1], 1);
-                        ok = false;
-                    } else {
-                        uint32_t *cg = A.pool + base;
-                        int n = 0, xm = 0, xo = 0, xg = 0;
-                        int ri = clipL, rj = jL;
-                        if (clipL) cg[n++] = ((uint32_t)clipL << 4) | MH_OP_S;
-                        for (int o = lo; o < hi;) {
-                            int p = o + 1;
-                            while (p < hi && ops[p] == ops[o]) ++p;
-                            const int len = p - o;
-                            cg[n++] = ((uint32_t)len << 4) | ops[o];
-                            if (ops[o] == MH_OP_M) {
-                                for (int x = 0; x < len; ++x, ++ri, ++rj) {
-                                    const int g = refw[rj - d0] >> 2;
-                                    const int rb = rdc[ri];
-                                    if (rb > 3 || g > 3 || rb != g) ++xm;
-                                }
-                            } else {
-                                ++xo;
-                                xg += len;
-                                if (ops[o] == MH_OP_I) ri += len; else rj += len;
-                            }
-                            o = p;
-                        }
-                        if (clipR) cg[n++] = ((uint32_t)clipR << 4) | MH_OP_S;
-                        out.valid = 1;
-                        out.pos = jL;
-                        out.end = jR + 1;
-                        out.score = best;
-                        out.xm = xm; out.xo = xo; out.xg = xg; out.nm = xm + xg;
-                        out.n_cigar = n;
-                        out.cig_off = (int32_t)base;
-                    }
-                }
-            }
-            A.slot[sid] = out;
+            nn = wave_sum(nn);
+            if (nn > A.len_tab[2 * (MAXLEN + 1) + m]) tb_ok = 0;
         }
+        if (tb_ok) {
+            // trim overhanging columns into soft clips, on the runs (lane 0)
+            int c_ok = 0, clipL = t_start, clipR = m - 1 - bi, jL = t_first, jR = bi + d0 + bl;
+            if (lane == 0) {
+                int lo = t_nrun - 1, hi = 0;   // forward order is runs[nrun-1] .. runs[0]
+                uint32_t front = lo >= 0 ? runs[lo] : 0, back = runs[0];
+                while (lo >= hi) {
+                    const int op = front & 15, len = (int)(front >> 4);
+                    if (op == MH_OP_M && jL >= 0) break;
+                    if (op == MH_OP_M) {
+                        const int t = -jL < len ? -jL : len;
+                        clipL += t; jL += t;
+                        if (t < len) { front = ((uint32_t)(len - t) << 4) | MH_OP_M; continue; }
+                    } else if (op == MH_OP_I) {
+                        clipL += len;
+                    } else {
+                        jL += len;
+                    }
+                    if (--lo >= hi) front = runs[lo];
+                }
+                if (lo == hi) back = front;   // one run left: keep the front's trim
+                while (hi <= lo) {
+                    const int op = back & 15, len = (int)(back >> 4);
+                    if (op == MH_OP_M && jR < reflen) break;
+                    if (op == MH_OP_M) {
+                        const int t = jR - reflen + 1 < len ? jR - reflen + 1 : len;
+                        clipR += t; jR -= t;
+                        if (t < len) { back = ((uint32_t)(len - t) << 4) | MH_OP_M; continue; }
+                    } else if (op == MH_OP_I) {
+                        clipR += len;
+                    } else {
+                        jR -= len;
+                    }
+                    if (++hi <= lo) back = hi == lo ? front : runs[hi];
+                }
+                if (lo >= hi) {
+                    int nc = (clipL > 0) + (clipR > 0) + (lo - hi + 1);
+                    if (nc <= MH_MAXOPS - 1) {
+                        const int64_t base = atomicAdd(&A.pool_ctr[0], nc);
+                        if (base + nc > A.pool_cap) {
+                            atomicExch(&A.pool_ctr[1], 1);
+                        } else {
+                            uint32_t *cg = A.pool + base;
+                            int n = 0, xo = 0, xg = 0;
+                            if (clipL) cg[n++] = ((uint32_t)clipL << 4) | MH_OP_S;
+                            for (int z = lo; z >= hi; --z) {
+                                const uint32_t rr = z == hi ? back : (z == lo ? front : runs[z]);
+                                cg[n++] = rr;
+                                if ((rr & 15) != MH_OP_M) { ++xo; xg += (int)(rr >> 4); }
+                            }
+                            if (clipR) cg[n++] = ((uint32_t)clipR << 4) | MH_OP_S;
+                            out.valid = 1;
+                            out.pos = jL;
+                            out.end = jR + 1;
+                            out.score = best;
+                            out.xo = xo; out.xg = xg;
+                            out.n_cigar = n;
+                            out.cig_off = (int32_t)base;
+                            c_ok = 1;
+                        }
+                    }
+                }
+            }
+            c_ok = __builtin_amdgcn_readfirstlane(c_ok);
+            clipL = __builtin_amdgcn_readfirstlane(clipL);
+            clipR = __builtin_amdgcn_readfirstlane(clipR);
+            if (c_ok) {
+                // mismatches over the M rows of the trimmed alignment
+                int xm = 0;
+                for (int i = clipL + lane; i <= m - 1 - clipR; i += 64) {
+                    const int k = rowk[i];
+                    if (k == 255) continue;
+                    const int g = refw[i + k] >> 2, rb = rdc[i];
+                    if (rb > 3 || g > 3 || rb != g) ++xm;
+                }
+                xm = wave_sum(xm);
+                out.xm = xm;
+                out.nm = xm + out.xg;
+            }
+        }
+        if (lane == 0) A.slot[sid] = out;
         wave_sync();
     }
 }
@@ -698,9 +740,37 @@ __device__ __forceinline__ bool concordant(const Slot &x, const Slot &y, int max
     return true;
 }
 
-__device__ void tally(const PairArgs &A, const Rec &o, int64_t row)
+// Per-reference line tallies (remap.py:494-506, :743-755).  Almost every
+// read of a pass lands on the same one or two references, so the counters
+// are reduced per block in LDS and flushed with one global atomic each.
+constexpr int TALLY_LDS_REFS = 256;
+
+struct TallyLds {
+    unsigned int lines[TALLY_LDS_REFS], filt[TALLY_LDS_REFS], mapped[TALLY_LDS_REFS];
+    int first[TALLY_LDS_REFS], firstm[TALLY_LDS_REFS];
+    unsigned int unmapped, star;
+    int star_first;
+};
+
+__device__ void tally(const PairArgs &A, TallyLds *T, const Rec &o, int64_t row)
 {
     const int n = A.n_refs;
+    if (T) {
+        if (o.sam_ref >= 0) {
+            atomicAdd(&T->lines[o.sam_ref], 1u);
+            if (!(o.flag & 4)) {
+                if (o.maxm > 50) atomicAdd(&T->filt[o.sam_ref], 1u);
+                atomicAdd(&T->mapped[o.sam_ref], 1u);
+                atomicMin(&T->firstm[o.sam_ref], (int)row);
+            }
+            atomicMin(&T->first[o.sam_ref], (int)row);
+        } else {
+            atomicAdd(&T->star, 1u);
+            atomicMin(&T->star_first, (int)row);
+        }
+        if (o.flag & 4) atomicAdd(&T->unmapped, 1u);
+        return;
+    }
     if (o.sam_ref >= 0) {
         atomicAdd((unsigned long long *)&A.ref_stats[o.sam_ref], 1ull);
         if (!(o.flag & 4)) {
@@ -716,11 +786,43 @@ __device__ void tally(const PairArgs &A, const Rec &o, int64_t row)
     if (o.flag & 4) atomicAdd((unsigned long long *)&A.ref_stats[5 * n], 1ull);
 }
 
+__device__ void tally_flush(const PairArgs &A, TallyLds *T)
+{
+    const int n = A.n_refs;
+    unsigned long long *S = (unsigned long long *)A.ref_stats;
+    for (int r = threadIdx.x; r < n; r += blockDim.x) {
+        if (T->lines[r]) atomicAdd(&S[r], (unsigned long long)T->lines[r]);
+        if (T->filt[r]) atomicAdd(&S[n + r], (unsigned long long)T->filt[r]);
+        if (T->mapped[r]) atomicAdd(&S[2 * n + r], (unsigned long long)T->mapped[r]);
+        if (T->first[r] != INT32_MAX) atomicMin((long long *)&A.ref_stats[3 * n + r], (long long)T->first[r]);
+        if (T->firstm[r] != INT32_MAX) atomicMin((long long *)&A.ref_stats[4 * n + r], (long long)T->firstm[r]);
+    }
+    if (threadIdx.x == 0) {
+        if (T->unmapped) atomicAdd(&S[5 * n], (unsigned long long)T->unmapped);
+        if (T->star) atomicAdd(&S[5 * n + 1], (unsigned long long)T->star);
+        if (T->star_first != INT32_MAX) atomicMin((long long *)&A.ref_stats[5 * n + 2], (long long)T->star_first);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_pair(PairArgs A)
 {
+    __shared__ TallyLds sT;
+    TallyLds *T = (A.n_refs <= TALLY_LDS_REFS && A.R.n < INT32_MAX) ? &sT : nullptr;
+    if (T) {
+        for (int r = threadIdx.x; r < TALLY_LDS_REFS; r += blockDim.x) {
+            T->lines[r] = T->filt[r] = T->mapped[r] = 0;
+            T->first[r] = T->firstm[r] = INT32_MAX;
+        }
+        if (threadIdx.x == 0) { T->unmapped = T->star = 0; T->star_first = INT32_MAX; }
+        __syncthreads();
+    }
     const int64_t units = A.paired ? A.R.n / 2 : A.R.n;
-    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units;
-         u += (int64_t)gridDim.x * blockDim.x) {
+    // every thread runs the same trip count so the final barrier is uniform
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t trips = (units + stride - 1) / stride;
+    for (int64_t it = 0; it < trips; ++it) {
+        const int64_t u = it * stride + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (u >= units) continue;
         if (!A.paired) {
             MateView mv;
             load_mate(A, u, mv);
@@ -735,7 +837,7 @@ __global__ __launch_bounds__(256) void k_pair(PairArgs A)
                 o.flag = 0x4;
             }
             A.rec[u] = o;
-            tally(A, o, u);
+            tally(A, T, o, u);
             continue;
         }
         const int64_t r1 = 2 * u, r2 = 2 * u + 1;
@@ -803,8 +905,12 @@ __global__ __launch_bounds__(256) void k_pair(PairArgs A)
         }
         A.rec[r1] = o1;
         A.rec[r2] = o2;
-        tally(A, o1, r1);
-        tally(A, o2, r2);
+        tally(A, T, o1, r1);
+        tally(A, T, o2, r2);
+    }
+    if (T) {
+        __syncthreads();
+        tally_flush(A, T);
     }
 }
 
@@ -889,7 +995,7 @@ int run_map(Ctx &c, const mh_params &par)
         MH_HIP(hipGetLastError());
 
         const int rows_pad = ((c.reads.max_len + 7) / 8) * 8;
-        const int wave_lds = ((rows_pad * 40 + 192) + 15) & ~15;
+        const int wave_lds = ((rows_pad * 43 + 4 * 128 + 64) + 15) & ~15;
         for (int attempt = 0; attempt < 2; ++attempt) {
             MH_HIP(hipMemsetAsync(M.counters + 1, 0, sizeof(int32_t) * 2, s));
             DpArgs da{c.reads, c.index, c.len_tab, M.cand, M.work, M.counters, M.slot, M.pool,

@@ -74,6 +74,10 @@ def _declare(L):
                             ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         'mh_rows_load': ([_P, ctypes.c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                           ctypes.c_int64, _P], ctypes.c_int),
+        'mh_rows_load_csv': ([_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int,
+                              ctypes.POINTER(ctypes.c_char_p), _I64P, _I64P, _I32P], ctypes.c_int),
+        'mh_rows_info': ([_P, _P, _P, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+        'mh_reads_fastq_lines': ([_P, _I64P], ctypes.c_int),
         'mh_pileup': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),
         'mh_pileup_dims': ([_P, ctypes.POINTER(ctypes.c_int), _I32P, _I64P, _I64P], ctypes.c_int),
         'mh_pileup_fetch': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
@@ -289,6 +293,32 @@ class Context:
         n_units = len(arrs[10]) // 2
         check(lib().mh_rows_load(self.h, len(arrs[0]), *[_ptr(a) for a in arrs[:10]], n_units,
                                  _ptr(arrs[10])), 'mh_rows_load')
+
+    def rows_load_csv(self, text, refnames):
+        """prelim.csv text -> device rows.  Returns dict(n_rows, n_units,
+        info, present, unknown): info[:, 0..3] = name id (>= 0: index into
+        refnames, < 0: unknown[-1 - id]), flag, longest M run, compact ref id;
+        present[k] = refnames index of compact ref k."""
+        data = text.encode() if isinstance(text, str) else text
+        names = (ctypes.c_char_p * max(len(refnames), 1))(*[r.encode() for r in refnames])
+        nr = ctypes.c_int64()
+        nu = ctypes.c_int64()
+        npres = ctypes.c_int32()
+        check(lib().mh_rows_load_csv(self.h, data, len(data), len(refnames), names,
+                                     ctypes.byref(nr), ctypes.byref(nu), ctypes.byref(npres)),
+              'mh_rows_load_csv')
+        info = np.zeros((max(nr.value, 1), 4), dtype=np.int32)
+        present = np.zeros(max(npres.value, 1), dtype=np.int32)
+        buf = ctypes.create_string_buffer(1 << 20)
+        check(lib().mh_rows_info(self.h, _ptr(info), _ptr(present), buf, len(buf)), 'mh_rows_info')
+        unknown = buf.value.decode().split('\n')[:-1]
+        return dict(n_rows=nr.value, n_units=nu.value, info=info[:nr.value],
+                    present=present[:npres.value], unknown=unknown)
+
+    def fastq_lines(self):
+        n = ctypes.c_int64()
+        check(lib().mh_reads_fastq_lines(self.h, ctypes.byref(n)), 'mh_reads_fastq_lines')
+        return n.value
 
     def pileup(self, source, q_cutoff, ref_lens):
         rl = np.ascontiguousarray(ref_lens, dtype=np.int32)

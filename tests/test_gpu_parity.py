@@ -217,3 +217,18 @@ def test_gotoh_pol_sized(ctx):
                   0, 0, 0, 0, 0], 'ACGT?'
     want = oracle.gotoh_align(POL, conseq, 15, 3, True, alpha, mat)
     assert ctx.gotoh_align(POL, conseq, 15, 3, True, alpha, mat) == want
+
+
+@pytest.mark.parametrize('mode', [oracle.E2E, oracle.LOCAL])
+def test_map_overhang_trimming(ctx, mode):
+    """Reads from a genome that extends past both ends of the reference:
+    overhanging columns become soft clips (trimming on the CIGAR runs)."""
+    rng = np.random.default_rng(29)
+    flank = lambda n: ''.join(rng.choice(list('ACGT'), size=n))
+    genome = flank(200) + POL[:600] + flank(150)
+    names, seqs, quals = _reads(600, 31, genomes={'g': genome}, indel_rate=0.02, sub_rate=0.03)
+    ref = _oracle_alns([POL[:600]], mode, seqs, quals, True)
+    gpu = _gpu_alns(ctx, ['p'], [POL[:600]], mode, seqs, quals, True)
+    _assert_same(gpu, ref, seqs)
+    clipped = sum(1 for a in ref if a['n_cigar'] and (a['cigar'][0] & 15) == 4)
+    assert clipped > 20
