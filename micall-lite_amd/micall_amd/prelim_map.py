@@ -1,0 +1,113 @@
+"""
+Drop-in for micall/core/prelim_map.py: same function, arguments, output file.
+
+prelim_map() maps every read pair end-to-end against every seed reference
+of the project file and writes prelim.csv (the SAM columns qname..qual,
+rows grouped by rname in first-seen order, prelim_map.py:134-151).  The
+bowtie2-build + bowtie2 subprocesses (prelim_map.py:106, :134) are replaced
+by the HIP mapper (mh_index_build + mh_map); bt2_path / bt2build_path /
+nthreads are accepted for signature compatibility and ignored.
+"""
+import argparse
+import csv
+import logging
+import os
+import sys
+
+import numpy as np
+
+from . import _native, session
+from .projects import ProjectConfig
+
+BOWTIE_THREADS = 4
+BOWTIE_VERSION = '2.2.8'
+BOWTIE_PATH = 'bowtie2'
+BOWTIE_BUILD_PATH = 'bowtie2-build-s'
+
+READ_GAP_OPEN = 10
+READ_GAP_EXTEND = 3
+REF_GAP_OPEN = 10
+REF_GAP_EXTEND = 3
+E2E_SEEDLEN = 22
+MAXINS = 1200
+
+FIELDNAMES = ['qname', 'flag', 'rname', 'pos', 'mapq', 'cigar', 'rnext', 'pnext', 'tlen', 'seq',
+              'qual']
+
+logger = logging.getLogger(__name__)
+
+
+def check_fastq(fastq1, fastq2):
+    """prelim_map.py:62-69 / remap.py:415-422: exit(1) on a missing file."""
+    if not os.path.exists(fastq1):
+        logger.error('No FASTQ found at %s', fastq1)
+        sys.exit(1)
+    if fastq2 is not None and not os.path.exists(fastq2):
+        logger.error('No FASTQ found at %s', fastq2)
+        sys.exit(1)
+
+
+def grouped_order(sam_ref):
+    """Row order of prelim.csv: rows grouped by rname, groups in first-seen
+    order, rows in output order within a group (prelim_map.py:137-151)."""
+    sam_ref = np.asarray(sam_ref)
+    if len(sam_ref) == 0:
+        return np.zeros(0, dtype=np.int64)
+    values, first = np.unique(sam_ref, return_index=True)
+    rank_of_value = np.empty(len(values), dtype=np.int64)
+    rank_of_value[np.argsort(first, kind='stable')] = np.arange(len(values))
+    ranks = rank_of_value[np.searchsorted(values, sam_ref)]
+    return np.argsort(ranks, kind='stable').astype(np.int64)
+
+
+def prelim_map(fastq1, fastq2, prelim_csv,
+               bt2_path='bowtie2', bt2build_path='bowtie2-build-s',
+               nthreads=BOWTIE_THREADS, callback=None,
+               rdgopen=READ_GAP_OPEN, rfgopen=REF_GAP_OPEN, stderr=sys.stderr,
+               gzip=False, work_path='', keep=False, json=None):
+    """Run the preliminary mapping step (prelim_map.py:36-161)."""
+    check_fastq(fastq1, fastq2)
+    rdgopen = READ_GAP_OPEN if rdgopen is None else int(rdgopen)
+    rfgopen = REF_GAP_OPEN if rfgopen is None else int(rfgopen)
+    ctx = session.load_fastq(fastq1, fastq2)
+    if callback:
+        total_reads = ctx.fastq_line_count / 2
+        callback(message='... preliminary mapping', progress=0, max_progress=total_reads)
+    projects = ProjectConfig.loadDefault() if json is None else ProjectConfig.loadCustom(json)
+    seeds = projects.seed_sequences()
+    names = list(seeds)
+    if keep:
+        with open(os.path.join(work_path, 'micall.fasta'), 'w') as ref:
+            projects.writeSeedFasta(ref)
+    ctx.index_build(names, [seeds[n] for n in names], E2E_SEEDLEN)
+    ctx.map(_native.params(_native.E2E, rdg=(rdgopen, READ_GAP_EXTEND),
+                           rfg=(rfgopen, REF_GAP_EXTEND), maxins=MAXINS))
+    recs = ctx.recs()
+    order = grouped_order(recs[:, _native.ALN_FIELDS.index('sam_ref')])
+    writer = csv.DictWriter(prelim_csv, FIELDNAMES, lineterminator=os.linesep)
+    writer.writeheader()
+    prelim_csv.write(ctx.format_rows(1, order=order))
+    if callback:
+        callback(progress=ctx.fastq_line_count / 2)
+
+
+def main():
+    parser = argparse.ArgumentParser(
+        description='Map contents of FASTQ R1 and R2 data sets to references (MI355X).')
+    parser.add_argument('-fastq1', help='<input> FASTQ containing forward or unpaired reads')
+    parser.add_argument('-fastq2', default=None,
+                        help='<input, optional> FASTQ containing reverse reads if paired')
+    parser.add_argument('-prelim_csv', type=argparse.FileType('w'),
+                        help='<output> CSV containing preliminary mapping (modified SAM)')
+    parser.add_argument("--rdgopen", default=None, help="<optional> read gap open penalty")
+    parser.add_argument("--rfgopen", default=None, help="<optional> reference gap open penalty")
+    parser.add_argument("--gzip", action='store_true', help="<optional> FASTQs are compressed")
+    parser.add_argument("--keep", action='store_true',
+                        help="<optional> retain temporary files for debugging.")
+    args = parser.parse_args()
+    prelim_map(fastq1=args.fastq1, fastq2=args.fastq2, prelim_csv=args.prelim_csv,
+               rdgopen=args.rdgopen, rfgopen=args.rfgopen, gzip=args.gzip, keep=args.keep)
+
+
+if __name__ == '__main__':
+    main()

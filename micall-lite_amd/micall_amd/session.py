@@ -1,0 +1,50 @@
+"""
+Process-wide device context and resident-read cache.
+
+bin/micall calls prelim_map() and then remap() on the same FASTQ files
+(bin/micall:142-169); the reference re-reads and re-decompresses them in
+bowtie2 on every pass.  Here the first call ingests them into HBM and later
+calls on the same (unchanged) files reuse the resident reads.
+"""
+import os
+
+from . import _native
+
+_ctx = None
+_key = None
+
+
+def context():
+    global _ctx
+    if _ctx is None:
+        _ctx = _native.Context(int(os.environ.get('MICALL_HIP_DEVICE', '0')))
+    return _ctx
+
+
+def _file_key(*paths):
+    out = []
+    for p in paths:
+        if p is None:
+            out.append(None)
+        else:
+            st = os.stat(p)
+            out.append((os.path.abspath(p), st.st_mtime_ns, st.st_size))
+    return tuple(out)
+
+
+def load_fastq(fastq1, fastq2=None):
+    """The context with these FASTQ files resident (loaded once)."""
+    global _key
+    ctx = context()
+    key = _file_key(fastq1, fastq2)
+    if key != _key:
+        ctx.reads_load_fastq(fastq1, fastq2)
+        _key = key
+        ctx.fastq_line_count = ctx.fastq_lines()
+    return ctx
+
+
+def invalidate():
+    """The resident reads were replaced (e.g. by split re-mapping)."""
+    global _key
+    _key = None

@@ -17,7 +17,14 @@ itself produced for them.  Sections:
   sam2aln  every apply_cigar / merge_pairs / merge_inserts call made by
            micall/tests/sam2aln_test.py.
 
-usage: python tests/golden/gen_golden.py [gotoh] [pileup] [sam2aln]
+  e2e      the stock reference prelim_map() + remap() (nthreads=1, so its
+           pileup runs without a process pool and is deterministic) with
+           oracle/shim_bin/bowtie2 standing in for bowtie2, on small committed
+           FASTQ inputs (synthetic sets and some of micall/tests/microtest/);
+           outputs prelim.csv, remap.csv, remap_counts.csv, remap_conseq.csv
+           and the unmapped FASTQs under tests/golden/e2e/<case>/.
+
+usage: python tests/golden/gen_golden.py [gotoh] [pileup] [sam2aln] [e2e]
 """
 import io
 import json
@@ -223,7 +230,94 @@ def gen_sam2aln():
     print('sam2aln: {} calls'.format(len(records)))
 
 
+E2E_MICROTESTS = ['1234A-V3LOOP_S1', '2020A-GP41_S4', '2040A-HLA-B_S6', '2070A-PR_S9',
+                  '2100A-HCV-1337B-V3LOOP_S12']
+
+
+def _e2e_cases():
+    """(name, R1 writer, R2 writer or None) for every end-to-end case."""
+    from micall_amd import projects, synth
+    seeds = projects.load_default().seed_sequences()
+    cases = []
+
+    def syn(name, n, genomes, **kw):
+        pairs = synth.make_pairs(n, genomes={g: seeds[g] for g in genomes}, **kw)
+        cases.append((name, pairs))
+
+    syn('syn_pol', 1500, ['HIV1B-pol-seed'], genome_seed=101, read_seed=102)
+    syn('syn_pol_indel', 600, ['HIV1B-pol-seed'], genome_seed=103, read_seed=104, indel_rate=0.01)
+    syn('syn_hiv3', 900, ['HIV1B-pol-seed', 'HIV1B-gag-seed', 'HIV1B-env-seed'],
+        genome_seed=105, read_seed=106)
+    syn('syn_unpaired300', 500, ['HIV1B-pol-seed'], genome_seed=107, read_seed=108, read_len=300,
+        paired=False)
+    return cases
+
+
+def gen_e2e():
+    import gzip
+    import shutil
+    import tempfile
+    refharness.setup()
+    from micall.core.prelim_map import prelim_map
+    from micall.core.remap import remap
+    from micall_amd import synth
+    shim = os.path.join(REPO, 'oracle', 'shim_bin')
+    out_root = os.path.join(HERE, 'e2e')
+    os.makedirs(out_root, exist_ok=True)
+    inputs = []
+    for name, pairs in _e2e_cases():
+        d = os.path.join(out_root, name)
+        os.makedirs(d, exist_ok=True)
+        r1 = os.path.join(d, 'R1.fastq.gz')
+        r2 = os.path.join(d, 'R2.fastq.gz') if pairs['r2'] is not None else None
+        synth.write_fastq(pairs, r1, r2)
+        inputs.append((name, r1, r2))
+    micro = os.path.join(refharness.REF, 'micall', 'tests', 'microtest')
+    for stem in E2E_MICROTESTS:
+        d = os.path.join(out_root, 'micro_' + stem.split('_')[0])
+        os.makedirs(d, exist_ok=True)
+        paths = []
+        for mate in ('R1', 'R2'):
+            src = os.path.join(micro, '{}_L001_{}_001.fastq'.format(stem, mate))
+            dst = os.path.join(d, mate + '.fastq.gz')
+            with open(src, 'rb') as fi, gzip.open(dst, 'wb') as fo:
+                shutil.copyfileobj(fi, fo)
+            paths.append(dst)
+        inputs.append(('micro_' + stem.split('_')[0], paths[0], paths[1]))
+    for name, r1, r2 in inputs:
+        d = os.path.join(out_root, name)
+        work = tempfile.mkdtemp(prefix='e2e_')
+        cwd = os.getcwd()
+        os.chdir(work)   # the reference writes split FASTQs into the cwd
+        try:
+            prelim = os.path.join(work, 'prelim.csv')
+            with open(prelim, 'w') as handle:
+                prelim_map(r1, r2, handle, bt2_path=os.path.join(shim, 'bowtie2'),
+                           bt2build_path=os.path.join(shim, 'bowtie2-build-s'), nthreads=1,
+                           gzip=True, work_path=work)
+            outs = {k: open(os.path.join(work, k), 'w') for k in
+                    ('remap.csv', 'remap_counts.csv', 'remap_conseq.csv', 'unmapped1.fastq',
+                     'unmapped2.fastq')}
+            with open(prelim) as pre:
+                remap(r1, r2, pre, outs['remap.csv'], outs['remap_counts.csv'],
+                      outs['remap_conseq.csv'], outs['unmapped1.fastq'], outs['unmapped2.fastq'],
+                      work_path=work, bt2_path=os.path.join(shim, 'bowtie2'),
+                      bt2build_path=os.path.join(shim, 'bowtie2-build-s'), nthreads=1, gzip=True,
+                      keep=True)
+            for f in outs.values():
+                f.close()
+            for k in ('prelim.csv', 'remap.csv', 'remap_counts.csv', 'remap_conseq.csv',
+                      'unmapped1.fastq', 'unmapped2.fastq'):
+                with open(os.path.join(work, k), 'rb') as fi, \
+                        gzip.open(os.path.join(d, k + '.gz'), 'wb') as fo:
+                    shutil.copyfileobj(fi, fo)
+        finally:
+            os.chdir(cwd)
+            shutil.rmtree(work, ignore_errors=True)
+        print('e2e:', name)
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['gotoh', 'pileup', 'sam2aln']
+    which = sys.argv[1:] or ['gotoh', 'pileup', 'sam2aln', 'e2e']
     for w in which:
         globals()['gen_' + w]()
