@@ -73,11 +73,11 @@ class Shard:
         """All-reduce the device counters in place (sum, and max for flags /
         max_pos / first unit) and gather the sparse events."""
         torch = self.torch
-        sum_b, max_b = ctx.pileup_packed_bytes()
         dev = self.device
-        s = torch.empty(sum_b // 4, dtype=torch.int32, device=dev)
-        m = torch.empty(max_b // 4, dtype=torch.int32, device=dev)
         if dev.type == 'cuda':
+            sum_b, max_b = ctx.pileup_packed_bytes()
+            s = torch.empty(sum_b // 4, dtype=torch.int32, device=dev)
+            m = torch.empty(max_b // 4, dtype=torch.int32, device=dev)
             ctx.pileup_export(s.data_ptr(), m.data_ptr(), unit_base)
             self.dist.all_reduce(s, op=self.dist.ReduceOp.SUM)
             self.dist.all_reduce(m, op=self.dist.ReduceOp.MAX)
