@@ -87,6 +87,43 @@ def read_pmc_traffic(kernel, pairs):
         return None
 
 
+def instrument(pipe, ctx, stages):
+    """Wrap the pipeline's stages and the context's calls with synchronised
+    wall-clock timers (diagnostics only: it serialises host and device)."""
+    def wrap(obj, name, label):
+        fn = getattr(obj, name)
+
+        def timed(*a, **kw):
+            ctx.sync()
+            t = time.perf_counter()
+            r = fn(*a, **kw)
+            ctx.sync()
+            acc = stages.setdefault(label, [0.0, 0])
+            acc[0] += time.perf_counter() - t
+            acc[1] += 1
+            if name == 'map':
+                stages.setdefault('_map_stats', []).append(ctx.map_stats())
+            return r
+        setattr(obj, name, timed)
+
+    for name in ('index_build', 'map', 'map_counts', 'pileup', 'pileup_fetch'):
+        wrap(ctx, name, 'ctx.' + name)
+    for name in ('prelim', 'prelim_conseqs', 'map_to_reference', 'build_conseqs_filtered'):
+        wrap(pipe, name, 'pipe.' + name)
+    from micall_amd import pipeline as pl
+    for name in ('counts_to_conseqs', 'filter_conseqs'):
+        fn = getattr(pl, name)
+
+        def timed(*a, _fn=fn, _label='host.' + name, **kw):
+            t = time.perf_counter()
+            r = _fn(*a, **kw)
+            acc = stages.setdefault(_label, [0.0, 0])
+            acc[0] += time.perf_counter() - t
+            acc[1] += 1
+            return r
+        setattr(pl, name, timed)
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split('\n\n')[0])
     ap.add_argument('--gpus', type=int, default=1)
@@ -95,6 +132,8 @@ def main():
     ap.add_argument('--pairs', type=int, default=1000000, help='read pairs per GPU')
     ap.add_argument('--cpu-sample', type=int, default=100000)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--breakdown', action='store_true',
+                    help='time each pipeline stage (synchronising) and print it to stderr')
     args = ap.parse_args()
 
     import torch
@@ -122,6 +161,10 @@ def main():
 
     def step():
         return pipe.run(raw_count, max_iterations=1)
+
+    stages = {}
+    if args.breakdown:
+        instrument(pipe, ctx, stages)
 
     for _ in range(args.warmup):
         step()
@@ -179,6 +222,10 @@ def main():
                        'mapped_lines': dict(new_counts)},
         }
         print(json.dumps(out))
+        if args.breakdown:
+            print(json.dumps({'stage_ms_per_step': {k: round(v[0] * 1e3 / (args.steps + args.warmup), 3)
+                                                    for k, v in stages.items() if not k.startswith('_')},
+                              'map_stats': stages.get('_map_stats')}), file=sys.stderr)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

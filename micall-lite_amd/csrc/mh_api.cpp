@@ -657,6 +657,18 @@ int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mappe
     return 0;
 }
 
+int mh_map_stats(mh_ctx *ctx, int64_t *out3)
+{
+    if (!ctx || !out3) return -3;
+    CtxEx *c = X(ctx);
+    MapState &M = c->map;
+    if (!M.valid) { set_error("no mapping results (call mh_map)"); return -3; }
+    out3[0] = M.n_reads;
+    out3[1] = M.last_work;
+    out3[2] = M.last_cigar;
+    return 0;
+}
+
 int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20)
 {
     if (!ctx || (n > 0 && !out20)) return -3;

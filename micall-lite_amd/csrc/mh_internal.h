@@ -104,6 +104,8 @@ struct MapState {
     int64_t *ref_stats = nullptr;// per ref: lines, filtered, mapped, first_row, first_mapped; + unmapped, star
     int64_t cap_reads = 0;
     int cap_refs = 0;
+    int64_t last_work = 0;       // extensions (k_dp work items) of the last pass
+    int64_t last_cigar = 0;      // CIGAR ops written by the last pass
     bool valid = false;
 };
 

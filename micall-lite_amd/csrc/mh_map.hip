@@ -343,6 +343,88 @@ __device__ __forceinline__ int mm_pen(int qchar)
     return 2 + q / 10;
 }
 
+// Scores inside the row recurrence carry a bias of 2^20, so every live value
+// is positive and the 0 that a DPP move with bound_ctrl shifts in at the band
+// edges acts as minus infinity.  The moves then fold into the ALU op that uses
+// them (v_max_i32_dpp, v_add_u32_dpp) instead of costing a mov + a fill each.
+constexpr int BIAS = 1 << 20;
+
+template <int CTRL>
+__device__ __forceinline__ int dppz(int v)
+{
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+
+__device__ __forceinline__ uint32_t umin1(int v) { return (uint32_t)v < 1u ? (uint32_t)v : 1u; }
+
+// inclusive prefix max over the 64 lanes (x > 0)
+__device__ __forceinline__ int scan_max(int x)
+{
+    x = imax(x, dppz<DPP_ROW_SHR1>(x));
+    x = imax(x, dppz<DPP_ROW_SHR2>(x));
+    x = imax(x, dppz<DPP_ROW_SHR4>(x));
+    x = imax(x, dppz<DPP_ROW_SHR8>(x));
+    x = imax(x, __builtin_amdgcn_update_dpp(x, x, DPP_ROW_BCAST15, 0xA, 0xF, false));
+    x = imax(x, __builtin_amdgcn_update_dpp(x, x, DPP_ROW_BCAST31, 0xC, 0xF, false));
+    return x;
+}
+
+struct DpConst {
+    int exI, oeI, cE;   // cE = exI - oeI
+    int xD, cF;         // per lane: exD * lane, -(oeD - exD) - exD * lane
+};
+
+// One DP row inside the gap window (oracle dp_extend, og_mapper.c:283-322):
+// returns the 4 traceback bits of this lane's cell.
+template <int LOCAL>
+__device__ __forceinline__ uint32_t dp_row_gap(uint32_t tbv, int rc, int &Hp, int &Ep,
+                                               uint32_t &bestKey, int ci, const DpConst &K)
+{
+    const int Hd = Hp + (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4) - 8;
+    // vertical (insertion) move from lane k+1 of the previous row
+    const int Es = imax(Ep - K.exI, Hp - K.oeI);
+    const int E = dppz<DPP_WAVE_SHL1>(Es);
+    const uint32_t eb = (uint32_t)(K.cE - dppz<DPP_WAVE_SHL1>(Ep - Hp)) >> 31;
+    int H1 = imax(Hd, E);
+    if (LOCAL) H1 = imax(H1, BIAS);
+    // horizontal (deletion) moves: prefix max of X = H1 + exD * lane
+    const int X = H1 + K.xD;
+    const int P = scan_max(X);
+    const uint32_t gt = (uint32_t)(X - P) >> 31;
+    const int F = dppz<DPP_WAVE_SHR1>(P) + K.cF;
+    const uint32_t fb = (uint32_t)dppz<DPP_WAVE_SHR1>((int)gt);
+    const int H = imax(H1, F);
+    // src: 1 diagonal, 2 from E, 3 from F (priority in that order); 0 local stop
+    const uint32_t a = umin1(H - Hd), b = umin1(H - E);
+    uint32_t src = 1u + a + (a & b);
+    if (LOCAL) {
+        src *= umin1(H - BIAS);
+        const uint32_t key = (uint32_t)H * 1024u + (uint32_t)ci;
+        bestKey = bestKey > key ? bestKey : key;
+    }
+    Hp = H;
+    Ep = E;
+    return src | (eb << 2) | (fb << 3);
+}
+
+// A row outside the gap window (first / last GBAR rows): no E, no F.
+template <int LOCAL>
+__device__ __forceinline__ uint32_t dp_row_nogap(uint32_t tbv, int rc, int &Hp, int &Ep,
+                                                 uint32_t &bestKey, int ci)
+{
+    int H = Hp + (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4) - 8;
+    uint32_t src = 1u;
+    if (LOCAL) {
+        H = imax(H, BIAS);
+        src = umin1(H - BIAS);
+        const uint32_t key = (uint32_t)H * 1024u + (uint32_t)ci;
+        bestKey = bestKey > key ? bestKey : key;
+    }
+    Hp = H;
+    Ep = 0;
+    return src;
+}
+
 template <int LOCAL>
 __global__ __launch_bounds__(256) void k_dp(DpArgs A)
 {
@@ -359,8 +441,12 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     uint8_t *rowk = rdc + A.rows_pad;                         // rows_pad: lane of the M cell, 255 none
     const int ma = LOCAL ? 2 : 0;
     const int n_work = A.counters[0];
-    const int xD = lane * A.exD;                  // X = H1 + exD*lane
-    const int cF = -(A.oeD - A.exD) - A.exD * lane;
+    DpConst K;
+    K.exI = A.exI;
+    K.oeI = A.oeI;
+    K.cE = A.exI - A.oeI;
+    K.xD = lane * A.exD;
+    K.cF = -(A.oeD - A.exD) - A.exD * lane;
 
     for (int w = blockIdx.x * wpb + wv; w < n_work; w += gridDim.x * wpb) {
         const int sid = A.work[w];
@@ -398,9 +484,10 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         }
         wave_sync();
 
-        // ---- DP over rows, 8 rows per group: the group's LDS loads first ----
-        int Hp = 0, Ep = NEG;
-        int bestH = NEG, bestI = 0;
+        // ---- DP over rows, 8 rows per group (one u32 of traceback bits per
+        // lane); groups wholly inside the gap window run branch-free ----
+        int Hp = BIAS, Ep = 0;
+        uint32_t bestKey = 0;
         for (int i0 = 0; i0 < m; i0 += 8) {
             uint32_t tbv[8];
             int rcv[8];
@@ -410,51 +497,33 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                 rcv[t] = refw[i0 + t + lane];
             }
             uint32_t acc = 0;
+            if (i0 >= GBAR && i0 + 8 <= m - GBAR) {
 #pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                const int i = i0 + t;
-                if (i < m) {
-                    const bool gap_ok = i >= GBAR && i < m - GBAR;
-                    const int s = (int)((tbv[t] >> rcv[t]) & 15u) - 8;
-                    const int Hd = Hp + s;
-                    int E = NEG, eb = 0, H, fb = 0;
-                    if (gap_ok) {
-                        const int eu = dpp<DPP_WAVE_SHL1>(NEG, Ep) - A.exI;
-                        const int hu = dpp<DPP_WAVE_SHL1>(NEG, Hp) - A.oeI;
-                        E = imax(eu, hu);
-                        eb = eu > hu;
+                for (int t = 0; t < 8; ++t)
+                    acc |= dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K)
+                           << (4 * t);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int i = i0 + t;
+                    if (i < m) {
+                        const uint32_t nib =
+                            (i >= GBAR && i < m - GBAR)
+                                ? dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K)
+                                : dp_row_nogap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i);
+                        acc |= nib << (4 * t);
                     }
-                    int H1 = imax(Hd, E);
-                    if (LOCAL) H1 = imax(H1, 0);
-                    if (gap_ok) {
-                        const int X = H1 + xD;
-                        int P = X;
-                        P = imax(P, dpp<DPP_ROW_SHR1>(NEG, P));
-                        P = imax(P, dpp<DPP_ROW_SHR2>(NEG, P));
-                        P = imax(P, dpp<DPP_ROW_SHR4>(NEG, P));
-                        P = imax(P, dpp<DPP_ROW_SHR8>(NEG, P));
-                        P = imax(P, dpp<DPP_ROW_BCAST15, 0xA>(NEG, P));
-                        P = imax(P, dpp<DPP_ROW_BCAST31, 0xC>(NEG, P));
-                        const int gt = P > X;
-                        fb = dpp<DPP_WAVE_SHR1>(0, gt);
-                        const int F = dpp<DPP_WAVE_SHR1>(NEG, P) + cF;
-                        H = imax(H1, F);
-                    } else {
-                        H = H1;
-                    }
-                    const int src = (LOCAL && H == 0) ? 0 : (H == Hd ? 1 : (H == E ? 2 : 3));
-                    acc |= (uint32_t)(src | (eb << 2) | (fb << 3)) << (4 * t);
-                    if (LOCAL) {
-                        if (H > bestH) { bestH = H; bestI = i; }
-                    } else if (i == m - 1) {
-                        bestH = H;
-                        bestI = i;
-                    }
-                    Hp = H;
-                    Ep = E;
                 }
             }
             bits[(i0 >> 3) * 64 + lane] = acc;
+        }
+        int bestH, bestI;
+        if (LOCAL) {
+            bestH = (int)(bestKey >> 10) - BIAS;
+            bestI = 1023 - (int)(bestKey & 1023u);
+        } else {
+            bestH = Hp - BIAS;   // end-to-end: the last row
+            bestI = m - 1;
         }
         // best cell: max score, then smallest row, then smallest lane
         const long long key = (long long)bestH * 1048576ll + (long long)((1023 - bestI) << 6) +
@@ -478,6 +547,20 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             for (;;) {
                 const int g = i >> 3;
                 if (g != wr || k != wk) { word = bits[g * 64 + k]; wr = g; wk = k; }
+                if (state == 0 && (i & 7) == 7 && (word & 0x33333333u) == 0x11111111u) {
+                    // eight diagonal moves on this lane: one M step of 8 rows
+                    if (rop == MH_OP_M) rlen += 8;
+                    else {
+                        if (rlen) runs[nrun++] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                        rop = MH_OP_M;
+                        rlen = 8;
+                    }
+                    *(uint64_t *)(rowk + i - 7) = 0x0101010101010101ull * (uint64_t)k;
+                    first_j = i - 7 + d0 + k;
+                    i -= 8;
+                    if (i < 0) break;
+                    continue;
+                }
                 const uint32_t nib = (word >> (4 * (i & 7))) & 15u;
                 int op;
                 if (state == 0) {
@@ -984,6 +1067,7 @@ int run_map(Ctx &c, const mh_params &par)
     M.par = par;
     hipStream_t s = c.stream;
     MH_HIP(hipMemsetAsync(M.counters, 0, sizeof(int32_t) * 4, s));
+    M.last_work = M.last_cigar = 0;
     hipLaunchKernelGGL(k_init_stats, dim3(64), dim3(256), 0, s, M.ref_stats, M.n_refs);
     if (n > 0) {
         SeedArgs sa{c.reads, c.index, par.mode, c.len_tab, M.cand, M.n_cand, M.yf, M.work, M.counters};
@@ -1022,6 +1106,8 @@ int run_map(Ctx &c, const mh_params &par)
             int32_t ctr[3];
             MH_HIP(hipMemcpyAsync(ctr, M.counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
             MH_HIP(hipStreamSynchronize(s));
+            M.last_work = ctr[0];
+            M.last_cigar = ctr[1];
             if (!ctr[2]) break;
             // CIGAR pool overflow: grow to what was asked for and redo the extensions
             hipFree(M.pool);

@@ -68,6 +68,7 @@ def _declare(L):
         'mh_map': ([_P, ctypes.POINTER(Params)], ctypes.c_int),
         'mh_alns_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
         'mh_map_counts': ([_P, _P, _P, _P, _P, _P, _I64P, _I64P, _I64P], ctypes.c_int),
+        'mh_map_stats': ([_P, _P], ctypes.c_int),
         'mh_recs_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
         'mh_format_rows': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.c_int64,
                             ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_size_t,
@@ -251,6 +252,12 @@ class Context:
         return dict(lines=lines[:n], filtered=filt[:n], mapped=mapped[:n], first_row=first[:n],
                     first_mapped=firstm[:n], unmapped=unm.value, star=star.value,
                     star_first=star_first.value)
+
+    def map_stats(self):
+        """(reads, banded extensions, CIGAR ops) of the last mapping pass."""
+        out = np.zeros(3, dtype=np.int64)
+        check(lib().mh_map_stats(self.h, _ptr(out)), 'mh_map_stats')
+        return tuple(int(x) for x in out)
 
     def recs(self, first=0, n=None):
         """(n, 20) int32 SAM header fields (ALN_FIELDS order) without CIGARs."""
