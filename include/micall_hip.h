@@ -158,10 +158,12 @@ int mh_pileup_dims(mh_ctx *ctx, int *n_refs, int32_t *cap, int64_t *n_events,
                    int64_t *event_bytes);
 int mh_pileup_fetch(mh_ctx *ctx, int32_t *dense, uint8_t *nflag, uint8_t *dflag,
                     int64_t *read_counts, int64_t *first_unit, int32_t *max_pos);
-/* sparse tokens (base + insertion with len % 3 == 0): per event ref, pos
- * and the token bytes at tok_off[e] .. tok_off[e] + tok_len[e] of pool. */
+/* Sparse tokens (base + insertion with len % 3 == 0), aggregated over the
+ * pileup: n_events (mh_pileup_dims) distinct (ref, pos, token) entries in
+ * (ref, pos, token) order, each with the number of merged pairs that voted
+ * for it; the token is pool[tok_off[e] .. tok_off[e] + tok_len[e]). */
 int mh_pileup_events(mh_ctx *ctx, int32_t *ref, int32_t *pos, int32_t *tok_off,
-                     int32_t *tok_len, char *pool);
+                     int32_t *tok_len, int64_t *count, char *pool);
 /* Multi-GPU: copy the device counters to / from a caller-owned device
  * buffer of `bytes` (>= mh_pileup_packed_bytes) so the caller can all-reduce
  * them with RCCL (int32 sum; flags are 0/1 and are OR-ed by max-reduce of

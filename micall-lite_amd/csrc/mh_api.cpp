@@ -16,6 +16,9 @@
 
 #include "mh_internal.h"
 
+#include <map>
+#include <tuple>
+
 namespace mh {
 
 static thread_local char g_err[1024];
@@ -117,6 +120,12 @@ struct CtxEx : Ctx {
     std::vector<int32_t> csv_present;     // compact ref id -> index into the @SQ list
     std::vector<std::string> csv_unknown; // names outside @SQ, by -1 - name id
     int64_t fastq_lines1 = -1;            // newlines in FASTQ 1 (LineCounter, externals.py:206)
+    DevIndex small;                       // reusable buffers of the non-cached (consensus) index
+    // insertion tokens of the last pileup, aggregated: (ref, pos, token) -> count
+    int64_t tok_gen = -1;
+    std::vector<int32_t> tok_ref, tok_pos, tok_off, tok_len;
+    std::vector<int64_t> tok_count;
+    std::string tok_pool;
 };
 
 static void free_index(DevIndex &ix)
@@ -203,13 +212,34 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     ix.total = (int64_t)codes.size();
     ix.hmask = cap - 1;
     codes.resize(codes.size() + 64, 4);
-    MH_HIP(hipMalloc(&ix.codes, codes.size()));
-    MH_HIP(hipMalloc(&ix.ref_off, sizeof(int64_t) * (n_refs > 0 ? n_refs : 1)));
-    MH_HIP(hipMalloc(&ix.ref_len, sizeof(int32_t) * (n_refs > 0 ? n_refs : 1)));
-    MH_HIP(hipMalloc(&ix.hkey, sizeof(uint64_t) * cap));
-    MH_HIP(hipMalloc(&ix.hstart, sizeof(uint32_t) * cap));
-    MH_HIP(hipMalloc(&ix.hcount, sizeof(uint32_t) * cap));
-    MH_HIP(hipMalloc(&ix.hits, sizeof(int2) * hits.size()));
+    // (re)allocate only what does not fit the buffers this DevIndex already owns
+    if ((int64_t)codes.size() > ix.cap_codes) {
+        hipFree(ix.codes);
+        ix.codes = nullptr;
+        ix.cap_codes = (int64_t)codes.size() * 2;
+        MH_HIP(hipMalloc(&ix.codes, ix.cap_codes));
+    }
+    if (n_refs > ix.cap_refs || !ix.ref_off) {
+        hipFree(ix.ref_off); hipFree(ix.ref_len);
+        ix.ref_off = nullptr; ix.ref_len = nullptr;
+        ix.cap_refs = n_refs > 16 ? n_refs : 16;
+        MH_HIP(hipMalloc(&ix.ref_off, sizeof(int64_t) * ix.cap_refs));
+        MH_HIP(hipMalloc(&ix.ref_len, sizeof(int32_t) * ix.cap_refs));
+    }
+    if ((int64_t)cap > ix.cap_hash) {
+        hipFree(ix.hkey); hipFree(ix.hstart); hipFree(ix.hcount);
+        ix.hkey = nullptr; ix.hstart = nullptr; ix.hcount = nullptr;
+        ix.cap_hash = (int64_t)cap;
+        MH_HIP(hipMalloc(&ix.hkey, sizeof(uint64_t) * cap));
+        MH_HIP(hipMalloc(&ix.hstart, sizeof(uint32_t) * cap));
+        MH_HIP(hipMalloc(&ix.hcount, sizeof(uint32_t) * cap));
+    }
+    if ((int64_t)hits.size() > ix.cap_hits) {
+        hipFree(ix.hits);
+        ix.hits = nullptr;
+        ix.cap_hits = (int64_t)hits.size() * 2;
+        MH_HIP(hipMalloc(&ix.hits, sizeof(int2) * ix.cap_hits));
+    }
     MH_HIP(hipMemcpy(ix.codes, codes.data(), codes.size(), hipMemcpyHostToDevice));
     if (n_refs > 0) {
         MH_HIP(hipMemcpy(ix.ref_off, ref_off.data(), sizeof(int64_t) * n_refs, hipMemcpyHostToDevice));
@@ -415,8 +445,8 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipStreamSynchronize(c->stream);
     free_reads(c->reads);
     free_reads(c->rows.reads);
-    for (auto &ix : c->cache) if (ix.hkey != c->index.hkey) free_index(ix);
-    free_index(c->index);
+    for (auto &ix : c->cache) free_index(ix);   // c->index only views one of these
+    free_index(c->small);
     MapState &M = c->map;
     hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work); hipFree(M.slot);
     hipFree(M.pool); hipFree(M.rec); hipFree(M.counters); hipFree(M.ref_stats);
@@ -461,24 +491,24 @@ int mh_index_build(mh_ctx *ctx, int n_refs, const char *const *seqs, int seedlen
     for (int r = 0; r < n_refs; ++r) total += (int64_t)std::strlen(seqs[r]);
     const uint64_t sig = signature(n_refs, seqs, seedlen);
     const bool cacheable = total > 65536;
-    // current index is not cached: drop it unless it lives in the cache
-    bool cur_cached = false;
-    for (auto &ix : c->cache) cur_cached |= ix.hkey == c->index.hkey;
-    if (!cur_cached) free_index(c->index);
-    c->index = DevIndex{};
+    c->index = DevIndex{};   // cache entries and c->small own their buffers
     for (auto &ix : c->cache) {
         if (ix.sig == sig && ix.n_refs == n_refs && ix.seedlen == seedlen) {
             c->index = ix;
             return 0;
         }
     }
+    if (!cacheable) {
+        if (int st = build_index(c->small, n_refs, seqs, seedlen)) return st;
+        c->small.sig = sig;
+        c->index = c->small;
+        return 0;
+    }
     DevIndex ix;
     if (int st = build_index(ix, n_refs, seqs, seedlen)) { free_index(ix); return st; }
     ix.sig = sig;
-    if (cacheable) {
-        if (c->cache.size() >= 2) { free_index(c->cache.front()); c->cache.erase(c->cache.begin()); }
-        c->cache.push_back(ix);
-    }
+    if (c->cache.size() >= 2) { free_index(c->cache.front()); c->cache.erase(c->cache.begin()); }
+    c->cache.push_back(ix);
     c->index = ix;
     return 0;
 }
@@ -1071,6 +1101,41 @@ int mh_pileup(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *
     return st;
 }
 
+// The kernel emits one event per merged pair and position carrying a base +
+// insertion token; a pass over a 3-base insertion site yields one per
+// covering pair.  They are aggregated here to (ref, pos, token) -> count, in
+// (ref, pos, token) order, so the host never handles per-pair records.
+static int aggregate_tokens(CtxEx &c)
+{
+    PileState &P = c.pile;
+    if (c.tok_gen == P.gen) return 0;
+    c.tok_ref.clear(); c.tok_pos.clear(); c.tok_off.clear(); c.tok_len.clear();
+    c.tok_count.clear(); c.tok_pool.clear();
+    int64_t ctr[4] = {0, 0, 0, 0};
+    if (P.ev_counters) MH_HIP(hipMemcpy(ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
+    const int64_t ne = ctr[0];
+    if (ne > 0) {
+        std::vector<int32_t> ev(4 * ne);
+        std::string pool((size_t)ctr[1], '\0');
+        MH_HIP(hipMemcpy(ev.data(), P.ev, sizeof(int32_t) * 4 * ne, hipMemcpyDeviceToHost));
+        if (ctr[1] > 0) MH_HIP(hipMemcpy(&pool[0], P.ev_pool, ctr[1], hipMemcpyDeviceToHost));
+        std::map<std::tuple<int32_t, int32_t, std::string>, int64_t> agg;
+        for (int64_t e = 0; e < ne; ++e)
+            ++agg[std::make_tuple(ev[4 * e], ev[4 * e + 1],
+                                  pool.substr((size_t)ev[4 * e + 2], (size_t)ev[4 * e + 3]))];
+        for (const auto &kv : agg) {
+            c.tok_ref.push_back(std::get<0>(kv.first));
+            c.tok_pos.push_back(std::get<1>(kv.first));
+            c.tok_off.push_back((int32_t)c.tok_pool.size());
+            c.tok_len.push_back((int32_t)std::get<2>(kv.first).size());
+            c.tok_count.push_back(kv.second);
+            c.tok_pool += std::get<2>(kv.first);
+        }
+    }
+    c.tok_gen = P.gen;
+    return 0;
+}
+
 int mh_pileup_dims(mh_ctx *ctx, int *n_refs, int32_t *cap, int64_t *n_events, int64_t *event_bytes)
 {
     if (!ctx) return -3;
@@ -1078,13 +1143,10 @@ int mh_pileup_dims(mh_ctx *ctx, int *n_refs, int32_t *cap, int64_t *n_events, in
     PileState &P = c->pile;
     if (n_refs) *n_refs = P.n_refs;
     if (cap) *cap = P.cap;
-    int64_t ctr[4] = {0, 0, 0, 0};
-    if (P.ev_counters) {
-        MH_HIP(hipSetDevice(c->device));
-        MH_HIP(hipMemcpy(ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
-    }
-    if (n_events) *n_events = ctr[0];
-    if (event_bytes) *event_bytes = ctr[1];
+    MH_HIP(hipSetDevice(c->device));
+    if (int st = aggregate_tokens(*c)) return st;
+    if (n_events) *n_events = (int64_t)c->tok_ref.size();
+    if (event_bytes) *event_bytes = (int64_t)c->tok_pool.size();
     return 0;
 }
 
@@ -1107,24 +1169,19 @@ int mh_pileup_fetch(mh_ctx *ctx, int32_t *dense, uint8_t *nflag, uint8_t *dflag,
 }
 
 int mh_pileup_events(mh_ctx *ctx, int32_t *ref, int32_t *pos, int32_t *tok_off, int32_t *tok_len,
-                     char *pool)
+                     int64_t *count, char *pool)
 {
     if (!ctx) return -3;
     CtxEx *c = X(ctx);
-    PileState &P = c->pile;
     MH_HIP(hipSetDevice(c->device));
-    int64_t ctr[4] = {0, 0, 0, 0};
-    if (P.ev_counters) MH_HIP(hipMemcpy(ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
-    const int64_t ne = ctr[0];
-    std::vector<int32_t> ev(4 * (ne > 0 ? ne : 1));
-    if (ne > 0) MH_HIP(hipMemcpy(ev.data(), P.ev, sizeof(int32_t) * 4 * ne, hipMemcpyDeviceToHost));
-    for (int64_t e = 0; e < ne; ++e) {
-        if (ref) ref[e] = ev[4 * e];
-        if (pos) pos[e] = ev[4 * e + 1];
-        if (tok_off) tok_off[e] = ev[4 * e + 2];
-        if (tok_len) tok_len[e] = ev[4 * e + 3];
-    }
-    if (pool && ctr[1] > 0) MH_HIP(hipMemcpy(pool, P.ev_pool, ctr[1], hipMemcpyDeviceToHost));
+    if (int st = aggregate_tokens(*c)) return st;
+    const size_t n = c->tok_ref.size();
+    if (ref) std::memcpy(ref, c->tok_ref.data(), sizeof(int32_t) * n);
+    if (pos) std::memcpy(pos, c->tok_pos.data(), sizeof(int32_t) * n);
+    if (tok_off) std::memcpy(tok_off, c->tok_off.data(), sizeof(int32_t) * n);
+    if (tok_len) std::memcpy(tok_len, c->tok_len.data(), sizeof(int32_t) * n);
+    if (count) std::memcpy(count, c->tok_count.data(), sizeof(int64_t) * n);
+    if (pool) std::memcpy(pool, c->tok_pool.data(), c->tok_pool.size());
     return 0;
 }
 

@@ -58,6 +58,9 @@ struct DevIndex {
     uint64_t hmask = 0;
     int2 *hits = nullptr;          // (ref, pos) sorted per key
     uint64_t sig = 0;              // content signature (cache key)
+    // allocated capacities (a small index is rebuilt in place every remap pass)
+    int64_t cap_codes = 0, cap_hash = 0, cap_hits = 0;
+    int cap_refs = 0;
 };
 
 constexpr uint64_t HEMPTY = ~0ull;
@@ -134,6 +137,7 @@ struct PileState {
     int64_t *ev_counters = nullptr; // [n_events, pool_used, overflow, error]
     int64_t alloc_cells = 0;
     int alloc_refs = 0;
+    int64_t gen = 0;                // bumped by every mh_pileup / mh_pileup_import
 };
 
 // ---- kernels' host-side launchers (defined in the .hip files) ----------

@@ -438,6 +438,7 @@ static int ensure_pile(Ctx &c)
 int run_pileup(Ctx &c, int source, int q_cutoff)
 {
     PileState &P = c.pile;
+    ++P.gen;
     int64_t n_units;
     const DevReads *R;
     if (source == 0) {

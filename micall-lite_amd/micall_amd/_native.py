@@ -82,7 +82,7 @@ def _declare(L):
         'mh_pileup': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),
         'mh_pileup_dims': ([_P, ctypes.POINTER(ctypes.c_int), _I32P, _I64P, _I64P], ctypes.c_int),
         'mh_pileup_fetch': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
-        'mh_pileup_events': ([_P, _P, _P, _P, _P, _P], ctypes.c_int),
+        'mh_pileup_events': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
         'mh_pileup_packed_bytes': ([_P, _I64P, _I64P], ctypes.c_int),
         'mh_pileup_export': ([_P, _P, _P], ctypes.c_int),
         'mh_pileup_export_base': ([_P, ctypes.c_int64, _P, _P], ctypes.c_int),
@@ -351,12 +351,14 @@ class Context:
         epos = np.zeros(max(ne, 1), dtype=np.int32)
         eoff = np.zeros(max(ne, 1), dtype=np.int32)
         elen = np.zeros(max(ne, 1), dtype=np.int32)
+        ecnt = np.zeros(max(ne, 1), dtype=np.int64)
         pool = ctypes.create_string_buffer(max(nb, 1))
-        check(lib().mh_pileup_events(self.h, _ptr(eref), _ptr(epos), _ptr(eoff), _ptr(elen), pool),
-              'mh_pileup_events')
+        check(lib().mh_pileup_events(self.h, _ptr(eref), _ptr(epos), _ptr(eoff), _ptr(elen),
+                                     _ptr(ecnt), pool), 'mh_pileup_events')
         raw = pool.raw
-        events = [(int(eref[e]), int(epos[e]), raw[eoff[e]:eoff[e] + elen[e]].decode())
-                  for e in range(ne)]
+        # (ref, pos, token, number of merged pairs with that token)
+        events = [(int(eref[e]), int(epos[e]), raw[eoff[e]:eoff[e] + elen[e]].decode(),
+                   int(ecnt[e])) for e in range(ne)]
         return dict(dense=dense[:n], nflag=nflag[:n], dflag=dflag[:n], read_counts=rc[:n],
                     first_unit=fu[:n], max_pos=mp[:n], events=events, cap=cap)
 

@@ -44,8 +44,8 @@ class Pileup:
         self.max_pos = fetched['max_pos']
         self.cap = fetched['cap']
         self.events = {}
-        for r, pos, tok in fetched['events']:
-            self.events.setdefault(r, {}).setdefault(pos, Counter())[tok] += 1
+        for r, pos, tok, count in fetched['events']:
+            self.events.setdefault(r, {}).setdefault(pos, Counter())[tok] += count
 
     def refs_with_reads(self, rank=None):
         """Reference indices that received a merged pair, in refmap order:

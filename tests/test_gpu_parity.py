@@ -116,8 +116,8 @@ def _gpu_pileup_as_refmap(ctx, refnames, reflens, q_cutoff, source=0):
     ctx.pileup(source, q_cutoff, reflens)
     p = ctx.pileup_fetch()
     events = {}
-    for r, pos, tok in p['events']:
-        events.setdefault((r, pos), Counter())[tok] += 1
+    for r, pos, tok, count in p['events']:
+        events.setdefault((r, pos), Counter())[tok] += count
     refmap, counts = {}, Counter()
     order = sorted((p['first_unit'][r], r) for r in range(len(refnames)) if p['first_unit'][r] >= 0)
     for _, r in order:

@@ -73,8 +73,9 @@ def _fetched(alns, seqs, quals, ref_lens, pair_lo, pair_hi):
                 read_counts=np.frombuffer(rc, dtype=np.int64).copy(),
                 first_unit=np.frombuffer(fu, dtype=np.int64).copy(),
                 max_pos=np.frombuffer(mpos, dtype=np.int32).copy(),
-                events=[(e.ref, e.pos, raw[e.tok_off:e.tok_off + e.tok_len].decode())
-                        for e in ev[:ne.value]], cap=cap)
+                events=[k + (n,) for k, n in sorted(Counter(
+                    (e.ref, e.pos, raw[e.tok_off:e.tok_off + e.tok_len].decode())
+                    for e in ev[:ne.value]).items())], cap=cap)
 
 
 def _map_counts(alns, lo, hi):
@@ -152,7 +153,10 @@ def _worker(rank, world, port, out_dir):
             full = _fetched(alns, seqs, qs, lens, 0, N_PAIRS)
             for key in ('dense', 'nflag', 'dflag', 'read_counts', 'first_unit', 'max_pos'):
                 np.testing.assert_array_equal(fetched[key], full[key], err_msg=key)
-            assert Counter(fetched['events']) == Counter(full['events'])
+            merged = Counter()
+            for r, pos, tok, n in fetched['events']:
+                merged[r, pos, tok] += n
+            assert merged == Counter({(r, pos, tok): n for r, pos, tok, n in full['events']})
             want = _map_counts(alns, 0, 2 * N_PAIRS)
             for key, v in want.items():
                 np.testing.assert_array_equal(counts[key], v, err_msg=key)
