@@ -183,136 +183,160 @@ __device__ __forceinline__ bool cand_before(const Cand &x, const Cand &y)
     return x.center < y.center;
 }
 
+// Seeds, hit sort and candidate clustering of read r by one wave; writes the
+// candidates, n_cand and yf, returns the candidate count (wave-uniform).
+__device__ int seed_read(const SeedArgs &A, int64_t r, int lane, uint64_t *hits, Cand *best)
+{
+    const int SL = A.I.seedlen;
+    const int m = A.R.len[r];
+    const int64_t off = A.R.off[r];
+    if (m == 0) {
+        if (lane == 0) { A.n_cand[r] = 0; A.yf[r] = 2; }
+        return 0;
+    }
+    int nn = 0;
+    for (int w = lane; w * 32 < m; w += 64) {
+        uint32_t bits = A.R.nmask[(off >> 5) + w];
+        const int rem = m - w * 32;
+        if (rem < 32) bits &= (1u << rem) - 1;
+        nn += __popc(bits);
+    }
+    nn = wave_sum(nn);
+    if (nn > A.len_tab[2 * (MAXLEN + 1) + m]) {
+        if (lane == 0) { A.n_cand[r] = 0; A.yf[r] = 1; }
+        return 0;
+    }
+    if (lane == 0) A.yf[r] = 0;
+    if (m < SL) {
+        if (lane == 0) A.n_cand[r] = 0;
+        return 0;
+    }
+    const int iv = A.len_tab[m];
+    int ns = 1 + (m - SL) / iv;
+    if (ns > MAXSEEDS) ns = MAXSEEDS;
+    const int s = lane >> 5, t = lane & 31;
+    const int o = t * iv;
+    int cnt = 0;
+    uint32_t start = 0;
+    if (t < ns) {
+        const int p = s == 0 ? o : m - o - SL;
+        if (window_nmask(A.R, off + p, SL) == 0) {
+            uint64_t key = window_key(A.R, off + p, SL);
+            if (s) key = revcomp_key(key, SL);
+            uint64_t h = hash_key(key) & A.I.hmask;
+            for (;;) {
+                const uint64_t k = A.I.hkey[h];
+                if (k == HEMPTY) break;
+                if (k == key) {
+                    start = A.I.hstart[h];
+                    cnt = (int)A.I.hcount[h];
+                    break;
+                }
+                h = (h + 1) & A.I.hmask;
+            }
+            if (cnt > MAXHITS_SEED) cnt = 0;
+        }
+    }
+    const int pre = wave_excl_scan(cnt, lane);
+    int total = wave_sum(cnt);
+    if (total > MAXHITS_MATE) total = MAXHITS_MATE;
+    for (int e = 0; e < cnt && pre + e < MAXHITS_MATE; ++e) {
+        const int2 h = A.I.hits[start + e];
+        const int diag = h.y - o;
+        hits[pre + e] = ((uint64_t)s << 62) | ((uint64_t)h.x << 32) |
+                        (uint64_t)(uint32_t)(diag + (1 << 30));
+    }
+    if (total == 0) {
+        if (lane == 0) A.n_cand[r] = 0;
+        return 0;
+    }
+    int N = 1;
+    while (N < total) N <<= 1;
+    for (int x = total + lane; x < N; x += 64) hits[x] = ~0ull;
+    wave_sync();
+    // bitonic sort, ascending
+    for (int k = 2; k <= N; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int tt = lane; tt < (N >> 1); tt += 64) {
+                const int i = 2 * j * (tt / j) + (tt % j);
+                const int q = i + j;
+                const uint64_t a = hits[i], b = hits[q];
+                const bool up = (i & k) == 0;
+                if ((a > b) == up) { hits[i] = b; hits[q] = a; }
+            }
+            wave_sync();
+        }
+    }
+    int nc = 0;
+    if (lane == 0) {
+        int h0 = 0;
+        while (h0 < total) {
+            const uint64_t k0 = hits[h0];
+            const int st = (int)(k0 >> 62), rf = (int)((k0 >> 32) & 0x3fffffff);
+            int h1 = h0 + 1;
+            int prev = (int)(uint32_t)k0 - (1 << 30);
+            while (h1 < total) {
+                const uint64_t k1 = hits[h1];
+                const int d1 = (int)(uint32_t)k1 - (1 << 30);
+                if ((k1 >> 32) != (k0 >> 32) || d1 - prev > CLUSTER_GAP) break;
+                prev = d1;
+                ++h1;
+            }
+            int center = (int)(uint32_t)k0 - (1 << 30), center_n = 0;
+            for (int a = h0; a < h1;) {
+                int b = a + 1;
+                while (b < h1 && hits[b] == hits[a]) ++b;
+                if (b - a > center_n) {
+                    center_n = b - a;
+                    center = (int)(uint32_t)hits[a] - (1 << 30);
+                }
+                a = b;
+            }
+            Cand c{st, rf, center, h1 - h0};
+            int at = nc;
+            while (at > 0 && cand_before(c, best[at - 1])) --at;
+            if (at < MAXCAND) {
+                const int last = nc < MAXCAND ? nc : MAXCAND - 1;
+                for (int z = last; z > at; --z) best[z] = best[z - 1];
+                best[at] = c;
+                if (nc < MAXCAND) ++nc;
+            }
+            h0 = h1;
+        }
+        for (int c = 0; c < nc; ++c) A.cand[r * MAXCAND + c] = best[c];
+        A.n_cand[r] = nc;
+    }
+    wave_sync();
+    return __builtin_amdgcn_readfirstlane(nc);
+}
+
+// One wave per chunk of SEED_CHUNK consecutive reads: the chunk's extension
+// work items are collected in LDS and appended to the work list with one
+// atomic (a returning same-address atomic costs ~11 ns device-wide).
+constexpr int SEED_CHUNK = 32;
+
 __global__ __launch_bounds__(256) void k_seed(SeedArgs A)
 {
     __shared__ uint64_t sh_hits[4][MAXHITS_MATE];
     __shared__ Cand sh_best[4][MAXCAND];
+    __shared__ int32_t sh_work[4][SEED_CHUNK * MAXCAND];
     const int lane = threadIdx.x & 63;
     const int wv = wave_uniform(threadIdx.x >> 6);
-    uint64_t *hits = sh_hits[wv];
-    Cand *best = sh_best[wv];
-    const int SL = A.I.seedlen;
-    for (int64_t r = (int64_t)blockIdx.x * 4 + wv; r < A.R.n; r += (int64_t)gridDim.x * 4) {
-        const int m = A.R.len[r];
-        const int64_t off = A.R.off[r];
-        if (m == 0) {
-            if (lane == 0) { A.n_cand[r] = 0; A.yf[r] = 2; }
-            continue;
+    const int64_t n_chunks = (A.R.n + SEED_CHUNK - 1) / SEED_CHUNK;
+    for (int64_t ch = (int64_t)blockIdx.x * 4 + wv; ch < n_chunks; ch += (int64_t)gridDim.x * 4) {
+        int n_work = 0;
+        const int64_t r0 = ch * SEED_CHUNK;
+        const int64_t r1 = r0 + SEED_CHUNK < A.R.n ? r0 + SEED_CHUNK : A.R.n;
+        for (int64_t r = r0; r < r1; ++r) {
+            const int nc = seed_read(A, r, lane, sh_hits[wv], sh_best[wv]);
+            if (lane < nc) sh_work[wv][n_work + lane] = (int32_t)(r * MAXCAND + lane);
+            n_work += nc;
         }
-        int nn = 0;
-        for (int w = lane; w * 32 < m; w += 64) {
-            uint32_t bits = A.R.nmask[(off >> 5) + w];
-            const int rem = m - w * 32;
-            if (rem < 32) bits &= (1u << rem) - 1;
-            nn += __popc(bits);
-        }
-        nn = wave_sum(nn);
-        if (nn > A.len_tab[2 * (MAXLEN + 1) + m]) {
-            if (lane == 0) { A.n_cand[r] = 0; A.yf[r] = 1; }
-            continue;
-        }
-        if (lane == 0) A.yf[r] = 0;
-        if (m < SL) {
-            if (lane == 0) A.n_cand[r] = 0;
-            continue;
-        }
-        const int iv = A.len_tab[m];
-        int ns = 1 + (m - SL) / iv;
-        if (ns > MAXSEEDS) ns = MAXSEEDS;
-        const int s = lane >> 5, t = lane & 31;
-        const int o = t * iv;
-        int cnt = 0;
-        uint32_t start = 0;
-        if (t < ns) {
-            const int p = s == 0 ? o : m - o - SL;
-            if (window_nmask(A.R, off + p, SL) == 0) {
-                uint64_t key = window_key(A.R, off + p, SL);
-                if (s) key = revcomp_key(key, SL);
-                uint64_t h = hash_key(key) & A.I.hmask;
-                for (;;) {
-                    const uint64_t k = A.I.hkey[h];
-                    if (k == HEMPTY) break;
-                    if (k == key) {
-                        start = A.I.hstart[h];
-                        cnt = (int)A.I.hcount[h];
-                        break;
-                    }
-                    h = (h + 1) & A.I.hmask;
-                }
-                if (cnt > MAXHITS_SEED) cnt = 0;
-            }
-        }
-        const int pre = wave_excl_scan(cnt, lane);
-        int total = wave_sum(cnt);
-        if (total > MAXHITS_MATE) total = MAXHITS_MATE;
-        for (int e = 0; e < cnt && pre + e < MAXHITS_MATE; ++e) {
-            const int2 h = A.I.hits[start + e];
-            const int diag = h.y - o;
-            hits[pre + e] = ((uint64_t)s << 62) | ((uint64_t)h.x << 32) |
-                            (uint64_t)(uint32_t)(diag + (1 << 30));
-        }
-        if (total == 0) {
-            if (lane == 0) A.n_cand[r] = 0;
-            continue;
-        }
-        int N = 1;
-        while (N < total) N <<= 1;
-        for (int x = total + lane; x < N; x += 64) hits[x] = ~0ull;
         wave_sync();
-        // bitonic sort, ascending
-        for (int k = 2; k <= N; k <<= 1) {
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int tt = lane; tt < (N >> 1); tt += 64) {
-                    const int i = 2 * j * (tt / j) + (tt % j);
-                    const int q = i + j;
-                    const uint64_t a = hits[i], b = hits[q];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) { hits[i] = b; hits[q] = a; }
-                }
-                wave_sync();
-            }
-        }
-        if (lane == 0) {
-            int nc = 0;
-            int h0 = 0;
-            while (h0 < total) {
-                const uint64_t k0 = hits[h0];
-                const int st = (int)(k0 >> 62), rf = (int)((k0 >> 32) & 0x3fffffff);
-                int h1 = h0 + 1;
-                int prev = (int)(uint32_t)k0 - (1 << 30);
-                while (h1 < total) {
-                    const uint64_t k1 = hits[h1];
-                    const int d1 = (int)(uint32_t)k1 - (1 << 30);
-                    if ((k1 >> 32) != (k0 >> 32) || d1 - prev > CLUSTER_GAP) break;
-                    prev = d1;
-                    ++h1;
-                }
-                int center = (int)(uint32_t)k0 - (1 << 30), center_n = 0;
-                for (int a = h0; a < h1;) {
-                    int b = a + 1;
-                    while (b < h1 && hits[b] == hits[a]) ++b;
-                    if (b - a > center_n) {
-                        center_n = b - a;
-                        center = (int)(uint32_t)hits[a] - (1 << 30);
-                    }
-                    a = b;
-                }
-                Cand c{st, rf, center, h1 - h0};
-                int at = nc;
-                while (at > 0 && cand_before(c, best[at - 1])) --at;
-                if (at < MAXCAND) {
-                    const int last = nc < MAXCAND ? nc : MAXCAND - 1;
-                    for (int z = last; z > at; --z) best[z] = best[z - 1];
-                    best[at] = c;
-                    if (nc < MAXCAND) ++nc;
-                }
-                h0 = h1;
-            }
-            for (int c = 0; c < nc; ++c) A.cand[r * MAXCAND + c] = best[c];
-            A.n_cand[r] = nc;
-            const int base = atomicAdd(&A.counters[0], nc);
-            for (int c = 0; c < nc; ++c) A.work[base + c] = (int32_t)(r * MAXCAND + c);
-        }
+        int base = 0;
+        if (lane == 0 && n_work) base = atomicAdd(&A.counters[0], n_work);
+        base = __builtin_amdgcn_readfirstlane(base);
+        for (int x = lane; x < n_work; x += 64) A.work[base + x] = sh_work[wv][x];
         wave_sync();
     }
 }
@@ -348,6 +372,10 @@ __device__ __forceinline__ int mm_pen(int qchar)
 // edges acts as minus infinity.  The moves then fold into the ALU op that uses
 // them (v_max_i32_dpp, v_add_u32_dpp) instead of costing a mov + a fill each.
 constexpr int BIAS = 1 << 20;
+// CIGAR ops are reserved per wave in chunks (one atomic per chunk, not per
+// extension); the pool is sized for every resident wave's partial chunk.
+constexpr int POOL_CHUNK = 256;
+constexpr int DP_MAX_BLOCKS = 256 * 48;
 
 template <int CTRL>
 __device__ __forceinline__ int dppz(int v)
@@ -448,6 +476,8 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     K.xD = lane * A.exD;
     K.cF = -(A.oeD - A.exD) - A.exD * lane;
 
+    int64_t ck_base = 0;   // lane 0: this wave's current CIGAR pool chunk
+    int ck_left = 0;
     for (int w = blockIdx.x * wpb + wv; w < n_work; w += gridDim.x * wpb) {
         const int sid = A.work[w];
         const int64_t r = sid / MAXCAND;
@@ -656,7 +686,13 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                 if (lo >= hi) {
                     int nc = (clipL > 0) + (clipR > 0) + (lo - hi + 1);
                     if (nc <= MH_MAXOPS - 1) {
-                        const int64_t base = atomicAdd(&A.pool_ctr[0], nc);
+                        if (nc > ck_left) {   // next wave-private chunk of the pool
+                            ck_base = atomicAdd(&A.pool_ctr[0], POOL_CHUNK);
+                            ck_left = POOL_CHUNK;
+                        }
+                        const int64_t base = ck_base;
+                        ck_base += nc;
+                        ck_left -= nc;
                         if (base + nc > A.pool_cap) {
                             atomicExch(&A.pool_ctr[1], 1);
                         } else {
@@ -1024,7 +1060,7 @@ static int ensure_map_buffers(Ctx &c)
         M.cap_refs = cr;
     }
     if (M.pool == nullptr) {
-        M.pool_cap = (n > 0 ? n : 1) * 8 + 4096;
+        M.pool_cap = (n > 0 ? n : 1) * 8 + 4096 + (int64_t)DP_MAX_BLOCKS * 4 * POOL_CHUNK;
         MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * M.pool_cap));
     }
     return 0;
@@ -1071,7 +1107,7 @@ int run_map(Ctx &c, const mh_params &par)
     hipLaunchKernelGGL(k_init_stats, dim3(64), dim3(256), 0, s, M.ref_stats, M.n_refs);
     if (n > 0) {
         SeedArgs sa{c.reads, c.index, par.mode, c.len_tab, M.cand, M.n_cand, M.yf, M.work, M.counters};
-        int64_t blocks = (n + 3) / 4;
+        int64_t blocks = ((n + SEED_CHUNK - 1) / SEED_CHUNK + 3) / 4;
         if (blocks > 1 << 16) blocks = 1 << 16;
         const int pk = prof_begin(c, "k_seed");
         hipLaunchKernelGGL(k_seed, dim3((unsigned)blocks), dim3(256), 0, s, sa);
@@ -1090,7 +1126,7 @@ int run_map(Ctx &c, const mh_params &par)
             if (wpb > 4) wpb = 4;
             if (wpb < 1) { set_error("mh_map: reads too long for LDS"); return -3; }
             int64_t dblocks = (n * 2 + wpb - 1) / wpb;
-            if (dblocks > 256 * 48) dblocks = 256 * 48;
+            if (dblocks > DP_MAX_BLOCKS) dblocks = DP_MAX_BLOCKS;
             const int pd = prof_begin(c, "k_dp");
             if (par.mode == MH_LOCAL) {
                 MH_HIP(hipFuncSetAttribute((const void *)k_dp<1>,
@@ -1111,7 +1147,7 @@ int run_map(Ctx &c, const mh_params &par)
             if (!ctr[2]) break;
             // CIGAR pool overflow: grow to what was asked for and redo the extensions
             hipFree(M.pool);
-            M.pool_cap = (int64_t)ctr[1] * 2 + 4096;
+            M.pool_cap = (int64_t)ctr[1] * 2 + 4096 + (int64_t)DP_MAX_BLOCKS * 4 * POOL_CHUNK;
             MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * M.pool_cap));
             if (attempt == 1) { set_error("mh_map: CIGAR pool overflow"); return -2; }
         }
