@@ -857,6 +857,22 @@ int mh_rows_load(mh_ctx *ctx, int64_t n_rows, const int32_t *flag, const int32_t
             }
         }
     }
+    {
+        // hot reference (most mapped rows) and the longest reference span
+        std::unordered_map<int32_t, int64_t> per_ref;
+        int64_t best = 0;
+        for (int64_t i = 0; i < n_rows; ++i) {
+            if (flag[i] & 4) continue;
+            int span = 0;
+            for (int k = 0; k < n_cigar[i]; ++k) {
+                const uint32_t op = cigar[cigar_off[i] + k];
+                if ((op & 15) == MH_OP_M || (op & 15) == MH_OP_D) span += (int)(op >> 4);
+            }
+            R.max_span = std::max(R.max_span, span);
+            const int64_t cnt = ++per_ref[ref[i]];
+            if (cnt > best || (cnt == best && ref[i] < R.hot_ref)) { best = cnt; R.hot_ref = ref[i]; }
+        }
+    }
     const int64_t nr = n_rows > 0 ? n_rows : 1;
     MH_HIP(hipMalloc(&R.flag, sizeof(int32_t) * nr));
     MH_HIP(hipMalloc(&R.ref, sizeof(int32_t) * nr));
@@ -1095,6 +1111,7 @@ int mh_pileup(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *
     for (int r = 0; r < n_refs; ++r) cap = std::max(cap, ref_lens[r] + MH_PILEUP_SLACK);
     c->pile.n_refs = n_refs;
     c->pile.cap = cap;
+    c->pile.ref_lens.assign(ref_lens, ref_lens + n_refs);
     int st = run_pileup(*c, source, q_cutoff);
     if (st == 0) MH_HIP(hipStreamSynchronize(c->stream));
     prof_flush(*c);

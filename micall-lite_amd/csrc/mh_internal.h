@@ -120,6 +120,8 @@ struct RowState {
     uint32_t *cigar = nullptr;
     int64_t *units = nullptr;
     DevReads reads;
+    int hot_ref = -1;      // reference of most mapped rows (pileup LDS window)
+    int max_span = 0;      // longest reference span (M + D) of a mapped row
 };
 
 struct PileState {
@@ -138,6 +140,7 @@ struct PileState {
     int64_t alloc_cells = 0;
     int alloc_refs = 0;
     int64_t gen = 0;                // bumped by every mh_pileup / mh_pileup_import
+    std::vector<int32_t> ref_lens;  // host copy (sizes the LDS window)
 };
 
 // ---- kernels' host-side launchers (defined in the .hip files) ----------

@@ -14,8 +14,9 @@
 
 namespace mh {
 
-constexpr int PU_MAXREF = 2048;   // reference span per mate staged in LDS
 constexpr int PU_INSBUF = 2048;   // merged insertion bytes per unit
+constexpr int PU_MAXINS = 2 * MH_MAXOPS;
+constexpr int PU_LDS = 160 * 1024;
 
 struct RowV {
     int present, flag, ref, pos, n_cigar, rev, m;
@@ -47,6 +48,11 @@ struct PileArgs {
     long long ev_cap, pool_cap;
     unsigned long long *ev_ctr;  // [0] events, [1] pool bytes, [2] overflow, [3] error
     int q_cutoff;
+    // LDS layout: the hot reference's counters for positions 1..win_pos
+    // (A/C/G/T planes) and its per-ref scalars, then one staging area per wave
+    int hot_ref, win_pos;
+    int span_cap;                // reference span per mate staged in LDS
+    int unit_bytes;              // staging bytes per wave
 };
 
 template <int SRC>
@@ -87,21 +93,44 @@ __device__ __forceinline__ void sam_base(const DevReads &R, const RowV &v, int x
     q = (char)R.qual[g];
 }
 
-struct MateLds {
-    char c[PU_MAXREF];
-    char q[PU_MAXREF];
-    int32_t opref[MH_MAXOPS + 1];   // reference offset at the start of each op
-    int32_t opread[MH_MAXOPS + 1];  // read offset at the start of each op
+// One wave's LDS staging area (span_cap = SPAN):
+//   c[2][SPAN], q[2][SPAN]                 both mates in reference coordinates
+//   opref[2][MH_MAXOPS+1], opread[2][...]  reference / read offset of every op
+//   ins_key/off/len[PU_MAXINS], insbuf[PU_INSBUF], n_ins
+struct UnitView {
+    char *c[2], *q[2];
+    int32_t *opref[2], *opread[2];
+    int32_t *ins_key, *ins_off, *ins_len;
+    char *insbuf;
+    int32_t *n_ins;
 };
 
-struct UnitLds {
-    MateLds mate[2];
-    int32_t ins_key[2 * MH_MAXOPS];
-    int32_t ins_off[2 * MH_MAXOPS];   // into insbuf
-    int32_t ins_len[2 * MH_MAXOPS];
-    char insbuf[PU_INSBUF];
-    int32_t n_ins;
-    int32_t misc[8];
+__host__ __device__ inline int unit_bytes_for(int span)
+{
+    return 4 * span + 4 * 4 * (MH_MAXOPS + 1) + 3 * 4 * PU_MAXINS + PU_INSBUF + 16;
+}
+
+__device__ inline UnitView unit_view(unsigned char *base, int span)
+{
+    UnitView v;
+    for (int k = 0; k < 2; ++k) {
+        v.c[k] = (char *)base + (2 * k) * span;
+        v.q[k] = (char *)base + (2 * k + 1) * span;
+    }
+    int32_t *ip = (int32_t *)(base + 4 * span);
+    v.opref[0] = ip; v.opread[0] = ip + (MH_MAXOPS + 1);
+    v.opref[1] = ip + 2 * (MH_MAXOPS + 1); v.opread[1] = ip + 3 * (MH_MAXOPS + 1);
+    ip += 4 * (MH_MAXOPS + 1);
+    v.ins_key = ip; v.ins_off = ip + PU_MAXINS; v.ins_len = ip + 2 * PU_MAXINS;
+    v.insbuf = (char *)(ip + 3 * PU_MAXINS);
+    v.n_ins = (int32_t *)(v.insbuf + PU_INSBUF);
+    return v;
+}
+
+struct HotLds {
+    unsigned int read_count;
+    int max_pos;
+    long long first_unit;
 };
 
 // merge_pairs on two short strings without '-' (insertions), sam2aln.py:156-237
@@ -139,14 +168,21 @@ __device__ int merge_ins_strings(const char *s1, const char *q1, int l1, const c
 }
 
 template <int SRC>
-__global__ __launch_bounds__(256) void k_pileup(PileArgs A)
+__global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wpb = blockDim.x >> 6;
-    UnitLds &L = *reinterpret_cast<UnitLds *>(smem + (size_t)wv * sizeof(UnitLds));
+    const int WP = A.win_pos;
+    unsigned int *win = (unsigned int *)smem;                 // [4][WP]
+    HotLds *hot = (HotLds *)(smem + (size_t)16 * WP);
+    UnitView L = unit_view(smem + (size_t)16 * WP + sizeof(HotLds) + (size_t)wv * A.unit_bytes,
+                           A.span_cap);
     const unsigned char cut = (unsigned char)(A.q_cutoff + 33);
+    for (int x = threadIdx.x; x < 4 * WP; x += blockDim.x) win[x] = 0;
+    if (threadIdx.x == 0) { hot->read_count = 0; hot->max_pos = 0; hot->first_unit = INT64_MAX; }
+    __syncthreads();
 
     for (int64_t u = (int64_t)blockIdx.x * wpb + wv; u < A.n_units; u += (int64_t)gridDim.x * wpb) {
         int64_t row1, row2;
@@ -181,15 +217,15 @@ __global__ __launch_bounds__(256) void k_pileup(PileArgs A)
             for (int o = 0; o < mp[k].n_cigar; ++o) {
                 const uint32_t op = mp[k].cig[o];
                 const int n = (int)(op >> 4), t = (int)(op & 15);
-                if (lane == 0 && o < MH_MAXOPS) { L.mate[k].opref[o] = rf; L.mate[k].opread[o] = rd; }
+                if (lane == 0 && o < MH_MAXOPS) { L.opref[k][o] = rf; L.opread[k][o] = rd; }
                 if (t == MH_OP_M) { rf += n; rd += n; }
                 else if (t == MH_OP_D) rf += n;
                 else if (t == MH_OP_I || t == MH_OP_S) rd += n;
                 else bad = 1;
                 if (rd > mp[k].m) bad = 1;
             }
-            if (lane == 0 && mp[k].n_cigar <= MH_MAXOPS) { L.mate[k].opref[mp[k].n_cigar] = rf; L.mate[k].opread[mp[k].n_cigar] = rd; }
-            if (rd != mp[k].m || rf > PU_MAXREF || mp[k].pos < 1 || mp[k].n_cigar > MH_MAXOPS) bad = 1;
+            if (lane == 0 && mp[k].n_cigar <= MH_MAXOPS) { L.opref[k][mp[k].n_cigar] = rf; L.opread[k][mp[k].n_cigar] = rd; }
+            if (rd != mp[k].m || rf > A.span_cap || mp[k].pos < 1 || mp[k].n_cigar > MH_MAXOPS) bad = 1;
             pad[k] = mp[k].pos - 1;
             len[k] = pad[k] + rf;
         }
@@ -202,14 +238,14 @@ __global__ __launch_bounds__(256) void k_pileup(PileArgs A)
             const int span = len[k] - pad[k];
             for (int t = lane; t < span; t += 64) {
                 int o = 0;
-                while (L.mate[k].opref[o + 1] <= t ||
+                while (L.opref[k][o + 1] <= t ||
                        ((mp[k].cig[o] & 15) != MH_OP_M && (mp[k].cig[o] & 15) != MH_OP_D))
                     ++o;
                 const uint32_t op = mp[k].cig[o];
                 char c = '-', q = ' ';
-                if ((op & 15) == MH_OP_M) sam_base(A.R, mp[k], L.mate[k].opread[o] + (t - L.mate[k].opref[o]), c, q);
-                L.mate[k].c[t] = c;
-                L.mate[k].q[t] = q;
+                if ((op & 15) == MH_OP_M) sam_base(A.R, mp[k], L.opread[k][o] + (t - L.opref[k][o]), c, q);
+                L.c[k][t] = c;
+                L.q[k][t] = q;
             }
         }
         // ---- merge_inserts (lane 0): keys left + pad, sam2aln.py:133-135 ----
@@ -221,11 +257,11 @@ __global__ __launch_bounds__(256) void k_pileup(PileArgs A)
                 for (int o = 0; o < v.n_cigar; ++o) {
                     if ((v.cig[o] & 15) != MH_OP_I) continue;
                     const int il = (int)(v.cig[o] >> 4);
-                    const int key = L.mate[pass].opread[o] + pad[pass];
+                    const int key = L.opread[pass][o] + pad[pass];
                     char tc[1], tq[1];
                     unsigned char mn = 255;
                     for (int x = 0; x < il; ++x) {
-                        sam_base(A.R, v, L.mate[pass].opread[o] + x, tc[0], tq[0]);
+                        sam_base(A.R, v, L.opread[pass][o] + x, tc[0], tq[0]);
                         if ((unsigned char)tq[0] < mn) mn = (unsigned char)tq[0];
                     }
                     if (!(mn > cut)) continue;
@@ -236,7 +272,7 @@ __global__ __launch_bounds__(256) void k_pileup(PileArgs A)
                     char *dst = L.insbuf + used;
                     int outlen;
                     if (pass == 0) {
-                        for (int x = 0; x < il; ++x) sam_base(A.R, v, L.mate[pass].opread[o] + x, dst[x], tc[0]);
+                        for (int x = 0; x < il; ++x) sam_base(A.R, v, L.opread[pass][o] + x, dst[x], tc[0]);
                         outlen = il;
                     } else {
                         // ins1 at this key (even if it failed quality) merges with ins2
@@ -245,13 +281,13 @@ __global__ __launch_bounds__(256) void k_pileup(PileArgs A)
                         const RowV &w = mp[0];
                         for (int o1 = 0; o1 < w.n_cigar; ++o1) {
                             if ((w.cig[o1] & 15) != MH_OP_I) continue;
-                            if (L.mate[0].opread[o1] + pad[0] != key) continue;
+                            if (L.opread[0][o1] + pad[0] != key) continue;
                             l1 = (int)(w.cig[o1] >> 4);
                             if (l1 > PU_INSBUF / 8) l1 = PU_INSBUF / 8;
-                            for (int x = 0; x < l1; ++x) sam_base(A.R, w, L.mate[0].opread[o1] + x, s1[x], q1[x]);
+                            for (int x = 0; x < l1; ++x) sam_base(A.R, w, L.opread[0][o1] + x, s1[x], q1[x]);
                         }
                         const int l2 = il > PU_INSBUF / 8 ? PU_INSBUF / 8 : il;
-                        for (int x = 0; x < l2; ++x) sam_base(A.R, v, L.mate[pass].opread[o] + x, s2[x], q2[x]);
+                        for (int x = 0; x < l2; ++x) sam_base(A.R, v, L.opread[pass][o] + x, s2[x], q2[x]);
                         outlen = merge_ins_strings(s1, q1, l1, s2, q2, l2, A.q_cutoff, dst);
                     }
                     if (at < 0) at = n++;
@@ -261,7 +297,7 @@ __global__ __launch_bounds__(256) void k_pileup(PileArgs A)
                     used += outlen;
                 }
             }
-            L.n_ins = n;
+            *L.n_ins = n;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -279,10 +315,10 @@ __global__ __launch_bounds__(256) void k_pileup(PileArgs A)
         len2 = len[b];
         pad2 = pad[b];
         auto ch1 = [&](int i, char &c, char &q) {
-            if (i < pad1) { c = '-'; q = '!'; } else { c = L.mate[a].c[i - pad1]; q = L.mate[a].q[i - pad1]; }
+            if (i < pad1) { c = '-'; q = '!'; } else { c = L.c[a][i - pad1]; q = L.q[a][i - pad1]; }
         };
         auto ch2 = [&](int i, char &c, char &q) {
-            if (i < pad2) { c = '-'; q = '!'; } else { c = L.mate[b].c[i - pad2]; q = L.mate[b].q[i - pad2]; }
+            if (i < pad2) { c = '-'; q = '!'; } else { c = L.c[b][i - pad2]; q = L.q[b][i - pad2]; }
         };
         const int lo = a >= 0 ? (pad1 < pad2 ? pad1 : pad2) : pad2;
         // first index where seq2 is not '-' (is_reverse_started) and where the
@@ -323,7 +359,8 @@ __global__ __launch_bounds__(256) void k_pileup(PileArgs A)
         // ---- update_counts over mseq (remap.py:284-301) ----
         int mxp = 0;
         int err = 0;
-        const int n_ins = L.n_ins;
+        const int n_ins = *L.n_ins;
+        const bool is_hot = ref == A.hot_ref;
         for (int i0 = begin; i0 < len2; i0 += 64) {
             const int i = i0 + lane;
             if (i >= len2) break;
@@ -375,7 +412,8 @@ __global__ __launch_bounds__(256) void k_pileup(PileArgs A)
                 }
             } else {
                 const int code = mc == 'A' ? 0 : mc == 'C' ? 1 : mc == 'G' ? 2 : 3;
-                atomicAdd(&A.dense[cell * 4 + code], 1);
+                if (is_hot && P <= WP) atomicAdd(&win[code * WP + (P - 1)], 1u);
+                else atomicAdd(&A.dense[cell * 4 + code], 1);
             }
         }
         for (int o = 32; o > 0; o >>= 1) {
@@ -383,12 +421,33 @@ __global__ __launch_bounds__(256) void k_pileup(PileArgs A)
             err |= __shfl_xor(err, o, 64);
         }
         if (lane == 0) {
-            atomicAdd(&A.read_counts[ref], 1ull);
-            atomicMin(&A.first_unit[ref], (long long)u);
-            if (mxp > 0) atomicMax(&A.max_pos[ref], mxp);
+            if (is_hot) {
+                atomicAdd(&hot->read_count, 1u);
+                atomicMin(&hot->first_unit, (long long)u);
+                if (mxp > 0) atomicMax(&hot->max_pos, mxp);
+            } else {
+                atomicAdd(&A.read_counts[ref], 1ull);
+                atomicMin(&A.first_unit[ref], (long long)u);
+                if (mxp > 0) atomicMax(&A.max_pos[ref], mxp);
+            }
             if (err) atomicExch(&A.ev_ctr[3], 1ull);
         }
         __builtin_amdgcn_wave_barrier();
+    }
+    // ---- flush the block's hot-reference counters: consecutive threads add
+    // to consecutive words of dense (cell-major, A/C/G/T minor) ----
+    __syncthreads();
+    if (A.hot_ref >= 0) {
+        int32_t *dst = A.dense + (int64_t)A.hot_ref * A.cap * 4;
+        for (int x = threadIdx.x; x < 4 * WP; x += blockDim.x) {
+            const unsigned int v = win[(x & 3) * WP + (x >> 2)];
+            if (v) atomicAdd(&dst[x], (int)v);
+        }
+        if (threadIdx.x == 0 && hot->read_count) {
+            atomicAdd(&A.read_counts[A.hot_ref], (unsigned long long)hot->read_count);
+            atomicMin(&A.first_unit[A.hot_ref], hot->first_unit);
+            if (hot->max_pos > 0) atomicMax(&A.max_pos[A.hot_ref], hot->max_pos);
+        }
     }
 }
 
@@ -435,6 +494,55 @@ static int ensure_pile(Ctx &c)
     return 0;
 }
 
+// Launch shape of k_pileup.  The reference most units map to gets its A/C/G/T
+// counters for positions 1..win_pos in LDS, shared by all waves of a block
+// (the memory-side int atomics of the dense counters are the kernel's cost
+// otherwise); the rest of the LDS holds one staging area per wave.
+struct PileGeometry {
+    int hot_ref = -1, win_pos = 0, span = 0, unit_bytes = 0, wpb = 1;
+    int64_t blocks = 1;
+    size_t lds = 0;
+};
+
+static int pile_geometry(Ctx &c, int source, int64_t n_units, PileGeometry &g)
+{
+    PileState &P = c.pile;
+    int hot = -1, span = 0;
+    if (source == 0) {
+        span = c.reads.max_len + BAND;   // M + D <= read length + band width
+        const int n = c.map.n_refs;
+        std::vector<int64_t> st(5 * (size_t)n + 3);
+        MH_HIP(hipMemcpy(st.data(), c.map.ref_stats, sizeof(int64_t) * st.size(), hipMemcpyDeviceToHost));
+        int64_t best = 0;
+        for (int r = 0; r < n && r < P.n_refs; ++r)
+            if (st[2 * n + r] > best) { best = st[2 * n + r]; hot = r; }
+    } else {
+        span = c.rows.max_span;
+        hot = c.rows.hot_ref < P.n_refs ? c.rows.hot_ref : -1;
+    }
+    g.span = ((span > 16 ? span : 16) + 15) & ~15;
+    g.unit_bytes = (unit_bytes_for(g.span) + 15) & ~15;
+    const int base = (int)sizeof(HotLds);
+    if (base + g.unit_bytes > PU_LDS) { set_error("mh_pileup: reference span %d too long", span); return -3; }
+    if (hot >= 0) {
+        int want = P.ref_lens[hot] + 64;
+        if (want > P.cap) want = P.cap;
+        const int room = (PU_LDS - base - 8 * g.unit_bytes) / 16;
+        g.win_pos = want < room ? want : room;
+        if (g.win_pos < 256) g.win_pos = 0;
+    }
+    g.hot_ref = g.win_pos > 0 ? hot : -1;
+    g.wpb = (PU_LDS - base - 16 * g.win_pos) / g.unit_bytes;
+    if (g.wpb > 16) g.wpb = 16;
+    if (g.wpb < 1) g.wpb = 1;
+    g.lds = (size_t)16 * g.win_pos + base + (size_t)g.wpb * g.unit_bytes;
+    g.blocks = (n_units + g.wpb - 1) / g.wpb;
+    const int64_t max_blocks = g.win_pos > 0 ? 256 : 256 * 8;
+    if (g.blocks > max_blocks) g.blocks = max_blocks;
+    if (g.blocks < 1) g.blocks = 1;
+    return 0;
+}
+
 int run_pileup(Ctx &c, int source, int q_cutoff)
 {
     PileState &P = c.pile;
@@ -451,6 +559,8 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
     }
     if (int st = ensure_pile(c)) return st;
     hipStream_t s = c.stream;
+    PileGeometry geo;
+    if (int st = pile_geometry(c, source, n_units, geo)) return st;
     const int64_t cells = (int64_t)P.n_refs * P.cap;
     for (int attempt = 0; attempt < 3; ++attempt) {
         MH_HIP(hipMemsetAsync(P.dense, 0, sizeof(int32_t) * 4 * (cells > 0 ? cells : 1), s));
@@ -477,18 +587,18 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
         A.ev = P.ev; A.ev_pool = P.ev_pool; A.ev_cap = P.ev_cap; A.pool_cap = P.pool_cap;
         A.ev_ctr = (unsigned long long *)P.ev_counters;
         A.q_cutoff = q_cutoff;
+        A.hot_ref = geo.hot_ref;
+        A.win_pos = geo.win_pos;
+        A.span_cap = geo.span;
+        A.unit_bytes = geo.unit_bytes;
         if (n_units > 0) {
-            const int wpb = 2;
-            const size_t lds = sizeof(UnitLds) * wpb;
-            int64_t blocks = (n_units + wpb - 1) / wpb;
-            if (blocks > 256 * 32) blocks = 256 * 32;
             const int pk = prof_begin(c, "k_pileup");
             if (source == 0) {
-                MH_HIP(hipFuncSetAttribute((const void *)k_pileup<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                hipLaunchKernelGGL(k_pileup<0>, dim3((unsigned)blocks), dim3(64 * wpb), lds, s, A);
+                MH_HIP(hipFuncSetAttribute((const void *)k_pileup<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds));
+                hipLaunchKernelGGL(k_pileup<0>, dim3((unsigned)geo.blocks), dim3(64 * geo.wpb), geo.lds, s, A);
             } else {
-                MH_HIP(hipFuncSetAttribute((const void *)k_pileup<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                hipLaunchKernelGGL(k_pileup<1>, dim3((unsigned)blocks), dim3(64 * wpb), lds, s, A);
+                MH_HIP(hipFuncSetAttribute((const void *)k_pileup<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds));
+                hipLaunchKernelGGL(k_pileup<1>, dim3((unsigned)geo.blocks), dim3(64 * geo.wpb), geo.lds, s, A);
             }
             prof_end(c, pk);
             MH_HIP(hipGetLastError());
