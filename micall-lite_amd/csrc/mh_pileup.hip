@@ -53,6 +53,7 @@ struct PileArgs {
     int hot_ref, win_pos;
     int span_cap;                // reference span per mate staged in LDS
     int unit_bytes;              // staging bytes per wave
+    char *ins_scratch;           // PU_INS_BYTES per wave of the grid
 };
 
 template <int SRC>
@@ -96,34 +97,49 @@ __device__ __forceinline__ void sam_base(const DevReads &R, const RowV &v, int x
 // One wave's LDS staging area (span_cap = SPAN):
 //   c[2][SPAN], q[2][SPAN]                 both mates in reference coordinates
 //   opref[2][MH_MAXOPS+1], opread[2][...]  reference / read offset of every op
-//   ins_key/off/len[PU_MAXINS], insbuf[PU_INSBUF], n_ins
+//   n_ins
 struct UnitView {
-    char *c[2], *q[2];
-    int32_t *opref[2], *opread[2];
-    int32_t *ins_key, *ins_off, *ins_len;
-    char *insbuf;
+    char *cq;        // c of mate k at cq + 2k*span, q at cq + (2k+1)*span
+    int32_t *ops;    // opref of mate k at ops + 2k*(MH_MAXOPS+1), opread after it
+    int span;
     int32_t *n_ins;
+    __device__ char *c(int k) const { return cq + 2 * k * span; }
+    __device__ char *q(int k) const { return cq + (2 * k + 1) * span; }
+    __device__ int32_t *opref(int k) const { return ops + 2 * k * (MH_MAXOPS + 1); }
+    __device__ int32_t *opread(int k) const { return ops + (2 * k + 1) * (MH_MAXOPS + 1); }
 };
 
 __host__ __device__ inline int unit_bytes_for(int span)
 {
-    return 4 * span + 4 * 4 * (MH_MAXOPS + 1) + 3 * 4 * PU_MAXINS + PU_INSBUF + 16;
+    return 4 * span + 4 * 4 * (MH_MAXOPS + 1) + 16;
 }
 
 __device__ inline UnitView unit_view(unsigned char *base, int span)
 {
     UnitView v;
-    for (int k = 0; k < 2; ++k) {
-        v.c[k] = (char *)base + (2 * k) * span;
-        v.q[k] = (char *)base + (2 * k + 1) * span;
-    }
-    int32_t *ip = (int32_t *)(base + 4 * span);
-    v.opref[0] = ip; v.opread[0] = ip + (MH_MAXOPS + 1);
-    v.opref[1] = ip + 2 * (MH_MAXOPS + 1); v.opread[1] = ip + 3 * (MH_MAXOPS + 1);
-    ip += 4 * (MH_MAXOPS + 1);
-    v.ins_key = ip; v.ins_off = ip + PU_MAXINS; v.ins_len = ip + 2 * PU_MAXINS;
-    v.insbuf = (char *)(ip + 3 * PU_MAXINS);
-    v.n_ins = (int32_t *)(v.insbuf + PU_INSBUF);
+    v.cq = (char *)base;
+    v.span = span;
+    v.ops = (int32_t *)(base + 4 * span);
+    v.n_ins = v.ops + 4 * (MH_MAXOPS + 1);
+    return v;
+}
+
+// Merged insertions of the unit a wave is on (rare: units with I ops), in a
+// per-wave slice of global scratch: key, offset and length of each entry and
+// the merged bytes.
+constexpr int PU_INS_BYTES = 3 * 4 * PU_MAXINS + PU_INSBUF;
+struct InsView {
+    int32_t *key, *off, *len;
+    char *buf;
+};
+
+__device__ inline InsView ins_view(char *base)
+{
+    InsView v;
+    v.key = (int32_t *)base;
+    v.off = v.key + PU_MAXINS;
+    v.len = v.key + 2 * PU_MAXINS;
+    v.buf = (char *)(v.key + 3 * PU_MAXINS);
     return v;
 }
 
@@ -133,22 +149,27 @@ struct HotLds {
     long long first_unit;
 };
 
-// merge_pairs on two short strings without '-' (insertions), sam2aln.py:156-237
-__device__ int merge_ins_strings(const char *s1, const char *q1, int l1, const char *s2,
-                                 const char *q2, int l2, int q_cutoff, char *out)
+// merge_pairs on two insertions (strings without '-'), sam2aln.py:156-237:
+// s1 = bases [o1, o1 + l1) of mate w, s2 = bases [o2, o2 + l2) of mate v,
+// read from the resident reads; the shorter one plays seq1.
+__device__ int merge_ins_strings(const DevReads &R, const RowV &w, int o1, int l1, const RowV &v,
+                                 int o2, int l2, int q_cutoff, char *out)
 {
+    const RowV *r1 = &w, *r2 = &v;
     if (l1 > l2) {
-        const char *t = s1; s1 = s2; s2 = t;
-        t = q1; q1 = q2; q2 = t;
-        int x = l1; l1 = l2; l2 = x;
+        r1 = &v; r2 = &w;
+        int x = o1; o1 = o2; o2 = x;
+        x = l1; l1 = l2; l2 = x;
     }
     const unsigned char cut = (unsigned char)(q_cutoff + 33);
     for (int i = 0; i < l2; ++i) {
-        const char c2 = s2[i];
-        const unsigned char b = (unsigned char)q2[i];
+        char c2, q2c;
+        sam_base(R, *r2, o2 + i, c2, q2c);
+        const unsigned char b = (unsigned char)q2c;
         if (i < l1) {
-            const char c1 = s1[i];
-            const unsigned char a = (unsigned char)q1[i];
+            char c1, q1c;
+            sam_base(R, *r1, o1 + i, c1, q1c);
+            const unsigned char a = (unsigned char)q1c;
             if (c1 == c2) {
                 out[i] = (a > cut || b > cut) ? c1 : 'N';
             } else {
@@ -167,6 +188,15 @@ __device__ int merge_ins_strings(const char *s1, const char *q1, int l1, const c
     return l2;
 }
 
+__device__ __forceinline__ int wave_incl_scan(int v, int lane)
+{
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    return v;
+}
+
 template <int SRC>
 __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
 {
@@ -179,6 +209,7 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
     HotLds *hot = (HotLds *)(smem + (size_t)16 * WP);
     UnitView L = unit_view(smem + (size_t)16 * WP + sizeof(HotLds) + (size_t)wv * A.unit_bytes,
                            A.span_cap);
+    const InsView I = ins_view(A.ins_scratch + ((size_t)blockIdx.x * wpb + wv) * PU_INS_BYTES);
     const unsigned char cut = (unsigned char)(A.q_cutoff + 33);
     for (int x = threadIdx.x; x < 4 * WP; x += blockDim.x) win[x] = 0;
     if (threadIdx.x == 0) { hot->read_count = 0; hot->max_pos = 0; hot->first_unit = INT64_MAX; }
@@ -199,10 +230,11 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
         if (SRC == 0 && !r1.present && r2.present) { r1 = r2; r2.present = 0; }  // unpaired view
         if (!r1.present) continue;
         if (r2.present && r1.ref != r2.ref) continue;           // remap.py:96-98
-        RowV mp[2];
-        int nm = 0;
-        if (!(r1.flag & 4)) mp[nm++] = r1;
-        if (r2.present && !(r2.flag & 4)) mp[nm++] = r2;
+        // the mapped mates (merge_reads filters unmapped ones): m0, m1
+        const bool u1 = !(r1.flag & 4), u2 = r2.present && !(r2.flag & 4);
+        const int nm = (int)u1 + (int)u2;
+        const RowV m0 = u1 ? r1 : r2, m1 = r2;
+        auto mate = [&](int k) -> RowV { return k ? m1 : m0; };
         if (nm == 0) continue;                                 // remap.py:111-112
         const int ref = r1.ref;
         if (ref < 0 || ref >= A.n_refs) {
@@ -210,90 +242,111 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
             continue;
         }
 
-        // ---- apply_cigar: op offsets (lane 0), then expand lane-parallel ----
-        int pad[2], len[2], bad = 0;
-        for (int k = 0; k < nm; ++k) {
-            int rf = 0, rd = 0;
-            for (int o = 0; o < mp[k].n_cigar; ++o) {
-                const uint32_t op = mp[k].cig[o];
-                const int n = (int)(op >> 4), t = (int)(op & 15);
-                if (lane == 0 && o < MH_MAXOPS) { L.opref[k][o] = rf; L.opread[k][o] = rd; }
-                if (t == MH_OP_M) { rf += n; rd += n; }
-                else if (t == MH_OP_D) rf += n;
-                else if (t == MH_OP_I || t == MH_OP_S) rd += n;
-                else bad = 1;
-                if (rd > mp[k].m) bad = 1;
+        // ---- apply_cigar: op offsets by a lane-parallel prefix scan, then
+        // expand each mate into reference coordinates lane-parallel ----
+        int padA = 0, padB = 0, lenA = 0, lenB = 0, bad = 0, n_iops = 0;
+        auto pad = [&](int k) { return k ? padB : padA; };
+        auto len = [&](int k) { return k ? lenB : lenA; };
+        #pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (k >= nm) break;
+            const RowV mk = mate(k);
+            const int nc = mk.n_cigar;
+            if (nc > MH_MAXOPS) { bad = 1; break; }
+            int rf0 = 0, rd0 = 0;
+            for (int o0 = 0; o0 < nc; o0 += 64) {
+                const int o = o0 + lane;
+                int dref = 0, dread = 0, isd = 0, isi = 0, badop = 0;
+                if (o < nc) {
+                    const uint32_t op = mk.cig[o];
+                    const int n = (int)(op >> 4), t = (int)(op & 15);
+                    if (t == MH_OP_M) { dref = n; dread = n; }
+                    else if (t == MH_OP_D) { dref = n; isd = 1; }
+                    else if (t == MH_OP_I) { dread = n; isi = 1; }
+                    else if (t == MH_OP_S) dread = n;
+                    else badop = 1;
+                }
+                const int iref = wave_incl_scan(dref, lane), iread = wave_incl_scan(dread, lane);
+                if (o < nc) {
+                    L.opref(k)[o] = rf0 + iref - dref;
+                    L.opread(k)[o] = isd ? -1 : rd0 + iread - dread;   // -1: deletion
+                }
+                bad |= __any(badop);
+                n_iops += __popcll(__ballot(isi));
+                rf0 += __shfl(iref, 63, 64);
+                rd0 += __shfl(iread, 63, 64);
             }
-            if (lane == 0 && mp[k].n_cigar <= MH_MAXOPS) { L.opref[k][mp[k].n_cigar] = rf; L.opread[k][mp[k].n_cigar] = rd; }
-            if (rd != mp[k].m || rf > A.span_cap || mp[k].pos < 1 || mp[k].n_cigar > MH_MAXOPS) bad = 1;
-            pad[k] = mp[k].pos - 1;
-            len[k] = pad[k] + rf;
+            if (lane == 0) { L.opref(k)[nc] = rf0; L.opread(k)[nc] = rd0; }
+            if (rd0 != mk.m || rf0 > A.span_cap || mk.pos < 1) bad = 1;
+            if (k) { padB = mk.pos - 1; lenB = padB + rf0; }
+            else { padA = mk.pos - 1; lenA = padA + rf0; }
         }
         if (bad) {
             if (lane == 0) atomicExch(&A.ev_ctr[3], 1ull);
             continue;
         }
         __builtin_amdgcn_wave_barrier();
-        for (int k = 0; k < nm; ++k) {
-            const int span = len[k] - pad[k];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (k >= nm) break;
+            const int span = len(k) - pad(k);
+            const RowV mk = mate(k);
             for (int t = lane; t < span; t += 64) {
+                // the M/D op covering reference offset t (I/S ops span nothing)
                 int o = 0;
-                while (L.opref[k][o + 1] <= t ||
-                       ((mp[k].cig[o] & 15) != MH_OP_M && (mp[k].cig[o] & 15) != MH_OP_D))
-                    ++o;
-                const uint32_t op = mp[k].cig[o];
+                while (L.opref(k)[o + 1] <= t) ++o;
+                const int rd = L.opread(k)[o];
                 char c = '-', q = ' ';
-                if ((op & 15) == MH_OP_M) sam_base(A.R, mp[k], L.opread[k][o] + (t - L.opref[k][o]), c, q);
-                L.c[k][t] = c;
-                L.q[k][t] = q;
+                if (rd >= 0) sam_base(A.R, mk, rd + (t - L.opref(k)[o]), c, q);
+                L.c(k)[t] = c;
+                L.q(k)[t] = q;
             }
         }
-        // ---- merge_inserts (lane 0): keys left + pad, sam2aln.py:133-135 ----
+        // ---- merge_inserts (lane 0, only units with I ops): keys left + pad,
+        // sam2aln.py:133-135, :240-273 ----
         if (lane == 0) {
             int n = 0, used = 0;
-            // ins1 entries passing quality
-            for (int pass = 0; pass < nm; ++pass) {
-                const RowV &v = mp[pass];
+            for (int pass = 0; pass < nm && n_iops; ++pass) {
+                const RowV v = mate(pass);
                 for (int o = 0; o < v.n_cigar; ++o) {
                     if ((v.cig[o] & 15) != MH_OP_I) continue;
                     const int il = (int)(v.cig[o] >> 4);
-                    const int key = L.opread[pass][o] + pad[pass];
-                    char tc[1], tq[1];
+                    const int key = L.opread(pass)[o] + pad(pass);
+                    char tc, tq;
                     unsigned char mn = 255;
                     for (int x = 0; x < il; ++x) {
-                        sam_base(A.R, v, L.opread[pass][o] + x, tc[0], tq[0]);
-                        if ((unsigned char)tq[0] < mn) mn = (unsigned char)tq[0];
+                        sam_base(A.R, v, L.opread(pass)[o] + x, tc, tq);
+                        if ((unsigned char)tq < mn) mn = (unsigned char)tq;
                     }
                     if (!(mn > cut)) continue;
                     if (used + 2 * il + 2 > PU_INSBUF) { atomicExch(&A.ev_ctr[3], 1ull); continue; }
                     // locate an existing entry with the same key (ins1 vs ins2)
                     int at = -1;
-                    for (int z = 0; z < n; ++z) if (L.ins_key[z] == key) at = z;
-                    char *dst = L.insbuf + used;
+                    for (int z = 0; z < n; ++z) if (I.key[z] == key) at = z;
+                    char *dst = I.buf + used;
                     int outlen;
                     if (pass == 0) {
-                        for (int x = 0; x < il; ++x) sam_base(A.R, v, L.opread[pass][o] + x, dst[x], tc[0]);
+                        for (int x = 0; x < il; ++x) sam_base(A.R, v, L.opread(pass)[o] + x, dst[x], tc);
                         outlen = il;
                     } else {
                         // ins1 at this key (even if it failed quality) merges with ins2
-                        char s1[PU_INSBUF / 8], q1[PU_INSBUF / 8], s2[PU_INSBUF / 8], q2[PU_INSBUF / 8];
-                        int l1 = 0;
-                        const RowV &w = mp[0];
+                        int l1 = 0, o1s = 0;
+                        const RowV &w = m0;
                         for (int o1 = 0; o1 < w.n_cigar; ++o1) {
                             if ((w.cig[o1] & 15) != MH_OP_I) continue;
-                            if (L.opread[0][o1] + pad[0] != key) continue;
+                            if (L.opread(0)[o1] + padA != key) continue;
                             l1 = (int)(w.cig[o1] >> 4);
                             if (l1 > PU_INSBUF / 8) l1 = PU_INSBUF / 8;
-                            for (int x = 0; x < l1; ++x) sam_base(A.R, w, L.opread[0][o1] + x, s1[x], q1[x]);
+                            o1s = L.opread(0)[o1];
                         }
                         const int l2 = il > PU_INSBUF / 8 ? PU_INSBUF / 8 : il;
-                        for (int x = 0; x < l2; ++x) sam_base(A.R, v, L.opread[pass][o] + x, s2[x], q2[x]);
-                        outlen = merge_ins_strings(s1, q1, l1, s2, q2, l2, A.q_cutoff, dst);
+                        outlen = merge_ins_strings(A.R, w, o1s, l1, v, L.opread(pass)[o], l2,
+                                                   A.q_cutoff, dst);
                     }
                     if (at < 0) at = n++;
-                    L.ins_key[at] = key;
-                    L.ins_off[at] = used;
-                    L.ins_len[at] = outlen;
+                    I.key[at] = key;
+                    I.off[at] = used;
+                    I.len[at] = outlen;
                     used += outlen;
                 }
             }
@@ -308,17 +361,17 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
         if (nm == 1) {
             a = -1; b = 0;
             len1 = 0; pad1 = 0;
-        } else if (len[0] > len[1]) {
+        } else if (lenA > lenB) {
             a = 1; b = 0;
         }
-        if (a >= 0) { len1 = len[a]; pad1 = pad[a]; }
-        len2 = len[b];
-        pad2 = pad[b];
+        if (a >= 0) { len1 = len(a); pad1 = pad(a); }
+        len2 = len(b);
+        pad2 = pad(b);
         auto ch1 = [&](int i, char &c, char &q) {
-            if (i < pad1) { c = '-'; q = '!'; } else { c = L.c[a][i - pad1]; q = L.q[a][i - pad1]; }
+            if (i < pad1) { c = '-'; q = '!'; } else { c = L.c(a)[i - pad1]; q = L.q(a)[i - pad1]; }
         };
         auto ch2 = [&](int i, char &c, char &q) {
-            if (i < pad2) { c = '-'; q = '!'; } else { c = L.c[b][i - pad2]; q = L.q[b][i - pad2]; }
+            if (i < pad2) { c = '-'; q = '!'; } else { c = L.c(b)[i - pad2]; q = L.q(b)[i - pad2]; }
         };
         const int lo = a >= 0 ? (pad1 < pad2 ? pad1 : pad2) : pad2;
         // first index where seq2 is not '-' (is_reverse_started) and where the
@@ -395,9 +448,9 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
             if (mc == '-') { A.dflag[cell] = 1; continue; }
             int hit = -1;
             for (int z = 0; z < n_ins; ++z)
-                if (L.ins_key[z] == P) hit = z;
-            if (hit >= 0 && L.ins_len[hit] > 0 && L.ins_len[hit] % 3 == 0) {
-                const int tl = 1 + L.ins_len[hit];
+                if (I.key[z] == P) hit = z;
+            if (hit >= 0 && I.len[hit] > 0 && I.len[hit] % 3 == 0) {
+                const int tl = 1 + I.len[hit];
                 const unsigned long long e = atomicAdd(&A.ev_ctr[0], 1ull);
                 const unsigned long long p = atomicAdd(&A.ev_ctr[1], (unsigned long long)tl);
                 if ((long long)e < A.ev_cap && (long long)(p + tl) <= A.pool_cap) {
@@ -406,7 +459,7 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
                     A.ev[4 * e + 2] = (int32_t)p;
                     A.ev[4 * e + 3] = tl;
                     A.ev_pool[p] = mc;
-                    for (int x = 0; x < tl - 1; ++x) A.ev_pool[p + 1 + x] = L.insbuf[L.ins_off[hit] + x];
+                    for (int x = 0; x < tl - 1; ++x) A.ev_pool[p + 1 + x] = I.buf[I.off[hit] + x];
                 } else {
                     atomicExch(&A.ev_ctr[2], 1ull);
                 }
@@ -561,6 +614,15 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
     hipStream_t s = c.stream;
     PileGeometry geo;
     if (int st = pile_geometry(c, source, n_units, geo)) return st;
+    {
+        const int64_t need = geo.blocks * geo.wpb * (int64_t)PU_INS_BYTES;
+        if (P.ins_scratch_bytes < need) {
+            hipFree(P.ins_scratch);
+            P.ins_scratch = nullptr;
+            MH_HIP(hipMalloc(&P.ins_scratch, need));
+            P.ins_scratch_bytes = need;
+        }
+    }
     const int64_t cells = (int64_t)P.n_refs * P.cap;
     for (int attempt = 0; attempt < 3; ++attempt) {
         MH_HIP(hipMemsetAsync(P.dense, 0, sizeof(int32_t) * 4 * (cells > 0 ? cells : 1), s));
@@ -591,6 +653,7 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
         A.win_pos = geo.win_pos;
         A.span_cap = geo.span;
         A.unit_bytes = geo.unit_bytes;
+        A.ins_scratch = P.ins_scratch;
         if (n_units > 0) {
             const int pk = prof_begin(c, "k_pileup");
             if (source == 0) {
