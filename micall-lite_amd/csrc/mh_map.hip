@@ -372,6 +372,16 @@ __device__ __forceinline__ int mm_pen(int qchar)
 // edges acts as minus infinity.  The moves then fold into the ALU op that uses
 // them (v_max_i32_dpp, v_add_u32_dpp) instead of costing a mov + a fill each.
 constexpr int BIAS = 1 << 20;
+#ifndef MH_DP_WPB
+#define MH_DP_WPB 4          // waves per k_dp workgroup (4 measured best)
+#endif
+#ifndef MH_DP_PREFETCH
+#define MH_DP_PREFETCH 0     // load the next 8-row group's LDS operands early
+#endif
+static_assert(MH_DP_WPB >= 1 && MH_DP_WPB <= 4, "k_dp is compiled for <= 256 threads");
+// CIGAR runs kept by the traceback.  A path with more runs cannot end up
+// with <= MH_MAXOPS - 1 ops: overhang trimming removes at most ~2 x 64 runs.
+constexpr int RUNS_CAP = 256;
 // CIGAR ops are reserved per wave in chunks (one atomic per chunk, not per
 // extension); the pool is sized for every resident wave's partial chunk.
 constexpr int POOL_CHUNK = 256;
@@ -463,8 +473,10 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     unsigned char *wbase = smem + (size_t)wv * A.wave_lds;
     uint32_t *bits = (uint32_t *)wbase;                       // rows_pad/8 * 64: 4 bits/cell
     uint32_t *tab = bits + (A.rows_pad >> 3) * 64;            // rows_pad: score nibbles per row
-    uint32_t *runs = tab + A.rows_pad;                        // rows_pad + 128: CIGAR runs (reversed)
-    uint8_t *refw = (uint8_t *)(runs + A.rows_pad + 128);     // rows_pad + 64: ref code * 4
+    uint32_t *runs = tab;                                     // RUNS_CAP: CIGAR runs (reversed),
+                                                              // written after the DP is done with tab
+    uint8_t *refw = (uint8_t *)(runs + (A.rows_pad > RUNS_CAP ? A.rows_pad : RUNS_CAP));
+                                                              // rows_pad + 64: ref code * 4
     uint8_t *rdc = refw + A.rows_pad + 64;                    // rows_pad: read codes
     uint8_t *rowk = rdc + A.rows_pad;                         // rows_pad: lane of the M cell, 255 none
     const int ma = LOCAL ? 2 : 0;
@@ -489,42 +501,82 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         const int d0 = cd.center - HALF;
         const int strand = cd.strand;
 
-        // ---- stage per-row score tables, read codes and the ref window ----
-        for (int i = lane; i < A.rows_pad; i += 64) {
-            uint32_t tb = 0x88888u, c = 4;
-            if (i < m) {
-                const int b = strand ? m - 1 - i : i;
-                c = read_code(A.R, roff, b);
-                if (strand && c < 4) c = 3 - c;
-                const int pen = mm_pen(A.R.qual[roff + b]);
-                tb = 0;
-                for (int g = 0; g < 5; ++g) {
-                    const int sc = (c > 3 || g > 3) ? -NPEN : (c == (uint32_t)g ? ma : -pen);
-                    tb |= (uint32_t)(sc + 8) << (4 * g);
-                }
+        // ---- stage per-row score tables, read codes and the ref window:
+        // every load of a round is issued before any is used ----
+        for (int i0 = 0; i0 < A.rows_pad; i0 += 64 * 4) {
+            uint32_t nmw[4], sqw[4], qv[4];
+            int bb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + 64 * u + lane;
+                const int b = i < m ? (strand ? m - 1 - i : i) : 0;
+                const int64_t g = roff + b;
+                bb[u] = (int)(g & 31);
+                nmw[u] = A.R.nmask[g >> 5];
+                sqw[u] = A.R.seq2[g >> 4] >> (2 * (g & 15));
+                qv[u] = A.R.qual[g];
             }
-            tab[i] = tb;
-            rdc[i] = (uint8_t)c;
-            rowk[i] = 255;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + 64 * u + lane;
+                if (i >= A.rows_pad) break;
+                uint32_t tb = 0x88888u, c = 4;
+                if (i < m) {
+                    c = ((nmw[u] >> bb[u]) & 1) ? 4u : (sqw[u] & 3u);
+                    if (strand && c < 4) c = 3 - c;
+                    const int pen = mm_pen((int)qv[u]);
+                    tb = 0;
+                    for (int g = 0; g < 5; ++g) {
+                        const int sc = (c > 3 || g > 3) ? -NPEN : (c == (uint32_t)g ? ma : -pen);
+                        tb |= (uint32_t)(sc + 8) << (4 * g);
+                    }
+                }
+                tab[i] = tb;
+                rdc[i] = (uint8_t)c;
+                rowk[i] = 255;
+            }
         }
-        for (int x = lane; x < A.rows_pad + 64; x += 64) {
-            const int j = d0 + x;
-            const int g = (j >= 0 && j < reflen) ? A.I.codes[gref + j] : 4;
-            refw[x] = (uint8_t)(g * 4);
+        for (int x0 = 0; x0 < A.rows_pad + 64; x0 += 64 * 5) {
+            uint32_t gv[5];
+#pragma unroll
+            for (int u = 0; u < 5; ++u) {
+                const int j = d0 + x0 + 64 * u + lane;
+                gv[u] = (j >= 0 && j < reflen) ? A.I.codes[gref + j] : 4u;
+            }
+#pragma unroll
+            for (int u = 0; u < 5; ++u) {
+                const int x = x0 + 64 * u + lane;
+                if (x < A.rows_pad + 64) refw[x] = (uint8_t)(gv[u] * 4);
+            }
         }
         wave_sync();
 
         // ---- DP over rows, 8 rows per group (one u32 of traceback bits per
-        // lane); groups wholly inside the gap window run branch-free ----
+        // lane); groups wholly inside the gap window run branch-free; the next
+        // group's LDS operands are loaded while this group computes ----
         int Hp = BIAS, Ep = 0;
         uint32_t bestKey = 0;
+        uint32_t tbn[8];
+        int rcn[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            tbn[t] = tab[t];
+            rcn[t] = refw[t + lane];
+        }
         for (int i0 = 0; i0 < m; i0 += 8) {
             uint32_t tbv[8];
             int rcv[8];
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                tbv[t] = tab[i0 + t];
-                rcv[t] = refw[i0 + t + lane];
+                tbv[t] = MH_DP_PREFETCH ? tbn[t] : tab[i0 + t];
+                rcv[t] = MH_DP_PREFETCH ? rcn[t] : refw[i0 + t + lane];
+            }
+            if (MH_DP_PREFETCH && i0 + 8 < m) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    tbn[t] = tab[i0 + 8 + t];
+                    rcn[t] = refw[i0 + 8 + t + lane];
+                }
             }
             uint32_t acc = 0;
             if (i0 >= GBAR && i0 + 8 <= m - GBAR) {
@@ -581,7 +633,10 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                     // eight diagonal moves on this lane: one M step of 8 rows
                     if (rop == MH_OP_M) rlen += 8;
                     else {
-                        if (rlen) runs[nrun++] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                        if (rlen) {
+                            if (nrun >= RUNS_CAP - 1) { ok = 0; break; }
+                            runs[nrun++] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                        }
                         rop = MH_OP_M;
                         rlen = 8;
                     }
@@ -603,7 +658,10 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                 }
                 if (op == rop) ++rlen;
                 else {
-                    if (rlen) runs[nrun++] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                    if (rlen) {
+                        if (nrun >= RUNS_CAP - 1) { ok = 0; break; }
+                        runs[nrun++] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                    }
                     rop = op;
                     rlen = 1;
                 }
@@ -1115,16 +1173,20 @@ int run_map(Ctx &c, const mh_params &par)
         MH_HIP(hipGetLastError());
 
         const int rows_pad = ((c.reads.max_len + 7) / 8) * 8;
-        const int wave_lds = ((rows_pad * 43 + 4 * 128 + 64) + 15) & ~15;
+        // bits 32/row, tab|runs 4 * max(rows, RUNS_CAP), refw rows + 64, rdc, rowk
+        const int wave_lds =
+            ((rows_pad * 35 + 4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP) + 64) + 15) & ~15;
         for (int attempt = 0; attempt < 2; ++attempt) {
             MH_HIP(hipMemsetAsync(M.counters + 1, 0, sizeof(int32_t) * 2, s));
             DpArgs da{c.reads, c.index, c.len_tab, M.cand, M.work, M.counters, M.slot, M.pool,
                       M.counters + 1, M.pool_cap, rows_pad, wave_lds,
                       par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext,
                       par.rdg_ext};
-            int wpb = (160 * 1024) / wave_lds;
-            if (wpb > 4) wpb = 4;
-            if (wpb < 1) { set_error("mh_map: reads too long for LDS"); return -3; }
+            // one wave per workgroup: the CU then packs floor(160 KiB / wave_lds)
+            // waves (15 at 251-nt reads) with no workgroup rounding loss
+            int wpb = MH_DP_WPB;
+            while (wpb > 1 && wpb * wave_lds > 160 * 1024) --wpb;
+            if (wave_lds > 160 * 1024) { set_error("mh_map: reads too long for LDS"); return -3; }
             int64_t dblocks = (n * 2 + wpb - 1) / wpb;
             if (dblocks > DP_MAX_BLOCKS) dblocks = DP_MAX_BLOCKS;
             const int pd = prof_begin(c, "k_dp");
