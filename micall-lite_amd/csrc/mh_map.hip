@@ -402,8 +402,15 @@ __device__ __forceinline__ int scan_max(int x)
     x = imax(x, dppz<DPP_ROW_SHR2>(x));
     x = imax(x, dppz<DPP_ROW_SHR4>(x));
     x = imax(x, dppz<DPP_ROW_SHR8>(x));
-    x = imax(x, __builtin_amdgcn_update_dpp(x, x, DPP_ROW_BCAST15, 0xA, 0xF, false));
-    x = imax(x, __builtin_amdgcn_update_dpp(x, x, DPP_ROW_BCAST31, 0xC, 0xF, false));
+    // cross-row steps in place: rows a step does not write keep x (measured on
+    // gfx950 with profiles/diag/dpp_probe.hip); the hazard nops of the
+    // VALU-write -> DPP-read pairs are inside the string
+    asm volatile("s_nop 1\n\t"
+                 "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+                 "s_nop 1\n\t"
+                 "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+                 "s_nop 1"
+                 : "+v"(x));
     return x;
 }
 
