@@ -415,9 +415,19 @@ __device__ __forceinline__ int scan_max(int x)
 }
 
 struct DpConst {
-    int exI, oeI, cE;   // cE = exI - oeI
+    int mexI, moeI;     // -exI, -oeI in VGPRs (operands of fused DPP adds)
     int xD, cF;         // per lane: exD * lane, -(oeD - exD) - exD * lane
+    int eight;          // 8 in a VGPR (operand of a fused DPP and)
 };
+
+// a wave-uniform value the compiler must keep in a VGPR: VOP2 DPP forms take
+// their second operand from a VGPR only
+__device__ __forceinline__ int in_vgpr(int v)
+{
+    int r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(v));
+    return r;
+}
 
 // One DP row inside the gap window (oracle dp_extend, og_mapper.c:283-322):
 // returns the 4 traceback bits of this lane's cell.
@@ -426,18 +436,20 @@ __device__ __forceinline__ uint32_t dp_row_gap(uint32_t tbv, int rc, int &Hp, in
                                                uint32_t &bestKey, int ci, const DpConst &K)
 {
     const int Hd = Hp + (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4) - 8;
-    // vertical (insertion) move from lane k+1 of the previous row
-    const int Es = imax(Ep - K.exI, Hp - K.oeI);
-    const int E = dppz<DPP_WAVE_SHL1>(Es);
-    const uint32_t eb = (uint32_t)(K.cE - dppz<DPP_WAVE_SHL1>(Ep - Hp)) >> 31;
+    // vertical (insertion) move from lane k+1 of the previous row; eb4 = 4
+    // when extending beats opening (ties open)
+    const int e1 = dppz<DPP_WAVE_SHL1>(Ep) + K.mexI;
+    const int h1 = dppz<DPP_WAVE_SHL1>(Hp) + K.moeI;
+    const int E = imax(e1, h1);
+    const uint32_t eb4 = (uint32_t)((h1 - e1) >> 31) & 4u;
     int H1 = imax(Hd, E);
     if (LOCAL) H1 = imax(H1, BIAS);
     // horizontal (deletion) moves: prefix max of X = H1 + exD * lane
     const int X = H1 + K.xD;
     const int P = scan_max(X);
-    const uint32_t gt = (uint32_t)(X - P) >> 31;
+    const int gtm = (X - P) >> 31;              // -1 where the left lane's F extends
     const int F = dppz<DPP_WAVE_SHR1>(P) + K.cF;
-    const uint32_t fb = (uint32_t)dppz<DPP_WAVE_SHR1>((int)gt);
+    const uint32_t fb8 = (uint32_t)(dppz<DPP_WAVE_SHR1>(gtm) & K.eight);
     const int H = imax(H1, F);
     // src: 1 diagonal, 2 from E, 3 from F (priority in that order); 0 local stop
     const uint32_t a = umin1(H - Hd), b = umin1(H - E);
@@ -449,7 +461,7 @@ __device__ __forceinline__ uint32_t dp_row_gap(uint32_t tbv, int rc, int &Hp, in
     }
     Hp = H;
     Ep = E;
-    return src | (eb << 2) | (fb << 3);
+    return src | eb4 | fb8;
 }
 
 // A row outside the gap window (first / last GBAR rows): no E, no F.
@@ -489,9 +501,9 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     const int ma = LOCAL ? 2 : 0;
     const int n_work = A.counters[0];
     DpConst K;
-    K.exI = A.exI;
-    K.oeI = A.oeI;
-    K.cE = A.exI - A.oeI;
+    K.mexI = in_vgpr(-A.exI);
+    K.moeI = in_vgpr(-A.oeI);
+    K.eight = in_vgpr(8);
     K.xD = lane * A.exD;
     K.cF = -(A.oeD - A.exD) - A.exD * lane;
 
