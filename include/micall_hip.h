@@ -158,6 +158,10 @@ int mh_pileup_dims(mh_ctx *ctx, int *n_refs, int32_t *cap, int64_t *n_events,
                    int64_t *event_bytes);
 int mh_pileup_fetch(mh_ctx *ctx, int32_t *dense, uint8_t *nflag, uint8_t *dflag,
                     int64_t *read_counts, int64_t *first_unit, int32_t *max_pos);
+/* The dense / nflag / dflag rows of one reference (cap positions each):
+ * fetching only the references that received pairs keeps a pileup over many
+ * seeds from copying every seed's counters. */
+int mh_pileup_fetch_ref(mh_ctx *ctx, int ref, int32_t *dense, uint8_t *nflag, uint8_t *dflag);
 /* Sparse tokens (base + insertion with len % 3 == 0), aggregated over the
  * pileup: n_events (mh_pileup_dims) distinct (ref, pos, token) entries in
  * (ref, pos, token) order, each with the number of merged pairs that voted

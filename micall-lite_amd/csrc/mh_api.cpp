@@ -1186,6 +1186,21 @@ int mh_pileup_fetch(mh_ctx *ctx, int32_t *dense, uint8_t *nflag, uint8_t *dflag,
     return 0;
 }
 
+int mh_pileup_fetch_ref(mh_ctx *ctx, int ref, int32_t *dense, uint8_t *nflag, uint8_t *dflag)
+{
+    if (!ctx) return -3;
+    CtxEx *c = X(ctx);
+    PileState &P = c->pile;
+    if (!P.dense) { set_error("no pileup (call mh_pileup)"); return -3; }
+    if (ref < 0 || ref >= P.n_refs) { set_error("mh_pileup_fetch_ref: ref %d out of range", ref); return -3; }
+    MH_HIP(hipSetDevice(c->device));
+    const int64_t base = (int64_t)ref * P.cap;
+    if (dense) MH_HIP(hipMemcpy(dense, P.dense + 4 * base, sizeof(int32_t) * 4 * P.cap, hipMemcpyDeviceToHost));
+    if (nflag) MH_HIP(hipMemcpy(nflag, P.nflag + base, P.cap, hipMemcpyDeviceToHost));
+    if (dflag) MH_HIP(hipMemcpy(dflag, P.dflag + base, P.cap, hipMemcpyDeviceToHost));
+    return 0;
+}
+
 int mh_pileup_events(mh_ctx *ctx, int32_t *ref, int32_t *pos, int32_t *tok_off, int32_t *tok_len,
                      int64_t *count, char *pool)
 {

@@ -82,6 +82,7 @@ def _declare(L):
         'mh_pileup': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),
         'mh_pileup_dims': ([_P, ctypes.POINTER(ctypes.c_int), _I32P, _I64P, _I64P], ctypes.c_int),
         'mh_pileup_fetch': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+        'mh_pileup_fetch_ref': ([_P, ctypes.c_int, _P, _P, _P], ctypes.c_int),
         'mh_pileup_events': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
         'mh_pileup_packed_bytes': ([_P, _I64P, _I64P], ctypes.c_int),
         'mh_pileup_export': ([_P, _P, _P], ctypes.c_int),
@@ -345,8 +346,14 @@ class Context:
         rc = np.zeros(max(n, 1), dtype=np.int64)
         fu = np.zeros(max(n, 1), dtype=np.int64)
         mp = np.zeros(max(n, 1), dtype=np.int32)
-        check(lib().mh_pileup_fetch(self.h, _ptr(dense), _ptr(nflag), _ptr(dflag), _ptr(rc),
-                                    _ptr(fu), _ptr(mp)), 'mh_pileup_fetch')
+        # scalars first; then the counter rows of the references that received
+        # pairs (np.zeros leaves the other rows as untouched zero pages)
+        check(lib().mh_pileup_fetch(self.h, None, None, None, _ptr(rc), _ptr(fu), _ptr(mp)),
+              'mh_pileup_fetch')
+        for r in range(n):
+            if fu[r] >= 0 or mp[r] > 0:
+                check(lib().mh_pileup_fetch_ref(self.h, r, _ptr(dense[r]), _ptr(nflag[r]),
+                                                _ptr(dflag[r])), 'mh_pileup_fetch_ref')
         eref = np.zeros(max(ne, 1), dtype=np.int32)
         epos = np.zeros(max(ne, 1), dtype=np.int32)
         eoff = np.zeros(max(ne, 1), dtype=np.int32)
