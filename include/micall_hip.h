@@ -168,17 +168,22 @@ int mh_pileup_fetch_ref(mh_ctx *ctx, int ref, int32_t *dense, uint8_t *nflag, ui
  * for it; the token is pool[tok_off[e] .. tok_off[e] + tok_len[e]). */
 int mh_pileup_events(mh_ctx *ctx, int32_t *ref, int32_t *pos, int32_t *tok_off,
                      int32_t *tok_len, int64_t *count, char *pool);
-/* Multi-GPU: copy the device counters to / from a caller-owned device
- * buffer of `bytes` (>= mh_pileup_packed_bytes) so the caller can all-reduce
- * them with RCCL (int32 sum; flags are 0/1 and are OR-ed by max-reduce of
- * the second segment).  Layout: [dense | read_counts(int32)] summed, then
- * [nflag|dflag as int32 | max_pos | -first_unit] max-reduced. */
-int mh_pileup_packed_bytes(mh_ctx *ctx, int64_t *sum_bytes, int64_t *max_bytes);
-int mh_pileup_export(mh_ctx *ctx, void *dev_sum, void *dev_max);
-/* as mh_pileup_export, with this rank's first unit index added to
- * first_unit so the max-reduce yields the global refmap order */
-int mh_pileup_export_base(mh_ctx *ctx, int64_t unit_base, void *dev_sum, void *dev_max);
-int mh_pileup_import(mh_ctx *ctx, const void *dev_sum, const void *dev_max);
+/* Multi-GPU: the caller all-reduces three device buffers with RCCL after
+ * mh_pileup_export and hands them to mh_pileup_import.  Only the rows of the
+ * n_sel references in sel (the same list on every rank: those with data on
+ * any rank) travel:
+ *   sum   int32, SUM: dense rows of sel, then read_counts of every ref
+ *   max   int32, MAX: max_pos of every ref, then -(first_unit + unit_base)
+ *         (unit_base = this rank's first unit index: the MAX yields the
+ *         global first unit, i.e. the reference's refmap order)
+ *   flags uint8, MAX: nflag rows, then dflag rows of sel (0/1: MAX = OR)
+ * mh_pileup_exchange_bytes gives the three sizes. */
+int mh_pileup_exchange_bytes(mh_ctx *ctx, int n_sel, int64_t *sum_bytes, int64_t *max_bytes,
+                             int64_t *flag_bytes);
+int mh_pileup_export(mh_ctx *ctx, int n_sel, const int32_t *sel, int64_t unit_base,
+                     void *dev_sum, void *dev_max, void *dev_flags);
+int mh_pileup_import(mh_ctx *ctx, int n_sel, const int32_t *sel, const void *dev_sum,
+                     const void *dev_max, const void *dev_flags);
 
 /* ---- Gotoh: replaces _gotoh2.align (_gotoh2.c:544-607) ---------------- */
 /* seq1/seq2 already cleaned (gotoh2.py:70-72).  out1/out2 need

@@ -458,6 +458,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipFree(P.first_unit); hipFree(P.max_pos); hipFree(P.ev); hipFree(P.ev_pool);
     hipFree(P.ev_counters);
     hipFree(P.ins_scratch);
+    hipFree(P.sel);
     hipFree(c->len_tab);
     hipStreamDestroy(c->stream);
     delete c;

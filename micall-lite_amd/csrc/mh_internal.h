@@ -141,6 +141,8 @@ struct PileState {
     int alloc_refs = 0;
     int64_t gen = 0;                // bumped by every mh_pileup / mh_pileup_import
     std::vector<int32_t> ref_lens;  // host copy (sizes the LDS window)
+    int32_t *sel = nullptr;         // references of a multi-GPU exchange
+    int sel_cap = 0;
     char *ins_scratch = nullptr;    // per-wave merged-insertion scratch of k_pileup
     int64_t ins_scratch_bytes = 0;
 };

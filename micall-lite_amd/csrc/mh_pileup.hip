@@ -683,42 +683,60 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
 }
 
 // ---- multi-GPU exchange layout ---------------------------------------------
+// Multi-GPU exchange of the references selected on every rank (those with
+// data anywhere): blockIdx.y = position in sel.  Buffers:
+//   sum   int32: dense rows of the selected refs, then read_counts of all refs
+//   mx    int32: max_pos of all refs, then -(first_unit + unit_base)
+//   flags uint8: nflag rows, then dflag rows of the selected refs (MAX = OR)
 __global__ void k_pile_export(const int32_t *dense, const uint8_t *nflag, const uint8_t *dflag,
                               const int64_t *read_counts, const int64_t *first_unit,
-                              const int32_t *max_pos, int64_t cells, int n_refs, int64_t unit_base,
-                              int32_t *sum, int32_t *mx)
+                              const int32_t *max_pos, int32_t cap, int n_refs, const int32_t *sel,
+                              int n_sel, int64_t unit_base, int32_t *sum, int32_t *mx,
+                              uint8_t *flags)
 {
+    const int sidx = blockIdx.y;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 4 * cells; i += stride)
-        sum[i] = dense[i];
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_refs; i += stride)
-        sum[4 * cells + i] = (int32_t)read_counts[i];
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += stride) {
-        mx[i] = nflag[i];
-        mx[cells + i] = dflag[i];
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sidx < n_sel) {
+        const int64_t src = (int64_t)sel[sidx] * cap, dst = (int64_t)sidx * cap;
+        for (int64_t i = t0; i < 4 * (int64_t)cap; i += stride) sum[4 * dst + i] = dense[4 * src + i];
+        for (int64_t i = t0; i < cap; i += stride) {
+            flags[dst + i] = nflag[src + i];
+            flags[(int64_t)n_sel * cap + dst + i] = dflag[src + i];
+        }
     }
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_refs; i += stride) {
-        mx[2 * cells + i] = max_pos[i];
-        mx[2 * cells + n_refs + i] = first_unit[i] < 0 ? INT32_MIN : (int32_t)(-(first_unit[i] + unit_base));
+    if (sidx == 0) {
+        for (int64_t i = t0; i < n_refs; i += stride) {
+            sum[4 * (int64_t)n_sel * cap + i] = (int32_t)read_counts[i];
+            mx[i] = max_pos[i];
+            mx[n_refs + i] = first_unit[i] < 0 ? INT32_MIN : (int32_t)(-(first_unit[i] + unit_base));
+        }
     }
 }
 
 __global__ void k_pile_import(int32_t *dense, uint8_t *nflag, uint8_t *dflag, int64_t *read_counts,
-                              int64_t *first_unit, int32_t *max_pos, int64_t cells, int n_refs,
-                              const int32_t *sum, const int32_t *mx)
+                              int64_t *first_unit, int32_t *max_pos, int32_t cap, int n_refs,
+                              const int32_t *sel, int n_sel, const int32_t *sum, const int32_t *mx,
+                              const uint8_t *flags)
 {
+    const int sidx = blockIdx.y;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 4 * cells; i += stride)
-        dense[i] = sum[i];
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_refs; i += stride) {
-        read_counts[i] = sum[4 * cells + i];
-        max_pos[i] = mx[2 * cells + i];
-        const int32_t f = mx[2 * cells + n_refs + i];
-        first_unit[i] = f == INT32_MIN ? -1 : -(int64_t)f;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sidx < n_sel) {
+        const int64_t dst = (int64_t)sel[sidx] * cap, src = (int64_t)sidx * cap;
+        for (int64_t i = t0; i < 4 * (int64_t)cap; i += stride) dense[4 * dst + i] = sum[4 * src + i];
+        for (int64_t i = t0; i < cap; i += stride) {
+            nflag[dst + i] = flags[src + i] ? 1 : 0;
+            dflag[dst + i] = flags[(int64_t)n_sel * cap + src + i] ? 1 : 0;
+        }
     }
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += stride) {
-        nflag[i] = (uint8_t)mx[i];
-        dflag[i] = (uint8_t)mx[cells + i];
+    if (sidx == 0) {
+        for (int64_t i = t0; i < n_refs; i += stride) {
+            read_counts[i] = sum[4 * (int64_t)n_sel * cap + i];
+            max_pos[i] = mx[i];
+            const int32_t f = mx[n_refs + i];
+            first_unit[i] = f == INT32_MIN ? -1 : -(int64_t)f;
+        }
     }
 }
 
@@ -726,48 +744,67 @@ __global__ void k_pile_import(int32_t *dense, uint8_t *nflag, uint8_t *dflag, in
 
 using namespace mh;
 
-extern "C" int mh_pileup_packed_bytes(mh_ctx *ctx, int64_t *sum_bytes, int64_t *max_bytes)
+extern "C" int mh_pileup_exchange_bytes(mh_ctx *ctx, int n_sel, int64_t *sum_bytes,
+                                        int64_t *max_bytes, int64_t *flag_bytes)
 {
-    if (!ctx) return -3;
+    if (!ctx || n_sel < 0) return -3;
     Ctx &c = *reinterpret_cast<Ctx *>(ctx);
-    const int64_t cells = (int64_t)c.pile.n_refs * c.pile.cap;
+    const int64_t cells = (int64_t)n_sel * c.pile.cap;
     if (sum_bytes) *sum_bytes = sizeof(int32_t) * (4 * cells + c.pile.n_refs);
-    if (max_bytes) *max_bytes = sizeof(int32_t) * (2 * cells + 2 * c.pile.n_refs);
+    if (max_bytes) *max_bytes = sizeof(int32_t) * 2 * c.pile.n_refs;
+    if (flag_bytes) *flag_bytes = 2 * cells;
     return 0;
 }
 
-extern "C" int mh_pileup_export_base(mh_ctx *ctx, int64_t unit_base, void *dev_sum, void *dev_max)
+static int upload_sel(Ctx &c, int n_sel, const int32_t *sel, int32_t **dsel)
 {
-    if (!ctx || !dev_sum || !dev_max) return -3;
+    PileState &P = c.pile;
+    for (int i = 0; i < n_sel; ++i)
+        if (sel[i] < 0 || sel[i] >= P.n_refs) { set_error("pileup exchange: ref %d out of range", sel[i]); return -3; }
+    if (P.sel_cap < n_sel || !P.sel) {
+        hipFree(P.sel);
+        P.sel = nullptr;
+        P.sel_cap = n_sel > 64 ? n_sel : 64;
+        MH_HIP(hipMalloc(&P.sel, sizeof(int32_t) * P.sel_cap));
+    }
+    if (n_sel) MH_HIP(hipMemcpy(P.sel, sel, sizeof(int32_t) * n_sel, hipMemcpyHostToDevice));
+    *dsel = P.sel;
+    return 0;
+}
+
+extern "C" int mh_pileup_export(mh_ctx *ctx, int n_sel, const int32_t *sel, int64_t unit_base,
+                                void *dev_sum, void *dev_max, void *dev_flags)
+{
+    if (!ctx || !dev_sum || !dev_max || (n_sel > 0 && (!sel || !dev_flags))) return -3;
     Ctx &c = *reinterpret_cast<Ctx *>(ctx);
     PileState &P = c.pile;
     if (!P.dense) { set_error("no pileup to export"); return -3; }
     MH_HIP(hipSetDevice(c.device));
-    const int64_t cells = (int64_t)P.n_refs * P.cap;
-    hipLaunchKernelGGL(k_pile_export, dim3(1024), dim3(256), 0, c.stream, P.dense, P.nflag, P.dflag,
-                       P.read_counts, P.first_unit, P.max_pos, cells, P.n_refs, unit_base,
-                       (int32_t *)dev_sum, (int32_t *)dev_max);
+    int32_t *dsel = nullptr;
+    if (int st = upload_sel(c, n_sel, sel, &dsel)) return st;
+    hipLaunchKernelGGL(k_pile_export, dim3(64, n_sel > 0 ? n_sel : 1), dim3(256), 0, c.stream,
+                       P.dense, P.nflag, P.dflag, P.read_counts, P.first_unit, P.max_pos, P.cap,
+                       P.n_refs, n_sel > 0 ? dsel : nullptr, n_sel, unit_base, (int32_t *)dev_sum,
+                       (int32_t *)dev_max, (uint8_t *)dev_flags);
     MH_HIP(hipGetLastError());
     MH_HIP(hipStreamSynchronize(c.stream));
     return 0;
 }
 
-extern "C" int mh_pileup_export(mh_ctx *ctx, void *dev_sum, void *dev_max)
+extern "C" int mh_pileup_import(mh_ctx *ctx, int n_sel, const int32_t *sel, const void *dev_sum,
+                                const void *dev_max, const void *dev_flags)
 {
-    return mh_pileup_export_base(ctx, 0, dev_sum, dev_max);
-}
-
-extern "C" int mh_pileup_import(mh_ctx *ctx, const void *dev_sum, const void *dev_max)
-{
-    if (!ctx || !dev_sum || !dev_max) return -3;
+    if (!ctx || !dev_sum || !dev_max || (n_sel > 0 && (!sel || !dev_flags))) return -3;
     Ctx &c = *reinterpret_cast<Ctx *>(ctx);
     PileState &P = c.pile;
     if (!P.dense) { set_error("no pileup to import into"); return -3; }
     MH_HIP(hipSetDevice(c.device));
-    const int64_t cells = (int64_t)P.n_refs * P.cap;
-    hipLaunchKernelGGL(k_pile_import, dim3(1024), dim3(256), 0, c.stream, P.dense, P.nflag, P.dflag,
-                       P.read_counts, P.first_unit, P.max_pos, cells, P.n_refs,
-                       (const int32_t *)dev_sum, (const int32_t *)dev_max);
+    int32_t *dsel = nullptr;
+    if (int st = upload_sel(c, n_sel, sel, &dsel)) return st;
+    hipLaunchKernelGGL(k_pile_import, dim3(64, n_sel > 0 ? n_sel : 1), dim3(256), 0, c.stream,
+                       P.dense, P.nflag, P.dflag, P.read_counts, P.first_unit, P.max_pos, P.cap,
+                       P.n_refs, n_sel > 0 ? dsel : nullptr, n_sel, (const int32_t *)dev_sum,
+                       (const int32_t *)dev_max, (const uint8_t *)dev_flags);
     MH_HIP(hipGetLastError());
     MH_HIP(hipStreamSynchronize(c.stream));
     return 0;

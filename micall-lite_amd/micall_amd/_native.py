@@ -84,10 +84,9 @@ def _declare(L):
         'mh_pileup_fetch': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
         'mh_pileup_fetch_ref': ([_P, ctypes.c_int, _P, _P, _P], ctypes.c_int),
         'mh_pileup_events': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
-        'mh_pileup_packed_bytes': ([_P, _I64P, _I64P], ctypes.c_int),
-        'mh_pileup_export': ([_P, _P, _P], ctypes.c_int),
-        'mh_pileup_export_base': ([_P, ctypes.c_int64, _P, _P], ctypes.c_int),
-        'mh_pileup_import': ([_P, _P, _P], ctypes.c_int),
+        'mh_pileup_exchange_bytes': ([_P, ctypes.c_int, _I64P, _I64P, _I64P], ctypes.c_int),
+        'mh_pileup_export': ([_P, ctypes.c_int, _P, ctypes.c_int64, _P, _P, _P], ctypes.c_int),
+        'mh_pileup_import': ([_P, ctypes.c_int, _P, _P, _P, _P], ctypes.c_int),
         'mh_gotoh_align': ([_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                             ctypes.c_int, ctypes.c_char_p, _P, ctypes.c_char_p, ctypes.c_char_p,
                             ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
@@ -369,20 +368,35 @@ class Context:
         return dict(dense=dense[:n], nflag=nflag[:n], dflag=dflag[:n], read_counts=rc[:n],
                     first_unit=fu[:n], max_pos=mp[:n], events=events, cap=cap)
 
-    def pileup_packed_bytes(self):
-        s = ctypes.c_int64()
-        m = ctypes.c_int64()
-        check(lib().mh_pileup_packed_bytes(self.h, ctypes.byref(s), ctypes.byref(m)),
-              'mh_pileup_packed_bytes')
-        return s.value, m.value
+    def pileup_scalars(self):
+        """read_counts, first_unit, max_pos of the last pileup (n_refs each)."""
+        n = ctypes.c_int()
+        check(lib().mh_pileup_dims(self.h, ctypes.byref(n), None, None, None), 'mh_pileup_dims')
+        k = max(n.value, 1)
+        rc = np.zeros(k, dtype=np.int64)
+        fu = np.zeros(k, dtype=np.int64)
+        mp = np.zeros(k, dtype=np.int32)
+        check(lib().mh_pileup_fetch(self.h, None, None, None, _ptr(rc), _ptr(fu), _ptr(mp)),
+              'mh_pileup_fetch')
+        return rc[:n.value], fu[:n.value], mp[:n.value]
 
-    def pileup_export(self, dev_sum_ptr, dev_max_ptr, unit_base=0):
-        check(lib().mh_pileup_export_base(self.h, unit_base, ctypes.c_void_p(dev_sum_ptr),
-                                          ctypes.c_void_p(dev_max_ptr)), 'mh_pileup_export')
+    def pileup_exchange_bytes(self, n_sel):
+        s, m, f = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(lib().mh_pileup_exchange_bytes(self.h, n_sel, ctypes.byref(s), ctypes.byref(m),
+                                             ctypes.byref(f)), 'mh_pileup_exchange_bytes')
+        return s.value, m.value, f.value
 
-    def pileup_import(self, dev_sum_ptr, dev_max_ptr):
-        check(lib().mh_pileup_import(self.h, ctypes.c_void_p(dev_sum_ptr),
-                                     ctypes.c_void_p(dev_max_ptr)), 'mh_pileup_import')
+    def pileup_export(self, sel, unit_base, dev_sum_ptr, dev_max_ptr, dev_flags_ptr):
+        sel = np.ascontiguousarray(sel, dtype=np.int32)
+        check(lib().mh_pileup_export(self.h, len(sel), _ptr(sel), unit_base,
+                                     ctypes.c_void_p(dev_sum_ptr), ctypes.c_void_p(dev_max_ptr),
+                                     ctypes.c_void_p(dev_flags_ptr)), 'mh_pileup_export')
+
+    def pileup_import(self, sel, dev_sum_ptr, dev_max_ptr, dev_flags_ptr):
+        sel = np.ascontiguousarray(sel, dtype=np.int32)
+        check(lib().mh_pileup_import(self.h, len(sel), _ptr(sel), ctypes.c_void_p(dev_sum_ptr),
+                                     ctypes.c_void_p(dev_max_ptr), ctypes.c_void_p(dev_flags_ptr)),
+              'mh_pileup_import')
 
     # ---- kernel timing ---------------------------------------------------
     def profile(self, enable=True):

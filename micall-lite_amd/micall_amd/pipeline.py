@@ -70,19 +70,29 @@ class Shard:
         return np.where(out == np.iinfo(np.int64).max, -1, out)
 
     def pileup(self, ctx, unit_base):
-        """All-reduce the device counters in place (sum, and max for flags /
-        max_pos / first unit) and gather the sparse events."""
+        """All-reduce the device counters in place and gather the insertion
+        tokens.  Ranks first agree (MAX of a per-reference flag) on the
+        references that hold data anywhere; only their rows travel: dense
+        counts and read counts summed, N/deletion flags as bytes under MAX
+        (an OR of 0/1), max_pos and the negated global first unit under MAX."""
         torch = self.torch
         dev = self.device
         if dev.type == 'cuda':
-            sum_b, max_b = ctx.pileup_packed_bytes()
+            _rc, fu, mp = ctx.pileup_scalars()
+            has = torch.as_tensor(((fu >= 0) | (mp > 0)).astype(np.int32), device=dev)
+            self.dist.all_reduce(has, op=self.dist.ReduceOp.MAX)
+            sel = np.nonzero(has.cpu().numpy())[0].astype(np.int32)
+            sum_b, max_b, flag_b = ctx.pileup_exchange_bytes(len(sel))
             s = torch.empty(sum_b // 4, dtype=torch.int32, device=dev)
             m = torch.empty(max_b // 4, dtype=torch.int32, device=dev)
-            ctx.pileup_export(s.data_ptr(), m.data_ptr(), unit_base)
+            f = torch.empty(max(flag_b, 1), dtype=torch.uint8, device=dev)
+            ctx.pileup_export(sel, unit_base, s.data_ptr(), m.data_ptr(), f.data_ptr())
             self.dist.all_reduce(s, op=self.dist.ReduceOp.SUM)
             self.dist.all_reduce(m, op=self.dist.ReduceOp.MAX)
+            if flag_b:
+                self.dist.all_reduce(f, op=self.dist.ReduceOp.MAX)
             torch.cuda.synchronize(dev)
-            ctx.pileup_import(s.data_ptr(), m.data_ptr())
+            ctx.pileup_import(sel, s.data_ptr(), m.data_ptr(), f.data_ptr())
             fetched = ctx.pileup_fetch()
         else:  # CPU collective (tests): go through host copies
             fetched = ctx.pileup_fetch()
