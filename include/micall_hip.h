@@ -77,6 +77,12 @@ int mh_device_count(int *n);
 int mh_ctx_create(int device, mh_ctx **out);
 int mh_ctx_destroy(mh_ctx *ctx);
 int mh_ctx_sync(mh_ctx *ctx);
+/* Tuning / ablation switches (not part of the reference interface):
+ *   "dp_fast" (default 1): resolve a banded extension by the exact ungapped
+ *   fast path when its score bound proves the full DP would pick the same
+ *   all-M alignment; 0 always runs the full DP.  Results are
+ *   identical either way. */
+int mh_ctx_set_option(mh_ctx *ctx, const char *name, int value);
 /* the hipStream_t the context launches on (as an opaque handle) */
 int mh_ctx_stream(mh_ctx *ctx, void **stream);
 
@@ -112,8 +118,9 @@ int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mappe
                   int64_t *star_lines, int64_t *star_first);
 /* Work done by the last mh_map: out[0] reads, out[1] banded extensions
  * (candidates aligned by the DP, 64 diagonals x read length cells each),
- * out[2] CIGAR pool words reserved (per-wave chunks). */
-int mh_map_stats(mh_ctx *ctx, int64_t *out3);
+ * out[2] CIGAR pool words reserved (per-wave chunks), out[3] extensions
+ * resolved by the ungapped fast path (no DP). */
+int mh_map_stats(mh_ctx *ctx, int64_t *out4);
 /* The 20 int32 header fields of mh_aln (no CIGAR) for reads [first, first+n). */
 int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20);
 /* SAM text for reads order[first .. first+n) (order NULL: reads first ..

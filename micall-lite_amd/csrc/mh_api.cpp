@@ -473,6 +473,17 @@ int mh_ctx_sync(mh_ctx *ctx)
     return 0;
 }
 
+int mh_ctx_set_option(mh_ctx *ctx, const char *name, int value)
+{
+    if (!ctx || !name) return -3;
+    if (!strcmp(name, "dp_fast")) {
+        X(ctx)->dp_fast = value != 0;
+        return 0;
+    }
+    set_error("mh_ctx_set_option: unknown option '%s'", name);
+    return -3;
+}
+
 int mh_ctx_stream(mh_ctx *ctx, void **stream)
 {
     if (!ctx || !stream) return -3;
@@ -689,15 +700,16 @@ int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mappe
     return 0;
 }
 
-int mh_map_stats(mh_ctx *ctx, int64_t *out3)
+int mh_map_stats(mh_ctx *ctx, int64_t *out4)
 {
-    if (!ctx || !out3) return -3;
+    if (!ctx || !out4) return -3;
     CtxEx *c = X(ctx);
     MapState &M = c->map;
     if (!M.valid) { set_error("no mapping results (call mh_map)"); return -3; }
-    out3[0] = M.n_reads;
-    out3[1] = M.last_work;
-    out3[2] = M.last_cigar;
+    out4[0] = M.n_reads;
+    out4[1] = M.last_work;
+    out4[2] = M.last_cigar;
+    out4[3] = M.last_fast;
     return 0;
 }
 

@@ -109,6 +109,7 @@ struct MapState {
     int cap_refs = 0;
     int64_t last_work = 0;       // extensions (k_dp work items) of the last pass
     int64_t last_cigar = 0;      // CIGAR ops written by the last pass
+    int64_t last_fast = 0;       // extensions resolved by the ungapped fast path
     bool valid = false;
 };
 
@@ -182,6 +183,7 @@ struct Ctx {
     PileState pile;
     // per-length tables (host-computed, uploaded): seed interval, min score, n ceil
     int32_t *len_tab = nullptr;      // [3][MAXLEN + 1]
+    int dp_fast = 1;                 // option "dp_fast": exact ungapped fast path of k_dp
     int len_tab_mode = -1;
 };
 

@@ -358,6 +358,7 @@ struct DpArgs {
     int rows_pad;             // per-wave LDS row capacity (multiple of 8)
     int wave_lds;             // bytes of LDS per wave
     int oeI, exI, oeD, exD;
+    int fast;                 // try the exact ungapped fast path (dp_ungapped)
 };
 
 __device__ __forceinline__ int mm_pen(int qchar)
@@ -482,6 +483,169 @@ __device__ __forceinline__ uint32_t dp_row_nogap(uint32_t tbv, int rc, int &Hp, 
     return src;
 }
 
+__device__ __forceinline__ int wave_excl_scan_min(int v, int lane, int init)
+{
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x = x < y ? x : y;
+    }
+    const int e = __shfl_up(x, 1, 64);
+    return lane == 0 ? init : e;
+}
+
+__device__ __forceinline__ int wave_max(int v)
+{
+    for (int o = 32; o > 0; o >>= 1) v = imax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Exact ungapped fast path of k_dp.
+//
+// Every path through the band that contains a gap pays at least one open +
+// extend, gmin = min(oeI, oeD) (13 with --rdg/--rfg 10,3), and scores at most
+// ma per M row, so the DP value of any cell (i, k) is
+//     H(i, k) = max(U(i, k), g)   with g <= Gb(i) = ma * (i + 1) - gmin,
+// where U is the ungapped recurrence along diagonal k alone (no gap can open
+// before row GBAR, so Gb only applies from there).  Hence if the best
+// ungapped cell (S, i*, kb) satisfies
+//   (A) S > Gb(m - 1)                      (no gapped cell reaches S),
+//   (B) U(i, k) < S for every k != kb      (bounded by ma * matches(k) in
+//       local mode, -non_matches(k) at the last row end-to-end),
+//   (C) U(r, kb) >= Gb(r) on every row r of the traced segment (so H = U
+//       there and the traceback's "diagonal first" choice is the same),
+// the full DP picks the same best cell and traces the same all-M path.  The
+// fast path then writes only that lane's traceback bits and k_dp skips the
+// DP; otherwise (any condition false, read > 512 nt) it runs the full DP.
+// Candidates are screened first by a cheap per-diagonal non-match count
+// (4 rows per LDS word) that gives up as soon as no lane can satisfy (A).
+// The result is bit-identical to the full DP (tests/test_gpu_parity.py
+// runs both and compares them with the oracle, og_mapper.c:dp_extend).
+// ---------------------------------------------------------------------------
+template <int LOCAL>
+__device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint8_t *rdc,
+                            uint32_t *bits, int m, int lane, int gmin, int &best, int &bi,
+                            int &bl)
+{
+    const int ma = LOCAL ? 2 : 0;
+    const int gb_max = ma * m - gmin;   // Gb(m - 1)
+    // ---- non-matches per diagonal: read bytes rdc[i..i+3] against ref
+    // bytes refw[i+lane .. i+lane+3] (codes * 4), 4 rows per step ----
+    const uint8_t *rp = refw + (lane & ~3);
+    const uint32_t sh = (uint32_t)(lane & 3);
+    int nm = 0;
+    for (int i = 0; i < m; i += 4) {
+        const uint32_t rd = *(const uint32_t *)(rdc + i);
+        const uint32_t lo = *(const uint32_t *)(rp + i), hi = *(const uint32_t *)(rp + i + 4);
+        const uint32_t rv = __builtin_amdgcn_alignbyte(hi, lo, sh) >> 2;
+        uint32_t x = (rd ^ rv) | ((rd | rv) & 0x04040404u);
+        x = (x | (x >> 1) | (x >> 2)) & 0x01010101u;
+        nm += __builtin_popcount(x);
+        if ((i & 63) == 60) {
+            // the best ungapped score of a lane is at most ma*(m - nm) (local)
+            // or -nm (end-to-end); give up when no lane can beat Gb(m-1)
+            const int ub = LOCAL ? ma * (m - nm) : -nm;
+            if (__builtin_amdgcn_ballot_w64(ub > gb_max) == 0) return false;
+        }
+    }
+    nm -= (4 - (m & 3)) & 3;   // rows past the read end are coded 4
+    const int ub = LOCAL ? ma * (m - nm) : -nm;
+    // candidate lane: fewest non-matches, then smallest lane (any choice is
+    // exact: (B) below checks every other lane)
+    int key = nm * 64 + lane;
+    for (int o = 32; o > 0; o >>= 1) {
+        const int y = __shfl_xor(key, o, 64);
+        key = y < key ? y : key;
+    }
+    const int kb = key & 63;
+    const int ub_other = wave_max(lane == kb ? INT32_MIN + 1 : ub);
+    const int ub_kb = __shfl(ub, kb, 64);
+    if (ub_kb <= gb_max || ub_other >= ub_kb) return false;   // (A) / (B) cannot hold
+
+    // ---- exact ungapped recurrence on lane kb: rows 8*lane .. 8*lane+7 ----
+    const int r0 = 8 * lane;
+    int s[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int r = r0 + u;
+        s[u] = r < m ? (int)__builtin_amdgcn_ubfe(tab[r], (uint32_t)refw[r + kb], 4) - 8 : 0;
+    }
+    int tot = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) tot += s[u];
+    const int pbase = wave_excl_scan(tot, lane);   // prefix sum before row r0
+    int P[8], mn = 0;
+    {
+        int p = pbase, lm = INT32_MAX;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            p += s[u];
+            P[u] = p;
+            lm = p < lm ? p : lm;
+        }
+        mn = wave_excl_scan_min(lm, lane, 0);      // min(0, prefix sums before r0)
+        mn = mn < 0 ? mn : 0;
+    }
+    int H[8];
+    int hbest = -1, rbest = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        if (LOCAL) {
+            mn = P[u] < mn ? P[u] : mn;
+            H[u] = P[u] - mn;           // Kadane: max(H(r-1) + s(r), 0)
+        } else {
+            H[u] = P[u];
+        }
+        if (LOCAL && r0 + u < m && H[u] > hbest) { hbest = H[u]; rbest = r0 + u; }
+    }
+    int S, istar;
+    if (LOCAL) {
+        const int k2 = wave_max(hbest >= 0 ? hbest * 1024 + (1023 - rbest) : -1);
+        S = k2 >> 10;
+        istar = 1023 - (k2 & 1023);
+    } else {
+        const int last = m - 1;
+        int v = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) if (r0 + u == last) v = H[u];
+        S = __shfl(v, last >> 3, 64);
+        istar = last;
+    }
+    // (A) and (B)
+    if (!(S > gb_max) || !(ub_other < S)) return false;
+    if (LOCAL && S <= 0) return false;
+    // start of the traced segment: last row <= i* where H == 0 (local)
+    int istop = -1;
+    if (LOCAL) {
+        int z = -1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) if (r0 + u <= istar && H[u] == 0) z = r0 + u;
+        istop = wave_max(z);
+    }
+    // (C)
+    bool bad = false;
+    const int lo = istop > 0 ? istop : 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int r = r0 + u;
+        if (r >= lo && r <= istar && r >= GBAR && H[u] < ma * (r + 1) - gmin) bad = true;
+    }
+    if (__builtin_amdgcn_ballot_w64(bad) != 0) return false;
+    // traceback bits of lane kb: diagonal (1) where H > 0, local stop (0)
+    if (r0 < m) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (r0 + u < m && (!LOCAL || H[u] > 0)) w |= 1u << (4 * u);
+        bits[lane * 64 + kb] = w;
+    }
+    best = S;
+    bi = istar;
+    bl = kb;
+    return true;
+}
+
 template <int LOCAL>
 __global__ __launch_bounds__(256) void k_dp(DpArgs A)
 {
@@ -509,6 +673,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
 
     int64_t ck_base = 0;   // lane 0: this wave's current CIGAR pool chunk
     int ck_left = 0;
+    int n_fast = 0;        // extensions resolved by dp_ungapped
     for (int w = blockIdx.x * wpb + wv; w < n_work; w += gridDim.x * wpb) {
         const int sid = A.work[w];
         const int64_t r = sid / MAXCAND;
@@ -570,69 +735,76 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         }
         wave_sync();
 
-        // ---- DP over rows, 8 rows per group (one u32 of traceback bits per
-        // lane); groups wholly inside the gap window run branch-free; the next
-        // group's LDS operands are loaded while this group computes ----
-        int Hp = BIAS, Ep = 0;
-        uint32_t bestKey = 0;
-        uint32_t tbn[8];
-        int rcn[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            tbn[t] = tab[t];
-            rcn[t] = refw[t + lane];
-        }
-        for (int i0 = 0; i0 < m; i0 += 8) {
-            uint32_t tbv[8];
-            int rcv[8];
+        int best, bi, bl;
+        const bool fast = A.fast && m > 2 * GBAR + 8 && m <= 512 &&
+                          dp_ungapped<LOCAL>(tab, refw, rdc, bits, m, lane,
+                                             A.oeI < A.oeD ? A.oeI : A.oeD, best, bi, bl);
+        n_fast += fast;
+        if (!fast) {
+            // ---- DP over rows, 8 rows per group (one u32 of traceback bits per
+            // lane); groups wholly inside the gap window run branch-free; the next
+            // group's LDS operands are loaded while this group computes ----
+            int Hp = BIAS, Ep = 0;
+            uint32_t bestKey = 0;
+            uint32_t tbn[8];
+            int rcn[8];
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                tbv[t] = MH_DP_PREFETCH ? tbn[t] : tab[i0 + t];
-                rcv[t] = MH_DP_PREFETCH ? rcn[t] : refw[i0 + t + lane];
+                tbn[t] = tab[t];
+                rcn[t] = refw[t + lane];
             }
-            if (MH_DP_PREFETCH && i0 + 8 < m) {
+            for (int i0 = 0; i0 < m; i0 += 8) {
+                uint32_t tbv[8];
+                int rcv[8];
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
-                    tbn[t] = tab[i0 + 8 + t];
-                    rcn[t] = refw[i0 + 8 + t + lane];
+                    tbv[t] = MH_DP_PREFETCH ? tbn[t] : tab[i0 + t];
+                    rcv[t] = MH_DP_PREFETCH ? rcn[t] : refw[i0 + t + lane];
                 }
-            }
-            uint32_t acc = 0;
-            if (i0 >= GBAR && i0 + 8 <= m - GBAR) {
+                if (MH_DP_PREFETCH && i0 + 8 < m) {
 #pragma unroll
-                for (int t = 0; t < 8; ++t)
-                    acc |= dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K)
-                           << (4 * t);
-            } else {
-#pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const int i = i0 + t;
-                    if (i < m) {
-                        const uint32_t nib =
-                            (i >= GBAR && i < m - GBAR)
-                                ? dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K)
-                                : dp_row_nogap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i);
-                        acc |= nib << (4 * t);
+                    for (int t = 0; t < 8; ++t) {
+                        tbn[t] = tab[i0 + 8 + t];
+                        rcn[t] = refw[i0 + 8 + t + lane];
                     }
                 }
+                uint32_t acc = 0;
+                if (i0 >= GBAR && i0 + 8 <= m - GBAR) {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t)
+                        acc |= dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K)
+                               << (4 * t);
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const int i = i0 + t;
+                        if (i < m) {
+                            const uint32_t nib =
+                                (i >= GBAR && i < m - GBAR)
+                                    ? dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K)
+                                    : dp_row_nogap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i);
+                            acc |= nib << (4 * t);
+                        }
+                    }
+                }
+                bits[(i0 >> 3) * 64 + lane] = acc;
             }
-            bits[(i0 >> 3) * 64 + lane] = acc;
+            int bestH, bestI;
+            if (LOCAL) {
+                bestH = (int)(bestKey >> 10) - BIAS;
+                bestI = 1023 - (int)(bestKey & 1023u);
+            } else {
+                bestH = Hp - BIAS;   // end-to-end: the last row
+                bestI = m - 1;
+            }
+            // best cell: max score, then smallest row, then smallest lane
+            const long long key = (long long)bestH * 1048576ll + (long long)((1023 - bestI) << 6) +
+                                  (long long)(63 - lane);
+            const long long bk = wave_max64(key);
+            best = (int)(bk >> 20);
+            bi = 1023 - (int)((bk >> 6) & 1023);
+            bl = 63 - (int)(bk & 63);
         }
-        int bestH, bestI;
-        if (LOCAL) {
-            bestH = (int)(bestKey >> 10) - BIAS;
-            bestI = 1023 - (int)(bestKey & 1023u);
-        } else {
-            bestH = Hp - BIAS;   // end-to-end: the last row
-            bestI = m - 1;
-        }
-        // best cell: max score, then smallest row, then smallest lane
-        const long long key = (long long)bestH * 1048576ll + (long long)((1023 - bestI) << 6) +
-                              (long long)(63 - lane);
-        const long long bk = wave_max64(key);
-        const int best = (int)(bk >> 20);
-        const int bi = 1023 - (int)((bk >> 6) & 1023);
-        const int bl = 63 - (int)(bk & 63);
         const int minsc = A.len_tab[(MAXLEN + 1) + m];
         wave_sync();
 
@@ -814,6 +986,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         if (lane == 0) A.slot[sid] = out;
         wave_sync();
     }
+    if (lane == 0 && n_fast) atomicAdd(&A.pool_ctr[2], n_fast);
 }
 
 // ---------------------------------------------------------------------------
@@ -1196,11 +1369,11 @@ int run_map(Ctx &c, const mh_params &par)
         const int wave_lds =
             ((rows_pad * 35 + 4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP) + 64) + 15) & ~15;
         for (int attempt = 0; attempt < 2; ++attempt) {
-            MH_HIP(hipMemsetAsync(M.counters + 1, 0, sizeof(int32_t) * 2, s));
+            MH_HIP(hipMemsetAsync(M.counters + 1, 0, sizeof(int32_t) * 3, s));
             DpArgs da{c.reads, c.index, c.len_tab, M.cand, M.work, M.counters, M.slot, M.pool,
                       M.counters + 1, M.pool_cap, rows_pad, wave_lds,
                       par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext,
-                      par.rdg_ext};
+                      par.rdg_ext, c.dp_fast};
             // one wave per workgroup: the CU then packs floor(160 KiB / wave_lds)
             // waves (15 at 251-nt reads) with no workgroup rounding loss
             int wpb = MH_DP_WPB;
@@ -1220,11 +1393,12 @@ int run_map(Ctx &c, const mh_params &par)
             }
             prof_end(c, pd);
             MH_HIP(hipGetLastError());
-            int32_t ctr[3];
+            int32_t ctr[4];
             MH_HIP(hipMemcpyAsync(ctr, M.counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
             MH_HIP(hipStreamSynchronize(s));
             M.last_work = ctr[0];
             M.last_cigar = ctr[1];
+            M.last_fast = ctr[3];
             if (!ctr[2]) break;
             // CIGAR pool overflow: grow to what was asked for and redo the extensions
             hipFree(M.pool);

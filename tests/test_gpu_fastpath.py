@@ -1,0 +1,114 @@
+"""The exact ungapped fast path of k_dp (mh_map.hip dp_ungapped) against the
+full banded DP and the CPU oracle (og_mapper.c dp_extend): reads built to sit
+on both sides of every bound the fast path relies on -- 0/1/2 mismatches at
+every quality band and at the read ends, local clips, Ns, reference ends,
+tandem repeats (other diagonals with few mismatches), indels, short and long
+reads.  All three must agree bit for bit."""
+import numpy as np
+import pytest
+
+import oracle
+from micall_amd import _native, projects
+
+pytestmark = pytest.mark.gpu
+
+SEEDS = projects.load_default().seed_sequences()
+POL = SEEDS['HIV1B-pol-seed']
+COMP = {'A': 'T', 'C': 'G', 'G': 'C', 'T': 'A', 'N': 'N'}
+
+
+def _revcomp(s):
+    return ''.join(COMP[c] for c in reversed(s))
+
+
+def _reference():
+    rng = np.random.default_rng(17)
+    unit = 'ACGTTGCA'
+    rep = unit * 40 + ''.join('ACGT'[x] for x in rng.integers(0, 4, 200)) + 'AAT' * 60
+    return [POL, rep + POL[:400]]
+
+
+def _cases():
+    rng = np.random.default_rng(23)
+    refs = _reference()
+    seqs, quals = [], []
+
+    def add(s, q):
+        seqs.append(s)
+        quals.append(q)
+
+    def mutate(s, at):
+        s = list(s)
+        for p in at:
+            s[p] = 'ACGT'[('ACGT'.index(s[p]) + 1 + int(rng.integers(0, 3))) % 4]
+        return ''.join(s)
+
+    qchars = ['#', '+', '5', '?', 'G', 'I']   # penalties 2..6
+    for m in (251, 300, 150, 40, 17, 12, 512, 600):
+        for _ in range(6):
+            ref = refs[int(rng.integers(0, 2))] if m <= 600 else POL
+            if len(ref) < m:
+                ref = POL
+            st = int(rng.integers(0, len(ref) - m + 1))
+            base = ref[st:st + m]
+            qc = qchars[int(rng.integers(0, len(qchars)))]
+            q = qc * m
+            add(base, q)                                    # exact
+            for p in (0, 1, 3, 5, 6, 7, m // 2, m - 8, m - 6, m - 2, m - 1):
+                if 0 <= p < m:
+                    add(mutate(base, [p]), q)               # one mismatch
+            for a, b in ((m // 3, 2 * m // 3), (2, m - 3), (5, 9), (m - 9, m - 5)):
+                if 0 <= a < b < m:
+                    for q2 in ('#', 'G'):
+                        add(mutate(base, [a, b]), q2 * m)   # two mismatches
+            add(mutate(base, list(range(10, min(m, 90), 12))), q)
+            if m > 40:
+                add(base[:m // 2] + 'N' + base[m // 2 + 1:], q)   # an N
+                ins = base[:m // 2] + 'ACG' + base[m // 2:m - 3]
+                add(ins, q)                                        # insertion
+                dele = base[:m // 2] + ref[st + m // 2 + 2:st + m + 2]
+                if len(dele) == m:
+                    add(dele, q)                                   # deletion
+            add(_revcomp(base), q)                          # reverse strand
+    # reference-end overhangs and tandem-repeat reads
+    for m in (251, 120):
+        add(POL[:m - 30].rjust(m, 'A'), 'G' * m)
+        add(POL[-(m - 25):] + 'C' * 25, 'G' * m)
+        rep = refs[1]
+        for st in (0, 16, 40, 320, 400):
+            add(rep[st:st + m], 'G' * m)
+            add(mutate(rep[st:st + m], [m // 2]), 'G' * m)
+    return refs, seqs, quals
+
+
+def _gpu(ctx, refs, mode, seqs, quals, fast):
+    ctx.set_option('dp_fast', fast)
+    ctx.index_build(['ref%d' % i for i in range(len(refs))], refs, oracle.seed_len(mode))
+    ctx.reads_load(seqs, quals, False)
+    ctx.map(_native.params(mode))
+    return ctx.fetch(), ctx.map_stats()
+
+
+@pytest.mark.parametrize('mode', [oracle.E2E, oracle.LOCAL])
+def test_fast_path_equals_full_dp_and_oracle(mode):
+    refs, seqs, quals = _cases()
+    ix = oracle.Index(refs, oracle.seed_len(mode))
+    ref = np.frombuffer(bytes(oracle.map_reads(ix, oracle.params(mode), seqs, quals, False)),
+                        dtype=_native.ALN_DTYPE)[:len(seqs)]
+    ctx = _native.Context(0)
+    try:
+        full, st_full = _gpu(ctx, refs, mode, seqs, quals, 0)
+        fast, st_fast = _gpu(ctx, refs, mode, seqs, quals, 1)
+    finally:
+        ctx.set_option('dp_fast', 1)
+        ctx.close()
+    assert st_full[3] == 0
+    assert st_fast[3] > 0.2 * st_fast[1], st_fast    # the fast path is exercised
+    assert st_fast[3] < st_fast[1], st_fast          # and so is the fallback
+    for name, got in (('full DP', full), ('fast path', fast)):
+        for i in range(len(ref)):
+            for f in _native.ALN_FIELDS:
+                assert got[i][f] == ref[i][f], (name, i, f, got[i][f], ref[i][f], seqs[i][:40])
+            n = ref[i]['n_cigar']
+            assert np.array_equal(got[i]['cigar'][:n], ref[i]['cigar'][:n]), (
+                name, i, _native.cigar_text(got[i]), _native.cigar_text(ref[i]))
