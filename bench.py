@@ -124,6 +124,87 @@ def instrument(pipe, ctx, stages):
         setattr(pl, name, timed)
 
 
+def s2a_algo_bytes(text_rows, res_pairs, body_bytes):
+    """k_s2a_merge's algorithmic bytes: read seq + qual of every mate of a
+    merged pair, write the merged body, 16 B of results and 16 B of hashes
+    per pair."""
+    return text_rows + body_bytes + 32 * res_pairs
+
+
+def bench_sam2aln(args):
+    """sam2aln (micall_amd.sam2aln, mh_sam2aln_csv) over remap.csv text of
+    one C2 remap pass: host CSV parse + upload + device merge/group + fetch,
+    then the three CSV outputs."""
+    import torch
+    from micall_amd import _native
+    from micall_amd.pipeline import RemapPipeline
+    import og_sam2aln
+    ctx = _native.Context(0)
+    reads, quals = make_reads(args.pairs, block=0)
+    ctx.reads_load_fixed(reads, quals, True)
+    del reads, quals
+    ctx.set_names(['M00000:1:000000000-AAAAA:1:1101:{}:{}'.format(1000 + i // 1000000,
+                                                                         1000 + i % 1000000)
+                         for i in range(args.pairs) for _ in (0, 1)])
+    pipe = RemapPipeline(ctx)
+    pipe.run(2.0 * args.pairs, max_iterations=1)
+    text = ('qname,flag,rname,pos,mapq,cigar,rnext,pnext,tlen,seq,qual\n' +
+            ctx.format_rows(1, 0, 2 * args.pairs)).encode()
+    for _ in range(args.warmup):
+        ctx.sam2aln_csv(text)
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.sam2aln_csv(text)
+    elapsed = time.perf_counter() - t0
+    kern = {k: ctx.profile_get(k) for k in ('k_s2a_merge', 'k_s2a_group')}
+    t1 = time.perf_counter()
+    outs = {w: ctx.sam2aln_output(w) for w in ('aligned', 'insert', 'failed')}
+    t_out = time.perf_counter() - t1
+    st = ctx.sam2aln_stats()
+    merge_ms, merge_n = kern['k_s2a_merge']
+    avg_s = merge_ms / 1e3 / max(merge_n, 1)
+    # algorithmic bytes: every merged mate's seq + qual, the merged bodies
+    body = sum(int(line.rsplit(',', 1)[1].__len__()) * int(line.split(',')[3])
+               for line in outs['aligned'].splitlines()[1:])
+    mate_bytes = 2 * 2 * READ_LEN * st[1]
+    algo = s2a_algo_bytes(mate_bytes, st[1], body)
+    achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
+    sample = min(20000, args.pairs)
+    lines = text.decode().split('\n', 2 * sample + 1)
+    stext = '\n'.join(lines[:2 * sample + 1]) + '\n'
+    t2 = time.perf_counter()
+    og_sam2aln.sam2aln(stext)
+    cpu_s = time.perf_counter() - t2
+    dev_ms = sum(v[0] for v in kern.values()) / args.steps
+    out = {
+        'metric': 'sam2aln read pairs/sec (remap.csv -> aligned/insert/failed)',
+        'value': round(st[0] * args.steps / elapsed, 1), 'unit': 'pairs/s', 'n_gpus': 1,
+        'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(1e3 * elapsed / args.steps, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
+        'config': {'workload': 'sam2aln over the remap.csv of one C2 remap pass (1M pairs '
+                               'of synthetic 2x251 HIV-1 pol reads), q-cutoff 15',
+                   'pairs': st[0], 'merged': st[1], 'distinct': st[2], 'failed': st[3],
+                   'csv_bytes': len(text)},
+        'device_ms_per_step': round(dev_ms, 3),
+        'device_pairs_per_s': round(st[0] / (dev_ms / 1e3), 1) if dev_ms > 0 else None,
+        'output_format_ms': round(1e3 * t_out, 1),
+        'roofline': {'kernel': 'k_s2a_merge', 'bound': 'hbm', 'achieved': round(achieved, 3),
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 6),
+                     'traffic': None, 'algo_bytes_per_launch': algo,
+                     'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': merge_n},
+        'kernels_ms_per_step': {k: round(v[0] / args.steps, 3) for k, v in kern.items()},
+        'cpu_baseline': {'value': round(sample / cpu_s, 1), 'unit': 'pairs/s', 'cores': 1,
+                         'kind': 'port',
+                         'sample': 'first {} pairs of the same remap.csv through the pure-Python '
+                                   'restatement oracle/og_sam2aln.py, {:.1f} s'.format(sample, cpu_s)},
+    }
+    print(json.dumps(out))
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split('\n\n')[0])
     ap.add_argument('--gpus', type=int, default=1)
@@ -134,7 +215,12 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--breakdown', action='store_true',
                     help='time each pipeline stage (synchronising) and print it to stderr')
+    ap.add_argument('--stage', choices=('remap', 'sam2aln'), default='remap',
+                    help='remap: the headline hot path (default); sam2aln: the next stage '
+                         '(SURVEY.md 8(f)) over the remap.csv of one C2 pass')
     args = ap.parse_args()
+    if args.stage == 'sam2aln':
+        return bench_sam2aln(args)
 
     import torch
     import torch.distributed as dist

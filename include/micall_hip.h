@@ -26,7 +26,10 @@
  *             ranks, done by the caller on device buffers);
  *   3. the _gotoh2 C-extension boundary, micall/alignment/src/_gotoh2.c:544-607
  *      (align_wrapper, "ssiiisO")
- *          -> mh_gotoh_align.
+ *          -> mh_gotoh_align;
+ *   4. (next stage) sam2aln's Python merge of remap.csv,
+ *      micall/core/sam2aln.py:395-478
+ *          -> mh_sam2aln_csv, mh_sam2aln_output.
  *
  * Conventions: every function returns 0 on success, -1 on traceback failure
  * (mh_gotoh_align only), -2 on out-of-memory, -3 on a bad argument, -4 on a
@@ -191,6 +194,24 @@ int mh_pileup_export(mh_ctx *ctx, int n_sel, const int32_t *sel, int64_t unit_ba
                      void *dev_sum, void *dev_max, void *dev_flags);
 int mh_pileup_import(mh_ctx *ctx, int n_sel, const int32_t *sel, const void *dev_sum,
                      const void *dev_max, const void *dev_flags);
+
+/* ---- sam2aln: replaces sam2aln.sam2aln (sam2aln.py:395-478) ----------- */
+/* remap.csv text (the SAM columns remap() writes) read as DictReader does,
+ * paired by qname (matchmaker, sam2aln.py:291-312), every pair merged on the
+ * device (parse_sam, :315-391: apply_cigar, merge_pairs at q_cutoff, the
+ * prop_N > max_prop_n test) and identical merged sequences counted per rname
+ * (:449-456).  MiCall passes q_cutoff 15 and max_prop_n 0.5
+ * (SAM2ALN_Q_CUTOFFS, MAX_PROP_N).  Fails (-3, message as the reference's
+ * RuntimeError) on a CIGAR apply_cigar rejects.  *n_units = matchmaker pairs. */
+int mh_sam2aln_csv(mh_ctx *ctx, const char *text, int64_t len, int q_cutoff, double max_prop_n,
+                   int64_t *n_units);
+/* CSV text of the last mh_sam2aln_csv: which 0 = aligned.csv, 1 =
+ * insert.csv, 2 = failed.csv (DictWriter, '\n' line ends, with header).
+ * buf NULL: only *used = bytes needed. */
+int mh_sam2aln_output(mh_ctx *ctx, int which, char *buf, size_t cap, size_t *used);
+/* out[0] pairs, out[1] pairs merged on the device, out[2] distinct merged
+ * sequences, out[3] failed pairs. */
+int mh_sam2aln_stats(mh_ctx *ctx, int64_t *out4);
 
 /* ---- Gotoh: replaces _gotoh2.align (_gotoh2.c:544-607) ---------------- */
 /* seq1/seq2 already cleaned (gotoh2.py:70-72).  out1/out2 need

@@ -92,6 +92,11 @@ def _declare(L):
                             ctypes.c_int, ctypes.c_char_p, _P, ctypes.c_char_p, ctypes.c_char_p,
                             ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         'mh_levenshtein': ([ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
+        'mh_sam2aln_csv': ([_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                            _I64P], ctypes.c_int),
+        'mh_sam2aln_output': ([_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                               ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        'mh_sam2aln_stats': ([_P, _P], ctypes.c_int),
         'mh_profile': ([_P, ctypes.c_int], ctypes.c_int),
         'mh_profile_get': ([_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _I64P],
                            ctypes.c_int),
@@ -176,6 +181,32 @@ class Context:
 
     def sync(self):
         check(lib().mh_ctx_sync(self.h), 'mh_ctx_sync')
+
+    # ---- sam2aln --------------------------------------------------------
+    def sam2aln_csv(self, text, q_cutoff=15, max_prop_n=0.5):
+        """mh_sam2aln_csv on remap.csv text (str or bytes); returns the
+        number of matchmaker pairs."""
+        data = text.encode() if isinstance(text, str) else bytes(text)
+        n = ctypes.c_int64()
+        check(lib().mh_sam2aln_csv(self.h, data, len(data), int(q_cutoff), float(max_prop_n),
+                                   ctypes.byref(n)), 'mh_sam2aln_csv')
+        return n.value
+
+    def sam2aln_output(self, which):
+        """'aligned' | 'insert' | 'failed' CSV text of the last sam2aln."""
+        w = {'aligned': 0, 'insert': 1, 'failed': 2}[which]
+        used = ctypes.c_size_t()
+        check(lib().mh_sam2aln_output(self.h, w, None, 0, ctypes.byref(used)), 'mh_sam2aln_output')
+        buf = ctypes.create_string_buffer(used.value + 1)
+        check(lib().mh_sam2aln_output(self.h, w, buf, used.value + 1, ctypes.byref(used)),
+              'mh_sam2aln_output')
+        return buf.raw[:used.value].decode()
+
+    def sam2aln_stats(self):
+        """(pairs, merged on the device, distinct merged sequences, failed)."""
+        out = np.zeros(4, dtype=np.int64)
+        check(lib().mh_sam2aln_stats(self.h, _ptr(out)), 'mh_sam2aln_stats')
+        return tuple(int(x) for x in out)
 
     # ---- reference set --------------------------------------------------
     def index_build(self, names, seqs, seedlen):

@@ -1,0 +1,57 @@
+"""
+Drop-in for micall/core/sam2aln.py: same function, arguments and output files.
+
+sam2aln() reads remap.csv, pairs rows by qname, merges each pair into one
+sequence in consensus coordinates (apply_cigar + merge_pairs at q-cutoff 15),
+drops pairs with more than half of their bases censored, and writes the
+distinct merged sequences with their counts per reference (aligned.csv), the
+insertions the merge removed (insert.csv) and the pairs that failed
+(failed.csv) -- sam2aln.py:395-478.  The per-pair work and the count of
+identical sequences run on the device (mh_sam2aln_csv, mh_sam2aln.hip); the
+host parses the CSV and writes the text.  nthreads is accepted for signature
+compatibility and ignored.  There is no CPU fallback.
+"""
+import argparse
+
+from . import session
+
+SAM2ALN_Q_CUTOFFS = [15]  # sam2aln.py:24
+MAX_PROP_N = 0.5          # sam2aln.py:25
+
+
+def sam2aln(remap_csv, aligned_csv, insert_csv=None, failed_csv=None, nthreads=None):
+    """sam2aln.sam2aln (sam2aln.py:395-478)."""
+    if len(SAM2ALN_Q_CUTOFFS) != 1:
+        raise NotImplementedError('the device merge takes one q-cutoff per pass')
+    text = remap_csv.read()
+    ctx = session.context()
+    ctx.sam2aln_csv(text, q_cutoff=SAM2ALN_Q_CUTOFFS[0], max_prop_n=MAX_PROP_N)
+    if insert_csv:
+        insert_csv.write(ctx.sam2aln_output('insert'))
+    if failed_csv:
+        failed_csv.write(ctx.sam2aln_output('failed'))
+    aligned_csv.write(ctx.sam2aln_output('aligned'))
+
+
+def parseArgs():
+    parser = argparse.ArgumentParser(description='Conversion of SAM data into aligned format.')
+    parser.add_argument('remap_csv', type=argparse.FileType('r'),
+                        help='<input> SAM output of bowtie2 in CSV format')
+    parser.add_argument('aligned_csv', type=argparse.FileType('w'),
+                        help='<output> CSV containing cleaned and merged reads')
+    parser.add_argument('insert_csv', nargs='?', default=None, type=argparse.FileType('w'),
+                        help='<output> CSV containing insertions relative to sample consensus')
+    parser.add_argument('failed_csv', nargs='?', default=None, type=argparse.FileType('w'),
+                        help='<output> CSV containing reads that failed to merge')
+    parser.add_argument('-p', type=int, default=None, help='(optional) number of threads')
+    return parser.parse_args()
+
+
+def main():
+    args = parseArgs()
+    sam2aln(remap_csv=args.remap_csv, aligned_csv=args.aligned_csv, insert_csv=args.insert_csv,
+            failed_csv=args.failed_csv, nthreads=args.p)
+
+
+if __name__ == '__main__':
+    main()

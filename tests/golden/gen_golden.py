@@ -17,6 +17,12 @@ itself produced for them.  Sections:
   sam2aln  every apply_cigar / merge_pairs / merge_inserts call made by
            micall/tests/sam2aln_test.py.
 
+  s2a      the reference's sam2aln() (the next stage) on
+           every call micall/tests/sam2aln_test.py makes, on edge-case
+           remap.csv texts derived from the e2e cases below, and on every
+           e2e case's remap.csv: aligned.csv / insert.csv / failed.csv under
+           tests/golden/sam2aln_e2e.json and tests/golden/e2e/<case>/.
+
   e2e      the stock reference prelim_map() + remap() (nthreads=1, so its
            pileup runs without a process pool and is deterministic) with
            oracle/shim_bin/bowtie2 standing in for bowtie2, on small committed
@@ -317,7 +323,130 @@ def gen_e2e():
         print('e2e:', name)
 
 
+def _s2a_edge_texts():
+    """remap.csv texts that reach every branch of parse_sam / merge_pairs:
+    built from the first rows of the syn_pol case's remap.csv."""
+    import csv
+    import gzip
+    import random
+    src = os.path.join(HERE, 'e2e', 'syn_pol', 'remap.csv.gz')
+    with gzip.open(src, 'rt') as f:
+        rows = list(csv.DictReader(f))
+    fields = ['qname', 'flag', 'rname', 'pos', 'mapq', 'cigar', 'rnext', 'pnext', 'tlen', 'seq',
+              'qual']
+    rng = random.Random(31)
+
+    def text(rs):
+        out = io.StringIO()
+        w = csv.DictWriter(out, fields, lineterminator='\n')
+        w.writeheader()
+        for r in rs:
+            w.writerow(r)
+        return out.getvalue()
+
+    mapped = [r for r in rows if r['cigar'] != '*'][:400]
+    cases = {}
+    base = [dict(r) for r in mapped]
+    cases['plain'] = text(base)
+    # failures: unmatched mate, '*' CIGAR, different references, low quality
+    t = [dict(r) for r in mapped[:120]]
+    del t[5]
+    t[10]['cigar'] = '*'
+    t[20]['rname'] = 'OTHER-REF'
+    for r in t[30:34]:
+        r['qual'] = '#' * len(r['seq'])
+    for r in t[40:42]:
+        r['qual'] = ''.join(rng.choice('#+5') for _ in r['seq'])
+    cases['failures'] = text(t)
+    # indels, soft clips, far-apart and overlapping mates, unpaired flags,
+    # duplicated qnames, escaped quality characters
+    t = [dict(r) for r in mapped[:160]]
+    for k in range(0, 40, 2):
+        r = t[k]
+        n = len(r['seq'])
+        a = 5 + k
+        if k % 4 == 0:
+            r['cigar'] = '{}M3I{}M'.format(a, n - a - 3)
+        else:
+            r['cigar'] = '{}S{}M4D{}M'.format(3, a, n - a - 3)
+    for k in range(40, 60, 2):
+        t[k + 1]['pos'] = str(int(t[k]['pos']) + 700)
+    for k in range(60, 70):
+        t[k]['flag'] = str(int(t[k]['flag']) & ~1)
+    dup = [dict(t[80]), dict(t[81]), dict(t[80])]
+    t += dup
+    for k in range(90, 100):
+        q = list(t[k]['qual'])
+        q[3] = ','
+        q[7] = '"'
+        t[k]['qual'] = ''.join(q)
+    for k in range(100, 110):
+        t[k]['seq'] = t[k]['seq'][:50] + 'N' * 10 + t[k]['seq'][60:]
+    cases['shapes'] = text(t)
+    # identical merged sequences (counts > 1, rank ties broken by offset/seq)
+    t = []
+    for k in range(0, 60, 2):
+        for rep in range(1 + k % 3):
+            a, b = dict(mapped[k]), dict(mapped[k + 1])
+            a['qname'] = b['qname'] = '{}_{}'.format(mapped[k]['qname'], rep)
+            t += [a, b]
+    rng.shuffle(t)
+    cases['duplicates'] = text(t)
+    # two references interleaved
+    t = []
+    for k in range(0, 80, 2):
+        a, b = dict(mapped[k]), dict(mapped[k + 1])
+        if k % 3 == 0:
+            a['rname'] = b['rname'] = 'HIV1B-gag-seed'
+        t += [a, b]
+    cases['two_refs'] = text(t)
+    return cases
+
+
+def gen_s2a():
+    import gzip
+    refharness.setup()
+    from micall.core import sam2aln as ref_s2a
+    real = ref_s2a.sam2aln
+    records = []
+
+    def recorder(remap_csv, aligned_csv, insert_csv=None, failed_csv=None, nthreads=None):
+        text = remap_csv.read()
+        remap_csv.seek(0)
+        real(remap_csv, aligned_csv, insert_csv, failed_csv, nthreads)
+        records.append(dict(source='micall/tests/sam2aln_test.py', remap_csv=text,
+                            aligned=aligned_csv.getvalue(),
+                            insert=insert_csv.getvalue() if insert_csv else None,
+                            failed=failed_csv.getvalue() if failed_csv else None))
+    import micall.tests.sam2aln_test as st
+    st.sam2aln = recorder
+    _run_suite(st)
+    st.sam2aln = real
+    n_tests = len(records)
+
+    def run(text):
+        al, ins, fa = io.StringIO(), io.StringIO(), io.StringIO()
+        real(io.StringIO(text), al, ins, fa)
+        return al.getvalue(), ins.getvalue(), fa.getvalue()
+
+    for name, text in _s2a_edge_texts().items():
+        al, ins, fa = run(text)
+        records.append(dict(source='edge case ' + name, remap_csv=text, aligned=al, insert=ins,
+                            failed=fa))
+    with open(os.path.join(HERE, 'sam2aln_e2e.json'), 'w') as f:
+        json.dump(dict(source='reference micall.core.sam2aln.sam2aln outputs', cases=records), f,
+                  indent=0)
+    for case in sorted(os.listdir(os.path.join(HERE, 'e2e'))):
+        d = os.path.join(HERE, 'e2e', case)
+        with gzip.open(os.path.join(d, 'remap.csv.gz'), 'rt') as f:
+            text = f.read()
+        for name, body in zip(('aligned.csv', 'insert.csv', 'failed.csv'), run(text)):
+            with gzip.open(os.path.join(d, name + '.gz'), 'wt') as f:
+                f.write(body)
+    print('s2a: {} calls ({} from sam2aln_test)'.format(len(records), n_tests))
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['gotoh', 'pileup', 'sam2aln', 'e2e']
+    which = sys.argv[1:] or ['gotoh', 'pileup', 'sam2aln', 'e2e', 's2a']
     for w in which:
         globals()['gen_' + w]()
