@@ -162,6 +162,7 @@ def bench_sam2aln(args):
     t1 = time.perf_counter()
     outs = {w: ctx.sam2aln_output(w) for w in ('aligned', 'insert', 'failed')}
     t_out = time.perf_counter() - t1
+    host_ms = ctx.sam2aln_timing()
     st = ctx.sam2aln_stats()
     merge_ms, merge_n = kern['k_s2a_merge']
     avg_s = merge_ms / 1e3 / max(merge_n, 1)
@@ -191,6 +192,10 @@ def bench_sam2aln(args):
         'device_ms_per_step': round(dev_ms, 3),
         'device_pairs_per_s': round(st[0] / (dev_ms / 1e3), 1) if dev_ms > 0 else None,
         'output_format_ms': round(1e3 * t_out, 1),
+        'host_ms_last_step': {'parse': round(host_ms[0], 1), 'device_call': round(host_ms[1], 1),
+                              'format_aligned': round(host_ms[2], 1),
+                              'format_insert': round(host_ms[3], 1),
+                              'format_failed': round(host_ms[4], 1)},
         'roofline': {'kernel': 'k_s2a_merge', 'bound': 'hbm', 'achieved': round(achieved, 3),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 6),
                      'traffic': None, 'algo_bytes_per_launch': algo,

@@ -212,6 +212,10 @@ int mh_sam2aln_output(mh_ctx *ctx, int which, char *buf, size_t cap, size_t *use
 /* out[0] pairs, out[1] pairs merged on the device, out[2] distinct merged
  * sequences, out[3] failed pairs. */
 int mh_sam2aln_stats(mh_ctx *ctx, int64_t *out4);
+/* Host wall time (ms) of the last call: [0] CSV parse + matchmaker, [1]
+ * upload + device merge/group + fetch, [2..4] formatting of the three
+ * outputs (0 until formatted). */
+int mh_sam2aln_timing(mh_ctx *ctx, double *ms5);
 
 /* ---- Gotoh: replaces _gotoh2.align (_gotoh2.c:544-607) ---------------- */
 /* seq1/seq2 already cleaned (gotoh2.py:70-72).  out1/out2 need

@@ -18,66 +18,25 @@
 //   k_s2a_gather  distinct sequences copied out for the host's sort
 // Bit-for-bit specification: the reference itself (tests/golden/e2e/*/aligned.csv
 // etc. were produced by running micall.core.sam2aln on the same remap.csv).
-#include <algorithm>
-#include <cstdio>
-#include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <string>
-#include <unordered_map>
 #include <vector>
 
-#include "mh_internal.h"
-#include "mh_text.h"
+#include "mh_sam2aln.h"
 
 namespace mh {
-
-enum { S2A_OK = 0, S2A_UNMATCHED = 1, S2A_BADCIGAR = 2, S2A_2REFS = 3, S2A_MANYNS = 4,
-       S2A_EMPTY = 5 };
-static const char *const S2A_CAUSE[] = {"", "unmatched", "badCigar", "2refs", "manyNs", ""};
-
-struct S2AState {
-    // host rows of the last remap.csv
-    std::vector<std::string> qname, rname;
-    std::vector<int32_t> flag, pos, name_id;
-    std::vector<std::string> cigar_txt;
-    std::string seq, qual;                  // concatenated
-    std::vector<int64_t> soff;
-    std::vector<int32_t> slen;
-    std::vector<int32_t> cig_off, n_cig;
-    std::vector<uint32_t> cig;
-    // units in matchmaker order
-    std::vector<int64_t> u1, u2;            // rows; u2 = -1 for None
-    std::vector<int32_t> ucause;            // host-decided cause, or -1 = merged on device
-    std::vector<int32_t> upaired;           // is_paired of row1
-    std::vector<int64_t> merge_of_unit;     // index into the device merge list, -1 if none
-    std::vector<std::string> names;         // rname ids (first seen over units)
-    int q_cutoff = 15;
-    // device
-    uint8_t *d_seq = nullptr, *d_qual = nullptr, *d_out = nullptr, *d_gather = nullptr;
-    int64_t *d_soff = nullptr, *d_units = nullptr, *d_slot = nullptr, *d_goff = nullptr;
-    int32_t *d_slen = nullptr, *d_pos = nullptr, *d_cigoff = nullptr, *d_ncig = nullptr,
-            *d_uref = nullptr, *d_res = nullptr, *d_tcnt = nullptr, *d_trep = nullptr,
-            *d_uniq = nullptr, *d_ctr = nullptr;
-    uint32_t *d_cig = nullptr;
-    uint64_t *d_h = nullptr, *d_tkey = nullptr;
-    // results of the device pass
-    int64_t n_merge = 0, n_unique = 0;
-    std::vector<int32_t> res;               // per merge unit: status, offset, body_len, strip_len
-    std::vector<int32_t> uniq;              // rep merge unit, count
-    std::vector<int64_t> uniq_off;          // offsets into gathered
-    std::string gathered;                   // bodies of the distinct sequences
-};
 
 static void s2a_free_device(S2AState &S)
 {
     hipFree(S.d_seq); hipFree(S.d_qual); hipFree(S.d_out); hipFree(S.d_gather);
     hipFree(S.d_soff); hipFree(S.d_units); hipFree(S.d_slot); hipFree(S.d_goff);
-    hipFree(S.d_slen); hipFree(S.d_pos); hipFree(S.d_cigoff); hipFree(S.d_ncig);
+    hipFree(S.d_pos); hipFree(S.d_cigoff); hipFree(S.d_ncig);
     hipFree(S.d_uref); hipFree(S.d_res); hipFree(S.d_tcnt); hipFree(S.d_trep);
     hipFree(S.d_uniq); hipFree(S.d_ctr); hipFree(S.d_cig); hipFree(S.d_h); hipFree(S.d_tkey);
     S.d_seq = S.d_qual = S.d_out = S.d_gather = nullptr;
     S.d_soff = S.d_units = S.d_slot = S.d_goff = nullptr;
-    S.d_slen = S.d_pos = S.d_cigoff = S.d_ncig = S.d_uref = S.d_res = S.d_tcnt = S.d_trep =
+    S.d_pos = S.d_cigoff = S.d_ncig = S.d_uref = S.d_res = S.d_tcnt = S.d_trep =
         S.d_uniq = S.d_ctr = nullptr;
     S.d_cig = nullptr;
     S.d_h = S.d_tkey = nullptr;
@@ -97,7 +56,7 @@ void s2a_free(Ctx &c)
 struct S2AArgs {
     const uint8_t *seq, *qual;
     const int64_t *soff;
-    const int32_t *slen, *pos, *cig_off, *n_cig;
+    const int32_t *pos, *cig_off, *n_cig;
     const uint32_t *cig;
     const int64_t *units;     // per merge unit: row1, row2 (-1: single)
     const int32_t *uref;
@@ -432,150 +391,18 @@ static int s2a_upload(T *&dst, const std::vector<T> &v, hipStream_t s)
     return 0;
 }
 
+static int s2a_upload_bytes(uint8_t *&dst, const std::string &v, hipStream_t s)
+{
+    hipFree(dst);
+    dst = nullptr;
+    MH_HIP(hipMalloc(&dst, v.size() > 0 ? v.size() : 1));
+    if (!v.empty()) MH_HIP(hipMemcpyAsync(dst, v.data(), v.size(), hipMemcpyHostToDevice, s));
+    return 0;
+}
+
 // apply_cigar's checks on one row (sam2aln.py:113-151): the regex, the
 // supported ops and the read length; the reference raises RuntimeError.
-static int s2a_check_row(const S2AState &S, int64_t r)
-{
-    const std::string &cg = S.cigar_txt[r];
-    size_t i = 0;
-    int64_t left = 0;
-    const int64_t L = S.slen[r];
-    // validity first (the regex runs before any token is applied)
-    while (i < cg.size()) {
-        size_t j = i;
-        while (j < cg.size() && cg[j] >= '0' && cg[j] <= '9') ++j;
-        if (j == i || j >= cg.size() || !strchr("MIDNSHPX=", cg[j])) {
-            set_error("Invalid CIGAR string: '%s'.", cg.c_str());
-            return -3;
-        }
-        i = j + 1;
-    }
-    i = 0;
-    while (i < cg.size()) {
-        size_t j = i;
-        int64_t n = 0;
-        while (cg[j] >= '0' && cg[j] <= '9') { n = n * 10 + (cg[j] - '0'); ++j; }
-        const char op = cg[j];
-        if (op == 'M' || op == 'I' || op == 'S') left += n;
-        else if (op != 'D') {
-            set_error("Unsupported CIGAR token: '%lld%c'.", (long long)n, op);
-            return -3;
-        }
-        if (left > L) {
-            set_error("CIGAR string '%s' is too long for sequence.", cg.c_str());
-            return -3;
-        }
-        i = j + 1;
-    }
-    if (left < L) {
-        set_error("CIGAR string '%s' is too short for sequence.", cg.c_str());
-        return -3;
-    }
-    if (S.pos[r] == INT32_MIN) {
-        set_error("invalid pos in remap.csv row %lld", (long long)r);
-        return -3;
-    }
-    return 0;
-}
-
-static int s2a_parse(S2AState &S, const char *text, int64_t len)
-{
-    S.qname.clear(); S.rname.clear(); S.flag.clear(); S.pos.clear(); S.name_id.clear();
-    S.cigar_txt.clear(); S.seq.clear(); S.qual.clear(); S.soff.clear(); S.slen.clear();
-    S.cig_off.clear(); S.n_cig.clear(); S.cig.clear();
-    S.u1.clear(); S.u2.clear(); S.ucause.clear(); S.upaired.clear(); S.merge_of_unit.clear();
-    S.names.clear();
-    const char *p = text, *end = text + len;
-    std::vector<std::string> f;
-    if (!csv_record(p, end, f)) {
-        set_error("remap csv: empty");
-        return -3;
-    }
-    const char *want[11] = {"qname", "flag", "rname", "pos", "mapq", "cigar", "rnext", "pnext",
-                            "tlen", "seq", "qual"};
-    int col[11];
-    for (int k = 0; k < 11; ++k) {
-        col[k] = -1;
-        for (size_t z = 0; z < f.size(); ++z) if (f[z] == want[k]) col[k] = (int)z;
-        if (col[k] < 0 && (k == 0 || k == 1 || k == 2 || k == 3 || k == 5 || k == 9 || k == 10)) {
-            set_error("remap csv: missing column %s", want[k]);
-            return -3;
-        }
-    }
-    std::unordered_map<std::string, int64_t> cached;    // qname -> index into pend
-    std::vector<std::pair<int64_t, bool>> pend;         // dict insertion order
-    std::vector<uint32_t> ops;
-    while (csv_record(p, end, f)) {
-        if (f.size() == 1 && f[0].empty()) continue;     // blank line: DictReader skips it
-        if ((int)f.size() < 11) {
-            set_error("remap csv: short row %lld", (long long)S.flag.size() + 1);
-            return -3;
-        }
-        const int64_t row = (int64_t)S.flag.size();
-        S.qname.push_back(f[col[0]]);
-        S.flag.push_back(std::atoi(f[col[1]].c_str()));
-        S.rname.push_back(f[col[2]]);
-        {
-            const std::string &ps = f[col[3]];
-            char *e = nullptr;
-            const long v = std::strtol(ps.c_str(), &e, 10);
-            S.pos.push_back(ps.empty() || *e ? INT32_MIN : (int32_t)v);
-        }
-        S.cigar_txt.push_back(f[col[5]]);
-        const std::string &sq = f[col[9]], &ql = f[col[10]];
-        S.soff.push_back((int64_t)S.seq.size());
-        S.slen.push_back((int32_t)sq.size());
-        S.seq += sq;
-        std::string q = ql;
-        q.resize(sq.size(), '!');
-        S.qual += q;
-        int maxm = 0;
-        S.cig_off.push_back((int32_t)S.cig.size());
-        if (!parse_cigar_ops(f[col[5]], ops, maxm)) ops.clear();
-        S.cig.insert(S.cig.end(), ops.begin(), ops.end());
-        S.n_cig.push_back((int32_t)ops.size());
-        // matchmaker (sam2aln.py:291-312)
-        auto it = cached.find(f[col[0]]);
-        if (it == cached.end()) {
-            cached.emplace(f[col[0]], (int64_t)pend.size());
-            pend.push_back({row, true});
-        } else {
-            pend[it->second].second = false;
-            S.u1.push_back(pend[it->second].first);
-            S.u2.push_back(row);
-            cached.erase(it);
-        }
-    }
-    for (auto &o : pend) if (o.second) { S.u1.push_back(o.first); S.u2.push_back(-1); }
-    // parse_sam's early causes (sam2aln.py:340-348) and rname order
-    std::unordered_map<std::string, int> nid;
-    const int64_t nu = (int64_t)S.u1.size();
-    S.ucause.assign(nu, -1);
-    S.upaired.assign(nu, 0);
-    S.merge_of_unit.assign(nu, -1);
-    for (int64_t u = 0; u < nu; ++u) {
-        const int64_t r1 = S.u1[u], r2 = S.u2[u];
-        auto ins = nid.emplace(S.rname[r1], (int)S.names.size());
-        if (ins.second) S.names.push_back(S.rname[r1]);
-        const int paired = S.flag[r1] & 1;
-        S.upaired[u] = paired;
-        int cause = -1;
-        if (paired && r2 < 0) cause = S2A_UNMATCHED;
-        else if (S.cigar_txt[r1] == "*" || (r2 >= 0 && S.cigar_txt[r2] == "*")) cause = S2A_BADCIGAR;
-        else if (paired && S.rname[r1] != S.rname[r2]) cause = S2A_2REFS;
-        S.ucause[u] = cause;
-        if (cause < 0) {
-            if (int st = s2a_check_row(S, r1)) return st;
-            if (paired)
-                if (int st = s2a_check_row(S, r2)) return st;
-        }
-    }
-    S.name_id.assign(nu, 0);
-    for (int64_t u = 0; u < nu; ++u) S.name_id[u] = nid[S.rname[S.u1[u]]];
-    return 0;
-}
-
-static int s2a_run(Ctx &c, S2AState &S, double max_prop_n)
+int s2a_run(Ctx &c, S2AState &S, double max_prop_n)
 {
     hipStream_t s = c.stream;
     const int64_t nu = (int64_t)S.u1.size();
@@ -624,11 +451,9 @@ static int s2a_run(Ctx &c, S2AState &S, double max_prop_n)
         set_error("sam2aln: reference span %d too long for LDS", span_cap);
         return -3;
     }
-    std::vector<uint8_t> seqv(S.seq.begin(), S.seq.end()), qualv(S.qual.begin(), S.qual.end());
-    if (int st = s2a_upload(S.d_seq, seqv, s)) return st;
-    if (int st = s2a_upload(S.d_qual, qualv, s)) return st;
+    if (int st = s2a_upload_bytes(S.d_seq, S.seq, s)) return st;
+    if (int st = s2a_upload_bytes(S.d_qual, S.qual, s)) return st;
     if (int st = s2a_upload(S.d_soff, S.soff, s)) return st;
-    if (int st = s2a_upload(S.d_slen, S.slen, s)) return st;
     if (int st = s2a_upload(S.d_pos, S.pos, s)) return st;
     if (int st = s2a_upload(S.d_cigoff, S.cig_off, s)) return st;
     if (int st = s2a_upload(S.d_ncig, S.n_cig, s)) return st;
@@ -656,7 +481,7 @@ static int s2a_run(Ctx &c, S2AState &S, double max_prop_n)
     MH_HIP(hipMemsetAsync(S.d_tcnt, 0, sizeof(int32_t) * tsize, s));
     MH_HIP(hipMemsetAsync(S.d_trep, 0x7f, sizeof(int32_t) * tsize, s));
 
-    S2AArgs a{S.d_seq, S.d_qual, S.d_soff, S.d_slen, S.d_pos, S.d_cigoff, S.d_ncig, S.d_cig,
+    S2AArgs a{S.d_seq, S.d_qual, S.d_soff, S.d_pos, S.d_cigoff, S.d_ncig, S.d_cig,
               S.d_units, S.d_uref, S.d_slot, nm, S.q_cutoff, max_prop_n, span_cap, ops_cap,
               wave_bytes, S.d_out, S.d_res, S.d_h, S.d_ctr};
     int64_t blocks = (nm + wpb - 1) / wpb;
@@ -729,95 +554,6 @@ static int s2a_run(Ctx &c, S2AState &S, double max_prop_n)
     return 0;
 }
 
-// aligned.csv (sam2aln.py:465-478): per rname in first-seen order, the
-// distinct merged sequences sorted by (count, gap prefix, sequence), all
-// descending; seq written without its leading / trailing gaps.
-static void s2a_aligned(const S2AState &S, std::string &out)
-{
-    out = "refname,qcut,rank,count,offset,seq\n";
-    const int nn = (int)S.names.size();
-    std::vector<std::vector<int64_t>> by(nn);
-    std::vector<int32_t> mref(S.n_merge);
-    for (int64_t u = 0; u < (int64_t)S.u1.size(); ++u)
-        if (S.merge_of_unit[u] >= 0) mref[S.merge_of_unit[u]] = S.name_id[u];
-    for (int64_t k = 0; k < S.n_unique; ++k) by[mref[S.uniq[2 * k]]].push_back(k);
-    char num[64];
-    for (int r = 0; r < nn; ++r) {
-        auto &v = by[r];
-        if (v.empty()) continue;
-        std::sort(v.begin(), v.end(), [&](int64_t x, int64_t y) {
-            const int64_t rx = S.uniq[2 * x], ry = S.uniq[2 * y];
-            const int cx = S.uniq[2 * x + 1], cy = S.uniq[2 * y + 1];
-            if (cx != cy) return cx > cy;
-            const int ox = S.res[4 * rx + 1], oy = S.res[4 * ry + 1];
-            if (ox != oy) return ox > oy;
-            const int64_t lx = S.uniq_off[x + 1] - S.uniq_off[x], ly = S.uniq_off[y + 1] - S.uniq_off[y];
-            const int cmp = memcmp(S.gathered.data() + S.uniq_off[x], S.gathered.data() + S.uniq_off[y],
-                                   (size_t)std::min(lx, ly));
-            if (cmp != 0) return cmp > 0;
-            return lx > ly;
-        });
-        std::string ref;
-        csv_field(ref, S.names[r].data(), S.names[r].size());
-        for (size_t rank = 0; rank < v.size(); ++rank) {
-            const int64_t k = v[rank], rep = S.uniq[2 * k];
-            out += ref;
-            snprintf(num, sizeof num, ",%d,%zu,%d,%d,", S.q_cutoff, rank, S.uniq[2 * k + 1],
-                     S.res[4 * rep + 1]);
-            out += num;
-            out.append(S.gathered.data() + S.uniq_off[k], (size_t)S.res[4 * rep + 3]);
-            out.push_back('\n');
-        }
-    }
-}
-
-// insert.csv rows of parse_sam (sam2aln.py:357-380): every I op of the
-// mates of a unit that reached apply_cigar, keyed by pos - 1 + read offset.
-static void s2a_inserts(const S2AState &S, std::string &out)
-{
-    out = "qname,fwd_rev,refname,pos,insert,qual\n";
-    char num[32];
-    for (int64_t u = 0; u < (int64_t)S.u1.size(); ++u) {
-        if (S.ucause[u] >= 0) continue;
-        const int64_t r1 = S.u1[u];
-        for (int k = 0; k < (S.upaired[u] ? 2 : 1); ++k) {
-            const int64_t r = k ? S.u2[u] : r1;
-            int64_t left = 0;
-            for (int o = 0; o < S.n_cig[r]; ++o) {
-                const uint32_t op = S.cig[S.cig_off[r] + o];
-                const int n = (int)(op >> 4), t = (int)(op & 15);
-                if (t == MH_OP_I) {
-                    csv_field(out, S.qname[r1].data(), S.qname[r1].size());
-                    out += (S.flag[r] & 0x40) ? ",F," : ",R,";
-                    csv_field(out, S.rname[r1].data(), S.rname[r1].size());
-                    snprintf(num, sizeof num, ",%lld,", (long long)(S.pos[r] - 1 + left));
-                    out += num;
-                    csv_field(out, S.seq.data() + S.soff[r] + left, (size_t)n);
-                    out.push_back(',');
-                    csv_field(out, S.qual.data() + S.soff[r] + left, (size_t)n);
-                    out.push_back('\n');
-                }
-                if (t == MH_OP_M || t == MH_OP_I || t == MH_OP_S) left += n;
-            }
-        }
-    }
-}
-
-static void s2a_failed(const S2AState &S, std::string &out)
-{
-    out = "qname,cause\n";
-    for (int64_t u = 0; u < (int64_t)S.u1.size(); ++u) {
-        int cause = S.ucause[u];
-        if (cause < 0 && S.res[4 * S.merge_of_unit[u]] == S2A_MANYNS) cause = S2A_MANYNS;
-        if (cause < 0) continue;
-        const std::string &q = S.qname[S.u1[u]];
-        csv_field(out, q.data(), q.size());
-        out.push_back(',');
-        out += S2A_CAUSE[cause];
-        out.push_back('\n');
-    }
-}
-
 }  // namespace mh
 
 using namespace mh;
@@ -833,14 +569,21 @@ extern "C" int mh_sam2aln_csv(mh_ctx *ctx, const char *text, int64_t len, int q_
     S.q_cutoff = q_cutoff;
     S.n_merge = S.n_unique = 0;
     S.res.clear();
+    for (auto &o : S.out_cache) o.clear();
+    S.out_valid = 0;
+    auto t0 = std::chrono::steady_clock::now();
     if (int st = s2a_parse(S, text ? text : "", len)) {
         S.u1.clear();
         return st;
     }
+    auto t1 = std::chrono::steady_clock::now();
     if (int st = s2a_run(c, S, max_prop_n)) {
         S.u1.clear();
         return st;
     }
+    auto t2 = std::chrono::steady_clock::now();
+    S.t_parse = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    S.t_device = std::chrono::duration<double, std::milli>(t2 - t1).count();
     if (n_units) *n_units = (int64_t)S.u1.size();
     return 0;
 }
@@ -851,14 +594,32 @@ extern "C" int mh_sam2aln_output(mh_ctx *ctx, int which, char *buf, size_t cap, 
     Ctx &c = *ctx_of(ctx);
     if (!c.s2a) { set_error("mh_sam2aln_output: no sam2aln results"); return -3; }
     S2AState &S = *c.s2a;
-    std::string out;
-    if (which == 0) s2a_aligned(S, out);
-    else if (which == 1) s2a_inserts(S, out);
-    else s2a_failed(S, out);
+    std::string &out = S.out_cache[which];
+    if (!(S.out_valid & (1 << which))) {
+        auto t0 = std::chrono::steady_clock::now();
+        s2a_format(S, which, out);
+        S.t_format[which] = std::chrono::duration<double, std::milli>(
+                                std::chrono::steady_clock::now() - t0).count();
+        S.out_valid |= 1 << which;
+    }
     *used = out.size();
     if (!buf) return 0;
     if (cap < out.size()) { set_error("mh_sam2aln_output: buffer too small"); return -2; }
     memcpy(buf, out.data(), out.size());
+    std::string().swap(out);          // handed over: free the cached text
+    S.out_valid &= ~(1 << which);
+    return 0;
+}
+
+extern "C" int mh_sam2aln_timing(mh_ctx *ctx, double *ms5)
+{
+    if (!ctx || !ms5) return -3;
+    Ctx &c = *ctx_of(ctx);
+    if (!c.s2a) { set_error("mh_sam2aln_timing: no sam2aln results"); return -3; }
+    const S2AState &S = *c.s2a;
+    ms5[0] = S.t_parse;
+    ms5[1] = S.t_device;
+    for (int k = 0; k < 3; ++k) ms5[2 + k] = S.t_format[k];
     return 0;
 }
 

@@ -97,6 +97,7 @@ def _declare(L):
         'mh_sam2aln_output': ([_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
                                ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         'mh_sam2aln_stats': ([_P, _P], ctypes.c_int),
+        'mh_sam2aln_timing': ([_P, _P], ctypes.c_int),
         'mh_profile': ([_P, ctypes.c_int], ctypes.c_int),
         'mh_profile_get': ([_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _I64P],
                            ctypes.c_int),
@@ -197,10 +198,19 @@ class Context:
         w = {'aligned': 0, 'insert': 1, 'failed': 2}[which]
         used = ctypes.c_size_t()
         check(lib().mh_sam2aln_output(self.h, w, None, 0, ctypes.byref(used)), 'mh_sam2aln_output')
-        buf = ctypes.create_string_buffer(used.value + 1)
-        check(lib().mh_sam2aln_output(self.h, w, buf, used.value + 1, ctypes.byref(used)),
+        buf = bytearray(used.value)
+        cbuf = (ctypes.c_char * max(len(buf), 1)).from_buffer(buf) if buf else None
+        check(lib().mh_sam2aln_output(self.h, w, cbuf, len(buf), ctypes.byref(used)),
               'mh_sam2aln_output')
-        return buf.raw[:used.value].decode()
+        del cbuf
+        return buf.decode()
+
+    def sam2aln_timing(self):
+        """Host ms of the last sam2aln: parse, device, and formatting of
+        aligned / insert / failed."""
+        out = np.zeros(5, dtype=np.float64)
+        check(lib().mh_sam2aln_timing(self.h, _ptr(out)), 'mh_sam2aln_timing')
+        return [float(x) for x in out]
 
     def sam2aln_stats(self):
         """(pairs, merged on the device, distinct merged sequences, failed)."""
