@@ -210,6 +210,95 @@ def bench_sam2aln(args):
     ctx.close()
 
 
+def _fastq_text(reads, quals, mate, tiles=8):
+    """FASTQ text of one mate's reads with Illumina headers over `tiles` tiles."""
+    n = reads.shape[0]
+    out = []
+    for i in range(n):
+        out.append('@M00000:1:000000000-AAAAA:1:{}:{}:{} {}:N:0:1\n{}\n+\n{}\n'.format(
+            1101 + i % tiles, 1000 + i // 1000, 1000 + i % 1000, mate,
+            reads[i].tobytes().decode(), quals[i].tobytes().decode()))
+    return ''.join(out).encode()
+
+
+def bench_censor(args):
+    """censor_fastq.censor (mh_censor_fastq) of the C2 R1 file (gzip in and
+    out) with ~2 % bad (tile, cycle) pairs (BASELINE config C5's censor
+    shape), and the FASTQ ingest of the pair (mh_reads_load_fastq)."""
+    import gzip
+    import random
+    import tempfile
+    import og_censor
+    from micall_amd import _native, synth, projects
+    pol = projects.load_default().seed_sequences()['HIV1B-pol-seed']
+    d = synth.make_pairs(args.pairs, genomes={'HIV1B-pol-seed': pol}, genome_seed=SEED,
+                         read_seed=SEED, block=0, read_len=READ_LEN)
+    raw1 = _fastq_text(d['r1'], d['q1'], 1)
+    raw2 = _fastq_text(d['r2'], d['q2'], 2)
+    gz1 = gzip.compress(raw1, compresslevel=1)
+    gz2 = gzip.compress(raw2, compresslevel=1)
+    rng = random.Random(SEED)
+    bad = sorted({(str(1101 + t), c) for t in range(8) for c in range(1, READ_LEN + 1)
+                  if rng.random() < 0.02})
+    ctx = _native.Context(0)
+    for _ in range(args.warmup):
+        ctx.censor_fastq(gz1, bad, True, True)
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, n_bases, total = ctx.censor_fastq(gz1, bad, True, True)
+    elapsed = time.perf_counter() - t0
+    host_ms = ctx.censor_timing()
+    k_ms, k_n = ctx.profile_get('k_censor')
+    avg_s = k_ms / 1e3 / max(k_n, 1)
+    # algorithmic bytes per launch: read and write every base and quality
+    # byte once (the kernel censors in place), 16 B of spans per record
+    algo = 2 * 2 * READ_LEN * args.pairs + 16 * args.pairs
+    achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
+    # FASTQ ingest of the pair (what prelim_map does first)
+    tmp = tempfile.mkdtemp(prefix='bench_fq_')
+    p1, p2 = os.path.join(tmp, 'R1.fastq.gz'), os.path.join(tmp, 'R2.fastq.gz')
+    with open(p1, 'wb') as f:
+        f.write(gz1)
+    with open(p2, 'wb') as f:
+        f.write(gz2)
+    t1 = time.perf_counter()
+    ctx.reads_load_fastq(p1, p2)
+    ingest_s = time.perf_counter() - t1
+    sample = min(20000, args.pairs)
+    stext = b'\n'.join(raw1.split(b'\n', 4 * sample)[:4 * sample]) + b'\n'
+    t2 = time.perf_counter()
+    og_censor.censor_bytes(stext, set(bad))
+    cpu_s = time.perf_counter() - t2
+    res = {
+        'metric': 'censor reads/sec (FASTQ.gz in -> censored FASTQ.gz out)',
+        'value': round(args.pairs * args.steps / elapsed, 1), 'unit': 'reads/s', 'n_gpus': 1,
+        'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(1e3 * elapsed / args.steps, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
+        'config': {'workload': 'censor of the C2 R1 file (1M synthetic 2x251 reads over 8 tiles, '
+                               'gzip level 1 in, level 6 out), 2 % bad tile-cycles',
+                   'reads': args.pairs, 'bad_cycles': len(bad), 'fastq_bytes': len(raw1),
+                   'gz_bytes': len(gz1)},
+        'host_ms_last_step': {'gunzip_split': round(host_ms[0], 1),
+                              'device_call': round(host_ms[1], 1),
+                              'rewrite_gzip': round(host_ms[2], 1)},
+        'ingest_pair_s': round(ingest_s, 3),
+        'ingest_reads_per_s': round(2 * args.pairs / ingest_s, 1),
+        'roofline': {'kernel': 'k_censor', 'bound': 'hbm', 'achieved': round(achieved, 3),
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 6),
+                     'traffic': None, 'algo_bytes_per_launch': algo,
+                     'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': k_n},
+        'cpu_baseline': {'value': round(sample / cpu_s, 1), 'unit': 'reads/s', 'cores': 1,
+                         'kind': 'port',
+                         'sample': 'first {} reads of the same R1 (plain text) through the '
+                                   'pure-Python restatement oracle/og_censor.py, {:.1f} s'.format(
+                                       sample, cpu_s)},
+    }
+    print(json.dumps(res))
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split('\n\n')[0])
     ap.add_argument('--gpus', type=int, default=1)
@@ -220,12 +309,15 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--breakdown', action='store_true',
                     help='time each pipeline stage (synchronising) and print it to stderr')
-    ap.add_argument('--stage', choices=('remap', 'sam2aln'), default='remap',
+    ap.add_argument('--stage', choices=('remap', 'sam2aln', 'censor'), default='remap',
                     help='remap: the headline hot path (default); sam2aln: the next stage '
-                         '(SURVEY.md 8(f)) over the remap.csv of one C2 pass')
+                         '(SURVEY.md 8(f)) over the remap.csv of one C2 pass; censor: the '
+                         'stage before (FASTQ censor of the C2 reads) plus the FASTQ ingest')
     args = ap.parse_args()
     if args.stage == 'sam2aln':
         return bench_sam2aln(args)
+    if args.stage == 'censor':
+        return bench_censor(args)
 
     import torch
     import torch.distributed as dist

@@ -29,7 +29,10 @@
  *          -> mh_gotoh_align;
  *   4. (next stage) sam2aln's Python merge of remap.csv,
  *      micall/core/sam2aln.py:395-478
- *          -> mh_sam2aln_csv, mh_sam2aln_output.
+ *          -> mh_sam2aln_csv, mh_sam2aln_output;
+ *   5. (the stage before) censor_fastq.censor's per-base
+ *      Python loop, micall/core/censor_fastq.py:32-102
+ *          -> mh_censor_fastq, mh_censor_output.
  *
  * Conventions: every function returns 0 on success, -1 on traceback failure
  * (mh_gotoh_align only), -2 on out-of-memory, -3 on a bad argument, -4 on a
@@ -216,6 +219,23 @@ int mh_sam2aln_stats(mh_ctx *ctx, int64_t *out4);
  * upload + device merge/group + fetch, [2..4] formatting of the three
  * outputs (0 until formatted). */
 int mh_sam2aln_timing(mh_ctx *ctx, double *ms5);
+
+/* ---- censor: replaces censor_fastq.censor (censor_fastq.py:32-102) ---- */
+/* One FASTQ file (src, gzip when src_gzip) censored on the device: bases /
+ * qualities at the bad (tile, cycle) pairs (tiles[k], cycles[k]; negative
+ * cycles = reverse reads) become 'N' / '#', a trailing run of bad cycles is
+ * dropped as the reference drops it, header and '+' lines are kept
+ * verbatim.  *base_count / *score_sum = number and sum (Phred) of all
+ * quality characters, for the summary row (:94-102).  The censored file
+ * (gzip when dst_gzip: independent deflate members, level 6) is then
+ * copied out with mh_censor_output (buf NULL: *used = size). */
+int mh_censor_fastq(mh_ctx *ctx, const uint8_t *src, int64_t len, int src_gzip, int n_bad,
+                    const char *const *tiles, const int32_t *cycles, int dst_gzip,
+                    int64_t *base_count, int64_t *score_sum);
+int mh_censor_output(mh_ctx *ctx, char *buf, size_t cap, size_t *used);
+/* Host wall ms of the last call: [0] gunzip + record split, [1] upload +
+ * k_censor + download, [2] rewrite + gzip. */
+int mh_censor_timing(mh_ctx *ctx, double *ms3);
 
 /* ---- Gotoh: replaces _gotoh2.align (_gotoh2.c:544-607) ---------------- */
 /* seq1/seq2 already cleaned (gotoh2.py:70-72).  out1/out2 need

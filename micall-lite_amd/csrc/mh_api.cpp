@@ -11,6 +11,8 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <functional>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -31,6 +33,8 @@ void set_error(const char *fmt, ...)
     vsnprintf(g_err, sizeof(g_err), fmt, ap);
     va_end(ap);
 }
+
+static std::string last_error_text() { return std::string(g_err); }
 
 int hip_fail(hipError_t e, const char *what)
 {
@@ -327,49 +331,114 @@ struct Fastq {
     std::vector<std::string> names;
     std::vector<uint8_t> seq, qual;
     std::vector<int32_t> len;
+    std::vector<int64_t> off;     // start of each read in seq / qual
 };
 
-static int read_fastq(const char *path, Fastq &fq, bool paired, int64_t *newlines = nullptr)
+int s2a_threads();   // mh_s2a_host.cpp: host worker count
+
+static void par_for(int nt, const std::function<void(int)> &fn)
 {
+    if (nt <= 1) { fn(0); return; }
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(fn, t);
+    fn(0);
+    for (auto &x : th) x.join();
+}
+
+// The whole (gzip or plain) file; gzread decodes concatenated members.
+static int slurp(const char *path, std::string &data)
+{
+    data.clear();
     gzFile f = gzopen(path, "rb");
     if (!f) { set_error("cannot open FASTQ %s", path); return -3; }
-    gzbuffer(f, 1 << 20);
-    std::string data;
-    std::vector<char> buf(1 << 22);
+    gzbuffer(f, 1 << 22);
+    FILE *raw = fopen(path, "rb");
+    if (raw) {
+        fseek(raw, 0, SEEK_END);
+        const long sz = ftell(raw);
+        fclose(raw);
+        if (sz > 0) data.reserve((size_t)sz * 3);
+    }
+    std::vector<char> buf(1 << 24);
     int got;
     while ((got = gzread(f, buf.data(), (unsigned)buf.size())) > 0) data.append(buf.data(), got);
     const bool err = got < 0;
     gzclose(f);
     if (err) { set_error("gzip error reading %s", path); return -3; }
-    if (newlines) *newlines = (int64_t)std::count(data.begin(), data.end(), '\n');
-    size_t p = 0, n = data.size();
-    auto line = [&](size_t &a, size_t &b) -> bool {
-        if (p >= n) return false;
-        a = p;
-        const void *nl = memchr(data.data() + p, '\n', n - p);
-        b = nl ? (size_t)((const char *)nl - data.data()) : n;
-        p = b + 1;
-        size_t e = b;
-        if (e > a && data[e - 1] == '\r') --e;
-        b = e;
-        return true;
-    };
-    size_t h0, h1, s0, s1, x0, x1, q0, q1;
-    while (line(h0, h1)) {
-        if (h1 == h0) continue;
-        if (!line(s0, s1) || !line(x0, x1) || !line(q0, q1)) {
-            set_error("truncated FASTQ record in %s", path);
-            return -3;
-        }
-        if (s1 - s0 > (size_t)MAXLEN) { set_error("read longer than %d in %s", MAXLEN, path); return -3; }
-        fq.names.push_back(qname_of(data.data() + h0, h1 - h0, paired));
-        fq.seq.insert(fq.seq.end(), data.begin() + s0, data.begin() + s1);
-        std::string q(data.begin() + q0, data.begin() + q1);
-        q.resize(s1 - s0, 'I');
-        fq.qual.insert(fq.qual.end(), q.begin(), q.end());
-        fq.len.push_back((int32_t)(s1 - s0));
-    }
     return 0;
+}
+
+// FASTQ records of `data` (blank lines between records skipped), parsed
+// with the line scan and the per-record copies split over host threads.
+static int parse_fastq(const std::string &data, const char *path, Fastq &fq, bool paired,
+                       int64_t *newlines)
+{
+    const int64_t n = (int64_t)data.size();
+    const char *D = data.data();
+    const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 20) + 1));
+    std::vector<std::vector<int64_t>> ls(nt);
+    par_for(nt, [&](int t) {
+        const int64_t a = n * t / nt, b = n * (t + 1) / nt;
+        const char *p = D + a, *e = D + b;
+        while (p < e) {
+            const char *nl = (const char *)memchr(p, '\n', (size_t)(e - p));
+            if (!nl) break;
+            ls[t].push_back(nl - D);
+            p = nl + 1;
+        }
+    });
+    std::vector<int64_t> nlpos;
+    for (auto &v : ls) nlpos.insert(nlpos.end(), v.begin(), v.end());
+    if (newlines) *newlines = (int64_t)nlpos.size();
+    // line k spans [start_k, end_k) without '\n' / trailing '\r'
+    const int64_t nl = (int64_t)nlpos.size() + (nlpos.empty() || nlpos.back() + 1 < n ? 1 : 0);
+    auto lstart = [&](int64_t k) { return k == 0 ? (int64_t)0 : nlpos[k - 1] + 1; };
+    auto lend = [&](int64_t k) {
+        int64_t e = k < (int64_t)nlpos.size() ? nlpos[k] : n;
+        if (e > lstart(k) && D[e - 1] == '\r') --e;
+        return e;
+    };
+    std::vector<int64_t> rec;   // first line of each record
+    for (int64_t k = 0; k < nl;) {
+        if (lend(k) == lstart(k)) { ++k; continue; }
+        if (k + 3 >= nl) { set_error("truncated FASTQ record in %s", path); return -3; }
+        rec.push_back(k);
+        k += 4;
+    }
+    const int64_t nr = (int64_t)rec.size();
+    fq.len.resize(nr);
+    fq.off.resize(nr);
+    fq.names.resize(nr);
+    int64_t total = 0;
+    for (int64_t r = 0; r < nr; ++r) {
+        const int64_t L = lend(rec[r] + 1) - lstart(rec[r] + 1);
+        if (L > MAXLEN) { set_error("read longer than %d in %s", MAXLEN, path); return -3; }
+        fq.len[r] = (int32_t)L;
+        fq.off[r] = total;
+        total += L;
+    }
+    fq.seq.resize((size_t)total);
+    fq.qual.resize((size_t)total);
+    par_for(nt, [&](int t) {
+        for (int64_t r = nr * t / nt; r < nr * (t + 1) / nt; ++r) {
+            const int64_t k = rec[r];
+            fq.names[r] = qname_of(D + lstart(k), (size_t)(lend(k) - lstart(k)), paired);
+            const int64_t L = fq.len[r];
+            memcpy(&fq.seq[fq.off[r]], D + lstart(k + 1), (size_t)L);
+            const int64_t q0 = lstart(k + 3), ql = lend(k + 3) - q0;
+            const int64_t c = std::min(L, ql);
+            if (c > 0) memcpy(&fq.qual[fq.off[r]], D + q0, (size_t)c);
+            for (int64_t x = c; x < L; ++x) fq.qual[fq.off[r] + x] = 'I';
+        }
+    });
+    return 0;
+}
+
+static int read_fastq(const char *path, Fastq &fq, bool paired, int64_t *newlines = nullptr)
+{
+    std::string data;
+    if (int st = slurp(path, data)) return st;
+    return parse_fastq(data, path, fq, paired, newlines);
 }
 
 }  // namespace mh
@@ -451,6 +520,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipFree(P.sel);
     hipFree(c->len_tab);
     s2a_free(*c);
+    censor_free(*c);
     hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -536,39 +606,53 @@ int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64
     const bool paired = path2 != nullptr;
     Fastq a, b;
     int64_t lines1 = 0;
-    if (int st = read_fastq(path1, a, paired, &lines1)) return st;
+    int st2 = 0;
+    std::string err2;
+    // the two files are decoded concurrently (gzip inflate is serial per file)
+    std::thread t2;
+    if (paired)
+        t2 = std::thread([&]() {
+            st2 = read_fastq(path2, b, paired);
+            if (st2) err2 = last_error_text();
+        });
+    const int st1 = read_fastq(path1, a, paired, &lines1);
+    if (paired) t2.join();
+    if (st1) return st1;
+    if (st2) { set_error("%s", err2.c_str()); return st2; }
     std::vector<std::string> names;
     std::vector<uint8_t> seq, qual;
     std::vector<int64_t> off;
     std::vector<int32_t> len;
     if (paired) {
-        if (int st = read_fastq(path2, b, paired)) return st;
         if (a.len.size() != b.len.size()) {
             set_error("paired FASTQ files hold %zu and %zu reads", a.len.size(), b.len.size());
             return -3;
         }
-        int64_t pa = 0, pb = 0;
-        for (size_t i = 0; i < a.len.size(); ++i) {
-            off.push_back((int64_t)seq.size());
-            len.push_back(a.len[i]);
-            seq.insert(seq.end(), a.seq.begin() + pa, a.seq.begin() + pa + a.len[i]);
-            qual.insert(qual.end(), a.qual.begin() + pa, a.qual.begin() + pa + a.len[i]);
-            pa += a.len[i];
-            off.push_back((int64_t)seq.size());
-            len.push_back(b.len[i]);
-            seq.insert(seq.end(), b.seq.begin() + pb, b.seq.begin() + pb + b.len[i]);
-            qual.insert(qual.end(), b.qual.begin() + pb, b.qual.begin() + pb + b.len[i]);
-            pb += b.len[i];
-            names.push_back(a.names[i]);
-            names.push_back(b.names[i]);
+        const int64_t np = (int64_t)a.len.size();
+        off.resize(2 * np);
+        len.resize(2 * np);
+        names.resize(2 * np);
+        int64_t total = 0;
+        for (int64_t i = 0; i < np; ++i) {
+            off[2 * i] = total; len[2 * i] = a.len[i]; total += a.len[i];
+            off[2 * i + 1] = total; len[2 * i + 1] = b.len[i]; total += b.len[i];
         }
+        seq.resize((size_t)total);
+        qual.resize((size_t)total);
+        const int nt = std::max(1, std::min(s2a_threads(), (int)(np >> 14) + 1));
+        par_for(nt, [&](int t) {
+            for (int64_t i = np * t / nt; i < np * (t + 1) / nt; ++i) {
+                memcpy(&seq[off[2 * i]], &a.seq[a.off[i]], (size_t)a.len[i]);
+                memcpy(&qual[off[2 * i]], &a.qual[a.off[i]], (size_t)a.len[i]);
+                memcpy(&seq[off[2 * i + 1]], &b.seq[b.off[i]], (size_t)b.len[i]);
+                memcpy(&qual[off[2 * i + 1]], &b.qual[b.off[i]], (size_t)b.len[i]);
+                names[2 * i].swap(a.names[i]);
+                names[2 * i + 1].swap(b.names[i]);
+            }
+        });
     } else {
-        int64_t pa = 0;
-        for (size_t i = 0; i < a.len.size(); ++i) {
-            off.push_back(pa);
-            len.push_back(a.len[i]);
-            pa += a.len[i];
-        }
+        off.swap(a.off);
+        len.swap(a.len);
         seq.swap(a.seq);
         qual.swap(a.qual);
         names.swap(a.names);

@@ -167,7 +167,8 @@ struct ProfPending {
     hipEvent_t a, b;
 };
 
-struct S2AState;   // mh_sam2aln.hip
+struct S2AState;      // mh_sam2aln.h
+struct CensorState;   // mh_censor.hip
 
 struct Ctx {
     int device = 0;
@@ -187,12 +188,14 @@ struct Ctx {
     int32_t *len_tab = nullptr;      // [3][MAXLEN + 1]
     int dp_fast = 1;                 // option "dp_fast": exact ungapped fast path of k_dp
     S2AState *s2a = nullptr;         // sam2aln rows and results (mh_sam2aln_csv)
+    CensorState *censor = nullptr;   // censored FASTQ of the last mh_censor_fastq
     int len_tab_mode = -1;
 };
 
 void set_error(const char *fmt, ...);
 Ctx *ctx_of(mh_ctx *ctx);          // the context behind a C-ABI handle
 void s2a_free(Ctx &c);
+void censor_free(Ctx &c);
 // bracket one kernel launch on c.stream when profiling is on
 int prof_begin(Ctx &c, const char *name);
 void prof_end(Ctx &c, int slot);

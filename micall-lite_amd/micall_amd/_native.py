@@ -98,6 +98,12 @@ def _declare(L):
                                ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         'mh_sam2aln_stats': ([_P, _P], ctypes.c_int),
         'mh_sam2aln_timing': ([_P, _P], ctypes.c_int),
+        'mh_censor_fastq': ([_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                             ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_int, _I64P, _I64P],
+                            ctypes.c_int),
+        'mh_censor_output': ([_P, ctypes.c_char_p, ctypes.c_size_t,
+                              ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        'mh_censor_timing': ([_P, _P], ctypes.c_int),
         'mh_profile': ([_P, ctypes.c_int], ctypes.c_int),
         'mh_profile_get': ([_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _I64P],
                            ctypes.c_int),
@@ -204,6 +210,28 @@ class Context:
               'mh_sam2aln_output')
         del cbuf
         return buf.decode()
+
+    def censor_fastq(self, data, bad_cycles, src_gzip, dst_gzip):
+        """mh_censor_fastq: (censored bytes, base_count, score_sum) for FASTQ
+        bytes and [(tile, cycle)] bad cycles."""
+        tiles = (ctypes.c_char_p * max(len(bad_cycles), 1))(*[t.encode() for t, _ in bad_cycles])
+        cycles = np.array([c for _, c in bad_cycles] or [0], dtype=np.int32)
+        bc, ss = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().mh_censor_fastq(self.h, bytes(data), len(data), int(src_gzip), len(bad_cycles),
+                                    tiles, _ptr(cycles), int(dst_gzip), ctypes.byref(bc),
+                                    ctypes.byref(ss)), 'mh_censor_fastq')
+        used = ctypes.c_size_t()
+        check(lib().mh_censor_output(self.h, None, 0, ctypes.byref(used)), 'mh_censor_output')
+        buf = bytearray(used.value)
+        cbuf = (ctypes.c_char * max(len(buf), 1)).from_buffer(buf) if buf else None
+        check(lib().mh_censor_output(self.h, cbuf, len(buf), ctypes.byref(used)), 'mh_censor_output')
+        del cbuf
+        return bytes(buf), bc.value, ss.value
+
+    def censor_timing(self):
+        out = np.zeros(3, dtype=np.float64)
+        check(lib().mh_censor_timing(self.h, _ptr(out)), 'mh_censor_timing')
+        return [float(x) for x in out]
 
     def sam2aln_timing(self):
         """Host ms of the last sam2aln: parse, device, and formatting of

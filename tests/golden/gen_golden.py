@@ -23,6 +23,14 @@ itself produced for them.  Sections:
            e2e case's remap.csv: aligned.csv / insert.csv / failed.csv under
            tests/golden/sam2aln_e2e.json and tests/golden/e2e/<case>/.
 
+  censor   the reference's parse_interop.read_errors / write_phix_csv,
+           filter_quality.report_bad_cycles and censor_fastq.censor (the
+           stage before prelim_map) on a synthetic
+           ErrorMetricsOut.bin and synthetic multi-tile FASTQ files, run the
+           way bin/micall:90-126 chains them (R2 with the exhausted bad-cycle
+           reader), plus censor_fastq_test.py's scenarios:
+           tests/golden/censor/.
+
   e2e      the stock reference prelim_map() + remap() (nthreads=1, so its
            pileup runs without a process pool and is deterministic) with
            oracle/shim_bin/bowtie2 standing in for bowtie2, on small committed
@@ -403,6 +411,100 @@ def _s2a_edge_texts():
     return cases
 
 
+def gen_censor():
+    import base64
+    import csv
+    import gzip
+    import random
+    import struct
+    refharness.setup()
+    from micall.core.censor_fastq import censor
+    from micall.core.filter_quality import report_bad_cycles
+    from micall.core.parse_interop import read_errors, write_phix_csv
+    from micall_amd import projects, synth
+    out_dir = os.path.join(HERE, 'censor')
+    os.makedirs(out_dir, exist_ok=True)
+    rng = random.Random(7)
+    # -- synthetic ErrorMetricsOut.bin: 4 tiles, 2x251 + 2x8 cycles, ~3 % bad,
+    # some cycles missing, one tile absent
+    lengths = [251, 8, 8, 251]
+    recs = []
+    for tile in (1101, 1102, 1103, 2101):
+        for cycle in range(1, sum(lengths) + 1):
+            if rng.random() < 0.01:
+                continue
+            rate = rng.choice([0.1, 0.25, 0.5, 1.0, 2.0]) if rng.random() > 0.03 else 7.5 + rng.random() * 10
+            recs.append(struct.pack('<HHHfLLLLL', 1, tile, cycle, rate, 1, 2, 3, 4, 5))
+    rng.shuffle(recs)
+    binary = struct.pack('!BB', 3, 30) + b''.join(recs)
+
+    class Named(io.BytesIO):
+        name = 'ErrorMetricsOut.bin'
+    quality = io.StringIO()
+    summary = {}
+    write_phix_csv(quality, read_errors(Named(binary)), lengths, summary)
+    bad = io.StringIO()
+    tiles_csv = io.StringIO()
+    report_bad_cycles(io.StringIO(quality.getvalue()), bad, tiles_csv)
+    # -- synthetic FASTQ pair, tiles 1101-1104 (1104 has no metrics)
+    pol = projects.load_default().seed_sequences()['HIV1B-pol-seed']
+    pairs = synth.make_pairs(1500, genomes={'HIV1B-pol-seed': pol}, genome_seed=9, read_seed=10)
+    fq = {1: [], 2: []}
+    for i in range(pairs['n']):
+        tile = 1101 + i % 4
+        for mate, (r, q) in ((1, (pairs['r1'], pairs['q1'])), (2, (pairs['r2'], pairs['q2']))):
+            name = '@M01841:45:000000000-A5FEG:1:{}:{}:{} {}:N:0:9'.format(tile, 1000 + i, 2000 + i, mate)
+            fq[mate].append('{}\n{}\n+\n{}\n'.format(name, r[i].tobytes().decode(),
+                                                     q[i].tobytes().decode()))
+    raw = {m: ''.join(v).encode() for m, v in fq.items()}
+    results = {}
+    reader = csv.DictReader(io.StringIO(bad.getvalue()))
+
+    class WriteBytes(io.BytesIO):
+        mode = 'wb'        # GzipFile(fileobj=...) takes its mode from the file
+
+    class ReadBytes(io.BytesIO):
+        mode = 'rb'
+    for mate in (1, 2):
+        src = ReadBytes(gzip.compress(raw[mate]))
+        dest = WriteBytes()
+        summ = io.StringIO()
+        censor(src, reader, dest, use_gzip=True, summary_file=summ)   # R2: exhausted reader
+        results[mate] = (gzip.decompress(dest.getvalue()), summ.getvalue())
+    for mate in (1, 2):
+        with gzip.open(os.path.join(out_dir, 'R{}.fastq.gz'.format(mate)), 'wb') as f:
+            f.write(raw[mate])
+        with gzip.open(os.path.join(out_dir, 'R{}.censor.fastq.gz'.format(mate)), 'wb') as f:
+            f.write(results[mate][0])
+    # -- censor_fastq_test.py scenarios (its StringIO.StringIO set-up does
+    # not run on Python 3; the same texts through BytesIO)
+    one = (b'@M01841:45:000000000-A5FEG:1:1101:5296:13227 1:N:0:9\nACGT\n+\nAAAA\n')
+    rev = one.replace(b' 1:N', b' 2:N')
+    two = one + b'@M01841:45:000000000-A5FEG:1:1102:1234:12345 1:N:0:9\nTGCA\n+\nBBBB\n'
+    scen = [(one, []), (one, [('1101', '3')]), (one, [('1101', '3'), ('1101', '4')]),
+            (one, [('1102', '3')]), (rev, [('1101', '3')]), (rev, [('1101', '-3')]),
+            (two, [('1101', '2'), ('1102', '3')]), (b'', []),
+            (one.replace(b'AAAA', b'AACC'), [('1101', '3')]),
+            (one.replace(b'ACGT\n', b'ACGT  \r\n'), [('1101', '1'), ('1101', '4')]),
+            (two, [('1101', '1'), ('1101', '2'), ('1101', '3'), ('1101', '4')])]
+    cases = []
+    for text, bc in scen:
+        dest, summ = io.BytesIO(), io.StringIO()
+        censor(io.BytesIO(text), [dict(tile=t, cycle=c) for t, c in bc], dest, use_gzip=False,
+               summary_file=summ)
+        cases.append(dict(fastq=text.decode(), bad_cycles=bc, censored=dest.getvalue().decode(),
+                          summary=summ.getvalue()))
+    golden = dict(
+        source='reference micall.core parse_interop / filter_quality / censor_fastq outputs',
+        read_lengths=lengths, error_metrics_b64=base64.b64encode(binary).decode(),
+        quality_csv=quality.getvalue(), phix_summary=summary, bad_cycles_csv=bad.getvalue(),
+        bad_tiles_csv=tiles_csv.getvalue(), summary_r1=results[1][1], summary_r2=results[2][1],
+        cases=cases)
+    with open(os.path.join(out_dir, 'censor_golden.json'), 'w') as f:
+        json.dump(golden, f, indent=0)
+    print('censor: {} bad cycles, {} scenarios'.format(bad.getvalue().count('\n') - 1, len(cases)))
+
+
 def gen_s2a():
     import gzip
     refharness.setup()
@@ -447,6 +549,6 @@ def gen_s2a():
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['gotoh', 'pileup', 'sam2aln', 'e2e', 's2a']
+    which = sys.argv[1:] or ['gotoh', 'pileup', 'sam2aln', 'e2e', 's2a', 'censor']
     for w in which:
         globals()['gen_' + w]()
