@@ -32,7 +32,12 @@
  *          -> mh_sam2aln_csv, mh_sam2aln_output;
  *   5. (the stage before) censor_fastq.censor's per-base
  *      Python loop, micall/core/censor_fastq.py:32-102
- *          -> mh_censor_fastq, mh_censor_output.
+ *          -> mh_censor_fastq, mh_censor_output;
+ *   6. (the stage after sam2aln) aln2counts' per-read loops,
+ *      SequenceReport._count_reads (micall/core/aln2counts.py:115-172) and
+ *      InsertionWriter.write (:748-811)
+ *          -> mh_a2c_load_csv / mh_a2c_load_rows, mh_a2c_counts,
+ *             mh_a2c_inserts.
  *
  * Conventions: every function returns 0 on success, -1 on traceback failure
  * (mh_gotoh_align only), -2 on out-of-memory, -3 on a bad argument, -4 on a
@@ -236,6 +241,51 @@ int mh_censor_output(mh_ctx *ctx, char *buf, size_t cap, size_t *used);
 /* Host wall ms of the last call: [0] gunzip + record split, [1] upload +
  * k_censor + download, [2] rewrite + gzip. */
 int mh_censor_timing(mh_ctx *ctx, double *ms3);
+
+/* ---- aln2counts: replaces the per-read loops of aln2counts.py ---------- */
+/* aligned.csv text (refname, qcut, count, offset, seq columns) read as
+ * csv.DictReader reads it; consecutive rows with equal (refname, qcut) form a
+ * group (itertools.groupby, aln2counts.py:884-887).  Every row is counted on
+ * the device in the three reading frames of _count_reads (:147-169): per
+ * codon the 21 amino acids of AMINO_ALPHABET and, per codon position, the
+ * bases A C G T N - (an 'n' is not counted, :642-645), each counter with the
+ * first row of its group that touched it (the Counter insertion order that
+ * most_common() breaks ties by).  codon_chars = the translations of the 216
+ * codons over A C G T N - (translation.py:40-142), index 36 c0 + 6 c1 + c2.
+ * slot 0..3 selects one of four independent row tables of the context.
+ * Rejects (-3) seq characters outside A C G T N - n, offsets outside
+ * 0..2^28 and counts outside 0..2^32-1.  *n_groups = number of groups. */
+int mh_a2c_load_csv(mh_ctx *ctx, int slot, const char *text, int64_t len,
+                    const char *codon_chars, int64_t *n_groups);
+/* The same from rows in memory: row r's seq is pool[seq_off[r] ..
+ * seq_off[r] + seq_len[r]); group g = rows group_first[g] ..
+ * group_first[g + 1] - 1 (group names are empty). */
+int mh_a2c_load_rows(mh_ctx *ctx, int slot, int64_t n_rows, const char *pool, int64_t pool_len,
+                     const int64_t *seq_off, const int32_t *seq_len, const int64_t *offset,
+                     const int64_t *count, int64_t n_groups, const int64_t *group_first,
+                     const char *codon_chars);
+/* info5 = first row, rows, and the SeedAmino list length of frames 0, 1, 2;
+ * names = refname '\0' qcut (names NULL: only *used = bytes needed). */
+int mh_a2c_group(mh_ctx *ctx, int slot, int64_t g, int64_t *info5, char *names, size_t cap,
+                 size_t *used);
+/* Counters of group g, frame 0..2, codons 0 .. info5[2 + frame] - 1:
+ * aa_count / aa_first [codon][21], nuc_count / nuc_first [codon][3][6]
+ * (position in the codon, base A C G T N -); first = 0xffffffff when never
+ * touched (the Counter has no such key). */
+int mh_a2c_counts(mh_ctx *ctx, int slot, int64_t g, int frame, uint32_t *aa_count,
+                  uint32_t *aa_first, uint32_t *nuc_count, uint32_t *nuc_first);
+/* InsertionWriter.write's read loop (:779-795) over the rows of group g for
+ * the codon ranges [left[k], right[k]) in reading frame `frame`: distinct
+ * amino-acid strings per range with their summed counts, in (range, first
+ * row) order.  *n_entries = number of strings; fetch them with
+ * mh_a2c_insert_entries (aminos: one string per line). */
+int mh_a2c_inserts(mh_ctx *ctx, int slot, int64_t g, int frame, int n_ranges,
+                   const int32_t *left, const int32_t *right, int64_t *n_entries);
+int mh_a2c_insert_entries(mh_ctx *ctx, int slot, int32_t *range, int64_t *count,
+                          uint32_t *first, char *aminos, size_t cap, size_t *used);
+/* Host wall ms: [0] parse of the last load, [1] its upload + k_a2c_count +
+ * fetch, [2] mh_a2c_inserts since the last call of this function. */
+int mh_a2c_timing(mh_ctx *ctx, int slot, double *ms3);
 
 /* ---- Gotoh: replaces _gotoh2.align (_gotoh2.c:544-607) ---------------- */
 /* seq1/seq2 already cleaned (gotoh2.py:70-72).  out1/out2 need

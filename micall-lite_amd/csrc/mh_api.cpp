@@ -521,6 +521,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipFree(c->len_tab);
     s2a_free(*c);
     censor_free(*c);
+    a2c_free(*c);
     hipStreamDestroy(c->stream);
     delete c;
     return 0;

@@ -169,6 +169,7 @@ struct ProfPending {
 
 struct S2AState;      // mh_sam2aln.h
 struct CensorState;   // mh_censor.hip
+struct A2CState;      // mh_a2c.hip
 
 struct Ctx {
     int device = 0;
@@ -189,6 +190,7 @@ struct Ctx {
     int dp_fast = 1;                 // option "dp_fast": exact ungapped fast path of k_dp
     S2AState *s2a = nullptr;         // sam2aln rows and results (mh_sam2aln_csv)
     CensorState *censor = nullptr;   // censored FASTQ of the last mh_censor_fastq
+    A2CState **a2c = nullptr;        // aln2counts row tables (mh_a2c_*), one per slot
     int len_tab_mode = -1;
 };
 
@@ -196,6 +198,7 @@ void set_error(const char *fmt, ...);
 Ctx *ctx_of(mh_ctx *ctx);          // the context behind a C-ABI handle
 void s2a_free(Ctx &c);
 void censor_free(Ctx &c);
+void a2c_free(Ctx &c);
 // bracket one kernel launch on c.stream when profiling is on
 int prof_begin(Ctx &c, const char *name);
 void prof_end(Ctx &c, int slot);

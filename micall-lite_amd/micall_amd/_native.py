@@ -104,6 +104,19 @@ def _declare(L):
         'mh_censor_output': ([_P, ctypes.c_char_p, ctypes.c_size_t,
                               ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         'mh_censor_timing': ([_P, _P], ctypes.c_int),
+        'mh_a2c_load_csv': ([_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p,
+                             _I64P], ctypes.c_int),
+        'mh_a2c_load_rows': ([_P, ctypes.c_int, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64,
+                              _P, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_char_p], ctypes.c_int),
+        'mh_a2c_group': ([_P, ctypes.c_int, ctypes.c_int64, _P, ctypes.c_char_p, ctypes.c_size_t,
+                          ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        'mh_a2c_counts': ([_P, ctypes.c_int, ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P],
+                          ctypes.c_int),
+        'mh_a2c_inserts': ([_P, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _P, _P,
+                            _I64P], ctypes.c_int),
+        'mh_a2c_insert_entries': ([_P, ctypes.c_int, _P, _P, _P, ctypes.c_char_p, ctypes.c_size_t,
+                                   ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        'mh_a2c_timing': ([_P, ctypes.c_int, _P], ctypes.c_int),
         'mh_profile': ([_P, ctypes.c_int], ctypes.c_int),
         'mh_profile_get': ([_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _I64P],
                            ctypes.c_int),
@@ -231,6 +244,82 @@ class Context:
     def censor_timing(self):
         out = np.zeros(3, dtype=np.float64)
         check(lib().mh_censor_timing(self.h, _ptr(out)), 'mh_censor_timing')
+        return [float(x) for x in out]
+
+    # ---- aln2counts -----------------------------------------------------
+    def a2c_load_csv(self, slot, text, codon_chars):
+        """mh_a2c_load_csv on aligned.csv text (str or bytes): number of
+        (refname, qcut) groups."""
+        data = text.encode() if isinstance(text, str) else bytes(text)
+        n = ctypes.c_int64()
+        check(lib().mh_a2c_load_csv(self.h, slot, data, len(data), codon_chars, ctypes.byref(n)),
+              'mh_a2c_load_csv')
+        return n.value
+
+    def a2c_load_rows(self, slot, seqs, offsets, counts, group_first, codon_chars):
+        """mh_a2c_load_rows from lists: seq strings, offsets, counts and the
+        first row of every group (plus the row count at the end)."""
+        enc = [s.encode() for s in seqs]
+        lens = np.array([len(s) for s in enc] or [0], dtype=np.int32)
+        soff = np.zeros(max(len(enc), 1), dtype=np.int64)
+        if len(enc) > 1:
+            np.cumsum(lens[:-1], out=soff[1:])
+        pool = b''.join(enc)
+        off = np.array(list(offsets) or [0], dtype=np.int64)
+        cnt = np.array(list(counts) or [0], dtype=np.int64)
+        gf = np.array(group_first, dtype=np.int64)
+        check(lib().mh_a2c_load_rows(self.h, slot, len(enc), pool, len(pool), _ptr(soff), _ptr(lens),
+                                     _ptr(off), _ptr(cnt), len(gf) - 1, _ptr(gf), codon_chars),
+              'mh_a2c_load_rows')
+
+    def a2c_group(self, slot, g):
+        info = np.zeros(5, dtype=np.int64)
+        used = ctypes.c_size_t()
+        check(lib().mh_a2c_group(self.h, slot, g, _ptr(info), None, 0, ctypes.byref(used)),
+              'mh_a2c_group')
+        buf = ctypes.create_string_buffer(used.value + 1)
+        check(lib().mh_a2c_group(self.h, slot, g, _ptr(info), buf, len(buf), ctypes.byref(used)),
+              'mh_a2c_group')
+        ref, qcut = buf.raw[:used.value].split(b'\0', 1)
+        return dict(first=int(info[0]), n_rows=int(info[1]), ncod=[int(x) for x in info[2:5]],
+                    refname=ref.decode(), qcut=qcut.decode())
+
+    def a2c_counts(self, slot, g, frame, ncod):
+        """(aa_count, aa_first) [ncod, 21] and (nuc_count, nuc_first)
+        [ncod, 18] uint32 of one group and frame."""
+        n = max(ncod, 1)
+        aa_c = np.zeros((n, 21), np.uint32)
+        aa_f = np.zeros((n, 21), np.uint32)
+        nt_c = np.zeros((n, 18), np.uint32)
+        nt_f = np.zeros((n, 18), np.uint32)
+        check(lib().mh_a2c_counts(self.h, slot, g, frame, _ptr(aa_c), _ptr(aa_f), _ptr(nt_c),
+                                  _ptr(nt_f)), 'mh_a2c_counts')
+        return aa_c[:ncod], aa_f[:ncod], nt_c[:ncod], nt_f[:ncod]
+
+    def a2c_inserts(self, slot, g, frame, lefts, rights):
+        """[(range index, count, first row, amino-acid string)] in
+        (range, first row) order."""
+        lo = np.array(list(lefts) or [0], dtype=np.int32)
+        hi = np.array(list(rights) or [0], dtype=np.int32)
+        n = ctypes.c_int64()
+        check(lib().mh_a2c_inserts(self.h, slot, g, frame, len(lefts), _ptr(lo), _ptr(hi),
+                                   ctypes.byref(n)), 'mh_a2c_inserts')
+        k = n.value
+        rng = np.zeros(max(k, 1), np.int32)
+        cnt = np.zeros(max(k, 1), np.int64)
+        first = np.zeros(max(k, 1), np.uint32)
+        used = ctypes.c_size_t()
+        check(lib().mh_a2c_insert_entries(self.h, slot, _ptr(rng), _ptr(cnt), _ptr(first), None, 0,
+                                          ctypes.byref(used)), 'mh_a2c_insert_entries')
+        buf = ctypes.create_string_buffer(max(used.value, 1))
+        check(lib().mh_a2c_insert_entries(self.h, slot, None, None, None, buf, len(buf),
+                                          ctypes.byref(used)), 'mh_a2c_insert_entries')
+        aminos = buf.raw[:used.value].decode().split('\n')[:k]
+        return [(int(rng[i]), int(cnt[i]), int(first[i]), aminos[i]) for i in range(k)]
+
+    def a2c_timing(self, slot):
+        out = np.zeros(3, dtype=np.float64)
+        check(lib().mh_a2c_timing(self.h, slot, _ptr(out)), 'mh_a2c_timing')
         return [float(x) for x in out]
 
     def sam2aln_timing(self):

@@ -31,6 +31,15 @@ itself produced for them.  Sections:
            reader), plus censor_fastq_test.py's scenarios:
            tests/golden/censor/.
 
+  a2c      aln2counts (the stage after sam2aln): every
+           call micall/tests/aln2counts_test.py makes on SequenceReport,
+           InsertionWriter, SeedAmino and SeedNucleotide, recorded around the
+           reference code with what each call wrote or returned
+           (tests/golden/aln2counts_golden.json); the reference aln2counts()
+           on every e2e case's aligned.csv (tests/golden/e2e/<case>/a2c_*.csv.gz)
+           and on edge-case aligned.csv texts over a small project file cut
+           from HIV-1 pol (tests/golden/aln2counts_edge.json).
+
   e2e      the stock reference prelim_map() + remap() (nthreads=1, so its
            pileup runs without a process pool and is deterministic) with
            oracle/shim_bin/bowtie2 standing in for bowtie2, on small committed
@@ -546,6 +555,271 @@ def gen_s2a():
             with gzip.open(os.path.join(d, name + '.gz'), 'wt') as f:
                 f.write(body)
     print('s2a: {} calls ({} from sam2aln_test)'.format(len(records), n_tests))
+
+A2C_OUTPUTS = ('nuc', 'amino', 'coord_ins', 'conseq', 'failed', 'coverage')
+
+
+def _a2c_reference(A, text, json_path=None):
+    outs = {k: io.StringIO() for k in A2C_OUTPUTS}
+    A.aln2counts(io.StringIO(text), outs['nuc'], outs['amino'], outs['coord_ins'],
+                 outs['conseq'], failed_align_csv=outs['failed'],
+                 coverage_summary_csv=outs['coverage'], json=json_path)
+    return {k: v.getvalue() for k, v in outs.items()}
+
+
+def _a2c_edge_config():
+    """A small project file: seeds cut from HIV-1 pol, coordinate references
+    translated from them (one with an inserted and a deleted amino acid), a
+    seed linked to two projects, one without a coordinate region, one in no
+    project."""
+    from micall_amd import projects, translation
+    pol = projects.load_default().seed_sequences()['HIV1B-pol-seed']
+    s1, s2, s3 = pol[:420], pol[600:900], pol[1200:1350]
+    aa1 = translation.translate(s1[30:390])
+    c1 = aa1[:40] + 'W' + aa1[40:80] + aa1[81:]
+    return {'projects': {
+        'P1': {'max_variants': 0, 'regions': [
+            {'coordinate_region': 'C1', 'seed_region_names': ['S1-seed']},
+            {'coordinate_region': 'C1b', 'seed_region_names': ['S1-seed']}]},
+        'P2': {'max_variants': 0, 'regions': [
+            {'coordinate_region': 'C2', 'seed_region_names': ['S2-seed', 'S1-seed']},
+            {'coordinate_region': None, 'seed_region_names': ['S3-seed']}]}},
+        'regions': {
+            'S1-seed': {'is_nucleotide': True, 'reference': [s1[:200], s1[200:]]},
+            'S2-seed': {'is_nucleotide': True, 'reference': [s2]},
+            'S3-seed': {'is_nucleotide': True, 'reference': [s3]},
+            'S4-seed': {'is_nucleotide': True, 'reference': [pol[2000:2100]]},
+            'C1': {'is_nucleotide': False, 'reference': [c1]},
+            'C1b': {'is_nucleotide': False, 'reference': [translation.translate(s1[:150])]},
+            'C2': {'is_nucleotide': False, 'reference': [translation.translate(s2, 1)[5:90]]}}}
+
+
+def _a2c_edge_texts(cfg, n_texts=16, seed=77):
+    """aligned.csv texts over cfg: samples with an inserted / deleted codon,
+    substitutions, N, '-' (single and whole codons), 'n' gaps, junk reads
+    that do not align, tied counts, several groups and a group key that
+    comes back later (a new groupby group)."""
+    rng = random.Random(seed)
+    seqs = {k: ''.join(v['reference']) for k, v in cfg['regions'].items() if v['is_nucleotide']}
+    texts = []
+    for t in range(n_texts):
+        keys = [(rng.choice(sorted(seqs)), rng.choice(['15', '15', '20']))
+                for _ in range(rng.randint(1, 4))]
+        if t % 4 == 3 and len(keys) > 1:
+            keys.append(keys[0])
+        rows = []
+        for name, qcut in keys:
+            sample = list(seqs[name])
+            if rng.random() < 0.6:
+                k = rng.randrange(30, len(sample) - 30) // 3 * 3
+                sample[k:k] = list(rng.choice(['GGG', 'AAC', 'TTT']))
+            if rng.random() < 0.4:
+                k = rng.randrange(30, len(sample) - 30) // 3 * 3
+                del sample[k:k + 3]
+            sample = ''.join(sample)
+            seen = set()
+            for rank in range(rng.randint(1, 25)):
+                if rng.random() < 0.08:
+                    s = ''.join(rng.choice('ACGT') for _ in range(rng.randint(10, 60)))
+                    off = rng.randint(0, 40)
+                else:
+                    off = rng.randint(0, max(0, len(sample) - 30))
+                    s = list(sample[off:off + rng.randint(6, 140)])
+                    for i in range(len(s)):
+                        r = rng.random()
+                        if r < 0.03:
+                            s[i] = rng.choice('ACGT')
+                        elif r < 0.05:
+                            s[i] = 'N'
+                    if rng.random() < 0.2 and len(s) > 12:
+                        i = rng.randrange(3, len(s) - 6)
+                        w = rng.randint(1, 5)
+                        s[i:i + w] = ['n'] * w
+                    if rng.random() < 0.15 and len(s) > 9:
+                        i = rng.randrange(0, len(s) - 3)
+                        w = rng.choice([1, 3])
+                        s[i:i + w] = ['-'] * w
+                    s = ''.join(s).strip('-')
+                if not s or (off, s) in seen:
+                    continue
+                seen.add((off, s))
+                rows.append('{},{},{},{},{},{}\n'.format(name, qcut, rank,
+                                                         rng.choice([1, 1, 2, 3, 5, 8, 13, 40]),
+                                                         off, s))
+        texts.append('refname,qcut,rank,count,offset,seq\n' + ''.join(rows))
+    texts.append('refname,qcut,rank,count,offset,seq\n')
+    texts.append('')
+    return texts
+
+
+def gen_a2c():
+    import copy
+    import gzip
+    import tempfile
+    refharness.setup()
+    from micall.core import aln2counts as A
+    from micall.core import project_config as PC
+
+    # Python-3 harness fixes, no algorithm touched: ProjectConfig.load keeps
+    # json_file.name, which io.StringIO lacks, and the tests call both
+    # StringIO() and StringIO.StringIO().
+    def load(self, json_file):
+        self.json_file = getattr(json_file, 'name', None)
+        self.config = json.load(json_file)
+    PC.ProjectConfig.load = load
+    import micall.tests.aln2counts_test as T
+
+    class _SIO(io.StringIO):
+        StringIO = io.StringIO
+    T.StringIO = _SIO
+    st = {'depth': 0, 'calls': None, 'tags': {}}
+
+    def tag(obj):
+        t = st['tags'].get(id(obj))
+        if t is None:
+            t = st['tags'][id(obj)] = 'o{}'.format(len(st['tags']))
+        return t
+
+    def plain(v):
+        return sorted(v) if isinstance(v, (set, frozenset)) else list(v) if isinstance(v, tuple) else v
+
+    def wrap(cls, name, kind):
+        fn = getattr(cls, name)
+
+        def wrapper(self, *args, **kwargs):
+            top = st['depth'] == 0 and st['calls'] is not None
+            st['depth'] += 1
+            try:
+                entry = {'op': name, 'obj': tag(self)} if top else None
+                f = n0 = summary = None
+                if kind == 'read':
+                    rows = [dict(r) for r in args[0]]
+                    args = (rows,) + args[1:]
+                    if top:
+                        entry.update(rows=rows, config=copy.deepcopy(self.projects.config),
+                                     overrides=[[k[0], k[1], list(v)] for k, v in
+                                                getattr(self, 'overrides', {}).items()])
+                elif kind == 'file':
+                    f = args[0]
+                    summary = kwargs.get('coverage_summary')
+                    if top:
+                        entry['file'] = tag(f)
+                        if summary is not None:
+                            entry['summary_in'] = dict(summary)
+                elif kind == 'ins':
+                    f = (self.insert_writer if isinstance(self, A.SequenceReport) else self)._rec_file
+                    if top:
+                        entry['args'] = [plain(a) for a in args]
+                        entry['kwargs'] = {k: plain(v) for k, v in kwargs.items()}
+                elif kind == 'args' and top:
+                    entry['args'] = [plain(a) for a in args]
+                    entry['kwargs'] = {k: plain(v) for k, v in kwargs.items()}
+                if f is not None:
+                    n0 = len(f.getvalue())
+                try:
+                    res = fn(self, *args, **kwargs)
+                except Exception as ex:
+                    if top:
+                        entry['raises'] = type(ex).__name__
+                        st['calls'].append(entry)
+                    raise
+                if top:
+                    if f is not None:
+                        entry['out'] = f.getvalue()[n0:]
+                    if summary is not None:
+                        entry['summary_out'] = dict(summary)
+                    if kind == 'args':
+                        entry['result'] = res
+                    st['calls'].append(entry)
+                return res
+            finally:
+                st['depth'] -= 1
+        setattr(cls, name, wrapper)
+
+    def wrap_init(cls, describe):
+        fn = cls.__init__
+
+        def init(self, *args, **kwargs):
+            top = st['depth'] == 0 and st['calls'] is not None
+            st['depth'] += 1
+            try:
+                f = (args[0] if args else kwargs['insert_file']) if cls is A.InsertionWriter else None
+                n0 = len(f.getvalue()) if f is not None else 0
+                fn(self, *args, **kwargs)
+                if f is not None:
+                    self._rec_file = f
+                if top:
+                    entry = {'op': cls.__name__, 'obj': tag(self)}
+                    entry.update(describe(self, args, kwargs))
+                    if f is not None:
+                        entry['out'] = f.getvalue()[n0:]
+                    st['calls'].append(entry)
+            finally:
+                st['depth'] -= 1
+        cls.__init__ = init
+
+    wrap_init(A.InsertionWriter, lambda s, a, k: {'file': tag(a[0] if a else k['insert_file'])})
+    wrap_init(A.SequenceReport, lambda s, a, k: {'writer': tag(a[0]), 'cutoffs': list(a[2])})
+    wrap_init(A.SeedAmino, lambda s, a, k: {'index': a[0], 'nucs': [tag(n) for n in s.nucleotides]})
+    wrap_init(A.SeedNucleotide, lambda s, a, k: {})
+    wrap(A.SequenceReport, 'read', 'read')
+    for name in ('write_amino_header', 'write_nuc_header', 'write_consensus_header',
+                 'write_nuc_variants_header', 'write_failure_header', 'write_amino_counts',
+                 'write_nuc_counts', 'write_consensus', 'write_failure', 'write_nuc_variants'):
+        wrap(A.SequenceReport, name, 'file')
+    wrap(A.SequenceReport, 'write_insertions', 'ins')
+    wrap(A.InsertionWriter, 'write', 'ins')
+    for name in ('start_group', 'add_nuc_read'):
+        wrap(A.InsertionWriter, name, 'args')
+    for name in ('count_aminos', 'get_report', 'get_consensus'):
+        wrap(A.SeedAmino, name, 'args')
+    for name in ('count_nucleotides', 'get_report', 'get_consensus'):
+        wrap(A.SeedNucleotide, name, 'args')
+
+    def each(suite):
+        for t in suite:
+            if isinstance(t, unittest.TestSuite):
+                yield from each(t)
+            else:
+                yield t
+    scripts = []
+    for test in each(unittest.defaultTestLoader.loadTestsFromModule(T)):
+        st['calls'], st['tags'] = [], {}
+        test.run(unittest.TestResult())
+        scripts.append({'test': '.'.join(test.id().split('.')[-2:]), 'calls': st['calls']})
+    st['calls'] = None
+    with open(os.path.join(HERE, 'aln2counts_golden.json'), 'w') as f:
+        json.dump({'source': 'reference micall.core.aln2counts classes as called by '
+                             'micall/tests/aln2counts_test.py', 'scripts': scripts}, f, indent=0)
+    n_calls = sum(len(s['calls']) for s in scripts)
+    print('a2c: {} scripts, {} calls'.format(len(scripts), n_calls))
+
+    # the reference aln2counts() on every e2e case
+    for case in sorted(os.listdir(os.path.join(HERE, 'e2e'))):
+        d = os.path.join(HERE, 'e2e', case)
+        with gzip.open(os.path.join(d, 'aligned.csv.gz'), 'rt') as f:
+            text = f.read()
+        for k, body in _a2c_reference(A, text).items():
+            with gzip.open(os.path.join(d, 'a2c_{}.csv.gz'.format(k)), 'wt') as f:
+                f.write(body)
+        print('a2c e2e:', case)
+
+    # edge cases over a small project file
+    cfg = _a2c_edge_config()
+    tmp = tempfile.mkdtemp(prefix='a2c_')
+    path = os.path.join(tmp, 'projects.json')
+    with open(path, 'w') as f:
+        json.dump(cfg, f)
+    cases = []
+    for text in _a2c_edge_texts(cfg):
+        try:
+            cases.append({'text': text, 'outputs': _a2c_reference(A, text, path)})
+        except Exception as ex:
+            print('a2c edge: reference raised {!r}; case dropped'.format(ex))
+    with open(os.path.join(HERE, 'aln2counts_edge.json'), 'w') as f:
+        json.dump({'source': 'reference micall.core.aln2counts.aln2counts on edge-case texts',
+                   'config': cfg, 'cases': cases}, f, indent=0)
+    print('a2c edge: {} cases'.format(len(cases)))
 
 
 if __name__ == '__main__':
