@@ -277,7 +277,7 @@ def bench_censor(args):
         'ms_per_step': round(1e3 * elapsed / args.steps, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
         'config': {'workload': 'censor of the C2 R1 file (1M synthetic 2x251 reads over 8 tiles, '
-                               'gzip level 1 in, level 6 out), 2 % bad tile-cycles',
+                               'gzip level 1 in, level 1 out), 2 % bad tile-cycles',
                    'reads': args.pairs, 'bad_cycles': len(bad), 'fastq_bytes': len(raw1),
                    'gz_bytes': len(gz1)},
         'host_ms_last_step': {'gunzip_split': round(host_ms[0], 1),
@@ -299,6 +299,90 @@ def bench_censor(args):
     ctx.close()
 
 
+def bench_aln2counts(args):
+    """aln2counts (micall_amd.aln2counts: mh_a2c_load_csv + k_a2c_count, the
+    coordinate mapping with k_gotoh, mh_a2c_inserts, the CSV reports) over
+    the aligned.csv that sam2aln makes from one C2 remap pass."""
+    import io
+    import torch
+    from micall_amd import _native, session
+    from micall_amd import aln2counts as a2c
+    from micall_amd.pipeline import RemapPipeline
+    import og_aln2counts
+    ctx = session.context()
+    reads, quals = make_reads(args.pairs, block=0)
+    ctx.reads_load_fixed(reads, quals, True)
+    del reads, quals
+    ctx.set_names(['M00000:1:000000000-AAAAA:1:1101:{}:{}'.format(1000 + i // 1000000,
+                                                                         1000 + i % 1000000)
+                         for i in range(args.pairs) for _ in (0, 1)])
+    pipe = RemapPipeline(ctx)
+    pipe.run(2.0 * args.pairs, max_iterations=1)
+    remap_text = ('qname,flag,rname,pos,mapq,cigar,rnext,pnext,tlen,seq,qual\n' +
+                  ctx.format_rows(1, 0, 2 * args.pairs)).encode()
+    ctx.sam2aln_csv(remap_text)
+    del remap_text
+    aligned = ctx.sam2aln_output('aligned')
+    n_rows = aligned.count('\n') - 1
+    seq_bytes = sum(len(line.rsplit(',', 1)[1]) for line in aligned.splitlines()[1:])
+
+    def step():
+        outs = [io.StringIO() for _ in range(6)]
+        a2c.aln2counts(io.StringIO(aligned), *outs[:4], failed_align_csv=outs[4],
+                       coverage_summary_csv=outs[5])
+        return outs
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.a2c_timing(a2c.SLOT_REPORT)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        outs = step()
+    elapsed = time.perf_counter() - t0
+    host_ms = ctx.a2c_timing(a2c.SLOT_REPORT)
+    kern = {k: ctx.profile_get(k) for k in ('k_a2c_count', 'k_a2c_ins')}
+    n_groups = ctx.a2c_load_csv(a2c.SLOT_REPORT, aligned, a2c._CODON_CHARS)
+    bins = sum(-(-max(ctx.a2c_group(a2c.SLOT_REPORT, g)['ncod']) // 64) for g in range(n_groups))
+    k_ms, k_n = kern['k_a2c_count']
+    avg_s = k_ms / 1e3 / max(k_n, 1)
+    # algorithmic bytes per launch: every row's seq once, its 24-B record,
+    # and the counters (count + first row, 4 B each) of every (bin, frame)
+    algo = seq_bytes + 24 * n_rows + 2 * 4 * bins * 3 * 64 * 39
+    achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
+    sample = min(3000, n_rows)
+    lines = aligned.split('\n', sample + 1)
+    stext = '\n'.join(lines[:sample + 1]) + '\n'
+    t2 = time.perf_counter()
+    og_aln2counts.aln2counts(stext, og_aln2counts.default_projects())
+    cpu_s = time.perf_counter() - t2
+    out = {
+        'metric': 'aln2counts aligned rows/sec (aligned.csv -> nuc/amino/coord_ins/conseq/failed)',
+        'value': round(n_rows * args.steps / elapsed, 1), 'unit': 'rows/s', 'n_gpus': 1,
+        'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(1e3 * elapsed / args.steps, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32', 'data': 'synthetic',
+        'config': {'workload': 'aln2counts over the aligned.csv sam2aln makes from one C2 remap '
+                               'pass (1M pairs of synthetic 2x251 HIV-1 pol reads; coordinate '
+                               'regions PR, RT, INT)',
+                   'rows': n_rows, 'groups': n_groups, 'seq_bytes': seq_bytes,
+                   'csv_bytes': len(aligned)},
+        'host_ms_last_load': {'parse': round(host_ms[0], 1),
+                             'upload_count_fetch': round(host_ms[1], 1),
+                             'inserts': round(host_ms[2] / args.steps, 1)},
+        'roofline': {'kernel': 'k_a2c_count', 'bound': 'hbm', 'achieved': round(achieved, 3),
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 6),
+                     'traffic': None, 'algo_bytes_per_launch': algo,
+                     'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': k_n},
+        'kernels_ms_per_step': {k: round(v[0] / args.steps, 3) for k, v in kern.items()},
+        'cpu_baseline': {'value': round(sample / cpu_s, 1), 'unit': 'rows/s', 'cores': 1,
+                         'kind': 'port',
+                         'sample': 'first {} rows of the same aligned.csv through the pure-Python '
+                                   'restatement oracle/og_aln2counts.py, {:.1f} s'.format(sample, cpu_s)},
+    }
+    print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split('\n\n')[0])
     ap.add_argument('--gpus', type=int, default=1)
@@ -309,13 +393,15 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--breakdown', action='store_true',
                     help='time each pipeline stage (synchronising) and print it to stderr')
-    ap.add_argument('--stage', choices=('remap', 'sam2aln', 'censor'), default='remap',
+    ap.add_argument('--stage', choices=('remap', 'sam2aln', 'censor', 'aln2counts'), default='remap',
                     help='remap: the headline hot path (default); sam2aln: the next stage '
                          '(SURVEY.md 8(f)) over the remap.csv of one C2 pass; censor: the '
                          'stage before (FASTQ censor of the C2 reads) plus the FASTQ ingest')
     args = ap.parse_args()
     if args.stage == 'sam2aln':
         return bench_sam2aln(args)
+    if args.stage == 'aln2counts':
+        return bench_aln2counts(args)
     if args.stage == 'censor':
         return bench_censor(args)
 

@@ -232,7 +232,7 @@ int mh_sam2aln_timing(mh_ctx *ctx, double *ms5);
  * dropped as the reference drops it, header and '+' lines are kept
  * verbatim.  *base_count / *score_sum = number and sum (Phred) of all
  * quality characters, for the summary row (:94-102).  The censored file
- * (gzip when dst_gzip: independent deflate members, level 6) is then
+ * (gzip when dst_gzip: independent deflate members, level 1) is then
  * copied out with mh_censor_output (buf NULL: *used = size). */
 int mh_censor_fastq(mh_ctx *ctx, const uint8_t *src, int64_t len, int src_gzip, int n_bad,
                     const char *const *tiles, const int32_t *cycles, int dst_gzip,

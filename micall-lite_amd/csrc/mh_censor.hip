@@ -407,7 +407,7 @@ extern "C" int mh_censor_fastq(mh_ctx *ctx, const uint8_t *src, int64_t len, int
     std::string().swap(C.text);
     if (dst_gzip) {
         std::string z;
-        if (int st = gzip_parallel(C.out, z, 6)) return st;
+        if (int st = gzip_parallel(C.out, z, 1)) return st;
         C.out.swap(z);
     }
     auto t3 = std::chrono::steady_clock::now();

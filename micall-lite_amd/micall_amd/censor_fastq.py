@@ -5,7 +5,7 @@ device (mh_censor_fastq, csrc/mh_censor.hip): bases and qualities read in a
 bad (tile, cycle) become 'N' / '#', a trailing run of bad cycles is dropped as
 the reference drops it, header and '+' lines are copied verbatim.  gzip in
 and out as the reference's use_gzip (the output is gzip members compressed
-in parallel at level 6: same decompressed bytes, different compressed bytes
+in parallel at level 1: same decompressed bytes, different compressed bytes
 than GzipFile's level 9 -- whose header holds a timestamp anyway).  There is
 no CPU fallback.
 """
