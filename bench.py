@@ -304,8 +304,9 @@ def bench_aln2counts(args):
     coordinate mapping with k_gotoh, mh_a2c_inserts, the CSV reports) over
     the aligned.csv that sam2aln makes from one C2 remap pass."""
     import io
+    import tempfile
     import torch
-    from micall_amd import _native, session
+    from micall_amd import session
     from micall_amd import aln2counts as a2c
     from micall_amd.pipeline import RemapPipeline
     import og_aln2counts
@@ -326,10 +327,19 @@ def bench_aln2counts(args):
     n_rows = aligned.count('\n') - 1
     seq_bytes = sum(len(line.rsplit(',', 1)[1]) for line in aligned.splitlines()[1:])
 
+    # aligned.csv on disk, opened the way bin/micall hands it over
+    tmp = tempfile.mkdtemp(prefix='bench_a2c_')
+    path = os.path.join(tmp, 'aligned.csv')
+    with open(path, 'w') as f:
+        f.write(aligned)
+
     def step():
+        # a fresh process aligns every consensus: no memoised alignment
+        # survives from the previous step
+        a2c.aligner._memo.clear()
         outs = [io.StringIO() for _ in range(6)]
-        a2c.aln2counts(io.StringIO(aligned), *outs[:4], failed_align_csv=outs[4],
-                       coverage_summary_csv=outs[5])
+        with open(path) as f:
+            a2c.aln2counts(f, *outs[:4], failed_align_csv=outs[4], coverage_summary_csv=outs[5])
         return outs
     for _ in range(args.warmup):
         step()

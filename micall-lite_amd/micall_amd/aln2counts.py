@@ -687,6 +687,21 @@ def format_cutoff(cutoff):
     return '{:0.3f}'.format(cutoff)
 
 
+def _read_all(handle):
+    """The rest of an open aligned.csv: the raw bytes of a text file that
+    nothing has read from yet (no decode / encode of the whole file), the
+    text otherwise."""
+    raw = getattr(handle, 'buffer', None)
+    if raw is not None:
+        try:
+            fresh = handle.tell() == 0
+        except (OSError, ValueError):
+            fresh = False
+        if fresh and (handle.encoding or '').lower().replace('-', '') in ('utf8', 'ascii'):
+            return raw.read()
+    return handle.read()
+
+
 def aln2counts(aligned_csv,
                nuc_csv,
                amino_csv,
@@ -726,7 +741,7 @@ def aln2counts(aligned_csv,
         if aligned_filename:
             report.enable_callback(callback, os.stat(aligned_filename).st_size)
     ctx = session.context()
-    n_groups = ctx.a2c_load_csv(SLOT_REPORT, aligned_csv.read(), _CODON_CHARS)
+    n_groups = ctx.a2c_load_csv(SLOT_REPORT, _read_all(aligned_csv), _CODON_CHARS)
     for g in range(n_groups):
         report._read_group(ctx, SLOT_REPORT, g)
         report.write_amino_counts(amino_csv, coverage_summary=coverage_summary)
