@@ -35,6 +35,7 @@ outside A C G T N - n, negative offsets and counts >= 2**32 are rejected.
 """
 import argparse
 import csv
+import io
 import json as jsonlib
 import os
 import re
@@ -619,6 +620,7 @@ class InsertionWriter(object):
                                              'before'],
                                             lineterminator=os.linesep)
         self.insert_writer.writeheader()
+        self._file = insert_file
         self.nuc_seqs = Counter()
         self._source = None
 
@@ -669,15 +671,21 @@ class InsertionWriter(object):
                   if not report_aminos or insert_targets.get(left) not in (1, None)]
         if not wanted:
             return
-        for k, count, _first, insert_seq in self._insert_counts(wanted, reading_frame):
-            left = wanted[k][0]
-            self.insert_writer.writerow(dict(seed=self.seed,
-                                             region=region,
-                                             qcut=self.qcut,
-                                             left=left + 1,
-                                             insert=insert_seq,
-                                             count=count,
-                                             before=insert_targets.get(left)))
+        entries = self._insert_counts(wanted, reading_frame)
+        if not entries:
+            return
+        # DictWriter's row text, built in one pass: the three leading fields
+        # through the csv module (quoting), the rest are numbers and amino-acid
+        # letters, which never need quotes
+        head = io.StringIO()
+        csv.writer(head, lineterminator='').writerow([self.seed, region, self.qcut, ''])
+        head = head.getvalue()
+        tails = {k: (wanted[k][0] + 1, insert_targets.get(wanted[k][0]))
+                 for k in range(len(wanted))}
+        self._file.write(''.join(
+            '{}{},{},{},{}{}'.format(head, tails[k][0], insert_seq, count,
+                                     '' if tails[k][1] is None else tails[k][1], os.linesep)
+            for k, count, _first, insert_seq in entries))
 
 
 def format_cutoff(cutoff):
