@@ -444,10 +444,20 @@ def main():
     stages = {}
     if args.breakdown:
         instrument(pipe, ctx, stages)
+    # extensions per mapping pass (host-side counters of the last mh_map; no sync)
+    dp_log = []
+    real_map = ctx.map
+
+    def counted_map(*a, **kw):
+        r = real_map(*a, **kw)
+        dp_log.append(ctx.map_stats())
+        return r
+    ctx.map = counted_map
 
     for _ in range(args.warmup):
         step()
     ctx.profile(True)
+    del dp_log[:]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -472,6 +482,13 @@ def main():
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
     total_pairs = args.pairs * world * args.steps
     value = 2 * total_pairs / elapsed
+    # DP cell updates (GCUPS next to the roofline): every
+    # extension the full DP runs is read_len rows x the 64-diagonal band; the
+    # ungapped fast path resolves the rest without the DP
+    ext = sum(int(m[1]) for m in dp_log)
+    fast = sum(int(m[3]) for m in dp_log)
+    cells = (ext - fast) * READ_LEN * 64
+    dp_ms = kernels['k_dp'][0]
 
     if rank == 0:
         cpu = None
@@ -496,6 +513,10 @@ def main():
                          'algo_bytes_per_launch': bytes_per_launch,
                          'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': dom_n},
             'kernels_ms_per_step': {k: round(v[0] / args.steps, 3) for k, v in kernels.items()},
+            'dp': {'extensions_per_step': ext // max(args.steps, 1),
+                   'fast_path_per_step': fast // max(args.steps, 1),
+                   'cells_per_step': cells // max(args.steps, 1),
+                   'gcups': round(cells / (dp_ms / 1e3) / 1e9, 1) if dp_ms > 0 else None},
             'cpu_baseline': cpu,
             'result': {'conseqs': {k: len(v) for k, v in conseqs.items()},
                        'mapped_lines': dict(new_counts)},
