@@ -71,11 +71,13 @@ def cpu_baseline(sample_pairs):
                       'with OpenMP over pairs, {:.1f} s'.format(sample_pairs, secs)}
 
 
-def read_pmc_traffic(kernel, pairs):
+def read_pmc_traffic(kernel, pairs, stage='remap'):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC
-    summary (separate --pmc pass, FETCH_SIZE doubled per the gfx950 rule),
-    when it was measured on the same per-GPU pair count."""
-    path = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
+    summary of this stage (separate --pmc passes, FETCH_SIZE doubled per the
+    gfx950 rule; profiles/collect_pmc_stages.sh), when it was measured on the
+    same per-GPU pair count."""
+    name = 'pmc_traffic.json' if stage == 'remap' else 'pmc_traffic_{}.json'.format(stage)
+    path = os.path.join(REPO, 'profiles', name)
     try:
         with open(path) as f:
             d = json.load(f)
@@ -198,7 +200,7 @@ def bench_sam2aln(args):
                               'format_failed': round(host_ms[4], 1)},
         'roofline': {'kernel': 'k_s2a_merge', 'bound': 'hbm', 'achieved': round(achieved, 3),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 6),
-                     'traffic': None, 'algo_bytes_per_launch': algo,
+                     'traffic': read_pmc_traffic('k_s2a_merge', args.pairs, 'sam2aln'), 'algo_bytes_per_launch': algo,
                      'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': merge_n},
         'kernels_ms_per_step': {k: round(v[0] / args.steps, 3) for k, v in kern.items()},
         'cpu_baseline': {'value': round(sample / cpu_s, 1), 'unit': 'pairs/s', 'cores': 1,
@@ -287,7 +289,7 @@ def bench_censor(args):
         'ingest_reads_per_s': round(2 * args.pairs / ingest_s, 1),
         'roofline': {'kernel': 'k_censor', 'bound': 'hbm', 'achieved': round(achieved, 3),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 6),
-                     'traffic': None, 'algo_bytes_per_launch': algo,
+                     'traffic': read_pmc_traffic('k_censor', args.pairs, 'censor'), 'algo_bytes_per_launch': algo,
                      'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': k_n},
         'cpu_baseline': {'value': round(sample / cpu_s, 1), 'unit': 'reads/s', 'cores': 1,
                          'kind': 'port',
@@ -382,7 +384,7 @@ def bench_aln2counts(args):
                              'inserts': round(host_ms[2] / args.steps, 1)},
         'roofline': {'kernel': 'k_a2c_count', 'bound': 'hbm', 'achieved': round(achieved, 3),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 6),
-                     'traffic': None, 'algo_bytes_per_launch': algo,
+                     'traffic': read_pmc_traffic('k_a2c_count', args.pairs, 'aln2counts'), 'algo_bytes_per_launch': algo,
                      'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': k_n},
         'kernels_ms_per_step': {k: round(v[0] / args.steps, 3) for k, v in kern.items()},
         'cpu_baseline': {'value': round(sample / cpu_s, 1), 'unit': 'rows/s', 'cores': 1,
