@@ -1,6 +1,8 @@
 // mh_censor.hip -- censor_fastq.censor (micall/core/censor_fastq.py:32-102)
 // on gfx950, behind mh_censor_fastq / mh_censor_output:
-//   host      gunzip (zlib, multi-member), FASTQ records split in parallel,
+//   host      streaming gunzip (zlib, multi-member): a producer thread
+//             inflates ~32 MB chunks while the whole records of the chunks
+//             already there are censored; records split in parallel,
 //             tile + read direction from each header exactly as :59-63 parse
 //             them, bad (tile, cycle) set from the caller
 //   k_censor  one wave64 per read: the bases / qualities of bad cycles
@@ -14,6 +16,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <cstring>
 #include <functional>
 #include <string>
@@ -36,9 +41,27 @@ struct CensorState {
     std::vector<int32_t> tile, sign;        // tile id (-1: no bad cycle) / +1, -1
     std::vector<int32_t> keep;              // 2 per record: kept seq / qual length
     int64_t base_count = 0, score_sum = 0;
+    int64_t rec_base = 0;                   // records before this piece (messages)
     std::string out;
     double t_host_in = 0, t_device = 0, t_host_out = 0;
+    // device buffers, grown on demand and kept between pieces and calls
+    uint8_t *d_text = nullptr;
+    int64_t *d_s0 = nullptr, *d_q0 = nullptr;
+    int32_t *d_sl = nullptr, *d_ql = nullptr, *d_tile = nullptr, *d_sign = nullptr, *d_keep = nullptr;
+    uint32_t *d_bad = nullptr;
+    unsigned long long *d_sums = nullptr;
+    int64_t cap_text = 0, cap_rec = 0, cap_bad = 0;
 };
+
+static void censor_free_device(CensorState &C)
+{
+    hipFree(C.d_text); hipFree(C.d_s0); hipFree(C.d_q0); hipFree(C.d_sl); hipFree(C.d_ql);
+    hipFree(C.d_tile); hipFree(C.d_sign); hipFree(C.d_keep); hipFree(C.d_bad); hipFree(C.d_sums);
+    C.d_text = nullptr; C.d_s0 = C.d_q0 = nullptr;
+    C.d_sl = C.d_ql = C.d_tile = C.d_sign = C.d_keep = nullptr;
+    C.d_bad = nullptr; C.d_sums = nullptr;
+    C.cap_text = C.cap_rec = C.cap_bad = 0;
+}
 
 static void cz_parallel(int nt, const std::function<void(int)> &fn)
 {
@@ -51,6 +74,7 @@ static void cz_parallel(int nt, const std::function<void(int)> &fn)
 
 void censor_free(Ctx &c)
 {
+    if (c.censor) censor_free_device(*c.censor);
     delete c.censor;
     c.censor = nullptr;
 }
@@ -125,45 +149,6 @@ __global__ __launch_bounds__(256) void k_censor(CensorArgs A)
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
-static int gunzip_all(const uint8_t *src, int64_t len, std::string &out)
-{
-    out.clear();
-    if (len == 0) return 0;
-    z_stream z{};
-    if (inflateInit2(&z, 15 + 32) != Z_OK) { set_error("censor: zlib init"); return -3; }
-    std::vector<char> buf(1 << 22);
-    int64_t pos = 0;
-    bool ended = false;
-    for (;;) {
-        if (z.avail_in == 0) {
-            if (pos >= len) break;
-            const int64_t chunk = std::min<int64_t>(len - pos, 1 << 30);
-            z.next_in = (Bytef *)(src + pos);
-            z.avail_in = (uInt)chunk;
-            pos += chunk;
-        }
-        z.next_out = (Bytef *)buf.data();
-        z.avail_out = (uInt)buf.size();
-        const int st = inflate(&z, Z_NO_FLUSH);
-        out.append(buf.data(), buf.size() - z.avail_out);
-        if (st == Z_STREAM_END) {
-            ended = true;
-            if (z.avail_in == 0 && pos >= len) break;
-            inflateReset(&z);          // GzipFile reads concatenated members
-            ended = false;
-            continue;
-        }
-        if (st != Z_OK && !(st == Z_BUF_ERROR && z.avail_in == 0)) {
-            inflateEnd(&z);
-            set_error("censor: not a valid gzip stream (zlib %d)", st);
-            return -3;
-        }
-    }
-    inflateEnd(&z);
-    if (!ended) { set_error("censor: truncated gzip stream"); return -3; }
-    return 0;
-}
-
 // gzip of `in` as independent members of `block` bytes, compressed in parallel
 static int gzip_parallel(const std::string &in, std::string &out, int level)
 {
@@ -223,7 +208,8 @@ static int split_records(CensorState &C, const std::unordered_map<std::string, i
     for (auto &v : ls) starts.insert(starts.end(), v.begin(), v.end());
     const int64_t nl = (int64_t)starts.size();
     if (nl % 4) {
-        set_error("censor: FASTQ has %lld lines, not a multiple of 4", (long long)nl);
+        set_error("censor: FASTQ has %lld lines, not a multiple of 4",
+                  (long long)(nl + 4 * C.rec_base));
         return -3;
     }
     const int64_t nr = nl / 4;
@@ -270,20 +256,20 @@ static int split_records(CensorState &C, const std::unordered_map<std::string, i
         if (bad[t]) {
             set_error(bad[t] == 1 ? "censor: header of record %lld has no space (ValueError)"
                                   : "censor: header of record %lld has no tile field (IndexError)",
-                      (long long)bad_rec[t] + 1);
+                      (long long)(bad_rec[t] + 1 + C.rec_base));
             return -3;
         }
     return 0;
 }
 
-static int censor_run(Ctx &c, CensorState &C, int n_bad, const char *const *tiles,
-                      const int32_t *cycles)
+static int censor_run(Ctx &c, CensorState &C, CensorState &D, int n_bad,
+                      const char *const *tiles, const int32_t *cycles)
 {
     const int64_t nr = (int64_t)C.h0.size();
     C.keep.assign(2 * (size_t)nr, 0);
     C.base_count = C.score_sum = 0;
     if (nr == 0) return 0;
-    // bad-cycle bitmaps per bad tile id
+    // bad-cycle bitmaps per bad tile id, over the cycles of this piece's reads
     std::unordered_map<std::string, int> tid;
     for (int k = 0; k < n_bad; ++k) tid.emplace(tiles[k], (int)tid.size());
     int maxc = 1;
@@ -297,42 +283,47 @@ static int censor_run(Ctx &c, CensorState &C, int n_bad, const char *const *tile
         bm[(size_t)tid[tiles[k]] * words + (b >> 5)] |= 1u << (b & 31);
     }
     hipStream_t s = c.stream;
-    uint8_t *d_text = nullptr;
-    int64_t *d_s0 = nullptr, *d_q0 = nullptr;
-    int32_t *d_sl = nullptr, *d_ql = nullptr, *d_tile = nullptr, *d_sign = nullptr, *d_keep = nullptr;
-    uint32_t *d_bad = nullptr;
-    unsigned long long *d_sums = nullptr;
-    auto cleanup = [&]() {
-        hipFree(d_text); hipFree(d_s0); hipFree(d_q0); hipFree(d_sl); hipFree(d_ql);
-        hipFree(d_tile); hipFree(d_sign); hipFree(d_keep); hipFree(d_bad); hipFree(d_sums);
-    };
     int st = 0;
     auto H = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && !st) st = hip_fail(e, what);
         return st == 0;
     };
-    H(hipMalloc(&d_text, C.text.size() + 1), "hipMalloc text");
-    H(hipMalloc(&d_s0, 8 * nr), "hipMalloc");
-    H(hipMalloc(&d_q0, 8 * nr), "hipMalloc");
-    H(hipMalloc(&d_sl, 4 * nr), "hipMalloc");
-    H(hipMalloc(&d_ql, 4 * nr), "hipMalloc");
-    H(hipMalloc(&d_tile, 4 * nr), "hipMalloc");
-    H(hipMalloc(&d_sign, 4 * nr), "hipMalloc");
-    H(hipMalloc(&d_keep, 8 * nr), "hipMalloc");
-    H(hipMalloc(&d_bad, 4 * bm.size()), "hipMalloc");
-    H(hipMalloc(&d_sums, 16), "hipMalloc");
-    if (st) { cleanup(); return st; }
-    H(hipMemcpyAsync(d_text, C.text.data(), C.text.size(), hipMemcpyHostToDevice, s), "H2D");
-    H(hipMemcpyAsync(d_s0, C.s0.data(), 8 * nr, hipMemcpyHostToDevice, s), "H2D");
-    H(hipMemcpyAsync(d_q0, C.q0.data(), 8 * nr, hipMemcpyHostToDevice, s), "H2D");
-    H(hipMemcpyAsync(d_sl, C.sl.data(), 4 * nr, hipMemcpyHostToDevice, s), "H2D");
-    H(hipMemcpyAsync(d_ql, C.ql.data(), 4 * nr, hipMemcpyHostToDevice, s), "H2D");
-    H(hipMemcpyAsync(d_tile, C.tile.data(), 4 * nr, hipMemcpyHostToDevice, s), "H2D");
-    H(hipMemcpyAsync(d_sign, C.sign.data(), 4 * nr, hipMemcpyHostToDevice, s), "H2D");
-    H(hipMemcpyAsync(d_bad, bm.data(), 4 * bm.size(), hipMemcpyHostToDevice, s), "H2D");
-    H(hipMemsetAsync(d_sums, 0, 16, s), "memset");
-    CensorArgs a{d_text, d_s0, d_q0, d_sl, d_ql, d_tile, d_sign, nr, d_bad, maxc, words, d_keep,
-                 d_sums};
+    if ((int64_t)C.text.size() + 1 > D.cap_text) {
+        hipFree(D.d_text);
+        D.d_text = nullptr;
+        D.cap_text = (int64_t)C.text.size() + 1;
+        H(hipMalloc(&D.d_text, D.cap_text), "hipMalloc text");
+    }
+    if (nr > D.cap_rec) {
+        hipFree(D.d_s0); hipFree(D.d_q0); hipFree(D.d_sl); hipFree(D.d_ql);
+        hipFree(D.d_tile); hipFree(D.d_sign); hipFree(D.d_keep);
+        D.cap_rec = nr;
+        H(hipMalloc(&D.d_s0, 8 * nr), "hipMalloc");
+        H(hipMalloc(&D.d_q0, 8 * nr), "hipMalloc");
+        H(hipMalloc(&D.d_sl, 4 * nr), "hipMalloc");
+        H(hipMalloc(&D.d_ql, 4 * nr), "hipMalloc");
+        H(hipMalloc(&D.d_tile, 4 * nr), "hipMalloc");
+        H(hipMalloc(&D.d_sign, 4 * nr), "hipMalloc");
+        H(hipMalloc(&D.d_keep, 8 * nr), "hipMalloc");
+    }
+    if ((int64_t)bm.size() > D.cap_bad) {
+        hipFree(D.d_bad);
+        D.cap_bad = (int64_t)bm.size();
+        H(hipMalloc(&D.d_bad, 4 * bm.size()), "hipMalloc");
+    }
+    if (!D.d_sums) H(hipMalloc(&D.d_sums, 16), "hipMalloc");
+    if (st) { censor_free_device(D); return st; }
+    H(hipMemcpyAsync(D.d_text, C.text.data(), C.text.size(), hipMemcpyHostToDevice, s), "H2D");
+    H(hipMemcpyAsync(D.d_s0, C.s0.data(), 8 * nr, hipMemcpyHostToDevice, s), "H2D");
+    H(hipMemcpyAsync(D.d_q0, C.q0.data(), 8 * nr, hipMemcpyHostToDevice, s), "H2D");
+    H(hipMemcpyAsync(D.d_sl, C.sl.data(), 4 * nr, hipMemcpyHostToDevice, s), "H2D");
+    H(hipMemcpyAsync(D.d_ql, C.ql.data(), 4 * nr, hipMemcpyHostToDevice, s), "H2D");
+    H(hipMemcpyAsync(D.d_tile, C.tile.data(), 4 * nr, hipMemcpyHostToDevice, s), "H2D");
+    H(hipMemcpyAsync(D.d_sign, C.sign.data(), 4 * nr, hipMemcpyHostToDevice, s), "H2D");
+    H(hipMemcpyAsync(D.d_bad, bm.data(), 4 * bm.size(), hipMemcpyHostToDevice, s), "H2D");
+    H(hipMemsetAsync(D.d_sums, 0, 16, s), "memset");
+    CensorArgs a{D.d_text, D.d_s0, D.d_q0, D.d_sl, D.d_ql, D.d_tile, D.d_sign, nr, D.d_bad, maxc,
+                 words, D.d_keep, D.d_sums};
     int64_t blocks = (nr + 3) / 4;
     if (blocks > 256 * 64) blocks = 256 * 64;
     if (!st) {
@@ -342,11 +333,10 @@ static int censor_run(Ctx &c, CensorState &C, int n_bad, const char *const *tile
         H(hipGetLastError(), "k_censor");
     }
     unsigned long long sums[2] = {0, 0};
-    H(hipMemcpyAsync(&C.text[0], d_text, C.text.size(), hipMemcpyDeviceToHost, s), "D2H");
-    H(hipMemcpyAsync(C.keep.data(), d_keep, 8 * nr, hipMemcpyDeviceToHost, s), "D2H");
-    H(hipMemcpyAsync(sums, d_sums, 16, hipMemcpyDeviceToHost, s), "D2H");
+    H(hipMemcpyAsync(&C.text[0], D.d_text, C.text.size(), hipMemcpyDeviceToHost, s), "D2H");
+    H(hipMemcpyAsync(C.keep.data(), D.d_keep, 8 * nr, hipMemcpyDeviceToHost, s), "D2H");
+    H(hipMemcpyAsync(sums, D.d_sums, 16, hipMemcpyDeviceToHost, s), "D2H");
     H(hipStreamSynchronize(s), "sync");
-    cleanup();
     if (st) return st;
     prof_flush(c);
     C.score_sum = (long long)sums[0];
@@ -377,6 +367,120 @@ static void censor_write(CensorState &C)
     for (auto &p : piece) C.out += p;
 }
 
+// One piece of whole records: split, censor on the device, rewrite, deflate;
+// the output and the sums go to C.
+static int censor_piece(Ctx &c, CensorState &C, std::string &&text,
+                        const std::unordered_map<std::string, int> &tid, int n_bad,
+                        const char *const *tiles, const int32_t *cycles, int dst_gzip)
+{
+    CensorState P;
+    P.text.swap(text);
+    P.rec_base = C.rec_base;
+    if (int st = split_records(P, tid)) return st;
+    C.rec_base += (int64_t)P.h0.size();
+    auto t0 = std::chrono::steady_clock::now();
+    if (int st = censor_run(c, P, C, n_bad, tiles, cycles)) return st;
+    C.t_device += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    censor_write(P);
+    std::string().swap(P.text);
+    if (dst_gzip) {
+        std::string z;
+        if (int st = gzip_parallel(P.out, z, 1)) return st;
+        C.out += z;
+    } else {
+        C.out += P.out;
+    }
+    C.base_count += P.base_count;
+    C.score_sum += P.score_sum;
+    return 0;
+}
+
+// Streaming inflate: a producer thread inflates the gzip input (multi-member)
+// into ~32 MB chunks while the caller censors the records of the chunks
+// already there (serial inflate is this stage's bound).
+struct InflateQueue {
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<std::string> q;
+    bool done = false;
+    int err = 0;
+    std::string msg;
+};
+
+static void inflate_producer(const uint8_t *src, int64_t len, InflateQueue &Q)
+{
+    const size_t chunk = 32u << 20;
+    auto push = [&](std::string &&piece) {
+        std::unique_lock<std::mutex> lk(Q.m);
+        Q.cv.wait(lk, [&] { return Q.q.size() < 4; });
+        Q.q.push_back(std::move(piece));
+        Q.cv.notify_all();
+    };
+    auto finish = [&](int err, const char *msg) {
+        std::lock_guard<std::mutex> lk(Q.m);
+        Q.err = err;
+        if (msg) Q.msg = msg;
+        Q.done = true;
+        Q.cv.notify_all();
+    };
+    if (len == 0) { finish(0, nullptr); return; }
+    z_stream z{};
+    if (inflateInit2(&z, 15 + 32) != Z_OK) { finish(1, "censor: zlib init"); return; }
+    std::string cur;
+    cur.reserve(chunk + (4u << 20));
+    std::vector<char> buf(4u << 20);
+    int64_t pos = 0;
+    bool ended = false;
+    for (;;) {
+        if (z.avail_in == 0) {
+            if (pos >= len) break;
+            const int64_t take = std::min<int64_t>(len - pos, 1 << 30);
+            z.next_in = (Bytef *)(src + pos);
+            z.avail_in = (uInt)take;
+            pos += take;
+        }
+        z.next_out = (Bytef *)buf.data();
+        z.avail_out = (uInt)buf.size();
+        const int st = inflate(&z, Z_NO_FLUSH);
+        cur.append(buf.data(), buf.size() - z.avail_out);
+        if (cur.size() >= chunk) {
+            push(std::move(cur));
+            cur = std::string();
+            cur.reserve(chunk + (4u << 20));
+        }
+        if (st == Z_STREAM_END) {
+            ended = true;
+            if (z.avail_in == 0 && pos >= len) break;
+            inflateReset(&z);          // GzipFile reads concatenated members
+            ended = false;
+            continue;
+        }
+        if (st != Z_OK && !(st == Z_BUF_ERROR && z.avail_in == 0)) {
+            inflateEnd(&z);
+            finish(1, "censor: not a valid gzip stream");
+            return;
+        }
+    }
+    inflateEnd(&z);
+    if (!ended) { finish(1, "censor: truncated gzip stream"); return; }
+    if (!cur.empty()) push(std::move(cur));
+    finish(0, nullptr);
+}
+
+// end of the last whole record (4 lines) in t, from its start
+static size_t last_record_end(const std::string &t)
+{
+    size_t cut = 0, at = 0;
+    int lines = 0;
+    for (;;) {
+        const void *nl = memchr(t.data() + at, '\n', t.size() - at);
+        if (!nl) break;
+        at = (size_t)((const char *)nl - t.data()) + 1;
+        if (++lines == 4) { lines = 0; cut = at; }
+    }
+    return cut;
+}
+
 }  // namespace mh
 
 using namespace mh;
@@ -391,29 +495,93 @@ extern "C" int mh_censor_fastq(mh_ctx *ctx, const uint8_t *src, int64_t len, int
     if (!c.censor) c.censor = new CensorState();
     CensorState &C = *c.censor;
     C.out.clear();
-    auto t0 = std::chrono::steady_clock::now();
-    if (src_gzip) {
-        if (int st = gunzip_all(src, len, C.text)) return st;
-    } else {
-        C.text.assign((const char *)src, (size_t)len);
-    }
+    C.base_count = C.score_sum = 0;
+    C.rec_base = 0;
+    C.t_host_in = C.t_device = C.t_host_out = 0;
     std::unordered_map<std::string, int> tid;
     for (int k = 0; k < n_bad; ++k) tid.emplace(tiles[k], (int)tid.size());
-    if (int st = split_records(C, tid)) return st;
-    auto t1 = std::chrono::steady_clock::now();
-    if (int st = censor_run(c, C, n_bad, tiles, cycles)) return st;
-    auto t2 = std::chrono::steady_clock::now();
-    censor_write(C);
-    std::string().swap(C.text);
-    if (dst_gzip) {
-        std::string z;
-        if (int st = gzip_parallel(C.out, z, 1)) return st;
-        C.out.swap(z);
+    auto t0 = std::chrono::steady_clock::now();
+    int pieces = 0;
+    if (!src_gzip) {
+        std::string text((const char *)src, (size_t)len);
+        if (len) {
+            if (int st = censor_piece(c, C, std::move(text), tid, n_bad, tiles, cycles, dst_gzip))
+                return st;
+            ++pieces;
+        }
+    } else {
+        InflateQueue Q;
+        std::thread producer(inflate_producer, src, len, std::ref(Q));
+        std::string carry;
+        int st = 0;
+        for (;;) {
+            std::string chunk;
+            bool last = false;
+            {
+                std::unique_lock<std::mutex> lk(Q.m);
+                Q.cv.wait(lk, [&] { return !Q.q.empty() || Q.done; });
+                if (!Q.q.empty()) {
+                    chunk = std::move(Q.q.front());
+                    Q.q.pop_front();
+                    Q.cv.notify_all();
+                } else {
+                    last = true;
+                    if (Q.err) {
+                        set_error("%s", Q.msg.c_str());
+                        st = -3;
+                    }
+                }
+            }
+            if (st) break;
+            if (last) {
+                C.t_host_in = std::chrono::duration<double, std::milli>(
+                                  std::chrono::steady_clock::now() - t0).count();
+                // a trailing partial record (or one without its last newline)
+                if (!carry.empty()) {
+                    st = censor_piece(c, C, std::move(carry), tid, n_bad, tiles, cycles, dst_gzip);
+                    ++pieces;
+                }
+                break;
+            }
+            carry += chunk;
+            std::string().swap(chunk);
+            const size_t cut = last_record_end(carry);
+            if (cut == 0) continue;
+            std::string rest(carry, cut);
+            carry.resize(cut);
+            st = censor_piece(c, C, std::move(carry), tid, n_bad, tiles, cycles, dst_gzip);
+            ++pieces;
+            carry.swap(rest);
+            if (st) break;
+        }
+        if (st) {
+            // drain the producer before leaving
+            {
+                std::unique_lock<std::mutex> lk(Q.m);
+                Q.q.clear();
+                Q.cv.notify_all();
+            }
+            for (;;) {
+                std::unique_lock<std::mutex> lk(Q.m);
+                if (Q.done) break;
+                Q.cv.wait(lk, [&] { return !Q.q.empty() || Q.done; });
+                Q.q.clear();
+                Q.cv.notify_all();
+            }
+            producer.join();
+            C.out.clear();
+            return st;
+        }
+        producer.join();
     }
-    auto t3 = std::chrono::steady_clock::now();
-    C.t_host_in = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    C.t_device = std::chrono::duration<double, std::milli>(t2 - t1).count();
-    C.t_host_out = std::chrono::duration<double, std::milli>(t3 - t2).count();
+    if (!pieces && dst_gzip) {
+        // an empty FASTQ still makes one (empty) gzip member
+        if (int st = gzip_parallel(std::string(), C.out, 1)) return st;
+    }
+    const double total = std::chrono::duration<double, std::milli>(
+                             std::chrono::steady_clock::now() - t0).count();
+    if (!src_gzip) C.t_host_in = 0;
+    C.t_host_out = total - C.t_host_in;
     if (base_count) *base_count = C.base_count;
     if (score_sum) *score_sum = C.score_sum;
     return 0;
