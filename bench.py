@@ -252,11 +252,18 @@ def bench_censor(args):
     elapsed = time.perf_counter() - t0
     host_ms = ctx.censor_timing()
     k_ms, k_n = ctx.profile_get('k_censor')
-    avg_s = k_ms / 1e3 / max(k_n, 1)
-    # algorithmic bytes per launch: read and write every base and quality
-    # byte once (the kernel censors in place), 16 B of spans per record
+    # k_censor runs once per inflated piece (~32 MB of FASTQ): account per
+    # file.  Algorithmic bytes: read and write every base and quality byte
+    # once (the kernel censors in place), 16 B of spans per record.
+    step_s = k_ms / 1e3 / max(args.steps, 1)
     algo = 2 * 2 * READ_LEN * args.pairs + 16 * args.pairs
-    achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
+    achieved = algo / step_s / 1e9 if step_s > 0 else 0.0
+    pmc = read_pmc_traffic('k_censor', args.pairs, 'censor')
+    try:
+        with open(os.path.join(REPO, 'profiles', 'pmc_traffic_censor.json')) as f:
+            pmc_launches = json.load(f)['kernels']['k_censor']['launches']
+    except (OSError, KeyError, ValueError):
+        pmc_launches = 1
     # FASTQ ingest of the pair (what prelim_map does first)
     tmp = tempfile.mkdtemp(prefix='bench_fq_')
     p1, p2 = os.path.join(tmp, 'R1.fastq.gz'), os.path.join(tmp, 'R2.fastq.gz')
@@ -289,8 +296,9 @@ def bench_censor(args):
         'ingest_reads_per_s': round(2 * args.pairs / ingest_s, 1),
         'roofline': {'kernel': 'k_censor', 'bound': 'hbm', 'achieved': round(achieved, 3),
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 6),
-                     'traffic': read_pmc_traffic('k_censor', args.pairs, 'censor'), 'algo_bytes_per_launch': algo,
-                     'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': k_n},
+                     'traffic': None if pmc is None else pmc * pmc_launches,
+                     'per': 'file (all pieces of one step)', 'algo_bytes': algo,
+                     'kernel_ms_per_file': round(1e3 * step_s, 4), 'launches': k_n},
         'cpu_baseline': {'value': round(sample / cpu_s, 1), 'unit': 'reads/s', 'cores': 1,
                          'kind': 'port',
                          'sample': 'first {} reads of the same R1 (plain text) through the '
