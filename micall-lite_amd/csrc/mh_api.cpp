@@ -16,6 +16,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "mh_gunzip.h"
 #include "mh_internal.h"
 #include "mh_text.h"
 
@@ -345,26 +346,35 @@ static void par_for(int nt, const std::function<void(int)> &fn)
     for (auto &x : th) x.join();
 }
 
-// The whole (gzip or plain) file; gzread decodes concatenated members.
+// The whole (gzip or plain) file; every concatenated gzip member is decoded
+// (as gzread does), with libdeflate when the system has it (mh_gunzip.cpp).
 static int slurp(const char *path, std::string &data)
 {
     data.clear();
-    gzFile f = gzopen(path, "rb");
+    FILE *f = fopen(path, "rb");
     if (!f) { set_error("cannot open FASTQ %s", path); return -3; }
-    gzbuffer(f, 1 << 22);
-    FILE *raw = fopen(path, "rb");
-    if (raw) {
-        fseek(raw, 0, SEEK_END);
-        const long sz = ftell(raw);
-        fclose(raw);
-        if (sz > 0) data.reserve((size_t)sz * 3);
+    std::string raw;
+    fseek(f, 0, SEEK_END);
+    const long sz = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    if (sz > 0) {
+        raw.resize((size_t)sz);
+        if (fread(&raw[0], 1, (size_t)sz, f) != (size_t)sz) {
+            fclose(f);
+            set_error("cannot read FASTQ %s", path);
+            return -3;
+        }
     }
-    std::vector<char> buf(1 << 24);
-    int got;
-    while ((got = gzread(f, buf.data(), (unsigned)buf.size())) > 0) data.append(buf.data(), got);
-    const bool err = got < 0;
-    gzclose(f);
-    if (err) { set_error("gzip error reading %s", path); return -3; }
+    fclose(f);
+    if (raw.size() >= 2 && (uint8_t)raw[0] == 0x1f && (uint8_t)raw[1] == 0x8b) {
+        std::string why;
+        if (gunzip_buffer((const uint8_t *)raw.data(), (int64_t)raw.size(), data, why)) {
+            set_error("gzip error reading %s: %s", path, why.c_str());
+            return -3;
+        }
+    } else {
+        data.swap(raw);
+    }
     return 0;
 }
 

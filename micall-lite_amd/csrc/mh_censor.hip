@@ -1,8 +1,9 @@
 // mh_censor.hip -- censor_fastq.censor (micall/core/censor_fastq.py:32-102)
 // on gfx950, behind mh_censor_fastq / mh_censor_output:
-//   host      streaming gunzip (zlib, multi-member): a producer thread
-//             inflates ~32 MB chunks while the whole records of the chunks
-//             already there are censored; records split in parallel,
+//   host      gunzip (multi-member): libdeflate on the whole file when the
+//             system has it, else streaming zlib (a producer thread inflates
+//             ~32 MB chunks while the whole records of the chunks already
+//             there are censored); records split in parallel,
 //             tile + read direction from each header exactly as :59-63 parse
 //             them, bad (tile, cycle) set from the caller
 //   k_censor  one wave64 per read: the bases / qualities of bad cycles
@@ -26,6 +27,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "mh_gunzip.h"
 #include "mh_internal.h"
 
 namespace mh {
@@ -509,6 +511,21 @@ extern "C" int mh_censor_fastq(mh_ctx *ctx, const uint8_t *src, int64_t len, int
                 return st;
             ++pieces;
         }
+    } else if (gunzip_fast_available()) {
+        // libdeflate decodes the whole file faster than the streaming zlib
+        // producer below can overlap it with the rest
+        std::string text, why;
+        if (gunzip_buffer(src, len, text, why)) {
+            set_error("censor: %s", why.c_str());
+            return -3;
+        }
+        C.t_host_in = std::chrono::duration<double, std::milli>(
+                          std::chrono::steady_clock::now() - t0).count();
+        if (!text.empty()) {
+            if (int st = censor_piece(c, C, std::move(text), tid, n_bad, tiles, cycles, dst_gzip))
+                return st;
+            ++pieces;
+        }
     } else {
         InflateQueue Q;
         std::thread producer(inflate_producer, src, len, std::ref(Q));
@@ -581,6 +598,7 @@ extern "C" int mh_censor_fastq(mh_ctx *ctx, const uint8_t *src, int64_t len, int
     const double total = std::chrono::duration<double, std::milli>(
                              std::chrono::steady_clock::now() - t0).count();
     if (!src_gzip) C.t_host_in = 0;
+    if (!C.t_host_in) C.t_host_in = 0;
     C.t_host_out = total - C.t_host_in;
     if (base_count) *base_count = C.base_count;
     if (score_sum) *score_sum = C.score_sum;
