@@ -161,21 +161,8 @@ static int gzip_parallel(const std::string &in, std::string &out, int level)
     const int nt = (int)std::min<int64_t>(s2a_threads(), nblk);
     cz_parallel(nt, [&](int t) {
         for (int64_t b = t; b < nblk; b += nt) {
-            z_stream z{};
-            if (deflateInit2(&z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
-                err[b] = 1;
-                continue;
-            }
             const int64_t a = b * block, e = std::min<int64_t>((int64_t)in.size(), a + block);
-            std::string &o = parts[b];
-            o.resize(deflateBound(&z, (uLong)(e - a)) + 64);
-            z.next_in = (Bytef *)(in.data() + a);
-            z.avail_in = (uInt)(e - a);
-            z.next_out = (Bytef *)&o[0];
-            z.avail_out = (uInt)o.size();
-            if (deflate(&z, Z_FINISH) != Z_STREAM_END) err[b] = 1;
-            o.resize(o.size() - z.avail_out);
-            deflateEnd(&z);
+            if (gzip_member(in.data() + a, (size_t)(e - a), parts[b], level)) err[b] = 1;
         }
     });
     for (int e : err) if (e) { set_error("censor: deflate failed"); return -2; }

@@ -23,12 +23,21 @@ enum { LD_SUCCESS = 0, LD_BAD_DATA = 1, LD_SHORT_OUTPUT = 2, LD_INSUFFICIENT_SPA
 typedef Ld *(*ld_alloc_t)(void);
 typedef void (*ld_free_t)(Ld *);
 typedef int (*ld_gunzip_ex_t)(Ld *, const void *, size_t, void *, size_t, size_t *, size_t *);
+struct Lc;
+typedef Lc *(*lc_alloc_t)(int);
+typedef void (*lc_free_t)(Lc *);
+typedef size_t (*lc_gzip_t)(Lc *, const void *, size_t, void *, size_t);
+typedef size_t (*lc_bound_t)(Lc *, size_t);
 
 struct LdApi {
     ld_alloc_t alloc = nullptr;
     ld_free_t free_ = nullptr;
     ld_gunzip_ex_t gunzip = nullptr;
-    bool ok = false;
+    lc_alloc_t c_alloc = nullptr;
+    lc_free_t c_free = nullptr;
+    lc_gzip_t c_gzip = nullptr;
+    lc_bound_t c_bound = nullptr;
+    bool ok = false, c_ok = false;
 };
 
 const LdApi &ld_api()
@@ -43,6 +52,11 @@ const LdApi &ld_api()
         api.free_ = (ld_free_t)dlsym(h, "libdeflate_free_decompressor");
         api.gunzip = (ld_gunzip_ex_t)dlsym(h, "libdeflate_gzip_decompress_ex");
         api.ok = api.alloc && api.free_ && api.gunzip;
+        api.c_alloc = (lc_alloc_t)dlsym(h, "libdeflate_alloc_compressor");
+        api.c_free = (lc_free_t)dlsym(h, "libdeflate_free_compressor");
+        api.c_gzip = (lc_gzip_t)dlsym(h, "libdeflate_gzip_compress");
+        api.c_bound = (lc_bound_t)dlsym(h, "libdeflate_gzip_compress_bound");
+        api.c_ok = api.c_alloc && api.c_free && api.c_gzip && api.c_bound;
     });
     return api;
 }
@@ -131,6 +145,31 @@ int gunzip_buffer(const uint8_t *src, int64_t len, std::string &out, std::string
     if (len <= 0) return 0;
     const LdApi &api = ld_api();
     return api.ok ? gunzip_ld(api, src, len, out, why) : gunzip_zlib(src, len, out, why);
+}
+
+int gzip_member(const char *src, size_t len, std::string &out, int level)
+{
+    const LdApi &api = ld_api();
+    if (api.c_ok) {
+        Lc *c = api.c_alloc(level);
+        if (c) {
+            out.resize(api.c_bound(c, len) + 64);
+            const size_t n = api.c_gzip(c, src, len, &out[0], out.size());
+            api.c_free(c);
+            if (n) { out.resize(n); return 0; }
+        }
+    }
+    z_stream z{};
+    if (deflateInit2(&z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return -2;
+    out.resize(deflateBound(&z, (uLong)len) + 64);
+    z.next_in = (Bytef *)src;
+    z.avail_in = (uInt)len;
+    z.next_out = (Bytef *)&out[0];
+    z.avail_out = (uInt)out.size();
+    const int st = deflate(&z, Z_FINISH);
+    out.resize(out.size() - z.avail_out);
+    deflateEnd(&z);
+    return st == Z_STREAM_END ? 0 : -2;
 }
 
 }  // namespace mh

@@ -11,5 +11,8 @@ namespace mh {
 int gunzip_buffer(const uint8_t *src, int64_t len, std::string &out, std::string &why);
 // true when the libdeflate decoder is in use
 bool gunzip_fast_available();
+// One gzip member of src[0 .. len) at `level` (libdeflate when present);
+// 0, or -2 when compression fails.
+int gzip_member(const char *src, size_t len, std::string &out, int level);
 
 }  // namespace mh
