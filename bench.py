@@ -363,12 +363,13 @@ def bench_aln2counts(args):
     host_ms = ctx.a2c_timing(a2c.SLOT_REPORT)
     kern = {k: ctx.profile_get(k) for k in ('k_a2c_count', 'k_a2c_ins')}
     n_groups = ctx.a2c_load_csv(a2c.SLOT_REPORT, aligned, a2c._CODON_CHARS)
-    bins = sum(-(-max(ctx.a2c_group(a2c.SLOT_REPORT, g)['ncod']) // 64) for g in range(n_groups))
+    bins = sum(-(-max(ctx.a2c_group(a2c.SLOT_REPORT, g)['ncod']) // 21) for g in range(n_groups))
     k_ms, k_n = kern['k_a2c_count']
     avg_s = k_ms / 1e3 / max(k_n, 1)
     # algorithmic bytes per launch: every row's seq once, its 24-B record,
-    # and the counters (count + first row, 4 B each) of every (bin, frame)
-    algo = seq_bytes + 24 * n_rows + 2 * 4 * bins * 3 * 64 * 39
+    # and the counters (count + first row, 4 B each) of every bin: 21 codons
+    # x 3 frames x (21 amino acids + 18 bases)
+    algo = seq_bytes + 24 * n_rows + 2 * 4 * bins * 63 * 39
     achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
     sample = min(3000, n_rows)
     lines = aligned.split('\n', sample + 1)

@@ -4,10 +4,13 @@
 //
 //   k_a2c_count   SequenceReport._count_reads (:115-172) with
 //                 SeedAmino.count_aminos / SeedNucleotide.count_nucleotides
-//                 (:595-606, :636-645).  Work unit: (chunk of <= 1024 rows of
-//                 one bin, reading frame); a bin is 64 consecutive codons of
-//                 one (refname, qcut) group.  A wave takes a row, a lane one
-//                 codon of the bin: the three characters of the frame- and
+//                 (:595-606, :636-645).  Work unit: a chunk of <= 1024 rows of
+//                 one bin; a bin is 21 consecutive codons of one (refname,
+//                 qcut) group.  A wave takes a row, lane 21 f + c codon c of
+//                 the bin in reading frame f (63 lanes: the three frames read
+//                 the same bytes in one load instruction, so every row is
+//                 fetched once per bin, not once per frame): the three
+//                 characters of the frame- and
 //                 offset-padded read ('-' outside it, :155-157), the amino
 //                 acid from the codon table, then LDS counters per (codon,
 //                 amino acid) and per (codon, position, base): a count and
@@ -43,11 +46,12 @@
 
 namespace mh {
 
-constexpr int A2C_W = 64;                       // codons per bin (one per lane)
+constexpr int A2C_W = 21;                       // codons per bin (x 3 frames = 63 lanes)
+constexpr int A2C_LANES = 3 * A2C_W;
 constexpr int A2C_CHUNK = 1024;                 // rows per workgroup
 constexpr int A2C_NAA = 21;                     // AMINO_ALPHABET
 constexpr int A2C_STRIDE = A2C_NAA + 18;        // per codon: 21 amino acids, 3 x 6 bases
-constexpr int A2C_CELLS = A2C_W * A2C_STRIDE;   // counters per (bin, frame)
+constexpr int A2C_CELLS = A2C_LANES * A2C_STRIDE;   // counters per bin (3 frames)
 constexpr int A2C_SLOTS = 4;
 constexpr uint32_t A2C_NONE = 0xffffffffu;
 constexpr int64_t A2C_MAX_SPAN = 1 << 28;
@@ -86,7 +90,7 @@ struct A2CState {
     std::vector<std::string> g_ref, g_qcut;
     std::vector<int32_t> g_ncod;              // 3 per group
     std::vector<int64_t> g_bin0;              // n_groups + 1
-    std::vector<uint32_t> h_cnt, h_first;     // [bin][frame][A2C_CELLS]
+    std::vector<uint32_t> h_cnt, h_first;     // [bin][frame * 21 + codon][39]
     int8_t code[512];
     uint8_t cls[256];
     std::string pool;                         // row text when it is not the caller's CSV
@@ -121,7 +125,6 @@ __global__ __launch_bounds__(256) void k_a2c_count(A2CCountArgs A)
     __shared__ uint32_t s_cnt[A2C_CELLS], s_first[A2C_CELLS];
     __shared__ int8_t s_code[512];
     __shared__ uint8_t s_cls[256];
-    const int f = blockIdx.y;
     const A2CChunk ch = A.chunks[blockIdx.x];
     for (int i = threadIdx.x; i < A2C_CELLS; i += 256) {
         s_cnt[i] = 0;
@@ -132,10 +135,12 @@ __global__ __launch_bounds__(256) void k_a2c_count(A2CCountArgs A)
     s_cls[threadIdx.x] = A.cls[threadIdx.x];
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int j = ch.codon0 + lane;              // this lane's codon
-    // lane stride 39 words: odd, so the lanes of a wave hit 64 distinct banks
+    const int f = lane / A2C_W;                  // this lane's frame and codon
+    const int j = ch.codon0 + lane - A2C_W * f;
+    // lane stride 39 words: odd, so the lanes of a wave hit distinct banks
     uint32_t *cc = s_cnt + lane * A2C_STRIDE, *cf = s_first + lane * A2C_STRIDE;
     for (int64_t i = ch.beg + (threadIdx.x >> 6); i < ch.end; i += 4) {
+        if (lane >= A2C_LANES) continue;
         const A2CRow R = A.rows[A.bin_rows[i]];
         // codons offset // 3 .. ceil((frame + offset + len) / 3) - 1 (:155-160)
         if (j < R.off / 3 || j >= (f + R.off + R.len + 2) / 3) continue;
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(256) void k_a2c_count(A2CCountArgs A)
             }
     }
     __syncthreads();
-    const size_t base = ((size_t)ch.bin * 3 + f) * A2C_CELLS;
+    const size_t base = (size_t)ch.bin * A2C_CELLS;
     for (int i = threadIdx.x; i < A2C_CELLS; i += 256) {
         const uint32_t fr = s_first[i];
         if (fr == A2C_NONE) continue;
@@ -573,7 +578,7 @@ static int a2c_count(Ctx &c, A2CState &S, const char *text, int64_t text_len)
     if (int st = a2c_upload(S.d_chunks, chunks.data(), chunks.size(), s)) return st;
     if (int st = a2c_upload(S.d_code, S.code, 512, s)) return st;
     if (int st = a2c_upload(S.d_cls, S.cls, 256, s)) return st;
-    const size_t cells = (size_t)S.n_bins * 3 * A2C_CELLS;
+    const size_t cells = (size_t)S.n_bins * A2C_CELLS;
     MH_HIP(hipMalloc(&S.d_cnt, sizeof(uint32_t) * (cells ? cells : 1)));
     MH_HIP(hipMalloc(&S.d_first, sizeof(uint32_t) * (cells ? cells : 1)));
     if (cells) {
@@ -584,7 +589,7 @@ static int a2c_count(Ctx &c, A2CState &S, const char *text, int64_t text_len)
         A2CCountArgs a{S.d_text, S.d_rows, S.d_bin_rows, S.d_chunks, S.d_code, S.d_cls,
                        S.d_cnt, S.d_first};
         const int p0 = prof_begin(c, "k_a2c_count");
-        hipLaunchKernelGGL(k_a2c_count, dim3((unsigned)chunks.size(), 3), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_a2c_count, dim3((unsigned)chunks.size()), dim3(256), 0, s, a);
         prof_end(c, p0);
         MH_HIP(hipGetLastError());
     }
@@ -848,8 +853,8 @@ extern "C" int mh_a2c_counts(mh_ctx *ctx, int slot, int64_t g, int frame, uint32
     const int n = S.g_ncod[3 * g + frame];
     if (n && (!aa_count || !aa_first || !nuc_count || !nuc_first)) return -3;
     for (int j = 0; j < n; ++j) {
-        const size_t at = ((size_t)(S.g_bin0[g] + j / A2C_W) * 3 + frame) * A2C_CELLS +
-                          (size_t)(j % A2C_W) * A2C_STRIDE;
+        const size_t at = (size_t)(S.g_bin0[g] + j / A2C_W) * A2C_CELLS +
+                          (size_t)(A2C_W * frame + j % A2C_W) * A2C_STRIDE;
         memcpy(aa_count + (size_t)j * A2C_NAA, &S.h_cnt[at], 4 * A2C_NAA);
         memcpy(aa_first + (size_t)j * A2C_NAA, &S.h_first[at], 4 * A2C_NAA);
         memcpy(nuc_count + (size_t)j * 18, &S.h_cnt[at + A2C_NAA], 4 * 18);
