@@ -155,20 +155,22 @@ struct HotLds {
 __device__ int merge_ins_strings(const DevReads &R, const RowV &w, int o1, int l1, const RowV &v,
                                  int o2, int l2, int q_cutoff, char *out)
 {
-    const RowV *r1 = &w, *r2 = &v;
-    if (l1 > l2) {
-        r1 = &v; r2 = &w;
+    // the two mates as values (a swap of pointers to them would put them
+    // in scratch memory)
+    const bool sw = l1 > l2;
+    const RowV r1 = sw ? v : w, r2 = sw ? w : v;
+    if (sw) {
         int x = o1; o1 = o2; o2 = x;
         x = l1; l1 = l2; l2 = x;
     }
     const unsigned char cut = (unsigned char)(q_cutoff + 33);
     for (int i = 0; i < l2; ++i) {
         char c2, q2c;
-        sam_base(R, *r2, o2 + i, c2, q2c);
+        sam_base(R, r2, o2 + i, c2, q2c);
         const unsigned char b = (unsigned char)q2c;
         if (i < l1) {
             char c1, q1c;
-            sam_base(R, *r1, o1 + i, c1, q1c);
+            sam_base(R, r1, o1 + i, c1, q1c);
             const unsigned char a = (unsigned char)q1c;
             if (c1 == c2) {
                 out[i] = (a > cut || b > cut) ? c1 : 'N';
@@ -306,7 +308,11 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
         // sam2aln.py:133-135, :240-273 ----
         if (lane == 0) {
             int n = 0, used = 0;
-            for (int pass = 0; pass < nm && n_iops; ++pass) {
+            // unrolled: mate(pass) with a run-time pass would keep the two
+            // RowV in scratch memory
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {
+                if (pass >= nm || !n_iops) break;
                 const RowV v = mate(pass);
                 for (int o = 0; o < v.n_cigar; ++o) {
                     if ((v.cig[o] & 15) != MH_OP_I) continue;

@@ -134,7 +134,11 @@ __global__ __launch_bounds__(256) void k_s2a_merge(S2AArgs A)
     for (int64_t u = (int64_t)blockIdx.x * wpb + wv; u < A.n; u += (int64_t)gridDim.x * wpb) {
         const int64_t rows[2] = {A.units[2 * u], A.units[2 * u + 1]};
         const int nm = rows[1] >= 0 ? 2 : 1;
+        // every loop over the mates is unrolled: mt[k] with a run-time k
+        // would put the array in scratch memory (80 B per lane, ~5 GB of
+        // HBM writes per launch at C2)
         Mate mt[2];
+#pragma unroll
         for (int k = 0; k < 2; ++k) {
             mt[k].row = -1; mt[k].pad = 0; mt[k].rf = 0; mt[k].len = 0;
             mt[k].c = cq + 2 * k * A.span_cap;
@@ -142,7 +146,9 @@ __global__ __launch_bounds__(256) void k_s2a_merge(S2AArgs A)
         }
         // ---- apply_cigar (sam2aln.py:84-153): op offsets by a lane-parallel
         // scan, then the read expanded into reference coordinates ----
-        for (int k = 0; k < nm; ++k) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (k >= nm) break;
             const int64_t r = rows[k];
             const int nc = A.n_cig[r];
             const uint32_t *ops = A.cig + A.cig_off[r];
@@ -174,7 +180,9 @@ __global__ __launch_bounds__(256) void k_s2a_merge(S2AArgs A)
             mt[k].len = mt[k].pad + rf0;
         }
         __builtin_amdgcn_wave_barrier();
-        for (int k = 0; k < nm; ++k) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (k >= nm) break;
             const int64_t r = rows[k];
             const int32_t *oref = opref + k * (A.ops_cap + 1), *ord = opread + k * (A.ops_cap + 1);
             const uint8_t *s = A.seq + A.soff[r], *q = A.qual + A.soff[r];
