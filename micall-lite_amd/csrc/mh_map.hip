@@ -674,16 +674,36 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     int64_t ck_base = 0;   // lane 0: this wave's current CIGAR pool chunk
     int ck_left = 0;
     int n_fast = 0;        // extensions resolved by dp_ungapped
-    for (int w = blockIdx.x * wpb + wv; w < n_work; w += gridDim.x * wpb) {
-        const int sid = A.work[w];
-        const int64_t r = sid / MAXCAND;
-        const Cand cd = A.cand[sid];
-        const int m = A.R.len[r];
-        const int64_t roff = A.R.off[r];
-        const int reflen = A.I.ref_len[cd.ref];
-        const int64_t gref = A.I.ref_off[cd.ref];
+    // Software pipeline over the work items: the descriptor chain of the next
+    // item (work id -> candidate and read -> reference) is loaded while this
+    // one is aligned, so a wave pays one dependent global round trip per
+    // extension (its staging loads) instead of four.
+    const int wstride = gridDim.x * wpb;
+    int w = blockIdx.x * wpb + wv;
+    int sid_n = 0, m_n = 0, reflen_n = 0;
+    Cand cd_n{};
+    int64_t roff_n = 0, gref_n = 0;
+    if (w < n_work) {
+        sid_n = A.work[w];
+        cd_n = A.cand[sid_n];
+        m_n = A.R.len[sid_n / MAXCAND];
+        roff_n = A.R.off[sid_n / MAXCAND];
+        reflen_n = A.I.ref_len[cd_n.ref];
+        gref_n = A.I.ref_off[cd_n.ref];
+    }
+    for (; w < n_work; w += wstride) {
+        const int sid = sid_n;
+        const Cand cd = cd_n;
+        const int m = m_n;
+        const int64_t roff = roff_n;
+        const int reflen = reflen_n;
+        const int64_t gref = gref_n;
         const int d0 = cd.center - HALF;
         const int strand = cd.strand;
+        const int wn = w + wstride;
+        const bool more = wn < n_work;
+        int sid_nn = 0;
+        if (more) sid_nn = A.work[wn];   // lands with the staging loads below
 
         // ---- stage per-row score tables, read codes and the ref window:
         // every load of a round is issued before any is used ----
@@ -734,6 +754,12 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             }
         }
         wave_sync();
+        if (more) {   // next item's candidate and read descriptors: land during the DP
+            sid_n = sid_nn;
+            cd_n = A.cand[sid_nn];
+            m_n = A.R.len[sid_nn / MAXCAND];
+            roff_n = A.R.off[sid_nn / MAXCAND];
+        }
 
         int best, bi, bl;
         const bool fast = A.fast && m > 2 * GBAR + 8 && m <= 512 &&
@@ -806,6 +832,10 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             bl = 63 - (int)(bk & 63);
         }
         const int minsc = A.len_tab[(MAXLEN + 1) + m];
+        if (more) {   // next item's reference window: lands during the traceback
+            reflen_n = A.I.ref_len[cd_n.ref];
+            gref_n = A.I.ref_off[cd_n.ref];
+        }
         wave_sync();
 
         // ---- traceback (lane 0): CIGAR runs, back to front, and the lane of

@@ -17,12 +17,21 @@ namespace mh {
 constexpr int PU_INSBUF = 2048;   // merged insertion bytes per unit
 constexpr int PU_MAXINS = 2 * MH_MAXOPS;
 constexpr int PU_LDS = 160 * 1024;
+constexpr int PU_XCH = 5;        // 64-position chunks per mate expanded with all loads in flight
 
 struct RowV {
     int present, flag, ref, pos, n_cigar, rev, m;
     const uint32_t *cig;
     int64_t roff;
+    uint32_t op0;   // this lane's op of the first 64 (fetch_ops)
 };
+
+// This lane's CIGAR op of the first 64, loaded ahead of apply_cigar.
+__device__ __forceinline__ void fetch_ops(RowV &v, int lane)
+{
+    v.op0 = 0;
+    if (v.present && lane < v.n_cigar) v.op0 = v.cig[lane];
+}
 
 struct PileArgs {
     // source 0: mapped records
@@ -62,15 +71,17 @@ __device__ __forceinline__ void load_row(const PileArgs &A, int64_t row, RowV &v
     v.present = 0;
     if (row < 0) return;
     if (SRC == 0) {
+        // no branch on the loaded fields, so a prefetch of the next unit's
+        // rows does not wait for them here
         const Rec &r = A.rec[row];
-        if (r.sam_ref < 0) return;      // RNAME '*' is not in @SQ (matchmaker)
-        v.present = 1;
-        v.flag = r.flag;
-        v.ref = r.sam_ref;
+        const int sref = r.sam_ref, flag = r.flag;
+        v.present = sref >= 0;          // RNAME '*' is not in @SQ (matchmaker)
+        v.flag = flag;
+        v.ref = sref;
         v.pos = r.sam_pos;
-        v.n_cigar = (r.flag & 4) ? 0 : r.n_cigar;
+        v.n_cigar = (flag & 4) ? 0 : r.n_cigar;
         v.cig = A.pool + r.cig_off;
-        v.rev = (r.flag & 4) ? 0 : r.rev;
+        v.rev = (flag & 4) ? 0 : r.rev;
     } else {
         v.present = 1;
         v.flag = A.flag[row];
@@ -217,18 +228,34 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
     if (threadIdx.x == 0) { hot->read_count = 0; hot->max_pos = 0; hot->first_unit = INT64_MAX; }
     __syncthreads();
 
-    for (int64_t u = (int64_t)blockIdx.x * wpb + wv; u < A.n_units; u += (int64_t)gridDim.x * wpb) {
+    // the next unit's rows are loaded while this one is processed
+    const int64_t ustride = (int64_t)gridDim.x * wpb;
+    int64_t u = (int64_t)blockIdx.x * wpb + wv;
+    auto unit_rows = [&](int64_t uu, RowV &a, RowV &b) {
         int64_t row1, row2;
         if (SRC == 0) {
-            row1 = A.paired ? 2 * u : u;
-            row2 = A.paired ? 2 * u + 1 : -1;
+            row1 = A.paired ? 2 * uu : uu;
+            row2 = A.paired ? 2 * uu + 1 : -1;
         } else {
-            row1 = A.units[2 * u];
-            row2 = A.units[2 * u + 1];
+            row1 = A.units[2 * uu];
+            row2 = A.units[2 * uu + 1];
         }
-        RowV r1, r2;
-        load_row<SRC>(A, row1, r1);
-        load_row<SRC>(A, row2, r2);
+        load_row<SRC>(A, row1, a);
+        load_row<SRC>(A, row2, b);
+    };
+    RowV n1, n2;
+    n1.present = n2.present = 0;
+    bool ops_ready = false;   // the CIGAR ops of n1 / n2 were fetched (not on a skipped unit)
+    if (u < A.n_units) unit_rows(u, n1, n2);
+    for (; u < A.n_units; u += ustride) {
+        RowV r1 = n1, r2 = n2;
+        if (!ops_ready) {
+            fetch_ops(r1, lane);
+            fetch_ops(r2, lane);
+        }
+        ops_ready = false;
+        const bool more = u + ustride < A.n_units;
+        if (more) unit_rows(u + ustride, n1, n2);
         if (SRC == 0 && !r1.present && r2.present) { r1 = r2; r2.present = 0; }  // unpaired view
         if (!r1.present) continue;
         if (r2.present && r1.ref != r2.ref) continue;           // remap.py:96-98
@@ -260,7 +287,7 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
                 const int o = o0 + lane;
                 int dref = 0, dread = 0, isd = 0, isi = 0, badop = 0;
                 if (o < nc) {
-                    const uint32_t op = mk.cig[o];
+                    const uint32_t op = o0 == 0 ? mk.op0 : mk.cig[o];
                     const int n = (int)(op >> 4), t = (int)(op & 15);
                     if (t == MH_OP_M) { dref = n; dread = n; }
                     else if (t == MH_OP_D) { dref = n; isd = 1; }
@@ -288,21 +315,91 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
             continue;
         }
         __builtin_amdgcn_wave_barrier();
+        const int spanA = lenA - padA, spanB = nm > 1 ? lenB - padB : 0;
+        if (spanA <= PU_XCH * 64 && spanB <= PU_XCH * 64) {
+            // Both mates at once: every chunk's op lookup (LDS) first, then
+            // all base loads in flight together, then the LDS writes; one
+            // dependent global round trip per unit instead of one per chunk.
+            int bx[2][PU_XCH];   // strand-adjusted read index; -1 deletion, -2 none
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (k >= nm) break;
-            const int span = len(k) - pad(k);
-            const RowV mk = mate(k);
-            for (int t = lane; t < span; t += 64) {
-                // the M/D op covering reference offset t (I/S ops span nothing)
-                int o = 0;
-                while (L.opref(k)[o + 1] <= t) ++o;
-                const int rd = L.opread(k)[o];
-                char c = '-', q = ' ';
-                if (rd >= 0) sam_base(A.R, mk, rd + (t - L.opref(k)[o]), c, q);
-                L.c(k)[t] = c;
-                L.q(k)[t] = q;
+            for (int k = 0; k < 2; ++k) {
+                const RowV mk = mate(k);
+                const int span = k ? spanB : spanA;
+#pragma unroll
+                for (int ch = 0; ch < PU_XCH; ++ch) {
+                    const int t = ch * 64 + lane;
+                    int x = -2;
+                    if (k < nm && t < span) {
+                        // the M/D op covering reference offset t (I/S ops span nothing)
+                        int o = 0;
+                        while (L.opref(k)[o + 1] <= t) ++o;
+                        const int rd = L.opread(k)[o];
+                        x = -1;
+                        if (rd >= 0) {
+                            x = rd + (t - L.opref(k)[o]);
+                            if (mk.rev) x = mk.m - 1 - x;
+                        }
+                    }
+                    bx[k][ch] = x;
+                }
             }
+            uint32_t nw[2][PU_XCH], sw[2][PU_XCH], qw[2][PU_XCH];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int64_t roff = mate(k).roff;
+#pragma unroll
+                for (int ch = 0; ch < PU_XCH; ++ch) {
+                    nw[k][ch] = 0; sw[k][ch] = 0; qw[k][ch] = 0;
+                    if (bx[k][ch] >= 0) {
+                        const int64_t g = roff + bx[k][ch];
+                        nw[k][ch] = A.R.nmask[g >> 5];
+                        sw[k][ch] = A.R.seq2[g >> 4];
+                        qw[k][ch] = A.R.qual[g];
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const RowV mk = mate(k);
+#pragma unroll
+                for (int ch = 0; ch < PU_XCH; ++ch) {
+                    const int t = ch * 64 + lane;
+                    const int x = bx[k][ch];
+                    if (x == -2) continue;
+                    char c = '-', q = ' ';
+                    if (x >= 0) {
+                        const int64_t g = mk.roff + x;
+                        uint32_t code = ((nw[k][ch] >> (g & 31)) & 1) ? 4u : (sw[k][ch] >> (2 * (g & 15))) & 3u;
+                        if (mk.rev && code < 4) code = 3 - code;
+                        c = "ACGTN"[code];
+                        q = (char)qw[k][ch];
+                    }
+                    L.c(k)[t] = c;
+                    L.q(k)[t] = q;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (k >= nm) break;
+                const int span = len(k) - pad(k);
+                const RowV mk = mate(k);
+                for (int t = lane; t < span; t += 64) {
+                    // the M/D op covering reference offset t (I/S ops span nothing)
+                    int o = 0;
+                    while (L.opref(k)[o + 1] <= t) ++o;
+                    const int rd = L.opread(k)[o];
+                    char c = '-', q = ' ';
+                    if (rd >= 0) sam_base(A.R, mk, rd + (t - L.opref(k)[o]), c, q);
+                    L.c(k)[t] = c;
+                    L.q(k)[t] = q;
+                }
+            }
+        }
+        if (more) {   // the next unit's rows have landed: its CIGAR ops land during the merge
+            fetch_ops(n1, lane);
+            fetch_ops(n2, lane);
+            ops_ready = true;
         }
         // ---- merge_inserts (lane 0, only units with I ops): keys left + pad,
         // sam2aln.py:133-135, :240-273 ----
