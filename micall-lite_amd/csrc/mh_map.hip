@@ -838,31 +838,42 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         }
         wave_sync();
 
-        // ---- traceback (lane 0): CIGAR runs, back to front, and the lane of
-        // every M row (rowk) for the lane-parallel statistics below ----
+        // ---- traceback: CIGAR runs, back to front, and the lane of every M
+        // row (rowk) for the lane-parallel statistics below.  The walk is
+        // serial, so it runs wave-uniform: its state lives in SGPRs and its
+        // arithmetic and branches are scalar instructions, leaving the vector
+        // ALU to the other waves' DP rows; only lane 0 stores. ----
         int tb_ok = 0, t_start = 0, t_first = 0, t_nrun = 0;
+        best = __builtin_amdgcn_readfirstlane(best);
+        bi = __builtin_amdgcn_readfirstlane(bi);
+        bl = __builtin_amdgcn_readfirstlane(bl);
 #ifndef MH_ABLATE_NOTB
-        if (lane == 0 && !(LOCAL && best <= 0) && best >= minsc) {
+        if (!(LOCAL && best <= 0) && best >= __builtin_amdgcn_readfirstlane(minsc)) {
+            const int d0u = __builtin_amdgcn_readfirstlane(d0);
             int i = bi, k = bl, state = 0, ok = 1;
             int wr = -1, wk = -1;
             uint32_t word = 0;
             int rop = -1, rlen = 0, nrun = 0, first_j = 0;
             for (;;) {
                 const int g = i >> 3;
-                if (g != wr || k != wk) { word = bits[g * 64 + k]; wr = g; wk = k; }
+                if (g != wr || k != wk) {
+                    word = __builtin_amdgcn_readfirstlane(bits[g * 64 + k]);
+                    wr = g; wk = k;
+                }
                 if (state == 0 && (i & 7) == 7 && (word & 0x33333333u) == 0x11111111u) {
                     // eight diagonal moves on this lane: one M step of 8 rows
                     if (rop == MH_OP_M) rlen += 8;
                     else {
                         if (rlen) {
                             if (nrun >= RUNS_CAP - 1) { ok = 0; break; }
-                            runs[nrun++] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                            if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                            ++nrun;
                         }
                         rop = MH_OP_M;
                         rlen = 8;
                     }
-                    *(uint64_t *)(rowk + i - 7) = 0x0101010101010101ull * (uint64_t)k;
-                    first_j = i - 7 + d0 + k;
+                    if (lane == 0) *(uint64_t *)(rowk + i - 7) = 0x0101010101010101ull * (uint64_t)k;
+                    first_j = i - 7 + d0u + k;
                     i -= 8;
                     if (i < 0) break;
                     continue;
@@ -881,14 +892,15 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                 else {
                     if (rlen) {
                         if (nrun >= RUNS_CAP - 1) { ok = 0; break; }
-                        runs[nrun++] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                        if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                        ++nrun;
                     }
                     rop = op;
                     rlen = 1;
                 }
                 if (op == MH_OP_M) {
-                    rowk[i] = (uint8_t)k;
-                    first_j = i + d0 + k;
+                    if (lane == 0) rowk[i] = (uint8_t)k;
+                    first_j = i + d0u + k;
                     if (--i < 0) break;
                 } else if (op == MH_OP_I) {
                     state = (nib >> 2) & 1 ? 1 : 0;
@@ -900,7 +912,10 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                     if (k < 0) { ok = 0; break; }
                 }
             }
-            if (rlen) runs[nrun++] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+            if (rlen) {
+                if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                ++nrun;
+            }
             tb_ok = ok;
             t_start = i + 1;
             t_first = first_j;
@@ -908,11 +923,6 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         }
 #endif
         wave_sync();
-        tb_ok = __builtin_amdgcn_readfirstlane(tb_ok);
-        t_start = __builtin_amdgcn_readfirstlane(t_start);
-        t_first = __builtin_amdgcn_readfirstlane(t_first);
-        t_nrun = __builtin_amdgcn_readfirstlane(t_nrun);
-
         Slot out{};
         out.valid = 0;
         out.strand = strand;
