@@ -430,45 +430,91 @@ __device__ __forceinline__ int in_vgpr(int v)
     return r;
 }
 
-// One DP row inside the gap window (oracle dp_extend, og_mapper.c:283-322):
-// returns the 4 traceback bits of this lane's cell.
+// One DP row inside the gap window (oracle dp_extend, og_mapper.c:283-322).  The row's traceback nibble is shifted
+// into acc (acc = 16 acc + nibble, so row t of an 8-row group sits at nibble
+// 7 - t): bit 0/1 src (1 diagonal, 2 E, 3 F, 0 local stop), bit 2 E extends,
+// bit 3 F extends.  Every bit is a compare into a lane mask (the src logic is
+// scalar mask arithmetic) and enters acc by an add with carry-in, 2 acc + bit.
 template <int LOCAL>
-__device__ __forceinline__ uint32_t dp_row_gap(uint32_t tbv, int rc, int &Hp, int &Ep,
-                                               uint32_t &bestKey, int ci, const DpConst &K)
+__device__ __forceinline__ void dp_row_gap(uint32_t tbv, int rc, int &Hp, int &Ep,
+                                           uint32_t &bestKey, int ci, const DpConst &K,
+                                           uint32_t &acc)
 {
     const int Hd = Hp + (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4) - 8;
-    // vertical (insertion) move from lane k+1 of the previous row; eb4 = 4
+    // vertical (insertion) move from lane k+1 of the previous row; E extends
     // when extending beats opening (ties open)
     const int e1 = dppz<DPP_WAVE_SHL1>(Ep) + K.mexI;
     const int h1 = dppz<DPP_WAVE_SHL1>(Hp) + K.moeI;
     const int E = imax(e1, h1);
-    const uint32_t eb4 = (uint32_t)((h1 - e1) >> 31) & 4u;
     int H1 = imax(Hd, E);
     if (LOCAL) H1 = imax(H1, BIAS);
     // horizontal (deletion) moves: prefix max of X = H1 + exD * lane
     const int X = H1 + K.xD;
     const int P = scan_max(X);
-    const int gtm = (X - P) >> 31;              // -1 where the left lane's F extends
     const int F = dppz<DPP_WAVE_SHR1>(P) + K.cF;
-    const uint32_t fb8 = (uint32_t)(dppz<DPP_WAVE_SHR1>(gtm) & K.eight);
     const int H = imax(H1, F);
-    // src: 1 diagonal, 2 from E, 3 from F (priority in that order); 0 local stop
-    const uint32_t a = umin1(H - Hd), b = umin1(H - E);
-    uint32_t src = 1u + a + (a & b);
     if (LOCAL) {
-        src *= umin1(H - BIAS);
         const uint32_t key = (uint32_t)H * 1024u + (uint32_t)ci;
         bestKey = bestKey > key ? bestKey : key;
     }
+    // The nibble: src (1 diagonal, 2 E, 3 F by priority; 0 local stop) in
+    // bits 0-1, E extends (h1 < e1) in bit 2, F extends in bit 3 (the left
+    // lane's X is below its prefix max, compared on F's scale: X(k-1) + cF(k)
+    // < P(k-1) + cF(k)).  Every bit is a compare into a lane mask, the src
+    // logic is scalar mask arithmetic, and each bit enters acc by an add with
+    // carry-in (acc = 2 acc + bit).  Hazards: X is written before the scan,
+    // so its DPP read is far from the write; >= 2 instructions separate
+    // each mask write from its read as a carry.
+    uint64_t ma, mb, mz, me, mf;
+    int xl;
+    if (LOCAL) {
+        asm volatile(
+            "v_cmp_ne_u32_e64 %[ma], %[H], %[Hd]\n\t"
+            "v_cmp_ne_u32_e64 %[mb], %[H], %[E]\n\t"
+            "v_cmp_ne_u32_e64 %[mz], %[bias], %[H]\n\t"
+            "v_cmp_lt_i32_e64 %[me], %[h1], %[e1]\n\t"
+            "v_add_u32_dpp %[xl], %[X], %[cF] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "s_orn2_b64 %[mb], %[mb], %[ma]\n\t"
+            "v_cmp_lt_i32_e64 %[mf], %[xl], %[F]\n\t"
+            "s_and_b64 %[ma], %[ma], %[mz]\n\t"
+            "s_and_b64 %[mb], %[mb], %[mz]\n\t"
+            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[mf]\n\t"
+            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[me]\n\t"
+            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[ma]\n\t"
+            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[mb]"
+            : [acc] "+v"(acc), [ma] "=&s"(ma), [mb] "=&s"(mb), [mz] "=&s"(mz), [me] "=&s"(me),
+              [mf] "=&s"(mf), [xl] "=&v"(xl)
+            : [H] "v"(H), [Hd] "v"(Hd), [E] "v"(E), [h1] "v"(h1), [e1] "v"(e1), [X] "v"(X),
+              [cF] "v"(K.cF), [F] "v"(F), [bias] "s"(BIAS)
+            : "vcc");
+    } else {
+        asm volatile(
+            "v_cmp_ne_u32_e64 %[ma], %[H], %[Hd]\n\t"
+            "v_cmp_ne_u32_e64 %[mb], %[H], %[E]\n\t"
+            "v_cmp_lt_i32_e64 %[me], %[h1], %[e1]\n\t"
+            "v_add_u32_dpp %[xl], %[X], %[cF] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "s_orn2_b64 %[mb], %[mb], %[ma]\n\t"
+            "v_cmp_lt_i32_e64 %[mf], %[xl], %[F]\n\t"
+            "s_nop 1\n\t"
+            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[mf]\n\t"
+            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[me]\n\t"
+            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[ma]\n\t"
+            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[mb]"
+            : [acc] "+v"(acc), [ma] "=&s"(ma), [mb] "=&s"(mb), [me] "=&s"(me), [mf] "=&s"(mf),
+              [xl] "=&v"(xl)
+            : [H] "v"(H), [Hd] "v"(Hd), [E] "v"(E), [h1] "v"(h1), [e1] "v"(e1), [X] "v"(X),
+              [cF] "v"(K.cF), [F] "v"(F)
+            : "vcc");
+        (void)mz;
+    }
     Hp = H;
     Ep = E;
-    return src | eb4 | fb8;
 }
 
 // A row outside the gap window (first / last GBAR rows): no E, no F.
 template <int LOCAL>
-__device__ __forceinline__ uint32_t dp_row_nogap(uint32_t tbv, int rc, int &Hp, int &Ep,
-                                                 uint32_t &bestKey, int ci)
+__device__ __forceinline__ void dp_row_nogap(uint32_t tbv, int rc, int &Hp, int &Ep,
+                                             uint32_t &bestKey, int ci, uint32_t &acc)
 {
     int H = Hp + (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4) - 8;
     uint32_t src = 1u;
@@ -478,9 +524,9 @@ __device__ __forceinline__ uint32_t dp_row_nogap(uint32_t tbv, int rc, int &Hp, 
         const uint32_t key = (uint32_t)H * 1024u + (uint32_t)ci;
         bestKey = bestKey > key ? bestKey : key;
     }
+    acc = (acc << 4) + src;
     Hp = H;
     Ep = 0;
-    return src;
 }
 
 __device__ __forceinline__ int wave_excl_scan_min(int v, int lane, int init)
@@ -637,7 +683,7 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
         uint32_t w = 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-            if (r0 + u < m && (!LOCAL || H[u] > 0)) w |= 1u << (4 * u);
+            if (r0 + u < m && (!LOCAL || H[u] > 0)) w |= 1u << (4 * (7 - u));   // row u of the group at nibble 7 - u
         bits[lane * 64 + kb] = w;
     }
     best = S;
@@ -798,19 +844,16 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                 if (i0 >= GBAR && i0 + 8 <= m - GBAR) {
 #pragma unroll
                     for (int t = 0; t < 8; ++t)
-                        acc |= dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K)
-                               << (4 * t);
+                        dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K, acc);
                 } else {
 #pragma unroll
                     for (int t = 0; t < 8; ++t) {
                         const int i = i0 + t;
-                        if (i < m) {
-                            const uint32_t nib =
-                                (i >= GBAR && i < m - GBAR)
-                                    ? dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K)
-                                    : dp_row_nogap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i);
-                            acc |= nib << (4 * t);
-                        }
+                        if (i >= m) acc <<= 4;   // past the read: an empty nibble
+                        else if (i >= GBAR && i < m - GBAR)
+                            dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K, acc);
+                        else
+                            dp_row_nogap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, acc);
                     }
                 }
                 bits[(i0 >> 3) * 64 + lane] = acc;
@@ -878,7 +921,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                     if (i < 0) break;
                     continue;
                 }
-                const uint32_t nib = (word >> (4 * (i & 7))) & 15u;
+                const uint32_t nib = (word >> (4 * (7 - (i & 7)))) & 15u;
                 int op;
                 if (state == 0) {
                     const int src = nib & 3;
