@@ -581,14 +581,25 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
     const uint8_t *rp = refw + (lane & ~3);
     const uint32_t sh = (uint32_t)(lane & 3);
     int nm = 0;
-    for (int i = 0; i < m; i += 4) {
-        const uint32_t rd = *(const uint32_t *)(rdc + i);
-        const uint32_t lo = *(const uint32_t *)(rp + i), hi = *(const uint32_t *)(rp + i + 4);
-        const uint32_t rv = __builtin_amdgcn_alignbyte(hi, lo, sh) >> 2;
-        uint32_t x = (rd ^ rv) | ((rd | rv) & 0x04040404u);
-        x = (x | (x >> 1) | (x >> 2)) & 0x01010101u;
-        nm += __builtin_popcount(x);
-        if ((i & 63) == 60) {
+    // 16 rows per step, every LDS read of the step issued before any is used
+    // (reads past rows_pad stay inside this wave's LDS area and are unused)
+    for (int i = 0; i < m; i += 16) {
+        uint32_t rd[4], lo[4], hi[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            rd[u] = *(const uint32_t *)(rdc + i + 4 * u);
+            lo[u] = *(const uint32_t *)(rp + i + 4 * u);
+            hi[u] = *(const uint32_t *)(rp + i + 4 * u + 4);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (i + 4 * u >= m) break;
+            const uint32_t rv = __builtin_amdgcn_alignbyte(hi[u], lo[u], sh) >> 2;
+            uint32_t x = (rd[u] ^ rv) | ((rd[u] | rv) & 0x04040404u);
+            x = (x | (x >> 1) | (x >> 2)) & 0x01010101u;
+            nm += __builtin_popcount(x);
+        }
+        if ((i & 63) == 48) {
             // the best ungapped score of a lane is at most ma*(m - nm) (local)
             // or -nm (end-to-end); give up when no lane can beat Gb(m-1)
             const int ub = LOCAL ? ma * (m - nm) : -nm;
