@@ -315,7 +315,10 @@ __device__ int seed_read(const SeedArgs &A, int64_t r, int lane, uint64_t *hits,
 // atomic (a returning same-address atomic costs ~11 ns device-wide).
 constexpr int SEED_CHUNK = 32;
 
-__global__ __launch_bounds__(256) void k_seed(SeedArgs A)
+#ifndef MH_SEED_WPS
+#define MH_SEED_WPS 8        // min waves per SIMD: <= 64 VGPRs, 8 waves/SIMD (latency-bound probes)
+#endif
+__global__ __launch_bounds__(256, MH_SEED_WPS) void k_seed(SeedArgs A)
 {
     __shared__ uint64_t sh_hits[4][MAXHITS_MATE];
     __shared__ Cand sh_best[4][MAXCAND];
