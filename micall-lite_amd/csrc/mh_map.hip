@@ -602,7 +602,7 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
             x = (x | (x >> 1) | (x >> 2)) & 0x01010101u;
             nm += __builtin_popcount(x);
         }
-        if ((i & 63) == 48) {
+        if ((i & 63) == 48 && i + 16 <= m) {   // rows past the read would count as non-matches
             // the best ungapped score of a lane is at most ma*(m - nm) (local)
             // or -nm (end-to-end); give up when no lane can beat Gb(m-1)
             const int ub = LOCAL ? ma * (m - nm) : -nm;
