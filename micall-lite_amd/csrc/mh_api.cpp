@@ -1176,17 +1176,51 @@ static int aggregate_tokens(CtxEx &c)
         std::string pool((size_t)ctr[1], '\0');
         MH_HIP(hipMemcpy(ev.data(), P.ev, sizeof(int32_t) * 4 * ne, hipMemcpyDeviceToHost));
         if (ctr[1] > 0) MH_HIP(hipMemcpy(&pool[0], P.ev_pool, ctr[1], hipMemcpyDeviceToHost));
-        std::map<std::tuple<int32_t, int32_t, std::string>, int64_t> agg;
-        for (int64_t e = 0; e < ne; ++e)
-            ++agg[std::make_tuple(ev[4 * e], ev[4 * e + 1],
-                                  pool.substr((size_t)ev[4 * e + 2], (size_t)ev[4 * e + 3]))];
-        for (const auto &kv : agg) {
-            c.tok_ref.push_back(std::get<0>(kv.first));
-            c.tok_pos.push_back(std::get<1>(kv.first));
+        // distinct (ref, pos, token) in an open-addressing table over the
+        // event array (no per-event allocation), then the few distinct keys
+        // sorted in (ref, pos, token) order
+        struct Key { int32_t ref, pos, off, len; int64_t count; };
+        std::vector<Key> uniq;
+        uint64_t cap = 64;
+        while (cap < 2 * (uint64_t)ne) cap <<= 1;
+        std::vector<int32_t> slot(cap, -1);
+        const char *pb = pool.data();
+        for (int64_t e = 0; e < ne; ++e) {
+            const int32_t r = ev[4 * e], ps = ev[4 * e + 1], of = ev[4 * e + 2], ln = ev[4 * e + 3];
+            uint64_t h = 1469598103934665603ull;
+            for (int32_t x = 0; x < ln; ++x) h = (h ^ (unsigned char)pb[of + x]) * 1099511628211ull;
+            h ^= ((uint64_t)(uint32_t)r << 32) | (uint32_t)ps;
+            h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33;
+            uint64_t i = h & (cap - 1);
+            for (;;) {
+                const int32_t u = slot[i];
+                if (u < 0) {
+                    slot[i] = (int32_t)uniq.size();
+                    uniq.push_back(Key{r, ps, of, ln, 1});
+                    break;
+                }
+                Key &k = uniq[u];
+                if (k.ref == r && k.pos == ps && k.len == ln && std::memcmp(pb + k.off, pb + of, ln) == 0) {
+                    ++k.count;
+                    break;
+                }
+                i = (i + 1) & (cap - 1);
+            }
+        }
+        std::sort(uniq.begin(), uniq.end(), [pb](const Key &a, const Key &b) {
+            if (a.ref != b.ref) return a.ref < b.ref;
+            if (a.pos != b.pos) return a.pos < b.pos;
+            const int cmp = std::memcmp(pb + a.off, pb + b.off, (size_t)std::min(a.len, b.len));
+            if (cmp != 0) return cmp < 0;
+            return a.len < b.len;
+        });
+        for (const Key &k : uniq) {
+            c.tok_ref.push_back(k.ref);
+            c.tok_pos.push_back(k.pos);
             c.tok_off.push_back((int32_t)c.tok_pool.size());
-            c.tok_len.push_back((int32_t)std::get<2>(kv.first).size());
-            c.tok_count.push_back(kv.second);
-            c.tok_pool += std::get<2>(kv.first);
+            c.tok_len.push_back(k.len);
+            c.tok_count.push_back(k.count);
+            c.tok_pool.append(pb + k.off, (size_t)k.len);
         }
     }
     c.tok_gen = P.gen;
