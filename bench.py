@@ -410,6 +410,12 @@ def main():
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--pairs', type=int, default=1000000, help='read pairs per GPU')
+    ap.add_argument('--iterations', type=int, default=1,
+                    help='cap on remap iterations per step (1: C2; 3 with --pairs 10000000: C3 on '
+                         'one GPU); the reference\'s stopping rules still apply')
+    ap.add_argument('--force-iterations', action='store_true',
+                    help='run exactly --iterations remap passes per step (C3: "3 remap '
+                         'iterations"), the stopping rules applying only after them')
     ap.add_argument('--cpu-sample', type=int, default=100000)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--breakdown', action='store_true',
@@ -450,7 +456,9 @@ def main():
     raw_count = 2.0 * args.pairs * world     # lines(R1) / 2, remap.py:457
 
     def step():
-        return pipe.run(raw_count, max_iterations=1)
+        del pipe.log[:]
+        return pipe.run(raw_count, max_iterations=args.iterations,
+                        min_iterations=args.iterations if args.force_iterations else None)
 
     stages = {}
     if args.breakdown:
@@ -510,10 +518,12 @@ def main():
             'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(1e3 * elapsed / args.steps, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'int32', 'data': 'synthetic',
-            'config': {'workload': 'C2: synthetic 2x251 nt HIV-1 pol read pairs (10% divergent '
+            'config': {'workload': ('C2' if args.iterations == 1 else 'C3-style') +
+                                   ': synthetic 2x251 nt HIV-1 pol read pairs (10% divergent '
                                    'sample genome, 0.5% errors), prelim_map end-to-end vs 74 seeds '
-                                   '+ 1 remap iteration (--local vs consensus) + 2 pileups, '
-                                   'default projects.json',
+                                   '+ {} remap iteration(s) (--local vs consensus) + pileups, '
+                                   'default projects.json'.format(args.iterations),
+                       'remap_iterations_cap': args.iterations,
                        'pairs_per_gpu': args.pairs, 'read_len': READ_LEN,
                        'parallelism': 'dp{} (read-pair shards, RCCL all-reduce of pileup '
                                       'counters)'.format(world)},
@@ -529,7 +539,8 @@ def main():
                    'cells_per_step': cells // max(args.steps, 1),
                    'gcups': round(cells / (dp_ms / 1e3) / 1e9, 1) if dp_ms > 0 else None},
             'cpu_baseline': cpu,
-            'result': {'conseqs': {k: len(v) for k, v in conseqs.items()},
+            'result': {'remap_iterations_run': len(pipe.log),
+                       'conseqs': {k: len(v) for k, v in conseqs.items()},
                        'mapped_lines': dict(new_counts)},
         }
         print(json.dumps(out))

@@ -242,9 +242,11 @@ class RemapPipeline:
         return filter_conseqs(self.ctx, pile, order, new, self.seeds, self.count_threshold / 2,
                               distance_report)
 
-    def run(self, raw_count, max_iterations=None, remap_counts_writer=None):
+    def run(self, raw_count, max_iterations=None, remap_counts_writer=None, min_iterations=None):
         """The whole of remap()'s loop.  max_iterations caps the number of
-        mapping passes (benchmark configs); None = the reference's rules."""
+        mapping passes (benchmark configs); None = the reference's rules.
+        min_iterations (benchmark configs only, e.g. BASELINE C3's "3 remap
+        iterations") runs that many passes before the stopping rules apply."""
         self.raw_count = raw_count
         self.prelim()
         groups = self.prelim_groups()
@@ -274,6 +276,9 @@ class RemapPipeline:
                                    distance_report)
             if max_iterations is not None and n_remaps >= max_iterations:
                 break
+            if min_iterations is not None and n_remaps < min_iterations:
+                map_counts = dict(new_counts)
+                continue
             if new_seed_names == old_seed_names:
                 if all((count <= map_counts[refname]) for refname, count in new_counts.items()):
                     break
