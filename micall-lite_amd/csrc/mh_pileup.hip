@@ -201,13 +201,41 @@ __device__ int merge_ins_strings(const DevReads &R, const RowV &w, int o1, int l
     return l2;
 }
 
-__device__ __forceinline__ int wave_incl_scan(int v, int lane)
+// Wave-wide scans and reductions on DPP (row shifts, then the two row
+// broadcasts): register-to-register, where __shfl goes through the LDS
+// crossbar (ds_bpermute) and pays its latency on every step.  A lane with
+// no source, or in a row the step does not write, takes the identity.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_id(int identity, int v)
 {
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(v, o, 64);
-        if (lane >= o) v += y;
-    }
+    return __builtin_amdgcn_update_dpp(identity, v, CTRL, ROWMASK, 0xF, false);
+}
+
+template <class Op>
+__device__ __forceinline__ int wave_scan_dpp(int v, int identity, Op op)
+{
+    v = op(v, dpp_id<0x111, 0xF>(identity, v));   // row_shr:1
+    v = op(v, dpp_id<0x112, 0xF>(identity, v));   // row_shr:2
+    v = op(v, dpp_id<0x114, 0xF>(identity, v));   // row_shr:4
+    v = op(v, dpp_id<0x118, 0xF>(identity, v));   // row_shr:8
+    v = op(v, dpp_id<0x142, 0xA>(identity, v));   // row_bcast:15 into rows 1, 3
+    v = op(v, dpp_id<0x143, 0xC>(identity, v));   // row_bcast:31 into rows 2, 3
     return v;
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v, int /*lane*/)
+{
+    return wave_scan_dpp(v, 0, [](int x, int y) { return x + y; });
+}
+
+__device__ __forceinline__ int wave_min_all(int v)
+{
+    return __builtin_amdgcn_readlane(wave_scan_dpp(v, INT32_MAX, [](int x, int y) { return x < y ? x : y; }), 63);
+}
+
+__device__ __forceinline__ int wave_max_all(int v)
+{
+    return __builtin_amdgcn_readlane(wave_scan_dpp(v, INT32_MIN, [](int x, int y) { return x > y ? x : y; }), 63);
 }
 
 template <int SRC>
@@ -302,8 +330,8 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
                 }
                 bad |= __any(badop);
                 n_iops += __popcll(__ballot(isi));
-                rf0 += __shfl(iref, 63, 64);
-                rd0 += __shfl(iread, 63, 64);
+                rf0 += __builtin_amdgcn_readlane(iref, 63);
+                rd0 += __builtin_amdgcn_readlane(iread, 63);
             }
             if (lane == 0) { L.opref(k)[nc] = rf0; L.opread(k)[nc] = rd0; }
             if (rd0 != mk.m || rf0 > A.span_cap || mk.pos < 1) bad = 1;
@@ -493,10 +521,8 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
                     if (!(c1 == '-' && c2 == '-')) fs = i;
                 }
             }
-            for (int o = 32; o > 0; o >>= 1) {
-                rs = min(rs, __shfl_xor(rs, o, 64));
-                fs = min(fs, __shfl_xor(fs, o, 64));
-            }
+            rs = wave_min_all(rs);
+            fs = wave_min_all(fs);
             rev_start = min(rev_start, rs);
             fwd_start = min(fwd_start, fs);
             if (rev_start < (1 << 30) && (a < 0 || fwd_start < (1 << 30) || i0 + 64 >= len1)) break;
@@ -572,10 +598,8 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
                 else atomicAdd(&A.dense[cell * 4 + code], 1);
             }
         }
-        for (int o = 32; o > 0; o >>= 1) {
-            mxp = max(mxp, __shfl_xor(mxp, o, 64));
-            err |= __shfl_xor(err, o, 64);
-        }
+        mxp = wave_max_all(mxp);
+        err = wave_max_all(err);
         if (lane == 0) {
             if (is_hot) {
                 atomicAdd(&hot->read_count, 1u);
