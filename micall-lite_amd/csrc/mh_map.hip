@@ -38,29 +38,55 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Wave-wide scans and reductions on DPP (row shifts, then the two row
+// broadcasts), register to register: __shfl goes through the LDS crossbar
+// (ds_bpermute) and pays its latency on every step.  A lane with no source,
+// or in a row a step does not write, takes the identity.  Full wave only.
+template <class Op>
+__device__ __forceinline__ int wave_scan_dpp(int v, int identity, Op op)
+{
+    v = op(v, dpp<0x111>(identity, v));           // row_shr:1
+    v = op(v, dpp<0x112>(identity, v));           // row_shr:2
+    v = op(v, dpp<0x114>(identity, v));           // row_shr:4
+    v = op(v, dpp<0x118>(identity, v));           // row_shr:8
+    v = op(v, dpp<0x142, 0xA>(identity, v));      // row_bcast:15 into rows 1, 3
+    v = op(v, dpp<0x143, 0xC>(identity, v));      // row_bcast:31 into rows 2, 3
+    return v;
+}
+
+__device__ __forceinline__ int op_add(int x, int y) { return x + y; }
+__device__ __forceinline__ int op_min(int x, int y) { return x < y ? x : y; }
+__device__ __forceinline__ int op_max(int x, int y) { return x > y ? x : y; }
+
 __device__ __forceinline__ int wave_sum(int v)
 {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return __builtin_amdgcn_readlane(wave_scan_dpp(v, 0, op_add), 63);
 }
 
-__device__ __forceinline__ int wave_excl_scan(int v, int lane)
+__device__ __forceinline__ int wave_excl_scan(int v, int /*lane*/)
 {
-    int x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    return x - v;
+    return wave_scan_dpp(v, 0, op_add) - v;
 }
 
+__device__ __forceinline__ int wave_min(int v)
+{
+    return __builtin_amdgcn_readlane(wave_scan_dpp(v, INT32_MAX, op_min), 63);
+}
+
+__device__ __forceinline__ int wave_max(int v)
+{
+    return __builtin_amdgcn_readlane(wave_scan_dpp(v, INT32_MIN, op_max), 63);
+}
+
+// signed 64-bit max: the high words first, then the low words (as unsigned,
+// sign bit flipped) among the lanes holding the high maximum
 __device__ __forceinline__ long long wave_max64(long long v)
 {
-    for (int o = 32; o > 0; o >>= 1) {
-        long long y = __shfl_xor(v, o, 64);
-        v = y > v ? y : v;
-    }
-    return v;
+    const int hi = (int)(v >> 32);
+    const int mhi = wave_max(hi);
+    const int lo = (int)((uint32_t)v ^ 0x80000000u);
+    const int mlo = wave_max(hi == mhi ? lo : INT32_MIN);
+    return (long long)(((uint64_t)(uint32_t)mhi << 32) | (uint32_t)(mlo ^ (int)0x80000000u));
 }
 
 __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
@@ -532,21 +558,10 @@ __device__ __forceinline__ void dp_row_nogap(uint32_t tbv, int rc, int &Hp, int 
     Ep = 0;
 }
 
-__device__ __forceinline__ int wave_excl_scan_min(int v, int lane, int init)
+// exclusive prefix min, init at lane 0
+__device__ __forceinline__ int wave_excl_scan_min(int v, int /*lane*/, int init)
 {
-    int x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x = x < y ? x : y;
-    }
-    const int e = __shfl_up(x, 1, 64);
-    return lane == 0 ? init : e;
-}
-
-__device__ __forceinline__ int wave_max(int v)
-{
-    for (int o = 32; o > 0; o >>= 1) v = imax(v, __shfl_xor(v, o, 64));
-    return v;
+    return dpp<DPP_WAVE_SHR1>(init, wave_scan_dpp(v, INT32_MAX, op_min));
 }
 
 // ---------------------------------------------------------------------------
@@ -613,14 +628,10 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
     const int ub = LOCAL ? ma * (m - nm) : -nm;
     // candidate lane: fewest non-matches, then smallest lane (any choice is
     // exact: (B) below checks every other lane)
-    int key = nm * 64 + lane;
-    for (int o = 32; o > 0; o >>= 1) {
-        const int y = __shfl_xor(key, o, 64);
-        key = y < key ? y : key;
-    }
+    const int key = wave_min(nm * 64 + lane);
     const int kb = key & 63;
     const int ub_other = wave_max(lane == kb ? INT32_MIN + 1 : ub);
-    const int ub_kb = __shfl(ub, kb, 64);
+    const int ub_kb = __builtin_amdgcn_readlane(ub, kb);
     if (ub_kb <= gb_max || ub_other >= ub_kb) return false;   // (A) / (B) cannot hold
 
     // ---- exact ungapped recurrence on lane kb: rows 8*lane .. 8*lane+7 ----
@@ -669,7 +680,7 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
         int v = 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u) if (r0 + u == last) v = H[u];
-        S = __shfl(v, last >> 3, 64);
+        S = __builtin_amdgcn_readlane(v, __builtin_amdgcn_readfirstlane(last >> 3));
         istar = last;
     }
     // (A) and (B)
