@@ -468,12 +468,19 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         print('warning: --gpus {} but WORLD_SIZE {}'.format(args.gpus, world), file=sys.stderr)
-    device = torch.device('cuda', local)
+    # MICALL_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on
+    # one GPU (tests only; the measured multi-GPU runs use RCCL)
+    backend = os.environ.get('MICALL_BENCH_BACKEND', 'nccl')
+    ndev = torch.cuda.device_count()
+    device = torch.device('cuda', local if backend == 'nccl' else local % max(ndev, 1))
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group('nccl', device_id=device)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=device)
+        else:
+            dist.init_process_group(backend)
 
-    ctx = _native.Context(local)
+    ctx = _native.Context(device.index)
     reads, quals = make_reads(args.pairs, block=rank)
     ctx.reads_load_fixed(reads, quals, True)
     del reads, quals
