@@ -40,13 +40,15 @@ def algo_bytes_per_pair(L=READ_LEN):
     return 2 * -(-L // 4) + 2 * -(-L // 8) + 2 * L + 64
 
 
-def make_reads(pairs, block):
+def make_reads(pairs, block, read_len=READ_LEN, paired=True):
     from micall_amd import projects, synth
     pol = projects.load_default().seed_sequences()['HIV1B-pol-seed']
     d = synth.make_pairs(pairs, genomes={'HIV1B-pol-seed': pol}, genome_seed=SEED,
-                         read_seed=SEED, block=block, read_len=READ_LEN)
-    reads = np.stack([d['r1'], d['r2']], axis=1).reshape(2 * pairs, READ_LEN)
-    quals = np.stack([d['q1'], d['q2']], axis=1).reshape(2 * pairs, READ_LEN)
+                         read_seed=SEED, block=block, read_len=read_len, paired=paired)
+    if not paired:
+        return d['r1'], d['q1']
+    reads = np.stack([d['r1'], d['r2']], axis=1).reshape(2 * pairs, read_len)
+    quals = np.stack([d['q1'], d['q2']], axis=1).reshape(2 * pairs, read_len)
     return reads, quals
 
 
@@ -439,6 +441,9 @@ def main():
     ap.add_argument('--iterations', type=int, default=1,
                     help='cap on remap iterations per step (1: C2; 3 with --pairs 10000000: C3 on '
                          'one GPU); the reference\'s stopping rules still apply')
+    ap.add_argument('--unpaired', action='store_true',
+                    help='unpaired reads (--pairs reads per GPU; C5-style with --read-len 300)')
+    ap.add_argument('--read-len', type=int, default=READ_LEN)
     ap.add_argument('--force-iterations', action='store_true',
                     help='run exactly --iterations remap passes per step (C3: "3 remap '
                          'iterations"), the stopping rules applying only after them')
@@ -481,8 +486,10 @@ def main():
             dist.init_process_group(backend)
 
     ctx = _native.Context(device.index)
-    reads, quals = make_reads(args.pairs, block=rank)
-    ctx.reads_load_fixed(reads, quals, True)
+    paired = not args.unpaired
+    L = args.read_len
+    reads, quals = make_reads(args.pairs, block=rank, read_len=L, paired=paired)
+    ctx.reads_load_fixed(reads, quals, paired)
     del reads, quals
     shard = Shard(rank, world, read_base=rank * 2 * args.pairs, device=device) if world > 1 else None
     pipe = RemapPipeline(ctx, shard=shard)
@@ -529,44 +536,50 @@ def main():
     dom = max(kernels, key=lambda k: kernels[k][0])
     dom_ms, dom_n = kernels[dom]
     # every launch of a mapping / pileup kernel processes this rank's pairs once
-    bytes_per_launch = algo_bytes_per_pair() * args.pairs
+    # per unit (pair, or read when unpaired): SURVEY.md 8(d), 756 B per 2x251
+    # pair, 445 B per unpaired 300-nt read
+    unit_bytes = algo_bytes_per_pair(L) if paired else -(-L // 4) + -(-L // 8) + L + 32
+    bytes_per_launch = unit_bytes * args.pairs
     avg_s = dom_ms / 1e3 / max(dom_n, 1)
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
     total_pairs = args.pairs * world * args.steps
-    value = 2 * total_pairs / elapsed
+    value = (2 if paired else 1) * total_pairs / elapsed
     # DP cell updates (GCUPS next to the roofline): every
     # extension the full DP runs is read_len rows x the 64-diagonal band; the
     # ungapped fast path resolves the rest without the DP
     ext = sum(int(m[1]) for m in dp_log)
     fast = sum(int(m[3]) for m in dp_log)
-    cells = (ext - fast) * READ_LEN * 64
+    cells = (ext - fast) * L * 64
     dp_ms = kernels['k_dp'][0]
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and paired and L == READ_LEN:
             cpu = cpu_baseline(args.cpu_sample)
         out = {
             'metric': METRIC, 'value': round(value, 1), 'unit': 'reads/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(1e3 * elapsed / args.steps, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'int32', 'data': 'synthetic',
-            'config': {'workload': ('C2' if args.iterations == 1 else 'C3-style') +
-                                   ': synthetic 2x251 nt HIV-1 pol read pairs (10% divergent '
+            'config': {'workload': ('C5-style (mapping half): synthetic unpaired 1x{} nt HIV-1 pol reads'.format(L)
+                                    if not paired else
+                                    ('C2' if args.iterations == 1 else 'C3-style') +
+                                    ': synthetic 2x{} nt HIV-1 pol read pairs'.format(L)) +
+                                   ' (10% divergent '
                                    'sample genome, 0.5% errors), prelim_map end-to-end vs 74 seeds '
                                    '+ {} remap iteration(s) (--local vs consensus) + pileups, '
                                    'default projects.json'.format(args.iterations),
                        'remap_iterations_cap': args.iterations,
-                       'pairs_per_gpu': args.pairs, 'read_len': READ_LEN,
+                       'pairs_per_gpu' if paired else 'reads_per_gpu': args.pairs, 'read_len': L,
                        'parallelism': 'dp{} (read-pair shards, RCCL all-reduce of pileup '
                                       'counters)'.format(world)},
             'roofline': {'kernel': dom, 'bound': 'hbm', 'achieved': round(achieved, 3),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 6),
-                         'traffic': read_pmc_traffic(dom, args.pairs),
+                         'traffic': read_pmc_traffic(dom, args.pairs) if paired and L == READ_LEN else None,
                          'algo_bytes_per_launch': bytes_per_launch,
                          'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': dom_n},
-            'valu_issue': read_valu_issue(dom, args.pairs, 1e3 * avg_s),
+            'valu_issue': read_valu_issue(dom, args.pairs, 1e3 * avg_s) if paired and L == READ_LEN else None,
             'kernels_ms_per_step': {k: round(v[0] / args.steps, 3) for k, v in kernels.items()},
             'dp': {'extensions_per_step': ext // max(args.steps, 1),
                    'fast_path_per_step': fast // max(args.steps, 1),
