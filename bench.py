@@ -40,10 +40,20 @@ def algo_bytes_per_pair(L=READ_LEN):
     return 2 * -(-L // 4) + 2 * -(-L // 8) + 2 * L + 64
 
 
-def make_reads(pairs, block, read_len=READ_LEN, paired=True):
-    from micall_amd import projects, synth
-    pol = projects.load_default().seed_sequences()['HIV1B-pol-seed']
-    d = synth.make_pairs(pairs, genomes={'HIV1B-pol-seed': pol}, genome_seed=SEED,
+def bench_genomes(which='pol', read_len=READ_LEN):
+    """Seeds the synthetic sample genomes derive from: 'pol' (C2/C3/C5) or
+    'hiv' (C4: the HIV-1 seeds that hold a fragment of >= 260 nt; vpu, 246 nt,
+    is shorter than a read)."""
+    from micall_amd import projects
+    seeds = projects.load_default().seed_sequences()
+    if which == 'pol':
+        return {'HIV1B-pol-seed': seeds['HIV1B-pol-seed']}
+    return {k: v for k, v in seeds.items() if k.startswith('HIV') and len(v) >= max(260, read_len + 9)}
+
+
+def make_reads(pairs, block, read_len=READ_LEN, paired=True, genomes='pol'):
+    from micall_amd import synth
+    d = synth.make_pairs(pairs, genomes=bench_genomes(genomes, read_len), genome_seed=SEED,
                          read_seed=SEED, block=block, read_len=read_len, paired=paired)
     if not paired:
         return d['r1'], d['q1']
@@ -444,6 +454,9 @@ def main():
     ap.add_argument('--unpaired', action='store_true',
                     help='unpaired reads (--pairs reads per GPU; C5-style with --read-len 300)')
     ap.add_argument('--read-len', type=int, default=READ_LEN)
+    ap.add_argument('--genomes', choices=('pol', 'hiv'), default='pol',
+                    help='pol: HIV-1 pol sample genome (C2/C3/C5); hiv: mixed-region reads over '
+                         'the HIV-1 seeds in proportion to length (C4)')
     ap.add_argument('--force-iterations', action='store_true',
                     help='run exactly --iterations remap passes per step (C3: "3 remap '
                          'iterations"), the stopping rules applying only after them')
@@ -488,7 +501,7 @@ def main():
     ctx = _native.Context(device.index)
     paired = not args.unpaired
     L = args.read_len
-    reads, quals = make_reads(args.pairs, block=rank, read_len=L, paired=paired)
+    reads, quals = make_reads(args.pairs, block=rank, read_len=L, paired=paired, genomes=args.genomes)
     ctx.reads_load_fixed(reads, quals, paired)
     del reads, quals
     shard = Shard(rank, world, read_base=rank * 2 * args.pairs, device=device) if world > 1 else None
@@ -554,7 +567,7 @@ def main():
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and paired and L == READ_LEN:
+        if world == 1 and not args.no_cpu_baseline and paired and L == READ_LEN and args.genomes == 'pol':
             cpu = cpu_baseline(args.cpu_sample)
         out = {
             'metric': METRIC, 'value': round(value, 1), 'unit': 'reads/s', 'n_gpus': world,
@@ -563,6 +576,9 @@ def main():
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'int32', 'data': 'synthetic',
             'config': {'workload': ('C5-style (mapping half): synthetic unpaired 1x{} nt HIV-1 pol reads'.format(L)
                                     if not paired else
+                                    'C4-style: synthetic 2x{} nt mixed-region read pairs over the HIV-1 '
+                                    'seeds {}'.format(L, ','.join(bench_genomes('hiv', L)))
+                                    if args.genomes == 'hiv' else
                                     ('C2' if args.iterations == 1 else 'C3-style') +
                                     ': synthetic 2x{} nt HIV-1 pol read pairs'.format(L)) +
                                    ' (10% divergent '
@@ -576,10 +592,12 @@ def main():
             'roofline': {'kernel': dom, 'bound': 'hbm', 'achieved': round(achieved, 3),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 6),
-                         'traffic': read_pmc_traffic(dom, args.pairs) if paired and L == READ_LEN else None,
+                         'traffic': (read_pmc_traffic(dom, args.pairs)
+                                     if paired and L == READ_LEN and args.genomes == 'pol' else None),
                          'algo_bytes_per_launch': bytes_per_launch,
                          'avg_launch_ms': round(1e3 * avg_s, 4), 'launches': dom_n},
-            'valu_issue': read_valu_issue(dom, args.pairs, 1e3 * avg_s) if paired and L == READ_LEN else None,
+            'valu_issue': (read_valu_issue(dom, args.pairs, 1e3 * avg_s)
+                           if paired and L == READ_LEN and args.genomes == 'pol' else None),
             'kernels_ms_per_step': {k: round(v[0] / args.steps, 3) for k, v in kernels.items()},
             'dp': {'extensions_per_step': ext // max(args.steps, 1),
                    'fast_path_per_step': fast // max(args.steps, 1),

@@ -1332,22 +1332,52 @@ int mh_gotoh_align(mh_ctx *ctx, const char *seq1, const char *seq2, int gop, int
     return run_gotoh(*c, seq1, seq2, gop, gep, is_global, alphabet, matrix, out1, out2, cap, score);
 }
 
+// Unit-cost edit distance (python-Levenshtein's distance, remap.py:259) by
+// the bit-vector recurrence of Myers / Hyyro: a's characters in 64-row
+// blocks, one pass over b, ~15 word operations per block and column instead
+// of one DP cell per (i, j).  a is padded to whole blocks with rows that match
+// every character; their vertical deltas in the last column are taken back
+// off the bottom-row score at the end, so the result is D[|a|][|b|] exactly.
 int mh_levenshtein(const char *a, const char *b)
 {
     if (!a || !b) return -3;
     const size_t m = std::strlen(a), n = std::strlen(b);
-    std::vector<int> row(n + 1);
-    for (size_t j = 0; j <= n; ++j) row[j] = (int)j;
-    for (size_t i = 1; i <= m; ++i) {
-        int diag = row[0];
-        row[0] = (int)i;
-        for (size_t j = 1; j <= n; ++j) {
-            const int up = row[j];
-            row[j] = std::min({diag + (a[i - 1] != b[j - 1]), up + 1, row[j - 1] + 1});
-            diag = up;
+    if (m == 0) return (int)n;
+    if (n == 0) return (int)m;
+    const size_t nb = (m + 63) / 64;
+    const size_t pad = nb * 64 - m;
+    const uint64_t padmask = pad ? ~0ull << (64 - pad) : 0;   // padded rows of the last block
+    std::vector<uint64_t> peq(nb * 256, 0);
+    for (size_t c = 0; c < 256; ++c) peq[(nb - 1) * 256 + c] = padmask;
+    for (size_t i = 0; i < m; ++i) peq[(i / 64) * 256 + (unsigned char)a[i]] |= 1ull << (i % 64);
+    std::vector<uint64_t> P(nb, ~0ull), M(nb, 0);   // vertical deltas +1 / -1 (D[i][0] = i)
+    long long score = (long long)(nb * 64);         // D[bottom row][0]
+    for (size_t j = 0; j < n; ++j) {
+        const uint64_t *eqc = &peq[(unsigned char)b[j]];
+        int hin = 1;                                 // D[0][j+1] - D[0][j] = +1 (global)
+        for (size_t k = 0; k < nb; ++k) {
+            uint64_t Eq = eqc[k * 256];
+            const uint64_t Pv = P[k], Mv = M[k];
+            const uint64_t Xv = Eq | Mv;
+            if (hin < 0) Eq |= 1ull;
+            const uint64_t Xh = (((Eq & Pv) + Pv) ^ Pv) | Eq;
+            uint64_t Ph = Mv | ~(Xh | Pv);
+            uint64_t Mh = Pv & Xh;
+            const int hout = (Ph >> 63) ? 1 : ((Mh >> 63) ? -1 : 0);
+            Ph <<= 1;
+            Mh <<= 1;
+            if (hin < 0) Mh |= 1ull;
+            else if (hin > 0) Ph |= 1ull;
+            P[k] = Mh | ~(Xv | Ph);
+            M[k] = Ph & Xv;
+            hin = hout;
         }
+        score += hin;
     }
-    return row[n];
+    // D[m][n] = D[bottom][n] - (deltas of the padded rows in the last column)
+    score -= (long long)__builtin_popcountll(P[nb - 1] & padmask) -
+             (long long)__builtin_popcountll(M[nb - 1] & padmask);
+    return (int)score;
 }
 
 }  // extern "C"

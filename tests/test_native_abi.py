@@ -46,3 +46,33 @@ def test_no_cpu_fallback_without_gpu(native):
         pytest.skip('a GPU is visible')
     with pytest.raises(native.NativeUnavailable):
         native.Context(0)
+
+
+def test_levenshtein_bit_parallel_matches_dp(native):
+    """mh_levenshtein (bit-vector, 64-row blocks) against the oracle's
+    cell-by-cell DP, across block boundaries and with the consensus alphabet."""
+    import random
+
+    import oracle
+    rng = random.Random(7)
+    alphabet = 'ACGTN-'
+    lengths = [0, 1, 2, 63, 64, 65, 127, 128, 129, 300, 701]
+    for la in lengths:
+        for lb in (0, 1, 64, 65, la, la + 3, max(la - 5, 0), 500):
+            a = ''.join(rng.choice(alphabet) for _ in range(la))
+            # b: a mutated copy half the time (small distances), random otherwise
+            if rng.random() < 0.5 and la:
+                b = list(a)
+                for _ in range(rng.randint(0, 8)):
+                    op, p = rng.randint(0, 2), rng.randrange(len(b) + 1)
+                    if op == 0 and p < len(b):
+                        b[p] = rng.choice(alphabet)
+                    elif op == 1:
+                        b.insert(p, rng.choice(alphabet))
+                    elif b and p < len(b):
+                        del b[p]
+                b = ''.join(b)
+            else:
+                b = ''.join(rng.choice(alphabet) for _ in range(lb))
+            assert native.levenshtein(a, b) == oracle.levenshtein(a, b), (la, len(b))
+            assert native.levenshtein(b, a) == oracle.levenshtein(a, b), (la, len(b))
