@@ -523,6 +523,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipFree(R.flag); hipFree(R.ref); hipFree(R.pos); hipFree(R.cig_off); hipFree(R.n_cigar);
     hipFree(R.cigar); hipFree(R.units);
     PileState &P = c->pile;
+    hipFree(c->gotoh_buf);
     hipFree(P.dense); hipFree(P.nflag); hipFree(P.dflag); hipFree(P.read_counts);
     hipFree(P.first_unit); hipFree(P.max_pos); hipFree(P.ev); hipFree(P.ev_pool);
     hipFree(P.ev_counters);

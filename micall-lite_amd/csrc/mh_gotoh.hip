@@ -179,8 +179,14 @@ int run_gotoh(Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_g
                  sz_diag = sizeof(int) * 3 * (m + 2) * 3, sz_last = sizeof(int) * (m + n + 4),
                  sz_bits = 3 * cells, sz_str = (size_t)2 * (m + n + 2) * 2, sz_res = 64;
     const size_t total = sz_codes + sz_mat + sz_diag + sz_last + sz_bits + sz_str + sz_res + 256;
-    char *d = nullptr;
-    MH_HIP(hipMalloc(&d, total));
+    if (c.gotoh_cap < total) {
+        hipFree(c.gotoh_buf);
+        c.gotoh_buf = nullptr;
+        c.gotoh_cap = 0;
+        MH_HIP(hipMalloc(&c.gotoh_buf, total));
+        c.gotoh_cap = total;
+    }
+    char *d = c.gotoh_buf;
     size_t o = 0;
     auto take = [&](size_t sz) { char *p = d + o; o += (sz + 15) & ~(size_t)15; return p; };
     GotohArgs A{};
@@ -218,7 +224,6 @@ int run_gotoh(Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_g
         e = hipMemcpy(t1.data(), A.out1, res[2], hipMemcpyDeviceToHost);
         if (e == hipSuccess) e = hipMemcpy(t2.data(), A.out2, res[2], hipMemcpyDeviceToHost);
     }
-    hipFree(d);
     if (e != hipSuccess) return hip_fail(e, "k_gotoh");
     if (res[0] != 0) { set_error("Traceback failed, try local alignment"); return -1; }
     const int len = res[2];

@@ -192,6 +192,10 @@ struct Ctx {
     CensorState *censor = nullptr;   // censored FASTQ of the last mh_censor_fastq
     A2CState **a2c = nullptr;        // aln2counts row tables (mh_a2c_*), one per slot
     int len_tab_mode = -1;
+    // k_gotoh's device scratch (traceback planes etc.), grown on demand and
+    // kept: a hipMalloc / hipFree pair per alignment cost more than the kernel
+    char *gotoh_buf = nullptr;
+    size_t gotoh_cap = 0;
 };
 
 void set_error(const char *fmt, ...);
