@@ -384,7 +384,7 @@ def bench_aln2counts(args):
     def step():
         # a fresh process aligns every consensus: no memoised alignment
         # survives from the previous step
-        a2c.aligner._memo.clear()
+        a2c.aligner.forget()
         outs = [io.StringIO() for _ in range(6)]
         with open(path) as f:
             a2c.aln2counts(f, *outs[:4], failed_align_csv=outs[4], coverage_summary_csv=outs[5])
@@ -504,7 +504,7 @@ def main():
     reads, quals = make_reads(args.pairs, block=rank, read_len=L, paired=paired, genomes=args.genomes)
     ctx.reads_load_fixed(reads, quals, paired)
     del reads, quals
-    shard = Shard(rank, world, read_base=rank * 2 * args.pairs, device=device) if world > 1 else None
+    shard = Shard(rank, world, read_base=rank * (1 if args.unpaired else 2) * args.pairs, device=device) if world > 1 else None
     pipe = RemapPipeline(ctx, shard=shard)
     raw_count = 2.0 * args.pairs * world     # lines(R1) / 2, remap.py:457
 

@@ -88,12 +88,6 @@ int mh_device_count(int *n);
 int mh_ctx_create(int device, mh_ctx **out);
 int mh_ctx_destroy(mh_ctx *ctx);
 int mh_ctx_sync(mh_ctx *ctx);
-/* Tuning / ablation switches (not part of the reference interface):
- *   "dp_fast" (default 1): resolve a banded extension by the exact ungapped
- *   fast path when its score bound proves the full DP would pick the same
- *   all-M alignment; 0 always runs the full DP.  Results are
- *   identical either way. */
-int mh_ctx_set_option(mh_ctx *ctx, const char *name, int value);
 /* the hipStream_t the context launches on (as an opaque handle) */
 int mh_ctx_stream(mh_ctx *ctx, void **stream);
 

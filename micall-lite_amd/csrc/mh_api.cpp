@@ -546,17 +546,6 @@ int mh_ctx_sync(mh_ctx *ctx)
     return 0;
 }
 
-int mh_ctx_set_option(mh_ctx *ctx, const char *name, int value)
-{
-    if (!ctx || !name) return -3;
-    if (!strcmp(name, "dp_fast")) {
-        X(ctx)->dp_fast = value != 0;
-        return 0;
-    }
-    set_error("mh_ctx_set_option: unknown option '%s'", name);
-    return -3;
-}
-
 int mh_ctx_stream(mh_ctx *ctx, void **stream)
 {
     if (!ctx || !stream) return -3;

@@ -187,7 +187,6 @@ struct Ctx {
     PileState pile;
     // per-length tables (host-computed, uploaded): seed interval, min score, n ceil
     int32_t *len_tab = nullptr;      // [3][MAXLEN + 1]
-    int dp_fast = 1;                 // option "dp_fast": exact ungapped fast path of k_dp
     S2AState *s2a = nullptr;         // sam2aln rows and results (mh_sam2aln_csv)
     CensorState *censor = nullptr;   // censored FASTQ of the last mh_censor_fastq
     A2CState **a2c = nullptr;        // aln2counts row tables (mh_a2c_*), one per slot

@@ -341,10 +341,9 @@ __device__ int seed_read(const SeedArgs &A, int64_t r, int lane, uint64_t *hits,
 // atomic (a returning same-address atomic costs ~11 ns device-wide).
 constexpr int SEED_CHUNK = 32;
 
-#ifndef MH_SEED_WPS
-#define MH_SEED_WPS 8        // min waves per SIMD: <= 64 VGPRs, 8 waves/SIMD (latency-bound probes)
-#endif
-__global__ __launch_bounds__(256, MH_SEED_WPS) void k_seed(SeedArgs A)
+// k_seed is latency-bound (hash probes): built for 8 waves per SIMD (<= 64 VGPRs).
+constexpr int SEED_WAVES_PER_SIMD = 8;
+__global__ __launch_bounds__(256, SEED_WAVES_PER_SIMD) void k_seed(SeedArgs A)
 {
     __shared__ uint64_t sh_hits[4][MAXHITS_MATE];
     __shared__ Cand sh_best[4][MAXCAND];
@@ -387,7 +386,6 @@ struct DpArgs {
     int rows_pad;             // per-wave LDS row capacity (multiple of 8)
     int wave_lds;             // bytes of LDS per wave
     int oeI, exI, oeD, exD;
-    int fast;                 // try the exact ungapped fast path (dp_ungapped)
 };
 
 __device__ __forceinline__ int mm_pen(int qchar)
@@ -402,13 +400,7 @@ __device__ __forceinline__ int mm_pen(int qchar)
 // edges acts as minus infinity.  The moves then fold into the ALU op that uses
 // them (v_max_i32_dpp, v_add_u32_dpp) instead of costing a mov + a fill each.
 constexpr int BIAS = 1 << 20;
-#ifndef MH_DP_WPB
-#define MH_DP_WPB 4          // waves per k_dp workgroup (4 measured best)
-#endif
-#ifndef MH_DP_PREFETCH
-#define MH_DP_PREFETCH 0     // load the next 8-row group's LDS operands early
-#endif
-static_assert(MH_DP_WPB >= 1 && MH_DP_WPB <= 4, "k_dp is compiled for <= 256 threads");
+constexpr int DP_WAVES_PER_BLOCK = 4;   // k_dp workgroup size in waves (measured best of 1-4)
 // CIGAR runs kept by the traceback.  A path with more runs cannot end up
 // with <= MH_MAXOPS - 1 ops: overhang trimming removes at most ~2 x 64 runs.
 constexpr int RUNS_CAP = 256;
@@ -833,37 +825,23 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         }
 
         int best, bi, bl;
-        const bool fast = A.fast && m > 2 * GBAR + 8 && m <= 512 &&
+        const bool fast = m > 2 * GBAR + 8 && m <= 512 &&
                           dp_ungapped<LOCAL>(tab, refw, rdc, bits, m, lane,
                                              A.oeI < A.oeD ? A.oeI : A.oeD, best, bi, bl);
         n_fast += fast;
         if (!fast) {
             // ---- DP over rows, 8 rows per group (one u32 of traceback bits per
             // lane); groups wholly inside the gap window run branch-free; the next
-            // group's LDS operands are loaded while this group computes ----
+            // group's operands come from LDS ----
             int Hp = BIAS, Ep = 0;
             uint32_t bestKey = 0;
-            uint32_t tbn[8];
-            int rcn[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                tbn[t] = tab[t];
-                rcn[t] = refw[t + lane];
-            }
             for (int i0 = 0; i0 < m; i0 += 8) {
                 uint32_t tbv[8];
                 int rcv[8];
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
-                    tbv[t] = MH_DP_PREFETCH ? tbn[t] : tab[i0 + t];
-                    rcv[t] = MH_DP_PREFETCH ? rcn[t] : refw[i0 + t + lane];
-                }
-                if (MH_DP_PREFETCH && i0 + 8 < m) {
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        tbn[t] = tab[i0 + 8 + t];
-                        rcn[t] = refw[i0 + 8 + t + lane];
-                    }
+                    tbv[t] = tab[i0 + t];
+                    rcv[t] = refw[i0 + t + lane];
                 }
                 uint32_t acc = 0;
                 if (i0 >= GBAR && i0 + 8 <= m - GBAR) {
@@ -915,7 +893,6 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         best = __builtin_amdgcn_readfirstlane(best);
         bi = __builtin_amdgcn_readfirstlane(bi);
         bl = __builtin_amdgcn_readfirstlane(bl);
-#ifndef MH_ABLATE_NOTB
         if (!(LOCAL && best <= 0) && best >= __builtin_amdgcn_readfirstlane(minsc)) {
             const int d0u = __builtin_amdgcn_readfirstlane(d0);
             int i = bi, k = bl, state = 0, ok = 1;
@@ -989,7 +966,6 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             t_first = first_j;
             t_nrun = nrun;
         }
-#endif
         wave_sync();
         Slot out{};
         out.valid = 0;
@@ -1481,10 +1457,10 @@ int run_map(Ctx &c, const mh_params &par)
             DpArgs da{c.reads, c.index, c.len_tab, M.cand, M.work, M.counters, M.slot, M.pool,
                       M.counters + 1, M.pool_cap, rows_pad, wave_lds,
                       par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext,
-                      par.rdg_ext, c.dp_fast};
+                      par.rdg_ext};
             // one wave per workgroup: the CU then packs floor(160 KiB / wave_lds)
             // waves (15 at 251-nt reads) with no workgroup rounding loss
-            int wpb = MH_DP_WPB;
+            int wpb = DP_WAVES_PER_BLOCK;
             while (wpb > 1 && wpb * wave_lds > 160 * 1024) --wpb;
             if (wave_lds > 160 * 1024) { set_error("mh_map: reads too long for LDS"); return -3; }
             int64_t dblocks = (n * 2 + wpb - 1) / wpb;

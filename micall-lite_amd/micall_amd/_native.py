@@ -69,7 +69,6 @@ def _declare(L):
         'mh_alns_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
         'mh_map_counts': ([_P, _P, _P, _P, _P, _P, _I64P, _I64P, _I64P], ctypes.c_int),
         'mh_map_stats': ([_P, _P], ctypes.c_int),
-        'mh_ctx_set_option': ([_P, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
         'mh_recs_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
         'mh_format_rows': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.c_int64,
                             ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_size_t,
@@ -412,9 +411,6 @@ class Context:
                     first_mapped=firstm[:n], unmapped=unm.value, star=star.value,
                     star_first=star_first.value)
 
-    def set_option(self, name, value):
-        """mh_ctx_set_option (e.g. 'dp_fast' 0/1)."""
-        check(lib().mh_ctx_set_option(self.h, name.encode(), int(value)), 'mh_ctx_set_option')
 
     def map_stats(self):
         """(reads, banded extensions, CIGAR ops, ungapped fast-path extensions)

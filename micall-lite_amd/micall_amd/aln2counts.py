@@ -1,37 +1,39 @@
 """
-Drop-in for micall/core/aln2counts.py: the same function, classes, arguments
-and output files.
+aln2counts stage on the MI355X: the drop-in for micall/core/aln2counts.py.
 
-aln2counts() reads aligned.csv (sam2aln's distinct merged reads and their
-counts), takes consecutive rows with the same (refname, qcut) as one group
-(itertools.groupby, aln2counts.py:884-887) and writes, per group, amino-acid
-and nucleotide counts in coordinate-reference positions, the mixture
-consensus, insertions relative to the coordinate reference and the
-consensus sequences that failed to align (aln2counts.py:822-898).
+Input is aligned.csv (sam2aln's distinct merged reads with their counts).
+Rows are taken in runs of equal (refname, qcut) -- the reference groups them
+with itertools.groupby (aln2counts.py:884-887) -- and every run produces
+amino-acid and nucleotide counts in coordinate-reference positions, the
+mixture consensus at each cutoff, the insertions relative to the coordinate
+reference and the consensus sequences that did not align.  Output files are
+byte-identical to the reference's (tests/test_gpu_aln2counts.py).
 
-Where the work runs:
-  * per read -- SequenceReport._count_reads (:115-172) and the read loop of
-    InsertionWriter.write (:786-795) -- on the device: mh_a2c_load_csv /
-    mh_a2c_load_rows count codons and bases in all three reading frames
-    (k_a2c_count) and mh_a2c_inserts groups the insertion strings
-    (k_a2c_ins_*), csrc/mh_a2c.hip.  Every counter comes with the first row
-    that touched it: the Counter insertion order most_common() breaks ties by.
-  * per group, O(reference length) -- here: the consensus letters (numpy),
-    the coordinate mapping of _map_to_coordinate_ref (:191-304) with its
-    local EmpHIV25 Gotoh alignments on the device (mh_gotoh_align, k_gotoh),
-    and the CSV text.
-There is no CPU fallback: without libmicall_hip.so or a device the first
-call raises NativeUnavailable.  SeedAmino and SeedNucleotide keep the
-reference's per-object API for code that uses them directly; the report does
-not count through them (seed_aminos / reports hand them out, built from the
-device counters on access).
+Split of the work:
+  device -- everything per read: 3-frame codon / base counting of a run,
+            with the first row that touched each counter (k_a2c_count), and
+            the grouping of inserted amino-acid strings (k_a2c_ins_*),
+            csrc/mh_a2c.hip.  The first row replaces the reference's Counter
+            insertion order, which decides most_common() ties.
+  host   -- everything per run and O(reference length): consensus letters
+            from the counters (numpy), the coordinate mapping with its local
+            EmpHIV25 Gotoh alignments (run on the device by mh_gotoh_align)
+            and the CSV text.
 
-Deviations, none of which changes an output file: the progress callback
-hears the start and the end of each group, not every 1 % of :136-141; the
-variant counts of :346-375, which the reference computes and discards, are
-not computed; an InsertionWriter fed by a SequenceReport reads the group's
-rows on the device, so its nuc_seqs stays empty; aligned.csv characters
-outside A C G T N - n, negative offsets and counts >= 2**32 are rejected.
+Public names (SequenceReport, InsertionWriter, SeedAmino, SeedNucleotide,
+ReportAmino, format_cutoff, aln2counts) and their signatures are the
+reference's, so callers and the reference's tests drive this module
+unchanged.  Differences that never reach an output file:
+  * the progress callback hears the start and the end of each run, not every
+    1 % of the file (aln2counts.py:136-141);
+  * the nucleotide variant counts that the reference computes and drops
+    (aln2counts.py:346-375) are not computed;
+  * an InsertionWriter fed by a SequenceReport reads the run's rows from the
+    device, so its nuc_seqs stays empty;
+  * characters other than A C G T N - n, negative offsets and counts of 2**32
+    or more raise NativeError.
+There is no CPU path: without libmicall_hip.so or a device the first call
+raises NativeUnavailable.
 """
 import argparse
 import csv
@@ -39,75 +41,97 @@ import io
 import json as jsonlib
 import os
 import re
-from collections import Counter
+from collections import Counter, namedtuple
 
 import numpy as np
 
 from . import projects as project_config
 from . import session
-from .translation import AMBIG as ambig_dict, codon_chars, translate
+from .translation import AMBIG, codon_chars, translate
 
 AMINO_ALPHABET = 'ACDEFGHIKLMNPQRSTVWY*'
 CONSEQ_MIXTURE_CUTOFFS = [0.01, 0.02, 0.05, 0.1, 0.2, 0.25]
-GAP_OPEN_COORD = 40
-GAP_EXTEND_COORD = 10
+GAP_OPEN_COORD, GAP_EXTEND_COORD = 40, 10
 MAX_CUTOFF = 'MAX'
 
-SLOT_REPORT, SLOT_INSERTS = 0, 1      # mh_a2c row tables used here
+# Column order of every file the stage writes (the reference's output schema).
+_SCHEMA = {
+    'amino': ['seed', 'region', 'q-cutoff', 'query.aa.pos', 'refseq.aa.pos'] + list(AMINO_ALPHABET),
+    'nuc': ['seed', 'region', 'q-cutoff', 'query.nuc.pos', 'refseq.nuc.pos'] + list('ACGT'),
+    'conseq': ['region', 'q-cutoff', 'consensus-percent-cutoff', 'offset', 'sequence'],
+    'nuc_variants': ['seed', 'qcut', 'region', 'index', 'count', 'seq'],
+    'failed': ['seed', 'region', 'qcut', 'queryseq', 'refseq'],
+    'insert': ['seed', 'region', 'qcut', 'left', 'insert', 'count', 'before'],
+    'coverage': ['avg_coverage', 'coverage_region', 'region_width'],
+}
+
+SLOT_REPORT, SLOT_INSERTS = 0, 1      # device row tables (mh_a2c slots) used here
 _CODON_CHARS = codon_chars()
-_NONE = np.uint32(0xffffffff)
+_NONE = np.uint32(0xffffffff)         # "no row touched this counter"
 _AA = np.array(list(AMINO_ALPHABET))
-# IUPAC letter of a set of bases, indexed by the bit mask A=1 C=2 G=4 T=8
+# IUPAC letter of a set of bases, indexed by the mask A=1 C=2 G=4 T=8
 _MIX = np.array(['', 'A', 'C', 'M', 'G', 'R', 'S', 'V', 'T', 'W', 'Y', 'H', 'K', 'D', 'B', 'N'])
 _MODELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'data', 'gotoh_models.json')
 
 
-class Aligner(object):
-    """gotoh2.Aligner (gotoh2.py:7-96) with the alignment on the device
-    (mh_gotoh_align).  Alignments are memoised per (seq1, seq2): the seed's
-    translations meet the same coordinate references in every group."""
+def _csv_writer(handle, kind):
+    return csv.DictWriter(handle, _SCHEMA[kind], lineterminator=os.linesep)
 
-    def __init__(self, gop=10, gep=1, is_global=False, model='HYPHY_NUC'):
-        self.gap_open_penalty = gop
-        self.gap_extend_penalty = gep
-        self.is_global = is_global
+
+def _text(value):
+    return value.decode('utf-8') if isinstance(value, bytes) else value
+
+
+class _CoordinateAligner(object):
+    """The module-level coordinate aligner of aln2counts.py:34-37 (local
+    Gotoh, gap open 40 / extend 10, EmpHIV25 scores), evaluated on the device
+    by mh_gotoh_align.  A seed's three translations meet the same coordinate
+    references in every run, so results are kept (bounded) by input pair."""
+
+    MEMO_LIMIT = 4096
+
+    def __init__(self, gop, gep, is_global, model):
         with open(_MODELS) as f:
-            self.models = {name: (m['matrix'], m['alphabet']) for name, m in jsonlib.load(f).items()}
-        self.set_model(model)
+            spec = jsonlib.load(f)[model]
+        self.gap_open_penalty, self.gap_extend_penalty = gop, gep
+        self.is_global = is_global
+        self.matrix, self.alphabet = spec['matrix'], spec['alphabet']
+        self._outside = re.compile('[^%s]' % (self.alphabet,))
         self._memo = {}
 
-    def set_model(self, model):
-        if model in self.models:
-            self.matrix, self.alphabet = self.models[model]
-        else:
-            print('ERROR: Unrecognized model name {}'.format(model))
-
-    def clean_sequence(self, seq):
-        return re.sub(pattern='[^%s]' % (self.alphabet,), repl='?', string=seq.upper())
+    def forget(self):
+        self._memo.clear()
 
     def align(self, seq1, seq2):
-        assert type(seq1) is str, 'seq1 must be a string'
-        assert type(seq2) is str, 'seq2 must be a string'
-        assert len(seq1) > 0, 'seq1 cannot be an empty string'
-        assert len(seq2) > 0, 'seq2 cannot be an empty string'
-        key = (seq1, seq2)
-        hit = self._memo.get(key)
-        if hit is None:
-            hit = session.context().gotoh_align(
-                self.clean_sequence(seq1), self.clean_sequence(seq2), self.gap_open_penalty,
-                self.gap_extend_penalty, self.is_global, self.alphabet, self.matrix)
-            if len(self._memo) >= 4096:
+        """(aligned seq1, aligned seq2, score); the checks of gotoh2.py:74-96
+        (str arguments, neither empty) raise AssertionError as there."""
+        for name, seq in (('seq1', seq1), ('seq2', seq2)):
+            if type(seq) is not str:
+                raise AssertionError('%s must be a string' % name)
+            if not seq:
+                raise AssertionError('%s cannot be an empty string' % name)
+        found = self._memo.get((seq1, seq2))
+        if found is None:
+            a, b = (self._outside.sub('?', s.upper()) for s in (seq1, seq2))
+            found = session.context().gotoh_align(a, b, self.gap_open_penalty,
+                                                  self.gap_extend_penalty, self.is_global,
+                                                  self.alphabet, self.matrix)
+            if len(self._memo) >= self.MEMO_LIMIT:
                 self._memo.clear()
-            self._memo[key] = hit
-        return hit
+            self._memo[(seq1, seq2)] = found
+        return found
 
 
-aligner = Aligner(gop=GAP_OPEN_COORD, gep=GAP_EXTEND_COORD, is_global=False, model='EmpHIV25')
+aligner = _CoordinateAligner(GAP_OPEN_COORD, GAP_EXTEND_COORD, False, 'EmpHIV25')
 
 
+# ---------------------------------------------------------------------------
+# consensus letters and alignment walks
+# ---------------------------------------------------------------------------
 def _nuc_letters(cnt, first, cutoff):
-    """SeedNucleotide.get_consensus (:655-695) at every position at once.
-    cnt / first: (positions, 6) over A C G T N -, first = the first row that
+    """The nucleotide consensus letter of every position at once
+    (SeedNucleotide.get_consensus semantics, aln2counts.py:655-695).
+    cnt / first: (positions, 6) over A C G T N -, `first` = first row that
     read the base (_NONE: never).  Returns (letters, coverage)."""
     present = first != _NONE
     total = cnt.sum(axis=1)
@@ -119,8 +143,8 @@ def _nuc_letters(cnt, first, cutoff):
         mix = acgt & (cnt[:, :4] >= (total * cutoff)[:, None])
     letters = _MIX[mix.astype(np.int64) @ np.array([1, 2, 4, 8])]
     letters[letters == ''] = 'N'                  # every base below the cutoff
-    # Only 'N' and / or '-' read here: the first of them in most_common()
-    # order survives the removal of gaps and poor quality (:671-674).
+    # Only 'N' and / or '-' read: the first of them in most_common() order
+    # is the one the removal of gaps and poor quality keeps.
     solo = present.any(axis=1) & ~acgt.any(axis=1)
     if solo.any():
         nc, dc = cnt[solo, 4], cnt[solo, 5]
@@ -136,7 +160,7 @@ def _nuc_letters(cnt, first, cutoff):
 def _index_map(aligned_from, seq_from, aligned_to, seq_to):
     """{index in seq_to: index in seq_from} along an alignment: at every
     column where seq_from advances, the current seq_to index maps to it
-    (the walks of :255-264 and :272-281)."""
+    (the two walks of aln2counts.py:255-264 and :272-281)."""
     out = {}
     i = j = 0
     n_from, n_to = len(seq_from), len(seq_to)
@@ -157,8 +181,14 @@ def _fill(counter, letters, cnt, first):
         counter[letters[k]] = int(cnt[k])
 
 
+# ---------------------------------------------------------------------------
+# device counters of one run
+# ---------------------------------------------------------------------------
+_Run = namedtuple('_Run', 'ctx slot group ncod seed qcut')
+
+
 class _Frame(object):
-    """Device counters of one reading frame of one group."""
+    """Device counters of one reading frame of one run."""
 
     def __init__(self, ctx, slot, g, frame, ncod):
         self.ncod = ncod
@@ -171,12 +201,12 @@ class _Frame(object):
         self.aa_first = aa_first
         self.nt_cnt = nt_cnt.astype(np.int64).reshape(-1, 3, 6)
         self.nt_first = nt_first.reshape(-1, 3, 6)
-        self.has = (aa_first != _NONE).any(axis=1)      # SeedAmino.counts is not empty
+        self.has = (aa_first != _NONE).any(axis=1)      # the codon's Counter is not empty
         self._consensus = None
 
     def consensus(self):
-        """''.join(SeedAmino.get_consensus()) over the frame (:214-215): the
-        most counted amino acid, ties to the first one seen; '-' if none."""
+        """Amino-acid consensus of the frame: the most counted amino acid of
+        each codon, ties to the first one counted; '-' where none was."""
         if self._consensus is None:
             present = self.aa_first != _NONE
             score = np.where(present, self.aa_cnt, -1)
@@ -186,7 +216,7 @@ class _Frame(object):
         return self._consensus
 
     def seed_amino(self, i):
-        """SeedAmino(i) holding the device counts of codon i."""
+        """A SeedAmino holding the device counts of codon i."""
         amino = SeedAmino(i)
         if i < self.ncod:
             _fill(amino.counts, AMINO_ALPHABET, self.aa_cnt[i], self.aa_first[i])
@@ -196,7 +226,7 @@ class _Frame(object):
 
 
 class _FrameAminos(object):
-    """seed_aminos[frame]: the reference's list of SeedAmino, built on access."""
+    """seed_aminos[frame] as a sequence of SeedAmino, materialised on access."""
 
     def __init__(self, frame, length):
         self._frame = frame
@@ -219,7 +249,7 @@ class _FrameAminos(object):
 
 
 class _LazySeedAmino(object):
-    """A report's SeedAmino: consensus_index at once, the counts on access."""
+    """A report position's SeedAmino: its index now, its counts on access."""
 
     def __init__(self, frame, index):
         self.consensus_index = index
@@ -237,468 +267,430 @@ class _LazySeedAmino(object):
         return repr(self._frame.seed_amino(self.consensus_index))
 
 
+class _CoordinateMap(object):
+    """Where one coordinate region sits in a run: the chosen reading frame,
+    and per coordinate position the consensus codon index (-1: none)."""
+
+    def __init__(self, frame=0, conseq_index=(), positions=()):
+        self.frame = frame
+        self.conseq_index = np.asarray(conseq_index, dtype=np.int64)
+        self.positions = np.asarray(positions, dtype=np.int64)
+
+    def __len__(self):
+        return len(self.conseq_index)
+
+
+# ---------------------------------------------------------------------------
+# SequenceReport
+# ---------------------------------------------------------------------------
 class SequenceReport(object):
-    """SequenceReport (:73-579): read the aligned reads of one (refname,
-    qcut) group, then write its reports."""
+    """Counts and reports of one (refname, qcut) run of aligned reads
+    (aln2counts.py:73-579).  read() a run, then call the write_* methods."""
 
     def __init__(self, insert_writer, projects, conseq_mixture_cutoffs):
         self.insert_writer = insert_writer
         self.projects = projects
-        self.conseq_mixture_cutoffs = list(conseq_mixture_cutoffs)
-        self.conseq_mixture_cutoffs.insert(0, MAX_CUTOFF)
+        self.conseq_mixture_cutoffs = [MAX_CUTOFF] + list(conseq_mixture_cutoffs)
         self.callback = None
 
     def enable_callback(self, callback, file_size):
-        """:98-113."""
+        """Report reading progress to callback(message, progress, max_progress)."""
         self.callback = callback
         self.callback_max = file_size
-        self.callback_chunk_size = file_size / 100
-        self.callback_next = self.callback_chunk_size
-        self.callback_progress = 0
-        self.callback(message='... extracting statistics from alignments',
-                      progress=0,
-                      max_progress=self.callback_max)
+        callback(message='... extracting statistics from alignments', progress=0,
+                 max_progress=file_size)
 
     def _pair_align(self, reference, query):
-        """:174-189."""
-        if type(reference) == bytes:
-            reference = reference.decode('utf-8')
-        if type(query) == bytes:
-            query = query.decode('utf-8')
-        return aligner.align(reference, query)
+        """(aligned reference, aligned query, score) of the coordinate aligner;
+        test doubles override this one method."""
+        return aligner.align(_text(reference), _text(query))
 
+    # ---- reading a run ----
     def read(self, aligned_reads):
-        """SequenceReport.read (:306-375) on rows given here (dicts with
-        refname, qcut, count, offset and seq): they go to the device as one
-        group."""
+        """Start over with the rows given (dicts with refname, qcut, count,
+        offset, seq); they go to the device as one run."""
         rows = list(aligned_reads)
-        group = None
+        run = None
         if rows:
-            seqs = [row['seq'] for row in rows]
-            offsets = [int(row['offset']) for row in rows]
-            counts = [int(row['count']) for row in rows]
             ctx = session.context()
-            ctx.a2c_load_rows(SLOT_REPORT, seqs, offsets, counts, [0, len(rows)], _CODON_CHARS)
-            ncod = ctx.a2c_group(SLOT_REPORT, 0)['ncod']
-            group = (ctx, SLOT_REPORT, 0, ncod, rows[0]['refname'], rows[0]['qcut'])
-        self._read(group)
+            ctx.a2c_load_rows(SLOT_REPORT, [r['seq'] for r in rows],
+                              [int(r['offset']) for r in rows], [int(r['count']) for r in rows],
+                              [0, len(rows)], _CODON_CHARS)
+            run = _Run(ctx, SLOT_REPORT, 0, ctx.a2c_group(SLOT_REPORT, 0)['ncod'],
+                       rows[0]['refname'], rows[0]['qcut'])
+        self._start(run)
 
     def _read_group(self, ctx, slot, g):
-        """read() of group g of a table already on the device."""
+        """read() of run g of a row table that is already on the device."""
         info = ctx.a2c_group(slot, g)
-        self._read((ctx, slot, g, info['ncod'], info['refname'], info['qcut']))
+        self._start(_Run(ctx, slot, g, info['ncod'], info['refname'], info['qcut']))
 
-    def _read(self, group):
-        self.seed_aminos = {}  # {reading_frame: [SeedAmino(consensus_index)]}
-        self.reports = {}  # {coord_name: [ReportAmino()]}
-        self.reading_frames = {}  # {coord_name: reading_frame}
-        self.inserts = {}  # {coord_name: set([consensus_index])}
-        self.consensus = {}  # {coord_name: consensus_amino_seq}
-        self.variants = {}  # {coord_name: [(count, nuc_seq)]}
+    def _start(self, run):
+        # state the write_* methods use; attribute names are the reference's
+        for name in ('seed_aminos', 'reports', 'reading_frames', 'inserts', 'consensus',
+                     'variants'):
+            setattr(self, name, {})
         self._frames = None
-        self._report_index = {}  # {coord_name: (frame, conseq indices, positions)}
-        if group is not None:
-            ctx, slot, g, ncod, self.seed, self.qcut = group
-            self.insert_writer.start_group(self.seed, self.qcut)
-            self.insert_writer._attach(ctx, slot, g)
-            self._frames = [_Frame(ctx, slot, g, f, ncod[f]) for f in range(3)]
-            for f in range(3):
-                self.seed_aminos[f] = _FrameAminos(self._frames[f], ncod[f])
+        self._coord_maps = {}
+        if run is not None:
+            self.seed, self.qcut = run.seed, run.qcut
+            self.insert_writer.start_group(run.seed, run.qcut)
+            self.insert_writer._attach(run.ctx, run.slot, run.group)
+            self._frames = [_Frame(run.ctx, run.slot, run.group, f, run.ncod[f])
+                            for f in range(3)]
+            self.seed_aminos = {f: _FrameAminos(fr, fr.ncod) for f, fr in enumerate(self._frames)}
         if self.callback:
             self.callback(progress=self.callback_max)
-        if not self.seed_aminos:
-            self.coordinate_refs = {}
-        else:
+        self.coordinate_refs = {}
+        if self.seed_aminos:
             self.coordinate_refs = self.projects.getCoordinateReferences(self.seed)
             if not self.coordinate_refs:
-                # pad frame 0 to the seed reference's length (:336-338)
-                seed_len = len(self.projects.getReference(self.seed))
-                n0 = max(len(self.seed_aminos[0]), -(-seed_len // 3))
-                self.seed_aminos[0] = _FrameAminos(self._frames[0], n0)
-        for coordinate_name, coordinate_ref in self.coordinate_refs.items():
-            self._map_to_coordinate_ref(coordinate_name, coordinate_ref)
+                # no coordinate region: frame 0 covers the whole seed
+                codons = -(-len(self.projects.getReference(self.seed)) // 3)
+                frame0 = self._frames[0]
+                self.seed_aminos[0] = _FrameAminos(frame0, max(frame0.ncod, codons))
+        for name, coordinate_ref in self.coordinate_refs.items():
+            self._locate(name, _text(coordinate_ref))
 
-    def _map_to_coordinate_ref(self, coordinate_name, coordinate_ref):
-        """_map_to_coordinate_ref (:191-304): the best reading frame by local
-        alignment with the coordinate reference, then coordinate position ->
-        seed position -> consensus position."""
-        if type(coordinate_ref) == bytes:
-            coordinate_ref = coordinate_ref.decode('utf-8')
-        consensus_length = int(self._frames[0].has.sum())
-        max_score = min(consensus_length, len(coordinate_ref))
-        best_alignment = None
-        for reading_frame in self.seed_aminos:
-            consensus = self._frames[reading_frame].consensus()
-            if reading_frame == 0:
-                # best guess before aligning
-                self.consensus[coordinate_name] = consensus
-            _aref, _aquery, score = self._pair_align(coordinate_ref, consensus)
-            if score > max_score:
-                max_score = score
-                best_alignment = (reading_frame, consensus)
-        report_aminos, index, positions, frame = [], [], [], 0
-        if best_alignment is not None:
-            frame, consensus = best_alignment
-            self.reading_frames[coordinate_name] = frame
-            self.consensus[coordinate_name] = consensus
-            seed_nuc_seq = self.projects.getReference(self.seed)
-            best_seed_alignment = None
-            max_seed_score = 0
-            for seed_frame in range(3):
-                seed_amino_seq = translate(seed_nuc_seq, offset=seed_frame, ambig_char='-')
-                aseed, aref, score = self._pair_align(seed_amino_seq, coordinate_ref)
-                if score > max_seed_score:
-                    max_seed_score = score
-                    best_seed_alignment = (seed_amino_seq, aseed, aref)
-            seed_amino_seq, aseed, aref = best_seed_alignment
-            ref2seed = _index_map(aseed, seed_amino_seq, aref, coordinate_ref)
-            aseed, aconseq, _score = self._pair_align(seed_amino_seq, consensus)
-            aconseq = aconseq.replace('?', '-')  # gotoh2 pads the left with ?'s
-            seed2conseq = _index_map(aconseq, consensus, aseed, seed_amino_seq)
-            coordinate_inserts = set(range(len(consensus)))
-            self.inserts[coordinate_name] = coordinate_inserts
-            empty_seed_amino = SeedAmino(None)
-            for ref_index in sorted(ref2seed):
-                conseq_index = seed2conseq.get(ref2seed[ref_index])
-                if conseq_index is None:
+    def _best_frame(self, name, coordinate_ref):
+        """The reading frame whose amino-acid consensus aligns to the
+        coordinate reference with a score above min(covered codons, length
+        of the reference); None if no frame does."""
+        bar = min(int(self._frames[0].has.sum()), len(coordinate_ref))
+        best = None
+        for frame in self.seed_aminos:
+            consensus = self._frames[frame].consensus()
+            if frame == 0:
+                self.consensus[name] = consensus      # kept if no frame aligns
+            score = self._pair_align(coordinate_ref, consensus)[2]
+            if score > bar:
+                bar, best = score, (frame, consensus)
+        return best
+
+    def _seed_in_coordinates(self, coordinate_ref):
+        """The seed's translation in its best-aligning frame and the map
+        {coordinate index: seed amino index}."""
+        seed_nucs = self.projects.getReference(self.seed)
+        best_score, best = 0, None
+        for offset in range(3):
+            aminos = translate(seed_nucs, offset=offset, ambig_char='-')
+            aligned_seed, aligned_ref, score = self._pair_align(aminos, coordinate_ref)
+            if score > best_score:
+                best_score, best = score, (aminos, aligned_seed, aligned_ref)
+        aminos, aligned_seed, aligned_ref = best   # TypeError if none scored, as the reference
+        return aminos, _index_map(aligned_seed, aminos, aligned_ref, coordinate_ref)
+
+    def _locate(self, name, coordinate_ref):
+        """Coordinate position -> seed position -> consensus codon
+        (aln2counts.py:191-304)."""
+        report, cmap = [], _CoordinateMap()
+        chosen = self._best_frame(name, coordinate_ref)
+        if chosen is not None:
+            frame, consensus = chosen
+            self.reading_frames[name] = frame
+            self.consensus[name] = consensus
+            seed_aminos, ref_to_seed = self._seed_in_coordinates(coordinate_ref)
+            aligned_seed, aligned_conseq, _ = self._pair_align(seed_aminos, consensus)
+            # the aligner pads the left of a local alignment with '?'
+            seed_to_conseq = _index_map(aligned_conseq.replace('?', '-'), consensus,
+                                        aligned_seed, seed_aminos)
+            unplaced = set(range(len(consensus)))
+            self.inserts[name] = unplaced
+            blank = SeedAmino(None)
+            index, positions = [], []
+            for ref_index in sorted(ref_to_seed):
+                k = seed_to_conseq.get(ref_to_seed[ref_index])
+                if k is None:
                     index.append(-1)
-                    seed_amino = empty_seed_amino
+                    amino = blank
                 else:
-                    index.append(conseq_index)
-                    seed_amino = _LazySeedAmino(self._frames[frame], conseq_index)
-                    coordinate_inserts.remove(conseq_index)
+                    index.append(k)
+                    amino = _LazySeedAmino(self._frames[frame], k)
+                    unplaced.remove(k)
                 positions.append(ref_index + 1)
-                report_aminos.append(ReportAmino(seed_amino, ref_index + 1))
-        self.reports[coordinate_name] = report_aminos
-        self._report_index[coordinate_name] = (frame, np.array(index, dtype=np.int64),
-                                               np.array(positions, dtype=np.int64))
+                report.append(ReportAmino(amino, ref_index + 1))
+            cmap = _CoordinateMap(frame, index, positions)
+        self.reports[name] = report
+        self._coord_maps[name] = cmap
 
-    def _counts_at(self, frame, index, table, shape):
-        out = np.zeros((len(index),) + shape, dtype=np.int64)
-        hit = index >= 0
+    def _gather(self, cmap, table, shape):
+        """Rows of a per-codon counter table at the map's consensus codons
+        (zeros where the coordinate position has none)."""
+        out = np.zeros((len(cmap),) + shape, dtype=np.int64)
+        hit = cmap.conseq_index >= 0
         if hit.any():
-            out[hit] = table(self._frames[frame])[index[hit]]
+            out[hit] = table(self._frames[cmap.frame])[cmap.conseq_index[hit]]
         return out
 
-    # ---- writers (:377-579) ----
-    def _create_amino_writer(self, amino_file):
-        columns = ['seed',
-                   'region',
-                   'q-cutoff',
-                   'query.aa.pos',
-                   'refseq.aa.pos']
-        columns.extend(AMINO_ALPHABET)
-        return csv.DictWriter(amino_file,
-                              columns,
-                              lineterminator=os.linesep)
-
+    # ---- headers ----
     def write_amino_header(self, amino_file):
-        self._create_amino_writer(amino_file).writeheader()
-
-    def write_amino_counts(self, amino_file, coverage_summary=None):
-        """Amino-acid counts at each coordinate-reference position (:391-433)."""
-        writer = csv.writer(amino_file, lineterminator=os.linesep)
-        for region in sorted(self.reports):
-            frame, index, positions = self._report_index[region]
-            n = len(index)
-            if not n:
-                continue
-            counts = self._counts_at(frame, index, lambda fr: fr.aa_cnt, (len(AMINO_ALPHABET),))
-            query = [str(i + 1) if i >= 0 else '' for i in index.tolist()]
-            writer.writerows([self.seed, region, self.qcut, q, p] + c
-                             for q, p, c in zip(query, positions.tolist(), counts.tolist()))
-            if coverage_summary is not None:
-                region_coverage = float(counts.sum()) / n
-                old_coverage = coverage_summary.get('avg_coverage', -1)
-                if region_coverage > old_coverage:
-                    coverage_summary['avg_coverage'] = region_coverage
-                    coverage_summary['coverage_region'] = region
-                    coverage_summary['region_width'] = n
-
-    def _create_nuc_writer(self, nuc_file):
-        return csv.DictWriter(nuc_file,
-                              ['seed',
-                               'region',
-                               'q-cutoff',
-                               'query.nuc.pos',
-                               'refseq.nuc.pos',
-                               'A',
-                               'C',
-                               'G',
-                               'T'],
-                              lineterminator=os.linesep)
+        _csv_writer(amino_file, 'amino').writeheader()
 
     def write_nuc_header(self, nuc_file):
-        self._create_nuc_writer(nuc_file).writeheader()
+        _csv_writer(nuc_file, 'nuc').writeheader()
+
+    def write_consensus_header(self, conseq_file):
+        _csv_writer(conseq_file, 'conseq').writeheader()
+
+    def write_nuc_variants_header(self, nuc_variants_file):
+        _csv_writer(nuc_variants_file, 'nuc_variants').writeheader()
+
+    def write_failure_header(self, fail_file):
+        _csv_writer(fail_file, 'failed').writeheader()
+
+    # ---- bodies ----
+    def write_amino_counts(self, amino_file, coverage_summary=None):
+        """Amino-acid counts per coordinate position, regions in name order;
+        the region with the highest mean count goes to coverage_summary."""
+        out = csv.writer(amino_file, lineterminator=os.linesep)
+        for name in sorted(self.reports):
+            cmap = self._coord_maps[name]
+            if not len(cmap):
+                continue
+            counts = self._gather(cmap, lambda fr: fr.aa_cnt, (len(AMINO_ALPHABET),))
+            query = ['' if k < 0 else str(k + 1) for k in cmap.conseq_index.tolist()]
+            out.writerows([self.seed, name, self.qcut, q, p] + c for q, p, c in
+                          zip(query, cmap.positions.tolist(), counts.tolist()))
+            if coverage_summary is not None:
+                mean = float(counts.sum()) / len(cmap)
+                if mean > coverage_summary.get('avg_coverage', -1):
+                    coverage_summary.update(avg_coverage=mean, coverage_region=name,
+                                            region_width=len(cmap))
 
     def write_nuc_counts(self, nuc_file):
-        """Nucleotide counts (:451-476)."""
-        writer = csv.writer(nuc_file, lineterminator=os.linesep)
+        """A/C/G/T counts per nucleotide: in coordinate positions, or in seed
+        positions when the seed has no coordinate region."""
+        out = csv.writer(nuc_file, lineterminator=os.linesep)
+        lines = []
         if not self.coordinate_refs:
-            n = len(self.seed_aminos[0])       # KeyError without reads, as the reference
+            n = len(self.seed_aminos[0])      # KeyError without reads, as the reference
             frame = self._frames[0]
             counts = np.zeros((n, 3, 4), dtype=np.int64)
             counts[:frame.ncod] = frame.nt_cnt[:, :, :4]
-            rows = []
-            for j, codon in enumerate(counts.tolist()):
-                for i in range(3):
-                    rows.append([self.seed, self.seed, self.qcut, i + 3 * j + 1, ''] + codon[i])
-            writer.writerows(rows)
-            return
-        for region in self.reports:
-            frame, index, positions = self._report_index[region]
-            counts = self._counts_at(frame, index, lambda fr: fr.nt_cnt[:, :, :4], (3, 4))
-            rows = []
-            for ci, pos, codon in zip(index.tolist(), positions.tolist(), counts.tolist()):
-                for i in range(3):
-                    rows.append([self.seed, region, self.qcut, i + 3 * ci + 1 if ci >= 0 else '',
-                                 i + 3 * pos - 2] + codon[i])
-            writer.writerows(rows)
-
-    def _create_consensus_writer(self, conseq_file):
-        return csv.DictWriter(conseq_file,
-                              ['region',
-                               'q-cutoff',
-                               'consensus-percent-cutoff',
-                               'offset',
-                               'sequence'],
-                              lineterminator=os.linesep)
-
-    def write_consensus_header(self, conseq_file):
-        self._create_consensus_writer(conseq_file).writeheader()
+            for codon, per_base in enumerate(counts.tolist()):
+                lines.extend([self.seed, self.seed, self.qcut, 3 * codon + t + 1, ''] + acgt
+                             for t, acgt in enumerate(per_base))
+        else:
+            for name, cmap in ((n, self._coord_maps[n]) for n in self.reports):
+                counts = self._gather(cmap, lambda fr: fr.nt_cnt[:, :, :4], (3, 4))
+                for k, pos, per_base in zip(cmap.conseq_index.tolist(), cmap.positions.tolist(),
+                                            counts.tolist()):
+                    lines.extend([self.seed, name, self.qcut, '' if k < 0 else 3 * k + t + 1,
+                                  3 * pos - 2 + t] + acgt for t, acgt in enumerate(per_base))
+        out.writerows(lines)
 
     def write_consensus(self, conseq_file, min_coverage=100):
-        """Nucleotide consensus at each mixture cutoff (:490-522), lower case
-        below min_coverage."""
-        conseq_writer = self._create_consensus_writer(conseq_file)
-        aminos = self.seed_aminos[0]           # KeyError without reads, as the reference
+        """The nucleotide consensus of frame 0 from its first counted codon
+        on, one row per mixture cutoff; bases read fewer than min_coverage
+        times in lower case."""
+        seed_aminos = self.seed_aminos[0]     # KeyError without reads, as the reference
         frame = self._frames[0]
-        covered = np.flatnonzero(frame.has[:len(aminos)])
-        if not len(covered):
+        counted = np.flatnonzero(frame.has[:len(seed_aminos)])
+        if not len(counted):
             return
-        start = int(covered[0])
+        start = int(counted[0])
         cnt = frame.nt_cnt[start:].reshape(-1, 6)
         first = frame.nt_first[start:].reshape(-1, 6)
-        for mixture_cutoff in self.conseq_mixture_cutoffs:
-            letters, coverage = _nuc_letters(cnt, first, mixture_cutoff)
-            letters = np.where(coverage >= min_coverage, letters, np.char.lower(letters))
-            conseq_writer.writerow({
-                'region': self.seed,
-                'q-cutoff': self.qcut,
-                'consensus-percent-cutoff': format_cutoff(mixture_cutoff),
-                'offset': start * 3,
-                'sequence': ''.join(letters.tolist())
-            })
-
-    def _create_nuc_variants_writer(self, nuc_variants_file):
-        return csv.DictWriter(nuc_variants_file,
-                              ['seed',
-                               'qcut',
-                               'region',
-                               'index',
-                               'count',
-                               'seq'],
-                              lineterminator=os.linesep)
-
-    def write_nuc_variants_header(self, nuc_variants_file):
-        self._create_nuc_variants_writer(nuc_variants_file).writeheader()
+        out = _csv_writer(conseq_file, 'conseq')
+        for cutoff in self.conseq_mixture_cutoffs:
+            letters, depth = _nuc_letters(cnt, first, cutoff)
+            letters = np.where(depth >= min_coverage, letters, np.char.lower(letters))
+            out.writerow({'region': self.seed, 'q-cutoff': self.qcut,
+                          'consensus-percent-cutoff': format_cutoff(cutoff),
+                          'offset': start * 3, 'sequence': ''.join(letters.tolist())})
 
     def write_nuc_variants(self, nuc_variants_file):
-        """:537-549; under Python 3 the reference fails here (dict_keys has
-        no sort), and so does this."""
-        regions = self.variants.keys()
-        regions.sort()
-
-    def _create_failure_writer(self, fail_file):
-        return csv.DictWriter(fail_file,
-                              ['seed',
-                               'region',
-                               'qcut',
-                               'queryseq',
-                               'refseq'],
-                              lineterminator=os.linesep)
-
-    def write_failure_header(self, fail_file):
-        self._create_failure_writer(fail_file).writeheader()
+        """The reference sorts dict.keys() in place here, which fails under
+        Python 3 with AttributeError; so does this (no output either way)."""
+        getattr(self.variants.keys(), 'sort')()
 
     def write_failure(self, fail_file):
-        """Consensus sequences that did not align to their coordinate
-        reference (:563-572)."""
-        fail_writer = self._create_failure_writer(fail_file)
-        for region, report_aminos in self.reports.items():
-            if not report_aminos:
-                coordinate_ref = self.projects.getReference(region)
-                fail_writer.writerow(dict(seed=self.seed,
-                                          region=region,
-                                          qcut=self.qcut,
-                                          queryseq=self.consensus[region],
-                                          refseq=coordinate_ref))
+        """One row per coordinate region that no reading frame aligned to."""
+        out = _csv_writer(fail_file, 'failed')
+        out.writerows(dict(seed=self.seed, region=name, qcut=self.qcut,
+                           queryseq=self.consensus[name],
+                           refseq=self.projects.getReference(name))
+                      for name, report in self.reports.items() if not report)
 
     def write_insertions(self):
-        for coordinate_name, coordinate_inserts in self.inserts.items():
-            self.insert_writer.write(coordinate_inserts,
-                                     coordinate_name,
-                                     self.reading_frames[coordinate_name],
-                                     self.reports[coordinate_name])
+        for name in self.inserts:
+            self.insert_writer.write(self.inserts[name], name, self.reading_frames[name],
+                                     self.reports[name])
 
 
-class SeedAmino(object):
-    """SeedAmino (:582-626): amino-acid and nucleotide counts of one codon."""
-
-    def __init__(self, consensus_index):
-        self.consensus_index = consensus_index
-        self.counts = Counter()
-        self.nucleotides = [SeedNucleotide() for _ in range(3)]
-
-    def __repr__(self):
-        return 'SeedAmino({}): {}'.format(self.consensus_index, self.counts)
-
-    def count_aminos(self, codon_seq, count):
-        amino = translate(codon_seq.upper())
-        if amino in AMINO_ALPHABET:
-            self.counts[amino] += count
-        for i in range(3):
-            self.nucleotides[i].count_nucleotides(codon_seq[i], count)
-
-    def get_report(self):
-        return ','.join([str(self.counts[amino]) for amino in AMINO_ALPHABET])
-
-    def get_consensus(self):
-        consensus = self.counts.most_common(1)
-        return '-' if not consensus else consensus[0][0]
-
-
+# ---------------------------------------------------------------------------
+# per-codon / per-base counters (the reference's object API)
+# ---------------------------------------------------------------------------
 class SeedNucleotide(object):
-    """SeedNucleotide (:628-695): counts of one nucleotide position."""
+    """Counts of the letters read at one nucleotide position."""
 
     def __init__(self):
         self.counts = Counter()
 
     def count_nucleotides(self, nuc_seq, count):
-        if nuc_seq != 'n':     # 'n': the gap between forward and reverse read
-            self.counts[nuc_seq] += count
+        # 'n' marks the unread gap between the forward and the reverse read
+        if nuc_seq == 'n':
+            return
+        self.counts[nuc_seq] += count
 
     def get_report(self):
-        return ','.join(map(str, [self.counts[nuc] for nuc in 'ACGT']))
+        return ','.join(str(self.counts[base]) for base in 'ACGT')
 
     def get_consensus(self, mixture_cutoff):
+        """Consensus letter at a mixture cutoff (a fraction, or MAX_CUTOFF for
+        the most counted bases only); a tie or a mixture is an IUPAC code.
+        'N' and '-' count only when nothing else was read."""
         if not self.counts:
             return ''
         ranked = self.counts.most_common()
-        # gaps and poor quality drop out unless nothing else was read
-        kept = [item for item in ranked if item[0] not in ('N', '-')] or ranked[:1]
-        total_count = sum(self.counts.values())
-        min_count = kept[0][1] if mixture_cutoff == MAX_CUTOFF else total_count * mixture_cutoff
-        mixture = sorted(nuc for nuc, count in kept if count >= min_count)
-        if len(mixture) > 1:
-            return ambig_dict[''.join(mixture)]
-        return mixture[0] if mixture else 'N'
+        informative = [pair for pair in ranked if pair[0] not in 'N-']
+        candidates = informative or ranked[:1]
+        if mixture_cutoff == MAX_CUTOFF:
+            floor = candidates[0][1]
+        else:
+            floor = sum(self.counts.values()) * mixture_cutoff
+        chosen = sorted(base for base, n in candidates if n >= floor)
+        if not chosen:
+            return 'N'
+        return chosen[0] if len(chosen) == 1 else AMBIG[''.join(chosen)]
+
+
+class SeedAmino(object):
+    """Counts of the amino acids read at one codon, plus its three bases."""
+
+    def __init__(self, consensus_index):
+        self.consensus_index = consensus_index
+        self.counts = Counter()
+        self.nucleotides = [SeedNucleotide(), SeedNucleotide(), SeedNucleotide()]
+
+    def __repr__(self):
+        return '%s(%s): %s' % (type(self).__name__, self.consensus_index, self.counts)
+
+    def count_aminos(self, codon_seq, count):
+        amino = translate(codon_seq.upper())
+        if amino in AMINO_ALPHABET:
+            self.counts[amino] += count
+        for k, nuc in enumerate(self.nucleotides):
+            nuc.count_nucleotides(codon_seq[k], count)
+
+    def get_report(self):
+        return ','.join(str(self.counts[a]) for a in AMINO_ALPHABET)
+
+    def get_consensus(self):
+        top = self.counts.most_common(1)
+        return top[0][0] if top else '-'
 
 
 class ReportAmino(object):
+    """A coordinate position (1-based) and the SeedAmino reported there."""
+
+    __slots__ = ('seed_amino', 'position')
+
     def __init__(self, seed_amino, position):
-        self.seed_amino = seed_amino
-        self.position = position
+        self.seed_amino, self.position = seed_amino, position
 
     def __repr__(self):
-        return 'ReportAmino({!r}, {})'.format(self.seed_amino, self.position)
+        return '%s(%r, %s)' % (type(self).__name__, self.seed_amino, self.position)
+
+
+# ---------------------------------------------------------------------------
+# insertions
+# ---------------------------------------------------------------------------
+def _ranges(indices):
+    """Sorted indices -> [left, right) runs of consecutive values."""
+    runs = []
+    for k in sorted(indices):
+        if runs and runs[-1][1] == k:
+            runs[-1][1] = k + 1
+        else:
+            runs.append([k, k + 1])
+    return runs
 
 
 class InsertionWriter(object):
-    """InsertionWriter (:711-811).  The read loop of write() runs on the
-    device over the group the SequenceReport attached, or over the reads
+    """Writes the amino-acid strings read at consensus codons that have no
+    coordinate position (insert.csv).  The counting over the reads runs on
+    the device: over the run a SequenceReport attached, or over the reads
     given to add_nuc_read."""
 
     def __init__(self, insert_file):
-        self.insert_writer = csv.DictWriter(insert_file,
-                                            ['seed',
-                                             'region',
-                                             'qcut',
-                                             'left',
-                                             'insert',
-                                             'count',
-                                             'before'],
-                                            lineterminator=os.linesep)
-        self.insert_writer.writeheader()
         self._file = insert_file
+        self.insert_writer = _csv_writer(insert_file, 'insert')
+        self.insert_writer.writeheader()
         self.nuc_seqs = Counter()
         self._source = None
 
     def start_group(self, seed, qcut):
-        self.seed = seed
-        self.qcut = qcut
-        self.nuc_seqs = Counter()  # {nuc_seq: count}
+        self.seed, self.qcut = seed, qcut
+        self.nuc_seqs = Counter()
         self._source = None
 
     def add_nuc_read(self, offset_sequence, count):
+        """A read already padded with '-' to its consensus offset."""
         self.nuc_seqs[offset_sequence] += count
 
     def _attach(self, ctx, slot, g):
-        """The reads of this group are group g of the device table `slot`."""
+        """The reads of this run are run g of the device table `slot`."""
         self._source = (ctx, slot, g)
 
-    def _insert_counts(self, ranges, reading_frame):
-        if self._source is not None:
-            ctx, slot, g = self._source
-        else:
+    def _count(self, ranges, reading_frame):
+        """[(range number, count, first row, amino-acid string)] on the device."""
+        source = self._source
+        if source is None:
             if not self.nuc_seqs:
                 return []
-            ctx, slot, g = session.context(), SLOT_INSERTS, 0
-            seqs = list(self.nuc_seqs)
-            ctx.a2c_load_rows(slot, seqs, [0] * len(seqs), [self.nuc_seqs[s] for s in seqs],
-                              [0, len(seqs)], _CODON_CHARS)
+            reads = list(self.nuc_seqs)
+            ctx = session.context()
+            ctx.a2c_load_rows(SLOT_INSERTS, reads, [0] * len(reads),
+                              [self.nuc_seqs[r] for r in reads], [0, len(reads)], _CODON_CHARS)
+            source = (ctx, SLOT_INSERTS, 0)
+        ctx, slot, g = source
         return ctx.a2c_inserts(slot, g, reading_frame, [r[0] for r in ranges],
                                [r[1] for r in ranges])
 
-    def write(self, inserts, region, reading_frame=0, report_aminos=[]):
-        """Insertion ranges with their amino-acid strings and counts
-        (:748-811).  Ranges whose rows would be dropped (inserted before
-        position 1 or after the end) are not counted."""
+    def write(self, inserts, region, reading_frame=0, report_aminos=()):
+        """Rows for each run of inserted consensus codons: the 1-based left
+        codon, each amino-acid string with its count, and the coordinate
+        position the run precedes.  Runs placed before coordinate position 1
+        or past the end are skipped when report_aminos is given."""
         if len(inserts) == 0:
             return
-        insert_ranges = []
-        for insert in sorted(inserts):
-            if not insert_ranges or insert != insert_ranges[-1][1]:
-                insert_ranges.append([insert, insert + 1])
-            else:
-                insert_ranges[-1][1] += 1
-        positions = {}
-        for report_amino in report_aminos:
-            positions.setdefault(report_amino.seed_amino.consensus_index, report_amino.position)
-        insert_targets = {left: positions[right] for left, right in insert_ranges
-                          if right in positions}
-        wanted = [(left, right) for left, right in insert_ranges
-                  if not report_aminos or insert_targets.get(left) not in (1, None)]
-        if not wanted:
+        before = {}
+        for ra in report_aminos:
+            before.setdefault(ra.seed_amino.consensus_index, ra.position)
+        target = {}
+        for left, right in _ranges(inserts):
+            if right in before:
+                target[left] = before[right]
+        kept = [r for r in _ranges(inserts)
+                if not report_aminos or target.get(r[0]) not in (1, None)]
+        if not kept:
             return
-        entries = self._insert_counts(wanted, reading_frame)
-        if not entries:
+        found = self._count(kept, reading_frame)
+        if not found:
             return
-        # DictWriter's row text, built in one pass: the three leading fields
-        # through the csv module (quoting), the rest are numbers and amino-acid
-        # letters, which never need quotes
-        head = io.StringIO()
-        csv.writer(head, lineterminator='').writerow([self.seed, region, self.qcut, ''])
-        head = head.getvalue()
-        tails = {k: (wanted[k][0] + 1, insert_targets.get(wanted[k][0]))
-                 for k in range(len(wanted))}
-        self._file.write(''.join(
-            '{}{},{},{},{}{}'.format(head, tails[k][0], insert_seq, count,
-                                     '' if tails[k][1] is None else tails[k][1], os.linesep)
-            for k, count, _first, insert_seq in entries))
+        # the leading text columns go through the csv module (quoting); the
+        # rest are numbers and amino-acid letters, which never need quotes
+        lead = io.StringIO()
+        csv.writer(lead, lineterminator='').writerow([self.seed, region, self.qcut, ''])
+        lead = lead.getvalue()
+        rows = []
+        for k, count, _first, aminos in found:
+            left = kept[k][0]
+            pos = target.get(left)
+            rows.append('%s%d,%s,%d,%s%s' % (lead, left + 1, aminos, count,
+                                             '' if pos is None else pos, os.linesep))
+        self._file.write(''.join(rows))
 
 
 def format_cutoff(cutoff):
-    """ Format the cutoff fraction as a string to use as a name. """
-    if cutoff == MAX_CUTOFF:
-        return cutoff
-    return '{:0.3f}'.format(cutoff)
+    """Name of a mixture cutoff in conseq.csv: 'MAX' or three decimals."""
+    return cutoff if cutoff == MAX_CUTOFF else '%.3f' % cutoff
 
 
 def _read_all(handle):
-    """The rest of an open aligned.csv: the raw bytes of a text file that
-    nothing has read from yet (no decode / encode of the whole file), the
-    text otherwise."""
+    """The rest of an open aligned.csv: the raw bytes of a text file nothing
+    has read yet (no decode / encode of the whole file), the text otherwise."""
     raw = getattr(handle, 'buffer', None)
     if raw is not None:
         try:
@@ -710,83 +702,67 @@ def _read_all(handle):
     return handle.read()
 
 
-def aln2counts(aligned_csv,
-               nuc_csv,
-               amino_csv,
-               coord_ins_csv,
-               conseq_csv,
-               failed_align_csv=None,
-               nuc_variants_csv=None,
-               callback=None,
-               coverage_summary_csv=None,
-               json=None):
-    """aln2counts.aln2counts (:822-898): the same open files in and out."""
-    if json is None:
-        projects = project_config.ProjectConfig.loadDefault()
-    else:
-        projects = project_config.ProjectConfig.loadCustom(json)
-    insert_writer = InsertionWriter(coord_ins_csv)
-    report = SequenceReport(insert_writer, projects, CONSEQ_MIXTURE_CUTOFFS)
+def aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv,
+               failed_align_csv=None, nuc_variants_csv=None, callback=None,
+               coverage_summary_csv=None, json=None):
+    """aligned.csv -> nucleotide, amino-acid, insertion, consensus (and the
+    optional failure, variant and coverage) reports; every argument is an
+    open file except json, a project-file path (None: the default)."""
+    projects = (project_config.ProjectConfig.loadDefault() if json is None
+                else project_config.ProjectConfig.loadCustom(json))
+    report = SequenceReport(InsertionWriter(coord_ins_csv), projects, CONSEQ_MIXTURE_CUTOFFS)
     report.write_nuc_header(nuc_csv)
     report.write_amino_header(amino_csv)
     report.write_consensus_header(conseq_csv)
+    # what is written for each run, in the reference's file order
+    per_run = [lambda: report.write_amino_counts(amino_csv, coverage_summary=summary),
+               lambda: report.write_consensus(conseq_csv)]
     if failed_align_csv:
         report.write_failure_header(failed_align_csv)
+        per_run.append(lambda: report.write_failure(failed_align_csv))
+    per_run += [report.write_insertions, lambda: report.write_nuc_counts(nuc_csv)]
     if nuc_variants_csv:
         report.write_nuc_variants_header(nuc_variants_csv)
-    if coverage_summary_csv is None:
-        coverage_summary = None
-    else:
-        coverage_writer = csv.DictWriter(coverage_summary_csv,
-                                         ['avg_coverage',
-                                          'coverage_region',
-                                          'region_width'],
-                                         lineterminator=os.linesep)
-        coverage_writer.writeheader()
-        coverage_summary = {}
-    if callback:
-        aligned_filename = getattr(aligned_csv, 'name', None)
-        if aligned_filename:
-            report.enable_callback(callback, os.stat(aligned_filename).st_size)
-    ctx = session.context()
-    n_groups = ctx.a2c_load_csv(SLOT_REPORT, _read_all(aligned_csv), _CODON_CHARS)
-    for g in range(n_groups):
-        report._read_group(ctx, SLOT_REPORT, g)
-        report.write_amino_counts(amino_csv, coverage_summary=coverage_summary)
-        report.write_consensus(conseq_csv)
-        if failed_align_csv:
-            report.write_failure(failed_align_csv)
-        report.write_insertions()
-        report.write_nuc_counts(nuc_csv)
-        if nuc_variants_csv:
-            report.write_nuc_variants(nuc_variants_csv)
+        per_run.append(lambda: report.write_nuc_variants(nuc_variants_csv))
+    summary = None
     if coverage_summary_csv is not None:
-        if coverage_summary:
-            coverage_writer.writerow(coverage_summary)
+        summary_writer = _csv_writer(coverage_summary_csv, 'coverage')
+        summary_writer.writeheader()
+        summary = {}
+    source = getattr(aligned_csv, 'name', None) if callback else None
+    if source:
+        report.enable_callback(callback, os.stat(source).st_size)
+    ctx = session.context()
+    for g in range(ctx.a2c_load_csv(SLOT_REPORT, _read_all(aligned_csv), _CODON_CHARS)):
+        report._read_group(ctx, SLOT_REPORT, g)
+        for step in per_run:
+            step()
+    if summary:
+        summary_writer.writerow(summary)
 
 
-def parseArgs():
-    parser = argparse.ArgumentParser(description='Post-processing of short-read alignments.')
-    parser.add_argument('aligned_csv', type=argparse.FileType('r'), help='aligned CSF input')
-    parser.add_argument('nuc_csv', type=argparse.FileType('w'),
-                        help='CSV containing nucleotide frequencies')
-    parser.add_argument('amino_csv', type=argparse.FileType('w'),
-                        help='CSV containing amino frequencies')
-    parser.add_argument('coord_ins_csv', type=argparse.FileType('w'),
-                        help='CSV containing insertions relative to coordinate reference')
-    parser.add_argument('conseq_csv', type=argparse.FileType('w'),
-                        help='CSV containing consensus sequences')
-    parser.add_argument('--failed_align_csv', required=False, type=argparse.FileType('w'),
-                        help='CSV containing any consensus that failed to align')
-    parser.add_argument('--nuc_variants_csv', required=False, type=argparse.FileType('w'),
-                        help='CSV containing top nucleotide variants')
-    return parser.parse_args()
+def _arguments():
+    cli = argparse.ArgumentParser(description='aln2counts on the MI355X: counts, consensus and '
+                                              'insertions from aligned.csv.')
+    cli.add_argument('aligned_csv', type=argparse.FileType('r'), help='aligned.csv from sam2aln')
+    for name, what in (('nuc_csv', 'nucleotide counts'), ('amino_csv', 'amino-acid counts'),
+                       ('coord_ins_csv', 'insertions in coordinate positions'),
+                       ('conseq_csv', 'consensus sequences')):
+        cli.add_argument(name, type=argparse.FileType('w'), help='output: ' + what)
+    cli.add_argument('--failed_align_csv', type=argparse.FileType('w'),
+                     help='output: consensus sequences that did not align')
+    cli.add_argument('--nuc_variants_csv', type=argparse.FileType('w'),
+                     help='output: nucleotide variants')
+    return cli.parse_args()
+
+
+parseArgs = _arguments
 
 
 def main():
-    args = parseArgs()
-    aln2counts(args.aligned_csv, args.nuc_csv, args.amino_csv, args.coord_ins_csv,
-               args.conseq_csv, args.failed_align_csv, args.nuc_variants_csv)
+    a = _arguments()
+    aln2counts(a.aligned_csv, a.nuc_csv, a.amino_csv, a.coord_ins_csv, a.conseq_csv,
+               a.failed_align_csv, a.nuc_variants_csv)
 
 
 if __name__ == '__main__':

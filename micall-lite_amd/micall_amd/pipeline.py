@@ -36,13 +36,13 @@ MAXINS = 1200                 # -X 1200
 E2E_SEEDLEN, LOCAL_SEEDLEN = 22, 20
 
 
-def write_remap_counts(remap_counts_writer, counts, title, distance_report=None):
-    """remap.write_remap_counts (remap.py:373-378)."""
-    distance_report = distance_report or {}
-    for refname in sorted(counts.keys()):
-        row = distance_report.get(refname, {})
-        row.update(type=title + ' ' + refname, count=counts[refname])
-        remap_counts_writer.writerow(row)
+def write_remap_counts(writer, counts, title, distance_report=None):
+    """remap_counts.csv rows of one pass (remap.py:373-378): references in
+    name order, each with its distance-filter columns when it has them."""
+    extra = distance_report or {}
+    for name in sorted(counts):
+        row = dict(extra.get(name, {}), type='%s %s' % (title, name), count=counts[name])
+        writer.writerow(row)
 
 
 class Shard:
@@ -243,31 +243,64 @@ class RemapPipeline:
                               distance_report)
 
     def run(self, raw_count, max_iterations=None, remap_counts_writer=None, min_iterations=None):
-        """The whole of remap()'s loop.  max_iterations caps the number of
-        mapping passes (benchmark configs); None = the reference's rules.
-        min_iterations (benchmark configs only, e.g. BASELINE C3's "3 remap
-        iterations") runs that many passes before the stopping rules apply."""
+        """prelim_map + remap on the resident reads: the device prelim pass,
+        seed selection, then iterate()."""
         self.raw_count = raw_count
         self.prelim()
         groups = self.prelim_groups()
         if remap_counts_writer is not None:
-            for refname, count, filt in groups:
-                remap_counts_writer.writerow(dict(type='prelim %s' % refname, count=count,
-                                                  filtered_count=filt))
-        seed_counts = self.select_seeds(groups)
-        conseqs, map_counts = self.prelim_conseqs(seed_counts)
+            remap_counts_writer.writerows(dict(type='prelim %s' % name, count=count,
+                                               filtered_count=filt)
+                                          for name, count, filt in groups)
+        conseqs, map_counts = self.prelim_conseqs(self.select_seeds(groups))
+        return self.iterate(conseqs, map_counts, raw_count, max_iterations=max_iterations,
+                            min_iterations=min_iterations, remap_counts_writer=remap_counts_writer)
+
+    @staticmethod
+    def converged(old_names, new_names, new_counts, map_counts, raw_count, n_remaps):
+        """The stopping rules of remap.py:591-603.  They apply only while the
+        set of consensus names is stable; then any one of them ends the loop:
+        no reference mapped more lines than on the pass before, more than
+        MIN_MAPPING_EFFICIENCY of raw_count mapped, or MAX_REMAPS passes."""
+        if new_names != old_names:
+            return False
+        if all(n <= map_counts[name] for name, n in new_counts.items()):
+            return True
+        if sum(new_counts.values()) / float(raw_count) > MIN_MAPPING_EFFICIENCY:
+            return True
+        return n_remaps >= MAX_REMAPS
+
+    def iterate(self, conseqs, map_counts, raw_count, max_iterations=None, min_iterations=None,
+                remap_counts_writer=None, before_pass=None, after_pass=None):
+        """remap()'s loop (remap.py:544-606) from the seed-group winners and
+        their prelim counts: map with --local against the current consensus
+        set, rebuild and filter the consensus, stop by converged().  Both the
+        device pipeline (run) and the file-level drop-in (remap.remap) use
+        this one loop.
+
+        before_pass() / after_pass() hook the file outputs around each
+        mapping pass (the unmapped FASTQs).  max_iterations caps the passes
+        and min_iterations (BASELINE C3's "3 remap iterations") holds the
+        stopping rules off; both are for benchmark configs only and are None
+        for the reference's behaviour.
+        Returns (consensus set after the last pass, its per-reference
+        mapped-line counts, unmapped lines)."""
+        self.raw_count = raw_count
         n_remaps = 0
         new_counts = Counter()
         unmapped_count = raw_count
+        self.mapped_to = None
         while conseqs:
             if self.callback:
                 self.callback(message='... remap iteration %d' % n_remaps, progress=0)
-            mapped_to = conseqs
+            if before_pass is not None:
+                before_pass()
+            self.mapped_to = mapped_to = conseqs
             new_counts, unmapped_count = self.map_to_reference(conseqs)
-            old_seed_names = set(conseqs.keys())
+            if after_pass is not None:
+                after_pass()
             distance_report = {}
             conseqs = self.build_conseqs_filtered(mapped_to, distance_report)
-            new_seed_names = set(conseqs.keys())
             n_remaps += 1
             self.log.append(dict(iteration=n_remaps, mapped=dict(new_counts),
                                  conseqs={k: len(v) for k, v in conseqs.items()}))
@@ -276,17 +309,10 @@ class RemapPipeline:
                                    distance_report)
             if max_iterations is not None and n_remaps >= max_iterations:
                 break
-            if min_iterations is not None and n_remaps < min_iterations:
-                map_counts = dict(new_counts)
-                continue
-            if new_seed_names == old_seed_names:
-                if all((count <= map_counts[refname]) for refname, count in new_counts.items()):
-                    break
-                mapping_efficiency = sum(new_counts.values()) / float(raw_count)
-                if mapping_efficiency > MIN_MAPPING_EFFICIENCY:
-                    break
-                if n_remaps >= MAX_REMAPS:
-                    break
+            forced = min_iterations is not None and n_remaps < min_iterations
+            if not forced and self.converged(set(mapped_to), set(conseqs), new_counts,
+                                             map_counts, raw_count, n_remaps):
+                break
             map_counts = dict(new_counts)
         self.conseqs = conseqs
         self.new_counts = new_counts

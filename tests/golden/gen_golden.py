@@ -16,6 +16,8 @@ itself produced for them.  Sections:
            SAMs produced by the oracle mapper on synthetic reads.
   sam2aln  every apply_cigar / merge_pairs / merge_inserts call made by
            micall/tests/sam2aln_test.py.
+  splitter every MixedReferenceSplitter.split() call of remap_test.py and
+           seeded random SAM texts: rows kept and split FASTQ texts.
 
   s2a      the reference's sam2aln() (the next stage) on
            every call micall/tests/sam2aln_test.py makes, on edge-case
@@ -251,6 +253,87 @@ def gen_sam2aln():
     with open(os.path.join(HERE, 'sam2aln_golden.json'), 'w') as f:
         json.dump(out, f, indent=0)
     print('sam2aln: {} calls'.format(len(records)))
+
+
+def gen_splitter():
+    """Every MixedReferenceSplitter.split() call of the reference's
+    MixedReferenceSplitterTest (remap_test.py:594-716), plus seeded random
+    SAM texts (string-compared MAPQs such as '8' vs '44', tied MAPQ, equal
+    AS, unmapped flags, lone mates): input text, the rows split() yields and
+    the split FASTQ text per reference."""
+    refharness.setup()
+    from micall.core import remap as R
+    records = []
+
+    class Memory(R.MixedReferenceSplitter):
+        def create_split_file(self, refname, direction):
+            return io.StringIO()
+
+        def close_split_file(self, split_file):
+            pass
+
+    real_split = R.MixedReferenceSplitter.split
+
+    def record(text, source):
+        sp = Memory()
+        try:
+            rows = list(real_split(sp, io.StringIO(text)))
+            rec = dict(source=source, sam=text, rows=rows,
+                       splits=[[k, f1.getvalue(), f2.getvalue()] for k, (f1, f2) in sp.splits.items()])
+        except Exception as ex:      # e.g. a tied MAPQ with no AS:i tag
+            rec = dict(source=source, sam=text, raises=type(ex).__name__)
+        records.append(rec)
+
+    def recorder(self, sam_lines):
+        text = sam_lines.getvalue() if hasattr(sam_lines, 'getvalue') else ''.join(sam_lines)
+        record(text, 'remap_test.py MixedReferenceSplitterTest')
+        return real_split(self, io.StringIO(text))
+    R.MixedReferenceSplitter.split = recorder
+    import micall.tests.remap_test as rt
+    suite = unittest.defaultTestLoader.loadTestsFromTestCase(rt.MixedReferenceSplitterTest)
+    unittest.TextTestRunner(stream=io.StringIO(), verbosity=0).run(suite)
+    R.MixedReferenceSplitter.split = real_split
+    n_tests = len(records)
+    rng = random.Random(4242)
+    refs = ['HIV1B-gag-seed', 'HIV1B-pol-seed', 'HIV1B-env-seed']
+    for t in range(40):
+        lines = ['@HD\tVN:1.0\tSO:unsorted\n'] + ['@SQ\tSN:%s\tLN:9000\n' % r for r in refs]
+        for q in range(rng.randint(1, 30)):
+            qname = 'M01:%d:%d' % (t, q)
+            seqs = [''.join(rng.choice('ACGTN') for _ in range(rng.randint(1, 12))) for _ in (0, 1)]
+            quals = [''.join(rng.choice('#5<AFGJ') for _ in s) for s in seqs]
+            r1, r2 = rng.choice(refs), rng.choice(refs)
+            kind = rng.random()
+            f1, f2 = 0x1 | 0x40, 0x1 | 0x80
+            if kind < 0.15:
+                f1 |= 0x4
+                f2 |= 0x8
+            elif kind < 0.25:
+                f2 |= 0x4
+                f1 |= 0x8
+            mapqs = [rng.choice(['0', '1', '8', '11', '23', '42', '44', '255']) for _ in (0, 1)]
+            if rng.random() < 0.3:
+                mapqs[1] = mapqs[0]
+            scores = [rng.choice([-20, 0, 15, 100, 200]) for _ in (0, 1)]
+            if rng.random() < 0.3:
+                scores[1] = scores[0]
+            rn = [r2 if r1 != r2 else '=', r1 if r1 != r2 else '=']
+            mates = []
+            for k, (flag, ref, nxt) in enumerate(((f1, r1, rn[0]), (f2, r2, rn[1]))):
+                tags = ['AS:i:%d' % scores[k]] if t % 4 != 3 or rng.random() > 0.05 else ['YT:Z:DP']
+                mates.append('\t'.join([qname, str(flag), ref, str(rng.randint(1, 900)), mapqs[k],
+                                         '%dM' % len(seqs[k]), nxt, '1', '0', seqs[k], quals[k]]
+                                        + tags) + '\n')
+            if rng.random() < 0.5:
+                mates.reverse()
+            if rng.random() < 0.05:
+                mates = mates[:1]          # lone mate
+            lines += mates
+        record(''.join(lines), 'seeded random')
+    with open(os.path.join(HERE, 'splitter_golden.json'), 'w') as f:
+        json.dump(dict(source='reference remap.MixedReferenceSplitter.split', n_tests=n_tests,
+                       cases=records), f, indent=0)
+    print('splitter: {} cases ({} from remap_test)'.format(len(records), n_tests))
 
 
 E2E_MICROTESTS = ['1234A-V3LOOP_S1', '2020A-GP41_S4', '2040A-HLA-B_S6', '2070A-PR_S9',
