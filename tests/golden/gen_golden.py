@@ -51,6 +51,7 @@ itself produced for them.  Sections:
 
 usage: python tests/golden/gen_golden.py [gotoh] [pileup] [sam2aln] [e2e]
 """
+import gzip
 import io
 import json
 import os
@@ -336,19 +337,65 @@ def gen_splitter():
     print('splitter: {} cases ({} from remap_test)'.format(len(records), n_tests))
 
 
-E2E_MICROTESTS = ['1234A-V3LOOP_S1', '2020A-GP41_S4', '2040A-HLA-B_S6', '2070A-PR_S9',
+E2E_MICROTESTS = ['1234A-V3LOOP_S1', '2000A-V3LOOP_S2', '2010A-V3LOOP_S3', '2020A-GP41_S4',
+                  '2030A-V3LOOP_S5', '2040A-HLA-B_S6', '2050A-V3LOOP_S7', '2060A-V3LOOP_S8',
+                  '2070A-PR_S9', '2080A-V3LOOP_S10', '2090A-HCV_S11',
                   '2100A-HCV-1337B-V3LOOP_S12']
+# BASELINE config C1: the reference's own example input (9,600 pairs of
+# simulated HIV-1 subtype C pol reads named CONSENSUS_C-N/1, /2)
+EXAMPLE = ('c1_example', 'examples/HIV1C-pol_S1_L001_R{}_001.fastq.gz')
+
+
+def _gz_write(path, data):
+    """gzip with a fixed header (mtime 0), so regenerating unchanged data
+    leaves the committed bytes unchanged."""
+    if isinstance(data, str):
+        data = data.encode()
+    with open(path, 'wb') as raw, gzip.GzipFile(fileobj=raw, mode='wb', mtime=0) as f:
+        f.write(data)
+
+
+def _garbage(pairs, n, seed):
+    """Replace the first n pairs by random sequence (reads that map nowhere)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    for key in ('r1', 'r2'):
+        if pairs[key] is not None:
+            pairs[key][:n] = np.frombuffer(b'ACGT', dtype=np.uint8)[
+                rng.integers(0, 4, size=pairs[key][:n].shape)]
+    return pairs
+
+
+def _chimeric(seeds):
+    """Pairs from HIV-1 gag and env sample genomes; 60 pairs of each have
+    their R2 swapped with the other's, so their mates map to two seeds and
+    the final remap pass hands them to MixedReferenceSplitter (RNEXT names
+    the other reference, remap.py:787-850)."""
+    import numpy as np
+    from micall_amd import synth
+    gag = synth.make_pairs(500, genomes={'HIV1B-gag-seed': seeds['HIV1B-gag-seed']},
+                           genome_seed=111, read_seed=112, sub_rate=0.06)
+    env = synth.make_pairs(500, genomes={'HIV1B-env-seed': seeds['HIV1B-env-seed']},
+                           genome_seed=113, read_seed=114, sub_rate=0.06)
+    out = {'block': 0, 'n': 1000}
+    for key in ('r1', 'q1', 'r2', 'q2'):
+        out[key] = np.concatenate([gag[key], env[key]])
+    for key in ('r2', 'q2'):
+        a = out[key][:60].copy()
+        out[key][:60] = out[key][500:560]
+        out[key][500:560] = a
+    return out
 
 
 def _e2e_cases():
-    """(name, R1 writer, R2 writer or None) for every end-to-end case."""
+    """(name, synthetic pairs) for every synthetic end-to-end case."""
     from micall_amd import projects, synth
     seeds = projects.load_default().seed_sequences()
+    pol = {'HIV1B-pol-seed': seeds['HIV1B-pol-seed']}
     cases = []
 
     def syn(name, n, genomes, **kw):
-        pairs = synth.make_pairs(n, genomes={g: seeds[g] for g in genomes}, **kw)
-        cases.append((name, pairs))
+        cases.append((name, synth.make_pairs(n, genomes={g: seeds[g] for g in genomes}, **kw)))
 
     syn('syn_pol', 1500, ['HIV1B-pol-seed'], genome_seed=101, read_seed=102)
     syn('syn_pol_indel', 600, ['HIV1B-pol-seed'], genome_seed=103, read_seed=104, indel_rate=0.01)
@@ -356,18 +403,79 @@ def _e2e_cases():
         genome_seed=105, read_seed=106)
     syn('syn_unpaired300', 500, ['HIV1B-pol-seed'], genome_seed=107, read_seed=108, read_len=300,
         paired=False)
+    cases.append(('syn_chimera', _chimeric(seeds)))
+    # 14 % divergence: every pass maps more reads than the one before, and
+    # 10 % random pairs keep the mapped fraction below 0.95, so only
+    # MAX_REMAPS (remap.py:602-603) ends the loop, after the third pass
+    cases.append(('syn_maxremaps', _garbage(synth.make_pairs(1500, genomes=pol, genome_seed=201,
+                                                             read_seed=202, sub_rate=0.14),
+                                            150, 5)))
+    # 18 % divergence: no seed reaches the count threshold, the loop never
+    # runs (the reference then fails removing temp.fasta, remap.py:653-655)
+    cases.append(('syn_noseed', _garbage(synth.make_pairs(1500, genomes=pol, genome_seed=201,
+                                                          read_seed=202, sub_rate=0.18),
+                                         150, 5)))
     return cases
 
 
-def gen_e2e():
-    import gzip
+def _fastq_text(pairs, mate):
+    from micall_amd import synth
+    r, q = pairs['r%d' % mate], pairs['q%d' % mate]
+    return ''.join('{}\n{}\n+\n{}\n'.format(synth.read_name(pairs['block'], i, mate),
+                                             r[i].tobytes().decode(), q[i].tobytes().decode())
+                   for i in range(pairs['n']))
+
+
+def _reference_e2e(r1, r2, keep):
+    """Stock prelim_map() + remap() in a scratch directory; returns
+    ({file name: text}, exception raised by remap or None)."""
     import shutil
     import tempfile
-    refharness.setup()
     from micall.core.prelim_map import prelim_map
     from micall.core.remap import remap
-    from micall_amd import synth
     shim = os.path.join(REPO, 'oracle', 'shim_bin')
+    work = tempfile.mkdtemp(prefix='e2e_')
+    cwd = os.getcwd()
+    os.chdir(work)   # the reference writes split FASTQs into the cwd
+    raised = None
+    try:
+        prelim = os.path.join(work, 'prelim.csv')
+        with open(prelim, 'w') as handle:
+            prelim_map(r1, r2, handle, bt2_path=os.path.join(shim, 'bowtie2'),
+                       bt2build_path=os.path.join(shim, 'bowtie2-build-s'), nthreads=1,
+                       gzip=True, work_path=work)
+        names = ('remap.csv', 'remap_counts.csv', 'remap_conseq.csv', 'unmapped1.fastq',
+                 'unmapped2.fastq')
+        outs = {k: open(os.path.join(work, k), 'w') for k in names}
+        try:
+            with open(prelim) as pre:
+                remap(r1, r2, pre, outs['remap.csv'], outs['remap_counts.csv'],
+                      outs['remap_conseq.csv'], outs['unmapped1.fastq'], outs['unmapped2.fastq'],
+                      work_path=work, bt2_path=os.path.join(shim, 'bowtie2'),
+                      bt2build_path=os.path.join(shim, 'bowtie2-build-s'), nthreads=1, gzip=True,
+                      keep=keep)
+        except Exception as ex:    # recorded, see remap.py:653-655
+            name = getattr(ex, 'filename', None)
+            raised = '{} {}'.format(type(ex).__name__, os.path.basename(name) if name else ex)
+        for f in outs.values():
+            f.close()
+        texts = {}
+        for k in ('prelim.csv',) + names:
+            with open(os.path.join(work, k)) as f:
+                texts[k] = f.read()
+        return texts, raised
+    finally:
+        os.chdir(cwd)
+        shutil.rmtree(work, ignore_errors=True)
+
+
+def gen_e2e(only=None):
+    """The stock reference pipeline on every e2e input.  Outputs are taken
+    from a run with keep=True (the reference completes); when the remap loop
+    never ran, the same input is run again with keep=False and the exception
+    the reference raises is recorded in reference_raises.txt."""
+    import shutil
+    refharness.setup()
     out_root = os.path.join(HERE, 'e2e')
     os.makedirs(out_root, exist_ok=True)
     inputs = []
@@ -376,51 +484,49 @@ def gen_e2e():
         os.makedirs(d, exist_ok=True)
         r1 = os.path.join(d, 'R1.fastq.gz')
         r2 = os.path.join(d, 'R2.fastq.gz') if pairs['r2'] is not None else None
-        synth.write_fastq(pairs, r1, r2)
+        for mate, path in ((1, r1), (2, r2)):
+            if path is not None:
+                _gz_write(path, _fastq_text(pairs, mate))
         inputs.append((name, r1, r2))
     micro = os.path.join(refharness.REF, 'micall', 'tests', 'microtest')
     for stem in E2E_MICROTESTS:
-        d = os.path.join(out_root, 'micro_' + stem.split('_')[0])
+        name = 'micro_' + stem.split('_')[0]
+        d = os.path.join(out_root, name)
         os.makedirs(d, exist_ok=True)
         paths = []
         for mate in ('R1', 'R2'):
             src = os.path.join(micro, '{}_L001_{}_001.fastq'.format(stem, mate))
             dst = os.path.join(d, mate + '.fastq.gz')
-            with open(src, 'rb') as fi, gzip.open(dst, 'wb') as fo:
-                shutil.copyfileobj(fi, fo)
+            with open(src, 'rb') as fi:
+                _gz_write(dst, fi.read())
             paths.append(dst)
-        inputs.append(('micro_' + stem.split('_')[0], paths[0], paths[1]))
+        inputs.append((name, paths[0], paths[1]))
+    name, pattern = EXAMPLE
+    d = os.path.join(out_root, name)
+    os.makedirs(d, exist_ok=True)
+    paths = []
+    for mate in (1, 2):
+        dst = os.path.join(d, 'R{}.fastq.gz'.format(mate))
+        shutil.copyfile(os.path.join(refharness.REF, pattern.format(mate)), dst)
+        paths.append(dst)
+    inputs.append((name, paths[0], paths[1]))
     for name, r1, r2 in inputs:
+        if only and name not in only:
+            continue
         d = os.path.join(out_root, name)
-        work = tempfile.mkdtemp(prefix='e2e_')
-        cwd = os.getcwd()
-        os.chdir(work)   # the reference writes split FASTQs into the cwd
-        try:
-            prelim = os.path.join(work, 'prelim.csv')
-            with open(prelim, 'w') as handle:
-                prelim_map(r1, r2, handle, bt2_path=os.path.join(shim, 'bowtie2'),
-                           bt2build_path=os.path.join(shim, 'bowtie2-build-s'), nthreads=1,
-                           gzip=True, work_path=work)
-            outs = {k: open(os.path.join(work, k), 'w') for k in
-                    ('remap.csv', 'remap_counts.csv', 'remap_conseq.csv', 'unmapped1.fastq',
-                     'unmapped2.fastq')}
-            with open(prelim) as pre:
-                remap(r1, r2, pre, outs['remap.csv'], outs['remap_counts.csv'],
-                      outs['remap_conseq.csv'], outs['unmapped1.fastq'], outs['unmapped2.fastq'],
-                      work_path=work, bt2_path=os.path.join(shim, 'bowtie2'),
-                      bt2build_path=os.path.join(shim, 'bowtie2-build-s'), nthreads=1, gzip=True,
-                      keep=True)
-            for f in outs.values():
-                f.close()
-            for k in ('prelim.csv', 'remap.csv', 'remap_counts.csv', 'remap_conseq.csv',
-                      'unmapped1.fastq', 'unmapped2.fastq'):
-                with open(os.path.join(work, k), 'rb') as fi, \
-                        gzip.open(os.path.join(d, k + '.gz'), 'wb') as fo:
-                    shutil.copyfileobj(fi, fo)
-        finally:
-            os.chdir(cwd)
-            shutil.rmtree(work, ignore_errors=True)
-        print('e2e:', name)
+        texts, raised = _reference_e2e(r1, r2, keep=True)
+        assert raised is None, (name, raised)
+        for k, text in texts.items():
+            _gz_write(os.path.join(d, k + '.gz'), text)
+        marker = os.path.join(d, 'reference_raises.txt')
+        if os.path.exists(marker):
+            os.remove(marker)
+        if 'remap-1 ' not in texts['remap_counts.csv']:
+            _, raised = _reference_e2e(r1, r2, keep=False)
+            if raised:
+                with open(marker, 'w') as f:
+                    f.write(raised + '\n')
+        print('e2e:', name, '' if raised is None else '(reference raises without keep)')
 
 
 def _s2a_edge_texts():
@@ -635,8 +741,7 @@ def gen_s2a():
         with gzip.open(os.path.join(d, 'remap.csv.gz'), 'rt') as f:
             text = f.read()
         for name, body in zip(('aligned.csv', 'insert.csv', 'failed.csv'), run(text)):
-            with gzip.open(os.path.join(d, name + '.gz'), 'wt') as f:
-                f.write(body)
+            _gz_write(os.path.join(d, name + '.gz'), body)
     print('s2a: {} calls ({} from sam2aln_test)'.format(len(records), n_tests))
 
 A2C_OUTPUTS = ('nuc', 'amino', 'coord_ins', 'conseq', 'failed', 'coverage')
@@ -883,8 +988,7 @@ def gen_a2c():
         with gzip.open(os.path.join(d, 'aligned.csv.gz'), 'rt') as f:
             text = f.read()
         for k, body in _a2c_reference(A, text).items():
-            with gzip.open(os.path.join(d, 'a2c_{}.csv.gz'.format(k)), 'wt') as f:
-                f.write(body)
+            _gz_write(os.path.join(d, 'a2c_{}.csv.gz'.format(k)), body)
         print('a2c e2e:', case)
 
     # edge cases over a small project file
@@ -906,6 +1010,7 @@ def gen_a2c():
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['gotoh', 'pileup', 'sam2aln', 'e2e', 's2a', 'censor']
+    which = sys.argv[1:] or ['gotoh', 'pileup', 'sam2aln', 'splitter', 'e2e', 's2a', 'censor',
+                             'a2c']
     for w in which:
         globals()['gen_' + w]()
