@@ -122,10 +122,11 @@ int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mappe
                   int64_t *first_row, int64_t *first_mapped, int64_t *unmapped,
                   int64_t *star_lines, int64_t *star_first);
 /* Work done by the last mh_map: out[0] reads, out[1] banded extensions
- * (candidates aligned by the DP, 64 diagonals x read length cells each),
- * out[2] CIGAR pool words reserved (per-wave chunks), out[3] extensions
- * resolved by the ungapped fast path (no DP). */
-int mh_map_stats(mh_ctx *ctx, int64_t *out4);
+ * (candidates aligned by the DP, 64 diagonals x read length cells each,
+ * mate rescues included), out[2] CIGAR pool words reserved (per-wave
+ * chunks), out[3] extensions resolved by the ungapped fast path (no DP),
+ * out[4] mate-rescue extensions. */
+int mh_map_stats(mh_ctx *ctx, int64_t *out5);
 /* The 20 int32 header fields of mh_aln (no CIGAR) for reads [first, first+n). */
 int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20);
 /* SAM text for reads order[first .. first+n) (order NULL: reads first ..

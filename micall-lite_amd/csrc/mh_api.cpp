@@ -517,7 +517,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     for (auto &ix : c->cache) free_index(ix);   // c->index only views one of these
     free_index(c->small);
     MapState &M = c->map;
-    hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work); hipFree(M.slot);
+    hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work); hipFree(M.rwork); hipFree(M.slot);
     hipFree(M.pool); hipFree(M.rec); hipFree(M.counters); hipFree(M.ref_stats);
     RowState &R = c->rows;
     hipFree(R.flag); hipFree(R.ref); hipFree(R.pos); hipFree(R.cig_off); hipFree(R.n_cigar);
@@ -776,9 +776,10 @@ int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mappe
     return 0;
 }
 
-int mh_map_stats(mh_ctx *ctx, int64_t *out4)
+int mh_map_stats(mh_ctx *ctx, int64_t *out5)
 {
-    if (!ctx || !out4) return -3;
+    if (!ctx || !out5) return -3;
+    int64_t *out4 = out5;
     CtxEx *c = X(ctx);
     MapState &M = c->map;
     if (!M.valid) { set_error("no mapping results (call mh_map)"); return -3; }
@@ -786,6 +787,7 @@ int mh_map_stats(mh_ctx *ctx, int64_t *out4)
     out4[1] = M.last_work;
     out4[2] = M.last_cigar;
     out4[3] = M.last_fast;
+    out5[4] = M.last_rescue;
     return 0;
 }
 

@@ -99,17 +99,19 @@ struct MapState {
     int32_t *n_cand = nullptr;   // n_reads
     int32_t *yf = nullptr;       // n_reads
     int32_t *work = nullptr;     // slot ids to extend
+    int32_t *rwork = nullptr;    // slot ids of mate-rescue candidates (one per pair at most)
     Slot *slot = nullptr;        // n_reads * MAXCAND
     uint32_t *pool = nullptr;    // CIGAR ops of all slots
     int64_t pool_cap = 0;
     Rec *rec = nullptr;          // n_reads
-    int32_t *counters = nullptr; // [work_n, pool_used, pool_overflow, pad]
+    int32_t *counters = nullptr; // [work_n, pool_used, pool_overflow, fast, rescue_n, pad..]
     int64_t *ref_stats = nullptr;// per ref: lines, filtered, mapped, first_row, first_mapped; + unmapped, star
     int64_t cap_reads = 0;
     int cap_refs = 0;
     int64_t last_work = 0;       // extensions (k_dp work items) of the last pass
     int64_t last_cigar = 0;      // CIGAR ops written by the last pass
     int64_t last_fast = 0;       // extensions resolved by the ungapped fast path
+    int64_t last_rescue = 0;     // mate-rescue extensions
     bool valid = false;
 };
 

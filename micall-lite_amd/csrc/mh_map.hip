@@ -11,6 +11,9 @@
 //                 diagonal center-32+k, rows = read bases; vertical moves by a
 //                 DPP wave shift, horizontal gaps by a DPP prefix-max scan;
 //                 4 traceback bits per cell in LDS; lane-0 traceback -> CIGAR
+//   k_rescue      paired reads with one aligned mate: the other mate's best
+//                 diagonal in the -X window next to it (mate rescue), then
+//                 k_dp again over those candidates
 //   k_pair        one thread per pair: concordance, flags, MAPQ, SAM fields,
 //                 per-reference line tallies
 #include "mh_internal.h"
@@ -1074,6 +1077,143 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
 }
 
 // ---------------------------------------------------------------------------
+// k_rescue: mate rescue (og_mapper.c rescue_pair / rescue_diagonal).  When
+// exactly one mate of a pair aligned, the other is looked for in the -X
+// window next to the aligned mate, on the opposite strand: the diagonal with
+// the most base matches over the window (ties: leftmost) becomes the mate's
+// only candidate and k_dp extends it like any other.  One wave per 64 pairs:
+// lane = pair for the test, then the whole wave scans each selected mate's
+// window, lane = diagonal, 4 read bases per LDS word.
+// ---------------------------------------------------------------------------
+struct RescueArgs {
+    DevReads R;
+    DevIndex I;
+    const Slot *slot;
+    int32_t *n_cand;
+    const int32_t *yf;
+    Cand *cand;
+    int32_t *work;        // rescue work list (slot ids)
+    int32_t *counter;     // [0] rescue work items
+    int maxins;
+};
+
+constexpr int RESCUE_CHUNK = 256;   // diagonals per staged reference window
+
+__device__ __forceinline__ int best_slot(const Slot *sl, int n)
+{
+    int best = -1, bs = 0;
+    for (int c = 0; c < n; ++c) {
+        const int v = sl[c].valid, sc = sl[c].score;
+        if (v && (best < 0 || sc > bs)) { best = c; bs = sc; }
+    }
+    return best;
+}
+
+__global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t sh_read[4][MAXLEN + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t sh_ref[4][RESCUE_CHUNK + MAXLEN + 16];
+    __shared__ int32_t sh_items[4][64];
+    const int lane = threadIdx.x & 63;
+    const int wv = wave_uniform(threadIdx.x >> 6);
+    uint8_t *rd = sh_read[wv];
+    uint8_t *rf = sh_ref[wv];
+    const int64_t units = A.R.n / 2;
+    for (int64_t u0 = ((int64_t)blockIdx.x * 4 + wv) * 64; u0 < units;
+         u0 += (int64_t)gridDim.x * 256) {
+        const int64_t u = u0 + lane;
+        // the mate to rescue and its anchor (the other mate's best slot)
+        int need = 0, tgt_mate = 0, a_ref = 0, a_strand = 0, a_pos = 0, a_end = 0;
+        if (u < units) {
+            const int64_t r1 = 2 * u, r2 = r1 + 1;
+            const int b1 = best_slot(A.slot + r1 * MAXCAND, A.n_cand[r1]);
+            const int b2 = best_slot(A.slot + r2 * MAXCAND, A.n_cand[r2]);
+            if ((b1 >= 0) != (b2 >= 0)) {
+                const int64_t an = b1 >= 0 ? r1 : r2, tg = b1 >= 0 ? r2 : r1;
+                if (A.yf[tg] == 0 && A.R.len[tg] > 0) {
+                    const Slot s = A.slot[an * MAXCAND + (b1 >= 0 ? b1 : b2)];
+                    need = 1;
+                    tgt_mate = b1 >= 0 ? 1 : 0;
+                    a_ref = s.ref; a_strand = s.strand; a_pos = s.pos; a_end = s.end;
+                }
+            }
+        }
+        uint64_t todo = __builtin_amdgcn_ballot_w64(need != 0);
+        int n_items = 0;
+        while (todo) {
+            const int l = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int64_t tg = 2 * (u0 + l) + __builtin_amdgcn_readlane(tgt_mate, l);
+            const int ref = __builtin_amdgcn_readlane(a_ref, l);
+            const int ast = __builtin_amdgcn_readlane(a_strand, l);
+            const int apos = __builtin_amdgcn_readlane(a_pos, l);
+            const int aend = __builtin_amdgcn_readlane(a_end, l);
+            const int m = wave_uniform(A.R.len[tg]);
+            const int64_t off = A.R.off[tg];
+            const int reflen = wave_uniform(A.I.ref_len[ref]);
+            const int64_t gref = A.I.ref_off[ref];
+            int64_t lo = ast == 0 ? (int64_t)apos : (int64_t)aend - A.maxins;
+            int64_t hi = ast == 0 ? (int64_t)apos + A.maxins : (int64_t)aend;
+            if (lo < 0) lo = 0;
+            if (hi > reflen) hi = reflen;
+            if (hi - lo < m) continue;
+            const int s = 1 - ast;
+            // the mate's codes on strand s, 4 (never matches) past its end
+            for (int i = lane; i < m + 16; i += 64) {
+                uint32_t c = 4;
+                if (i < m) {
+                    c = read_code(A.R, off, s ? m - 1 - i : i);
+                    if (s && c < 4) c = 3 - c;
+                }
+                rd[i] = (uint8_t)c;
+            }
+            int bestM = -1, bestd = 0;
+            const int dlast = (int)(hi - m);
+            for (int d0 = (int)lo; d0 <= dlast; d0 += RESCUE_CHUNK) {
+                const int nd = dlast - d0 + 1 < RESCUE_CHUNK ? dlast - d0 + 1 : RESCUE_CHUNK;
+                for (int x = lane; x < nd + m + 8; x += 64) {
+                    const int j = d0 + x;
+                    rf[x] = j < hi ? A.I.codes[gref + j] : (uint8_t)7;
+                }
+                wave_sync();
+                for (int t = lane; t < nd; t += 64) {
+                    int cnt = 0;
+                    for (int i = 0; i < m; i += 4) {
+                        const uint32_t rw = *(const uint32_t *)(rd + i);
+                        const int b = t + i;
+                        const uint32_t w0 = *(const uint32_t *)(rf + (b & ~3));
+                        const uint32_t w1 = *(const uint32_t *)(rf + (b & ~3) + 4);
+                        const uint32_t rv = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(b & 3));
+                        const uint32_t x = rw ^ rv;
+                        // byte matches: equal codes (values < 8), read base not N
+                        const uint32_t eq = ~(x | (x >> 1) | (x >> 2) | (rw >> 2)) & 0x01010101u;
+                        cnt += __builtin_popcount(eq);
+                    }
+                    if (cnt > bestM) { bestM = cnt; bestd = d0 + t; }
+                }
+                wave_sync();
+            }
+            const int mmax = wave_max(bestM);
+            const int dsel = wave_min(bestM == mmax ? bestd : INT32_MAX);
+            if (lane == 0) {
+                A.cand[tg * MAXCAND] = Cand{s, ref, dsel, 0};
+                A.n_cand[tg] = 1;
+                sh_items[wv][n_items] = (int32_t)(tg * MAXCAND);
+            }
+            ++n_items;
+        }
+        wave_sync();
+        if (n_items) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(A.counter, n_items);
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (lane < n_items) A.work[base + lane] = sh_items[wv][lane];
+        }
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_pair: pairing, flags, MAPQ (unpinned V2-style table, see og_mapq)
 // ---------------------------------------------------------------------------
 __device__ int mapq_v2(int local, int perfect, int minsc, int best, int has_sec, int sec)
@@ -1376,17 +1516,18 @@ static int ensure_map_buffers(Ctx &c)
     const int64_t n = c.reads.n;
     if (M.cap_reads < n || M.cand == nullptr) {
         hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work);
-        hipFree(M.slot); hipFree(M.rec);
+        hipFree(M.rwork); hipFree(M.slot); hipFree(M.rec);
         const int64_t cap = n > 0 ? n : 1;
         MH_HIP(hipMalloc(&M.cand, sizeof(Cand) * cap * MAXCAND));
         MH_HIP(hipMalloc(&M.n_cand, sizeof(int32_t) * cap));
         MH_HIP(hipMalloc(&M.yf, sizeof(int32_t) * cap));
         MH_HIP(hipMalloc(&M.work, sizeof(int32_t) * cap * MAXCAND));
+        MH_HIP(hipMalloc(&M.rwork, sizeof(int32_t) * (cap / 2 + 1)));
         MH_HIP(hipMalloc(&M.slot, sizeof(Slot) * cap * MAXCAND));
         MH_HIP(hipMalloc(&M.rec, sizeof(Rec) * cap));
         M.cap_reads = cap;
     }
-    if (M.counters == nullptr) MH_HIP(hipMalloc(&M.counters, sizeof(int32_t) * 4));
+    if (M.counters == nullptr) MH_HIP(hipMalloc(&M.counters, sizeof(int32_t) * 8));
     if (M.cap_refs < c.index.n_refs || M.ref_stats == nullptr) {
         hipFree(M.ref_stats);
         const int cr = c.index.n_refs > 0 ? c.index.n_refs : 1;
@@ -1452,20 +1593,21 @@ int run_map(Ctx &c, const mh_params &par)
         // bits 32/row, tab|runs 4 * max(rows, RUNS_CAP), refw rows + 64, rdc, rowk
         const int wave_lds =
             ((rows_pad * 35 + 4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP) + 64) + 15) & ~15;
-        for (int attempt = 0; attempt < 2; ++attempt) {
-            MH_HIP(hipMemsetAsync(M.counters + 1, 0, sizeof(int32_t) * 3, s));
-            DpArgs da{c.reads, c.index, c.len_tab, M.cand, M.work, M.counters, M.slot, M.pool,
+        // one wave per workgroup: the CU then packs floor(160 KiB / wave_lds)
+        // waves (15 at 251-nt reads) with no workgroup rounding loss
+        int wpb = DP_WAVES_PER_BLOCK;
+        while (wpb > 1 && wpb * wave_lds > 160 * 1024) --wpb;
+        if (wave_lds > 160 * 1024) { set_error("mh_map: reads too long for LDS"); return -3; }
+        auto launch_dp = [&](const int32_t *work, const int32_t *count, int64_t max_items,
+                             const char *name) -> int {
+            DpArgs da{c.reads, c.index, c.len_tab, M.cand, work, count, M.slot, M.pool,
                       M.counters + 1, M.pool_cap, rows_pad, wave_lds,
                       par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext,
                       par.rdg_ext};
-            // one wave per workgroup: the CU then packs floor(160 KiB / wave_lds)
-            // waves (15 at 251-nt reads) with no workgroup rounding loss
-            int wpb = DP_WAVES_PER_BLOCK;
-            while (wpb > 1 && wpb * wave_lds > 160 * 1024) --wpb;
-            if (wave_lds > 160 * 1024) { set_error("mh_map: reads too long for LDS"); return -3; }
-            int64_t dblocks = (n * 2 + wpb - 1) / wpb;
+            int64_t dblocks = (max_items + wpb - 1) / wpb;
             if (dblocks > DP_MAX_BLOCKS) dblocks = DP_MAX_BLOCKS;
-            const int pd = prof_begin(c, "k_dp");
+            if (dblocks < 1) dblocks = 1;
+            const int pd = prof_begin(c, name);
             if (par.mode == MH_LOCAL) {
                 MH_HIP(hipFuncSetAttribute((const void *)k_dp<1>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, wpb * wave_lds));
@@ -1477,14 +1619,36 @@ int run_map(Ctx &c, const mh_params &par)
             }
             prof_end(c, pd);
             MH_HIP(hipGetLastError());
-            int32_t ctr[4];
+            return 0;
+        };
+        const int64_t units = c.reads.paired ? n / 2 : n;
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            // counters: [0] work items, [1] pool used, [2] overflow, [3] fast path,
+            // [4] rescue work items
+            MH_HIP(hipMemsetAsync(M.counters + 1, 0, sizeof(int32_t) * 4, s));
+            if (int st = launch_dp(M.work, M.counters, n * 2, "k_dp")) return st;
+            if (c.reads.paired && units > 0) {
+                RescueArgs ra{c.reads, c.index, M.slot, M.n_cand, M.yf, M.cand, M.rwork,
+                              M.counters + 4, par.maxins};
+                int64_t rblocks = (units + 255) / 256;
+                if (rblocks > 4096) rblocks = 4096;
+                const int pr = prof_begin(c, "k_rescue");
+                hipLaunchKernelGGL(k_rescue, dim3((unsigned)rblocks), dim3(256), 0, s, ra);
+                prof_end(c, pr);
+                MH_HIP(hipGetLastError());
+                if (int st = launch_dp(M.rwork, M.counters + 4, units, "k_dp_rescue")) return st;
+            }
+            int32_t ctr[5];
             MH_HIP(hipMemcpyAsync(ctr, M.counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
             MH_HIP(hipStreamSynchronize(s));
-            M.last_work = ctr[0];
+            M.last_work = ctr[0] + ctr[4];
+            M.last_rescue = ctr[4];
             M.last_cigar = ctr[1];
             M.last_fast = ctr[3];
             if (!ctr[2]) break;
             // CIGAR pool overflow: grow to what was asked for and redo the extensions
+            // (the rescue's candidates are the only ones of their mates, so the
+            // second attempt reaches the same result)
             hipFree(M.pool);
             M.pool_cap = (int64_t)ctr[1] * 2 + 4096 + (int64_t)DP_MAX_BLOCKS * 4 * POOL_CHUNK;
             MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * M.pool_cap));
@@ -1492,7 +1656,6 @@ int run_map(Ctx &c, const mh_params &par)
         }
         PairArgs pa{c.reads, c.len_tab, M.slot, M.n_cand, M.yf, M.pool, M.rec, M.ref_stats,
                     M.n_refs, par.mode == MH_LOCAL, par.maxins, c.reads.paired};
-        const int64_t units = c.reads.paired ? n / 2 : n;
         int64_t pblocks = (units + 255) / 256;
         if (pblocks > 1 << 16) pblocks = 1 << 16;
         if (pblocks < 1) pblocks = 1;

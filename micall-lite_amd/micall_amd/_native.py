@@ -413,9 +413,9 @@ class Context:
 
 
     def map_stats(self):
-        """(reads, banded extensions, CIGAR ops, ungapped fast-path extensions)
-        of the last mapping pass."""
-        out = np.zeros(4, dtype=np.int64)
+        """(reads, banded extensions, CIGAR ops, ungapped fast-path extensions,
+        mate-rescue extensions) of the last mapping pass."""
+        out = np.zeros(5, dtype=np.int64)
         check(lib().mh_map_stats(self.h, _ptr(out)), 'mh_map_stats')
         return tuple(int(x) for x in out)
 

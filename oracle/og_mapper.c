@@ -185,8 +185,9 @@ static int cand_before(const cand_t *x, const cand_t *y)
 
 /* Returns the number of candidates written to out (<= OG_MAXCAND). */
 static int find_candidates(const og_index *ix, int mode, const uint8_t *const codes[2], int m,
-                           cand_t *out, hit_t *hits)
+                           cand_t *out, hit_t *hits, int *n_clusters)
 {
+    *n_clusters = 0;
     const int SL = ix->seedlen;
     if (m < SL) return 0;
     const int iv = og_seed_interval(mode, m);
@@ -234,6 +235,7 @@ static int find_candidates(const og_index *ix, int mode, const uint8_t *const co
             a = b;
         }
         cand_t c = { hits[h0].strand, hits[h0].ref, center, h1 - h0 };
+        ++*n_clusters;
         /* insert into the top-K list (sorted by cand_before) */
         int at = nc;
         while (at > 0 && cand_before(&c, &best[at - 1])) --at;
@@ -254,6 +256,7 @@ static int find_candidates(const og_index *ix, int mode, const uint8_t *const co
 /* ------------------------------------------------------------------ */
 typedef struct {
     int valid;
+    int fail;                  /* why not valid: FAIL_* (diagnostics only) */
     int strand, ref, pos, end; /* [pos, end) reference span after trimming */
     int score;
     int xm, xo, xg, nm;
@@ -262,6 +265,8 @@ typedef struct {
 } caln_t;
 
 static inline int imax(int a, int b) { return a > b ? a : b; }
+
+enum { FAIL_NONE = 0, FAIL_SCORE = 1, FAIL_NCEIL = 2, FAIL_OTHER = 3 };
 
 static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *rd,
                       const uint8_t *qv, int m, const cand_t *cd, uint8_t *bits,
@@ -279,6 +284,7 @@ static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *r
     for (int k = 0; k < OG_BAND; ++k) { Hp[k] = 0; Ep[k] = OG_NEG; }
     int best = OG_NEG, bi = -1, bk = -1;
     out->valid = 0;
+    out->fail = FAIL_SCORE;
 
     for (int i = 0; i < m; ++i) {
         const int gap_ok = i >= GBAR && i < m - GBAR;
@@ -323,6 +329,7 @@ static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *r
     if (bi < 0) return;
     if (local && best <= 0) return;
     if (best < og_min_score(par->mode, m)) return;
+    out->fail = FAIL_OTHER;
 
     /* traceback: ops collected back to front */
     int i = bi, k = bk, state = 0, nops = 0;
@@ -367,7 +374,7 @@ static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *r
             } else if (ops[o] == OG_OP_I) ++ri;
             else ++rj;
         }
-        if (nn > og_n_ceil(m)) return;
+        if (nn > og_n_ceil(m)) { out->fail = FAIL_NCEIL; return; }
     }
 
     /* trim columns that hang off either reference end into soft clips */
@@ -411,6 +418,7 @@ static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *r
     if (clipR) out->cigar[nc++] = ((uint32_t)clipR << 4) | OG_OP_S;
     out->n_cigar = nc;
     out->valid = 1;
+    out->fail = FAIL_NONE;
     out->strand = cd->strand;
     out->ref = cd->ref;
     out->pos = jL;
@@ -467,6 +475,8 @@ typedef struct {
     caln_t a[OG_MAXCAND];
     int best;         /* index of best valid alignment, -1 if none */
     int yf;
+    int n_clusters;   /* hit clusters before the top-OG_MAXCAND cut (diagnostics) */
+    int rescued;      /* the alignment came from mate rescue */
 } mate_t;
 
 typedef struct {
@@ -475,13 +485,10 @@ typedef struct {
     uint8_t *bits, *ops;
 } scratch_t;
 
-static void map_mate(const og_index *ix, const og_params *par, const uint8_t *seq,
-                     const uint8_t *qual, int m, scratch_t *sc, mate_t *mt)
+/* 2-bit codes of a read on both strands (strand 1 = reverse complement,
+ * qualities reversed with it); returns the number of ambiguous bases. */
+static int load_codes(const uint8_t *seq, const uint8_t *qual, int m, scratch_t *sc)
 {
-    mt->n = 0;
-    mt->best = -1;
-    mt->yf = OG_YF_NONE;
-    if (m == 0) { mt->yf = OG_YF_LN; return; }
     int nN = 0;
     for (int i = 0; i < m; ++i) {
         const uint8_t c = base_code(seq[i]);
@@ -491,10 +498,22 @@ static void map_mate(const og_index *ix, const og_params *par, const uint8_t *se
         sc->quals[1][m - 1 - i] = qual[i];
         nN += c > 3;
     }
-    if (nN > og_n_ceil(m)) { mt->yf = OG_YF_NS; return; }
+    return nN;
+}
+
+static void map_mate(const og_index *ix, const og_params *par, const uint8_t *seq,
+                     const uint8_t *qual, int m, scratch_t *sc, mate_t *mt)
+{
+    mt->n = 0;
+    mt->best = -1;
+    mt->yf = OG_YF_NONE;
+    mt->n_clusters = 0;
+    mt->rescued = 0;
+    if (m == 0) { mt->yf = OG_YF_LN; return; }
+    if (load_codes(seq, qual, m, sc) > og_n_ceil(m)) { mt->yf = OG_YF_NS; return; }
     cand_t cands[OG_MAXCAND];
     const uint8_t *cc[2] = { sc->codes[0], sc->codes[1] };
-    const int nc = find_candidates(ix, par->mode, cc, m, cands, sc->hits);
+    const int nc = find_candidates(ix, par->mode, cc, m, cands, sc->hits, &mt->n_clusters);
     for (int c = 0; c < nc; ++c) {
         const int s = cands[c].strand;
         dp_extend(ix, par, sc->codes[s], sc->quals[s], m, &cands[c], sc->bits, sc->ops, &mt->a[c]);
@@ -502,6 +521,65 @@ static void map_mate(const og_index *ix, const og_params *par, const uint8_t *se
         if (mt->a[c].valid && (mt->best < 0 || mt->a[c].score > mt->a[mt->best].score)) mt->best = c;
     }
     mt->n = nc;
+}
+
+/* ------------------------------------------------------------------ */
+/* Mate rescue.  When only one mate of a pair aligns, bowtie2 looks for */
+/* the other one in the reference window the fragment-length limit     */
+/* allows next to the aligned mate (the anchor) and aligns it there by  */
+/* dynamic programming (Langmead & Salzberg 2012, paired-end search;    */
+/* bowtie2 2.2.8 SwDriver::extendSeedsPaired, not in this image).  Here */
+/* the window is the -X span on the anchor's side in fr orientation:    */
+/*   anchor forward at [pos, end): the mate lies in [pos, pos + maxins) */
+/*   anchor reverse at [pos, end): the mate lies in [end - maxins, end) */
+/* (clipped to the reference), on the opposite strand.  Its diagonal is */
+/* the one with the most base matches over the window (ties: leftmost), */
+/* and the standard banded DP around it (dp_extend, same scoring, same  */
+/* --score-min and --n-ceil) decides whether the mate aligns.            */
+/* ------------------------------------------------------------------ */
+static int rescue_diagonal(const og_index *ix, const caln_t *anchor, const uint8_t *codes, int m,
+                           int maxins, int *diag)
+{
+    const int L = ix->lens[anchor->ref];
+    long lo = anchor->strand == 0 ? anchor->pos : (long)anchor->end - maxins;
+    long hi = anchor->strand == 0 ? (long)anchor->pos + maxins : anchor->end;
+    if (lo < 0) lo = 0;
+    if (hi > L) hi = L;
+    if (m == 0 || hi - lo < m) return 0;
+    const uint8_t *ref = ix->codes[anchor->ref];
+    int best = -1;
+    for (long d = lo; d + m <= hi; ++d) {
+        int s = 0;
+        for (int i = 0; i < m; ++i) s += codes[i] < 4 && codes[i] == ref[d + i];
+        if (s > best) { best = s; *diag = (int)d; }
+    }
+    return 1;
+}
+
+static void rescue_pair(const og_index *ix, const og_params *par, const uint8_t *seq1,
+                        const uint8_t *qual1, int len1, const uint8_t *seq2, const uint8_t *qual2,
+                        int len2, scratch_t *sc, mate_t *m1, mate_t *m2)
+{
+    if ((m1->best >= 0) == (m2->best >= 0)) return;
+    const mate_t *an = m1->best >= 0 ? m1 : m2;
+    mate_t *tg = m1->best >= 0 ? m2 : m1;
+    const uint8_t *seq = tg == m1 ? seq1 : seq2, *qual = tg == m1 ? qual1 : qual2;
+    const int m = tg == m1 ? len1 : len2;
+    if (tg->yf != OG_YF_NONE || m == 0) return;
+    const caln_t *anchor = &an->a[an->best];
+    load_codes(seq, qual, m, sc);
+    const int s = 1 - anchor->strand;
+    int diag = 0;
+    if (!rescue_diagonal(ix, anchor, sc->codes[s], m, par->maxins, &diag)) return;
+    const cand_t cd = { s, anchor->ref, diag, 0 };
+    caln_t out;
+    dp_extend(ix, par, sc->codes[s], sc->quals[s], m, &cd, sc->bits, sc->ops, &out);
+    out.strand = s;
+    if (!out.valid) return;
+    tg->a[0] = out;
+    tg->n = 1;
+    tg->best = 0;
+    tg->rescued = 1;
 }
 
 static int same_place(const caln_t *x, const caln_t *y)
@@ -631,9 +709,30 @@ static void single_up(const og_params *par, const mate_t *mt, int len, og_aln *o
     }
 }
 
-int og_map(const og_index *ix, const og_params *par, int64_t n_reads, int paired,
-           const uint8_t *seq, const uint8_t *qual, const int64_t *offsets,
-           const int32_t *lens, og_aln *out, int nthreads)
+/* per-read diagnostics (og_map_diag): why a mate did or did not align */
+static void diagnose(const mate_t *mt, int32_t *d)
+{
+    int cause;
+    if (mt->best >= 0) cause = mt->rescued ? OG_CAUSE_RESCUED : OG_CAUSE_ALIGNED;
+    else if (mt->yf != OG_YF_NONE) cause = OG_CAUSE_FILTERED;
+    else if (mt->n == 0) cause = OG_CAUSE_NO_CANDIDATE;
+    else {
+        cause = OG_CAUSE_OTHER;
+        int any_score = 0, any_nceil = 0;
+        for (int c = 0; c < mt->n; ++c) {
+            any_score |= mt->a[c].fail == FAIL_SCORE;
+            any_nceil |= mt->a[c].fail == FAIL_NCEIL;
+        }
+        if (any_nceil) cause = OG_CAUSE_NCEIL;
+        if (any_score) cause = OG_CAUSE_SCORE_MIN;
+    }
+    d[0] = cause;
+    d[1] = mt->n_clusters;
+}
+
+static int map_all(const og_index *ix, const og_params *par, int64_t n_reads, int paired,
+                   const uint8_t *seq, const uint8_t *qual, const int64_t *offsets,
+                   const int32_t *lens, og_aln *out, int nthreads, int32_t *diag)
 {
     for (int64_t r = 0; r < n_reads; ++r)
         if (lens[r] < 0 || lens[r] > OG_MAXLEN) return -3;
@@ -661,10 +760,14 @@ int og_map(const og_index *ix, const og_params *par, int64_t n_reads, int paired
                 const int64_t r1 = 2 * u, r2 = 2 * u + 1;
                 map_mate(ix, par, seq + offsets[r1], qual + offsets[r1], lens[r1], &sc, ma);
                 map_mate(ix, par, seq + offsets[r2], qual + offsets[r2], lens[r2], &sc, mb);
+                rescue_pair(ix, par, seq + offsets[r1], qual + offsets[r1], lens[r1],
+                            seq + offsets[r2], qual + offsets[r2], lens[r2], &sc, ma, mb);
                 pair_up(par, ma, mb, lens[r1], lens[r2], &out[r1], &out[r2]);
+                if (diag) { diagnose(ma, diag + 2 * r1); diagnose(mb, diag + 2 * r2); }
             } else {
                 map_mate(ix, par, seq + offsets[u], qual + offsets[u], lens[u], &sc, ma);
                 single_up(par, ma, lens[u], &out[u]);
+                if (diag) diagnose(ma, diag + 2 * u);
             }
         }
         for (int s = 0; s < 2; ++s) { free(sc.codes[s]); free(sc.quals[s]); }
@@ -672,4 +775,18 @@ int og_map(const og_index *ix, const og_params *par, int64_t n_reads, int paired
     }
     (void)nthreads;
     return 0;
+}
+
+int og_map(const og_index *ix, const og_params *par, int64_t n_reads, int paired,
+           const uint8_t *seq, const uint8_t *qual, const int64_t *offsets,
+           const int32_t *lens, og_aln *out, int nthreads)
+{
+    return map_all(ix, par, n_reads, paired, seq, qual, offsets, lens, out, nthreads, NULL);
+}
+
+int og_map_diag(const og_index *ix, const og_params *par, int64_t n_reads, int paired,
+                const uint8_t *seq, const uint8_t *qual, const int64_t *offsets,
+                const int32_t *lens, og_aln *out, int nthreads, int32_t *diag)
+{
+    return map_all(ix, par, n_reads, paired, seq, qual, offsets, lens, out, nthreads, diag);
 }

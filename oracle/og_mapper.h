@@ -61,6 +61,14 @@ int og_map(const og_index *ix, const og_params *par, int64_t n_reads, int paired
            const uint8_t *seq, const uint8_t *qual, const int64_t *offsets,
            const int32_t *lens, og_aln *out, int nthreads);
 
+/* og_map plus two int32 per read: the cause (OG_CAUSE_*) and the number of
+ * seed-hit clusters before the top-OG_MAXCAND cut.  Diagnostics only. */
+enum { OG_CAUSE_ALIGNED = 0, OG_CAUSE_RESCUED = 1, OG_CAUSE_FILTERED = 2,
+       OG_CAUSE_NO_CANDIDATE = 3, OG_CAUSE_SCORE_MIN = 4, OG_CAUSE_NCEIL = 5, OG_CAUSE_OTHER = 6 };
+int og_map_diag(const og_index *ix, const og_params *par, int64_t n_reads, int paired,
+                const uint8_t *seq, const uint8_t *qual, const int64_t *offsets,
+                const int32_t *lens, og_aln *out, int nthreads, int32_t *diag);
+
 /* Per-length tables shared with the device path (host-computed). */
 int og_seed_interval(int mode, int len);
 int og_min_score(int mode, int len);

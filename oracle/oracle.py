@@ -81,6 +81,7 @@ def _declare(L):
     L.og_map.argtypes = [ctypes.c_void_p, ctypes.POINTER(OgParams), ctypes.c_int64, ctypes.c_int,
                          ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64),
                          ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(OgAln), ctypes.c_int]
+    L.og_map_diag.argtypes = L.og_map.argtypes + [ctypes.POINTER(ctypes.c_int32)]
     L.og_seed_interval.argtypes = [ctypes.c_int, ctypes.c_int]
     L.og_min_score.argtypes = [ctypes.c_int, ctypes.c_int]
     L.og_n_ceil.argtypes = [ctypes.c_int]
@@ -157,8 +158,14 @@ def params(mode, rdg=(10, 3), rfg=(10, 3), maxins=1200):
     return OgParams(mode, rdg[0], rdg[1], rfg[0], rfg[1], maxins)
 
 
-def map_reads(index, par, seqs, quals, paired, nthreads=0):
-    """Map reads (paired: mates interleaved).  Returns a ctypes OgAln array."""
+CAUSES = ['aligned', 'rescued', 'filtered (N / empty)', 'no candidate', 'below --score-min',
+          'over --n-ceil', 'other']
+
+
+def map_reads(index, par, seqs, quals, paired, nthreads=0, diag=None):
+    """Map reads (paired: mates interleaved).  Returns a ctypes OgAln array.
+    diag: optional list that receives (cause index into CAUSES, seed-hit
+    clusters) per read."""
     n = len(seqs)
     offs = (ctypes.c_int64 * max(n, 1))()
     lens = (ctypes.c_int32 * max(n, 1))()
@@ -170,8 +177,14 @@ def map_reads(index, par, seqs, quals, paired, nthreads=0):
     sbuf = ''.join(seqs).encode()
     qbuf = ''.join(quals).encode()
     out = (OgAln * max(n, 1))()
-    st = lib().og_map(index.handle, ctypes.byref(par), n, int(paired), sbuf, qbuf, offs, lens,
-                      out, nthreads)
+    if diag is None:
+        st = lib().og_map(index.handle, ctypes.byref(par), n, int(paired), sbuf, qbuf, offs, lens,
+                          out, nthreads)
+    else:
+        d = (ctypes.c_int32 * max(2 * n, 1))()
+        st = lib().og_map_diag(index.handle, ctypes.byref(par), n, int(paired), sbuf, qbuf, offs,
+                               lens, out, nthreads, d)
+        diag[:] = [(d[2 * i], d[2 * i + 1]) for i in range(n)]
     if st != 0:
         raise ValueError('og_map status {}'.format(st))
     return out

@@ -366,6 +366,14 @@ def _garbage(pairs, n, seed):
     return pairs
 
 
+def _half_diverged(seq, keep, sub_rate, seed):
+    """seq's first `keep` bases, then a sample of the rest at sub_rate."""
+    import numpy as np
+    from micall_amd import synth
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return seq[:keep] + synth.sample_genome(seq[keep:], rng, sub_rate, 0.002).tobytes().decode()
+
+
 def _chimeric(seeds):
     """Pairs from HIV-1 gag and env sample genomes; 60 pairs of each have
     their R2 swapped with the other's, so their mates map to two seeds and
@@ -404,12 +412,14 @@ def _e2e_cases():
     syn('syn_unpaired300', 500, ['HIV1B-pol-seed'], genome_seed=107, read_seed=108, read_len=300,
         paired=False)
     cases.append(('syn_chimera', _chimeric(seeds)))
-    # 14 % divergence: every pass maps more reads than the one before, and
-    # 10 % random pairs keep the mapped fraction below 0.95, so only
+    # SARS-CoV-2 (29.9 kb): a sample identical to the seed over its first
+    # 600 nt and 22 % divergent after that, plus 10 % random pairs.  The
+    # consensus improves a stretch at a time, every pass maps more reads than
+    # the one before and the mapped fraction stays below 0.95, so only
     # MAX_REMAPS (remap.py:602-603) ends the loop, after the third pass
-    cases.append(('syn_maxremaps', _garbage(synth.make_pairs(1500, genomes=pol, genome_seed=201,
-                                                             read_seed=202, sub_rate=0.14),
-                                            150, 5)))
+    cases.append(('syn_maxremaps', _garbage(synth.make_pairs(
+        2000, genomes={'SARS-CoV-2': _half_diverged(seeds['SARS-CoV-2'], 600, 0.22, 77)},
+        genome_seed=78, read_seed=79, sub_rate=0.0, indel_rate=0.0), 200, 5)))
     # 18 % divergence: no seed reaches the count threshold, the loop never
     # runs (the reference then fails removing temp.fasta, remap.py:653-655)
     cases.append(('syn_noseed', _garbage(synth.make_pairs(1500, genomes=pol, genome_seed=201,

@@ -54,10 +54,10 @@ def test_maxremaps_case_stops_on_max_remaps():
     # growing counts every pass, mapped fraction <= 0.95: only MAX_REMAPS
     # (remap.py:602-603) can end the loop, after pass 3
     c = _counts('syn_maxremaps')
-    passes = [int(c['remap-%d HIV1B-pol-seed' % k]) for k in (1, 2, 3)]
+    passes = [int(c['remap-%d SARS-CoV-2' % k]) for k in (1, 2, 3)]
     assert passes[0] < passes[1] < passes[2]
     assert passes[2] / float(c['raw']) <= 0.95
-    assert 'remap-4 HIV1B-pol-seed' not in c
+    assert 'remap-4 SARS-CoV-2' not in c
 
 
 @pytest.mark.parametrize('case', ['syn_noseed', 'micro_2030A-V3LOOP'])

@@ -63,6 +63,51 @@ def test_map_pol_vs_oracle(ctx, mode):
     assert (ref["flag"] & 4 == 0).mean() > 0.25  # the test exercises real alignments
 
 
+def _unseedable(seq, rng, every=12):
+    """A copy with a substitution every `every` bases (phase random): no
+    exact 20- or 22-mer survives, the read still aligns in the band."""
+    out = list(seq)
+    for i in range(int(rng.integers(0, every)), len(out), every):
+        out[i] = 'ACGT'[('ACGT'.index(out[i]) + 1) % 4] if out[i] in 'ACGT' else out[i]
+    return ''.join(out)
+
+
+@pytest.mark.parametrize('mode', [oracle.E2E, oracle.LOCAL])
+def test_mate_rescue_vs_oracle(ctx, mode):
+    """Pairs whose second (or first) mate has no exact seed left: only mate
+    rescue (og_mapper.c rescue_pair, k_rescue) can align it, in the -X window
+    next to its aligned mate.  Includes mates near the reference ends (window
+    clipped), a mate that is random sequence (scan runs, DP fails) and pairs
+    whose anchor is reverse."""
+    rng = np.random.default_rng(21)
+    names, seqs, quals = _reads(600, 17, sub_rate=0.02)
+    seqs = list(seqs)
+    for p in range(len(seqs) // 2):
+        k = 2 * p + (p % 2)              # mate 1 of odd pairs, mate 2 of even ones
+        if p % 7 == 3:
+            seqs[k] = ''.join(rng.choice(list('ACGT'), size=len(seqs[k])))
+        elif p % 5 != 4:
+            seqs[k] = _unseedable(seqs[k], rng)
+    # anchors at both reference ends
+    for st in (0, len(POL) - 251):
+        a = POL[st:st + 251]
+        b = _unseedable(POL[max(0, st - 200):max(0, st - 200) + 251] if st else POL[300:551], rng)
+        comp = str.maketrans('ACGT', 'TGCA')
+        seqs += [a, b.translate(comp)[::-1]]
+        quals += ['G' * 251, 'F' * 251]
+        names += ['@end%d 1:N:0:1' % st, '@end%d 2:N:0:1' % st]
+    diag = []
+    ix = oracle.Index([POL], oracle.seed_len(mode))
+    out = oracle.map_reads(ix, oracle.params(mode), seqs, quals, True, diag=diag)
+    ref = np.frombuffer(bytes(out), dtype=_native.ALN_DTYPE)[:len(seqs)]
+    gpu = _gpu_alns(ctx, ['HIV1B-pol-seed'], [POL], mode, seqs, quals, True)
+    _assert_same(gpu, ref, seqs)
+    rescued = sum(1 for c, _ in diag if oracle.CAUSES[c] == 'rescued')
+    assert rescued > 150, rescued
+    stats = ctx.map_stats()
+    assert stats[4] >= rescued, stats       # rescue extensions (some fail the DP)
+
+
 def test_map_all_seeds_e2e_vs_oracle(ctx):
     """prelim_map's pass: every seed of projects.json, reads from 3 HIV genes."""
     genomes = {k: SEEDS[k] for k in ('HIV1B-pol-seed', 'HIV1B-env-seed', 'HIV1B-gag-seed')}
