@@ -62,25 +62,116 @@ def make_reads(pairs, block, read_len=READ_LEN, paired=True, genomes='pol'):
     return reads, quals
 
 
+def cpu_threads():
+    """Threads for the CPU baseline: every CPU this process may run on
+    (sched_getaffinity), capped by OMP_NUM_THREADS when the launcher sets it
+    (the GPU box's CPU share: nproc there shows the whole machine)."""
+    affinity = len(os.sched_getaffinity(0))
+    omp = os.environ.get('OMP_NUM_THREADS')
+    threads = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
+    return threads, affinity, omp
+
+
 def cpu_baseline(sample_pairs):
-    """The CPU oracle (C restatement, OpenMP over pairs) on a bounded sample
-    of the same workload, on this host's cores."""
+    """The CPU oracle's step (C restatement: og_map + og_rows_from_alns +
+    og_pileup_mt, OpenMP over read pairs; O(reference length) consensus in
+    Python) on a bounded sample of the same workload.  The reads are packed
+    before the clock starts, so the timed region holds no per-read Python."""
     import cpu_pipeline
     from micall_amd import projects
     cfg = projects.load_default()
     seed_set = cfg.seed_sequences()
     groups = {k: cfg.getSeedGroup(k) for k in seed_set}
     reads, quals = make_reads(sample_pairs, block=0)
-    seqs = [r.tobytes().decode() for r in reads]
-    qs = [q.tobytes().decode() for q in quals]
-    threads = min(16, os.cpu_count() or 1)
-    _, secs = cpu_pipeline.run_step(seed_set, cfg.all_region_sequences(), groups, seqs, qs,
-                                    True, threads)
+    prep = cpu_pipeline.Prepared([r.tobytes().decode() for r in reads],
+                                 [q.tobytes().decode() for q in quals], True)
+    del reads, quals
+    threads, affinity, omp = cpu_threads()
+    _, secs = cpu_pipeline.timed_step(seed_set, cfg.all_region_sequences(), groups, prep, threads)
     return {'value': round(2 * sample_pairs / secs, 1), 'unit': 'reads/s', 'cores': threads,
-            'kind': 'port',
+            'kind': 'port', 'host_cpus': {'sched_getaffinity': affinity, 'nproc': os.cpu_count(),
+                                          'OMP_NUM_THREADS': omp},
             'sample': '{} synthetic pairs (first block of the bench input): prelim e2e pass over '
                       '74 seeds + 1 local remap pass + 2 pileups/consensus, oracle C restatement '
-                      'with OpenMP over pairs, {:.1f} s'.format(sample_pairs, secs)}
+                      '(og_map, og_pileup_mt) with OpenMP over pairs on {} threads, reads packed '
+                      'before timing, {:.1f} s'.format(sample_pairs, threads, secs)}
+
+
+def write_fastq_gz(pairs, path1, path2, threads=16):
+    """The pairs as gzip FASTQ files (independent gzip members compressed on
+    `threads` threads; a multi-member file is one valid gzip stream)."""
+    import zlib
+    from concurrent.futures import ThreadPoolExecutor
+    from micall_amd import synth
+
+    def member(chunk):
+        c = zlib.compressobj(1, zlib.DEFLATED, 31)
+        return c.compress(chunk) + c.flush()
+    for mate, path in ((1, path1), (2, path2)):
+        r, q = pairs['r%d' % mate], pairs['q%d' % mate]
+        recs = [b'%s\n%s\n+\n%s\n' % (synth.read_name(pairs['block'], i, mate).encode(),
+                                      r[i].tobytes(), q[i].tobytes()) for i in range(pairs['n'])]
+        step = -(-len(recs) // (threads * 4))
+        chunks = [b''.join(recs[k:k + step]) for k in range(0, len(recs), step)]
+        del recs
+        with ThreadPoolExecutor(threads) as ex, open(path, 'wb') as f:
+            for blob in ex.map(member, chunks):
+                f.write(blob)
+
+
+def end_to_end(n_pairs, workdir):
+    """The file-to-file path bin/micall runs (prelim_map() then remap(), the
+    drop-ins) on the C2 input written as gzip FASTQ: ingest (gunzip + parse
+    + H2D + 2-bit packing), the cold 74-seed index, the prelim pass and
+    prelim.csv text, remap's prelim.csv parse, one remap pass, remap.csv
+    text.  A new device context is used, so nothing is cached from the
+    device-resident bench.  Returns the result dict (reads/s over the whole
+    call sequence, seconds per part)."""
+    import io
+    from micall_amd import _native, prelim_map, remap, session, synth
+    r1 = os.path.join(workdir, 'R1.fastq.gz')
+    r2 = os.path.join(workdir, 'R2.fastq.gz')
+    pairs = synth.make_pairs(n_pairs, genomes=bench_genomes('pol'), genome_seed=SEED,
+                             read_seed=SEED, block=0)
+    write_fastq_gz(pairs, r1, r2)
+    del pairs
+    sizes = os.path.getsize(r1) + os.path.getsize(r2)
+    # cold index build alone, on its own context
+    from micall_amd import projects
+    seeds = projects.load_default().seed_sequences()
+    probe = _native.Context(0)
+    probe.sync()
+    t = time.perf_counter()
+    probe.index_build(list(seeds), list(seeds.values()), 22)
+    probe.sync()
+    index_cold_ms = 1e3 * (time.perf_counter() - t)
+    probe.close()
+    session.reset()
+    prelim_path = os.path.join(workdir, 'prelim.csv')
+    remap_path = os.path.join(workdir, 'remap.csv')
+    t0 = time.perf_counter()
+    with open(prelim_path, 'w') as f:
+        prelim_map.prelim_map(r1, r2, f, gzip=True)
+    t1 = time.perf_counter()
+    with open(prelim_path) as pre, open(remap_path, 'w') as out:
+        counts = io.StringIO()
+        remap.remap(r1, r2, pre, out, counts, gzip=True)
+    t2 = time.perf_counter()
+    session.context().sync()
+    out = {'value': round(2 * n_pairs / (t2 - t0), 1), 'unit': 'reads/s',
+           'seconds': round(t2 - t0, 3), 'prelim_map_s': round(t1 - t0, 3),
+           'remap_s': round(t2 - t1, 3), 'index_build_cold_ms': round(index_cold_ms, 2),
+           'fastq_gz_bytes': sizes, 'prelim_csv_bytes': os.path.getsize(prelim_path),
+           'remap_csv_bytes': os.path.getsize(remap_path),
+           'remap_counts': counts.getvalue().strip().split('\n')[-3:],
+           'what': 'prelim_map() + remap() drop-ins file to file on {} pairs of gzip FASTQ '
+                   '(C2 input): ingest, cold 74-seed index, prelim pass, prelim.csv write and '
+                   'read back, remap pass(es) by the reference\'s stopping rules, remap.csv write; '
+                   'new device context'.format(n_pairs)}
+    session.reset()
+    for p in (r1, r2, prelim_path, remap_path):
+        os.remove(p)
+    return out
 
 
 def read_pmc_traffic(kernel, pairs, stage='remap'):
@@ -460,8 +551,10 @@ def main():
     ap.add_argument('--force-iterations', action='store_true',
                     help='run exactly --iterations remap passes per step (C3: "3 remap '
                          'iterations"), the stopping rules applying only after them')
-    ap.add_argument('--cpu-sample', type=int, default=100000)
+    ap.add_argument('--cpu-sample', type=int, default=200000)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-e2e', action='store_true',
+                    help='skip the end-to-end (file to file) leg of the default C2 run')
     ap.add_argument('--breakdown', action='store_true',
                     help='time each pipeline stage (synchronising) and print it to stderr')
     ap.add_argument('--stage', choices=('remap', 'sam2aln', 'censor', 'aln2counts'), default='remap',
@@ -545,7 +638,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kernels = {k: ctx.profile_get(k) for k in ('k_seed', 'k_dp', 'k_pair', 'k_pileup')}
+    kernels = {k: ctx.profile_get(k) for k in ('k_seed', 'k_dp', 'k_rescue', 'k_dp_rescue', 'k_pair',
+                                              'k_pileup')}
     dom = max(kernels, key=lambda k: kernels[k][0])
     dom_ms, dom_n = kernels[dom]
     # every launch of a mapping / pileup kernel processes this rank's pairs once
@@ -562,13 +656,20 @@ def main():
     # ungapped fast path resolves the rest without the DP
     ext = sum(int(m[1]) for m in dp_log)
     fast = sum(int(m[3]) for m in dp_log)
+    rescue = sum(int(m[4]) for m in dp_log)
     cells = (ext - fast) * L * 64
-    dp_ms = kernels['k_dp'][0]
+    dp_ms = kernels['k_dp'][0] + kernels['k_dp_rescue'][0]
 
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and paired and L == READ_LEN and args.genomes == 'pol':
             cpu = cpu_baseline(args.cpu_sample)
+        e2e = None
+        if (world == 1 and not args.no_e2e and paired and L == READ_LEN and args.genomes == 'pol'
+                and args.iterations == 1 and not args.force_iterations):
+            import tempfile
+            with tempfile.TemporaryDirectory(prefix='micall_e2e_') as work:
+                e2e = end_to_end(args.pairs, work)
         out = {
             'metric': METRIC, 'value': round(value, 1), 'unit': 'reads/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup,
@@ -601,9 +702,11 @@ def main():
             'kernels_ms_per_step': {k: round(v[0] / args.steps, 3) for k, v in kernels.items()},
             'dp': {'extensions_per_step': ext // max(args.steps, 1),
                    'fast_path_per_step': fast // max(args.steps, 1),
+                   'rescue_per_step': rescue // max(args.steps, 1),
                    'cells_per_step': cells // max(args.steps, 1),
                    'gcups': round(cells / (dp_ms / 1e3) / 1e9, 1) if dp_ms > 0 else None},
             'cpu_baseline': cpu,
+            'end_to_end': e2e,
             'result': {'remap_iterations_run': len(pipe.log),
                        'conseqs': {k: len(v) for k, v in conseqs.items()},
                        'mapped_lines': dict(new_counts)},

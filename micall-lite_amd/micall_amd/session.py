@@ -48,3 +48,12 @@ def invalidate():
     """The resident reads were replaced (e.g. by split re-mapping)."""
     global _key
     _key = None
+
+
+def reset():
+    """Close the process-wide context (the next call creates a new one)."""
+    global _ctx, _key
+    if _ctx is not None:
+        _ctx.close()
+    _ctx = None
+    _key = None

@@ -12,6 +12,8 @@ import ctypes
 import time
 from collections import Counter
 
+import numpy as np
+
 import oracle
 
 
@@ -129,3 +131,130 @@ def run_step(seed_set, all_seeds, seed_groups, seqs, quals, paired=True, nthread
         order2 = sorted((r for r in range(len(cn)) if pile2[2][r] >= 0), key=lambda r: pile2[2][r])
         conseqs = _conseqs(cn, all_seeds, pile2, order2)
     return conseqs, time.perf_counter() - t0
+
+
+# ---------------------------------------------------------------------------
+# bench.py's cpu_baseline: the same step with every per-read loop in C
+# (OpenMP over read pairs on all the cores given) and the inputs marshalled
+# before the clock starts.
+# ---------------------------------------------------------------------------
+class Prepared:
+    """Reads packed once into the buffers og_map / og_rows_from_alns take."""
+
+    def __init__(self, seqs, quals, paired):
+        self.n = len(seqs)
+        self.paired = paired
+        self.offs = (ctypes.c_int64 * max(self.n, 1))()
+        self.lens = (ctypes.c_int32 * max(self.n, 1))()
+        pos = 0
+        for i, s in enumerate(seqs):
+            self.offs[i] = pos
+            self.lens[i] = len(s)
+            pos += len(s)
+        self.sbuf = ''.join(seqs).encode()
+        self.qbuf = ''.join(quals).encode()
+        self.seq_out = ctypes.create_string_buffer(max(pos, 1))
+        self.qual_out = ctypes.create_string_buffer(max(pos, 1))
+        self.rows = (oracle.OgRow * max(self.n, 1))()
+        self.alns = (oracle.OgAln * max(self.n, 1))()
+
+
+def _declare_fast(L):
+    if getattr(L, '_fast_declared', False):
+        return
+    L.og_rows_from_alns.argtypes = [ctypes.POINTER(oracle.OgAln), ctypes.c_int64, ctypes.c_char_p,
+                                    ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64),
+                                    ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p,
+                                    ctypes.c_char_p, ctypes.POINTER(oracle.OgRow), ctypes.c_int]
+    L.og_pileup_mt.argtypes = list(L.og_pileup.argtypes) + [ctypes.c_int]
+    L._fast_declared = True
+
+
+def _map_fast(prep, ix, mode, nthreads):
+    st = oracle.lib().og_map(ix.handle, ctypes.byref(oracle.params(mode)), prep.n, int(prep.paired),
+                             prep.sbuf, prep.qbuf, prep.offs, prep.lens, prep.alns, nthreads)
+    if st:
+        raise RuntimeError('og_map status %d' % st)
+    return np.frombuffer(prep.alns, dtype=_ALN_DTYPE, count=prep.n)
+
+
+def _pileup_fast(prep, recs, n_refs, ref_lens, nthreads, q=20):
+    L = oracle.lib()
+    L.og_rows_from_alns(prep.alns, prep.n, prep.sbuf, prep.qbuf, prep.offs, prep.lens,
+                        prep.seq_out, prep.qual_out, prep.rows, nthreads)
+    sam_ref = recs['sam_ref']
+    if prep.paired:
+        both = (sam_ref[0::2] >= 0) & (sam_ref[1::2] >= 0)
+        first = 2 * np.flatnonzero(both)
+        units = np.stack([first, first + 1], axis=1).reshape(-1).astype(np.int64)
+    else:
+        one = np.flatnonzero(sam_ref >= 0)
+        units = np.stack([one, np.full_like(one, -1)], axis=1).reshape(-1).astype(np.int64)
+    n_units = len(units) // 2
+    cap = max(ref_lens) + 2048
+    dense = np.zeros(n_refs * cap * 6, dtype=np.int32)
+    rc = np.zeros(n_refs, dtype=np.int64)
+    fu = np.full(n_refs, -1, dtype=np.int64)
+    mp = np.zeros(n_refs, dtype=np.int32)
+    ev_cap = prep.n * 256 + 16
+    ev = (oracle.OgEvent * ev_cap)()
+    pool = ctypes.create_string_buffer(ev_cap * 4)
+    ne, used = ctypes.c_int64(), ctypes.c_int64()
+    p = lambda a, t: a.ctypes.data_as(ctypes.POINTER(t))  # noqa: E731
+    st = L.og_pileup_mt(n_refs, cap, prep.rows, n_units,
+                        p(units, ctypes.c_int64) if n_units else None, q,
+                        p(dense, ctypes.c_int32), p(rc, ctypes.c_int64), p(fu, ctypes.c_int64),
+                        p(mp, ctypes.c_int32), ev, ev_cap, ctypes.byref(ne), pool, len(pool),
+                        ctypes.byref(used), nthreads)
+    if st:
+        raise RuntimeError('og_pileup_mt status %d' % st)
+    return dense, rc, fu, mp, ev, ne.value, pool.raw, cap
+
+
+def timed_step(seed_set, all_seeds, seed_groups, prep, nthreads, count_threshold=10):
+    """run_step on prepared reads: prelim e2e pass over every seed, seed
+    selection, prelim consensus, one --local pass, pileup and consensus.
+    Returns (conseqs, seconds); only this function's body is timed."""
+    _declare_fast(oracle.lib())
+    t0 = time.perf_counter()
+    names = list(seed_set)
+    ix = oracle.Index([seed_set[k] for k in names], 22)
+    recs = _map_fast(prep, ix, oracle.E2E, nthreads)
+    sam_ref = recs['sam_ref']
+    mapped = (recs['flag'] & 4) == 0
+    longest_m = _longest_m(recs)
+    lines = np.bincount(sam_ref[sam_ref >= 0], minlength=len(names))
+    filt = np.bincount(sam_ref[(sam_ref >= 0) & mapped & (longest_m > 50)], minlength=len(names))
+    first = {}
+    for r in np.flatnonzero(lines):
+        first[names[r]] = int(np.argmax(sam_ref == r))
+    refgroups = {}
+    for name in sorted(first, key=first.get):
+        thr = 1 if name == 'HIV1B-env-seed' else count_threshold
+        _b, best = refgroups.get(seed_groups[name], (None, thr - 1))
+        f = int(filt[names.index(name)])
+        if f > best:
+            refgroups[seed_groups[name]] = (name, f)
+    seed_counts = {r: c for r, c in refgroups.values()}
+    pile = _pileup_fast(prep, recs, len(names), [len(seed_set[k]) for k in names], nthreads)
+    order = sorted((r for r in range(len(names)) if pile[2][r] >= 0), key=lambda r: first[names[r]])
+    conseqs = {k: v for k, v in _conseqs(names, all_seeds, pile, order).items() if k in seed_counts}
+    if conseqs:
+        cn = list(conseqs)
+        ix2 = oracle.Index([conseqs[k] for k in cn], 20)
+        recs2 = _map_fast(prep, ix2, oracle.LOCAL, nthreads)
+        pile2 = _pileup_fast(prep, recs2, len(cn), [len(conseqs[k]) for k in cn], nthreads)
+        order2 = sorted((r for r in range(len(cn)) if pile2[2][r] >= 0), key=lambda r: pile2[2][r])
+        conseqs = _conseqs(cn, all_seeds, pile2, order2)
+    return conseqs, time.perf_counter() - t0
+
+
+_ALN_DTYPE = np.dtype([(name, np.int32) for name, _ in oracle.OgAln._fields_[:-1]] +
+                      [('cigar', np.uint32, (oracle.MAXOPS,))])
+
+
+def _longest_m(recs):
+    ops = recs['cigar']
+    n = recs['n_cigar'][:, None]
+    is_m = ((ops & 15) == 0) & (np.arange(ops.shape[1])[None, :] < n)
+    return np.where(is_m, ops >> 4, 0).max(axis=1)

@@ -790,3 +790,50 @@ int og_map_diag(const og_index *ix, const og_params *par, int64_t n_reads, int p
 {
     return map_all(ix, par, n_reads, paired, seq, qual, offsets, lens, out, nthreads, diag);
 }
+
+/* ------------------------------------------------------------------ */
+/* SAM-orientation rows of the mapped reads for og_pileup (what temp.sam */
+/* holds after a pass): sequence printed as upper-case ACGT / N, reverse  */
+/* complemented with the qualities reversed when the read aligned to the  */
+/* reverse strand.  The row layout is og_pileup.c's og_row.  Used by the  */
+/* CPU baseline (oracle/cpu_pipeline.py) to keep Python out of its timed  */
+/* region.                                                                */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int32_t flag, ref, pos, n_cigar;
+    const uint32_t *cigar;
+    int32_t len;
+    const char *seq, *qual;
+} og_row_view;
+
+int og_rows_from_alns(const og_aln *alns, int64_t n, const uint8_t *seq, const uint8_t *qual,
+                      const int64_t *offsets, const int32_t *lens, char *seq_out,
+                      char *qual_out, og_row_view *rows, int nthreads)
+{
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int64_t i = 0; i < n; ++i) {
+        const og_aln *a = &alns[i];
+        const int m = lens[i];
+        const uint8_t *s = seq + offsets[i], *q = qual + offsets[i];
+        char *so = seq_out + offsets[i], *qo = qual_out + offsets[i];
+        const int rev = a->ref >= 0 && a->rev;
+        for (int k = 0; k < m; ++k) {
+            const int src = rev ? m - 1 - k : k;
+            const uint8_t c = base_code(s[src]);
+            so[k] = c > 3 ? 'N' : "ACGT"[rev ? 3 - c : c];
+            qo[k] = (char)q[src];
+        }
+        og_row_view *r = &rows[i];
+        r->flag = a->flag;
+        r->ref = a->sam_ref;
+        r->pos = a->sam_pos;
+        r->n_cigar = a->ref >= 0 && !(a->flag & 4) ? a->n_cigar : 0;
+        r->cigar = a->cigar;
+        r->len = m;
+        r->seq = so;
+        r->qual = qo;
+    }
+    return 0;
+}

@@ -20,6 +20,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 enum { OP_M = 0, OP_I = 1, OP_D = 2, OP_S = 4 };
 
@@ -206,6 +209,108 @@ static int add_event(og_event *ev, int64_t ev_cap, int64_t *n_ev, char *pool, in
     return 0;
 }
 
+/* Where one merged pair's counts go.  Serial: plain stores.  Threaded
+ * (og_pileup_mt): the dense counters, read counts, first unit and max
+ * position are updated atomically (every update commutes), and the events
+ * go to a per-thread list that is appended in unit order afterwards. */
+typedef struct {
+    int n_refs;
+    int32_t cap;
+    int32_t *dense;
+    int64_t *read_counts, *first_unit;
+    int32_t *max_pos;
+    og_event *ev;
+    int64_t ev_cap, *n_ev;
+    char *pool;
+    int64_t pool_cap, *pool_used;
+    int atomic;
+} sink_t;
+
+static void max_i32(int32_t *p, int32_t v, int atomic)
+{
+    if (!atomic) { if (v > *p) *p = v; return; }
+    int32_t cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+    while (v > cur && !__atomic_compare_exchange_n(p, &cur, v, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED))
+        ;
+}
+
+static void min_first(int64_t *p, int64_t v, int atomic)
+{
+    if (!atomic) { if (*p < 0) *p = v; return; }
+    int64_t cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+    while ((cur < 0 || v < cur) &&
+           !__atomic_compare_exchange_n(p, &cur, v, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED))
+        ;
+}
+
+static void bump32(int32_t *p, int atomic)
+{
+    if (atomic) __atomic_fetch_add(p, 1, __ATOMIC_RELAXED); else *p += 1;
+}
+
+/* one unit (merge_reads + update_counts); returns a status */
+static int pile_unit(const og_row *rows, const int64_t *unit_rows, int64_t u, int q_cutoff,
+                     const sink_t *k)
+{
+    const og_row *r1 = unit_rows[2 * u] >= 0 ? &rows[unit_rows[2 * u]] : NULL;
+    const og_row *r2 = unit_rows[2 * u + 1] >= 0 ? &rows[unit_rows[2 * u + 1]] : NULL;
+    if (!r1) return 0;
+    if (r2 && r1->ref != r2->ref) return 0;                 /* remap.py:96-98 */
+    const og_row *mapped[2];
+    int nm = 0;
+    if (!(r1->flag & 4)) mapped[nm++] = r1;
+    if (r2 && !(r2->flag & 4)) mapped[nm++] = r2;
+    if (nm == 0) return 0;                                  /* :111-112 */
+    const int ref = mapped[0]->ref;
+    if (ref < 0 || ref >= k->n_refs) return -3;
+    applied_t a1, a2;
+    memset(&a2, 0, sizeof(a2));
+    if (apply_cigar(mapped[0], mapped[0]->pos - 1, &a1)) return -3;
+    if (nm == 2 && apply_cigar(mapped[1], mapped[1]->pos - 1, &a2)) { free_applied(&a1); return -3; }
+    const int mlen_cap = (a1.len > a2.len ? a1.len : a2.len) + 1;
+    char *mseq = malloc((size_t)mlen_cap);
+    const int ml = merge_pairs(a1.seq, a1.qual, a1.len, nm == 2 ? a2.seq : "", nm == 2 ? a2.qual : "",
+                               nm == 2 ? a2.len : 0, q_cutoff, 5, mseq);
+    mins_t *mi = malloc(sizeof(mins_t) * (size_t)(a1.n_ins + a2.n_ins + 1));
+    const int nmi = merge_inserts(&a1, nm == 2 ? &a2 : NULL, q_cutoff, mi);
+
+    if (k->atomic) __atomic_fetch_add(&k->read_counts[ref], 1, __ATOMIC_RELAXED);
+    else k->read_counts[ref] += 1;
+    min_first(&k->first_unit[ref], u, k->atomic);
+    int started = 0, status = 0;
+    for (int i = 0; i < ml && status == 0; ++i) {
+        const char c = mseq[i];
+        const int pos = i + 1;
+        if (!started) {
+            if (c == '-') continue;
+            started = 1;
+        }
+        if (c == 'n') continue;
+        if (pos > k->cap) { status = -3; break; }
+        max_i32(&k->max_pos[ref], pos, k->atomic);
+        int32_t *cell = k->dense + ((size_t)ref * (size_t)k->cap + (size_t)(pos - 1)) * 6;
+        if (c == 'N') { cell[4] = 1; continue; }     /* flags: every writer stores 1 */
+        if (c == '-') { cell[5] = 1; continue; }
+        const mins_t *ins = NULL;
+        for (int z = 0; z < nmi; ++z) if (mi[z].key == pos) ins = &mi[z];
+        if (ins && ins->len > 0 && ins->len % 3 == 0) {
+            status = add_event(k->ev, k->ev_cap, k->n_ev, k->pool, k->pool_cap, k->pool_used, ref,
+                               pos, c, ins->seq, ins->len);
+        } else if (c == 'A') bump32(&cell[0], k->atomic);
+        else if (c == 'C') bump32(&cell[1], k->atomic);
+        else if (c == 'G') bump32(&cell[2], k->atomic);
+        else if (c == 'T') bump32(&cell[3], k->atomic);
+        else status = add_event(k->ev, k->ev_cap, k->n_ev, k->pool, k->pool_cap, k->pool_used, ref,
+                                pos, c, "", 0);
+    }
+    for (int z = 0; z < nmi; ++z) free(mi[z].seq);
+    free(mi);
+    free(mseq);
+    free_applied(&a1);
+    if (nm == 2) free_applied(&a2);
+    return status;
+}
+
 /*
  * units: n_units pairs of row indices (unit_rows[2u], unit_rows[2u+1]; -1 =
  * no mate), as matchmaker (remap.py:853-889) yields them.
@@ -221,61 +326,58 @@ int og_pileup(int n_refs, int32_t cap, const og_row *rows, int64_t n_units,
 {
     *n_ev = 0;
     *pool_used = 0;
+    const sink_t k = { n_refs, cap, dense, read_counts, first_unit, max_pos, ev, ev_cap, n_ev,
+                       pool, pool_cap, pool_used, 0 };
     int status = 0;
-    for (int64_t u = 0; u < n_units && status == 0; ++u) {
-        const og_row *r1 = unit_rows[2 * u] >= 0 ? &rows[unit_rows[2 * u]] : NULL;
-        const og_row *r2 = unit_rows[2 * u + 1] >= 0 ? &rows[unit_rows[2 * u + 1]] : NULL;
-        if (!r1) continue;
-        if (r2 && r1->ref != r2->ref) continue;                 /* remap.py:96-98 */
-        const og_row *mapped[2];
-        int nm = 0;
-        if (!(r1->flag & 4)) mapped[nm++] = r1;
-        if (r2 && !(r2->flag & 4)) mapped[nm++] = r2;
-        if (nm == 0) continue;                                  /* :111-112 */
-        const int ref = mapped[0]->ref;
-        if (ref < 0 || ref >= n_refs) { status = -3; break; }
-        applied_t a1, a2;
-        memset(&a2, 0, sizeof(a2));
-        if (apply_cigar(mapped[0], mapped[0]->pos - 1, &a1)) { status = -3; break; }
-        if (nm == 2 && apply_cigar(mapped[1], mapped[1]->pos - 1, &a2)) { free_applied(&a1); status = -3; break; }
-        const int mlen_cap = (a1.len > a2.len ? a1.len : a2.len) + 1;
-        char *mseq = malloc((size_t)mlen_cap);
-        const int ml = merge_pairs(a1.seq, a1.qual, a1.len, nm == 2 ? a2.seq : "", nm == 2 ? a2.qual : "",
-                                   nm == 2 ? a2.len : 0, q_cutoff, 5, mseq);
-        mins_t *mi = malloc(sizeof(mins_t) * (size_t)(a1.n_ins + a2.n_ins + 1));
-        const int nmi = merge_inserts(&a1, nm == 2 ? &a2 : NULL, q_cutoff, mi);
+    for (int64_t u = 0; u < n_units && status == 0; ++u) status = pile_unit(rows, unit_rows, u, q_cutoff, &k);
+    return status;
+}
 
-        read_counts[ref] += 1;
-        if (first_unit[ref] < 0) first_unit[ref] = u;
-        int started = 0;
-        for (int i = 0; i < ml && status == 0; ++i) {
-            const char c = mseq[i];
-            const int pos = i + 1;
-            if (!started) {
-                if (c == '-') continue;
-                started = 1;
-            }
-            if (c == 'n') continue;
-            if (pos > cap) { status = -3; break; }
-            if (pos > max_pos[ref]) max_pos[ref] = pos;
-            int32_t *cell = dense + ((size_t)ref * (size_t)cap + (size_t)(pos - 1)) * 6;
-            if (c == 'N') { cell[4] = 1; continue; }
-            if (c == '-') { cell[5] = 1; continue; }
-            const mins_t *ins = NULL;
-            for (int z = 0; z < nmi; ++z) if (mi[z].key == pos) ins = &mi[z];
-            if (ins && ins->len > 0 && ins->len % 3 == 0) {
-                status = add_event(ev, ev_cap, n_ev, pool, pool_cap, pool_used, ref, pos, c, ins->seq, ins->len);
-            } else if (c == 'A') cell[0] += 1;
-            else if (c == 'C') cell[1] += 1;
-            else if (c == 'G') cell[2] += 1;
-            else if (c == 'T') cell[3] += 1;
-            else status = add_event(ev, ev_cap, n_ev, pool, pool_cap, pool_used, ref, pos, c, "", 0);
+/* og_pileup over nthreads threads (the CPU baseline of bench.py): the same
+ * counters and the same event list, in the same order. */
+int og_pileup_mt(int n_refs, int32_t cap, const og_row *rows, int64_t n_units,
+                 const int64_t *unit_rows, int q_cutoff, int32_t *dense, int64_t *read_counts,
+                 int64_t *first_unit, int32_t *max_pos, og_event *ev, int64_t ev_cap,
+                 int64_t *n_ev, char *pool, int64_t pool_cap, int64_t *pool_used, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    *n_ev = 0;
+    *pool_used = 0;
+    int status = 0;
+    og_event **tev = calloc((size_t)nthreads, sizeof(og_event *));
+    char **tpool = calloc((size_t)nthreads, sizeof(char *));
+    int64_t *tn = calloc((size_t)nthreads, sizeof(int64_t)), *tused = calloc((size_t)nthreads, sizeof(int64_t));
+    const int64_t tev_cap = ev_cap / nthreads + 1024, tpool_cap = pool_cap / nthreads + 4096;
+#pragma omp parallel num_threads(nthreads)
+    {
+        int t = 0;
+#ifdef _OPENMP
+        t = omp_get_thread_num();
+#endif
+        tev[t] = malloc(sizeof(og_event) * (size_t)tev_cap);
+        tpool[t] = malloc((size_t)tpool_cap);
+        const sink_t k = { n_refs, cap, dense, read_counts, first_unit, max_pos, tev[t], tev_cap,
+                           &tn[t], tpool[t], tpool_cap, &tused[t], 1 };
+        const int64_t per = (n_units + nthreads - 1) / nthreads;
+        const int64_t lo = per * t, hi = lo + per < n_units ? lo + per : n_units;
+        int st = 0;
+        for (int64_t u = lo; u < hi && st == 0; ++u) st = pile_unit(rows, unit_rows, u, q_cutoff, &k);
+        if (st) {
+#pragma omp critical
+            if (st < status) status = st;
         }
-        for (int z = 0; z < nmi; ++z) free(mi[z].seq);
-        free(mi);
-        free(mseq);
-        free_applied(&a1);
-        if (nm == 2) free_applied(&a2);
     }
+    for (int t = 0; t < nthreads && status == 0; ++t) {     /* contiguous blocks: unit order */
+        if (*n_ev + tn[t] > ev_cap || *pool_used + tused[t] > pool_cap) { status = -2; break; }
+        for (int64_t e = 0; e < tn[t]; ++e) {
+            ev[*n_ev + e] = tev[t][e];
+            ev[*n_ev + e].tok_off += (int32_t)*pool_used;
+        }
+        memcpy(pool + *pool_used, tpool[t], (size_t)tused[t]);
+        *n_ev += tn[t];
+        *pool_used += tused[t];
+    }
+    for (int t = 0; t < nthreads; ++t) { free(tev[t]); free(tpool[t]); }
+    free(tev); free(tpool); free(tn); free(tused);
     return status;
 }
