@@ -1097,7 +1097,9 @@ struct RescueArgs {
     int maxins;
 };
 
-constexpr int RESCUE_CHUNK = 256;   // diagonals per staged reference window
+// diagonals per staged reference window (the -X window of C2 has ~950)
+constexpr int RESCUE_CHUNK = 1024;
+constexpr int RESCUE_WORDS = (RESCUE_CHUNK + MAXLEN) / 16 + 4;   // 2-bit words of a staged window
 
 __device__ __forceinline__ int best_slot(const Slot *sl, int n)
 {
@@ -1111,13 +1113,15 @@ __device__ __forceinline__ int best_slot(const Slot *sl, int n)
 
 __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t sh_read[4][MAXLEN + 16];
-    __shared__ __attribute__((aligned(16))) uint8_t sh_ref[4][RESCUE_CHUNK + MAXLEN + 16];
+    // the mate and the reference window as 2-bit words (16 bases each) plus
+    // "N" masks (01 in the base's bit pair)
+    __shared__ uint32_t sh_rd[4][2][MAXLEN / 16 + 1];
+    __shared__ uint32_t sh_rf[4][2][RESCUE_WORDS];
     __shared__ int32_t sh_items[4][64];
     const int lane = threadIdx.x & 63;
     const int wv = wave_uniform(threadIdx.x >> 6);
-    uint8_t *rd = sh_read[wv];
-    uint8_t *rf = sh_ref[wv];
+    uint32_t *rdw = sh_rd[wv][0], *rdn = sh_rd[wv][1];
+    uint32_t *rfw = sh_rf[wv][0], *rfn = sh_rf[wv][1];
     const int64_t units = A.R.n / 2;
     for (int64_t u0 = ((int64_t)blockIdx.x * 4 + wv) * 64; u0 < units;
          u0 += (int64_t)gridDim.x * 256) {
@@ -1158,36 +1162,52 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
             if (hi > reflen) hi = reflen;
             if (hi - lo < m) continue;
             const int s = 1 - ast;
-            // the mate's codes on strand s, 4 (never matches) past its end
-            for (int i = lane; i < m + 16; i += 64) {
-                uint32_t c = 4;
-                if (i < m) {
-                    c = read_code(A.R, off, s ? m - 1 - i : i);
-                    if (s && c < 4) c = 3 - c;
+            // the mate on strand s; bases past its end count as N (never match)
+            const int nw = (m + 15) >> 4;
+            for (int w = lane; w < nw; w += 64) {
+                uint32_t code = 0, nmk = 0;
+                for (int x = 0; x < 16; ++x) {
+                    const int b = 16 * w + x;
+                    uint32_t c = 4;
+                    if (b < m) {
+                        c = read_code(A.R, off, s ? m - 1 - b : b);
+                        if (s && c < 4) c = 3 - c;
+                    }
+                    if (c > 3) nmk |= 1u << (2 * x);
+                    else code |= c << (2 * x);
                 }
-                rd[i] = (uint8_t)c;
+                rdw[w] = code;
+                rdn[w] = nmk;
             }
             int bestM = -1, bestd = 0;
             const int dlast = (int)(hi - m);
             for (int d0 = (int)lo; d0 <= dlast; d0 += RESCUE_CHUNK) {
                 const int nd = dlast - d0 + 1 < RESCUE_CHUNK ? dlast - d0 + 1 : RESCUE_CHUNK;
-                for (int x = lane; x < nd + m + 8; x += 64) {
-                    const int j = d0 + x;
-                    rf[x] = j < hi ? A.I.codes[gref + j] : (uint8_t)7;
+                // reference bases d0 .. d0 + nd + m (+ one word), N past the window
+                const int nrw = (nd + m + 15) / 16 + 1;
+                for (int w = lane; w < nrw; w += 64) {
+                    uint32_t code = 0, nmk = 0;
+                    for (int x = 0; x < 16; ++x) {
+                        const int64_t j = (int64_t)d0 + 16 * w + x;
+                        const uint32_t c = j < hi ? A.I.codes[gref + j] : 4u;
+                        if (c > 3) nmk |= 1u << (2 * x);
+                        else code |= c << (2 * x);
+                    }
+                    rfw[w] = code;
+                    rfn[w] = nmk;
                 }
                 wave_sync();
                 for (int t = lane; t < nd; t += 64) {
+                    // matches on diagonal d0 + t: 16 bases per step, the window
+                    // words aligned to the diagonal by a funnel shift
+                    const int w0 = t >> 4;
+                    const uint32_t sh = (uint32_t)(2 * (t & 15));
                     int cnt = 0;
-                    for (int i = 0; i < m; i += 4) {
-                        const uint32_t rw = *(const uint32_t *)(rd + i);
-                        const int b = t + i;
-                        const uint32_t w0 = *(const uint32_t *)(rf + (b & ~3));
-                        const uint32_t w1 = *(const uint32_t *)(rf + (b & ~3) + 4);
-                        const uint32_t rv = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(b & 3));
-                        const uint32_t x = rw ^ rv;
-                        // byte matches: equal codes (values < 8), read base not N
-                        const uint32_t eq = ~(x | (x >> 1) | (x >> 2) | (rw >> 2)) & 0x01010101u;
-                        cnt += __builtin_popcount(eq);
+                    for (int i = 0; i < nw; ++i) {
+                        const uint32_t v = __builtin_amdgcn_alignbit(rfw[w0 + i + 1], rfw[w0 + i], sh);
+                        const uint32_t vn = __builtin_amdgcn_alignbit(rfn[w0 + i + 1], rfn[w0 + i], sh);
+                        const uint32_t x = rdw[i] ^ v;
+                        cnt += __builtin_popcount(~(x | (x >> 1) | rdn[i] | vn) & 0x55555555u);
                     }
                     if (cnt > bestM) { bestM = cnt; bestd = d0 + t; }
                 }
