@@ -289,6 +289,16 @@ int mh_gotoh_align(mh_ctx *ctx, const char *seq1, const char *seq2, int gop, int
                    int is_global, const char *alphabet, const int *matrix, char *out1,
                    char *out2, int cap, int *score);
 
+/* Many alignments with the same scoring in one launch (one workgroup each):
+ * the consensus-distance filter's K x K alignments (remap.py:244-263) and
+ * aln2counts' coordinate alignments.  status[t] = 0, or -1 where
+ * _gotoh2.align would raise "Traceback failed"; the call itself returns
+ * -3 / -2 / -4 for a bad argument / out of memory / a HIP error. */
+int mh_gotoh_align_batch(mh_ctx *ctx, int count, const char *const *seq1,
+                         const char *const *seq2, int gop, int gep, int is_global,
+                         const char *alphabet, const int *matrix, char *const *out1,
+                         char *const *out2, const int *cap, int *score, int *status);
+
 /* Per-kernel device time measured with HIP events on the context's stream
  * (k_seed, k_dp, k_pair, k_pileup).  mh_profile(ctx, 1) enables and resets. */
 int mh_profile(mh_ctx *ctx, int enable);
@@ -296,6 +306,8 @@ int mh_profile_get(mh_ctx *ctx, const char *kernel, double *total_ms, int64_t *l
 
 /* Unit-cost edit distance (Levenshtein.distance, remap.py:250). */
 int mh_levenshtein(const char *a, const char *b);
+/* out[t] = mh_levenshtein(a[t], b[t]) for count pairs, on host threads. */
+int mh_levenshtein_batch(int count, const char *const *a, const char *const *b, int *out);
 
 #ifdef __cplusplus
 }

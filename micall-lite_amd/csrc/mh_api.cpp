@@ -4,6 +4,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1322,6 +1323,37 @@ int mh_gotoh_align(mh_ctx *ctx, const char *seq1, const char *seq2, int gop, int
     CtxEx *c = X(ctx);
     MH_HIP(hipSetDevice(c->device));
     return run_gotoh(*c, seq1, seq2, gop, gep, is_global, alphabet, matrix, out1, out2, cap, score);
+}
+
+int mh_gotoh_align_batch(mh_ctx *ctx, int count, const char *const *seq1,
+                         const char *const *seq2, int gop, int gep, int is_global,
+                         const char *alphabet, const int *matrix, char *const *out1,
+                         char *const *out2, const int *cap, int *score, int *status)
+{
+    if (!ctx || count < 0 || (count > 0 && (!seq1 || !seq2 || !out1 || !out2 || !cap || !score ||
+                                            !status)) || !alphabet || !matrix)
+        return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    return run_gotoh_batch(*c, count, seq1, seq2, gop, gep, is_global, alphabet, matrix, out1,
+                           out2, cap, score, status);
+}
+
+int mh_levenshtein_batch(int count, const char *const *a, const char *const *b, int *out)
+{
+    if (count < 0 || (count > 0 && (!a || !b || !out))) return -3;
+    for (int t = 0; t < count; ++t)
+        if (!a[t] || !b[t]) return -3;
+    // one pair per thread: the pairs of a consensus-distance filter are few and long
+    const int threads = count < 16 ? count : 16;
+    std::vector<std::thread> pool;
+    std::atomic<int> next(0);
+    for (int w = 0; w < threads; ++w)
+        pool.emplace_back([&]() {
+            for (int t = next++; t < count; t = next++) out[t] = mh_levenshtein(a[t], b[t]);
+        });
+    for (auto &th : pool) th.join();
+    return 0;
 }
 
 // Unit-cost edit distance (python-Levenshtein's distance, remap.py:259) by

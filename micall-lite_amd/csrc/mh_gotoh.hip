@@ -1,6 +1,8 @@
 // mh_gotoh.hip -- the _gotoh2 aligner (micall/alignment/src/_gotoh2.c) on
 // gfx950, used by the consensus-distance filter (remap.py:244-263: global,
-// gop 15, gep 3, HYPHY_NUC).  One workgroup of 1024 threads per alignment:
+// gop 15, gep 3, HYPHY_NUC) and aln2counts' coordinate mapping (local,
+// EmpHIV25).  A batch of alignments is one launch, one workgroup of 1024
+// threads per alignment (blockIdx.x = alignment), each with its own scratch:
 //   phase 1  cost assignment (_gotoh2.c:137-201) by anti-diagonals; R/P/Q
 //            live in three rolling diagonal buffers; each cell's tie bits go
 //            to three byte planes so no two cells of a diagonal write the
@@ -13,6 +15,7 @@
 // Bit-for-bit specification: oracle/og_gotoh.c.
 #include <limits.h>
 
+#include <mutex>
 #include <vector>
 
 #include "mh_internal.h"
@@ -38,8 +41,9 @@ struct GotohArgs {
 
 __device__ __forceinline__ int gmin(int x, int y) { return x <= y ? x : y; }
 
-__global__ __launch_bounds__(1024) void k_gotoh(GotohArgs A)
+__global__ __launch_bounds__(1024) void k_gotoh(const GotohArgs *batch)
 {
+    const GotohArgs A = batch[blockIdx.x];
     const int m = A.m, n = A.n;
     const int W = n + 2;
     const int u = A.u, v = A.v;
@@ -162,23 +166,59 @@ __global__ __launch_bounds__(1024) void k_gotoh(GotohArgs A)
     }
 }
 
-int run_gotoh(Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_global,
-              const char *alphabet, const int *matrix, char *out1, char *out2, int cap, int *score)
+static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// Per alignment: an "io" block (codes, strings, output strings, result: what
+// crosses PCIe) and a "work" block (diagonal buffers, last row / column and
+// the three tie planes, zeroed on the device).
+static size_t gotoh_io_bytes(int m, int n)
 {
-    const int m = (int)strlen(s1), n = (int)strlen(s2), L = (int)strlen(alphabet);
-    if (m == 0 || n == 0 || L == 0 || cap < m + n + 1) { set_error("mh_gotoh_align: bad arguments"); return -3; }
+    return align16(m + 8) + align16(n + 8) + align16(m + 1) + align16(n + 1) +
+           2 * align16(m + n + 1) + 64;
+}
+
+static size_t gotoh_work_bytes(int m, int n)
+{
+    return 3 * align16(sizeof(int) * 3 * (m + 2)) + align16(sizeof(int) * (m + 2)) +
+           align16(sizeof(int) * (n + 2)) + 3 * align16((size_t)(m + 2) * (n + 2));
+}
+
+// Retained scratch above this is released after the call (one very long
+// alignment must not pin device memory for the rest of the session).
+constexpr size_t GOTOH_KEEP_BYTES = (size_t)1 << 30;
+
+int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const *s2, int gop,
+                    int gep, int is_global, const char *alphabet, const int *matrix,
+                    char *const *out1, char *const *out2, const int *cap, int *score, int *status)
+{
+    const int L = (int)strlen(alphabet);
+    if (count < 0 || L == 0) { set_error("mh_gotoh_align: bad arguments"); return -3; }
+    if (count == 0) return 0;
     int code[256];
     for (int k = 0; k < 256; ++k) code[k] = -1;
     for (int k = 0; k < L; ++k) code[(unsigned char)alphabet[k]] = k;
-    std::vector<int8_t> ha(m), hb(n);
-    for (int i = 0; i < m; ++i) if ((ha[i] = (int8_t)code[(unsigned char)s1[i]]) < 0) { set_error("mh_gotoh_align: '%c' not in alphabet", s1[i]); return -3; }
-    for (int j = 0; j < n; ++j) if ((hb[j] = (int8_t)code[(unsigned char)s2[j]]) < 0) { set_error("mh_gotoh_align: '%c' not in alphabet", s2[j]); return -3; }
-    const size_t cells = (size_t)(m + 2) * (n + 2);
-    // one allocation for everything
-    const size_t sz_codes = (size_t)m + n + 16, sz_mat = sizeof(int) * L * L,
-                 sz_diag = sizeof(int) * 3 * (m + 2) * 3, sz_last = sizeof(int) * (m + n + 4),
-                 sz_bits = 3 * cells, sz_str = (size_t)2 * (m + n + 2) * 2, sz_res = 64;
-    const size_t total = sz_codes + sz_mat + sz_diag + sz_last + sz_bits + sz_str + sz_res + 256;
+    std::vector<int> ms(count), ns(count);
+    std::vector<size_t> io(count + 1, 0), work(count + 1, 0);
+    for (int t = 0; t < count; ++t) {
+        if (!s1[t] || !s2[t] || !out1[t] || !out2[t]) { set_error("mh_gotoh_align: null argument"); return -3; }
+        ms[t] = (int)strlen(s1[t]);
+        ns[t] = (int)strlen(s2[t]);
+        if (ms[t] == 0 || ns[t] == 0 || cap[t] < ms[t] + ns[t] + 1) {
+            set_error("mh_gotoh_align: bad arguments (alignment %d)", t);
+            return -3;
+        }
+        for (int i = 0; i < ms[t]; ++i)
+            if (code[(unsigned char)s1[t][i]] < 0) { set_error("mh_gotoh_align: '%c' not in alphabet", s1[t][i]); return -3; }
+        for (int j = 0; j < ns[t]; ++j)
+            if (code[(unsigned char)s2[t][j]] < 0) { set_error("mh_gotoh_align: '%c' not in alphabet", s2[t][j]); return -3; }
+        io[t + 1] = io[t] + gotoh_io_bytes(ms[t], ns[t]);
+        work[t + 1] = work[t] + gotoh_work_bytes(ms[t], ns[t]);
+    }
+    const size_t sz_mat = align16(sizeof(int) * L * L), sz_args = align16(sizeof(GotohArgs) * count);
+    // device buffer: [io blocks][matrix][argument blocks][work blocks]
+    const size_t off_mat = io[count], off_args = off_mat + sz_mat, off_work = off_args + sz_args;
+    const size_t total = off_work + work[count] + 256;
+    std::lock_guard<std::mutex> guard(c.gotoh_mutex);   // the scratch is per context
     if (c.gotoh_cap < total) {
         hipFree(c.gotoh_buf);
         c.gotoh_buf = nullptr;
@@ -187,49 +227,81 @@ int run_gotoh(Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_g
         c.gotoh_cap = total;
     }
     char *d = c.gotoh_buf;
-    size_t o = 0;
-    auto take = [&](size_t sz) { char *p = d + o; o += (sz + 15) & ~(size_t)15; return p; };
-    GotohArgs A{};
-    int8_t *da = (int8_t *)take(m + 8), *db = (int8_t *)take(n + 8);
-    int *dm = (int *)take(sz_mat);
-    A.diagR = (int *)take(sizeof(int) * 3 * (m + 2));
-    A.diagP = (int *)take(sizeof(int) * 3 * (m + 2));
-    A.diagQ = (int *)take(sizeof(int) * 3 * (m + 2));
-    A.lastcol = (int *)take(sizeof(int) * (m + 2));
-    A.lastrow = (int *)take(sizeof(int) * (n + 2));
-    A.abc = (uint8_t *)take(cells);
-    A.de = (uint8_t *)take(cells);
-    A.fg = (uint8_t *)take(cells);
-    char *ds1 = take(m + 1), *ds2 = take(n + 1);
-    A.out1 = take(m + n + 1);
-    A.out2 = take(m + n + 1);
-    A.result = (int *)take(sz_res);
-    hipStream_t st = c.stream;
-    MH_HIP(hipMemsetAsync(A.abc, 0, 3 * ((cells + 15) & ~(size_t)15), st));
-    MH_HIP(hipMemcpyAsync(da, ha.data(), m, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(db, hb.data(), n, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(dm, matrix, sz_mat, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(ds1, s1, m, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(ds2, s2, n, hipMemcpyHostToDevice, st));
-    A.a = da; A.b = db; A.m = m; A.n = n; A.L = L; A.mat = dm;
-    A.u = gep; A.v = gop; A.is_global = is_global ? 1 : 0;
-    A.s1 = ds1; A.s2 = ds2;
-    hipLaunchKernelGGL(k_gotoh, dim3(1), dim3(1024), 0, st, A);
-    hipError_t e = hipGetLastError();
-    int res[3] = {0, 0, 0};
-    std::vector<char> t1(m + n + 1), t2(m + n + 1);
-    if (e == hipSuccess) e = hipMemcpyAsync(res, A.result, sizeof(res), hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e == hipSuccess && res[0] == 0) {
-        e = hipMemcpy(t1.data(), A.out1, res[2], hipMemcpyDeviceToHost);
-        if (e == hipSuccess) e = hipMemcpy(t2.data(), A.out2, res[2], hipMemcpyDeviceToHost);
+    std::vector<char> img(io[count], 0);   // host image of the io blocks
+    std::vector<GotohArgs> args(count);
+    for (int t = 0; t < count; ++t) {
+        const int m = ms[t], n = ns[t];
+        size_t o = io[t], w = off_work + work[t];
+        auto take_io = [&](size_t sz) { const size_t at = o; o += align16(sz); return at; };
+        auto take_w = [&](size_t sz) { char *at = d + w; w += align16(sz); return at; };
+        GotohArgs &A = args[t];
+        const size_t oa = take_io(m + 8), ob = take_io(n + 8), o1 = take_io(m + 1),
+                     o2 = take_io(n + 1), oo1 = take_io(m + n + 1), oo2 = take_io(m + n + 1),
+                     ores = take_io(64);
+        A.diagR = (int *)take_w(sizeof(int) * 3 * (m + 2));
+        A.diagP = (int *)take_w(sizeof(int) * 3 * (m + 2));
+        A.diagQ = (int *)take_w(sizeof(int) * 3 * (m + 2));
+        A.lastcol = (int *)take_w(sizeof(int) * (m + 2));
+        A.lastrow = (int *)take_w(sizeof(int) * (n + 2));
+        const size_t cells = (size_t)(m + 2) * (n + 2);
+        A.abc = (uint8_t *)take_w(cells);
+        A.de = (uint8_t *)take_w(cells);
+        A.fg = (uint8_t *)take_w(cells);
+        for (int i = 0; i < m; ++i) img[oa + i] = (char)code[(unsigned char)s1[t][i]];
+        for (int j = 0; j < n; ++j) img[ob + j] = (char)code[(unsigned char)s2[t][j]];
+        memcpy(&img[o1], s1[t], m);
+        memcpy(&img[o2], s2[t], n);
+        A.a = (const int8_t *)(d + oa);
+        A.b = (const int8_t *)(d + ob);
+        A.s1 = d + o1;
+        A.s2 = d + o2;
+        A.out1 = d + oo1;
+        A.out2 = d + oo2;
+        A.result = (int *)(d + ores);
+        A.m = m; A.n = n; A.L = L; A.mat = (const int *)(d + off_mat);
+        A.u = gep; A.v = gop; A.is_global = is_global ? 1 : 0;
     }
+    hipStream_t st = c.stream;
+    MH_HIP(hipMemsetAsync(d + off_work, 0, work[count], st));
+    MH_HIP(hipMemcpyAsync(d, img.data(), io[count], hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(d + off_mat, matrix, sizeof(int) * L * L, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(d + off_args, args.data(), sizeof(GotohArgs) * count,
+                          hipMemcpyHostToDevice, st));
+    const int pg = prof_begin(c, "k_gotoh");
+    hipLaunchKernelGGL(k_gotoh, dim3((unsigned)count), dim3(1024), 0, st,
+                       (const GotohArgs *)(d + off_args));
+    prof_end(c, pg);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(img.data(), d, io[count], hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "k_gotoh");
-    if (res[0] != 0) { set_error("Traceback failed, try local alignment"); return -1; }
-    const int len = res[2];
-    for (int k = 0; k < len; ++k) { out1[k] = t1[len - 1 - k]; out2[k] = t2[len - 1 - k]; }
-    out1[len] = out2[len] = '\0';
-    *score = res[1];
+    for (int t = 0; t < count; ++t) {
+        const GotohArgs &A = args[t];
+        int res[3];
+        memcpy(res, &img[(const char *)A.result - d], sizeof(res));
+        status[t] = res[0] ? -1 : 0;
+        score[t] = res[1];
+        const int len = res[0] ? 0 : res[2];
+        const char *t1 = &img[A.out1 - d], *t2 = &img[A.out2 - d];
+        for (int k = 0; k < len; ++k) { out1[t][k] = t1[len - 1 - k]; out2[t][k] = t2[len - 1 - k]; }
+        out1[t][len] = out2[t][len] = '\0';
+    }
+    if (c.gotoh_cap > GOTOH_KEEP_BYTES) {
+        hipFree(c.gotoh_buf);
+        c.gotoh_buf = nullptr;
+        c.gotoh_cap = 0;
+    }
+    return 0;
+}
+
+int run_gotoh(Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_global,
+              const char *alphabet, const int *matrix, char *out1, char *out2, int cap, int *score)
+{
+    int status = 0;
+    if (int st = run_gotoh_batch(c, 1, &s1, &s2, gop, gep, is_global, alphabet, matrix, &out1,
+                                 &out2, &cap, score, &status))
+        return st;
+    if (status) { set_error("Traceback failed, try local alignment"); return -1; }
     return 0;
 }
 

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -158,6 +159,10 @@ int run_pileup(struct Ctx &c, int source, int q_cutoff);
 int run_gotoh(struct Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_global,
               const char *alphabet, const int *matrix, char *out1, char *out2, int cap,
               int *score);
+int run_gotoh_batch(struct Ctx &c, int count, const char *const *s1, const char *const *s2,
+                    int gop, int gep, int is_global, const char *alphabet, const int *matrix,
+                    char *const *out1, char *const *out2, const int *cap, int *score,
+                    int *status);
 
 struct ProfEntry {
     double ms = 0.0;
@@ -194,9 +199,12 @@ struct Ctx {
     A2CState **a2c = nullptr;        // aln2counts row tables (mh_a2c_*), one per slot
     int len_tab_mode = -1;
     // k_gotoh's device scratch (traceback planes etc.), grown on demand and
-    // kept: a hipMalloc / hipFree pair per alignment cost more than the kernel
+    // kept up to 1 GiB: a hipMalloc / hipFree pair per call cost more than
+    // the kernel.  The mutex serialises callers of one context (ctypes
+    // releases the GIL).
     char *gotoh_buf = nullptr;
     size_t gotoh_cap = 0;
+    std::mutex gotoh_mutex;
 };
 
 void set_error(const char *fmt, ...);

@@ -91,6 +91,10 @@ def _declare(L):
                             ctypes.c_int, ctypes.c_char_p, _P, ctypes.c_char_p, ctypes.c_char_p,
                             ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         'mh_levenshtein': ([ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
+        'mh_gotoh_align_batch': ([_P, ctypes.c_int, _P, _P, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_char_p, _P, _P, _P, _P, _P, _P],
+                                 ctypes.c_int),
+        'mh_levenshtein_batch': ([ctypes.c_int, _P, _P, _P], ctypes.c_int),
         'mh_sam2aln_csv': ([_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
                             _I64P], ctypes.c_int),
         'mh_sam2aln_output': ([_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
@@ -582,8 +586,49 @@ class Context:
         return o1.value.decode(), o2.value.decode(), score.value
 
 
+    def gotoh_align_many(self, pairs, gop, gep, is_global, alphabet, matrix):
+        """[(aligned1, aligned2, score)] for [(seq1, seq2)], one launch; a
+        pair whose traceback fails gives RuntimeError in its place."""
+        n = len(pairs)
+        if n == 0:
+            return []
+        s1 = (ctypes.c_char_p * n)(*[a.encode() for a, _ in pairs])
+        s2 = (ctypes.c_char_p * n)(*[b.encode() for _, b in pairs])
+        caps = np.array([len(a) + len(b) + 1 for a, b in pairs], dtype=np.int32)
+        o1 = [ctypes.create_string_buffer(int(c)) for c in caps]
+        o2 = [ctypes.create_string_buffer(int(c)) for c in caps]
+        p1 = (ctypes.c_char_p * n)(*[ctypes.cast(b, ctypes.c_char_p) for b in o1])
+        p2 = (ctypes.c_char_p * n)(*[ctypes.cast(b, ctypes.c_char_p) for b in o2])
+        score = np.zeros(n, dtype=np.int32)
+        status = np.zeros(n, dtype=np.int32)
+        mat = np.ascontiguousarray(matrix, dtype=np.int32)
+        check(lib().mh_gotoh_align_batch(self.h, n, ctypes.cast(s1, ctypes.c_void_p),
+                                         ctypes.cast(s2, ctypes.c_void_p), gop, gep,
+                                         int(is_global), alphabet.encode(), _ptr(mat),
+                                         ctypes.cast(p1, ctypes.c_void_p),
+                                         ctypes.cast(p2, ctypes.c_void_p), _ptr(caps),
+                                         _ptr(score), _ptr(status)),
+              'mh_gotoh_align_batch')
+        return [RuntimeError('Traceback failed, try local alignment') if status[t] else
+                (o1[t].value.decode(), o2[t].value.decode(), int(score[t])) for t in range(n)]
+
+
 def levenshtein(a, b):
     return lib().mh_levenshtein(a.encode(), b.encode())
+
+
+def levenshtein_many(pairs):
+    """[edit distance] for [(a, b)], pairs spread over host threads."""
+    n = len(pairs)
+    if n == 0:
+        return []
+    a = (ctypes.c_char_p * n)(*[x.encode() for x, _ in pairs])
+    b = (ctypes.c_char_p * n)(*[y.encode() for _, y in pairs])
+    out = np.zeros(n, dtype=np.int32)
+    check(lib().mh_levenshtein_batch(n, ctypes.cast(a, ctypes.c_void_p),
+                                     ctypes.cast(b, ctypes.c_void_p), _ptr(out)),
+          'mh_levenshtein_batch')
+    return [int(x) for x in out]
 
 
 def cigar_text(aln):

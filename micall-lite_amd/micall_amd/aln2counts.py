@@ -102,24 +102,40 @@ class _CoordinateAligner(object):
     def forget(self):
         self._memo.clear()
 
-    def align(self, seq1, seq2):
-        """(aligned seq1, aligned seq2, score); the checks of gotoh2.py:74-96
-        (str arguments, neither empty) raise AssertionError as there."""
+    @staticmethod
+    def _check(seq1, seq2):
+        # gotoh2.py:74-96 asserts these (AssertionError as there)
         for name, seq in (('seq1', seq1), ('seq2', seq2)):
             if type(seq) is not str:
                 raise AssertionError('%s must be a string' % name)
             if not seq:
                 raise AssertionError('%s cannot be an empty string' % name)
-        found = self._memo.get((seq1, seq2))
-        if found is None:
-            a, b = (self._outside.sub('?', s.upper()) for s in (seq1, seq2))
-            found = session.context().gotoh_align(a, b, self.gap_open_penalty,
-                                                  self.gap_extend_penalty, self.is_global,
-                                                  self.alphabet, self.matrix)
-            if len(self._memo) >= self.MEMO_LIMIT:
+
+    def align(self, seq1, seq2):
+        """(aligned seq1, aligned seq2, score)."""
+        return self.align_many([(seq1, seq2)])[0]
+
+    def align_many(self, pairs):
+        """align() of every pair; the pairs not seen before go to the device
+        in one launch (mh_gotoh_align_batch).  A pair that fails raises, in
+        pair order."""
+        for seq1, seq2 in pairs:
+            self._check(seq1, seq2)
+        todo = list(dict.fromkeys(p for p in pairs if p not in self._memo))
+        if todo:
+            found = session.context().gotoh_align_many(
+                [(self._outside.sub('?', a.upper()), self._outside.sub('?', b.upper()))
+                 for a, b in todo],
+                self.gap_open_penalty, self.gap_extend_penalty, self.is_global, self.alphabet,
+                self.matrix)
+            if len(self._memo) + len(todo) > self.MEMO_LIMIT:
                 self._memo.clear()
-            self._memo[(seq1, seq2)] = found
-        return found
+            self._memo.update(zip(todo, found))
+        out = [self._memo[p] for p in pairs]
+        for result in out:
+            if isinstance(result, Exception):
+                raise result
+        return out
 
 
 aligner = _CoordinateAligner(GAP_OPEN_COORD, GAP_EXTEND_COORD, False, 'EmpHIV25')
@@ -305,6 +321,14 @@ class SequenceReport(object):
         test doubles override this one method."""
         return aligner.align(_text(reference), _text(query))
 
+    def _pair_align_many(self, pairs):
+        """_pair_align of every (reference, query) pair: one device launch,
+        unless a subclass (a test double) replaces _pair_align, which then
+        answers each pair in turn."""
+        if type(self)._pair_align is not SequenceReport._pair_align:
+            return [self._pair_align(r, q) for r, q in pairs]
+        return aligner.align_many([(_text(r), _text(q)) for r, q in pairs])
+
     # ---- reading a run ----
     def read(self, aligned_reads):
         """Start over with the rows given (dicts with refname, qcut, count,
@@ -349,69 +373,81 @@ class SequenceReport(object):
                 codons = -(-len(self.projects.getReference(self.seed)) // 3)
                 frame0 = self._frames[0]
                 self.seed_aminos[0] = _FrameAminos(frame0, max(frame0.ncod, codons))
-        for name, coordinate_ref in self.coordinate_refs.items():
-            self._locate(name, _text(coordinate_ref))
+        if self.coordinate_refs:
+            self._locate_all({name: _text(ref) for name, ref in self.coordinate_refs.items()})
 
-    def _best_frame(self, name, coordinate_ref):
-        """The reading frame whose amino-acid consensus aligns to the
-        coordinate reference with a score above min(covered codons, length
-        of the reference); None if no frame does."""
-        bar = min(int(self._frames[0].has.sum()), len(coordinate_ref))
-        best = None
-        for frame in self.seed_aminos:
-            consensus = self._frames[frame].consensus()
-            if frame == 0:
-                self.consensus[name] = consensus      # kept if no frame aligns
-            score = self._pair_align(coordinate_ref, consensus)[2]
-            if score > bar:
-                bar, best = score, (frame, consensus)
-        return best
-
-    def _seed_in_coordinates(self, coordinate_ref):
-        """The seed's translation in its best-aligning frame and the map
-        {coordinate index: seed amino index}."""
-        seed_nucs = self.projects.getReference(self.seed)
-        best_score, best = 0, None
-        for offset in range(3):
-            aminos = translate(seed_nucs, offset=offset, ambig_char='-')
-            aligned_seed, aligned_ref, score = self._pair_align(aminos, coordinate_ref)
-            if score > best_score:
-                best_score, best = score, (aminos, aligned_seed, aligned_ref)
-        aminos, aligned_seed, aligned_ref = best   # TypeError if none scored, as the reference
-        return aminos, _index_map(aligned_seed, aminos, aligned_ref, coordinate_ref)
-
-    def _locate(self, name, coordinate_ref):
-        """Coordinate position -> seed position -> consensus codon
-        (aln2counts.py:191-304)."""
-        report, cmap = [], _CoordinateMap()
-        chosen = self._best_frame(name, coordinate_ref)
-        if chosen is not None:
-            frame, consensus = chosen
-            self.reading_frames[name] = frame
-            self.consensus[name] = consensus
-            seed_aminos, ref_to_seed = self._seed_in_coordinates(coordinate_ref)
-            aligned_seed, aligned_conseq, _ = self._pair_align(seed_aminos, consensus)
-            # the aligner pads the left of a local alignment with '?'
-            seed_to_conseq = _index_map(aligned_conseq.replace('?', '-'), consensus,
-                                        aligned_seed, seed_aminos)
-            unplaced = set(range(len(consensus)))
-            self.inserts[name] = unplaced
-            blank = SeedAmino(None)
-            index, positions = [], []
-            for ref_index in sorted(ref_to_seed):
-                k = seed_to_conseq.get(ref_to_seed[ref_index])
-                if k is None:
-                    index.append(-1)
-                    amino = blank
-                else:
-                    index.append(k)
-                    amino = _LazySeedAmino(self._frames[frame], k)
-                    unplaced.remove(k)
-                positions.append(ref_index + 1)
-                report.append(ReportAmino(amino, ref_index + 1))
-            cmap = _CoordinateMap(frame, index, positions)
-        self.reports[name] = report
-        self._coord_maps[name] = cmap
+    def _locate_all(self, refs):
+        """Coordinate position -> seed position -> consensus codon for every
+        coordinate region of the seed (aln2counts.py:191-304), the regions'
+        alignments batched in three launches:
+          1. every frame's amino-acid consensus against every coordinate
+             reference: a region's frame is the one scoring above
+             min(covered codons, reference length), best first;
+          2. the seed's three translations against each located region's
+             reference: the best one maps coordinate -> seed positions;
+          3. that translation against the chosen consensus: seed ->
+             consensus positions."""
+        frames = list(self.seed_aminos)
+        conseqs = [self._frames[f].consensus() for f in frames]
+        covered = int(self._frames[0].has.sum())
+        for name in refs:
+            self.consensus[name] = conseqs[0]           # kept if no frame aligns
+        scores = iter(r[2] for r in self._pair_align_many(
+            [(refs[name], c) for name in refs for c in conseqs]))
+        chosen = {}
+        for name, ref in refs.items():
+            bar = min(covered, len(ref))
+            for f, c in zip(frames, conseqs):
+                score = next(scores)
+                if score > bar:
+                    bar, chosen[name] = score, (f, c)
+        placed = {}
+        if chosen:
+            seed_nucs = self.projects.getReference(self.seed)
+            translations = [translate(seed_nucs, offset=o, ambig_char='-') for o in range(3)]
+            found = iter(self._pair_align_many(
+                [(t, refs[name]) for name in chosen for t in translations]))
+            for name in chosen:
+                best_score, best = 0, None
+                for t in translations:
+                    aligned_seed, aligned_ref, score = next(found)
+                    if score > best_score:
+                        best_score, best = score, (t, aligned_seed, aligned_ref)
+                t, aligned_seed, aligned_ref = best   # TypeError if none scored, as the reference
+                placed[name] = (t, _index_map(aligned_seed, t, aligned_ref, refs[name]))
+            final = self._pair_align_many([(placed[name][0], chosen[name][1]) for name in chosen])
+        else:
+            final = []
+        blank = SeedAmino(None)
+        finals = dict(zip(chosen, final))
+        for name in refs:
+            report, cmap = [], _CoordinateMap()
+            if name in chosen:
+                frame, consensus = chosen[name]
+                self.reading_frames[name] = frame
+                self.consensus[name] = consensus
+                seed_aminos, ref_to_seed = placed[name]
+                aligned_seed, aligned_conseq, _ = finals[name]
+                # the aligner pads the left of a local alignment with '?'
+                seed_to_conseq = _index_map(aligned_conseq.replace('?', '-'), consensus,
+                                            aligned_seed, seed_aminos)
+                unplaced = set(range(len(consensus)))
+                self.inserts[name] = unplaced
+                index, positions = [], []
+                for ref_index in sorted(ref_to_seed):
+                    k = seed_to_conseq.get(ref_to_seed[ref_index])
+                    if k is None:
+                        index.append(-1)
+                        amino = blank
+                    else:
+                        index.append(k)
+                        amino = _LazySeedAmino(self._frames[frame], k)
+                        unplaced.remove(k)
+                    positions.append(ref_index + 1)
+                    report.append(ReportAmino(amino, ref_index + 1))
+                cmap = _CoordinateMap(frame, index, positions)
+            self.reports[name] = report
+            self._coord_maps[name] = cmap
 
     def _gather(self, cmap, table, shape):
         """Rows of a per-codon counter table at the map's consensus codons

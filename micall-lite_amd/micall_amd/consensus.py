@@ -181,32 +181,52 @@ def clean_sequence(seq, alphabet=HYPHY_NUC_ALPHABET):
 
 def filter_conseqs(ctx, pile, order, new_conseqs, seeds, filter_coverage, distance_report=None):
     """The consensus-distance filter of remap.sam_to_conseqs (:228-268).
-    Alignments run on the GPU (mh_gotoh_align)."""
+
+    For every consensus (name order) its well-covered positions -- where the
+    position's counts, sentinels included, sum to at least filter_coverage
+    -- are aligned to every seed (global Gotoh, gop 15 / gep 3, HYPHY_NUC);
+    the edit distance to the part of each seed they cover decides: a
+    consensus stays when its own seed is no farther than the nearest other
+    one.  If none stays, the one with the most merged pairs does.  All the
+    K x K alignments are one device launch (mh_gotoh_align_batch), the edit
+    distances one host call spread over threads."""
     from . import _native
     if not seeds or len(new_conseqs) < 2:
         return new_conseqs
     index = {pile.refnames[r]: r for r in order}
-    filtered = {}
-    for name in sorted(new_conseqs):
+    names = sorted(new_conseqs)
+    relevant = {}
+    for name in names:
         conseq = new_conseqs[name]
-        r = index[name]
-        sums = pile.position_sums(r, seeds.get(name), len(conseq))
-        keep = sums >= filter_coverage
-        relevant = ''.join(c for c, k in zip(conseq, keep) if k)
-        if not relevant:
+        keep = pile.position_sums(index[name], seeds.get(name), len(conseq)) >= filter_coverage
+        covered = ''.join(c for c, k in zip(conseq, keep) if k)
+        if covered:
+            relevant[name] = covered
+    jobs = [(name, seed_name) for name in names if name in relevant for seed_name in names]
+    aligned = ctx.gotoh_align_many(
+        [(clean_sequence(seeds[seed_name]), clean_sequence(relevant[name]))
+         for name, seed_name in jobs], FILTER_GOP, FILTER_GEP, True, HYPHY_NUC_ALPHABET, HYPHY_NUC)
+    for result in aligned:
+        if isinstance(result, Exception):
+            raise result
+    dists = _native.levenshtein_many(
+        [(extract_relevant_seed(a_conseq, a_seed), relevant[name])
+         for (name, _seed), (a_seed, a_conseq, _score) in zip(jobs, aligned)])
+    per_name = {}
+    for (name, seed_name), d in zip(jobs, dists):
+        per_name.setdefault(name, []).append((seed_name, d))
+    filtered = {}
+    for name in names:
+        if name not in relevant:
             continue
-        other_seed = other_dist = seed_dist = None
-        for seed_name in sorted(new_conseqs):
-            a_seed, a_conseq, _ = ctx.gotoh_align(clean_sequence(seeds[seed_name]),
-                                                  clean_sequence(relevant), FILTER_GOP, FILTER_GEP,
-                                                  True, HYPHY_NUC_ALPHABET, HYPHY_NUC)
-            d = _native.levenshtein(extract_relevant_seed(a_conseq, a_seed), relevant)
+        seed_dist = other_dist = other_seed = None
+        for seed_name, d in per_name[name]:
             if seed_name == name:
                 seed_dist = d
             elif other_dist is None or d < other_dist:
                 other_seed, other_dist = seed_name, d
         if seed_dist <= other_dist:
-            filtered[name] = conseq
+            filtered[name] = new_conseqs[name]
         if distance_report is not None:
             distance_report[name] = dict(seed_dist=seed_dist, other_dist=other_dist,
                                          other_seed=other_seed)

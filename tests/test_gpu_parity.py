@@ -254,6 +254,28 @@ def test_gotoh_vs_golden(ctx, golden_dir):
         assert ctx.gotoh_align(*args) == want, c
 
 
+def test_gotoh_batch_vs_golden(ctx, golden_dir):
+    """Every golden case with the same scoring in one mh_gotoh_align_batch
+    launch (one workgroup each): the same strings, scores and traceback
+    failures as the oracle (pinned on these cases, test_oracle_gotoh.py)."""
+    with open(os.path.join(golden_dir, 'gotoh_golden.json')) as f:
+        cases = json.load(f)['cases']
+    groups = {}
+    for c in cases:
+        key = (c['gop'], c['gep'], c['is_global'], c['alphabet'], tuple(c['matrix']))
+        groups.setdefault(key, []).append(c)
+    assert max(len(g) for g in groups.values()) > 20
+    for (gop, gep, is_global, alphabet, matrix), group in groups.items():
+        got = ctx.gotoh_align_many([(c['seq1'], c['seq2']) for c in group], gop, gep, is_global,
+                                   alphabet, list(matrix))
+        for c, g in zip(group, got):
+            if c['error']:
+                assert isinstance(g, RuntimeError), c
+            else:
+                assert g == oracle.gotoh_align(c['seq1'], c['seq2'], gop, gep, is_global, alphabet,
+                                               list(matrix)), c
+
+
 def test_gotoh_pol_sized(ctx):
     """A 3,039 x ~2,900 global alignment (the remap filter's size) vs oracle."""
     rng = np.random.default_rng(3)
