@@ -197,6 +197,19 @@ int mh_pileup_export(mh_ctx *ctx, int n_sel, const int32_t *sel, int64_t unit_ba
                      void *dev_sum, void *dev_max, void *dev_flags);
 int mh_pileup_import(mh_ctx *ctx, int n_sel, const int32_t *sel, const void *dev_sum,
                      const void *dev_max, const void *dev_flags);
+/* Insertion-token events across ranks (the sparse side table of the pileup):
+ * mh_pileup_event_bytes gives this rank's raw event count and pool bytes;
+ * mh_pileup_events_export copies them (4 int32 per event, then the bytes)
+ * into caller device buffers; after an all-gather of those buffers,
+ * mh_pileup_events_import replaces the rank's events by the concatenation of
+ * `parts` parts (part p at dev_events + p * events_stride int32 words and
+ * dev_pool + p * pool_stride bytes), so mh_pileup_events aggregates every
+ * rank's tokens. */
+int mh_pileup_event_bytes(mh_ctx *ctx, int64_t *n_events, int64_t *pool_bytes);
+int mh_pileup_events_export(mh_ctx *ctx, void *dev_events, void *dev_pool);
+int mh_pileup_events_import(mh_ctx *ctx, int parts, const int64_t *n_events,
+                            const int64_t *pool_bytes, const void *dev_events,
+                            int64_t events_stride, const void *dev_pool, int64_t pool_stride);
 
 /* ---- sam2aln: replaces sam2aln.sam2aln (sam2aln.py:395-478) ----------- */
 /* remap.csv text (the SAM columns remap() writes) read as DictReader does,

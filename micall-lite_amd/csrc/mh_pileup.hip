@@ -936,3 +936,107 @@ extern "C" int mh_pileup_import(mh_ctx *ctx, int n_sel, const int32_t *sel, cons
     MH_HIP(hipStreamSynchronize(c.stream));
     return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Multi-GPU exchange of the raw insertion-token events (ref, pos, tok_off,
+// tok_len) + their byte pool: each rank exports its events into a caller
+// device buffer, the caller all-gathers the buffers (RCCL), and every rank
+// imports the concatenation (rank order).  The token aggregation of
+// mh_pileup_events then runs over every rank's events.  Nothing of the
+// exchange goes through the host.
+// ---------------------------------------------------------------------------
+namespace mh {
+
+__global__ void k_ev_rebase(int32_t *ev, int64_t first, int64_t n, int32_t pool_base)
+{
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)gridDim.x * blockDim.x)
+        ev[4 * (first + e) + 2] += pool_base;
+}
+
+}  // namespace mh
+
+extern "C" int mh_pileup_event_bytes(mh_ctx *ctx, int64_t *n_events, int64_t *pool_bytes)
+{
+    if (!ctx) return -3;
+    Ctx &c = *reinterpret_cast<Ctx *>(ctx);
+    PileState &P = c.pile;
+    int64_t ctr[4] = {0, 0, 0, 0};
+    MH_HIP(hipSetDevice(c.device));
+    if (P.ev_counters) MH_HIP(hipMemcpy(ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
+    if (n_events) *n_events = ctr[0];
+    if (pool_bytes) *pool_bytes = ctr[1];
+    return 0;
+}
+
+extern "C" int mh_pileup_events_export(mh_ctx *ctx, void *dev_events, void *dev_pool)
+{
+    if (!ctx) return -3;
+    Ctx &c = *reinterpret_cast<Ctx *>(ctx);
+    PileState &P = c.pile;
+    int64_t n = 0, bytes = 0;
+    if (int st = mh_pileup_event_bytes(ctx, &n, &bytes)) return st;
+    if ((n > 0 && !dev_events) || (bytes > 0 && !dev_pool)) return -3;
+    if (n > 0) MH_HIP(hipMemcpyAsync(dev_events, P.ev, sizeof(int32_t) * 4 * n,
+                                     hipMemcpyDeviceToDevice, c.stream));
+    if (bytes > 0) MH_HIP(hipMemcpyAsync(dev_pool, P.ev_pool, bytes, hipMemcpyDeviceToDevice, c.stream));
+    MH_HIP(hipStreamSynchronize(c.stream));
+    return 0;
+}
+
+extern "C" int mh_pileup_events_import(mh_ctx *ctx, int parts, const int64_t *n_events,
+                                       const int64_t *pool_bytes, const void *dev_events,
+                                       int64_t events_stride, const void *dev_pool,
+                                       int64_t pool_stride)
+{
+    if (!ctx || parts < 0 || (parts > 0 && (!n_events || !pool_bytes))) return -3;
+    Ctx &c = *reinterpret_cast<Ctx *>(ctx);
+    PileState &P = c.pile;
+    int64_t tot_n = 0, tot_b = 0;
+    for (int p = 0; p < parts; ++p) {
+        if (n_events[p] < 0 || pool_bytes[p] < 0 || 4 * n_events[p] > events_stride ||
+            pool_bytes[p] > pool_stride) { set_error("mh_pileup_events_import: bad part %d", p); return -3; }
+        tot_n += n_events[p];
+        tot_b += pool_bytes[p];
+    }
+    if ((tot_n > 0 && !dev_events) || (tot_b > 0 && !dev_pool)) return -3;
+    if (tot_b >= INT32_MAX) { set_error("mh_pileup_events_import: pool too large"); return -2; }
+    MH_HIP(hipSetDevice(c.device));
+    if (P.ev_cap < tot_n || !P.ev) {
+        hipFree(P.ev);
+        P.ev_cap = tot_n * 2 + 1024;
+        MH_HIP(hipMalloc(&P.ev, sizeof(int32_t) * 4 * P.ev_cap));
+    }
+    if (P.pool_cap < tot_b || !P.ev_pool) {
+        hipFree(P.ev_pool);
+        P.pool_cap = tot_b * 2 + 4096;
+        MH_HIP(hipMalloc(&P.ev_pool, P.pool_cap));
+    }
+    if (!P.ev_counters) MH_HIP(hipMalloc(&P.ev_counters, sizeof(int64_t) * 4));
+    int64_t at_n = 0, at_b = 0;
+    for (int p = 0; p < parts; ++p) {
+        const int32_t *src_e = (const int32_t *)dev_events + (size_t)p * events_stride;
+        const char *src_b = (const char *)dev_pool + (size_t)p * pool_stride;
+        if (n_events[p] > 0) {
+            MH_HIP(hipMemcpyAsync(P.ev + 4 * at_n, src_e, sizeof(int32_t) * 4 * n_events[p],
+                                  hipMemcpyDeviceToDevice, c.stream));
+            if (at_b > 0) {
+                int64_t blocks = (n_events[p] + 255) / 256;
+                if (blocks > 4096) blocks = 4096;
+                hipLaunchKernelGGL(k_ev_rebase, dim3((unsigned)blocks), dim3(256), 0, c.stream,
+                                   P.ev, at_n, n_events[p], (int32_t)at_b);
+                MH_HIP(hipGetLastError());
+            }
+        }
+        if (pool_bytes[p] > 0)
+            MH_HIP(hipMemcpyAsync(P.ev_pool + at_b, src_b, pool_bytes[p], hipMemcpyDeviceToDevice,
+                                  c.stream));
+        at_n += n_events[p];
+        at_b += pool_bytes[p];
+    }
+    const int64_t ctr[4] = {tot_n, tot_b, 0, 0};
+    MH_HIP(hipMemcpyAsync(P.ev_counters, ctr, sizeof(ctr), hipMemcpyHostToDevice, c.stream));
+    MH_HIP(hipStreamSynchronize(c.stream));
+    ++P.gen;   // the aggregated tokens are recomputed from the new events
+    return 0;
+}

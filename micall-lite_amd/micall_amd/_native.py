@@ -95,6 +95,10 @@ def _declare(L):
                                   ctypes.c_int, ctypes.c_char_p, _P, _P, _P, _P, _P, _P],
                                  ctypes.c_int),
         'mh_levenshtein_batch': ([ctypes.c_int, _P, _P, _P], ctypes.c_int),
+        'mh_pileup_event_bytes': ([_P, _P, _P], ctypes.c_int),
+        'mh_pileup_events_export': ([_P, _P, _P], ctypes.c_int),
+        'mh_pileup_events_import': ([_P, ctypes.c_int, _P, _P, _P, ctypes.c_int64, _P,
+                                     ctypes.c_int64], ctypes.c_int),
         'mh_sam2aln_csv': ([_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
                             _I64P], ctypes.c_int),
         'mh_sam2aln_output': ([_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
@@ -563,6 +567,27 @@ class Context:
               'mh_pileup_import')
 
     # ---- kernel timing ---------------------------------------------------
+    def pileup_event_bytes(self):
+        """(raw insertion-token events, pool bytes) of the last pileup."""
+        n, b = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().mh_pileup_event_bytes(self.h, ctypes.byref(n), ctypes.byref(b)),
+              'mh_pileup_event_bytes')
+        return n.value, b.value
+
+    def pileup_events_export(self, dev_events_ptr, dev_pool_ptr):
+        check(lib().mh_pileup_events_export(self.h, ctypes.c_void_p(dev_events_ptr),
+                                            ctypes.c_void_p(dev_pool_ptr)),
+              'mh_pileup_events_export')
+
+    def pileup_events_import(self, n_events, pool_bytes, dev_events_ptr, events_stride,
+                             dev_pool_ptr, pool_stride):
+        n = np.ascontiguousarray(n_events, dtype=np.int64)
+        b = np.ascontiguousarray(pool_bytes, dtype=np.int64)
+        check(lib().mh_pileup_events_import(self.h, len(n), _ptr(n), _ptr(b),
+                                            ctypes.c_void_p(dev_events_ptr), int(events_stride),
+                                            ctypes.c_void_p(dev_pool_ptr), int(pool_stride)),
+              'mh_pileup_events_import')
+
     def profile(self, enable=True):
         check(lib().mh_profile(self.h, int(enable)), 'mh_profile')
 

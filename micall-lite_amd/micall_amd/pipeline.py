@@ -69,12 +69,27 @@ class Shard:
         out = t.cpu().numpy()
         return np.where(out == np.iinfo(np.int64).max, -1, out)
 
+    def _gather(self, t):
+        """all_gather of one equal-shaped tensor per rank, concatenated in rank
+        order."""
+        parts = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return self.torch.cat(parts)
+
+    def _gather_sizes(self, values):
+        t = self.torch.as_tensor(np.asarray(values, dtype=np.int64), device=self.device)
+        return self._gather(t).cpu().numpy().reshape(self.world, len(values))
+
     def pileup(self, ctx, unit_base):
-        """All-reduce the device counters in place and gather the insertion
-        tokens.  Ranks first agree (MAX of a per-reference flag) on the
-        references that hold data anywhere; only their rows travel: dense
-        counts and read counts summed, N/deletion flags as bytes under MAX
-        (an OR of 0/1), max_pos and the negated global first unit under MAX."""
+        """All-reduce the device counters in place and all-gather the
+        insertion-token events.  Ranks first agree (MAX of a per-reference
+        flag) on the references that hold data anywhere; only their rows
+        travel: dense counts and read counts summed, N/deletion flags as bytes
+        under MAX (an OR of 0/1), max_pos and the negated global first unit
+        under MAX.  The events (4 int32 + token bytes each) are padded to the
+        largest rank's size and all-gathered, then imported in rank order, so
+        the token aggregation sees every rank's events.  No host objects are
+        exchanged."""
         torch = self.torch
         dev = self.device
         if dev.type == 'cuda':
@@ -93,14 +108,45 @@ class Shard:
                 self.dist.all_reduce(f, op=self.dist.ReduceOp.MAX)
             torch.cuda.synchronize(dev)
             ctx.pileup_import(sel, s.data_ptr(), m.data_ptr(), f.data_ptr())
-            fetched = ctx.pileup_fetch()
-        else:  # CPU collective (tests): go through host copies
-            fetched = ctx.pileup_fetch()
-            fetched = reduce_fetched_host(self, fetched, unit_base)
-        events = [None] * self.world
-        self.dist.all_gather_object(events, fetched['events'])
-        fetched['events'] = [e for part in events for e in part]
+            sizes = self._gather_sizes(ctx.pileup_event_bytes())
+            n_max, b_max = max(int(sizes[:, 0].max()), 1), max(int(sizes[:, 1].max()), 1)
+            ev = torch.zeros(4 * n_max, dtype=torch.int32, device=dev)
+            pool = torch.zeros(b_max, dtype=torch.uint8, device=dev)
+            ctx.pileup_events_export(ev.data_ptr(), pool.data_ptr())
+            ev_all, pool_all = self._gather(ev), self._gather(pool)
+            torch.cuda.synchronize(dev)
+            ctx.pileup_events_import(sizes[:, 0], sizes[:, 1], ev_all.data_ptr(), 4 * n_max,
+                                     pool_all.data_ptr(), b_max)
+            return ctx.pileup_fetch()
+        # CPU collective (tests): the same exchange over host copies
+        fetched = reduce_fetched_host(self, ctx.pileup_fetch(), unit_base)
+        fetched['events'] = self._gather_events(fetched['events'])
         return fetched
+
+    def _gather_events(self, events):
+        """(ref, pos, token, count) tuples of every rank, rank order, through
+        fixed-size tensors: 4 int64 per event (ref, pos, count, token length)
+        and the token bytes."""
+        torch = self.torch
+        meta = np.array([(r, p, n, len(t)) for r, p, t, n in events], dtype=np.int64).reshape(-1, 4)
+        blob = np.frombuffer(''.join(t for _r, _p, t, _n in events).encode(), dtype=np.uint8)
+        sizes = self._gather_sizes([len(meta), len(blob)])
+        n_max, b_max = max(int(sizes[:, 0].max()), 1), max(int(sizes[:, 1].max()), 1)
+        m = np.zeros((n_max, 4), dtype=np.int64)
+        m[:len(meta)] = meta
+        b = np.zeros(b_max, dtype=np.uint8)
+        b[:len(blob)] = blob
+        m_all = self._gather(torch.as_tensor(m, device=self.device)).cpu().numpy()
+        b_all = self._gather(torch.as_tensor(b, device=self.device)).cpu().numpy()
+        out = []
+        for k in range(self.world):
+            rows = m_all[k * n_max:k * n_max + int(sizes[k, 0])]
+            text = b_all[k * b_max:k * b_max + int(sizes[k, 1])].tobytes().decode()
+            at = 0
+            for r, p, n, ln in rows.tolist():
+                out.append((r, p, text[at:at + ln], n))
+                at += ln
+        return out
 
 
 def reduce_fetched_host(shard, f, unit_base):
