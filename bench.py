@@ -179,8 +179,10 @@ def read_pmc_traffic(kernel, pairs, stage='remap'):
     summary of this stage (separate --pmc passes, FETCH_SIZE doubled per the
     gfx950 rule; profiles/collect_pmc_stages.sh), when it was measured on the
     same per-GPU pair count."""
-    name = 'pmc_traffic.json' if stage == 'remap' else 'pmc_traffic_{}.json'.format(stage)
-    path = os.path.join(REPO, 'profiles', name)
+    if stage == 'remap':
+        path = os.path.join(REPO, 'profiles', 'r02', 'c2', 'pmc_traffic.json')
+    else:
+        path = os.path.join(REPO, 'profiles', 'pmc_traffic_{}.json'.format(stage))
     try:
         with open(path) as f:
             d = json.load(f)
@@ -198,13 +200,16 @@ VALU_ISSUE_CYCLES = 2      # MI355X_MICROARCH.md: a wave64 VALU instruction issu
 def read_valu_issue(kernel, pairs, avg_launch_ms):
     """Issue-side roofline of `kernel` (it is bound by integer VALU issue and
     its dependency chain, not HBM): VALU wave-instructions per launch from the
-    committed SQ_INSTS_VALU pass (profiles/r01/remap/sq_issue.json, same
-    per-GPU pair count), over this run's average launch time, against 1024
-    SIMDs x the measured clock / VALU_ISSUE_CYCLES."""
-    path = os.path.join(REPO, 'profiles', 'r01', 'remap', 'sq_issue.json')
+    committed SQ_INSTS_VALU pass (profiles/r02/c2/sq_issue.json, same
+    per-GPU pair count; the mate-rescue DP launch, the one after k_rescue, is
+    left out), over this run's average launch time, against 1024 SIMDs x the
+    measured clock / VALU_ISSUE_CYCLES."""
+    path = os.path.join(REPO, 'profiles', 'r02', 'c2', 'sq_issue.json')
     try:
         with open(path) as f:
-            d = [x for x in json.load(f)['dispatches'] if x['kernel'] == kernel]
+            every = json.load(f)['dispatches']
+        d = [x for k, x in enumerate(every) if x['kernel'] == kernel and
+             not (k and every[k - 1]['kernel'] == 'k_rescue')]
         if not d or pairs != 1000000 or avg_launch_ms <= 0:
             return None
         insts = sum(x['valu_insts'] for x in d) / len(d)
@@ -213,7 +218,7 @@ def read_valu_issue(kernel, pairs, avg_launch_ms):
         peak = 1024 * clk / VALU_ISSUE_CYCLES
         return {'unit': 'G wave-instr/s', 'valu_insts_per_launch': insts, 'achieved': round(achieved, 1),
                 'peak': round(peak, 1), 'frac': round(achieved / peak, 4), 'clock_ghz': round(clk, 3),
-                'source': 'profiles/r01/remap/sq_issue.json (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)'}
+                'source': 'profiles/r02/c2/sq_issue.json (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)'}
     except (OSError, KeyError, ValueError):
         return None
 

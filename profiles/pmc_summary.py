@@ -8,6 +8,9 @@ doubled: hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Reads that are
 narrower than 16 B/lane are not calibrated by that rule; the doubled figure
 is an upper estimate for them.
 
+A k_dp dispatch that follows a k_rescue dispatch is the mate-rescue DP
+launch and is reported as k_dp_rescue (same kernel, different work).
+
 usage: pmc_summary.py FETCH_CSV WRITE_CSV PAIRS OUT_JSON
 """
 import csv
@@ -17,11 +20,18 @@ from collections import defaultdict
 
 
 def per_kernel(path, counter):
-    acc = defaultdict(list)
+    rows = {}
     with open(path) as f:
         for row in csv.DictReader(f):
             if row['Counter_Name'] == counter:
-                acc[row['Kernel_Name']].append(float(row['Counter_Value']))
+                rows[int(row['Dispatch_Id'])] = (row['Kernel_Name'], float(row['Counter_Value']))
+    acc = defaultdict(list)
+    prev = None
+    for d in sorted(rows):
+        name, value = rows[d]
+        label = 'k_dp_rescue' if name == 'k_dp' and prev == 'k_rescue' else name
+        acc[label].append(value)
+        prev = name
     return acc
 
 
