@@ -44,6 +44,9 @@ __device__ __forceinline__ int scan_max(int x)
 
 struct RowK { int mexI, moeI, xD, cF; };
 
+// AB (ablation, timing only): bit 0 drops the traceback bits, bit 1 the best-cell
+// key, bit 2 replaces the 6-step prefix-max scan by one neighbour step
+template <int AB>
 __device__ __forceinline__ void row_gap(uint32_t tbv, int rc, int &Hp, int &Ep, uint32_t &bestKey,
                                         int ci, const RowK &K, uint32_t &acc)
 {
@@ -53,14 +56,19 @@ __device__ __forceinline__ void row_gap(uint32_t tbv, int rc, int &Hp, int &Ep, 
     const int E = imax(e1, h1);
     int H1 = imax(imax(Hd, E), BIAS);
     const int X = H1 + K.xD;
-    const int P = scan_max(X);
+    const int P = (AB & 4) ? imax(X, dppz<ROW_SHR1>(X)) : scan_max(X);
     const int F = dppz<WAVE_SHR1>(P) + K.cF;
     const int H = imax(H1, F);
-    const uint32_t key = (uint32_t)H * 1024u + (uint32_t)ci;
-    bestKey = bestKey > key ? bestKey : key;
+    if (!(AB & 2)) {
+        const uint32_t key = (uint32_t)H * 1024u + (uint32_t)ci;
+        bestKey = bestKey > key ? bestKey : key;
+    } else {
+        bestKey = bestKey > (uint32_t)H ? bestKey : (uint32_t)H;
+    }
     uint64_t ma, mb, mz, me, mf;
     int xl;
-    asm volatile(
+    if (AB & 1) acc += (uint32_t)(H ^ E ^ Hd);
+    else asm volatile(
         "v_cmp_ne_u32_e64 %[ma], %[H], %[Hd]\n\t"
         "v_cmp_ne_u32_e64 %[mb], %[H], %[E]\n\t"
         "v_cmp_ne_u32_e64 %[mz], %[bias], %[H]\n\t"
@@ -96,15 +104,21 @@ __device__ __forceinline__ void row_nogap(uint32_t tbv, int rc, int &Hp, int &Ep
     Ep = 0;
 }
 
-// tab: n_ext x ROWS u32; ref: n_ext x (ROWS + 72) bytes (code * 4)
+// tab: n_ext x ROWS u32; ref: n_ext x (ROWS + 72) bytes (code * 4).
+// GB = 0: traceback bits in LDS (the r02 layout, 9.5 KB per wave, 4 waves
+// per SIMD); GB = 1: bits in a per-wave global slab (LDS 1.3 KB per wave, the
+// VGPR count sets the occupancy).  After the DP a serial walk reads 32
+// dependent traceback words, like the real traceback does.
+template <int GB, int AB = 0>
 __global__ __launch_bounds__(256) void k_rows(const uint32_t *gtab, const uint8_t *gref, int n_ext,
-                                              int *out)
+                                              int *out, uint32_t *gbits)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    unsigned char *wb = smem + wv * (ROWS / 8 * 64 * 4 + ROWS * 4 + ROWS + 72);
-    uint32_t *bits = (uint32_t *)wb;
-    uint32_t *tab = bits + ROWS / 8 * 64;
+    constexpr int WL = GB ? ROWS * 4 + ROWS + 72 : ROWS / 8 * 64 * 4 + ROWS * 4 + ROWS + 72;
+    unsigned char *wb = smem + wv * WL;
+    uint32_t *bits = GB ? gbits + (size_t)(blockIdx.x * 4 + wv) * (ROWS / 8 * 64) : (uint32_t *)wb;
+    uint32_t *tab = GB ? (uint32_t *)wb : (uint32_t *)wb + ROWS / 8 * 64;
     uint8_t *refw = (uint8_t *)(tab + ROWS);
     RowK K;
     K.mexI = in_vgpr(-EXI);
@@ -125,13 +139,13 @@ __global__ __launch_bounds__(256) void k_rows(const uint32_t *gtab, const uint8_
             uint32_t acc = 0;
             if (i0 >= GBAR && i0 + 8 <= M - GBAR) {
 #pragma unroll
-                for (int t = 0; t < 8; ++t) row_gap(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K, acc);
+                for (int t = 0; t < 8; ++t) row_gap<AB>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K, acc);
             } else {
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
                     const int i = i0 + t;
                     if (i >= M) acc <<= 4;
-                    else if (i >= GBAR && i < M - GBAR) row_gap(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K, acc);
+                    else if (i >= GBAR && i < M - GBAR) row_gap<AB>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K, acc);
                     else row_nogap(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, acc);
                 }
             }
@@ -141,159 +155,25 @@ __global__ __launch_bounds__(256) void k_rows(const uint32_t *gtab, const uint8_
         const int bestH = (int)(bestKey >> 10) - BIAS, bestI = 1023 - (int)(bestKey & 1023u);
         long long key = (long long)bestH * 1048576ll + (long long)((1023 - bestI) << 6) + (63 - lane);
         for (int o = 32; o; o >>= 1) { long long y = __shfl_xor(key, o); key = key > y ? key : y; }
+        if (GB) {   // the wave's own vector stores, visible to its loads below
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        } else {
+            __builtin_amdgcn_wave_barrier();
+        }
+        // serial walk: 32 dependent words from the best cell's group down
+        int k = __builtin_amdgcn_readfirstlane(63 - (int)(key & 63));
+        uint32_t sum = 0;
+        for (int g = __builtin_amdgcn_readfirstlane((1023 - (int)((key >> 6) & 1023)) >> 3); g >= 0; --g) {
+            const uint32_t word = __builtin_amdgcn_readfirstlane(bits[g * 64 + k]);
+            sum += word;
+            k = (k + (int)(word >> 31)) & 63;
+        }
         if (lane == 0) {
-            out[3 * x] = (int)(key >> 20);
-            out[3 * x + 1] = 1023 - (int)((key >> 6) & 1023);
-            out[3 * x + 2] = 63 - (int)(key & 63);
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// ------------------------------------------------------------------ anti-diagonals
-constexpr int BX = 1 << 14;
-constexpr int TSTEPS = M + 31;           // T = 0 .. M + 30
-constexpr int NW = (TSTEPS + 3) / 4;     // words of 8 steps per lane
-
-struct DiagK { int mexI, moeI, mexD, moeD; };
-
-// one step: cell (i, k); Hd from the lane's own previous cell of this parity;
-// E from (i-1, k+1) = (eE, hE) already shifted; F from (i, k-1) = (eF, hF)
-template <bool EDGE>
-__device__ __forceinline__ void diag_cell(int Hd, int e1, int h1, int f1, int g1, bool gap, bool valid,
-                                          int &Hr, int &Er, int &Fr, uint32_t keybase,
-                                          uint32_t &bestKey, uint32_t &acc)
-{
-    int E = imax(e1, h1), F = imax(f1, g1);
-    if (EDGE) {
-        E = gap ? E : 0;
-        F = gap ? F : 0;
-    }
-    const int H1 = imax(imax(Hd, E), BX);
-    const int H = imax(H1, F);
-    uint32_t key = ((uint32_t)H << 16) + keybase;
-    if (EDGE) key = valid ? key : 0u;
-    bestKey = bestKey > key ? bestKey : key;
-    uint64_t ma, mb, mz, me, mf;
-    const uint64_t gm = EDGE ? __builtin_amdgcn_ballot_w64(gap) : ~0ull;
-    asm volatile(
-        "v_cmp_ne_u32_e64 %[ma], %[H], %[Hd]\n\t"
-        "v_cmp_ne_u32_e64 %[mb], %[H], %[E]\n\t"
-        "v_cmp_ne_u32_e64 %[mz], %[bias], %[H]\n\t"
-        "v_cmp_lt_i32_e64 %[me], %[h1], %[e1]\n\t"
-        "v_cmp_lt_i32_e64 %[mf], %[g1], %[f1]\n\t"
-        "s_orn2_b64 %[mb], %[mb], %[ma]\n\t"
-        "s_and_b64 %[ma], %[ma], %[mz]\n\t"
-        "s_and_b64 %[mb], %[mb], %[mz]\n\t"
-        "s_and_b64 %[me], %[me], %[gm]\n\t"
-        "s_and_b64 %[mf], %[mf], %[gm]\n\t"
-        "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[mf]\n\t"
-        "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[me]\n\t"
-        "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[ma]\n\t"
-        "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[mb]"
-        : [acc] "+v"(acc), [ma] "=&s"(ma), [mb] "=&s"(mb), [mz] "=&s"(mz), [me] "=&s"(me),
-          [mf] "=&s"(mf)
-        : [H] "v"(H), [Hd] "v"(Hd), [E] "v"(E), [h1] "v"(h1), [e1] "v"(e1), [g1] "v"(g1),
-          [f1] "v"(f1), [bias] "s"(BX), [gm] "s"(gm)
-        : "vcc");
-    if (EDGE) {
-        if (valid) { Hr = H; Er = E; Fr = F; }
-    } else {
-        Hr = H; Er = E; Fr = F;
-    }
-}
-
-template <bool EDGE>
-__device__ __forceinline__ void diag_T(int T, int lp, bool lane31, bool lane32, const uint32_t *tabL,
-                                       const uint8_t *refL, int mL, const DiagK &K, int &He, int &Ee,
-                                       int &Fe, int &Ho, int &Eo, int &Fo, uint32_t kbe,
-                                       uint32_t &bestKey, uint32_t &acc)
-{
-    const int i = T - lp;
-    const uint32_t tabv = tabL[i];
-    const uint32_t rce = refL[T + lp], rco = refL[T + lp + 1];
-    const bool gap = EDGE ? (i >= GBAR && i < mL - GBAR) : true;
-    const bool valid = EDGE ? (i >= 0 && i < mL) : true;
-    // even cell (i, 2l): E from the lane's odd cell (i-1, 2l+1), F from lane l-1's odd cell (i, 2l-1)
-    {
-        const int Hd = He + (int)__builtin_amdgcn_ubfe(tabv, rce, 4) - 8;
-        const int e1 = Eo + K.mexI, h1 = Ho + K.moeI;
-        int f1 = dppz<WAVE_SHR1>(Fo) + K.mexD, g1 = dppz<WAVE_SHR1>(Ho) + K.moeD;
-        f1 = lane32 ? 0 : f1;
-        g1 = lane32 ? 0 : g1;
-        diag_cell<EDGE>(Hd, e1, h1, f1, g1, gap, valid, He, Ee, Fe, kbe, bestKey, acc);
-    }
-    // odd cell (i, 2l+1): E from lane l+1's even cell (i-1, 2l+2), F from the lane's even cell (i, 2l)
-    {
-        const int Hd = Ho + (int)__builtin_amdgcn_ubfe(tabv, rco, 4) - 8;
-        int e1 = dppz<WAVE_SHL1>(Ee) + K.mexI, h1 = dppz<WAVE_SHL1>(He) + K.moeI;
-        e1 = lane31 ? 0 : e1;
-        h1 = lane31 ? 0 : h1;
-        const int f1 = Fe + K.mexD, g1 = He + K.moeD;
-        diag_cell<EDGE>(Hd, e1, h1, f1, g1, gap, valid, Ho, Eo, Fo, kbe - 1u, bestKey, acc);
-    }
-}
-
-__global__ __launch_bounds__(64) void k_diag(const uint32_t *gtab, const uint8_t *gref, int n_ext,
-                                             int *out)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x & 63, lp = lane & 31, h = lane >> 5;
-    uint32_t *bits = (uint32_t *)smem;                                  // NW x 64
-    uint32_t *tab2 = bits + NW * 64;                                    // 2 x (ROWS + 64), rows -32 ..
-    uint8_t *ref2 = (uint8_t *)(tab2 + 2 * (ROWS + 64));                // 2 x (ROWS + 72)
-    const uint32_t *tabL = tab2 + h * (ROWS + 64) + 32;
-    const uint8_t *refL = ref2 + h * (ROWS + 72);
-    DiagK K;
-    K.mexI = in_vgpr(-EXI);
-    K.moeI = in_vgpr(-OEI);
-    K.mexD = in_vgpr(-EXD);
-    K.moeD = in_vgpr(-OED);
-    const bool lane31 = lane == 31, lane32 = lane == 32;
-    // key = ((H - BX) << 16) | (1023 - i) << 6 | (63 - k), even cell k = 2lp, i = T - lp
-    const uint32_t kb0 = ((uint32_t)(1023 + lp) << 6 | (uint32_t)(63 - 2 * lp)) - ((uint32_t)BX << 16);
-    for (int x0 = blockIdx.x * 2; x0 < n_ext; x0 += gridDim.x * 2) {
-        for (int hh = 0; hh < 2; ++hh) {
-            const int x = x0 + hh < n_ext ? x0 + hh : x0;
-            for (int i = lane; i < ROWS + 64; i += 64) {
-                const int r = i - 32;
-                tab2[hh * (ROWS + 64) + i] = (r >= 0 && r < ROWS) ? gtab[(size_t)x * ROWS + r] : 0x88888u;
-            }
-            for (int i = lane; i < ROWS + 72; i += 64) ref2[hh * (ROWS + 72) + i] = gref[(size_t)x * (ROWS + 72) + i];
-        }
-        __builtin_amdgcn_wave_barrier();
-        int He = BX, Ee = 0, Fe = 0, Ho = BX, Eo = 0, Fo = 0;
-        uint32_t bestKey = 0, acc = 0;
-        const int mL = M;
-        int T = 0;
-        for (; T < 36; ++T) {
-            diag_T<true>(T, lp, lane31, lane32, tabL, refL, mL, K, He, Ee, Fe, Ho, Eo, Fo,
-                         kb0 - ((uint32_t)T << 6), bestKey, acc);
-            if ((T & 3) == 3) bits[(T >> 2) * 64 + lane] = acc;
-        }
-        for (; T + 3 + GBAR < M; T += 4) {   // interior: every lane's rows in the gap window
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                diag_T<false>(T + u, lp, lane31, lane32, tabL, refL, mL, K, He, Ee, Fe, Ho, Eo, Fo,
-                              kb0 - ((uint32_t)(T + u) << 6), bestKey, acc);
-            bits[((T + 3) >> 2) * 64 + lane] = acc;
-        }
-        for (; T < TSTEPS; ++T) {
-            diag_T<true>(T, lp, lane31, lane32, tabL, refL, mL, K, He, Ee, Fe, Ho, Eo, Fo,
-                         kb0 - ((uint32_t)T << 6), bestKey, acc);
-            if ((T & 3) == 3) bits[(T >> 2) * 64 + lane] = acc;
-        }
-        bits[(T >> 2) * 64 + lane] = acc;
-        // best of each half
-        uint32_t k = bestKey;
-        for (int o = 16; o; o >>= 1) { uint32_t y = __shfl_xor(k, o); k = k > y ? k : y; }
-        if (lp == 0) {
-            const int x = x0 + h;
-            if (x < n_ext) {
-                out[3 * x] = (int)(k >> 16);
-                out[3 * x + 1] = 1023 - (int)((k >> 6) & 1023);
-                out[3 * x + 2] = 63 - (int)(k & 63);
-            }
+            out[4 * x] = (int)(key >> 20);
+            out[4 * x + 1] = 1023 - (int)((key >> 6) & 1023);
+            out[4 * x + 2] = 63 - (int)(key & 63);
+            out[4 * x + 3] = (int)sum;
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -324,45 +204,71 @@ int main(int argc, char **argv)
             tab[(size_t)x * ROWS + i] = tb;
         }
     }
-    uint32_t *dt; uint8_t *dr; int *o1, *o2;
+    uint32_t *dt; uint8_t *dr; int *o1, *o2; uint32_t *gb;
+    const int g_lds = 256 * 12, g_glb = 256 * 8;   // grids: LDS variant 4 blocks/CU resident (grid-stride), global variant 8 blocks/CU
     CHECK(hipMalloc(&dt, tab.size() * 4));
     CHECK(hipMalloc(&dr, ref.size()));
-    CHECK(hipMalloc(&o1, (size_t)n * 12));
-    CHECK(hipMalloc(&o2, (size_t)n * 12));
+    CHECK(hipMalloc(&o1, (size_t)n * 16));
+    CHECK(hipMalloc(&o2, (size_t)n * 16));
+    CHECK(hipMalloc(&gb, (size_t)g_glb * 4 * (ROWS / 8 * 64) * 4));
     CHECK(hipMemcpy(dt, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(dr, ref.data(), ref.size(), hipMemcpyHostToDevice));
-    const int lds_rows = 4 * (ROWS / 8 * 64 * 4 + ROWS * 4 + ROWS + 72);
-    const int lds_diag = NW * 64 * 4 + 2 * (ROWS + 64) * 4 + 2 * (ROWS + 72);
-    CHECK(hipFuncSetAttribute((const void *)k_rows, hipFuncAttributeMaxDynamicSharedMemorySize, lds_rows));
-    CHECK(hipFuncSetAttribute((const void *)k_diag, hipFuncAttributeMaxDynamicSharedMemorySize, lds_diag));
+    const int lds0 = 4 * (ROWS / 8 * 64 * 4 + ROWS * 4 + ROWS + 72);
+    const int lds1 = 4 * (ROWS * 4 + ROWS + 72);
+    CHECK(hipFuncSetAttribute((const void *)k_rows<0>, hipFuncAttributeMaxDynamicSharedMemorySize, lds0));
+    CHECK(hipFuncSetAttribute((const void *)k_rows<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds1));
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     float ms1 = 0, ms2 = 0;
     for (int rep = 0; rep < 3; ++rep) {
         hipEventRecord(a);
-        hipLaunchKernelGGL(k_rows, dim3(256 * 48), dim3(256), lds_rows, 0, dt, dr, n, o1);
+        hipLaunchKernelGGL(k_rows<0>, dim3(g_lds), dim3(256), lds0, 0, dt, dr, n, o1, gb);
         hipEventRecord(b);
         hipEventSynchronize(b);
         hipEventElapsedTime(&ms1, a, b);
         hipEventRecord(a);
-        hipLaunchKernelGGL(k_diag, dim3(256 * 64), dim3(64), lds_diag, 0, dt, dr, n, o2);
+        hipLaunchKernelGGL(k_rows<1>, dim3(g_glb), dim3(256), lds1, 0, dt, dr, n, o2, gb);
         hipEventRecord(b);
         hipEventSynchronize(b);
         hipEventElapsedTime(&ms2, a, b);
         CHECK(hipGetLastError());
     }
-    std::vector<int> r1((size_t)n * 3), r2((size_t)n * 3);
+    std::vector<int> r1((size_t)n * 4), r2((size_t)n * 4);
     CHECK(hipMemcpy(r1.data(), o1, r1.size() * 4, hipMemcpyDeviceToHost));
     CHECK(hipMemcpy(r2.data(), o2, r2.size() * 4, hipMemcpyDeviceToHost));
     int bad = 0;
     for (int x = 0; x < n; ++x)
-        if (r1[3 * x] != r2[3 * x] || r1[3 * x + 1] != r2[3 * x + 1] || r1[3 * x + 2] != r2[3 * x + 2]) {
-            if (bad < 5) printf("ext %d: rows (%d,%d,%d) diag (%d,%d,%d)\n", x, r1[3 * x], r1[3 * x + 1],
-                                r1[3 * x + 2], r2[3 * x], r2[3 * x + 1], r2[3 * x + 2]);
-            ++bad;
+        for (int q = 0; q < 4; ++q)
+            if (r1[4 * x + q] != r2[4 * x + q]) {
+                if (bad < 5) printf("ext %d: lds (%d,%d,%d,%d) global (%d,%d,%d,%d)\n", x, r1[4 * x], r1[4 * x + 1],
+                                    r1[4 * x + 2], r1[4 * x + 3], r2[4 * x], r2[4 * x + 1], r2[4 * x + 2], r2[4 * x + 3]);
+                ++bad;
+                break;
+            }
+    // ablations (timing only): ns per row per SIMD
+    float ab[4] = {0, 0, 0, 0};
+    const int abk[4] = {1, 2, 4, 7};
+    for (int q = 0; q < 4; ++q) {
+        for (int rep = 0; rep < 2; ++rep) {
+            hipEventRecord(a);
+            switch (abk[q]) {
+                case 1: hipLaunchKernelGGL((k_rows<0, 1>), dim3(g_lds), dim3(256), lds0, 0, dt, dr, n, o2, gb); break;
+                case 2: hipLaunchKernelGGL((k_rows<0, 2>), dim3(g_lds), dim3(256), lds0, 0, dt, dr, n, o2, gb); break;
+                case 4: hipLaunchKernelGGL((k_rows<0, 4>), dim3(g_lds), dim3(256), lds0, 0, dt, dr, n, o2, gb); break;
+                default: hipLaunchKernelGGL((k_rows<0, 7>), dim3(g_lds), dim3(256), lds0, 0, dt, dr, n, o2, gb); break;
+            }
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            hipEventElapsedTime(&ab[q], a, b);
         }
-    printf("{\"extensions\": %d, \"lds_rows_per_wave\": %d, \"lds_diag_per_wave\": %d, \"k_rows_ms\": %.3f, "
-           "\"k_diag_ms\": %.3f, \"speedup\": %.3f, \"mismatches\": %d, \"example_best\": [%d, %d, %d]}\n",
-           n, lds_rows / 4, lds_diag, ms1, ms2, ms1 / ms2, bad, r1[0], r1[1], r1[2]);
+        CHECK(hipGetLastError());
+    }
+    const double rows_per_simd = (double)n * M / 1024.0;
+    printf("{\"ns_per_row_per_simd\": {\"full\": %.2f, \"no_bits\": %.2f, \"no_key\": %.2f, \"no_scan\": %.2f, "
+           "\"none_of_the_three\": %.2f}}\n", ms1 * 1e6 / rows_per_simd, ab[0] * 1e6 / rows_per_simd,
+           ab[1] * 1e6 / rows_per_simd, ab[2] * 1e6 / rows_per_simd, ab[3] * 1e6 / rows_per_simd);
+    printf("{\"extensions\": %d, \"lds_bits_ms\": %.3f, \"global_bits_ms\": %.3f, \"speedup\": %.3f, "
+           "\"mismatches\": %d, \"example_best\": [%d, %d, %d]}\n",
+           n, ms1, ms2, ms1 / ms2, bad, r1[0], r1[1], r1[2]);
     return bad != 0;
 }
