@@ -888,10 +888,13 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         wave_sync();
 
         // ---- traceback: CIGAR runs, back to front, and the lane of every M
-        // row (rowk) for the lane-parallel statistics below.  The walk is
-        // serial, so it runs wave-uniform: its state lives in SGPRs and its
-        // arithmetic and branches are scalar instructions, leaving the vector
-        // ALU to the other waves' DP rows; only lane 0 stores. ----
+        // row (rowk) for the lane-parallel statistics below.  The walk's
+        // state is wave-uniform (SGPRs, scalar branches).  A diagonal run is
+        // found in one step: lane L tests the traceback word of row group
+        // (i >> 3) - L on the current diagonal, and a ballot gives the first
+        // group below row i that holds a non-diagonal cell (one LDS round
+        // trip per run instead of one per 8 rows).  Gap moves are single
+        // steps.  Only lane 0 writes runs. ----
         int tb_ok = 0, t_start = 0, t_first = 0, t_nrun = 0;
         best = __builtin_amdgcn_readfirstlane(best);
         bi = __builtin_amdgcn_readfirstlane(bi);
@@ -903,39 +906,57 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             uint32_t word = 0;
             int rop = -1, rlen = 0, nrun = 0, first_j = 0;
             for (;;) {
+                if (state == 0) {
+                    // rf: the highest row <= i on diagonal k whose source is
+                    // not the diagonal (-1: the run reaches row 0)
+                    int rf = -1;
+                    uint32_t wf = 0;
+                    for (int g0 = i >> 3, top = i & 7; g0 >= 0; g0 -= 64, top = 7) {
+                        const int g = g0 - lane;
+                        uint32_t w = g >= 0 ? bits[g * 64 + k] : 0x11111111u;
+                        if (lane == 0 && top < 7) {   // rows above i count as diagonal
+                            const uint32_t above = (1u << (4 * (7 - top))) - 1u;
+                            w = (w & ~above) | (0x11111111u & above);
+                        }
+                        const uint32_t nd = (w & 0x33333333u) ^ 0x11111111u;
+                        const uint64_t hit = __builtin_amdgcn_ballot_w64(nd != 0);
+                        if (hit) {
+                            const int L = (int)__builtin_ctzll(hit);
+                            wf = (uint32_t)__builtin_amdgcn_readlane((int)w, L);
+                            const uint32_t ndf = (uint32_t)__builtin_amdgcn_readlane((int)nd, L);
+                            rf = (g0 - L) * 8 + 7 - (int)(__builtin_ctz(ndf) >> 2);
+                            break;
+                        }
+                    }
+                    if (i > rf) {   // rows rf+1 .. i: one M run
+                        const int len = i - rf;
+                        if (rop == MH_OP_M) rlen += len;
+                        else {
+                            if (rlen) {
+                                if (nrun >= RUNS_CAP - 1) { ok = 0; break; }
+                                if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                                ++nrun;
+                            }
+                            rop = MH_OP_M;
+                            rlen = len;
+                        }
+                        for (int r = rf + 1 + lane; r <= i; r += 64) rowk[r] = (uint8_t)k;
+                        first_j = rf + 1 + d0u + k;
+                    }
+                    i = rf;
+                    if (i < 0) break;
+                    const int src = (int)(wf >> (4 * (7 - (i & 7)))) & 3;
+                    if (src == 0) break;   // local stop: the alignment starts at row i + 1
+                    state = src == 2 ? 1 : 2;
+                    continue;
+                }
                 const int g = i >> 3;
                 if (g != wr || k != wk) {
                     word = __builtin_amdgcn_readfirstlane(bits[g * 64 + k]);
                     wr = g; wk = k;
                 }
-                if (state == 0 && (i & 7) == 7 && (word & 0x33333333u) == 0x11111111u) {
-                    // eight diagonal moves on this lane: one M step of 8 rows
-                    if (rop == MH_OP_M) rlen += 8;
-                    else {
-                        if (rlen) {
-                            if (nrun >= RUNS_CAP - 1) { ok = 0; break; }
-                            if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
-                            ++nrun;
-                        }
-                        rop = MH_OP_M;
-                        rlen = 8;
-                    }
-                    if (lane == 0) *(uint64_t *)(rowk + i - 7) = 0x0101010101010101ull * (uint64_t)k;
-                    first_j = i - 7 + d0u + k;
-                    i -= 8;
-                    if (i < 0) break;
-                    continue;
-                }
                 const uint32_t nib = (word >> (4 * (7 - (i & 7)))) & 15u;
-                int op;
-                if (state == 0) {
-                    const int src = nib & 3;
-                    if (src == 0) break;
-                    if (src != 1) { state = src == 2 ? 1 : 2; continue; }
-                    op = MH_OP_M;
-                } else {
-                    op = state == 1 ? MH_OP_I : MH_OP_D;
-                }
+                const int op = state == 1 ? MH_OP_I : MH_OP_D;
                 if (op == rop) ++rlen;
                 else {
                     if (rlen) {
@@ -946,11 +967,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                     rop = op;
                     rlen = 1;
                 }
-                if (op == MH_OP_M) {
-                    if (lane == 0) rowk[i] = (uint8_t)k;
-                    first_j = i + d0u + k;
-                    if (--i < 0) break;
-                } else if (op == MH_OP_I) {
+                if (op == MH_OP_I) {
                     state = (nib >> 2) & 1 ? 1 : 0;
                     --i; ++k;
                     if (i < 0 || k >= BAND) { ok = 0; break; }
