@@ -440,9 +440,9 @@ __device__ __forceinline__ int scan_max(int x)
 }
 
 struct DpConst {
-    int mexI, moeI;     // -exI, -oeI in VGPRs (operands of fused DPP adds)
+    int mexI;           // -exI in a VGPR (operand of the fused DPP add)
+    int dIE;            // exI - oeI: h1 - e1 = (Hp + dIE) - Ep on the source lane
     int xD, cF;         // per lane: exD * lane, -(oeD - exD) - exD * lane
-    int eight;          // 8 in a VGPR (operand of a fused DPP and)
 };
 
 // a wave-uniform value the compiler must keep in a VGPR: VOP2 DPP forms take
@@ -454,22 +454,39 @@ __device__ __forceinline__ int in_vgpr(int v)
     return r;
 }
 
-// One DP row inside the gap window (oracle dp_extend, og_mapper.c:283-322).  The row's traceback nibble is shifted
-// into acc (acc = 16 acc + nibble, so row t of an 8-row group sits at nibble
-// 7 - t): bit 0/1 src (1 diagonal, 2 E, 3 F, 0 local stop), bit 2 E extends,
-// bit 3 F extends.  Every bit is a compare into a lane mask (the src logic is
-// scalar mask arithmetic) and enters acc by an add with carry-in, 2 acc + bit.
+// acc = 2 acc + (d < 0): the sign bit of d shifted into the traceback word
+__device__ __forceinline__ uint32_t push_sign(uint32_t acc, int d)
+{
+    return __builtin_amdgcn_alignbit(acc, (uint32_t)d, 31u);
+}
+
+// Traceback nibble of cell (i, k), four sign bits in this order (bit 3 first;
+// row t of an 8-row group sits at nibble 7 - t):
+//   bit 3  eb'  on lane k: E(i, k-1) extends (oracle eb of cell k-1: the
+//               extension beat the opening on lane k of row i-1)
+//   bit 2  fb'  on lane k: F(i, k+1) extends (oracle fb of cell k+1:
+//               X(k) < P(k), the prefix max came from a lane left of k)
+//   bit 1  Hd < H  (0: the diagonal is the source)
+//   bit 0  E  < H  (0: E is the source when the diagonal is not)
+// Each bit is one subtraction and one v_alignbit; no lane-mask compare.  The
+// local stop (H == 0) is not stored: the traceback knows H along its path.
+constexpr uint32_t TB_EB = 8u, TB_FB = 4u, TB_NE = 1u;   // (bit 1: Hd < H, tested as TB_ND_ALL)
+constexpr uint32_t TB_ND_ALL = 0x22222222u;   // bit 1 of every nibble
+
+// One DP row inside the gap window (oracle dp_extend, og_mapper.c:289-328).
 template <int LOCAL>
 __device__ __forceinline__ void dp_row_gap(uint32_t tbv, int rc, int &Hp, int &Ep,
                                            uint32_t &bestKey, int ci, const DpConst &K,
                                            uint32_t &acc)
 {
     const int Hd = Hp + (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4) - 8;
-    // vertical (insertion) move from lane k+1 of the previous row; E extends
-    // when extending beats opening (ties open)
-    const int e1 = dppz<DPP_WAVE_SHL1>(Ep) + K.mexI;
-    const int h1 = dppz<DPP_WAVE_SHL1>(Hp) + K.moeI;
-    const int E = imax(e1, h1);
+    // vertical (insertion) move from lane k+1 of the previous row: on the
+    // source lane q = max(Ep - exI, Hp - oeI) + exI, moved one lane down by
+    // the fused DPP add; ties open (eb needs h1 < e1 strictly)
+    const int hc = Hp + K.dIE;
+    const int q = imax(Ep, hc);
+    const int E = dppz<DPP_WAVE_SHL1>(q) + K.mexI;
+    acc = push_sign(acc, hc - Ep);
     int H1 = imax(Hd, E);
     if (LOCAL) H1 = imax(H1, BIAS);
     // horizontal (deletion) moves: prefix max of X = H1 + exD * lane
@@ -477,78 +494,30 @@ __device__ __forceinline__ void dp_row_gap(uint32_t tbv, int rc, int &Hp, int &E
     const int P = scan_max(X);
     const int F = dppz<DPP_WAVE_SHR1>(P) + K.cF;
     const int H = imax(H1, F);
+    acc = push_sign(acc, X - P);
+    acc = push_sign(acc, Hd - H);
+    acc = push_sign(acc, E - H);
     if (LOCAL) {
         const uint32_t key = (uint32_t)H * 1024u + (uint32_t)ci;
         bestKey = bestKey > key ? bestKey : key;
-    }
-    // The nibble: src (1 diagonal, 2 E, 3 F by priority; 0 local stop) in
-    // bits 0-1, E extends (h1 < e1) in bit 2, F extends in bit 3 (the left
-    // lane's X is below its prefix max, compared on F's scale: X(k-1) + cF(k)
-    // < P(k-1) + cF(k)).  Every bit is a compare into a lane mask, the src
-    // logic is scalar mask arithmetic, and each bit enters acc by an add with
-    // carry-in (acc = 2 acc + bit).  Hazards: X is written before the scan,
-    // so its DPP read is far from the write; >= 2 instructions separate
-    // each mask write from its read as a carry.
-    uint64_t ma, mb, mz, me, mf;
-    int xl;
-    if (LOCAL) {
-        asm volatile(
-            "v_cmp_ne_u32_e64 %[ma], %[H], %[Hd]\n\t"
-            "v_cmp_ne_u32_e64 %[mb], %[H], %[E]\n\t"
-            "v_cmp_ne_u32_e64 %[mz], %[bias], %[H]\n\t"
-            "v_cmp_lt_i32_e64 %[me], %[h1], %[e1]\n\t"
-            "v_add_u32_dpp %[xl], %[X], %[cF] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-            "s_orn2_b64 %[mb], %[mb], %[ma]\n\t"
-            "v_cmp_lt_i32_e64 %[mf], %[xl], %[F]\n\t"
-            "s_and_b64 %[ma], %[ma], %[mz]\n\t"
-            "s_and_b64 %[mb], %[mb], %[mz]\n\t"
-            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[mf]\n\t"
-            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[me]\n\t"
-            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[ma]\n\t"
-            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[mb]"
-            : [acc] "+v"(acc), [ma] "=&s"(ma), [mb] "=&s"(mb), [mz] "=&s"(mz), [me] "=&s"(me),
-              [mf] "=&s"(mf), [xl] "=&v"(xl)
-            : [H] "v"(H), [Hd] "v"(Hd), [E] "v"(E), [h1] "v"(h1), [e1] "v"(e1), [X] "v"(X),
-              [cF] "v"(K.cF), [F] "v"(F), [bias] "s"(BIAS)
-            : "vcc");
-    } else {
-        asm volatile(
-            "v_cmp_ne_u32_e64 %[ma], %[H], %[Hd]\n\t"
-            "v_cmp_ne_u32_e64 %[mb], %[H], %[E]\n\t"
-            "v_cmp_lt_i32_e64 %[me], %[h1], %[e1]\n\t"
-            "v_add_u32_dpp %[xl], %[X], %[cF] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-            "s_orn2_b64 %[mb], %[mb], %[ma]\n\t"
-            "v_cmp_lt_i32_e64 %[mf], %[xl], %[F]\n\t"
-            "s_nop 1\n\t"
-            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[mf]\n\t"
-            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[me]\n\t"
-            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[ma]\n\t"
-            "v_addc_co_u32_e64 %[acc], vcc, %[acc], %[acc], %[mb]"
-            : [acc] "+v"(acc), [ma] "=&s"(ma), [mb] "=&s"(mb), [me] "=&s"(me), [mf] "=&s"(mf),
-              [xl] "=&v"(xl)
-            : [H] "v"(H), [Hd] "v"(Hd), [E] "v"(E), [h1] "v"(h1), [e1] "v"(e1), [X] "v"(X),
-              [cF] "v"(K.cF), [F] "v"(F)
-            : "vcc");
-        (void)mz;
     }
     Hp = H;
     Ep = E;
 }
 
-// A row outside the gap window (first / last GBAR rows): no E, no F.
+// A row outside the gap window (first / last GBAR rows): no E, no F.  Its
+// nibble is 0: a local cell at H == 0 is a stop the traceback sees from H.
 template <int LOCAL>
 __device__ __forceinline__ void dp_row_nogap(uint32_t tbv, int rc, int &Hp, int &Ep,
                                              uint32_t &bestKey, int ci, uint32_t &acc)
 {
     int H = Hp + (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4) - 8;
-    uint32_t src = 1u;
     if (LOCAL) {
         H = imax(H, BIAS);
-        src = umin1(H - BIAS);
         const uint32_t key = (uint32_t)H * 1024u + (uint32_t)ci;
         bestKey = bestKey > key ? bestKey : key;
     }
-    acc = (acc << 4) + src;
+    acc <<= 4;
     Hp = H;
     Ep = 0;
 }
@@ -600,7 +569,7 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
         uint32_t rd[4], lo[4], hi[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            rd[u] = *(const uint32_t *)(rdc + i + 4 * u);
+            rd[u] = *(const uint32_t *)(rdc + i + 4 * u) & 0x07070707u;   // codes without the penalties
             lo[u] = *(const uint32_t *)(rp + i + 4 * u);
             hi[u] = *(const uint32_t *)(rp + i + 4 * u + 4);
         }
@@ -698,14 +667,9 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
         if (r >= lo && r <= istar && r >= GBAR && H[u] < ma * (r + 1) - gmin) bad = true;
     }
     if (__builtin_amdgcn_ballot_w64(bad) != 0) return false;
-    // traceback bits of lane kb: diagonal (1) where H > 0, local stop (0)
-    if (r0 < m) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (r0 + u < m && (!LOCAL || H[u] > 0)) w |= 1u << (4 * (7 - u));   // row u of the group at nibble 7 - u
-        bits[lane * 64 + kb] = w;
-    }
+    // traceback bits of lane kb: every row diagonal (nibble 0); the local
+    // stop at istop is the traceback's H == 0
+    if (r0 < m) bits[lane * 64 + kb] = 0u;
     best = S;
     bi = istar;
     bl = kb;
@@ -726,14 +690,13 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                                                               // written after the DP is done with tab
     uint8_t *refw = (uint8_t *)(runs + (A.rows_pad > RUNS_CAP ? A.rows_pad : RUNS_CAP));
                                                               // rows_pad + 64: ref code * 4
-    uint8_t *rdc = refw + A.rows_pad + 64;                    // rows_pad: read codes
+    uint8_t *rdc = refw + A.rows_pad + 64;                    // rows_pad: read code | mismatch penalty << 3
     uint8_t *rowk = rdc + A.rows_pad;                         // rows_pad: lane of the M cell, 255 none
     const int ma = LOCAL ? 2 : 0;
     const int n_work = A.counters[0];
     DpConst K;
     K.mexI = in_vgpr(-A.exI);
-    K.moeI = in_vgpr(-A.oeI);
-    K.eight = in_vgpr(8);
+    K.dIE = A.exI - A.oeI;
     K.xD = lane * A.exD;
     K.cF = -(A.oeD - A.exD) - A.exD * lane;
 
@@ -790,19 +753,19 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             for (int u = 0; u < 4; ++u) {
                 const int i = i0 + 64 * u + lane;
                 if (i >= A.rows_pad) break;
-                uint32_t tb = 0x88888u, c = 4;
+                uint32_t tb = 0x88888u, c = 4, pen = 0;
                 if (i < m) {
                     c = ((nmw[u] >> bb[u]) & 1) ? 4u : (sqw[u] & 3u);
                     if (strand && c < 4) c = 3 - c;
-                    const int pen = mm_pen((int)qv[u]);
+                    pen = (uint32_t)mm_pen((int)qv[u]);
                     tb = 0;
                     for (int g = 0; g < 5; ++g) {
-                        const int sc = (c > 3 || g > 3) ? -NPEN : (c == (uint32_t)g ? ma : -pen);
+                        const int sc = (c > 3 || g > 3) ? -NPEN : (c == (uint32_t)g ? ma : -(int)pen);
                         tb |= (uint32_t)(sc + 8) << (4 * g);
                     }
                 }
                 tab[i] = tb;
-                rdc[i] = (uint8_t)c;
+                rdc[i] = (uint8_t)(c | pen << 3);
                 rowk[i] = 255;
             }
         }
@@ -893,15 +856,18 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         // found in one step: lane L tests the traceback word of row group
         // (i >> 3) - L on the current diagonal, and a ballot gives the first
         // group below row i that holds a non-diagonal cell (one LDS round
-        // trip per run instead of one per 8 rows).  Gap moves are single
-        // steps.  Only lane 0 writes runs. ----
+        // trip per run instead of one per 8 rows).  In local mode the walk
+        // carries the value of its cell (hv): down a run the lanes rebuild H
+        // row by row (a prefix sum of the run's scores) and the first H == 0
+        // is the stop the oracle takes (og_mapper.c:319, src 0).  Gap moves
+        // are single steps.  Only lane 0 writes runs. ----
         int tb_ok = 0, t_start = 0, t_first = 0, t_nrun = 0;
         best = __builtin_amdgcn_readfirstlane(best);
         bi = __builtin_amdgcn_readfirstlane(bi);
         bl = __builtin_amdgcn_readfirstlane(bl);
         if (!(LOCAL && best <= 0) && best >= __builtin_amdgcn_readfirstlane(minsc)) {
             const int d0u = __builtin_amdgcn_readfirstlane(d0);
-            int i = bi, k = bl, state = 0, ok = 1;
+            int i = bi, k = bl, state = 0, ok = 1, hv = best;
             int wr = -1, wk = -1;
             uint32_t word = 0;
             int rop = -1, rlen = 0, nrun = 0, first_j = 0;
@@ -913,12 +879,10 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                     uint32_t wf = 0;
                     for (int g0 = i >> 3, top = i & 7; g0 >= 0; g0 -= 64, top = 7) {
                         const int g = g0 - lane;
-                        uint32_t w = g >= 0 ? bits[g * 64 + k] : 0x11111111u;
-                        if (lane == 0 && top < 7) {   // rows above i count as diagonal
-                            const uint32_t above = (1u << (4 * (7 - top))) - 1u;
-                            w = (w & ~above) | (0x11111111u & above);
-                        }
-                        const uint32_t nd = (w & 0x33333333u) ^ 0x11111111u;
+                        uint32_t w = g >= 0 ? bits[g * 64 + k] : 0u;
+                        if (lane == 0 && top < 7)   // rows above i count as diagonal
+                            w &= ~((1u << (4 * (7 - top))) - 1u);
+                        const uint32_t nd = w & TB_ND_ALL;
                         const uint64_t hit = __builtin_amdgcn_ballot_w64(nd != 0);
                         if (hit) {
                             const int L = (int)__builtin_ctzll(hit);
@@ -928,8 +892,28 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                             break;
                         }
                     }
-                    if (i > rf) {   // rows rf+1 .. i: one M run
-                        const int len = i - rf;
+                    int stop = -1;   // local: the highest row of rf .. i with H == 0
+                    if (LOCAL) {
+                        const int lo = rf > 0 ? rf : 0;
+                        for (int r0 = i; r0 >= lo; r0 -= 64) {
+                            const int r = r0 - lane;
+                            int sc = 0;   // score of the diagonal move out of row r
+                            if (r > rf && r >= 0) {
+                                const int rb = rdc[r], gc = refw[r + k] >> 2, c = rb & 7;
+                                sc = (c > 3 || gc > 3) ? -NPEN : (c == gc ? ma : -(rb >> 3));
+                            }
+                            const int ex = wave_excl_scan(sc, lane);
+                            const uint64_t z = __builtin_amdgcn_ballot_w64(r >= lo && hv - ex == 0);
+                            if (z) {
+                                stop = r0 - (int)__builtin_ctzll(z);
+                                break;
+                            }
+                            hv -= __builtin_amdgcn_readlane(ex + sc, 63);
+                        }
+                    }
+                    const int low = stop >= 0 ? stop : rf;
+                    if (i > low) {   // rows low+1 .. i: one M run
+                        const int len = i - low;
                         if (rop == MH_OP_M) rlen += len;
                         else {
                             if (rlen) {
@@ -940,20 +924,22 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                             rop = MH_OP_M;
                             rlen = len;
                         }
-                        for (int r = rf + 1 + lane; r <= i; r += 64) rowk[r] = (uint8_t)k;
-                        first_j = rf + 1 + d0u + k;
+                        for (int r = low + 1 + lane; r <= i; r += 64) rowk[r] = (uint8_t)k;
+                        first_j = low + 1 + d0u + k;
                     }
-                    i = rf;
-                    if (i < 0) break;
-                    const int src = (int)(wf >> (4 * (7 - (i & 7)))) & 3;
-                    if (src == 0) break;   // local stop: the alignment starts at row i + 1
-                    state = src == 2 ? 1 : 2;
+                    i = low;
+                    if (stop >= 0 || i < 0) break;   // a local stop starts the alignment at row i + 1
+                    const uint32_t nib = (wf >> (4 * (7 - (i & 7)))) & 15u;
+                    state = (nib & TB_NE) ? 2 : 1;
                     continue;
                 }
-                const int g = i >> 3;
-                if (g != wr || k != wk) {
-                    word = __builtin_amdgcn_readfirstlane(bits[g * 64 + k]);
-                    wr = g; wk = k;
+                // a gap step: the extend bit of cell (i, k) sits on lane k + 1
+                // (E, eb') or lane k - 1 (F, fb')
+                const int g = i >> 3, kk = state == 1 ? k + 1 : k - 1;
+                if (kk < 0 || kk >= BAND) { ok = 0; break; }
+                if (g != wr || kk != wk) {
+                    word = __builtin_amdgcn_readfirstlane(bits[g * 64 + kk]);
+                    wr = g; wk = kk;
                 }
                 const uint32_t nib = (word >> (4 * (7 - (i & 7)))) & 15u;
                 const int op = state == 1 ? MH_OP_I : MH_OP_D;
@@ -968,11 +954,15 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                     rlen = 1;
                 }
                 if (op == MH_OP_I) {
-                    state = (nib >> 2) & 1 ? 1 : 0;
+                    const bool ext = (nib & TB_EB) != 0;
+                    hv += ext ? A.exI : A.oeI;
+                    state = ext ? 1 : 0;
                     --i; ++k;
                     if (i < 0 || k >= BAND) { ok = 0; break; }
                 } else {
-                    state = (nib >> 3) & 1 ? 2 : 0;
+                    const bool ext = (nib & TB_FB) != 0;
+                    hv += ext ? A.exD : A.oeD;
+                    state = ext ? 2 : 0;
                     --k;
                     if (k < 0) { ok = 0; break; }
                 }
@@ -996,7 +986,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             int nn = 0;
             for (int i = t_start + lane; i <= bi; i += 64) {
                 const int k = rowk[i];
-                if (k != 255 && (rdc[i] > 3 || refw[i + k] > 12)) ++nn;
+                if (k != 255 && ((rdc[i] & 7) > 3 || refw[i + k] > 12)) ++nn;
             }
             nn = wave_sum(nn);
             if (nn > A.len_tab[2 * (MAXLEN + 1) + m]) tb_ok = 0;
@@ -1079,7 +1069,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                 for (int i = clipL + lane; i <= m - 1 - clipR; i += 64) {
                     const int k = rowk[i];
                     if (k == 255) continue;
-                    const int g = refw[i + k] >> 2, rb = rdc[i];
+                    const int g = refw[i + k] >> 2, rb = rdc[i] & 7;
                     if (rb > 3 || g > 3 || rb != g) ++xm;
                 }
                 xm = wave_sum(xm);
