@@ -546,8 +546,9 @@ __device__ __forceinline__ int wave_excl_scan_min(int v, int /*lane*/, int init)
 // the full DP picks the same best cell and traces the same all-M path.  The
 // fast path then writes only that lane's traceback bits and k_dp skips the
 // DP; otherwise (any condition false, read > 512 nt) it runs the full DP.
-// Candidates are screened first by a cheap per-diagonal non-match count
-// (4 rows per LDS word) that gives up as soon as no lane can satisfy (A).
+// The candidate is the seeded diagonal (lane HALF): its exact ungapped
+// recurrence decides (A) first, then a per-diagonal non-match count (4 rows
+// per LDS word) bounds every other lane for (B) and stops once all are below.
 // The result is bit-identical to the full DP (tests/test_gpu_parity.py
 // runs both and compares them with the oracle, og_mapper.c:dp_extend).
 // ---------------------------------------------------------------------------
@@ -558,46 +559,7 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
 {
     const int ma = LOCAL ? 2 : 0;
     const int gb_max = ma * m - gmin;   // Gb(m - 1)
-    // ---- non-matches per diagonal: read bytes rdc[i..i+3] against ref
-    // bytes refw[i+lane .. i+lane+3] (codes * 4), 4 rows per step ----
-    const uint8_t *rp = refw + (lane & ~3);
-    const uint32_t sh = (uint32_t)(lane & 3);
-    int nm = 0;
-    // 16 rows per step, every LDS read of the step issued before any is used
-    // (reads past rows_pad stay inside this wave's LDS area and are unused)
-    for (int i = 0; i < m; i += 16) {
-        uint32_t rd[4], lo[4], hi[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            rd[u] = *(const uint32_t *)(rdc + i + 4 * u) & 0x07070707u;   // codes without the penalties
-            lo[u] = *(const uint32_t *)(rp + i + 4 * u);
-            hi[u] = *(const uint32_t *)(rp + i + 4 * u + 4);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (i + 4 * u >= m) break;
-            const uint32_t rv = __builtin_amdgcn_alignbyte(hi[u], lo[u], sh) >> 2;
-            uint32_t x = (rd[u] ^ rv) | ((rd[u] | rv) & 0x04040404u);
-            x = (x | (x >> 1) | (x >> 2)) & 0x01010101u;
-            nm += __builtin_popcount(x);
-        }
-        if ((i & 63) == 48 && i + 16 <= m) {   // rows past the read would count as non-matches
-            // the best ungapped score of a lane is at most ma*(m - nm) (local)
-            // or -nm (end-to-end); give up when no lane can beat Gb(m-1)
-            const int ub = LOCAL ? ma * (m - nm) : -nm;
-            if (__builtin_amdgcn_ballot_w64(ub > gb_max) == 0) return false;
-        }
-    }
-    nm -= (4 - (m & 3)) & 3;   // rows past the read end are coded 4
-    const int ub = LOCAL ? ma * (m - nm) : -nm;
-    // candidate lane: fewest non-matches, then smallest lane (any choice is
-    // exact: (B) below checks every other lane)
-    const int key = wave_min(nm * 64 + lane);
-    const int kb = key & 63;
-    const int ub_other = wave_max(lane == kb ? INT32_MIN + 1 : ub);
-    const int ub_kb = __builtin_amdgcn_readlane(ub, kb);
-    if (ub_kb <= gb_max || ub_other >= ub_kb) return false;   // (A) / (B) cannot hold
-
+    const int kb = HALF;                // the seeded diagonal: the only candidate lane
     // ---- exact ungapped recurrence on lane kb: rows 8*lane .. 8*lane+7 ----
     const int r0 = 8 * lane;
     int s[8];
@@ -647,9 +609,46 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
         S = __builtin_amdgcn_readlane(v, __builtin_amdgcn_readfirstlane(last >> 3));
         istar = last;
     }
-    // (A) and (B)
-    if (!(S > gb_max) || !(ub_other < S)) return false;
+    // (A)
+    if (!(S > gb_max)) return false;
     if (LOCAL && S <= 0) return false;
+    // (B): non-matches per diagonal, read bytes rdc[i..i+3] against ref bytes
+    // refw[i+lane .. i+lane+3] (codes * 4), 16 rows per step with every LDS
+    // read of the step issued before any is used.  The bound ma*(m - nm)
+    // (local) or -nm (end-to-end) only falls as rows are counted, so the count
+    // stops as soon as every other lane is below S.
+    {
+        const uint8_t *rp = refw + (lane & ~3);
+        const uint32_t sh = (uint32_t)(lane & 3);
+        int nm = 0;
+        bool below = false;
+        for (int i = 0; i < m; i += 16) {
+            uint32_t rd[4], lo[4], hi[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                rd[u] = *(const uint32_t *)(rdc + i + 4 * u) & 0x07070707u;   // codes without the penalties
+                lo[u] = *(const uint32_t *)(rp + i + 4 * u);
+                hi[u] = *(const uint32_t *)(rp + i + 4 * u + 4);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (i + 4 * u >= m) break;
+                const uint32_t rv = __builtin_amdgcn_alignbyte(hi[u], lo[u], sh) >> 2;
+                uint32_t x = (rd[u] ^ rv) | ((rd[u] | rv) & 0x04040404u);
+                x = (x | (x >> 1) | (x >> 2)) & 0x01010101u;
+                nm += __builtin_popcount(x);
+            }
+            if (i + 16 <= m) {   // (rows past the read would count as non-matches)
+                const int ub = LOCAL ? ma * (m - nm) : -nm;
+                if (__builtin_amdgcn_ballot_w64(lane != kb && ub >= S) == 0) { below = true; break; }
+            }
+        }
+        if (!below) {
+            nm -= (4 - (m & 3)) & 3;   // rows past the read end are coded 4
+            const int ub = LOCAL ? ma * (m - nm) : -nm;
+            if (__builtin_amdgcn_ballot_w64(lane != kb && ub >= S) != 0) return false;
+        }
+    }
     // start of the traced segment: last row <= i* where H == 0 (local)
     int istop = -1;
     if (LOCAL) {
