@@ -893,21 +893,35 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                     }
                     int stop = -1;   // local: the highest row of rf .. i with H == 0
                     if (LOCAL) {
+                        // lane L rebuilds rows r0 - 4L .. r0 - 4L - 3: H(r) = hv minus the
+                        // scores of the diagonal moves out of the rows above r
                         const int lo = rf > 0 ? rf : 0;
-                        for (int r0 = i; r0 >= lo; r0 -= 64) {
-                            const int r = r0 - lane;
-                            int sc = 0;   // score of the diagonal move out of row r
-                            if (r > rf && r >= 0) {
-                                const int rb = rdc[r], gc = refw[r + k] >> 2, c = rb & 7;
-                                sc = (c > 3 || gc > 3) ? -NPEN : (c == gc ? ma : -(rb >> 3));
+                        for (int r0 = i; r0 >= lo; r0 -= 256) {
+                            int sc[4], tot = 0;
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int r = r0 - 4 * lane - u;
+                                sc[u] = 0;
+                                if (r > rf && r >= 0) {
+                                    const int rb = rdc[r], gc = refw[r + k] >> 2, c = rb & 7;
+                                    sc[u] = (c > 3 || gc > 3) ? -NPEN : (c == gc ? ma : -(rb >> 3));
+                                }
+                                tot += sc[u];
                             }
-                            const int ex = wave_excl_scan(sc, lane);
-                            const uint64_t z = __builtin_amdgcn_ballot_w64(r >= lo && hv - ex == 0);
+                            const int ex = wave_excl_scan(tot, lane);
+                            int run = ex, zrow = -1;
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int r = r0 - 4 * lane - u;
+                                if (zrow < 0 && r >= lo && hv - run == 0) zrow = r;
+                                run += sc[u];
+                            }
+                            const uint64_t z = __builtin_amdgcn_ballot_w64(zrow >= 0);
                             if (z) {
-                                stop = r0 - (int)__builtin_ctzll(z);
+                                stop = __builtin_amdgcn_readlane(zrow, (int)__builtin_ctzll(z));
                                 break;
                             }
-                            hv -= __builtin_amdgcn_readlane(ex + sc, 63);
+                            hv -= __builtin_amdgcn_readlane(run, 63);
                         }
                     }
                     const int low = stop >= 0 ? stop : rf;
@@ -981,21 +995,13 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         out.strand = strand;
         out.ref = cd.ref;
         if (tb_ok) {
-            // ambiguous positions over the untrimmed alignment (--n-ceil)
-            int nn = 0;
-            for (int i = t_start + lane; i <= bi; i += 64) {
-                const int k = rowk[i];
-                if (k != 255 && ((rdc[i] & 7) > 3 || refw[i + k] > 12)) ++nn;
-            }
-            nn = wave_sum(nn);
-            if (nn > A.len_tab[2 * (MAXLEN + 1) + m]) tb_ok = 0;
-        }
-        if (tb_ok) {
             // trim overhanging columns into soft clips, on the runs (lane 0)
-            int c_ok = 0, clipL = t_start, clipR = m - 1 - bi, jL = t_first, jR = bi + d0 + bl;
+            int lo = t_nrun - 1, hi = 0;   // forward order is runs[nrun-1] .. runs[0]
+            uint32_t front = 0, back = 0;
+            int clipL = t_start, clipR = m - 1 - bi, jL = t_first, jR = bi + d0 + bl;
             if (lane == 0) {
-                int lo = t_nrun - 1, hi = 0;   // forward order is runs[nrun-1] .. runs[0]
-                uint32_t front = lo >= 0 ? runs[lo] : 0, back = runs[0];
+                front = lo >= 0 ? runs[lo] : 0;
+                back = runs[0];
                 while (lo >= hi) {
                     const int op = front & 15, len = (int)(front >> 4);
                     if (op == MH_OP_M && jL >= 0) break;
@@ -1025,55 +1031,55 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                     }
                     if (++hi <= lo) back = hi == lo ? front : runs[hi];
                 }
-                if (lo >= hi) {
-                    int nc = (clipL > 0) + (clipR > 0) + (lo - hi + 1);
-                    if (nc <= MH_MAXOPS - 1) {
-                        if (nc > ck_left) {   // next wave-private chunk of the pool
-                            ck_base = atomicAdd(&A.pool_ctr[0], POOL_CHUNK);
-                            ck_left = POOL_CHUNK;
-                        }
-                        const int64_t base = ck_base;
-                        ck_base += nc;
-                        ck_left -= nc;
-                        if (base + nc > A.pool_cap) {
-                            atomicExch(&A.pool_ctr[1], 1);
-                        } else {
-                            uint32_t *cg = A.pool + base;
-                            int n = 0, xo = 0, xg = 0;
-                            if (clipL) cg[n++] = ((uint32_t)clipL << 4) | MH_OP_S;
-                            for (int z = lo; z >= hi; --z) {
-                                const uint32_t rr = z == hi ? back : (z == lo ? front : runs[z]);
-                                cg[n++] = rr;
-                                if ((rr & 15) != MH_OP_M) { ++xo; xg += (int)(rr >> 4); }
-                            }
-                            if (clipR) cg[n++] = ((uint32_t)clipR << 4) | MH_OP_S;
-                            out.valid = 1;
-                            out.pos = jL;
-                            out.end = jR + 1;
-                            out.score = best;
-                            out.xo = xo; out.xg = xg;
-                            out.n_cigar = n;
-                            out.cig_off = (int32_t)base;
-                            c_ok = 1;
-                        }
-                    }
-                }
             }
-            c_ok = __builtin_amdgcn_readfirstlane(c_ok);
             clipL = __builtin_amdgcn_readfirstlane(clipL);
             clipR = __builtin_amdgcn_readfirstlane(clipR);
-            if (c_ok) {
-                // mismatches over the M rows of the trimmed alignment
-                int xm = 0;
-                for (int i = clipL + lane; i <= m - 1 - clipR; i += 64) {
-                    const int k = rowk[i];
-                    if (k == 255) continue;
-                    const int g = refw[i + k] >> 2, rb = rdc[i] & 7;
-                    if (rb > 3 || g > 3 || rb != g) ++xm;
+            // one pass over the M rows: ambiguous positions over the untrimmed
+            // alignment (--n-ceil) and mismatches over the trimmed one, summed
+            // together (nn << 16 | xm)
+            int cnt = 0;
+            for (int i = t_start + lane; i <= bi; i += 64) {
+                const int k = rowk[i];
+                if (k == 255) continue;
+                const int g = refw[i + k] >> 2, rb = rdc[i] & 7;
+                if (rb > 3 || g > 3) cnt += 1 << 16;
+                if ((rb > 3 || g > 3 || rb != g) && i >= clipL && i <= m - 1 - clipR) ++cnt;
+            }
+            cnt = wave_sum(cnt);
+            if ((cnt >> 16) > A.len_tab[2 * (MAXLEN + 1) + m]) tb_ok = 0;
+            if (tb_ok && lane == 0 && lo >= hi) {
+                const int nc = (clipL > 0) + (clipR > 0) + (lo - hi + 1);
+                if (nc <= MH_MAXOPS - 1) {
+                    if (nc > ck_left) {   // next wave-private chunk of the pool
+                        ck_base = atomicAdd(&A.pool_ctr[0], POOL_CHUNK);
+                        ck_left = POOL_CHUNK;
+                    }
+                    const int64_t base = ck_base;
+                    ck_base += nc;
+                    ck_left -= nc;
+                    if (base + nc > A.pool_cap) {
+                        atomicExch(&A.pool_ctr[1], 1);
+                    } else {
+                        uint32_t *cg = A.pool + base;
+                        int n = 0, xo = 0, xg = 0;
+                        if (clipL) cg[n++] = ((uint32_t)clipL << 4) | MH_OP_S;
+                        for (int z = lo; z >= hi; --z) {
+                            const uint32_t rr = z == hi ? back : (z == lo ? front : runs[z]);
+                            cg[n++] = rr;
+                            if ((rr & 15) != MH_OP_M) { ++xo; xg += (int)(rr >> 4); }
+                        }
+                        if (clipR) cg[n++] = ((uint32_t)clipR << 4) | MH_OP_S;
+                        out.valid = 1;
+                        out.pos = jL;
+                        out.end = jR + 1;
+                        out.score = best;
+                        out.xo = xo; out.xg = xg;
+                        out.n_cigar = n;
+                        out.cig_off = (int32_t)base;
+                        out.xm = cnt & 0xffff;
+                        out.nm = out.xm + xg;
+                    }
                 }
-                xm = wave_sum(xm);
-                out.xm = xm;
-                out.nm = xm + out.xg;
             }
         }
         if (lane == 0) A.slot[sid] = out;
