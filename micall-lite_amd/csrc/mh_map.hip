@@ -498,7 +498,7 @@ __device__ __forceinline__ void dp_row_gap(uint32_t tbv, int rc, int &Hp, int &E
     acc = push_sign(acc, Hd - H);
     acc = push_sign(acc, E - H);
     if (LOCAL) {
-        const uint32_t key = (uint32_t)H * 1024u + (uint32_t)ci;
+        const uint32_t key = ((uint32_t)H << 10) | (uint32_t)ci;   // ci < 1024
         bestKey = bestKey > key ? bestKey : key;
     }
     Hp = H;
@@ -514,7 +514,7 @@ __device__ __forceinline__ void dp_row_nogap(uint32_t tbv, int rc, int &Hp, int 
     int H = Hp + (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4) - 8;
     if (LOCAL) {
         H = imax(H, BIAS);
-        const uint32_t key = (uint32_t)H * 1024u + (uint32_t)ci;
+        const uint32_t key = ((uint32_t)H << 10) | (uint32_t)ci;   // ci < 1024
         bestKey = bestKey > key ? bestKey : key;
     }
     acc <<= 4;
