@@ -439,10 +439,18 @@ __device__ __forceinline__ int scan_max(int x)
     return x;
 }
 
+// Row values are kept shifted so that the deletion scan needs no per-lane
+// add: lane k holds H~ = H + exD * k (and E~ the same), so X = H1~ directly
+// and F~ = P(k-1) - (oeD - exD) with one constant.  In end-to-end mode every
+// value of row i also carries + 8 (i + 1), the bias of the score nibbles, so
+// the diagonal move is one add (local mode keeps the - 8: its floor and the
+// best-cell key must not drift by row).  Lane-uniform offsets cancel in every
+// traceback bit; the best score subtracts them once at the end.
 struct DpConst {
-    int mexI;           // -exI in a VGPR (operand of the fused DPP add)
+    int mexI;           // E~ = dpp(q) + mexI: -(exI + exD), + 8 end-to-end
     int dIE;            // exI - oeI: h1 - e1 = (Hp + dIE) - Ep on the source lane
-    int xD, cF;         // per lane: exD * lane, -(oeD - exD) - exD * lane
+    int cF;             // F~ = dpp(P) + cF: -(oeD - exD), in a VGPR
+    int floor;          // local: BIAS + exD * lane, the shifted zero
 };
 
 // a wave-uniform value the compiler must keep in a VGPR: VOP2 DPP forms take
@@ -479,7 +487,8 @@ __device__ __forceinline__ void dp_row_gap(uint32_t tbv, int rc, int &Hp, int &E
                                            uint32_t &bestKey, int ci, const DpConst &K,
                                            uint32_t &acc)
 {
-    const int Hd = Hp + (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4) - 8;
+    const int nib = (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4);
+    const int Hd = LOCAL ? Hp + nib - 8 : Hp + nib;
     // vertical (insertion) move from lane k+1 of the previous row: on the
     // source lane q = max(Ep - exI, Hp - oeI) + exI, moved one lane down by
     // the fused DPP add; ties open (eb needs h1 < e1 strictly)
@@ -488,13 +497,12 @@ __device__ __forceinline__ void dp_row_gap(uint32_t tbv, int rc, int &Hp, int &E
     const int E = dppz<DPP_WAVE_SHL1>(q) + K.mexI;
     acc = push_sign(acc, hc - Ep);
     int H1 = imax(Hd, E);
-    if (LOCAL) H1 = imax(H1, BIAS);
-    // horizontal (deletion) moves: prefix max of X = H1 + exD * lane
-    const int X = H1 + K.xD;
-    const int P = scan_max(X);
+    if (LOCAL) H1 = imax(H1, K.floor);
+    // horizontal (deletion) moves: prefix max of X = H1~ over the lanes
+    const int P = scan_max(H1);
     const int F = dppz<DPP_WAVE_SHR1>(P) + K.cF;
     const int H = imax(H1, F);
-    acc = push_sign(acc, X - P);
+    acc = push_sign(acc, H1 - P);
     acc = push_sign(acc, Hd - H);
     acc = push_sign(acc, E - H);
     if (LOCAL) {
@@ -509,11 +517,12 @@ __device__ __forceinline__ void dp_row_gap(uint32_t tbv, int rc, int &Hp, int &E
 // nibble is 0: a local cell at H == 0 is a stop the traceback sees from H.
 template <int LOCAL>
 __device__ __forceinline__ void dp_row_nogap(uint32_t tbv, int rc, int &Hp, int &Ep,
-                                             uint32_t &bestKey, int ci, uint32_t &acc)
+                                             uint32_t &bestKey, int ci, int floor, uint32_t &acc)
 {
-    int H = Hp + (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4) - 8;
+    const int nib = (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4);
+    int H = LOCAL ? Hp + nib - 8 : Hp + nib;
     if (LOCAL) {
-        H = imax(H, BIAS);
+        H = imax(H, floor);
         const uint32_t key = ((uint32_t)H << 10) | (uint32_t)ci;   // ci < 1024
         bestKey = bestKey > key ? bestKey : key;
     }
@@ -694,10 +703,10 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     const int ma = LOCAL ? 2 : 0;
     const int n_work = A.counters[0];
     DpConst K;
-    K.mexI = in_vgpr(-A.exI);
+    K.mexI = in_vgpr(-(A.exI + A.exD) + (LOCAL ? 0 : 8));
     K.dIE = A.exI - A.oeI;
-    K.xD = lane * A.exD;
-    K.cF = -(A.oeD - A.exD) - A.exD * lane;
+    K.cF = in_vgpr(-(A.oeD - A.exD));
+    K.floor = BIAS + A.exD * lane;
 
     int64_t ck_base = 0;   // lane 0: this wave's current CIGAR pool chunk
     int ck_left = 0;
@@ -798,7 +807,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             // ---- DP over rows, 8 rows per group (one u32 of traceback bits per
             // lane); groups wholly inside the gap window run branch-free; the next
             // group's operands come from LDS ----
-            int Hp = BIAS, Ep = 0;
+            int Hp = BIAS + A.exD * lane, Ep = 0;   // row -1: H = 0 (shifted, see DpConst)
             uint32_t bestKey = 0;
             for (int i0 = 0; i0 < m; i0 += 8) {
                 uint32_t tbv[8];
@@ -821,17 +830,17 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
                         else if (i >= GBAR && i < m - GBAR)
                             dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K, acc);
                         else
-                            dp_row_nogap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, acc);
+                            dp_row_nogap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K.floor, acc);
                     }
                 }
                 bits[(i0 >> 3) * 64 + lane] = acc;
             }
             int bestH, bestI;
             if (LOCAL) {
-                bestH = (int)(bestKey >> 10) - BIAS;
+                bestH = (int)(bestKey >> 10) - BIAS - A.exD * lane;
                 bestI = 1023 - (int)(bestKey & 1023u);
             } else {
-                bestH = Hp - BIAS;   // end-to-end: the last row
+                bestH = Hp - BIAS - A.exD * lane - 8 * m;   // end-to-end: the last row
                 bestI = m - 1;
             }
             // best cell: max score, then smallest row, then smallest lane
