@@ -212,6 +212,76 @@ __device__ __forceinline__ bool cand_before(const Cand &x, const Cand &y)
     return x.center < y.center;
 }
 
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m)
+{
+    const int lo = __shfl_xor((int)(uint32_t)v, m), hi = __shfl_xor((int)(v >> 32), m);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Candidate clustering of <= 64 seed hits, one per lane (v; ~0 past total):
+// a bitonic sort across the lanes, then cluster and run boundaries as
+// ballots, and per cluster (a wave-uniform loop over the boundary bits) the
+// centre as the longest run of equal hits (the first on ties), by one wave
+// max.  The same clusters, centres, supports and top-MAXCAND order as the
+// serial walk below (og_mapper.c find_candidates); writes the candidates.
+__device__ int cluster_lanes(const SeedArgs &A, int64_t r, int lane, uint64_t v, int total,
+                             Cand *best)
+{
+    int N = 2;
+    while (N < total) N <<= 1;
+    for (int k = 2; k <= N; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t o = shfl_xor64(v, j);
+            const bool take_min = ((lane & j) == 0) == ((lane & k) == 0);
+            v = take_min ? (o < v ? o : v) : (o > v ? o : v);
+        }
+    }
+    const uint64_t pv = ((uint64_t)(uint32_t)dpp<DPP_WAVE_SHR1>(0, (int)(v >> 32)) << 32) |
+                        (uint32_t)dpp<DPP_WAVE_SHR1>(0, (int)(uint32_t)v);   // lane - 1's hit
+    const bool valid = lane < total;
+    const int dg = (int)(uint32_t)v - (1 << 30), pdg = (int)(uint32_t)pv - (1 << 30);
+    const bool bnd = valid && (lane == 0 || (v >> 32) != (pv >> 32) || dg - pdg > CLUSTER_GAP);
+    const bool rst = valid && (lane == 0 || v != pv);
+    uint64_t bm = __builtin_amdgcn_ballot_w64(bnd);
+    const uint64_t rm = __builtin_amdgcn_ballot_w64(rst);
+    const uint64_t above = lane == 63 ? 0ull : rm & (~0ull << (lane + 1));
+    const int runlen = (above ? (int)__builtin_ctzll(above) : total) - lane;
+    int nc = 0;
+    while (bm) {
+        const int cs = (int)__builtin_ctzll(bm);
+        bm &= bm - 1;
+        const int ce = bm ? (int)__builtin_ctzll(bm) : total;
+        const int key = (rst && lane >= cs && lane < ce) ? (runlen << 6) | (63 - lane) : -1;
+        const int cl = 63 - (wave_max(key) & 63);
+        const uint64_t v0 = readlane64(v, cs);
+        const int center = (int)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, cl) - (1 << 30);
+        const Cand c{(int)(v0 >> 62), (int)((v0 >> 32) & 0x3fffffff), center, ce - cs};
+        if (lane == 0) {
+            int at = nc;
+            while (at > 0 && cand_before(c, best[at - 1])) --at;
+            if (at < MAXCAND) {
+                const int last = nc < MAXCAND ? nc : MAXCAND - 1;
+                for (int z = last; z > at; --z) best[z] = best[z - 1];
+                best[at] = c;
+                if (nc < MAXCAND) ++nc;
+            }
+        }
+    }
+    if (lane == 0) {
+        for (int c = 0; c < nc; ++c) A.cand[r * MAXCAND + c] = best[c];
+        A.n_cand[r] = nc;
+    }
+    wave_sync();
+    return __builtin_amdgcn_readfirstlane(nc);
+}
+
 // Seeds, hit sort and candidate clustering of read r by one wave; writes the
 // candidates, n_cand and yf, returns the candidate count (wave-uniform).
 __device__ int seed_read(const SeedArgs &A, int64_t r, int lane, uint64_t *hits, Cand *best)
@@ -278,6 +348,10 @@ __device__ int seed_read(const SeedArgs &A, int64_t r, int lane, uint64_t *hits,
     if (total == 0) {
         if (lane == 0) A.n_cand[r] = 0;
         return 0;
+    }
+    if (total <= 64) {   // one hit per lane: register sort, lane-parallel clusters
+        wave_sync();
+        return cluster_lanes(A, r, lane, lane < total ? hits[lane] : ~0ull, total, best);
     }
     int N = 1;
     while (N < total) N <<= 1;
