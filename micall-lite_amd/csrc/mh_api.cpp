@@ -527,6 +527,8 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipFree(c->gotoh_buf);
     hipFree(P.dense); hipFree(P.nflag); hipFree(P.dflag); hipFree(P.read_counts);
     hipFree(P.first_unit); hipFree(P.max_pos); hipFree(P.ev); hipFree(P.ev_pool);
+    hipFree(P.tok_slot); hipFree(P.tok_cnt); hipFree(P.tok_used); hipFree(P.tok_meta);
+    hipFree(P.tok_bytes);
     hipFree(P.ev_counters);
     hipFree(P.ins_scratch);
     hipFree(P.sel);
@@ -1165,72 +1167,17 @@ static int aggregate_tokens(CtxEx &c)
     if (P.ev_counters) MH_HIP(hipMemcpy(ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
     const int64_t ne = ctr[0];
     if (ne > 0) {
-        std::vector<int32_t> ev(4 * ne);
-        std::string pool((size_t)ctr[1], '\0');
-        MH_HIP(hipMemcpy(ev.data(), P.ev, sizeof(int32_t) * 4 * ne, hipMemcpyDeviceToHost));
-        if (ctr[1] > 0) MH_HIP(hipMemcpy(&pool[0], P.ev_pool, ctr[1], hipMemcpyDeviceToHost));
-        // distinct (ref, pos, token) in open-addressing tables over the event
-        // array (no per-event allocation), partitioned by hash over host
-        // threads, then the few distinct keys sorted in (ref, pos, token) order
+        // distinct (ref, pos, token) keys and their counts come from the
+        // device (run_token_aggregate); only their order is fixed here
+        std::vector<int32_t> meta;
+        std::string bytes;
+        if (int st = run_token_aggregate(c, ne, meta, bytes)) return st;
         struct Key { int32_t ref, pos, off, len; int64_t count; };
-        const char *pb = pool.data();
-        std::vector<uint64_t> hv((size_t)ne);
-        const int nt = std::max(1, std::min(s2a_threads(), (int)(ne >> 13) + 1));
-        par_for(nt, [&](int t) {
-            for (int64_t e = ne * t / nt; e < ne * (t + 1) / nt; ++e) {
-                const int32_t r = ev[4 * e], ps = ev[4 * e + 1], of = ev[4 * e + 2], ln = ev[4 * e + 3];
-                uint64_t h = 1469598103934665603ull;
-                for (int32_t x = 0; x < ln; ++x) h = (h ^ (unsigned char)pb[of + x]) * 1099511628211ull;
-                h ^= ((uint64_t)(uint32_t)r << 32) | (uint32_t)ps;
-                h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33;
-                hv[e] = h;
-            }
-        });
-        std::vector<std::vector<Key>> part(nt);
-        par_for(nt, [&](int t) {
-            std::vector<Key> &uniq = part[t];
-            uint64_t cap = 64;
-            while (cap < 2 * (uint64_t)ne / nt + 64) cap <<= 1;
-            std::vector<int32_t> slot(cap, -1);
-            for (int64_t e = 0; e < ne; ++e) {
-                const uint64_t h = hv[e];
-                if ((int)((h >> 40) % (uint64_t)nt) != t) continue;
-                const int32_t r = ev[4 * e], ps = ev[4 * e + 1], of = ev[4 * e + 2], ln = ev[4 * e + 3];
-                uint64_t i = h & (cap - 1);
-                for (;;) {
-                    const int32_t u = slot[i];
-                    if (u < 0) {
-                        if (uniq.size() * 2 >= cap) {   // grow: rehash the distinct keys
-                            cap <<= 1;
-                            slot.assign(cap, -1);
-                            for (size_t z = 0; z < uniq.size(); ++z) {
-                                const Key &k = uniq[z];
-                                uint64_t hz = 1469598103934665603ull;
-                                for (int32_t x = 0; x < k.len; ++x) hz = (hz ^ (unsigned char)pb[k.off + x]) * 1099511628211ull;
-                                hz ^= ((uint64_t)(uint32_t)k.ref << 32) | (uint32_t)k.pos;
-                                hz ^= hz >> 33; hz *= 0xff51afd7ed558ccdull; hz ^= hz >> 33;
-                                uint64_t j = hz & (cap - 1);
-                                while (slot[j] >= 0) j = (j + 1) & (cap - 1);
-                                slot[j] = (int32_t)z;
-                            }
-                            i = h & (cap - 1);
-                            continue;
-                        }
-                        slot[i] = (int32_t)uniq.size();
-                        uniq.push_back(Key{r, ps, of, ln, 1});
-                        break;
-                    }
-                    Key &k = uniq[u];
-                    if (k.ref == r && k.pos == ps && k.len == ln && std::memcmp(pb + k.off, pb + of, ln) == 0) {
-                        ++k.count;
-                        break;
-                    }
-                    i = (i + 1) & (cap - 1);
-                }
-            }
-        });
-        std::vector<Key> uniq;
-        for (auto &p : part) uniq.insert(uniq.end(), p.begin(), p.end());
+        const size_t nd = meta.size() / 5;
+        std::vector<Key> uniq(nd);
+        for (size_t d = 0; d < nd; ++d)
+            uniq[d] = Key{meta[5 * d], meta[5 * d + 1], meta[5 * d + 2], meta[5 * d + 3], meta[5 * d + 4]};
+        const char *pb = bytes.data();
         std::sort(uniq.begin(), uniq.end(), [pb](const Key &a, const Key &b) {
             if (a.ref != b.ref) return a.ref < b.ref;
             if (a.pos != b.pos) return a.pos < b.pos;

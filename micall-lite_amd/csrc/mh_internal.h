@@ -149,6 +149,16 @@ struct PileState {
     int sel_cap = 0;
     char *ins_scratch = nullptr;    // per-wave merged-insertion scratch of k_pileup
     int64_t ins_scratch_bytes = 0;
+    // device aggregation of the token events (mh_pileup_events): an
+    // open-addressing table of representative event + count per distinct
+    // (ref, pos, token), and the list of used slots
+    int32_t *tok_slot = nullptr;    // event index + 1, 0 empty
+    uint32_t *tok_cnt = nullptr;
+    int32_t *tok_used = nullptr;    // [0] = number of distinct keys, then their slots
+    int64_t tok_cap = 0;            // slots (power of two)
+    int32_t *tok_meta = nullptr;    // gather: per distinct key (ref, pos, off, len, count)
+    char *tok_bytes = nullptr;
+    int64_t tok_meta_cap = 0, tok_bytes_cap = 0;
 };
 
 // ---- kernels' host-side launchers (defined in the .hip files) ----------
@@ -156,6 +166,10 @@ hipError_t launch_pack_reads(DevReads &r, const uint8_t *d_seq, const uint8_t *d
                              const int64_t *d_src_off, hipStream_t s);
 int run_map(struct Ctx &c, const mh_params &par);
 int run_pileup(struct Ctx &c, int source, int q_cutoff);
+// distinct (ref, pos, token) keys of the last pileup's events with their
+// counts, aggregated on the device; tokens concatenated in `bytes` at `off`
+int run_token_aggregate(struct Ctx &c, int64_t n_events, std::vector<int32_t> &meta,
+                        std::string &bytes);
 int run_gotoh(struct Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_global,
               const char *alphabet, const int *matrix, char *out1, char *out2, int cap,
               int *score);

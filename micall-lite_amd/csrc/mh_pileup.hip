@@ -809,6 +809,199 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
     return -2;
 }
 
+// ---- token events aggregated on the device -----------------------------------
+// Every merged pair with an insertion token at a counted position left one
+// event (ref, pos, tok_off, tok_len) and its bytes in the pool.  The host
+// needs the distinct (ref, pos, token) keys with their counts (remap.py's
+// per-position Counter of tokens).  One thread per event hashes its key and
+// claims or joins a slot of an open-addressing table (the first event to claim
+// a slot represents the key; joining compares the bytes with it); the used
+// slots are listed, and a second pass gathers the representatives' metadata and
+// bytes.  Only the distinct keys cross PCIe; the order is fixed on the host by
+// sorting them, so the result does not depend on which event claimed a slot.
+__device__ __forceinline__ uint64_t token_hash(int32_t ref, int32_t pos, const char *b, int32_t len)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (int32_t x = 0; x < len; ++x) h = (h ^ (unsigned char)b[x]) * 1099511628211ull;
+    h ^= ((uint64_t)(uint32_t)ref << 32) | (uint32_t)pos;
+    h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33;
+    return h;
+}
+
+// pass 1: every event finds (or claims) the slot of its key; eslot[e] = slot
+__global__ void k_tok_insert(const int32_t *ev, const char *pool, int64_t ne, int32_t *slot,
+                             int32_t *used, int32_t *eslot, int64_t mask)
+{
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = ev[4 * e], ps = ev[4 * e + 1], of = ev[4 * e + 2], ln = ev[4 * e + 3];
+        int64_t i = (int64_t)(token_hash(r, ps, pool + of, ln) & (uint64_t)mask);
+        for (;;) {
+            int32_t s = slot[i];
+            if (s == 0) {
+                s = atomicCAS(&slot[i], 0, (int32_t)(e + 1));
+                if (s == 0) {   // claimed: this event represents the key
+                    used[1 + atomicAdd(&used[0], 1)] = (int32_t)i;
+                    break;
+                }
+            }
+            const int64_t u = s - 1;
+            bool same = ev[4 * u] == r && ev[4 * u + 1] == ps && ev[4 * u + 3] == ln;
+            for (int32_t x = 0; same && x < ln; ++x) same = pool[ev[4 * u + 2] + x] == pool[of + x];
+            if (same) break;
+            i = (i + 1) & mask;
+        }
+        eslot[e] = (int32_t)i;
+    }
+}
+
+// key number of every used slot (slot -> d)
+__global__ void k_tok_number(const int32_t *used, int32_t *slotid)
+{
+    const int nd = used[0];
+    for (int d = blockIdx.x * blockDim.x + threadIdx.x; d < nd; d += gridDim.x * blockDim.x)
+        slotid[used[1 + d]] = d;
+}
+
+// pass 2: counts per key.  A few blocks, each over a contiguous range of
+// events, count in LDS and add their totals once per key: a popular key gets
+// one global atomic per block instead of one per event.
+constexpr int TOK_LDS_KEYS = 8192;
+__global__ __launch_bounds__(1024) void k_tok_count(const int32_t *eslot, int64_t ne,
+                                                    const int32_t *slotid, const int32_t *used,
+                                                    uint32_t *cnt)
+{
+    __shared__ uint32_t hist[TOK_LDS_KEYS];
+    const int nd = used[0];
+    const bool lds = nd <= TOK_LDS_KEYS;
+    if (lds)
+        for (int d = threadIdx.x; d < nd; d += blockDim.x) hist[d] = 0;
+    __syncthreads();
+    const int64_t per = (ne + gridDim.x - 1) / gridDim.x;
+    const int64_t a = (int64_t)blockIdx.x * per, b = a + per < ne ? a + per : ne;
+    for (int64_t e = a + threadIdx.x; e < b; e += blockDim.x) {
+        const int d = slotid[eslot[e]];
+        if (lds) atomicAdd(&hist[d], 1u);
+        else atomicAdd(&cnt[d], 1u);
+    }
+    __syncthreads();
+    if (lds)
+        for (int d = threadIdx.x; d < nd; d += blockDim.x)
+            if (hist[d]) atomicAdd(&cnt[d], hist[d]);
+}
+
+// distinct key d: meta[5d..5d+4] = (ref, pos, offset in bytes, len, count);
+// offsets are a prefix over the keys' lengths (one wave, serial chunks)
+__global__ void k_tok_gather(const int32_t *ev, const char *pool, const int32_t *slot,
+                             const uint32_t *cnt, const int32_t *used, int32_t *meta,
+                             char *bytes, int64_t bytes_cap, int32_t *overflow)
+{
+    const int lane = threadIdx.x;
+    const int nd = used[0];
+    int base = 0;
+    for (int d0 = 0; d0 < nd; d0 += 64) {
+        const int d = d0 + lane;
+        int32_t ln = 0, u = 0, i = 0;
+        if (d < nd) {
+            i = used[1 + d];
+            u = slot[i] - 1;
+            ln = ev[4 * u + 3];
+        }
+        const int incl = wave_incl_scan(ln, lane);
+        const int off = base + incl - ln;
+        if (d < nd) {
+            meta[5 * d] = ev[4 * u];
+            meta[5 * d + 1] = ev[4 * u + 1];
+            meta[5 * d + 2] = off;
+            meta[5 * d + 3] = ln;
+            meta[5 * d + 4] = (int32_t)cnt[d];
+            if (off + ln <= bytes_cap) {
+                for (int32_t x = 0; x < ln; ++x) bytes[off + x] = pool[ev[4 * u + 2] + x];
+            } else {
+                *overflow = 1;
+            }
+        }
+        base += __builtin_amdgcn_readlane(incl, 63);
+    }
+}
+
+int run_token_aggregate(Ctx &c, int64_t ne, std::vector<int32_t> &meta, std::string &bytes)
+{
+    PileState &P = c.pile;
+    hipStream_t s = c.stream;
+    meta.clear();
+    bytes.clear();
+    if (ne <= 0) return 0;
+    int64_t cap = 1024;
+    while (cap < 2 * ne) cap <<= 1;
+    if (P.tok_cap < cap) {
+        hipFree(P.tok_slot); hipFree(P.tok_cnt); hipFree(P.tok_used);
+        P.tok_slot = nullptr; P.tok_cnt = nullptr; P.tok_used = nullptr; P.tok_cap = 0;
+        // slot (cap), slot -> key number (cap), per-event slot (<= cap / 2)
+        MH_HIP(hipMalloc(&P.tok_slot, sizeof(int32_t) * 2 * cap + sizeof(int32_t) * (cap / 2 + 1)));
+        MH_HIP(hipMalloc(&P.tok_cnt, sizeof(uint32_t) * cap));
+        MH_HIP(hipMalloc(&P.tok_used, sizeof(int32_t) * (cap + 1)));
+        P.tok_cap = cap;
+    }
+    int32_t *slotid = P.tok_slot + cap, *eslot = P.tok_slot + 2 * cap;
+    MH_HIP(hipMemsetAsync(P.tok_slot, 0, sizeof(int32_t) * cap, s));
+    MH_HIP(hipMemsetAsync(P.tok_cnt, 0, sizeof(uint32_t) * cap, s));
+    MH_HIP(hipMemsetAsync(P.tok_used, 0, sizeof(int32_t), s));
+    int64_t blocks = (ne + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_tok_insert, dim3((unsigned)blocks), dim3(256), 0, s, P.ev, P.ev_pool, ne,
+                       P.tok_slot, P.tok_used, eslot, cap - 1);
+    hipLaunchKernelGGL(k_tok_number, dim3(64), dim3(256), 0, s, P.tok_used, slotid);
+    int64_t cblocks = (ne + 4095) / 4096;
+    if (cblocks > 256) cblocks = 256;
+    hipLaunchKernelGGL(k_tok_count, dim3((unsigned)cblocks), dim3(1024), 0, s, eslot, ne, slotid,
+                       P.tok_used, P.tok_cnt);
+    MH_HIP(hipGetLastError());
+    int32_t nd = 0;
+    MH_HIP(hipMemcpyAsync(&nd, P.tok_used, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    MH_HIP(hipStreamSynchronize(s));
+    if (nd <= 0) return 0;
+    // the tokens of the distinct keys: at most every event's bytes; usually few
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        if (P.tok_meta_cap < nd) {
+            hipFree(P.tok_meta);
+            P.tok_meta = nullptr;
+            MH_HIP(hipMalloc(&P.tok_meta, sizeof(int32_t) * 5 * (size_t)nd + sizeof(int32_t)));
+            P.tok_meta_cap = nd;
+        }
+        if (P.tok_bytes_cap < 64 * (int64_t)nd) {
+            hipFree(P.tok_bytes);
+            P.tok_bytes = nullptr;
+            MH_HIP(hipMalloc(&P.tok_bytes, 64 * (size_t)nd));
+            P.tok_bytes_cap = 64 * (int64_t)nd;
+        }
+        int32_t *ovf = P.tok_meta + 5 * (size_t)nd;
+        MH_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), s));
+        hipLaunchKernelGGL(k_tok_gather, dim3(1), dim3(64), 0, s, P.ev, P.ev_pool, P.tok_slot,
+                           P.tok_cnt, P.tok_used, P.tok_meta, P.tok_bytes, P.tok_bytes_cap, ovf);
+        MH_HIP(hipGetLastError());
+        meta.resize(5 * (size_t)nd + 1);
+        MH_HIP(hipMemcpyAsync(meta.data(), P.tok_meta, sizeof(int32_t) * meta.size(),
+                              hipMemcpyDeviceToHost, s));
+        MH_HIP(hipStreamSynchronize(s));
+        const int64_t total = (int64_t)meta[5 * (size_t)(nd - 1) + 2] + meta[5 * (size_t)(nd - 1) + 3];
+        if (!meta.back()) {
+            meta.pop_back();
+            bytes.resize((size_t)total);
+            if (total > 0)
+                MH_HIP(hipMemcpy(&bytes[0], P.tok_bytes, (size_t)total, hipMemcpyDeviceToHost));
+            return 0;
+        }
+        // longer tokens than 64 bytes on average: room for all of them
+        hipFree(P.tok_bytes);
+        P.tok_bytes = nullptr;
+        MH_HIP(hipMalloc(&P.tok_bytes, (size_t)total));
+        P.tok_bytes_cap = total;
+    }
+    set_error("mh_pileup_events: token gather overflow");
+    return -2;
+}
+
 // ---- multi-GPU exchange layout ---------------------------------------------
 // Multi-GPU exchange of the references selected on every rank (those with
 // data anywhere): blockIdx.y = position in sel.  Buffers:
