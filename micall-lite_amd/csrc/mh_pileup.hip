@@ -542,6 +542,13 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
         int mxp = 0;
         int err = 0;
         const int n_ins = *L.n_ins;
+        // the first merged-insertion keys in registers: a position tests them
+        // without a global load (keys are distinct; > 4 is rare)
+        int ik0 = -1, ik1 = -1, ik2 = -1, ik3 = -1;
+        if (n_ins > 0) ik0 = __builtin_amdgcn_readfirstlane(I.key[0]);
+        if (n_ins > 1) ik1 = __builtin_amdgcn_readfirstlane(I.key[1]);
+        if (n_ins > 2) ik2 = __builtin_amdgcn_readfirstlane(I.key[2]);
+        if (n_ins > 3) ik3 = __builtin_amdgcn_readfirstlane(I.key[3]);
         const bool is_hot = ref == A.hot_ref;
         for (int i0 = begin; i0 < len2; i0 += 64) {
             const int i = i0 + lane;
@@ -576,8 +583,11 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
             if (mc == 'N') { A.nflag[cell] = 1; continue; }
             if (mc == '-') { A.dflag[cell] = 1; continue; }
             int hit = -1;
-            for (int z = 0; z < n_ins; ++z)
-                if (I.key[z] == P) hit = z;
+            if (n_ins > 0) {
+                hit = P == ik0 ? 0 : P == ik1 ? 1 : P == ik2 ? 2 : P == ik3 ? 3 : -1;
+                for (int z = 4; z < n_ins; ++z)
+                    if (I.key[z] == P) hit = z;
+            }
             if (hit >= 0 && I.len[hit] > 0 && I.len[hit] % 3 == 0) {
                 const int tl = 1 + I.len[hit];
                 const unsigned long long e = atomicAdd(&A.ev_ctr[0], 1ull);
