@@ -95,6 +95,65 @@ __device__ __forceinline__ void load_row(const PileArgs &A, int64_t row, RowV &v
     v.roff = A.R.off[row];
 }
 
+// The next unit's two rows, prefetched lane-distributed in one VGPR (lanes
+// 0-9: row 1, 32-41: row 2; one field per lane) instead of two RowV in
+// SGPRs that stay live over the whole unit: k_pileup ran out of SGPRs and
+// spilled them to VGPR lanes, paying v_readlane reloads inside its loops.
+// Fields: 0 ref, 1 flag, 2 pos, 3 n_cigar, 4 cig_off, 5 rev, 6 m, 7-8 roff,
+// 9 row valid.
+template <int SRC>
+__device__ __forceinline__ int load_rows_packed(const PileArgs &A, int64_t uu, int lane)
+{
+    const int h = lane >> 5, f = lane & 31;
+    if (f > 9) return 0;
+    int64_t row;
+    if (SRC == 0) row = A.paired ? 2 * uu + h : (h ? -1 : uu);
+    else row = A.units[2 * uu + h];
+    if (row < 0) return 0;
+    if (f == 9) return 1;
+    if (f == 6) return A.R.len[row];
+    if (f >= 7) return ((const int32_t *)A.R.off)[2 * row + (f - 7)];
+    if (SRC == 0) {
+        const int32_t *r = (const int32_t *)&A.rec[row];
+        const int idx = f == 0 ? 10 : f == 1 ? 5 : f == 2 ? 11 : f == 3 ? 19 : f == 4 ? 20 : 2;
+        return r[idx];
+    }
+    switch (f) {
+    case 0: return A.ref[row];
+    case 1: return A.flag[row];
+    case 2: return A.pos[row];
+    case 3: return A.n_cigar[row];
+    case 4: return A.cig_off[row];
+    default: return 0;
+    }
+}
+
+template <int SRC>
+__device__ __forceinline__ RowV unpack_row(const PileArgs &A, int pk, int h)
+{
+    auto fld = [&](int f) { return __builtin_amdgcn_readlane(pk, 32 * h + f); };
+    RowV v;
+    const int valid = fld(9), ref = fld(0), flag = fld(1);
+    v.flag = flag;
+    v.ref = ref;
+    v.pos = fld(2);
+    if (SRC == 0) {
+        v.present = valid && ref >= 0;   // RNAME '*' is not in @SQ (matchmaker)
+        v.n_cigar = (flag & 4) ? 0 : fld(3);
+        v.rev = (flag & 4) ? 0 : fld(5);
+        v.cig = A.pool + (uint32_t)fld(4);
+    } else {
+        v.present = valid;
+        v.n_cigar = fld(3);
+        v.rev = 0;
+        v.cig = A.cigar + (uint32_t)fld(4);
+    }
+    v.m = fld(6);
+    v.roff = (int64_t)(((uint64_t)(uint32_t)fld(8) << 32) | (uint32_t)fld(7));
+    v.op0 = 0;
+    return v;
+}
+
 __device__ __forceinline__ void sam_base(const DevReads &R, const RowV &v, int x, char &c, char &q)
 {
     const int b = v.rev ? v.m - 1 - x : x;
@@ -259,39 +318,31 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
     // the next unit's rows are loaded while this one is processed
     const int64_t ustride = (int64_t)gridDim.x * wpb;
     int64_t u = (int64_t)blockIdx.x * wpb + wv;
-    auto unit_rows = [&](int64_t uu, RowV &a, RowV &b) {
-        int64_t row1, row2;
-        if (SRC == 0) {
-            row1 = A.paired ? 2 * uu : uu;
-            row2 = A.paired ? 2 * uu + 1 : -1;
-        } else {
-            row1 = A.units[2 * uu];
-            row2 = A.units[2 * uu + 1];
-        }
-        load_row<SRC>(A, row1, a);
-        load_row<SRC>(A, row2, b);
-    };
-    RowV n1, n2;
-    n1.present = n2.present = 0;
-    bool ops_ready = false;   // the CIGAR ops of n1 / n2 were fetched (not on a skipped unit)
-    if (u < A.n_units) unit_rows(u, n1, n2);
+    int npk = 0;                  // the next unit's rows, lane-distributed
+    uint32_t nop1 = 0, nop2 = 0;  // and this lane's CIGAR op of their first 64
+    bool ops_ready = false;       // the CIGAR ops of the next unit were fetched
+    if (u < A.n_units) npk = load_rows_packed<SRC>(A, u, lane);
     for (; u < A.n_units; u += ustride) {
-        RowV r1 = n1, r2 = n2;
-        if (!ops_ready) {
+        RowV r1 = unpack_row<SRC>(A, npk, 0), r2 = unpack_row<SRC>(A, npk, 1);
+        if (ops_ready) {
+            r1.op0 = nop1;
+            r2.op0 = nop2;
+        } else {
             fetch_ops(r1, lane);
             fetch_ops(r2, lane);
         }
         ops_ready = false;
         const bool more = u + ustride < A.n_units;
-        if (more) unit_rows(u + ustride, n1, n2);
+        if (more) npk = load_rows_packed<SRC>(A, u + ustride, lane);
         if (SRC == 0 && !r1.present && r2.present) { r1 = r2; r2.present = 0; }  // unpaired view
         if (!r1.present) continue;
         if (r2.present && r1.ref != r2.ref) continue;           // remap.py:96-98
         // the mapped mates (merge_reads filters unmapped ones): m0, m1
         const bool u1 = !(r1.flag & 4), u2 = r2.present && !(r2.flag & 4);
         const int nm = (int)u1 + (int)u2;
-        const RowV m0 = u1 ? r1 : r2, m1 = r2;
-        auto mate = [&](int k) -> RowV { return k ? m1 : m0; };
+        if (!u1) r1 = r2;   // mate 0 is the first mapped one (no copies: SGPRs are scarce)
+        const RowV &m0 = r1;
+        auto mate = [&](int k) -> const RowV & { return k ? r2 : r1; };
         if (nm == 0) continue;                                 // remap.py:111-112
         const int ref = r1.ref;
         if (ref < 0 || ref >= A.n_refs) {
@@ -425,8 +476,11 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
             }
         }
         if (more) {   // the next unit's rows have landed: its CIGAR ops land during the merge
-            fetch_ops(n1, lane);
-            fetch_ops(n2, lane);
+            RowV q1 = unpack_row<SRC>(A, npk, 0), q2 = unpack_row<SRC>(A, npk, 1);
+            fetch_ops(q1, lane);
+            fetch_ops(q2, lane);
+            nop1 = q1.op0;
+            nop2 = q2.op0;
             ops_ready = true;
         }
         // ---- merge_inserts (lane 0, only units with I ops): keys left + pad,
