@@ -133,7 +133,10 @@ int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20);
  * first+n-1): style 0 = tab-separated SAM with
  * optional tags, style 1 = the 11 CSV columns prelim.csv / remap.csv hold
  * (csv.QUOTE_MINIMAL).  Needs names from mh_reads_load_fastq or
- * mh_reads_set_names.  *used = bytes written; -2 if cap is too small. */
+ * mh_reads_set_names.  *used = bytes written; -2 if cap is too small.
+ * buf NULL: a size query; *used = the text's size, and the text is kept
+ * for the next call with the same arguments (a copy into buf, no
+ * reformatting).  Rows are formatted on host threads. */
 int mh_reads_set_names(mh_ctx *ctx, int64_t n, const char *const *names);
 int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
                    const char *const *refnames, char *buf, size_t cap, size_t *used);

@@ -133,6 +133,11 @@ struct CtxEx : Ctx {
     std::vector<int32_t> tok_ref, tok_pos, tok_off, tok_len;
     std::vector<int64_t> tok_count;
     std::string tok_pool;
+    // mh_format_rows: the text of a size query, kept for the copy after it
+    int64_t map_gen = 0;                  // bumped by every mh_map
+    uint64_t fmt_key = 0;
+    bool fmt_valid = false;
+    std::vector<std::string> fmt_chunks;
 };
 
 static void free_index(DevIndex &ix)
@@ -698,6 +703,9 @@ int mh_map(mh_ctx *ctx, const mh_params *par)
     if (st == 0) MH_HIP(hipStreamSynchronize(c->stream));
     prof_flush(*c);
     c->rec_cache.clear();
+    ++c->map_gen;
+    c->fmt_valid = false;
+    c->fmt_chunks.clear();
     return st;
 }
 
@@ -809,6 +817,96 @@ int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20)
     return 0;
 }
 
+// decimal text of v appended to out (no locale, no allocation)
+static inline void put_int(std::string &out, int64_t v)
+{
+    char t[24];
+    int n = 0;
+    uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+    do { t[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+    if (v < 0) out.push_back('-');
+    while (n) out.push_back(t[--n]);
+}
+
+// One row of SAM (style 0) or CSV (style 1) text, appended to out.
+static void format_row(const CtxEx *c, int style, const Rec &a, int64_t r, const uint32_t *pool,
+                       const char *const *refnames, std::string &out, std::string &seq,
+                       std::string &qual)
+{
+    static const char *ytn[4] = {"CP", "DP", "UP", "UU"};
+    static const char *yfn[3] = {"", "NS", "LN"};
+    const char sep = style == 0 ? '\t' : ',';
+    const int L = c->host.len[r];
+    const uint8_t *s = c->host.seq.data() + c->host.off[r];
+    const uint8_t *q = c->host.qual.data() + c->host.off[r];
+    seq.resize(L);
+    qual.resize(L);
+    const bool rev = a.ref >= 0 && a.rev;
+    for (int x = 0; x < L; ++x) {
+        const uint8_t cd = code_of((char)s[x]);
+        if (rev) {
+            seq[L - 1 - x] = "TGCAN"[cd];
+            qual[L - 1 - x] = (char)q[x];
+        } else {
+            seq[x] = "ACGTN"[cd];
+            qual[x] = (char)q[x];
+        }
+    }
+    auto put = [&](const char *p, size_t len) {
+        if (style == 1) csv_field(out, p, len); else out.append(p, len);
+    };
+    const std::string &qn = c->names[r];
+    put(qn.data(), qn.size());
+    out.push_back(sep);
+    put_int(out, a.flag);
+    out.push_back(sep);
+    const char *rn = a.sam_ref >= 0 ? refnames[a.sam_ref] : "*";
+    put(rn, std::strlen(rn));
+    out.push_back(sep);
+    put_int(out, a.sam_pos);
+    out.push_back(sep);
+    put_int(out, a.mapq);
+    out.push_back(sep);
+    if (a.ref < 0) {
+        out.push_back('*');
+    } else {
+        for (int z = 0; z < a.n_cigar; ++z) {
+            const uint32_t op = pool[a.cig_off + z];
+            put_int(out, op >> 4);
+            out.push_back("MIDxS"[op & 7]);
+        }
+    }
+    out.push_back(sep);
+    if (a.rnext == -2) out.push_back('*');
+    else if (a.rnext == -1) out.push_back('=');
+    else put(refnames[a.rnext], std::strlen(refnames[a.rnext]));
+    out.push_back(sep);
+    put_int(out, a.pnext);
+    out.push_back(sep);
+    put_int(out, a.tlen);
+    out.push_back(sep);
+    if (L == 0) out.push_back('*'); else put(seq.data(), seq.size());
+    out.push_back(sep);
+    if (L == 0) out.push_back('*'); else put(qual.data(), qual.size());
+    if (style == 0) {
+        if (a.ref >= 0) {
+            out += "\tAS:i:"; put_int(out, a.score);
+            if (a.secbest != I32MIN) { out += "\tXS:i:"; put_int(out, a.secbest); }
+            out += "\tXN:i:0\tXM:i:"; put_int(out, a.xm);
+            out += "\tXO:i:"; put_int(out, a.xo);
+            out += "\tXG:i:"; put_int(out, a.xg);
+            out += "\tNM:i:"; put_int(out, a.nm);
+            if (a.ys != I32MIN) { out += "\tYS:i:"; put_int(out, a.ys); }
+        } else {
+            if (a.ys != I32MIN) { out += "\tYS:i:"; put_int(out, a.ys); }
+            if (a.yf) { out += "\tYF:Z:"; out += yfn[a.yf]; }
+        }
+        out += "\tYT:Z:";
+        out += ytn[a.yt & 3];
+    }
+    out.push_back('\n');
+}
+
 int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
                    const char *const *refnames, char *buf, size_t cap, size_t *used)
 {
@@ -816,6 +914,20 @@ int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, 
     CtxEx *c = X(ctx);
     MH_HIP(hipSetDevice(c->device));
     if ((int64_t)c->names.size() != c->reads.n) { set_error("no read names loaded"); return -3; }
+    // the text of a size query (buf NULL) is kept for the copy that follows it
+    const uint64_t key = ((uint64_t)style << 62) ^ (uint64_t)(uintptr_t)order * 0x9e3779b97f4a7c15ull ^
+                         ((uint64_t)first << 20) ^ (uint64_t)n ^ (uint64_t)c->map_gen * 0x100000001b3ull;
+    if (buf && c->fmt_key == key && c->fmt_valid) {
+        size_t total = 0;
+        for (const std::string &t : c->fmt_chunks) total += t.size();
+        if (used) *used = total;
+        if (total > cap) { set_error("format buffer too small (%zu needed)", total); return -2; }
+        size_t at = 0;
+        for (const std::string &t : c->fmt_chunks) { std::memcpy(buf + at, t.data(), t.size()); at += t.size(); }
+        c->fmt_chunks.clear();
+        c->fmt_valid = false;
+        return 0;
+    }
     std::vector<Rec> rec;
     std::vector<uint32_t> pool;
     if (order) {
@@ -828,92 +940,32 @@ int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, 
     } else if (int st = fetch_recs(c, first, n, rec, pool)) {
         return st;
     }
-    static const char comp[256] = {};
-    (void)comp;
-    static const char *ytn[4] = {"CP", "DP", "UP", "UU"};
-    static const char *yfn[3] = {"", "NS", "LN"};
-    std::string out;
-    out.reserve((size_t)n * 700);
-    std::string seq, qual, cig, tmp;
-    char nb[64];
-    const char sep = style == 0 ? '\t' : ',';
-    for (int64_t k = 0; k < n; ++k) {
-        const int64_t r = order ? order[first + k] : first + k;
-        const Rec &a = order ? rec[r] : rec[k];
-        const int L = c->host.len[r];
-        const uint8_t *s = c->host.seq.data() + c->host.off[r];
-        const uint8_t *q = c->host.qual.data() + c->host.off[r];
-        seq.resize(L);
-        qual.resize(L);
-        const bool rev = a.ref >= 0 && a.rev;
-        for (int x = 0; x < L; ++x) {
-            const uint8_t cd = code_of((char)s[x]);
-            const char b = "ACGTN"[cd];
-            if (rev) {
-                seq[L - 1 - x] = "TGCAN"[cd];
-                qual[L - 1 - x] = (char)q[x];
-            } else {
-                seq[x] = b;
-                qual[x] = (char)q[x];
-            }
+    // contiguous row ranges on host threads, one text chunk each, in order
+    const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
+    std::vector<std::string> chunks(nt);
+    par_for(nt, [&](int t) {
+        const int64_t k0 = n * t / nt, k1 = n * (t + 1) / nt;
+        std::string &out = chunks[t];
+        out.reserve((size_t)(k1 - k0) * 640);
+        std::string seq, qual;
+        for (int64_t k = k0; k < k1; ++k) {
+            const int64_t r = order ? order[first + k] : first + k;
+            format_row(c, style, order ? rec[r] : rec[k], r, pool.data(), refnames, out, seq, qual);
         }
-        cig.clear();
-        if (a.ref < 0) {
-            cig = "*";
-        } else {
-            for (int z = 0; z < a.n_cigar; ++z) {
-                const uint32_t op = pool[a.cig_off + z];
-                snprintf(nb, sizeof(nb), "%u%c", op >> 4, "MIDxS"[op & 7]);
-                cig += nb;
-            }
-        }
-        const std::string &qn = c->names[r];
-        auto put = [&](const char *p, size_t len) {
-            if (style == 1) csv_field(out, p, len); else out.append(p, len);
-        };
-        put(qn.data(), qn.size());
-        out.push_back(sep);
-        out += std::to_string(a.flag);
-        out.push_back(sep);
-        const char *rn = a.sam_ref >= 0 ? refnames[a.sam_ref] : "*";
-        put(rn, std::strlen(rn));
-        out.push_back(sep);
-        out += std::to_string(a.sam_pos);
-        out.push_back(sep);
-        out += std::to_string(a.mapq);
-        out.push_back(sep);
-        out += cig;
-        out.push_back(sep);
-        if (a.rnext == -2) out += "*";
-        else if (a.rnext == -1) out += "=";
-        else put(refnames[a.rnext], std::strlen(refnames[a.rnext]));
-        out.push_back(sep);
-        out += std::to_string(a.pnext);
-        out.push_back(sep);
-        out += std::to_string(a.tlen);
-        out.push_back(sep);
-        if (L == 0) out += "*"; else put(seq.data(), seq.size());
-        out.push_back(sep);
-        if (L == 0) out += "*"; else put(qual.data(), qual.size());
-        if (style == 0) {
-            if (a.ref >= 0) {
-                out += "\tAS:i:" + std::to_string(a.score);
-                if (a.secbest != I32MIN) out += "\tXS:i:" + std::to_string(a.secbest);
-                out += "\tXN:i:0\tXM:i:" + std::to_string(a.xm) + "\tXO:i:" + std::to_string(a.xo) +
-                       "\tXG:i:" + std::to_string(a.xg) + "\tNM:i:" + std::to_string(a.nm);
-                if (a.ys != I32MIN) out += "\tYS:i:" + std::to_string(a.ys);
-            } else {
-                if (a.ys != I32MIN) out += "\tYS:i:" + std::to_string(a.ys);
-                if (a.yf) { out += "\tYF:Z:"; out += yfn[a.yf]; }
-            }
-            out += "\tYT:Z:";
-            out += ytn[a.yt & 3];
-        }
-        out.push_back('\n');
+    });
+    size_t total = 0;
+    for (const std::string &t : chunks) total += t.size();
+    if (used) *used = total;
+    if (!buf) {
+        c->fmt_chunks.swap(chunks);
+        c->fmt_key = key;
+        c->fmt_valid = true;
+        return 0;
     }
-    if (used) *used = out.size();
-    if (out.size() > cap || !buf) { set_error("format buffer too small (%zu needed)", out.size()); return -2; }
-    std::memcpy(buf, out.data(), out.size());
+    c->fmt_valid = false;
+    if (total > cap) { set_error("format buffer too small (%zu needed)", total); return -2; }
+    size_t at = 0;
+    for (const std::string &t : chunks) { std::memcpy(buf + at, t.data(), t.size()); at += t.size(); }
     return 0;
 }
 

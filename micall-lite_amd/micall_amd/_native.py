@@ -446,17 +446,15 @@ class Context:
             n = self.reads_count()[0] - first
         names = (ctypes.c_char_p * max(self.n_refs, 1))(*[r.encode() for r in self.refnames])
         used = ctypes.c_size_t()
-        cap = max(n, 1) * 900 + 4096
-        for _ in range(2):
-            buf = ctypes.create_string_buffer(cap)
-            st = lib().mh_format_rows(self.h, style, None if order is None else _ptr(order), first,
-                                      n, names, buf, cap, ctypes.byref(used))
-            if st == -2 and used.value > cap:
-                cap = used.value + 16
-                continue
-            check(st, 'mh_format_rows')
-            return buf.raw[:used.value].decode()
-        raise NativeError('mh_format_rows: buffer sizing failed')
+        optr = None if order is None else _ptr(order)
+        # a size query formats the rows (host threads) and keeps the text;
+        # the second call copies it into a buffer of exactly that size
+        check(lib().mh_format_rows(self.h, style, optr, first, n, names, None, 0,
+                                   ctypes.byref(used)), 'mh_format_rows')
+        buf = np.empty(max(used.value, 1), dtype=np.uint8)
+        check(lib().mh_format_rows(self.h, style, optr, first, n, names, _ptr(buf), used.value,
+                                   ctypes.byref(used)), 'mh_format_rows')
+        return buf[:used.value].tobytes().decode()
 
     # ---- pileup ---------------------------------------------------------
     def rows_load(self, flag, ref, pos, cig_off, n_cigar, cigar, seq, qual, offsets, lens, units):
