@@ -12,7 +12,9 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <deque>
 #include <functional>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -982,43 +984,63 @@ int mh_rows_load(mh_ctx *ctx, int64_t n_rows, const int32_t *flag, const int32_t
     hipFree(R.flag); hipFree(R.ref); hipFree(R.pos); hipFree(R.cig_off); hipFree(R.n_cigar);
     hipFree(R.cigar); hipFree(R.units);
     R = RowState{};
-    int64_t ncig = 0;
-    for (int64_t i = 0; i < n_rows; ++i) {
-        if (n_cigar[i] < 0 || n_cigar[i] > MH_MAXOPS || cigar_off[i] < 0) {
-            set_error("rows: bad cigar in row %lld", (long long)i);
-            return -3;
-        }
-        ncig = std::max<int64_t>(ncig, (int64_t)cigar_off[i] + n_cigar[i]);
-        for (int k = 0; k < n_cigar[i]; ++k) {
-            const uint32_t op = cigar[cigar_off[i] + k] & 15;
-            if (op != MH_OP_M && op != MH_OP_I && op != MH_OP_D && op != MH_OP_S && op != 3) {
-                set_error("Unsupported CIGAR token in row %lld", (long long)i);
-                return -3;
+    // row checks, the CIGAR extent, the hot reference (most mapped rows,
+    // smallest id on ties) and the longest reference span, on host threads
+    // over contiguous row blocks; the first bad row (in row order) reports
+    const int nt = std::max(1, std::min(s2a_threads(), (int)(n_rows >> 16) + 1));
+    std::vector<int64_t> t_ncig(nt, 0), t_bad(nt, -1);
+    std::vector<int> t_kind(nt, 0), t_span(nt, 0);
+    std::vector<char> t_ch(nt, 0);
+    std::vector<std::unordered_map<int32_t, int64_t>> t_ref(nt);
+    par_for(nt, [&](int t) {
+        const int64_t a = n_rows * t / nt, b = n_rows * (t + 1) / nt;
+        for (int64_t i = a; i < b; ++i) {
+            if (n_cigar[i] < 0 || n_cigar[i] > MH_MAXOPS || cigar_off[i] < 0) {
+                t_bad[t] = i; t_kind[t] = 1; return;
             }
-        }
-        for (int x = 0; x < lens[i]; ++x) {
-            const char ch = (char)seq[offsets[i] + x];
-            if (ch != 'A' && ch != 'C' && ch != 'G' && ch != 'T' && ch != 'N' && !(flag[i] & 4)) {
-                set_error("row %lld: base letter '%c' (only ACGTN as bowtie2 prints)", (long long)i, ch);
-                return -3;
-            }
-        }
-    }
-    {
-        // hot reference (most mapped rows) and the longest reference span
-        std::unordered_map<int32_t, int64_t> per_ref;
-        int64_t best = 0;
-        for (int64_t i = 0; i < n_rows; ++i) {
-            if (flag[i] & 4) continue;
+            t_ncig[t] = std::max<int64_t>(t_ncig[t], (int64_t)cigar_off[i] + n_cigar[i]);
             int span = 0;
             for (int k = 0; k < n_cigar[i]; ++k) {
-                const uint32_t op = cigar[cigar_off[i] + k];
-                if ((op & 15) == MH_OP_M || (op & 15) == MH_OP_D) span += (int)(op >> 4);
+                const uint32_t w = cigar[cigar_off[i] + k], op = w & 15;
+                if (op != MH_OP_M && op != MH_OP_I && op != MH_OP_D && op != MH_OP_S && op != 3) {
+                    t_bad[t] = i; t_kind[t] = 2; return;
+                }
+                if (op == MH_OP_M || op == MH_OP_D) span += (int)(w >> 4);
             }
-            R.max_span = std::max(R.max_span, span);
-            const int64_t cnt = ++per_ref[ref[i]];
-            if (cnt > best || (cnt == best && ref[i] < R.hot_ref)) { best = cnt; R.hot_ref = ref[i]; }
+            if (!(flag[i] & 4)) {
+                for (int x = 0; x < lens[i]; ++x) {
+                    const char ch = (char)seq[offsets[i] + x];
+                    if (ch != 'A' && ch != 'C' && ch != 'G' && ch != 'T' && ch != 'N') {
+                        t_bad[t] = i; t_kind[t] = 3; t_ch[t] = ch; return;
+                    }
+                }
+                t_span[t] = std::max(t_span[t], span);
+                ++t_ref[t][ref[i]];
+            }
         }
+    });
+    for (int t = 0; t < nt; ++t) {
+        if (t_bad[t] < 0) continue;
+        const long long i = (long long)t_bad[t];
+        if (t_kind[t] == 1) set_error("rows: bad cigar in row %lld", i);
+        else if (t_kind[t] == 2) set_error("Unsupported CIGAR token in row %lld", i);
+        else set_error("row %lld: base letter '%c' (only ACGTN as bowtie2 prints)", i, t_ch[t]);
+        return -3;
+    }
+    int64_t ncig = 0;
+    {
+        std::unordered_map<int32_t, int64_t> per_ref;
+        for (int t = 0; t < nt; ++t) {
+            ncig = std::max(ncig, t_ncig[t]);
+            R.max_span = std::max(R.max_span, t_span[t]);
+            for (auto &kv : t_ref[t]) per_ref[kv.first] += kv.second;
+        }
+        int64_t best = 0;
+        for (auto &kv : per_ref)
+            if (kv.second > best || (kv.second == best && kv.first < R.hot_ref)) {
+                best = kv.second;
+                R.hot_ref = kv.first;
+            }
     }
     const int64_t nr = n_rows > 0 ? n_rows : 1;
     MH_HIP(hipMalloc(&R.flag, sizeof(int32_t) * nr));
@@ -1045,6 +1067,18 @@ int mh_rows_load(mh_ctx *ctx, int64_t n_rows, const int32_t *flag, const int32_t
 }
 
 // ---- prelim.csv reader ------------------------------------------------------
+// std::atoi on a string_view (leading blanks and sign, then digits)
+static int sv_atoi(std::string_view v)
+{
+    size_t i = 0;
+    while (i < v.size() && (v[i] == ' ' || v[i] == '\t')) ++i;
+    bool neg = false;
+    if (i < v.size() && (v[i] == '-' || v[i] == '+')) neg = v[i++] == '-';
+    long long x = 0;
+    while (i < v.size() && v[i] >= '0' && v[i] <= '9') x = x * 10 + (v[i++] - '0');
+    return (int)(neg ? -x : x);
+}
+
 // csv.DictReader semantics for the 11 SAM columns prelim_map writes
 // (prelim_map.py:142-151), then remap.matchmaker (remap.py:853-889) over the
 // rows whose rname is in the @SQ set, then the rows go to the device.
@@ -1056,6 +1090,7 @@ struct CsvRows {
     std::vector<int64_t> off;
     std::vector<int32_t> len;
     std::vector<int64_t> units;
+    std::vector<std::string> qnames_own;   // serial (quoted) path: owned names
 };
 
 }  // namespace mh
@@ -1080,55 +1115,250 @@ extern "C" int mh_rows_load_csv(mh_ctx *ctx, const char *text, int64_t len, int 
         if (col[k] < 0) { set_error("prelim csv: missing column %s", want[k]); return -3; }
     }
     CsvRows R;
-    std::unordered_map<std::string, int64_t> pending;   // qname -> slot in order
-    std::vector<std::pair<int64_t, bool>> order;         // (row, alive) insertion order
-    std::vector<uint32_t> ops;
+    std::vector<std::string_view> qnames;   // per row, into text
     std::unordered_map<std::string, int> unknown;
-    while (csv_record(p, end, f)) {
-        if (f.size() == 1 && f[0].empty()) continue;
-        if ((int)f.size() < 11) { set_error("prelim csv: short row"); return -3; }
-        const int64_t row = (int64_t)R.flag.size();
-        const std::string &qname = f[col[0]], &rname = f[col[2]], &seqs = f[col[9]], &quals = f[col[10]];
-        const int flag = std::atoi(f[col[1]].c_str());
-        auto it = refidx.find(rname);
-        int ref = it == refidx.end() ? -1 : it->second;
-        int nid = ref;
-        if (ref < 0) {
-            auto u = unknown.emplace(rname, (int)unknown.size());
-            nid = -1 - u.first->second;   // '*' and other names outside @SQ
+    std::vector<uint32_t> ops;
+    bool parallel_ok = true;
+    std::vector<std::deque<std::string>> pown;   // unescaped names (stable addresses; qnames views them)
+    {
+        // rows parsed on host threads in contiguous blocks cut at record
+        // ends (a newline outside quotes: the count of '"' before it is
+        // even), concatenated in order.  A record this parser does not take
+        // (a newline inside a quoted field, text after a closing quote)
+        // sends the whole file to the serial csv_record path below.
+        int ncol = 11;   // fields a row needs: up to the last column used
+        for (int k = 0; k < 11; ++k) ncol = std::max(ncol, col[k] + 1);
+        const int64_t bytes = end - p;
+        const int nt = std::max(1, std::min(s2a_threads(), (int)(bytes >> 22) + 1));
+        std::vector<const char *> cut(nt + 1);
+        cut[0] = p;
+        cut[nt] = end;
+        for (int t = 1; t < nt; ++t) {
+            const char *q = p + bytes * t / nt;
+            if (q < cut[t - 1]) q = cut[t - 1];
+            const char *nl = (const char *)std::memchr(q, '\n', (size_t)(end - q));
+            cut[t] = nl ? nl + 1 : end;
         }
-        int maxm = 0;
-        R.cig_off.push_back((int32_t)R.cigar.size());
-        if (!(flag & 4)) {
-            if (!parse_cigar_ops(f[col[5]], ops, maxm)) ops.assign(1, 3u);  // invalid: fails if used
-            if (ops.size() > MH_MAXOPS) ops.assign(1, 3u);
-        } else {
-            ops.clear();
-        }
-        R.cigar.insert(R.cigar.end(), ops.begin(), ops.end());
-        R.n_cigar.push_back((int32_t)ops.size());
-        R.flag.push_back(flag);
-        R.ref.push_back(ref);
-        R.name_id.push_back(nid);
-        R.pos.push_back(std::atoi(f[col[3]].c_str()));
-        R.maxm.push_back(maxm);
-        R.off.push_back((int64_t)R.seq.size());
-        R.len.push_back((int32_t)seqs.size());
-        R.seq.insert(R.seq.end(), seqs.begin(), seqs.end());
-        std::string q = quals;
-        q.resize(seqs.size(), 'J');
-        R.qual.insert(R.qual.end(), q.begin(), q.end());
-        if (ref >= 0) {
-            auto pit = pending.find(qname);
-            if (pit == pending.end()) {
-                pending.emplace(qname, (int64_t)order.size());
-                order.push_back({row, true});
-            } else {
-                order[pit->second].second = false;
-                R.units.push_back(order[pit->second].first);
-                R.units.push_back(row);
-                pending.erase(pit);
+        std::vector<int64_t> nq(nt, 0);
+        par_for(nt, [&](int t) {
+            int64_t k = 0;
+            for (const char *q = cut[t]; q < cut[t + 1]; ++q) k += *q == '"';
+            nq[t] = k;
+        });
+        int64_t par = 0;
+        for (int t = 1; t < nt; ++t) {
+            par += nq[t - 1];
+            if (par & 1) {   // this cut is inside a quoted field: move it on
+                const char *q = cut[t];
+                int64_t seen = 0;
+                while (q < end && !(*q == '\n' && ((par + seen) & 1) == 0)) seen += *q++ == '"';
+                cut[t] = q < end ? q + 1 : end;
+                if (cut[t] > cut[t + 1]) cut[t + 1] = cut[t];
+                par += seen;
+                nq[t] -= seen;
             }
+        }
+        std::vector<CsvRows> part(nt);
+        std::vector<std::vector<std::string_view>> pq(nt);
+        std::vector<std::vector<std::string>> punk(nt);
+        pown.resize(nt);
+        std::vector<int> bad(nt, 0);
+        par_for(nt, [&](int t) {
+            CsvRows &P = part[t];
+            std::vector<uint32_t> lops;
+            std::vector<std::string_view> fv;
+            std::vector<char> fe;   // field holds "" escapes
+            std::string tmp, last_rname = "\x01", cig, seqv;
+            int last_ref = -1;
+            P.flag.reserve((size_t)((cut[t + 1] - cut[t]) / 500 + 16));
+            auto value = [&](size_t i) -> std::string_view {   // unescaped view (tmp may back it)
+                if (!fe[i]) return fv[i];
+                tmp.clear();
+                for (size_t x = 0; x < fv[i].size(); ++x) {
+                    tmp.push_back(fv[i][x]);
+                    if (fv[i][x] == '"') ++x;
+                }
+                return std::string_view(tmp);
+            };
+            const char *q = cut[t], *e = cut[t + 1];
+            while (q < e) {
+                const char *nl = (const char *)std::memchr(q, '\n', (size_t)(e - q));
+                const char *le = nl ? nl : e;
+                const char *next = nl ? nl + 1 : e;
+                if (le > q && le[-1] == '\r') --le;
+                fv.clear();
+                fe.clear();
+                for (const char *s0 = q;;) {
+                    if (s0 < le && *s0 == '"') {
+                        const char *c0 = s0 + 1, *x = c0;
+                        bool esc = false, closed = false;
+                        while (x < le) {
+                            if (*x == '"') {
+                                if (x + 1 < le && x[1] == '"') { esc = true; x += 2; continue; }
+                                closed = true;
+                                break;
+                            }
+                            ++x;
+                        }
+                        if (!closed || (x + 1 < le && x[1] != ',')) { bad[t] = 1; return; }
+                        fv.emplace_back(c0, (size_t)(x - c0));
+                        fe.push_back(esc);
+                        if (x + 1 >= le) break;
+                        s0 = x + 2;
+                        continue;
+                    }
+                    const char *cm = (const char *)std::memchr(s0, ',', (size_t)(le - s0));
+                    if (!cm) { fv.emplace_back(s0, (size_t)(le - s0)); fe.push_back(0); break; }
+                    fv.emplace_back(s0, (size_t)(cm - s0));
+                    fe.push_back(0);
+                    s0 = cm + 1;
+                }
+                q = next;
+                if (fv.size() == 1 && fv[0].empty()) continue;
+                if ((int)fv.size() < ncol) { bad[t] = 2; return; }
+                // rows come grouped by rname: look a name up only when it changes
+                const std::string_view rn = value(col[2]);
+                if (rn != last_rname) {
+                    last_rname.assign(rn.data(), rn.size());
+                    auto it = refidx.find(last_rname);
+                    last_ref = it == refidx.end() ? -1 : it->second;
+                }
+                const int ref = last_ref;
+                const int flag = sv_atoi(value(col[1]));
+                int maxm = 0;
+                P.cig_off.push_back((int32_t)P.cigar.size());
+                if (!(flag & 4)) {
+                    cig.assign(value(col[5]));
+                    if (!parse_cigar_ops(cig, lops, maxm)) lops.assign(1, 3u);
+                    if (lops.size() > MH_MAXOPS) lops.assign(1, 3u);
+                } else {
+                    lops.clear();
+                }
+                P.cigar.insert(P.cigar.end(), lops.begin(), lops.end());
+                P.n_cigar.push_back((int32_t)lops.size());
+                P.flag.push_back(flag);
+                P.ref.push_back(ref);
+                P.name_id.push_back(ref);
+                P.pos.push_back(sv_atoi(value(col[3])));
+                P.maxm.push_back(maxm);
+                seqv.assign(value(col[9]));   // (escapes are possible in principle)
+                const std::string_view quals = value(col[10]);
+                P.off.push_back((int64_t)P.seq.size());
+                P.len.push_back((int32_t)seqv.size());
+                P.seq.insert(P.seq.end(), seqv.begin(), seqv.end());
+                const size_t nqk = std::min(quals.size(), seqv.size());
+                P.qual.insert(P.qual.end(), quals.begin(), quals.begin() + nqk);
+                P.qual.insert(P.qual.end(), seqv.size() - nqk, 'J');
+                if (fe[col[0]]) {
+                    pown[t].emplace_back(value(col[0]));
+                    pq[t].emplace_back(pown[t].back());
+                } else {
+                    pq[t].push_back(fv[col[0]]);
+                }
+                punk[t].push_back(ref < 0 ? last_rname : std::string());
+            }
+        });
+        for (int t = 0; t < nt; ++t)
+            if (bad[t] == 1) parallel_ok = false;
+        if (parallel_ok)
+            for (int t = 0; t < nt; ++t)
+                if (bad[t] == 2) { set_error("prelim csv: short row"); return -3; }
+        if (parallel_ok) {
+            // sizes, then every part copied to its place on its own thread
+            std::vector<int64_t> rb(nt + 1, 0), cb(nt + 1, 0), sb(nt + 1, 0);
+            for (int t = 0; t < nt; ++t) {
+                rb[t + 1] = rb[t] + (int64_t)part[t].flag.size();
+                cb[t + 1] = cb[t] + (int64_t)part[t].cigar.size();
+                sb[t + 1] = sb[t] + (int64_t)part[t].seq.size();
+            }
+            const int64_t nrw = rb[nt];
+            R.flag.resize(nrw); R.ref.resize(nrw); R.pos.resize(nrw); R.cig_off.resize(nrw);
+            R.n_cigar.resize(nrw); R.maxm.resize(nrw); R.name_id.resize(nrw); R.off.resize(nrw);
+            R.len.resize(nrw); R.cigar.resize(cb[nt]); R.seq.resize(sb[nt]); R.qual.resize(sb[nt]);
+            qnames.resize(nrw);
+            for (int t = 0; t < nt; ++t)   // '*' and other names outside @SQ, ids in first-seen order
+                for (size_t i = 0; i < part[t].flag.size(); ++i)
+                    if (part[t].ref[i] < 0) {
+                        auto u = unknown.emplace(punk[t][i], (int)unknown.size());
+                        part[t].name_id[i] = -1 - u.first->second;
+                    }
+            par_for(nt, [&](int t) {
+                const CsvRows &P = part[t];
+                const size_t n0 = P.flag.size(), r0 = (size_t)rb[t];
+                std::copy(P.flag.begin(), P.flag.end(), R.flag.begin() + r0);
+                std::copy(P.ref.begin(), P.ref.end(), R.ref.begin() + r0);
+                std::copy(P.pos.begin(), P.pos.end(), R.pos.begin() + r0);
+                std::copy(P.n_cigar.begin(), P.n_cigar.end(), R.n_cigar.begin() + r0);
+                std::copy(P.maxm.begin(), P.maxm.end(), R.maxm.begin() + r0);
+                std::copy(P.name_id.begin(), P.name_id.end(), R.name_id.begin() + r0);
+                std::copy(P.len.begin(), P.len.end(), R.len.begin() + r0);
+                for (size_t i = 0; i < n0; ++i) {
+                    R.cig_off[r0 + i] = P.cig_off[i] + (int32_t)cb[t];
+                    R.off[r0 + i] = P.off[i] + sb[t];
+                }
+                std::copy(P.cigar.begin(), P.cigar.end(), R.cigar.begin() + cb[t]);
+                std::copy(P.seq.begin(), P.seq.end(), R.seq.begin() + sb[t]);
+                std::copy(P.qual.begin(), P.qual.end(), R.qual.begin() + sb[t]);
+                std::copy(pq[t].begin(), pq[t].end(), qnames.begin() + r0);
+            });
+        }
+    }
+    if (!parallel_ok) {
+        while (csv_record(p, end, f)) {
+            if (f.size() == 1 && f[0].empty()) continue;
+            if ((int)f.size() < 11) { set_error("prelim csv: short row"); return -3; }
+            const std::string &rname = f[col[2]], &seqs = f[col[9]], &quals = f[col[10]];
+            const int flag = std::atoi(f[col[1]].c_str());
+            auto it = refidx.find(rname);
+            int ref = it == refidx.end() ? -1 : it->second;
+            int nid = ref;
+            if (ref < 0) {
+                auto u = unknown.emplace(rname, (int)unknown.size());
+                nid = -1 - u.first->second;   // '*' and other names outside @SQ
+            }
+            int maxm = 0;
+            R.cig_off.push_back((int32_t)R.cigar.size());
+            if (!(flag & 4)) {
+                if (!parse_cigar_ops(f[col[5]], ops, maxm)) ops.assign(1, 3u);  // invalid: fails if used
+                if (ops.size() > MH_MAXOPS) ops.assign(1, 3u);
+            } else {
+                ops.clear();
+            }
+            R.cigar.insert(R.cigar.end(), ops.begin(), ops.end());
+            R.n_cigar.push_back((int32_t)ops.size());
+            R.flag.push_back(flag);
+            R.ref.push_back(ref);
+            R.name_id.push_back(nid);
+            R.pos.push_back(std::atoi(f[col[3]].c_str()));
+            R.maxm.push_back(maxm);
+            R.off.push_back((int64_t)R.seq.size());
+            R.len.push_back((int32_t)seqs.size());
+            R.seq.insert(R.seq.end(), seqs.begin(), seqs.end());
+            std::string q = quals;
+            q.resize(seqs.size(), 'J');
+            R.qual.insert(R.qual.end(), q.begin(), q.end());
+            R.qnames_own.push_back(f[col[0]]);
+        }
+        for (const std::string &x : R.qnames_own) qnames.emplace_back(x);
+    }
+    // matchmaker (remap.py:853-889) over the rows whose rname is in @SQ
+    const int64_t nrow = (int64_t)R.flag.size();
+    std::unordered_map<std::string_view, int64_t> pending;   // qname -> slot in order
+    pending.reserve((size_t)nrow);
+    std::vector<std::pair<int64_t, bool>> order;             // (row, alive) insertion order
+    order.reserve((size_t)nrow);
+    for (int64_t row = 0; row < nrow; ++row) {
+        if (R.ref[row] < 0) continue;
+        const std::string_view qname = qnames[row];
+        auto pit = pending.find(qname);
+        if (pit == pending.end()) {
+            pending.emplace(qname, (int64_t)order.size());
+            order.push_back({row, true});
+        } else {
+            order[pit->second].second = false;
+            R.units.push_back(order[pit->second].first);
+            R.units.push_back(row);
+            pending.erase(pit);
         }
     }
     for (auto &o : order) if (o.second) { R.units.push_back(o.first); R.units.push_back(-1); }

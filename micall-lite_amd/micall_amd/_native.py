@@ -456,6 +456,38 @@ class Context:
                                    ctypes.byref(used)), 'mh_format_rows')
         return buf[:used.value].tobytes().decode()
 
+    def write_rows(self, out, style, first=0, n=None, order=None):
+        """format_rows(...) written to the text file `out`.  For a UTF-8 /
+        ASCII file that writes '\n' as is (the text is ASCII), the bytes go
+        to its binary buffer without a str round trip."""
+        text = self.format_rows_bytes(style, first, n, order)
+        raw = getattr(out, 'buffer', None)
+        enc = (getattr(out, 'encoding', '') or '').lower().replace('-', '')
+        if (raw is not None and enc in ('utf8', 'ascii') and os.linesep == '\n' and
+                getattr(out, '_writenl', None) in (None, '\n')):
+            out.flush()
+            raw.write(text)
+        else:
+            out.write(bytes(text).decode())
+
+    def format_rows_bytes(self, style, first=0, n=None, order=None):
+        """format_rows as a uint8 array (no str)."""
+        if order is not None:
+            order = np.ascontiguousarray(order, dtype=np.int64)
+            if n is None:
+                n = len(order) - first
+        elif n is None:
+            n = self.reads_count()[0] - first
+        names = (ctypes.c_char_p * max(self.n_refs, 1))(*[r.encode() for r in self.refnames])
+        used = ctypes.c_size_t()
+        optr = None if order is None else _ptr(order)
+        check(lib().mh_format_rows(self.h, style, optr, first, n, names, None, 0,
+                                   ctypes.byref(used)), 'mh_format_rows')
+        buf = np.empty(max(used.value, 1), dtype=np.uint8)
+        check(lib().mh_format_rows(self.h, style, optr, first, n, names, _ptr(buf), used.value,
+                                   ctypes.byref(used)), 'mh_format_rows')
+        return memoryview(buf[:used.value])
+
     # ---- pileup ---------------------------------------------------------
     def rows_load(self, flag, ref, pos, cig_off, n_cigar, cigar, seq, qual, offsets, lens, units):
         arrs = [np.ascontiguousarray(a, dtype=t) for a, t in (

@@ -86,7 +86,7 @@ def prelim_map(fastq1, fastq2, prelim_csv,
     order = grouped_order(recs[:, _native.ALN_FIELDS.index('sam_ref')])
     writer = csv.DictWriter(prelim_csv, FIELDNAMES, lineterminator=os.linesep)
     writer.writeheader()
-    prelim_csv.write(ctx.format_rows(1, order=order))
+    ctx.write_rows(prelim_csv, 1, order=order)
     if callback:
         callback(progress=ctx.fastq_line_count / 2)
 

@@ -250,7 +250,7 @@ def _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv, unmapped1, unmap
     again, one reference at a time (remap.py:612-634).  new_counts gains
     each re-mapping's counts; returns the unmapped lines they add."""
     keep_rows, splits = split_mixed_references(ctx, ctx.recs())
-    remap_csv.write(ctx.format_rows(1, order=keep_rows))
+    ctx.write_rows(remap_csv, 1, order=keep_rows)
     extra_unmapped = 0
     for name, (reads1, reads2) in splits.items():
         names, seqs, quals = [], [], []
@@ -264,7 +264,7 @@ def _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv, unmapped1, unmap
         extra_unmapped += unmapped
         new_counts.update(counts)
         _write_unmapped(ctx, ctx.recs(), unmapped1, unmapped2)
-        remap_csv.write(ctx.format_rows(1))
+        ctx.write_rows(remap_csv, 1)
     return extra_unmapped
 
 
