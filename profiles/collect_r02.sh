@@ -22,6 +22,10 @@ if [ "$WHAT" = c2 ] || [ "$WHAT" = all ]; then
   timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
       -T --output-format csv -d $O/c2/pmc_sq -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e > $O/c2/pmc_sq.out 2>&1
   cd $R
+  cp $(ls $O/c2/prof/*kernel_stats.csv $O/c2/prof/*/*kernel_stats.csv 2>/dev/null | head -1) $O/c2/run_kernel_stats.csv
+  python3 profiles/pmc_summary.py $(ls $O/c2/pmc_fetch/*counter_collection.csv $O/c2/pmc_fetch/*/*counter_collection.csv 2>/dev/null | head -1) \
+      $(ls $O/c2/pmc_write/*counter_collection.csv $O/c2/pmc_write/*/*counter_collection.csv 2>/dev/null | head -1) 1000000 $O/c2/pmc_traffic.json
+  python3 profiles/sq_summary.py $(ls $O/c2/pmc_sq/*counter_collection.csv $O/c2/pmc_sq/*/*counter_collection.csv 2>/dev/null | head -1) $O/c2/sq_issue.json
 fi
 if [ "$WHAT" = c4 ] || [ "$WHAT" = all ]; then
   timeout -k 10 400 python3 bench.py --genomes hiv --pairs 5000000 --steps 3 --warmup 1 --breakdown > $O/c4/bench.json 2> $O/c4/bench.err
