@@ -144,8 +144,7 @@ struct CtxEx : Ctx {
 
 static void free_index(DevIndex &ix)
 {
-    hipFree(ix.codes); hipFree(ix.ref_off); hipFree(ix.ref_len); hipFree(ix.hkey);
-    hipFree(ix.hstart); hipFree(ix.hcount); hipFree(ix.hits);
+    hipFree(ix.blob);
     ix = DevIndex{};
 }
 
@@ -226,43 +225,34 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     ix.total = (int64_t)codes.size();
     ix.hmask = cap - 1;
     codes.resize(codes.size() + 64, 4);
-    // (re)allocate only what does not fit the buffers this DevIndex already owns
-    if ((int64_t)codes.size() > ix.cap_codes) {
-        hipFree(ix.codes);
-        ix.codes = nullptr;
-        ix.cap_codes = (int64_t)codes.size() * 2;
-        MH_HIP(hipMalloc(&ix.codes, ix.cap_codes));
+    // one blob: codes, ref_off, ref_len, hkey, hstart, hcount, hits (256-B
+    // aligned parts), staged on the host and uploaded with one copy
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t sz[7] = {codes.size(), sizeof(int64_t) * (size_t)n_refs, sizeof(int32_t) * (size_t)n_refs,
+                          sizeof(uint64_t) * cap, sizeof(uint32_t) * cap, sizeof(uint32_t) * cap,
+                          sizeof(int2) * hits.size()};
+    const void *src[7] = {codes.data(), ref_off.data(), ref_len.data(), hkey.data(), hstart.data(),
+                          hcount.data(), hits.data()};
+    size_t at[7], total = 0;
+    for (int x = 0; x < 7; ++x) { at[x] = total; total += al(sz[x]); }
+    if ((int64_t)total > ix.cap_blob) {   // (re)allocate only when it does not fit
+        hipFree(ix.blob);
+        ix.blob = nullptr;
+        ix.cap_blob = 0;
+        MH_HIP(hipMalloc(&ix.blob, total));
+        ix.cap_blob = (int64_t)total;
     }
-    if (n_refs > ix.cap_refs || !ix.ref_off) {
-        hipFree(ix.ref_off); hipFree(ix.ref_len);
-        ix.ref_off = nullptr; ix.ref_len = nullptr;
-        ix.cap_refs = n_refs > 16 ? n_refs : 16;
-        MH_HIP(hipMalloc(&ix.ref_off, sizeof(int64_t) * ix.cap_refs));
-        MH_HIP(hipMalloc(&ix.ref_len, sizeof(int32_t) * ix.cap_refs));
-    }
-    if ((int64_t)cap > ix.cap_hash) {
-        hipFree(ix.hkey); hipFree(ix.hstart); hipFree(ix.hcount);
-        ix.hkey = nullptr; ix.hstart = nullptr; ix.hcount = nullptr;
-        ix.cap_hash = (int64_t)cap;
-        MH_HIP(hipMalloc(&ix.hkey, sizeof(uint64_t) * cap));
-        MH_HIP(hipMalloc(&ix.hstart, sizeof(uint32_t) * cap));
-        MH_HIP(hipMalloc(&ix.hcount, sizeof(uint32_t) * cap));
-    }
-    if ((int64_t)hits.size() > ix.cap_hits) {
-        hipFree(ix.hits);
-        ix.hits = nullptr;
-        ix.cap_hits = (int64_t)hits.size() * 2;
-        MH_HIP(hipMalloc(&ix.hits, sizeof(int2) * ix.cap_hits));
-    }
-    MH_HIP(hipMemcpy(ix.codes, codes.data(), codes.size(), hipMemcpyHostToDevice));
-    if (n_refs > 0) {
-        MH_HIP(hipMemcpy(ix.ref_off, ref_off.data(), sizeof(int64_t) * n_refs, hipMemcpyHostToDevice));
-        MH_HIP(hipMemcpy(ix.ref_len, ref_len.data(), sizeof(int32_t) * n_refs, hipMemcpyHostToDevice));
-    }
-    MH_HIP(hipMemcpy(ix.hkey, hkey.data(), sizeof(uint64_t) * cap, hipMemcpyHostToDevice));
-    MH_HIP(hipMemcpy(ix.hstart, hstart.data(), sizeof(uint32_t) * cap, hipMemcpyHostToDevice));
-    MH_HIP(hipMemcpy(ix.hcount, hcount.data(), sizeof(uint32_t) * cap, hipMemcpyHostToDevice));
-    MH_HIP(hipMemcpy(ix.hits, hits.data(), sizeof(int2) * hits.size(), hipMemcpyHostToDevice));
+    std::vector<uint8_t> stage(total);
+    for (int x = 0; x < 7; ++x) if (sz[x]) std::memcpy(stage.data() + at[x], src[x], sz[x]);
+    uint8_t *d = (uint8_t *)ix.blob;
+    ix.codes = d + at[0];
+    ix.ref_off = (int64_t *)(d + at[1]);
+    ix.ref_len = (int32_t *)(d + at[2]);
+    ix.hkey = (uint64_t *)(d + at[3]);
+    ix.hstart = (uint32_t *)(d + at[4]);
+    ix.hcount = (uint32_t *)(d + at[5]);
+    ix.hits = (int2 *)(d + at[6]);
+    MH_HIP(hipMemcpy(ix.blob, stage.data(), total, hipMemcpyHostToDevice));
     return 0;
 }
 

@@ -59,9 +59,10 @@ struct DevIndex {
     uint64_t hmask = 0;
     int2 *hits = nullptr;          // (ref, pos) sorted per key
     uint64_t sig = 0;              // content signature (cache key)
-    // allocated capacities (a small index is rebuilt in place every remap pass)
-    int64_t cap_codes = 0, cap_hash = 0, cap_hits = 0;
-    int cap_refs = 0;
+    // every array above lives in one device allocation, uploaded with one
+    // copy (a small index is rebuilt in place every remap pass)
+    void *blob = nullptr;
+    int64_t cap_blob = 0;
 };
 
 constexpr uint64_t HEMPTY = ~0ull;

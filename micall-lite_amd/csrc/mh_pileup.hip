@@ -892,30 +892,72 @@ __device__ __forceinline__ uint64_t token_hash(int32_t ref, int32_t pos, const c
     return h;
 }
 
-// pass 1: every event finds (or claims) the slot of its key; eslot[e] = slot
-__global__ void k_tok_insert(const int32_t *ev, const char *pool, int64_t ne, int32_t *slot,
-                             int32_t *used, int32_t *eslot, int64_t mask)
+__device__ __forceinline__ bool same_event(const int32_t *ev, const char *pool, int64_t u, int32_t r,
+                                           int32_t ps, int32_t of, int32_t ln)
 {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t r = ev[4 * e], ps = ev[4 * e + 1], of = ev[4 * e + 2], ln = ev[4 * e + 3];
-        int64_t i = (int64_t)(token_hash(r, ps, pool + of, ln) & (uint64_t)mask);
-        for (;;) {
-            int32_t s = slot[i];
-            if (s == 0) {
-                s = atomicCAS(&slot[i], 0, (int32_t)(e + 1));
-                if (s == 0) {   // claimed: this event represents the key
-                    used[1 + atomicAdd(&used[0], 1)] = (int32_t)i;
-                    break;
+    bool same = ev[4 * u] == r && ev[4 * u + 1] == ps && ev[4 * u + 3] == ln;
+    for (int32_t x = 0; same && x < ln; ++x) same = pool[ev[4 * u + 2] + x] == pool[of + x];
+    return same;
+}
+
+// pass 1: every event finds (or claims) the slot of its key; eslot[e] = slot.
+// Most events repeat a few keys (one insertion at one position, seen by many
+// reads), and a claim on the global table is a same-address CAS that the
+// device serialises.  Each block therefore first groups its events in an LDS
+// table (the first event of a key in the block leads it); only the leaders go
+// to the global table, and the other events copy their leader's slot.
+constexpr int TOK_LDS_SLOTS = 4096;
+constexpr int TOK_LDS_PROBES = 32;
+__global__ __launch_bounds__(1024) void k_tok_insert(const int32_t *ev, const char *pool, int64_t ne,
+                                                     int32_t *slot, int32_t *used, int32_t *eslot,
+                                                     int64_t mask)
+{
+    __shared__ int32_t lrep[TOK_LDS_SLOTS];    // leader event + 1 (0: free)
+    __shared__ int32_t lglob[TOK_LDS_SLOTS];   // the leader's global slot
+    for (int x = threadIdx.x; x < TOK_LDS_SLOTS; x += blockDim.x) lrep[x] = 0;
+    __syncthreads();
+    const int64_t per = (ne + gridDim.x - 1) / gridDim.x;
+    const int64_t a = (int64_t)blockIdx.x * per, b = a + per < ne ? a + per : ne;
+    for (int64_t e0 = a; e0 < b; e0 += blockDim.x) {   // block-uniform rounds
+        const int64_t e = e0 + threadIdx.x;
+        const bool live = e < b;
+        int32_t r = 0, ps = 0, of = 0, ln = 0;
+        uint64_t h = 0;
+        int li = -1;          // LDS entry of this event's key (-1: table full)
+        bool lead = false;
+        if (live) {
+            r = ev[4 * e]; ps = ev[4 * e + 1]; of = ev[4 * e + 2]; ln = ev[4 * e + 3];
+            h = token_hash(r, ps, pool + of, ln);
+            int x = (int)((h >> 40) & (TOK_LDS_SLOTS - 1));
+            for (int p = 0; p < TOK_LDS_PROBES; ++p, x = (x + 1) & (TOK_LDS_SLOTS - 1)) {
+                int32_t s = lrep[x];
+                if (s == 0) {
+                    s = atomicCAS(&lrep[x], 0, (int32_t)(e + 1));
+                    if (s == 0) { li = x; lead = true; break; }
                 }
+                if (same_event(ev, pool, s - 1, r, ps, of, ln)) { li = x; break; }
             }
-            const int64_t u = s - 1;
-            bool same = ev[4 * u] == r && ev[4 * u + 1] == ps && ev[4 * u + 3] == ln;
-            for (int32_t x = 0; same && x < ln; ++x) same = pool[ev[4 * u + 2] + x] == pool[of + x];
-            if (same) break;
-            i = (i + 1) & mask;
         }
-        eslot[e] = (int32_t)i;
+        __syncthreads();
+        if (live && (lead || li < 0)) {   // global find-or-claim, once per key per block
+            int64_t i = (int64_t)(h & (uint64_t)mask);
+            for (;;) {
+                int32_t s = slot[i];
+                if (s == 0) {
+                    s = atomicCAS(&slot[i], 0, (int32_t)(e + 1));
+                    if (s == 0) {   // claimed: this event represents the key
+                        used[1 + atomicAdd(&used[0], 1)] = (int32_t)i;
+                        break;
+                    }
+                }
+                if (same_event(ev, pool, s - 1, r, ps, of, ln)) break;
+                i = (i + 1) & mask;
+            }
+            eslot[e] = (int32_t)i;
+            if (lead) lglob[li] = (int32_t)i;
+        }
+        __syncthreads();
+        if (live && !lead && li >= 0) eslot[e] = lglob[li];
     }
 }
 
@@ -1011,9 +1053,9 @@ int run_token_aggregate(Ctx &c, int64_t ne, std::vector<int32_t> &meta, std::str
     MH_HIP(hipMemsetAsync(P.tok_slot, 0, sizeof(int32_t) * cap, s));
     MH_HIP(hipMemsetAsync(P.tok_cnt, 0, sizeof(uint32_t) * cap, s));
     MH_HIP(hipMemsetAsync(P.tok_used, 0, sizeof(int32_t), s));
-    int64_t blocks = (ne + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_tok_insert, dim3((unsigned)blocks), dim3(256), 0, s, P.ev, P.ev_pool, ne,
+    int64_t blocks = (ne + 1023) / 1024;
+    if (blocks > 256) blocks = 256;
+    hipLaunchKernelGGL(k_tok_insert, dim3((unsigned)blocks), dim3(1024), 0, s, P.ev, P.ev_pool, ne,
                        P.tok_slot, P.tok_used, eslot, cap - 1);
     hipLaunchKernelGGL(k_tok_number, dim3(64), dim3(256), 0, s, P.tok_used, slotid);
     int64_t cblocks = (ne + 4095) / 4096;

@@ -19,7 +19,8 @@ from collections import Counter
 
 import numpy as np
 
-BASES = np.array(list('ACGT'))
+BASE_CODES = np.frombuffer(b'ACGT', dtype=np.uint8)
+DASH = ord('-')
 
 # micall/alignment/models/HYPHY_NUC.csv, the model of remap.py:33
 HYPHY_NUC_ALPHABET = 'ACGT?'
@@ -94,28 +95,33 @@ class Pileup:
         return bool(self.dense[r].max() > 0) or bool(self.events.get(r))
 
     def tokens(self, r, seed):
-        """Top token per position 1..end-1 (remap.py:318-321)."""
+        """Top token per position 1..end-1 (remap.py:318-321), one byte each
+        (0: no token), and {index: token} for the positions whose top token
+        is longer than one character (a base with its insertion)."""
         end = max(int(self.max_pos[r]), len(seed) if seed else 0) + 1
         length = end - 1
         d, nf, df = self._slice(r, length)
-        tok = np.full(length, None, dtype=object)
+        tok = np.zeros(length, dtype=np.uint8)
         if length:
-            cmax = d.max(axis=1)
-            positive = cmax > 0
+            positive = d.max(axis=1) > 0
             # a positive count wins; ties go to the first of A<C<G<T
-            tok[positive] = BASES[d.argmax(axis=1)[positive]]
+            tok[positive] = BASE_CODES[d.argmax(axis=1)[positive]]
             # otherwise: seed prefill (0) > 'N' (-1) > '-' (-2) > nothing
-            fill = np.full(length, None, dtype=object)
-            fill[df] = '-'
-            fill[nf] = 'N'
+            fill = np.zeros(length, dtype=np.uint8)
+            fill[df] = DASH
+            fill[nf] = ord('N')
             if seed:
                 k = min(len(seed), length)
-                fill[:k] = np.array(list(seed[:k]), dtype=object)
+                fill[:k] = np.frombuffer(seed[:k].encode('latin-1'), dtype=np.uint8)
             tok[~positive] = fill[~positive]
+        longer = {}
         for pos in self.events.get(r, {}):
             if pos <= length:
-                tok[pos - 1] = find_top_token(self.counter_at(r, pos, seed))
-        return tok
+                t = find_top_token(self.counter_at(r, pos, seed))
+                tok[pos - 1] = ord(t[0]) if t else 0
+                if t and len(t) > 1:
+                    longer[pos - 1] = t
+        return tok, longer
 
     def position_sums(self, r, seed, length):
         """sum(counts[pos].values()) for pos 1..length (remap.py:236-238)."""
@@ -136,24 +142,43 @@ def find_top_token(base_counts):
     return top_token
 
 
-def _assemble(tokens):
-    """The deletion-run rule of counts_to_conseqs (remap.py:322-332): a '-'
-    run is kept only when its length is not a multiple of 3; a trailing run
-    is dropped; no token -> 'N'."""
-    out = []
-    deletion = 0
-    for t in tokens:
-        if t is None:
-            out.append('N')
-        elif t == '-':
-            deletion += 1
-        else:
-            if deletion:
-                if deletion % 3 != 0:
-                    out.append('-' * deletion)
-                deletion = 0
-            out.append(t)
-    return ''.join(out)
+def _text(tok, longer, a, b):
+    """Positions [a, b) of a stretch without '-' or missing tokens."""
+    keys = [i for i in longer if a <= i < b]
+    if not keys:
+        return tok[a:b].tobytes().decode('latin-1')
+    parts, at = [], a
+    for i in sorted(keys):
+        parts.append(tok[at:i].tobytes().decode('latin-1'))
+        parts.append(longer[i])
+        at = i + 1
+    parts.append(tok[at:b].tobytes().decode('latin-1'))
+    return ''.join(parts)
+
+
+def _assemble(tok, longer):
+    """The deletion-run rule of counts_to_conseqs (remap.py:322-332) over the
+    token bytes: a missing token writes 'N' at once, a '-' adds to the open
+    deletion, any other token first writes the open deletion when its length
+    is not a multiple of 3.  So each maximal stretch of '-' and missing tokens
+    becomes its 'N's followed by its '-'s (dropped when their count is a
+    multiple of 3, or when the stretch ends the sequence)."""
+    n = len(tok)
+    gap = (tok == DASH) | (tok == 0)
+    if not gap.any():
+        return _text(tok, longer, 0, n)
+    starts = np.flatnonzero(gap & ~np.r_[False, gap[:-1]])
+    ends = np.flatnonzero(gap & ~np.r_[gap[1:], False]) + 1
+    parts, at = [], 0
+    for a, b in zip(starts.tolist(), ends.tolist()):
+        parts.append(_text(tok, longer, at, a))
+        dashes = int(np.count_nonzero(tok[a:b] == DASH))
+        parts.append('N' * (b - a - dashes))
+        if b < n and dashes % 3:
+            parts.append('-' * dashes)
+        at = b
+    parts.append(_text(tok, longer, at, n))
+    return ''.join(parts)
 
 
 def counts_to_conseqs(pile, order, seeds=None):
@@ -164,7 +189,7 @@ def counts_to_conseqs(pile, order, seeds=None):
         seed = seeds.get(name) if seeds else None
         if not pile.has_positive(r):
             continue
-        conseqs[name] = _assemble(pile.tokens(r, seed))
+        conseqs[name] = _assemble(*pile.tokens(r, seed))
     return conseqs
 
 

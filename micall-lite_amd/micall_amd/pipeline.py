@@ -101,6 +101,9 @@ class Shard:
             s = torch.empty(sum_b // 4, dtype=torch.int32, device=dev)
             m = torch.empty(max_b // 4, dtype=torch.int32, device=dev)
             f = torch.empty(max(flag_b, 1), dtype=torch.uint8, device=dev)
+            # the context's stream writes these buffers: torch's stream must be
+            # done with their memory (allocator reuse) first
+            torch.cuda.synchronize(dev)
             ctx.pileup_export(sel, unit_base, s.data_ptr(), m.data_ptr(), f.data_ptr())
             self.dist.all_reduce(s, op=self.dist.ReduceOp.SUM)
             self.dist.all_reduce(m, op=self.dist.ReduceOp.MAX)
@@ -112,6 +115,7 @@ class Shard:
             n_max, b_max = max(int(sizes[:, 0].max()), 1), max(int(sizes[:, 1].max()), 1)
             ev = torch.zeros(4 * n_max, dtype=torch.int32, device=dev)
             pool = torch.zeros(b_max, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize(dev)   # the zero fills run on torch's stream
             ctx.pileup_events_export(ev.data_ptr(), pool.data_ptr())
             ev_all, pool_all = self._gather(ev), self._gather(pool)
             torch.cuda.synchronize(dev)

@@ -1,8 +1,11 @@
 """Child process of tests/test_gpu_shard.py: one rank of a sharded remap run
 (or, with --world 1, the unsharded reference run) on cuda:0, results as JSON.
 
-Ranks use the gloo backend on CUDA tensors, which runs the same device
-export -> all-reduce -> import path that RCCL runs on a multi-GPU node."""
+Ranks use the gloo backend on CUDA tensors by default, which runs the same
+device export -> all-reduce -> import path that RCCL runs on a multi-GPU
+node.  --backend nccl --shard runs that path over RCCL itself with one rank
+(RCCL refuses two ranks on one GPU): every collective, dtype and stream
+hand-off of the multi-GPU exchange executes, with a world of one."""
 import argparse
 import json
 import os
@@ -20,6 +23,8 @@ def main():
     ap.add_argument('--world', type=int, default=1)
     ap.add_argument('--pairs', type=int, default=20000)
     ap.add_argument('--out', required=True)
+    ap.add_argument('--backend', default='gloo')
+    ap.add_argument('--shard', action='store_true', help='use the Shard path even with --world 1')
     args = ap.parse_args()
 
     import torch
@@ -38,8 +43,8 @@ def main():
     device = torch.device('cuda', 0)
     torch.cuda.set_device(device)
     shard = None
-    if args.world > 1:
-        dist.init_process_group('gloo', rank=args.rank, world_size=args.world)
+    if args.world > 1 or args.shard:
+        dist.init_process_group(args.backend, rank=args.rank, world_size=args.world)
         shard = Shard(args.rank, args.world, read_base=2 * lo, device=device)
     ctx = _native.Context(0)
     ctx.reads_load_fixed(reads[2 * lo:2 * hi], quals[2 * lo:2 * hi], True)

@@ -1,0 +1,91 @@
+"""consensus.Pileup.tokens / _assemble (byte arrays, deletion stretches
+vectorised) against a per-position restatement of remap.py:309-333 on
+random pileups that mix seed prefill, 'N' / '-' sentinels, empty positions,
+insertion tokens and deletion runs of every length."""
+from collections import Counter
+
+import numpy as np
+import pytest
+
+from micall_amd.consensus import Pileup, _assemble, find_top_token
+
+
+def _tokens_per_position(pile, r, seed):
+    end = max(int(pile.max_pos[r]), len(seed) if seed else 0) + 1
+    out = []
+    for pos in range(1, end):
+        c = pile.counter_at(r, pos, seed)
+        out.append(find_top_token(c) if c else None)
+    return out
+
+
+def _assemble_loop(tokens):
+    """remap.py:322-332 token by token."""
+    out, deletion = [], 0
+    for t in tokens:
+        if t is None:
+            out.append('N')
+        elif t == '-':
+            deletion += 1
+        else:
+            if deletion:
+                if deletion % 3 != 0:
+                    out.append('-' * deletion)
+                deletion = 0
+            out.append(t)
+    return ''.join(out)
+
+
+@pytest.mark.parametrize('seed_len', [0, 40, 120])
+@pytest.mark.parametrize('rs', range(12))
+def test_tokens_and_assembly_match_the_loop(rs, seed_len):
+    rng = np.random.default_rng(rs)
+    length, cap = 150, 160
+    dense = np.zeros((1, cap, 4), dtype=np.int32)
+    nflag = np.zeros((1, cap), dtype=np.uint8)
+    dflag = np.zeros((1, cap), dtype=np.uint8)
+    kind = rng.integers(0, 6, size=length)
+    for p in range(length):
+        if kind[p] == 0:
+            dense[0, p] = rng.integers(0, 3, size=4)        # ties included
+        elif kind[p] == 1:
+            dflag[0, p] = 1
+        elif kind[p] == 2:
+            nflag[0, p] = 1
+            dflag[0, p] = rng.integers(0, 2)
+    # deletion runs of 1..7 positions
+    for _ in range(4):
+        a = int(rng.integers(0, length - 8))
+        n = int(rng.integers(1, 8))
+        dense[0, a:a + n] = 0
+        nflag[0, a:a + n] = 0
+        dflag[0, a:a + n] = 1
+    events = []
+    for p in rng.choice(np.arange(1, length + 1), size=6, replace=False):
+        for _ in range(int(rng.integers(1, 3))):
+            tok = 'ACGT'[int(rng.integers(0, 4))] + ''.join(rng.choice(list('ACGT'), size=3))
+            events.append((0, int(p), tok, int(rng.integers(1, 4))))
+    seed = ''.join(rng.choice(list('ACGTRY'), size=seed_len)) if seed_len else None
+    fetched = dict(dense=dense, nflag=nflag, dflag=dflag, read_counts=np.array([5]),
+                   first_unit=np.array([0]), max_pos=np.array([length - int(rng.integers(0, 20))]),
+                   cap=cap, events=events)
+    pile = Pileup(fetched, ['r'])
+    want = _tokens_per_position(pile, 0, seed)
+    tok, longer = pile.tokens(0, seed)
+    got = [None if b == 0 else chr(b) for b in tok]
+    for i, t in longer.items():
+        got[i] = t
+    assert got == want
+    assert _assemble(tok, longer) == _assemble_loop(want)
+
+
+def test_assembly_edge_cases():
+    def run(tokens):
+        tok = np.array([0 if t is None else ord(t[0]) for t in tokens], dtype=np.uint8)
+        longer = {i: t for i, t in enumerate(tokens) if t and len(t) > 1}
+        return _assemble(tok, longer), _assemble_loop(tokens)
+    for tokens in ([], ['-'], [None], ['-', '-', '-', 'A'], ['-', None, '-', 'C'],
+                   ['A', '-', '-', None, None], ['ACCT', '-', 'G'], [None, 'ACGT', None],
+                   ['-', '-', 'T', '-', '-', '-', '-', 'G', '-']):
+        got, want = run(tokens)
+        assert got == want, tokens

@@ -49,3 +49,21 @@ def test_two_rank_remap_matches_single_rank(tmp_path):
         got = json.load(open(out))
         for key in ('groups', 'prelim', 'conseqs', 'counts', 'unmapped', 'n_remaps', 'log'):
             assert got[key] == ref[key], key
+
+
+@pytest.mark.timeout(600)
+def test_rccl_shard_path_matches_unsharded(tmp_path):
+    """The Shard exchange over the nccl backend (RCCL), one rank: the
+    collectives the driver's multi-GPU runs use, on device buffers, must leave
+    every result of the unsharded run unchanged."""
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_port()))
+    single = tmp_path / 'single.json'
+    rccl = tmp_path / 'rccl.json'
+    _run([[sys.executable, WORKER, '--world', '1', '--pairs', '8000', '--out', str(single)]], env)
+    _run([[sys.executable, WORKER, '--world', '1', '--pairs', '8000', '--backend', 'nccl', '--shard',
+           '--out', str(rccl)]], env)
+    ref = json.load(open(single))
+    got = json.load(open(rccl))
+    assert ref['conseqs']
+    for key in ('groups', 'prelim', 'conseqs', 'counts', 'unmapped', 'n_remaps', 'log'):
+        assert got[key] == ref[key], key
