@@ -286,6 +286,34 @@ def test_gotoh_pol_sized(ctx):
     assert ctx.gotoh_align(POL, conseq, 15, 3, True, alpha, mat) == want
 
 
+@pytest.mark.parametrize('is_global', [True, False])
+def test_gotoh_long_seq1_global_memory_variant(ctx, is_global):
+    """seq1 too long for the rolling diagonals in LDS (k_gotoh<false>: they
+    stay in global memory), in a batch with a short pair, and a batch of
+    LDS-sized pairs of ragged shapes: both variants equal the oracle."""
+    rng = np.random.default_rng(17)
+    mat, alpha = [5, -4, -4, -4, 0, -4, 5, -4, -4, 0, -4, -4, 5, -4, 0, -4, -4, -4, 5, 0,
+                  0, 0, 0, 0, 0], 'ACGT?'
+    rand = lambda k: ''.join(rng.choice(list('ACGT'), size=k))
+    long1 = POL + rand(2500)                                   # 5,539 nt
+    part = synth.sample_genome(POL, rng, 0.08, 0.01).tobytes().decode()[400:900]
+    pairs = [(long1, part), (part[:37], long1[1000:1011])]
+    got = ctx.gotoh_align_many(pairs, 15, 3, is_global, alpha, mat)
+    for (a, b), g in zip(pairs, got):
+        assert g == oracle.gotoh_align(a, b, 15, 3, is_global, alpha, mat)
+    ragged = [(rand(int(rng.integers(1, 900))), rand(int(rng.integers(1, 900)))) for _ in range(12)]
+    ragged.append((POL[:50], POL[:50]))
+    got = ctx.gotoh_align_many(ragged, 10, 2, is_global, alpha, mat)
+    for (a, b), g in zip(ragged, got):
+        want = None
+        try:
+            want = oracle.gotoh_align(a, b, 10, 2, is_global, alpha, mat)
+        except RuntimeError:
+            assert isinstance(g, RuntimeError)
+            continue
+        assert g == want
+
+
 @pytest.mark.parametrize('mode', [oracle.E2E, oracle.LOCAL])
 def test_map_overhang_trimming(ctx, mode):
     """Reads from a genome that extends past both ends of the reference:
