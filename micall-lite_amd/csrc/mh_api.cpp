@@ -529,6 +529,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipFree(P.ev_counters);
     hipFree(P.ins_scratch);
     hipFree(P.sel);
+    hipFree(P.win_map);
     hipFree(c->len_tab);
     s2a_free(*c);
     censor_free(*c);
@@ -1026,11 +1027,16 @@ int mh_rows_load(mh_ctx *ctx, int64_t n_rows, const int32_t *flag, const int32_t
             for (auto &kv : t_ref[t]) per_ref[kv.first] += kv.second;
         }
         int64_t best = 0;
-        for (auto &kv : per_ref)
+        for (auto &kv : per_ref) {
             if (kv.second > best || (kv.second == best && kv.first < R.hot_ref)) {
                 best = kv.second;
                 R.hot_ref = kv.first;
             }
+            if (kv.first >= 0) {
+                if ((size_t)kv.first >= R.ref_rows.size()) R.ref_rows.resize((size_t)kv.first + 1, 0);
+                R.ref_rows[(size_t)kv.first] += kv.second;
+            }
+        }
     }
     const int64_t nr = n_rows > 0 ? n_rows : 1;
     MH_HIP(hipMalloc(&R.flag, sizeof(int32_t) * nr));

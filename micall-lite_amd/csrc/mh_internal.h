@@ -125,7 +125,8 @@ struct RowState {
     uint32_t *cigar = nullptr;
     int64_t *units = nullptr;
     DevReads reads;
-    int hot_ref = -1;      // reference of most mapped rows (pileup LDS window)
+    int hot_ref = -1;      // reference of most mapped rows
+    std::vector<int64_t> ref_rows;   // mapped rows per reference (pileup LDS windows)
     int max_span = 0;      // longest reference span (M + D) of a mapped row
 };
 
@@ -148,6 +149,8 @@ struct PileState {
     std::vector<int32_t> ref_lens;  // host copy (sizes the LDS window)
     int32_t *sel = nullptr;         // references of a multi-GPU exchange
     int sel_cap = 0;
+    int32_t *win_map = nullptr;     // k_pileup: per reference (LDS window word offset or -1, positions)
+    int win_map_cap = 0;
     char *ins_scratch = nullptr;    // per-wave merged-insertion scratch of k_pileup
     int64_t ins_scratch_bytes = 0;
     // device aggregation of the token events (mh_pileup_events): an

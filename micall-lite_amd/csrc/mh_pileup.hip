@@ -57,9 +57,12 @@ struct PileArgs {
     long long ev_cap, pool_cap;
     unsigned long long *ev_ctr;  // [0] events, [1] pool bytes, [2] overflow, [3] error
     int q_cutoff;
-    // LDS layout: the hot reference's counters for positions 1..win_pos
-    // (A/C/G/T planes) and its per-ref scalars, then one staging area per wave
-    int hot_ref, win_pos;
+    // LDS layout: every reference's scalars (RefLds), the counter windows of
+    // the references that fit (win_map: per reference the window's first
+    // word or -1, and its positions; two u32 per position, A|C<<16 and
+    // G|T<<16), then one staging area per wave
+    const int32_t *win_map;
+    int win_words;
     int span_cap;                // reference span per mate staged in LDS
     int unit_bytes;              // staging bytes per wave
     char *ins_scratch;           // PU_INS_BYTES per wave of the grid
@@ -213,7 +216,7 @@ __device__ inline InsView ins_view(char *base)
     return v;
 }
 
-struct HotLds {
+struct RefLds {
     unsigned int read_count;
     int max_pos;
     long long first_unit;
@@ -304,15 +307,22 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wpb = blockDim.x >> 6;
-    const int WP = A.win_pos;
-    unsigned int *win = (unsigned int *)smem;                 // [4][WP]
-    HotLds *hot = (HotLds *)(smem + (size_t)16 * WP);
-    UnitView L = unit_view(smem + (size_t)16 * WP + sizeof(HotLds) + (size_t)wv * A.unit_bytes,
+    const int NR = A.n_refs;
+    RefLds *rl = (RefLds *)smem;                                   // [NR]
+    int32_t *wmap = (int32_t *)(smem + sizeof(RefLds) * (size_t)NR);   // [NR][2]
+    unsigned int *win = (unsigned int *)(wmap + 2 * NR);           // [win_words]
+    UnitView L = unit_view((unsigned char *)(win + A.win_words) + (size_t)wv * A.unit_bytes,
                            A.span_cap);
     const InsView I = ins_view(A.ins_scratch + ((size_t)blockIdx.x * wpb + wv) * PU_INS_BYTES);
     const unsigned char cut = (unsigned char)(A.q_cutoff + 33);
-    for (int x = threadIdx.x; x < 4 * WP; x += blockDim.x) win[x] = 0;
-    if (threadIdx.x == 0) { hot->read_count = 0; hot->max_pos = 0; hot->first_unit = INT64_MAX; }
+    for (int x = threadIdx.x; x < A.win_words; x += blockDim.x) win[x] = 0;
+    for (int x = threadIdx.x; x < NR; x += blockDim.x) {
+        rl[x].read_count = 0;
+        rl[x].max_pos = 0;
+        rl[x].first_unit = INT64_MAX;
+        wmap[2 * x] = A.win_map[2 * x];
+        wmap[2 * x + 1] = A.win_map[2 * x + 1];
+    }
     __syncthreads();
 
     // the next unit's rows are loaded while this one is processed
@@ -603,7 +613,9 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
         if (n_ins > 1) ik1 = __builtin_amdgcn_readfirstlane(I.key[1]);
         if (n_ins > 2) ik2 = __builtin_amdgcn_readfirstlane(I.key[2]);
         if (n_ins > 3) ik3 = __builtin_amdgcn_readfirstlane(I.key[3]);
-        const bool is_hot = ref == A.hot_ref;
+        // this reference's LDS counter window (wo < 0: none), wl positions
+        const int wo = __builtin_amdgcn_readfirstlane(wmap[2 * ref]);
+        const int wl = __builtin_amdgcn_readfirstlane(wmap[2 * ref + 1]);
         for (int i0 = begin; i0 < len2; i0 += 64) {
             const int i = i0 + lane;
             if (i >= len2) break;
@@ -658,40 +670,38 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
                 }
             } else {
                 const int code = mc == 'A' ? 0 : mc == 'C' ? 1 : mc == 'G' ? 2 : 3;
-                if (is_hot && P <= WP) atomicAdd(&win[code * WP + (P - 1)], 1u);
+                // u16 halves: a block counts < 65536 units (pile_geometry)
+                if (wo >= 0 && P <= wl) atomicAdd(&win[wo + 2 * (P - 1) + (code >> 1)], 1u << (16 * (code & 1)));
                 else atomicAdd(&A.dense[cell * 4 + code], 1);
             }
         }
         mxp = wave_max_all(mxp);
         err = wave_max_all(err);
         if (lane == 0) {
-            if (is_hot) {
-                atomicAdd(&hot->read_count, 1u);
-                atomicMin(&hot->first_unit, (long long)u);
-                if (mxp > 0) atomicMax(&hot->max_pos, mxp);
-            } else {
-                atomicAdd(&A.read_counts[ref], 1ull);
-                atomicMin(&A.first_unit[ref], (long long)u);
-                if (mxp > 0) atomicMax(&A.max_pos[ref], mxp);
-            }
+            atomicAdd(&rl[ref].read_count, 1u);
+            atomicMin(&rl[ref].first_unit, (long long)u);
+            if (mxp > 0) atomicMax(&rl[ref].max_pos, mxp);
             if (err) atomicExch(&A.ev_ctr[3], 1ull);
         }
         __builtin_amdgcn_wave_barrier();
     }
-    // ---- flush the block's hot-reference counters: consecutive threads add
-    // to consecutive words of dense (cell-major, A/C/G/T minor) ----
+    // ---- flush the block's windows (consecutive threads add to consecutive
+    // words of dense: cell-major, A/C/G/T minor) and per-reference scalars ----
     __syncthreads();
-    if (A.hot_ref >= 0) {
-        int32_t *dst = A.dense + (int64_t)A.hot_ref * A.cap * 4;
-        for (int x = threadIdx.x; x < 4 * WP; x += blockDim.x) {
-            const unsigned int v = win[(x & 3) * WP + (x >> 2)];
+    for (int r = 0; r < NR; ++r) {
+        const int wo = wmap[2 * r], wl = wmap[2 * r + 1];
+        if (wo < 0) continue;
+        int32_t *dst = A.dense + (int64_t)r * A.cap * 4;
+        for (int x = threadIdx.x; x < 4 * wl; x += blockDim.x) {
+            const unsigned int v = (win[wo + (x >> 1)] >> (16 * (x & 1))) & 0xffffu;
             if (v) atomicAdd(&dst[x], (int)v);
         }
-        if (threadIdx.x == 0 && hot->read_count) {
-            atomicAdd(&A.read_counts[A.hot_ref], (unsigned long long)hot->read_count);
-            atomicMin(&A.first_unit[A.hot_ref], hot->first_unit);
-            if (hot->max_pos > 0) atomicMax(&A.max_pos[A.hot_ref], hot->max_pos);
-        }
+    }
+    for (int r = threadIdx.x; r < NR; r += blockDim.x) {
+        if (!rl[r].read_count) continue;
+        atomicAdd(&A.read_counts[r], (unsigned long long)rl[r].read_count);
+        atomicMin(&A.first_unit[r], rl[r].first_unit);
+        if (rl[r].max_pos > 0) atomicMax(&A.max_pos[r], rl[r].max_pos);
     }
 }
 
@@ -738,51 +748,72 @@ static int ensure_pile(Ctx &c)
     return 0;
 }
 
-// Launch shape of k_pileup.  The reference most units map to gets its A/C/G/T
-// counters for positions 1..win_pos in LDS, shared by all waves of a block
-// (the memory-side int atomics of the dense counters are the kernel's cost
-// otherwise); the rest of the LDS holds one staging area per wave.
+// Launch shape of k_pileup.  Every reference keeps its scalars (read count,
+// first unit, last position) in LDS, and the references the units map to,
+// most-hit first, get their A/C/G/T counters for positions 1..len+64 in LDS
+// too (two u32 per position, one count per u16 half) as long as they fit
+// beside 8 waves' staging areas: the memory-side int atomics of the dense
+// counters are the kernel's cost otherwise.  The rest holds one staging
+// area per wave.
 struct PileGeometry {
-    int hot_ref = -1, win_pos = 0, span = 0, unit_bytes = 0, wpb = 1;
+    int span = 0, unit_bytes = 0, wpb = 1, win_words = 0;
+    std::vector<int32_t> win_map;   // per reference: first window word (-1: none), positions
     int64_t blocks = 1;
     size_t lds = 0;
 };
 
+// a block's u16 window halves must not wrap: fewer units per block than this
+constexpr int64_t PU_UNITS_PER_BLOCK = 60000;
+
 static int pile_geometry(Ctx &c, int source, int64_t n_units, PileGeometry &g)
 {
     PileState &P = c.pile;
-    int hot = -1, span = 0;
+    const int NR = P.n_refs;
+    std::vector<int64_t> hits((size_t)NR, 0);   // units expected per reference
+    int span = 0;
     if (source == 0) {
         span = c.reads.max_len + BAND;   // M + D <= read length + band width
         const int n = c.map.n_refs;
         std::vector<int64_t> st(5 * (size_t)n + 3);
         MH_HIP(hipMemcpy(st.data(), c.map.ref_stats, sizeof(int64_t) * st.size(), hipMemcpyDeviceToHost));
-        int64_t best = 0;
-        for (int r = 0; r < n && r < P.n_refs; ++r)
-            if (st[2 * n + r] > best) { best = st[2 * n + r]; hot = r; }
+        for (int r = 0; r < n && r < NR; ++r) hits[(size_t)r] = st[2 * (size_t)n + r];
     } else {
         span = c.rows.max_span;
-        hot = c.rows.hot_ref < P.n_refs ? c.rows.hot_ref : -1;
+        for (int r = 0; r < NR && r < (int)c.rows.ref_rows.size(); ++r) hits[(size_t)r] = c.rows.ref_rows[(size_t)r];
     }
     g.span = ((span > 16 ? span : 16) + 15) & ~15;
     g.unit_bytes = (unit_bytes_for(g.span) + 15) & ~15;
-    const int base = (int)sizeof(HotLds);
-    if (base + g.unit_bytes > PU_LDS) { set_error("mh_pileup: reference span %d too long", span); return -3; }
-    if (hot >= 0) {
-        int want = P.ref_lens[hot] + 64;
-        if (want > P.cap) want = P.cap;
-        const int room = (PU_LDS - base - 8 * g.unit_bytes) / 16;
-        g.win_pos = want < room ? want : room;
-        if (g.win_pos < 256) g.win_pos = 0;
+    const size_t base = (sizeof(RefLds) + 2 * sizeof(int32_t)) * (size_t)NR;
+    if (base + (size_t)g.unit_bytes > (size_t)PU_LDS) {
+        set_error("mh_pileup: reference span %d / %d references do not fit in LDS", span, NR);
+        return -3;
     }
-    g.hot_ref = g.win_pos > 0 ? hot : -1;
-    g.wpb = (PU_LDS - base - 16 * g.win_pos) / g.unit_bytes;
+    const int64_t room = (int64_t)PU_LDS - (int64_t)base - 8 * (int64_t)g.unit_bytes;
+    std::vector<int> order((size_t)NR);
+    for (int r = 0; r < NR; ++r) order[(size_t)r] = r;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return hits[(size_t)x] > hits[(size_t)y]; });
+    g.win_map.assign(2 * (size_t)NR, 0);
+    for (int r = 0; r < NR; ++r) g.win_map[2 * (size_t)r] = -1;
+    int64_t words = 0;
+    for (int r : order) {
+        if (hits[(size_t)r] <= 0) break;
+        int want = P.ref_lens[(size_t)r] + 64;
+        if (want > P.cap) want = P.cap;
+        if (want < 1 || 4 * (words + 2 * (int64_t)want) > room) continue;
+        g.win_map[2 * (size_t)r] = (int32_t)words;
+        g.win_map[2 * (size_t)r + 1] = want;
+        words += 2 * (int64_t)want;
+    }
+    g.win_words = (int)words;
+    g.wpb = (int)(((int64_t)PU_LDS - (int64_t)base - 4 * words) / g.unit_bytes);
     if (g.wpb > 16) g.wpb = 16;
     if (g.wpb < 1) g.wpb = 1;
-    g.lds = (size_t)16 * g.win_pos + base + (size_t)g.wpb * g.unit_bytes;
+    g.lds = base + 4 * (size_t)words + (size_t)g.wpb * g.unit_bytes;
     g.blocks = (n_units + g.wpb - 1) / g.wpb;
-    const int64_t max_blocks = g.win_pos > 0 ? 256 : 256 * 8;
+    const int64_t max_blocks = words > 0 ? 256 : 256 * 8;
     if (g.blocks > max_blocks) g.blocks = max_blocks;
+    if (words > 0 && g.blocks < (n_units + PU_UNITS_PER_BLOCK - 1) / PU_UNITS_PER_BLOCK)
+        g.blocks = (n_units + PU_UNITS_PER_BLOCK - 1) / PU_UNITS_PER_BLOCK;
     if (g.blocks < 1) g.blocks = 1;
     return 0;
 }
@@ -814,6 +845,15 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
             P.ins_scratch_bytes = need;
         }
     }
+    if (P.win_map_cap < 2 * P.n_refs || !P.win_map) {
+        hipFree(P.win_map);
+        P.win_map = nullptr;
+        P.win_map_cap = 2 * (P.n_refs > 16 ? P.n_refs : 16);
+        MH_HIP(hipMalloc(&P.win_map, sizeof(int32_t) * P.win_map_cap));
+    }
+    if (P.n_refs > 0)
+        MH_HIP(hipMemcpyAsync(P.win_map, geo.win_map.data(), sizeof(int32_t) * 2 * P.n_refs,
+                              hipMemcpyHostToDevice, s));
     const int64_t cells = (int64_t)P.n_refs * P.cap;
     for (int attempt = 0; attempt < 3; ++attempt) {
         MH_HIP(hipMemsetAsync(P.dense, 0, sizeof(int32_t) * 4 * (cells > 0 ? cells : 1), s));
@@ -840,8 +880,8 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
         A.ev = P.ev; A.ev_pool = P.ev_pool; A.ev_cap = P.ev_cap; A.pool_cap = P.pool_cap;
         A.ev_ctr = (unsigned long long *)P.ev_counters;
         A.q_cutoff = q_cutoff;
-        A.hot_ref = geo.hot_ref;
-        A.win_pos = geo.win_pos;
+        A.win_map = P.win_map;
+        A.win_words = geo.win_words;
         A.span_cap = geo.span;
         A.unit_bytes = geo.unit_bytes;
         A.ins_scratch = P.ins_scratch;

@@ -724,20 +724,6 @@ def format_cutoff(cutoff):
     return cutoff if cutoff == MAX_CUTOFF else '%.3f' % cutoff
 
 
-def _read_all(handle):
-    """The rest of an open aligned.csv: the raw bytes of a text file nothing
-    has read yet (no decode / encode of the whole file), the text otherwise."""
-    raw = getattr(handle, 'buffer', None)
-    if raw is not None:
-        try:
-            fresh = handle.tell() == 0
-        except (OSError, ValueError):
-            fresh = False
-        if fresh and (handle.encoding or '').lower().replace('-', '') in ('utf8', 'ascii'):
-            return raw.read()
-    return handle.read()
-
-
 def aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv,
                failed_align_csv=None, nuc_variants_csv=None, callback=None,
                coverage_summary_csv=None, json=None):
@@ -769,7 +755,7 @@ def aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv,
     if source:
         report.enable_callback(callback, os.stat(source).st_size)
     ctx = session.context()
-    for g in range(ctx.a2c_load_csv(SLOT_REPORT, _read_all(aligned_csv), _CODON_CHARS)):
+    for g in range(ctx.a2c_load_csv(SLOT_REPORT, session.read_text(aligned_csv), _CODON_CHARS)):
         report._read_group(ctx, SLOT_REPORT, g)
         for step in per_run:
             step()

@@ -92,7 +92,7 @@ class RemapRun(RemapPipeline):
         consensus sequences (remap.py:468-541)."""
         region_seqs = dict(self.seeds)
         refnames = list(region_seqs)                      # temp.sam @SQ order
-        rows = self.ctx.rows_load_csv(prelim_csv.read(), refnames)
+        rows = self.ctx.rows_load_csv(session.read_text(prelim_csv), refnames)
         info = rows['info']
         groups = []
         if len(info):

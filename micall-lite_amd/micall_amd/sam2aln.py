@@ -23,7 +23,7 @@ def sam2aln(remap_csv, aligned_csv, insert_csv=None, failed_csv=None, nthreads=N
     """sam2aln.sam2aln (sam2aln.py:395-478)."""
     if len(SAM2ALN_Q_CUTOFFS) != 1:
         raise NotImplementedError('the device merge takes one q-cutoff per pass')
-    text = remap_csv.read()
+    text = session.read_text(remap_csv)
     ctx = session.context()
     ctx.sam2aln_csv(text, q_cutoff=SAM2ALN_Q_CUTOFFS[0], max_prop_n=MAX_PROP_N)
     if insert_csv:

@@ -44,6 +44,27 @@ def load_fastq(fastq1, fastq2=None):
     return ctx
 
 
+def read_text(handle):
+    """The rest of an open CSV/SAM text file for the native parsers: the raw
+    bytes when nothing has read from it yet and it is UTF-8 / ASCII (no
+    decode / encode round trip of a GB-sized file), with the newline
+    translation text mode would have made ('\r\n' and '\r' -> '\n');
+    otherwise handle.read()."""
+    raw = getattr(handle, 'buffer', None)
+    enc = (getattr(handle, 'encoding', '') or '').lower().replace('-', '')
+    if raw is not None and enc in ('utf8', 'ascii') and getattr(handle, 'newlines', None) is None:
+        try:
+            fresh = handle.tell() == 0
+        except (OSError, ValueError):
+            fresh = False
+        if fresh:
+            data = raw.read()
+            if b'\r' in data:
+                data = data.replace(b'\r\n', b'\n').replace(b'\r', b'\n')
+            return data
+    return handle.read()
+
+
 def invalidate():
     """The resident reads were replaced (e.g. by split re-mapping)."""
     global _key
