@@ -59,8 +59,8 @@ struct PileArgs {
     int q_cutoff;
     // LDS layout: every reference's scalars (RefLds), the counter windows of
     // the references that fit (win_map: per reference the window's first
-    // word or -1, and its positions; two u32 per position, A|C<<16 and
-    // G|T<<16), then one staging area per wave
+    // word or -1, and its positions wl: a plane of wl A|C<<16 words, then
+    // a plane of wl G|T<<16 words), then one staging area per wave
     const int32_t *win_map;
     int win_words;
     int span_cap;                // reference span per mate staged in LDS
@@ -671,7 +671,7 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
             } else {
                 const int code = mc == 'A' ? 0 : mc == 'C' ? 1 : mc == 'G' ? 2 : 3;
                 // u16 halves: a block counts < 65536 units (pile_geometry)
-                if (wo >= 0 && P <= wl) atomicAdd(&win[wo + 2 * (P - 1) + (code >> 1)], 1u << (16 * (code & 1)));
+                if (wo >= 0 && P <= wl) atomicAdd(&win[wo + (code >> 1) * wl + (P - 1)], 1u << (16 * (code & 1)));
                 else atomicAdd(&A.dense[cell * 4 + code], 1);
             }
         }
@@ -692,8 +692,8 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
         const int wo = wmap[2 * r], wl = wmap[2 * r + 1];
         if (wo < 0) continue;
         int32_t *dst = A.dense + (int64_t)r * A.cap * 4;
-        for (int x = threadIdx.x; x < 4 * wl; x += blockDim.x) {
-            const unsigned int v = (win[wo + (x >> 1)] >> (16 * (x & 1))) & 0xffffu;
+        for (int x = threadIdx.x; x < 4 * wl; x += blockDim.x) {   // x = 4 position + base
+            const unsigned int v = (win[wo + ((x & 3) >> 1) * wl + (x >> 2)] >> (16 * (x & 1))) & 0xffffu;
             if (v) atomicAdd(&dst[x], (int)v);
         }
     }
@@ -751,7 +751,7 @@ static int ensure_pile(Ctx &c)
 // Launch shape of k_pileup.  Every reference keeps its scalars (read count,
 // first unit, last position) in LDS, and the references the units map to,
 // most-hit first, get their A/C/G/T counters for positions 1..len+64 in LDS
-// too (two u32 per position, one count per u16 half) as long as they fit
+// too (an A|C and a G|T plane, one count per u16 half) as long as they fit
 // beside 8 waves' staging areas: the memory-side int atomics of the dense
 // counters are the kernel's cost otherwise.  The rest holds one staging
 // area per wave.
