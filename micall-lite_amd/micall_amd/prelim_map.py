@@ -19,17 +19,14 @@ import numpy as np
 from . import _native, session
 from .projects import ProjectConfig
 
-BOWTIE_THREADS = 4
-BOWTIE_VERSION = '2.2.8'
-BOWTIE_PATH = 'bowtie2'
-BOWTIE_BUILD_PATH = 'bowtie2-build-s'
-
-READ_GAP_OPEN = 10
-READ_GAP_EXTEND = 3
-REF_GAP_OPEN = 10
-REF_GAP_EXTEND = 3
-E2E_SEEDLEN = 22
-MAXINS = 1200
+# Module constants the reference exports (prelim_map.py:25-33); the bowtie2
+# names only describe the command contract the HIP mapper stands in for.
+BOWTIE_THREADS, BOWTIE_VERSION = 4, '2.2.8'
+BOWTIE_PATH, BOWTIE_BUILD_PATH = 'bowtie2', 'bowtie2-build-s'
+READ_GAP_OPEN, READ_GAP_EXTEND = 10, 3      # --rdg
+REF_GAP_OPEN, REF_GAP_EXTEND = 10, 3        # --rfg
+E2E_SEEDLEN = 22                            # -L of the end-to-end preset
+MAXINS = 1200                               # -X
 
 FIELDNAMES = ['qname', 'flag', 'rname', 'pos', 'mapq', 'cigar', 'rnext', 'pnext', 'tlen', 'seq',
               'qual']
@@ -39,11 +36,10 @@ logger = logging.getLogger(__name__)
 
 def check_fastq(fastq1, fastq2):
     """prelim_map.py:62-69 / remap.py:415-422: exit(1) on a missing file."""
-    if not os.path.exists(fastq1):
-        logger.error('No FASTQ found at %s', fastq1)
-        sys.exit(1)
-    if fastq2 is not None and not os.path.exists(fastq2):
-        logger.error('No FASTQ found at %s', fastq2)
+    for path in (fastq1, fastq2):
+        if path is None or os.path.exists(path):
+            continue
+        logger.error('No FASTQ found at %s', path)
         sys.exit(1)
 
 
@@ -91,22 +87,24 @@ def prelim_map(fastq1, fastq2, prelim_csv,
         callback(progress=ctx.fastq_line_count / 2)
 
 
+_CLI_OPTIONS = (
+    ('-fastq1', dict(help='<input> R1 (or unpaired) FASTQ')),
+    ('-fastq2', dict(default=None, help='<input, optional> R2 FASTQ of a paired run')),
+    ('-prelim_csv', dict(type=argparse.FileType('w'), help='<output> prelim.csv (SAM columns)')),
+    ('--rdgopen', dict(default=None, help='<optional> gap open penalty in the read')),
+    ('--rfgopen', dict(default=None, help='<optional> gap open penalty in the reference')),
+    ('--gzip', dict(action='store_true', help='<optional> the FASTQ files are gzipped')),
+    ('--keep', dict(action='store_true', help='<optional> keep the seed FASTA for debugging')),
+)
+
+
 def main():
     parser = argparse.ArgumentParser(
-        description='Map contents of FASTQ R1 and R2 data sets to references (MI355X).')
-    parser.add_argument('-fastq1', help='<input> FASTQ containing forward or unpaired reads')
-    parser.add_argument('-fastq2', default=None,
-                        help='<input, optional> FASTQ containing reverse reads if paired')
-    parser.add_argument('-prelim_csv', type=argparse.FileType('w'),
-                        help='<output> CSV containing preliminary mapping (modified SAM)')
-    parser.add_argument("--rdgopen", default=None, help="<optional> read gap open penalty")
-    parser.add_argument("--rfgopen", default=None, help="<optional> reference gap open penalty")
-    parser.add_argument("--gzip", action='store_true', help="<optional> FASTQs are compressed")
-    parser.add_argument("--keep", action='store_true',
-                        help="<optional> retain temporary files for debugging.")
-    args = parser.parse_args()
-    prelim_map(fastq1=args.fastq1, fastq2=args.fastq2, prelim_csv=args.prelim_csv,
-               rdgopen=args.rdgopen, rfgopen=args.rfgopen, gzip=args.gzip, keep=args.keep)
+        description='Preliminary end-to-end mapping of a FASTQ pair to the seed references (MI355X).')
+    for flag, opts in _CLI_OPTIONS:
+        parser.add_argument(flag, **opts)
+    args = vars(parser.parse_args())
+    prelim_map(**args)
 
 
 if __name__ == '__main__':
