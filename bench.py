@@ -657,12 +657,13 @@ def main():
     total_pairs = args.pairs * world * args.steps
     value = (2 if paired else 1) * total_pairs / elapsed
     # DP cell updates (GCUPS next to the roofline): every
-    # extension the full DP runs is read_len rows x the 64-diagonal band; the
-    # ungapped fast path resolves the rest without the DP
+    # extension the full DP runs is read_len rows x the 31-diagonal band
+    # (seeded diagonal +- 15, bowtie2's maxhalf); the ungapped fast path
+    # resolves the rest without the DP
     ext = sum(int(m[1]) for m in dp_log)
     fast = sum(int(m[3]) for m in dp_log)
     rescue = sum(int(m[4]) for m in dp_log)
-    cells = (ext - fast) * L * 64
+    cells = (ext - fast) * L * 31
     dp_ms = kernels['k_dp'][0] + kernels['k_dp_rescue'][0]
 
     if rank == 0:

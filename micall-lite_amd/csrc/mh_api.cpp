@@ -98,18 +98,44 @@ static int min_score(int mode, int len)
 
 static int n_ceil(int len) { return (int)(0.0 + 0.15 * (double)len); }
 
-static int prepare_len_tab(Ctx &c, int mode)
+// gaps of one kind an alignment can hold and still reach minsc from the
+// perfect score (bowtie2 Scoring::maxReadGaps / maxRefGaps)
+static int max_gaps(int perfect, int minsc, int oe, int ex)
 {
-    if (c.len_tab && c.len_tab_mode == mode) return 0;
-    std::vector<int32_t> t(3 * (MAXLEN + 1));
+    int sc = perfect, num = 0;
+    while (sc >= minsc) {
+        sc -= num == 0 ? oe : ex;
+        ++num;
+    }
+    return num - 1;
+}
+
+// DP band half-width: max(read gaps, ref gaps) capped at maxhalf
+// (DynProgFramer::frameSeedExtensionRect; oracle og_band_half)
+static int band_half(const mh_params &p, int len)
+{
+    const int perfect = p.mode == MH_LOCAL ? 2 * len : 0;
+    const int minsc = min_score(p.mode, len);
+    const int gd = max_gaps(perfect, minsc, p.rdg_open + p.rdg_ext, p.rdg_ext);
+    const int gi = max_gaps(perfect, minsc, p.rfg_open + p.rfg_ext, p.rfg_ext);
+    int h = gd > gi ? gd : gi;
+    if (h > MAXHALF) h = MAXHALF;
+    return h < 0 ? 0 : h;
+}
+
+static int prepare_len_tab(Ctx &c, const mh_params &par)
+{
+    if (c.len_tab && c.len_tab_key == len_tab_key(par)) return 0;
+    std::vector<int32_t> t(4 * (MAXLEN + 1));
     for (int l = 0; l <= MAXLEN; ++l) {
-        t[l] = seed_interval(mode, l);
-        t[(MAXLEN + 1) + l] = min_score(mode, l);
+        t[l] = seed_interval(par.mode, l);
+        t[(MAXLEN + 1) + l] = min_score(par.mode, l);
         t[2 * (MAXLEN + 1) + l] = n_ceil(l);
+        t[3 * (MAXLEN + 1) + l] = band_half(par, l);
     }
     if (!c.len_tab) MH_HIP(hipMalloc(&c.len_tab, sizeof(int32_t) * t.size()));
     MH_HIP(hipMemcpy(c.len_tab, t.data(), sizeof(int32_t) * t.size(), hipMemcpyHostToDevice));
-    c.len_tab_mode = mode;
+    c.len_tab_key = len_tab_key(par);
     return 0;
 }
 
@@ -691,7 +717,7 @@ int mh_map(mh_ctx *ctx, const mh_params *par)
     if (!ctx || !par) return -3;
     CtxEx *c = X(ctx);
     MH_HIP(hipSetDevice(c->device));
-    if (int st = prepare_len_tab(*c, par->mode)) return st;
+    if (int st = prepare_len_tab(*c, *par)) return st;
     int st = run_map(*c, *par);
     if (st == 0) MH_HIP(hipStreamSynchronize(c->stream));
     prof_flush(*c);

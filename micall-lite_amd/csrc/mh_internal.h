@@ -16,8 +16,7 @@ namespace mh {
 
 // Mapper constants (the specification lives in oracle/og_mapper.c, which the
 // kernels reproduce bit for bit).
-constexpr int BAND = 64;            // diagonals per band = lanes of one wave64
-constexpr int HALF = 32;            // band = [center - 32, center + 31]
+constexpr int BAND = 64;            // bound on the diagonals a DP band spans (2 * MAXHALF + 1 <= 64)
 constexpr int MAXCAND = 4;          // extension candidates per mate
 constexpr int MAXHITS_SEED = 64;    // seeds with more exact hits are skipped
 constexpr int MAXHITS_MATE = 512;   // hit budget per mate, in seed order
@@ -28,6 +27,14 @@ constexpr int GBAR = 4;             // --gbar 4
 constexpr int NPEN = 1;             // --np 1
 constexpr int NEG = -(1 << 29);     // minus infinity of the DP
 constexpr int32_t I32MIN = INT32_MIN;
+constexpr int MAXHALF = 15;         // bowtie2's maxhalf: DP band = center +- min(15, max gaps)
+
+// the mapping parameters the per-length tables depend on
+inline int64_t len_tab_key(const mh_params &p)
+{
+    return (int64_t)p.mode | (int64_t)(p.rdg_open & 0xff) << 8 | (int64_t)(p.rdg_ext & 0xff) << 16 |
+           (int64_t)(p.rfg_open & 0xff) << 24 | (int64_t)(p.rfg_ext & 0xff) << 32;
+}
 
 // Reads resident in HBM: each read starts on a 32-base boundary.
 //   seq2 : 2-bit codes, 16 bases per u32, base b at bits 2*(b%16)
@@ -210,12 +217,13 @@ struct Ctx {
     MapState map;
     RowState rows;
     PileState pile;
-    // per-length tables (host-computed, uploaded): seed interval, min score, n ceil
-    int32_t *len_tab = nullptr;      // [3][MAXLEN + 1]
+    // per-length tables (host-computed, uploaded): seed interval, min score,
+    // n ceil, DP band half-width
+    int32_t *len_tab = nullptr;      // [4][MAXLEN + 1]
     S2AState *s2a = nullptr;         // sam2aln rows and results (mh_sam2aln_csv)
     CensorState *censor = nullptr;   // censored FASTQ of the last mh_censor_fastq
     A2CState **a2c = nullptr;        // aln2counts row tables (mh_a2c_*), one per slot
-    int len_tab_mode = -1;
+    int64_t len_tab_key = -1;        // len_tab_key() of the parameters the tables hold
     // k_gotoh's device scratch (traceback planes etc.), grown on demand and
     // kept up to 1 GiB: a hipMalloc / hipFree pair per call cost more than
     // the kernel.  The mutex serialises callers of one context (ctypes

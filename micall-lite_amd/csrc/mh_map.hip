@@ -7,10 +7,12 @@
 //   k_seed        one wave64 per read: 2x32 exact seeds (one lane each),
 //                 hash lookups, hit sort (LDS bitonic), diagonal clustering,
 //                 top-4 candidates + work list
-//   k_dp          one wave64 per candidate: banded affine-gap DP, lane k =
-//                 diagonal center-32+k, rows = read bases; vertical moves by a
-//                 DPP wave shift, horizontal gaps by a DPP prefix-max scan;
-//                 4 traceback bits per cell in LDS; lane-0 traceback -> CIGAR
+//   k_dp          two candidates per wave64 (32 lanes each): banded affine-gap
+//                 DP over the seeded diagonal +- 15 (bowtie2's maxhalf), lane
+//                 = diagonal, rows = read bases; vertical moves by a DPP wave
+//                 shift, horizontal gaps by a DPP prefix-max scan within the
+//                 half; 4 traceback bits per cell in LDS; wave-uniform
+//                 traceback -> CIGAR; an exact ungapped fast path first
 //   k_rescue      paired reads with one aligned mate: the other mate's best
 //                 diagonal in the -X window next to it (mate rescue), then
 //                 k_dp again over those candidates
@@ -29,8 +31,7 @@ __device__ __forceinline__ int dpp(int old, int v)
     return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xF, false);
 }
 constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114,
-              DPP_ROW_SHR8 = 0x118, DPP_WAVE_SHL1 = 0x130, DPP_WAVE_SHR1 = 0x138,
-              DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143;
+              DPP_ROW_SHR8 = 0x118, DPP_WAVE_SHL1 = 0x130, DPP_WAVE_SHR1 = 0x138;
 
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -494,20 +495,19 @@ __device__ __forceinline__ int dppz(int v)
 
 __device__ __forceinline__ uint32_t umin1(int v) { return (uint32_t)v < 1u ? (uint32_t)v : 1u; }
 
-// inclusive prefix max over the 64 lanes (x > 0)
+// inclusive prefix max within each 32-lane half (x > 0): the row shifts,
+// then lane 15 of rows 0 and 2 into rows 1 and 3
 __device__ __forceinline__ int scan_max(int x)
 {
     x = imax(x, dppz<DPP_ROW_SHR1>(x));
     x = imax(x, dppz<DPP_ROW_SHR2>(x));
     x = imax(x, dppz<DPP_ROW_SHR4>(x));
     x = imax(x, dppz<DPP_ROW_SHR8>(x));
-    // cross-row steps in place: rows a step does not write keep x (measured on
+    // the cross-row step in place: rows it does not write keep x (measured on
     // gfx950 with profiles/diag/dpp_probe.hip); the hazard nops of the
-    // VALU-write -> DPP-read pairs are inside the string
+    // VALU-write -> DPP-read pair are inside the string
     asm volatile("s_nop 1\n\t"
                  "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-                 "s_nop 1\n\t"
-                 "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
                  "s_nop 1"
                  : "+v"(x));
     return x;
@@ -612,6 +612,81 @@ __device__ __forceinline__ int wave_excl_scan_min(int v, int /*lane*/, int init)
 }
 
 // ---------------------------------------------------------------------------
+// Two extensions per wave.  Lanes 0-31 hold one extension and lanes 32-63
+// another; lane kl = lane & 31 of a half is diagonal d0 + kl, d0 = center -
+// XCENTER.  The band is the seeded diagonal +- hb (og_band_half: the gap
+// limit bowtie2 puts on its DP rectangle, at most its maxhalf of 15), so
+// lanes 1 .. 31 cover the widest band and lane 0 of a half is never live.  A
+// lane outside its band holds values near 0 (minus infinity under the bias)
+// and its E and F constants are HUGE_NEG; the same constants sit on the top
+// live lane for E and on every dead lane for F, so the two moves that cross
+// between the halves (E into lane 31 from lane 32, F into lane 32 from lane
+// 31) carry nothing.  The deletion scan stops at 32 lanes (no row_bcast:31).
+// ---------------------------------------------------------------------------
+constexpr int XCENTER = 16;            // lane of the seeded diagonal within a half
+constexpr int HUGE_NEG = -(1 << 24);   // an E / F constant that can never win
+constexpr int XREFW_PAD = 48;          // ref window bytes past the last row
+
+// One extension's LDS tables (a wave holds two, after the traceback bits).
+struct XView {
+    uint32_t *tab;    // max(rows_pad, RUNS_CAP): score nibbles per row, then CIGAR runs
+    uint8_t *refw;    // rows_pad + XREFW_PAD: ref code * 4 of diagonal d0 + x
+    uint8_t *rdc;     // rows_pad: read code | mismatch penalty << 3
+    uint8_t *rowk;    // rows_pad: band lane of the M cell of each row, 255 none
+};
+
+__host__ __device__ constexpr int xview_bytes(int rows_pad)
+{
+    return (4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP) + rows_pad + XREFW_PAD + 2 * rows_pad +
+            15) & ~15;
+}
+
+__device__ __forceinline__ XView xview(unsigned char *base, int rows_pad, int h)
+{
+    unsigned char *p = base + (size_t)h * xview_bytes(rows_pad);
+    XView X;
+    X.tab = (uint32_t *)p;
+    p += 4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP);
+    X.refw = p;
+    p += rows_pad + XREFW_PAD;
+    X.rdc = p;
+    X.rowk = p + rows_pad;
+    return X;
+}
+
+// One work item (a candidate extension), wave-uniform.
+struct XItem {
+    int sid, m, reflen, d0, hb, strand, ref;
+    int64_t roff, gref;
+};
+
+// inclusive prefix max within each 32-lane half (rows 0-1 and rows 2-3)
+__device__ __forceinline__ int half_scan_max(int v)
+{
+    v = op_max(v, dpp<0x111>(INT32_MIN, v));
+    v = op_max(v, dpp<0x112>(INT32_MIN, v));
+    v = op_max(v, dpp<0x114>(INT32_MIN, v));
+    v = op_max(v, dpp<0x118>(INT32_MIN, v));
+    v = op_max(v, dpp<0x142, 0xA>(INT32_MIN, v));
+    return v;
+}
+
+// signed 64-bit max of each half (high words, then low words as unsigned
+// among the lanes holding the high maximum); k0 / k1 wave-uniform
+__device__ __forceinline__ void half_max64(long long v, int lane, long long &k0, long long &k1)
+{
+    const int hi = (int)(v >> 32);
+    const int s = half_scan_max(hi);
+    const int h0 = __builtin_amdgcn_readlane(s, 31), h1 = __builtin_amdgcn_readlane(s, 63);
+    const int mine = lane < 32 ? h0 : h1;
+    const int lo = (int)((uint32_t)v ^ 0x80000000u);
+    const int s2 = half_scan_max(hi == mine ? lo : INT32_MIN);
+    const int l0 = __builtin_amdgcn_readlane(s2, 31), l1 = __builtin_amdgcn_readlane(s2, 63);
+    k0 = (long long)(((uint64_t)(uint32_t)h0 << 32) | (uint32_t)(l0 ^ (int)0x80000000u));
+    k1 = (long long)(((uint64_t)(uint32_t)h1 << 32) | (uint32_t)(l1 ^ (int)0x80000000u));
+}
+
+// ---------------------------------------------------------------------------
 // Exact ungapped fast path of k_dp.
 //
 // Every path through the band that contains a gap pays at least one open +
@@ -629,21 +704,24 @@ __device__ __forceinline__ int wave_excl_scan_min(int v, int /*lane*/, int init)
 // the full DP picks the same best cell and traces the same all-M path.  The
 // fast path then writes only that lane's traceback bits and k_dp skips the
 // DP; otherwise (any condition false, read > 512 nt) it runs the full DP.
-// The candidate is the seeded diagonal (lane HALF): its exact ungapped
-// recurrence decides (A) first, then a per-diagonal non-match count (4 rows
-// per LDS word) bounds every other lane for (B) and stops once all are below.
-// The result is bit-identical to the full DP (tests/test_gpu_parity.py
-// runs both and compares them with the oracle, og_mapper.c:dp_extend).
+// The candidate is the seeded diagonal (band lane XCENTER): its exact
+// ungapped recurrence decides (A) first, then a per-diagonal non-match count
+// (4 rows per LDS word; wave lane L counts band lane L - 16) bounds every
+// other live diagonal for (B) and stops once all are below.  The whole wave
+// works on the one extension.  The result is bit-identical to the full DP
+// (tests/test_gpu_parity.py runs both and compares them with the oracle,
+// og_mapper.c:dp_extend).
 // ---------------------------------------------------------------------------
 template <int LOCAL>
-__device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint8_t *rdc,
-                            uint32_t *bits, int m, int lane, int gmin, int &best, int &bi,
-                            int &bl)
+__device__ bool dp_ungapped(const XView &X, uint32_t *bits, int m, int lane, int gmin, int hcol,
+                            int hb, int &best, int &bi, int &bl)
 {
+    const uint32_t *tab = X.tab;
+    const uint8_t *refw = X.refw, *rdc = X.rdc;
     const int ma = LOCAL ? 2 : 0;
     const int gb_max = ma * m - gmin;   // Gb(m - 1)
-    const int kb = HALF;                // the seeded diagonal: the only candidate lane
-    // ---- exact ungapped recurrence on lane kb: rows 8*lane .. 8*lane+7 ----
+    const int kb = XCENTER;             // the seeded diagonal: the only candidate lane
+    // ---- exact ungapped recurrence on band lane kb: rows 8*lane .. 8*lane+7 ----
     const int r0 = 8 * lane;
     int s[8];
 #pragma unroll
@@ -696,13 +774,16 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
     if (!(S > gb_max)) return false;
     if (LOCAL && S <= 0) return false;
     // (B): non-matches per diagonal, read bytes rdc[i..i+3] against ref bytes
-    // refw[i+lane .. i+lane+3] (codes * 4), 16 rows per step with every LDS
-    // read of the step issued before any is used.  The bound ma*(m - nm)
-    // (local) or -nm (end-to-end) only falls as rows are counted, so the count
-    // stops as soon as every other lane is below S.
+    // refw[i+kl .. i+kl+3] (codes * 4), 16 rows per step with every LDS read
+    // of the step issued before any is used.  The bound ma*(m - nm) (local)
+    // or -nm (end-to-end) only falls as rows are counted, so the count stops
+    // as soon as every other live diagonal is below S.
     {
-        const uint8_t *rp = refw + (lane & ~3);
-        const uint32_t sh = (uint32_t)(lane & 3);
+        const int kl = lane - 16;
+        const bool other = kl >= XCENTER - hb && kl <= XCENTER + hb && kl != kb;
+        const int kr = other ? kl : 0;
+        const uint8_t *rp = refw + (kr & ~3);
+        const uint32_t sh = (uint32_t)(kr & 3);
         int nm = 0;
         bool below = false;
         for (int i = 0; i < m; i += 16) {
@@ -723,13 +804,13 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
             }
             if (i + 16 <= m) {   // (rows past the read would count as non-matches)
                 const int ub = LOCAL ? ma * (m - nm) : -nm;
-                if (__builtin_amdgcn_ballot_w64(lane != kb && ub >= S) == 0) { below = true; break; }
+                if (__builtin_amdgcn_ballot_w64(other && ub >= S) == 0) { below = true; break; }
             }
         }
         if (!below) {
             nm -= (4 - (m & 3)) & 3;   // rows past the read end are coded 4
             const int ub = LOCAL ? ma * (m - nm) : -nm;
-            if (__builtin_amdgcn_ballot_w64(lane != kb && ub >= S) != 0) return false;
+            if (__builtin_amdgcn_ballot_w64(other && ub >= S) != 0) return false;
         }
     }
     // start of the traced segment: last row <= i* where H == 0 (local)
@@ -749,15 +830,415 @@ __device__ bool dp_ungapped(const uint32_t *tab, const uint8_t *refw, const uint
         if (r >= lo && r <= istar && r >= GBAR && H[u] < ma * (r + 1) - gmin) bad = true;
     }
     if (__builtin_amdgcn_ballot_w64(bad) != 0) return false;
-    // traceback bits of lane kb: every row diagonal (nibble 0); the local
-    // stop at istop is the traceback's H == 0
-    if (r0 < m) bits[lane * 64 + kb] = 0u;
+    // traceback bits of the seeded diagonal: every row diagonal (nibble 0);
+    // the local stop at istop is the traceback's H == 0
+    if (r0 < m) bits[lane * 64 + hcol + kb] = 0u;
     best = S;
     bi = istar;
     bl = kb;
     return true;
 }
 
+// Stage one extension's per-row score tables, read codes and reference window
+// into its half's LDS tables; every load of a round is issued before any is
+// used.
+template <int LOCAL>
+__device__ __forceinline__ void stage_ext(const DpArgs &A, const XItem &it, const XView &X, int lane)
+{
+    const int ma = LOCAL ? 2 : 0;
+    const int m = it.m;
+    for (int i0 = 0; i0 < A.rows_pad; i0 += 64 * 4) {
+        uint32_t nmw[4], sqw[4], qv[4];
+        int bb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 64 * u + lane;
+            const int b = i < m ? (it.strand ? m - 1 - i : i) : 0;
+            const int64_t g = it.roff + b;
+            bb[u] = (int)(g & 31);
+            nmw[u] = A.R.nmask[g >> 5];
+            sqw[u] = A.R.seq2[g >> 4] >> (2 * (g & 15));
+            qv[u] = A.R.qual[g];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 64 * u + lane;
+            if (i >= A.rows_pad) break;
+            uint32_t tb = 0x88888u, c = 4, pen = 0;
+            if (i < m) {
+                c = ((nmw[u] >> bb[u]) & 1) ? 4u : (sqw[u] & 3u);
+                if (it.strand && c < 4) c = 3 - c;
+                pen = (uint32_t)mm_pen((int)qv[u]);
+                tb = 0;
+                for (int g = 0; g < 5; ++g) {
+                    const int sc = (c > 3 || g > 3) ? -NPEN : (c == (uint32_t)g ? ma : -(int)pen);
+                    tb |= (uint32_t)(sc + 8) << (4 * g);
+                }
+            }
+            X.tab[i] = tb;
+            X.rdc[i] = (uint8_t)(c | pen << 3);
+            X.rowk[i] = 255;
+        }
+    }
+    const int wref = A.rows_pad + XREFW_PAD;
+    for (int x0 = 0; x0 < wref; x0 += 64 * 5) {
+        uint32_t gv[5];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int j = it.d0 + x0 + 64 * u + lane;
+            gv[u] = (j >= 0 && j < it.reflen) ? A.I.codes[it.gref + j] : 4u;
+        }
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int x = x0 + 64 * u + lane;
+            if (x < wref) X.refw[x] = (uint8_t)(gv[u] * 4);
+        }
+    }
+}
+
+// A row that is a gap row on some lanes and not on others, or past the read
+// of one half: the gap row with E and F switched off where the row has no
+// gap window (its nibble then says "diagonal", as the oracle's does), and no
+// update at all past the read.  Only the first and last GBAR-ish rows of an
+// extension come here.
+template <int LOCAL>
+__device__ __forceinline__ void dp_row_any(uint32_t tbv, int rc, int &Hp, int &Ep, uint32_t &bestKey,
+                                           int ci, const DpConst &K, uint32_t &acc, bool gap,
+                                           bool liverow)
+{
+    DpConst K2 = K;
+    K2.mexI = gap ? K.mexI : HUGE_NEG;
+    K2.cF = gap ? K.cF : HUGE_NEG;
+    int hp = Hp, ep = Ep;
+    uint32_t bk = bestKey, a = acc;
+    dp_row_gap<LOCAL>(tbv, rc, hp, ep, bk, ci, K2, a);
+    Hp = liverow ? hp : Hp;
+    Ep = liverow ? ep : Ep;
+    bestKey = liverow ? bk : bestKey;
+    acc = liverow ? a : acc << 4;
+}
+
+// The banded DP of the wave's two extensions (X0 on lanes 0-31, X1 on lanes
+// 32-63) over rows, 8 rows per group (one u32 of traceback bits per lane);
+// groups inside both gap windows run branch-free.  Returns each half's best
+// cell: max score, then smallest row, then smallest band lane.
+template <int LOCAL>
+__device__ void dp_pair(const DpArgs &A, const XView &X0, const XView &X1, int m0, int m1, int hb0,
+                        int hb1, uint32_t *bits, int lane, int &best0, int &bi0, int &bl0,
+                        int &best1, int &bi1, int &bl1)
+{
+    const int h = lane >> 5, kl = lane & 31;
+    const uint32_t *tab = h ? X1.tab : X0.tab;
+    const uint8_t *refw = (h ? X1.refw : X0.refw) + kl;
+    const int ml = h ? m1 : m0, hb = h ? hb1 : hb0;
+    const bool live = kl >= XCENTER - hb && kl <= XCENTER + hb;
+    DpConst K;
+    K.mexI = (live && kl < XCENTER + hb) ? -(A.exI + A.exD) + (LOCAL ? 0 : 8) : HUGE_NEG;
+    K.dIE = A.exI - A.oeI;
+    K.cF = live ? -(A.oeD - A.exD) : HUGE_NEG;
+    K.floor = live ? BIAS + A.exD * lane : 0;
+    int Hp = K.floor, Ep = 0;   // row -1: H = 0 (shifted, see DpConst); dead lanes near 0
+    uint32_t bestKey = 0;
+    const int mlo = m0 < m1 ? m0 : m1, mhi = m0 < m1 ? m1 : m0;
+    for (int i0 = 0; i0 < mhi; i0 += 8) {
+        uint32_t tbv[8];
+        int rcv[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            tbv[t] = tab[i0 + t];
+            rcv[t] = refw[i0 + t];
+        }
+        uint32_t acc = 0;
+        if (i0 >= GBAR && i0 + 8 <= mlo - GBAR) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K, acc);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int i = i0 + t;
+                dp_row_any<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K, acc,
+                                  i >= GBAR && i < ml - GBAR, i < ml);
+            }
+        }
+        bits[(i0 >> 3) * 64 + lane] = acc;
+    }
+    int bestH, bestI;
+    if (LOCAL) {
+        bestH = (int)(bestKey >> 10) - BIAS - A.exD * lane;
+        bestI = 1023 - (int)(bestKey & 1023u);
+    } else {
+        bestH = Hp - BIAS - A.exD * lane - 8 * ml;   // end-to-end: the last row
+        bestI = ml - 1;
+    }
+    const long long key = (long long)bestH * 1048576ll + (long long)((1023 - bestI) << 6) +
+                          (long long)(63 - lane);
+    long long k0, k1;
+    half_max64(key, lane, k0, k1);
+    best0 = (int)(k0 >> 20);
+    bi0 = 1023 - (int)((k0 >> 6) & 1023);
+    bl0 = (63 - (int)(k0 & 63)) & 31;
+    best1 = (int)(k1 >> 20);
+    bi1 = 1023 - (int)((k1 >> 6) & 1023);
+    bl1 = (63 - (int)(k1 & 63)) & 31;
+}
+
+// Traceback, overhang trimming, statistics and the slot of one extension
+// whose traceback bits sit in columns hcol .. hcol + 31 of the wave's bits.
+template <int LOCAL>
+__device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, const uint32_t *bits,
+                           int hcol, int best, int bi, int bl, int lane, int64_t &ck_base,
+                           int &ck_left)
+{
+    const int ma = LOCAL ? 2 : 0;
+    const int m = it.m, reflen = it.reflen, d0 = it.d0;
+    const int klo = XCENTER - it.hb, khi = XCENTER + it.hb;
+    uint32_t *runs = X.tab;   // the DP is done with the score tables
+    const uint8_t *refw = X.refw, *rdc = X.rdc;
+    uint8_t *rowk = X.rowk;
+    const int minsc = A.len_tab[(MAXLEN + 1) + m];
+
+    // ---- traceback: CIGAR runs, back to front, and the band lane of every
+    // M row (rowk) for the lane-parallel statistics below.  The walk's state
+    // is wave-uniform (SGPRs, scalar branches).  A diagonal run is found in
+    // one step: lane L tests the traceback word of row group (i >> 3) - L on
+    // the current diagonal, and a ballot gives the first group below row i
+    // that holds a non-diagonal cell (one LDS round trip per run instead of
+    // one per 8 rows).  In local mode the walk carries the value of its cell
+    // (hv): down a run the lanes rebuild H row by row (a prefix sum of the
+    // run's scores) and the first H == 0 is the stop the oracle takes
+    // (og_mapper.c dp_extend, src 0).  Gap moves are single steps.  Only
+    // lane 0 writes runs. ----
+    int tb_ok = 0, t_start = 0, t_first = 0, t_nrun = 0;
+    best = __builtin_amdgcn_readfirstlane(best);
+    bi = __builtin_amdgcn_readfirstlane(bi);
+    bl = __builtin_amdgcn_readfirstlane(bl);
+    if (!(LOCAL && best <= 0) && best >= __builtin_amdgcn_readfirstlane(minsc)) {
+        int i = bi, k = bl, state = 0, ok = 1, hv = best;
+        int wr = -1, wk = -1;
+        uint32_t word = 0;
+        int rop = -1, rlen = 0, nrun = 0, first_j = 0;
+        for (;;) {
+            if (state == 0) {
+                // rf: the highest row <= i on diagonal k whose source is
+                // not the diagonal (-1: the run reaches row 0)
+                int rf = -1;
+                uint32_t wf = 0;
+                for (int g0 = i >> 3, top = i & 7; g0 >= 0; g0 -= 64, top = 7) {
+                    const int g = g0 - lane;
+                    uint32_t w = g >= 0 ? bits[g * 64 + hcol + k] : 0u;
+                    if (lane == 0 && top < 7)   // rows above i count as diagonal
+                        w &= ~((1u << (4 * (7 - top))) - 1u);
+                    const uint32_t nd = w & TB_ND_ALL;
+                    const uint64_t hit = __builtin_amdgcn_ballot_w64(nd != 0);
+                    if (hit) {
+                        const int L = (int)__builtin_ctzll(hit);
+                        wf = (uint32_t)__builtin_amdgcn_readlane((int)w, L);
+                        const uint32_t ndf = (uint32_t)__builtin_amdgcn_readlane((int)nd, L);
+                        rf = (g0 - L) * 8 + 7 - (int)(__builtin_ctz(ndf) >> 2);
+                        break;
+                    }
+                }
+                int stop = -1;   // local: the highest row of rf .. i with H == 0
+                if (LOCAL) {
+                    // lane L rebuilds rows r0 - 4L .. r0 - 4L - 3: H(r) = hv minus the
+                    // scores of the diagonal moves out of the rows above r
+                    const int lo = rf > 0 ? rf : 0;
+                    for (int r0 = i; r0 >= lo; r0 -= 256) {
+                        int sc[4], tot = 0;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int r = r0 - 4 * lane - u;
+                            sc[u] = 0;
+                            if (r > rf && r >= 0) {
+                                const int rb = rdc[r], gc = refw[r + k] >> 2, c = rb & 7;
+                                sc[u] = (c > 3 || gc > 3) ? -NPEN : (c == gc ? ma : -(rb >> 3));
+                            }
+                            tot += sc[u];
+                        }
+                        const int ex = wave_excl_scan(tot, lane);
+                        int run = ex, zrow = -1;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int r = r0 - 4 * lane - u;
+                            if (zrow < 0 && r >= lo && hv - run == 0) zrow = r;
+                            run += sc[u];
+                        }
+                        const uint64_t z = __builtin_amdgcn_ballot_w64(zrow >= 0);
+                        if (z) {
+                            stop = __builtin_amdgcn_readlane(zrow, (int)__builtin_ctzll(z));
+                            break;
+                        }
+                        hv -= __builtin_amdgcn_readlane(run, 63);
+                    }
+                }
+                const int low = stop >= 0 ? stop : rf;
+                if (i > low) {   // rows low+1 .. i: one M run
+                    const int len = i - low;
+                    if (rop == MH_OP_M) rlen += len;
+                    else {
+                        if (rlen) {
+                            if (nrun >= RUNS_CAP - 1) { ok = 0; break; }
+                            if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                            ++nrun;
+                        }
+                        rop = MH_OP_M;
+                        rlen = len;
+                    }
+                    for (int r = low + 1 + lane; r <= i; r += 64) rowk[r] = (uint8_t)k;
+                    first_j = low + 1 + d0 + k;
+                }
+                i = low;
+                if (stop >= 0 || i < 0) break;   // a local stop starts the alignment at row i + 1
+                const uint32_t nib = (wf >> (4 * (7 - (i & 7)))) & 15u;
+                state = (nib & TB_NE) ? 2 : 1;
+                continue;
+            }
+            // a gap step: the extend bit of cell (i, k) sits on band lane k + 1
+            // (E, eb') or k - 1 (F, fb')
+            const int g = i >> 3, kk = state == 1 ? k + 1 : k - 1;
+            if (kk < klo || kk > khi) { ok = 0; break; }
+            if (g != wr || kk != wk) {
+                word = __builtin_amdgcn_readfirstlane(bits[g * 64 + hcol + kk]);
+                wr = g; wk = kk;
+            }
+            const uint32_t nib = (word >> (4 * (7 - (i & 7)))) & 15u;
+            const int op = state == 1 ? MH_OP_I : MH_OP_D;
+            if (op == rop) ++rlen;
+            else {
+                if (rlen) {
+                    if (nrun >= RUNS_CAP - 1) { ok = 0; break; }
+                    if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+                    ++nrun;
+                }
+                rop = op;
+                rlen = 1;
+            }
+            if (op == MH_OP_I) {
+                const bool ext = (nib & TB_EB) != 0;
+                hv += ext ? A.exI : A.oeI;
+                state = ext ? 1 : 0;
+                --i; ++k;
+                if (i < 0 || k > khi) { ok = 0; break; }
+            } else {
+                const bool ext = (nib & TB_FB) != 0;
+                hv += ext ? A.exD : A.oeD;
+                state = ext ? 2 : 0;
+                --k;
+                if (k < klo) { ok = 0; break; }
+            }
+        }
+        if (rlen) {
+            if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
+            ++nrun;
+        }
+        tb_ok = ok;
+        t_start = i + 1;
+        t_first = first_j;
+        t_nrun = nrun;
+    }
+    wave_sync();
+    Slot out{};
+    out.valid = 0;
+    out.strand = it.strand;
+    out.ref = it.ref;
+    if (tb_ok) {
+        // trim overhanging columns into soft clips, on the runs (lane 0)
+        int lo = t_nrun - 1, hi = 0;   // forward order is runs[nrun-1] .. runs[0]
+        uint32_t front = 0, back = 0;
+        int clipL = t_start, clipR = m - 1 - bi, jL = t_first, jR = bi + d0 + bl;
+        if (lane == 0) {
+            front = lo >= 0 ? runs[lo] : 0;
+            back = runs[0];
+            while (lo >= hi) {
+                const int op = front & 15, len = (int)(front >> 4);
+                if (op == MH_OP_M && jL >= 0) break;
+                if (op == MH_OP_M) {
+                    const int t = -jL < len ? -jL : len;
+                    clipL += t; jL += t;
+                    if (t < len) { front = ((uint32_t)(len - t) << 4) | MH_OP_M; continue; }
+                } else if (op == MH_OP_I) {
+                    clipL += len;
+                } else {
+                    jL += len;
+                }
+                if (--lo >= hi) front = runs[lo];
+            }
+            if (lo == hi) back = front;   // one run left: keep the front's trim
+            while (hi <= lo) {
+                const int op = back & 15, len = (int)(back >> 4);
+                if (op == MH_OP_M && jR < reflen) break;
+                if (op == MH_OP_M) {
+                    const int t = jR - reflen + 1 < len ? jR - reflen + 1 : len;
+                    clipR += t; jR -= t;
+                    if (t < len) { back = ((uint32_t)(len - t) << 4) | MH_OP_M; continue; }
+                } else if (op == MH_OP_I) {
+                    clipR += len;
+                } else {
+                    jR -= len;
+                }
+                if (++hi <= lo) back = hi == lo ? front : runs[hi];
+            }
+        }
+        clipL = __builtin_amdgcn_readfirstlane(clipL);
+        clipR = __builtin_amdgcn_readfirstlane(clipR);
+        // one pass over the M rows: ambiguous positions over the untrimmed
+        // alignment (--n-ceil) and mismatches over the trimmed one, summed
+        // together (nn << 16 | xm)
+        int cnt = 0;
+        for (int i = t_start + lane; i <= bi; i += 64) {
+            const int k = rowk[i];
+            if (k == 255) continue;
+            const int g = refw[i + k] >> 2, rb = rdc[i] & 7;
+            if (rb > 3 || g > 3) cnt += 1 << 16;
+            if ((rb > 3 || g > 3 || rb != g) && i >= clipL && i <= m - 1 - clipR) ++cnt;
+        }
+        cnt = wave_sum(cnt);
+        if ((cnt >> 16) > A.len_tab[2 * (MAXLEN + 1) + m]) tb_ok = 0;
+        if (tb_ok && lane == 0 && lo >= hi) {
+            const int nc = (clipL > 0) + (clipR > 0) + (lo - hi + 1);
+            if (nc <= MH_MAXOPS - 1) {
+                if (nc > ck_left) {   // next wave-private chunk of the pool
+                    ck_base = atomicAdd(&A.pool_ctr[0], POOL_CHUNK);
+                    ck_left = POOL_CHUNK;
+                }
+                const int64_t base = ck_base;
+                ck_base += nc;
+                ck_left -= nc;
+                if (base + nc > A.pool_cap) {
+                    atomicExch(&A.pool_ctr[1], 1);
+                } else {
+                    uint32_t *cg = A.pool + base;
+                    int n = 0, xo = 0, xg = 0;
+                    if (clipL) cg[n++] = ((uint32_t)clipL << 4) | MH_OP_S;
+                    for (int z = lo; z >= hi; --z) {
+                        const uint32_t rr = z == hi ? back : (z == lo ? front : runs[z]);
+                        cg[n++] = rr;
+                        if ((rr & 15) != MH_OP_M) { ++xo; xg += (int)(rr >> 4); }
+                    }
+                    if (clipR) cg[n++] = ((uint32_t)clipR << 4) | MH_OP_S;
+                    out.valid = 1;
+                    out.pos = jL;
+                    out.end = jR + 1;
+                    out.score = best;
+                    out.xo = xo; out.xg = xg;
+                    out.n_cigar = n;
+                    out.cig_off = (int32_t)base;
+                    out.xm = cnt & 0xffff;
+                    out.nm = out.xm + xg;
+                }
+            }
+        }
+    }
+    if (lane == 0) A.slot[it.sid] = out;
+    wave_sync();
+}
+
+// k_dp: a wave walks its share of the work list.  Each item is staged into
+// the free half's tables and tried on the exact ungapped fast path (the
+// whole wave); an item that needs the DP waits in half 0 until a second one
+// fills half 1, then both run through the rows together.  A last waiting
+// item runs with half 1 repeating it.
 template <int LOCAL>
 __global__ __launch_bounds__(256) void k_dp(DpArgs A)
 {
@@ -767,20 +1248,10 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     const int wpb = blockDim.x >> 6;
     unsigned char *wbase = smem + (size_t)wv * A.wave_lds;
     uint32_t *bits = (uint32_t *)wbase;                       // rows_pad/8 * 64: 4 bits/cell
-    uint32_t *tab = bits + (A.rows_pad >> 3) * 64;            // rows_pad: score nibbles per row
-    uint32_t *runs = tab;                                     // RUNS_CAP: CIGAR runs (reversed),
-                                                              // written after the DP is done with tab
-    uint8_t *refw = (uint8_t *)(runs + (A.rows_pad > RUNS_CAP ? A.rows_pad : RUNS_CAP));
-                                                              // rows_pad + 64: ref code * 4
-    uint8_t *rdc = refw + A.rows_pad + 64;                    // rows_pad: read code | mismatch penalty << 3
-    uint8_t *rowk = rdc + A.rows_pad;                         // rows_pad: lane of the M cell, 255 none
-    const int ma = LOCAL ? 2 : 0;
+    unsigned char *xbase = wbase + (size_t)32 * A.rows_pad;
+    const XView X0 = xview(xbase, A.rows_pad, 0), X1 = xview(xbase, A.rows_pad, 1);
     const int n_work = A.counters[0];
-    DpConst K;
-    K.mexI = in_vgpr(-(A.exI + A.exD) + (LOCAL ? 0 : 8));
-    K.dIE = A.exI - A.oeI;
-    K.cF = in_vgpr(-(A.oeD - A.exD));
-    K.floor = BIAS + A.exD * lane;
+    const int gmin = A.oeI < A.oeD ? A.oeI : A.oeD;
 
     int64_t ck_base = 0;   // lane 0: this wave's current CIGAR pool chunk
     int ck_left = 0;
@@ -802,68 +1273,27 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         reflen_n = A.I.ref_len[cd_n.ref];
         gref_n = A.I.ref_off[cd_n.ref];
     }
+    bool pend = false;   // half 0 holds an item waiting for the DP
+    XItem P{};
     for (; w < n_work; w += wstride) {
-        const int sid = sid_n;
-        const Cand cd = cd_n;
-        const int m = m_n;
-        const int64_t roff = roff_n;
-        const int reflen = reflen_n;
-        const int64_t gref = gref_n;
-        const int d0 = cd.center - HALF;
-        const int strand = cd.strand;
+        XItem it;
+        it.sid = sid_n;
+        it.m = m_n;
+        it.roff = roff_n;
+        it.reflen = reflen_n;
+        it.gref = gref_n;
+        it.d0 = cd_n.center - XCENTER;
+        it.strand = cd_n.strand;
+        it.ref = cd_n.ref;
+        it.hb = A.len_tab[3 * (MAXLEN + 1) + m_n];
         const int wn = w + wstride;
         const bool more = wn < n_work;
         int sid_nn = 0;
         if (more) sid_nn = A.work[wn];   // lands with the staging loads below
 
-        // ---- stage per-row score tables, read codes and the ref window:
-        // every load of a round is issued before any is used ----
-        for (int i0 = 0; i0 < A.rows_pad; i0 += 64 * 4) {
-            uint32_t nmw[4], sqw[4], qv[4];
-            int bb[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = i0 + 64 * u + lane;
-                const int b = i < m ? (strand ? m - 1 - i : i) : 0;
-                const int64_t g = roff + b;
-                bb[u] = (int)(g & 31);
-                nmw[u] = A.R.nmask[g >> 5];
-                sqw[u] = A.R.seq2[g >> 4] >> (2 * (g & 15));
-                qv[u] = A.R.qual[g];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = i0 + 64 * u + lane;
-                if (i >= A.rows_pad) break;
-                uint32_t tb = 0x88888u, c = 4, pen = 0;
-                if (i < m) {
-                    c = ((nmw[u] >> bb[u]) & 1) ? 4u : (sqw[u] & 3u);
-                    if (strand && c < 4) c = 3 - c;
-                    pen = (uint32_t)mm_pen((int)qv[u]);
-                    tb = 0;
-                    for (int g = 0; g < 5; ++g) {
-                        const int sc = (c > 3 || g > 3) ? -NPEN : (c == (uint32_t)g ? ma : -(int)pen);
-                        tb |= (uint32_t)(sc + 8) << (4 * g);
-                    }
-                }
-                tab[i] = tb;
-                rdc[i] = (uint8_t)(c | pen << 3);
-                rowk[i] = 255;
-            }
-        }
-        for (int x0 = 0; x0 < A.rows_pad + 64; x0 += 64 * 5) {
-            uint32_t gv[5];
-#pragma unroll
-            for (int u = 0; u < 5; ++u) {
-                const int j = d0 + x0 + 64 * u + lane;
-                gv[u] = (j >= 0 && j < reflen) ? A.I.codes[gref + j] : 4u;
-            }
-#pragma unroll
-            for (int u = 0; u < 5; ++u) {
-                const int x = x0 + 64 * u + lane;
-                if (x < A.rows_pad + 64) refw[x] = (uint8_t)(gv[u] * 4);
-            }
-        }
+        const int h = pend ? 1 : 0;
+        const XView X = h ? X1 : X0;
+        stage_ext<LOCAL>(A, it, X, lane);
         wave_sync();
         if (more) {   // next item's candidate and read descriptors: land during the DP
             sid_n = sid_nn;
@@ -871,302 +1301,34 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             m_n = A.R.len[sid_nn / MAXCAND];
             roff_n = A.R.off[sid_nn / MAXCAND];
         }
-
-        int best, bi, bl;
-        const bool fast = m > 2 * GBAR + 8 && m <= 512 &&
-                          dp_ungapped<LOCAL>(tab, refw, rdc, bits, m, lane,
-                                             A.oeI < A.oeD ? A.oeI : A.oeD, best, bi, bl);
+        int best = 0, bi = 0, bl = 0;
+        const bool fast = it.m > 2 * GBAR + 8 && it.m <= 512 &&
+                          dp_ungapped<LOCAL>(X, bits, it.m, lane, gmin, 32 * h, it.hb, best, bi, bl);
         n_fast += fast;
-        if (!fast) {
-            // ---- DP over rows, 8 rows per group (one u32 of traceback bits per
-            // lane); groups wholly inside the gap window run branch-free; the next
-            // group's operands come from LDS ----
-            int Hp = BIAS + A.exD * lane, Ep = 0;   // row -1: H = 0 (shifted, see DpConst)
-            uint32_t bestKey = 0;
-            for (int i0 = 0; i0 < m; i0 += 8) {
-                uint32_t tbv[8];
-                int rcv[8];
-#pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    tbv[t] = tab[i0 + t];
-                    rcv[t] = refw[i0 + t + lane];
-                }
-                uint32_t acc = 0;
-                if (i0 >= GBAR && i0 + 8 <= m - GBAR) {
-#pragma unroll
-                    for (int t = 0; t < 8; ++t)
-                        dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K, acc);
-                } else {
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        const int i = i0 + t;
-                        if (i >= m) acc <<= 4;   // past the read: an empty nibble
-                        else if (i >= GBAR && i < m - GBAR)
-                            dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K, acc);
-                        else
-                            dp_row_nogap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K.floor, acc);
-                    }
-                }
-                bits[(i0 >> 3) * 64 + lane] = acc;
-            }
-            int bestH, bestI;
-            if (LOCAL) {
-                bestH = (int)(bestKey >> 10) - BIAS - A.exD * lane;
-                bestI = 1023 - (int)(bestKey & 1023u);
-            } else {
-                bestH = Hp - BIAS - A.exD * lane - 8 * m;   // end-to-end: the last row
-                bestI = m - 1;
-            }
-            // best cell: max score, then smallest row, then smallest lane
-            const long long key = (long long)bestH * 1048576ll + (long long)((1023 - bestI) << 6) +
-                                  (long long)(63 - lane);
-            const long long bk = wave_max64(key);
-            best = (int)(bk >> 20);
-            bi = 1023 - (int)((bk >> 6) & 1023);
-            bl = 63 - (int)(bk & 63);
-        }
-        const int minsc = A.len_tab[(MAXLEN + 1) + m];
-        if (more) {   // next item's reference window: lands during the traceback
+        if (more) {   // next item's reference window: lands during the DP / traceback
             reflen_n = A.I.ref_len[cd_n.ref];
             gref_n = A.I.ref_off[cd_n.ref];
         }
-        wave_sync();
-
-        // ---- traceback: CIGAR runs, back to front, and the lane of every M
-        // row (rowk) for the lane-parallel statistics below.  The walk's
-        // state is wave-uniform (SGPRs, scalar branches).  A diagonal run is
-        // found in one step: lane L tests the traceback word of row group
-        // (i >> 3) - L on the current diagonal, and a ballot gives the first
-        // group below row i that holds a non-diagonal cell (one LDS round
-        // trip per run instead of one per 8 rows).  In local mode the walk
-        // carries the value of its cell (hv): down a run the lanes rebuild H
-        // row by row (a prefix sum of the run's scores) and the first H == 0
-        // is the stop the oracle takes (og_mapper.c:319, src 0).  Gap moves
-        // are single steps.  Only lane 0 writes runs. ----
-        int tb_ok = 0, t_start = 0, t_first = 0, t_nrun = 0;
-        best = __builtin_amdgcn_readfirstlane(best);
-        bi = __builtin_amdgcn_readfirstlane(bi);
-        bl = __builtin_amdgcn_readfirstlane(bl);
-        if (!(LOCAL && best <= 0) && best >= __builtin_amdgcn_readfirstlane(minsc)) {
-            const int d0u = __builtin_amdgcn_readfirstlane(d0);
-            int i = bi, k = bl, state = 0, ok = 1, hv = best;
-            int wr = -1, wk = -1;
-            uint32_t word = 0;
-            int rop = -1, rlen = 0, nrun = 0, first_j = 0;
-            for (;;) {
-                if (state == 0) {
-                    // rf: the highest row <= i on diagonal k whose source is
-                    // not the diagonal (-1: the run reaches row 0)
-                    int rf = -1;
-                    uint32_t wf = 0;
-                    for (int g0 = i >> 3, top = i & 7; g0 >= 0; g0 -= 64, top = 7) {
-                        const int g = g0 - lane;
-                        uint32_t w = g >= 0 ? bits[g * 64 + k] : 0u;
-                        if (lane == 0 && top < 7)   // rows above i count as diagonal
-                            w &= ~((1u << (4 * (7 - top))) - 1u);
-                        const uint32_t nd = w & TB_ND_ALL;
-                        const uint64_t hit = __builtin_amdgcn_ballot_w64(nd != 0);
-                        if (hit) {
-                            const int L = (int)__builtin_ctzll(hit);
-                            wf = (uint32_t)__builtin_amdgcn_readlane((int)w, L);
-                            const uint32_t ndf = (uint32_t)__builtin_amdgcn_readlane((int)nd, L);
-                            rf = (g0 - L) * 8 + 7 - (int)(__builtin_ctz(ndf) >> 2);
-                            break;
-                        }
-                    }
-                    int stop = -1;   // local: the highest row of rf .. i with H == 0
-                    if (LOCAL) {
-                        // lane L rebuilds rows r0 - 4L .. r0 - 4L - 3: H(r) = hv minus the
-                        // scores of the diagonal moves out of the rows above r
-                        const int lo = rf > 0 ? rf : 0;
-                        for (int r0 = i; r0 >= lo; r0 -= 256) {
-                            int sc[4], tot = 0;
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                const int r = r0 - 4 * lane - u;
-                                sc[u] = 0;
-                                if (r > rf && r >= 0) {
-                                    const int rb = rdc[r], gc = refw[r + k] >> 2, c = rb & 7;
-                                    sc[u] = (c > 3 || gc > 3) ? -NPEN : (c == gc ? ma : -(rb >> 3));
-                                }
-                                tot += sc[u];
-                            }
-                            const int ex = wave_excl_scan(tot, lane);
-                            int run = ex, zrow = -1;
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                const int r = r0 - 4 * lane - u;
-                                if (zrow < 0 && r >= lo && hv - run == 0) zrow = r;
-                                run += sc[u];
-                            }
-                            const uint64_t z = __builtin_amdgcn_ballot_w64(zrow >= 0);
-                            if (z) {
-                                stop = __builtin_amdgcn_readlane(zrow, (int)__builtin_ctzll(z));
-                                break;
-                            }
-                            hv -= __builtin_amdgcn_readlane(run, 63);
-                        }
-                    }
-                    const int low = stop >= 0 ? stop : rf;
-                    if (i > low) {   // rows low+1 .. i: one M run
-                        const int len = i - low;
-                        if (rop == MH_OP_M) rlen += len;
-                        else {
-                            if (rlen) {
-                                if (nrun >= RUNS_CAP - 1) { ok = 0; break; }
-                                if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
-                                ++nrun;
-                            }
-                            rop = MH_OP_M;
-                            rlen = len;
-                        }
-                        for (int r = low + 1 + lane; r <= i; r += 64) rowk[r] = (uint8_t)k;
-                        first_j = low + 1 + d0u + k;
-                    }
-                    i = low;
-                    if (stop >= 0 || i < 0) break;   // a local stop starts the alignment at row i + 1
-                    const uint32_t nib = (wf >> (4 * (7 - (i & 7)))) & 15u;
-                    state = (nib & TB_NE) ? 2 : 1;
-                    continue;
-                }
-                // a gap step: the extend bit of cell (i, k) sits on lane k + 1
-                // (E, eb') or lane k - 1 (F, fb')
-                const int g = i >> 3, kk = state == 1 ? k + 1 : k - 1;
-                if (kk < 0 || kk >= BAND) { ok = 0; break; }
-                if (g != wr || kk != wk) {
-                    word = __builtin_amdgcn_readfirstlane(bits[g * 64 + kk]);
-                    wr = g; wk = kk;
-                }
-                const uint32_t nib = (word >> (4 * (7 - (i & 7)))) & 15u;
-                const int op = state == 1 ? MH_OP_I : MH_OP_D;
-                if (op == rop) ++rlen;
-                else {
-                    if (rlen) {
-                        if (nrun >= RUNS_CAP - 1) { ok = 0; break; }
-                        if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
-                        ++nrun;
-                    }
-                    rop = op;
-                    rlen = 1;
-                }
-                if (op == MH_OP_I) {
-                    const bool ext = (nib & TB_EB) != 0;
-                    hv += ext ? A.exI : A.oeI;
-                    state = ext ? 1 : 0;
-                    --i; ++k;
-                    if (i < 0 || k >= BAND) { ok = 0; break; }
-                } else {
-                    const bool ext = (nib & TB_FB) != 0;
-                    hv += ext ? A.exD : A.oeD;
-                    state = ext ? 2 : 0;
-                    --k;
-                    if (k < 0) { ok = 0; break; }
-                }
-            }
-            if (rlen) {
-                if (lane == 0) runs[nrun] = ((uint32_t)rlen << 4) | (uint32_t)rop;
-                ++nrun;
-            }
-            tb_ok = ok;
-            t_start = i + 1;
-            t_first = first_j;
-            t_nrun = nrun;
+        if (fast) {
+            wave_sync();
+            finish_ext<LOCAL>(A, it, X, bits, 32 * h, best, bi, bl, lane, ck_base, ck_left);
+        } else if (!pend) {
+            P = it;
+            pend = true;
+        } else {
+            int b0, i0, l0, b1, i1, l1;
+            dp_pair<LOCAL>(A, X0, X1, P.m, it.m, P.hb, it.hb, bits, lane, b0, i0, l0, b1, i1, l1);
+            wave_sync();
+            finish_ext<LOCAL>(A, P, X0, bits, 0, b0, i0, l0, lane, ck_base, ck_left);
+            finish_ext<LOCAL>(A, it, X1, bits, 32, b1, i1, l1, lane, ck_base, ck_left);
+            pend = false;
         }
+    }
+    if (pend) {
+        int b0, i0, l0, b1, i1, l1;
+        dp_pair<LOCAL>(A, X0, X0, P.m, P.m, P.hb, P.hb, bits, lane, b0, i0, l0, b1, i1, l1);
         wave_sync();
-        Slot out{};
-        out.valid = 0;
-        out.strand = strand;
-        out.ref = cd.ref;
-        if (tb_ok) {
-            // trim overhanging columns into soft clips, on the runs (lane 0)
-            int lo = t_nrun - 1, hi = 0;   // forward order is runs[nrun-1] .. runs[0]
-            uint32_t front = 0, back = 0;
-            int clipL = t_start, clipR = m - 1 - bi, jL = t_first, jR = bi + d0 + bl;
-            if (lane == 0) {
-                front = lo >= 0 ? runs[lo] : 0;
-                back = runs[0];
-                while (lo >= hi) {
-                    const int op = front & 15, len = (int)(front >> 4);
-                    if (op == MH_OP_M && jL >= 0) break;
-                    if (op == MH_OP_M) {
-                        const int t = -jL < len ? -jL : len;
-                        clipL += t; jL += t;
-                        if (t < len) { front = ((uint32_t)(len - t) << 4) | MH_OP_M; continue; }
-                    } else if (op == MH_OP_I) {
-                        clipL += len;
-                    } else {
-                        jL += len;
-                    }
-                    if (--lo >= hi) front = runs[lo];
-                }
-                if (lo == hi) back = front;   // one run left: keep the front's trim
-                while (hi <= lo) {
-                    const int op = back & 15, len = (int)(back >> 4);
-                    if (op == MH_OP_M && jR < reflen) break;
-                    if (op == MH_OP_M) {
-                        const int t = jR - reflen + 1 < len ? jR - reflen + 1 : len;
-                        clipR += t; jR -= t;
-                        if (t < len) { back = ((uint32_t)(len - t) << 4) | MH_OP_M; continue; }
-                    } else if (op == MH_OP_I) {
-                        clipR += len;
-                    } else {
-                        jR -= len;
-                    }
-                    if (++hi <= lo) back = hi == lo ? front : runs[hi];
-                }
-            }
-            clipL = __builtin_amdgcn_readfirstlane(clipL);
-            clipR = __builtin_amdgcn_readfirstlane(clipR);
-            // one pass over the M rows: ambiguous positions over the untrimmed
-            // alignment (--n-ceil) and mismatches over the trimmed one, summed
-            // together (nn << 16 | xm)
-            int cnt = 0;
-            for (int i = t_start + lane; i <= bi; i += 64) {
-                const int k = rowk[i];
-                if (k == 255) continue;
-                const int g = refw[i + k] >> 2, rb = rdc[i] & 7;
-                if (rb > 3 || g > 3) cnt += 1 << 16;
-                if ((rb > 3 || g > 3 || rb != g) && i >= clipL && i <= m - 1 - clipR) ++cnt;
-            }
-            cnt = wave_sum(cnt);
-            if ((cnt >> 16) > A.len_tab[2 * (MAXLEN + 1) + m]) tb_ok = 0;
-            if (tb_ok && lane == 0 && lo >= hi) {
-                const int nc = (clipL > 0) + (clipR > 0) + (lo - hi + 1);
-                if (nc <= MH_MAXOPS - 1) {
-                    if (nc > ck_left) {   // next wave-private chunk of the pool
-                        ck_base = atomicAdd(&A.pool_ctr[0], POOL_CHUNK);
-                        ck_left = POOL_CHUNK;
-                    }
-                    const int64_t base = ck_base;
-                    ck_base += nc;
-                    ck_left -= nc;
-                    if (base + nc > A.pool_cap) {
-                        atomicExch(&A.pool_ctr[1], 1);
-                    } else {
-                        uint32_t *cg = A.pool + base;
-                        int n = 0, xo = 0, xg = 0;
-                        if (clipL) cg[n++] = ((uint32_t)clipL << 4) | MH_OP_S;
-                        for (int z = lo; z >= hi; --z) {
-                            const uint32_t rr = z == hi ? back : (z == lo ? front : runs[z]);
-                            cg[n++] = rr;
-                            if ((rr & 15) != MH_OP_M) { ++xo; xg += (int)(rr >> 4); }
-                        }
-                        if (clipR) cg[n++] = ((uint32_t)clipR << 4) | MH_OP_S;
-                        out.valid = 1;
-                        out.pos = jL;
-                        out.end = jR + 1;
-                        out.score = best;
-                        out.xo = xo; out.xg = xg;
-                        out.n_cigar = n;
-                        out.cig_off = (int32_t)base;
-                        out.xm = cnt & 0xffff;
-                        out.nm = out.xm + xg;
-                    }
-                }
-            }
-        }
-        if (lane == 0) A.slot[sid] = out;
-        wave_sync();
+        finish_ext<LOCAL>(A, P, X0, bits, 0, b0, i0, l0, lane, ck_base, ck_left);
     }
     if (lane == 0 && n_fast) atomicAdd(&A.pool_ctr[2], n_fast);
 }
@@ -1681,7 +1843,7 @@ int run_map(Ctx &c, const mh_params &par)
         set_error("mh_map: index seed length %d does not match mode (%d)", c.index.seedlen, SL);
         return -3;
     }
-    if (c.len_tab == nullptr || c.len_tab_mode != par.mode) {
+    if (c.len_tab == nullptr || c.len_tab_key != len_tab_key(par)) {
         set_error("mh_map: length tables not prepared");
         return -3;
     }
@@ -1705,9 +1867,8 @@ int run_map(Ctx &c, const mh_params &par)
         MH_HIP(hipGetLastError());
 
         const int rows_pad = ((c.reads.max_len + 7) / 8) * 8;
-        // bits 32/row, tab|runs 4 * max(rows, RUNS_CAP), refw rows + 64, rdc, rowk
-        const int wave_lds =
-            ((rows_pad * 35 + 4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP) + 64) + 15) & ~15;
+        // traceback bits 32 B per row, then the tables of the wave's two extensions
+        const int wave_lds = 32 * rows_pad + 2 * xview_bytes(rows_pad);
         // one wave per workgroup: the CU then packs floor(160 KiB / wave_lds)
         // waves (15 at 251-nt reads) with no workgroup rounding loss
         int wpb = DP_WAVES_PER_BLOCK;

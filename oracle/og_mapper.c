@@ -21,7 +21,8 @@
  *   20 (local) nt every 1+1.15*sqrt(L) / 1+0.75*sqrt(L) nt on both strands.
  * Deterministic choices where bowtie2 randomises (documented in DESIGN.md):
  *   hits are clustered by diagonal, the 4 best-supported clusters are
- *   extended by banded DP (64 diagonals), ties break towards the
+ *   extended by banded DP (the seeded diagonal +- og_band_half: bowtie2's
+ *   gap limit for its DP rectangle, maxhalf 15), ties break towards the
  *   lower-ranked candidate / smaller coordinates, traceback prefers
  *   diagonal > insertion > deletion and gap-open over gap-extend.
  */
@@ -60,6 +61,33 @@ int og_min_score(int mode, int len)
 }
 
 int og_n_ceil(int len) { return (int)(0.0 + 0.15 * (double)len); }
+
+/* Gaps of one kind an alignment can hold and still reach minsc from the
+ * perfect score: the first costs open + ext, each further one ext (bowtie2
+ * Scoring::maxReadGaps / maxRefGaps). */
+static int max_gaps(int perfect, int minsc, int oe, int ex)
+{
+    int sc = perfect, num = 0;
+    while (sc >= minsc) {
+        sc -= num == 0 ? oe : ex;
+        ++num;
+    }
+    return num - 1;
+}
+
+/* Half-width of the DP band around the seeded diagonal: the larger of the
+ * two gap limits, capped at bowtie2's maxhalf (DynProgFramer::
+ * frameSeedExtensionRect: maxgap = min(max(read gaps, ref gaps), maxhalf)). */
+int og_band_half(const og_params *par, int len)
+{
+    const int perfect = par->mode == OG_LOCAL ? 2 * len : 0;
+    const int minsc = og_min_score(par->mode, len);
+    const int gd = max_gaps(perfect, minsc, par->rdg_open + par->rdg_ext, par->rdg_ext);
+    const int gi = max_gaps(perfect, minsc, par->rfg_open + par->rfg_ext, par->rfg_ext);
+    int h = gd > gi ? gd : gi;
+    if (h > OG_MAXHALF) h = OG_MAXHALF;
+    return h < 0 ? 0 : h;
+}
 
 static inline int mm_pen(int qchar)
 {
@@ -278,7 +306,8 @@ static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *r
     const int oeD = par->rdg_open + par->rdg_ext, exD = par->rdg_ext;
     const uint8_t *ref = ix->codes[cd->ref];
     const int reflen = ix->lens[cd->ref];
-    const int d0 = cd->center - OG_HALF;
+    const int half = og_band_half(par, m), W = 2 * half + 1;   /* diagonals d0 .. d0 + W - 1 */
+    const int d0 = cd->center - half;
     int Hp[OG_BAND], Ep[OG_BAND], H[OG_BAND], E[OG_BAND], F[OG_BAND], Hd[OG_BAND], H1[OG_BAND];
     uint8_t eb[OG_BAND];
     for (int k = 0; k < OG_BAND; ++k) { Hp[k] = 0; Ep[k] = OG_NEG; }
@@ -289,12 +318,12 @@ static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *r
     for (int i = 0; i < m; ++i) {
         const int gap_ok = i >= GBAR && i < m - GBAR;
         const int rb = rd[i], pen = mm_pen(qv[i]);
-        for (int k = 0; k < OG_BAND; ++k) {
+        for (int k = 0; k < W; ++k) {
             const int j = i + d0 + k;
             const int g = (j >= 0 && j < reflen) ? ref[j] : 4;
             const int s = (rb > 3 || g > 3) ? -NPEN : (rb == g ? ma : -pen);
             Hd[k] = Hp[k] + s;
-            if (gap_ok && k + 1 < OG_BAND) {
+            if (gap_ok && k + 1 < W) {
                 const int ext = Ep[k + 1] - exI, opn = Hp[k + 1] - oeI;
                 E[k] = imax(ext, opn);
                 eb[k] = ext > opn;
@@ -305,7 +334,7 @@ static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *r
             H1[k] = imax(Hd[k], E[k]);
             if (local) H1[k] = imax(H1[k], 0);
         }
-        for (int k = 0; k < OG_BAND; ++k) {
+        for (int k = 0; k < W; ++k) {
             int fb = 0;
             if (gap_ok && k > 0) {
                 const int ext = F[k - 1] - exD, opn = H[k - 1] - oeD;
@@ -351,7 +380,7 @@ static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *r
             ops[nops++] = OG_OP_I;
             state = (b >> 2) & 1 ? 1 : 0;
             --i; ++k;
-            if (i < 0 || k >= OG_BAND) return; /* unreachable by construction */
+            if (i < 0 || k >= W) return; /* unreachable by construction */
         } else {
             ops[nops++] = OG_OP_D;
             state = (b >> 3) & 1 ? 2 : 0;

@@ -6,8 +6,8 @@
 #define OG_MAPPER_H
 #include <stdint.h>
 
-#define OG_BAND 64            /* diagonals per DP band (one wave64 lane each) */
-#define OG_HALF 32            /* band = [center-32, center+31] */
+#define OG_BAND 64            /* storage width of a DP row (>= 2 * OG_MAXHALF + 1) */
+#define OG_MAXHALF 15         /* bowtie2's maxhalf: band = center +- min(15, max gaps) */
 #define OG_MAXCAND 4          /* extension candidates per mate */
 #define OG_MAXHITS_SEED 64    /* seeds with more exact hits are skipped */
 #define OG_MAXHITS_MATE 512   /* hit budget per mate (seed order) */
@@ -73,4 +73,5 @@ int og_map_diag(const og_index *ix, const og_params *par, int64_t n_reads, int p
 int og_seed_interval(int mode, int len);
 int og_min_score(int mode, int len);
 int og_n_ceil(int len);
+int og_band_half(const og_params *par, int len);
 #endif

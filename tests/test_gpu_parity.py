@@ -327,3 +327,31 @@ def test_map_overhang_trimming(ctx, mode):
     _assert_same(gpu, ref, seqs)
     clipped = sum(1 for a in ref if a['n_cigar'] and (a['cigar'][0] & 15) == 4)
     assert clipped > 20
+
+
+@pytest.mark.parametrize('mode,rdg,rfg', [(oracle.E2E, (10, 3), (10, 3)), (oracle.LOCAL, (10, 3), (10, 3)),
+                                          (oracle.E2E, (4, 3), (14, 2)), (oracle.LOCAL, (20, 5), (6, 1))])
+def test_map_ragged_pairs_band_widths(ctx, mode, rdg, rfg):
+    """Pairs whose mates have different lengths (30-300 nt, so the two
+    extensions sharing a k_dp wave end on different rows and short reads get
+    a band narrower than bowtie2's maxhalf of 15), 2 % indels, and gap
+    penalties other than MiCall's (the band half-width follows them)."""
+    rng = np.random.default_rng(31)
+    names, seqs, quals = _reads(700, 23, read_len=300, sub_rate=0.03, indel_rate=0.02)
+    seqs, quals = list(seqs), list(quals)
+    for i in range(len(seqs)):
+        L = int(rng.integers(30, 301))
+        if rng.random() < 0.5:
+            seqs[i], quals[i] = seqs[i][:L], quals[i][:L]
+        else:
+            seqs[i], quals[i] = seqs[i][-L:], quals[i][-L:]
+    ix = oracle.Index([POL], oracle.seed_len(mode))
+    out = oracle.map_reads(ix, oracle.params(mode, rdg=rdg, rfg=rfg), seqs, quals, True)
+    ref = np.frombuffer(bytes(out), dtype=_native.ALN_DTYPE)[:len(seqs)]
+    ctx.index_build(['HIV1B-pol-seed'], [POL], oracle.seed_len(mode))
+    ctx.reads_load(seqs, quals, True)
+    ctx.map(_native.params(mode, rdg=rdg, rfg=rfg))
+    gpu = ctx.fetch()
+    _assert_same(gpu, ref, seqs)
+    assert (ref['flag'] & 4 == 0).mean() > 0.2
+    assert (ref['xo'] > 0).sum() > 20      # gapped alignments among them
