@@ -283,16 +283,29 @@ __device__ int cluster_lanes(const SeedArgs &A, int64_t r, int lane, uint64_t v,
     return __builtin_amdgcn_readfirstlane(nc);
 }
 
-// Seeds, hit sort and candidate clustering of read r by one wave; writes the
-// candidates, n_cand and yf, returns the candidate count (wave-uniform).
-__device__ int seed_read(const SeedArgs &A, int64_t r, int lane, uint64_t *hits, Cand *best)
+// Seeds, hit sort and candidate clustering of read r (length m, base offset
+// off) by one wave; writes the candidates, n_cand and yf, returns the
+// candidate count (wave-uniform).
+__device__ int seed_read(const SeedArgs &A, int64_t r, int m, int64_t off, int lane, uint64_t *hits,
+                         Cand *best)
 {
     const int SL = A.I.seedlen;
-    const int m = A.R.len[r];
-    const int64_t off = A.R.off[r];
     if (m == 0) {
         if (lane == 0) { A.n_cand[r] = 0; A.yf[r] = 2; }
         return 0;
+    }
+    // the seed windows' loads are issued with the N count's (one round trip)
+    const int iv = m >= SL ? A.len_tab[m] : 1;
+    int ns = m >= SL ? 1 + (m - SL) / iv : 0;
+    if (ns > MAXSEEDS) ns = MAXSEEDS;
+    const int s = lane >> 5, t = lane & 31;
+    const int o = t * iv;
+    uint32_t wnm = 1;
+    uint64_t wkey = 0;
+    if (t < ns) {
+        const int p = s == 0 ? o : m - o - SL;
+        wnm = window_nmask(A.R, off + p, SL);
+        wkey = window_key(A.R, off + p, SL);
     }
     int nn = 0;
     for (int w = lane; w * 32 < m; w += 64) {
@@ -311,17 +324,11 @@ __device__ int seed_read(const SeedArgs &A, int64_t r, int lane, uint64_t *hits,
         if (lane == 0) A.n_cand[r] = 0;
         return 0;
     }
-    const int iv = A.len_tab[m];
-    int ns = 1 + (m - SL) / iv;
-    if (ns > MAXSEEDS) ns = MAXSEEDS;
-    const int s = lane >> 5, t = lane & 31;
-    const int o = t * iv;
     int cnt = 0;
     uint32_t start = 0;
     if (t < ns) {
-        const int p = s == 0 ? o : m - o - SL;
-        if (window_nmask(A.R, off + p, SL) == 0) {
-            uint64_t key = window_key(A.R, off + p, SL);
+        if (wnm == 0) {
+            uint64_t key = wkey;
             if (s) key = revcomp_key(key, SL);
             uint64_t h = hash_key(key) & A.I.hmask;
             for (;;) {
@@ -433,8 +440,18 @@ __global__ __launch_bounds__(256, SEED_WAVES_PER_SIMD) void k_seed(SeedArgs A)
         int n_work = 0;
         const int64_t r0 = ch * SEED_CHUNK;
         const int64_t r1 = r0 + SEED_CHUNK < A.R.n ? r0 + SEED_CHUNK : A.R.n;
+        // the chunk's read lengths and offsets in one round trip (lane = read)
+        int my_m = 0;
+        int64_t my_off = 0;
+        if (r0 + lane < r1) {
+            my_m = A.R.len[r0 + lane];
+            my_off = A.R.off[r0 + lane];
+        }
         for (int64_t r = r0; r < r1; ++r) {
-            const int nc = seed_read(A, r, lane, sh_hits[wv], sh_best[wv]);
+            const int l = (int)(r - r0);
+            const int m = __builtin_amdgcn_readlane(my_m, l);
+            const int64_t off = (int64_t)readlane64((uint64_t)my_off, l);
+            const int nc = seed_read(A, r, m, off, lane, sh_hits[wv], sh_best[wv]);
             if (lane < nc) sh_work[wv][n_work + lane] = (int32_t)(r * MAXCAND + lane);
             n_work += nc;
         }
