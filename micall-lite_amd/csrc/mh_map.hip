@@ -719,8 +719,9 @@ __device__ __forceinline__ void half_max64(long long v, int lane, long long &k0,
 //   (C) U(r, kb) >= Gb(r) on every row r of the traced segment (so H = U
 //       there and the traceback's "diagonal first" choice is the same),
 // the full DP picks the same best cell and traces the same all-M path.  The
-// fast path then writes only that lane's traceback bits and k_dp skips the
-// DP; otherwise (any condition false, read > 512 nt) it runs the full DP.
+// fast path then hands that path (and its local stop) to finish_ext, and
+// k_dp skips the DP and the traceback walk; otherwise (any condition false,
+// read > 512 nt) it runs the full DP.
 // The candidate is the seeded diagonal (band lane XCENTER): its exact
 // ungapped recurrence decides (A) first, then a per-diagonal non-match count
 // (4 rows per LDS word; wave lane L counts band lane L - 16) bounds every
@@ -730,8 +731,8 @@ __device__ __forceinline__ void half_max64(long long v, int lane, long long &k0,
 // og_mapper.c:dp_extend).
 // ---------------------------------------------------------------------------
 template <int LOCAL>
-__device__ bool dp_ungapped(const XView &X, uint32_t *bits, int m, int lane, int gmin, int hcol,
-                            int hb, int &best, int &bi, int &bl)
+__device__ bool dp_ungapped(const XView &X, int m, int lane, int gmin, int hb, int &best, int &bi,
+                            int &bl, int &low)
 {
     const uint32_t *tab = X.tab;
     const uint8_t *refw = X.refw, *rdc = X.rdc;
@@ -847,12 +848,10 @@ __device__ bool dp_ungapped(const XView &X, uint32_t *bits, int m, int lane, int
         if (r >= lo && r <= istar && r >= GBAR && H[u] < ma * (r + 1) - gmin) bad = true;
     }
     if (__builtin_amdgcn_ballot_w64(bad) != 0) return false;
-    // traceback bits of the seeded diagonal: every row diagonal (nibble 0);
-    // the local stop at istop is the traceback's H == 0
-    if (r0 < m) bits[lane * 64 + hcol + kb] = 0u;
     best = S;
     bi = istar;
     bl = kb;
+    low = istop;   // the path is rows istop + 1 .. istar of lane kb, all M
     return true;
 }
 
@@ -1005,7 +1004,7 @@ __device__ void dp_pair(const DpArgs &A, const XView &X0, const XView &X1, int m
 template <int LOCAL>
 __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, const uint32_t *bits,
                            int hcol, int best, int bi, int bl, int lane, int64_t &ck_base,
-                           int &ck_left)
+                           int &ck_left, int fast_low = -2)
 {
     const int ma = LOCAL ? 2 : 0;
     const int m = it.m, reflen = it.reflen, d0 = it.d0;
@@ -1030,7 +1029,20 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
     best = __builtin_amdgcn_readfirstlane(best);
     bi = __builtin_amdgcn_readfirstlane(bi);
     bl = __builtin_amdgcn_readfirstlane(bl);
-    if (!(LOCAL && best <= 0) && best >= __builtin_amdgcn_readfirstlane(minsc)) {
+    fast_low = __builtin_amdgcn_readfirstlane(fast_low);
+    if (fast_low > -2) {
+        // the fast path's all-M path (rows fast_low + 1 .. bi of band lane
+        // bl, its local stop included): the walk would find one M run
+        if (!(LOCAL && best <= 0) && best >= __builtin_amdgcn_readfirstlane(minsc)) {
+            const int len = bi - fast_low;
+            if (lane == 0) runs[0] = ((uint32_t)len << 4) | (uint32_t)MH_OP_M;
+            for (int r = fast_low + 1 + lane; r <= bi; r += 64) rowk[r] = (uint8_t)bl;
+            tb_ok = 1;
+            t_start = fast_low + 1;
+            t_first = fast_low + 1 + d0 + bl;
+            t_nrun = 1;
+        }
+    } else if (!(LOCAL && best <= 0) && best >= __builtin_amdgcn_readfirstlane(minsc)) {
         int i = bi, k = bl, state = 0, ok = 1, hv = best;
         int wr = -1, wk = -1;
         uint32_t word = 0;
@@ -1318,9 +1330,9 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             m_n = A.R.len[sid_nn / MAXCAND];
             roff_n = A.R.off[sid_nn / MAXCAND];
         }
-        int best = 0, bi = 0, bl = 0;
+        int best = 0, bi = 0, bl = 0, low = -1;
         const bool fast = it.m > 2 * GBAR + 8 && it.m <= 512 &&
-                          dp_ungapped<LOCAL>(X, bits, it.m, lane, gmin, 32 * h, it.hb, best, bi, bl);
+                          dp_ungapped<LOCAL>(X, it.m, lane, gmin, it.hb, best, bi, bl, low);
         n_fast += fast;
         if (more) {   // next item's reference window: lands during the DP / traceback
             reflen_n = A.I.ref_len[cd_n.ref];
@@ -1328,7 +1340,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         }
         if (fast) {
             wave_sync();
-            finish_ext<LOCAL>(A, it, X, bits, 32 * h, best, bi, bl, lane, ck_base, ck_left);
+            finish_ext<LOCAL>(A, it, X, bits, 32 * h, best, bi, bl, lane, ck_base, ck_left, low);
         } else if (!pend) {
             P = it;
             pend = true;
