@@ -1450,6 +1450,7 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
             const int s = 1 - ast;
             // the mate on strand s; bases past its end count as N (never match)
             const int nw = (m + 15) >> 4;
+            bool read_n = false;   // an ambiguous base inside the read
             for (int w = lane; w < nw; w += 64) {
                 uint32_t code = 0, nmk = 0;
                 for (int x = 0; x < 16; ++x) {
@@ -1458,6 +1459,7 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
                     if (b < m) {
                         c = read_code(A.R, off, s ? m - 1 - b : b);
                         if (s && c < 4) c = 3 - c;
+                        read_n |= c > 3;
                     }
                     if (c > 3) nmk |= 1u << (2 * x);
                     else code |= c << (2 * x);
@@ -1465,17 +1467,20 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
                 rdw[w] = code;
                 rdn[w] = nmk;
             }
+            const bool any_read_n = __builtin_amdgcn_ballot_w64(read_n) != 0;
             int bestM = -1, bestd = 0;
             const int dlast = (int)(hi - m);
             for (int d0 = (int)lo; d0 <= dlast; d0 += RESCUE_CHUNK) {
                 const int nd = dlast - d0 + 1 < RESCUE_CHUNK ? dlast - d0 + 1 : RESCUE_CHUNK;
                 // reference bases d0 .. d0 + nd + m (+ one word), N past the window
                 const int nrw = (nd + m + 15) / 16 + 1;
+                bool win_n = false;   // an ambiguous reference base inside the window
                 for (int w = lane; w < nrw; w += 64) {
                     uint32_t code = 0, nmk = 0;
                     for (int x = 0; x < 16; ++x) {
                         const int64_t j = (int64_t)d0 + 16 * w + x;
                         const uint32_t c = j < hi ? A.I.codes[gref + j] : 4u;
+                        win_n |= j < hi && c > 3;
                         if (c > 3) nmk |= 1u << (2 * x);
                         else code |= c << (2 * x);
                     }
@@ -1483,6 +1488,34 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
                     rfn[w] = nmk;
                 }
                 wave_sync();
+                if (!any_read_n && __builtin_amdgcn_ballot_w64(win_n) == 0) {
+                    // no ambiguous base on either side: words 0 .. nw-2 pair read
+                    // bases < m with window bases < hi and need no N masks (the
+                    // window word of step i + 1 is carried over); the last word
+                    // masks the read's tail
+                    for (int t = lane; t < nd; t += 64) {
+                        const int w0 = t >> 4;
+                        const uint32_t sh = (uint32_t)(2 * (t & 15));
+                        uint32_t lo_w = rfw[w0];
+                        int cnt = 0;
+                        for (int i = 0; i < nw - 1; ++i) {
+                            const uint32_t hi_w = rfw[w0 + i + 1];
+                            const uint32_t x = rdw[i] ^ __builtin_amdgcn_alignbit(hi_w, lo_w, sh);
+                            cnt += __builtin_popcount(~(x | (x >> 1)) & 0x55555555u);
+                            lo_w = hi_w;
+                        }
+                        {
+                            const int i = nw - 1;
+                            const uint32_t v = __builtin_amdgcn_alignbit(rfw[w0 + i + 1], lo_w, sh);
+                            const uint32_t vn = __builtin_amdgcn_alignbit(rfn[w0 + i + 1], rfn[w0 + i], sh);
+                            const uint32_t x = rdw[i] ^ v;
+                            cnt += __builtin_popcount(~(x | (x >> 1) | rdn[i] | vn) & 0x55555555u);
+                        }
+                        if (cnt > bestM) { bestM = cnt; bestd = d0 + t; }
+                    }
+                    wave_sync();
+                    continue;
+                }
                 for (int t = lane; t < nd; t += 64) {
                     // matches on diagonal d0 + t: 16 bases per step, the window
                     // words aligned to the diagonal by a funnel shift
