@@ -8,6 +8,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "micall_hip.h"
@@ -160,6 +161,11 @@ struct PileState {
     int win_map_cap = 0;
     char *ins_scratch = nullptr;    // per-wave merged-insertion scratch of k_pileup
     int64_t ins_scratch_bytes = 0;
+    // k_pileup block shapes already sized by the occupancy query: key (source,
+    // LDS bytes before the staging areas, staging bytes per wave) -> waves
+    // per block, resident blocks per CU
+    std::map<std::tuple<int, int64_t, int>, std::pair<int, int>> shapes;
+    int n_cu = 0;
     // device aggregation of the token events (mh_pileup_events): an
     // open-addressing table of representative event + count per distinct
     // (ref, pos, token), and the list of used slots

@@ -805,12 +805,35 @@ static int pile_geometry(Ctx &c, int source, int64_t n_units, PileGeometry &g)
         words += 2 * (int64_t)want;
     }
     g.win_words = (int)words;
-    g.wpb = (int)(((int64_t)PU_LDS - (int64_t)base - 4 * words) / g.unit_bytes);
-    if (g.wpb > 16) g.wpb = 16;
-    if (g.wpb < 1) g.wpb = 1;
-    g.lds = base + 4 * (size_t)words + (size_t)g.wpb * g.unit_bytes;
+    // The block shape that keeps the most waves resident per CU: k_pileup is
+    // a chain of dependent loads per unit and runs as fast as the waves in
+    // flight; its 80 VGPRs allow 24 per CU, which one block of 16 waves
+    // leaves at 16 (2 blocks of 12 waves: 8.0 -> 6.5 ms per C2 step).  LDS
+    // per block is the windows plus the waves' staging areas.
+    const int64_t lds0 = (int64_t)base + 4 * words;
+    const auto key = std::make_tuple(source, lds0, g.unit_bytes);
+    auto hit = P.shapes.find(key);
+    if (hit == P.shapes.end()) {
+        if (!P.n_cu) MH_HIP(hipDeviceGetAttribute(&P.n_cu, hipDeviceAttributeMultiprocessorCount, c.device));
+        const void *kern = source == 0 ? (const void *)k_pileup<0> : (const void *)k_pileup<1>;
+        MH_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, PU_LDS));
+        int best_w = 0, best_wpb = 1, best_nb = 1;
+        for (int wpb = 16; wpb >= 1; --wpb) {
+            const int64_t lds = lds0 + (int64_t)wpb * g.unit_bytes;
+            if (lds > PU_LDS) continue;
+            int nb = 0;
+            MH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 64 * wpb, (size_t)lds));
+            if (nb * wpb > best_w) { best_w = nb * wpb; best_wpb = wpb; best_nb = nb; }
+        }
+        hit = P.shapes.emplace(key, std::make_pair(best_wpb, best_nb > 0 ? best_nb : 1)).first;
+    }
+    g.wpb = hit->second.first;
+    g.lds = (size_t)lds0 + (size_t)g.wpb * g.unit_bytes;
     g.blocks = (n_units + g.wpb - 1) / g.wpb;
-    const int64_t max_blocks = words > 0 ? 256 : 256 * 8;
+    // windows: one resident wave of blocks (each flushes its windows once);
+    // without windows more blocks than fit, grid-strided
+    const int64_t n_cu = P.n_cu > 0 ? P.n_cu : 256;
+    const int64_t max_blocks = words > 0 ? n_cu * hit->second.second : n_cu * 8;
     if (g.blocks > max_blocks) g.blocks = max_blocks;
     if (words > 0 && g.blocks < (n_units + PU_UNITS_PER_BLOCK - 1) / PU_UNITS_PER_BLOCK)
         g.blocks = (n_units + PU_UNITS_PER_BLOCK - 1) / PU_UNITS_PER_BLOCK;
