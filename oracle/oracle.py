@@ -85,6 +85,7 @@ def _declare(L):
     L.og_seed_interval.argtypes = [ctypes.c_int, ctypes.c_int]
     L.og_min_score.argtypes = [ctypes.c_int, ctypes.c_int]
     L.og_n_ceil.argtypes = [ctypes.c_int]
+    L.og_band_half.argtypes = [ctypes.POINTER(OgParams), ctypes.c_int]
     L.og_mapq.argtypes = [ctypes.c_int] * 5
     L.og_pileup.argtypes = [ctypes.c_int, ctypes.c_int32, ctypes.POINTER(OgRow), ctypes.c_int64,
                             ctypes.POINTER(ctypes.c_int64), ctypes.c_int,
@@ -156,6 +157,11 @@ def seed_len(mode):
 
 def params(mode, rdg=(10, 3), rfg=(10, 3), maxins=1200):
     return OgParams(mode, rdg[0], rdg[1], rfg[0], rfg[1], maxins)
+
+
+def band_half(par, length):
+    """Half-width of the DP band around the seeded diagonal (og_band_half)."""
+    return lib().og_band_half(ctypes.byref(par), length)
 
 
 CAUSES = ['aligned', 'rescued', 'filtered (N / empty)', 'no candidate', 'below --score-min',
