@@ -161,6 +161,10 @@ struct CtxEx : Ctx {
     std::vector<int32_t> tok_ref, tok_pos, tok_off, tok_len;
     std::vector<int64_t> tok_count;
     std::string tok_pool;
+    // pinned staging for the pileup fetches: several copies on the stream,
+    // one synchronisation (pageable hipMemcpy synchronises every copy)
+    void *pin = nullptr;
+    size_t pin_cap = 0;
     // mh_format_rows: the text of a size query, kept for the copy after it
     int64_t map_gen = 0;                  // bumped by every mh_map
     uint64_t fmt_key = 0;
@@ -557,6 +561,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipFree(P.sel);
     hipFree(P.win_map);
     hipFree(c->len_tab);
+    if (c->pin) hipHostFree(c->pin);
     s2a_free(*c);
     censor_free(*c);
     a2c_free(*c);
@@ -1516,6 +1521,51 @@ int mh_pileup_dims(mh_ctx *ctx, int *n_refs, int32_t *cap, int64_t *n_events, in
     return 0;
 }
 
+// Device-to-host copies of up to 6 (source, size, destination) parts: the
+// parts go through the context's pinned staging buffer with one stream
+// synchronisation; parts too large for it are copied directly.
+struct FetchPart {
+    const void *src;
+    size_t bytes;
+    void *dst;
+};
+
+static int fetch_parts(CtxEx &c, const FetchPart *parts, int n)
+{
+    size_t total = 0;
+    for (int i = 0; i < n; ++i) if (parts[i].dst) total += (parts[i].bytes + 255) & ~(size_t)255;
+    if (total > ((size_t)64 << 20)) {   // large fetches (all 74 seeds): plain copies
+        for (int i = 0; i < n; ++i)
+            if (parts[i].dst && parts[i].bytes)
+                MH_HIP(hipMemcpy(parts[i].dst, parts[i].src, parts[i].bytes, hipMemcpyDeviceToHost));
+        return 0;
+    }
+    if (c.pin_cap < total) {
+        if (c.pin) hipHostFree(c.pin);
+        c.pin = nullptr;
+        c.pin_cap = 0;
+        const size_t cap = total > ((size_t)1 << 20) ? total : ((size_t)1 << 20);
+        MH_HIP(hipHostMalloc(&c.pin, cap, hipHostMallocDefault));
+        c.pin_cap = cap;
+    }
+    size_t at = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!parts[i].dst) continue;
+        if (parts[i].bytes)
+            MH_HIP(hipMemcpyAsync((char *)c.pin + at, parts[i].src, parts[i].bytes, hipMemcpyDeviceToHost,
+                                  c.stream));
+        at += (parts[i].bytes + 255) & ~(size_t)255;
+    }
+    MH_HIP(hipStreamSynchronize(c.stream));
+    at = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!parts[i].dst) continue;
+        if (parts[i].bytes) std::memcpy(parts[i].dst, (const char *)c.pin + at, parts[i].bytes);
+        at += (parts[i].bytes + 255) & ~(size_t)255;
+    }
+    return 0;
+}
+
 int mh_pileup_fetch(mh_ctx *ctx, int32_t *dense, uint8_t *nflag, uint8_t *dflag,
                     int64_t *read_counts, int64_t *first_unit, int32_t *max_pos)
 {
@@ -1524,14 +1574,14 @@ int mh_pileup_fetch(mh_ctx *ctx, int32_t *dense, uint8_t *nflag, uint8_t *dflag,
     PileState &P = c->pile;
     if (!P.dense) { set_error("no pileup (call mh_pileup)"); return -3; }
     MH_HIP(hipSetDevice(c->device));
-    const int64_t cells = (int64_t)P.n_refs * P.cap;
-    if (dense) MH_HIP(hipMemcpy(dense, P.dense, sizeof(int32_t) * 4 * cells, hipMemcpyDeviceToHost));
-    if (nflag) MH_HIP(hipMemcpy(nflag, P.nflag, cells, hipMemcpyDeviceToHost));
-    if (dflag) MH_HIP(hipMemcpy(dflag, P.dflag, cells, hipMemcpyDeviceToHost));
-    if (read_counts) MH_HIP(hipMemcpy(read_counts, P.read_counts, sizeof(int64_t) * P.n_refs, hipMemcpyDeviceToHost));
-    if (first_unit) MH_HIP(hipMemcpy(first_unit, P.first_unit, sizeof(int64_t) * P.n_refs, hipMemcpyDeviceToHost));
-    if (max_pos) MH_HIP(hipMemcpy(max_pos, P.max_pos, sizeof(int32_t) * P.n_refs, hipMemcpyDeviceToHost));
-    return 0;
+    const size_t cells = (size_t)P.n_refs * P.cap, nr = (size_t)P.n_refs;
+    const FetchPart parts[6] = {{P.dense, sizeof(int32_t) * 4 * cells, dense},
+                                {P.nflag, cells, nflag},
+                                {P.dflag, cells, dflag},
+                                {P.read_counts, sizeof(int64_t) * nr, read_counts},
+                                {P.first_unit, sizeof(int64_t) * nr, first_unit},
+                                {P.max_pos, sizeof(int32_t) * nr, max_pos}};
+    return fetch_parts(*c, parts, 6);
 }
 
 int mh_pileup_fetch_ref(mh_ctx *ctx, int ref, int32_t *dense, uint8_t *nflag, uint8_t *dflag)
@@ -1543,10 +1593,10 @@ int mh_pileup_fetch_ref(mh_ctx *ctx, int ref, int32_t *dense, uint8_t *nflag, ui
     if (ref < 0 || ref >= P.n_refs) { set_error("mh_pileup_fetch_ref: ref %d out of range", ref); return -3; }
     MH_HIP(hipSetDevice(c->device));
     const int64_t base = (int64_t)ref * P.cap;
-    if (dense) MH_HIP(hipMemcpy(dense, P.dense + 4 * base, sizeof(int32_t) * 4 * P.cap, hipMemcpyDeviceToHost));
-    if (nflag) MH_HIP(hipMemcpy(nflag, P.nflag + base, P.cap, hipMemcpyDeviceToHost));
-    if (dflag) MH_HIP(hipMemcpy(dflag, P.dflag + base, P.cap, hipMemcpyDeviceToHost));
-    return 0;
+    const FetchPart parts[3] = {{P.dense + 4 * base, sizeof(int32_t) * 4 * (size_t)P.cap, dense},
+                                {P.nflag + base, (size_t)P.cap, nflag},
+                                {P.dflag + base, (size_t)P.cap, dflag}};
+    return fetch_parts(*c, parts, 3);
 }
 
 int mh_pileup_events(mh_ctx *ctx, int32_t *ref, int32_t *pos, int32_t *tok_off, int32_t *tok_len,

@@ -165,7 +165,6 @@ struct PileState {
     // LDS bytes before the staging areas, staging bytes per wave) -> waves
     // per block, resident blocks per CU
     std::map<std::tuple<int, int64_t, int>, std::pair<int, int>> shapes;
-    int n_cu = 0;
     // device aggregation of the token events (mh_pileup_events): an
     // open-addressing table of representative event + count per distinct
     // (ref, pos, token), and the list of used slots
@@ -211,6 +210,7 @@ struct A2CState;      // mh_a2c.hip
 
 struct Ctx {
     int device = 0;
+    int n_cu = 0;                    // compute units of the device (launch sizing)
     // per-kernel timing with HIP events on `stream` (mh_profile)
     bool prof = false;
     std::map<std::string, ProfEntry> prof_acc;

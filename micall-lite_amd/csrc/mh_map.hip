@@ -232,18 +232,70 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
 // centre as the longest run of equal hits (the first on ties), by one wave
 // max.  The same clusters, centres, supports and top-MAXCAND order as the
 // serial walk below (og_mapper.c find_candidates); writes the candidates.
+// The hit of lane ^ J.  J = 1, 2, 8 are one DPP move per word (quad_perm,
+// row_ror:8), J = 4 two moves and a select; J = 16, 32 go through
+// ds_bpermute.  Register to register where DPP reaches: a bpermute is an LDS
+// crossbar round trip, and the sort is a chain of them.
+template <int J>
+__device__ __forceinline__ uint64_t xor_lane64(uint64_t v, int lane)
+{
+    const int lo = (int)(uint32_t)v, hi = (int)(v >> 32);
+    int xl, xh;
+    if (J == 1) {
+        xl = dpp<0xB1>(lo, lo); xh = dpp<0xB1>(hi, hi);       // quad_perm [1,0,3,2]
+    } else if (J == 2) {
+        xl = dpp<0x4E>(lo, lo); xh = dpp<0x4E>(hi, hi);       // quad_perm [2,3,0,1]
+    } else if (J == 4) {
+        const bool up = (lane & 4) != 0;                      // take lane - 4, else lane + 4
+        const int ll = dpp<0x104>(lo, lo), lr = dpp<0x114>(lo, lo);   // row_shl:4, row_shr:4
+        const int hl = dpp<0x104>(hi, hi), hr = dpp<0x114>(hi, hi);
+        xl = up ? lr : ll;
+        xh = up ? hr : hl;
+    } else if (J == 8) {
+        xl = dpp<0x128>(lo, lo); xh = dpp<0x128>(hi, hi);     // row_ror:8
+    } else {
+        return shfl_xor64(v, J);
+    }
+    return ((uint64_t)(uint32_t)xh << 32) | (uint32_t)xl;
+}
+
+template <int K, int J>
+__device__ __forceinline__ void bitonic_step(uint64_t &v, int lane)
+{
+    const uint64_t o = xor_lane64<J>(v, lane);
+    const bool take_min = ((lane & J) == 0) == ((lane & K) == 0);
+    v = take_min ? (o < v ? o : v) : (o > v ? o : v);
+}
+
+// Bitonic sort of one 64-bit hit per lane over the first N lanes (N a power
+// of two <= 64; the stages of every block size k <= N, as the loop
+// for k in 2..N, j in k/2..1 runs them).
+__device__ __forceinline__ uint64_t bitonic_lanes(uint64_t v, int lane, int N)
+{
+    bitonic_step<2, 1>(v, lane);
+    if (N >= 4) { bitonic_step<4, 2>(v, lane); bitonic_step<4, 1>(v, lane); }
+    if (N >= 8) { bitonic_step<8, 4>(v, lane); bitonic_step<8, 2>(v, lane); bitonic_step<8, 1>(v, lane); }
+    if (N >= 16) {
+        bitonic_step<16, 8>(v, lane); bitonic_step<16, 4>(v, lane);
+        bitonic_step<16, 2>(v, lane); bitonic_step<16, 1>(v, lane);
+    }
+    if (N >= 32) {
+        bitonic_step<32, 16>(v, lane); bitonic_step<32, 8>(v, lane); bitonic_step<32, 4>(v, lane);
+        bitonic_step<32, 2>(v, lane); bitonic_step<32, 1>(v, lane);
+    }
+    if (N >= 64) {
+        bitonic_step<64, 32>(v, lane); bitonic_step<64, 16>(v, lane); bitonic_step<64, 8>(v, lane);
+        bitonic_step<64, 4>(v, lane); bitonic_step<64, 2>(v, lane); bitonic_step<64, 1>(v, lane);
+    }
+    return v;
+}
+
 __device__ int cluster_lanes(const SeedArgs &A, int64_t r, int lane, uint64_t v, int total,
                              Cand *best)
 {
     int N = 2;
     while (N < total) N <<= 1;
-    for (int k = 2; k <= N; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint64_t o = shfl_xor64(v, j);
-            const bool take_min = ((lane & j) == 0) == ((lane & k) == 0);
-            v = take_min ? (o < v ? o : v) : (o > v ? o : v);
-        }
-    }
+    v = bitonic_lanes(v, lane, N);
     const uint64_t pv = ((uint64_t)(uint32_t)dpp<DPP_WAVE_SHR1>(0, (int)(v >> 32)) << 32) |
                         (uint32_t)dpp<DPP_WAVE_SHR1>(0, (int)(uint32_t)v);   // lane - 1's hit
     const bool valid = lane < total;

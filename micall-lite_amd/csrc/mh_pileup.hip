@@ -814,7 +814,7 @@ static int pile_geometry(Ctx &c, int source, int64_t n_units, PileGeometry &g)
     const auto key = std::make_tuple(source, lds0, g.unit_bytes);
     auto hit = P.shapes.find(key);
     if (hit == P.shapes.end()) {
-        if (!P.n_cu) MH_HIP(hipDeviceGetAttribute(&P.n_cu, hipDeviceAttributeMultiprocessorCount, c.device));
+        if (!c.n_cu) MH_HIP(hipDeviceGetAttribute(&c.n_cu, hipDeviceAttributeMultiprocessorCount, c.device));
         const void *kern = source == 0 ? (const void *)k_pileup<0> : (const void *)k_pileup<1>;
         MH_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, PU_LDS));
         int best_w = 0, best_wpb = 1, best_nb = 1;
@@ -832,7 +832,7 @@ static int pile_geometry(Ctx &c, int source, int64_t n_units, PileGeometry &g)
     g.blocks = (n_units + g.wpb - 1) / g.wpb;
     // windows: one resident wave of blocks (each flushes its windows once);
     // without windows more blocks than fit, grid-strided
-    const int64_t n_cu = P.n_cu > 0 ? P.n_cu : 256;
+    const int64_t n_cu = c.n_cu > 0 ? c.n_cu : 256;
     const int64_t max_blocks = words > 0 ? n_cu * hit->second.second : n_cu * 8;
     if (g.blocks > max_blocks) g.blocks = max_blocks;
     if (words > 0 && g.blocks < (n_units + PU_UNITS_PER_BLOCK - 1) / PU_UNITS_PER_BLOCK)
