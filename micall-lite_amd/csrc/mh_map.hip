@@ -1078,6 +1078,7 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
     // (og_mapper.c dp_extend, src 0).  Gap moves are single steps.  Only
     // lane 0 writes runs. ----
     int tb_ok = 0, t_start = 0, t_first = 0, t_nrun = 0;
+    int path_cnt = 0;   // this lane's M rows of the path: ambiguous << 16 | mismatches
     best = __builtin_amdgcn_readfirstlane(best);
     bi = __builtin_amdgcn_readfirstlane(bi);
     bl = __builtin_amdgcn_readfirstlane(bl);
@@ -1088,7 +1089,12 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
         if (!(LOCAL && best <= 0) && best >= __builtin_amdgcn_readfirstlane(minsc)) {
             const int len = bi - fast_low;
             if (lane == 0) runs[0] = ((uint32_t)len << 4) | (uint32_t)MH_OP_M;
-            for (int r = fast_low + 1 + lane; r <= bi; r += 64) rowk[r] = (uint8_t)bl;
+            for (int r = fast_low + 1 + lane; r <= bi; r += 64) {
+                rowk[r] = (uint8_t)bl;
+                const int g = refw[r + bl] >> 2, rb = rdc[r] & 7;
+                const int amb = rb > 3 || g > 3;
+                path_cnt += (amb << 16) + (amb || rb != g);
+            }
             tb_ok = 1;
             t_start = fast_low + 1;
             t_first = fast_low + 1 + d0 + bl;
@@ -1166,7 +1172,12 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
                         rop = MH_OP_M;
                         rlen = len;
                     }
-                    for (int r = low + 1 + lane; r <= i; r += 64) rowk[r] = (uint8_t)k;
+                    for (int r = low + 1 + lane; r <= i; r += 64) {
+                        rowk[r] = (uint8_t)k;
+                        const int g = refw[r + k] >> 2, rb = rdc[r] & 7;
+                        const int amb = rb > 3 || g > 3;
+                        path_cnt += (amb << 16) + (amb || rb != g);
+                    }
                     first_j = low + 1 + d0 + k;
                 }
                 i = low;
@@ -1263,16 +1274,21 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
         }
         clipL = __builtin_amdgcn_readfirstlane(clipL);
         clipR = __builtin_amdgcn_readfirstlane(clipR);
-        // one pass over the M rows: ambiguous positions over the untrimmed
-        // alignment (--n-ceil) and mismatches over the trimmed one, summed
-        // together (nn << 16 | xm)
-        int cnt = 0;
-        for (int i = t_start + lane; i <= bi; i += 64) {
-            const int k = rowk[i];
-            if (k == 255) continue;
-            const int g = refw[i + k] >> 2, rb = rdc[i] & 7;
-            if (rb > 3 || g > 3) cnt += 1 << 16;
-            if ((rb > 3 || g > 3 || rb != g) && i >= clipL && i <= m - 1 - clipR) ++cnt;
+        // ambiguous positions over the untrimmed alignment (--n-ceil) and
+        // mismatches over the trimmed one, summed together (nn << 16 | xm):
+        // counted along the path by the traceback, so only a trim that moved
+        // a clip (the path overhangs a reference end, or starts / ends with
+        // an insertion) needs a pass over the M rows
+        int cnt = path_cnt;
+        if (clipL != t_start || clipR != m - 1 - bi) {
+            cnt = 0;
+            for (int i = t_start + lane; i <= bi; i += 64) {
+                const int k = rowk[i];
+                if (k == 255) continue;
+                const int g = refw[i + k] >> 2, rb = rdc[i] & 7;
+                if (rb > 3 || g > 3) cnt += 1 << 16;
+                if ((rb > 3 || g > 3 || rb != g) && i >= clipL && i <= m - 1 - clipR) ++cnt;
+            }
         }
         cnt = wave_sum(cnt);
         if ((cnt >> 16) > A.len_tab[2 * (MAXLEN + 1) + m]) tb_ok = 0;
