@@ -1021,6 +1021,19 @@ __device__ void dp_pair(const DpArgs &A, const XView &X0, const XView &X1, int m
 #pragma unroll
             for (int t = 0; t < 8; ++t)
                 dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K, acc);
+        } else if (m0 == m1) {
+            // both halves end on the same row: a row's gap window is the same
+            // on every lane (wave-uniform branches), rows past the read are
+            // skipped
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int i = i0 + t;
+                if (i >= m0) acc <<= 4;   // past the read: an empty nibble
+                else if (i >= GBAR && i < m0 - GBAR)
+                    dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K, acc);
+                else
+                    dp_row_nogap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - i, K.floor, acc);
+            }
         } else {
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
