@@ -937,11 +937,10 @@ __device__ __forceinline__ void stage_ext(const DpArgs &A, const XItem &it, cons
                 c = ((nmw[u] >> bb[u]) & 1) ? 4u : (sqw[u] & 3u);
                 if (it.strand && c < 4) c = 3 - c;
                 pen = (uint32_t)mm_pen((int)qv[u]);
-                tb = 0;
-                for (int g = 0; g < 5; ++g) {
-                    const int sc = (c > 3 || g > 3) ? -NPEN : (c == (uint32_t)g ? ma : -(int)pen);
-                    tb |= (uint32_t)(sc + 8) << (4 * g);
-                }
+                // nibble g = score(g) + 8: -pen for a mismatch, ma for g == c,
+                // -NPEN when either side is ambiguous (g == 4 or c == 4)
+                const uint32_t mis = (8u - pen) * 0x1111u | (uint32_t)(8 - NPEN) << 16;
+                tb = c < 4 ? mis + ((uint32_t)ma + pen) * (1u << (4 * c)) : 0x11111u * (uint32_t)(8 - NPEN);
             }
             X.tab[i] = tb;
             X.rdc[i] = (uint8_t)(c | pen << 3);
