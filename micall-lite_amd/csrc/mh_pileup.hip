@@ -300,8 +300,10 @@ __device__ __forceinline__ int wave_max_all(int v)
     return __builtin_amdgcn_readlane(wave_scan_dpp(v, INT32_MIN, [](int x, int y) { return x > y ? x : y; }), 63);
 }
 
+// 6 waves per SIMD: at most 80 VGPRs, so 24 waves stay resident per CU
+// (pile_geometry); k_pileup<0> keeps 2 VGPRs in scratch (12 B per lane)
 template <int SRC>
-__global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
+__global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
@@ -363,15 +365,20 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
         // ---- apply_cigar: op offsets by a lane-parallel prefix scan, then
         // expand each mate into reference coordinates lane-parallel ----
         int padA = 0, padB = 0, lenA = 0, lenB = 0, bad = 0, n_iops = 0;
+        // per mate: the read offset of its only reference-consuming op when
+        // that op is an M (S/M/S reads), else -1; such a mate expands as
+        // read offset + t with no op lookup
+        int oneA = -1, oneB = -1;
         auto pad = [&](int k) { return k ? padB : padA; };
         auto len = [&](int k) { return k ? lenB : lenA; };
+        auto one = [&](int k) { return k ? oneB : oneA; };
         #pragma unroll
         for (int k = 0; k < 2; ++k) {
             if (k >= nm) break;
             const RowV mk = mate(k);
             const int nc = mk.n_cigar;
             if (nc > MH_MAXOPS) { bad = 1; break; }
-            int rf0 = 0, rd0 = 0;
+            int rf0 = 0, rd0 = 0, n_refop = 0, first_rd = -1;
             for (int o0 = 0; o0 < nc; o0 += 64) {
                 const int o = o0 + lane;
                 int dref = 0, dread = 0, isd = 0, isi = 0, badop = 0;
@@ -391,13 +398,19 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
                 }
                 bad |= __any(badop);
                 n_iops += __popcll(__ballot(isi));
+                const uint64_t rops = __builtin_amdgcn_ballot_w64(dref > 0);
+                if (rops && n_refop == 0)
+                    first_rd = __builtin_amdgcn_readlane(isd ? -1 : rd0 + iread - dread,
+                                                         (int)__builtin_ctzll(rops));
+                n_refop += __popcll(rops);
                 rf0 += __builtin_amdgcn_readlane(iref, 63);
                 rd0 += __builtin_amdgcn_readlane(iread, 63);
             }
             if (lane == 0) { L.opref(k)[nc] = rf0; L.opread(k)[nc] = rd0; }
             if (rd0 != mk.m || rf0 > A.span_cap || mk.pos < 1) bad = 1;
-            if (k) { padB = mk.pos - 1; lenB = padB + rf0; }
-            else { padA = mk.pos - 1; lenA = padA + rf0; }
+            const int onek = n_refop == 1 ? first_rd : -1;
+            if (k) { padB = mk.pos - 1; lenB = padB + rf0; oneB = onek; }
+            else { padA = mk.pos - 1; lenA = padA + rf0; oneA = onek; }
         }
         if (bad) {
             if (lane == 0) atomicExch(&A.ev_ctr[3], 1ull);
@@ -419,13 +432,19 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
                     const int t = ch * 64 + lane;
                     int x = -2;
                     if (k < nm && t < span) {
-                        // the M/D op covering reference offset t (I/S ops span nothing)
-                        int o = 0;
-                        while (L.opref(k)[o + 1] <= t) ++o;
-                        const int rd = L.opread(k)[o];
+                        int rd, r0 = 0;
+                        if (one(k) >= 0) {
+                            rd = one(k);   // the one M op starts at reference offset 0
+                        } else {
+                            // the M/D op covering reference offset t (I/S ops span nothing)
+                            int o = 0;
+                            while (L.opref(k)[o + 1] <= t) ++o;
+                            rd = L.opread(k)[o];
+                            r0 = L.opref(k)[o];
+                        }
                         x = -1;
                         if (rd >= 0) {
-                            x = rd + (t - L.opref(k)[o]);
+                            x = rd + (t - r0);
                             if (mk.rev) x = mk.m - 1 - x;
                         }
                     }
@@ -572,7 +591,17 @@ __global__ __launch_bounds__(1024) void k_pileup(PileArgs A)
         // first index where seq2 is not '-' (is_reverse_started) and where the
         // forward read starts (first i < len1 not both '-')
         int rev_start = 1 << 30, fwd_start = 1 << 30;
-        for (int i0 = lo; i0 < len2; i0 += 64) {
+        // both padded reads start with a base at their pad (the common case):
+        // seq2 starts at pad2 and the forward read at min(pad1, pad2)
+        const bool starts_b = len2 > pad2 &&
+                              __builtin_amdgcn_readfirstlane((int)(unsigned char)L.c(b)[0]) != '-';
+        const bool starts_a = a < 0 || (len1 > pad1 &&
+                              __builtin_amdgcn_readfirstlane((int)(unsigned char)L.c(a)[0]) != '-');
+        if (starts_b && starts_a) {
+            rev_start = pad2;
+            if (a >= 0) fwd_start = pad1 < pad2 ? pad1 : pad2;
+        }
+        for (int i0 = lo; i0 < len2 && !(starts_b && starts_a); i0 += 64) {
             const int i = i0 + lane;
             int rs = 1 << 30, fs = 1 << 30;
             if (i < len2) {
