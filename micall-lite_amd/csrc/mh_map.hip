@@ -517,7 +517,7 @@ __global__ __launch_bounds__(256, SEED_WAVES_PER_SIMD) void k_seed(SeedArgs A)
 }
 
 // ---------------------------------------------------------------------------
-// k_dp: banded affine-gap DP, one wave64 per candidate
+// k_dp: banded affine-gap DP, two candidates per wave64 (32 lanes each)
 // ---------------------------------------------------------------------------
 struct DpArgs {
     DevReads R;
@@ -589,21 +589,14 @@ __device__ __forceinline__ int scan_max(int x)
 // the diagonal move is one add (local mode keeps the - 8: its floor and the
 // best-cell key must not drift by row).  Lane-uniform offsets cancel in every
 // traceback bit; the best score subtracts them once at the end.
+// All but dIE are per lane: a lane outside its extension's band (and, for
+// E, the band's top lane) holds HUGE_NEG in mexI / cF and 0 as its floor.
 struct DpConst {
     int mexI;           // E~ = dpp(q) + mexI: -(exI + exD), + 8 end-to-end
     int dIE;            // exI - oeI: h1 - e1 = (Hp + dIE) - Ep on the source lane
-    int cF;             // F~ = dpp(P) + cF: -(oeD - exD), in a VGPR
+    int cF;             // F~ = dpp(P) + cF: -(oeD - exD)
     int floor;          // local: BIAS + exD * lane, the shifted zero
 };
-
-// a wave-uniform value the compiler must keep in a VGPR: VOP2 DPP forms take
-// their second operand from a VGPR only
-__device__ __forceinline__ int in_vgpr(int v)
-{
-    int r;
-    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(v));
-    return r;
-}
 
 // acc = 2 acc + (d < 0): the sign bit of d shifted into the traceback word
 __device__ __forceinline__ uint32_t push_sign(uint32_t acc, int d)
