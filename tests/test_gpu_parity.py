@@ -3,6 +3,7 @@ same seeded inputs (bit-exact: every SAM field and CIGAR op, every pileup
 counter), and against the reference-generated golden vectors."""
 import json
 import os
+import re
 from collections import Counter
 
 import numpy as np
@@ -204,41 +205,94 @@ def test_pileup_rows_vs_golden_sams(ctx, golden_dir):
     with open(os.path.join(golden_dir, 'pileup_golden.json')) as f:
         cases = json.load(f)['cases']
     for c in cases:
-        ref_names, pairs = oracle.matchmaker(c['sam'].splitlines(True))
-        want_refmap, want_counts = oracle.pileup(ref_names, pairs, c['quality_cutoff'])
-        rows, units = [], []
-        for r1, r2 in pairs:
-            ids = []
-            for r in (r1, r2):
-                if r is None:
-                    ids.append(-1)
+        _rows_case_vs_oracle(ctx, c['sam'], c['quality_cutoff'])
+
+
+def _random_cigar_sam(rng, n_pairs, ref_len=240):
+    """SAM text whose CIGARs start with deletions, insertions or soft clips
+    (k_pileup's merge-start shortcut does not apply to a padded read that
+    starts with '-'), with inner indels; bases and qualities random."""
+    lines = ['@HD\tVN:1.0\tSO:unsorted\n', '@SQ\tSN:r1\tLN:{}\n'.format(ref_len)]
+    quals = 'FFFFF5#(:?'
+
+    def cigar(m):
+        ops, left = [], m
+        lead = rng.integers(0, 4)
+        if lead == 1:
+            ops.append('{}D'.format(int(rng.integers(1, 4))))
+        elif lead == 2:
+            k = int(rng.integers(1, 4)); ops.append('{}I'.format(k)); left -= k
+        elif lead == 3:
+            k = int(rng.integers(1, 6)); ops.append('{}S'.format(k)); left -= k
+        while left > 0:
+            k = int(min(left, rng.integers(4, 20)))
+            ops.append('{}M'.format(k)); left -= k
+            if left > 6 and rng.random() < 0.3:
+                if rng.random() < 0.5:
+                    ops.append('{}D'.format(int(rng.integers(1, 4))))
                 else:
-                    ids.append(len(rows))
-                    rows.append(r)
-            units += ids
-        flag = [int(r[1]) for r in rows]
-        ref = [ref_names.index(r[2]) for r in rows]
-        pos = [int(r[3]) for r in rows]
-        cig, cig_off, n_cig = [], [], []
-        for r, f in zip(rows, flag):
-            ops = oracle.parse_cigar(r[5]) if not (f & 4) else []
-            cig_off.append(len(cig))
-            n_cig.append(len(ops))
-            cig += ops
-        seq = ''.join(r[9] for r in rows).encode()
-        qual = ''.join(r[10][:len(r[9])].ljust(len(r[9]), 'J') for r in rows).encode()
-        lens = [len(r[9]) for r in rows]
-        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]) if rows else []
-        ctx.rows_load(flag, ref, pos, cig_off, n_cig, cig or [0], np.frombuffer(seq, np.uint8),
-                      np.frombuffer(qual, np.uint8), offs, lens, units)
-        cap_lens = [max([int(r[3]) + len(r[9]) for p in pairs for r in p if r] + [8])
-                    for _ in ref_names]
-        got_refmap, got_counts = _gpu_pileup_as_refmap(ctx, ref_names, cap_lens,
-                                                       c['quality_cutoff'], source=1)
-        assert list(got_refmap) == list(want_refmap)
-        assert got_counts == want_counts
-        for name in want_refmap:
-            assert got_refmap[name][0] == want_refmap[name][0], (name, c['sam'][:200])
+                    k = int(rng.integers(1, 4)); ops.append('{}I'.format(k)); left -= k
+        return ''.join(ops)
+
+    for p in range(n_pairs):
+        for mate, flag in ((1, 99), (2, 147)):
+            m = int(rng.integers(20, 60))
+            seq = ''.join(rng.choice(list('ACGTN'), p=[0.24, 0.24, 0.24, 0.24, 0.04], size=m))
+            qual = ''.join(rng.choice(list(quals), size=m))
+            pos = int(rng.integers(1, ref_len - 80))
+            lines.append('\t'.join(['q{}'.format(p), str(flag), 'r1', str(pos), '44', cigar(m), '=',
+                                    '1', '0', seq, qual]) + '\n')
+    return ''.join(lines)
+
+
+@pytest.mark.parametrize('q', [0, 20])
+def test_pileup_rows_leading_gaps_vs_oracle(ctx, q):
+    """Rows whose CIGARs start with D / I / S (the merge start found by the
+    scan, not from the pads) against the oracle pileup."""
+    rng = np.random.default_rng(41 + q)
+    _rows_case_vs_oracle(ctx, _random_cigar_sam(rng, 300), q)
+
+
+def _rows_case_vs_oracle(ctx, sam, quality_cutoff):
+    """One SAM text through source 1 (rows) against the oracle pileup."""
+    ref_names, pairs = oracle.matchmaker(sam.splitlines(True))
+    want_refmap, want_counts = oracle.pileup(ref_names, pairs, quality_cutoff)
+    rows, units = [], []
+    for r1, r2 in pairs:
+        ids = []
+        for r in (r1, r2):
+            if r is None:
+                ids.append(-1)
+            else:
+                ids.append(len(rows))
+                rows.append(r)
+        units += ids
+    flag = [int(r[1]) for r in rows]
+    ref = [ref_names.index(r[2]) for r in rows]
+    pos = [int(r[3]) for r in rows]
+    cig, cig_off, n_cig = [], [], []
+    for r, f in zip(rows, flag):
+        ops = oracle.parse_cigar(r[5]) if not (f & 4) else []
+        cig_off.append(len(cig))
+        n_cig.append(len(ops))
+        cig += ops
+    seq = ''.join(r[9] for r in rows).encode()
+    qual = ''.join(r[10][:len(r[9])].ljust(len(r[9]), 'J') for r in rows).encode()
+    lens = [len(r[9]) for r in rows]
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]) if rows else []
+    ctx.rows_load(flag, ref, pos, cig_off, n_cig, cig or [0], np.frombuffer(seq, np.uint8),
+                  np.frombuffer(qual, np.uint8), offs, lens, units)
+    # reference span of a row <= read length + its deletions
+    dels = [sum(int(n) for n, op in re.findall(r'(\d+)([MIDNS])', r[5]) if op == 'D') for r in rows]
+    span = {id(r): len(r[9]) + d for r, d in zip(rows, dels)}
+    cap_lens = [max([int(r[3]) + span[id(r)] for p in pairs for r in p if r] + [8])
+                for _ in ref_names]
+    got_refmap, got_counts = _gpu_pileup_as_refmap(ctx, ref_names, cap_lens, quality_cutoff,
+                                                   source=1)
+    assert list(got_refmap) == list(want_refmap)
+    assert got_counts == want_counts
+    for name in want_refmap:
+        assert got_refmap[name][0] == want_refmap[name][0], (name, sam[:200])
 
 
 def test_gotoh_vs_golden(ctx, golden_dir):
