@@ -798,13 +798,13 @@ int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mappe
     if (!M.valid) { set_error("no mapping results (call mh_map)"); return -3; }
     MH_HIP(hipSetDevice(c->device));
     const int n = M.n_refs;
-    std::vector<int64_t> s(5 * n + 3);
-    MH_HIP(hipMemcpy(s.data(), M.ref_stats, sizeof(int64_t) * s.size(), hipMemcpyDeviceToHost));
-    if (lines) std::memcpy(lines, s.data(), sizeof(int64_t) * n);
-    if (filtered) std::memcpy(filtered, s.data() + n, sizeof(int64_t) * n);
-    if (mapped) std::memcpy(mapped, s.data() + 2 * n, sizeof(int64_t) * n);
-    if (first_row) std::memcpy(first_row, s.data() + 3 * n, sizeof(int64_t) * n);
-    if (first_mapped) std::memcpy(first_mapped, s.data() + 4 * n, sizeof(int64_t) * n);
+    const int64_t *s = map_stats_host(*c);
+    if (!s) return -1;
+    if (lines) std::memcpy(lines, s, sizeof(int64_t) * n);
+    if (filtered) std::memcpy(filtered, s + n, sizeof(int64_t) * n);
+    if (mapped) std::memcpy(mapped, s + 2 * n, sizeof(int64_t) * n);
+    if (first_row) std::memcpy(first_row, s + 3 * n, sizeof(int64_t) * n);
+    if (first_mapped) std::memcpy(first_mapped, s + 4 * n, sizeof(int64_t) * n);
     if (unmapped) *unmapped = s[5 * n];
     if (star_lines) *star_lines = s[5 * n + 1];
     if (star_first) *star_first = s[5 * n + 2];

@@ -123,6 +123,10 @@ struct MapState {
     int64_t last_fast = 0;       // extensions resolved by the ungapped fast path
     int64_t last_rescue = 0;     // mate-rescue extensions
     bool valid = false;
+    // host copy of ref_stats (5 * n_refs + 3), filled on first use after a
+    // mapping pass: mh_map_counts and the pileup's window choice share it
+    std::vector<int64_t> stats_host;
+    bool stats_host_valid = false;
 };
 
 // External SAM rows for the pileup (prelim.csv read back).
@@ -181,6 +185,9 @@ struct PileState {
 hipError_t launch_pack_reads(DevReads &r, const uint8_t *d_seq, const uint8_t *d_qual,
                              const int64_t *d_src_off, hipStream_t s);
 int run_map(struct Ctx &c, const mh_params &par);
+// the per-reference tallies of the last mapping pass on the host (one copy
+// per pass); nullptr on a copy error
+const int64_t *map_stats_host(struct Ctx &c);
 int run_pileup(struct Ctx &c, int source, int q_cutoff);
 // distinct (ref, pos, token) keys of the last pileup's events with their
 // counts, aggregated on the device; tokens concatenated in `bytes` at `off`

@@ -1966,8 +1966,25 @@ __global__ void k_fix_first(int64_t *s, int n_refs)
     if (blockIdx.x == 0 && threadIdx.x == 0 && s[5 * n_refs + 2] == INT64_MAX) s[5 * n_refs + 2] = -1;
 }
 
+const int64_t *map_stats_host(Ctx &c)
+{
+    MapState &M = c.map;
+    if (!M.stats_host_valid) {
+        M.stats_host.resize(5 * (size_t)M.n_refs + 3);
+        if (hipMemcpyAsync(M.stats_host.data(), M.ref_stats, sizeof(int64_t) * M.stats_host.size(),
+                           hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
+            hipStreamSynchronize(c.stream) != hipSuccess) {
+            set_error("map_stats_host: copy failed");
+            return nullptr;
+        }
+        M.stats_host_valid = true;
+    }
+    return M.stats_host.data();
+}
+
 int run_map(Ctx &c, const mh_params &par)
 {
+    c.map.stats_host_valid = false;
     if (c.index.n_refs <= 0 || c.index.hkey == nullptr) {
         set_error("mh_map: no reference index (call mh_index_build first)");
         return -3;

@@ -803,8 +803,8 @@ static int pile_geometry(Ctx &c, int source, int64_t n_units, PileGeometry &g)
     if (source == 0) {
         span = c.reads.max_len + BAND;   // M + D <= read length + band width
         const int n = c.map.n_refs;
-        std::vector<int64_t> st(5 * (size_t)n + 3);
-        MH_HIP(hipMemcpy(st.data(), c.map.ref_stats, sizeof(int64_t) * st.size(), hipMemcpyDeviceToHost));
+        const int64_t *st = map_stats_host(c);
+        if (!st) return -1;
         for (int r = 0; r < n && r < NR; ++r) hits[(size_t)r] = st[2 * (size_t)n + r];
     } else {
         span = c.rows.max_span;
