@@ -344,7 +344,16 @@ class Context:
 
     # ---- reference set --------------------------------------------------
     def index_build(self, names, seqs, seedlen):
-        arr = (ctypes.c_char_p * max(len(seqs), 1))(*[s.encode() for s in seqs])
+        seqs = list(seqs)
+        # the same str objects again (the seed set of every prelim pass): reuse
+        # their encoded buffers; the cache holds the objects, so ids stay theirs
+        cached = getattr(self, '_index_enc', None)
+        if cached is not None and len(cached[0]) == len(seqs) and all(
+                a is b for a, b in zip(cached[0], seqs)):
+            arr = cached[1]
+        else:
+            arr = (ctypes.c_char_p * max(len(seqs), 1))(*[s.encode() for s in seqs])
+            self._index_enc = (seqs, arr)
         check(lib().mh_index_build(self.h, len(seqs), arr, seedlen), 'mh_index_build')
         self.refnames = list(names)
         self.reflens = [len(s) for s in seqs]
