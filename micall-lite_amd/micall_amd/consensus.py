@@ -103,9 +103,14 @@ class Pileup:
         d, nf, df = self._slice(r, length)
         tok = np.zeros(length, dtype=np.uint8)
         if length:
-            positive = d.max(axis=1) > 0
+            # column-wise: numpy's reductions over a 4-wide axis cost a
+            # per-row overhead (0.13 ms for 3 kb)
+            c0, c1, c2, c3 = d[:, 0], d[:, 1], d[:, 2], d[:, 3]
+            top = np.maximum(np.maximum(c0, c1), np.maximum(c2, c3))
+            positive = top > 0
             # a positive count wins; ties go to the first of A<C<G<T
-            tok[positive] = BASE_CODES[d.argmax(axis=1)[positive]]
+            first = np.where(c0 == top, 0, np.where(c1 == top, 1, np.where(c2 == top, 2, 3)))
+            tok[positive] = BASE_CODES[first[positive]]
             # otherwise: seed prefill (0) > 'N' (-1) > '-' (-2) > nothing
             fill = np.zeros(length, dtype=np.uint8)
             fill[df] = DASH
@@ -115,9 +120,27 @@ class Pileup:
                 fill[:k] = np.frombuffer(seed[:k].encode('latin-1'), dtype=np.uint8)
             tok[~positive] = fill[~positive]
         longer = {}
-        for pos in self.events.get(r, {}):
-            if pos <= length:
-                t = find_top_token(self.counter_at(r, pos, seed))
+        ev = self.events.get(r, {})
+        positions = [pos for pos in ev if pos <= length]
+        if positions:
+            # the counter rows of every position with tokens in one gather
+            # (counter_at's Counter, built from plain lists)
+            idx = np.asarray(positions, dtype=np.int64) - 1
+            rows, nfs, dfs = d[idx].tolist(), nf[idx].tolist(), df[idx].tolist()
+            nseed = len(seed) if seed else 0
+            for pos, row, n_flag, d_flag in zip(positions, rows, nfs, dfs):
+                c = {seed[pos - 1]: 0} if pos <= nseed else {}   # a plain dict: Counter's
+                for k, v in enumerate(row):                     # update is slow Python
+                    if v:
+                        base = 'ACGT'[k]
+                        c[base] = c.get(base, 0) + v
+                if n_flag:
+                    c['N'] = -1
+                if d_flag:
+                    c['-'] = -2
+                for token, count in ev[pos].items():
+                    c[token] = c.get(token, 0) + count
+                t = find_top_token(c)
                 tok[pos - 1] = ord(t[0]) if t else 0
                 if t and len(t) > 1:
                     longer[pos - 1] = t
@@ -126,7 +149,7 @@ class Pileup:
     def position_sums(self, r, seed, length):
         """sum(counts[pos].values()) for pos 1..length (remap.py:236-238)."""
         d, nf, df = self._slice(r, length)
-        s = d.sum(axis=1) - nf.astype(np.int64) - 2 * df.astype(np.int64)
+        s = d[:, 0] + d[:, 1] + d[:, 2] + d[:, 3] - nf.astype(np.int64) - 2 * df.astype(np.int64)
         for pos, c in self.events.get(r, {}).items():
             if pos <= length:
                 s[pos - 1] += sum(c.values())
