@@ -1947,7 +1947,9 @@ static int ensure_map_buffers(Ctx &c)
         M.cap_refs = cr;
     }
     if (M.pool == nullptr) {
-        M.pool_cap = (n > 0 ? n : 1) * 8 + 4096 + (int64_t)DP_MAX_BLOCKS * 4 * POOL_CHUNK;
+        // the ops themselves plus every wave's partly used chunk, for both
+        // k_dp launches of a pass (main and mate rescue share the pool)
+        M.pool_cap = (n > 0 ? n : 1) * 8 + 4096 + 2 * (int64_t)DP_MAX_BLOCKS * DP_WAVES_PER_BLOCK * POOL_CHUNK;
         MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * M.pool_cap));
     }
     return 0;
@@ -2006,17 +2008,21 @@ int run_map(Ctx &c, const mh_params &par)
     M.n_refs = c.index.n_refs;
     M.par = par;
     hipStream_t s = c.stream;
-    MH_HIP(hipMemsetAsync(M.counters, 0, sizeof(int32_t) * 4, s));
     M.last_work = M.last_cigar = 0;
     hipLaunchKernelGGL(k_init_stats, dim3(64), dim3(256), 0, s, M.ref_stats, M.n_refs);
     if (n > 0) {
-        SeedArgs sa{c.reads, c.index, par.mode, c.len_tab, M.cand, M.n_cand, M.yf, M.work, M.counters};
-        int64_t blocks = ((n + SEED_CHUNK - 1) / SEED_CHUNK + 3) / 4;
-        if (blocks > 1 << 16) blocks = 1 << 16;
-        const int pk = prof_begin(c, "k_seed");
-        hipLaunchKernelGGL(k_seed, dim3((unsigned)blocks), dim3(256), 0, s, sa);
-        prof_end(c, pk);
-        MH_HIP(hipGetLastError());
+        // seeds, candidates and the work list; run again by a retry, since
+        // k_rescue replaces the candidates of the mates it rescues
+        auto launch_seed = [&]() -> int {
+            SeedArgs sa{c.reads, c.index, par.mode, c.len_tab, M.cand, M.n_cand, M.yf, M.work, M.counters};
+            int64_t blocks = ((n + SEED_CHUNK - 1) / SEED_CHUNK + 3) / 4;
+            if (blocks > 1 << 16) blocks = 1 << 16;
+            const int pk = prof_begin(c, "k_seed");
+            hipLaunchKernelGGL(k_seed, dim3((unsigned)blocks), dim3(256), 0, s, sa);
+            prof_end(c, pk);
+            MH_HIP(hipGetLastError());
+            return 0;
+        };
 
         const int rows_pad = ((c.reads.max_len + 7) / 8) * 8;
         // traceback bits 32 B per row, then the tables of the wave's two extensions
@@ -2053,7 +2059,8 @@ int run_map(Ctx &c, const mh_params &par)
         for (int attempt = 0; attempt < 2; ++attempt) {
             // counters: [0] work items, [1] pool used, [2] overflow, [3] fast path,
             // [4] rescue work items
-            MH_HIP(hipMemsetAsync(M.counters + 1, 0, sizeof(int32_t) * 4, s));
+            MH_HIP(hipMemsetAsync(M.counters, 0, sizeof(int32_t) * 5, s));
+            if (int st = launch_seed()) return st;
             if (int st = launch_dp(M.work, M.counters, n * 2, "k_dp")) return st;
             if (c.reads.paired && units > 0) {
                 RescueArgs ra{c.reads, c.index, M.slot, M.n_cand, M.yf, M.cand, M.rwork,
@@ -2074,11 +2081,11 @@ int run_map(Ctx &c, const mh_params &par)
             M.last_cigar = ctr[1];
             M.last_fast = ctr[3];
             if (!ctr[2]) break;
-            // CIGAR pool overflow: grow to what was asked for and redo the extensions
-            // (the rescue's candidates are the only ones of their mates, so the
-            // second attempt reaches the same result)
+            // CIGAR pool overflow: grow to what was asked for and redo the pass
+            // from the seeds (k_rescue rewrote the candidates of the mates it
+            // rescued, and their slots point into the pool being replaced)
             hipFree(M.pool);
-            M.pool_cap = (int64_t)ctr[1] * 2 + 4096 + (int64_t)DP_MAX_BLOCKS * 4 * POOL_CHUNK;
+            M.pool_cap = (int64_t)ctr[1] * 2 + 4096 + 2 * (int64_t)DP_MAX_BLOCKS * DP_WAVES_PER_BLOCK * POOL_CHUNK;
             MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * M.pool_cap));
             if (attempt == 1) { set_error("mh_map: CIGAR pool overflow"); return -2; }
         }
