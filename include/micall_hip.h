@@ -122,11 +122,24 @@ int mh_map_counts(mh_ctx *ctx, int64_t *lines, int64_t *filtered, int64_t *mappe
                   int64_t *first_row, int64_t *first_mapped, int64_t *unmapped,
                   int64_t *star_lines, int64_t *star_first);
 /* Work done by the last mh_map: out[0] reads, out[1] banded extensions
- * (candidates aligned by the DP, 64 diagonals x read length cells each,
+ * (candidates aligned by the DP, up to 31 diagonals x read length cells each,
  * mate rescues included), out[2] CIGAR pool words reserved (per-wave
  * chunks), out[3] extensions resolved by the ungapped fast path (no DP),
  * out[4] mate-rescue extensions. */
 int mh_map_stats(mh_ctx *ctx, int64_t *out5);
+/* Test entry point (not a tuning knob): start the grow-and-retry buffers of
+ * every later call at these capacities (0 = the library's own sizing):
+ * the CIGAR pool of mh_map (uint32 words), the pileup's insertion-token
+ * events and their bytes (mh_pileup), the distinct-token bytes of the token
+ * aggregation (mh_pileup_events, mh_pileup_fetch).  A pass that needs more
+ * takes the retry path, which the parity tests then check bit for bit.  The
+ * call drops the buffers (and the last pass's records) so the next call
+ * sizes them again. */
+int mh_test_set_capacities(mh_ctx *ctx, int64_t cigar_pool_words, int64_t pileup_events,
+                           int64_t pileup_event_bytes, int64_t token_bytes);
+/* Retries taken so far by those paths: out3[0] CIGAR pool (a mapping pass
+ * run again from k_seed), out3[1] pileup events, out3[2] token bytes. */
+int mh_retry_counts(mh_ctx *ctx, int64_t *out3);
 /* The 20 int32 header fields of mh_aln (no CIGAR) for reads [first, first+n). */
 int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20);
 /* SAM text for reads order[first .. first+n) (order NULL: reads first ..

@@ -965,7 +965,7 @@ extern "C" int mh_a2c_inserts(mh_ctx *ctx, int slot, int64_t g, int frame, int n
         goto done;
     }
     ent.resize(ctr[2]);
-    e = hipMemcpy(ent.data(), d_ent, sizeof(A2CEntry) * ent.size(), hipMemcpyDeviceToHost);
+    e = copy_sync(c, ent.data(), d_ent, sizeof(A2CEntry) * ent.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) { fail(e, "mh_a2c_inserts fetch"); goto done; }
     // InsertionWriter order: ranges in order, then Counter insertion order
     std::sort(ent.begin(), ent.end(), [](const A2CEntry &x, const A2CEntry &y) {

@@ -46,6 +46,12 @@ int hip_fail(hipError_t e, const char *what)
     return -4;
 }
 
+hipError_t copy_sync(Ctx &c, void *dst, const void *src, size_t bytes, hipMemcpyKind kind)
+{
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, c.stream);
+    return e == hipSuccess ? hipStreamSynchronize(c.stream) : e;
+}
+
 int prof_begin(Ctx &c, const char *name)
 {
     if (!c.prof) return -1;
@@ -134,7 +140,7 @@ static int prepare_len_tab(Ctx &c, const mh_params &par)
         t[3 * (MAXLEN + 1) + l] = band_half(par, l);
     }
     if (!c.len_tab) MH_HIP(hipMalloc(&c.len_tab, sizeof(int32_t) * t.size()));
-    MH_HIP(hipMemcpy(c.len_tab, t.data(), sizeof(int32_t) * t.size(), hipMemcpyHostToDevice));
+    MH_HIP(copy_sync(c, c.len_tab, t.data(), sizeof(int32_t) * t.size(), hipMemcpyHostToDevice));
     c.len_tab_key = len_tab_key(par);
     return 0;
 }
@@ -300,6 +306,7 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     ix.hstart = (uint32_t *)(d + at[4]);
     ix.hcount = (uint32_t *)(d + at[5]);
     ix.hits = (int2 *)(d + at[6]);
+    // callers synchronise the context stream first (mh_index_build)
     MH_HIP(hipMemcpy(ix.blob, stage.data(), total, hipMemcpyHostToDevice));
     return 0;
 }
@@ -564,7 +571,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     free_index(c->small);
     MapState &M = c->map;
     hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work); hipFree(M.rwork); hipFree(M.slot);
-    hipFree(M.pool); hipFree(M.rec); hipFree(M.counters); hipFree(M.ref_stats);
+    hipFree(M.pool); hipFree(M.pool_used); hipFree(M.rec); hipFree(M.counters); hipFree(M.ref_stats);
     RowState &R = c->rows;
     hipFree(R.flag); hipFree(R.ref); hipFree(R.pos); hipFree(R.cig_off); hipFree(R.n_cigar);
     hipFree(R.cigar); hipFree(R.units);
@@ -779,12 +786,13 @@ static int fetch_recs(CtxEx *c, int64_t first, int64_t n, std::vector<Rec> &rec,
     if (first < 0 || n < 0 || first + n > M.n_reads) { set_error("record range out of bounds"); return -3; }
     rec.resize(n > 0 ? n : 1);
     if (n > 0)
-        MH_HIP(hipMemcpy(rec.data(), M.rec + first, sizeof(Rec) * n, hipMemcpyDeviceToHost));
-    int32_t used = 0;
-    MH_HIP(hipMemcpy(&used, M.counters + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+        MH_HIP(copy_sync(*c, rec.data(), M.rec + first, sizeof(Rec) * n, hipMemcpyDeviceToHost));
+    // the words claimed by the last pass (its chunks end within the pool:
+    // a pass that overflowed was run again with a larger one)
+    int64_t used = M.last_cigar < M.pool_cap ? M.last_cigar : M.pool_cap;
     pool.resize(used > 0 ? used : 1);
     if (used > 0)
-        MH_HIP(hipMemcpy(pool.data(), M.pool, sizeof(uint32_t) * used, hipMemcpyDeviceToHost));
+        MH_HIP(copy_sync(*c, pool.data(), M.pool, sizeof(uint32_t) * used, hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -844,6 +852,39 @@ int mh_map_stats(mh_ctx *ctx, int64_t *out5)
     return 0;
 }
 
+int mh_test_set_capacities(mh_ctx *ctx, int64_t cigar_pool_words, int64_t pileup_events,
+                           int64_t pileup_event_bytes, int64_t token_bytes)
+{
+    if (!ctx || cigar_pool_words < 0 || pileup_events < 0 || pileup_event_bytes < 0 || token_bytes < 0) {
+        set_error("mh_test_set_capacities: bad arguments");
+        return -3;
+    }
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    MH_HIP(hipStreamSynchronize(c->stream));
+    // the next call sizes every one of these buffers again
+    MapState &M = c->map;
+    PileState &P = c->pile;
+    hipFree(M.pool); M.pool = nullptr; M.pool_cap = 0;
+    hipFree(P.ev); P.ev = nullptr; P.ev_cap = 0;
+    hipFree(P.ev_pool); P.ev_pool = nullptr; P.pool_cap = 0;
+    hipFree(P.tok_bytes); P.tok_bytes = nullptr; P.tok_bytes_cap = 0;
+    M.valid = false;   // the records of the last pass pointed into the pool
+    TestCaps &t = c->test_caps;
+    t.cigar_pool_words = cigar_pool_words;
+    t.pile_events = pileup_events;
+    t.pile_event_bytes = pileup_event_bytes;
+    t.token_bytes = token_bytes;
+    return 0;
+}
+
+int mh_retry_counts(mh_ctx *ctx, int64_t *out3)
+{
+    if (!ctx || !out3) return -3;
+    for (int k = 0; k < RETRY_KINDS; ++k) out3[k] = X(ctx)->retries[k];
+    return 0;
+}
+
 int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20)
 {
     if (!ctx || (n > 0 && !out20)) return -3;
@@ -854,8 +895,9 @@ int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20)
     MH_HIP(hipSetDevice(c->device));
     if (n == 0) return 0;
     // Rec is 22 int32; copy with a 2D memcpy that keeps the first 20 of each
-    MH_HIP(hipMemcpy2D(out20, sizeof(int32_t) * 20, M.rec + first, sizeof(Rec), sizeof(int32_t) * 20,
-                       (size_t)n, hipMemcpyDeviceToHost));
+    MH_HIP(hipMemcpy2DAsync(out20, sizeof(int32_t) * 20, M.rec + first, sizeof(Rec), sizeof(int32_t) * 20,
+                            (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    MH_HIP(hipStreamSynchronize(c->stream));
     return 0;
 }
 
@@ -1096,15 +1138,15 @@ int mh_rows_load(mh_ctx *ctx, int64_t n_rows, const int32_t *flag, const int32_t
     MH_HIP(hipMalloc(&R.cigar, sizeof(uint32_t) * (ncig > 0 ? ncig : 1)));
     MH_HIP(hipMalloc(&R.units, sizeof(int64_t) * 2 * (n_units > 0 ? n_units : 1)));
     if (n_rows > 0) {
-        MH_HIP(hipMemcpy(R.flag, flag, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
-        MH_HIP(hipMemcpy(R.ref, ref, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
-        MH_HIP(hipMemcpy(R.pos, pos, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
-        MH_HIP(hipMemcpy(R.cig_off, cigar_off, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
-        MH_HIP(hipMemcpy(R.n_cigar, n_cigar, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
+        MH_HIP(copy_sync(*c, R.flag, flag, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
+        MH_HIP(copy_sync(*c, R.ref, ref, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
+        MH_HIP(copy_sync(*c, R.pos, pos, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
+        MH_HIP(copy_sync(*c, R.cig_off, cigar_off, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
+        MH_HIP(copy_sync(*c, R.n_cigar, n_cigar, sizeof(int32_t) * n_rows, hipMemcpyHostToDevice));
     }
-    if (ncig > 0) MH_HIP(hipMemcpy(R.cigar, cigar, sizeof(uint32_t) * ncig, hipMemcpyHostToDevice));
+    if (ncig > 0) MH_HIP(copy_sync(*c, R.cigar, cigar, sizeof(uint32_t) * ncig, hipMemcpyHostToDevice));
     if (n_units > 0)
-        MH_HIP(hipMemcpy(R.units, unit_rows, sizeof(int64_t) * 2 * n_units, hipMemcpyHostToDevice));
+        MH_HIP(copy_sync(*c, R.units, unit_rows, sizeof(int64_t) * 2 * n_units, hipMemcpyHostToDevice));
     R.n_rows = n_rows;
     R.n_units = n_units;
     HostReads dummy;
@@ -1491,7 +1533,7 @@ static int aggregate_tokens(CtxEx &c)
     c.tok_ref.clear(); c.tok_pos.clear(); c.tok_off.clear(); c.tok_len.clear();
     c.tok_count.clear(); c.tok_pool.clear();
     int64_t ctr[4] = {0, 0, 0, 0};
-    if (P.ev_counters) MH_HIP(hipMemcpy(ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
+    if (P.ev_counters) MH_HIP(copy_sync(c, ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
     const int64_t ne = ctr[0];
     if (ne > 0) {
         // distinct (ref, pos, token) keys and their counts come from the
@@ -1555,7 +1597,7 @@ static int fetch_parts(CtxEx &c, const FetchPart *parts, int n)
     if (total > ((size_t)64 << 20)) {   // large fetches (all 74 seeds): plain copies
         for (int i = 0; i < n; ++i)
             if (parts[i].dst && parts[i].bytes)
-                MH_HIP(hipMemcpy(parts[i].dst, parts[i].src, parts[i].bytes, hipMemcpyDeviceToHost));
+                MH_HIP(copy_sync(c, parts[i].dst, parts[i].src, parts[i].bytes, hipMemcpyDeviceToHost));
         return 0;
     }
     if (c.pin_cap < total) {

@@ -113,8 +113,9 @@ struct MapState {
     Slot *slot = nullptr;        // n_reads * MAXCAND
     uint32_t *pool = nullptr;    // CIGAR ops of all slots
     int64_t pool_cap = 0;
+    unsigned long long *pool_used = nullptr;  // words claimed (demand; may exceed pool_cap)
     Rec *rec = nullptr;          // n_reads
-    int32_t *counters = nullptr; // [work_n, pool_used, pool_overflow, fast, rescue_n, pad..]
+    int32_t *counters = nullptr; // [work_n, unused, pool_overflow, fast, rescue_n, pad..]
     int64_t *ref_stats = nullptr;// per ref: lines, filtered, mapped, first_row, first_mapped; + unmapped, star
     int64_t cap_reads = 0;
     int cap_refs = 0;
@@ -215,8 +216,24 @@ struct S2AState;      // mh_sam2aln.h
 struct CensorState;   // mh_censor.hip
 struct A2CState;      // mh_a2c.hip
 
+// Capacities a test can impose on the grow-and-retry buffers
+// (mh_test_set_capacities); 0 keeps the library's own sizing.  Each call that
+// sizes one of these buffers starts it at the imposed capacity, so every pass
+// that needs more goes through the retry.
+struct TestCaps {
+    int64_t cigar_pool_words = 0;   // MapState::pool
+    int64_t pile_events = 0;        // PileState::ev
+    int64_t pile_event_bytes = 0;   // PileState::ev_pool
+    int64_t token_bytes = 0;        // PileState::tok_bytes
+};
+
+// retries taken by the grow-and-retry paths (mh_retry_counts)
+enum { RETRY_CIGAR_POOL = 0, RETRY_PILE_EVENTS = 1, RETRY_TOKEN_BYTES = 2, RETRY_KINDS = 3 };
+
 struct Ctx {
     int device = 0;
+    TestCaps test_caps;
+    int64_t retries[RETRY_KINDS] = {0, 0, 0};
     int n_cu = 0;                    // compute units of the device (launch sizing)
     // per-kernel timing with HIP events on `stream` (mh_profile)
     bool prof = false;
@@ -256,6 +273,9 @@ int prof_begin(Ctx &c, const char *name);
 void prof_end(Ctx &c, int slot);
 void prof_flush(Ctx &c);   // after a stream sync: fold pending events
 int hip_fail(hipError_t e, const char *what);
+// a blocking copy ordered on c.stream: the stream is non-blocking, so a plain
+// hipMemcpy (legacy null stream) is not ordered after its kernels
+hipError_t copy_sync(Ctx &c, void *dst, const void *src, size_t bytes, hipMemcpyKind kind);
 
 }  // namespace mh
 

@@ -528,7 +528,8 @@ struct DpArgs {
     const int32_t *counters;  // [0] = number of work items
     Slot *slot;
     uint32_t *pool;
-    int32_t *pool_ctr;        // [0] used, [1] overflow
+    unsigned long long *pool_used;  // words claimed so far (64-bit: never wraps)
+    int32_t *pool_ctr;        // [1] overflow, [2] fast-path extensions
     int64_t pool_cap;
     int rows_pad;             // per-wave LDS row capacity (multiple of 8)
     int wave_lds;             // bytes of LDS per wave
@@ -1301,7 +1302,7 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
             const int nc = (clipL > 0) + (clipR > 0) + (lo - hi + 1);
             if (nc <= MH_MAXOPS - 1) {
                 if (nc > ck_left) {   // next wave-private chunk of the pool
-                    ck_base = atomicAdd(&A.pool_ctr[0], POOL_CHUNK);
+                    ck_base = (int64_t)atomicAdd(A.pool_used, (unsigned long long)POOL_CHUNK);
                     ck_left = POOL_CHUNK;
                 }
                 const int64_t base = ck_base;
@@ -1922,6 +1923,12 @@ __global__ __launch_bounds__(256) void k_pair(PairArgs A)
 // ---------------------------------------------------------------------------
 // host driver of one mapping pass
 // ---------------------------------------------------------------------------
+// CIGAR pool words for a pass over n reads (or what a retry found demanded)
+static int64_t pool_words_for(int64_t n)
+{
+    return (n > 0 ? n : 1) * 8 + 4096 + 2 * (int64_t)DP_MAX_BLOCKS * DP_WAVES_PER_BLOCK * POOL_CHUNK;
+}
+
 static int ensure_map_buffers(Ctx &c)
 {
     MapState &M = c.map;
@@ -1946,11 +1953,19 @@ static int ensure_map_buffers(Ctx &c)
         MH_HIP(hipMalloc(&M.ref_stats, sizeof(int64_t) * (5 * cr + 3)));
         M.cap_refs = cr;
     }
-    if (M.pool == nullptr) {
-        // the ops themselves plus every wave's partly used chunk, for both
-        // k_dp launches of a pass (main and mate rescue share the pool)
-        M.pool_cap = (n > 0 ? n : 1) * 8 + 4096 + 2 * (int64_t)DP_MAX_BLOCKS * DP_WAVES_PER_BLOCK * POOL_CHUNK;
-        MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * M.pool_cap));
+    if (M.pool_used == nullptr) MH_HIP(hipMalloc(&M.pool_used, sizeof(unsigned long long)));
+    // the ops themselves plus every wave's partly used chunk, for both k_dp
+    // launches of a pass (main and mate rescue share the pool); grown when a
+    // later pass has more reads than the one that sized it.  A capacity
+    // imposed by a test is where every pass starts.
+    const int64_t test_cap = c.test_caps.cigar_pool_words;
+    const int64_t need = test_cap > 0 ? test_cap : pool_words_for(n);
+    if (M.pool == nullptr || (test_cap > 0 ? M.pool_cap != need : M.pool_cap < need)) {
+        hipFree(M.pool);
+        M.pool = nullptr;
+        M.pool_cap = 0;
+        MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * need));
+        M.pool_cap = need;
     }
     return 0;
 }
@@ -2035,7 +2050,7 @@ int run_map(Ctx &c, const mh_params &par)
         auto launch_dp = [&](const int32_t *work, const int32_t *count, int64_t max_items,
                              const char *name) -> int {
             DpArgs da{c.reads, c.index, c.len_tab, M.cand, work, count, M.slot, M.pool,
-                      M.counters + 1, M.pool_cap, rows_pad, wave_lds,
+                      M.pool_used, M.counters + 1, M.pool_cap, rows_pad, wave_lds,
                       par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext,
                       par.rdg_ext};
             int64_t dblocks = (max_items + wpb - 1) / wpb;
@@ -2057,9 +2072,10 @@ int run_map(Ctx &c, const mh_params &par)
         };
         const int64_t units = c.reads.paired ? n / 2 : n;
         for (int attempt = 0; attempt < 2; ++attempt) {
-            // counters: [0] work items, [1] pool used, [2] overflow, [3] fast path,
-            // [4] rescue work items
+            // counters: [0] work items, [2] pool overflow, [3] fast path,
+            // [4] rescue work items; pool_used: CIGAR words claimed
             MH_HIP(hipMemsetAsync(M.counters, 0, sizeof(int32_t) * 5, s));
+            MH_HIP(hipMemsetAsync(M.pool_used, 0, sizeof(unsigned long long), s));
             if (int st = launch_seed()) return st;
             if (int st = launch_dp(M.work, M.counters, n * 2, "k_dp")) return st;
             if (c.reads.paired && units > 0) {
@@ -2074,20 +2090,26 @@ int run_map(Ctx &c, const mh_params &par)
                 if (int st = launch_dp(M.rwork, M.counters + 4, units, "k_dp_rescue")) return st;
             }
             int32_t ctr[5];
+            unsigned long long used = 0;
             MH_HIP(hipMemcpyAsync(ctr, M.counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
+            MH_HIP(hipMemcpyAsync(&used, M.pool_used, sizeof(used), hipMemcpyDeviceToHost, s));
             MH_HIP(hipStreamSynchronize(s));
             M.last_work = ctr[0] + ctr[4];
             M.last_rescue = ctr[4];
-            M.last_cigar = ctr[1];
+            M.last_cigar = (int64_t)used;
             M.last_fast = ctr[3];
             if (!ctr[2]) break;
+            if (attempt == 1) { set_error("mh_map: CIGAR pool overflow after a retry"); return -2; }
             // CIGAR pool overflow: grow to what was asked for and redo the pass
             // from the seeds (k_rescue rewrote the candidates of the mates it
             // rescued, and their slots point into the pool being replaced)
+            ++c.retries[RETRY_CIGAR_POOL];
             hipFree(M.pool);
-            M.pool_cap = (int64_t)ctr[1] * 2 + 4096 + 2 * (int64_t)DP_MAX_BLOCKS * DP_WAVES_PER_BLOCK * POOL_CHUNK;
-            MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * M.pool_cap));
-            if (attempt == 1) { set_error("mh_map: CIGAR pool overflow"); return -2; }
+            M.pool = nullptr;
+            M.pool_cap = 0;
+            const int64_t grown = (int64_t)used * 2 + pool_words_for(0);
+            MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * grown));
+            M.pool_cap = grown;
         }
         PairArgs pa{c.reads, c.len_tab, M.slot, M.n_cand, M.yf, M.pool, M.rec, M.ref_stats,
                     M.n_refs, par.mode == MH_LOCAL, par.maxins, c.reads.paired};

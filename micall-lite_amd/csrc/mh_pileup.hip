@@ -768,10 +768,19 @@ static int ensure_pile(Ctx &c)
         P.alloc_refs = nr;
     }
     if (!P.ev_counters) MH_HIP(hipMalloc(&P.ev_counters, sizeof(int64_t) * 4));
-    if (!P.ev) {
-        P.ev_cap = 1 << 16;
-        P.pool_cap = 1 << 20;
+    // event records and their token bytes: grown by the retry in run_pileup;
+    // a capacity imposed by a test is where every pileup starts
+    const int64_t t_ev = c.test_caps.pile_events, t_pool = c.test_caps.pile_event_bytes;
+    if (!P.ev || (t_ev > 0 && P.ev_cap != t_ev)) {
+        hipFree(P.ev);
+        P.ev = nullptr;
+        P.ev_cap = t_ev > 0 ? t_ev : 1 << 16;
         MH_HIP(hipMalloc(&P.ev, sizeof(int32_t) * 4 * P.ev_cap));
+    }
+    if (!P.ev_pool || (t_pool > 0 && P.pool_cap != t_pool)) {
+        hipFree(P.ev_pool);
+        P.ev_pool = nullptr;
+        P.pool_cap = t_pool > 0 ? t_pool : 1 << 20;
         MH_HIP(hipMalloc(&P.ev_pool, P.pool_cap));
     }
     return 0;
@@ -955,7 +964,11 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
         MH_HIP(hipStreamSynchronize(s));
         if (ctr[3]) { set_error("mh_pileup: malformed alignment row (CIGAR/position)"); return -3; }
         if (!ctr[2]) return 0;
+        // events or token bytes past their buffers: grow both to what the
+        // launch asked for (the counters count every claim) and run it again
+        ++c.retries[RETRY_PILE_EVENTS];
         hipFree(P.ev); hipFree(P.ev_pool);
+        P.ev = nullptr; P.ev_pool = nullptr;
         P.ev_cap = ctr[0] * 2 + 1024;
         P.pool_cap = ctr[1] * 2 + 4096;
         MH_HIP(hipMalloc(&P.ev, sizeof(int32_t) * 4 * P.ev_cap));
@@ -1167,11 +1180,14 @@ int run_token_aggregate(Ctx &c, int64_t ne, std::vector<int32_t> &meta, std::str
             MH_HIP(hipMalloc(&P.tok_meta, sizeof(int32_t) * 5 * (size_t)nd + sizeof(int32_t)));
             P.tok_meta_cap = nd;
         }
-        if (P.tok_bytes_cap < 64 * (int64_t)nd) {
+        // first attempt: 64 bytes per distinct key (or what a test imposes)
+        const int64_t want = c.test_caps.token_bytes > 0 ? c.test_caps.token_bytes : 64 * (int64_t)nd;
+        if (attempt == 0 && (P.tok_bytes_cap < want || (c.test_caps.token_bytes > 0 && P.tok_bytes_cap != want))) {
             hipFree(P.tok_bytes);
             P.tok_bytes = nullptr;
-            MH_HIP(hipMalloc(&P.tok_bytes, 64 * (size_t)nd));
-            P.tok_bytes_cap = 64 * (int64_t)nd;
+            P.tok_bytes_cap = 0;
+            MH_HIP(hipMalloc(&P.tok_bytes, (size_t)want));
+            P.tok_bytes_cap = want;
         }
         int32_t *ovf = P.tok_meta + 5 * (size_t)nd;
         MH_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), s));
@@ -1187,12 +1203,14 @@ int run_token_aggregate(Ctx &c, int64_t ne, std::vector<int32_t> &meta, std::str
             meta.pop_back();
             bytes.resize((size_t)total);
             if (total > 0)
-                MH_HIP(hipMemcpy(&bytes[0], P.tok_bytes, (size_t)total, hipMemcpyDeviceToHost));
+                MH_HIP(copy_sync(c, &bytes[0], P.tok_bytes, (size_t)total, hipMemcpyDeviceToHost));
             return 0;
         }
         // longer tokens than 64 bytes on average: room for all of them
+        ++c.retries[RETRY_TOKEN_BYTES];
         hipFree(P.tok_bytes);
         P.tok_bytes = nullptr;
+        P.tok_bytes_cap = 0;
         MH_HIP(hipMalloc(&P.tok_bytes, (size_t)total));
         P.tok_bytes_cap = total;
     }
@@ -1285,7 +1303,7 @@ static int upload_sel(Ctx &c, int n_sel, const int32_t *sel, int32_t **dsel)
         P.sel_cap = n_sel > 64 ? n_sel : 64;
         MH_HIP(hipMalloc(&P.sel, sizeof(int32_t) * P.sel_cap));
     }
-    if (n_sel) MH_HIP(hipMemcpy(P.sel, sel, sizeof(int32_t) * n_sel, hipMemcpyHostToDevice));
+    if (n_sel) MH_HIP(copy_sync(c, P.sel, sel, sizeof(int32_t) * n_sel, hipMemcpyHostToDevice));
     *dsel = P.sel;
     return 0;
 }
@@ -1354,7 +1372,7 @@ extern "C" int mh_pileup_event_bytes(mh_ctx *ctx, int64_t *n_events, int64_t *po
     PileState &P = c.pile;
     int64_t ctr[4] = {0, 0, 0, 0};
     MH_HIP(hipSetDevice(c.device));
-    if (P.ev_counters) MH_HIP(hipMemcpy(ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
+    if (P.ev_counters) MH_HIP(copy_sync(c, ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
     if (n_events) *n_events = ctr[0];
     if (pool_bytes) *pool_bytes = ctr[1];
     return 0;

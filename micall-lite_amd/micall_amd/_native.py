@@ -70,6 +70,9 @@ def _declare(L):
         'mh_map_counts': ([_P, _P, _P, _P, _P, _P, _I64P, _I64P, _I64P], ctypes.c_int),
         'mh_map_stats': ([_P, _P], ctypes.c_int),
         'mh_recs_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
+        'mh_test_set_capacities': ([_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_int64], ctypes.c_int),
+        'mh_retry_counts': ([_P, _P], ctypes.c_int),
         'mh_format_rows': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.c_int64,
                             ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_size_t,
                             ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
@@ -435,6 +438,20 @@ class Context:
         out = np.zeros(5, dtype=np.int64)
         check(lib().mh_map_stats(self.h, _ptr(out)), 'mh_map_stats')
         return tuple(int(x) for x in out)
+
+    def test_set_capacities(self, cigar_pool_words=0, pileup_events=0, pileup_event_bytes=0,
+                            token_bytes=0):
+        """Test entry point: start the grow-and-retry buffers of every later
+        call at these capacities (0 = the library's own sizing)."""
+        check(lib().mh_test_set_capacities(self.h, cigar_pool_words, pileup_events,
+                                           pileup_event_bytes, token_bytes),
+              'mh_test_set_capacities')
+
+    def retry_counts(self):
+        """Retries taken so far: dict(cigar_pool, pileup_events, token_bytes)."""
+        out = np.zeros(3, dtype=np.int64)
+        check(lib().mh_retry_counts(self.h, _ptr(out)), 'mh_retry_counts')
+        return dict(cigar_pool=int(out[0]), pileup_events=int(out[1]), token_bytes=int(out[2]))
 
     def recs(self, first=0, n=None):
         """(n, 20) int32 SAM header fields (ALN_FIELDS order) without CIGARs."""
