@@ -62,21 +62,31 @@ def make_reads(pairs, block, read_len=READ_LEN, paired=True, genomes='pol'):
     return reads, quals
 
 
-def cpu_threads():
-    """Threads for the CPU baseline: every CPU this process may run on
-    (sched_getaffinity), capped by OMP_NUM_THREADS when the launcher sets it
-    (the GPU box's CPU share: nproc there shows the whole machine)."""
+def host_cpus():
+    """The host CPUs as this process sees them: every CPU it may run on
+    (sched_getaffinity: all host cores, 256 on the GPU box), the launcher's
+    OMP_NUM_THREADS (the box's CPU share, 16) and the cgroup CPU quota."""
     affinity = len(os.sched_getaffinity(0))
     omp = os.environ.get('OMP_NUM_THREADS')
-    threads = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
-    return threads, affinity, omp
+    share = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
+    quota = None
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, period = f.read().split()
+            quota = None if q == 'max' else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return {'sched_getaffinity': affinity, 'nproc': os.cpu_count(), 'OMP_NUM_THREADS': omp,
+            'share_threads': share, 'cgroup_cpu_quota': quota}
 
 
 def cpu_baseline(sample_pairs):
     """The CPU oracle's step (C restatement: og_map + og_rows_from_alns +
     og_pileup_mt, OpenMP over read pairs; O(reference length) consensus in
-    Python) on a bounded sample of the same workload.  The reads are packed
-    before the clock starts, so the timed region holds no per-read Python."""
+    Python) on a bounded sample of the same workload, on every host core
+    (sched_getaffinity) and again on the box's CPU share (OMP_NUM_THREADS).
+    The reads are packed before the clock starts, so the timed region holds
+    no per-read Python: the device-resident step's CPU equivalent."""
     import cpu_pipeline
     from micall_amd import projects
     cfg = projects.load_default()
@@ -86,15 +96,64 @@ def cpu_baseline(sample_pairs):
     prep = cpu_pipeline.Prepared([r.tobytes().decode() for r in reads],
                                  [q.tobytes().decode() for q in quals], True)
     del reads, quals
-    threads, affinity, omp = cpu_threads()
-    _, secs = cpu_pipeline.timed_step(seed_set, cfg.all_region_sequences(), groups, prep, threads)
-    return {'value': round(2 * sample_pairs / secs, 1), 'unit': 'reads/s', 'cores': threads,
-            'kind': 'port', 'host_cpus': {'sched_getaffinity': affinity, 'nproc': os.cpu_count(),
-                                          'OMP_NUM_THREADS': omp},
+    cpus = host_cpus()
+    runs = {}
+    for threads in sorted({cpus['sched_getaffinity'], cpus['share_threads']}, reverse=True):
+        _, secs = cpu_pipeline.timed_step(seed_set, cfg.all_region_sequences(), groups, prep, threads)
+        runs[threads] = secs
+    allc = cpus['sched_getaffinity']
+    return {'value': round(2 * sample_pairs / runs[allc], 1), 'unit': 'reads/s', 'cores': allc,
+            'kind': 'port', 'host_cpus': cpus,
+            'at_share': {'value': round(2 * sample_pairs / runs[cpus['share_threads']], 1),
+                         'cores': cpus['share_threads']},
             'sample': '{} synthetic pairs (first block of the bench input): prelim e2e pass over '
                       '74 seeds + 1 local remap pass + 2 pileups/consensus, oracle C restatement '
-                      '(og_map, og_pileup_mt) with OpenMP over pairs on {} threads, reads packed '
-                      'before timing, {:.1f} s'.format(sample_pairs, threads, secs)}
+                      '(og_map, og_pileup_mt) with OpenMP over pairs on all {} host cores ({:.1f} s; '
+                      'on the {}-thread CPU share: {:.1f} s), reads packed before timing'.format(
+                          sample_pairs, allc, runs[allc], cpus['share_threads'],
+                          runs[cpus['share_threads']])}
+
+
+def cpu_end_to_end(sample_pairs, workdir):
+    """The reference's file-to-file path on the CPU (oracle/cpu_e2e.py: its
+    prelim_map() + remap() structure -- FASTQ parsed every pass, SAM text,
+    prelim.csv through csv.DictWriter / DictReader, sam_to_conseqs, the
+    stopping rules, the splitter -- with the oracle C mapper on every host
+    core where bowtie2 -p N stood), on a bounded sample of the C2 input
+    written as gzip FASTQ.  Byte-equal to the reference on the golden cases
+    (tests/test_cpu_e2e.py)."""
+    import cpu_e2e
+    from micall_amd import projects, synth
+    cfg = projects.load_default()
+    seeds = cfg.seed_sequences()
+    r1 = os.path.join(workdir, 'cpu_R1.fastq.gz')
+    r2 = os.path.join(workdir, 'cpu_R2.fastq.gz')
+    pairs = synth.make_pairs(sample_pairs, genomes=bench_genomes('pol'), genome_seed=SEED,
+                             read_seed=SEED, block=0)
+    write_fastq_gz(pairs, r1, r2)
+    del pairs
+    threads = host_cpus()['sched_getaffinity']
+    paths = {k: os.path.join(workdir, 'cpu_' + k) for k in ('prelim.csv', 'remap.csv', 'counts.csv',
+                                                           'conseq.csv', 'u1.fastq', 'u2.fastq')}
+    t0 = time.perf_counter()
+    with open(paths['prelim.csv'], 'w') as f:
+        cpu_e2e.prelim_map(r1, r2, f, seeds, threads)
+    t1 = time.perf_counter()
+    with open(paths['prelim.csv']) as pre, open(paths['remap.csv'], 'w') as out, \
+            open(paths['counts.csv'], 'w') as counts, open(paths['conseq.csv'], 'w') as conseq, \
+            open(paths['u1.fastq'], 'w+') as u1, open(paths['u2.fastq'], 'w+') as u2:
+        cpu_e2e.remap(r1, r2, pre, out, counts, conseq, u1, u2, cfg.all_region_sequences(),
+                      {k: cfg.getSeedGroup(k) for k in seeds}, workdir, threads)
+    t2 = time.perf_counter()
+    for p in list(paths.values()) + [r1, r2]:
+        os.remove(p)
+    return {'value': round(2 * sample_pairs / (t2 - t0), 1), 'unit': 'reads/s', 'cores': threads,
+            'kind': 'port', 'seconds': round(t2 - t0, 3), 'prelim_map_s': round(t1 - t0, 3),
+            'remap_s': round(t2 - t1, 3),
+            'sample': '{} pairs of the C2 input as gzip FASTQ, file to file (prelim.csv, remap.csv, '
+                      'remap_counts.csv, remap_conseq.csv, unmapped FASTQs): the reference\'s '
+                      'prelim_map() + remap() structure restated in oracle/cpu_e2e.py with the '
+                      'oracle C mapper on {} threads'.format(sample_pairs, threads)}
 
 
 def write_fastq_gz(pairs, path1, path2, threads=16):
@@ -557,6 +616,8 @@ def main():
                     help='run exactly --iterations remap passes per step (C3: "3 remap '
                          'iterations"), the stopping rules applying only after them')
     ap.add_argument('--cpu-sample', type=int, default=200000)
+    ap.add_argument('--cpu-e2e-sample', type=int, default=20000,
+                    help='pairs for the CPU end-to-end baseline (file to file)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-e2e', action='store_true',
                     help='skip the end-to-end (file to file) leg of the default C2 run')
@@ -676,6 +737,11 @@ def main():
             import tempfile
             with tempfile.TemporaryDirectory(prefix='micall_e2e_') as work:
                 e2e = end_to_end(args.pairs, work)
+                if not args.no_cpu_baseline:
+                    e2e['cpu_baseline'] = cpu_end_to_end(args.cpu_e2e_sample, work)
+                    e2e['vs_cpu'] = round(e2e['value'] / e2e['cpu_baseline']['value'], 2)
+        if cpu is not None:
+            cpu['device_resident_vs_cpu'] = round(value / cpu['value'], 1)
         out = {
             'metric': METRIC, 'value': round(value, 1), 'unit': 'reads/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup,

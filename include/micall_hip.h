@@ -102,6 +102,13 @@ int mh_reads_load(mh_ctx *ctx, int64_t n_reads, int paired, const uint8_t *seq,
 /* Parse (gzip or plain) FASTQ files and load them; path2 may be NULL.
  * Keeps the read names (bowtie2 QNAME rules) for mh_format_rows. */
 int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64_t *n_reads);
+/* One rank's block of a sharded run: the same parse (raw line count of the
+ * whole file included), but only units (pairs, or reads when unpaired)
+ * [U*part/parts, U*(part+1)/parts) of the U in the files stay resident;
+ * *first_unit receives the block's first unit.  parts = 1 is
+ * mh_reads_load_fastq. */
+int mh_reads_load_fastq_part(mh_ctx *ctx, const char *path1, const char *path2, int part, int parts,
+                             int64_t *n_reads, int64_t *first_unit);
 int mh_reads_count(mh_ctx *ctx, int64_t *n_reads, int *paired);
 /* newlines in FASTQ 1 of the last mh_reads_load_fastq (the `gunzip -c | wc
  * -l` of LineCounter, externals.py:206-231; raw_count = lines / 2). */

@@ -497,6 +497,17 @@ static int parse_fastq(const std::string &data, const char *path, Fastq &fq, boo
     return 0;
 }
 
+// keep records [u0, u1) of a parsed file (their bytes stay where they are)
+static void keep_block(Fastq &fq, int64_t u0, int64_t u1)
+{
+    fq.off.erase(fq.off.begin() + u1, fq.off.end());
+    fq.off.erase(fq.off.begin(), fq.off.begin() + u0);
+    fq.len.erase(fq.len.begin() + u1, fq.len.end());
+    fq.len.erase(fq.len.begin(), fq.len.begin() + u0);
+    fq.names.erase(fq.names.begin() + u1, fq.names.end());
+    fq.names.erase(fq.names.begin(), fq.names.begin() + u0);
+}
+
 static int read_fastq(const char *path, Fastq &fq, bool paired, int64_t *newlines = nullptr)
 {
     std::string data;
@@ -658,7 +669,16 @@ int mh_reads_load(mh_ctx *ctx, int64_t n_reads, int paired, const uint8_t *seq,
 
 int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64_t *n_reads)
 {
-    if (!ctx || !path1) return -3;
+    return mh_reads_load_fastq_part(ctx, path1, path2, 0, 1, n_reads, nullptr);
+}
+
+int mh_reads_load_fastq_part(mh_ctx *ctx, const char *path1, const char *path2, int part, int parts,
+                             int64_t *n_reads, int64_t *first_unit)
+{
+    if (!ctx || !path1 || parts < 1 || part < 0 || part >= parts) {
+        set_error("mh_reads_load_fastq_part: bad arguments");
+        return -3;
+    }
     CtxEx *c = X(ctx);
     MH_HIP(hipSetDevice(c->device));
     const bool paired = path2 != nullptr;
@@ -681,11 +701,21 @@ int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64
     std::vector<uint8_t> seq, qual;
     std::vector<int64_t> off;
     std::vector<int32_t> len;
+    if (paired && a.len.size() != b.len.size()) {
+        set_error("paired FASTQ files hold %zu and %zu reads", a.len.size(), b.len.size());
+        return -3;
+    }
+    // this part's contiguous block of units (pairs, or reads when unpaired):
+    // [U * part / parts, U * (part + 1) / parts), so every unit is in one
+    // block and the blocks differ in size by at most one
+    const int64_t units_all = (int64_t)a.len.size();
+    const int64_t u0 = units_all * part / parts, u1 = units_all * (part + 1) / parts;
+    if (first_unit) *first_unit = u0;
+    if (parts > 1) {
+        keep_block(a, u0, u1);
+        if (paired) keep_block(b, u0, u1);
+    }
     if (paired) {
-        if (a.len.size() != b.len.size()) {
-            set_error("paired FASTQ files hold %zu and %zu reads", a.len.size(), b.len.size());
-            return -3;
-        }
         const int64_t np = (int64_t)a.len.size();
         off.resize(2 * np);
         len.resize(2 * np);
@@ -708,6 +738,19 @@ int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64
                 names[2 * i + 1].swap(b.names[i]);
             }
         });
+    } else if (parts > 1) {   // the block's reads, packed from offset 0
+        const int64_t nr = (int64_t)a.len.size();
+        off.resize(nr);
+        len.assign(a.len.begin(), a.len.end());
+        int64_t total = 0;
+        for (int64_t i = 0; i < nr; ++i) { off[i] = total; total += a.len[i]; }
+        seq.resize((size_t)total);
+        qual.resize((size_t)total);
+        for (int64_t i = 0; i < nr; ++i) {
+            memcpy(&seq[off[i]], &a.seq[a.off[i]], (size_t)a.len[i]);
+            memcpy(&qual[off[i]], &a.qual[a.off[i]], (size_t)a.len[i]);
+        }
+        names.swap(a.names);
     } else {
         off.swap(a.off);
         len.swap(a.len);

@@ -63,6 +63,8 @@ def _declare(L):
         'mh_index_build': ([_P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int], ctypes.c_int),
         'mh_reads_load': ([_P, ctypes.c_int64, ctypes.c_int, _P, _P, _P, _P], ctypes.c_int),
         'mh_reads_load_fastq': ([_P, ctypes.c_char_p, ctypes.c_char_p, _I64P], ctypes.c_int),
+        'mh_reads_load_fastq_part': ([_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                      ctypes.c_int, _I64P, _I64P], ctypes.c_int),
         'mh_reads_count': ([_P, _I64P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         'mh_reads_set_names': ([_P, ctypes.c_int64, ctypes.POINTER(ctypes.c_char_p)], ctypes.c_int),
         'mh_map': ([_P, ctypes.POINTER(Params)], ctypes.c_int),
@@ -194,6 +196,9 @@ class Context:
         check(L.mh_ctx_create(device, ctypes.byref(h)), 'mh_ctx_create')
         self.h = h
         self.device = device
+        # bumped whenever the resident reads or the mapping records change
+        # (session.prelim_resident compares it)
+        self.map_serial = 0
         self.n_refs = 0
         self.refnames = []
         self.reflens = []
@@ -371,6 +376,7 @@ class Context:
         lens = np.ascontiguousarray(lens, dtype=np.int32)
         check(lib().mh_reads_load(self.h, len(lens), int(paired), _ptr(seq), _ptr(qual),
                                   _ptr(offsets), _ptr(lens)), 'mh_reads_load')
+        self.map_serial += 1
 
     def reads_load(self, seqs, quals, paired, names=None):
         lens = np.array([len(s) for s in seqs], dtype=np.int32)
@@ -394,7 +400,20 @@ class Context:
         n = ctypes.c_int64()
         check(lib().mh_reads_load_fastq(self.h, path1.encode(), path2.encode() if path2 else None,
                                         ctypes.byref(n)), 'mh_reads_load_fastq')
+        self.map_serial += 1
         return n.value
+
+    def reads_load_fastq_part(self, path1, path2, part, parts):
+        """One rank's contiguous block of the FASTQ units: (reads loaded,
+        first unit of the block)."""
+        n = ctypes.c_int64()
+        u0 = ctypes.c_int64()
+        check(lib().mh_reads_load_fastq_part(self.h, path1.encode(),
+                                             path2.encode() if path2 else None, part, parts,
+                                             ctypes.byref(n), ctypes.byref(u0)),
+              'mh_reads_load_fastq_part')
+        self.map_serial += 1
+        return n.value, u0.value
 
     def reads_count(self):
         n = ctypes.c_int64()
@@ -409,6 +428,7 @@ class Context:
     # ---- mapping --------------------------------------------------------
     def map(self, par):
         check(lib().mh_map(self.h, ctypes.byref(par)), 'mh_map')
+        self.map_serial += 1
 
     def fetch(self, first=0, n=None):
         if n is None:
@@ -446,6 +466,7 @@ class Context:
         check(lib().mh_test_set_capacities(self.h, cigar_pool_words, pileup_events,
                                            pileup_event_bytes, token_bytes),
               'mh_test_set_capacities')
+        self.map_serial += 1
 
     def retry_counts(self):
         """Retries taken so far: dict(cigar_pool, pileup_events, token_bytes)."""

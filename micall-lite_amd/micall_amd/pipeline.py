@@ -56,6 +56,11 @@ class Shard:
         self.rank, self.world, self.read_base = rank, world, read_base
         self.device = device if device is not None else torch.device('cpu')
 
+    def barrier(self):
+        """Every rank has reached this point (e.g. opened its output files,
+        so rank 0's writes cannot be truncated by a later open)."""
+        self.sum_i64([0])
+
     def sum_i64(self, arr):
         t = self.torch.as_tensor(np.ascontiguousarray(arr, dtype=np.int64), device=self.device)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
@@ -79,6 +84,63 @@ class Shard:
     def _gather_sizes(self, values):
         t = self.torch.as_tensor(np.asarray(values, dtype=np.int64), device=self.device)
         return self._gather(t).cpu().numpy().reshape(self.world, len(values))
+
+    def _text_device(self):
+        # gloo moves point-to-point messages in host memory; RCCL needs them
+        # on the device
+        return self.torch.device('cpu') if self.dist.get_backend() == 'gloo' else self.device
+
+    def all_gather_bytes(self, data):
+        """Every rank's bytes (small texts such as a list of names), in
+        rank order, on every rank."""
+        torch = self.torch
+        sizes = self._gather_sizes([len(data)])[:, 0]
+        m = max(int(sizes.max()), 1)
+        buf = np.zeros(m, dtype=np.uint8)
+        buf[:len(data)] = np.frombuffer(bytes(data), dtype=np.uint8)
+        dev = self._text_device()
+        parts = [torch.empty(m, dtype=torch.uint8, device=dev) for _ in range(self.world)]
+        self.dist.all_gather(parts, torch.as_tensor(buf, device=dev))
+        return [parts[k].cpu().numpy()[:int(sizes[k])].tobytes() for k in range(self.world)]
+
+    def gather_segments(self, segments):
+        """Output text to rank 0: every rank passes the same number k of
+        byte segments (e.g. its rows of each prelim.csv group, in the global
+        group order); rank 0 receives [rank][segment] memoryviews, the other
+        ranks None.  The lengths are all-gathered, then each rank's segments
+        travel as one point-to-point message (device buffers under RCCL)."""
+        torch = self.torch
+        lens = np.array([len(x) for x in segments], dtype=np.int64)
+        all_lens = self._gather_sizes(lens) if len(lens) else np.zeros((self.world, 0), np.int64)
+        dev = self._text_device()
+
+        def split(buf, ls):
+            out, at = [], 0
+            for n in ls.tolist():
+                out.append(buf[at:at + n])
+                at += n
+            return out
+
+        if self.rank != 0:
+            total = int(lens.sum())
+            if total:
+                buf = np.empty(total, dtype=np.uint8)
+                at = 0
+                for x in segments:
+                    buf[at:at + len(x)] = np.frombuffer(x, dtype=np.uint8)
+                    at += len(x)
+                self.dist.send(torch.from_numpy(buf).to(dev), dst=0)
+            return None
+        out = [[memoryview(x) for x in segments]]
+        for r in range(1, self.world):
+            total = int(all_lens[r].sum())
+            if total:
+                t = torch.empty(total, dtype=torch.uint8, device=dev)
+                self.dist.recv(t, src=r)
+                out.append(split(memoryview(t.cpu().numpy()), all_lens[r]))
+            else:
+                out.append([memoryview(b'')] * len(segments))
+        return out
 
     def pileup(self, ctx, unit_base):
         """All-reduce the device counters in place and all-gather the

@@ -9,7 +9,6 @@ by the HIP mapper (mh_index_build + mh_map); bt2_path / bt2build_path /
 nthreads are accepted for signature compatibility and ignored.
 """
 import argparse
-import csv
 import logging
 import os
 import sys
@@ -66,6 +65,9 @@ def prelim_map(fastq1, fastq2, prelim_csv,
     rdgopen = READ_GAP_OPEN if rdgopen is None else int(rdgopen)
     rfgopen = REF_GAP_OPEN if rfgopen is None else int(rfgopen)
     ctx = session.load_fastq(fastq1, fastq2)
+    sh = session.shard()
+    if sh is not None:
+        sh.barrier()
     if callback:
         total_reads = ctx.fastq_line_count / 2
         callback(message='... preliminary mapping', progress=0, max_progress=total_reads)
@@ -78,13 +80,47 @@ def prelim_map(fastq1, fastq2, prelim_csv,
     ctx.index_build(names, [seeds[n] for n in names], E2E_SEEDLEN)
     ctx.map(_native.params(_native.E2E, rdg=(rdgopen, READ_GAP_EXTEND),
                            rfg=(rfgopen, REF_GAP_EXTEND), maxins=MAXINS))
-    recs = ctx.recs()
-    order = grouped_order(recs[:, _native.ALN_FIELDS.index('sam_ref')])
-    writer = csv.DictWriter(prelim_csv, FIELDNAMES, lineterminator=os.linesep)
-    writer.writeheader()
-    ctx.write_rows(prelim_csv, 1, order=order)
+    sam_ref = ctx.recs()[:, _native.ALN_FIELDS.index('sam_ref')]
+    digest = session._digest()
+    if session.is_writer():
+        session.write_bytes(prelim_csv, (','.join(FIELDNAMES) + os.linesep).encode(), digest)
+    if sh is None:
+        session.write_bytes(prelim_csv, ctx.format_rows_bytes(1, order=grouped_order(sam_ref)),
+                            digest)
+    else:
+        _write_sharded(ctx, sh, sam_ref, len(names), prelim_csv, digest)
+    session.prelim_written(ctx, prelim_csv, digest, names)
     if callback:
         callback(progress=ctx.fastq_line_count / 2)
+
+
+def _write_sharded(ctx, sh, sam_ref, n_refs, prelim_csv, digest):
+    """prelim.csv of a sharded run: rname groups in global first-seen order
+    (the smallest global row index of each rname over all ranks), and in a
+    group the rows of rank 0, then rank 1, ... -- the ranks hold consecutive
+    blocks of the FASTQ, so that is FASTQ order, as on one GPU.  Every rank
+    formats its own rows; rank 0 writes."""
+    sam_ref = np.asarray(sam_ref, dtype=np.int64)
+    key = np.where(sam_ref < 0, n_refs, sam_ref)            # '*' is its own group
+    first = np.full(n_refs + 1, -1, dtype=np.int64)
+    if len(key):
+        k_vals, k_first = np.unique(key, return_index=True)
+        first[k_vals] = k_first + sh.read_base
+    first = sh.min_i64(first)
+    groups = [g for g in np.argsort(np.where(first < 0, np.iinfo(np.int64).max, first),
+                                    kind='stable') if first[g] >= 0]
+    rank_of = np.full(n_refs + 1, len(groups), dtype=np.int64)
+    rank_of[groups] = np.arange(len(groups))
+    local = np.argsort(rank_of[key], kind='stable').astype(np.int64)
+    bounds = np.searchsorted(rank_of[key][local], np.arange(len(groups) + 1))
+    segments = [ctx.format_rows_bytes(1, order=local[bounds[g]:bounds[g + 1]])
+                if bounds[g + 1] > bounds[g] else b'' for g in range(len(groups))]
+    parts = sh.gather_segments(segments)
+    if parts is not None:
+        for g in range(len(groups)):
+            for r in range(sh.world):
+                if len(parts[r][g]):
+                    session.write_bytes(prelim_csv, parts[r][g], digest)
 
 
 _CLI_OPTIONS = (

@@ -72,15 +72,39 @@ def _sam_fields(ctx, rows):
     return [line.split('\t') for line in text.split('\n')[:-1]]
 
 
-def _write_unmapped(ctx, recs, unmapped1, unmapped2):
-    """FASTQ records of the unmapped lines of the last pass, R1 and R2 apart
+def _unmapped_text(ctx, recs):
+    """FASTQ text of the unmapped lines of the last pass, R1 and R2 apart
     (remap.py:743-753)."""
+    out = ([], [])
+    for fields in _sam_fields(ctx, np.nonzero(recs[:, F['flag']] & _UNMAPPED)[0]):
+        out[0 if is_first_read(fields[1]) else 1].append('@{0[0]}\n{0[9]}\n+\n{0[10]}\n'.format(fields))
+    return ''.join(out[0]).encode(), ''.join(out[1]).encode()
+
+
+def _write_unmapped(ctx, recs, unmapped1, unmapped2, shard=None):
+    """Append the last pass's unmapped reads to the unmapped FASTQs (every
+    rank's, in rank order, written by rank 0 in a sharded run)."""
     if not (unmapped1 or unmapped2):
         return
-    for fields in _sam_fields(ctx, np.nonzero(recs[:, F['flag']] & _UNMAPPED)[0]):
-        handle = unmapped1 if is_first_read(fields[1]) else unmapped2
-        if handle:
-            handle.write('@{0[0]}\n{0[9]}\n+\n{0[10]}\n'.format(fields))
+    texts = _unmapped_text(ctx, recs)
+    _emit(shard, [(unmapped1, texts[0]), (unmapped2, texts[1])])
+
+
+def _emit(shard, outputs):
+    """Write (handle, bytes) pairs: directly on one GPU; in a sharded run
+    every rank's bytes of each output, rank order, by rank 0."""
+    if shard is None:
+        for handle, data in outputs:
+            if handle and len(data):
+                session.write_bytes(handle, data)
+        return
+    parts = shard.gather_segments([data for _h, data in outputs])
+    if parts is None:
+        return
+    for k, (handle, _data) in enumerate(outputs):
+        for r in range(shard.world):
+            if handle and len(parts[r][k]):
+                session.write_bytes(handle, parts[r][k])
 
 
 class RemapRun(RemapPipeline):
@@ -110,11 +134,30 @@ class RemapRun(RemapPipeline):
         winners = self.select_seeds(groups)
         # build_conseqs(temp.sam, seeds=seeds) over the prelim rows (remap.py:531)
         present = [refnames[k] for k in rows['present']]
+        # every rank of a sharded run parses all of prelim.csv, so this
+        # pileup is already global: no exchange
         self.ctx.pileup(1, CONSENSUS_Q_CUTOFF, [len(region_seqs[n]) for n in present])
         pile = Pileup(self.ctx.pileup_fetch(), present)
         built = counts_to_conseqs(pile, pile.refs_with_reads(), seeds=self.seeds)
         chosen = {name: seq for name, seq in built.items() if name in winners}
         return chosen, {name: winners[name] for name in chosen}
+
+    def prelim_from_device(self, remap_counts_writer=None):
+        """The same as prelim_from_csv when prelim.csv is the file this
+        process's prelim_map() wrote from the records still resident
+        (session.prelim_resident): the per-rname tallies and the pileup come
+        from those records (all-reduced over the ranks of a sharded run).
+        prelim.csv groups rows by rname in first-seen order, so its groups,
+        and the order in which its pairs reach each reference, follow the
+        tallies' first rows.  Skips the parse of a GB-sized text."""
+        self.prelim_names = list(self.seed_set)
+        self.prelim_stats = self._counts()
+        groups = self.prelim_groups()
+        if remap_counts_writer is not None:
+            remap_counts_writer.writerows(dict(type='prelim %s' % name, count=count,
+                                               filtered_count=filt)
+                                          for name, count, filt in groups)
+        return self.prelim_conseqs(self.select_seeds(groups))
 
 
 class MixedReferenceSplit(object):
@@ -194,13 +237,17 @@ def remap(fastq1, fastq2, prelim_csv, remap_csv, remap_counts_csv=None, remap_co
     rfgopen = REF_GAP_OPEN if rfgopen is None else int(rfgopen)
     projects = ProjectConfig.loadDefault() if json is None else ProjectConfig.loadCustom(json)
     ctx = session.load_fastq(fastq1, fastq2)
+    sh = session.shard()
+    if sh is not None:
+        sh.barrier()
+    writer = session.is_writer()
     run = RemapRun(ctx, projects, count_threshold=count_threshold, rdgopen=rdgopen,
-                   rfgopen=rfgopen, callback=callback)
+                   rfgopen=rfgopen, callback=callback, shard=sh)
     # bowtie2's input lines / 2, also for unpaired input (remap.py:457)
     raw_count = ctx.fastq_line_count / 2
 
     counts_out = None
-    if remap_counts_csv:
+    if remap_counts_csv and writer:
         counts_out = csv.DictWriter(remap_counts_csv, REMAP_COUNT_COLUMNS,
                                     lineterminator=os.linesep)
         counts_out.writeheader()
@@ -208,26 +255,31 @@ def remap(fastq1, fastq2, prelim_csv, remap_csv, remap_counts_csv=None, remap_co
     if callback:
         callback(message='... processing preliminary map', progress=0, max_progress=raw_count)
 
-    conseqs, map_counts = run.prelim_from_csv(prelim_csv, counts_out, callback)
+    if session.prelim_resident(ctx, prelim_csv, run.seed_set):
+        session.stats['prelim_source'] = 'device'
+        conseqs, map_counts = run.prelim_from_device(counts_out)
+    else:
+        session.stats['prelim_source'] = 'csv'
+        conseqs, map_counts = run.prelim_from_csv(prelim_csv, counts_out, callback)
 
-    def clear_unmapped():
-        # each pass rewrites the unmapped FASTQs (remap.py:552-558)
-        for handle in (unmapped1, unmapped2):
-            if handle:
-                handle.seek(0)
-                handle.truncate()
+    # Each pass rewrites the unmapped FASTQs (remap.py:552-558), so they hold
+    # the unmapped reads of the last pass: written once, after the loop.
+    for handle in (unmapped1, unmapped2):
+        if handle and writer and conseqs:
+            handle.seek(0)
+            handle.truncate()
+    conseqs, new_counts, unmapped_count = run.iterate(conseqs, map_counts, raw_count,
+                                                      remap_counts_writer=counts_out)
+    if run.mapped_to is not None:
+        _write_unmapped(ctx, ctx.recs(), unmapped1, unmapped2, sh)
 
-    conseqs, new_counts, unmapped_count = run.iterate(
-        conseqs, map_counts, raw_count, remap_counts_writer=counts_out,
-        before_pass=clear_unmapped,
-        after_pass=lambda: _write_unmapped(ctx, ctx.recs(), unmapped1, unmapped2))
-
-    csv.DictWriter(remap_csv, FIELDNAMES, lineterminator=os.linesep).writeheader()
+    if writer:
+        csv.DictWriter(remap_csv, FIELDNAMES, lineterminator=os.linesep).writeheader()
     if new_counts:
         unmapped_count += _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv,
-                                            unmapped1, unmapped2)
+                                            unmapped1, unmapped2, sh)
 
-    if remap_conseq_csv:
+    if remap_conseq_csv and writer:
         # the sequences the reads were last mapped to (remap.py:637-643)
         remap_conseq_csv.write('region,sequence\n')
         remap_conseq_csv.writelines('%s,%s\n' % (name, conseqs.get(name) or
@@ -235,9 +287,12 @@ def remap(fastq1, fastq2, prelim_csv, remap_csv, remap_counts_csv=None, remap_co
                                     for name in new_counts)
     if counts_out is not None:
         _write_final_counts(counts_out, new_counts, unmapped_count)
-    if keep and run.mapped_to is not None:
+    last = getattr(run, 'last_refseqs', None)
+    if keep and writer and run.mapped_to is not None and last is not None:
+        # the reference set of the last map_to_reference call, a split
+        # re-mapping's single reference included (remap.py:624-630, 689-692)
         with open(os.path.join(work_path, 'temp.fasta'), 'w') as f:
-            f.writelines('>%s\n%s\n' % item for item in run.mapped_to.items())
+            f.writelines('>%s\n%s\n' % item for item in last.items())
 
 
 def _write_final_counts(writer, new_counts, unmapped_count):
@@ -245,14 +300,28 @@ def _write_final_counts(writer, new_counts, unmapped_count):
     writer.writerow(dict(type='unmapped', count=unmapped_count))
 
 
-def _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv, unmapped1, unmapped2):
+def _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv, unmapped1, unmapped2, shard=None):
     """remap.csv rows of the last pass, then the mixed-reference pairs mapped
     again, one reference at a time (remap.py:612-634).  new_counts gains
-    each re-mapping's counts; returns the unmapped lines they add."""
+    each re-mapping's counts; returns the unmapped lines they add.
+
+    Sharded: mates are resident on one rank, so every rank splits its own
+    pairs; the references are re-mapped in their global order of first
+    split (rank order, then each rank's order), every rank taking part in
+    each one (with its own split pairs, possibly none), and the rows and
+    unmapped reads are written in rank order."""
     keep_rows, splits = split_mixed_references(ctx, ctx.recs())
-    ctx.write_rows(remap_csv, 1, order=keep_rows)
+    _emit(shard, [(remap_csv, ctx.format_rows_bytes(1, order=keep_rows))])
+    order = list(splits)
+    if shard is not None:
+        order = []
+        for text in shard.all_gather_bytes('\n'.join(splits).encode()):
+            for name in text.decode().split('\n') if text else []:
+                if name not in order:
+                    order.append(name)
     extra_unmapped = 0
-    for name, (reads1, reads2) in splits.items():
+    for name in order:
+        reads1, reads2 = splits.get(name, ([], []))
         names, seqs, quals = [], [], []
         for a, b in zip(reads1, reads2):
             names += [a[0], a[0]]
@@ -263,8 +332,8 @@ def _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv, unmapped1, unmap
         counts, unmapped = run.map_to_reference({name: conseqs[name]})
         extra_unmapped += unmapped
         new_counts.update(counts)
-        _write_unmapped(ctx, ctx.recs(), unmapped1, unmapped2)
-        ctx.write_rows(remap_csv, 1)
+        _write_unmapped(ctx, ctx.recs(), unmapped1, unmapped2, shard)
+        _emit(shard, [(remap_csv, ctx.format_rows_bytes(1) if seqs else b'')])
     return extra_unmapped
 
 
