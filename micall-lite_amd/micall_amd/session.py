@@ -64,6 +64,10 @@ def shard():
     if dist.get_world_size() <= 1:
         return None
     from .pipeline import Shard
+    # torch's HIP runtime must come up before this library's context does
+    # (load_fastq asks for the shard first); device buffers then carry the
+    # pileup exchange
+    torch.cuda.set_device(_device_index())
     _shard = Shard(dist.get_rank(), dist.get_world_size(), 0,
                    device=torch.device('cuda', _device_index()))
     return _shard
@@ -91,8 +95,8 @@ def load_fastq(fastq1, fastq2=None):
     sharded job only this rank's block of units is resident, and the
     shard's read_base is the block's first read."""
     global _key
-    ctx = context()
     sh = shard()
+    ctx = context()
     key = _file_key(fastq1, fastq2)
     if key != _key:
         if sh is None:

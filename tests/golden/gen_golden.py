@@ -713,6 +713,123 @@ def gen_censor():
     print('censor: {} bad cycles, {} scenarios'.format(bad.getvalue().count('\n') - 1, len(cases)))
 
 
+def _error_metrics(lengths, tiles, bad, seed):
+    """A version-3 ErrorMetricsOut.bin: every (tile, cycle) of the run, the
+    (tile, run cycle) pairs in `bad` at an error rate >= 7.5.  A bad cycle
+    makes every later cycle of its tile and read bad (filter_quality.py:
+    report_bad_cycles), so the bad entries sit in the reads' last cycles, as
+    phiX error rates climb at the end of a run."""
+    import random
+    import struct
+    rng = random.Random(seed)
+    recs = []
+    for tile in tiles:
+        for cycle in range(1, sum(lengths) + 1):
+            rate = (7.5 + rng.random() * 10 if (tile, cycle) in bad
+                    else rng.choice([0.1, 0.3, 0.6, 1.2]))
+            recs.append(struct.pack('<HHHfLLLLL', 1, tile, cycle, rate, 1, 2, 3, 4, 5))
+    rng.shuffle(recs)
+    return struct.pack('!BB', 3, 30) + b''.join(recs)
+
+
+def gen_chain():
+    """BASELINE C5's chain as bin/micall:91-169 runs it, on the stock
+    reference: read_errors -> write_phix_csv -> report_bad_cycles -> censor
+    (R1; a paired run would censor R2 with the exhausted DictReader,
+    bin/micall:116,126) -> prelim_map -U -> remap, on a synthetic
+    ErrorMetricsOut.bin (~2 % bad tile-cycles) and unpaired 1x300 reads over
+    4 tiles.  Every intermediate and final file is kept under
+    tests/golden/chain/<case>/."""
+    import csv
+    import gzip
+    import shutil
+    import tempfile
+    refharness.setup()
+    from micall.core.censor_fastq import censor
+    from micall.core.filter_quality import report_bad_cycles
+    from micall.core.parse_interop import read_errors, write_phix_csv
+    from micall.core.prelim_map import prelim_map
+    from micall.core.remap import remap
+    from micall_amd import projects, synth
+    shim = os.path.join(REPO, 'oracle', 'shim_bin')
+    seeds = projects.load_default().seed_sequences()
+    for name, pairs_kw, lengths in (
+            ('c5_unpaired300', dict(n=800, paired=False, read_len=300), [300, 8, 8, 300]),
+            ('c5_paired251', dict(n=600, paired=True, read_len=251), [251, 8, 8, 251])):
+        out = os.path.join(HERE, 'chain', name)
+        os.makedirs(out, exist_ok=True)
+        work = tempfile.mkdtemp(prefix='chain_')
+        cwd = os.getcwd()
+        os.chdir(work)
+        try:
+            tiles = (1101, 1102, 1103, 1104)
+            interop = os.path.join(work, 'ErrorMetricsOut.bin')
+            # ~2 % of the (tile, cycle) entries bad: the last 20 cycles of
+            # read 1 on tile 1102 and the last 30 of read 2 on tile 1104
+            r1_end, r2_end = lengths[0], sum(lengths)
+            bad = ({(1102, c) for c in range(r1_end - 19, r1_end + 1)} |
+                   {(1104, c) for c in range(r2_end - 29, r2_end + 1)})
+            with open(interop, 'wb') as f:
+                f.write(_error_metrics(lengths, tiles, bad, 11))
+            pairs = synth.make_pairs(pairs_kw['n'], genomes={'HIV1B-pol-seed': seeds['HIV1B-pol-seed']},
+                                     genome_seed=301, read_seed=302, read_len=pairs_kw['read_len'],
+                                     paired=pairs_kw['paired'])
+            fastqs = []
+            for mate in ((1, 2) if pairs_kw['paired'] else (1,)):
+                r, q = pairs['r%d' % mate], pairs['q%d' % mate]
+                text = ''.join('@M01841:45:000000000-A5FEG:1:{}:{}:{} {}:N:0:9\n{}\n+\n{}\n'.format(
+                    tiles[i % 4], 1000 + i, 2000 + i, mate, r[i].tobytes().decode(),
+                    q[i].tobytes().decode()) for i in range(pairs['n']))
+                path = os.path.join(work, 'S1_L001_R{}_001.fastq.gz'.format(mate))
+                _gz_write(path, text)
+                fastqs.append(path)
+            # bin/micall censor_fastqs (:91-129)
+            with open(interop, 'rb') as f:
+                records = read_errors(f)
+                with open('quality.csv', 'w') as q:
+                    write_phix_csv(out_file=q, records=records, read_lengths=lengths)
+            with open('quality.csv') as f1, open('bad_cycles.csv', 'w') as f2:
+                report_bad_cycles(f1, f2)
+            bad_cycles = csv.DictReader(open('bad_cycles.csv'))
+            censored = []
+            for k, src in enumerate(fastqs):
+                dst = src.replace('.fastq', '.censor.fastq')
+                with open(src, 'rb') as fi, open(dst, 'wb') as fo:
+                    censor(src=fi, bad_cycles_reader=bad_cycles, dest=fo, use_gzip=True)
+                censored.append(dst)
+            r1, r2 = censored[0], censored[1] if len(censored) > 1 else None
+            with open('prelim.csv', 'w') as handle:
+                prelim_map(fastq1=r1, fastq2=r2, prelim_csv=handle, gzip=True,
+                           bt2_path=os.path.join(shim, 'bowtie2'),
+                           bt2build_path=os.path.join(shim, 'bowtie2-build-s'), nthreads=1,
+                           work_path=work)
+            names = ('remap.csv', 'remap_counts.csv', 'remap_conseq.csv', 'unmapped1.fastq',
+                     'unmapped2.fastq')
+            outs = {k: open(k, 'w') for k in names}
+            with open('prelim.csv') as pre:
+                remap(r1, r2, pre, outs['remap.csv'], outs['remap_counts.csv'],
+                      outs['remap_conseq.csv'], outs['unmapped1.fastq'], outs['unmapped2.fastq'],
+                      work_path=work, bt2_path=os.path.join(shim, 'bowtie2'),
+                      bt2build_path=os.path.join(shim, 'bowtie2-build-s'), nthreads=1, gzip=True,
+                      keep=True)
+            for f in outs.values():
+                f.close()
+            shutil.copyfile(interop, os.path.join(out, 'ErrorMetricsOut.bin'))
+            for k, src in enumerate(fastqs):
+                shutil.copyfile(src, os.path.join(out, 'R{}.fastq.gz'.format(k + 1)))
+                with gzip.open(censored[k], 'rb') as f:
+                    _gz_write(os.path.join(out, 'R{}.censor.fastq.gz'.format(k + 1)), f.read().decode())
+            for k in ('quality.csv', 'bad_cycles.csv', 'prelim.csv') + names:
+                with open(k) as f:
+                    _gz_write(os.path.join(out, k + '.gz'), f.read())
+            with open(os.path.join(out, 'read_lengths.json'), 'w') as f:
+                json.dump(lengths, f)
+            print('chain:', name)
+        finally:
+            os.chdir(cwd)
+            shutil.rmtree(work, ignore_errors=True)
+
+
 def gen_s2a():
     import gzip
     refharness.setup()

@@ -19,6 +19,11 @@ def _rows(case, name):
         return list(csv.DictReader(io.StringIO(f.read())))
 
 
+def _read(path):
+    with gzip.open(path, 'rt') as f:
+        return f.read()
+
+
 def _counts(case):
     return {r['type']: r['count'] for r in _rows(case, 'remap_counts.csv')}
 
@@ -69,3 +74,27 @@ def test_no_seed_cases_record_the_reference_failure(case):
     c = _counts(case)
     assert not any(k.startswith('remap-') for k in c)
     assert c['unmapped'] == c['raw']
+
+
+def test_c5_chain_goldens_hold_their_scenarios(golden_dir):
+    """tests/golden/chain: bad tile-cycles censored in R1 (trailing bad
+    cycles dropped), R2 of the paired case left uncensored by the exhausted
+    DictReader (bin/micall:116,126), unpaired 1x300 reads mapped (-U)."""
+    import json
+    for case, paired in (('c5_unpaired300', False), ('c5_paired251', True)):
+        d = os.path.join(golden_dir, 'chain', case)
+        bad = _read(os.path.join(d, 'bad_cycles.csv.gz')).splitlines()[1:]
+        assert 30 <= len(bad) <= 80
+        raw = _read(os.path.join(d, 'R1.fastq.gz')).splitlines()
+        cen = _read(os.path.join(d, 'R1.censor.fastq.gz')).splitlines()
+        lengths = json.load(open(os.path.join(d, 'read_lengths.json')))
+        assert len(raw[1]) == lengths[0]
+        shorter = sum(1 for a, b in zip(raw[1::4], cen[1::4]) if len(b) < len(a))
+        assert shorter > 0
+        if paired:
+            assert (_read(os.path.join(d, 'R2.fastq.gz')) ==
+                    _read(os.path.join(d, 'R2.censor.fastq.gz')))
+        else:
+            assert not os.path.exists(os.path.join(d, 'R2.fastq.gz'))
+        counts = _read(os.path.join(d, 'remap_counts.csv.gz'))
+        assert 'remap-final HIV1B-pol-seed' in counts
