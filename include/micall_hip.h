@@ -160,6 +160,15 @@ int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20);
 int mh_reads_set_names(mh_ctx *ctx, int64_t n, const char *const *names);
 int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
                    const char *const *refnames, char *buf, size_t cap, size_t *used);
+/* The same rows written straight to an open file descriptor at `offset`
+ * (pwrite from the formatting threads, no copy through the caller):
+ * *written bytes.  The caller moves its file position past them. */
+int mh_write_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
+                  const char *const *refnames, int fd, int64_t offset, int64_t *written);
+/* (crc32 << 32) | adler32 of a whole open file (zlib's, computed over
+ * chunks on host threads) and its size: remap() checks with it that
+ * prelim.csv is the file prelim_map() wrote. */
+int mh_file_checksum(int fd, int64_t *size, uint64_t *sum);
 
 /* ---- pileup: replaces sam_to_conseqs' counting (remap.py:141-306) ------ */
 /* External SAM rows (e.g. prelim.csv read back, remap.py:474-498).

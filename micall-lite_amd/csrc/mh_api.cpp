@@ -1,6 +1,9 @@
 // mh_api.cpp -- host side of libmicall_hip.so: the extern "C" entry points of
 // include/micall_hip.h, context and device-memory management, the seed index
 // build (bowtie2-build's job), FASTQ ingest and SAM/CSV text emission.
+#include <errno.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -146,8 +149,22 @@ static int prepare_len_tab(Ctx &c, const mh_params &par)
 }
 
 // ---- host copies of the reads (SAM SEQ/QUAL text) ------------------------
+// Host bytes that are not zero-filled on allocation (the ingest writes
+// every byte it keeps; a std::vector's value-initialisation of a GB buffer
+// is a serial memset the ingest does not need).
+struct Bytes {
+    std::unique_ptr<uint8_t[]> p;
+    size_t n = 0;
+    void alloc(size_t k) { p.reset(new uint8_t[k > 0 ? k : 1]); n = k; }
+    void assign(const uint8_t *a, const uint8_t *b) { alloc((size_t)(b - a)); if (b > a) std::memcpy(p.get(), a, n); }
+    uint8_t *data() { return p.get(); }
+    const uint8_t *data() const { return p.get(); }
+    size_t size() const { return n; }
+};
+
+// the reads as text on the host (SEQ / QUAL of the SAM rows)
 struct HostReads {
-    std::vector<uint8_t> seq, qual;
+    Bytes seq, qual;
     std::vector<int64_t> off;
     std::vector<int32_t> len;
 };
@@ -311,9 +328,12 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     return 0;
 }
 
+// Upload n reads (text at seq / qual + offsets) and pack them on the device.
+// keep_host copies the text to `host`; `adopt` (the FASTQ ingest, whose
+// buffers are already laid out) moves its buffers there instead.
 static int load_reads(CtxEx &c, DevReads &dst, HostReads &host, int64_t n, int paired,
                       const uint8_t *seq, const uint8_t *qual, const int64_t *offsets,
-                      const int32_t *lens, bool keep_host)
+                      const int32_t *lens, bool keep_host, HostReads *adopt = nullptr)
 {
     if (n < 0 || (paired && (n & 1))) { set_error("reads: bad count"); return -3; }
     int max_len = 0;
@@ -359,7 +379,9 @@ static int load_reads(CtxEx &c, DevReads &dst, HostReads &host, int64_t n, int p
         MH_HIP(hipStreamSynchronize(c.stream));
         hipFree(dseq); hipFree(dqual); hipFree(doff);
     }
-    if (keep_host) {
+    if (adopt) {
+        host = std::move(*adopt);
+    } else if (keep_host) {
         host.seq.assign(seq, seq + src_total);
         host.qual.assign(qual, qual + src_total);
         host.off.assign(offsets, offsets + n);
@@ -381,11 +403,13 @@ static std::string qname_of(const char *h, size_t n, bool paired)
     return s;
 }
 
+// A FASTQ file decoded to text and indexed in place: per record the start
+// and length of its header, sequence and quality lines.
 struct Fastq {
-    std::vector<std::string> names;
-    std::vector<uint8_t> seq, qual;
-    std::vector<int32_t> len;
-    std::vector<int64_t> off;     // start of each read in seq / qual
+    std::string data;
+    std::vector<int64_t> name_at, seq_at, qual_at;
+    std::vector<int32_t> name_len, len, qual_len;
+    size_t size() const { return len.size(); }
 };
 
 int s2a_threads();   // mh_s2a_host.cpp: host worker count
@@ -400,7 +424,7 @@ static void par_for(int nt, const std::function<void(int)> &fn)
 }
 
 // The whole (gzip or plain) file; every concatenated gzip member is decoded
-// (as gzread does), with libdeflate when the system has it (mh_gunzip.cpp).
+// (as gzread does), in parallel when there are several (mh_gunzip.cpp).
 static int slurp(const char *path, std::string &data)
 {
     data.clear();
@@ -431,11 +455,11 @@ static int slurp(const char *path, std::string &data)
     return 0;
 }
 
-// FASTQ records of `data` (blank lines between records skipped), parsed
-// with the line scan and the per-record copies split over host threads.
-static int parse_fastq(const std::string &data, const char *path, Fastq &fq, bool paired,
-                       int64_t *newlines)
+// Index the FASTQ records of fq.data (blank lines between records skipped,
+// '\r' before '\n' dropped): the newline scan runs on host threads.
+static int index_fastq(Fastq &fq, const char *path, int64_t *newlines)
 {
+    const std::string &data = fq.data;
     const int64_t n = (int64_t)data.size();
     const char *D = data.data();
     const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 20) + 1));
@@ -443,6 +467,7 @@ static int parse_fastq(const std::string &data, const char *path, Fastq &fq, boo
     par_for(nt, [&](int t) {
         const int64_t a = n * t / nt, b = n * (t + 1) / nt;
         const char *p = D + a, *e = D + b;
+        ls[t].reserve((size_t)((b - a) / 60 + 16));
         while (p < e) {
             const char *nl = (const char *)memchr(p, '\n', (size_t)(e - p));
             if (!nl) break;
@@ -451,6 +476,9 @@ static int parse_fastq(const std::string &data, const char *path, Fastq &fq, boo
         }
     });
     std::vector<int64_t> nlpos;
+    size_t nn = 0;
+    for (auto &v : ls) nn += v.size();
+    nlpos.reserve(nn);
     for (auto &v : ls) nlpos.insert(nlpos.end(), v.begin(), v.end());
     if (newlines) *newlines = (int64_t)nlpos.size();
     // line k spans [start_k, end_k) without '\n' / trailing '\r'
@@ -462,6 +490,7 @@ static int parse_fastq(const std::string &data, const char *path, Fastq &fq, boo
         return e;
     };
     std::vector<int64_t> rec;   // first line of each record
+    rec.reserve((size_t)(nl / 4 + 1));
     for (int64_t k = 0; k < nl;) {
         if (lend(k) == lstart(k)) { ++k; continue; }
         if (k + 3 >= nl) { set_error("truncated FASTQ record in %s", path); return -3; }
@@ -469,50 +498,30 @@ static int parse_fastq(const std::string &data, const char *path, Fastq &fq, boo
         k += 4;
     }
     const int64_t nr = (int64_t)rec.size();
-    fq.len.resize(nr);
-    fq.off.resize(nr);
-    fq.names.resize(nr);
-    int64_t total = 0;
-    for (int64_t r = 0; r < nr; ++r) {
-        const int64_t L = lend(rec[r] + 1) - lstart(rec[r] + 1);
-        if (L > MAXLEN) { set_error("read longer than %d in %s", MAXLEN, path); return -3; }
-        fq.len[r] = (int32_t)L;
-        fq.off[r] = total;
-        total += L;
-    }
-    fq.seq.resize((size_t)total);
-    fq.qual.resize((size_t)total);
+    fq.name_at.resize(nr); fq.seq_at.resize(nr); fq.qual_at.resize(nr);
+    fq.name_len.resize(nr); fq.len.resize(nr); fq.qual_len.resize(nr);
+    std::atomic<int64_t> too_long(-1);
     par_for(nt, [&](int t) {
         for (int64_t r = nr * t / nt; r < nr * (t + 1) / nt; ++r) {
             const int64_t k = rec[r];
-            fq.names[r] = qname_of(D + lstart(k), (size_t)(lend(k) - lstart(k)), paired);
-            const int64_t L = fq.len[r];
-            memcpy(&fq.seq[fq.off[r]], D + lstart(k + 1), (size_t)L);
-            const int64_t q0 = lstart(k + 3), ql = lend(k + 3) - q0;
-            const int64_t c = std::min(L, ql);
-            if (c > 0) memcpy(&fq.qual[fq.off[r]], D + q0, (size_t)c);
-            for (int64_t x = c; x < L; ++x) fq.qual[fq.off[r] + x] = 'I';
+            fq.name_at[r] = lstart(k);
+            fq.name_len[r] = (int32_t)(lend(k) - lstart(k));
+            const int64_t L = lend(k + 1) - lstart(k + 1);
+            if (L > MAXLEN) { too_long = r; continue; }
+            fq.seq_at[r] = lstart(k + 1);
+            fq.len[r] = (int32_t)L;
+            fq.qual_at[r] = lstart(k + 3);
+            fq.qual_len[r] = (int32_t)(lend(k + 3) - lstart(k + 3));
         }
     });
+    if (too_long >= 0) { set_error("read longer than %d in %s", MAXLEN, path); return -3; }
     return 0;
 }
 
-// keep records [u0, u1) of a parsed file (their bytes stay where they are)
-static void keep_block(Fastq &fq, int64_t u0, int64_t u1)
+static int read_fastq(const char *path, Fastq &fq, int64_t *newlines = nullptr)
 {
-    fq.off.erase(fq.off.begin() + u1, fq.off.end());
-    fq.off.erase(fq.off.begin(), fq.off.begin() + u0);
-    fq.len.erase(fq.len.begin() + u1, fq.len.end());
-    fq.len.erase(fq.len.begin(), fq.len.begin() + u0);
-    fq.names.erase(fq.names.begin() + u1, fq.names.end());
-    fq.names.erase(fq.names.begin(), fq.names.begin() + u0);
-}
-
-static int read_fastq(const char *path, Fastq &fq, bool paired, int64_t *newlines = nullptr)
-{
-    std::string data;
-    if (int st = slurp(path, data)) return st;
-    return parse_fastq(data, path, fq, paired, newlines);
+    if (int st = slurp(path, fq.data)) return st;
+    return index_fastq(fq, path, newlines);
 }
 
 }  // namespace mh
@@ -686,81 +695,64 @@ int mh_reads_load_fastq_part(mh_ctx *ctx, const char *path1, const char *path2, 
     int64_t lines1 = 0;
     int st2 = 0;
     std::string err2;
-    // the two files are decoded concurrently (gzip inflate is serial per file)
+    // the two files are decoded concurrently
     std::thread t2;
     if (paired)
         t2 = std::thread([&]() {
-            st2 = read_fastq(path2, b, paired);
+            st2 = read_fastq(path2, b);
             if (st2) err2 = last_error_text();
         });
-    const int st1 = read_fastq(path1, a, paired, &lines1);
+    const int st1 = read_fastq(path1, a, &lines1);
     if (paired) t2.join();
     if (st1) return st1;
     if (st2) { set_error("%s", err2.c_str()); return st2; }
-    std::vector<std::string> names;
-    std::vector<uint8_t> seq, qual;
-    std::vector<int64_t> off;
-    std::vector<int32_t> len;
-    if (paired && a.len.size() != b.len.size()) {
-        set_error("paired FASTQ files hold %zu and %zu reads", a.len.size(), b.len.size());
+    if (paired && a.size() != b.size()) {
+        set_error("paired FASTQ files hold %zu and %zu reads", a.size(), b.size());
         return -3;
     }
     // this part's contiguous block of units (pairs, or reads when unpaired):
     // [U * part / parts, U * (part + 1) / parts), so every unit is in one
     // block and the blocks differ in size by at most one
-    const int64_t units_all = (int64_t)a.len.size();
+    const int64_t units_all = (int64_t)a.size();
     const int64_t u0 = units_all * part / parts, u1 = units_all * (part + 1) / parts;
     if (first_unit) *first_unit = u0;
-    if (parts > 1) {
-        keep_block(a, u0, u1);
-        if (paired) keep_block(b, u0, u1);
+    // the block's reads (mates interleaved) copied once from the decoded
+    // text into the buffers the context keeps for the SAM text
+    const int per = paired ? 2 : 1;
+    const int64_t n = per * (u1 - u0);
+    HostReads h;
+    h.off.resize((size_t)n);
+    h.len.resize((size_t)n);
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const Fastq &f = (paired && (i & 1)) ? b : a;
+        h.off[i] = total;
+        h.len[i] = f.len[u0 + i / per];
+        total += h.len[i];
     }
-    if (paired) {
-        const int64_t np = (int64_t)a.len.size();
-        off.resize(2 * np);
-        len.resize(2 * np);
-        names.resize(2 * np);
-        int64_t total = 0;
-        for (int64_t i = 0; i < np; ++i) {
-            off[2 * i] = total; len[2 * i] = a.len[i]; total += a.len[i];
-            off[2 * i + 1] = total; len[2 * i + 1] = b.len[i]; total += b.len[i];
+    h.seq.alloc((size_t)total);
+    h.qual.alloc((size_t)total);
+    std::vector<std::string> names((size_t)n);
+    const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
+    par_for(nt, [&](int t) {
+        for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
+            const Fastq &f = (paired && (i & 1)) ? b : a;
+            const int64_t r = u0 + i / per;
+            const char *D = f.data.data();
+            names[i] = qname_of(D + f.name_at[r], (size_t)f.name_len[r], paired);
+            const int64_t L = h.len[i];
+            memcpy(h.seq.data() + h.off[i], D + f.seq_at[r], (size_t)L);
+            const int64_t c = std::min<int64_t>(L, f.qual_len[r]);
+            if (c > 0) memcpy(h.qual.data() + h.off[i], D + f.qual_at[r], (size_t)c);
+            for (int64_t x = c; x < L; ++x) h.qual.data()[h.off[i] + x] = 'I';
         }
-        seq.resize((size_t)total);
-        qual.resize((size_t)total);
-        const int nt = std::max(1, std::min(s2a_threads(), (int)(np >> 14) + 1));
-        par_for(nt, [&](int t) {
-            for (int64_t i = np * t / nt; i < np * (t + 1) / nt; ++i) {
-                memcpy(&seq[off[2 * i]], &a.seq[a.off[i]], (size_t)a.len[i]);
-                memcpy(&qual[off[2 * i]], &a.qual[a.off[i]], (size_t)a.len[i]);
-                memcpy(&seq[off[2 * i + 1]], &b.seq[b.off[i]], (size_t)b.len[i]);
-                memcpy(&qual[off[2 * i + 1]], &b.qual[b.off[i]], (size_t)b.len[i]);
-                names[2 * i].swap(a.names[i]);
-                names[2 * i + 1].swap(b.names[i]);
-            }
-        });
-    } else if (parts > 1) {   // the block's reads, packed from offset 0
-        const int64_t nr = (int64_t)a.len.size();
-        off.resize(nr);
-        len.assign(a.len.begin(), a.len.end());
-        int64_t total = 0;
-        for (int64_t i = 0; i < nr; ++i) { off[i] = total; total += a.len[i]; }
-        seq.resize((size_t)total);
-        qual.resize((size_t)total);
-        for (int64_t i = 0; i < nr; ++i) {
-            memcpy(&seq[off[i]], &a.seq[a.off[i]], (size_t)a.len[i]);
-            memcpy(&qual[off[i]], &a.qual[a.off[i]], (size_t)a.len[i]);
-        }
-        names.swap(a.names);
-    } else {
-        off.swap(a.off);
-        len.swap(a.len);
-        seq.swap(a.seq);
-        qual.swap(a.qual);
-        names.swap(a.names);
-    }
-    const int64_t n = (int64_t)len.size();
-    int st = load_reads(*c, c->reads, c->host, n, paired, seq.data(), qual.data(), off.data(),
-                        len.data(), true);
+    });
+    a = Fastq{};
+    b = Fastq{};
+    const uint8_t *sq = h.seq.data(), *ql = h.qual.data();
+    const int64_t *of = h.off.data();
+    const int32_t *ln = h.len.data();
+    int st = load_reads(*c, c->reads, c->host, n, paired, sq, ql, of, ln, false, &h);
     if (st) return st;
     c->names.swap(names);
     c->map.valid = false;
@@ -945,20 +937,62 @@ int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20)
 }
 
 // decimal text of v appended to out (no locale, no allocation)
-static inline void put_int(std::string &out, int64_t v)
+// decimal text of v at o; returns the end
+static inline char *put_int(char *o, int64_t v)
 {
     char t[24];
     int n = 0;
     uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
     do { t[n++] = (char)('0' + u % 10); u /= 10; } while (u);
-    if (v < 0) out.push_back('-');
-    while (n) out.push_back(t[--n]);
+    if (v < 0) *o++ = '-';
+    while (n) *o++ = t[--n];
+    return o;
 }
 
-// One row of SAM (style 0) or CSV (style 1) text, appended to out.
+static inline char *put_str(char *o, const char *s, size_t n)
+{
+    std::memcpy(o, s, n);
+    return o + n;
+}
+
+// csv.writer QUOTE_MINIMAL (csv_field) into a buffer with room for 2n + 2
+static inline char *put_csv(char *o, const char *s, size_t n)
+{
+    bool quote = false;
+    for (size_t i = 0; i < n; ++i) {
+        const char ch = s[i];
+        quote |= ch == ',' || ch == '"' || ch == '\n' || ch == '\r';
+    }
+    if (!quote) return put_str(o, s, n);
+    *o++ = '"';
+    for (size_t i = 0; i < n; ++i) {
+        if (s[i] == '"') *o++ = '"';
+        *o++ = s[i];
+    }
+    *o++ = '"';
+    return o;
+}
+
+// bowtie2 prints a read's bases as ACGTN, reverse-complemented on the
+// reverse strand (code_of: a/c/g/t in either case, anything else N)
+struct BaseTables {
+    char fw[256], rc[256];
+    BaseTables()
+    {
+        for (int ch = 0; ch < 256; ++ch) {
+            const uint8_t cd = code_of((char)ch);
+            fw[ch] = "ACGTN"[cd];
+            rc[ch] = "TGCAN"[cd];
+        }
+    }
+};
+static const BaseTables kBases;
+
+// One row of SAM (style 0) or CSV (style 1) text, appended to out at *used
+// (out grows as needed; it is not zero-filled beyond what is written).
 static void format_row(const CtxEx *c, int style, const Rec &a, int64_t r, const uint32_t *pool,
-                       const char *const *refnames, std::string &out, std::string &seq,
-                       std::string &qual)
+                       const char *const *refnames, const size_t *refname_len, std::string &out,
+                       size_t &used, std::string &tmp)
 {
     static const char *ytn[4] = {"CP", "DP", "UP", "UU"};
     static const char *yfn[3] = {"", "NS", "LN"};
@@ -966,72 +1000,183 @@ static void format_row(const CtxEx *c, int style, const Rec &a, int64_t r, const
     const int L = c->host.len[r];
     const uint8_t *s = c->host.seq.data() + c->host.off[r];
     const uint8_t *q = c->host.qual.data() + c->host.off[r];
-    seq.resize(L);
-    qual.resize(L);
-    const bool rev = a.ref >= 0 && a.rev;
-    for (int x = 0; x < L; ++x) {
-        const uint8_t cd = code_of((char)s[x]);
-        if (rev) {
-            seq[L - 1 - x] = "TGCAN"[cd];
-            qual[L - 1 - x] = (char)q[x];
-        } else {
-            seq[x] = "ACGTN"[cd];
-            qual[x] = (char)q[x];
-        }
-    }
-    auto put = [&](const char *p, size_t len) {
-        if (style == 1) csv_field(out, p, len); else out.append(p, len);
-    };
     const std::string &qn = c->names[r];
-    put(qn.data(), qn.size());
-    out.push_back(sep);
-    put_int(out, a.flag);
-    out.push_back(sep);
     const char *rn = a.sam_ref >= 0 ? refnames[a.sam_ref] : "*";
-    put(rn, std::strlen(rn));
-    out.push_back(sep);
-    put_int(out, a.sam_pos);
-    out.push_back(sep);
-    put_int(out, a.mapq);
-    out.push_back(sep);
+    const size_t rnl = a.sam_ref >= 0 ? refname_len[a.sam_ref] : 1;
+    const size_t nxl = a.rnext >= 0 ? refname_len[a.rnext] : 1;
+    const size_t bound = 2 * qn.size() + 2 * rnl + 2 * nxl + 3 * (size_t)L + 8 +
+                         12 * (size_t)(a.ref >= 0 ? a.n_cigar : 1) + 16 * 12 + 160;
+    if (used + bound > out.size()) out.resize(std::max(out.size() * 2, used + bound));
+    char *o = &out[used];
+    const bool rev = a.ref >= 0 && a.rev;
+    o = style == 1 ? put_csv(o, qn.data(), qn.size()) : put_str(o, qn.data(), qn.size());
+    *o++ = sep;
+    o = put_int(o, a.flag);
+    *o++ = sep;
+    o = style == 1 ? put_csv(o, rn, rnl) : put_str(o, rn, rnl);
+    *o++ = sep;
+    o = put_int(o, a.sam_pos);
+    *o++ = sep;
+    o = put_int(o, a.mapq);
+    *o++ = sep;
     if (a.ref < 0) {
-        out.push_back('*');
+        *o++ = '*';
     } else {
         for (int z = 0; z < a.n_cigar; ++z) {
             const uint32_t op = pool[a.cig_off + z];
-            put_int(out, op >> 4);
-            out.push_back("MIDxS"[op & 7]);
+            o = put_int(o, op >> 4);
+            *o++ = "MIDxS"[op & 7];
         }
     }
-    out.push_back(sep);
-    if (a.rnext == -2) out.push_back('*');
-    else if (a.rnext == -1) out.push_back('=');
-    else put(refnames[a.rnext], std::strlen(refnames[a.rnext]));
-    out.push_back(sep);
-    put_int(out, a.pnext);
-    out.push_back(sep);
-    put_int(out, a.tlen);
-    out.push_back(sep);
-    if (L == 0) out.push_back('*'); else put(seq.data(), seq.size());
-    out.push_back(sep);
-    if (L == 0) out.push_back('*'); else put(qual.data(), qual.size());
+    *o++ = sep;
+    if (a.rnext == -2) *o++ = '*';
+    else if (a.rnext == -1) *o++ = '=';
+    else o = style == 1 ? put_csv(o, refnames[a.rnext], nxl) : put_str(o, refnames[a.rnext], nxl);
+    *o++ = sep;
+    o = put_int(o, a.pnext);
+    *o++ = sep;
+    o = put_int(o, a.tlen);
+    *o++ = sep;
+    if (L == 0) {
+        *o++ = '*';
+        *o++ = sep;
+        *o++ = '*';
+    } else {
+        // SEQ has no character csv quotes; QUAL may (',' is Phred 11)
+        if (rev) for (int x = 0; x < L; ++x) o[L - 1 - x] = kBases.rc[s[x]];
+        else for (int x = 0; x < L; ++x) o[x] = kBases.fw[s[x]];
+        o += L;
+        *o++ = sep;
+        const char *qq = (const char *)q;
+        if (rev) {
+            tmp.resize((size_t)L);
+            for (int x = 0; x < L; ++x) tmp[L - 1 - x] = (char)q[x];
+            qq = tmp.data();
+        }
+        o = style == 1 ? put_csv(o, qq, (size_t)L) : put_str(o, qq, (size_t)L);
+    }
     if (style == 0) {
+        auto tag = [&](const char *t, int64_t v) { o = put_str(o, t, std::strlen(t)); o = put_int(o, v); };
         if (a.ref >= 0) {
-            out += "\tAS:i:"; put_int(out, a.score);
-            if (a.secbest != I32MIN) { out += "\tXS:i:"; put_int(out, a.secbest); }
-            out += "\tXN:i:0\tXM:i:"; put_int(out, a.xm);
-            out += "\tXO:i:"; put_int(out, a.xo);
-            out += "\tXG:i:"; put_int(out, a.xg);
-            out += "\tNM:i:"; put_int(out, a.nm);
-            if (a.ys != I32MIN) { out += "\tYS:i:"; put_int(out, a.ys); }
+            tag("\tAS:i:", a.score);
+            if (a.secbest != I32MIN) tag("\tXS:i:", a.secbest);
+            tag("\tXN:i:0\tXM:i:", a.xm);
+            tag("\tXO:i:", a.xo);
+            tag("\tXG:i:", a.xg);
+            tag("\tNM:i:", a.nm);
+            if (a.ys != I32MIN) tag("\tYS:i:", a.ys);
         } else {
-            if (a.ys != I32MIN) { out += "\tYS:i:"; put_int(out, a.ys); }
-            if (a.yf) { out += "\tYF:Z:"; out += yfn[a.yf]; }
+            if (a.ys != I32MIN) tag("\tYS:i:", a.ys);
+            if (a.yf) { o = put_str(o, "\tYF:Z:", 6); o = put_str(o, yfn[a.yf], 2); }
         }
-        out += "\tYT:Z:";
-        out += ytn[a.yt & 3];
+        o = put_str(o, "\tYT:Z:", 6);
+        o = put_str(o, ytn[a.yt & 3], 2);
     }
-    out.push_back('\n');
+    *o++ = '\n';
+    used = (size_t)(o - out.data());
+}
+
+// The text of rows first .. first+n (or order[first ..]) as one chunk per
+// host thread, in order.
+static int format_chunks(CtxEx *c, int style, const int64_t *order, int64_t first, int64_t n,
+                         const char *const *refnames, std::vector<std::string> &chunks)
+{
+    std::vector<Rec> rec;
+    std::vector<uint32_t> pool;
+    if (order) {
+        if (int st = fetch_recs(c, 0, c->map.n_reads, rec, pool)) return st;
+        for (int64_t k = 0; k < n; ++k)
+            if (order[first + k] < 0 || order[first + k] >= c->map.n_reads) {
+                set_error("format order index out of range");
+                return -3;
+            }
+    } else if (int st = fetch_recs(c, first, n, rec, pool)) {
+        return st;
+    }
+    std::vector<size_t> rn_len(c->index.n_refs > 0 ? (size_t)c->index.n_refs : 1, 0);
+    for (int k = 0; k < c->index.n_refs; ++k) rn_len[k] = std::strlen(refnames[k]);
+    const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
+    chunks.assign(nt, std::string());
+    par_for(nt, [&](int t) {
+        const int64_t k0 = n * t / nt, k1 = n * (t + 1) / nt;
+        std::string &out = chunks[t];
+        size_t used = 0;
+        std::string tmp;
+        for (int64_t k = k0; k < k1; ++k) {
+            const int64_t r = order ? order[first + k] : first + k;
+            format_row(c, style, order ? rec[r] : rec[k], r, pool.data(), refnames, rn_len.data(),
+                       out, used, tmp);
+        }
+        out.resize(used);
+    });
+    return 0;
+}
+
+int mh_write_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
+                  const char *const *refnames, int fd, int64_t offset, int64_t *written)
+{
+    if (!ctx || !refnames || (style != 0 && style != 1) || fd < 0 || offset < 0) return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    if ((int64_t)c->names.size() != c->reads.n) { set_error("no read names loaded"); return -3; }
+    std::vector<std::string> chunks;
+    if (int st = format_chunks(c, style, order, first, n, refnames, chunks)) return st;
+    std::vector<int64_t> at(chunks.size() + 1, offset);
+    for (size_t t = 0; t < chunks.size(); ++t) at[t + 1] = at[t] + (int64_t)chunks[t].size();
+    std::atomic<int> bad(0);
+    par_for((int)chunks.size(), [&](int t) {
+        const char *p = chunks[t].data();
+        size_t left = chunks[t].size();
+        int64_t pos = at[t];
+        while (left > 0) {
+            const ssize_t w = pwrite(fd, p, left, (off_t)pos);
+            if (w <= 0) { bad = errno ? errno : EIO; return; }
+            p += w; left -= (size_t)w; pos += w;
+        }
+    });
+    if (bad) { set_error("mh_write_rows: write failed (%s)", strerror(bad.load())); return -4; }
+    if (written) *written = at.back() - offset;
+    return 0;
+}
+
+// crc32 and adler32 of a whole open file (zlib's, combined over chunks read
+// on host threads): (crc32 << 32) | adler32, and its size.
+int mh_file_checksum(int fd, int64_t *size, uint64_t *sum)
+{
+    if (fd < 0 || !sum) return -3;
+    struct stat st;
+    if (fstat(fd, &st) != 0) { set_error("mh_file_checksum: fstat failed"); return -4; }
+    const int64_t n = (int64_t)st.st_size;
+    const int64_t CH = (int64_t)16 << 20;
+    const int64_t nc = (n + CH - 1) / CH;
+    std::vector<uLong> crc((size_t)std::max<int64_t>(nc, 1)), adl((size_t)std::max<int64_t>(nc, 1));
+    std::atomic<int64_t> next(0);
+    std::atomic<int> bad(0);
+    const int nt = std::max(1, std::min<int>(s2a_threads(), (int)std::max<int64_t>(nc, 1)));
+    par_for(nt, [&](int) {
+        std::vector<unsigned char> buf((size_t)CH);
+        for (int64_t k; (k = next.fetch_add(1)) < nc;) {
+            const int64_t a = k * CH, len = std::min(CH, n - a);
+            int64_t got = 0;
+            while (got < len) {
+                const ssize_t r = pread(fd, buf.data() + got, (size_t)(len - got), (off_t)(a + got));
+                if (r <= 0) { bad = 1; return; }
+                got += r;
+            }
+            crc[k] = crc32(crc32(0L, Z_NULL, 0), buf.data(), (uInt)len);
+            adl[k] = adler32(adler32(0L, Z_NULL, 0), buf.data(), (uInt)len);
+        }
+    });
+    if (bad) { set_error("mh_file_checksum: read failed"); return -4; }
+    uLong c0 = crc32(0L, Z_NULL, 0), a0 = adler32(0L, Z_NULL, 0);
+    for (int64_t k = 0; k < nc; ++k) {
+        const int64_t len = std::min(CH, n - k * CH);
+        c0 = crc32_combine(c0, crc[k], (z_off_t)len);
+        a0 = adler32_combine(a0, adl[k], (z_off_t)len);
+    }
+    if (size) *size = n;
+    *sum = ((uint64_t)(c0 & 0xffffffffu) << 32) | (uint64_t)(a0 & 0xffffffffu);
+    return 0;
 }
 
 int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
@@ -1055,31 +1200,8 @@ int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, 
         c->fmt_valid = false;
         return 0;
     }
-    std::vector<Rec> rec;
-    std::vector<uint32_t> pool;
-    if (order) {
-        if (int st = fetch_recs(c, 0, c->map.n_reads, rec, pool)) return st;
-        for (int64_t k = 0; k < n; ++k)
-            if (order[first + k] < 0 || order[first + k] >= c->map.n_reads) {
-                set_error("format order index out of range");
-                return -3;
-            }
-    } else if (int st = fetch_recs(c, first, n, rec, pool)) {
-        return st;
-    }
-    // contiguous row ranges on host threads, one text chunk each, in order
-    const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
-    std::vector<std::string> chunks(nt);
-    par_for(nt, [&](int t) {
-        const int64_t k0 = n * t / nt, k1 = n * (t + 1) / nt;
-        std::string &out = chunks[t];
-        out.reserve((size_t)(k1 - k0) * 640);
-        std::string seq, qual;
-        for (int64_t k = k0; k < k1; ++k) {
-            const int64_t r = order ? order[first + k] : first + k;
-            format_row(c, style, order ? rec[r] : rec[k], r, pool.data(), refnames, out, seq, qual);
-        }
-    });
+    std::vector<std::string> chunks;
+    if (int st = format_chunks(c, style, order, first, n, refnames, chunks)) return st;
     size_t total = 0;
     for (const std::string &t : chunks) total += t.size();
     if (used) *used = total;

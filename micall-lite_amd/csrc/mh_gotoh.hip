@@ -1,23 +1,37 @@
 // mh_gotoh.hip -- the _gotoh2 aligner (micall/alignment/src/_gotoh2.c) on
 // gfx950, used by the consensus-distance filter (remap.py:244-263: global,
 // gop 15, gep 3, HYPHY_NUC) and aln2counts' coordinate mapping (local,
-// EmpHIV25).  A batch of alignments is one launch, one workgroup of 1024
-// threads per alignment (blockIdx.x = alignment), each with its own scratch:
-//   phase 1  cost assignment (_gotoh2.c:137-201) by anti-diagonals; R/P/Q
-//            live in three rolling diagonal buffers in LDS (with both
-//            sequences' codes and the score matrix; in global memory when a
-//            sequence is too long for LDS); each cell's tie bits go to three
-//            byte planes so no two cells of a diagonal write the same byte:
-//            abc(i,j) by (i,j), de(i,j) by (i+1,j), fg(i,j) by (i,j+1)
-//   phase 2  Altschul-Erickson edge assignment (:205-313) by anti-diagonals
-//            in reverse; its writes to d(i+1,j) and f(i,j+1) are never read
-//            again (each cell reads its own d/f before its upper/left
-//            neighbour runs) and are dropped
-//   phase 3  traceback (:316-438) by one thread.
+// EmpHIV25).  A batch of alignments is three launches.
+//
+// The DP grid (rows 0..m of seq1, columns 0..n of seq2) is cut into strips
+// of 64 rows, one wave (one workgroup) each, spread over the whole GPU.  In
+// a strip lane l owns row 64k + l and steps along the columns skewed by its
+// lane (at step t it is at column t - l), so the cell above a lane's cell is
+// the lane before it one step earlier and the cell up-left two steps
+// earlier: both arrive by one DPP lane shift, and a step needs no barrier.
+// Every step's 64 cells lie on one anti-diagonal.  A strip's first lane
+// takes the row above it from the strip before, which is running a few
+// dozen columns ahead: the last row of every strip goes to global memory
+// and is published in blocks of 32 columns (a per-strip progress counter,
+// release / acquire at device scope); the reader loads a block ahead.
+// Strips are taken by ticket (one atomic counter), in the order their
+// dependencies run, so a strip only ever waits for one already running.
+//   k_gotoh_fwd  cost assignment (_gotoh2.c:137-201): R/P/Q in registers,
+//                each cell's tie bits to three byte planes: abc(i,j) by
+//                (i,j), de(i,j) by (i+1,j), fg(i,j) by (i,j+1)
+//   k_gotoh_bwd  Altschul-Erickson edge assignment (:205-313), lane l at
+//                column n + 63 - l - t, strips bottom-up; a cell's final
+//                bits reach the lane above one step later and the strip
+//                above through its first row; its writes to d(i+1,j) and
+//                f(i,j+1) are never read again (each cell reads its own d/f
+//                before its upper/left neighbour runs) and are dropped
+//   k_gotoh_tb   traceback (:316-438) by one thread over LDS windows.
 // The planes are stored anti-diagonal-major over the (m+2) x (n+2) grid
-// (doff[s] = first byte of diagonal s, cells by row i): the cells a
-// diagonal step touches are consecutive bytes, so every plane access of a
-// step is coalesced (row-major planes put each thread on its own cache line).
+// (doff[s] = first byte of diagonal s, cells by row i), so a step's plane
+// bytes are consecutive; they are written and read through buffer
+// resources: the diagonal base is a scalar offset, a lane's row its vector
+// offset, and a lane with no cell this step points past the buffer (the
+// hardware drops the store / returns 0) instead of branching.
 // Bit-for-bit specification: oracle/og_gotoh.c.
 #include <limits.h>
 
@@ -30,20 +44,14 @@ namespace mh {
 
 constexpr int G_INF = INT_MAX;
 enum { GA = 1, GB = 2, GC = 4, GD = 8, GE_ = 16, GF = 32, GG = 64 };
-constexpr int GOTOH_THREADS = 1024;
-constexpr size_t GOTOH_LDS_MAX = 160 * 1024 - 256;   // (the traceback's static LDS)
-constexpr int GOTOH_PF = 4;   // LDS variant: cells per thread per diagonal (m < GOTOH_PF * 1024)
-
-// LDS variant layout: R/P/Q rolling diagonals 9 (m+2) ints, the L x L
-// matrix, seq1 codes, seq2 codes; phase 2 reuses the R/P/Q space for the
-// final abc of 3 diagonals
-__host__ __device__ inline size_t gotoh_al16(size_t x) { return (x + 15) & ~(size_t)15; }
-__host__ __device__ inline size_t gotoh_codes_end(int m, int n, int L)
-{
-    return sizeof(int) * (9 * (size_t)(m + 2) + (size_t)L * L) + gotoh_al16(m) + gotoh_al16(n);
-}
+constexpr int GOTOH_THREADS = 1024;        // k_gotoh_tb
+constexpr int GBLK = 32;                   // boundary columns published / awaited at a time
+constexpr int GBC_MAX = 32 * 1024;         // seq2 codes kept in LDS up to this length
+constexpr uint32_t GOOB = 0x80000000u;     // a buffer offset past every plane (planes < 2 GiB)
 constexpr int TB = 128;                                // traceback window (diagonals x rows)
 constexpr size_t TB_LDS = (size_t)TB * TB + 2 * TB;   // window + both sequences' characters
+
+__host__ __device__ inline size_t gotoh_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 struct GotohArgs {
     const int8_t *a;      // seq1 codes, m
@@ -51,34 +59,27 @@ struct GotohArgs {
     int m, n, L;
     const int *mat;       // L x L
     int u, v, is_global;
-    int *diagR, *diagP, *diagQ;   // 3 x (m + 2) each (global variant)
     int *lastcol, *lastrow;       // R(i, n), R(m, j)
-    uint8_t *abc, *de, *fg;       // (m+2) x (n+2), anti-diagonal-major
+    uint8_t *bits;                // (m+2) x (n+2) tie bits a..g of every cell, anti-diagonal-major
+    uint8_t *rowde;               // d / e bits of every strip's last row (strips x (n+1))
+    unsigned long long *brow1;    // k_gotoh_fwd: R, P of every strip's last row (strips x (n+1))
+    int *brow2;                   // k_gotoh_bwd: final abc of every strip's first row, by n - j
+    int *prog;                    // per strip: boundary columns published (fwd, then bwd)
+    int *flags;                   // [0] a wait timed out
     const char *s1, *s2;
     char *out1, *out2;            // m + n + 1
     int *result;                  // [0] status, [1] score, [2] length
 };
 
+// the strips of a batch, in ticket order (alignment-major)
+struct GotohStrips {
+    const GotohArgs *args;
+    const int *first;             // per alignment: its first ticket; [count] = total
+    int count;
+    int *ticket;                  // [0] fwd, [1] bwd
+};
+
 __device__ __forceinline__ int gmin(int x, int y) { return x <= y ? x : y; }
-
-// A workgroup barrier that orders LDS only.  __syncthreads() is also a
-// workgroup release fence for global memory, so every wave would wait for
-// its plane stores (and prefetch loads) to land at each anti-diagonal step;
-// the steps of the LDS variant never read back a global value written by
-// another step, so they only need the LDS ordering.
-__device__ __forceinline__ void lds_barrier()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-template <bool LDS>
-__device__ __forceinline__ void step_barrier()
-{
-    if (LDS) lds_barrier();
-    else __syncthreads();   // rolling diagonals in global memory
-}
 
 // First plane byte of anti-diagonal s of the (M+1) x (N+1) grid (M = m+1,
 // N = n+1): the sum of len(t) = min(t, M) - max(0, t - N) + 1 over t < s.
@@ -89,6 +90,12 @@ __host__ __device__ __forceinline__ int64_t doff_of(int64_t s, int64_t M, int64_
     return s + s1 - s2;
 }
 
+// cells of anti-diagonal s of the plane grid
+__host__ __device__ __forceinline__ int64_t dlen(int64_t s, int64_t M, int64_t N)
+{
+    return (s < M ? s : M) - (s - N > 0 ? s - N : 0) + 1;
+}
+
 // plane base of diagonal s, indexed by row i: diagonal s starts at row
 // max(0, s - (n+1))
 __device__ __forceinline__ int64_t dbase(int s, int m, int n)
@@ -97,169 +104,330 @@ __device__ __forceinline__ int64_t dbase(int s, int m, int n)
     return doff_of(s, m + 1, n + 1) - lo;
 }
 
-__device__ __forceinline__ size_t pidx(const GotohArgs &A, int i, int j)
+// lane l <- lane l - 1 (lane 0 keeps old) / lane l <- lane l + 1 (lane 63 keeps old)
+__device__ __forceinline__ int from_prev_lane(int old, int v)
 {
-    return (size_t)(dbase(i + j, A.m, A.n) + i);
+    return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int from_next_lane(int old, int v)
+{
+    return __builtin_amdgcn_update_dpp(old, v, 0x130, 0xF, 0xF, false);
 }
 
-template <bool LDS>
-__global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh(const GotohArgs *batch)
+// a wave-uniform value the compiler cannot prove uniform (loaded through a
+// pointer), moved to scalar registers
+template <class T>
+__device__ __forceinline__ T uni(T v)
+{
+    static_assert(sizeof(T) == 8 || sizeof(T) == 4, "uni: 4 or 8 bytes");
+    if constexpr (sizeof(T) == 8) {
+        uint64_t x;
+        __builtin_memcpy(&x, &v, 8);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+        x = (uint64_t)hi << 32 | lo;
+        __builtin_memcpy(&v, &x, 8);
+    } else {
+        uint32_t x;
+        __builtin_memcpy(&x, &v, 4);
+        x = __builtin_amdgcn_readfirstlane(x);
+        __builtin_memcpy(&v, &x, 4);
+    }
+    return v;
+}
+
+// a buffer resource over bytes [p, p + bytes): the base and size are
+// wave-uniform, so the descriptor lives in scalar registers
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc((void *)uni(p), (short)0, (int)uni(bytes), 0x00020000);
+}
+
+// Progress of a strip's boundary row (device scope: strips run on any CU).
+// A wait that outlasts any legitimate one (~0.25 s) sets flags[0] and gives
+// up, so a broken protocol ends the launch with an error instead of hanging.
+constexpr int GWAIT_MAX = 1 << 23;
+__device__ __forceinline__ void prog_wait(const int *c, int need, int *flags)
+{
+    for (int it = 0;; ++it) {
+        const int have = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (have >= need) return;
+        if (it >= GWAIT_MAX ||
+            __builtin_amdgcn_readfirstlane(__hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            __hip_atomic_store(flags, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+__device__ __forceinline__ void prog_publish(int *c, int v)
+{
+    // the boundary cells before it were stored with device-coherent (sc1)
+    // stores: once they have completed the counter may be seen.  (A release
+    // fence at agent scope would also write back this XCD's whole L2, plane
+    // stores included.)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// boundary cells: device-coherent loads / stores (another strip, on any XCD,
+// reads them while this launch runs)
+template <class T>
+__device__ __forceinline__ T dev_load(const T *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void dev_store(T *p, T v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the strip of ticket u: (alignment, index in ticket order)
+__device__ __forceinline__ void strip_of(const GotohStrips &S, int u, int &t, int &q)
+{
+    int lo = 0, hi = S.count;   // first[lo] <= u < first[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (S.first[mid] <= u) lo = mid; else hi = mid;
+    }
+    t = lo;
+    q = u - S.first[lo];
+}
+
+// a boundary cell (R, P) as one 64-bit word
+__device__ __forceinline__ unsigned long long rp_pack(int r, int p)
+{
+    return (unsigned long long)(uint32_t)r | (unsigned long long)(uint32_t)p << 32;
+}
+
+// Cost assignment of one strip.  Every cell's seven tie bits go to ONE plane
+// byte, stored one step late: at step t lane l holds abc of (i, j - 1) from
+// the step before, computes fg of (i, j - 1) itself (from cell (i, j)) and
+// gets de of (i, j - 1) from the lane below (cell (i + 1, j - 1)) by a lane
+// shift.  The strip's last row gets its de bits from the next strip's first
+// lane, which stores them in a side row (rowde).
+template <bool BCL>   // seq2's codes in LDS (else read from global memory every step)
+__global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
+    const int lane = threadIdx.x;
+    int u = 0;
+    if (lane == 0) u = atomicAdd(&S.ticket[0], 1);
+    u = __builtin_amdgcn_readfirstlane(__shfl(u, 0));
+    int ta, k;
+    strip_of(S, u, ta, k);
+    const GotohArgs &A = S.args[ta];
+    const int m = uni(A.m), n = uni(A.n), L = uni(A.L), uu = uni(A.u), v = uni(A.v);
+    const bool glob = uni(A.is_global);
+    int *mat = (int *)gsm;
+    int8_t *bcl = (int8_t *)(gsm + gotoh_al16(sizeof(int) * L * L));
+    for (int x = lane; x < L * L; x += 64) mat[x] = A.mat[x];
+    if (BCL)
+        for (int x = lane; x < n; x += 64) bcl[x] = A.b[x];
+    __syncthreads();
+    const int ns = (m + 1 + 63) / 64;
+    const int W1 = n + 1;
+    const int64_t cells = (int64_t)(m + 2) * (n + 2);
+    const __amdgpu_buffer_rsrc_t rbits = brsrc(A.bits, (uint32_t)cells);
+    const __amdgpu_buffer_rsrc_t rcol = brsrc(A.lastcol, 4u * (m + 1)), rrow = brsrc(A.lastrow, 4u * (n + 1));
+    const int i = 64 * k + lane;
+    const bool rowok = i <= m;
+    const int arow = (i >= 1 && rowok) ? A.a[i - 1] * L : 0;
+    const bool produce = k + 1 < ns, consume = k > 0;
+    const unsigned long long *above = A.brow1 + (size_t)(k - 1) * W1;   // row 64k - 1
+    unsigned long long *below = A.brow1 + (size_t)k * W1;
+    // de bits of row 64k - 1 (the strip above's last row), by column
+    const __amdgpu_buffer_rsrc_t rside = brsrc(A.rowde + (size_t)(k - 1) * W1, consume ? (uint32_t)W1 : 0u);
+    const int *pabove = A.prog + (k - 1), *flags = A.flags;
+    int *pme = A.prog + k;
+    int Rme = 0, Pme = G_INF, Qme = G_INF;   // this lane's cell of the last step: (i, j - 1)
+    int Rdg = 0;                              // R(i - 1, j - 1): the row above one step ago
+    int bcode = 0;                            // seq2 code of column j - 1
+    int abcp = 0;                             // abc of (i, j - 1), stored this step
+    unsigned long long blk = rp_pack(0, G_INF);   // lanes 0..31: the row above, this block's columns
+    // plane bases of diagonals s = 64 k + t and s - 1, kept running:
+    // D(s + 1) = D(s) + len(s)
+    int64_t Ds = doff_of(64 * k, m + 1, n + 1);
+    int64_t Dprev = Ds - (k > 0 ? dlen(64 * k - 1, m + 1, n + 1) : 0);
+    for (int t = 0; t <= n + 64; ++t) {
+        const int j = t - lane;
+        const int tq = t & (GBLK - 1);
+        if (consume && tq == 0 && t <= n) {
+            // this block of the row above: wait for it, load it, and use it
+            // at once (the wait then covers the load only here, not at
+            // every step's read)
+            prog_wait(pabove, t + GBLK < W1 ? t + GBLK : W1, (int *)flags);
+            if (lane < GBLK && t + lane < W1) blk = dev_load(above + t + lane);
+            asm volatile("; touch %0" : "+v"(blk));
+        }
+        int Rup = from_prev_lane(0, Rme), Pup = from_prev_lane(G_INF, Pme);
+        const int bnew = (t >= 1 && t <= n) ? (BCL ? (int)bcl[t - 1] : (int)A.b[t - 1]) : 0;
+        bcode = from_prev_lane(bnew, bcode);
+        if (consume && t <= n) {
+            const int r0 = __builtin_amdgcn_readlane((int)(uint32_t)blk, tq);
+            const int p0 = __builtin_amdgcn_readlane((int)(uint32_t)(blk >> 32), tq);
+            Rup = lane == 0 ? r0 : Rup;
+            Pup = lane == 0 ? p0 : Pup;
+        }
+        const bool act = rowok && j >= 0 && j <= n;
+        const bool top = i == 0, left = j == 0;
+        const int pm = gmin(Pup, Rup + v);
+        const int p = top ? G_INF : uu + pm;
+        const int qm = gmin(Qme, Rme + v);
+        const int q = left ? G_INF : uu + qm;
+        // de of (i - 1, j) and fg of (i, j - 1)
+        const int de = (act && !top) ? ((Pup != G_INF && pm == Pup) ? GD : 0) | (pm == Rup + v ? GE_ : 0) : 0;
+        const int fg = (act && !left) ? ((Qme != G_INF && qm == Qme) ? GF : 0) | (qm == Rme + v ? GG : 0) : 0;
+        const int dg = Rdg - mat[arow + bcode];
+        const int border = glob ? gmin(p, q) : 0;
+        const int r = (top && left) ? 0 : ((top || left) ? border : gmin(gmin(dg, p), q));
+        const int abc = (r == p ? GA : 0) | (r == q ? GB : 0) | ((!top && !left && r == dg) ? GC : 0);
+        // the byte of (i, j - 1): its abc (last step), fg (this lane now) and
+        // de (the lane below now; the strip's last row: rowde)
+        const int deb = from_next_lane(0, de);
+        const int s = 64 * k + t;
+        const uint32_t b1 = (uint32_t)(Dprev - (s - 1 - (n + 1) > 0 ? s - 1 - (n + 1) : 0));
+        Dprev = Ds;
+        Ds += dlen(s, m + 1, n + 1);
+        const bool pend = rowok && j >= 1 && j <= n + 1;
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(abcp | fg | (lane == 63 ? 0 : deb)), rbits,
+                                             pend ? (uint32_t)i : GOOB, b1, 0);
+        // the first lane's de belongs to the strip above's last row
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)de, rside, (lane == 0 && act) ? (uint32_t)j : GOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(r, rcol, (act && j == n) ? 4u * (uint32_t)i : GOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(r, rrow, (act && i == m) ? 4u * (uint32_t)j : GOOB, 0, 0);
+        abcp = act ? abc : 0;
+        Rdg = Rup;
+        Rme = act ? r : 0;
+        Pme = act ? p : G_INF;
+        Qme = act ? q : G_INF;
+        // the strip's last row (lane 63, column t - 63) to the strip below
+        const int jp = t - 63;
+        if (produce && jp >= 0 && jp <= n) {
+            if (lane == 63) dev_store(below + jp, rp_pack(r, p));
+            if (((jp + 1) & (GBLK - 1)) == 0 || jp == n)
+                if (lane == 63) prog_publish(pme, jp + 1);
+        }
+    }
+}
+
+// Edge assignment of one strip (bottom-up, right to left).  Each block of
+// GBLK steps first loads the block's plane bytes (loaded during the block
+// before), then computes, then stores the block's final bytes: loads and
+// stores never interleave inside a block, so no step waits on a store.
+__global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
+{
+    const int lane = threadIdx.x;
+    int u = 0;
+    if (lane == 0) u = atomicAdd(&S.ticket[1], 1);
+    u = __builtin_amdgcn_readfirstlane(__shfl(u, 0));
+    int ta, q0;
+    strip_of(S, u, ta, q0);
+    const GotohArgs &A = S.args[ta];
+    const int m = uni(A.m), n = uni(A.n);
+    const int ns = (m + 1 + 63) / 64;
+    const int k = ns - 1 - q0;                 // strips bottom-up
+    const int W1 = n + 1;
+    const int64_t cells = (int64_t)(m + 2) * (n + 2);
+    const __amdgpu_buffer_rsrc_t rbits = brsrc(A.bits, (uint32_t)cells);
+    const uint8_t bnd = A.is_global ? 0 : GC;
+    const int i = 64 * k + lane;
+    const bool rowok = i <= m, lastr = i == m;
+    const bool produce = k > 0, consume = k + 1 < ns;
+    const int *under = A.brow2 + (size_t)(k + 1) * W1;   // row 64k + 64, by tau = n - j
+    int *mytop = A.brow2 + (size_t)k * W1;
+    // de bits of this strip's last row (stored by the strip below), by column
+    const __amdgpu_buffer_rsrc_t rside = brsrc(A.rowde + (size_t)k * W1, consume ? (uint32_t)W1 : 0u);
+    const int *punder = A.prog + ns + (k + 1), *flags = A.flags;   // bwd counters after the fwd ones
+    int *pme = A.prog + ns + k;
+    int mine = 0;        // final abc of (i, j + 1): this lane, one step ago
+    int dnp = 0;         // final abc of (i + 1, j + 1): the lane below, two steps ago
+    // plane base of the step's diagonal s = 64 k + n + 63 - t, running down:
+    // D(s - 1) = D(s) - len(s - 1)
+    const int s0 = 64 * k + n + 63;
+    int64_t Dld = doff_of(s0, m + 1, n + 1), Dst = Dld;
+    int cx[GBLK], nx[GBLK], ox[GBLK];
+    // the plane bytes of steps t0 .. t0 + GBLK - 1
+    auto load_block = [&](int t0b, int *dst) {
+#pragma unroll
+        for (int q = 0; q < GBLK; ++q) {
+            const int tt = t0b + q, jj = n + 63 - lane - tt, sd = s0 - tt;
+            const uint32_t base = (uint32_t)(Dld - (sd - (n + 1) > 0 ? sd - (n + 1) : 0));
+            const bool ok = rowok && jj >= 0 && jj <= n && tt <= n + 63;
+            dst[q] = __builtin_amdgcn_raw_buffer_load_b8(rbits, ok ? (uint32_t)i : GOOB, base, 0);
+            Dld -= dlen(sd - 1, m + 1, n + 1);
+        }
+    };
+    load_block(0, cx);
+    for (int t0 = 0; t0 <= n + 63; t0 += GBLK) {
+        // the strip below's first row for this block (lane 63's cells below)
+        // and lanes 0..31: the de side bits of lane 63's cells (column n - t)
+        int blk = 0, side = 0;
+        if (consume && t0 <= n) {
+            prog_wait(punder, t0 + GBLK < W1 ? t0 + GBLK : W1, (int *)flags);
+            if (lane < GBLK && t0 + lane < W1) blk = dev_load(under + t0 + lane);
+            side = __builtin_amdgcn_raw_buffer_load_b8(rside, (lane < GBLK && t0 + lane <= n) ?
+                                                       (uint32_t)(n - t0 - lane) : GOOB, 0, 0);
+        }
+        asm volatile("; touch %0 %1" : "+v"(blk), "+v"(side));
+#pragma unroll
+        for (int q = 0; q < GBLK; ++q) asm volatile("; touch %0" : "+v"(cx[q]));
+        load_block(t0 + GBLK, nx);
+#pragma unroll
+        for (int q = 0; q < GBLK; ++q) {
+            const int t = t0 + q;
+            const int j = n + 63 - lane - t;
+            int dnb = from_next_lane(0, mine);                   // final abc of (i + 1, j)
+            const int d63 = __builtin_amdgcn_readlane(blk, q);
+            dnb = (lane == 63 && consume && t <= n) ? d63 : dnb;
+            const bool act = rowok && j >= 0 && j <= n;
+            const bool lastc = j == n;
+            const int c = cx[q] | (lane == 63 ? __builtin_amdgcn_readlane(side, q) : 0);
+            const int dn = lastr ? (lastc ? GC : bnd) : dnb;
+            const int rt = lastc ? (lastr ? GC : bnd) : mine;
+            const int dgn = (lastr || lastc) ? ((lastr && lastc) ? GC : bnd) : dnp;
+            // Altschul-Erickson steps 8-11 of the cell
+            int x = c;
+            const bool no_a_below = !(dn & GA), no_e = !(c & GE_), no_b_right = !(rt & GB), no_g = !(c & GG);
+            const bool no_c_diag = !(dgn & GC);
+            if ((no_a_below || no_e) && (no_b_right || no_g) && no_c_diag) x &= ~(GA | GB | GC);
+            if (!(no_a_below && no_b_right && no_c_diag)) {
+                if ((dn & GA) && (c & GD)) x |= GA;
+                if ((rt & GB) && (c & GF)) x |= GB;
+            }
+            ox[q] = act ? x : 0;
+            dnp = dnb;
+            mine = act ? x : 0;
+        }
+        // the block's final bytes; the strip's first row (lane 0) to the strip above
+#pragma unroll
+        for (int q = 0; q < GBLK; ++q) {
+            const int t = t0 + q, j = n + 63 - lane - t, sd = s0 - t;
+            const uint32_t b0 = (uint32_t)(Dst - (sd - (n + 1) > 0 ? sd - (n + 1) : 0));
+            Dst -= dlen(sd - 1, m + 1, n + 1);
+            const bool act = rowok && j >= 0 && j <= n && t <= n + 63;
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ox[q], rbits, act ? (uint32_t)i : GOOB, b0, 0);
+            const int tp = t - 63;
+            if (produce && tp >= 0 && tp <= n && lane == 0) dev_store(mytop + tp, ox[q]);
+        }
+        if (produce && t0 + GBLK - 1 - 63 >= 0) {
+            const int tp_end = t0 + GBLK - 1 - 63 < n ? t0 + GBLK - 1 - 63 : n;
+            if (lane == 0) prog_publish(pme, tp_end + 1);
+        }
+#pragma unroll
+        for (int q = 0; q < GBLK; ++q) cx[q] = nx[q];
+    }
+}
+
+// One workgroup per alignment: the best start cell and the traceback.
+__global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh_tb(const GotohArgs *batch)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
     const GotohArgs A = batch[blockIdx.x];
-    const int m = A.m, n = A.n, L = A.L;
-    const int u = A.u, v = A.v;
-    int *dR = A.diagR, *dP = A.diagP, *dQ = A.diagQ;
-    const int8_t *ca = A.a, *cb = A.b;
-    const int *mat = A.mat;
-    if (LDS) {   // rolling diagonals, codes and matrix in LDS
-        int *w = (int *)gsm;
-        dR = w;
-        dP = w + 3 * (m + 2);
-        dQ = w + 6 * (m + 2);
-        int *lm = w + 9 * (m + 2);
-        int8_t *la = (int8_t *)(lm + L * L), *lb = la + gotoh_al16(m);
-        for (int x = threadIdx.x; x < L * L; x += blockDim.x) lm[x] = A.mat[x];
-        for (int x = threadIdx.x; x < m; x += blockDim.x) la[x] = A.a[x];
-        for (int x = threadIdx.x; x < n; x += blockDim.x) lb[x] = A.b[x];
-        mat = lm; ca = la; cb = lb;
-        __syncthreads();
-    }
-    // ---- phase 1: cost assignment by anti-diagonals ----
-    for (int s = 0; s <= m + n; ++s) {
-        const int ilo = s - n > 0 ? s - n : 0, ihi = s < m ? s : m;
-        int *Rc = dR + (s % 3) * (m + 2), *Pc = dP + (s % 3) * (m + 2), *Qc = dQ + (s % 3) * (m + 2);
-        const int *R1 = dR + ((s + 2) % 3) * (m + 2), *P1 = dP + ((s + 2) % 3) * (m + 2),
-                  *Q1 = dQ + ((s + 2) % 3) * (m + 2);
-        const int *R2 = dR + ((s + 1) % 3) * (m + 2);
-        // plane bases of diagonals s and s - 1 (wave-uniform arithmetic)
-        uint8_t *abc0 = A.abc + dbase(s, m, n);
-        uint8_t *de1 = A.de + dbase(s - 1, m, n);
-        uint8_t *fg1 = A.fg + dbase(s - 1, m, n);
-        for (int i = ilo + (int)threadIdx.x; i <= ihi; i += blockDim.x) {
-            const int j = s - i;
-            int p, q, r, dg = 0;
-            if (i == 0) {
-                p = G_INF;
-            } else {
-                const int pu = P1[i - 1], ru = R1[i - 1];   // (i-1, j) on diagonal s-1
-                p = u + gmin(pu, ru + v);
-                uint8_t de = 0;
-                if (pu != G_INF && p == pu + u) de |= GD;
-                if (p == ru + v + u) de |= GE_;
-                de1[i - 1] = de;                            // de(i-1, j)
-            }
-            if (j == 0) {
-                q = G_INF;
-            } else {
-                const int ql = Q1[i], rl = R1[i];           // (i, j-1) on diagonal s-1
-                q = u + gmin(ql, rl + v);
-                uint8_t fg = 0;
-                if (ql != G_INF && q == ql + u) fg |= GF;
-                if (q == rl + v + u) fg |= GG;
-                fg1[i] = fg;                                // fg(i, j-1)
-            }
-            if (i == 0 && j == 0) {
-                r = 0;
-            } else if (i == 0 || j == 0) {
-                r = A.is_global ? gmin(p, q) : 0;
-            } else {
-                dg = R2[i - 1] - mat[ca[i - 1] * L + cb[j - 1]];
-                r = gmin(gmin(dg, p), q);
-            }
-            Rc[i] = r; Pc[i] = p; Qc[i] = q;
-            uint8_t abc = 0;
-            if (r == p) abc |= GA;
-            if (r == q) abc |= GB;
-            if (i > 0 && j > 0 && r == dg) abc |= GC;
-            abc0[i] = abc;
-            if (j == n) A.lastcol[i] = r;
-            if (i == m) A.lastrow[j] = r;
-        }
-        step_barrier<LDS>();
-    }
-    // boundary c bits (_gotoh2.c:117-131)
-    if (!A.is_global) {
-        for (int j = threadIdx.x; j <= n + 1; j += blockDim.x) A.abc[pidx(A, m + 1, j)] = GC;
-        for (int i = threadIdx.x; i <= m + 1; i += blockDim.x) A.abc[pidx(A, i, n + 1)] = GC;
-    }
-    if (threadIdx.x == 0) A.abc[pidx(A, m + 1, n + 1)] = GC;
-    __syncthreads();
-    // ---- phase 2: edge assignment, anti-diagonals in reverse ----
-    // A cell reads its own phase-1 bytes and the final abc of (i+1, j),
-    // (i, j+1) (diagonal s+1) and (i+1, j+1) (s+2).  The LDS variant keeps
-    // those final values of the last two diagonals in LDS and loads the next
-    // diagonal's phase-1 bytes while this one is computed, so a step waits on
-    // no global load.  Boundary cells (i = m+1 or j = n+1) hold GC in local
-    // mode, 0 in global mode, GC at (m+1, n+1).
-    const uint8_t bnd = A.is_global ? 0 : GC;
-    auto edge = [&](uint8_t x, uint8_t dep, uint8_t fgp, uint8_t dn, uint8_t rt, uint8_t dgn) -> uint8_t {
-        uint8_t e = dep & GE_, d = dep & GD;
-        uint8_t g = fgp & GG, f = fgp & GF;
-        const bool no_a_below = !(dn & GA), no_e = !e, no_b_right = !(rt & GB), no_g = !g;
-        const bool no_c_diag = !(dgn & GC);
-        if ((no_a_below || no_e) && (no_b_right || no_g) && no_c_diag) x &= (uint8_t)~(GA | GB | GC);
-        if (!(no_a_below && no_b_right && no_c_diag)) {
-            if ((dn & GA) && d) x |= GA;
-            if ((rt & GB) && f) x |= GB;
-        }
-        return x;
-    };
-    if (LDS) {
-        uint8_t *fin = (uint8_t *)gsm;   // 3 x (m + 2): final abc by row (phase 1's R/P/Q space)
-        uint8_t px[GOTOH_PF], pd[GOTOH_PF], pf[GOTOH_PF];
-        auto fetch = [&](int sd) {
-            const int ilo = sd - n > 0 ? sd - n : 0, ihi = sd < m ? sd : m;
-            const int64_t b0 = dbase(sd, m, n);
-#pragma unroll
-            for (int k = 0; k < GOTOH_PF; ++k) {
-                const int i = ilo + (int)threadIdx.x + k * GOTOH_THREADS;
-                if (i <= ihi) {
-                    px[k] = A.abc[b0 + i];
-                    pd[k] = A.de[b0 + i];
-                    pf[k] = A.fg[b0 + i];
-                }
-            }
-        };
-        fetch(m + n);
-        for (int s = m + n; s >= 0; --s) {
-            const int ilo = s - n > 0 ? s - n : 0, ihi = s < m ? s : m;
-            const int64_t b0 = dbase(s, m, n);
-            uint8_t cx[GOTOH_PF], cd[GOTOH_PF], cf[GOTOH_PF];
-#pragma unroll
-            for (int k = 0; k < GOTOH_PF; ++k) { cx[k] = px[k]; cd[k] = pd[k]; cf[k] = pf[k]; }
-            if (s > 0) fetch(s - 1);
-            uint8_t *f0 = fin + (s % 3) * (m + 2);
-            const uint8_t *f1 = fin + ((s + 1) % 3) * (m + 2), *f2 = fin + ((s + 2) % 3) * (m + 2);
-#pragma unroll
-            for (int k = 0; k < GOTOH_PF; ++k) {
-                const int i = ilo + (int)threadIdx.x + k * GOTOH_THREADS;
-                if (i > ihi) break;
-                const int j = s - i;
-                const bool lastr = i == m, lastc = j == n;
-                const uint8_t dn = lastr ? (lastc ? GC : bnd) : f1[i + 1];
-                const uint8_t rt = lastc ? (lastr ? GC : bnd) : f1[i];
-                const uint8_t dgn = (lastr || lastc) ? ((lastr && lastc) ? GC : bnd) : f2[i + 1];
-                const uint8_t x = edge(cx[k], cd[k], cf[k], dn, rt, dgn);
-                A.abc[b0 + i] = x;
-                f0[i] = x;
-            }
-            lds_barrier();
-        }
-        __syncthreads();   // the traceback reads the planes
-    } else {
-        for (int s = m + n; s >= 0; --s) {
-            const int ilo = s - n > 0 ? s - n : 0, ihi = s < m ? s : m;
-            const int64_t b0 = dbase(s, m, n), b1 = dbase(s + 1, m, n), b2 = dbase(s + 2, m, n);
-            for (int i = ilo + (int)threadIdx.x; i <= ihi; i += blockDim.x) {
-                const int64_t h = b0 + i;
-                // (i+1, j) and (i, j+1) on diagonal s+1, (i+1, j+1) on s+2
-                A.abc[h] = edge(A.abc[h], A.de[h], A.fg[h], A.abc[b1 + i + 1], A.abc[b1 + i],
-                                A.abc[b2 + i + 1]);
-            }
-            __syncthreads();
-        }
-    }
+    const int m = A.m, n = A.n;
+    const int gabort = A.flags[0];
     // ---- phase 3: traceback ----
     // The walk is serial, so it never waits on global memory: the block
     // stages a TB x TB window of abc (diagonals s0 .. s0-TB+1, rows
@@ -268,7 +436,7 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh(const GotohArgs *batch)
     // each sequence before ii / jj into LDS; thread 0 walks the window and
     // writes the output characters; repeat.  The gap runs at both ends are
     // written by the whole block.
-    uint8_t *win = (uint8_t *)gsm + (LDS ? gotoh_codes_end(m, n, L) : 0);
+    uint8_t *win = gsm;
     char *wc1 = (char *)win + TB * TB, *wc2 = wc1 + TB;
     __shared__ unsigned long long tb_key;
     __shared__ int tb_ii, tb_jj, tb_len, tb_status;
@@ -309,9 +477,9 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh(const GotohArgs *batch)
         for (int x = threadIdx.x; x < TB * TB; x += blockDim.x) {
             const int t = x / TB, r = x % TB;
             const int sd = s0 - t, i = i0 - r, j = sd - i;
-            uint8_t v = 0;
-            if (i >= 1 && j >= 1 && j <= n) v = A.abc[dbase(sd, m, n) + i];   // (r <= t on the path)
-            win[x] = v;
+            uint8_t vv = 0;
+            if (i >= 1 && j >= 1 && j <= n) vv = A.bits[dbase(sd, m, n) + i];   // (r <= t on the path)
+            win[x] = vv;
         }
         for (int x = threadIdx.x; x < TB; x += blockDim.x) {
             wc1[x] = i0 - 1 - x >= 0 ? A.s1[i0 - 1 - x] : 0;
@@ -344,7 +512,7 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh(const GotohArgs *batch)
         }
     }
     if (threadIdx.x == 0) {
-        A.result[0] = status;
+        A.result[0] = gabort ? -4 : status;
         A.result[1] = -best;
         A.result[2] = status == 0 ? flen + fi + fj : flen;
     }
@@ -361,16 +529,13 @@ static size_t gotoh_io_bytes(int m, int n)
            2 * align16(m + n + 1) + 64;
 }
 
-// LDS of the LDS variant: rolling R/P/Q diagonals, the score matrix, codes
-static size_t gotoh_lds_bytes(int m, int n, int L)
-{
-    return gotoh_codes_end(m, n, L) + TB_LDS;
-}
-
 static size_t gotoh_work_bytes(int m, int n)
 {
-    return 3 * align16(sizeof(int) * 3 * (m + 2)) + align16(sizeof(int) * (m + 2)) +
-           align16(sizeof(int) * (n + 2)) + 3 * align16((size_t)(m + 2) * (n + 2));
+    const size_t strips = (size_t)(m + 1 + 63) / 64;
+    return align16(sizeof(int) * (m + 2)) + align16(sizeof(int) * (n + 2)) +
+           align16((size_t)(m + 2) * (n + 2)) + align16(8 * strips * (n + 1)) +
+           align16(sizeof(int) * strips * (n + 1)) + align16(strips * (n + 1)) +
+           align16(sizeof(int) * 2 * strips) + 16;
 }
 
 // Retained scratch above this is released after the call (one very long
@@ -382,13 +547,12 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
                     char *const *out1, char *const *out2, const int *cap, int *score, int *status)
 {
     const int L = (int)strlen(alphabet);
-    if (count < 0 || L == 0) { set_error("mh_gotoh_align: bad arguments"); return -3; }
+    if (count < 0 || L == 0 || L > 64) { set_error("mh_gotoh_align: bad arguments"); return -3; }
     if (count == 0) return 0;
     int code[256];
     for (int k = 0; k < 256; ++k) code[k] = -1;
     for (int k = 0; k < L; ++k) code[(unsigned char)alphabet[k]] = k;
     std::vector<int> ms(count), ns(count);
-    size_t lds = 0;
     std::vector<size_t> io(count + 1, 0), work(count + 1, 0);
     for (int t = 0; t < count; ++t) {
         if (!s1[t] || !s2[t] || !out1[t] || !out2[t]) { set_error("mh_gotoh_align: null argument"); return -3; }
@@ -403,13 +567,20 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
         for (int j = 0; j < ns[t]; ++j)
             if (code[(unsigned char)s2[t][j]] < 0) { set_error("mh_gotoh_align: '%c' not in alphabet", s2[t][j]); return -3; }
         io[t + 1] = io[t] + gotoh_io_bytes(ms[t], ns[t]);
-        lds = std::max(lds, ms[t] < GOTOH_PF * GOTOH_THREADS ? gotoh_lds_bytes(ms[t], ns[t], L)
-                                                             : GOTOH_LDS_MAX + 1);
+        if ((uint64_t)(ms[t] + 2) * (uint64_t)(ns[t] + 2) >= (uint64_t)GOOB) {
+            set_error("mh_gotoh_align: alignment %d too large (%d x %d)", t, ms[t], ns[t]);
+            return -3;
+        }
         work[t + 1] = work[t] + gotoh_work_bytes(ms[t], ns[t]);
     }
+    // strips in ticket order: every alignment's, alignment by alignment
+    std::vector<int> first(count + 1, 0);
+    for (int t = 0; t < count; ++t) first[t + 1] = first[t] + (ms[t] + 1 + 63) / 64;
     const size_t sz_mat = align16(sizeof(int) * L * L), sz_args = align16(sizeof(GotohArgs) * count);
-    // device buffer: [io blocks][matrix][argument blocks][work blocks]
-    const size_t off_mat = io[count], off_args = off_mat + sz_mat, off_work = off_args + sz_args;
+    const size_t sz_first = align16(sizeof(int) * (count + 1)) + 16;   // + the two ticket counters
+    // device buffer: [io blocks][matrix][arguments][strip table, tickets][work blocks]
+    const size_t off_mat = io[count], off_args = off_mat + sz_mat, off_first = off_args + sz_args,
+                 off_work = off_first + sz_first;
     const size_t total = off_work + work[count] + 256;
     std::lock_guard<std::mutex> guard(c.gotoh_mutex);   // the scratch is per context
     if (c.gotoh_cap < total) {
@@ -431,15 +602,16 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
         const size_t oa = take_io(m + 8), ob = take_io(n + 8), o1 = take_io(m + 1),
                      o2 = take_io(n + 1), oo1 = take_io(m + n + 1), oo2 = take_io(m + n + 1),
                      ores = take_io(64);
-        A.diagR = (int *)take_w(sizeof(int) * 3 * (m + 2));
-        A.diagP = (int *)take_w(sizeof(int) * 3 * (m + 2));
-        A.diagQ = (int *)take_w(sizeof(int) * 3 * (m + 2));
         A.lastcol = (int *)take_w(sizeof(int) * (m + 2));
         A.lastrow = (int *)take_w(sizeof(int) * (n + 2));
         const size_t cells = (size_t)(m + 2) * (n + 2);
-        A.abc = (uint8_t *)take_w(cells);
-        A.de = (uint8_t *)take_w(cells);
-        A.fg = (uint8_t *)take_w(cells);
+        A.bits = (uint8_t *)take_w(cells);
+        const size_t strips = (size_t)(m + 1 + 63) / 64;
+        A.brow1 = (unsigned long long *)take_w(8 * strips * (n + 1));
+        A.brow2 = (int *)take_w(sizeof(int) * strips * (n + 1));
+        A.rowde = (uint8_t *)take_w(strips * (n + 1));
+        A.prog = (int *)take_w(sizeof(int) * 2 * strips);
+        A.flags = (int *)take_w(16);
         for (int i = 0; i < m; ++i) img[oa + i] = (char)code[(unsigned char)s1[t][i]];
         for (int j = 0; j < n; ++j) img[ob + j] = (char)code[(unsigned char)s2[t][j]];
         memcpy(&img[o1], s1[t], m);
@@ -456,20 +628,36 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
     }
     hipStream_t st = c.stream;
     MH_HIP(hipMemsetAsync(d + off_work, 0, work[count], st));
+    MH_HIP(hipMemsetAsync(d + off_first, 0, sz_first, st));
     MH_HIP(hipMemcpyAsync(d, img.data(), io[count], hipMemcpyHostToDevice, st));
     MH_HIP(hipMemcpyAsync(d + off_mat, matrix, sizeof(int) * L * L, hipMemcpyHostToDevice, st));
     MH_HIP(hipMemcpyAsync(d + off_args, args.data(), sizeof(GotohArgs) * count,
                           hipMemcpyHostToDevice, st));
-    const int pg = prof_begin(c, "k_gotoh");
-    if (lds <= GOTOH_LDS_MAX) {
-        MH_HIP(hipFuncSetAttribute((const void *)k_gotoh<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds));
-        hipLaunchKernelGGL(k_gotoh<true>, dim3((unsigned)count), dim3(GOTOH_THREADS), lds, st,
-                           (const GotohArgs *)(d + off_args));
+    MH_HIP(hipMemcpyAsync(d + off_first, first.data(), sizeof(int) * (count + 1), hipMemcpyHostToDevice, st));
+    GotohStrips S;
+    S.args = (const GotohArgs *)(d + off_args);
+    S.first = (const int *)(d + off_first);
+    S.count = count;
+    S.ticket = (int *)(d + off_first + sz_first - 16);
+    const int strips = first[count];
+    const int pf = prof_begin(c, "k_gotoh_fwd");
+    int nmax = 0;
+    for (int t = 0; t < count; ++t) nmax = std::max(nmax, ns[t]);
+    const size_t lds_fwd = gotoh_al16(sizeof(int) * L * L) + (nmax <= GBC_MAX ? gotoh_al16(nmax) : 0);
+    if (nmax <= GBC_MAX) {
+        MH_HIP(hipFuncSetAttribute((const void *)k_gotoh_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds_fwd));
+        hipLaunchKernelGGL(k_gotoh_fwd<true>, dim3((unsigned)strips), dim3(64), lds_fwd, st, S);
     } else {
-        hipLaunchKernelGGL(k_gotoh<false>, dim3((unsigned)count), dim3(GOTOH_THREADS), TB_LDS, st,
-                           (const GotohArgs *)(d + off_args));
+        hipLaunchKernelGGL(k_gotoh_fwd<false>, dim3((unsigned)strips), dim3(64), lds_fwd, st, S);
     }
+    prof_end(c, pf);
+    const int pb = prof_begin(c, "k_gotoh_bwd");
+    hipLaunchKernelGGL(k_gotoh_bwd, dim3((unsigned)strips), dim3(64), 0, st, S);
+    prof_end(c, pb);
+    const int pg = prof_begin(c, "k_gotoh");
+    hipLaunchKernelGGL(k_gotoh_tb, dim3((unsigned)count), dim3(GOTOH_THREADS), TB_LDS, st,
+                       (const GotohArgs *)(d + off_args));
     prof_end(c, pg);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(img.data(), d, io[count], hipMemcpyDeviceToHost, st);
@@ -479,6 +667,7 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
         const GotohArgs &A = args[t];
         int res[3];
         memcpy(res, &img[(const char *)A.result - d], sizeof(res));
+        if (res[0] == -4) { set_error("k_gotoh: a strip's wait for its neighbour timed out (alignment %d)", t); return -4; }
         status[t] = res[0] ? -1 : 0;
         score[t] = res[1];
         const int len = res[0] ? 0 : res[2];

@@ -7,9 +7,13 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "mh_gunzip.h"
 
@@ -135,15 +139,136 @@ int gunzip_ld(const LdApi &api, const uint8_t *src, int64_t len, std::string &ou
     return rc;
 }
 
+// One whole member [src, src + len) into out[0 .. isize): true when it
+// decodes, uses exactly len bytes and yields exactly isize bytes.
+bool member_exact(const LdApi &api, const uint8_t *src, int64_t len, char *out, uint32_t isize)
+{
+    if (api.ok) {
+        Ld *d = api.alloc();
+        if (!d) return false;
+        size_t in_used = 0, out_used = 0;
+        const int r = api.gunzip(d, src, (size_t)len, out, isize, &in_used, &out_used);
+        api.free_(d);
+        return r == LD_SUCCESS && (int64_t)in_used == len && out_used == isize;
+    }
+    z_stream z{};
+    if (inflateInit2(&z, 15 + 16) != Z_OK) return false;
+    z.next_in = (Bytef *)src;
+    z.avail_in = (uInt)len;
+    z.next_out = (Bytef *)out;
+    z.avail_out = isize;
+    const int st = inflate(&z, Z_FINISH);
+    const bool ok = st == Z_STREAM_END && z.avail_in == 0 && z.avail_out == 0;
+    inflateEnd(&z);
+    return ok;
+}
+
+// A gzip member header at p: magic, deflate, no reserved flag bits, a known
+// XFL and OS byte (RFC 1952).  Inside compressed data this pattern is rare;
+// a false candidate is caught by member_exact.
+bool member_header(const uint8_t *p, int64_t avail)
+{
+    return avail >= 18 && p[0] == 0x1f && p[1] == 0x8b && p[2] == 8 && (p[3] & 0xe0) == 0 &&
+           (p[8] == 0 || p[8] == 2 || p[8] == 4) && (p[9] <= 13 || p[9] == 255);
+}
+
+uint32_t le32(const uint8_t *p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
+
+void run_threads(int nt, const std::function<void(int)> &fn)
+{
+    if (nt <= 1) { fn(0); return; }
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(fn, t);
+    fn(0);
+    for (auto &x : th) x.join();
+}
+
+// Concatenated members decoded in parallel.  Every header-shaped offset is a
+// candidate member start; the member ending at the next candidate has its
+// size (ISIZE) in the 4 bytes before it.  Each candidate span is decoded
+// straight into its place in `out` and accepted only when it is exactly one
+// whole member of exactly that size.  Spans that fail (a false candidate
+// split a member) are merged with the next span(s) and decoded again;
+// -1 when that does not resolve them (the caller then decodes serially).
+int gunzip_members(const LdApi &api, const uint8_t *src, int64_t len, std::string &out, int threads)
+{
+    std::vector<int64_t> cand;
+    {
+        const int nt = threads;
+        std::vector<std::vector<int64_t>> part(nt);
+        run_threads(nt, [&](int t) {
+            const int64_t a = len * t / nt, b = len * (t + 1) / nt;
+            const uint8_t *p = src + a;
+            while (p < src + b) {
+                p = (const uint8_t *)memchr(p, 0x1f, (size_t)(src + b - p));
+                if (!p) break;
+                if (member_header(p, src + len - p)) part[t].push_back(p - src);
+                ++p;
+            }
+        });
+        for (auto &v : part) cand.insert(cand.end(), v.begin(), v.end());
+    }
+    if (cand.empty() || cand[0] != 0) return -1;
+    cand.push_back(len);
+    // spans [cand[j], cand[j + 1]) and their sizes, merging spans whose
+    // decode failed until every span is one whole member
+    std::vector<int64_t> beg(cand.begin(), cand.end() - 1), end(cand.begin() + 1, cand.end());
+    for (int round = 0; round < 8; ++round) {
+        const size_t k = beg.size();
+        std::vector<uint64_t> at(k + 1, 0);
+        for (size_t j = 0; j < k; ++j) {
+            if (end[j] - beg[j] < 18) return -1;
+            at[j + 1] = at[j] + le32(src + end[j] - 4);
+        }
+        if (at[k] > (uint64_t)len * 64 + (1u << 20)) return -1;   // implausible sizes
+        out.resize(at[k]);
+        std::vector<char> ok(k, 0);
+        std::atomic<size_t> next(0);
+        run_threads(std::min<int>(threads, (int)k), [&](int) {
+            for (size_t j; (j = next.fetch_add(1)) < k;)
+                ok[j] = member_exact(api, src + beg[j], end[j] - beg[j], &out[at[j]],
+                                     (uint32_t)(at[j + 1] - at[j]));
+        });
+        // a failed span absorbs the span after it (a false candidate split
+        // one member in two)
+        std::vector<int64_t> nb, ne;
+        bool all = true, pending = false;
+        for (size_t j = 0; j < k; ++j) {
+            if (pending) { ne.back() = end[j]; pending = false; continue; }
+            nb.push_back(beg[j]);
+            ne.push_back(end[j]);
+            if (!ok[j]) { all = false; pending = true; }
+        }
+        if (all) return 0;
+        if (pending) return -1;   // the last span failed: nothing follows it
+        beg.swap(nb);
+        end.swap(ne);
+    }
+    return -1;
+}
+
 }  // namespace
 
 bool gunzip_fast_available() { return ld_api().ok; }
+
+int gunzip_threads()
+{
+    const char *e = getenv("OMP_NUM_THREADS");
+    int n = e ? atoi(e) : 0;
+    if (n <= 0) n = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(n, 64));
+}
 
 int gunzip_buffer(const uint8_t *src, int64_t len, std::string &out, std::string &why)
 {
     out.clear();
     if (len <= 0) return 0;
     const LdApi &api = ld_api();
+    // concatenated members (as a parallel gzip writes them) decode in
+    // parallel; a single member, or anything the member scan cannot split,
+    // decodes serially
+    if (len > (1 << 22) && gunzip_members(api, src, len, out, gunzip_threads()) == 0) return 0;
+    out.clear();
     return api.ok ? gunzip_ld(api, src, len, out, why) : gunzip_zlib(src, len, out, why);
 }
 

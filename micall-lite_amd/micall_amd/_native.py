@@ -78,6 +78,10 @@ def _declare(L):
         'mh_format_rows': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.c_int64,
                             ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_size_t,
                             ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        'mh_write_rows': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.c_int64,
+                           ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_int64, _I64P],
+                          ctypes.c_int),
+        'mh_file_checksum': ([ctypes.c_int, _I64P, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         'mh_rows_load': ([_P, ctypes.c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                           ctypes.c_int64, _P], ctypes.c_int),
         'mh_rows_load_csv': ([_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int,
@@ -504,9 +508,27 @@ class Context:
         return buf[:used.value].tobytes().decode()
 
     def write_rows(self, out, style, first=0, n=None, order=None):
-        """format_rows(...) written to the text file `out`.  For a UTF-8 /
-        ASCII file that writes '\n' as is (the text is ASCII), the bytes go
-        to its binary buffer without a str round trip."""
+        """format_rows(...) written to the text file `out`.  A seekable
+        UTF-8 / ASCII file that writes '\n' as is (the text is ASCII) gets
+        the rows straight from the formatting threads (mh_write_rows at its
+        file position); another file gets them through its binary buffer, a
+        non-file stream as str."""
+        fd = _plain_fd(out)
+        if fd is not None:
+            if order is not None:
+                order = np.ascontiguousarray(order, dtype=np.int64)
+                if n is None:
+                    n = len(order) - first
+            elif n is None:
+                n = self.reads_count()[0] - first
+            names = (ctypes.c_char_p * max(self.n_refs, 1))(*[r.encode() for r in self.refnames])
+            out.flush()
+            off = os.lseek(fd, 0, os.SEEK_CUR)
+            written = ctypes.c_int64()
+            check(lib().mh_write_rows(self.h, style, None if order is None else _ptr(order), first, n,
+                                      names, fd, off, ctypes.byref(written)), 'mh_write_rows')
+            out.seek(off + written.value)
+            return
         text = self.format_rows_bytes(style, first, n, order)
         raw = getattr(out, 'buffer', None)
         enc = (getattr(out, 'encoding', '') or '').lower().replace('-', '')
@@ -713,6 +735,29 @@ class Context:
               'mh_gotoh_align_batch')
         return [RuntimeError('Traceback failed, try local alignment') if status[t] else
                 (o1[t].value.decode(), o2[t].value.decode(), int(score[t])) for t in range(n)]
+
+
+def _plain_fd(handle):
+    """The descriptor of an open text file the rows can be written to
+    directly (seekable, not appending, UTF-8 / ASCII, '\n' written as is),
+    else None."""
+    try:
+        enc = (getattr(handle, 'encoding', '') or '').lower().replace('-', '')
+        if (enc not in ('utf8', 'ascii') or os.linesep != '\n' or
+                getattr(handle, '_writenl', None) not in (None, '\n') or
+                'a' in getattr(handle, 'mode', 'a') or not handle.seekable()):
+            return None
+        return handle.fileno()
+    except (AttributeError, OSError, ValueError):
+        return None
+
+
+def file_checksum(fd):
+    """(size, checksum) of a whole open file: (crc32 << 32) | adler32."""
+    size = ctypes.c_int64()
+    sum_ = ctypes.c_uint64()
+    check(lib().mh_file_checksum(fd, ctypes.byref(size), ctypes.byref(sum_)), 'mh_file_checksum')
+    return size.value, sum_.value
 
 
 def levenshtein(a, b):

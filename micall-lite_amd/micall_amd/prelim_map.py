@@ -81,20 +81,18 @@ def prelim_map(fastq1, fastq2, prelim_csv,
     ctx.map(_native.params(_native.E2E, rdg=(rdgopen, READ_GAP_EXTEND),
                            rfg=(rfgopen, REF_GAP_EXTEND), maxins=MAXINS))
     sam_ref = ctx.recs()[:, _native.ALN_FIELDS.index('sam_ref')]
-    digest = session._digest()
     if session.is_writer():
-        session.write_bytes(prelim_csv, (','.join(FIELDNAMES) + os.linesep).encode(), digest)
+        session.write_bytes(prelim_csv, (','.join(FIELDNAMES) + os.linesep).encode())
     if sh is None:
-        session.write_bytes(prelim_csv, ctx.format_rows_bytes(1, order=grouped_order(sam_ref)),
-                            digest)
+        ctx.write_rows(prelim_csv, 1, order=grouped_order(sam_ref))
     else:
-        _write_sharded(ctx, sh, sam_ref, len(names), prelim_csv, digest)
-    session.prelim_written(ctx, prelim_csv, digest, names)
+        _write_sharded(ctx, sh, sam_ref, len(names), prelim_csv)
+    session.prelim_written(ctx, prelim_csv, names)
     if callback:
         callback(progress=ctx.fastq_line_count / 2)
 
 
-def _write_sharded(ctx, sh, sam_ref, n_refs, prelim_csv, digest):
+def _write_sharded(ctx, sh, sam_ref, n_refs, prelim_csv):
     """prelim.csv of a sharded run: rname groups in global first-seen order
     (the smallest global row index of each rname over all ranks), and in a
     group the rows of rank 0, then rank 1, ... -- the ranks hold consecutive
@@ -120,7 +118,7 @@ def _write_sharded(ctx, sh, sam_ref, n_refs, prelim_csv, digest):
         for g in range(len(groups)):
             for r in range(sh.world):
                 if len(parts[r][g]):
-                    session.write_bytes(prelim_csv, parts[r][g], digest)
+                    session.write_bytes(prelim_csv, parts[r][g])
 
 
 _CLI_OPTIONS = (

@@ -311,7 +311,10 @@ def _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv, unmapped1, unmap
     each one (with its own split pairs, possibly none), and the rows and
     unmapped reads are written in rank order."""
     keep_rows, splits = split_mixed_references(ctx, ctx.recs())
-    _emit(shard, [(remap_csv, ctx.format_rows_bytes(1, order=keep_rows))])
+    if shard is None:
+        ctx.write_rows(remap_csv, 1, order=keep_rows)
+    else:
+        _emit(shard, [(remap_csv, ctx.format_rows_bytes(1, order=keep_rows))])
     order = list(splits)
     if shard is not None:
         order = []

@@ -49,6 +49,9 @@ def shard():
     if _shard_checked:
         return _shard
     _shard_checked = True
+    import sys
+    if 'torch' not in sys.modules and int(os.environ.get('WORLD_SIZE', '1')) <= 1:
+        return None          # no process group can exist: skip importing torch
     try:
         import torch
         import torch.distributed as dist
@@ -109,79 +112,6 @@ def load_fastq(fastq1, fastq2=None):
     return ctx
 
 
-def _digest():
-    try:
-        import xxhash
-        return xxhash.xxh3_64()
-    except ImportError:      # pragma: no cover - xxhash is in the image
-        import hashlib
-        return hashlib.blake2b(digest_size=8)
-
-
-def _identity(handle):
-    """(device, inode, size) of an open file, None for a non-file stream."""
-    try:
-        handle.flush()
-        st = os.fstat(handle.fileno())
-    except (AttributeError, OSError, ValueError):
-        return None
-    return st.st_dev, st.st_ino, st.st_size
-
-
-def write_bytes(handle, data, digest=None):
-    """Write ASCII bytes to an open text file (through its binary buffer when
-    it is a UTF-8 / ASCII file that writes '\n' as is), feeding digest."""
-    if digest is not None:
-        digest.update(data)
-    raw = getattr(handle, 'buffer', None)
-    enc = (getattr(handle, 'encoding', '') or '').lower().replace('-', '')
-    if (raw is not None and enc in ('utf8', 'ascii') and os.linesep == '\n' and
-            getattr(handle, '_writenl', None) in (None, '\n')):
-        handle.flush()
-        raw.write(data)
-    else:
-        handle.write(bytes(data).decode())
-
-
-def prelim_written(ctx, handle, digest, seed_names):
-    """Record that prelim_map() wrote `handle` from the device records that
-    are resident now (ctx.map_serial) for these seeds."""
-    global _prelim
-    ident = _identity(handle) if is_writer() else None
-    _prelim = dict(identity=ident, digest=None if digest is None else digest.digest(),
-                   serial=ctx.map_serial, key=_key, seeds=list(seed_names))
-
-
-def prelim_resident(ctx, handle, seed_names):
-    """True when `handle` is the prelim.csv this process's last prelim_map()
-    wrote, unchanged (same file and the same bytes: xxh3 of its content),
-    and that pass's records are still resident: remap() then takes the
-    prelim rows from the device instead of parsing them again.  In a sharded
-    job rank 0 checks the file and every rank its own records."""
-    p = _prelim
-    ok = (p is not None and p['serial'] == ctx.map_serial and p['key'] == _key and
-          p['key'] is not None and p['seeds'] == list(seed_names))
-    if ok and is_writer():
-        ok = p['identity'] is not None and _identity(handle) == p['identity']
-        if ok:
-            ok = _file_digest(handle) == p['digest']
-    sh = shard()
-    if sh is not None:
-        ok = bool(sh.min_i64([1 if ok else 0])[0])
-    return ok
-
-
-def _file_digest(handle):
-    import mmap
-    d = _digest()
-    try:
-        with mmap.mmap(handle.fileno(), 0, access=mmap.ACCESS_READ) as m:
-            d.update(m)
-    except (OSError, ValueError):
-        return None
-    return d.digest()
-
-
 def read_text(handle):
     """The rest of an open CSV/SAM text file for the native parsers: the raw
     bytes when nothing has read from it yet and it is UTF-8 / ASCII (no
@@ -201,6 +131,80 @@ def read_text(handle):
                 data = data.replace(b'\r\n', b'\n').replace(b'\r', b'\n')
             return data
     return handle.read()
+
+
+def _identity(handle):
+    """(device, inode, size) of an open file, None for a non-file stream."""
+    try:
+        handle.flush()
+        st = os.fstat(handle.fileno())
+    except (AttributeError, OSError, ValueError):
+        return None
+    return st.st_dev, st.st_ino, st.st_size
+
+
+def write_bytes(handle, data):
+    """Write ASCII bytes to an open text file (through its binary buffer when
+    it is a UTF-8 / ASCII file that writes '\n' as is)."""
+    raw = getattr(handle, 'buffer', None)
+    enc = (getattr(handle, 'encoding', '') or '').lower().replace('-', '')
+    if (raw is not None and enc in ('utf8', 'ascii') and os.linesep == '\n' and
+            getattr(handle, '_writenl', None) in (None, '\n')):
+        handle.flush()
+        raw.write(data)
+    else:
+        handle.write(bytes(data).decode())
+
+
+def _written_checksum(handle):
+    """Checksum of the file behind a handle opened for writing (read back
+    through its path, after checking that the path is still that file)."""
+    ident = _identity(handle)
+    name = getattr(handle, 'name', None)
+    if ident is None or not isinstance(name, str):
+        return None, None
+    try:
+        fd = os.open(name, os.O_RDONLY)
+    except OSError:
+        return None, None
+    try:
+        st = os.fstat(fd)
+        if (st.st_dev, st.st_ino) != ident[:2]:
+            return None, None
+        return ident, _native.file_checksum(fd)
+    finally:
+        os.close(fd)
+
+
+def prelim_written(ctx, handle, seed_names):
+    """Record that prelim_map() wrote `handle` from the device records that
+    are resident now (ctx.map_serial) for these seeds."""
+    global _prelim
+    ident, sums = _written_checksum(handle) if is_writer() else (None, None)
+    _prelim = dict(identity=ident, checksum=sums, serial=ctx.map_serial, key=_key,
+                   seeds=list(seed_names))
+
+
+def prelim_resident(ctx, handle, seed_names):
+    """True when `handle` is the prelim.csv this process's last prelim_map()
+    wrote, unchanged (the same file, size and crc32 / adler32 of its
+    content), and that pass's records are still resident: remap() then
+    takes the prelim rows from the device instead of parsing them again.  In
+    a sharded job rank 0 checks the file and every rank its own records."""
+    p = _prelim
+    ok = (p is not None and p['serial'] == ctx.map_serial and p['key'] == _key and
+          p['key'] is not None and p['seeds'] == list(seed_names))
+    if ok and is_writer():
+        ok = p['identity'] is not None and _identity(handle) == p['identity']
+        if ok:
+            try:
+                ok = _native.file_checksum(handle.fileno()) == p['checksum']
+            except (OSError, ValueError, _native.NativeError):
+                ok = False
+    sh = shard()
+    if sh is not None:
+        ok = bool(sh.min_i64([1 if ok else 0])[0])
+    return ok
 
 
 def invalidate():
