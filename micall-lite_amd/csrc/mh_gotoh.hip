@@ -64,7 +64,6 @@ struct GotohArgs {
     uint8_t *rowde;               // d / e bits of every strip's last row (strips x (n+1))
     unsigned long long *brow1;    // k_gotoh_fwd: R, P of every strip's last row (strips x (n+1))
     int *brow2;                   // k_gotoh_bwd: final abc of every strip's first row, by n - j
-    int *prog;                    // per strip: boundary columns published (fwd, then bwd)
     int *flags;                   // [0] a wait timed out
     const char *s1, *s2;
     char *out1, *out2;            // m + n + 1
@@ -143,33 +142,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, uint32_t 
     return __builtin_amdgcn_make_buffer_rsrc((void *)uni(p), (short)0, (int)uni(bytes), 0x00020000);
 }
 
-// Progress of a strip's boundary row (device scope: strips run on any CU).
-// A wait that outlasts any legitimate one (~0.25 s) sets flags[0] and gives
-// up, so a broken protocol ends the launch with an error instead of hanging.
-constexpr int GWAIT_MAX = 1 << 23;
-__device__ __forceinline__ void prog_wait(const int *c, int need, int *flags)
-{
-    for (int it = 0;; ++it) {
-        const int have = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (have >= need) return;
-        if (it >= GWAIT_MAX ||
-            __builtin_amdgcn_readfirstlane(__hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-            __hip_atomic_store(flags, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-__device__ __forceinline__ void prog_publish(int *c, int v)
-{
-    // the boundary cells before it were stored with device-coherent (sc1)
-    // stores: once they have completed the counter may be seen.  (A release
-    // fence at agent scope would also write back this XCD's whole L2, plane
-    // stores included.)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+constexpr int GWAIT_MAX = 1 << 23;   // polls before a wait is declared broken (~0.25 s)
 
 // boundary cells: device-coherent loads / stores (another strip, on any XCD,
 // reads them while this launch runs)
@@ -196,10 +169,44 @@ __device__ __forceinline__ void strip_of(const GotohStrips &S, int u, int &t, in
     q = u - S.first[lo];
 }
 
-// a boundary cell (R, P) as one 64-bit word
-__device__ __forceinline__ unsigned long long rp_pack(int r, int p)
+// A boundary cell of the forward pass as one 64-bit word written by one
+// store: R (26 bits, signed), P (26 bits, signed; all ones = infinity) and
+// the producing strip's tag (12 bits, never 0), so the reader polls the
+// cells themselves and the writer needs no store-completion wait.  The
+// host bounds |R|, |P| < 2^24.
+constexpr uint32_t RP_INF = 0x1FFFFFFu;
+__device__ __forceinline__ uint32_t strip_tag(int k) { return (uint32_t)(k % 4095) + 1; }
+__device__ __forceinline__ unsigned long long rp_pack(int r, int p, uint32_t tag)
 {
-    return (unsigned long long)(uint32_t)r | (unsigned long long)(uint32_t)p << 32;
+    const uint64_t pf = p == G_INF ? RP_INF : ((uint32_t)p & 0x3FFFFFFu);
+    return ((uint64_t)(uint32_t)r & 0x3FFFFFFu) | pf << 26 | (uint64_t)tag << 52;
+}
+__device__ __forceinline__ int rp_r(unsigned long long w) { return ((int)((uint32_t)w << 6)) >> 6; }
+__device__ __forceinline__ int rp_p(unsigned long long w)
+{
+    const uint32_t f = (uint32_t)(w >> 26) & 0x3FFFFFFu;
+    return f == RP_INF ? G_INF : ((int)(f << 6)) >> 6;
+}
+__device__ __forceinline__ uint32_t rp_tag(unsigned long long w) { return (uint32_t)(w >> 52); }
+
+// Poll a block of boundary cells (lanes 0..31 hold one each) until every
+// cell the block has carries the producing strip's tag.  A wait that
+// outlasts any legitimate one (~0.25 s) sets flags[0] and gives up, so a
+// broken protocol ends the launch with an error instead of hanging.
+template <class T, class Tag>
+__device__ __forceinline__ T poll_block(const T *p, int lane, bool has, Tag tagged, int *flags)
+{
+    T v{};
+    for (int it = 0;; ++it) {
+        if (has) v = dev_load(p + lane);
+        if (__builtin_amdgcn_ballot_w64(has && !tagged(v)) == 0) return v;
+        if (it >= GWAIT_MAX ||
+            __builtin_amdgcn_readfirstlane(__hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            __hip_atomic_store(flags, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return v;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
 }
 
 // Cost assignment of one strip.  Every cell's seven tie bits go to ONE plane
@@ -240,13 +247,12 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
     unsigned long long *below = A.brow1 + (size_t)k * W1;
     // de bits of row 64k - 1 (the strip above's last row), by column
     const __amdgpu_buffer_rsrc_t rside = brsrc(A.rowde + (size_t)(k - 1) * W1, consume ? (uint32_t)W1 : 0u);
-    const int *pabove = A.prog + (k - 1), *flags = A.flags;
-    int *pme = A.prog + k;
+    const int *flags = A.flags;
     int Rme = 0, Pme = G_INF, Qme = G_INF;   // this lane's cell of the last step: (i, j - 1)
     int Rdg = 0;                              // R(i - 1, j - 1): the row above one step ago
     int bcode = 0;                            // seq2 code of column j - 1
     int abcp = 0;                             // abc of (i, j - 1), stored this step
-    unsigned long long blk = rp_pack(0, G_INF);   // lanes 0..31: the row above, this block's columns
+    unsigned long long blk = 0;                  // lanes 0..31: the row above, this block's columns
     // plane bases of diagonals s = 64 k + t and s - 1, kept running:
     // D(s + 1) = D(s) + len(s)
     int64_t Ds = doff_of(64 * k, m + 1, n + 1);
@@ -255,19 +261,22 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
         const int j = t - lane;
         const int tq = t & (GBLK - 1);
         if (consume && tq == 0 && t <= n) {
-            // this block of the row above: wait for it, load it, and use it
-            // at once (the wait then covers the load only here, not at
-            // every step's read)
-            prog_wait(pabove, t + GBLK < W1 ? t + GBLK : W1, (int *)flags);
-            if (lane < GBLK && t + lane < W1) blk = dev_load(above + t + lane);
+            // this block of the row above: poll its cells until they carry
+            // the strip above's tag, and use them at once (the wait then
+            // covers the load only here, not at every step's read)
+            const uint32_t want = strip_tag(k - 1);
+            blk = poll_block(above + t, lane, lane < GBLK && t + lane < W1,
+                             [&](unsigned long long w) { return rp_tag(w) == want; }, (int *)flags);
             asm volatile("; touch %0" : "+v"(blk));
         }
         int Rup = from_prev_lane(0, Rme), Pup = from_prev_lane(G_INF, Pme);
         const int bnew = (t >= 1 && t <= n) ? (BCL ? (int)bcl[t - 1] : (int)A.b[t - 1]) : 0;
         bcode = from_prev_lane(bnew, bcode);
         if (consume && t <= n) {
-            const int r0 = __builtin_amdgcn_readlane((int)(uint32_t)blk, tq);
-            const int p0 = __builtin_amdgcn_readlane((int)(uint32_t)(blk >> 32), tq);
+            const int r0 = rp_r(((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(blk >> 32), tq) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)blk, tq));
+            const int p0 = rp_p(((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(blk >> 32), tq) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)blk, tq));
             Rup = lane == 0 ? r0 : Rup;
             Pup = lane == 0 ? p0 : Pup;
         }
@@ -295,9 +304,12 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(abcp | fg | (lane == 63 ? 0 : deb)), rbits,
                                              pend ? (uint32_t)i : GOOB, b1, 0);
         // the first lane's de belongs to the strip above's last row
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)de, rside, (lane == 0 && act) ? (uint32_t)j : GOOB, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(r, rcol, (act && j == n) ? 4u * (uint32_t)i : GOOB, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(r, rrow, (act && i == m) ? 4u * (uint32_t)j : GOOB, 0, 0);
+        if (consume)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)de, rside, (lane == 0 && act) ? (uint32_t)j : GOOB, 0, 0);
+        if (t >= n)   // some lane is at column n
+            __builtin_amdgcn_raw_buffer_store_b32(r, rcol, (act && j == n) ? 4u * (uint32_t)i : GOOB, 0, 0);
+        if (!produce)   // the last strip holds row m
+            __builtin_amdgcn_raw_buffer_store_b32(r, rrow, (act && i == m) ? 4u * (uint32_t)j : GOOB, 0, 0);
         abcp = act ? abc : 0;
         Rdg = Rup;
         Rme = act ? r : 0;
@@ -305,11 +317,7 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
         Qme = act ? q : G_INF;
         // the strip's last row (lane 63, column t - 63) to the strip below
         const int jp = t - 63;
-        if (produce && jp >= 0 && jp <= n) {
-            if (lane == 63) dev_store(below + jp, rp_pack(r, p));
-            if (((jp + 1) & (GBLK - 1)) == 0 || jp == n)
-                if (lane == 63) prog_publish(pme, jp + 1);
-        }
+        if (produce && jp >= 0 && jp <= n && lane == 63) dev_store(below + jp, rp_pack(r, p, strip_tag(k)));
     }
 }
 
@@ -340,8 +348,7 @@ __global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
     int *mytop = A.brow2 + (size_t)k * W1;
     // de bits of this strip's last row (stored by the strip below), by column
     const __amdgpu_buffer_rsrc_t rside = brsrc(A.rowde + (size_t)k * W1, consume ? (uint32_t)W1 : 0u);
-    const int *punder = A.prog + ns + (k + 1), *flags = A.flags;   // bwd counters after the fwd ones
-    int *pme = A.prog + ns + k;
+    const int *flags = A.flags;
     int mine = 0;        // final abc of (i, j + 1): this lane, one step ago
     int dnp = 0;         // final abc of (i + 1, j + 1): the lane below, two steps ago
     // plane base of the step's diagonal s = 64 k + n + 63 - t, running down:
@@ -363,11 +370,13 @@ __global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
     load_block(0, cx);
     for (int t0 = 0; t0 <= n + 63; t0 += GBLK) {
         // the strip below's first row for this block (lane 63's cells below)
-        // and lanes 0..31: the de side bits of lane 63's cells (column n - t)
+        // (tagged with the strip below's tag), and lanes 0..31: the de side
+        // bits of lane 63's cells (column n - t)
         int blk = 0, side = 0;
         if (consume && t0 <= n) {
-            prog_wait(punder, t0 + GBLK < W1 ? t0 + GBLK : W1, (int *)flags);
-            if (lane < GBLK && t0 + lane < W1) blk = dev_load(under + t0 + lane);
+            const int want = (k + 1) % 0xFFFFFF + 1;
+            blk = poll_block(under + t0, lane, lane < GBLK && t0 + lane < W1,
+                             [&](int w) { return (w >> 8) == want; }, (int *)flags);
             side = __builtin_amdgcn_raw_buffer_load_b8(rside, (lane < GBLK && t0 + lane <= n) ?
                                                        (uint32_t)(n - t0 - lane) : GOOB, 0, 0);
         }
@@ -380,7 +389,7 @@ __global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
             const int t = t0 + q;
             const int j = n + 63 - lane - t;
             int dnb = from_next_lane(0, mine);                   // final abc of (i + 1, j)
-            const int d63 = __builtin_amdgcn_readlane(blk, q);
+            const int d63 = __builtin_amdgcn_readlane(blk, q) & 0xFF;
             dnb = (lane == 63 && consume && t <= n) ? d63 : dnb;
             const bool act = rowok && j >= 0 && j <= n;
             const bool lastc = j == n;
@@ -410,11 +419,7 @@ __global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
             const bool act = rowok && j >= 0 && j <= n && t <= n + 63;
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ox[q], rbits, act ? (uint32_t)i : GOOB, b0, 0);
             const int tp = t - 63;
-            if (produce && tp >= 0 && tp <= n && lane == 0) dev_store(mytop + tp, ox[q]);
-        }
-        if (produce && t0 + GBLK - 1 - 63 >= 0) {
-            const int tp_end = t0 + GBLK - 1 - 63 < n ? t0 + GBLK - 1 - 63 : n;
-            if (lane == 0) prog_publish(pme, tp_end + 1);
+            if (produce && tp >= 0 && tp <= n && lane == 0) dev_store(mytop + tp, (k % 0xFFFFFF + 1) << 8 | ox[q]);
         }
 #pragma unroll
         for (int q = 0; q < GBLK; ++q) cx[q] = nx[q];
@@ -534,8 +539,7 @@ static size_t gotoh_work_bytes(int m, int n)
     const size_t strips = (size_t)(m + 1 + 63) / 64;
     return align16(sizeof(int) * (m + 2)) + align16(sizeof(int) * (n + 2)) +
            align16((size_t)(m + 2) * (n + 2)) + align16(8 * strips * (n + 1)) +
-           align16(sizeof(int) * strips * (n + 1)) + align16(strips * (n + 1)) +
-           align16(sizeof(int) * 2 * strips) + 16;
+           align16(sizeof(int) * strips * (n + 1)) + align16(strips * (n + 1)) + 16;
 }
 
 // Retained scratch above this is released after the call (one very long
@@ -552,6 +556,9 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
     int code[256];
     for (int k = 0; k < 256; ++k) code[k] = -1;
     for (int k = 0; k < L; ++k) code[(unsigned char)alphabet[k]] = k;
+    int64_t mat_max = 0;
+    for (int x = 0; x < L * L; ++x) mat_max = std::max<int64_t>(mat_max, std::abs((int64_t)matrix[x]));
+    if (gop < 0 || gep < 0 || gop > (1 << 16) || gep > (1 << 16)) { set_error("mh_gotoh_align: bad gap penalties"); return -3; }
     std::vector<int> ms(count), ns(count);
     std::vector<size_t> io(count + 1, 0), work(count + 1, 0);
     for (int t = 0; t < count; ++t) {
@@ -567,6 +574,11 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
         for (int j = 0; j < ns[t]; ++j)
             if (code[(unsigned char)s2[t][j]] < 0) { set_error("mh_gotoh_align: '%c' not in alphabet", s2[t][j]); return -3; }
         io[t + 1] = io[t] + gotoh_io_bytes(ms[t], ns[t]);
+        // boundary cells carry R and P in 26 bits (k_gotoh_fwd rp_pack)
+        if ((int64_t)(ms[t] + ns[t] + 2) * (mat_max + gop + gep + 1) >= ((int64_t)1 << 24)) {
+            set_error("mh_gotoh_align: alignment %d too long for the score range", t);
+            return -3;
+        }
         if ((uint64_t)(ms[t] + 2) * (uint64_t)(ns[t] + 2) >= (uint64_t)GOOB) {
             set_error("mh_gotoh_align: alignment %d too large (%d x %d)", t, ms[t], ns[t]);
             return -3;
@@ -610,7 +622,6 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
         A.brow1 = (unsigned long long *)take_w(8 * strips * (n + 1));
         A.brow2 = (int *)take_w(sizeof(int) * strips * (n + 1));
         A.rowde = (uint8_t *)take_w(strips * (n + 1));
-        A.prog = (int *)take_w(sizeof(int) * 2 * strips);
         A.flags = (int *)take_w(16);
         for (int i = 0; i < m; ++i) img[oa + i] = (char)code[(unsigned char)s1[t][i]];
         for (int j = 0; j < n; ++j) img[ob + j] = (char)code[(unsigned char)s2[t][j]];

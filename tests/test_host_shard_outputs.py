@@ -62,7 +62,7 @@ def _worker(rank, world, port, out_dir):
         ctx = _RowsCtx(refs, lo)
         # prelim.csv groups
         out = io.StringIO()
-        pm._write_sharded(ctx, sh, refs[lo:hi], N_REFS, out, None)
+        pm._write_sharded(ctx, sh, refs[lo:hi], N_REFS, out)
         # remap.csv rows / unmapped reads in rank order, two outputs at once
         a, b = io.StringIO(), io.StringIO()
         mine = [('r%d\n' % i).encode() for i in range(lo, hi)]
