@@ -101,17 +101,18 @@ def cpu_baseline(sample_pairs):
     for threads in sorted({cpus['sched_getaffinity'], cpus['share_threads']}, reverse=True):
         _, secs = cpu_pipeline.timed_step(seed_set, cfg.all_region_sequences(), groups, prep, threads)
         runs[threads] = secs
-    allc = cpus['sched_getaffinity']
-    return {'value': round(2 * sample_pairs / runs[allc], 1), 'unit': 'reads/s', 'cores': allc,
+    allc, share = cpus['sched_getaffinity'], cpus['share_threads']
+    best = min(runs, key=runs.get)   # the faster of the two is the baseline
+    return {'value': round(2 * sample_pairs / runs[best], 1), 'unit': 'reads/s', 'cores': best,
             'kind': 'port', 'host_cpus': cpus,
-            'at_share': {'value': round(2 * sample_pairs / runs[cpus['share_threads']], 1),
-                         'cores': cpus['share_threads']},
+            'runs': {str(t): {'seconds': round(s, 3), 'value': round(2 * sample_pairs / s, 1)}
+                     for t, s in sorted(runs.items())},
             'sample': '{} synthetic pairs (first block of the bench input): prelim e2e pass over '
                       '74 seeds + 1 local remap pass + 2 pileups/consensus, oracle C restatement '
-                      '(og_map, og_pileup_mt) with OpenMP over pairs on all {} host cores ({:.1f} s; '
-                      'on the {}-thread CPU share: {:.1f} s), reads packed before timing'.format(
-                          sample_pairs, allc, runs[allc], cpus['share_threads'],
-                          runs[cpus['share_threads']])}
+                      '(og_map, og_pileup_mt) with OpenMP over pairs, timed on all {} host cores '
+                      '({:.1f} s) and on the {}-thread CPU share ({:.1f} s); value is the faster; '
+                      'reads packed before timing'.format(
+                          sample_pairs, allc, runs[allc], share, runs[share])}
 
 
 def cpu_end_to_end(sample_pairs, workdir):
