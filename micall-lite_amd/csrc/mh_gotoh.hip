@@ -36,6 +36,8 @@
 #include <limits.h>
 
 #include <mutex>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "mh_internal.h"
@@ -43,10 +45,10 @@
 namespace mh {
 
 constexpr int G_INF = INT_MAX;
+constexpr int G_HUGE = 1 << 29;
 enum { GA = 1, GB = 2, GC = 4, GD = 8, GE_ = 16, GF = 32, GG = 64 };
 constexpr int GOTOH_THREADS = 1024;        // k_gotoh_tb
 constexpr int GBLK = 32;                   // boundary columns published / awaited at a time
-constexpr int GBC_MAX = 32 * 1024;         // seq2 codes kept in LDS up to this length
 constexpr uint32_t GOOB = 0x80000000u;     // a buffer offset past every plane (planes < 2 GiB)
 constexpr int TB = 128;                                // traceback window (diagonals x rows)
 constexpr size_t TB_LDS = (size_t)TB * TB + 2 * TB;   // window + both sequences' characters
@@ -58,6 +60,7 @@ struct GotohArgs {
     const int8_t *b;      // seq2 codes, n
     int m, n, L;
     const int *mat;       // L x L
+    const int8_t *prof;   // L x prof_width(n): the score profile
     int u, v, is_global;
     int *lastcol, *lastrow;       // R(i, n), R(m, j)
     uint8_t *bits;                // (m+2) x (n+2) tie bits a..g of every cell, anti-diagonal-major
@@ -76,7 +79,20 @@ struct GotohStrips {
     const int *first;             // per alignment: its first ticket; [count] = total
     int count;
     int *ticket;                  // [0] fwd, [1] bwd
+    // diagnostics (MH_GOTOH_STAMPS=path, else null): per ticket and block,
+    // the shader clock before and after the block's wait, fwd then bwd
+    unsigned long long *stamps;
+    int stamp_blocks;
 };
+
+// a diagnostic clock stamp (lane 0 stores it)
+__device__ __forceinline__ void stamp(const GotohStrips &S, int pass, int u, int blk, int which)
+{
+    if (S.stamps == nullptr || blk >= S.stamp_blocks) return;
+    const unsigned long long now = clock64();
+    if (threadIdx.x == 0)
+        S.stamps[(((size_t)pass * S.first[S.count] + u) * S.stamp_blocks + blk) * 2 + which] = now;
+}
 
 __device__ __forceinline__ int gmin(int x, int y) { return x <= y ? x : y; }
 
@@ -146,15 +162,18 @@ constexpr int GWAIT_MAX = 1 << 23;   // polls before a wait is declared broken (
 
 // boundary cells: device-coherent loads / stores (another strip, on any XCD,
 // reads them while this launch runs)
+// through global (not flat) instructions: a flat access also counts in
+// lgkmcnt, so every later LDS wait would wait for the store's round trip
 template <class T>
 __device__ __forceinline__ T dev_load(const T *p)
 {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load((const __attribute__((address_space(1))) T *)p, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
 }
 template <class T>
 __device__ __forceinline__ void dev_store(T *p, T v)
 {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((__attribute__((address_space(1))) T *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // the strip of ticket u: (alignment, index in ticket order)
@@ -201,12 +220,38 @@ __device__ __forceinline__ T poll_block(const T *p, int lane, bool has, Tag tagg
         if (has) v = dev_load(p + lane);
         if (__builtin_amdgcn_ballot_w64(has && !tagged(v)) == 0) return v;
         if (it >= GWAIT_MAX ||
-            __builtin_amdgcn_readfirstlane(__hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-            __hip_atomic_store(flags, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_readfirstlane(dev_load(flags))) {
+            dev_store(flags, 1);
             return v;
         }
         __builtin_amdgcn_s_sleep(2);
     }
+}
+
+// The score profile: row c holds the score of seq1 code c against every
+// column of seq2 (mat[c][b[j - 1]] at c * PW + PROF_PAD + j; zero outside
+// 1..n), so a lane at column j reads its score at a fixed per-lane base + t.
+constexpr int PROF_PAD = 128;                       // >= 64 columns before 1 and 96 after n
+constexpr size_t GPROF_LDS_MAX = 64 * 1024;         // profiles up to this stay in LDS
+__host__ __device__ inline int prof_width(int n) { return (int)gotoh_al16((size_t)n + 2 * PROF_PAD); }
+
+// unrolled calls f(integral_constant<int, Q>) for Q = 0 .. N - 1
+template <class F, int... Q>
+__device__ __forceinline__ void unroll_seq(F &&f, std::integer_sequence<int, Q...>)
+{
+    (f(std::integral_constant<int, Q>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void unroll(F &&f)
+{
+    unroll_seq(f, std::make_integer_sequence<int, N>{});
+}
+
+// lane l <- lane l + 1; lane 63 <- x: after GBLK steps lanes 64 - GBLK ..
+// 63 hold lane 63's values of the block's steps in order
+__device__ __forceinline__ int shift_in63(int x, int reg)
+{
+    return __builtin_amdgcn_update_dpp(x, reg, 0x130, 0xF, 0xF, false);
 }
 
 // Cost assignment of one strip.  Every cell's seven tie bits go to ONE plane
@@ -215,7 +260,20 @@ __device__ __forceinline__ T poll_block(const T *p, int lane, bool has, Tag tagg
 // gets de of (i, j - 1) from the lane below (cell (i + 1, j - 1)) by a lane
 // shift.  The strip's last row gets its de bits from the next strip's first
 // lane, which stores them in a side row (rowde).
-template <bool BCL>   // seq2's codes in LDS (else read from global memory every step)
+//
+// The steps run in blocks of GBLK.  At a block's start the row above's
+// cells for its columns go to LDS (every lane reads step q's cell there, a
+// broadcast), and the plane bases of its steps to lanes 0..31 (read back by
+// lane index); lane 63's cells of the block's steps are shifted into lanes
+// 32..63 as they come and published to the strip below by one store at the
+// block's end.  Lanes off the grid (a column below 0 or above n, a row above
+// m) compute garbage instead of testing their column: off-grid values only
+// ever flow to off-grid cells (a lane's inputs are its own previous column
+// and the lane above's same column) and the stores test their cell.  So a
+// block away from the columns 0, 1 and n (the bulk of the grid) needs no
+// per-lane test at all (EDGE false), and only the first strip (row 0) and
+// the last (row m) carry their own few (TL).
+template <bool PL>   // the score profile in LDS (else read from global memory)
 __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
@@ -228,12 +286,15 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
     const GotohArgs &A = S.args[ta];
     const int m = uni(A.m), n = uni(A.n), L = uni(A.L), uu = uni(A.u), v = uni(A.v);
     const bool glob = uni(A.is_global);
-    int *mat = (int *)gsm;
-    int8_t *bcl = (int8_t *)(gsm + gotoh_al16(sizeof(int) * L * L));
-    for (int x = lane; x < L * L; x += 64) mat[x] = A.mat[x];
-    if (BCL)
-        for (int x = lane; x < n; x += 64) bcl[x] = A.b[x];
-    __syncthreads();
+    const int PW = prof_width(n);
+    int2 *brd = (int2 *)gsm;                        // the row above at the block's columns
+    int8_t *lprof = (int8_t *)(gsm + sizeof(int2) * GBLK);
+    if (PL) {
+        const uint4 *src = (const uint4 *)uni(A.prof);
+        for (int x = lane; x < L * PW / 16; x += 64) ((uint4 *)lprof)[x] = src[x];
+        __syncthreads();
+    }
+    const int8_t *prof = PL ? lprof : (const int8_t *)(const __attribute__((address_space(1))) int8_t *)uni(A.prof);
     const int ns = (m + 1 + 63) / 64;
     const int W1 = n + 1;
     const int64_t cells = (int64_t)(m + 2) * (n + 2);
@@ -241,92 +302,160 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
     const __amdgpu_buffer_rsrc_t rcol = brsrc(A.lastcol, 4u * (m + 1)), rrow = brsrc(A.lastrow, 4u * (n + 1));
     const int i = 64 * k + lane;
     const bool rowok = i <= m;
-    const int arow = (i >= 1 && rowok) ? A.a[i - 1] * L : 0;
+    const int code = (i >= 1 && rowok) ? A.a[i - 1] : 0;
+    const int prow = code * PW + PROF_PAD - lane;   // + t: the score of column t - lane
     const bool produce = k + 1 < ns, consume = k > 0;
+    const bool tl = k == 0 || !produce;             // the first or the last strip
     const unsigned long long *above = A.brow1 + (size_t)(k - 1) * W1;   // row 64k - 1
     unsigned long long *below = A.brow1 + (size_t)k * W1;
-    // de bits of row 64k - 1 (the strip above's last row), by column
+    // de bits of row 64k - 1 (the strip above's last row), by n - column
     const __amdgpu_buffer_rsrc_t rside = brsrc(A.rowde + (size_t)(k - 1) * W1, consume ? (uint32_t)W1 : 0u);
+    const uint32_t plane_off = rowok ? (uint32_t)i : GOOB;
+    const uint32_t col_off = rowok ? 4u * (uint32_t)i : GOOB;
+    const int de_keep = i < m ? 0x7F : 0;           // row m takes no de bits from below
+    const bool top = i == 0;
+    const bool left_p = glob && !top;               // column 0 holds P (global) or 0
     const int *flags = A.flags;
-    int Rme = 0, Pme = G_INF, Qme = G_INF;   // this lane's cell of the last step: (i, j - 1)
-    int Rdg = 0;                              // R(i - 1, j - 1): the row above one step ago
-    int bcode = 0;                            // seq2 code of column j - 1
+    const uint32_t tag = strip_tag(k);
+    // this lane's cell of the last step, (i, j - 1), and R(i - 1, j - 1), the
+    // row above one step ago.  Before column 0 they start huge: the values
+    // off the grid to the left then stay far above every real one, so that
+    // a global alignment's column 0 (R = P, Q infinite, no c tie) needs no
+    // test of its own (G_HUGE + 64 steps of drift stays below G_INF)
+    int Rme = G_HUGE, Pme = G_HUGE, Qme = G_HUGE;
+    int Rdg = G_HUGE;
     int abcp = 0;                             // abc of (i, j - 1), stored this step
-    unsigned long long blk = 0;                  // lanes 0..31: the row above, this block's columns
-    // plane bases of diagonals s = 64 k + t and s - 1, kept running:
-    // D(s + 1) = D(s) + len(s)
-    int64_t Ds = doff_of(64 * k, m + 1, n + 1);
-    int64_t Dprev = Ds - (k > 0 ? dlen(64 * k - 1, m + 1, n + 1) : 0);
-    for (int t = 0; t <= n + 64; ++t) {
-        const int j = t - lane;
-        const int tq = t & (GBLK - 1);
-        if (consume && tq == 0 && t <= n) {
+    int pR = 0, pP = 0;                       // lanes 32..63: lane 63's R, P at the block's steps
+    for (int t0 = 0; t0 <= n + 64; t0 += GBLK) {
+        stamp(S, 0, u, t0 / GBLK, 0);
+        int aR = 0, aP = G_INF;
+        if (consume && t0 <= n) {
             // this block of the row above: poll its cells until they carry
-            // the strip above's tag, and use them at once (the wait then
-            // covers the load only here, not at every step's read)
+            // the strip above's tag
             const uint32_t want = strip_tag(k - 1);
-            blk = poll_block(above + t, lane, lane < GBLK && t + lane < W1,
-                             [&](unsigned long long w) { return rp_tag(w) == want; }, (int *)flags);
-            asm volatile("; touch %0" : "+v"(blk));
+            const unsigned long long w = poll_block(above + t0, lane, lane < GBLK && t0 + lane < W1,
+                                                    [&](unsigned long long x) { return rp_tag(x) == want; },
+                                                    (int *)flags);
+            aR = rp_r(w);
+            aP = rp_p(w);
         }
-        int Rup = from_prev_lane(0, Rme), Pup = from_prev_lane(G_INF, Pme);
-        const int bnew = (t >= 1 && t <= n) ? (BCL ? (int)bcl[t - 1] : (int)A.b[t - 1]) : 0;
-        bcode = from_prev_lane(bnew, bcode);
-        if (consume && t <= n) {
-            const int r0 = rp_r(((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(blk >> 32), tq) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)blk, tq));
-            const int p0 = rp_p(((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(blk >> 32), tq) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)blk, tq));
-            Rup = lane == 0 ? r0 : Rup;
-            Pup = lane == 0 ? p0 : Pup;
+        if (lane < GBLK) brd[lane] = make_int2(aR, aP);
+        stamp(S, 0, u, t0 / GBLK, 1);
+        // lane q: the plane base of the diagonal s - 1 stored at step t0 + q
+        int vb1;
+        {
+            const int64_t sd = (int64_t)64 * k + t0 + lane - 1;
+            const int64_t sc = sd < 0 ? 0 : sd;
+            vb1 = (int)(doff_of(sc, m + 1, n + 1) - (sc - (n + 1) > 0 ? sc - (n + 1) : 0));
         }
-        const bool act = rowok && j >= 0 && j <= n;
-        const bool top = i == 0, left = j == 0;
-        const int pm = gmin(Pup, Rup + v);
-        const int p = top ? G_INF : uu + pm;
-        const int qm = gmin(Qme, Rme + v);
-        const int q = left ? G_INF : uu + qm;
-        // de of (i - 1, j) and fg of (i, j - 1)
-        const int de = (act && !top) ? ((Pup != G_INF && pm == Pup) ? GD : 0) | (pm == Rup + v ? GE_ : 0) : 0;
-        const int fg = (act && !left) ? ((Qme != G_INF && qm == Qme) ? GF : 0) | (qm == Rme + v ? GG : 0) : 0;
-        const int dg = Rdg - mat[arow + bcode];
-        const int border = glob ? gmin(p, q) : 0;
-        const int r = (top && left) ? 0 : ((top || left) ? border : gmin(gmin(dg, p), q));
-        const int abc = (r == p ? GA : 0) | (r == q ? GB : 0) | ((!top && !left && r == dg) ? GC : 0);
-        // the byte of (i, j - 1): its abc (last step), fg (this lane now) and
-        // de (the lane below now; the strip's last row: rowde)
-        const int deb = from_next_lane(0, de);
-        const int s = 64 * k + t;
-        const uint32_t b1 = (uint32_t)(Dprev - (s - 1 - (n + 1) > 0 ? s - 1 - (n + 1) : 0));
-        Dprev = Ds;
-        Ds += dlen(s, m + 1, n + 1);
-        const bool pend = rowok && j >= 1 && j <= n + 1;
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(abcp | fg | (lane == 63 ? 0 : deb)), rbits,
-                                             pend ? (uint32_t)i : GOOB, b1, 0);
-        // the first lane's de belongs to the strip above's last row
-        if (consume)
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)de, rside, (lane == 0 && act) ? (uint32_t)j : GOOB, 0, 0);
-        if (t >= n)   // some lane is at column n
-            __builtin_amdgcn_raw_buffer_store_b32(r, rcol, (act && j == n) ? 4u * (uint32_t)i : GOOB, 0, 0);
-        if (!produce)   // the last strip holds row m
-            __builtin_amdgcn_raw_buffer_store_b32(r, rrow, (act && i == m) ? 4u * (uint32_t)j : GOOB, 0, 0);
-        abcp = act ? abc : 0;
-        Rdg = Rup;
-        Rme = act ? r : 0;
-        Pme = act ? p : G_INF;
-        Qme = act ? q : G_INF;
-        // the strip's last row (lane 63, column t - 63) to the strip below
-        const int jp = t - 63;
-        if (produce && jp >= 0 && jp <= n && lane == 63) dev_store(below + jp, rp_pack(r, p, strip_tag(k)));
+        const int pbase = prow + t0;
+        // rowde is stored by n - j (k_gotoh_bwd reads it forward): lane 0 at
+        // step t0 + q writes n - t0 - q = side_v + GBLK - 1 - q
+        const uint32_t side_v = lane == 0 ? (uint32_t)(n - t0 - (GBLK - 1)) : GOOB;
+        const uint32_t side_r = lane == 0 ? (uint32_t)(n - t0) : GOOB;   // a right block: n - t0 - q, exact
+        const uint32_t lrow_v = i == m ? 4u * (uint32_t)(t0 - lane) : GOOB;
+        const int j0 = t0 - lane;
+        // LEFT: a lane may be at column 0; RIGHT: at column n or past it
+        // PRED: a lane's column may lie off the grid (its store is dropped)
+        auto step = [&](auto leftc, auto rightc, auto tlc, auto predc, int q) {
+            constexpr bool LEFT = decltype(leftc)::value, RIGHT = decltype(rightc)::value;
+            constexpr bool TL = decltype(tlc)::value, PRED = LEFT || RIGHT || decltype(predc)::value;
+            const int t = t0 + q, j = j0 + q;
+            const int2 bd = brd[q];
+            const int sc = prof[pbase + q];
+            const int Rup = __builtin_amdgcn_update_dpp(bd.x, Rme, 0x138, 0xF, 0xF, false);
+            const int Pup = __builtin_amdgcn_update_dpp(bd.y, Pme, 0x138, 0xF, 0xF, false);
+            const int dg = Rdg - sc;
+            const int Ru = Rup + v, Rv = Rme + v;
+            const int pm = gmin(Pup, Ru), qm = gmin(Qme, Rv);
+            int p = uu + pm, qv = uu + qm;
+            // de of (i - 1, j) and fg of (i, j - 1); a P or Q of infinity
+            // never equals its finite minimum
+            const int de = (pm == Pup ? GD : 0) | (pm == Ru ? GE_ : 0);
+            int fg = (qm == Qme ? GF : 0) | (qm == Rv ? GG : 0);
+            int r = gmin(gmin(dg, p), qv), ctie = r == dg ? GC : 0;
+            if constexpr (TL) {   // row 0: P infinite, R the border
+                p = top ? G_INF : p;
+                r = top ? (glob ? qv : 0) : r;
+                ctie = top ? 0 : ctie;
+            }
+            if constexpr (LEFT) {   // column 0: Q infinite, R the border
+                const bool left = j == 0;
+                qv = left ? G_INF : qv;
+                fg = left ? 0 : fg;
+                r = left ? (left_p ? p : 0) : r;
+                ctie = left ? 0 : ctie;
+            }
+            if constexpr (RIGHT) fg = j > n ? 0 : fg;   // no f/g past column n
+            const int abc = (r == p ? GA : 0) | (r == qv ? GB : 0) | ctie;
+            // the byte of (i, j - 1): its abc (last step), fg (this lane now)
+            // and de (the lane below now; the strip's last row: rowde)
+            int deb = __builtin_amdgcn_mov_dpp(de, 0x130, 0xF, 0xF, true);
+            if constexpr (TL) deb &= de_keep;
+            uint32_t off = plane_off;
+            if constexpr (PRED) off = (uint32_t)(j - 1) <= (uint32_t)n ? off : GOOB;
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(abcp | fg | deb), rbits, off,
+                                                 __builtin_amdgcn_readlane(vb1, q), 0);
+            // the first lane's de belongs to the strip above's last row
+            if constexpr (RIGHT)   // n - t below 0 is past the side row
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)de, rside, side_r - (uint32_t)q, 0, 0);
+            else
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)de, rside, side_v + (GBLK - 1 - q), 0, 0);
+            if constexpr (RIGHT) __builtin_amdgcn_raw_buffer_store_b32(r, rcol, j == n ? col_off : GOOB, 0, 0);
+            if constexpr (TL) __builtin_amdgcn_raw_buffer_store_b32(r, rrow, lrow_v + 4 * q, 0, 0);
+            abcp = abc;
+            Rdg = Rup;
+            Rme = r;
+            Pme = p;
+            Qme = qv;
+            pR = shift_in63(r, pR);
+            pP = shift_in63(p, pP);
+        };
+        // the block's kind (every kind unrolled: a slow block anywhere in a
+        // strip delays every strip below it)
+        const bool left = t0 < 64, right = t0 + GBLK > n;
+        constexpr std::true_type Y{};
+        constexpr std::false_type N{};
+        if (right && left) {   // n < 64 + GBLK - 1: short rows
+            if (tl) {
+                for (int q = 0; q < GBLK; ++q) step(Y, Y, Y, N, q);
+            } else {
+                for (int q = 0; q < GBLK; ++q) step(Y, Y, N, N, q);
+            }
+        } else if (right) {
+            if (tl) unroll<GBLK>([&](auto qc) { step(N, Y, Y, N, decltype(qc)::value); });
+            else unroll<GBLK>([&](auto qc) { step(N, Y, N, N, decltype(qc)::value); });
+        } else if (left) {
+            // a middle strip of a global alignment: column 0 comes out of
+            // the huge start values, only the stores test their column
+            if (tl) unroll<GBLK>([&](auto qc) { step(Y, N, Y, N, decltype(qc)::value); });
+            else if (glob) unroll<GBLK>([&](auto qc) { step(N, N, N, Y, decltype(qc)::value); });
+            else unroll<GBLK>([&](auto qc) { step(Y, N, N, N, decltype(qc)::value); });
+        } else {
+            if (tl) unroll<GBLK>([&](auto qc) { step(N, N, Y, N, decltype(qc)::value); });
+            else unroll<GBLK>([&](auto qc) { step(N, N, N, N, decltype(qc)::value); });
+        }
+        // the strip's last row (lane 63 at column t - 63) to the strip below
+        const int jp = t0 + lane - (64 - GBLK) - 63;
+        if (produce && lane >= 64 - GBLK && jp >= 0 && jp <= n) dev_store(below + jp, rp_pack(pR, pP, tag));
     }
 }
 
-// Edge assignment of one strip (bottom-up, right to left).  Each block of
-// GBLK steps first loads the block's plane bytes (loaded during the block
-// before), then computes, then stores the block's final bytes: loads and
-// stores never interleave inside a block, so no step waits on a store.
+// Edge assignment of one strip (bottom-up, right to left): lane l at step t
+// is at column j = n + 63 - l - t.  Each block of GBLK steps first takes the
+// row below's final bits for its steps (polled; to LDS, read back by every
+// lane as a broadcast), then computes from the block's plane bytes (loaded
+// during the block before, with lane 63's de side bits), then stores the
+// block's final bytes: loads and stores never interleave inside a block, so
+// no step waits on a store.  Lane 0's results are shifted into lanes 0..31
+// as they come and published to the strip above by one store per block.
+// As in k_gotoh_fwd, lanes off the grid compute garbage that only reaches
+// off-grid cells; a block away from the columns n and below 0 (EDGE false)
+// tests nothing per lane, and only the last strip (row m, TL) tests its row.
 __global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
 {
+    extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
+    int *bw = (int *)gsm;   // the row below's final abc at the block's steps
     const int lane = threadIdx.x;
     int u = 0;
     if (lane == 0) u = atomicAdd(&S.ticket[1], 1);
@@ -340,89 +469,107 @@ __global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
     const int W1 = n + 1;
     const int64_t cells = (int64_t)(m + 2) * (n + 2);
     const __amdgpu_buffer_rsrc_t rbits = brsrc(A.bits, (uint32_t)cells);
-    const uint8_t bnd = A.is_global ? 0 : GC;
+    const int bnd = A.is_global ? 0 : GC;
     const int i = 64 * k + lane;
     const bool rowok = i <= m, lastr = i == m;
     const bool produce = k > 0, consume = k + 1 < ns;
+    const bool tl = !consume;                  // the last strip: row m and past it
     const int *under = A.brow2 + (size_t)(k + 1) * W1;   // row 64k + 64, by tau = n - j
     int *mytop = A.brow2 + (size_t)k * W1;
-    // de bits of this strip's last row (stored by the strip below), by column
+    // de bits of this strip's last row (stored by the strip below), by n - j
     const __amdgpu_buffer_rsrc_t rside = brsrc(A.rowde + (size_t)k * W1, consume ? (uint32_t)W1 : 0u);
+    const uint32_t plane_off = rowok ? (uint32_t)i : GOOB;
+    const uint32_t side_off = lane == 63 ? 0u : GOOB;   // + t: lane 63 is at column n - t
     const int *flags = A.flags;
+    const int s0 = 64 * k + n + 63;            // the diagonal of step 0
+    const int tagk = (k % 0xFFFFFF + 1) << 8;
     int mine = 0;        // final abc of (i, j + 1): this lane, one step ago
     int dnp = 0;         // final abc of (i + 1, j + 1): the lane below, two steps ago
-    // plane base of the step's diagonal s = 64 k + n + 63 - t, running down:
-    // D(s - 1) = D(s) - len(s - 1)
-    const int s0 = 64 * k + n + 63;
-    int64_t Dld = doff_of(s0, m + 1, n + 1), Dst = Dld;
-    int cx[GBLK], nx[GBLK], ox[GBLK];
-    // the plane bytes of steps t0 .. t0 + GBLK - 1
-    auto load_block = [&](int t0b, int *dst) {
-#pragma unroll
-        for (int q = 0; q < GBLK; ++q) {
-            const int tt = t0b + q, jj = n + 63 - lane - tt, sd = s0 - tt;
-            const uint32_t base = (uint32_t)(Dld - (sd - (n + 1) > 0 ? sd - (n + 1) : 0));
-            const bool ok = rowok && jj >= 0 && jj <= n && tt <= n + 63;
-            dst[q] = __builtin_amdgcn_raw_buffer_load_b8(rbits, ok ? (uint32_t)i : GOOB, base, 0);
-            Dld -= dlen(sd - 1, m + 1, n + 1);
-        }
+    int pub = 0;         // lanes 0..31: lane 0's final abc at the block's steps (last step in lane 0)
+    int cx[GBLK], sx[GBLK], nx[GBLK], nsx[GBLK], ox[GBLK];
+    // lane q: the plane base of the diagonal of step t0 + q
+    auto bases = [&](int t0b) {
+        const int64_t sd = (int64_t)s0 - t0b - lane;
+        const int64_t sc = sd < 0 ? 0 : sd;
+        return (int)(doff_of(sc, m + 1, n + 1) - (sc - (n + 1) > 0 ? sc - (n + 1) : 0));
     };
-    load_block(0, cx);
+    // the plane bytes and lane 63's side bits of steps t0b .. t0b + GBLK - 1
+    // (a lane off the grid reads some other byte or 0: it only feeds garbage)
+    auto load_block = [&](int t0b, int vb, int *dst, int *dsts) {
+        unroll<GBLK>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            dst[q] = __builtin_amdgcn_raw_buffer_load_b8(rbits, plane_off, __builtin_amdgcn_readlane(vb, q), 0);
+            dsts[q] = __builtin_amdgcn_raw_buffer_load_b8(rside, side_off + (uint32_t)t0b + q, 0, 0);
+        });
+    };
+    int vb = bases(0);
+    load_block(0, vb, cx, sx);
     for (int t0 = 0; t0 <= n + 63; t0 += GBLK) {
-        // the strip below's first row for this block (lane 63's cells below)
-        // (tagged with the strip below's tag), and lanes 0..31: the de side
-        // bits of lane 63's cells (column n - t)
-        int blk = 0, side = 0;
+        stamp(S, 1, u, t0 / GBLK, 0);
+        // the strip below's first row for this block (lane 63's cells below),
+        // tagged with the strip below's tag
+        int d = 0;
         if (consume && t0 <= n) {
             const int want = (k + 1) % 0xFFFFFF + 1;
-            blk = poll_block(under + t0, lane, lane < GBLK && t0 + lane < W1,
-                             [&](int w) { return (w >> 8) == want; }, (int *)flags);
-            side = __builtin_amdgcn_raw_buffer_load_b8(rside, (lane < GBLK && t0 + lane <= n) ?
-                                                       (uint32_t)(n - t0 - lane) : GOOB, 0, 0);
+            d = poll_block(under + t0, lane, lane < GBLK && t0 + lane < W1,
+                           [&](int w) { return (w >> 8) == want; }, (int *)flags) & 0xFF;
         }
-        asm volatile("; touch %0 %1" : "+v"(blk), "+v"(side));
+        if (lane < GBLK) bw[lane] = d;
 #pragma unroll
-        for (int q = 0; q < GBLK; ++q) asm volatile("; touch %0" : "+v"(cx[q]));
-        load_block(t0 + GBLK, nx);
-#pragma unroll
-        for (int q = 0; q < GBLK; ++q) {
-            const int t = t0 + q;
-            const int j = n + 63 - lane - t;
-            int dnb = from_next_lane(0, mine);                   // final abc of (i + 1, j)
-            const int d63 = __builtin_amdgcn_readlane(blk, q) & 0xFF;
-            dnb = (lane == 63 && consume && t <= n) ? d63 : dnb;
-            const bool act = rowok && j >= 0 && j <= n;
-            const bool lastc = j == n;
-            const int c = cx[q] | (lane == 63 ? __builtin_amdgcn_readlane(side, q) : 0);
-            const int dn = lastr ? (lastc ? GC : bnd) : dnb;
-            const int rt = lastc ? (lastr ? GC : bnd) : mine;
-            const int dgn = (lastr || lastc) ? ((lastr && lastc) ? GC : bnd) : dnp;
-            // Altschul-Erickson steps 8-11 of the cell
-            int x = c;
-            const bool no_a_below = !(dn & GA), no_e = !(c & GE_), no_b_right = !(rt & GB), no_g = !(c & GG);
-            const bool no_c_diag = !(dgn & GC);
-            if ((no_a_below || no_e) && (no_b_right || no_g) && no_c_diag) x &= ~(GA | GB | GC);
-            if (!(no_a_below && no_b_right && no_c_diag)) {
-                if ((dn & GA) && (c & GD)) x |= GA;
-                if ((rt & GB) && (c & GF)) x |= GB;
+        for (int q = 0; q < GBLK; ++q) asm volatile("; touch %0 %1" : "+v"(cx[q]), "+v"(sx[q]));
+        stamp(S, 1, u, t0 / GBLK, 1);
+        const int vbn = bases(t0 + GBLK);
+        load_block(t0 + GBLK, vbn, nx, nsx);
+        const int j0 = n + 63 - lane - t0;
+        auto step = [&](auto edgec, auto tlc, int q) {
+            constexpr bool EDGE = decltype(edgec)::value, TL = decltype(tlc)::value;
+            const int j = j0 - q;
+            const int dnb = __builtin_amdgcn_update_dpp(bw[q], mine, 0x130, 0xF, 0xF, false);   // (i + 1, j)
+            const int c = cx[q] | sx[q];
+            int dn = dnb, rt = mine, dgn = dnp;
+            if constexpr (EDGE || TL) {
+                const bool lastc = EDGE && j == n, lr = TL && lastr;
+                dn = lr ? (lastc ? GC : bnd) : dn;
+                rt = lastc ? (lr ? GC : bnd) : rt;
+                dgn = (lr || lastc) ? ((lr && lastc) ? GC : bnd) : dgn;
             }
-            ox[q] = act ? x : 0;
+            // Altschul-Erickson steps 8-11 of the cell, bitwise: keep a/b/c
+            // unless no edge reaches the cell; add a (b) through d (f)
+            const int dA = dn & GA, rB = rt & GB, dC = dgn & GC;
+            const int c3 = c >> 3, c4 = c >> 4, c5 = c >> 5;
+            const int add = (c3 & dA) | (c4 & rB);
+            const int keep = (c4 & dA) | (c5 & rB) | dC;
+            const int x = (keep ? c : (c & ~(GA | GB | GC))) | add;
+            ox[q] = x;
             dnp = dnb;
-            mine = act ? x : 0;
+            mine = x;
+            pub = __builtin_amdgcn_update_dpp(x, pub, 0x138, 0xF, 0xF, false);   // lane 0 <- x
+        };
+        constexpr std::true_type Y{};
+        constexpr std::false_type N{};
+        const bool edge = t0 < 64 || t0 + GBLK - 1 > n;
+        if (tl) {
+            if (edge) unroll<GBLK>([&](auto qc) { step(Y, Y, decltype(qc)::value); });
+            else unroll<GBLK>([&](auto qc) { step(N, Y, decltype(qc)::value); });
+        } else {
+            if (edge) unroll<GBLK>([&](auto qc) { step(Y, N, decltype(qc)::value); });
+            else unroll<GBLK>([&](auto qc) { step(N, N, decltype(qc)::value); });
         }
         // the block's final bytes; the strip's first row (lane 0) to the strip above
-#pragma unroll
-        for (int q = 0; q < GBLK; ++q) {
-            const int t = t0 + q, j = n + 63 - lane - t, sd = s0 - t;
-            const uint32_t b0 = (uint32_t)(Dst - (sd - (n + 1) > 0 ? sd - (n + 1) : 0));
-            Dst -= dlen(sd - 1, m + 1, n + 1);
-            const bool act = rowok && j >= 0 && j <= n && t <= n + 63;
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ox[q], rbits, act ? (uint32_t)i : GOOB, b0, 0);
-            const int tp = t - 63;
-            if (produce && tp >= 0 && tp <= n && lane == 0) dev_store(mytop + tp, (k % 0xFFFFFF + 1) << 8 | ox[q]);
-        }
-#pragma unroll
-        for (int q = 0; q < GBLK; ++q) cx[q] = nx[q];
+        unroll<GBLK>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const int j = j0 - q;
+            const uint32_t off = (!edge || (uint32_t)j <= (uint32_t)n) ? plane_off : GOOB;
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ox[q], rbits, off, __builtin_amdgcn_readlane(vb, q), 0);
+        });
+        const int tp = t0 + (GBLK - 1 - lane) - 63;
+        if (produce && lane < GBLK && tp >= 0 && tp <= n) dev_store(mytop + tp, tagk | pub);
+        unroll<GBLK>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            cx[q] = nx[q];
+            sx[q] = nsx[q];
+        });
+        vb = vbn;
     }
 }
 
@@ -528,10 +675,10 @@ static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 // Per alignment: an "io" block (codes, strings, output strings, result: what
 // crosses PCIe) and a "work" block (diagonal buffers, last row / column and
 // the three tie planes, zeroed on the device).
-static size_t gotoh_io_bytes(int m, int n)
+static size_t gotoh_io_bytes(int m, int n, int L)
 {
     return align16(m + 8) + align16(n + 8) + align16(m + 1) + align16(n + 1) +
-           2 * align16(m + n + 1) + 64;
+           2 * align16(m + n + 1) + 64 + (size_t)L * prof_width(n);
 }
 
 static size_t gotoh_work_bytes(int m, int n)
@@ -558,6 +705,7 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
     for (int k = 0; k < L; ++k) code[(unsigned char)alphabet[k]] = k;
     int64_t mat_max = 0;
     for (int x = 0; x < L * L; ++x) mat_max = std::max<int64_t>(mat_max, std::abs((int64_t)matrix[x]));
+    if (mat_max > 127) { set_error("mh_gotoh_align: scores outside -127..127"); return -3; }
     if (gop < 0 || gep < 0 || gop > (1 << 16) || gep > (1 << 16)) { set_error("mh_gotoh_align: bad gap penalties"); return -3; }
     std::vector<int> ms(count), ns(count);
     std::vector<size_t> io(count + 1, 0), work(count + 1, 0);
@@ -573,7 +721,7 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
             if (code[(unsigned char)s1[t][i]] < 0) { set_error("mh_gotoh_align: '%c' not in alphabet", s1[t][i]); return -3; }
         for (int j = 0; j < ns[t]; ++j)
             if (code[(unsigned char)s2[t][j]] < 0) { set_error("mh_gotoh_align: '%c' not in alphabet", s2[t][j]); return -3; }
-        io[t + 1] = io[t] + gotoh_io_bytes(ms[t], ns[t]);
+        io[t + 1] = io[t] + gotoh_io_bytes(ms[t], ns[t], L);
         // boundary cells carry R and P in 26 bits (k_gotoh_fwd rp_pack)
         if ((int64_t)(ms[t] + ns[t] + 2) * (mat_max + gop + gep + 1) >= ((int64_t)1 << 24)) {
             set_error("mh_gotoh_align: alignment %d too long for the score range", t);
@@ -613,7 +761,7 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
         GotohArgs &A = args[t];
         const size_t oa = take_io(m + 8), ob = take_io(n + 8), o1 = take_io(m + 1),
                      o2 = take_io(n + 1), oo1 = take_io(m + n + 1), oo2 = take_io(m + n + 1),
-                     ores = take_io(64);
+                     ores = take_io(64), oprof = take_io((size_t)L * prof_width(n));
         A.lastcol = (int *)take_w(sizeof(int) * (m + 2));
         A.lastrow = (int *)take_w(sizeof(int) * (n + 2));
         const size_t cells = (size_t)(m + 2) * (n + 2);
@@ -625,6 +773,15 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
         A.flags = (int *)take_w(16);
         for (int i = 0; i < m; ++i) img[oa + i] = (char)code[(unsigned char)s1[t][i]];
         for (int j = 0; j < n; ++j) img[ob + j] = (char)code[(unsigned char)s2[t][j]];
+        {   // the score profile (prof_width)
+            const int PW = prof_width(n);
+            for (int cc = 0; cc < L; ++cc) {
+                int8_t *row = (int8_t *)&img[oprof + (size_t)cc * PW];
+                for (int j = 1; j <= n; ++j)
+                    row[PROF_PAD + j] = (int8_t)matrix[cc * L + code[(unsigned char)s2[t][j - 1]]];
+            }
+        }
+        A.prof = (const int8_t *)(d + oprof);
         memcpy(&img[o1], s1[t], m);
         memcpy(&img[o2], s2[t], n);
         A.a = (const int8_t *)(d + oa);
@@ -651,20 +808,31 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
     S.count = count;
     S.ticket = (int *)(d + off_first + sz_first - 16);
     const int strips = first[count];
+    S.stamps = nullptr;
+    S.stamp_blocks = 0;
+    const char *stamp_path = getenv("MH_GOTOH_STAMPS");
+    if (stamp_path && *stamp_path) {
+        int nmx = 0;
+        for (int t = 0; t < count; ++t) nmx = std::max(nmx, ns[t]);
+        S.stamp_blocks = (nmx + 64) / GBLK + 2;
+        MH_HIP(hipMalloc(&S.stamps, sizeof(unsigned long long) * 4 * strips * S.stamp_blocks));
+        MH_HIP(hipMemsetAsync(S.stamps, 0, sizeof(unsigned long long) * 4 * strips * S.stamp_blocks, st));
+    }
     const int pf = prof_begin(c, "k_gotoh_fwd");
     int nmax = 0;
     for (int t = 0; t < count; ++t) nmax = std::max(nmax, ns[t]);
-    const size_t lds_fwd = gotoh_al16(sizeof(int) * L * L) + (nmax <= GBC_MAX ? gotoh_al16(nmax) : 0);
-    if (nmax <= GBC_MAX) {
+    const size_t prof_bytes = (size_t)L * prof_width(nmax);
+    if (prof_bytes <= GPROF_LDS_MAX) {
+        const size_t lds_fwd = sizeof(int2) * GBLK + prof_bytes;
         MH_HIP(hipFuncSetAttribute((const void *)k_gotoh_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_fwd));
         hipLaunchKernelGGL(k_gotoh_fwd<true>, dim3((unsigned)strips), dim3(64), lds_fwd, st, S);
     } else {
-        hipLaunchKernelGGL(k_gotoh_fwd<false>, dim3((unsigned)strips), dim3(64), lds_fwd, st, S);
+        hipLaunchKernelGGL(k_gotoh_fwd<false>, dim3((unsigned)strips), dim3(64), sizeof(int2) * GBLK, st, S);
     }
     prof_end(c, pf);
     const int pb = prof_begin(c, "k_gotoh_bwd");
-    hipLaunchKernelGGL(k_gotoh_bwd, dim3((unsigned)strips), dim3(64), 0, st, S);
+    hipLaunchKernelGGL(k_gotoh_bwd, dim3((unsigned)strips), dim3(64), sizeof(int) * GBLK, st, S);
     prof_end(c, pb);
     const int pg = prof_begin(c, "k_gotoh");
     hipLaunchKernelGGL(k_gotoh_tb, dim3((unsigned)count), dim3(GOTOH_THREADS), TB_LDS, st,
@@ -674,6 +842,17 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
     if (e == hipSuccess) e = hipMemcpyAsync(img.data(), d, io[count], hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "k_gotoh");
+    if (S.stamps) {   // header: strips, blocks per strip; then fwd and bwd stamps
+        std::vector<unsigned long long> h((size_t)4 * strips * S.stamp_blocks);
+        MH_HIP(hipMemcpy(h.data(), S.stamps, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost));
+        MH_HIP(hipFree(S.stamps));
+        if (FILE *f = fopen(stamp_path, "wb")) {
+            const int64_t hdr[2] = {strips, S.stamp_blocks};
+            fwrite(hdr, sizeof(hdr), 1, f);
+            fwrite(h.data(), sizeof(h[0]), h.size(), f);
+            fclose(f);
+        }
+    }
     for (int t = 0; t < count; ++t) {
         const GotohArgs &A = args[t];
         int res[3];
