@@ -157,9 +157,11 @@ def cpu_end_to_end(sample_pairs, workdir):
                       'oracle C mapper on {} threads'.format(sample_pairs, threads)}
 
 
-def write_fastq_gz(pairs, path1, path2, threads=16):
+def write_fastq_gz(pairs, path1, path2, threads=16, single=False):
     """The pairs as gzip FASTQ files (independent gzip members compressed on
-    `threads` threads; a multi-member file is one valid gzip stream)."""
+    `threads` threads; a multi-member file is one valid gzip stream).  With
+    single=True each file is one gzip member, as bcl2fastq writes it (its
+    inflate cannot be split across threads)."""
     import zlib
     from concurrent.futures import ThreadPoolExecutor
     from micall_amd import synth
@@ -167,6 +169,8 @@ def write_fastq_gz(pairs, path1, path2, threads=16):
     def member(chunk):
         c = zlib.compressobj(1, zlib.DEFLATED, 31)
         return c.compress(chunk) + c.flush()
+    if single:
+        threads = 1
     for mate, path in ((1, path1), (2, path2)):
         r, q = pairs['r%d' % mate], pairs['q%d' % mate]
         recs = [b'%s\n%s\n+\n%s\n' % (synth.read_name(pairs['block'], i, mate).encode(),
@@ -179,7 +183,7 @@ def write_fastq_gz(pairs, path1, path2, threads=16):
                 f.write(blob)
 
 
-def end_to_end(n_pairs, workdir):
+def end_to_end(n_pairs, workdir, single_member=False):
     """The file-to-file path bin/micall runs (prelim_map() then remap(), the
     drop-ins) on the C2 input written as gzip FASTQ: ingest (gunzip + parse
     + H2D + 2-bit packing), the cold 74-seed index, the prelim pass and
@@ -193,7 +197,7 @@ def end_to_end(n_pairs, workdir):
     r2 = os.path.join(workdir, 'R2.fastq.gz')
     pairs = synth.make_pairs(n_pairs, genomes=bench_genomes('pol'), genome_seed=SEED,
                              read_seed=SEED, block=0)
-    write_fastq_gz(pairs, r1, r2)
+    write_fastq_gz(pairs, r1, r2, single=single_member)
     del pairs
     sizes = os.path.getsize(r1) + os.path.getsize(r2)
     # cold index build alone, on its own context
@@ -221,7 +225,8 @@ def end_to_end(n_pairs, workdir):
     out = {'value': round(2 * n_pairs / (t2 - t0), 1), 'unit': 'reads/s',
            'seconds': round(t2 - t0, 3), 'prelim_map_s': round(t1 - t0, 3),
            'remap_s': round(t2 - t1, 3), 'index_build_cold_ms': round(index_cold_ms, 2),
-           'fastq_gz_bytes': sizes, 'prelim_csv_bytes': os.path.getsize(prelim_path),
+           'fastq_gz_bytes': sizes, 'fastq_gz_members': 'one' if single_member else 'many (64 per file)',
+           'prelim_csv_bytes': os.path.getsize(prelim_path),
            'remap_csv_bytes': os.path.getsize(remap_path),
            'remap_counts': counts.getvalue().strip().split('\n')[-3:],
            'what': 'prelim_map() + remap() drop-ins file to file on {} pairs of gzip FASTQ '
@@ -622,6 +627,9 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-e2e', action='store_true',
                     help='skip the end-to-end (file to file) leg of the default C2 run')
+    ap.add_argument('--e2e-gzip', choices=('members', 'single'), default='members',
+                    help='gzip layout of the end-to-end FASTQ input: 64 members per file '
+                         '(as a parallel gzip writes it) or one member (as bcl2fastq does)')
     ap.add_argument('--breakdown', action='store_true',
                     help='time each pipeline stage (synchronising) and print it to stderr')
     ap.add_argument('--stage', choices=('remap', 'sam2aln', 'censor', 'aln2counts'), default='remap',
@@ -737,7 +745,7 @@ def main():
                 and args.iterations == 1 and not args.force_iterations):
             import tempfile
             with tempfile.TemporaryDirectory(prefix='micall_e2e_') as work:
-                e2e = end_to_end(args.pairs, work)
+                e2e = end_to_end(args.pairs, work, single_member=args.e2e_gzip == 'single')
                 if not args.no_cpu_baseline:
                     e2e['cpu_baseline'] = cpu_end_to_end(args.cpu_e2e_sample, work)
                     e2e['vs_cpu'] = round(e2e['value'] / e2e['cpu_baseline']['value'], 2)

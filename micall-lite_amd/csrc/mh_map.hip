@@ -95,6 +95,34 @@ __device__ __forceinline__ long long wave_max64(long long v)
 
 __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
 
+// A load through the constant address space: from a wave-uniform address it
+// is a scalar (SMEM) load, counted in lgkmcnt, so waiting for it does not
+// wait for the wave's vector loads in flight.  Only for data no kernel of the
+// launch writes (descriptors and tables written by earlier launches).
+template <class T>
+__device__ __forceinline__ T ldc(const T *p)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const __attribute__((address_space(4))) T *)p;
+#else
+    return *p;
+#endif
+}
+
+// a candidate's strand, reference and centre as three 4-byte scalar loads
+// (volatile: merged into one 12-byte load, which only the vector unit has,
+// they would cost a vector round trip)
+__device__ __forceinline__ Cand ldc_cand(const Cand *p)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const volatile __attribute__((address_space(4))) int *q =
+        (const volatile __attribute__((address_space(4))) int *)p;
+    return Cand{q[0], q[1], q[2], 0};
+#else
+    return *p;
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // k_pack_reads: one wave per read, one lane per 32-base chunk
 // ---------------------------------------------------------------------------
@@ -540,7 +568,7 @@ __device__ __forceinline__ int mm_pen(int qchar)
 {
     int q = qchar - 33;
     q = q < 0 ? 0 : (q > 40 ? 40 : q);
-    return 2 + q / 10;
+    return 2 + ((q * 205) >> 11);   // q / 10 for 0 <= q <= 40
 }
 
 // Scores inside the row recurrence carry a bias of 2^20, so every live value
@@ -691,29 +719,33 @@ constexpr int HUGE_NEG = -(1 << 24);   // an E / F constant that can never win
 constexpr int XREFW_PAD = 48;          // ref window bytes past the last row
 
 // One extension's LDS tables (a wave holds two, after the traceback bits).
+// Rows are allocated for at least one staging round (256 rows and 320
+// reference bytes), so the one-round staging writes them unguarded.
 struct XView {
-    uint32_t *tab;    // max(rows_pad, RUNS_CAP): score nibbles per row, then CIGAR runs
-    uint8_t *refw;    // rows_pad + XREFW_PAD: ref code * 4 of diagonal d0 + x
-    uint8_t *rdc;     // rows_pad: read code | mismatch penalty << 3
-    uint8_t *rowk;    // rows_pad: band lane of the M cell of each row, 255 none
+    uint32_t *tab;    // max(rows, RUNS_CAP): score nibbles per row, then CIGAR runs
+    uint8_t *refw;    // rows + 64 (>= rows_pad + XREFW_PAD): ref code * 4 of diagonal d0 + x
+    uint8_t *rdc;     // rows: read code | mismatch penalty << 3
+    uint8_t *rowk;    // rows: band lane of the M cell of each row, 255 none
 };
+
+__host__ __device__ constexpr int xview_rows(int rows_pad) { return rows_pad > 256 ? rows_pad : 256; }
 
 __host__ __device__ constexpr int xview_bytes(int rows_pad)
 {
-    return (4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP) + rows_pad + XREFW_PAD + 2 * rows_pad +
-            15) & ~15;
+    return (4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP) + 3 * xview_rows(rows_pad) + 64 + 15) & ~15;
 }
 
 __device__ __forceinline__ XView xview(unsigned char *base, int rows_pad, int h)
 {
     unsigned char *p = base + (size_t)h * xview_bytes(rows_pad);
+    const int rows = xview_rows(rows_pad);
     XView X;
     X.tab = (uint32_t *)p;
     p += 4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP);
     X.refw = p;
-    p += rows_pad + XREFW_PAD;
+    p += rows + 64;
     X.rdc = p;
-    X.rowk = p + rows_pad;
+    X.rowk = p + rows;
     return X;
 }
 
@@ -785,6 +817,28 @@ __device__ bool dp_ungapped(const XView &X, int m, int lane, int gmin, int hb, i
     const int ma = LOCAL ? 2 : 0;
     const int gb_max = ma * m - gmin;   // Gb(m - 1)
     const int kb = XCENTER;             // the seeded diagonal: the only candidate lane
+    // ---- screen for (A): every non-match of the seeded diagonal scores <= -1
+    // (end-to-end, where a match scores 0) or loses ma (local), so S <= -nm
+    // or S <= ma * (m - nm).  Lane L compares rows 4L .. 4L+3 (and 256 on),
+    // one LDS word of read codes against one of reference codes (the window
+    // of lane XCENTER is word-aligned). ----
+    {
+        int nm = 0;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int i = 4 * lane + 256 * r;
+            if (i < m) {
+                const uint32_t rd = *(const uint32_t *)(rdc + i) & 0x07070707u;
+                const uint32_t rv = *(const uint32_t *)(refw + i + kb) >> 2;
+                uint32_t x = (rd ^ rv) | ((rd | rv) & 0x04040404u);
+                x = (x | (x >> 1) | (x >> 2)) & 0x01010101u;
+                if (m - i < 4) x &= (1u << (8 * (m - i))) - 1u;   // rows past the read
+                nm += __builtin_popcount(x);
+            }
+        }
+        nm = wave_sum(nm);
+        if ((LOCAL ? ma * (m - nm) : -nm) <= gb_max) return false;
+    }
     // ---- exact ungapped recurrence on band lane kb: rows 8*lane .. 8*lane+7 ----
     const int r0 = 8 * lane;
     int s[8];
@@ -901,59 +955,181 @@ __device__ bool dp_ungapped(const XView &X, int m, int lane, int gmin, int hb, i
     return true;
 }
 
-// Stage one extension's per-row score tables, read codes and reference window
-// into its half's LDS tables; every load of a round is issued before any is
-// used.
+// Staging of one extension: its per-row score tables, read codes and
+// reference window go into its half's LDS tables.
+
+// Row i of the tables from the read's base code c (4: ambiguous, already
+// complemented on the reverse strand) and quality character qc; rows past the
+// read (live = false) get code 4 and a nibble of 8 (score 0).
+template <int LOCAL>
+__device__ __forceinline__ void put_row(const XView &X, int i, bool live, uint32_t c, int qc)
+{
+    const uint32_t ma = LOCAL ? 2 : 0;
+    // branch-free (a branch here serialises the staging's LDS reads): lm is
+    // all ones on a row of the read
+    const uint32_t lm = 0u - (uint32_t)live;
+    const uint32_t pen = (uint32_t)mm_pen(qc) & lm;
+    c = (c & lm) | (4u & ~lm);
+    // nibble g = score(g) + 8: -pen for a mismatch, ma for g == c, -NPEN when
+    // either side is ambiguous (g == 4 or c == 4); past the read all 8 (0)
+    const uint32_t mis = (8u - pen) * 0x1111u | (uint32_t)(8 - NPEN) << 16;
+    const uint32_t hit = mis + (ma + pen) * (1u << (4 * (c & 3)));
+    uint32_t tb = c < 4 ? hit : 0x11111u * (uint32_t)(8 - NPEN);
+    tb = (tb & lm) | (0x88888u & ~lm);
+    X.tab[i] = tb;
+    X.rdc[i] = (uint8_t)(c | pen << 3);
+    X.rowk[i] = 255;
+}
+
+// Reads longer than one round of 256 rows (4 per lane) and 320 reference
+// bytes (5 per lane): every load of a round is issued before any is used.
+struct StageRegs {
+    uint32_t nmw[4], sqw[4], qv[4], gv[5];
+};
+
+__device__ __forceinline__ void stage_load(const DpArgs &A, int m, int strand, int64_t roff, int d0,
+                                           int reflen, int64_t gref, int i0, int x0, int lane,
+                                           StageRegs &S)
+{
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 64 * u + lane;
+        const int b = i < m ? (strand ? m - 1 - i : i) : 0;
+        const int64_t g = roff + b;
+        S.nmw[u] = A.R.nmask[g >> 5];
+        S.sqw[u] = A.R.seq2[g >> 4];
+        S.qv[u] = A.R.qual[g];
+    }
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+        int j = d0 + x0 + 64 * u + lane;
+        j = j < 0 ? 0 : (j >= reflen ? reflen - 1 : j);
+        S.gv[u] = A.I.codes[gref + j];
+    }
+}
+
+template <int LOCAL>
+__device__ __forceinline__ void stage_rows(const DpArgs &A, const XItem &it, const XView &X, int i0,
+                                           int lane, const StageRegs &S)
+{
+    const int m = it.m;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 64 * u + lane;
+        if (i >= A.rows_pad) break;
+        const int64_t g = it.roff + (it.strand ? m - 1 - i : i);
+        uint32_t c = ((S.nmw[u] >> (g & 31)) & 1) ? 4u : ((S.sqw[u] >> (2 * (g & 15))) & 3u);
+        if (it.strand && c < 4) c = 3 - c;
+        put_row<LOCAL>(X, i, i < m, c, (int)S.qv[u]);
+    }
+}
+
+__device__ __forceinline__ void stage_ref(const DpArgs &A, const XItem &it, const XView &X, int x0,
+                                          int lane, const StageRegs &S)
+{
+    const int wref = A.rows_pad + XREFW_PAD;
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+        const int x = x0 + 64 * u + lane, j = it.d0 + x;
+        const uint32_t g = (j >= 0 && j < it.reflen) ? S.gv[u] : 4u;
+        if (x < wref) X.refw[x] = (uint8_t)(g * 4);
+    }
+}
+
+// rows_pad <= 256: one round, whose loads k_dp issues an item ahead
+constexpr int STAGE_ROWS = 256;
+
+// Reads of one round (rows_pad <= 256) are staged in two halves: k_dp issues
+// the next item's raw bytes into a per-wave raw area by LDS-DMA
+// (global_load_lds_dword: no VGPR destination, so nothing in the compiler's
+// waits depends on them) before the current item's DP and traceback, and
+// builds the tables from the raw area when the item's turn comes.  Raw area
+// (RAW_BYTES): [0, 256) qualities; [256, 512) the 2-bit words (lanes 0-15)
+// and N-mask words (lanes 16-23) of the read; [512, 1024) 128 dwords of
+// reference codes from the aligned dword below the window's first byte.
+constexpr int RAW_BYTES = 1024;
+
+// s_waitcnt vmcnt(0): every vector memory operation of the wave, the
+// LDS-DMA of stage_dma included, has completed
+__device__ __forceinline__ void vm_wait() { __builtin_amdgcn_s_waitcnt(0x3f70); }
+
+__device__ __forceinline__ void dma4(const void *g, unsigned char *lds)
+{
+    __builtin_amdgcn_global_load_lds((const void *)g, (__attribute__((address_space(3))) void *)lds, 4, 0, 0);
+}
+
+__device__ __forceinline__ void stage_dma(const DpArgs &A, const XItem &x, unsigned char *raw, int lane)
+{
+    // qualities: lane l the bytes 4l .. 4l+3 of the read (a lane past the
+    // read re-reads its first dword)
+    const int64_t q = x.roff + (4 * lane < x.m ? 4 * lane : 0);
+    dma4(A.R.qual + q, raw);
+    // 2-bit words (16 bases each) and N-mask words (32 bases each); roff is a
+    // multiple of 32
+    const int64_t sw = x.roff >> 4, nw = x.roff >> 5;
+    const uint32_t *sp = A.R.seq2 + sw + (16 * lane < x.m && lane < 16 ? lane : 0);
+    const uint32_t *np = A.R.nmask + nw + (lane >= 16 && lane < 24 && 32 * (lane - 16) < x.m ? lane - 16 : 0);
+    dma4(lane < 16 ? (const void *)sp : (const void *)np, raw + 256);
+    // reference codes: dwords from the aligned dword at or below gref + d0,
+    // clamped into the code array (bytes off the reference are masked later)
+    const int64_t a0 = (x.gref + x.d0) & ~(int64_t)3;
+    const int64_t last = ((A.I.total + 64) & ~(int64_t)3) - 4;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        int64_t a = a0 + 4 * (64 * k + lane);
+        a = a < 0 ? 0 : (a > last ? last : a);
+        dma4(A.I.codes + a, raw + 512 + 256 * k);
+    }
+}
+
+// the tables of an item whose raw bytes stage_dma brought in (after a wait
+// for the wave's vector memory operations)
+template <int LOCAL>
+__device__ __forceinline__ void stage_raw(const DpArgs &A, const XItem &it, const XView &X,
+                                          const unsigned char *raw, int lane)
+{
+    const int m = it.m;
+    const uint32_t *sw = (const uint32_t *)(raw + 256), *nw = sw + 16;
+    // every LDS read first (no branches: rows past the read read base 0)
+    int b[4];
+    uint32_t nmw[4], sqw[4], qv[4], gv[5];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = 64 * u + lane;
+        b[u] = i < m ? (it.strand ? m - 1 - i : i) : 0;
+        nmw[u] = nw[b[u] >> 5];
+        sqw[u] = sw[b[u] >> 4];
+        qv[u] = raw[b[u]];
+    }
+    const int sh = (int)((it.gref + it.d0) & 3);
+#pragma unroll
+    for (int u = 0; u < 5; ++u) gv[u] = raw[512 + sh + 64 * u + lane];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {   // rows 0 .. 255 (the tables hold 256)
+        const int i = 64 * u + lane;
+        uint32_t c = ((nmw[u] >> (b[u] & 31)) & 1) ? 4u : ((sqw[u] >> (2 * (b[u] & 15))) & 3u);
+        if (it.strand && c < 4) c = 3 - c;
+        put_row<LOCAL>(X, i, i < m, c, (int)qv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {   // reference bytes 0 .. 319 (the window holds 320)
+        const int x = 64 * u + lane, j = it.d0 + x;
+        const uint32_t g = (j >= 0 && j < it.reflen) ? gv[u] : 4u;
+        X.refw[x] = (uint8_t)(g * 4);
+    }
+}
+
+// Staging of reads longer than one round: the rounds load and store in turn.
 template <int LOCAL>
 __device__ __forceinline__ void stage_ext(const DpArgs &A, const XItem &it, const XView &X, int lane)
 {
-    const int ma = LOCAL ? 2 : 0;
-    const int m = it.m;
-    for (int i0 = 0; i0 < A.rows_pad; i0 += 64 * 4) {
-        uint32_t nmw[4], sqw[4], qv[4];
-        int bb[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = i0 + 64 * u + lane;
-            const int b = i < m ? (it.strand ? m - 1 - i : i) : 0;
-            const int64_t g = it.roff + b;
-            bb[u] = (int)(g & 31);
-            nmw[u] = A.R.nmask[g >> 5];
-            sqw[u] = A.R.seq2[g >> 4] >> (2 * (g & 15));
-            qv[u] = A.R.qual[g];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = i0 + 64 * u + lane;
-            if (i >= A.rows_pad) break;
-            uint32_t tb = 0x88888u, c = 4, pen = 0;
-            if (i < m) {
-                c = ((nmw[u] >> bb[u]) & 1) ? 4u : (sqw[u] & 3u);
-                if (it.strand && c < 4) c = 3 - c;
-                pen = (uint32_t)mm_pen((int)qv[u]);
-                // nibble g = score(g) + 8: -pen for a mismatch, ma for g == c,
-                // -NPEN when either side is ambiguous (g == 4 or c == 4)
-                const uint32_t mis = (8u - pen) * 0x1111u | (uint32_t)(8 - NPEN) << 16;
-                tb = c < 4 ? mis + ((uint32_t)ma + pen) * (1u << (4 * c)) : 0x11111u * (uint32_t)(8 - NPEN);
-            }
-            X.tab[i] = tb;
-            X.rdc[i] = (uint8_t)(c | pen << 3);
-            X.rowk[i] = 255;
-        }
-    }
     const int wref = A.rows_pad + XREFW_PAD;
-    for (int x0 = 0; x0 < wref; x0 += 64 * 5) {
-        uint32_t gv[5];
-#pragma unroll
-        for (int u = 0; u < 5; ++u) {
-            const int j = it.d0 + x0 + 64 * u + lane;
-            gv[u] = (j >= 0 && j < it.reflen) ? A.I.codes[it.gref + j] : 4u;
-        }
-#pragma unroll
-        for (int u = 0; u < 5; ++u) {
-            const int x = x0 + 64 * u + lane;
-            if (x < wref) X.refw[x] = (uint8_t)(gv[u] * 4);
-        }
+    for (int r0 = 0; r0 < A.rows_pad || 320 * (r0 / STAGE_ROWS) < wref; r0 += STAGE_ROWS) {
+        const int x0 = 320 * (r0 / STAGE_ROWS);
+        StageRegs S;
+        stage_load(A, it.m, it.strand, it.roff, it.d0, it.reflen, it.gref, r0, x0, lane, S);
+        if (r0 < A.rows_pad) stage_rows<LOCAL>(A, it, X, r0, lane, S);
+        if (x0 < wref) stage_ref(A, it, X, x0, lane, S);
     }
 }
 
@@ -1070,7 +1246,7 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
     uint32_t *runs = X.tab;   // the DP is done with the score tables
     const uint8_t *refw = X.refw, *rdc = X.rdc;
     uint8_t *rowk = X.rowk;
-    const int minsc = A.len_tab[(MAXLEN + 1) + m];
+    const int minsc = ldc(&A.len_tab[(MAXLEN + 1) + m]);
 
     // ---- traceback: CIGAR runs, back to front, and the band lane of every
     // M row (rowk) for the lane-parallel statistics below.  The walk's state
@@ -1095,11 +1271,23 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
         if (!(LOCAL && best <= 0) && best >= __builtin_amdgcn_readfirstlane(minsc)) {
             const int len = bi - fast_low;
             if (lane == 0) runs[0] = ((uint32_t)len << 4) | (uint32_t)MH_OP_M;
-            for (int r = fast_low + 1 + lane; r <= bi; r += 64) {
-                rowk[r] = (uint8_t)bl;
-                const int g = refw[r + bl] >> 2, rb = rdc[r] & 7;
-                const int amb = rb > 3 || g > 3;
-                path_cnt += (amb << 16) + (amb || rb != g);
+            for (int r0 = bi; r0 > fast_low; r0 -= 256) {   // lane L: rows r0 - 4L .. r0 - 4L - 3
+                int rb[4], g[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int r = r0 - 4 * lane - u;
+                    rb[u] = r > fast_low ? rdc[r] & 7 : 0;
+                    g[u] = r > fast_low ? refw[r + bl] >> 2 : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int r = r0 - 4 * lane - u;
+                    if (r > fast_low) {
+                        rowk[r] = (uint8_t)bl;
+                        const int amb = rb[u] > 3 || g[u] > 3;
+                        path_cnt += (amb << 16) + (amb || rb[u] != g[u]);
+                    }
+                }
             }
             tb_ok = 1;
             t_start = fast_low + 1;
@@ -1132,25 +1320,35 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
                         break;
                     }
                 }
-                int stop = -1;   // local: the highest row of rf .. i with H == 0
-                if (LOCAL) {
-                    // lane L rebuilds rows r0 - 4L .. r0 - 4L - 3: H(r) = hv minus the
-                    // scores of the diagonal moves out of the rows above r
-                    const int lo = rf > 0 ? rf : 0;
-                    for (int r0 = i; r0 >= lo; r0 -= 256) {
+                // the rows rf + 1 .. i of the run, 256 per round (lane L: rows
+                // r0 - 4L .. r0 - 4L - 3), read once for the local stop, the
+                // band lane of every M row (rowk) and the n-ceil / mismatch
+                // counts.  Local mode rebuilds H(r) = hv minus the scores of
+                // the diagonal moves out of the rows above r; the highest row
+                // of rf .. i with H == 0 is the stop, and the run is the rows
+                // above it.
+                int stop = -1;
+                const int lo = LOCAL ? (rf > 0 ? rf : 0) : rf + 1;
+                for (int r0 = i; r0 >= lo; r0 -= 256) {
+                    int rb[4], gc[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int r = r0 - 4 * lane - u;
+                        rb[u] = r > rf ? rdc[r] : 0;
+                        gc[u] = r > rf ? refw[r + k] >> 2 : 0;
+                    }
+                    int stop_c = -1, run = 0;
+                    if (LOCAL) {
                         int sc[4], tot = 0;
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
-                            const int r = r0 - 4 * lane - u;
-                            sc[u] = 0;
-                            if (r > rf && r >= 0) {
-                                const int rb = rdc[r], gc = refw[r + k] >> 2, c = rb & 7;
-                                sc[u] = (c > 3 || gc > 3) ? -NPEN : (c == gc ? ma : -(rb >> 3));
-                            }
+                            const int r = r0 - 4 * lane - u, c = rb[u] & 7;
+                            sc[u] = r <= rf ? 0 : (c > 3 || gc[u] > 3) ? -NPEN
+                                                  : (c == gc[u] ? ma : -(rb[u] >> 3));
                             tot += sc[u];
                         }
-                        const int ex = wave_excl_scan(tot, lane);
-                        int run = ex, zrow = -1;
+                        run = wave_excl_scan(tot, lane);
+                        int zrow = -1;
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             const int r = r0 - 4 * lane - u;
@@ -1158,12 +1356,19 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
                             run += sc[u];
                         }
                         const uint64_t z = __builtin_amdgcn_ballot_w64(zrow >= 0);
-                        if (z) {
-                            stop = __builtin_amdgcn_readlane(zrow, (int)__builtin_ctzll(z));
-                            break;
-                        }
-                        hv -= __builtin_amdgcn_readlane(run, 63);
+                        if (z) stop_c = __builtin_amdgcn_readlane(zrow, (int)__builtin_ctzll(z));
                     }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int r = r0 - 4 * lane - u, c = rb[u] & 7;
+                        if (r > rf && r > stop_c) {
+                            rowk[r] = (uint8_t)k;
+                            const int amb = c > 3 || gc[u] > 3;
+                            path_cnt += (amb << 16) + (amb || c != gc[u]);
+                        }
+                    }
+                    if (stop_c >= 0) { stop = stop_c; break; }
+                    if (LOCAL) hv -= __builtin_amdgcn_readlane(run, 63);
                 }
                 const int low = stop >= 0 ? stop : rf;
                 if (i > low) {   // rows low+1 .. i: one M run
@@ -1177,12 +1382,6 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
                         }
                         rop = MH_OP_M;
                         rlen = len;
-                    }
-                    for (int r = low + 1 + lane; r <= i; r += 64) {
-                        rowk[r] = (uint8_t)k;
-                        const int g = refw[r + k] >> 2, rb = rdc[r] & 7;
-                        const int amb = rb > 3 || g > 3;
-                        path_cnt += (amb << 16) + (amb || rb != g);
                     }
                     first_j = low + 1 + d0 + k;
                 }
@@ -1297,7 +1496,7 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
             }
         }
         cnt = wave_sum(cnt);
-        if ((cnt >> 16) > A.len_tab[2 * (MAXLEN + 1) + m]) tb_ok = 0;
+        if ((cnt >> 16) > ldc(&A.len_tab[2 * (MAXLEN + 1) + m])) tb_ok = 0;
         if (tb_ok && lane == 0 && lo >= hi) {
             const int nc = (clipL > 0) + (clipR > 0) + (lo - hi + 1);
             if (nc <= MH_MAXOPS - 1) {
@@ -1342,7 +1541,7 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
 // whole wave); an item that needs the DP waits in half 0 until a second one
 // fills half 1, then both run through the rows together.  A last waiting
 // item runs with half 1 repeating it.
-template <int LOCAL>
+template <int LOCAL, int ONE_ROUND>
 __global__ __launch_bounds__(256) void k_dp(DpArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1353,67 +1552,86 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     uint32_t *bits = (uint32_t *)wbase;                       // rows_pad/8 * 64: 4 bits/cell
     unsigned char *xbase = wbase + (size_t)32 * A.rows_pad;
     const XView X0 = xview(xbase, A.rows_pad, 0), X1 = xview(xbase, A.rows_pad, 1);
+    unsigned char *raw = xbase + 2 * xview_bytes(A.rows_pad);   // RAW_BYTES (reads of one round)
     const int n_work = A.counters[0];
     const int gmin = A.oeI < A.oeD ? A.oeI : A.oeD;
 
     int64_t ck_base = 0;   // lane 0: this wave's current CIGAR pool chunk
     int ck_left = 0;
     int n_fast = 0;        // extensions resolved by dp_ungapped
-    // Software pipeline over the work items: the descriptor chain of the next
-    // item (work id -> candidate and read -> reference) is loaded while this
-    // one is aligned, so a wave pays one dependent global round trip per
-    // extension (its staging loads) instead of four.
+    // Software pipeline over the work items, three deep: while item w is
+    // aligned, the candidate and read descriptors of item w + 2s are loaded
+    // (scalar loads; and the work id of w + 3s), and item w + s, whose
+    // descriptors landed during the previous item, gets its reference window
+    // and (reads of one staging round) its raw bytes issued by LDS-DMA, so
+    // they land while w is aligned.  A wave then waits on no global round
+    // trip between items.
     const int wstride = gridDim.x * wpb;
+    constexpr bool one_round = ONE_ROUND;   // rows_pad <= STAGE_ROWS
     int w = blockIdx.x * wpb + wv;
-    int sid_n = 0, m_n = 0, reflen_n = 0;
-    Cand cd_n{};
-    int64_t roff_n = 0, gref_n = 0;
+    XItem cur{};                       // item w: every field, staging loads issued
+    int sid1 = 0, m1 = 0, sid2 = 0;    // item w + s: work id, candidate, read; w + 2s: work id
+    Cand cd1{};
+    int64_t roff1 = 0;
+    auto to_item = [&](int sid, const Cand &cd, int m, int64_t roff) {
+        XItem x;
+        x.sid = sid;
+        x.m = m;
+        x.roff = roff;
+        x.d0 = cd.center - XCENTER;
+        x.strand = cd.strand;
+        x.ref = cd.ref;
+        x.reflen = ldc(&A.I.ref_len[cd.ref]);
+        x.gref = ldc(&A.I.ref_off[cd.ref]);
+        x.hb = ldc(&A.len_tab[3 * (MAXLEN + 1) + m]);
+        if (one_round) stage_dma(A, x, raw, lane);
+        return x;
+    };
     if (w < n_work) {
-        sid_n = A.work[w];
-        cd_n = A.cand[sid_n];
-        m_n = A.R.len[sid_n / MAXCAND];
-        roff_n = A.R.off[sid_n / MAXCAND];
-        reflen_n = A.I.ref_len[cd_n.ref];
-        gref_n = A.I.ref_off[cd_n.ref];
+        const int sid = ldc(&A.work[w]);
+        cur = to_item(sid, ldc_cand(&A.cand[sid]), ldc(&A.R.len[sid / MAXCAND]),
+                      ldc(&A.R.off[sid / MAXCAND]));
     }
-    bool pend = false;   // half 0 holds an item waiting for the DP
+    if (w + wstride < n_work) {
+        sid1 = ldc(&A.work[w + wstride]);
+        cd1 = ldc_cand(&A.cand[sid1]);
+        m1 = ldc(&A.R.len[sid1 / MAXCAND]);
+        roff1 = ldc(&A.R.off[sid1 / MAXCAND]);
+    }
+    if (w + 2 * wstride < n_work) sid2 = ldc(&A.work[w + 2 * wstride]);
+    bool pend = false;     // half 0 holds an item waiting for the DP
+    bool landed = false;   // the raw bytes of `cur` were waited for
     XItem P{};
     for (; w < n_work; w += wstride) {
-        XItem it;
-        it.sid = sid_n;
-        it.m = m_n;
-        it.roff = roff_n;
-        it.reflen = reflen_n;
-        it.gref = gref_n;
-        it.d0 = cd_n.center - XCENTER;
-        it.strand = cd_n.strand;
-        it.ref = cd_n.ref;
-        it.hb = A.len_tab[3 * (MAXLEN + 1) + m_n];
-        const int wn = w + wstride;
-        const bool more = wn < n_work;
-        int sid_nn = 0;
-        if (more) sid_nn = A.work[wn];   // lands with the staging loads below
-
+        const XItem it = cur;
         const int h = pend ? 1 : 0;
         const XView X = h ? X1 : X0;
-        stage_ext<LOCAL>(A, it, X, lane);
-        wave_sync();
-        if (more) {   // next item's candidate and read descriptors: land during the DP
-            sid_n = sid_nn;
-            cd_n = A.cand[sid_nn];
-            m_n = A.R.len[sid_nn / MAXCAND];
-            roff_n = A.R.off[sid_nn / MAXCAND];
+        if (one_round) {
+            if (!landed) vm_wait();   // (after a pending item: nothing ran to cover them)
+            stage_raw<LOCAL>(A, it, X, raw, lane);
+        } else {
+            stage_ext<LOCAL>(A, it, X, lane);
         }
+        wave_sync();
         int best = 0, bi = 0, bl = 0, low = -1;
         const bool fast = it.m > 2 * GBAR + 8 && it.m <= 512 &&
                           dp_ungapped<LOCAL>(X, it.m, lane, gmin, it.hb, best, bi, bl, low);
         n_fast += fast;
-        if (more) {   // next item's reference window: lands during the DP / traceback
-            reflen_n = A.I.ref_len[cd_n.ref];
-            gref_n = A.I.ref_off[cd_n.ref];
+        if (w + wstride < n_work) cur = to_item(sid1, cd1, m1, roff1);
+        if (w + 2 * wstride < n_work) {
+            sid1 = sid2;
+            cd1 = ldc_cand(&A.cand[sid2]);
+            m1 = ldc(&A.R.len[sid2 / MAXCAND]);
+            roff1 = ldc(&A.R.off[sid2 / MAXCAND]);
         }
+        if (w + 3 * wstride < n_work) sid2 = ldc(&A.work[w + 3 * wstride]);
+        // The next item's raw bytes are waited for before this item's
+        // traceback stores anything: the vector memory counter is in order,
+        // so a wait after the stores would also wait for their write acks.
+        landed = false;
         if (fast) {
             wave_sync();
+            if (one_round) { vm_wait(); landed = true; }
             finish_ext<LOCAL>(A, it, X, bits, 32 * h, best, bi, bl, lane, ck_base, ck_left, low);
         } else if (!pend) {
             P = it;
@@ -1422,6 +1640,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             int b0, i0, l0, b1, i1, l1;
             dp_pair<LOCAL>(A, X0, X1, P.m, it.m, P.hb, it.hb, bits, lane, b0, i0, l0, b1, i1, l1);
             wave_sync();
+            if (one_round) { vm_wait(); landed = true; }
             finish_ext<LOCAL>(A, P, X0, bits, 0, b0, i0, l0, lane, ck_base, ck_left);
             finish_ext<LOCAL>(A, it, X1, bits, 32, b1, i1, l1, lane, ck_base, ck_left);
             pend = false;
@@ -2041,7 +2260,8 @@ int run_map(Ctx &c, const mh_params &par)
 
         const int rows_pad = ((c.reads.max_len + 7) / 8) * 8;
         // traceback bits 32 B per row, then the tables of the wave's two extensions
-        const int wave_lds = 32 * rows_pad + 2 * xview_bytes(rows_pad);
+        const int wave_lds = 32 * rows_pad + 2 * xview_bytes(rows_pad) +
+                             (rows_pad <= STAGE_ROWS ? RAW_BYTES : 0);
         // one wave per workgroup: the CU then packs floor(160 KiB / wave_lds)
         // waves (15 at 251-nt reads) with no workgroup rounding loss
         int wpb = DP_WAVES_PER_BLOCK;
@@ -2057,14 +2277,20 @@ int run_map(Ctx &c, const mh_params &par)
             if (dblocks > DP_MAX_BLOCKS) dblocks = DP_MAX_BLOCKS;
             if (dblocks < 1) dblocks = 1;
             const int pd = prof_begin(c, name);
+            const bool one = rows_pad <= STAGE_ROWS;
+            const void *kf = par.mode == MH_LOCAL ? (one ? (const void *)k_dp<1, 1> : (const void *)k_dp<1, 0>)
+                                                  : (one ? (const void *)k_dp<0, 1> : (const void *)k_dp<0, 0>);
+            MH_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, wpb * wave_lds));
             if (par.mode == MH_LOCAL) {
-                MH_HIP(hipFuncSetAttribute((const void *)k_dp<1>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, wpb * wave_lds));
-                hipLaunchKernelGGL(k_dp<1>, dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
+                if (one)
+                    hipLaunchKernelGGL((k_dp<1, 1>), dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
+                else
+                    hipLaunchKernelGGL((k_dp<1, 0>), dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
             } else {
-                MH_HIP(hipFuncSetAttribute((const void *)k_dp<0>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, wpb * wave_lds));
-                hipLaunchKernelGGL(k_dp<0>, dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
+                if (one)
+                    hipLaunchKernelGGL((k_dp<0, 1>), dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
+                else
+                    hipLaunchKernelGGL((k_dp<0, 0>), dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
             }
             prof_end(c, pd);
             MH_HIP(hipGetLastError());
