@@ -1233,15 +1233,21 @@ __device__ void dp_pair(const DpArgs &A, const XView &X0, const XView &X1, int m
     bl1 = (63 - (int)(k1 & 63)) & 31;
 }
 
-// Traceback, overhang trimming, statistics and the slot of one extension
-// whose traceback bits sit in columns hcol .. hcol + 31 of the wave's bits.
+// What a traceback leaves for post_ext besides the CIGAR runs (back to
+// front in X.tab) and the band lane of every M row (X.rowk).
+struct WalkOut {
+    int tb_ok, t_start, t_first, t_nrun;   // wave-uniform
+    int path_cnt;                          // per lane: ambiguous << 16 | mismatches of its M rows
+};
+
+// Traceback of one extension whose traceback bits sit in columns hcol ..
+// hcol + 31 of the wave's bits, with the whole wave.
 template <int LOCAL>
-__device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, const uint32_t *bits,
-                           int hcol, int best, int bi, int bl, int lane, int64_t &ck_base,
-                           int &ck_left, int fast_low = -2)
+__device__ WalkOut walk1(const DpArgs &A, const XItem &it, const XView &X, const uint32_t *bits,
+                         int hcol, int best, int bi, int bl, int lane, int fast_low)
 {
     const int ma = LOCAL ? 2 : 0;
-    const int m = it.m, reflen = it.reflen, d0 = it.d0;
+    const int m = it.m, d0 = it.d0;
     const int klo = XCENTER - it.hb, khi = XCENTER + it.hb;
     uint32_t *runs = X.tab;   // the DP is done with the score tables
     const uint8_t *refw = X.refw, *rdc = X.rdc;
@@ -1434,7 +1440,20 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
         t_first = first_j;
         t_nrun = nrun;
     }
-    wave_sync();
+    return WalkOut{tb_ok, t_start, t_first, t_nrun, path_cnt};
+}
+
+// Overhang trimming, statistics, the CIGAR and the slot of one extension
+// after its traceback (W's first four fields wave-uniform).
+template <int LOCAL>
+__device__ void post_ext(const DpArgs &A, const XItem &it, const XView &X, int best, int bi, int bl,
+                         int lane, int64_t &ck_base, int &ck_left, const WalkOut &W)
+{
+    const int m = it.m, reflen = it.reflen, d0 = it.d0;
+    const uint32_t *runs = X.tab;
+    const uint8_t *refw = X.refw, *rdc = X.rdc, *rowk = X.rowk;
+    int tb_ok = W.tb_ok;
+    const int t_start = W.t_start, t_first = W.t_first, t_nrun = W.t_nrun, path_cnt = W.path_cnt;
     Slot out{};
     out.valid = 0;
     out.strand = it.strand;
@@ -1534,6 +1553,20 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
     }
     if (lane == 0) A.slot[it.sid] = out;
     wave_sync();
+}
+
+// Traceback, overhang trimming, statistics and the slot of one extension.
+template <int LOCAL>
+__device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, const uint32_t *bits,
+                           int hcol, int best, int bi, int bl, int lane, int64_t &ck_base,
+                           int &ck_left, int fast_low = -2)
+{
+    best = __builtin_amdgcn_readfirstlane(best);
+    bi = __builtin_amdgcn_readfirstlane(bi);
+    bl = __builtin_amdgcn_readfirstlane(bl);
+    const WalkOut W = walk1<LOCAL>(A, it, X, bits, hcol, best, bi, bl, lane, fast_low);
+    wave_sync();
+    post_ext<LOCAL>(A, it, X, best, bi, bl, lane, ck_base, ck_left, W);
 }
 
 // k_dp: a wave walks its share of the work list.  Each item is staged into

@@ -54,14 +54,29 @@ def main():
                '            wave_sync();\n',
             '            dp_pair<LOCAL>(A, X0, X1, P.m, it.m, P.hb, it.hb, bits, lane, b0, i0, l0, b1, i1, l1);\n'
             '            wave_sync();\n            PH(2);\n')
-    t = sub(t, '            finish_ext<LOCAL>(A, it, X1, bits, 32, b1, i1, l1, lane, ck_base, ck_left);\n'
+    t = sub(t, '            finish_pair<LOCAL>(A, P, X0, it, X1, bits, b0, i0, l0, b1, i1, l1, lane, ck_base, ck_left);\n'
                '            pend = false;\n',
-            '            finish_ext<LOCAL>(A, it, X1, bits, 32, b1, i1, l1, lane, ck_base, ck_left);\n'
+            '            finish_pair<LOCAL>(A, P, X0, it, X1, bits, b0, i0, l0, b1, i1, l1, lane, ck_base, ck_left);\n'
             '            pend = false;\n            PH(4);\n')
     t = sub(t, '    if (lane == 0 && n_fast) atomicAdd(&A.pool_ctr[2], n_fast);\n}',
             '    if (lane == 0 && n_fast) atomicAdd(&A.pool_ctr[2], n_fast);\n'
             '    PH(5);\n'
             '    if (lane == 0) for (int k = 0; k < 8; ++k) atomicAdd(&g_ph[LOCAL][k], ph[k]);\n}')
+    # the traceback walk inside finish_ext, summed into ph[7]
+    t = sub(t, 'int &ck_left, int fast_low = -2)\n{\n',
+            'int &ck_left, unsigned long long &fw, int fast_low = -2)\n{\n'
+            '    const unsigned long long f0 = __builtin_readcyclecounter();\n')
+    t = sub(t, '    const WalkOut W = walk1<LOCAL>(A, it, X, bits, hcol, best, bi, bl, lane, fast_low);\n    wave_sync();\n',
+            '    const WalkOut W = walk1<LOCAL>(A, it, X, bits, hcol, best, bi, bl, lane, fast_low);\n    wave_sync();\n'
+            '    fw += __builtin_readcyclecounter() - f0;\n')
+    t = sub(t, 'int i1, int l1, int lane, int64_t &ck_base, int &ck_left)\n{\n',
+            'int i1, int l1, int lane, int64_t &ck_base, int &ck_left, unsigned long long &fw)\n{\n'
+            '    const unsigned long long f0 = __builtin_readcyclecounter();\n')
+    t = sub(t, '    walk2<LOCAL>(A, it0, it1, X0, X1, bits, b0, i0, l0, b1, i1, l1, lane, W0, W1);\n    wave_sync();\n',
+            '    walk2<LOCAL>(A, it0, it1, X0, X1, bits, b0, i0, l0, b1, i1, l1, lane, W0, W1);\n    wave_sync();\n'
+            '    fw += __builtin_readcyclecounter() - f0;\n')
+    t = t.replace('ck_base, ck_left, low);', 'ck_base, ck_left, ph[7], low);')
+    t = t.replace('lane, ck_base, ck_left);', 'lane, ck_base, ck_left, ph[7]);')
     t = sub(t, '            M.last_fast = ctr[3];\n',
             '            M.last_fast = ctr[3];\n'
             '            {\n'
@@ -69,11 +84,11 @@ def main():
             '                MH_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof(ph)));\n'
             '                const int L = par.mode == MH_LOCAL;\n'
             '                double tot = 0;\n'
-            '                for (int k = 0; k < 8; ++k) tot += (double)ph[L][k];\n'
+            '                for (int k = 0; k < 7; ++k) tot += (double)ph[L][k];\n'
             '                fprintf(stderr, "KDP_PHASES mode=%s stage=%.4f fasttry=%.4f rows=%.4f '
-            'finish_fast=%.4f finish_pair=%.4f tail=%.4f loopctl=%.4f total_gcyc=%.3f work=%d fast=%d rescue=%d\\n",\n'
+            'finish_fast=%.4f finish_pair=%.4f tail=%.4f loopctl=%.4f walk=%.4f total_gcyc=%.3f work=%d fast=%d rescue=%d\\n",\n'
             '                        L ? "local" : "e2e", ph[L][0] / tot, ph[L][1] / tot, ph[L][2] / tot,\n'
-            '                        ph[L][3] / tot, ph[L][4] / tot, ph[L][5] / tot, ph[L][6] / tot, tot / 1e9,\n'
+            '                        ph[L][3] / tot, ph[L][4] / tot, ph[L][5] / tot, ph[L][6] / tot, ph[L][7] / tot, tot / 1e9,\n'
             '                        ctr[0], ctr[3], ctr[4]);\n'
             '                memset(ph, 0, sizeof(ph));\n'
             '                MH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ph), ph, sizeof(ph)));\n'
