@@ -157,6 +157,17 @@ __device__ __forceinline__ RowV unpack_row(const PileArgs &A, int pk, int h)
     return v;
 }
 
+__device__ __forceinline__ void sam_base_at(const DevReads &R, int rev, int m, int64_t roff, int x,
+                                            char &c, char &q)
+{
+    const int b = rev ? m - 1 - x : x;
+    const int64_t g = roff + b;
+    uint32_t code = ((R.nmask[g >> 5] >> (g & 31)) & 1) ? 4 : (R.seq2[g >> 4] >> (2 * (g & 15))) & 3;
+    if (rev && code < 4) code = 3 - code;
+    c = "ACGTN"[code];
+    q = (char)R.qual[g];
+}
+
 __device__ __forceinline__ void sam_base(const DevReads &R, const RowV &v, int x, char &c, char &q)
 {
     const int b = v.rev ? v.m - 1 - x : x;
@@ -221,47 +232,6 @@ struct RefLds {
     int max_pos;
     long long first_unit;
 };
-
-// merge_pairs on two insertions (strings without '-'), sam2aln.py:156-237:
-// s1 = bases [o1, o1 + l1) of mate w, s2 = bases [o2, o2 + l2) of mate v,
-// read from the resident reads; the shorter one plays seq1.
-__device__ int merge_ins_strings(const DevReads &R, const RowV &w, int o1, int l1, const RowV &v,
-                                 int o2, int l2, int q_cutoff, char *out)
-{
-    // the two mates as values (a swap of pointers to them would put them
-    // in scratch memory)
-    const bool sw = l1 > l2;
-    const RowV r1 = sw ? v : w, r2 = sw ? w : v;
-    if (sw) {
-        int x = o1; o1 = o2; o2 = x;
-        x = l1; l1 = l2; l2 = x;
-    }
-    const unsigned char cut = (unsigned char)(q_cutoff + 33);
-    for (int i = 0; i < l2; ++i) {
-        char c2, q2c;
-        sam_base(R, r2, o2 + i, c2, q2c);
-        const unsigned char b = (unsigned char)q2c;
-        if (i < l1) {
-            char c1, q1c;
-            sam_base(R, r1, o1 + i, c1, q1c);
-            const unsigned char a = (unsigned char)q1c;
-            if (c1 == c2) {
-                out[i] = (a > cut || b > cut) ? c1 : 'N';
-            } else {
-                const int dq = (int)b - (int)a;
-                if ((dq < 0 ? -dq : dq) >= 5) {
-                    const unsigned char m2 = b > cut ? b : cut, m1 = a > cut ? a : cut;
-                    out[i] = a > m2 ? c1 : (b > m1 ? c2 : 'N');
-                } else {
-                    out[i] = 'N';
-                }
-            }
-        } else {
-            out[i] = b > cut ? c2 : 'N';
-        }
-    }
-    return l2;
-}
 
 // Wave-wide scans and reductions on DPP (row shifts, then the two row
 // broadcasts): register-to-register, where __shfl goes through the LDS
@@ -369,6 +339,9 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
         // that op is an M (S/M/S reads), else -1; such a mate expands as
         // read offset + t with no op lookup
         int oneA = -1, oneB = -1;
+        // lane o: reference end and read offset (-1: deletion) of op o
+        // of each mate, for the first 64 ops (the expansion's op lookup)
+        int oendA = 0, ordA = 0, oendB = 0, ordB = 0;
         auto pad = [&](int k) { return k ? padB : padA; };
         auto len = [&](int k) { return k ? lenB : lenA; };
         auto one = [&](int k) { return k ? oneB : oneA; };
@@ -395,6 +368,10 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
                 if (o < nc) {
                     L.opref(k)[o] = rf0 + iref - dref;
                     L.opread(k)[o] = isd ? -1 : rd0 + iread - dread;   // -1: deletion
+                }
+                if (o0 == 0) {
+                    if (k) { oendB = iref; ordB = isd ? -1 : iread - dread; }
+                    else { oendA = iref; ordA = isd ? -1 : iread - dread; }
                 }
                 bad |= __any(badop);
                 n_iops += __popcll(__ballot(isi));
@@ -427,6 +404,28 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
             for (int k = 0; k < 2; ++k) {
                 const RowV mk = mate(k);
                 const int span = k ? spanB : spanA;
+                // the M/D op covering reference offset t (I/S ops span nothing):
+                // the last op whose reference start is <= t, found by a
+                // wave-uniform pass over the op ends (lane values, no LDS
+                // round trips) when the mate has <= 64 ops
+                // dl[ch]: read offset minus reference offset of the op, or
+                // DEL_MARK for a deletion
+                constexpr int DEL_MARK = -(1 << 30);
+                int dl[PU_XCH];
+                const int nc = mk.n_cigar;
+                if (one(k) < 0 && nc <= 64) {
+                    const int oend = k ? oendB : oendA, ord = k ? ordB : ordA;
+                    const int rd0 = __builtin_amdgcn_readlane(ord, 0);
+#pragma unroll
+                    for (int ch = 0; ch < PU_XCH; ++ch) dl[ch] = rd0 >= 0 ? rd0 : DEL_MARK;
+                    for (int o = 0; o + 1 < nc; ++o) {
+                        const int e = __builtin_amdgcn_readlane(oend, o);
+                        const int rdn = __builtin_amdgcn_readlane(ord, o + 1);
+                        const int dn = rdn >= 0 ? rdn - e : DEL_MARK;
+#pragma unroll
+                        for (int ch = 0; ch < PU_XCH; ++ch) dl[ch] = ch * 64 + lane >= e ? dn : dl[ch];
+                    }
+                }
 #pragma unroll
                 for (int ch = 0; ch < PU_XCH; ++ch) {
                     const int t = ch * 64 + lane;
@@ -435,8 +434,10 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
                         int rd, r0 = 0;
                         if (one(k) >= 0) {
                             rd = one(k);   // the one M op starts at reference offset 0
+                        } else if (nc <= 64) {
+                            rd = dl[ch] == DEL_MARK ? -1 : t + dl[ch];
+                            r0 = t;
                         } else {
-                            // the M/D op covering reference offset t (I/S ops span nothing)
                             int o = 0;
                             while (L.opref(k)[o + 1] <= t) ++o;
                             rd = L.opread(k)[o];
@@ -512,59 +513,118 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
             nop2 = q2.op0;
             ops_ready = true;
         }
-        // ---- merge_inserts (lane 0, only units with I ops): keys left + pad,
-        // sam2aln.py:133-135, :240-273 ----
-        if (lane == 0) {
+        // ---- merge_inserts (only units with I ops): keys left + pad,
+        // sam2aln.py:133-135, :240-273.  A wave-uniform walk over the I ops;
+        // the inserted bases of each are read, tested and merged
+        // lane-parallel (64 per round). ----
+        {
             int n = 0, used = 0;
-            // unrolled: mate(pass) with a run-time pass would keep the two
-            // RowV in scratch memory
+            int keyv = -1;   // lane z < 64: key of entry z
 #pragma unroll
             for (int pass = 0; pass < 2; ++pass) {
                 if (pass >= nm || !n_iops) break;
                 const RowV v = mate(pass);
                 for (int o = 0; o < v.n_cigar; ++o) {
-                    if ((v.cig[o] & 15) != MH_OP_I) continue;
-                    const int il = (int)(v.cig[o] >> 4);
-                    const int key = L.opread(pass)[o] + pad(pass);
-                    char tc, tq;
-                    unsigned char mn = 255;
-                    for (int x = 0; x < il; ++x) {
-                        sam_base(A.R, v, L.opread(pass)[o] + x, tc, tq);
-                        if ((unsigned char)tq < mn) mn = (unsigned char)tq;
+                    const uint32_t op = o < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)v.op0, o)
+                                               : (uint32_t)__builtin_amdgcn_readfirstlane((int)v.cig[o]);
+                    if ((op & 15) != MH_OP_I) continue;
+                    const int il = (int)(op >> 4);
+                    const int rdo = __builtin_amdgcn_readfirstlane(L.opread(pass)[o]);
+                    const int key = rdo + pad(pass);
+                    int mn = 255;
+                    for (int x0 = 0; x0 < il; x0 += 64) {
+                        char tc, tq;
+                        if (x0 + lane < il) {
+                            sam_base(A.R, v, rdo + x0 + lane, tc, tq);
+                            mn = (unsigned char)tq < mn ? (unsigned char)tq : mn;
+                        }
                     }
+                    mn = wave_min_all(mn);
                     if (!(mn > cut)) continue;
-                    if (used + 2 * il + 2 > PU_INSBUF) { atomicExch(&A.ev_ctr[3], 1ull); continue; }
-                    // locate an existing entry with the same key (ins1 vs ins2)
+                    if (used + 2 * il + 2 > PU_INSBUF) {
+                        if (lane == 0) atomicExch(&A.ev_ctr[3], 1ull);
+                        continue;
+                    }
+                    // an existing entry with the same key (ins1 vs ins2): the last one
                     int at = -1;
-                    for (int z = 0; z < n; ++z) if (I.key[z] == key) at = z;
+                    const uint64_t same = __builtin_amdgcn_ballot_w64(lane < n && keyv == key);
+                    if (same) at = 63 - (int)__builtin_clzll(same);
+                    for (int z = 64; z < n; ++z)
+                        if (__builtin_amdgcn_readfirstlane(I.key[z]) == key) at = z;
                     char *dst = I.buf + used;
                     int outlen;
                     if (pass == 0) {
-                        for (int x = 0; x < il; ++x) sam_base(A.R, v, L.opread(pass)[o] + x, dst[x], tc);
+                        for (int x0 = 0; x0 < il; x0 += 64) {
+                            char tc, tq;
+                            if (x0 + lane < il) {
+                                sam_base(A.R, v, rdo + x0 + lane, tc, tq);
+                                dst[x0 + lane] = tc;
+                            }
+                        }
                         outlen = il;
                     } else {
                         // ins1 at this key (even if it failed quality) merges with ins2
                         int l1 = 0, o1s = 0;
                         const RowV &w = m0;
                         for (int o1 = 0; o1 < w.n_cigar; ++o1) {
-                            if ((w.cig[o1] & 15) != MH_OP_I) continue;
-                            if (L.opread(0)[o1] + padA != key) continue;
-                            l1 = (int)(w.cig[o1] >> 4);
+                            const uint32_t op1 = o1 < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)w.op0, o1)
+                                                         : (uint32_t)__builtin_amdgcn_readfirstlane((int)w.cig[o1]);
+                            if ((op1 & 15) != MH_OP_I) continue;
+                            const int r1 = __builtin_amdgcn_readfirstlane(L.opread(0)[o1]);
+                            if (r1 + padA != key) continue;
+                            l1 = (int)(op1 >> 4);
                             if (l1 > PU_INSBUF / 8) l1 = PU_INSBUF / 8;
-                            o1s = L.opread(0)[o1];
+                            o1s = r1;
                         }
                         const int l2 = il > PU_INSBUF / 8 ? PU_INSBUF / 8 : il;
-                        outlen = merge_ins_strings(A.R, w, o1s, l1, v, L.opread(pass)[o], l2,
-                                                   A.q_cutoff, dst);
+                        // merge_pairs on the two strings (sam2aln.py:156-237): the
+                        // shorter one plays seq1
+                        const bool sw = l1 > l2;
+                        const int la = sw ? l2 : l1, lb = sw ? l1 : l2;
+                        const int oa = sw ? rdo : o1s, ob = sw ? o1s : rdo;
+                        const int reva = sw ? v.rev : w.rev, ma = sw ? v.m : w.m;
+                        const int revb = sw ? w.rev : v.rev, mb = sw ? w.m : v.m;
+                        const int64_t roffa = sw ? v.roff : w.roff, roffb = sw ? w.roff : v.roff;
+                        for (int i0 = 0; i0 < lb; i0 += 64) {
+                            const int i = i0 + lane;
+                            if (i >= lb) continue;
+                            char c2, q2c;
+                            sam_base_at(A.R, revb, mb, roffb, ob + i, c2, q2c);
+                            const unsigned char b = (unsigned char)q2c;
+                            char oc;
+                            if (i < la) {
+                                char c1, q1c;
+                                sam_base_at(A.R, reva, ma, roffa, oa + i, c1, q1c);
+                                const unsigned char a = (unsigned char)q1c;
+                                if (c1 == c2) {
+                                    oc = (a > cut || b > cut) ? c1 : 'N';
+                                } else {
+                                    const int dq = (int)b - (int)a;
+                                    if ((dq < 0 ? -dq : dq) >= 5) {
+                                        const unsigned char m2 = b > cut ? b : cut, m1 = a > cut ? a : cut;
+                                        oc = a > m2 ? c1 : (b > m1 ? c2 : 'N');
+                                    } else {
+                                        oc = 'N';
+                                    }
+                                }
+                            } else {
+                                oc = b > cut ? c2 : 'N';
+                            }
+                            dst[i] = oc;
+                        }
+                        outlen = lb;
                     }
                     if (at < 0) at = n++;
-                    I.key[at] = key;
-                    I.off[at] = used;
-                    I.len[at] = outlen;
+                    if (lane == 0) {
+                        I.key[at] = key;
+                        I.off[at] = used;
+                        I.len[at] = outlen;
+                    }
+                    if (lane == at) keyv = key;
                     used += outlen;
                 }
             }
-            *L.n_ins = n;
+            if (lane == 0) *L.n_ins = n;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
