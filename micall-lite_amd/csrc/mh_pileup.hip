@@ -16,7 +16,7 @@ namespace mh {
 
 constexpr int PU_INSBUF = 2048;   // merged insertion bytes per unit
 constexpr int PU_MAXINS = 2 * MH_MAXOPS;
-constexpr int PU_LDS = 160 * 1024;
+constexpr int PU_LDS = 160 * 1024 - 64;   // dynamic LDS (the static s_next beside it)
 constexpr int PU_XCH = 5;        // 64-position chunks per mate expanded with all loads in flight
 
 struct RowV {
@@ -287,6 +287,8 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
                            A.span_cap);
     const InsView I = ins_view(A.ins_scratch + ((size_t)blockIdx.x * wpb + wv) * PU_INS_BYTES);
     const unsigned char cut = (unsigned char)(A.q_cutoff + 33);
+    __shared__ int s_next;   // the block's next unit slot (see unit_of)
+    if (threadIdx.x == 0) s_next = wpb;
     for (int x = threadIdx.x; x < A.win_words; x += blockDim.x) win[x] = 0;
     for (int x = threadIdx.x; x < NR; x += blockDim.x) {
         rl[x].read_count = 0;
@@ -297,14 +299,19 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
     }
     __syncthreads();
 
-    // the next unit's rows are loaded while this one is processed
+    // The block's units are the grid-strided set {block * wpb + x + k * wpb *
+    // blocks}; its waves take them in order from an LDS counter (slot c ->
+    // unit_of(c)), so a wave that drew cheap units takes more and the block
+    // ends when its units do, not when its slowest wave's fixed share does.
+    // The next unit's rows are loaded while this one is processed.
     const int64_t ustride = (int64_t)gridDim.x * wpb;
-    int64_t u = (int64_t)blockIdx.x * wpb + wv;
+    auto unit_of = [&](int64_t c) { return (int64_t)blockIdx.x * wpb + c % wpb + (c / wpb) * ustride; };
+    int64_t u = unit_of(wv), un = A.n_units;
     int npk = 0;                  // the next unit's rows, lane-distributed
     uint32_t nop1 = 0, nop2 = 0;  // and this lane's CIGAR op of their first 64
     bool ops_ready = false;       // the CIGAR ops of the next unit were fetched
     if (u < A.n_units) npk = load_rows_packed<SRC>(A, u, lane);
-    for (; u < A.n_units; u += ustride) {
+    for (; u < A.n_units; u = un) {
         RowV r1 = unpack_row<SRC>(A, npk, 0), r2 = unpack_row<SRC>(A, npk, 1);
         if (ops_ready) {
             r1.op0 = nop1;
@@ -314,8 +321,13 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
             fetch_ops(r2, lane);
         }
         ops_ready = false;
-        const bool more = u + ustride < A.n_units;
-        if (more) npk = load_rows_packed<SRC>(A, u + ustride, lane);
+        {
+            int cn = 0;
+            if (lane == 0) cn = atomicAdd(&s_next, 1);
+            un = unit_of(__builtin_amdgcn_readfirstlane(cn));
+        }
+        const bool more = un < A.n_units;
+        if (more) npk = load_rows_packed<SRC>(A, un, lane);
         if (SRC == 0 && !r1.present && r2.present) { r1 = r2; r2.present = 0; }  // unpaired view
         if (!r1.present) continue;
         if (r2.present && r1.ref != r2.ref) continue;           // remap.py:96-98
@@ -705,15 +717,19 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
         // this reference's LDS counter window (wo < 0: none), wl positions
         const int wo = __builtin_amdgcn_readfirstlane(wmap[2 * ref]);
         const int wl = __builtin_amdgcn_readfirstlane(wmap[2 * ref + 1]);
-        for (int i0 = begin; i0 < len2; i0 += 64) {
-            const int i = i0 + lane;
-            if (i >= len2) break;
+        // the merged character of position i (sam2aln merge_pairs, :192-237),
+        // 0 past seq2; every LDS read unconditional (clamped index) so the two
+        // positions of a round read together
+        auto merged = [&](int i) -> char {
+            const bool in2 = i < len2, in1 = a >= 0 && i < len1;
+            const int j2 = i >= pad2 && in2 ? i - pad2 : 0;
+            const int j1 = in1 && i >= pad1 ? i - pad1 : 0;
+            const char c2r = L.c(b)[j2], q2r = L.q(b)[j2];
+            const char c1r = L.c(a >= 0 ? a : 0)[j1], q1r = L.q(a >= 0 ? a : 0)[j1];
+            const char c2 = i < pad2 ? '-' : c2r, q2 = i < pad2 ? '!' : q2r;
+            const char c1 = i < pad1 ? '-' : c1r, q1 = i < pad1 ? '!' : q1r;
             char mc;
-            char c2, q2;
-            ch2(i, c2, q2);
-            if (i < len1) {
-                char c1, q1;
-                ch1(i, c1, q1);
+            if (in1) {
                 const unsigned char qa = (unsigned char)q1, qb = (unsigned char)q2;
                 if (c1 == '-' && c2 == '-') mc = '-';
                 else if (c1 == c2) mc = (qa > cut || qb > cut) ? c1 : 'N';
@@ -730,13 +746,17 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
                 if (c2 == '-') mc = i >= rev_start ? '-' : 'n';
                 else mc = (unsigned char)q2 > cut ? c2 : 'N';
             }
-            if (mc == 'n') continue;
+            return in2 ? mc : (char)0;
+        };
+        // update_counts of one merged character
+        auto count = [&](int i, char mc) {
+            if (mc == 0 || mc == 'n') return;
             const int P = i - shift + 1;
-            if (P > A.cap) { err = 1; continue; }
+            if (P > A.cap) { err = 1; return; }
             mxp = P > mxp ? P : mxp;
             const int64_t cell = (int64_t)ref * A.cap + (P - 1);
-            if (mc == 'N') { A.nflag[cell] = 1; continue; }
-            if (mc == '-') { A.dflag[cell] = 1; continue; }
+            if (mc == 'N') { A.nflag[cell] = 1; return; }
+            if (mc == '-') { A.dflag[cell] = 1; return; }
             int hit = -1;
             if (n_ins > 0) {
                 hit = P == ik0 ? 0 : P == ik1 ? 1 : P == ik2 ? 2 : P == ik3 ? 3 : -1;
@@ -763,6 +783,12 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
                 if (wo >= 0 && P <= wl) atomicAdd(&win[wo + (code >> 1) * wl + (P - 1)], 1u << (16 * (code & 1)));
                 else atomicAdd(&A.dense[cell * 4 + code], 1);
             }
+        };
+        for (int i0 = begin; i0 < len2; i0 += 128) {
+            const int ia = i0 + lane, ib = ia + 64;
+            const char ma = merged(ia), mb = merged(ib);
+            count(ia, ma);
+            count(ib, mb);
         }
         mxp = wave_max_all(mxp);
         err = wave_max_all(err);
