@@ -728,56 +728,51 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
             const char c1r = L.c(a >= 0 ? a : 0)[j1], q1r = L.q(a >= 0 ? a : 0)[j1];
             const char c2 = i < pad2 ? '-' : c2r, q2 = i < pad2 ? '!' : q2r;
             const char c1 = i < pad1 ? '-' : c1r, q1 = i < pad1 ? '!' : q1r;
-            char mc;
-            if (in1) {
-                const unsigned char qa = (unsigned char)q1, qb = (unsigned char)q2;
-                if (c1 == '-' && c2 == '-') mc = '-';
-                else if (c1 == c2) mc = (qa > cut || qb > cut) ? c1 : 'N';
-                else {
-                    const int dq = (int)qb - (int)qa;
-                    if ((dq < 0 ? -dq : dq) >= 5) {
-                        const unsigned char m2 = qb > cut ? qb : cut, m1 = qa > cut ? qa : cut;
-                        mc = qa > m2 ? c1 : (qb > m1 ? c2 : 'N');
-                    } else {
-                        mc = 'N';
-                    }
-                }
-            } else {
-                if (c2 == '-') mc = i >= rev_start ? '-' : 'n';
-                else mc = (unsigned char)q2 > cut ? c2 : 'N';
-            }
+            // as selects, not branches: the lanes of a round take every case
+            const int qa = (unsigned char)q1, qb = (unsigned char)q2, ic = (int)cut;
+            const int dq = qb > qa ? qb - qa : qa - qb;
+            const int m2 = qb > ic ? qb : ic, m1 = qa > ic ? qa : ic;
+            const char mdiff = qa > m2 ? c1 : (qb > m1 ? c2 : 'N');
+            const char msame = (qa > ic || qb > ic) ? c1 : 'N';
+            const char m_in1 = (c1 == '-' && c2 == '-') ? '-' : (c1 == c2 ? msame : (dq >= 5 ? mdiff : 'N'));
+            const char m_out = c2 == '-' ? (i >= rev_start ? '-' : 'n') : (qb > ic ? c2 : 'N');
+            const char mc = in1 ? m_in1 : m_out;
             return in2 ? mc : (char)0;
         };
         // update_counts of one merged character
         auto count = [&](int i, char mc) {
-            if (mc == 0 || mc == 'n') return;
             const int P = i - shift + 1;
-            if (P > A.cap) { err = 1; return; }
-            mxp = P > mxp ? P : mxp;
+            const bool live = mc != 0 && mc != 'n';
+            if (live && P > A.cap) err = 1;
+            const bool ok = live && P <= A.cap;
+            mxp = ok && P > mxp ? P : mxp;
             const int64_t cell = (int64_t)ref * A.cap + (P - 1);
-            if (mc == 'N') { A.nflag[cell] = 1; return; }
-            if (mc == '-') { A.dflag[cell] = 1; return; }
-            int hit = -1;
+            const bool isN = mc == 'N', isD = mc == '-';
+            if (ok && isN) A.nflag[cell] = 1;
+            if (ok && isD) A.dflag[cell] = 1;
+            bool base = ok && !isN && !isD;
             if (n_ins > 0) {
-                hit = P == ik0 ? 0 : P == ik1 ? 1 : P == ik2 ? 2 : P == ik3 ? 3 : -1;
+                int hit = P == ik0 ? 0 : P == ik1 ? 1 : P == ik2 ? 2 : P == ik3 ? 3 : -1;
                 for (int z = 4; z < n_ins; ++z)
                     if (I.key[z] == P) hit = z;
-            }
-            if (hit >= 0 && I.len[hit] > 0 && I.len[hit] % 3 == 0) {
-                const int tl = 1 + I.len[hit];
-                const unsigned long long e = atomicAdd(&A.ev_ctr[0], 1ull);
-                const unsigned long long p = atomicAdd(&A.ev_ctr[1], (unsigned long long)tl);
-                if ((long long)e < A.ev_cap && (long long)(p + tl) <= A.pool_cap) {
-                    A.ev[4 * e] = ref;
-                    A.ev[4 * e + 1] = P;
-                    A.ev[4 * e + 2] = (int32_t)p;
-                    A.ev[4 * e + 3] = tl;
-                    A.ev_pool[p] = mc;
-                    for (int x = 0; x < tl - 1; ++x) A.ev_pool[p + 1 + x] = I.buf[I.off[hit] + x];
-                } else {
-                    atomicExch(&A.ev_ctr[2], 1ull);
+                if (base && hit >= 0 && I.len[hit] > 0 && I.len[hit] % 3 == 0) {
+                    base = false;
+                    const int tl = 1 + I.len[hit];
+                    const unsigned long long e = atomicAdd(&A.ev_ctr[0], 1ull);
+                    const unsigned long long p = atomicAdd(&A.ev_ctr[1], (unsigned long long)tl);
+                    if ((long long)e < A.ev_cap && (long long)(p + tl) <= A.pool_cap) {
+                        A.ev[4 * e] = ref;
+                        A.ev[4 * e + 1] = P;
+                        A.ev[4 * e + 2] = (int32_t)p;
+                        A.ev[4 * e + 3] = tl;
+                        A.ev_pool[p] = mc;
+                        for (int x = 0; x < tl - 1; ++x) A.ev_pool[p + 1 + x] = I.buf[I.off[hit] + x];
+                    } else {
+                        atomicExch(&A.ev_ctr[2], 1ull);
+                    }
                 }
-            } else {
+            }
+            if (base) {
                 const int code = mc == 'A' ? 0 : mc == 'C' ? 1 : mc == 'G' ? 2 : 3;
                 // u16 halves: a block counts < 65536 units (pile_geometry)
                 if (wo >= 0 && P <= wl) atomicAdd(&win[wo + (code >> 1) * wl + (P - 1)], 1u << (16 * (code & 1)));
