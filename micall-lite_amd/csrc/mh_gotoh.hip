@@ -360,7 +360,7 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
         auto step = [&](auto leftc, auto rightc, auto tlc, auto predc, int q) {
             constexpr bool LEFT = decltype(leftc)::value, RIGHT = decltype(rightc)::value;
             constexpr bool TL = decltype(tlc)::value, PRED = LEFT || RIGHT || decltype(predc)::value;
-            const int t = t0 + q, j = j0 + q;
+            const int j = j0 + q;
             const int2 bd = brd[q];
             const int sc = prof[pbase + q];
             const int Rup = __builtin_amdgcn_update_dpp(bd.x, Rme, 0x138, 0xF, 0xF, false);

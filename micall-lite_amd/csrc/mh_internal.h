@@ -92,6 +92,7 @@ struct Cand {
 // Result of one banded extension (one candidate of one read).
 struct Slot {
     int32_t valid, strand, ref, pos, end, score, xm, xo, xg, nm, n_cigar, cig_off;
+    int32_t maxm;   // longest M run of the CIGAR (remap.py:500-506 filter), from the traceback
 };
 
 // Final per-read SAM record (mh_aln without the inline CIGAR).
@@ -115,7 +116,7 @@ struct MapState {
     int64_t pool_cap = 0;
     unsigned long long *pool_used = nullptr;  // words claimed (demand; may exceed pool_cap)
     Rec *rec = nullptr;          // n_reads
-    int32_t *counters = nullptr; // [work_n, unused, pool_overflow, fast, rescue_n, pad..]
+    int32_t *counters = nullptr; // [work_n, unused, pool_overflow, fast, rescue_n, queue, rescue queue, pad]
     int64_t *ref_stats = nullptr;// per ref: lines, filtered, mapped, first_row, first_mapped; + unmapped, star
     int64_t cap_reads = 0;
     int cap_refs = 0;

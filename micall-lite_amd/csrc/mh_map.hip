@@ -558,6 +558,7 @@ struct DpArgs {
     uint32_t *pool;
     unsigned long long *pool_used;  // words claimed so far (64-bit: never wraps)
     int32_t *pool_ctr;        // [1] overflow, [2] fast-path extensions
+    int32_t *queue;           // work-queue counter (chunks past the static first ones), zeroed
     int64_t pool_cap;
     int rows_pad;             // per-wave LDS row capacity (multiple of 8)
     int wave_lds;             // bytes of LDS per wave
@@ -584,6 +585,7 @@ constexpr int RUNS_CAP = 256;
 // extension); the pool is sized for every resident wave's partial chunk.
 constexpr int POOL_CHUNK = 256;
 constexpr int DP_MAX_BLOCKS = 256 * 48;
+constexpr int DP_QUEUE_CHUNK = 8;       // k_dp work items per queue chunk
 
 template <int CTRL>
 __device__ __forceinline__ int dppz(int v)
@@ -1530,12 +1532,13 @@ __device__ void post_ext(const DpArgs &A, const XItem &it, const XView &X, int b
                     atomicExch(&A.pool_ctr[1], 1);
                 } else {
                     uint32_t *cg = A.pool + base;
-                    int n = 0, xo = 0, xg = 0;
+                    int n = 0, xo = 0, xg = 0, mx = 0;
                     if (clipL) cg[n++] = ((uint32_t)clipL << 4) | MH_OP_S;
                     for (int z = lo; z >= hi; --z) {
                         const uint32_t rr = z == hi ? back : (z == lo ? front : runs[z]);
                         cg[n++] = rr;
                         if ((rr & 15) != MH_OP_M) { ++xo; xg += (int)(rr >> 4); }
+                        else if ((int)(rr >> 4) > mx) mx = (int)(rr >> 4);
                     }
                     if (clipR) cg[n++] = ((uint32_t)clipR << 4) | MH_OP_S;
                     out.valid = 1;
@@ -1547,6 +1550,7 @@ __device__ void post_ext(const DpArgs &A, const XItem &it, const XView &X, int b
                     out.cig_off = (int32_t)base;
                     out.xm = cnt & 0xffff;
                     out.nm = out.xm + xg;
+                    out.maxm = mx;
                 }
             }
         }
@@ -1592,18 +1596,35 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     int64_t ck_base = 0;   // lane 0: this wave's current CIGAR pool chunk
     int ck_left = 0;
     int n_fast = 0;        // extensions resolved by dp_ungapped
-    // Software pipeline over the work items, three deep: while item w is
-    // aligned, the candidate and read descriptors of item w + 2s are loaded
-    // (scalar loads; and the work id of w + 3s), and item w + s, whose
-    // descriptors landed during the previous item, gets its reference window
-    // and (reads of one staging round) its raw bytes issued by LDS-DMA, so
-    // they land while w is aligned.  A wave then waits on no global round
-    // trip between items.
-    const int wstride = gridDim.x * wpb;
+    // Work items come in chunks of QCH from a queue: a wave's first chunk is
+    // its own (wave id), the next ones are taken by one atomic each on lane 0,
+    // issued a chunk ahead, so the waves of a launch sized to what is resident
+    // finish together.  Item position p of the wave is chunk cA's item p (or,
+    // past QCH, chunk cB's item p - QCH).
+    // Software pipeline over the items, three deep: while item w is aligned,
+    // the candidate and read descriptors of the item after next are loaded
+    // (scalar loads; and the work id of the one after that), and the next
+    // item, whose descriptors landed during the previous one, gets its
+    // reference window and (reads of one staging round) its raw bytes issued
+    // by LDS-DMA, so they land while w is aligned.  A wave then waits on no
+    // global round trip between items.
+    constexpr int QCH = DP_QUEUE_CHUNK;
+    const int gwaves = gridDim.x * wpb;
     constexpr bool one_round = ONE_ROUND;   // rows_pad <= STAGE_ROWS
-    int w = blockIdx.x * wpb + wv;
-    XItem cur{};                       // item w: every field, staging loads issued
-    int sid1 = 0, m1 = 0, sid2 = 0;    // item w + s: work id, candidate, read; w + 2s: work id
+    int cA = (blockIdx.x * wpb + wv) * QCH, cB = 0, qv = 0, p = 0;
+    auto grab = [&]() {   // lane 0: the base of a later chunk (in flight until read)
+        if (lane == 0) qv = atomicAdd(A.queue, QCH) + gwaves * QCH;
+    };
+    grab();
+    cB = __builtin_amdgcn_readfirstlane(qv);
+    grab();
+    auto at = [&](int d) {   // item index at position p + d (d <= 3 < QCH)
+        const int q = p + d;
+        return q < QCH ? cA + q : cB + (q - QCH);
+    };
+    int w = cA;
+    XItem cur{};                       // item w: every field, staging issued
+    int sid1 = 0, m1 = 0, sid2 = 0;    // next item: work id, candidate, read; the one after: work id
     Cand cd1{};
     int64_t roff1 = 0;
     auto to_item = [&](int sid, const Cand &cd, int m, int64_t roff) {
@@ -1625,17 +1646,17 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         cur = to_item(sid, ldc_cand(&A.cand[sid]), ldc(&A.R.len[sid / MAXCAND]),
                       ldc(&A.R.off[sid / MAXCAND]));
     }
-    if (w + wstride < n_work) {
-        sid1 = ldc(&A.work[w + wstride]);
+    if (at(1) < n_work) {
+        sid1 = ldc(&A.work[at(1)]);
         cd1 = ldc_cand(&A.cand[sid1]);
         m1 = ldc(&A.R.len[sid1 / MAXCAND]);
         roff1 = ldc(&A.R.off[sid1 / MAXCAND]);
     }
-    if (w + 2 * wstride < n_work) sid2 = ldc(&A.work[w + 2 * wstride]);
+    if (at(2) < n_work) sid2 = ldc(&A.work[at(2)]);
     bool pend = false;     // half 0 holds an item waiting for the DP
     bool landed = false;   // the raw bytes of `cur` were waited for
     XItem P{};
-    for (; w < n_work; w += wstride) {
+    while (w < n_work) {
         const XItem it = cur;
         const int h = pend ? 1 : 0;
         const XView X = h ? X1 : X0;
@@ -1650,14 +1671,14 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         const bool fast = it.m > 2 * GBAR + 8 && it.m <= 512 &&
                           dp_ungapped<LOCAL>(X, it.m, lane, gmin, it.hb, best, bi, bl, low);
         n_fast += fast;
-        if (w + wstride < n_work) cur = to_item(sid1, cd1, m1, roff1);
-        if (w + 2 * wstride < n_work) {
+        if (at(1) < n_work) cur = to_item(sid1, cd1, m1, roff1);
+        if (at(2) < n_work) {
             sid1 = sid2;
             cd1 = ldc_cand(&A.cand[sid2]);
             m1 = ldc(&A.R.len[sid2 / MAXCAND]);
             roff1 = ldc(&A.R.off[sid2 / MAXCAND]);
         }
-        if (w + 3 * wstride < n_work) sid2 = ldc(&A.work[w + 3 * wstride]);
+        if (at(3) < n_work) sid2 = ldc(&A.work[at(3)]);
         // The next item's raw bytes are waited for before this item's
         // traceback stores anything: the vector memory counter is in order,
         // so a wait after the stores would also wait for their write acks.
@@ -1678,6 +1699,13 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
             finish_ext<LOCAL>(A, it, X1, bits, 32, b1, i1, l1, lane, ck_base, ck_left);
             pend = false;
         }
+        if (++p == QCH) {   // into the next chunk; take the one after it
+            p = 0;
+            cA = cB;
+            cB = __builtin_amdgcn_readfirstlane(qv);
+            grab();
+        }
+        w = at(0);
     }
     if (pend) {
         int b0, i0, l0, b1, i1, l1;
@@ -1976,12 +2004,7 @@ __device__ void fill_aligned(const PairArgs &A, Rec &o, const MateView &mv, int 
     o.xm = a.xm; o.xo = a.xo; o.xg = a.xg; o.nm = a.nm;
     o.n_cigar = a.n_cigar;
     o.cig_off = a.cig_off;
-    int mx = 0;
-    for (int k = 0; k < a.n_cigar; ++k) {
-        const uint32_t op = A.pool[a.cig_off + k];
-        if ((op & 15) == MH_OP_M && (int)(op >> 4) > mx) mx = (int)(op >> 4);
-    }
-    o.maxm = mx;
+    o.maxm = a.maxm;
     o.sam_ref = a.ref;
     o.sam_pos = a.pos + 1;
 }
@@ -2300,20 +2323,27 @@ int run_map(Ctx &c, const mh_params &par)
         int wpb = DP_WAVES_PER_BLOCK;
         while (wpb > 1 && wpb * wave_lds > 160 * 1024) --wpb;
         if (wave_lds > 160 * 1024) { set_error("mh_map: reads too long for LDS"); return -3; }
-        auto launch_dp = [&](const int32_t *work, const int32_t *count, int64_t max_items,
-                             const char *name) -> int {
+        auto launch_dp = [&](const int32_t *work, const int32_t *count, int32_t *queue,
+                             int64_t max_items, const char *name) -> int {
             DpArgs da{c.reads, c.index, c.len_tab, M.cand, work, count, M.slot, M.pool,
-                      M.pool_used, M.counters + 1, M.pool_cap, rows_pad, wave_lds,
+                      M.pool_used, M.counters + 1, queue, M.pool_cap, rows_pad, wave_lds,
                       par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext,
                       par.rdg_ext};
-            int64_t dblocks = (max_items + wpb - 1) / wpb;
-            if (dblocks > DP_MAX_BLOCKS) dblocks = DP_MAX_BLOCKS;
-            if (dblocks < 1) dblocks = 1;
-            const int pd = prof_begin(c, name);
             const bool one = rows_pad <= STAGE_ROWS;
             const void *kf = par.mode == MH_LOCAL ? (one ? (const void *)k_dp<1, 1> : (const void *)k_dp<1, 0>)
                                                   : (one ? (const void *)k_dp<0, 1> : (const void *)k_dp<0, 0>);
             MH_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, wpb * wave_lds));
+            // the waves that fit at once (the queue balances them), no more
+            // than the items need
+            if (!c.n_cu) MH_HIP(hipDeviceGetAttribute(&c.n_cu, hipDeviceAttributeMultiprocessorCount, c.device));
+            int per_cu = 0;
+            MH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 64 * wpb, (size_t)wpb * wave_lds));
+            int64_t dblocks = (int64_t)(c.n_cu > 0 ? c.n_cu : 256) * (per_cu > 0 ? per_cu : 1);
+            const int64_t need = (max_items + (int64_t)wpb * DP_QUEUE_CHUNK - 1) / ((int64_t)wpb * DP_QUEUE_CHUNK);
+            if (dblocks > need) dblocks = need;
+            if (dblocks > DP_MAX_BLOCKS) dblocks = DP_MAX_BLOCKS;
+            if (dblocks < 1) dblocks = 1;
+            const int pd = prof_begin(c, name);
             if (par.mode == MH_LOCAL) {
                 if (one)
                     hipLaunchKernelGGL((k_dp<1, 1>), dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
@@ -2333,10 +2363,10 @@ int run_map(Ctx &c, const mh_params &par)
         for (int attempt = 0; attempt < 2; ++attempt) {
             // counters: [0] work items, [2] pool overflow, [3] fast path,
             // [4] rescue work items; pool_used: CIGAR words claimed
-            MH_HIP(hipMemsetAsync(M.counters, 0, sizeof(int32_t) * 5, s));
+            MH_HIP(hipMemsetAsync(M.counters, 0, sizeof(int32_t) * 8, s));
             MH_HIP(hipMemsetAsync(M.pool_used, 0, sizeof(unsigned long long), s));
             if (int st = launch_seed()) return st;
-            if (int st = launch_dp(M.work, M.counters, n * 2, "k_dp")) return st;
+            if (int st = launch_dp(M.work, M.counters, M.counters + 5, n * 2, "k_dp")) return st;
             if (c.reads.paired && units > 0) {
                 RescueArgs ra{c.reads, c.index, M.slot, M.n_cand, M.yf, M.cand, M.rwork,
                               M.counters + 4, par.maxins};
@@ -2346,7 +2376,7 @@ int run_map(Ctx &c, const mh_params &par)
                 hipLaunchKernelGGL(k_rescue, dim3((unsigned)rblocks), dim3(256), 0, s, ra);
                 prof_end(c, pr);
                 MH_HIP(hipGetLastError());
-                if (int st = launch_dp(M.rwork, M.counters + 4, units, "k_dp_rescue")) return st;
+                if (int st = launch_dp(M.rwork, M.counters + 4, M.counters + 6, units, "k_dp_rescue")) return st;
             }
             int32_t ctr[5];
             unsigned long long used = 0;

@@ -54,9 +54,9 @@ def main():
                '            wave_sync();\n',
             '            dp_pair<LOCAL>(A, X0, X1, P.m, it.m, P.hb, it.hb, bits, lane, b0, i0, l0, b1, i1, l1);\n'
             '            wave_sync();\n            PH(2);\n')
-    t = sub(t, '            finish_pair<LOCAL>(A, P, X0, it, X1, bits, b0, i0, l0, b1, i1, l1, lane, ck_base, ck_left);\n'
+    t = sub(t, '            finish_ext<LOCAL>(A, it, X1, bits, 32, b1, i1, l1, lane, ck_base, ck_left);\n'
                '            pend = false;\n',
-            '            finish_pair<LOCAL>(A, P, X0, it, X1, bits, b0, i0, l0, b1, i1, l1, lane, ck_base, ck_left);\n'
+            '            finish_ext<LOCAL>(A, it, X1, bits, 32, b1, i1, l1, lane, ck_base, ck_left);\n'
             '            pend = false;\n            PH(4);\n')
     t = sub(t, '    if (lane == 0 && n_fast) atomicAdd(&A.pool_ctr[2], n_fast);\n}',
             '    if (lane == 0 && n_fast) atomicAdd(&A.pool_ctr[2], n_fast);\n'
@@ -68,12 +68,6 @@ def main():
             '    const unsigned long long f0 = __builtin_readcyclecounter();\n')
     t = sub(t, '    const WalkOut W = walk1<LOCAL>(A, it, X, bits, hcol, best, bi, bl, lane, fast_low);\n    wave_sync();\n',
             '    const WalkOut W = walk1<LOCAL>(A, it, X, bits, hcol, best, bi, bl, lane, fast_low);\n    wave_sync();\n'
-            '    fw += __builtin_readcyclecounter() - f0;\n')
-    t = sub(t, 'int i1, int l1, int lane, int64_t &ck_base, int &ck_left)\n{\n',
-            'int i1, int l1, int lane, int64_t &ck_base, int &ck_left, unsigned long long &fw)\n{\n'
-            '    const unsigned long long f0 = __builtin_readcyclecounter();\n')
-    t = sub(t, '    walk2<LOCAL>(A, it0, it1, X0, X1, bits, b0, i0, l0, b1, i1, l1, lane, W0, W1);\n    wave_sync();\n',
-            '    walk2<LOCAL>(A, it0, it1, X0, X1, bits, b0, i0, l0, b1, i1, l1, lane, W0, W1);\n    wave_sync();\n'
             '    fw += __builtin_readcyclecounter() - f0;\n')
     t = t.replace('ck_base, ck_left, low);', 'ck_base, ck_left, ph[7], low);')
     t = t.replace('lane, ck_base, ck_left);', 'lane, ck_base, ck_left, ph[7]);')
