@@ -134,7 +134,14 @@ static int band_half(const mh_params &p, int len)
 
 static int prepare_len_tab(Ctx &c, const mh_params &par)
 {
-    if (c.len_tab && c.len_tab_key == len_tab_key(par)) return 0;
+    const int64_t key = len_tab_key(par);
+    if (c.len_tab && c.len_tab_key == key) return 0;
+    const auto hit = c.len_tabs.find(key);
+    if (hit != c.len_tabs.end()) {
+        c.len_tab = hit->second;
+        c.len_tab_key = key;
+        return 0;
+    }
     std::vector<int32_t> t(4 * (MAXLEN + 1));
     for (int l = 0; l <= MAXLEN; ++l) {
         t[l] = seed_interval(par.mode, l);
@@ -142,9 +149,12 @@ static int prepare_len_tab(Ctx &c, const mh_params &par)
         t[2 * (MAXLEN + 1) + l] = n_ceil(l);
         t[3 * (MAXLEN + 1) + l] = band_half(par, l);
     }
-    if (!c.len_tab) MH_HIP(hipMalloc(&c.len_tab, sizeof(int32_t) * t.size()));
-    MH_HIP(copy_sync(c, c.len_tab, t.data(), sizeof(int32_t) * t.size(), hipMemcpyHostToDevice));
-    c.len_tab_key = len_tab_key(par);
+    int32_t *d = nullptr;
+    MH_HIP(hipMalloc(&d, sizeof(int32_t) * t.size()));
+    c.len_tabs[key] = d;
+    MH_HIP(copy_sync(c, d, t.data(), sizeof(int32_t) * t.size(), hipMemcpyHostToDevice));
+    c.len_tab = d;
+    c.len_tab_key = key;
     return 0;
 }
 
@@ -605,7 +615,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipFree(P.ins_scratch);
     hipFree(P.sel);
     hipFree(P.win_map);
-    hipFree(c->len_tab);
+    for (auto &kv : c->len_tabs) hipFree(kv.second);
     if (c->pin) hipHostFree(c->pin);
     s2a_free(*c);
     censor_free(*c);

@@ -128,6 +128,9 @@ struct MapState {
     // host copy of ref_stats (5 * n_refs + 3), filled on first use after a
     // mapping pass: mh_map_counts and the pileup's window choice share it
     std::vector<int64_t> stats_host;
+    // k_dp launch shapes already sized: (kernel, LDS bytes) -> blocks per CU
+    // that fit (the occupancy query is a host call worth skipping per launch)
+    std::map<std::pair<const void *, int>, int> dp_occ;
     bool stats_host_valid = false;
 };
 
@@ -255,6 +258,10 @@ struct Ctx {
     CensorState *censor = nullptr;   // censored FASTQ of the last mh_censor_fastq
     A2CState **a2c = nullptr;        // aln2counts row tables (mh_a2c_*), one per slot
     int64_t len_tab_key = -1;        // len_tab_key() of the parameters the tables hold
+    // every parameter set's tables seen so far (a prelim pass and a remap
+    // pass alternate end-to-end and local; the band column's gap counts take
+    // a few hundred microseconds of host time to rebuild): key -> device copy
+    std::map<int64_t, int32_t *> len_tabs;
     // k_gotoh's device scratch (traceback planes etc.), grown on demand and
     // kept up to 1 GiB: a hipMalloc / hipFree pair per call cost more than
     // the kernel.  The mutex serialises callers of one context (ctypes

@@ -2299,7 +2299,7 @@ int run_map(Ctx &c, const mh_params &par)
     M.par = par;
     hipStream_t s = c.stream;
     M.last_work = M.last_cigar = 0;
-    hipLaunchKernelGGL(k_init_stats, dim3(64), dim3(256), 0, s, M.ref_stats, M.n_refs);
+    if (n == 0) hipLaunchKernelGGL(k_init_stats, dim3(64), dim3(256), 0, s, M.ref_stats, M.n_refs);
     if (n > 0) {
         // seeds, candidates and the work list; run again by a retry, since
         // k_rescue replaces the candidates of the mates it rescues
@@ -2332,12 +2332,19 @@ int run_map(Ctx &c, const mh_params &par)
             const bool one = rows_pad <= STAGE_ROWS;
             const void *kf = par.mode == MH_LOCAL ? (one ? (const void *)k_dp<1, 1> : (const void *)k_dp<1, 0>)
                                                   : (one ? (const void *)k_dp<0, 1> : (const void *)k_dp<0, 0>);
-            MH_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, wpb * wave_lds));
             // the waves that fit at once (the queue balances them), no more
             // than the items need
-            if (!c.n_cu) MH_HIP(hipDeviceGetAttribute(&c.n_cu, hipDeviceAttributeMultiprocessorCount, c.device));
-            int per_cu = 0;
-            MH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 64 * wpb, (size_t)wpb * wave_lds));
+            const auto okey = std::make_pair(kf, wpb * wave_lds);
+            auto occ = M.dp_occ.find(okey);
+            if (occ == M.dp_occ.end()) {
+                // the cap every k_dp launch fits under (set once per kernel and shape)
+                MH_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                if (!c.n_cu) MH_HIP(hipDeviceGetAttribute(&c.n_cu, hipDeviceAttributeMultiprocessorCount, c.device));
+                int nb = 0;
+                MH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kf, 64 * wpb, (size_t)wpb * wave_lds));
+                occ = M.dp_occ.emplace(okey, nb).first;
+            }
+            const int per_cu = occ->second;
             int64_t dblocks = (int64_t)(c.n_cu > 0 ? c.n_cu : 256) * (per_cu > 0 ? per_cu : 1);
             const int64_t need = (max_items + (int64_t)wpb * DP_QUEUE_CHUNK - 1) / ((int64_t)wpb * DP_QUEUE_CHUNK);
             if (dblocks > need) dblocks = need;
@@ -2360,9 +2367,18 @@ int run_map(Ctx &c, const mh_params &par)
             return 0;
         };
         const int64_t units = c.reads.paired ? n / 2 : n;
+        PairArgs pa{c.reads, c.len_tab, M.slot, M.n_cand, M.yf, M.pool, M.rec, M.ref_stats,
+                    M.n_refs, par.mode == MH_LOCAL, par.maxins, c.reads.paired};
+        int64_t pblocks = (units + 255) / 256;
+        if (pblocks > 1 << 16) pblocks = 1 << 16;
+        if (pblocks < 1) pblocks = 1;
         for (int attempt = 0; attempt < 2; ++attempt) {
             // counters: [0] work items, [2] pool overflow, [3] fast path,
-            // [4] rescue work items; pool_used: CIGAR words claimed
+            // [4] rescue work items; pool_used: CIGAR words claimed.  The
+            // pairing runs before the overflow check (it reads the slots,
+            // not the pool; a retry starts the tallies again), so a pass
+            // synchronises once.
+            hipLaunchKernelGGL(k_init_stats, dim3(64), dim3(256), 0, s, M.ref_stats, M.n_refs);
             MH_HIP(hipMemsetAsync(M.counters, 0, sizeof(int32_t) * 8, s));
             MH_HIP(hipMemsetAsync(M.pool_used, 0, sizeof(unsigned long long), s));
             if (int st = launch_seed()) return st;
@@ -2378,6 +2394,11 @@ int run_map(Ctx &c, const mh_params &par)
                 MH_HIP(hipGetLastError());
                 if (int st = launch_dp(M.rwork, M.counters + 4, M.counters + 6, units, "k_dp_rescue")) return st;
             }
+            pa.pool = M.pool;
+            const int pp = prof_begin(c, "k_pair");
+            hipLaunchKernelGGL(k_pair, dim3((unsigned)pblocks), dim3(256), 0, s, pa);
+            prof_end(c, pp);
+            MH_HIP(hipGetLastError());
             int32_t ctr[5];
             unsigned long long used = 0;
             MH_HIP(hipMemcpyAsync(ctr, M.counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
@@ -2400,15 +2421,6 @@ int run_map(Ctx &c, const mh_params &par)
             MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * grown));
             M.pool_cap = grown;
         }
-        PairArgs pa{c.reads, c.len_tab, M.slot, M.n_cand, M.yf, M.pool, M.rec, M.ref_stats,
-                    M.n_refs, par.mode == MH_LOCAL, par.maxins, c.reads.paired};
-        int64_t pblocks = (units + 255) / 256;
-        if (pblocks > 1 << 16) pblocks = 1 << 16;
-        if (pblocks < 1) pblocks = 1;
-        const int pp = prof_begin(c, "k_pair");
-        hipLaunchKernelGGL(k_pair, dim3((unsigned)pblocks), dim3(256), 0, s, pa);
-        prof_end(c, pp);
-        MH_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(k_fix_first, dim3(8), dim3(256), 0, s, M.ref_stats, M.n_refs);
     MH_HIP(hipGetLastError());
