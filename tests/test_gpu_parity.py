@@ -109,6 +109,44 @@ def test_mate_rescue_vs_oracle(ctx, mode):
     assert stats[4] >= rescued, stats       # rescue extensions (some fail the DP)
 
 
+@pytest.mark.parametrize('mode', [oracle.E2E, oracle.LOCAL])
+def test_mate_rescue_ties_and_ambiguous_bases(ctx, mode):
+    """The rescue window search counts every diagonal over its first 64 read
+    bases and only finishes the ones that can still reach the best count
+    (k_rescue, exact): a reference of tandem repeats (many diagonals tie or
+    come within a few matches of the maximum), mates with N bases and N
+    bases in the window (the masked path), mates shorter than 64 bases (no
+    bases left after the first words) and random mates (nothing pruned)."""
+    rng = np.random.default_rng(44)
+    unit = ''.join(rng.choice(list('ACGT'), size=37))
+    rep = ''.join(unit if i % 3 else unit[:-1] + 'A' for i in range(60))   # ~2.2 kb of near-repeats
+    ref = POL[:1500] + rep + POL[1500:2600].replace('G', 'N', 3)
+    comp = str.maketrans('ACGTN', 'TGCAN')
+    seqs, quals, names = [], [], []
+
+    def pair(a_st, b_st, lb, tweak):
+        a = ref[a_st:a_st + 251]
+        b = tweak(_unseedable(ref[b_st:b_st + lb], rng))
+        seqs.extend([a, b.translate(comp)[::-1]])
+        quals.extend(['I' * 251, ''.join(chr(33 + int(q)) for q in rng.integers(2, 41, size=lb))])
+        names.extend(['@p%d 1:N:0:1' % len(names), '@p%d 2:N:0:1' % len(names)])
+
+    for k in range(60):
+        st = 1500 + int(rng.integers(0, 1500))
+        pair(st, st + int(rng.integers(100, 700)), 251, lambda s: s)               # repeats: near ties
+        pair(st, st + int(rng.integers(100, 700)), 251,
+             lambda s: s[:40] + 'N' + s[41:120] + 'NN' + s[122:])                 # N in the mate
+        pair(st, st + 300, int(rng.integers(20, 64)), lambda s: s)                 # < 64 bases
+    for k in range(20):
+        st = 2800 + int(rng.integers(0, 700))                                      # N in the window
+        pair(st, st + int(rng.integers(100, 500)), 251, lambda s: s)
+        pair(st, st + 200, 251, lambda s: ''.join(rng.choice(list('ACGT'), size=len(s))))
+    want = _oracle_alns([ref], mode, seqs, quals, True)
+    gpu = _gpu_alns(ctx, ['rep'], [ref], mode, seqs, quals, True)
+    _assert_same(gpu, want, seqs)
+    assert ctx.map_stats()[4] > 100
+
+
 def test_map_all_seeds_e2e_vs_oracle(ctx):
     """prelim_map's pass: every seed of projects.json, reads from 3 HIV genes."""
     genomes = {k: SEEDS[k] for k in ('HIV1B-pol-seed', 'HIV1B-env-seed', 'HIV1B-gag-seed')}
