@@ -187,6 +187,51 @@ __device__ __forceinline__ uint32_t read_code(const DevReads &R, int64_t off, in
     return (R.seq2[g >> 4] >> (2 * (g & 15))) & 3;
 }
 
+// Word w (bases 16w .. 16w+15) of read (off, m) on strand s, taken from the
+// packed words: code = the 2-bit codes (0 where ambiguous or past the read),
+// nmk = 1 in the low bit of every such base's pair.  The reverse complement
+// reverses 16 pairs of the forward bases m-16w-16 .. m-16w-1 (a funnel of two
+// words; indices before the read's start only feed bases past its end).
+__device__ __forceinline__ void read_word2(const DevReads &R, int64_t off, int m, int s, int w,
+                                           uint32_t &code, uint32_t &nmk)
+{
+    const int nv = m - 16 * w < 16 ? (m - 16 * w > 0 ? m - 16 * w : 0) : 16;   // bases of the read
+    const uint32_t valid = nv >= 16 ? 0xffffffffu : ((1u << (2 * nv)) - 1u);
+    uint32_t c, nb;
+    if (!s) {
+        const int64_t g = off + 16 * w;   // off is a multiple of 32
+        c = R.seq2[g >> 4];
+        nb = (R.nmask[g >> 5] >> (g & 31)) & 0xffffu;
+    } else {
+        const int64_t g = off + m - 16 * w - 16;
+        // word indices clamped into the read (arithmetic shifts: before the
+        // first read g is negative); a clamped word only feeds bits that are
+        // past the read or shifted out
+        const int64_t wlast = (off + m - 1) >> 4, nlast = (off + m - 1) >> 5;
+        const int64_t wl = g >> 4, nl = g >> 5;
+        const int64_t w0 = wl > 0 ? wl : 0, w1 = wl + 1 < wlast ? (wl + 1 > 0 ? wl + 1 : 0) : wlast;
+        const int64_t n0i = nl > 0 ? nl : 0, n1i = nl + 1 < nlast ? (nl + 1 > 0 ? nl + 1 : 0) : nlast;
+        const uint32_t c0 = R.seq2[w0], c1 = R.seq2[w1];
+        const uint32_t n0 = R.nmask[n0i], n1 = R.nmask[n1i];
+        const uint32_t cf = __builtin_amdgcn_alignbit(c1, c0, (uint32_t)(2 * (g & 15)));
+        const uint32_t nf = __builtin_amdgcn_alignbit(n1, n0, (uint32_t)(g & 31));
+        // reverse the 16 pairs (bit reverse, then swap the bits of each pair), complement
+        uint32_t r = __builtin_bitreverse32(cf);
+        r = ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);
+        c = ~r;
+        nb = __builtin_bitreverse32(nf & 0xffffu) >> 16;
+    }
+    // spread the 16 N bits to the low bit of each pair
+    uint32_t sp = nb;
+    sp = (sp | (sp << 8)) & 0x00ff00ffu;
+    sp = (sp | (sp << 4)) & 0x0f0f0f0fu;
+    sp = (sp | (sp << 2)) & 0x33333333u;
+    sp = (sp | (sp << 1)) & 0x55555555u;
+    sp = (sp & valid) | (~valid & 0x55555555u);
+    nmk = sp;
+    code = c & ~(sp * 3u) & valid;
+}
+
 // SL (<= 32) consecutive 2-bit codes starting at absolute base g, base x at
 // bits 2x+1:2x; and the N-mask bits of the same window.
 __device__ __forceinline__ uint64_t window_key(const DevReads &R, int64_t g, int SL)
@@ -1806,18 +1851,11 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
             const int nw = (m + 15) >> 4;
             bool read_n = false;   // an ambiguous base inside the read
             for (int w = lane; w < nw; w += 64) {
-                uint32_t code = 0, nmk = 0;
-                for (int x = 0; x < 16; ++x) {
-                    const int b = 16 * w + x;
-                    uint32_t c = 4;
-                    if (b < m) {
-                        c = read_code(A.R, off, s ? m - 1 - b : b);
-                        if (s && c < 4) c = 3 - c;
-                        read_n |= c > 3;
-                    }
-                    if (c > 3) nmk |= 1u << (2 * x);
-                    else code |= c << (2 * x);
-                }
+                uint32_t code, nmk;
+                read_word2(A.R, off, m, s, w, code, nmk);
+                const int nv = m - 16 * w < 16 ? m - 16 * w : 16;
+                const uint32_t valid = nv >= 16 ? 0xffffffffu : ((1u << (2 * nv)) - 1u);
+                read_n |= (nmk & valid) != 0;
                 rdw[w] = code;
                 rdn[w] = nmk;
             }
