@@ -306,16 +306,23 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     ix.total = (int64_t)codes.size();
     ix.hmask = cap - 1;
     codes.resize(codes.size() + 64, 4);
-    // one blob: codes, ref_off, ref_len, hkey, hstart, hcount, hits (256-B
-    // aligned parts), staged on the host and uploaded with one copy
+    // packed copies for word-wise window reads (k_rescue), with the padding
+    std::vector<uint32_t> code2((codes.size() + 15) / 16 + 2, 0), ncode((codes.size() + 31) / 32 + 2, 0);
+    for (size_t j = 0; j < codes.size(); ++j) {
+        if (codes[j] > 3) ncode[j >> 5] |= 1u << (j & 31);
+        else code2[j >> 4] |= (uint32_t)codes[j] << (2 * (j & 15));
+    }
+    // one blob: codes, ref_off, ref_len, hkey, hstart, hcount, hits, code2,
+    // ncode (256-B aligned parts), staged on the host and uploaded with one copy
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t sz[7] = {codes.size(), sizeof(int64_t) * (size_t)n_refs, sizeof(int32_t) * (size_t)n_refs,
+    const size_t sz[9] = {codes.size(), sizeof(int64_t) * (size_t)n_refs, sizeof(int32_t) * (size_t)n_refs,
                           sizeof(uint64_t) * cap, sizeof(uint32_t) * cap, sizeof(uint32_t) * cap,
-                          sizeof(int2) * hits.size()};
-    const void *src[7] = {codes.data(), ref_off.data(), ref_len.data(), hkey.data(), hstart.data(),
-                          hcount.data(), hits.data()};
-    size_t at[7], total = 0;
-    for (int x = 0; x < 7; ++x) { at[x] = total; total += al(sz[x]); }
+                          sizeof(int2) * hits.size(), sizeof(uint32_t) * code2.size(),
+                          sizeof(uint32_t) * ncode.size()};
+    const void *src[9] = {codes.data(), ref_off.data(), ref_len.data(), hkey.data(), hstart.data(),
+                          hcount.data(), hits.data(), code2.data(), ncode.data()};
+    size_t at[9], total = 0;
+    for (int x = 0; x < 9; ++x) { at[x] = total; total += al(sz[x]); }
     if ((int64_t)total > ix.cap_blob) {   // (re)allocate only when it does not fit
         hipFree(ix.blob);
         ix.blob = nullptr;
@@ -324,7 +331,7 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
         ix.cap_blob = (int64_t)total;
     }
     std::vector<uint8_t> stage(total);
-    for (int x = 0; x < 7; ++x) if (sz[x]) std::memcpy(stage.data() + at[x], src[x], sz[x]);
+    for (int x = 0; x < 9; ++x) if (sz[x]) std::memcpy(stage.data() + at[x], src[x], sz[x]);
     uint8_t *d = (uint8_t *)ix.blob;
     ix.codes = d + at[0];
     ix.ref_off = (int64_t *)(d + at[1]);
@@ -333,6 +340,8 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     ix.hstart = (uint32_t *)(d + at[4]);
     ix.hcount = (uint32_t *)(d + at[5]);
     ix.hits = (int2 *)(d + at[6]);
+    ix.code2 = (uint32_t *)(d + at[7]);
+    ix.ncode = (uint32_t *)(d + at[8]);
     // callers synchronise the context stream first (mh_index_build)
     MH_HIP(hipMemcpy(ix.blob, stage.data(), total, hipMemcpyHostToDevice));
     return 0;

@@ -59,6 +59,8 @@ struct DevIndex {
     int seedlen = 0;
     int64_t total = 0;
     uint8_t *codes = nullptr;      // 0..3, 4 = ambiguous; refs back to back
+    uint32_t *code2 = nullptr;     // the same packed: 16 bases per word (0 where ambiguous)
+    uint32_t *ncode = nullptr;     // 1 bit per base: ambiguous
     int64_t *ref_off = nullptr;
     int32_t *ref_len = nullptr;
     uint64_t *hkey = nullptr;      // open addressing, EMPTY = ~0

@@ -1867,17 +1867,26 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
                 // reference bases d0 .. d0 + nd + m (+ one word), N past the window
                 const int nrw = (nd + m + 15) / 16 + 1;
                 bool win_n = false;   // an ambiguous reference base inside the window
+#pragma unroll 1
                 for (int w = lane; w < nrw; w += 64) {
-                    uint32_t code = 0, nmk = 0;
-                    for (int x = 0; x < 16; ++x) {
-                        const int64_t j = (int64_t)d0 + 16 * w + x;
-                        const uint32_t c = j < hi ? A.I.codes[gref + j] : 4u;
-                        win_n |= j < hi && c > 3;
-                        if (c > 3) nmk |= 1u << (2 * x);
-                        else code |= c << (2 * x);
-                    }
-                    rfw[w] = code;
-                    rfn[w] = nmk;
+                    // 16 reference bases from the packed copies (a funnel shift of
+                    // two words each); bases from hi on count as ambiguous
+                    const int64_t g = gref + d0 + 16 * w;
+                    const uint32_t cf = __builtin_amdgcn_alignbit(A.I.code2[(g >> 4) + 1], A.I.code2[g >> 4],
+                                                                  (uint32_t)(2 * (g & 15)));
+                    const uint32_t nf = __builtin_amdgcn_alignbit(A.I.ncode[(g >> 5) + 1], A.I.ncode[g >> 5],
+                                                                  (uint32_t)(g & 31)) & 0xffffu;
+                    const int64_t nin = hi - (d0 + 16 * (int64_t)w);
+                    const uint32_t valid = nin >= 16 ? 0xffffffffu : (nin > 0 ? (1u << (2 * nin)) - 1u : 0u);
+                    uint32_t sp = nf;
+                    sp = (sp | (sp << 8)) & 0x00ff00ffu;
+                    sp = (sp | (sp << 4)) & 0x0f0f0f0fu;
+                    sp = (sp | (sp << 2)) & 0x33333333u;
+                    sp = (sp | (sp << 1)) & 0x55555555u;
+                    win_n |= (sp & valid) != 0;
+                    sp = (sp & valid) | (~valid & 0x55555555u);
+                    rfw[w] = cf & ~(sp * 3u) & valid;
+                    rfn[w] = sp;
                 }
                 wave_sync();
                 if (!any_read_n && __builtin_amdgcn_ballot_w64(win_n) == 0) {
