@@ -312,17 +312,23 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
         if (codes[j] > 3) ncode[j >> 5] |= 1u << (j & 31);
         else code2[j >> 4] |= (uint32_t)codes[j] << (2 * (j & 15));
     }
+    std::vector<uint32_t> cplane(2 * ((codes.size() + 31) / 32 + 2), 0);
+    for (size_t j = 0; j < codes.size(); ++j) {
+        const uint32_t c = codes[j] > 3 ? 0u : codes[j];
+        cplane[2 * (j >> 5)] |= (c & 1u) << (j & 31);
+        cplane[2 * (j >> 5) + 1] |= (c >> 1) << (j & 31);
+    }
     // one blob: codes, ref_off, ref_len, hkey, hstart, hcount, hits, code2,
-    // ncode (256-B aligned parts), staged on the host and uploaded with one copy
+    // ncode, cplane (256-B aligned parts), staged on the host and uploaded with one copy
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t sz[9] = {codes.size(), sizeof(int64_t) * (size_t)n_refs, sizeof(int32_t) * (size_t)n_refs,
+    const size_t sz[10] = {codes.size(), sizeof(int64_t) * (size_t)n_refs, sizeof(int32_t) * (size_t)n_refs,
                           sizeof(uint64_t) * cap, sizeof(uint32_t) * cap, sizeof(uint32_t) * cap,
                           sizeof(int2) * hits.size(), sizeof(uint32_t) * code2.size(),
-                          sizeof(uint32_t) * ncode.size()};
-    const void *src[9] = {codes.data(), ref_off.data(), ref_len.data(), hkey.data(), hstart.data(),
-                          hcount.data(), hits.data(), code2.data(), ncode.data()};
-    size_t at[9], total = 0;
-    for (int x = 0; x < 9; ++x) { at[x] = total; total += al(sz[x]); }
+                          sizeof(uint32_t) * ncode.size(), sizeof(uint32_t) * cplane.size()};
+    const void *src[10] = {codes.data(), ref_off.data(), ref_len.data(), hkey.data(), hstart.data(),
+                           hcount.data(), hits.data(), code2.data(), ncode.data(), cplane.data()};
+    size_t at[10], total = 0;
+    for (int x = 0; x < 10; ++x) { at[x] = total; total += al(sz[x]); }
     if ((int64_t)total > ix.cap_blob) {   // (re)allocate only when it does not fit
         hipFree(ix.blob);
         ix.blob = nullptr;
@@ -331,7 +337,7 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
         ix.cap_blob = (int64_t)total;
     }
     std::vector<uint8_t> stage(total);
-    for (int x = 0; x < 9; ++x) if (sz[x]) std::memcpy(stage.data() + at[x], src[x], sz[x]);
+    for (int x = 0; x < 10; ++x) if (sz[x]) std::memcpy(stage.data() + at[x], src[x], sz[x]);
     uint8_t *d = (uint8_t *)ix.blob;
     ix.codes = d + at[0];
     ix.ref_off = (int64_t *)(d + at[1]);
@@ -342,6 +348,7 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     ix.hits = (int2 *)(d + at[6]);
     ix.code2 = (uint32_t *)(d + at[7]);
     ix.ncode = (uint32_t *)(d + at[8]);
+    ix.cplane = (uint32_t *)(d + at[9]);
     // callers synchronise the context stream first (mh_index_build)
     MH_HIP(hipMemcpy(ix.blob, stage.data(), total, hipMemcpyHostToDevice));
     return 0;

@@ -61,6 +61,7 @@ struct DevIndex {
     uint8_t *codes = nullptr;      // 0..3, 4 = ambiguous; refs back to back
     uint32_t *code2 = nullptr;     // the same packed: 16 bases per word (0 where ambiguous)
     uint32_t *ncode = nullptr;     // 1 bit per base: ambiguous
+    uint32_t *cplane = nullptr;    // bit planes, 32 bases per word: [2k] low code bits, [2k+1] high
     int64_t *ref_off = nullptr;
     int32_t *ref_len = nullptr;
     uint64_t *hkey = nullptr;      // open addressing, EMPTY = ~0

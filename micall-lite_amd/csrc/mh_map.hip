@@ -1785,6 +1785,17 @@ struct RescueArgs {
 // diagonals per staged reference window (the -X window of C2 has ~950)
 constexpr int RESCUE_CHUNK = 1024;
 constexpr int RESCUE_WORDS = (RESCUE_CHUNK + MAXLEN) / 16 + 4;   // 2-bit words of a staged window
+constexpr int RESCUE_W32 = (RESCUE_CHUNK + MAXLEN) / 32 + 4;     // bit-plane words of a staged window
+
+// the 16 low bits of each bit pair of x, packed into 16 bits
+__device__ __forceinline__ uint32_t compact16(uint32_t x)
+{
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0f0f0f0fu;
+    x = (x | (x >> 4)) & 0x00ff00ffu;
+    return (x | (x >> 8)) & 0x0000ffffu;
+}
 
 __device__ __forceinline__ int best_slot(const Slot *sl, int n)
 {
@@ -1802,11 +1813,16 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
     // "N" masks (01 in the base's bit pair)
     __shared__ uint32_t sh_rd[4][2][MAXLEN / 16 + 1];
     __shared__ uint32_t sh_rf[4][2][RESCUE_WORDS];
+    // the same as bit planes (32 bases a word: low code bits, high code bits)
+    // for the count without ambiguous bases
+    __shared__ uint2 sh_rp[4][MAXLEN / 32 + 1];
+    __shared__ uint2 sh_pl[4][RESCUE_W32];
     __shared__ int32_t sh_items[4][64];
     const int lane = threadIdx.x & 63;
     const int wv = wave_uniform(threadIdx.x >> 6);
     uint32_t *rdw = sh_rd[wv][0], *rdn = sh_rd[wv][1];
     uint32_t *rfw = sh_rf[wv][0], *rfn = sh_rf[wv][1];
+    uint2 *rp = sh_rp[wv], *pl = sh_pl[wv];
     const int64_t units = A.R.n / 2;
     for (int64_t u0 = ((int64_t)blockIdx.x * 4 + wv) * 64; u0 < units;
          u0 += (int64_t)gridDim.x * 256) {
@@ -1860,13 +1876,70 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
                 rdn[w] = nmk;
             }
             const bool any_read_n = __builtin_amdgcn_ballot_w64(read_n) != 0;
+            wave_sync();
+            // the read's bit planes (bases past m are masked in the count)
+            const int nw32 = (m + 31) >> 5;
+            for (int w = lane; w < nw32; w += 64) {
+                const uint32_t c0 = rdw[2 * w], c1 = rdw[2 * w + 1];
+                rp[w] = make_uint2(compact16(c0) | (compact16(c1) << 16),
+                                   compact16(c0 >> 1) | (compact16(c1 >> 1) << 16));
+            }
+            const int tail = m - 32 * (nw32 - 1);
+            const uint32_t tmask = tail >= 32 ? 0xffffffffu : (1u << tail) - 1u;
             int bestM = -1, bestd = 0;
             const int dlast = (int)(hi - m);
             for (int d0 = (int)lo; d0 <= dlast; d0 += RESCUE_CHUNK) {
                 const int nd = dlast - d0 + 1 < RESCUE_CHUNK ? dlast - d0 + 1 : RESCUE_CHUNK;
+                // the window's bit planes (bases d0 .. d0 + nd + m - 2 are
+                // compared; the ones from hi on are never reached)
+                const int nrw32 = (nd + m + 31) / 32 + 1;
+                const int64_t wend = d0 + nd + m - 1 < hi ? (int64_t)d0 + nd + m - 1 : hi;
+                bool win_n = false;   // an ambiguous reference base among the compared ones
+#pragma unroll 1
+                for (int w = lane; w < nrw32; w += 64) {
+                    const int64_t g = gref + d0 + 32 * w;
+                    const uint32_t *cp = A.I.cplane + 2 * (g >> 5);
+                    const uint32_t sh = (uint32_t)(g & 31);
+                    const uint32_t pl0 = __builtin_amdgcn_alignbit(cp[2], cp[0], sh);
+                    const uint32_t pl1 = __builtin_amdgcn_alignbit(cp[3], cp[1], sh);
+                    const uint32_t nf = __builtin_amdgcn_alignbit(A.I.ncode[(g >> 5) + 1], A.I.ncode[g >> 5], sh);
+                    const int64_t nin = wend - (d0 + 32 * (int64_t)w);
+                    const uint32_t valid = nin >= 32 ? 0xffffffffu : (nin > 0 ? (1u << nin) - 1u : 0u);
+                    win_n |= (nf & valid) != 0;
+                    pl[w] = make_uint2(pl0, pl1);
+                }
+                wave_sync();
+                if (!any_read_n && __builtin_amdgcn_ballot_w64(win_n) == 0) {
+                    // no ambiguous base on either side: mismatches over 32 bases
+                    // per step from the two planes (the window's words aligned to
+                    // the diagonal by a funnel shift, carried over a step); the
+                    // last word masks the read's tail
+                    for (int t = lane; t < nd; t += 64) {
+                        const int w0 = t >> 5;
+                        const uint32_t sh = (uint32_t)(t & 31);
+                        uint2 cur = pl[w0];
+                        int mis = 0;
+                        for (int i = 0; i < nw32 - 1; ++i) {
+                            const uint2 nx = pl[w0 + i + 1], r = rp[i];
+                            const uint32_t x0 = __builtin_amdgcn_alignbit(nx.x, cur.x, sh) ^ r.x;
+                            const uint32_t x1 = __builtin_amdgcn_alignbit(nx.y, cur.y, sh) ^ r.y;
+                            mis += __builtin_popcount(x0 | x1);
+                            cur = nx;
+                        }
+                        {
+                            const uint2 nx = pl[w0 + nw32], r = rp[nw32 - 1];
+                            const uint32_t x0 = __builtin_amdgcn_alignbit(nx.x, cur.x, sh) ^ r.x;
+                            const uint32_t x1 = __builtin_amdgcn_alignbit(nx.y, cur.y, sh) ^ r.y;
+                            mis += __builtin_popcount((x0 | x1) & tmask);
+                        }
+                        const int cnt = m - mis;
+                        if (cnt > bestM) { bestM = cnt; bestd = d0 + t; }
+                    }
+                    wave_sync();
+                    continue;
+                }
                 // reference bases d0 .. d0 + nd + m (+ one word), N past the window
                 const int nrw = (nd + m + 15) / 16 + 1;
-                bool win_n = false;   // an ambiguous reference base inside the window
 #pragma unroll 1
                 for (int w = lane; w < nrw; w += 64) {
                     // 16 reference bases from the packed copies (a funnel shift of
@@ -1883,40 +1956,11 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
                     sp = (sp | (sp << 4)) & 0x0f0f0f0fu;
                     sp = (sp | (sp << 2)) & 0x33333333u;
                     sp = (sp | (sp << 1)) & 0x55555555u;
-                    win_n |= (sp & valid) != 0;
                     sp = (sp & valid) | (~valid & 0x55555555u);
                     rfw[w] = cf & ~(sp * 3u) & valid;
                     rfn[w] = sp;
                 }
                 wave_sync();
-                if (!any_read_n && __builtin_amdgcn_ballot_w64(win_n) == 0) {
-                    // no ambiguous base on either side: words 0 .. nw-2 pair read
-                    // bases < m with window bases < hi and need no N masks (the
-                    // window word of step i + 1 is carried over); the last word
-                    // masks the read's tail
-                    for (int t = lane; t < nd; t += 64) {
-                        const int w0 = t >> 4;
-                        const uint32_t sh = (uint32_t)(2 * (t & 15));
-                        uint32_t lo_w = rfw[w0];
-                        int cnt = 0;
-                        for (int i = 0; i < nw - 1; ++i) {
-                            const uint32_t hi_w = rfw[w0 + i + 1];
-                            const uint32_t x = rdw[i] ^ __builtin_amdgcn_alignbit(hi_w, lo_w, sh);
-                            cnt += __builtin_popcount(~(x | (x >> 1)) & 0x55555555u);
-                            lo_w = hi_w;
-                        }
-                        {
-                            const int i = nw - 1;
-                            const uint32_t v = __builtin_amdgcn_alignbit(rfw[w0 + i + 1], lo_w, sh);
-                            const uint32_t vn = __builtin_amdgcn_alignbit(rfn[w0 + i + 1], rfn[w0 + i], sh);
-                            const uint32_t x = rdw[i] ^ v;
-                            cnt += __builtin_popcount(~(x | (x >> 1) | rdn[i] | vn) & 0x55555555u);
-                        }
-                        if (cnt > bestM) { bestM = cnt; bestd = d0 + t; }
-                    }
-                    wave_sync();
-                    continue;
-                }
                 for (int t = lane; t < nd; t += 64) {
                     // matches on diagonal d0 + t: 16 bases per step, the window
                     // words aligned to the diagonal by a funnel shift

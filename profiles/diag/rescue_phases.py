@@ -42,8 +42,8 @@ def main():
             '        uint64_t todo = __builtin_amdgcn_ballot_w64(need != 0);\n        RPH(0);\n')
     t = sub(t, '            const bool any_read_n = __builtin_amdgcn_ballot_w64(read_n) != 0;\n',
             '            const bool any_read_n = __builtin_amdgcn_ballot_w64(read_n) != 0;\n            RPH(1);\n')
-    t = sub(t, '                    rfn[w] = sp;\n                }\n                wave_sync();\n',
-            '                    rfn[w] = sp;\n                }\n                wave_sync();\n'
+    t = sub(t, '                    pl[w] = make_uint2(pl0, pl1);\n                }\n                wave_sync();\n',
+            '                    pl[w] = make_uint2(pl0, pl1);\n                }\n                wave_sync();\n'
             '                RPH(2);\n')
     t = sub(t, '            const int mmax = wave_max(bestM);\n',
             '            RPH(3);\n            const int mmax = wave_max(bestM);\n')
