@@ -1829,6 +1829,8 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
         const int64_t u = u0 + lane;
         // the mate to rescue and its anchor (the other mate's best slot)
         int need = 0, tgt_mate = 0, a_ref = 0, a_strand = 0, a_pos = 0, a_end = 0;
+        int t_len = 0, r_len = 0;
+        int64_t t_off = 0, r_off = 0;   // the mate's and the reference's (loaded lane-parallel here)
         if (u < units) {
             const int64_t r1 = 2 * u, r2 = r1 + 1;
             const int b1 = best_slot(A.slot + r1 * MAXCAND, A.n_cand[r1]);
@@ -1840,6 +1842,10 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
                     need = 1;
                     tgt_mate = b1 >= 0 ? 1 : 0;
                     a_ref = s.ref; a_strand = s.strand; a_pos = s.pos; a_end = s.end;
+                    t_len = A.R.len[tg];
+                    t_off = A.R.off[tg];
+                    r_len = A.I.ref_len[s.ref];
+                    r_off = A.I.ref_off[s.ref];
                 }
             }
         }
@@ -1853,10 +1859,10 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
             const int ast = __builtin_amdgcn_readlane(a_strand, l);
             const int apos = __builtin_amdgcn_readlane(a_pos, l);
             const int aend = __builtin_amdgcn_readlane(a_end, l);
-            const int m = wave_uniform(A.R.len[tg]);
-            const int64_t off = A.R.off[tg];
-            const int reflen = wave_uniform(A.I.ref_len[ref]);
-            const int64_t gref = A.I.ref_off[ref];
+            const int m = __builtin_amdgcn_readlane(t_len, l);
+            const int64_t off = readlane64(t_off, l);
+            const int reflen = __builtin_amdgcn_readlane(r_len, l);
+            const int64_t gref = readlane64(r_off, l);
             int64_t lo = ast == 0 ? (int64_t)apos : (int64_t)aend - A.maxins;
             int64_t hi = ast == 0 ? (int64_t)apos + A.maxins : (int64_t)aend;
             if (lo < 0) lo = 0;
