@@ -111,12 +111,12 @@ def test_mate_rescue_vs_oracle(ctx, mode):
 
 @pytest.mark.parametrize('mode', [oracle.E2E, oracle.LOCAL])
 def test_mate_rescue_ties_and_ambiguous_bases(ctx, mode):
-    """The rescue window search counts every diagonal over its first 64 read
-    bases and only finishes the ones that can still reach the best count
-    (k_rescue, exact): a reference of tandem repeats (many diagonals tie or
-    come within a few matches of the maximum), mates with N bases and N
-    bases in the window (the masked path), mates shorter than 64 bases (no
-    bases left after the first words) and random mates (nothing pruned)."""
+    """The rescue window search picks the diagonal with the most matches,
+    the leftmost on ties (k_rescue): a reference of tandem repeats (many
+    diagonals tie or come within a few matches of the maximum), mates with N
+    bases and N bases in the window (the 2-bit path with N masks), mates
+    shorter than 64 bases (windows of more than one 1024-diagonal chunk) and
+    random mates."""
     rng = np.random.default_rng(44)
     unit = ''.join(rng.choice(list('ACGT'), size=37))
     rep = ''.join(unit if i % 3 else unit[:-1] + 'A' for i in range(60))   # ~2.2 kb of near-repeats
@@ -145,6 +145,40 @@ def test_mate_rescue_ties_and_ambiguous_bases(ctx, mode):
     gpu = _gpu_alns(ctx, ['rep'], [ref], mode, seqs, quals, True)
     _assert_same(gpu, want, seqs)
     assert ctx.map_stats()[4] > 100
+
+
+@pytest.mark.parametrize('mode', [oracle.E2E, oracle.LOCAL])
+def test_mate_rescue_long_mates(ctx, mode):
+    """Mates of 255-1024 bases rescued next to a 251-base anchor (the -X 1200
+    window still holds them): the bit-plane count's read words run to 32 per
+    diagonal with every tail length around the 32-base word edges, the
+    window's staged words to 65; either mate order, N bases in some mates."""
+    rng = np.random.default_rng(77)
+    ref = POL + SEEDS['HIV1B-env-seed'][:1500]
+    comp = str.maketrans('ACGTN', 'TGCAN')
+    seqs, quals = [], []
+    lens = [255, 256, 257, 288, 300, 383, 480, 511, 512, 513, 600, 700, 767, 800, 900, 1000, 1023, 1024]
+    for k in range(90):
+        lb = lens[k % len(lens)]
+        st = int(rng.integers(0, len(ref) - 1200))
+        off = int(rng.integers(0, 1200 - lb + 1))
+        a = ref[st:st + 251]
+        b = _unseedable(ref[st + off:st + off + lb], rng, every=int(rng.integers(9, 14)))
+        if k % 4 == 1:
+            b = b[:100] + 'N' + b[101:]
+        b = b.translate(comp)[::-1]
+        qa = 'I' * 251
+        qb = ''.join(chr(33 + int(q)) for q in rng.integers(2, 41, size=lb))
+        if k % 2:
+            seqs += [b, a]
+            quals += [qb, qa]
+        else:
+            seqs += [a, b]
+            quals += [qa, qb]
+    want = _oracle_alns([ref], mode, seqs, quals, True)
+    gpu = _gpu_alns(ctx, ['polenv'], [ref], mode, seqs, quals, True)
+    _assert_same(gpu, want, seqs)
+    assert ctx.map_stats()[4] >= 60
 
 
 def test_map_all_seeds_e2e_vs_oracle(ctx):
