@@ -408,66 +408,115 @@ __device__ int cluster_lanes(const SeedArgs &A, int64_t r, int lane, uint64_t v,
     return __builtin_amdgcn_readfirstlane(nc);
 }
 
-// Seeds, hit sort and candidate clustering of read r (length m, base offset
-// off) by one wave; writes the candidates, n_cand and yf, returns the
-// candidate count (wave-uniform).
-__device__ int seed_read(const SeedArgs &A, int64_t r, int m, int64_t off, int lane, uint64_t *hits,
-                         Cand *best)
+// The raw words a read's seeding starts from, loaded one read ahead: lane
+// (strand s = lane >> 5, seed t = lane & 31) holds the three 2-bit words and
+// two N-mask words under its seed window, and lane w < 32 the read's N-mask
+// word w for the N count.  k_seed issues the next read's loads right after
+// the current read's first hash probe, so they land while the probe chain
+// waits (loads return in order: issued after the probe, they hold no wait
+// of its back).
+struct SeedPre {
+    uint32_t s0, s1, s2, n0, n1, nw;
+    int m, iv, ns;
+    int64_t off;
+};
+
+__device__ __forceinline__ SeedPre seed_prefetch(const SeedArgs &A, int m, int64_t off, int lane)
 {
     const int SL = A.I.seedlen;
+    SeedPre P;
+    P.m = m;
+    P.off = off;
+    P.iv = m >= SL ? ldc(&A.len_tab[m]) : 1;
+    int ns = m >= SL ? 1 + (m - SL) / P.iv : 0;
+    P.ns = ns > MAXSEEDS ? MAXSEEDS : ns;
+    // unconditional loads (lanes without a window read the read's first
+    // words): a load under a branch ends in a copy at the join, and the copy
+    // waits for it
+    const int s = lane >> 5, t = lane & 31;
+    const int o = t * P.iv;
+    const int64_t g = t < P.ns ? off + (s == 0 ? o : m - o - SL) : off;
+    const uint32_t *sq = A.R.seq2 + (g >> 4), *nq = A.R.nmask + (g >> 5);
+    P.s0 = sq[0]; P.s1 = sq[1]; P.s2 = sq[2];
+    P.n0 = nq[0]; P.n1 = nq[1];
+    P.nw = A.R.nmask[(off >> 5) + (lane * 32 < m ? lane : 0)];   // m <= MAXLEN: one word per lane
+    return P;
+}
+
+// Seeds, hit sort and candidate clustering of read r (its words in P) by one
+// wave; writes the candidates, n_cand and yf, returns the candidate count
+// (wave-uniform).  Q receives the next read's words (m_next, off_next).
+__device__ int seed_read(const SeedArgs &A, int64_t r, const SeedPre &P, int lane, uint64_t *hits,
+                         Cand *best, SeedPre &Q, int m_next, int64_t off_next)
+{
+    const int SL = A.I.seedlen;
+    const int m = P.m, iv = P.iv, ns = P.ns;
+    bool fetched = false;
+    auto fetch_next = [&]() {
+        if (!fetched) Q = seed_prefetch(A, m_next, off_next, lane);
+        fetched = true;
+    };
     if (m == 0) {
+        fetch_next();
         if (lane == 0) { A.n_cand[r] = 0; A.yf[r] = 2; }
         return 0;
     }
-    // the seed windows' loads are issued with the N count's (one round trip)
-    const int iv = m >= SL ? A.len_tab[m] : 1;
-    int ns = m >= SL ? 1 + (m - SL) / iv : 0;
-    if (ns > MAXSEEDS) ns = MAXSEEDS;
     const int s = lane >> 5, t = lane & 31;
     const int o = t * iv;
     uint32_t wnm = 1;
     uint64_t wkey = 0;
     if (t < ns) {
-        const int p = s == 0 ? o : m - o - SL;
-        wnm = window_nmask(A.R, off + p, SL);
-        wkey = window_key(A.R, off + p, SL);
+        const int64_t g = P.off + (s == 0 ? o : m - o - SL);
+        const int sh2 = 2 * (int)(g & 15), sh1 = (int)(g & 31);
+        const uint64_t lo = (uint64_t)P.s0 | ((uint64_t)P.s1 << 32);
+        const uint64_t k = sh2 ? (lo >> sh2) | ((uint64_t)P.s2 << (64 - sh2)) : lo;
+        wkey = SL >= 32 ? k : (k & ((1ull << (2 * SL)) - 1));
+        const uint64_t v = ((uint64_t)P.n0 | ((uint64_t)P.n1 << 32)) >> sh1;
+        wnm = (uint32_t)(v & ((1ull << SL) - 1));
     }
     int nn = 0;
-    for (int w = lane; w * 32 < m; w += 64) {
-        uint32_t bits = A.R.nmask[(off >> 5) + w];
-        const int rem = m - w * 32;
+    if (lane * 32 < m) {
+        uint32_t bits = P.nw;
+        const int rem = m - lane * 32;
         if (rem < 32) bits &= (1u << rem) - 1;
-        nn += __popc(bits);
+        nn = __popc(bits);
     }
     nn = wave_sum(nn);
-    if (nn > A.len_tab[2 * (MAXLEN + 1) + m]) {
+    if (nn > ldc(&A.len_tab[2 * (MAXLEN + 1) + m])) {
+        fetch_next();
         if (lane == 0) { A.n_cand[r] = 0; A.yf[r] = 1; }
         return 0;
     }
     if (lane == 0) A.yf[r] = 0;
     if (m < SL) {
+        fetch_next();
         if (lane == 0) A.n_cand[r] = 0;
         return 0;
     }
     int cnt = 0;
     uint32_t start = 0;
-    if (t < ns) {
-        if (wnm == 0) {
-            uint64_t key = wkey;
-            if (s) key = revcomp_key(key, SL);
-            uint64_t h = hash_key(key) & A.I.hmask;
-            for (;;) {
-                const uint64_t k = A.I.hkey[h];
-                if (k == HEMPTY) break;
-                if (k == key) {
-                    start = A.I.hstart[h];
-                    cnt = (int)A.I.hcount[h];
-                    break;
-                }
-                h = (h + 1) & A.I.hmask;
+    // the first probe of every seed, then the next read's loads, then the
+    // rest of the probe chains
+    const bool probe = t < ns && wnm == 0;
+    uint64_t key = 0, h = 0, k = HEMPTY;
+    if (probe) {
+        key = s ? revcomp_key(wkey, SL) : wkey;
+        h = hash_key(key) & A.I.hmask;
+        k = A.I.hkey[h];
+    }
+    fetch_next();
+    if (probe) {
+        for (;;) {
+            if (k == HEMPTY) break;
+            if (k == key) {
+                start = A.I.hstart[h];
+                cnt = (int)A.I.hcount[h];
+                break;
             }
-            if (cnt > MAXHITS_SEED) cnt = 0;
+            h = (h + 1) & A.I.hmask;
+            k = A.I.hkey[h];
         }
+        if (cnt > MAXHITS_SEED) cnt = 0;
     }
     const int pre = wave_excl_scan(cnt, lane);
     int total = wave_sum(cnt);
@@ -572,11 +621,17 @@ __global__ __launch_bounds__(256, SEED_WAVES_PER_SIMD) void k_seed(SeedArgs A)
             my_m = A.R.len[r0 + lane];
             my_off = A.R.off[r0 + lane];
         }
+        SeedPre P = seed_prefetch(A, __builtin_amdgcn_readlane(my_m, 0),
+                                  (int64_t)readlane64((uint64_t)my_off, 0), lane);
         for (int64_t r = r0; r < r1; ++r) {
             const int l = (int)(r - r0);
-            const int m = __builtin_amdgcn_readlane(my_m, l);
-            const int64_t off = (int64_t)readlane64((uint64_t)my_off, l);
-            const int nc = seed_read(A, r, m, off, lane, sh_hits[wv], sh_best[wv]);
+            // the next read of the chunk (past its end: an empty read, no loads)
+            const int ln = l + 1 < (int)(r1 - r0) ? l + 1 : 0;
+            const int mn = l + 1 < (int)(r1 - r0) ? __builtin_amdgcn_readlane(my_m, ln) : 0;
+            const int64_t offn = (int64_t)readlane64((uint64_t)my_off, ln);
+            SeedPre Q;
+            const int nc = seed_read(A, r, P, lane, sh_hits[wv], sh_best[wv], Q, mn, offn);
+            P = Q;
             if (lane < nc) sh_work[wv][n_work + lane] = (int32_t)(r * MAXCAND + lane);
             n_work += nc;
         }
