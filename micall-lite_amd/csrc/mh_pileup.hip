@@ -773,7 +773,8 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
                 }
             }
             if (base) {
-                const int code = mc == 'A' ? 0 : mc == 'C' ? 1 : mc == 'G' ? 2 : 3;
+                // A C G T (0x41 0x43 0x47 0x54) -> 0 1 2 3 without a branch
+                const int code = (((int)mc >> 1) ^ ((int)mc >> 2)) & 3;
                 // u16 halves: a block counts < 65536 units (pile_geometry)
                 if (wo >= 0 && P <= wl) atomicAdd(&win[wo + (code >> 1) * wl + (P - 1)], 1u << (16 * (code & 1)));
                 else atomicAdd(&A.dense[cell * 4 + code], 1);
