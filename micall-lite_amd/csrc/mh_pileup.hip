@@ -157,6 +157,13 @@ __device__ __forceinline__ RowV unpack_row(const PileArgs &A, int pk, int h)
     return v;
 }
 
+// base code 0..4 -> 'A' 'C' 'G' 'T' 'N' from a register constant (a string
+// literal indexed per lane is a global load)
+__device__ __forceinline__ char base_char(uint32_t code)
+{
+    return (char)((0x4E54474341ull >> (8 * code)) & 0xffu);
+}
+
 __device__ __forceinline__ void sam_base_at(const DevReads &R, int rev, int m, int64_t roff, int x,
                                             char &c, char &q)
 {
@@ -164,7 +171,7 @@ __device__ __forceinline__ void sam_base_at(const DevReads &R, int rev, int m, i
     const int64_t g = roff + b;
     uint32_t code = ((R.nmask[g >> 5] >> (g & 31)) & 1) ? 4 : (R.seq2[g >> 4] >> (2 * (g & 15))) & 3;
     if (rev && code < 4) code = 3 - code;
-    c = "ACGTN"[code];
+    c = base_char(code);
     q = (char)R.qual[g];
 }
 
@@ -174,7 +181,7 @@ __device__ __forceinline__ void sam_base(const DevReads &R, const RowV &v, int x
     const int64_t g = v.roff + b;
     uint32_t code = ((R.nmask[g >> 5] >> (g & 31)) & 1) ? 4 : (R.seq2[g >> 4] >> (2 * (g & 15))) & 3;
     if (v.rev && code < 4) code = 3 - code;
-    c = "ACGTN"[code];
+    c = base_char(code);
     q = (char)R.qual[g];
 }
 
@@ -492,7 +499,7 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
                         const int64_t g = mk.roff + x;
                         uint32_t code = ((nw[k][ch] >> (g & 31)) & 1) ? 4u : (sw[k][ch] >> (2 * (g & 15))) & 3u;
                         if (mk.rev && code < 4) code = 3 - code;
-                        c = "ACGTN"[code];
+                        c = base_char(code);
                         q = (char)qw[k][ch];
                     }
                     L.c(k)[t] = c;
@@ -741,18 +748,23 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
         };
         // update_counts of one merged character
         auto count = [&](int i, char mc) {
+            // bitwise, not short-circuit: the tests stay selects, not branches
             const int P = i - shift + 1;
-            const bool live = mc != 0 && mc != 'n';
-            if (live && P > A.cap) err = 1;
-            const bool ok = live && P <= A.cap;
-            mxp = ok && P > mxp ? P : mxp;
+            const bool live = (mc != 0) & (mc != 'n');
+            err |= (int)(live & (P > A.cap));
+            const bool ok = live & (P <= A.cap);
+            mxp = (ok & (P > mxp)) ? P : mxp;
             const int64_t cell = (int64_t)ref * A.cap + (P - 1);
             const bool isN = mc == 'N', isD = mc == '-';
-            if (ok && isN) A.nflag[cell] = 1;
-            if (ok && isD) A.dflag[cell] = 1;
-            bool base = ok && !isN && !isD;
+            if (ok & isN) A.nflag[cell] = 1;
+            if (ok & isD) A.dflag[cell] = 1;
+            bool base = ok & !isN & !isD;
             if (n_ins > 0) {
-                int hit = P == ik0 ? 0 : P == ik1 ? 1 : P == ik2 ? 2 : P == ik3 ? 3 : -1;
+                int hit = -1;   // keys are distinct and >= 1 (-1: no key)
+                hit = P == ik3 ? 3 : hit;
+                hit = P == ik2 ? 2 : hit;
+                hit = P == ik1 ? 1 : hit;
+                hit = P == ik0 ? 0 : hit;
                 for (int z = 4; z < n_ins; ++z)
                     if (I.key[z] == P) hit = z;
                 if (base && hit >= 0 && I.len[hit] > 0 && I.len[hit] % 3 == 0) {
