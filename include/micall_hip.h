@@ -110,6 +110,43 @@ int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64
 int mh_reads_load_fastq_part(mh_ctx *ctx, const char *path1, const char *path2, int part, int parts,
                              int64_t *n_reads, int64_t *first_unit);
 int mh_reads_count(mh_ctx *ctx, int64_t *n_reads, int *paired);
+
+/* ---- sharded FASTQ ingest (host only; replaces each rank's decode of the
+ * whole file: the reference streams the FASTQ once per pass,
+ * prelim_map.py:114-134 / censor_fastq.py:58-96) ---------------------------
+ * mh_fastq_open_part decodes part `part` of `parts` of a FASTQ file (path,
+ * or an open descriptor when path is NULL): with parts > 1 the gzip members
+ * starting in the part's byte range (mode 1), the byte range of a plain file
+ * (mode 2); the whole file otherwise (mode 0; also with parts == 1).
+ * info[10]: mode, first and end file offset read, decoded bytes, newlines in
+ * them, ends with '\n', starts with '\n', file bytes decoded, file size,
+ * wall time (microseconds). */
+typedef struct mh_fastq mh_fastq;
+int mh_fastq_open_part(const char *path, int fd, int part, int parts, mh_fastq **out, int64_t *info);
+/* Record starts of the held text, a record being four lines: line0 = lines
+ * of the file before its first byte, starts_line = 1 if that byte starts a
+ * line.  out[5]: offset of the first record start (the size if none),
+ * record starts, that start's line number in the file (-1 if none), 1 if a
+ * blank line sits where a record starts (the ingest's parser would skip it),
+ * 1 if the text ends in an unterminated record-start line that is only a
+ * '\r'. */
+int mh_fastq_frame(mh_fastq *fq, int64_t line0, int starts_line, int64_t *out5);
+/* byte offset of framed record k (k = the record count: the text's size) */
+int mh_fastq_record_offset(mh_fastq *fq, int64_t k, int64_t *off);
+/* the held text becomes front + text[lo, hi) + back (framing is dropped) */
+int mh_fastq_splice(mh_fastq *fq, int64_t lo, int64_t hi, const char *front, int64_t flen,
+                    const char *back, int64_t blen);
+/* the held text (valid until the handle changes or is closed) */
+int mh_fastq_view(mh_fastq *fq, const char **data, int64_t *len);
+int mh_fastq_close(mh_fastq *fq);
+/* Load the reads of staged FASTQ text: units [range[0], range[1]) of fq1's
+ * records and [range[2], range[3]) of fq2's (-1, -1: all of them; the two
+ * counts must agree), mates interleaved when fq2 is given.  The records are
+ * parsed as mh_reads_load_fastq parses a file; the texts are moved into the
+ * context (the handles are left empty).  fastq_lines1 is the newline count
+ * of the whole FASTQ 1 (mh_reads_fastq_lines, raw_count). */
+int mh_reads_load_staged(mh_ctx *ctx, mh_fastq *fq1, mh_fastq *fq2, const int64_t *range4,
+                         int64_t fastq_lines1, int64_t *n_reads);
 /* newlines in FASTQ 1 of the last mh_reads_load_fastq (the `gunzip -c | wc
  * -l` of LineCounter, externals.py:206-231; raw_count = lines / 2). */
 int mh_reads_fastq_lines(mh_ctx *ctx, int64_t *lines1);
@@ -144,9 +181,14 @@ int mh_map_stats(mh_ctx *ctx, int64_t *out5);
  * sizes them again. */
 int mh_test_set_capacities(mh_ctx *ctx, int64_t cigar_pool_words, int64_t pileup_events,
                            int64_t pileup_event_bytes, int64_t token_bytes);
-/* Retries taken so far by those paths: out3[0] CIGAR pool (a mapping pass
- * run again from k_seed), out3[1] pileup events, out3[2] token bytes. */
-int mh_retry_counts(mh_ctx *ctx, int64_t *out3);
+/* Retries taken so far by those paths: out4[0] CIGAR pool (a mapping pass
+ * run again from k_seed), out4[1] pileup events, out4[2] token bytes,
+ * out4[3] Gotoh batches run again after a strip's wait timed out. */
+int mh_retry_counts(mh_ctx *ctx, int64_t *out4);
+/* Test entry point: k_gotoh's first attempt of every later batch gives up a
+ * neighbour wait after `ticks` of the 100 MHz real-time clock (0: the
+ * default 20 s), so the timeout-and-retry path of mh_gotoh_align_batch runs. */
+int mh_test_set_gotoh_wait(mh_ctx *ctx, int64_t ticks);
 /* The 20 int32 header fields of mh_aln (no CIGAR) for reads [first, first+n). */
 int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20);
 /* SAM text for reads order[first .. first+n) (order NULL: reads first ..
@@ -160,6 +202,29 @@ int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20);
 int mh_reads_set_names(mh_ctx *ctx, int64_t n, const char *const *names);
 int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
                    const char *const *refnames, char *buf, size_t cap, size_t *used);
+/* Rows order[0 .. n) (order NULL: reads 0 .. n - 1) formatted as style 0 /
+ * 1 text (as mh_format_rows) in n_seg segments, segment s being rows
+ * seg_rows[s] .. seg_rows[s + 1] (ascending, seg_rows[n_seg] <= n).  The
+ * text is kept; seg_bytes[s] = its size per segment.  A sharded run
+ * all-gathers the sizes to place every rank's segments in one file. */
+int mh_format_segments(mh_ctx *ctx, int style, const int64_t *order, int64_t n,
+                       const char *const *refnames, int n_seg, const int64_t *seg_rows,
+                       int64_t *seg_bytes);
+/* Write the text of the last mh_format_segments to fd, segment s at file
+ * offset seg_off[s] (pwrite on host threads; the file position is not
+ * used); crc[s] = crc32 of segment s (crc NULL: none).  Frees the text. */
+int mh_write_segments(mh_ctx *ctx, int fd, const int64_t *seg_off, uint32_t *crc);
+/* crc32 (zlib's) of A then B, from crc32(A), crc32(B) and B's length */
+uint32_t mh_crc32_combine(uint32_t a, uint32_t b, int64_t len_b);
+/* crc32 of a whole open file and its size (a read-back check) */
+int mh_file_crc32(int fd, int64_t *size, uint32_t *crc);
+/* Host wall time (ms) per phase of the file path since the last reset:
+ * MH_PHASE_INFLATE (FASTQ gunzip), _PARSE (record scan, names, copies),
+ * _UPLOAD (H2D + 2-bit packing), _FORMAT (SAM / CSV text), _WRITE (pwrite).
+ * ms[MH_PHASES]; reset != 0 zeroes them after the copy. */
+enum { MH_PHASE_INFLATE = 0, MH_PHASE_PARSE = 1, MH_PHASE_UPLOAD = 2, MH_PHASE_FORMAT = 3,
+       MH_PHASE_WRITE = 4, MH_PHASES = 5 };
+int mh_phase_times(mh_ctx *ctx, double *ms, int reset);
 /* The same rows written straight to an open file descriptor at `offset`
  * (pwrite from the formatting threads, no copy through the caller):
  * *written bytes.  The caller moves its file position past them. */

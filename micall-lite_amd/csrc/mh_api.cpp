@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -22,6 +23,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "mh_fastq.h"
 #include "mh_gunzip.h"
 #include "mh_internal.h"
 #include "mh_text.h"
@@ -203,6 +205,12 @@ struct CtxEx : Ctx {
     uint64_t fmt_key = 0;
     bool fmt_valid = false;
     std::vector<std::string> fmt_chunks;
+    // host wall time per phase of the file-to-file path (mh_phase_times)
+    double phase_ms[MH_PHASES] = {};
+    // mh_format_segments: the formatted chunks and the byte offset of every
+    // segment bound in their concatenation, kept for mh_write_segments
+    std::vector<std::string> seg_chunks;
+    std::vector<int64_t> seg_at;
 };
 
 static void free_index(DevIndex &ix)
@@ -544,10 +552,22 @@ static int index_fastq(Fastq &fq, const char *path, int64_t *newlines)
     return 0;
 }
 
-static int read_fastq(const char *path, Fastq &fq, int64_t *newlines = nullptr)
+static double ms_since(std::chrono::steady_clock::time_point t)
 {
-    if (int st = slurp(path, fq.data)) return st;
-    return index_fastq(fq, path, newlines);
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+// decode + index one file; the wall time of each half in *dec_ms / *ix_ms
+static int read_fastq(const char *path, Fastq &fq, int64_t *newlines, double *dec_ms, double *ix_ms)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    const int st = slurp(path, fq.data);
+    *dec_ms = ms_since(t0);
+    if (st) return st;
+    const auto t1 = std::chrono::steady_clock::now();
+    const int si = index_fastq(fq, path, newlines);
+    *ix_ms = ms_since(t1);
+    return si;
 }
 
 }  // namespace mh
@@ -707,6 +727,68 @@ int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64
     return mh_reads_load_fastq_part(ctx, path1, path2, 0, 1, n_reads, nullptr);
 }
 
+// The reads of units [a0, a1) of FASTQ a (and [b0, b1) of b, the mates):
+// copied once from the decoded text into the buffers the context keeps for
+// the SAM text, uploaded and packed.
+static int load_fastq_units(CtxEx *c, Fastq &a, Fastq *b, int64_t a0, int64_t a1, int64_t b0,
+                            int64_t b1, int64_t lines1, int64_t *n_reads)
+{
+    const bool paired = b != nullptr;
+    if (a0 < 0 || a1 < a0 || a1 > (int64_t)a.size() ||
+        (paired && (b0 < 0 || b1 < b0 || b1 > (int64_t)b->size() || b1 - b0 != a1 - a0))) {
+        set_error("paired FASTQ blocks hold %lld and %lld reads", (long long)(a1 - a0),
+                  (long long)(paired ? b1 - b0 : a1 - a0));
+        return -3;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    const int per = paired ? 2 : 1;
+    const int64_t n = per * (a1 - a0);
+    HostReads h;
+    h.off.resize((size_t)n);
+    h.len.resize((size_t)n);
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const bool mate2 = paired && (i & 1);
+        const Fastq &f = mate2 ? *b : a;
+        h.off[i] = total;
+        h.len[i] = f.len[(mate2 ? b0 : a0) + i / per];
+        total += h.len[i];
+    }
+    h.seq.alloc((size_t)total);
+    h.qual.alloc((size_t)total);
+    std::vector<std::string> names((size_t)n);
+    const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
+    par_for(nt, [&](int t) {
+        for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
+            const bool mate2 = paired && (i & 1);
+            const Fastq &f = mate2 ? *b : a;
+            const int64_t r = (mate2 ? b0 : a0) + i / per;
+            const char *D = f.data.data();
+            names[i] = qname_of(D + f.name_at[r], (size_t)f.name_len[r], paired);
+            const int64_t L = h.len[i];
+            memcpy(h.seq.data() + h.off[i], D + f.seq_at[r], (size_t)L);
+            const int64_t cq = std::min<int64_t>(L, f.qual_len[r]);
+            if (cq > 0) memcpy(h.qual.data() + h.off[i], D + f.qual_at[r], (size_t)cq);
+            for (int64_t x = cq; x < L; ++x) h.qual.data()[h.off[i] + x] = 'I';
+        }
+    });
+    a = Fastq{};
+    if (b) *b = Fastq{};
+    c->phase_ms[MH_PHASE_PARSE] += ms_since(t0);
+    const auto t1 = std::chrono::steady_clock::now();
+    const uint8_t *sq = h.seq.data(), *ql = h.qual.data();
+    const int64_t *of = h.off.data();
+    const int32_t *ln = h.len.data();
+    int st = load_reads(*c, c->reads, c->host, n, paired, sq, ql, of, ln, false, &h);
+    c->phase_ms[MH_PHASE_UPLOAD] += ms_since(t1);
+    if (st) return st;
+    c->names.swap(names);
+    c->map.valid = false;
+    c->fastq_lines1 = lines1;
+    if (n_reads) *n_reads = n;
+    return 0;
+}
+
 int mh_reads_load_fastq_part(mh_ctx *ctx, const char *path1, const char *path2, int part, int parts,
                              int64_t *n_reads, int64_t *first_unit)
 {
@@ -721,15 +803,18 @@ int mh_reads_load_fastq_part(mh_ctx *ctx, const char *path1, const char *path2, 
     int64_t lines1 = 0;
     int st2 = 0;
     std::string err2;
+    double dec1 = 0, dec2 = 0, ix1 = 0, ix2 = 0;
     // the two files are decoded concurrently
     std::thread t2;
     if (paired)
         t2 = std::thread([&]() {
-            st2 = read_fastq(path2, b);
+            st2 = read_fastq(path2, b, nullptr, &dec2, &ix2);
             if (st2) err2 = last_error_text();
         });
-    const int st1 = read_fastq(path1, a, &lines1);
+    const int st1 = read_fastq(path1, a, &lines1, &dec1, &ix1);
     if (paired) t2.join();
+    c->phase_ms[MH_PHASE_INFLATE] += std::max(dec1, dec2);
+    c->phase_ms[MH_PHASE_PARSE] += std::max(ix1, ix2);
     if (st1) return st1;
     if (st2) { set_error("%s", err2.c_str()); return st2; }
     if (paired && a.size() != b.size()) {
@@ -742,49 +827,49 @@ int mh_reads_load_fastq_part(mh_ctx *ctx, const char *path1, const char *path2, 
     const int64_t units_all = (int64_t)a.size();
     const int64_t u0 = units_all * part / parts, u1 = units_all * (part + 1) / parts;
     if (first_unit) *first_unit = u0;
-    // the block's reads (mates interleaved) copied once from the decoded
-    // text into the buffers the context keeps for the SAM text
-    const int per = paired ? 2 : 1;
-    const int64_t n = per * (u1 - u0);
-    HostReads h;
-    h.off.resize((size_t)n);
-    h.len.resize((size_t)n);
-    int64_t total = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        const Fastq &f = (paired && (i & 1)) ? b : a;
-        h.off[i] = total;
-        h.len[i] = f.len[u0 + i / per];
-        total += h.len[i];
+    return load_fastq_units(c, a, paired ? &b : nullptr, u0, u1, u0, u1, lines1, n_reads);
+}
+
+int mh_reads_load_staged(mh_ctx *ctx, mh_fastq *fq1, mh_fastq *fq2, const int64_t *range4,
+                         int64_t fastq_lines1, int64_t *n_reads)
+{
+    if (!ctx || !fq1 || !range4) { set_error("mh_reads_load_staged: bad arguments"); return -3; }
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    const bool paired = fq2 != nullptr;
+    Fastq a, b;
+    double ix1 = 0, ix2 = 0;
+    int st1 = 0, st2 = 0;
+    std::string err2;
+    try {
+        a.data = take_fastq_text(fq1);
+        if (paired) b.data = take_fastq_text(fq2);
+    } catch (const std::bad_alloc &) {
+        set_error("mh_reads_load_staged: out of memory");
+        return -2;
     }
-    h.seq.alloc((size_t)total);
-    h.qual.alloc((size_t)total);
-    std::vector<std::string> names((size_t)n);
-    const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
-    par_for(nt, [&](int t) {
-        for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
-            const Fastq &f = (paired && (i & 1)) ? b : a;
-            const int64_t r = u0 + i / per;
-            const char *D = f.data.data();
-            names[i] = qname_of(D + f.name_at[r], (size_t)f.name_len[r], paired);
-            const int64_t L = h.len[i];
-            memcpy(h.seq.data() + h.off[i], D + f.seq_at[r], (size_t)L);
-            const int64_t c = std::min<int64_t>(L, f.qual_len[r]);
-            if (c > 0) memcpy(h.qual.data() + h.off[i], D + f.qual_at[r], (size_t)c);
-            for (int64_t x = c; x < L; ++x) h.qual.data()[h.off[i] + x] = 'I';
-        }
-    });
-    a = Fastq{};
-    b = Fastq{};
-    const uint8_t *sq = h.seq.data(), *ql = h.qual.data();
-    const int64_t *of = h.off.data();
-    const int32_t *ln = h.len.data();
-    int st = load_reads(*c, c->reads, c->host, n, paired, sq, ql, of, ln, false, &h);
-    if (st) return st;
-    c->names.swap(names);
-    c->map.valid = false;
-    c->fastq_lines1 = lines1;
-    if (n_reads) *n_reads = n;
-    return 0;
+    std::thread t2;
+    if (paired)
+        t2 = std::thread([&]() {
+            const auto t = std::chrono::steady_clock::now();
+            st2 = index_fastq(b, "FASTQ 2", nullptr);
+            ix2 = ms_since(t);
+            if (st2) err2 = last_error_text();
+        });
+    {
+        const auto t = std::chrono::steady_clock::now();
+        st1 = index_fastq(a, "FASTQ 1", nullptr);
+        ix1 = ms_since(t);
+    }
+    if (paired) t2.join();
+    c->phase_ms[MH_PHASE_PARSE] += std::max(ix1, ix2);
+    if (st1) return st1;
+    if (st2) { set_error("%s", err2.c_str()); return st2; }
+    const int64_t a0 = range4[0] < 0 ? 0 : range4[0];
+    const int64_t a1 = range4[1] < 0 ? (int64_t)a.size() : range4[1];
+    const int64_t b0 = range4[2] < 0 ? 0 : range4[2];
+    const int64_t b1 = range4[3] < 0 ? (int64_t)b.size() : range4[3];
+    return load_fastq_units(c, a, paired ? &b : nullptr, a0, a1, b0, b1, fastq_lines1, n_reads);
 }
 
 int mh_reads_count(mh_ctx *ctx, int64_t *n_reads, int *paired)
@@ -939,10 +1024,17 @@ int mh_test_set_capacities(mh_ctx *ctx, int64_t cigar_pool_words, int64_t pileup
     return 0;
 }
 
-int mh_retry_counts(mh_ctx *ctx, int64_t *out3)
+int mh_retry_counts(mh_ctx *ctx, int64_t *out4)
 {
-    if (!ctx || !out3) return -3;
-    for (int k = 0; k < RETRY_KINDS; ++k) out3[k] = X(ctx)->retries[k];
+    if (!ctx || !out4) return -3;
+    for (int k = 0; k < RETRY_KINDS; ++k) out4[k] = X(ctx)->retries[k];
+    return 0;
+}
+
+int mh_test_set_gotoh_wait(mh_ctx *ctx, int64_t ticks)
+{
+    if (!ctx || ticks < 0) { set_error("mh_test_set_gotoh_wait: bad arguments"); return -3; }
+    X(ctx)->test_caps.gotoh_wait_ticks = ticks;
     return 0;
 }
 
@@ -1103,10 +1195,15 @@ static void format_row(const CtxEx *c, int style, const Rec &a, int64_t r, const
 }
 
 // The text of rows first .. first+n (or order[first ..]) as one chunk per
-// host thread, in order.
+// host thread, in order.  With segment row bounds seg_rows[0 .. n_seg]
+// (relative to `first`, ascending), *seg_at gets the byte offset in the
+// concatenated text at which each bound row starts.
 static int format_chunks(CtxEx *c, int style, const int64_t *order, int64_t first, int64_t n,
-                         const char *const *refnames, std::vector<std::string> &chunks)
+                         const char *const *refnames, std::vector<std::string> &chunks,
+                         int n_seg = 0, const int64_t *seg_rows = nullptr,
+                         std::vector<int64_t> *seg_at = nullptr)
 {
+    const auto t0 = std::chrono::steady_clock::now();
     std::vector<Rec> rec;
     std::vector<uint32_t> pool;
     if (order) {
@@ -1123,18 +1220,36 @@ static int format_chunks(CtxEx *c, int style, const int64_t *order, int64_t firs
     for (int k = 0; k < c->index.n_refs; ++k) rn_len[k] = std::strlen(refnames[k]);
     const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
     chunks.assign(nt, std::string());
+    // per thread: (segment bound, byte offset in the thread's chunk)
+    std::vector<std::vector<std::pair<int, size_t>>> marks(nt);
     par_for(nt, [&](int t) {
         const int64_t k0 = n * t / nt, k1 = n * (t + 1) / nt;
         std::string &out = chunks[t];
         size_t used = 0;
         std::string tmp;
+        int sb = 0;
+        if (seg_rows) {
+            while (sb <= n_seg && seg_rows[sb] < k0) ++sb;
+        }
         for (int64_t k = k0; k < k1; ++k) {
+            while (seg_rows && sb <= n_seg && seg_rows[sb] == k) marks[t].emplace_back(sb++, used);
             const int64_t r = order ? order[first + k] : first + k;
             format_row(c, style, order ? rec[r] : rec[k], r, pool.data(), refnames, rn_len.data(),
                        out, used, tmp);
         }
         out.resize(used);
     });
+    if (seg_at) {
+        seg_at->assign((size_t)n_seg + 1, -1);
+        int64_t base = 0;
+        for (int t = 0; t < nt; ++t) {
+            for (auto &m : marks[t]) (*seg_at)[m.first] = base + (int64_t)m.second;
+            base += (int64_t)chunks[t].size();
+        }
+        for (int sb = 0; sb <= n_seg; ++sb)   // bounds at the end (row n)
+            if ((*seg_at)[sb] < 0) (*seg_at)[sb] = base;
+    }
+    c->phase_ms[MH_PHASE_FORMAT] += ms_since(t0);
     return 0;
 }
 
@@ -1147,6 +1262,7 @@ int mh_write_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, i
     if ((int64_t)c->names.size() != c->reads.n) { set_error("no read names loaded"); return -3; }
     std::vector<std::string> chunks;
     if (int st = format_chunks(c, style, order, first, n, refnames, chunks)) return st;
+    const auto tw = std::chrono::steady_clock::now();
     std::vector<int64_t> at(chunks.size() + 1, offset);
     for (size_t t = 0; t < chunks.size(); ++t) at[t + 1] = at[t] + (int64_t)chunks[t].size();
     std::atomic<int> bad(0);
@@ -1160,8 +1276,138 @@ int mh_write_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, i
             p += w; left -= (size_t)w; pos += w;
         }
     });
+    c->phase_ms[MH_PHASE_WRITE] += ms_since(tw);
     if (bad) { set_error("mh_write_rows: write failed (%s)", strerror(bad.load())); return -4; }
     if (written) *written = at.back() - offset;
+    return 0;
+}
+
+int mh_format_segments(mh_ctx *ctx, int style, const int64_t *order, int64_t n,
+                       const char *const *refnames, int n_seg, const int64_t *seg_rows,
+                       int64_t *seg_bytes)
+{
+    if (!ctx || !refnames || (style != 0 && style != 1) || n < 0 || n_seg < 1 || !seg_rows ||
+        !seg_bytes) {
+        set_error("mh_format_segments: bad arguments");
+        return -3;
+    }
+    for (int k = 0; k < n_seg; ++k)
+        if (seg_rows[k] < 0 || seg_rows[k + 1] < seg_rows[k] || seg_rows[k + 1] > n) {
+            set_error("mh_format_segments: segment bounds out of order");
+            return -3;
+        }
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    if ((int64_t)c->names.size() != c->reads.n) { set_error("no read names loaded"); return -3; }
+    c->seg_chunks.clear();
+    c->seg_at.clear();
+    if (int st = format_chunks(c, style, order, 0, n, refnames, c->seg_chunks, n_seg, seg_rows,
+                               &c->seg_at))
+        return st;
+    for (int k = 0; k < n_seg; ++k) seg_bytes[k] = c->seg_at[k + 1] - c->seg_at[k];
+    return 0;
+}
+
+int mh_write_segments(mh_ctx *ctx, int fd, const int64_t *seg_off, uint32_t *crc)
+{
+    if (!ctx || fd < 0 || !seg_off) { set_error("mh_write_segments: bad arguments"); return -3; }
+    CtxEx *c = X(ctx);
+    const int n_seg = (int)c->seg_at.size() - 1;
+    if (n_seg < 1) { set_error("mh_write_segments: nothing formatted"); return -3; }
+    for (int k = 0; k < n_seg; ++k)
+        if (seg_off[k] < 0) { set_error("mh_write_segments: negative offset"); return -3; }
+    const auto tw = std::chrono::steady_clock::now();
+    std::vector<std::string> &ch = c->seg_chunks;
+    const int nt = (int)ch.size();
+    std::vector<int64_t> cbase(nt + 1, 0);
+    for (int t = 0; t < nt; ++t) cbase[t + 1] = cbase[t] + (int64_t)ch[t].size();
+    // pieces: a chunk cut at the segment starts; each written at its
+    // segment's file offset, its crc32 computed beside the write
+    struct Piece { int t, seg; int64_t a, b; uint32_t crc; };
+    std::vector<Piece> pieces;
+    for (int t = 0; t < nt; ++t) {
+        int64_t a = cbase[t];
+        while (a < cbase[t + 1]) {
+            // the segment holding byte a: the last start <= a with a non-empty span
+            int sg = (int)(std::upper_bound(c->seg_at.begin(), c->seg_at.end(), a) - c->seg_at.begin()) - 1;
+            while (sg < n_seg - 1 && c->seg_at[sg + 1] <= a) ++sg;
+            const int64_t b = std::min(cbase[t + 1], c->seg_at[sg + 1]);
+            pieces.push_back(Piece{t, sg, a, b, 0});
+            a = b;
+        }
+    }
+    std::atomic<size_t> next(0);
+    std::atomic<int> bad(0);
+    const int nw = std::max(1, std::min<int>(s2a_threads(), (int)pieces.size()));
+    par_for(nw, [&](int) {
+        for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
+            Piece &p = pieces[i];
+            const char *src = ch[p.t].data() + (p.a - cbase[p.t]);
+            const size_t len = (size_t)(p.b - p.a);
+            if (crc) p.crc = crc32_update(0, src, len);
+            size_t left = len;
+            int64_t pos = seg_off[p.seg] + (p.a - c->seg_at[p.seg]);
+            while (left > 0) {
+                const ssize_t w = pwrite(fd, src, left, (off_t)pos);
+                if (w <= 0) { bad = errno ? errno : EIO; return; }
+                src += w; left -= (size_t)w; pos += w;
+            }
+        }
+    });
+    if (crc) {
+        for (int k = 0; k < n_seg; ++k) crc[k] = 0;
+        for (const Piece &p : pieces) crc[p.seg] = crc32_join(crc[p.seg], p.crc, p.b - p.a);
+    }
+    c->seg_chunks.clear();
+    c->seg_at.clear();
+    c->phase_ms[MH_PHASE_WRITE] += ms_since(tw);
+    if (bad) { set_error("mh_write_segments: write failed (%s)", strerror(bad.load())); return -4; }
+    return 0;
+}
+
+uint32_t mh_crc32_combine(uint32_t a, uint32_t b, int64_t len_b) { return crc32_join(a, b, len_b); }
+
+int mh_file_crc32(int fd, int64_t *size, uint32_t *crc)
+{
+    if (fd < 0 || !crc) return -3;
+    struct stat st;
+    if (fstat(fd, &st) != 0) { set_error("mh_file_crc32: fstat failed"); return -4; }
+    const int64_t n = (int64_t)st.st_size;
+    const int64_t CH = (int64_t)16 << 20;
+    const int64_t nc = (n + CH - 1) / CH;
+    std::vector<uint32_t> part((size_t)std::max<int64_t>(nc, 1), 0);
+    std::atomic<int64_t> next(0);
+    std::atomic<int> bad(0);
+    const int nt = std::max(1, std::min<int>(s2a_threads(), (int)std::max<int64_t>(nc, 1)));
+    par_for(nt, [&](int) {
+        std::vector<unsigned char> buf((size_t)CH);
+        for (int64_t k; (k = next.fetch_add(1)) < nc;) {
+            const int64_t a = k * CH, len = std::min(CH, n - a);
+            int64_t got = 0;
+            while (got < len) {
+                const ssize_t r = pread(fd, buf.data() + got, (size_t)(len - got), (off_t)(a + got));
+                if (r <= 0) { bad = 1; return; }
+                got += r;
+            }
+            part[k] = crc32_update(0, buf.data(), (size_t)len);
+        }
+    });
+    if (bad) { set_error("mh_file_crc32: read failed"); return -4; }
+    uint32_t c0 = 0;
+    for (int64_t k = 0; k < nc; ++k) c0 = crc32_join(c0, part[k], std::min(CH, n - k * CH));
+    if (size) *size = n;
+    *crc = c0;
+    return 0;
+}
+
+int mh_phase_times(mh_ctx *ctx, double *ms, int reset)
+{
+    if (!ctx) return -3;
+    CtxEx *c = X(ctx);
+    for (int k = 0; k < MH_PHASES; ++k) {
+        if (ms) ms[k] = c->phase_ms[k];
+        if (reset) c->phase_ms[k] = 0.0;
+    }
     return 0;
 }
 

@@ -1,0 +1,340 @@
+// mh_fastq.cpp -- staged FASTQ text for a sharded ingest (host code only).
+//
+// In a job of W ranks every rank must end up with the reads of its own
+// contiguous block of FASTQ records without decoding the whole file.  The
+// reference streams each file once per mapping pass (prelim_map.py:114-134,
+// bowtie2 reading the FASTQ; censor_fastq.py:58-96 line by line); here a rank
+// reads its 1/W share of the file:
+//
+//   * a gzip file of many members (as a parallel gzip, or this library's
+//     censor, writes it): the members that start in the rank's byte range
+//     [size * p / W, size * (p + 1) / W), the cuts moved to the nearest
+//     member start (found by probing the header-shaped offsets either side:
+//     a false one fails to decode), so the ranges of consecutive ranks meet
+//     exactly;
+//   * a plain file: the byte range itself;
+//   * anything else (one gzip member, as bcl2fastq writes it): the whole file
+//     (mode 0), and the rank keeps its records by count.
+//
+// The text a rank holds then starts and ends mid-record.  mh_fastq_frame
+// locates its record starts from the number of lines before it (a record is
+// four lines); the caller moves the bytes before the first record start to
+// the rank before (mh_fastq_splice), and exchanges whole records between
+// ranks to align the mates of R1 and R2.  All of that exchange is the
+// caller's (torch.distributed in micall_amd/ingest.py); this file only
+// decodes, frames and splices host buffers.
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mh_fastq.h"
+#include "mh_gunzip.h"
+#include "micall_hip.h"
+
+namespace mh {
+void set_error(const char *fmt, ...);
+int s2a_threads();
+}
+
+using namespace mh;
+
+struct mh_fastq {
+    std::string data;              // the held text
+    std::vector<int64_t> rec;      // byte offsets of its record starts (mh_fastq_frame)
+    bool framed = false;
+};
+
+namespace {
+
+// a read-only view of a whole file (mmap, or read() for what cannot be mapped)
+struct FileView {
+    const uint8_t *p = nullptr;
+    int64_t size = 0;
+    void *map = nullptr;
+    std::string copy;
+    ~FileView() { if (map) munmap(map, (size_t)size); }
+};
+
+int view_file(const char *path, int fd_in, FileView &v)
+{
+    int fd = fd_in;
+    if (path) {
+        fd = open(path, O_RDONLY | O_CLOEXEC);
+        if (fd < 0) { set_error("cannot open FASTQ %s", path); return -3; }
+    }
+    struct stat st;
+    if (fd < 0 || fstat(fd, &st) != 0) {
+        if (path) close(fd);
+        set_error("cannot stat FASTQ %s", path ? path : "(descriptor)");
+        return -3;
+    }
+    v.size = (int64_t)st.st_size;
+    int rc = 0;
+    if (v.size > 0 && S_ISREG(st.st_mode)) {
+        void *m = mmap(nullptr, (size_t)v.size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m != MAP_FAILED) {
+            v.map = m;
+            v.p = (const uint8_t *)m;
+        }
+    }
+    if (!v.p && v.size > 0) {
+        v.copy.resize((size_t)v.size);
+        int64_t got = 0;
+        while (got < v.size) {
+            const ssize_t r = pread(fd, &v.copy[got], (size_t)(v.size - got), (off_t)got);
+            if (r <= 0) { set_error("cannot read FASTQ %s", path ? path : "(descriptor)"); rc = -3; break; }
+            got += r;
+        }
+        v.p = (const uint8_t *)v.copy.data();
+    }
+    if (path) close(fd);
+    return rc;
+}
+
+// the first offset in [from, size) where a gzip member starts (probed), or size
+int64_t next_member(const FileView &v, int64_t from)
+{
+    const uint8_t *p = v.p + from, *e = v.p + v.size;
+    while (p < e) {
+        p = (const uint8_t *)memchr(p, 0x1f, (size_t)(e - p));
+        if (!p) break;
+        if (gzip_header_at(p, e - p) && gzip_member_probe(p, e - p, 1 << 16)) return p - v.p;
+        ++p;
+    }
+    return v.size;
+}
+
+// the last offset in [0, before) where a gzip member starts (probed); 0 if
+// none is found (offset 0 starts the file's first member)
+int64_t prev_member(const FileView &v, int64_t before)
+{
+    for (int64_t at = std::min(before, v.size) - 1; at > 0; --at) {
+        const uint8_t *p = (const uint8_t *)memrchr(v.p, 0x1f, (size_t)at + 1);
+        if (!p) break;
+        at = p - v.p;
+        if (at > 0 && gzip_header_at(p, v.size - at) && gzip_member_probe(p, v.size - at, 1 << 16))
+            return at;
+    }
+    return 0;
+}
+
+// the member start nearest to x (the earlier one on a tie): the cut between
+// parts, the same on both ranks that share it
+int64_t cut_at(const FileView &v, int64_t x)
+{
+    const int64_t before = prev_member(v, x), after = next_member(v, x);
+    return x - before <= after - x ? before : after;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t)
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+}  // namespace
+
+extern "C" {
+
+int mh_fastq_open_part(const char *path, int fd, int part, int parts, mh_fastq **out, int64_t *info)
+{
+    if (!out || !info || (!path && fd < 0) || parts < 1 || part < 0 || part >= parts) {
+        set_error("mh_fastq_open_part: bad arguments");
+        return -3;
+    }
+    *out = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        FileView v;
+        if (int st = view_file(path, fd, v)) return st;
+        std::unique_ptr<mh_fastq> fq(new mh_fastq());
+        const bool gz = v.size >= 2 && v.p[0] == 0x1f && v.p[1] == 0x8b;
+        int64_t mode = 0, c0 = 0, c1 = v.size;
+        if (parts > 1 && !gz) {
+            mode = 2;
+            c0 = v.size * part / parts;
+            c1 = v.size * (part + 1) / parts;
+        } else if (parts > 1) {
+            mode = 1;
+            const int64_t lo = v.size * part / parts, hi = v.size * (part + 1) / parts;
+            c0 = part == 0 ? 0 : cut_at(v, lo);
+            c1 = part == parts - 1 ? v.size : std::max(c0, cut_at(v, hi));
+            if (c0 >= c1) c0 = c1 = std::max(c0, c1);
+        }
+        std::string why;
+        if (gz && c1 > c0) {
+            if (gunzip_buffer(v.p + c0, c1 - c0, fq->data, why)) {
+                set_error("gzip error reading %s: %s", path ? path : "(descriptor)", why.c_str());
+                return -3;
+            }
+        } else if (c1 > c0) {
+            fq->data.assign((const char *)v.p + c0, (size_t)(c1 - c0));
+        }
+        const std::string &d = fq->data;
+        const int64_t n = (int64_t)d.size();
+        // newlines, counted on host threads
+        const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 22) + 1));
+        std::vector<int64_t> cnt(nt, 0);
+        std::vector<std::thread> th;
+        auto count = [&](int t) {
+            const char *a = d.data() + n * t / nt, *b = d.data() + n * (t + 1) / nt;
+            int64_t k = 0;
+            while (a < b) {
+                const char *q = (const char *)memchr(a, '\n', (size_t)(b - a));
+                if (!q) break;
+                ++k;
+                a = q + 1;
+            }
+            cnt[t] = k;
+        };
+        for (int t = 1; t < nt; ++t) th.emplace_back(count, t);
+        count(0);
+        for (auto &x : th) x.join();
+        int64_t nl = 0;
+        for (int64_t k : cnt) nl += k;
+        info[0] = mode;
+        info[1] = c0;
+        info[2] = c1;
+        info[3] = n;
+        info[4] = nl;
+        info[5] = n > 0 && d[n - 1] == '\n';
+        info[6] = n > 0 && d[0] == '\n';
+        info[7] = c1 - c0;
+        info[8] = v.size;
+        info[9] = (int64_t)(ms_since(t0) * 1000.0);   // microseconds
+        *out = fq.release();
+        return 0;
+    } catch (const std::bad_alloc &) {
+        set_error("mh_fastq_open_part: out of memory");
+        return -2;
+    } catch (const std::exception &e) {
+        set_error("mh_fastq_open_part: %s", e.what());
+        return -4;
+    }
+}
+
+int mh_fastq_frame(mh_fastq *fq, int64_t line0, int starts_line, int64_t *out)
+{
+    if (!fq || !out || line0 < 0) { set_error("mh_fastq_frame: bad arguments"); return -3; }
+    try {
+        const std::string &d = fq->data;
+        const int64_t n = (int64_t)d.size();
+        fq->rec.clear();
+        int64_t first_line = -1;
+        int64_t blank = 0, tail_cr = 0;
+        // line starts: offset 0 when the text starts a line (its index is
+        // line0), else the first byte continues line line0 and the next line
+        // (line0 + 1) starts after the first '\n'
+        int64_t at = 0, line = line0;
+        if (!starts_line) {
+            const char *q = (const char *)memchr(d.data(), '\n', (size_t)n);
+            at = q ? (q - d.data()) + 1 : n;
+            line = line0 + 1;
+        }
+        while (at < n) {
+            const char *q = (const char *)memchr(d.data() + at, '\n', (size_t)(n - at));
+            const int64_t end = q ? q - d.data() : n;
+            if ((line & 3) == 0) {
+                if (first_line < 0) first_line = line;
+                fq->rec.push_back(at);
+                int64_t e = end;
+                if (e > at && d[e - 1] == '\r') --e;
+                if (q && e == at) blank = 1;          // a blank line where a record starts
+                if (!q && end - at == 1 && d[at] == '\r') tail_cr = 1;
+            }
+            at = end + 1;
+            ++line;
+        }
+        fq->framed = true;
+        out[0] = fq->rec.empty() ? n : fq->rec[0];
+        out[1] = (int64_t)fq->rec.size();
+        out[2] = first_line;
+        out[3] = blank;
+        out[4] = tail_cr;
+        return 0;
+    } catch (const std::bad_alloc &) {
+        set_error("mh_fastq_frame: out of memory");
+        return -2;
+    }
+}
+
+int mh_fastq_record_offset(mh_fastq *fq, int64_t k, int64_t *off)
+{
+    if (!fq || !off || !fq->framed || k < 0 || k > (int64_t)fq->rec.size()) {
+        set_error("mh_fastq_record_offset: bad arguments");
+        return -3;
+    }
+    *off = k == (int64_t)fq->rec.size() ? (int64_t)fq->data.size() : fq->rec[k];
+    return 0;
+}
+
+int mh_fastq_splice(mh_fastq *fq, int64_t lo, int64_t hi, const char *front, int64_t flen,
+                    const char *back, int64_t blen)
+{
+    if (!fq || lo < 0 || hi < lo || hi > (int64_t)fq->data.size() || flen < 0 || blen < 0 ||
+        (flen && !front) || (blen && !back)) {
+        set_error("mh_fastq_splice: bad arguments");
+        return -3;
+    }
+    try {
+        std::string &d = fq->data;
+        if (flen == 0) {
+            d.resize((size_t)hi);
+            d.erase(0, (size_t)lo);
+        } else {
+            std::string t;
+            t.reserve((size_t)(flen + (hi - lo) + blen));
+            t.append(front, (size_t)flen);
+            t.append(d, (size_t)lo, (size_t)(hi - lo));
+            d.swap(t);
+        }
+        if (blen) d.append(back, (size_t)blen);
+        fq->rec.clear();
+        fq->framed = false;
+        return 0;
+    } catch (const std::bad_alloc &) {
+        set_error("mh_fastq_splice: out of memory");
+        return -2;
+    }
+}
+
+int mh_fastq_view(mh_fastq *fq, const char **data, int64_t *len)
+{
+    if (!fq || !data || !len) return -3;
+    *data = fq->data.data();
+    *len = (int64_t)fq->data.size();
+    return 0;
+}
+
+int mh_fastq_close(mh_fastq *fq)
+{
+    delete fq;
+    return 0;
+}
+
+}  // extern "C"
+
+namespace mh {
+
+std::string take_fastq_text(mh_fastq *fq)
+{
+    std::string out;
+    out.swap(fq->data);
+    fq->rec.clear();
+    fq->framed = false;
+    return out;
+}
+
+}  // namespace mh

@@ -1,0 +1,10 @@
+// mh_fastq.h -- staged FASTQ text (mh_fastq.cpp) handed to the read loader.
+#pragma once
+#include <string>
+
+struct mh_fastq;
+
+namespace mh {
+// move the held text out of a staged FASTQ (the handle keeps an empty text)
+std::string take_fastq_text(mh_fastq *fq);
+}  // namespace mh

@@ -83,6 +83,9 @@ struct GotohStrips {
     // the shader clock before and after the block's wait, fwd then bwd
     unsigned long long *stamps;
     int stamp_blocks;
+    // a wait longer than this many ticks of the 100 MHz s_memrealtime clock
+    // is declared broken (the host retries the batch once)
+    unsigned long long wait_ticks;
 };
 
 // a diagnostic clock stamp (lane 0 stores it)
@@ -158,7 +161,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, uint32_t 
     return __builtin_amdgcn_make_buffer_rsrc((void *)uni(p), (short)0, (int)uni(bytes), 0x00020000);
 }
 
-constexpr int GWAIT_MAX = 1 << 23;   // polls before a wait is declared broken (~0.25 s)
+// default wait limit: 20 s of the 100 MHz real-time clock, far past any
+// legitimate wait (a strip waits for the strip above it, which holds a
+// lower ticket and is resident or done), also on a GPU shared by several
+// processes or running at a throttled clock
+constexpr unsigned long long GWAIT_TICKS = 20ull * 100000000ull;
 
 // boundary cells: device-coherent loads / stores (another strip, on any XCD,
 // reads them while this launch runs)
@@ -210,19 +217,25 @@ __device__ __forceinline__ uint32_t rp_tag(unsigned long long w) { return (uint3
 
 // Poll a block of boundary cells (lanes 0..31 hold one each) until every
 // cell the block has carries the producing strip's tag.  A wait that
-// outlasts any legitimate one (~0.25 s) sets flags[0] and gives up, so a
-// broken protocol ends the launch with an error instead of hanging.
+// outlasts S.wait_ticks of real time sets flags[0] and gives up, so a broken
+// protocol ends the launch with an error instead of hanging.
 template <class T, class Tag>
-__device__ __forceinline__ T poll_block(const T *p, int lane, bool has, Tag tagged, int *flags)
+__device__ __forceinline__ T poll_block(const T *p, int lane, bool has, Tag tagged, int *flags,
+                                        unsigned long long wait_ticks)
 {
     T v{};
+    unsigned long long t0 = 0;
     for (int it = 0;; ++it) {
         if (has) v = dev_load(p + lane);
         if (__builtin_amdgcn_ballot_w64(has && !tagged(v)) == 0) return v;
-        if (it >= GWAIT_MAX ||
-            __builtin_amdgcn_readfirstlane(dev_load(flags))) {
-            dev_store(flags, 1);
-            return v;
+        // the clock is read every 64 polls (every poll under a short test limit)
+        if ((it & 63) == 0 || wait_ticks < 4096) {
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            if (it == 0) t0 = now;
+            if (now - t0 > wait_ticks || __builtin_amdgcn_readfirstlane(dev_load(flags))) {
+                dev_store(flags, 1);
+                return v;
+            }
         }
         __builtin_amdgcn_s_sleep(2);
     }
@@ -335,7 +348,7 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
             const uint32_t want = strip_tag(k - 1);
             const unsigned long long w = poll_block(above + t0, lane, lane < GBLK && t0 + lane < W1,
                                                     [&](unsigned long long x) { return rp_tag(x) == want; },
-                                                    (int *)flags);
+                                                    (int *)flags, S.wait_ticks);
             aR = rp_r(w);
             aP = rp_p(w);
         }
@@ -512,7 +525,7 @@ __global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
         if (consume && t0 <= n) {
             const int want = (k + 1) % 0xFFFFFF + 1;
             d = poll_block(under + t0, lane, lane < GBLK && t0 + lane < W1,
-                           [&](int w) { return (w >> 8) == want; }, (int *)flags) & 0xFF;
+                           [&](int w) { return (w >> 8) == want; }, (int *)flags, S.wait_ticks) & 0xFF;
         }
         if (lane < GBLK) bw[lane] = d;
 #pragma unroll
@@ -693,9 +706,10 @@ static size_t gotoh_work_bytes(int m, int n)
 // alignment must not pin device memory for the rest of the session).
 constexpr size_t GOTOH_KEEP_BYTES = (size_t)1 << 30;
 
-int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const *s2, int gop,
-                    int gep, int is_global, const char *alphabet, const int *matrix,
-                    char *const *out1, char *const *out2, const int *cap, int *score, int *status)
+static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char *const *s2, int gop,
+                            int gep, int is_global, const char *alphabet, const int *matrix,
+                            char *const *out1, char *const *out2, const int *cap, int *score,
+                            int *status, unsigned long long wait_ticks)
 {
     const int L = (int)strlen(alphabet);
     if (count < 0 || L == 0 || L > 64) { set_error("mh_gotoh_align: bad arguments"); return -3; }
@@ -810,6 +824,7 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
     const int strips = first[count];
     S.stamps = nullptr;
     S.stamp_blocks = 0;
+    S.wait_ticks = wait_ticks;
     const char *stamp_path = getenv("MH_GOTOH_STAMPS");
     if (stamp_path && *stamp_path) {
         int nmx = 0;
@@ -871,6 +886,26 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
         c.gotoh_cap = 0;
     }
     return 0;
+}
+
+// A strip that waited past its limit for its neighbour (a broken protocol,
+// or a producer starved for that long) fails the whole launch with -4; the
+// batch is then run once more before the error is reported.  The test
+// entry mh_test_set_capacities can impose a first-attempt limit (ticks of
+// the 100 MHz clock) so the retry is exercised.
+int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const *s2, int gop,
+                    int gep, int is_global, const char *alphabet, const int *matrix,
+                    char *const *out1, char *const *out2, const int *cap, int *score, int *status)
+{
+    const unsigned long long first = c.test_caps.gotoh_wait_ticks > 0
+                                         ? (unsigned long long)c.test_caps.gotoh_wait_ticks
+                                         : GWAIT_TICKS;
+    int st = gotoh_batch_once(c, count, s1, s2, gop, gep, is_global, alphabet, matrix, out1, out2,
+                              cap, score, status, first);
+    if (st != -4) return st;
+    ++c.retries[RETRY_GOTOH_WAIT];
+    return gotoh_batch_once(c, count, s1, s2, gop, gep, is_global, alphabet, matrix, out1, out2,
+                            cap, score, status, GWAIT_TICKS);
 }
 
 int run_gotoh(Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_global,

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <exception>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -32,6 +33,7 @@ typedef Lc *(*lc_alloc_t)(int);
 typedef void (*lc_free_t)(Lc *);
 typedef size_t (*lc_gzip_t)(Lc *, const void *, size_t, void *, size_t);
 typedef size_t (*lc_bound_t)(Lc *, size_t);
+typedef uint32_t (*l_crc32_t)(uint32_t, const void *, size_t);
 
 struct LdApi {
     ld_alloc_t alloc = nullptr;
@@ -41,6 +43,7 @@ struct LdApi {
     lc_free_t c_free = nullptr;
     lc_gzip_t c_gzip = nullptr;
     lc_bound_t c_bound = nullptr;
+    l_crc32_t crc32 = nullptr;
     bool ok = false, c_ok = false;
 };
 
@@ -61,6 +64,7 @@ const LdApi &ld_api()
         api.c_gzip = (lc_gzip_t)dlsym(h, "libdeflate_gzip_compress");
         api.c_bound = (lc_bound_t)dlsym(h, "libdeflate_gzip_compress_bound");
         api.c_ok = api.c_alloc && api.c_free && api.c_gzip && api.c_bound;
+        api.crc32 = (l_crc32_t)dlsym(h, "libdeflate_crc32");
     });
     return api;
 }
@@ -215,18 +219,26 @@ int gunzip_members(const LdApi &api, const uint8_t *src, int64_t len, std::strin
     std::vector<int64_t> beg(cand.begin(), cand.end() - 1), end(cand.begin() + 1, cand.end());
     for (int round = 0; round < 8; ++round) {
         const size_t k = beg.size();
+        // a span's size is the ISIZE word before its end; deflate expands at
+        // most 1032:1, so a larger word comes from a false boundary: the span
+        // is not decoded (size 0) and fails, which merges it with the next
         std::vector<uint64_t> at(k + 1, 0);
+        std::vector<char> plausible(k, 1);
         for (size_t j = 0; j < k; ++j) {
-            if (end[j] - beg[j] < 18) return -1;
-            at[j + 1] = at[j] + le32(src + end[j] - 4);
+            const int64_t span = end[j] - beg[j];
+            if (span < 18) return -1;
+            const uint64_t isize = le32(src + end[j] - 4);
+            plausible[j] = isize <= (uint64_t)span * 1032 + 64;
+            at[j + 1] = at[j] + (plausible[j] ? isize : 0);
         }
-        if (at[k] > (uint64_t)len * 64 + (1u << 20)) return -1;   // implausible sizes
+        if (at[k] > (uint64_t)len * 1032 + (1u << 20)) return -1;
         out.resize(at[k]);
         std::vector<char> ok(k, 0);
         std::atomic<size_t> next(0);
         run_threads(std::min<int>(threads, (int)k), [&](int) {
             for (size_t j; (j = next.fetch_add(1)) < k;)
-                ok[j] = member_exact(api, src + beg[j], end[j] - beg[j], &out[at[j]],
+                ok[j] = plausible[j] &&
+                        member_exact(api, src + beg[j], end[j] - beg[j], &out[at[j]],
                                      (uint32_t)(at[j + 1] - at[j]));
         });
         // a failed span absorbs the span after it (a false candidate split
@@ -251,6 +263,54 @@ int gunzip_members(const LdApi &api, const uint8_t *src, int64_t len, std::strin
 
 bool gunzip_fast_available() { return ld_api().ok; }
 
+uint32_t crc32_update(uint32_t crc, const void *p, size_t n)
+{
+    const LdApi &api = ld_api();
+    if (api.crc32) return api.crc32(crc, p, n);
+    const Bytef *b = (const Bytef *)p;
+    uLong c = crc;
+    while (n > 0) {
+        const uInt take = (uInt)std::min<size_t>(n, 1u << 30);
+        c = ::crc32(c, b, take);
+        b += take;
+        n -= take;
+    }
+    return (uint32_t)c;
+}
+
+uint32_t crc32_join(uint32_t a, uint32_t b, int64_t len_b)
+{
+    return (uint32_t)crc32_combine((uLong)a, (uLong)b, (z_off_t)len_b);
+}
+
+bool gzip_header_at(const uint8_t *src, int64_t avail) { return member_header(src, avail); }
+
+bool gzip_member_probe(const uint8_t *src, int64_t len, size_t probe)
+{
+    if (!member_header(src, len)) return false;
+    std::string out(probe, '\0');
+    const LdApi &api = ld_api();
+    if (api.ok) {
+        Ld *d = api.alloc();
+        if (!d) return false;
+        size_t in_used = 0, out_used = 0;
+        const int r = api.gunzip(d, src, (size_t)len, &out[0], probe, &in_used, &out_used);
+        api.free_(d);
+        // a member longer than the probe stops with the output full
+        return r == LD_SUCCESS || r == LD_INSUFFICIENT_SPACE;
+    }
+    z_stream z{};
+    if (inflateInit2(&z, 15 + 16) != Z_OK) return false;
+    z.next_in = (Bytef *)src;
+    z.avail_in = (uInt)std::min<int64_t>(len, 1 << 30);
+    z.next_out = (Bytef *)&out[0];
+    z.avail_out = (uInt)probe;
+    const int st = inflate(&z, Z_NO_FLUSH);
+    const bool ok = st == Z_STREAM_END || (st == Z_OK && z.avail_out == 0);
+    inflateEnd(&z);
+    return ok;
+}
+
 int gunzip_threads()
 {
     const char *e = getenv("OMP_NUM_THREADS");
@@ -267,9 +327,23 @@ int gunzip_buffer(const uint8_t *src, int64_t len, std::string &out, std::string
     // concatenated members (as a parallel gzip writes them) decode in
     // parallel; a single member, or anything the member scan cannot split,
     // decodes serially
-    if (len > (1 << 22) && gunzip_members(api, src, len, out, gunzip_threads()) == 0) return 0;
-    out.clear();
-    return api.ok ? gunzip_ld(api, src, len, out, why) : gunzip_zlib(src, len, out, why);
+    if (len > (1 << 22)) {
+        int st = -1;
+        try {
+            st = gunzip_members(api, src, len, out, gunzip_threads());
+        } catch (const std::exception &) {   // bad_alloc / length_error: decode serially
+            st = -1;
+        }
+        if (st == 0) return 0;
+        std::string().swap(out);
+    }
+    try {
+        return api.ok ? gunzip_ld(api, src, len, out, why) : gunzip_zlib(src, len, out, why);
+    } catch (const std::exception &) {
+        std::string().swap(out);
+        why = "out of memory";
+        return -2;
+    }
 }
 
 int gzip_member(const char *src, size_t len, std::string &out, int level)

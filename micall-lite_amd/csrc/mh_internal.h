@@ -232,15 +232,17 @@ struct TestCaps {
     int64_t pile_events = 0;        // PileState::ev
     int64_t pile_event_bytes = 0;   // PileState::ev_pool
     int64_t token_bytes = 0;        // PileState::tok_bytes
+    int64_t gotoh_wait_ticks = 0;   // k_gotoh's first-attempt wait limit (0: the default)
 };
 
 // retries taken by the grow-and-retry paths (mh_retry_counts)
-enum { RETRY_CIGAR_POOL = 0, RETRY_PILE_EVENTS = 1, RETRY_TOKEN_BYTES = 2, RETRY_KINDS = 3 };
+enum { RETRY_CIGAR_POOL = 0, RETRY_PILE_EVENTS = 1, RETRY_TOKEN_BYTES = 2, RETRY_GOTOH_WAIT = 3,
+       RETRY_KINDS = 4 };
 
 struct Ctx {
     int device = 0;
     TestCaps test_caps;
-    int64_t retries[RETRY_KINDS] = {0, 0, 0};
+    int64_t retries[RETRY_KINDS] = {0, 0, 0, 0};
     int n_cu = 0;                    // compute units of the device (launch sizing)
     // per-kernel timing with HIP events on `stream` (mh_profile)
     bool prof = false;

@@ -2387,6 +2387,12 @@ static int ensure_map_buffers(Ctx &c)
     // imposed by a test is where every pass starts.
     const int64_t test_cap = c.test_caps.cigar_pool_words;
     const int64_t need = test_cap > 0 ? test_cap : pool_words_for(n);
+    // slots and records address the pool with int32 offsets (Slot / Rec cig_off)
+    if (need > (int64_t)INT32_MAX) {
+        set_error("mh_map: %lld reads need a CIGAR pool past 2^31 words; map them in batches",
+                  (long long)n);
+        return -3;
+    }
     if (M.pool == nullptr || (test_cap > 0 ? M.pool_cap != need : M.pool_cap < need)) {
         hipFree(M.pool);
         M.pool = nullptr;
@@ -2569,7 +2575,13 @@ int run_map(Ctx &c, const mh_params &par)
             hipFree(M.pool);
             M.pool = nullptr;
             M.pool_cap = 0;
-            const int64_t grown = (int64_t)used * 2 + pool_words_for(0);
+            int64_t grown = (int64_t)used * 2 + pool_words_for(0);
+            if (grown > (int64_t)INT32_MAX) grown = INT32_MAX;   // int32 cig_off
+            if ((int64_t)used > grown) {
+                set_error("mh_map: CIGAR pool demand %llu words passes the int32 offsets",
+                          (unsigned long long)used);
+                return -2;
+            }
             MH_HIP(hipMalloc(&M.pool, sizeof(uint32_t) * grown));
             M.pool_cap = grown;
         }

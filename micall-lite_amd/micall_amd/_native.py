@@ -75,6 +75,7 @@ def _declare(L):
         'mh_test_set_capacities': ([_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                     ctypes.c_int64], ctypes.c_int),
         'mh_retry_counts': ([_P, _P], ctypes.c_int),
+        'mh_test_set_gotoh_wait': ([_P, ctypes.c_int64], ctypes.c_int),
         'mh_format_rows': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.c_int64,
                             ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_size_t,
                             ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
@@ -133,6 +134,21 @@ def _declare(L):
         'mh_a2c_insert_entries': ([_P, ctypes.c_int, _P, _P, _P, ctypes.c_char_p, ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         'mh_a2c_timing': ([_P, ctypes.c_int, _P], ctypes.c_int),
+        'mh_fastq_open_part': ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.POINTER(_P), _I64P], ctypes.c_int),
+        'mh_fastq_frame': ([_P, ctypes.c_int64, ctypes.c_int, _I64P], ctypes.c_int),
+        'mh_fastq_record_offset': ([_P, ctypes.c_int64, _I64P], ctypes.c_int),
+        'mh_fastq_splice': ([_P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int64, _P,
+                             ctypes.c_int64], ctypes.c_int),
+        'mh_fastq_view': ([_P, ctypes.POINTER(_P), _I64P], ctypes.c_int),
+        'mh_fastq_close': ([_P], ctypes.c_int),
+        'mh_reads_load_staged': ([_P, _P, _P, _I64P, ctypes.c_int64, _I64P], ctypes.c_int),
+        'mh_format_segments': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_char_p),
+                                ctypes.c_int, _P, _P], ctypes.c_int),
+        'mh_write_segments': ([_P, ctypes.c_int, _P, _P], ctypes.c_int),
+        'mh_crc32_combine': ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64], ctypes.c_uint32),
+        'mh_file_crc32': ([ctypes.c_int, _I64P, ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+        'mh_phase_times': ([_P, _P, ctypes.c_int], ctypes.c_int),
         'mh_profile': ([_P, ctypes.c_int], ctypes.c_int),
         'mh_profile_get': ([_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _I64P],
                            ctypes.c_int),
@@ -419,6 +435,51 @@ class Context:
         self.map_serial += 1
         return n.value, u0.value
 
+    def reads_load_staged(self, fq1, fq2, ranges, fastq_lines1):
+        """Reads of staged FASTQ text (Fastq handles; their texts move into
+        the context): ranges = (u0, u1, v0, v1) record ranges of fq1 / fq2,
+        -1 for all."""
+        r = np.ascontiguousarray(ranges, dtype=np.int64)
+        n = ctypes.c_int64()
+        check(lib().mh_reads_load_staged(self.h, fq1.h, fq2.h if fq2 is not None else None,
+                                         r.ctypes.data_as(_I64P), int(fastq_lines1),
+                                         ctypes.byref(n)), 'mh_reads_load_staged')
+        self.map_serial += 1
+        return n.value
+
+    def phase_times(self, reset=False):
+        """Host wall ms per phase of the file path (inflate, parse, upload,
+        format, write) since the last reset."""
+        out = np.zeros(5, dtype=np.float64)
+        check(lib().mh_phase_times(self.h, _ptr(out), int(reset)), 'mh_phase_times')
+        return dict(zip(('inflate', 'parse', 'upload', 'format', 'write'), (float(x) for x in out)))
+
+    def format_segments(self, style, order, seg_rows):
+        """Format rows order[0 ..] (None: every read) in segments
+        [seg_rows[s], seg_rows[s + 1]); the text stays in the library for
+        write_segments.  Returns the bytes per segment (int64 array)."""
+        if order is not None:
+            order = np.ascontiguousarray(order, dtype=np.int64)
+            n = len(order)
+        else:
+            n = self.reads_count()[0]
+        seg_rows = np.ascontiguousarray(seg_rows, dtype=np.int64)
+        k = len(seg_rows) - 1
+        out = np.zeros(max(k, 1), dtype=np.int64)
+        names = (ctypes.c_char_p * max(self.n_refs, 1))(*[r.encode() for r in self.refnames])
+        check(lib().mh_format_segments(self.h, style, None if order is None else _ptr(order), n,
+                                       names, k, _ptr(seg_rows), _ptr(out)), 'mh_format_segments')
+        return out[:k]
+
+    def write_segments(self, fd, offsets, crc=True):
+        """Write the last format_segments text, segment s at file offset
+        offsets[s] of descriptor fd; returns the crc32 of every segment."""
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        out = np.zeros(max(len(offsets), 1), dtype=np.uint32)
+        check(lib().mh_write_segments(self.h, int(fd), _ptr(offsets), _ptr(out) if crc else None),
+              'mh_write_segments')
+        return out[:len(offsets)]
+
     def reads_count(self):
         n = ctypes.c_int64()
         p = ctypes.c_int()
@@ -473,10 +534,17 @@ class Context:
         self.map_serial += 1
 
     def retry_counts(self):
-        """Retries taken so far: dict(cigar_pool, pileup_events, token_bytes)."""
-        out = np.zeros(3, dtype=np.int64)
+        """Retries taken so far: dict(cigar_pool, pileup_events, token_bytes,
+        gotoh_wait)."""
+        out = np.zeros(4, dtype=np.int64)
         check(lib().mh_retry_counts(self.h, _ptr(out)), 'mh_retry_counts')
-        return dict(cigar_pool=int(out[0]), pileup_events=int(out[1]), token_bytes=int(out[2]))
+        return dict(cigar_pool=int(out[0]), pileup_events=int(out[1]), token_bytes=int(out[2]),
+                    gotoh_wait=int(out[3]))
+
+    def test_set_gotoh_wait(self, ticks):
+        """Test entry point: the first attempt of every later Gotoh batch gives
+        up a neighbour wait after `ticks` of the 100 MHz clock (0: default)."""
+        check(lib().mh_test_set_gotoh_wait(self.h, int(ticks)), 'mh_test_set_gotoh_wait')
 
     def recs(self, first=0, n=None):
         """(n, 20) int32 SAM header fields (ALN_FIELDS order) without CIGARs."""
@@ -750,6 +818,89 @@ def _plain_fd(handle):
         return handle.fileno()
     except (AttributeError, OSError, ValueError):
         return None
+
+
+class Fastq:
+    """A FASTQ file's text staged on the host for a sharded ingest
+    (mh_fastq_*): this part's share of the file, framed into records,
+    spliced as the ranks exchange boundary records.  Host memory only; no
+    device needed."""
+    INFO = ('mode', 'c0', 'c1', 'bytes', 'newlines', 'ends_nl', 'starts_nl', 'file_bytes_read',
+            'file_size', 'decode_us')
+
+    def __init__(self, path=None, fd=-1, part=0, parts=1):
+        h = ctypes.c_void_p()
+        info = np.zeros(10, dtype=np.int64)
+        check(lib().mh_fastq_open_part(path.encode() if path else None, int(fd), int(part),
+                                       int(parts), ctypes.byref(h), info.ctypes.data_as(_I64P)),
+              'mh_fastq_open_part')
+        self.h = h
+        self.info = dict(zip(self.INFO, (int(x) for x in info)))
+
+    def frame(self, line0, starts_line):
+        """(first record offset, record starts, first record's file line,
+        blank record-start line, tail is a lone '\r')."""
+        out = np.zeros(5, dtype=np.int64)
+        check(lib().mh_fastq_frame(self.h, int(line0), int(bool(starts_line)),
+                                   out.ctypes.data_as(_I64P)), 'mh_fastq_frame')
+        return tuple(int(x) for x in out)
+
+    def record_offset(self, k):
+        off = ctypes.c_int64()
+        check(lib().mh_fastq_record_offset(self.h, int(k), ctypes.byref(off)),
+              'mh_fastq_record_offset')
+        return off.value
+
+    def view(self, lo=0, hi=None):
+        """The held text [lo, hi) as a read-only numpy view (no copy; valid
+        until the next splice)."""
+        p = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        check(lib().mh_fastq_view(self.h, ctypes.byref(p), ctypes.byref(n)), 'mh_fastq_view')
+        hi = n.value if hi is None else hi
+        if hi <= lo or not p.value:
+            return np.zeros(0, dtype=np.uint8)
+        buf = (ctypes.c_uint8 * (hi - lo)).from_address(p.value + lo)
+        a = np.ctypeslib.as_array(buf)
+        a.flags.writeable = False
+        return a
+
+    def size(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        check(lib().mh_fastq_view(self.h, ctypes.byref(p), ctypes.byref(n)), 'mh_fastq_view')
+        return n.value
+
+    def splice(self, lo, hi, front=b'', back=b''):
+        """The held text becomes front + text[lo, hi) + back."""
+        f = np.frombuffer(bytes(front), dtype=np.uint8) if len(front) else None
+        b = np.frombuffer(bytes(back), dtype=np.uint8) if len(back) else None
+        check(lib().mh_fastq_splice(self.h, int(lo), int(hi), None if f is None else _ptr(f),
+                                    0 if f is None else len(f), None if b is None else _ptr(b),
+                                    0 if b is None else len(b)), 'mh_fastq_splice')
+
+    def close(self):
+        if getattr(self, 'h', None):
+            lib().mh_fastq_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def crc32_combine(a, b, len_b):
+    return int(lib().mh_crc32_combine(int(a) & 0xffffffff, int(b) & 0xffffffff, int(len_b)))
+
+
+def file_crc32(fd):
+    """(size, crc32) of a whole open file."""
+    size = ctypes.c_int64()
+    crc = ctypes.c_uint32()
+    check(lib().mh_file_crc32(fd, ctypes.byref(size), ctypes.byref(crc)), 'mh_file_crc32')
+    return size.value, crc.value
 
 
 def file_checksum(fd):

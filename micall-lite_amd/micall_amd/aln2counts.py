@@ -729,7 +729,18 @@ def aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv,
                coverage_summary_csv=None, json=None):
     """aligned.csv -> nucleotide, amino-acid, insertion, consensus (and the
     optional failure, variant and coverage) reports; every argument is an
-    open file except json, a project-file path (None: the default)."""
+    open file except json, a project-file path (None: the default).  In a
+    sharded job rank 0 computes and writes while the other ranks wait
+    (session.writer_stage)."""
+    with session.writer_stage(nuc_csv, amino_csv, coord_ins_csv, conseq_csv, failed_align_csv,
+                              nuc_variants_csv, coverage_summary_csv) as stage:
+        if stage.active:
+            _aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv,
+                        failed_align_csv, nuc_variants_csv, callback, coverage_summary_csv, json)
+
+
+def _aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv, failed_align_csv,
+                nuc_variants_csv, callback, coverage_summary_csv, json):
     projects = (project_config.ProjectConfig.loadDefault() if json is None
                 else project_config.ProjectConfig.loadCustom(json))
     report = SequenceReport(InsertionWriter(coord_ins_csv), projects, CONSEQ_MIXTURE_CUTOFFS)

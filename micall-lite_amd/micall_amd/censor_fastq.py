@@ -8,11 +8,27 @@ and out as the reference's use_gzip (the output is gzip members compressed
 in parallel at level 1: same decompressed bytes, different compressed bytes
 than GzipFile's level 9 -- whose header holds a timestamp anyway).  There is
 no CPU fallback.
+
+In a sharded job (bin/micall under torchrun: every rank calls censor() with
+its own handles on the same files) each rank censors its own block of
+records: it reads its share of the source (sharded_io.stage_fastq, strict
+four-line records as the reference's zip_longest over lines, :58), censors
+it, and writes its gzip members at its offset of the destination, so the
+destination is one multi-member gzip stream holding the records in file
+order.  The base count and quality sum are summed over the ranks.
 """
 import csv
 import os
 
-from . import session
+from . import session, sharded_io
+from .sharded_io import _binary_fd
+
+
+def _is_gzip_file(fd):
+    try:
+        return os.pread(fd, 2, 0) == b'\x1f\x8b'
+    except OSError:
+        return False
 
 
 def censor(src, bad_cycles_reader, dest, use_gzip=True, summary_file=None):
@@ -21,16 +37,55 @@ def censor(src, bad_cycles_reader, dest, use_gzip=True, summary_file=None):
     bad_cycles = set()
     for cycle in bad_cycles_reader:
         bad_cycles.add((cycle['tile'], int(cycle['cycle'])))
-    data = src.read()
-    text_mode = isinstance(data, str)
-    if text_mode:
-        data = data.encode('utf-8')
-    out, base_count, score_sum = session.context().censor_fastq(
-        data, sorted(bad_cycles), src_gzip=use_gzip, dst_gzip=use_gzip)
-    dest.write(out.decode('utf-8') if text_mode else out)
-    if summary_file is not None:
+    sh = session.shard()
+    if sh is not None:
+        sh.barrier()     # every rank has opened (truncated) dest
+        fd = _binary_fd(src)
+        ok = (fd is not None and _binary_fd(dest) is not None and
+              _is_gzip_file(fd) == bool(use_gzip))
+        if bool(sh.min_i64([1 if ok else 0])[0]):
+            base_count, score_sum = _censor_block(sh, fd, sorted(bad_cycles), dest, use_gzip)
+        else:            # rank 0 censors the whole file, the others wait
+            base_count = score_sum = 0
+            if sh.rank == 0:
+                base_count, score_sum = _censor_whole(src, sorted(bad_cycles), dest, use_gzip)
+            base_count, score_sum = (int(x) for x in sh.sum_i64([base_count, score_sum]))
+        sh.barrier()     # dest is complete on every rank
+    else:
+        base_count, score_sum = _censor_whole(src, sorted(bad_cycles), dest, use_gzip)
+    if summary_file is not None and session.is_writer():
         avg_quality = float(score_sum) / base_count if base_count > 0 else None
         writer = csv.DictWriter(summary_file, ['avg_quality', 'base_count'],
                                 lineterminator=os.linesep)
         writer.writeheader()
         writer.writerow(dict(base_count=base_count, avg_quality=avg_quality))
+
+
+def _censor_whole(src, bad_cycles, dest, use_gzip):
+    """The whole file by one process."""
+    data = src.read()
+    text_mode = isinstance(data, str)
+    if text_mode:
+        data = data.encode('utf-8')
+    out, base_count, score_sum = session.context().censor_fastq(
+        data, bad_cycles, src_gzip=use_gzip, dst_gzip=use_gzip)
+    dest.write(out.decode('utf-8') if text_mode else out)
+    dest.flush()
+    return base_count, score_sum
+
+
+def _censor_block(sh, fd, bad_cycles, dest, use_gzip):
+    """This rank's block of records, censored and written at its offset."""
+    st = sharded_io.stage_fastq(sh, [(None, fd)], strict=True)
+    fq = st['frames'][0].fq
+    text = fq.view().tobytes()
+    fq.close()
+    out, base_count, score_sum = session.context().censor_fastq(
+        text, bad_cycles, src_gzip=False, dst_gzip=use_gzip)
+    if sh.rank == 0:
+        dest.flush()
+    shared = sharded_io.SharedOutput(sh, dest, binary=True)
+    shared.write_bytes([out])
+    shared.finish()
+    sums = sh.sum_i64([base_count, score_sum])
+    return int(sums[0]), int(sums[1])

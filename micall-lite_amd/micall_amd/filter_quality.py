@@ -14,6 +14,15 @@ BAD_ERROR_RATE = 7.5
 
 
 def report_bad_cycles(quality_csv, bad_cycles_csv, bad_tiles_csv=None):
+    """filter_quality.report_bad_cycles.  In a sharded job rank 0 writes
+    while the other ranks wait."""
+    from . import session
+    with session.writer_stage(bad_cycles_csv, bad_tiles_csv) as stage:
+        if stage.active:
+            _report_bad_cycles(quality_csv, bad_cycles_csv, bad_tiles_csv)
+
+
+def _report_bad_cycles(quality_csv, bad_cycles_csv, bad_tiles_csv):
     reader = csv.DictReader(quality_csv)
     writer = csv.DictWriter(bad_cycles_csv, ['tile', 'cycle', 'errorrate'],
                             lineterminator=os.linesep)

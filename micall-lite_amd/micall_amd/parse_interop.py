@@ -57,7 +57,15 @@ def _cycles(records, read_lengths):
 
 def write_phix_csv(out_file, records, read_lengths=None, summary=None):
     """tile,cycle,errorrate rows with every missing cycle written blank, per
-    tile and direction; optional average error rates in summary."""
+    tile and direction; optional average error rates in summary.  In a
+    sharded job rank 0 writes while the other ranks wait."""
+    from . import session
+    with session.writer_stage(out_file) as stage:
+        if stage.active:
+            _write_phix_csv(out_file, records, read_lengths, summary)
+
+
+def _write_phix_csv(out_file, records, read_lengths, summary):
     writer = csv.writer(out_file, lineterminator=os.linesep)
     writer.writerow(['tile', 'cycle', 'errorrate'])
     sums, counts = [0.0, 0.0], [0, 0]

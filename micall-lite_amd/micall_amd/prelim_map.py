@@ -15,7 +15,7 @@ import sys
 
 import numpy as np
 
-from . import _native, session
+from . import _native, session, sharded_io
 from .projects import ProjectConfig
 
 # Module constants the reference exports (prelim_map.py:25-33); the bowtie2
@@ -81,44 +81,46 @@ def prelim_map(fastq1, fastq2, prelim_csv,
     ctx.map(_native.params(_native.E2E, rdg=(rdgopen, READ_GAP_EXTEND),
                            rfg=(rfgopen, REF_GAP_EXTEND), maxins=MAXINS))
     sam_ref = ctx.recs()[:, _native.ALN_FIELDS.index('sam_ref')]
+    header = (','.join(FIELDNAMES) + os.linesep).encode()
     if session.is_writer():
-        session.write_bytes(prelim_csv, (','.join(FIELDNAMES) + os.linesep).encode())
-    if sh is None:
-        ctx.write_rows(prelim_csv, 1, order=grouped_order(sam_ref))
-    else:
-        _write_sharded(ctx, sh, sam_ref, len(names), prelim_csv)
-    session.prelim_written(ctx, prelim_csv, names)
+        session.write_bytes(prelim_csv, header)
+    out = sharded_io.SharedOutput(sh, prelim_csv)
+    order, bounds = grouped_segments(sam_ref, len(names), sh)
+    out.write_rows(ctx, 1, order, bounds)
+    if sh is not None:
+        sh.barrier()            # every rank's rows are in the file
+    out.finish()
+    session.prelim_written(ctx, prelim_csv, names, out.crc_of_file(header) if out.direct else None)
     if callback:
         callback(progress=ctx.fastq_line_count / 2)
 
 
-def _write_sharded(ctx, sh, sam_ref, n_refs, prelim_csv):
-    """prelim.csv of a sharded run: rname groups in global first-seen order
-    (the smallest global row index of each rname over all ranks), and in a
-    group the rows of rank 0, then rank 1, ... -- the ranks hold consecutive
-    blocks of the FASTQ, so that is FASTQ order, as on one GPU.  Every rank
-    formats its own rows; rank 0 writes."""
+def grouped_segments(sam_ref, n_refs, sh=None):
+    """prelim.csv's row order for this rank's records and its segments, one
+    per rname group (prelim_map.py:137-151: rows grouped by rname, groups in
+    first-seen order, rows in output order within a group).  Sharded, the
+    groups are in global first-seen order (the smallest global row index of
+    each rname over all ranks, '*' a group of its own) and every rank has
+    every group, possibly empty: written segment-major, a group holds the
+    rows of rank 0, then rank 1, ... -- the ranks hold consecutive blocks of
+    the FASTQ, so that is FASTQ order, as on one GPU."""
     sam_ref = np.asarray(sam_ref, dtype=np.int64)
-    key = np.where(sam_ref < 0, n_refs, sam_ref)            # '*' is its own group
+    key = np.where(sam_ref < 0, n_refs, sam_ref)
     first = np.full(n_refs + 1, -1, dtype=np.int64)
     if len(key):
         k_vals, k_first = np.unique(key, return_index=True)
-        first[k_vals] = k_first + sh.read_base
-    first = sh.min_i64(first)
+        first[k_vals] = k_first + (sh.read_base if sh is not None else 0)
+    if sh is not None:
+        first = sh.min_i64(first)
     groups = [g for g in np.argsort(np.where(first < 0, np.iinfo(np.int64).max, first),
                                     kind='stable') if first[g] >= 0]
     rank_of = np.full(n_refs + 1, len(groups), dtype=np.int64)
     rank_of[groups] = np.arange(len(groups))
-    local = np.argsort(rank_of[key], kind='stable').astype(np.int64)
-    bounds = np.searchsorted(rank_of[key][local], np.arange(len(groups) + 1))
-    segments = [ctx.format_rows_bytes(1, order=local[bounds[g]:bounds[g + 1]])
-                if bounds[g + 1] > bounds[g] else b'' for g in range(len(groups))]
-    parts = sh.gather_segments(segments)
-    if parts is not None:
-        for g in range(len(groups)):
-            for r in range(sh.world):
-                if len(parts[r][g]):
-                    session.write_bytes(prelim_csv, parts[r][g])
+    order = np.argsort(rank_of[key], kind='stable').astype(np.int64)
+    bounds = np.searchsorted(rank_of[key][order], np.arange(len(groups) + 1)).astype(np.int64)
+    if len(groups) == 0:
+        bounds = np.zeros(2, dtype=np.int64)
+    return order, bounds
 
 
 _CLI_OPTIONS = (

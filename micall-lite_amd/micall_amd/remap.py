@@ -26,7 +26,7 @@ import sys
 
 import numpy as np
 
-from . import _native, session
+from . import _native, session, sharded_io
 from .consensus import Pileup, counts_to_conseqs
 from .pipeline import CONSENSUS_Q_CUTOFF, RemapPipeline, write_remap_counts
 from .prelim_map import BOWTIE_THREADS, FIELDNAMES, READ_GAP_OPEN, REF_GAP_OPEN, check_fastq
@@ -81,30 +81,16 @@ def _unmapped_text(ctx, recs):
     return ''.join(out[0]).encode(), ''.join(out[1]).encode()
 
 
-def _write_unmapped(ctx, recs, unmapped1, unmapped2, shard=None):
+def _write_unmapped(ctx, recs, outs):
     """Append the last pass's unmapped reads to the unmapped FASTQs (every
-    rank's, in rank order, written by rank 0 in a sharded run)."""
-    if not (unmapped1 or unmapped2):
+    rank's, in rank order, in a sharded run).  outs: the SharedOutput of
+    unmapped1 and unmapped2 (None where not requested)."""
+    if not any(outs):
         return
     texts = _unmapped_text(ctx, recs)
-    _emit(shard, [(unmapped1, texts[0]), (unmapped2, texts[1])])
-
-
-def _emit(shard, outputs):
-    """Write (handle, bytes) pairs: directly on one GPU; in a sharded run
-    every rank's bytes of each output, rank order, by rank 0."""
-    if shard is None:
-        for handle, data in outputs:
-            if handle and len(data):
-                session.write_bytes(handle, data)
-        return
-    parts = shard.gather_segments([data for _h, data in outputs])
-    if parts is None:
-        return
-    for k, (handle, _data) in enumerate(outputs):
-        for r in range(shard.world):
-            if handle and len(parts[r][k]):
-                session.write_bytes(handle, parts[r][k])
+    for out, text in zip(outs, texts):
+        if out is not None:
+            out.write_bytes([text])
 
 
 class RemapRun(RemapPipeline):
@@ -270,14 +256,21 @@ def remap(fastq1, fastq2, prelim_csv, remap_csv, remap_counts_csv=None, remap_co
             handle.truncate()
     conseqs, new_counts, unmapped_count = run.iterate(conseqs, map_counts, raw_count,
                                                       remap_counts_writer=counts_out)
-    if run.mapped_to is not None:
-        _write_unmapped(ctx, ctx.recs(), unmapped1, unmapped2, sh)
-
     if writer:
         csv.DictWriter(remap_csv, FIELDNAMES, lineterminator=os.linesep).writeheader()
+    # every rank writes its own rows / reads (sharded_io.SharedOutput)
+    rows_out = sharded_io.SharedOutput(sh, remap_csv)
+    unmapped_outs = [sharded_io.SharedOutput(sh, h) if h else None for h in (unmapped1, unmapped2)]
+    if run.mapped_to is not None:
+        _write_unmapped(ctx, ctx.recs(), unmapped_outs)
     if new_counts:
-        unmapped_count += _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv,
-                                            unmapped1, unmapped2, sh)
+        unmapped_count += _write_remap_rows(ctx, run, conseqs, new_counts, rows_out,
+                                            unmapped_outs, sh)
+    if sh is not None:
+        sh.barrier()            # every rank's rows are in the files
+    for out in [rows_out] + unmapped_outs:
+        if out is not None:
+            out.finish()
 
     if remap_conseq_csv and writer:
         # the sequences the reads were last mapped to (remap.py:637-643)
@@ -300,7 +293,7 @@ def _write_final_counts(writer, new_counts, unmapped_count):
     writer.writerow(dict(type='unmapped', count=unmapped_count))
 
 
-def _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv, unmapped1, unmapped2, shard=None):
+def _write_remap_rows(ctx, run, conseqs, new_counts, rows_out, unmapped_outs, shard=None):
     """remap.csv rows of the last pass, then the mixed-reference pairs mapped
     again, one reference at a time (remap.py:612-634).  new_counts gains
     each re-mapping's counts; returns the unmapped lines they add.
@@ -309,12 +302,9 @@ def _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv, unmapped1, unmap
     pairs; the references are re-mapped in their global order of first
     split (rank order, then each rank's order), every rank taking part in
     each one (with its own split pairs, possibly none), and the rows and
-    unmapped reads are written in rank order."""
+    unmapped reads land in rank order."""
     keep_rows, splits = split_mixed_references(ctx, ctx.recs())
-    if shard is None:
-        ctx.write_rows(remap_csv, 1, order=keep_rows)
-    else:
-        _emit(shard, [(remap_csv, ctx.format_rows_bytes(1, order=keep_rows))])
+    rows_out.write_rows(ctx, 1, keep_rows, [0, len(keep_rows)])
     order = list(splits)
     if shard is not None:
         order = []
@@ -335,8 +325,8 @@ def _write_remap_rows(ctx, run, conseqs, new_counts, remap_csv, unmapped1, unmap
         counts, unmapped = run.map_to_reference({name: conseqs[name]})
         extra_unmapped += unmapped
         new_counts.update(counts)
-        _write_unmapped(ctx, ctx.recs(), unmapped1, unmapped2, shard)
-        _emit(shard, [(remap_csv, ctx.format_rows_bytes(1) if seqs else b'')])
+        _write_unmapped(ctx, ctx.recs(), unmapped_outs)
+        rows_out.write_rows(ctx, 1, None, [0, len(seqs)])
     return extra_unmapped
 
 

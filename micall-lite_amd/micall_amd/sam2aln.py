@@ -20,17 +20,21 @@ MAX_PROP_N = 0.5          # sam2aln.py:25
 
 
 def sam2aln(remap_csv, aligned_csv, insert_csv=None, failed_csv=None, nthreads=None):
-    """sam2aln.sam2aln (sam2aln.py:395-478)."""
+    """sam2aln.sam2aln (sam2aln.py:395-478).  In a sharded job rank 0
+    computes and writes while the other ranks wait (session.writer_stage)."""
     if len(SAM2ALN_Q_CUTOFFS) != 1:
         raise NotImplementedError('the device merge takes one q-cutoff per pass')
-    text = session.read_text(remap_csv)
-    ctx = session.context()
-    ctx.sam2aln_csv(text, q_cutoff=SAM2ALN_Q_CUTOFFS[0], max_prop_n=MAX_PROP_N)
-    if insert_csv:
-        insert_csv.write(ctx.sam2aln_output('insert'))
-    if failed_csv:
-        failed_csv.write(ctx.sam2aln_output('failed'))
-    aligned_csv.write(ctx.sam2aln_output('aligned'))
+    with session.writer_stage(aligned_csv, insert_csv, failed_csv) as stage:
+        if not stage.active:
+            return
+        text = session.read_text(remap_csv)
+        ctx = session.context()
+        ctx.sam2aln_csv(text, q_cutoff=SAM2ALN_Q_CUTOFFS[0], max_prop_n=MAX_PROP_N)
+        if insert_csv:
+            insert_csv.write(ctx.sam2aln_output('insert'))
+        if failed_csv:
+            failed_csv.write(ctx.sam2aln_output('failed'))
+        aligned_csv.write(ctx.sam2aln_output('aligned'))
 
 
 def parseArgs():

@@ -95,8 +95,9 @@ def _file_key(*paths):
 
 def load_fastq(fastq1, fastq2=None):
     """The context with these FASTQ files resident (loaded once).  In a
-    sharded job only this rank's block of units is resident, and the
-    shard's read_base is the block's first read."""
+    sharded job only this rank's block of units is resident (read from its
+    share of the files, sharded_io.load_reads), and the shard's read_base is
+    the block's first read."""
     global _key
     sh = shard()
     ctx = context()
@@ -105,11 +106,49 @@ def load_fastq(fastq1, fastq2=None):
         if sh is None:
             ctx.reads_load_fastq(fastq1, fastq2)
         else:
-            _n, first_unit = ctx.reads_load_fastq_part(fastq1, fastq2, sh.rank, sh.world)
+            from . import sharded_io
+            first_unit = sharded_io.load_reads(ctx, sh, fastq1, fastq2)
             sh.read_base = 2 * first_unit if fastq2 else first_unit
         _key = key
         ctx.fastq_line_count = ctx.fastq_lines()
     return ctx
+
+
+class writer_stage:
+    """A stage that one process computes and writes while the other ranks of
+    a sharded job wait (sam2aln, aln2counts, the InterOp reports).  Every rank
+    opened (and so truncated) the stage's output files before the call,
+    as bin/micall does on every rank: the entry barrier keeps rank 0 from
+    writing before the last of those opens; on exit rank 0 flushes the given
+    handles and the barrier holds the others until the files are complete.
+    A failure on rank 0 is raised on every rank.  `active` is True on the
+    process that does the work.
+
+        with session.writer_stage(out1, out2) as st:
+            if st.active:
+                ...compute and write..."""
+
+    def __init__(self, *handles):
+        self.handles = handles
+        self.sh = shard()
+        self.active = self.sh is None or self.sh.rank == 0
+
+    def __enter__(self):
+        if self.sh is not None:
+            self.sh.barrier()
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        if self.active:
+            for h in self.handles:
+                flush = getattr(h, 'flush', None)
+                if flush is not None and not getattr(h, 'closed', False):
+                    flush()
+        if self.sh is not None:
+            failed = int(self.sh.sum_i64([1 if exc_type is not None else 0])[0])
+            if failed and exc_type is None:
+                raise RuntimeError('the stage failed on rank 0 of the sharded job')
+        return False
 
 
 def read_text(handle):
@@ -133,19 +172,13 @@ def read_text(handle):
     return handle.read()
 
 
-def _identity(handle):
-    """(device, inode, size) of an open file, None for a non-file stream."""
-    try:
-        handle.flush()
-        st = os.fstat(handle.fileno())
-    except (AttributeError, OSError, ValueError):
-        return None
-    return st.st_dev, st.st_ino, st.st_size
-
-
 def write_bytes(handle, data):
     """Write ASCII bytes to an open text file (through its binary buffer when
-    it is a UTF-8 / ASCII file that writes '\n' as is)."""
+    it is a UTF-8 / ASCII file that writes '\n' as is), or to a binary one."""
+    import io
+    if not isinstance(handle, io.TextIOBase) and 'b' in getattr(handle, 'mode', 'b'):
+        handle.write(bytes(data))
+        return
     raw = getattr(handle, 'buffer', None)
     enc = (getattr(handle, 'encoding', '') or '').lower().replace('-', '')
     if (raw is not None and enc in ('utf8', 'ascii') and os.linesep == '\n' and
@@ -156,50 +189,60 @@ def write_bytes(handle, data):
         handle.write(bytes(data).decode())
 
 
-def _written_checksum(handle):
-    """Checksum of the file behind a handle opened for writing (read back
-    through its path, after checking that the path is still that file)."""
-    ident = _identity(handle)
-    name = getattr(handle, 'name', None)
-    if ident is None or not isinstance(name, str):
-        return None, None
+def _file_identity(handle):
+    """(device, inode, size, mtime, ctime) of the file behind an open
+    handle, None for a non-file stream.  ctime cannot be set from user
+    space: any later write to the file changes it."""
     try:
-        fd = os.open(name, os.O_RDONLY)
-    except OSError:
-        return None, None
-    try:
-        st = os.fstat(fd)
-        if (st.st_dev, st.st_ino) != ident[:2]:
-            return None, None
-        return ident, _native.file_checksum(fd)
-    finally:
-        os.close(fd)
+        st = os.fstat(handle.fileno())
+    except (AttributeError, OSError, ValueError):
+        return None
+    return st.st_dev, st.st_ino, st.st_size, st.st_mtime_ns, st.st_ctime_ns
 
 
-def prelim_written(ctx, handle, seed_names):
+def prelim_written(ctx, handle, seed_names, checksum=None):
     """Record that prelim_map() wrote `handle` from the device records that
-    are resident now (ctx.map_serial) for these seeds."""
+    are resident now (ctx.map_serial) for these seeds: the file's identity
+    after the last write and, when known, (crc32, size) of its content as
+    formatted (no read-back)."""
     global _prelim
-    ident, sums = _written_checksum(handle) if is_writer() else (None, None)
-    _prelim = dict(identity=ident, checksum=sums, serial=ctx.map_serial, key=_key,
+    ident = None
+    if is_writer():
+        try:
+            handle.flush()
+        except (AttributeError, OSError, ValueError):
+            pass
+        ident = _file_identity(handle)
+    _prelim = dict(identity=ident, checksum=checksum, serial=ctx.map_serial, key=_key,
                    seeds=list(seed_names))
 
 
 def prelim_resident(ctx, handle, seed_names):
     """True when `handle` is the prelim.csv this process's last prelim_map()
-    wrote, unchanged (the same file, size and crc32 / adler32 of its
-    content), and that pass's records are still resident: remap() then
-    takes the prelim rows from the device instead of parsing them again.  In
-    a sharded job rank 0 checks the file and every rank its own records."""
+    wrote, unchanged, and that pass's records are still resident: remap()
+    then takes the prelim rows from the device instead of parsing them
+    again.  Unchanged: the same file identity (device, inode, size, mtime,
+    ctime); failing that, the same size and crc32 as the rows formatted (a
+    file rewritten with the same bytes; read back only then).  In a sharded
+    job rank 0 checks the file and every rank its own records."""
     p = _prelim
     ok = (p is not None and p['serial'] == ctx.map_serial and p['key'] == _key and
           p['key'] is not None and p['seeds'] == list(seed_names))
     if ok and is_writer():
-        ok = p['identity'] is not None and _identity(handle) == p['identity']
+        ident = _file_identity(handle)
+        ok = ident is not None and p['identity'] is not None
+        if ok and ident != p['identity']:
+            ok = False
+            want = p['checksum']
+            if want is not None and ident[2] == want[1] and ident[:2] == p['identity'][:2]:
+                try:
+                    ok = _native.file_crc32(handle.fileno()) == (want[1], want[0])
+                except (OSError, ValueError, _native.NativeError):
+                    ok = False
         if ok:
             try:
-                ok = _native.file_checksum(handle.fileno()) == p['checksum']
-            except (OSError, ValueError, _native.NativeError):
+                ok = handle.tell() == 0
+            except (OSError, ValueError):
                 ok = False
     sh = shard()
     if sh is not None:

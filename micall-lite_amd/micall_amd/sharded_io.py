@@ -1,0 +1,413 @@
+"""
+File input and output of a sharded job (one process per GPU under torchrun).
+
+The reference reads each FASTQ once per bowtie2 pass and writes every output
+file from its one process (prelim_map.py:114-151, remap.py:612-658,
+censor_fastq.py:58-96).  In a job of W ranks each rank here
+
+  * reads its 1/W share of every FASTQ file (`stage_fastq`): the gzip members
+    that start in its byte range (a plain file: the byte range), frames the
+    text into four-line records from the line counts of the ranks before it,
+    passes the bytes in front of its first record to the rank before, and, for
+    a pair of files, exchanges whole records so that its R1 and R2 blocks hold
+    the same reads.  A file that cannot be split that way (one gzip member, as
+    bcl2fastq writes it; a blank line where a record starts) is decoded whole
+    by every rank, which keeps its records by count -- the round-3 behaviour;
+  * writes its own rows of every output file (`SharedOutput`) with pwrite at
+    offsets computed from the all-gathered segment sizes, so the file holds
+    the rows in single-GPU order (segment 0 of rank 0, rank 1, ..., then
+    segment 1, ...) and no rank's text travels to another.
+
+Counters (bytes decoded, bytes written) go to `IO_STATS` so a test can check
+that each rank did about 1/W of the work.
+"""
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from . import _native
+
+IO_STATS = dict(fastq_file_bytes=0, fastq_text_bytes=0, fastq_mode=None, written_bytes=0)
+
+
+def reset_stats():
+    IO_STATS.update(fastq_file_bytes=0, fastq_text_bytes=0, fastq_mode=None, written_bytes=0)
+
+
+# ---- collective helpers ------------------------------------------------------
+def _agree_ok(sh, ok):
+    """True on every rank when `ok` holds on every rank."""
+    return bool(sh.min_i64([1 if ok else 0])[0])
+
+
+def _checked(sh, fn):
+    """Run fn() on every rank; if it raises on any rank, raise on all of them
+    (so no rank waits in a collective for one that failed)."""
+    err = None
+    try:
+        out = fn()
+    except Exception as ex:    # re-raised below, after the agreement
+        err, out = ex, None
+    if not _agree_ok(sh, err is None):
+        if err is not None:
+            raise err
+        raise _native.NativeError('a FASTQ read failed on another rank of the job')
+    return out
+
+
+def _p2p(sh, sends, recv_sizes):
+    """Point-to-point exchange of byte blocks: sends = {peer: uint8 array},
+    recv_sizes = {peer: bytes}; returns {peer: bytes received}."""
+    torch, dist = sh.torch, sh.dist
+    dev = sh._text_device()
+    ops, bufs, keep = [], {}, []
+    for peer, n in sorted(recv_sizes.items()):
+        if n > 0:
+            t = torch.empty(int(n), dtype=torch.uint8, device=dev)
+            bufs[peer] = t
+            ops.append(dist.P2POp(dist.irecv, t, peer))
+    for peer, data in sorted(sends.items()):
+        if len(data) > 0:
+            t = torch.from_numpy(np.array(data, dtype=np.uint8, copy=True)).to(dev)
+            keep.append(t)
+            ops.append(dist.P2POp(dist.isend, t, peer))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return {peer: t.cpu().numpy().tobytes() for peer, t in bufs.items()}
+
+
+# ---- FASTQ staging -------------------------------------------------------------
+class _Frame:
+    """One file's framing on this rank after the boundary exchange."""
+
+    def __init__(self, fq, first, count, total, lines):
+        self.fq, self.first, self.count, self.total, self.lines = fq, first, count, total, lines
+
+
+def _open_all(sh, sources, part, parts):
+    def one(src):
+        path, fd = src
+        return _native.Fastq(path, fd if fd is not None else -1, part, parts)
+    if len(sources) == 1:
+        return [one(sources[0])]
+    with ThreadPoolExecutor(len(sources)) as ex:
+        return list(ex.map(one, sources))
+
+
+def _frame_sharded(sh, fq, strict):
+    """Frame this rank's share of a file split by member / byte range and
+    move the bytes before its first record to the rank before.  Returns a
+    _Frame, or None when the split cannot be used (then no rank uses it)."""
+    W, r = sh.world, sh.rank
+    inf = fq.info
+    rows = sh._gather_sizes([inf['mode'], inf['c0'], inf['c1'], inf['bytes'], inf['newlines'],
+                             inf['ends_nl'], inf['starts_nl'], inf['file_size']])
+    mode, c0, c1, nbytes, nl, ends_nl, starts_nl, size = (rows[:, k] for k in range(8))
+    chain = (all(m in (1, 2) for m in mode) and c0[0] == 0 and c1[W - 1] == size[0] and
+             all(c1[k] == c0[k + 1] for k in range(W - 1)))
+    if not chain:
+        return None
+    line0 = int(nl[:r].sum())
+    starts_line = True
+    for s in range(r - 1, -1, -1):     # the last non-empty part before this one
+        if nbytes[s] > 0:
+            starts_line = bool(ends_nl[s])
+            break
+    first_off, count, first_line, blank, tail_cr = fq.frame(line0, starts_line)
+    fr = sh._gather_sizes([first_off, count, first_line, blank, tail_cr])
+    counts, first_lines = fr[:, 1], fr[:, 2]
+    blank_any = bool(fr[:, 3].any())
+    for k in range(W - 1):   # a '\r'-only record-start line finished by the next part's '\n'
+        if fr[k, 4] and starts_nl[k + 1]:
+            blank_any = True
+    mean = float(nbytes.sum()) / W
+    usable = (all(counts > 0) and (strict or not blank_any) and
+              float(nbytes.min()) >= 0.5 * mean and
+              all(first_lines[k] == 4 * int(counts[:k].sum()) for k in range(W)))
+    if not usable:
+        return None
+    prefix = fq.view(0, first_off).tobytes()
+    prefixes = sh.all_gather_bytes(prefix)
+    back = prefixes[r + 1] if r + 1 < W else b''
+    fq.splice(first_off, fq.size(), back=back)
+    fq.frame(0, True)   # local record offsets of the records now held
+    return _Frame(fq, int(counts[:r].sum()), int(counts[r]), int(counts.sum()), int(nl.sum()))
+
+
+def _frame_whole(fq, strict):
+    """A whole file held by every rank: its records by four-line framing.
+    None when a blank line sits where a record starts and the caller parses
+    records as the ingest does (strict=False)."""
+    _off, count, _line, blank, _tail = fq.frame(0, True)
+    if blank and not strict:
+        return None
+    return _Frame(fq, 0, count, count, fq.info['newlines'])
+
+
+def _keep_records(fr, lo, hi):
+    """Cut a framed text down to its global records [lo, hi)."""
+    a = fr.fq.record_offset(lo - fr.first)
+    b = fr.fq.record_offset(hi - fr.first)
+    fr.fq.splice(a, b)
+    fr.fq.frame(0, True)
+    fr.first, fr.count = lo, hi - lo
+
+
+def _realign(sh, fr, target):
+    """Exchange whole records so that this rank holds records target[rank]
+    of a file whose ranks hold contiguous blocks in rank order."""
+    W, r = sh.world, sh.rank
+    held = sh._gather_sizes([fr.first, fr.first + fr.count])
+    sends, send_sizes = {}, np.zeros(W, dtype=np.int64)
+    for s in range(W):
+        if s == r:
+            continue
+        o0, o1 = max(fr.first, target[s][0]), min(fr.first + fr.count, target[s][1])
+        if o1 > o0:
+            a, b = fr.fq.record_offset(o0 - fr.first), fr.fq.record_offset(o1 - fr.first)
+            sends[s] = fr.fq.view(a, b)
+            send_sizes[s] = b - a
+    matrix = sh._gather_sizes(send_sizes)            # [sender, receiver]
+    got = _p2p(sh, sends, {s: int(matrix[s, r]) for s in range(W) if s != r})
+    t0, t1 = target[r]
+    o0, o1 = max(fr.first, t0), min(fr.first + fr.count, t1)
+    if o1 > o0:
+        a, b = fr.fq.record_offset(o0 - fr.first), fr.fq.record_offset(o1 - fr.first)
+    else:
+        a = b = 0
+    front = b''.join(got[s] for s in range(W) if s != r and held[s, 0] < fr.first and s in got)
+    back = b''.join(got[s] for s in range(W) if s != r and held[s, 0] > fr.first and s in got)
+    if o1 <= o0:   # nothing of our own: everything came from the others, in rank order
+        front = b''.join(got[s] for s in range(W) if s in got)
+        back = b''
+    fr.fq.splice(a, b, front=front, back=back)
+    fr.fq.frame(0, True)
+    fr.first, fr.count = t0, t1 - t0
+
+
+def stage_fastq(sh, sources, strict=False):
+    """This rank's block of FASTQ records from every source file.
+
+    sources: [(path, fd)] of one file (unpaired, or the censor's one file) or
+    two (R1, R2; their blocks hold the same records).  strict=True frames
+    every four lines as a record (the censor's zip_longest over lines,
+    censor_fastq.py:58); otherwise a blank record-start line (which the
+    ingest's parser skips) makes the files be read whole.
+
+    Returns dict(frames=[_Frame per source], first=first record of the
+    block, units=records in the block, total=records in the file,
+    lines=newlines of source 0 (raw_count), mode='members'|'whole'); None
+    when the ingest should fall back to the whole-file loader
+    (mh_reads_load_fastq_part)."""
+    W, r = sh.world, sh.rank
+    fqs = _checked(sh, lambda: _open_all(sh, sources, r, W))
+    frames = [_checked(sh, lambda fq=fq: _frame_sharded(sh, fq, strict)) for fq in fqs]
+    IO_STATS['fastq_file_bytes'] += sum(fq.info['file_bytes_read'] for fq in fqs)
+    if all(f is None for f in frames):
+        for fq in fqs:
+            fq.close()
+        if not strict:
+            return None            # every rank reads the files whole (the part loader)
+        fqs = _checked(sh, lambda: _open_all(sh, sources, 0, 1))
+        IO_STATS['fastq_file_bytes'] += sum(fq.info['file_bytes_read'] for fq in fqs)
+        frames = [_frame_whole(fq, strict) for fq in fqs]
+        mode = 'whole'
+    else:
+        for k, f in enumerate(frames):
+            if f is None:          # this one is read whole, its partner split
+                fqs[k].close()
+                whole = _checked(sh, lambda k=k: _open_all(sh, [sources[k]], 0, 1)[0])
+                IO_STATS['fastq_file_bytes'] += whole.info['file_bytes_read']
+                frames[k] = _frame_whole(whole, strict)
+                if frames[k] is None:
+                    for f2 in frames:
+                        if f2 is not None:
+                            f2.fq.close()
+                    return None
+        mode = 'members'
+    totals = [f.total for f in frames]
+    if len(set(totals)) != 1:
+        raise _native.NativeError('paired FASTQ files hold {} and {} reads'.format(*totals))
+    total = totals[0]
+    # the block of this rank: the first split file's, or the floor split
+    lead = next((f for f in frames if f.total == total and f.count != f.total), None)
+    if lead is not None:
+        blocks = sh._gather_sizes([lead.first, lead.first + lead.count])
+        target = [(int(a), int(b)) for a, b in blocks]
+    else:
+        target = [(total * k // W, total * (k + 1) // W) for k in range(W)]
+    for f in frames:
+        if f is lead:
+            continue
+        if f.count == f.total and W > 1:
+            _keep_records(f, *target[r])       # held whole: keep the block
+        else:
+            _realign(sh, f, target)
+    IO_STATS['fastq_text_bytes'] += sum(f.fq.size() for f in frames)
+    IO_STATS['fastq_mode'] = mode
+    return dict(frames=frames, first=target[r][0], units=target[r][1] - target[r][0], total=total,
+                lines=frames[0].lines, mode=mode)
+
+
+def load_reads(ctx, sh, path1, path2=None):
+    """The sharded ingest of prelim_map / remap: this rank's block of pairs
+    (or reads) resident in ctx.  Returns the first unit of the block."""
+    st = stage_fastq(sh, [(path1, None)] + ([(path2, None)] if path2 else []))
+    if st is None:
+        _n, first_unit = ctx.reads_load_fastq_part(path1, path2, sh.rank, sh.world)
+        IO_STATS['fastq_mode'] = 'part-loader'
+        return first_unit
+    fr = st['frames']
+    ctx.reads_load_staged(fr[0].fq, fr[1].fq if len(fr) > 1 else None, (-1, -1, -1, -1),
+                          st['lines'])
+    for f in fr:
+        f.fq.close()
+    return st['first']
+
+
+# ---- output ----------------------------------------------------------------------
+def _binary_fd(handle):
+    """Descriptor of a seekable binary file handle (not appending), else None."""
+    import io
+    try:
+        if isinstance(handle, io.TextIOBase) or not handle.seekable():
+            return None
+        if 'a' in getattr(handle, 'mode', ''):
+            return None
+        return handle.fileno()
+    except (AttributeError, OSError, ValueError, io.UnsupportedOperation):
+        return None
+
+
+class SharedOutput:
+    """One output file, written by every rank of a sharded job (sh) or by
+    the one process (sh None).
+
+    Every rank opened the same path (bin/micall opens its outputs on every
+    rank).  place(lens) all-gathers each rank's segment sizes and returns
+    this rank's file offsets, segment-major (segment 0 of rank 0, 1, ...,
+    then segment 1 ...); the ranks then pwrite their own bytes there.  When
+    the handles are not one plain file on every rank (a StringIO, a pipe),
+    `direct` is False and the bytes go to rank 0, which writes them through
+    its handle (Shard.gather_segments)."""
+
+    def __init__(self, sh, handle, binary=False):
+        self.sh, self.handle = sh, handle
+        if not handle:
+            fd = None
+        elif binary:
+            fd = _binary_fd(handle)
+        else:
+            fd = _native._plain_fd(handle)
+        ident = (0, 0)
+        pos = 0
+        if fd is not None:
+            handle.flush()
+            st = os.fstat(fd)
+            ident = (st.st_dev, st.st_ino)
+            pos = os.lseek(fd, 0, os.SEEK_CUR)
+        self.fd = fd
+        self.written = []     # (offset, length, crc) of this rank's segments
+        if sh is None:
+            self.direct = fd is not None
+            self.end = pos
+            return
+        rows = sh._gather_sizes([1 if fd is not None else 0, ident[0], ident[1]])
+        self.direct = bool(rows[:, 0].all()) and len({(a, b) for _f, a, b in rows}) == 1
+        self.end = int(sh.sum_i64([pos if sh.rank == 0 else 0])[0]) if self.direct else None
+
+    @property
+    def rank(self):
+        return 0 if self.sh is None else self.sh.rank
+
+    def place(self, lens):
+        """File offsets of this rank's segments (lens: bytes per segment)."""
+        lens = np.asarray(lens, dtype=np.int64)
+        if len(lens) == 0:
+            return np.zeros(0, dtype=np.int64)
+        if self.sh is None:
+            offs = self.end + np.concatenate([[0], np.cumsum(lens)[:-1]])
+            self.end += int(lens.sum())
+        else:
+            all_lens = self.sh._gather_sizes(lens)            # [rank, segment]
+            seg_total = all_lens.sum(axis=0)
+            seg_base = self.end + np.concatenate([[0], np.cumsum(seg_total)[:-1]])
+            offs = seg_base + all_lens[:self.sh.rank].sum(axis=0)
+            self.end += int(seg_total.sum())
+        IO_STATS['written_bytes'] += int(lens.sum())
+        return offs
+
+    def write_bytes(self, segments):
+        """Write this rank's byte segments (same count on every rank)."""
+        from . import session
+        if not self.direct:
+            if self.sh is None:
+                for data in segments:
+                    if len(data) and self.handle:
+                        session.write_bytes(self.handle, data)
+                return
+            parts = self.sh.gather_segments(segments)
+            if parts is not None and self.handle:
+                for g in range(len(segments)):
+                    for rr in range(self.sh.world):
+                        if len(parts[rr][g]):
+                            session.write_bytes(self.handle, parts[rr][g])
+            return
+        import zlib
+        offs = self.place([len(x) for x in segments])
+        for off, data in zip(offs, segments):
+            mv = memoryview(data).cast('B')
+            at = 0
+            while at < len(mv):
+                at += os.pwrite(self.fd, mv[at:], int(off) + at)
+            self.written.append((int(off), len(mv), zlib.crc32(mv)))
+
+    def write_rows(self, ctx, style, order, seg_rows):
+        """Format rows order[...] (None: every read) in segments (seg_rows
+        bounds) and write them: straight from the formatting threads when
+        direct."""
+        if not self.direct:
+            if order is None:
+                order = np.arange(ctx.reads_count()[0], dtype=np.int64)
+            segs = [ctx.format_rows_bytes(style, order=np.asarray(order)[a:b]) if b > a else b''
+                    for a, b in zip(seg_rows[:-1], seg_rows[1:])]
+            self.write_bytes(segs)
+            return
+        lens = ctx.format_segments(style, order, seg_rows)
+        offs = self.place(lens)
+        crcs = ctx.write_segments(self.fd, offs)
+        self.written += [(int(o), int(n), int(c)) for o, n, c in zip(offs, lens, crcs)]
+
+    def finish(self):
+        """After every rank's writes (sharded callers end with a barrier):
+        rank 0's handle is positioned at the end of what was written."""
+        if self.direct and self.rank == 0 and self.handle:
+            self.handle.seek(self.end)
+
+    def crc_of_file(self, head=b''):
+        """(crc32, size) of the whole file as written, when it starts at
+        offset 0 with `head` (rank 0's bytes written through its handle
+        before) and this object wrote the rest; None otherwise."""
+        import zlib
+        mine = np.array(self.written, dtype=np.int64).reshape(-1, 3)
+        if self.sh is None:
+            segs = sorted(tuple(int(x) for x in row) for row in mine)
+        else:
+            sh = self.sh
+            n = sh._gather_sizes([len(mine)])[:, 0]
+            m = max(int(n.max()), 1)
+            pad = np.zeros((m, 3), dtype=np.int64)
+            pad[:len(mine)] = mine
+            t = sh.torch.as_tensor(pad.reshape(-1), device=sh.device)
+            allw = sh._gather(t).cpu().numpy().reshape(sh.world, m, 3)
+            segs = sorted(tuple(int(x) for x in allw[k, j]) for k in range(sh.world)
+                          for j in range(int(n[k])))
+        crc, at = zlib.crc32(head), len(head)
+        for off, ln, c in segs:
+            if off != at:
+                return None
+            crc = _native.crc32_combine(crc, c, ln)
+            at += ln
+        return crc, at

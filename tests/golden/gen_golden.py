@@ -42,6 +42,12 @@ itself produced for them.  Sections:
            and on edge-case aligned.csv texts over a small project file cut
            from HIV-1 pol (tests/golden/aln2counts_edge.json).
 
+  chain_tail  the rest of bin/micall's run_sample (:171-188) on each chain
+           case's remap.csv: the reference sam2aln(remap_csv, aligned_csv)
+           and aln2counts(aligned, nuc, amino, coord_ins, conseq) called as
+           bin/micall calls them; align.csv, nuc.csv, amino.csv, insert.csv
+           and conseq.csv under tests/golden/chain/<case>/.
+
   e2e      the stock reference prelim_map() + remap() (nthreads=1, so its
            pileup runs without a process pool and is deterministic) with
            oracle/shim_bin/bowtie2 standing in for bowtie2, on small committed
@@ -828,6 +834,28 @@ def gen_chain():
         finally:
             os.chdir(cwd)
             shutil.rmtree(work, ignore_errors=True)
+
+
+def gen_chain_tail():
+    """bin/micall:171-188 after remap, on the chain cases' remap.csv."""
+    import gzip
+    refharness.setup()
+    from micall.core.aln2counts import aln2counts
+    from micall.core.sam2aln import sam2aln
+    for name in ('c5_unpaired300', 'c5_paired251'):
+        d = os.path.join(HERE, 'chain', name)
+        with gzip.open(os.path.join(d, 'remap.csv.gz'), 'rt') as f:
+            text = f.read()
+        align = io.StringIO()
+        sam2aln(remap_csv=io.StringIO(text), aligned_csv=align)
+        outs = {k: io.StringIO() for k in ('nuc', 'amino', 'insert', 'conseq')}
+        aln2counts(aligned_csv=io.StringIO(align.getvalue()), nuc_csv=outs['nuc'],
+                   amino_csv=outs['amino'], coord_ins_csv=outs['insert'],
+                   conseq_csv=outs['conseq'])
+        _gz_write(os.path.join(d, 'align.csv.gz'), align.getvalue())
+        for k, v in outs.items():
+            _gz_write(os.path.join(d, k + '.csv.gz'), v.getvalue())
+        print('chain tail:', name, align.getvalue().count('\n') - 1, 'aligned rows')
 
 
 def gen_s2a():

@@ -79,7 +79,7 @@ def test_pool_grows_with_a_larger_batch():
                                        True), ref, seqs)
         par.test_mate_rescue_vs_oracle(c, oracle.LOCAL)
         par.test_map_pol_vs_oracle(c, oracle.E2E)
-        assert c.retry_counts() == dict(cigar_pool=0, pileup_events=0, token_bytes=0)
+        assert c.retry_counts() == dict(cigar_pool=0, pileup_events=0, token_bytes=0, gotoh_wait=0)
     finally:
         c.close()
 
@@ -93,4 +93,24 @@ def test_caps_reset_to_library_sizing(tiny):
     par._gpu_alns(tiny, ['HIV1B-pol-seed'], [par.POL], oracle.LOCAL, seqs, quals, True)
     tiny.pileup(0, 20, [len(par.POL)])
     tiny.pileup_fetch()
-    assert tiny.retry_counts() == dict(cigar_pool=1, pileup_events=0, token_bytes=0)
+    assert tiny.retry_counts() == dict(cigar_pool=1, pileup_events=0, token_bytes=0, gotoh_wait=0)
+
+
+def test_gotoh_wait_timeout_is_retried():
+    """k_gotoh's strips wait for the strip above by polling its boundary
+    cells; a wait past its real-time limit fails the launch (-4) and the
+    batch runs once more with the default 20 s limit.  With a first-attempt
+    limit of 1 tick (10 ns) some strip of a 3 kb alignment gives up, the retry
+    runs, and the result still equals the oracle (_gotoh2.c:442-541)."""
+    c = _native.Context(0)
+    try:
+        c.test_set_gotoh_wait(1)
+        rng = np.random.default_rng(3)
+        conseq = par.synth.sample_genome(par.POL, rng, 0.1, 0.004).tobytes().decode()[100:3000]
+        mat, alpha = [5, -4, -4, -4, 0, -4, 5, -4, -4, 0, -4, -4, 5, -4, 0, -4, -4, -4, 5, 0,
+                      0, 0, 0, 0, 0], 'ACGT?'
+        want = oracle.gotoh_align(par.POL, conseq, 15, 3, True, alpha, mat)
+        assert c.gotoh_align(par.POL, conseq, 15, 3, True, alpha, mat) == want
+        assert c.retry_counts()['gotoh_wait'] == 1
+    finally:
+        c.close()

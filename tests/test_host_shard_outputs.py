@@ -1,12 +1,15 @@
 """The file assembly of a sharded run on the CPU (gloo, world sizes 2 and 3):
-every rank formats the rows of its own contiguous block of reads and rank 0
-writes them, and the bytes must be the ones a single GPU writes.
+every rank formats the rows of its own contiguous block of reads and writes
+them at its offsets of the shared file (sharded_io.SharedOutput: sizes
+all-gathered, pwrite), or -- when the handles are not one plain file on every
+rank -- sends them to rank 0, which writes them.  The bytes must be the ones
+a single GPU writes.
 
 - prelim.csv (prelim_map.py:142-151): rname groups in global first-seen
-  order, FASTQ order within a group (micall_amd.prelim_map._write_sharded
-  against grouped_order over the whole set);
-- remap.csv rows / unmapped FASTQs (remap.py:612-634): rank order
-  (micall_amd.remap._emit);
+  order, FASTQ order within a group (prelim_map.grouped_segments over the
+  ranks against grouped_order over the whole set), and the crc32 the job
+  computes for it without reading it back;
+- remap.csv rows / unmapped FASTQs (remap.py:612-634): rank order;
 - the split references' global order (Shard.all_gather_bytes).
 
 A fake context stands in for the device: it formats read i as one text line
@@ -21,8 +24,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from micall_amd import prelim_map as pm
-from micall_amd import remap as rm
-from micall_amd import session
+from micall_amd import session, sharded_io
 from micall_amd.pipeline import Shard
 
 N_READS = 1001          # not a multiple of the world size
@@ -40,12 +42,31 @@ def _line(i, ref):
 
 
 class _RowsCtx:
+    """format_rows_bytes / format_segments / write_segments of the device
+    context over text lines (the segments API formats, keeps, then writes at
+    the given file offsets)."""
+
     def __init__(self, refs, lo):
         self.refs, self.lo = refs, lo
+        self.kept = None
+
+    def _text(self, order):
+        return b''.join(_line(self.lo + int(i), self.refs[self.lo + int(i)]) for i in order)
 
     def format_rows_bytes(self, style, first=0, n=None, order=None):
         assert style == 1
-        return b''.join(_line(self.lo + int(i), self.refs[self.lo + int(i)]) for i in order)
+        return self._text(order)
+
+    def format_segments(self, style, order, seg_rows):
+        assert style == 1
+        self.kept = [self._text(order[a:b]) for a, b in zip(seg_rows[:-1], seg_rows[1:])]
+        return np.array([len(t) for t in self.kept], dtype=np.int64)
+
+    def write_segments(self, fd, offsets, crc=True):
+        import zlib
+        for t, off in zip(self.kept, offsets):
+            os.pwrite(fd, t, int(off))
+        return np.array([zlib.crc32(t) for t in self.kept], dtype=np.uint32)
 
 
 def _block(rank, world, n):
@@ -53,6 +74,7 @@ def _block(rank, world, n):
 
 
 def _worker(rank, world, port, out_dir):
+    import zlib
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
@@ -60,13 +82,46 @@ def _worker(rank, world, port, out_dir):
         lo, hi = _block(rank, world, N_READS)
         sh = Shard(rank, world, read_base=lo)
         ctx = _RowsCtx(refs, lo)
-        # prelim.csv groups
-        out = io.StringIO()
-        pm._write_sharded(ctx, sh, refs[lo:hi], N_REFS, out)
+        want = b''.join(_line(i, refs[i]) for i in pm.grouped_order(refs))
+        head = b'qname,flag,rname\n'
+        for direct in (True, False):
+            # prelim.csv groups: every rank opened the file, rank 0 wrote the header
+            path = os.path.join(out_dir, 'prelim%d.csv' % direct)
+            f = open(path, 'w') if direct else io.StringIO()
+            sh.barrier()
+            if rank == 0:
+                f.write(head.decode())
+            out = sharded_io.SharedOutput(sh, f)
+            assert out.direct == direct
+            order, bounds = pm.grouped_segments(refs[lo:hi], N_REFS, sh)
+            out.write_rows(ctx, 1, order, bounds)
+            sh.barrier()
+            out.finish()
+            crc = out.crc_of_file(head) if out.direct else None
+            if direct:
+                f.close()
+                text = open(path, 'rb').read()
+                assert text == head + want
+                assert crc == (zlib.crc32(text), len(text))
+            elif rank == 0:
+                assert f.getvalue().encode() == head + want
+            else:
+                assert f.getvalue() == ''
         # remap.csv rows / unmapped reads in rank order, two outputs at once
         a, b = io.StringIO(), io.StringIO()
+        pa = os.path.join(out_dir, 'rows.csv')
+        fa = open(pa, 'w')
+        sh.barrier()
         mine = [('r%d\n' % i).encode() for i in range(lo, hi)]
-        rm._emit(sh, [(a, b''.join(mine)), (b, b''.join(mine[::2]))])
+        outs = [sharded_io.SharedOutput(sh, h) for h in (a, b, fa)]
+        outs[0].write_bytes([b''.join(mine)])
+        outs[1].write_bytes([b''.join(mine[::2])])
+        outs[2].write_bytes([b''.join(mine)])
+        outs[2].write_bytes([b''.join(mine[::3])])
+        sh.barrier()
+        for o in outs:
+            o.finish()
+        fa.close()
         # split references: first-split order over the ranks
         names = ['s%d' % ((i * 7) % 5) for i in range(lo, hi, 97)]
         seen = []
@@ -75,18 +130,20 @@ def _worker(rank, world, port, out_dir):
                 if name not in seen:
                     seen.append(name)
         if rank == 0:
-            want = b''.join(_line(i, refs[i]) for i in pm.grouped_order(refs)).decode()
-            assert out.getvalue() == want
             assert a.getvalue() == ''.join('r%d\n' % i for i in range(N_READS))
             want_b = ''.join(''.join('r%d\n' % i for i in range(*_block(r, world, N_READS))[::2])
                              for r in range(world))
             assert b.getvalue() == want_b
+            want_rows = ''.join('r%d\n' % i for i in range(N_READS)) + ''.join(
+                ''.join('r%d\n' % i for i in range(*_block(r, world, N_READS))[::3])
+                for r in range(world))
+            assert open(pa).read() == want_rows
             all_names = ['s%d' % ((i * 7) % 5) for r in range(world)
                          for i in range(_block(r, world, N_READS)[0], _block(r, world, N_READS)[1], 97)]
             assert seen == list(dict.fromkeys(all_names))
             open(os.path.join(out_dir, 'ok'), 'w').close()
         else:
-            assert out.getvalue() == '' and a.getvalue() == '' and b.getvalue() == ''
+            assert a.getvalue() == '' and b.getvalue() == ''
     finally:
         dist.destroy_process_group()
 

@@ -1,0 +1,209 @@
+"""Sharded FASTQ ingest on the CPU (gloo, world sizes 2 and 3): every rank
+reads only its share of each file (the gzip members starting in its byte
+range, or the byte range of a plain file), frames its text into four-line
+records from the line counts of the ranks before it, hands the bytes before
+its first record to the rank before, and realigns R2 to R1's blocks by
+point-to-point exchange (micall_amd.sharded_io.stage_fastq).
+
+The block each rank ends up with must be exactly the records
+[first, first + units) of both files, the blocks must tile the file in rank
+order, raw_count's line count must be the whole file's, and with many
+members a rank must decode only about 1/W of the file.  Files that cannot
+be split (one gzip member; a blank line where a record starts) fall back to
+the whole-file loader (non-strict) or to a whole read plus a floor split of
+the records (strict, the censor's framing).  Reference behaviour: the FASTQ
+records bowtie2 reads (prelim_map.py:114-134) and censor's four-line records
+(censor_fastq.py:58)."""
+import gzip
+import os
+import socket
+import zlib
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from micall_amd import _native, sharded_io
+from micall_amd.pipeline import Shard
+
+
+def _records(n, mate, seed, crlf=False, fake_header_at=None):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        L = int(rng.integers(30, 120))
+        seq = ''.join(rng.choice(list('ACGTN'), size=L))
+        qual = ''.join(rng.choice(list('#,:AFG'), size=L))
+        name = '@M00:1:FC:1:%d:%d:%d %d:N:0:1' % (1101 + i % 3, i, 7 * i, mate)
+        rec = '%s\n%s\n+\n%s\n' % (name, seq, qual)
+        if crlf:
+            rec = rec.replace('\n', '\r\n')
+        rec = rec.encode()
+        if fake_header_at is not None and i == fake_header_at:
+            # a gzip-member-shaped byte run inside the text (it reaches the
+            # compressed stream verbatim in a stored member)
+            rec = rec.replace(b' %d:N' % mate, b'\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\x03ZZ %d:N' % mate)
+        out.append(rec)
+    return out
+
+
+def _gz_members(data, member_bytes, level=1, stored_member=None):
+    out, k = [], 0
+    for at in range(0, len(data), member_bytes):
+        lvl = 0 if (stored_member is not None and k == stored_member) else level
+        c = zlib.compressobj(lvl, zlib.DEFLATED, 31)
+        out.append(c.compress(data[at:at + member_bytes]) + c.flush())
+        k += 1
+    return b''.join(out)
+
+
+def _make_case(d, case):
+    """Write the case's files; returns (paths, [records per file])."""
+    n = 700
+    recs = [_records(n, 1, 1, crlf=case == 'crlf'), _records(n, 2, 2, crlf=case == 'crlf')]
+    if case == 'unpaired':
+        recs = recs[:1]
+    if case == 'blank':
+        recs[0][n // 2] = b'\n' + recs[0][n // 2]
+    if case == 'fake_header':
+        recs[0] = _records(n, 1, 1, fake_header_at=n // 2)
+    paths = []
+    for k, rs in enumerate(recs):
+        data = b''.join(rs)
+        p = os.path.join(d, 'R%d.fastq%s' % (k + 1, '' if case == 'plain' else '.gz'))
+        if case == 'plain':
+            blob = data
+        elif case == 'single' or (case == 'mixed' and k == 1):
+            blob = gzip.compress(data, 6)
+        elif case == 'fake_header':
+            mb = 9000 + 1000 * k
+            at = data.find(b'\x1f\x8b')
+            blob = _gz_members(data, mb, stored_member=at // mb if at >= 0 else None)
+            assert k == 1 or b'\x1f\x8b\x08\x00' in blob
+        else:
+            blob = _gz_members(data, 7000 + 3100 * k)        # R1 / R2 members do not line up
+        with open(p, 'wb') as f:
+            f.write(blob)
+        paths.append(p)
+    return paths, recs
+
+
+def _worker(rank, world, port, d, case, strict):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        paths, recs = _make_case(d, case) if rank == 0 else (None, None)
+        dist.barrier()
+        if rank != 0:
+            paths, recs = _make_case(d + '_r%d' % rank, case)   # same content, own copy of the expectation
+            paths = [os.path.join(d, os.path.basename(p)) for p in paths]
+        sh = Shard(rank, world, 0)
+        sharded_io.reset_stats()
+        st = sharded_io.stage_fastq(sh, [(p, None) for p in paths], strict=strict)
+        result = dict(rank=rank)
+        if st is None:
+            result['fallback'] = True
+        else:
+            first, units = st['first'], st['units']
+            for k, f in enumerate(st['frames']):
+                got = f.fq.view().tobytes()
+                want = b''.join(recs[k][first:first + units])
+                assert got == want, (rank, k, first, units, len(got), len(want))
+                f.fq.close()
+            total_nl = sum(r.count(b'\n') for r in recs[0])
+            assert st['lines'] == total_nl
+            assert st['total'] == len(recs[0])
+            result.update(first=first, units=units, mode=st['mode'],
+                          file_bytes=sharded_io.IO_STATS['fastq_file_bytes'],
+                          file_size=sum(os.path.getsize(p) for p in paths))
+        np.save(os.path.join(d, 'rank%d.npy' % rank), np.array([
+            result.get('fallback', False), result.get('first', -1), result.get('units', -1),
+            result.get('mode') == 'members', result.get('file_bytes', 0),
+            result.get('file_size', 0)], dtype=np.int64))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _run(tmp_path, world, case, strict=False):
+    d = str(tmp_path / 'files')
+    os.makedirs(d, exist_ok=True)
+    for r in range(1, world):
+        os.makedirs(d + '_r%d' % r, exist_ok=True)
+    mp.spawn(_worker, args=(world, _free_port(), d, case, strict), nprocs=world, join=True)
+    return [np.load(os.path.join(d, 'rank%d.npy' % r)) for r in range(world)]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('world', [2, 3])
+@pytest.mark.parametrize('case', ['members', 'plain', 'unpaired', 'crlf', 'fake_header'])
+def test_split_blocks_tile_the_file(tmp_path, world, case):
+    res = _run(tmp_path, world, case)
+    assert not any(r[0] for r in res)
+    firsts, units = [int(r[1]) for r in res], [int(r[2]) for r in res]
+    assert firsts[0] == 0 and all(firsts[k] + units[k] == firsts[k + 1] for k in range(world - 1))
+    assert firsts[-1] + units[-1] == 700
+    assert all(r[3] for r in res)                    # split, not read whole
+    # each rank decoded about its share of the files (members are whole units)
+    size = int(res[0][5])
+    for r in res:
+        assert r[4] <= size / world * 1.6 + 20000, (r[4], size)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('world', [2, 3])
+def test_mixed_split_and_whole_files(tmp_path, world):
+    """R1 in many members, R2 one member: R2 is read whole and cut to R1's
+    blocks."""
+    res = _run(tmp_path, world, 'mixed')
+    assert not any(r[0] for r in res)
+    assert sum(int(r[2]) for r in res) == 700
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('case', ['single', 'blank'])
+def test_unsplittable_files_fall_back(tmp_path, case):
+    res = _run(tmp_path, 2, case)
+    assert all(r[0] for r in res)                    # the whole-file part loader
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('case', ['single', 'members'])
+def test_strict_framing_for_censor(tmp_path, case):
+    """The censor's framing: one member is read whole by every rank and its
+    records split by count; many members are split."""
+    res = _run(tmp_path, 3, case, strict=True)
+    assert not any(r[0] for r in res)
+    units = [int(r[2]) for r in res]
+    assert sum(units) == 700
+    if case == 'single':
+        assert units == [700 * (k + 1) // 3 - 700 * k // 3 for k in range(3)]
+
+
+def test_parallel_gunzip_matches_serial(tmp_path):
+    """mh_gunzip's member-parallel path (inputs over 4 MiB): a multi-member
+    file whose stored member holds gzip-header-shaped bytes (a false member
+    candidate: the span is merged with its neighbour), and one whose false
+    candidate sits in the last member (the parallel path gives up and the
+    file is decoded serially).  Both equal Python's gzip."""
+    rng = np.random.default_rng(5)
+    body = rng.choice(np.frombuffer(b'ACGT\n', dtype=np.uint8), size=6 << 20).tobytes()
+    fake = b'\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\x03' + b'\x00' * 12 + b'\xff\xff\xff\x7f'
+    for where in ('middle', 'last'):
+        parts = [body[k:k + (1 << 20)] for k in range(0, len(body), 1 << 20)]
+        k = 2 if where == 'middle' else len(parts) - 1
+        parts[k] = parts[k][:1000] + fake + parts[k][1000:]
+        blob = b''.join(_gz_members(p, len(p) + 1, level=0 if j == k else 1)
+                        for j, p in enumerate(parts))
+        assert fake in blob
+        path = tmp_path / ('f_%s.gz' % where)
+        path.write_bytes(blob)
+        fq = _native.Fastq(str(path))
+        assert fq.view().tobytes() == gzip.decompress(blob)
+        fq.close()
