@@ -230,6 +230,12 @@ int mh_phase_times(mh_ctx *ctx, double *ms, int reset);
  * *written bytes.  The caller moves its file position past them. */
 int mh_write_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
                   const char *const *refnames, int fd, int64_t offset, int64_t *written);
+/* mh_write_rows that also returns the crc32 of the bytes written (crc NULL:
+ * none).  The rows are formatted in chunks on host threads while one
+ * thread writes the finished chunks in order. */
+int mh_write_rows_crc(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
+                      const char *const *refnames, int fd, int64_t offset, int64_t *written,
+                      uint32_t *crc);
 /* (crc32 << 32) | adler32 of a whole open file (zlib's, computed over
  * chunks on host threads) and its size: remap() checks with it that
  * prelim.csv is the file prelim_map() wrote. */

@@ -2,6 +2,8 @@
 // include/micall_hip.h, context and device-memory management, the seed index
 // build (bowtie2-build's job), FASTQ ingest and SAM/CSV text emission.
 #include <errno.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
@@ -16,7 +18,9 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <condition_variable>
 #include <deque>
+#include <mutex>
 #include <functional>
 #include <string_view>
 #include <thread>
@@ -204,12 +208,12 @@ struct CtxEx : Ctx {
     int64_t map_gen = 0;                  // bumped by every mh_map
     uint64_t fmt_key = 0;
     bool fmt_valid = false;
-    std::vector<std::string> fmt_chunks;
+    std::vector<TextBuf> fmt_chunks;
     // host wall time per phase of the file-to-file path (mh_phase_times)
     double phase_ms[MH_PHASES] = {};
     // mh_format_segments: the formatted chunks and the byte offset of every
     // segment bound in their concatenation, kept for mh_write_segments
-    std::vector<std::string> seg_chunks;
+    std::vector<TextBuf> seg_chunks;
     std::vector<int64_t> seg_at;
 };
 
@@ -424,23 +428,23 @@ static int load_reads(CtxEx &c, DevReads &dst, HostReads &host, int64_t n, int p
     return 0;
 }
 
-// bowtie2 read name: header up to the first whitespace, /1 or /2 dropped for mates
-static std::string qname_of(const char *h, size_t n, bool paired)
+// bowtie2 read name: header up to the first whitespace, /1 or /2 dropped
+// for mates; the span [*at, *at + *len) of the header h
+static inline void qname_span(const char *h, size_t n, bool paired, size_t *at, size_t *len)
 {
     size_t a = (n && h[0] == '@') ? 1 : 0;
     while (a < n && (h[a] == ' ' || h[a] == '\t')) ++a;
     size_t b = a;
     while (b < n && h[b] != ' ' && h[b] != '\t' && h[b] != '\r') ++b;
-    std::string s(h + a, b - a);
-    if (paired && s.size() > 2 && s[s.size() - 2] == '/' && (s.back() == '1' || s.back() == '2'))
-        s.resize(s.size() - 2);
-    return s;
+    if (paired && b - a > 2 && h[b - 2] == '/' && (h[b - 1] == '1' || h[b - 1] == '2')) b -= 2;
+    *at = a;
+    *len = b - a;
 }
 
 // A FASTQ file decoded to text and indexed in place: per record the start
 // and length of its header, sequence and quality lines.
 struct Fastq {
-    std::string data;
+    TextBuf data;
     std::vector<int64_t> name_at, seq_at, qual_at;
     std::vector<int32_t> name_len, len, qual_len;
     size_t size() const { return len.size(); }
@@ -459,41 +463,53 @@ static void par_for(int nt, const std::function<void(int)> &fn)
 
 // The whole (gzip or plain) file; every concatenated gzip member is decoded
 // (as gzread does), in parallel when there are several (mh_gunzip.cpp).
-static int slurp(const char *path, std::string &data)
+static int slurp(const char *path, TextBuf &data)
 {
     data.clear();
-    FILE *f = fopen(path, "rb");
-    if (!f) { set_error("cannot open FASTQ %s", path); return -3; }
-    std::string raw;
-    fseek(f, 0, SEEK_END);
-    const long sz = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    if (sz > 0) {
-        raw.resize((size_t)sz);
-        if (fread(&raw[0], 1, (size_t)sz, f) != (size_t)sz) {
-            fclose(f);
-            set_error("cannot read FASTQ %s", path);
-            return -3;
+    const int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) { set_error("cannot open FASTQ %s", path); return -3; }
+    struct stat st;
+    if (fstat(fd, &st) != 0) { close(fd); set_error("cannot stat FASTQ %s", path); return -3; }
+    const int64_t sz = (int64_t)st.st_size;
+    // the file mapped (no copy); a file that cannot be mapped is read
+    const uint8_t *raw = nullptr;
+    void *map = MAP_FAILED;
+    TextBuf copy;
+    if (sz > 0 && S_ISREG(st.st_mode)) map = mmap(nullptr, (size_t)sz, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (map != MAP_FAILED) {
+        raw = (const uint8_t *)map;
+    } else if (sz > 0) {
+        copy.resize((size_t)sz);
+        int64_t got = 0;
+        while (got < sz) {
+            const ssize_t r = pread(fd, copy.data() + got, (size_t)(sz - got), (off_t)got);
+            if (r <= 0) break;
+            got += r;
         }
+        if (got != sz) { close(fd); set_error("cannot read FASTQ %s", path); return -3; }
+        raw = (const uint8_t *)copy.data();
     }
-    fclose(f);
-    if (raw.size() >= 2 && (uint8_t)raw[0] == 0x1f && (uint8_t)raw[1] == 0x8b) {
+    close(fd);
+    int rc = 0;
+    if (sz >= 2 && raw[0] == 0x1f && raw[1] == 0x8b) {
         std::string why;
-        if (gunzip_buffer((const uint8_t *)raw.data(), (int64_t)raw.size(), data, why)) {
+        if (gunzip_buffer(raw, sz, data, why)) {
             set_error("gzip error reading %s: %s", path, why.c_str());
-            return -3;
+            rc = -3;
         }
-    } else {
-        data.swap(raw);
+    } else if (sz > 0) {
+        if (map != MAP_FAILED) data.assign((const char *)raw, (size_t)sz);
+        else data.swap(copy);
     }
-    return 0;
+    if (map != MAP_FAILED) munmap(map, (size_t)sz);
+    return rc;
 }
 
 // Index the FASTQ records of fq.data (blank lines between records skipped,
 // '\r' before '\n' dropped): the newline scan runs on host threads.
 static int index_fastq(Fastq &fq, const char *path, int64_t *newlines)
 {
-    const std::string &data = fq.data;
+    const TextBuf &data = fq.data;
     const int64_t n = (int64_t)data.size();
     const char *D = data.data();
     const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 20) + 1));
@@ -756,15 +772,49 @@ static int load_fastq_units(CtxEx *c, Fastq &a, Fastq *b, int64_t a0, int64_t a1
     }
     h.seq.alloc((size_t)total);
     h.qual.alloc((size_t)total);
-    std::vector<std::string> names((size_t)n);
+    const auto tn = std::chrono::steady_clock::now();
+    // names: spans first (sizes), then every thread copies its names into the pool
+    NameTable names;
+    names.off.resize((size_t)n + 1);
+    std::vector<int64_t> nstart((size_t)n);
     const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
+    std::vector<int64_t> tsum(nt + 1, 0);
+    par_for(nt, [&](int t) {
+        int64_t sum = 0;
+        for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
+            const bool mate2 = paired && (i & 1);
+            const Fastq &f = mate2 ? *b : a;
+            const int64_t r = (mate2 ? b0 : a0) + i / per;
+            size_t at = 0, len = 0;
+            qname_span(f.data.data() + f.name_at[r], (size_t)f.name_len[r], paired, &at, &len);
+            nstart[i] = f.name_at[r] + (int64_t)at;
+            names.off[i + 1] = (int64_t)len;
+            sum += (int64_t)len;
+        }
+        tsum[t + 1] = sum;
+    });
+    for (int t = 0; t < nt; ++t) tsum[t + 1] += tsum[t];
+    names.pool.resize((size_t)tsum[nt]);
+    par_for(nt, [&](int t) {
+        int64_t o = tsum[t];
+        for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
+            const bool mate2 = paired && (i & 1);
+            const Fastq &f = mate2 ? *b : a;
+            const int64_t len = names.off[i + 1];
+            memcpy(&names.pool[(size_t)o], f.data.data() + nstart[i], (size_t)len);
+            names.off[i + 1] = o + len;
+            o += len;
+        }
+    });
+    names.off[0] = 0;
+    const double names_ms = ms_since(tn);
+    const auto tc = std::chrono::steady_clock::now();
     par_for(nt, [&](int t) {
         for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
             const bool mate2 = paired && (i & 1);
             const Fastq &f = mate2 ? *b : a;
             const int64_t r = (mate2 ? b0 : a0) + i / per;
             const char *D = f.data.data();
-            names[i] = qname_of(D + f.name_at[r], (size_t)f.name_len[r], paired);
             const int64_t L = h.len[i];
             memcpy(h.seq.data() + h.off[i], D + f.seq_at[r], (size_t)L);
             const int64_t cq = std::min<int64_t>(L, f.qual_len[r]);
@@ -772,8 +822,13 @@ static int load_fastq_units(CtxEx *c, Fastq &a, Fastq *b, int64_t a0, int64_t a1
             for (int64_t x = cq; x < L; ++x) h.qual.data()[h.off[i] + x] = 'I';
         }
     });
+    const double copy_ms = ms_since(tc);
+    const auto tf = std::chrono::steady_clock::now();
     a = Fastq{};
     if (b) *b = Fastq{};
+    if (getenv("MH_INGEST_TRACE"))
+        fprintf(stderr, "ingest: names %.1f ms, copy %.1f ms, free %.1f ms\n", names_ms, copy_ms,
+                ms_since(tf));
     c->phase_ms[MH_PHASE_PARSE] += ms_since(t0);
     const auto t1 = std::chrono::steady_clock::now();
     const uint8_t *sq = h.seq.data(), *ql = h.qual.data();
@@ -815,6 +870,8 @@ int mh_reads_load_fastq_part(mh_ctx *ctx, const char *path1, const char *path2, 
     if (paired) t2.join();
     c->phase_ms[MH_PHASE_INFLATE] += std::max(dec1, dec2);
     c->phase_ms[MH_PHASE_PARSE] += std::max(ix1, ix2);
+    if (getenv("MH_INGEST_TRACE"))
+        fprintf(stderr, "ingest: decode %.1f / %.1f ms, index %.1f / %.1f ms\n", dec1, dec2, ix1, ix2);
     if (st1) return st1;
     if (st2) { set_error("%s", err2.c_str()); return st2; }
     if (paired && a.size() != b.size()) {
@@ -884,7 +941,7 @@ int mh_reads_set_names(mh_ctx *ctx, int64_t n, const char *const *names)
 {
     if (!ctx || n != X(ctx)->reads.n) { set_error("mh_reads_set_names: count mismatch"); return -3; }
     CtxEx *c = X(ctx);
-    c->names.assign(names, names + n);
+    c->names.assign(names, n);
     return 0;
 }
 
@@ -1074,13 +1131,33 @@ static inline char *put_str(char *o, const char *s, size_t n)
 }
 
 // csv.writer QUOTE_MINIMAL (csv_field) into a buffer with room for 2n + 2
-static inline char *put_csv(char *o, const char *s, size_t n)
+// any byte of w equal to c (bit tricks over 8 bytes at a time)
+static inline uint64_t has_byte(uint64_t w, uint8_t c)
 {
-    bool quote = false;
-    for (size_t i = 0; i < n; ++i) {
+    const uint64_t x = w ^ (0x0101010101010101ull * c);
+    return (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+}
+
+static inline bool needs_quotes(const char *s, size_t n)
+{
+    size_t i = 0;
+    uint64_t hit = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, s + i, 8);
+        hit |= has_byte(w, ',') | has_byte(w, '"') | has_byte(w, '\n') | has_byte(w, '\r');
+    }
+    bool quote = hit != 0;
+    for (; i < n; ++i) {
         const char ch = s[i];
         quote |= ch == ',' || ch == '"' || ch == '\n' || ch == '\r';
     }
+    return quote;
+}
+
+static inline char *put_csv(char *o, const char *s, size_t n)
+{
+    const bool quote = needs_quotes(s, n);
     if (!quote) return put_str(o, s, n);
     *o++ = '"';
     for (size_t i = 0; i < n; ++i) {
@@ -1109,7 +1186,7 @@ static const BaseTables kBases;
 // One row of SAM (style 0) or CSV (style 1) text, appended to out at *used
 // (out grows as needed; it is not zero-filled beyond what is written).
 static void format_row(const CtxEx *c, int style, const Rec &a, int64_t r, const uint32_t *pool,
-                       const char *const *refnames, const size_t *refname_len, std::string &out,
+                       const char *const *refnames, const size_t *refname_len, TextBuf &out,
                        size_t &used, std::string &tmp)
 {
     static const char *ytn[4] = {"CP", "DP", "UP", "UU"};
@@ -1118,7 +1195,7 @@ static void format_row(const CtxEx *c, int style, const Rec &a, int64_t r, const
     const int L = c->host.len[r];
     const uint8_t *s = c->host.seq.data() + c->host.off[r];
     const uint8_t *q = c->host.qual.data() + c->host.off[r];
-    const std::string &qn = c->names[r];
+    const std::string_view qn = c->names[r];
     const char *rn = a.sam_ref >= 0 ? refnames[a.sam_ref] : "*";
     const size_t rnl = a.sam_ref >= 0 ? refname_len[a.sam_ref] : 1;
     const size_t nxl = a.rnext >= 0 ? refname_len[a.rnext] : 1;
@@ -1194,12 +1271,86 @@ static void format_row(const CtxEx *c, int style, const Rec &a, int64_t r, const
     used = (size_t)(o - out.data());
 }
 
+// Bytes at file offsets, written by host threads with pwrite.  (Buffered
+// writes to one file serialise on its inode lock; a shared writable mapping
+// filled by every thread instead -- MICALL_WRITE_MMAP=1: the file extended
+// by fallocate, which never shrinks it, so ranks of a sharded job writing
+// their own ranges cannot cut each other's bytes -- measured slower on the
+// GPU box's overlay file system: 0.45 vs 0.24 s for a 1.17 GB prelim.csv.)
+// 0, or an errno.
+struct WritePiece {
+    const char *src;
+    size_t len;
+    int64_t off;
+};
+
+static int write_pieces(int fd, std::vector<WritePiece> pieces)
+{
+    pieces.erase(std::remove_if(pieces.begin(), pieces.end(),
+                                [](const WritePiece &p) { return p.len == 0; }),
+                 pieces.end());
+    if (pieces.empty()) return 0;
+    int64_t lo = INT64_MAX, hi = 0;
+    for (const WritePiece &p : pieces) {
+        lo = std::min(lo, p.off);
+        hi = std::max(hi, p.off + (int64_t)p.len);
+    }
+    // balance: pieces of at most 4 MiB
+    std::vector<WritePiece> work;
+    for (const WritePiece &p : pieces)
+        for (size_t a = 0; a < p.len; a += (size_t)4 << 20)
+            work.push_back(WritePiece{p.src + a, std::min(p.len - a, (size_t)4 << 20), p.off + (int64_t)a});
+    const int nt = std::max(1, std::min<int>(s2a_threads(), (int)work.size()));
+    std::atomic<size_t> next(0);
+    std::atomic<int> bad(0);
+    const long pg = sysconf(_SC_PAGESIZE);
+    const int64_t base = lo / pg * pg;
+    void *map = MAP_FAILED;
+    static const bool use_map = getenv("MICALL_WRITE_MMAP") && *getenv("MICALL_WRITE_MMAP") == '1';
+    if (use_map && hi - lo >= ((int64_t)1 << 20) && fallocate(fd, 0, lo, hi - lo) == 0) {
+        // a shared writable mapping needs a descriptor open for reading too:
+        // an output opened 'w' is write-only, so it is opened again read-write
+        // through /proc (the same file; its own offset is not used)
+        char self[64];
+        snprintf(self, sizeof(self), "/proc/self/fd/%d", fd);
+        const int rw = open(self, O_RDWR | O_CLOEXEC);
+        if (rw >= 0) {
+            struct stat a, b;
+            if (fstat(fd, &a) == 0 && fstat(rw, &b) == 0 && a.st_dev == b.st_dev && a.st_ino == b.st_ino)
+                map = mmap(nullptr, (size_t)(hi - base), PROT_WRITE, MAP_SHARED, rw, (off_t)base);
+            close(rw);
+        }
+    }
+    if (map != MAP_FAILED) {
+        char *m = (char *)map;
+        par_for(nt, [&](int) {
+            for (size_t i; (i = next.fetch_add(1)) < work.size();)
+                std::memcpy(m + (work[i].off - base), work[i].src, work[i].len);
+        });
+        munmap(map, (size_t)(hi - base));
+        return 0;
+    }
+    par_for(nt, [&](int) {
+        for (size_t i; (i = next.fetch_add(1)) < work.size();) {
+            const char *src = work[i].src;
+            size_t left = work[i].len;
+            int64_t pos = work[i].off;
+            while (left > 0) {
+                const ssize_t w = pwrite(fd, src, left, (off_t)pos);
+                if (w <= 0) { bad = errno ? errno : EIO; return; }
+                src += w; left -= (size_t)w; pos += w;
+            }
+        }
+    });
+    return bad.load();
+}
+
 // The text of rows first .. first+n (or order[first ..]) as one chunk per
 // host thread, in order.  With segment row bounds seg_rows[0 .. n_seg]
 // (relative to `first`, ascending), *seg_at gets the byte offset in the
 // concatenated text at which each bound row starts.
 static int format_chunks(CtxEx *c, int style, const int64_t *order, int64_t first, int64_t n,
-                         const char *const *refnames, std::vector<std::string> &chunks,
+                         const char *const *refnames, std::vector<TextBuf> &chunks,
                          int n_seg = 0, const int64_t *seg_rows = nullptr,
                          std::vector<int64_t> *seg_at = nullptr)
 {
@@ -1219,12 +1370,24 @@ static int format_chunks(CtxEx *c, int style, const int64_t *order, int64_t firs
     std::vector<size_t> rn_len(c->index.n_refs > 0 ? (size_t)c->index.n_refs : 1, 0);
     for (int k = 0; k < c->index.n_refs; ++k) rn_len[k] = std::strlen(refnames[k]);
     const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
-    chunks.assign(nt, std::string());
+    chunks.clear();
+    chunks.resize(nt);
+    // a chunk's bytes are reserved for its rows' upper bound up front (not
+    // touched until written: no zero fill, no regrowth copies)
+    size_t name_max = 1;
+    for (size_t r = 0; r < c->names.size(); ++r)
+        name_max = std::max(name_max, (size_t)(c->names.off[r + 1] - c->names.off[r]));
+    size_t ref_max = 1;
+    for (int k = 0; k < c->index.n_refs; ++k) ref_max = std::max(ref_max, rn_len[k]);
+    const size_t row_max = 2 * name_max + 4 * ref_max + 3 * (size_t)std::max(c->reads.max_len, 1) +
+                           12 * MH_MAXOPS + 16 * 12 + 200;
     // per thread: (segment bound, byte offset in the thread's chunk)
     std::vector<std::vector<std::pair<int, size_t>>> marks(nt);
     par_for(nt, [&](int t) {
         const int64_t k0 = n * t / nt, k1 = n * (t + 1) / nt;
-        std::string &out = chunks[t];
+        TextBuf &out = chunks[t];
+        out.reserve((size_t)(k1 - k0) * row_max + 1);
+        out.resize((size_t)(k1 - k0) * row_max + 1);
         size_t used = 0;
         std::string tmp;
         int sb = 0;
@@ -1253,33 +1416,121 @@ static int format_chunks(CtxEx *c, int style, const int64_t *order, int64_t firs
     return 0;
 }
 
+// Rows formatted and written in one stream: the rows are cut into many
+// chunks, formatted by host threads in chunk order, and one writer thread
+// writes each chunk as soon as it and every chunk before it are done (a
+// file's buffered writes are serialised by its inode lock, so one writer
+// loses nothing, and the formatting hides under the write).  *crc_out =
+// crc32 of everything written.
+static int format_write_stream(CtxEx *c, int style, const int64_t *order, int64_t first, int64_t n,
+                               const char *const *refnames, int fd, int64_t offset,
+                               int64_t *written, uint32_t *crc_out)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<Rec> rec;
+    std::vector<uint32_t> pool;
+    if (order) {
+        if (int st = fetch_recs(c, 0, c->map.n_reads, rec, pool)) return st;
+        for (int64_t k = 0; k < n; ++k)
+            if (order[first + k] < 0 || order[first + k] >= c->map.n_reads) {
+                set_error("format order index out of range");
+                return -3;
+            }
+    } else if (int st = fetch_recs(c, first, n, rec, pool)) {
+        return st;
+    }
+    std::vector<size_t> rn_len(c->index.n_refs > 0 ? (size_t)c->index.n_refs : 1, 0);
+    for (int k = 0; k < c->index.n_refs; ++k) rn_len[k] = std::strlen(refnames[k]);
+    size_t name_max = 1, ref_max = 1;
+    for (size_t r = 0; r < c->names.size(); ++r)
+        name_max = std::max(name_max, (size_t)(c->names.off[r + 1] - c->names.off[r]));
+    for (int k = 0; k < c->index.n_refs; ++k) ref_max = std::max(ref_max, rn_len[k]);
+    const size_t row_max = 2 * name_max + 4 * ref_max + 3 * (size_t)std::max(c->reads.max_len, 1) +
+                           12 * MH_MAXOPS + 16 * 12 + 200;
+    const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(n / 4096 + 1, 1024));
+    std::vector<TextBuf> buf((size_t)nch);
+    std::vector<uint32_t> crc((size_t)nch, 0);
+    std::unique_ptr<std::atomic<int>[]> done(new std::atomic<int>[(size_t)nch]);
+    for (int64_t k = 0; k < nch; ++k) done[k].store(0);
+    std::atomic<int64_t> next(0);
+    std::mutex mu;
+    std::condition_variable cv;
+    const int nf = std::max(1, s2a_threads() - 1);
+    std::atomic<int> finished(0);
+    std::atomic<double> fmt_end(0.0);
+    std::vector<std::thread> fmt;
+    auto worker = [&]() {
+        std::string tmp;
+        for (int64_t k; (k = next.fetch_add(1)) < nch;) {
+            const int64_t k0 = n * k / nch, k1 = n * (k + 1) / nch;
+            TextBuf &out = buf[(size_t)k];
+            out.resize((size_t)(k1 - k0) * row_max + 1);
+            size_t used = 0;
+            for (int64_t j = k0; j < k1; ++j) {
+                const int64_t r = order ? order[first + j] : first + j;
+                format_row(c, style, order ? rec[r] : rec[j], r, pool.data(), refnames, rn_len.data(),
+                           out, used, tmp);
+            }
+            out.resize(used);
+            if (crc_out) crc[(size_t)k] = crc32_update(0, out.data(), used);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                done[k].store(1);
+            }
+            cv.notify_all();
+        }
+        if (finished.fetch_add(1) + 1 == nf) fmt_end.store(ms_since(t0));
+    };
+    for (int t = 0; t < nf; ++t) fmt.emplace_back(worker);
+    int bad = 0;
+    int64_t pos = offset;
+    uint32_t total_crc = 0;
+    for (int64_t k = 0; k < nch; ++k) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return done[k].load() != 0; });
+        }
+        const char *p = buf[(size_t)k].data();
+        size_t left = buf[(size_t)k].size();
+        if (crc_out) total_crc = crc32_join(total_crc, crc[(size_t)k], (int64_t)left);
+        while (left > 0 && !bad) {
+            const ssize_t w = pwrite(fd, p, left, (off_t)pos);
+            if (w <= 0) { bad = errno ? errno : EIO; break; }
+            p += w; left -= (size_t)w; pos += w;
+        }
+        buf[(size_t)k].release();
+    }
+    for (auto &t : fmt) t.join();
+    // the formatting (overlapped with the first writes), then the write tail
+    const double all_ms = ms_since(t0), f_ms = fmt_end.load();
+    c->phase_ms[MH_PHASE_FORMAT] += f_ms;
+    c->phase_ms[MH_PHASE_WRITE] += all_ms - f_ms;
+    if (bad) { set_error("mh_write_rows: write failed (%s)", strerror(bad)); return -4; }
+    if (written) *written = pos - offset;
+    if (crc_out) *crc_out = total_crc;
+    return 0;
+}
+
 int mh_write_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
                   const char *const *refnames, int fd, int64_t offset, int64_t *written)
 {
-    if (!ctx || !refnames || (style != 0 && style != 1) || fd < 0 || offset < 0) return -3;
+    return mh_write_rows_crc(ctx, style, order, first, n, refnames, fd, offset, written, nullptr);
+}
+
+int mh_write_rows_crc(mh_ctx *ctx, int style, const int64_t *order, int64_t first, int64_t n,
+                      const char *const *refnames, int fd, int64_t offset, int64_t *written,
+                      uint32_t *crc)
+{
+    if (!ctx || !refnames || (style != 0 && style != 1) || fd < 0 || offset < 0 || n < 0) return -3;
     CtxEx *c = X(ctx);
     MH_HIP(hipSetDevice(c->device));
     if ((int64_t)c->names.size() != c->reads.n) { set_error("no read names loaded"); return -3; }
-    std::vector<std::string> chunks;
-    if (int st = format_chunks(c, style, order, first, n, refnames, chunks)) return st;
-    const auto tw = std::chrono::steady_clock::now();
-    std::vector<int64_t> at(chunks.size() + 1, offset);
-    for (size_t t = 0; t < chunks.size(); ++t) at[t + 1] = at[t] + (int64_t)chunks[t].size();
-    std::atomic<int> bad(0);
-    par_for((int)chunks.size(), [&](int t) {
-        const char *p = chunks[t].data();
-        size_t left = chunks[t].size();
-        int64_t pos = at[t];
-        while (left > 0) {
-            const ssize_t w = pwrite(fd, p, left, (off_t)pos);
-            if (w <= 0) { bad = errno ? errno : EIO; return; }
-            p += w; left -= (size_t)w; pos += w;
-        }
-    });
-    c->phase_ms[MH_PHASE_WRITE] += ms_since(tw);
-    if (bad) { set_error("mh_write_rows: write failed (%s)", strerror(bad.load())); return -4; }
-    if (written) *written = at.back() - offset;
-    return 0;
+    try {
+        return format_write_stream(c, style, order, first, n, refnames, fd, offset, written, crc);
+    } catch (const std::bad_alloc &) {
+        set_error("mh_write_rows: out of memory");
+        return -2;
+    }
 }
 
 int mh_format_segments(mh_ctx *ctx, int style, const int64_t *order, int64_t n,
@@ -1317,7 +1568,7 @@ int mh_write_segments(mh_ctx *ctx, int fd, const int64_t *seg_off, uint32_t *crc
     for (int k = 0; k < n_seg; ++k)
         if (seg_off[k] < 0) { set_error("mh_write_segments: negative offset"); return -3; }
     const auto tw = std::chrono::steady_clock::now();
-    std::vector<std::string> &ch = c->seg_chunks;
+    std::vector<TextBuf> &ch = c->seg_chunks;
     const int nt = (int)ch.size();
     std::vector<int64_t> cbase(nt + 1, 0);
     for (int t = 0; t < nt; ++t) cbase[t + 1] = cbase[t] + (int64_t)ch[t].size();
@@ -1336,24 +1587,19 @@ int mh_write_segments(mh_ctx *ctx, int fd, const int64_t *seg_off, uint32_t *crc
             a = b;
         }
     }
-    std::atomic<size_t> next(0);
-    std::atomic<int> bad(0);
-    const int nw = std::max(1, std::min<int>(s2a_threads(), (int)pieces.size()));
-    par_for(nw, [&](int) {
-        for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
-            Piece &p = pieces[i];
-            const char *src = ch[p.t].data() + (p.a - cbase[p.t]);
-            const size_t len = (size_t)(p.b - p.a);
-            if (crc) p.crc = crc32_update(0, src, len);
-            size_t left = len;
-            int64_t pos = seg_off[p.seg] + (p.a - c->seg_at[p.seg]);
-            while (left > 0) {
-                const ssize_t w = pwrite(fd, src, left, (off_t)pos);
-                if (w <= 0) { bad = errno ? errno : EIO; return; }
-                src += w; left -= (size_t)w; pos += w;
-            }
-        }
-    });
+    std::vector<WritePiece> wp;
+    for (const Piece &p : pieces)
+        wp.push_back(WritePiece{ch[p.t].data() + (p.a - cbase[p.t]), (size_t)(p.b - p.a),
+                                seg_off[p.seg] + (p.a - c->seg_at[p.seg])});
+    if (crc) {
+        std::atomic<size_t> next(0);
+        const int nw = std::max(1, std::min<int>(s2a_threads(), (int)pieces.size()));
+        par_for(nw, [&](int) {
+            for (size_t i; (i = next.fetch_add(1)) < pieces.size();)
+                pieces[i].crc = crc32_update(0, wp[i].src, wp[i].len);
+        });
+    }
+    const int bad = write_pieces(fd, wp);
     if (crc) {
         for (int k = 0; k < n_seg; ++k) crc[k] = 0;
         for (const Piece &p : pieces) crc[p.seg] = crc32_join(crc[p.seg], p.crc, p.b - p.a);
@@ -1361,7 +1607,7 @@ int mh_write_segments(mh_ctx *ctx, int fd, const int64_t *seg_off, uint32_t *crc
     c->seg_chunks.clear();
     c->seg_at.clear();
     c->phase_ms[MH_PHASE_WRITE] += ms_since(tw);
-    if (bad) { set_error("mh_write_segments: write failed (%s)", strerror(bad.load())); return -4; }
+    if (bad) { set_error("mh_write_segments: write failed (%s)", strerror(bad)); return -4; }
     return 0;
 }
 
@@ -1463,19 +1709,19 @@ int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, 
                          ((uint64_t)first << 20) ^ (uint64_t)n ^ (uint64_t)c->map_gen * 0x100000001b3ull;
     if (buf && c->fmt_key == key && c->fmt_valid) {
         size_t total = 0;
-        for (const std::string &t : c->fmt_chunks) total += t.size();
+        for (const TextBuf &t : c->fmt_chunks) total += t.size();
         if (used) *used = total;
         if (total > cap) { set_error("format buffer too small (%zu needed)", total); return -2; }
         size_t at = 0;
-        for (const std::string &t : c->fmt_chunks) { std::memcpy(buf + at, t.data(), t.size()); at += t.size(); }
+        for (const TextBuf &t : c->fmt_chunks) { std::memcpy(buf + at, t.data(), t.size()); at += t.size(); }
         c->fmt_chunks.clear();
         c->fmt_valid = false;
         return 0;
     }
-    std::vector<std::string> chunks;
+    std::vector<TextBuf> chunks;
     if (int st = format_chunks(c, style, order, first, n, refnames, chunks)) return st;
     size_t total = 0;
-    for (const std::string &t : chunks) total += t.size();
+    for (const TextBuf &t : chunks) total += t.size();
     if (used) *used = total;
     if (!buf) {
         c->fmt_chunks.swap(chunks);
@@ -1486,7 +1732,7 @@ int mh_format_rows(mh_ctx *ctx, int style, const int64_t *order, int64_t first, 
     c->fmt_valid = false;
     if (total > cap) { set_error("format buffer too small (%zu needed)", total); return -2; }
     size_t at = 0;
-    for (const std::string &t : chunks) { std::memcpy(buf + at, t.data(), t.size()); at += t.size(); }
+    for (const TextBuf &t : chunks) { std::memcpy(buf + at, t.data(), t.size()); at += t.size(); }
     return 0;
 }
 

@@ -52,7 +52,7 @@ int s2a_threads();
 using namespace mh;
 
 struct mh_fastq {
-    std::string data;              // the held text
+    TextBuf data;                  // the held text
     std::vector<int64_t> rec;      // byte offsets of its record starts (mh_fastq_frame)
     bool framed = false;
 };
@@ -64,7 +64,7 @@ struct FileView {
     const uint8_t *p = nullptr;
     int64_t size = 0;
     void *map = nullptr;
-    std::string copy;
+    TextBuf copy;
     ~FileView() { if (map) munmap(map, (size_t)size); }
 };
 
@@ -94,7 +94,7 @@ int view_file(const char *path, int fd_in, FileView &v)
         v.copy.resize((size_t)v.size);
         int64_t got = 0;
         while (got < v.size) {
-            const ssize_t r = pread(fd, &v.copy[got], (size_t)(v.size - got), (off_t)got);
+            const ssize_t r = pread(fd, v.copy.data() + got, (size_t)(v.size - got), (off_t)got);
             if (r <= 0) { set_error("cannot read FASTQ %s", path ? path : "(descriptor)"); rc = -3; break; }
             got += r;
         }
@@ -182,7 +182,7 @@ int mh_fastq_open_part(const char *path, int fd, int part, int parts, mh_fastq *
         } else if (c1 > c0) {
             fq->data.assign((const char *)v.p + c0, (size_t)(c1 - c0));
         }
-        const std::string &d = fq->data;
+        const TextBuf &d = fq->data;
         const int64_t n = (int64_t)d.size();
         // newlines, counted on host threads
         const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 22) + 1));
@@ -229,7 +229,7 @@ int mh_fastq_frame(mh_fastq *fq, int64_t line0, int starts_line, int64_t *out)
 {
     if (!fq || !out || line0 < 0) { set_error("mh_fastq_frame: bad arguments"); return -3; }
     try {
-        const std::string &d = fq->data;
+        const TextBuf &d = fq->data;
         const int64_t n = (int64_t)d.size();
         fq->rec.clear();
         int64_t first_line = -1;
@@ -289,15 +289,15 @@ int mh_fastq_splice(mh_fastq *fq, int64_t lo, int64_t hi, const char *front, int
         return -3;
     }
     try {
-        std::string &d = fq->data;
+        TextBuf &d = fq->data;
         if (flen == 0) {
-            d.resize((size_t)hi);
-            d.erase(0, (size_t)lo);
+            if (lo > 0) memmove(d.data(), d.data() + lo, (size_t)(hi - lo));
+            d.resize((size_t)(hi - lo));
         } else {
-            std::string t;
+            TextBuf t;
             t.reserve((size_t)(flen + (hi - lo) + blen));
             t.append(front, (size_t)flen);
-            t.append(d, (size_t)lo, (size_t)(hi - lo));
+            t.append(d.data() + lo, (size_t)(hi - lo));
             d.swap(t);
         }
         if (blen) d.append(back, (size_t)blen);
@@ -328,9 +328,9 @@ int mh_fastq_close(mh_fastq *fq)
 
 namespace mh {
 
-std::string take_fastq_text(mh_fastq *fq)
+TextBuf take_fastq_text(mh_fastq *fq)
 {
-    std::string out;
+    TextBuf out;
     out.swap(fq->data);
     fq->rec.clear();
     fq->framed = false;

@@ -2,9 +2,11 @@
 #pragma once
 #include <string>
 
+#include "mh_gunzip.h"
+
 struct mh_fastq;
 
 namespace mh {
 // move the held text out of a staged FASTQ (the handle keeps an empty text)
-std::string take_fastq_text(mh_fastq *fq);
+TextBuf take_fastq_text(mh_fastq *fq);
 }  // namespace mh

@@ -69,7 +69,8 @@ const LdApi &ld_api()
     return api;
 }
 
-int gunzip_zlib(const uint8_t *src, int64_t len, std::string &out, std::string &why)
+template <class Buf>
+int gunzip_zlib(const uint8_t *src, int64_t len, Buf &out, std::string &why)
 {
     z_stream z{};
     if (inflateInit2(&z, 15 + 32) != Z_OK) { why = "zlib init"; return -3; }
@@ -106,7 +107,8 @@ int gunzip_zlib(const uint8_t *src, int64_t len, std::string &out, std::string &
     return 0;
 }
 
-int gunzip_ld(const LdApi &api, const uint8_t *src, int64_t len, std::string &out, std::string &why)
+template <class Buf>
+int gunzip_ld(const LdApi &api, const uint8_t *src, int64_t len, Buf &out, std::string &why)
 {
     Ld *d = api.alloc();
     if (!d) { why = "libdeflate: out of memory"; return -2; }
@@ -194,7 +196,8 @@ void run_threads(int nt, const std::function<void(int)> &fn)
 // whole member of exactly that size.  Spans that fail (a false candidate
 // split a member) are merged with the next span(s) and decoded again;
 // -1 when that does not resolve them (the caller then decodes serially).
-int gunzip_members(const LdApi &api, const uint8_t *src, int64_t len, std::string &out, int threads)
+template <class Buf>
+int gunzip_members(const LdApi &api, const uint8_t *src, int64_t len, Buf &out, int threads)
 {
     std::vector<int64_t> cand;
     {
@@ -319,7 +322,8 @@ int gunzip_threads()
     return std::max(1, std::min(n, 64));
 }
 
-int gunzip_buffer(const uint8_t *src, int64_t len, std::string &out, std::string &why)
+template <class Buf>
+int gunzip_any(const uint8_t *src, int64_t len, Buf &out, std::string &why)
 {
     out.clear();
     if (len <= 0) return 0;
@@ -335,15 +339,25 @@ int gunzip_buffer(const uint8_t *src, int64_t len, std::string &out, std::string
             st = -1;
         }
         if (st == 0) return 0;
-        std::string().swap(out);
+        Buf().swap(out);
     }
     try {
         return api.ok ? gunzip_ld(api, src, len, out, why) : gunzip_zlib(src, len, out, why);
     } catch (const std::exception &) {
-        std::string().swap(out);
+        Buf().swap(out);
         why = "out of memory";
         return -2;
     }
+}
+
+int gunzip_buffer(const uint8_t *src, int64_t len, std::string &out, std::string &why)
+{
+    return gunzip_any(src, len, out, why);
+}
+
+int gunzip_buffer(const uint8_t *src, int64_t len, TextBuf &out, std::string &why)
+{
+    return gunzip_any(src, len, out, why);
 }
 
 int gzip_member(const char *src, size_t len, std::string &out, int level)

@@ -2,13 +2,59 @@
 #pragma once
 #include <stdint.h>
 
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
 #include <string>
 
 namespace mh {
 
+// A growable byte buffer whose new bytes are not zero-filled (a GB-sized
+// std::string::resize is a serial memset before the threads that fill it
+// can start; here the pages are first touched by the threads that write
+// them).
+class TextBuf {
+  public:
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    char *data() { return p_.get(); }
+    const char *data() const { return p_.get(); }
+    char &operator[](size_t i) { return p_[i]; }
+    const char &operator[](size_t i) const { return p_[i]; }
+    void reserve(size_t k)
+    {
+        if (k <= cap_) return;
+        std::unique_ptr<char[]> q(new char[k]);
+        if (n_) memcpy(q.get(), p_.get(), n_);
+        p_.swap(q);
+        cap_ = k;
+    }
+    void resize(size_t k)   // new bytes are left uninitialised
+    {
+        if (k > cap_) reserve(std::max(k, cap_ + cap_ / 2));
+        n_ = k;
+    }
+    void append(const char *s, size_t k)
+    {
+        const size_t at = n_;
+        resize(n_ + k);
+        if (k) memcpy(p_.get() + at, s, k);
+    }
+    void assign(const char *s, size_t k) { n_ = 0; append(s, k); }
+    void clear() { n_ = 0; }
+    void release() { p_.reset(); n_ = cap_ = 0; }
+    void swap(TextBuf &o) { p_.swap(o.p_); std::swap(n_, o.n_); std::swap(cap_, o.cap_); }
+
+  private:
+    std::unique_ptr<char[]> p_;
+    size_t n_ = 0, cap_ = 0;
+};
+
 // Decode a whole gzip buffer (all concatenated members) into `out`.
 // 0 on success; -3 (or -2 out of memory) with `why` set otherwise.
 int gunzip_buffer(const uint8_t *src, int64_t len, std::string &out, std::string &why);
+int gunzip_buffer(const uint8_t *src, int64_t len, TextBuf &out, std::string &why);
 // true when the libdeflate decoder is in use
 bool gunzip_fast_available();
 // One gzip member of src[0 .. len) at `level` (libdeflate when present);

@@ -8,6 +8,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <tuple>
 #include <vector>
 
@@ -209,6 +210,28 @@ int run_gotoh_batch(struct Ctx &c, int count, const char *const *s1, const char 
                     char *const *out1, char *const *out2, const int *cap, int *score,
                     int *status);
 
+// Read names (QNAMEs) in one byte pool: name r is bytes off[r] .. off[r + 1]
+// (one allocation for millions of names instead of one string each).
+struct NameTable {
+    std::string pool;
+    std::vector<int64_t> off{0};
+    size_t size() const { return off.size() - 1; }
+    std::string_view operator[](size_t r) const
+    {
+        return std::string_view(pool.data() + off[r], (size_t)(off[r + 1] - off[r]));
+    }
+    void clear() { pool.clear(); off.assign(1, 0); }
+    void assign(const char *const *names, int64_t n)
+    {
+        clear();
+        off.resize((size_t)n + 1);
+        for (int64_t r = 0; r < n; ++r) off[r + 1] = off[r] + (int64_t)strlen(names[r]);
+        pool.resize((size_t)off[n]);
+        for (int64_t r = 0; r < n; ++r) memcpy(&pool[off[r]], names[r], (size_t)(off[r + 1] - off[r]));
+    }
+    void swap(NameTable &o) { pool.swap(o.pool); off.swap(o.off); }
+};
+
 struct ProfEntry {
     double ms = 0.0;
     int64_t launches = 0;
@@ -250,7 +273,7 @@ struct Ctx {
     std::vector<ProfPending> prof_pending;
     hipStream_t stream = nullptr;
     DevReads reads;
-    std::vector<std::string> names;  // QNAMEs for SAM text
+    NameTable names;                 // QNAMEs for SAM text
     std::vector<std::string> host_seq, host_qual; // kept only when names are
     DevIndex index;
     MapState map;

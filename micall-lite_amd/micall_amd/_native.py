@@ -82,6 +82,9 @@ def _declare(L):
         'mh_write_rows': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.c_int64,
                            ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_int64, _I64P],
                           ctypes.c_int),
+        'mh_write_rows_crc': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.c_int64,
+                               ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_int64, _I64P,
+                               ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
         'mh_file_checksum': ([ctypes.c_int, _I64P, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         'mh_rows_load': ([_P, ctypes.c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                           ctypes.c_int64, _P], ctypes.c_int),
@@ -470,6 +473,23 @@ class Context:
         check(lib().mh_format_segments(self.h, style, None if order is None else _ptr(order), n,
                                        names, k, _ptr(seg_rows), _ptr(out)), 'mh_format_segments')
         return out[:k]
+
+    def write_rows_at(self, fd, offset, style, order=None):
+        """Rows order[...] (None: every read) formatted and written to
+        descriptor fd at `offset` in one stream (formatting overlapped with
+        the write); returns (bytes written, crc32)."""
+        if order is not None:
+            order = np.ascontiguousarray(order, dtype=np.int64)
+            n = len(order)
+        else:
+            n = self.reads_count()[0]
+        names = (ctypes.c_char_p * max(self.n_refs, 1))(*[r.encode() for r in self.refnames])
+        written = ctypes.c_int64()
+        crc = ctypes.c_uint32()
+        check(lib().mh_write_rows_crc(self.h, style, None if order is None else _ptr(order), 0, n,
+                                      names, int(fd), int(offset), ctypes.byref(written),
+                                      ctypes.byref(crc)), 'mh_write_rows_crc')
+        return written.value, crc.value
 
     def write_segments(self, fd, offsets, crc=True):
         """Write the last format_segments text, segment s at file offset

@@ -375,6 +375,15 @@ class SharedOutput:
                     for a, b in zip(seg_rows[:-1], seg_rows[1:])]
             self.write_bytes(segs)
             return
+        if self.sh is None:
+            # one process: the segments are contiguous; one formatting +
+            # writing stream
+            o = np.asarray(order)[seg_rows[0]:seg_rows[-1]] if order is not None else None
+            n, crc = ctx.write_rows_at(self.fd, self.end, style, o)
+            self.written.append((self.end, n, crc))
+            self.end += n
+            IO_STATS['written_bytes'] += n
+            return
         lens = ctx.format_segments(style, order, seg_rows)
         offs = self.place(lens)
         crcs = ctx.write_segments(self.fd, offs)
