@@ -165,3 +165,43 @@ def test_writer_and_block_rule_without_a_group():
     """Outside a process group the drop-ins write everything themselves."""
     assert session.shard() is None
     assert session.is_writer()
+
+
+def _stage_worker(rank, world, port, out_dir):
+    """session.writer_stage under gloo: rank 0 writes, the others wait and
+    see the complete file after the stage; a failure on rank 0 is raised on
+    every rank."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank), MICALL_DIST_BACKEND='gloo')
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        session._shard_checked = False
+        session._shard = None
+        sh = Shard(rank, world, 0)
+        session._shard, session._shard_checked = sh, True
+        path = os.path.join(out_dir, 'stage.csv')
+        with open(path, 'w') as f:
+            with session.writer_stage(f) as st:
+                assert st.active == (rank == 0)
+                if st.active:
+                    f.write('a,b\n' * 1000)
+            assert open(path).read() == 'a,b\n' * 1000      # complete on every rank
+        raised = None
+        try:
+            with session.writer_stage() as st:
+                if st.active:
+                    raise ValueError('rank 0 fails')
+        except Exception as ex:
+            raised = type(ex).__name__
+        assert raised == ('ValueError' if rank == 0 else 'RuntimeError'), raised
+        open(os.path.join(out_dir, 'ok%d' % rank), 'w').close()
+    finally:
+        session._shard, session._shard_checked = None, False
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('world', [2, 3])
+def test_writer_stage_barriers_and_failures_gloo(tmp_path, world):
+    mp.spawn(_stage_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert all((tmp_path / ('ok%d' % r)).exists() for r in range(world))
