@@ -41,13 +41,16 @@ def algo_bytes_per_pair(L=READ_LEN):
 
 
 def bench_genomes(which='pol', read_len=READ_LEN):
-    """Seeds the synthetic sample genomes derive from: 'pol' (C2/C3/C5) or
+    """Seeds the synthetic sample genomes derive from: 'pol' (C2/C3/C5),
     'hiv' (C4: the HIV-1 seeds that hold a fragment of >= 260 nt; vpu, 246 nt,
-    is shorter than a read)."""
+    is shorter than a read) or 'all' (C4's other reading: every seed region of
+    the project file long enough for a fragment)."""
     from micall_amd import projects
     seeds = projects.load_default().seed_sequences()
     if which == 'pol':
         return {'HIV1B-pol-seed': seeds['HIV1B-pol-seed']}
+    if which == 'all':   # SURVEY.md 8(d) C4, the all-seed-regions reading
+        return {k: v for k, v in seeds.items() if len(v) >= max(260, read_len + 9)}
     return {k: v for k, v in seeds.items() if k.startswith('HIV') and len(v) >= max(260, read_len + 9)}
 
 
@@ -686,9 +689,10 @@ def main():
     ap.add_argument('--unpaired', action='store_true',
                     help='unpaired reads (--pairs reads per GPU; C5-style with --read-len 300)')
     ap.add_argument('--read-len', type=int, default=READ_LEN)
-    ap.add_argument('--genomes', choices=('pol', 'hiv'), default='pol',
+    ap.add_argument('--genomes', choices=('pol', 'hiv', 'all'), default='pol',
                     help='pol: HIV-1 pol sample genome (C2/C3/C5); hiv: mixed-region reads over '
-                         'the HIV-1 seeds in proportion to length (C4)')
+                         'the HIV-1 seeds in proportion to length (C4); all: over every seed '
+                         'region (the all-seed reading of C4)')
     ap.add_argument('--force-iterations', action='store_true',
                     help='run exactly --iterations remap passes per step (C3: "3 remap '
                          'iterations"), the stopping rules applying only after them')
@@ -832,6 +836,9 @@ def main():
                                     'C4-style: synthetic 2x{} nt mixed-region read pairs over the HIV-1 '
                                     'seeds {}'.format(L, ','.join(bench_genomes('hiv', L)))
                                     if args.genomes == 'hiv' else
+                                    'C4-style, all seed regions: synthetic 2x{} nt read pairs over the {} '
+                                    'seeds of >= 260 nt'.format(L, len(bench_genomes('all', L)))
+                                    if args.genomes == 'all' else
                                     ('C2' if args.iterations == 1 else 'C3-style') +
                                     ': synthetic 2x{} nt HIV-1 pol read pairs'.format(L)) +
                                    ' (10% divergent '

@@ -139,6 +139,15 @@ int mh_fastq_splice(mh_fastq *fq, int64_t lo, int64_t hi, const char *front, int
 /* the held text (valid until the handle changes or is closed) */
 int mh_fastq_view(mh_fastq *fq, const char **data, int64_t *len);
 int mh_fastq_close(mh_fastq *fq);
+/* Host-only parse of staged FASTQ text (fq2 NULL: unpaired) as the loader
+ * parses it (records, bowtie2 QNAMEs, SEQ / QUAL; the texts are kept): the
+ * QNAMEs '\n'-terminated in names, the bases and qualities concatenated,
+ * the lengths per read (mates interleaved).  With names, seq, qual or lens
+ * NULL only the sizes are returned.  For tests of the ingest without a
+ * device. */
+int mh_fastq_parse(mh_fastq *fq1, mh_fastq *fq2, char *names, size_t names_cap, uint8_t *seq,
+                   uint8_t *qual, size_t bases_cap, int32_t *lens, int64_t reads_cap, int64_t *n_reads,
+                   int64_t *n_bases, size_t *names_used);
 /* Load the reads of staged FASTQ text: units [range[0], range[1]) of fq1's
  * records and [range[2], range[3]) of fq2's (-1, -1: all of them; the two
  * counts must agree), mates interleaved when fq2 is given.  The records are

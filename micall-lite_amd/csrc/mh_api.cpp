@@ -746,8 +746,11 @@ int mh_reads_load_fastq(mh_ctx *ctx, const char *path1, const char *path2, int64
 // The reads of units [a0, a1) of FASTQ a (and [b0, b1) of b, the mates):
 // copied once from the decoded text into the buffers the context keeps for
 // the SAM text, uploaded and packed.
-static int load_fastq_units(CtxEx *c, Fastq &a, Fastq *b, int64_t a0, int64_t a1, int64_t b0,
-                            int64_t b1, int64_t lines1, int64_t *n_reads)
+// The host half of a FASTQ load: the reads of units [a0, a1) of FASTQ a
+// (and [b0, b1) of b, the mates, interleaved) copied once from the decoded
+// text into `h` (SEQ / QUAL of the SAM rows) and their QNAMEs into `names`.
+static int host_reads_from(Fastq &a, Fastq *b, int64_t a0, int64_t a1, int64_t b0, int64_t b1,
+                           HostReads &h, NameTable &names, double *names_ms, double *copy_ms)
 {
     const bool paired = b != nullptr;
     if (a0 < 0 || a1 < a0 || a1 > (int64_t)a.size() ||
@@ -756,10 +759,8 @@ static int load_fastq_units(CtxEx *c, Fastq &a, Fastq *b, int64_t a0, int64_t a1
                   (long long)(paired ? b1 - b0 : a1 - a0));
         return -3;
     }
-    const auto t0 = std::chrono::steady_clock::now();
     const int per = paired ? 2 : 1;
     const int64_t n = per * (a1 - a0);
-    HostReads h;
     h.off.resize((size_t)n);
     h.len.resize((size_t)n);
     int64_t total = 0;
@@ -774,7 +775,7 @@ static int load_fastq_units(CtxEx *c, Fastq &a, Fastq *b, int64_t a0, int64_t a1
     h.qual.alloc((size_t)total);
     const auto tn = std::chrono::steady_clock::now();
     // names: spans first (sizes), then every thread copies its names into the pool
-    NameTable names;
+    names.clear();
     names.off.resize((size_t)n + 1);
     std::vector<int64_t> nstart((size_t)n);
     const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
@@ -807,7 +808,7 @@ static int load_fastq_units(CtxEx *c, Fastq &a, Fastq *b, int64_t a0, int64_t a1
         }
     });
     names.off[0] = 0;
-    const double names_ms = ms_since(tn);
+    *names_ms = ms_since(tn);
     const auto tc = std::chrono::steady_clock::now();
     par_for(nt, [&](int t) {
         for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
@@ -822,7 +823,20 @@ static int load_fastq_units(CtxEx *c, Fastq &a, Fastq *b, int64_t a0, int64_t a1
             for (int64_t x = cq; x < L; ++x) h.qual.data()[h.off[i] + x] = 'I';
         }
     });
-    const double copy_ms = ms_since(tc);
+    *copy_ms = ms_since(tc);
+    return 0;
+}
+
+static int load_fastq_units(CtxEx *c, Fastq &a, Fastq *b, int64_t a0, int64_t a1, int64_t b0,
+                            int64_t b1, int64_t lines1, int64_t *n_reads)
+{
+    const bool paired = b != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    HostReads h;
+    NameTable names;
+    double names_ms = 0, copy_ms = 0;
+    if (int st = host_reads_from(a, b, a0, a1, b0, b1, h, names, &names_ms, &copy_ms)) return st;
+    const int64_t n = (int64_t)h.len.size();
     const auto tf = std::chrono::steady_clock::now();
     a = Fastq{};
     if (b) *b = Fastq{};
@@ -927,6 +941,58 @@ int mh_reads_load_staged(mh_ctx *ctx, mh_fastq *fq1, mh_fastq *fq2, const int64_
     const int64_t b0 = range4[2] < 0 ? 0 : range4[2];
     const int64_t b1 = range4[3] < 0 ? (int64_t)b.size() : range4[3];
     return load_fastq_units(c, a, paired ? &b : nullptr, a0, a1, b0, b1, fastq_lines1, n_reads);
+}
+
+int mh_fastq_parse(mh_fastq *fq1, mh_fastq *fq2, char *names, size_t names_cap, uint8_t *seq,
+                   uint8_t *qual, size_t bases_cap, int32_t *lens, int64_t reads_cap, int64_t *n_reads,
+                   int64_t *n_bases, size_t *names_used)
+{
+    if (!fq1 || !n_reads || !n_bases || !names_used) { set_error("mh_fastq_parse: bad arguments"); return -3; }
+    try {
+        const bool paired = fq2 != nullptr;
+        Fastq a, b;
+        a.data.assign(fastq_text(fq1).data(), fastq_text(fq1).size());
+        if (paired) b.data.assign(fastq_text(fq2).data(), fastq_text(fq2).size());
+        if (int st = index_fastq(a, "FASTQ 1", nullptr)) return st;
+        if (paired)
+            if (int st = index_fastq(b, "FASTQ 2", nullptr)) return st;
+        if (paired && a.size() != b.size()) {
+            set_error("paired FASTQ files hold %zu and %zu reads", a.size(), b.size());
+            return -3;
+        }
+        HostReads h;
+        NameTable nt;
+        double x = 0, y = 0;
+        if (int st = host_reads_from(a, paired ? &b : nullptr, 0, (int64_t)a.size(), 0,
+                                     paired ? (int64_t)b.size() : 0, h, nt, &x, &y))
+            return st;
+        const int64_t n = (int64_t)h.len.size();
+        const int64_t bases = n ? h.off[n - 1] + h.len[n - 1] : 0;
+        *n_reads = n;
+        *n_bases = bases;
+        *names_used = nt.pool.size() + (size_t)n;
+        if (!names || !seq || !qual || !lens) return 0;   // a size query
+        if (reads_cap < n || bases_cap < (size_t)bases || names_cap < *names_used) {
+            set_error("mh_fastq_parse: buffers too small");
+            return -2;
+        }
+        size_t at = 0;
+        for (int64_t r = 0; r < n; ++r) {
+            const std::string_view v = nt[(size_t)r];
+            memcpy(names + at, v.data(), v.size());
+            at += v.size();
+            names[at++] = '\n';
+            lens[r] = h.len[r];
+        }
+        if (bases) {
+            memcpy(seq, h.seq.data(), (size_t)bases);
+            memcpy(qual, h.qual.data(), (size_t)bases);
+        }
+        return 0;
+    } catch (const std::bad_alloc &) {
+        set_error("mh_fastq_parse: out of memory");
+        return -2;
+    }
 }
 
 int mh_reads_count(mh_ctx *ctx, int64_t *n_reads, int *paired)

@@ -328,6 +328,8 @@ int mh_fastq_close(mh_fastq *fq)
 
 namespace mh {
 
+const TextBuf &fastq_text(const mh_fastq *fq) { return fq->data; }
+
 TextBuf take_fastq_text(mh_fastq *fq)
 {
     TextBuf out;

@@ -9,4 +9,6 @@ struct mh_fastq;
 namespace mh {
 // move the held text out of a staged FASTQ (the handle keeps an empty text)
 TextBuf take_fastq_text(mh_fastq *fq);
+// the held text of a staged FASTQ
+const TextBuf &fastq_text(const mh_fastq *fq);
 }  // namespace mh

@@ -145,6 +145,8 @@ def _declare(L):
                              ctypes.c_int64], ctypes.c_int),
         'mh_fastq_view': ([_P, ctypes.POINTER(_P), _I64P], ctypes.c_int),
         'mh_fastq_close': ([_P], ctypes.c_int),
+        'mh_fastq_parse': ([_P, _P, ctypes.c_char_p, ctypes.c_size_t, _P, _P, ctypes.c_size_t, _P,
+                            ctypes.c_int64, _I64P, _I64P, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         'mh_reads_load_staged': ([_P, _P, _P, _I64P, ctypes.c_int64, _I64P], ctypes.c_int),
         'mh_format_segments': ([_P, ctypes.c_int, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_char_p),
                                 ctypes.c_int, _P, _P], ctypes.c_int),
@@ -898,6 +900,29 @@ class Fastq:
         check(lib().mh_fastq_splice(self.h, int(lo), int(hi), None if f is None else _ptr(f),
                                     0 if f is None else len(f), None if b is None else _ptr(b),
                                     0 if b is None else len(b)), 'mh_fastq_splice')
+
+    def parse(self, mate=None):
+        """The reads the loader would take from this text (and `mate`'s, the
+        R2 text, interleaved): ([qname], [seq bytes], [qual bytes]).  Host
+        only (tests of the ingest without a device)."""
+        n, nb, nn = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_size_t()
+        m = mate.h if mate is not None else None
+        check(lib().mh_fastq_parse(self.h, m, None, 0, None, None, 0, None, 0, ctypes.byref(n),
+                                   ctypes.byref(nb), ctypes.byref(nn)), 'mh_fastq_parse')
+        names = ctypes.create_string_buffer(max(nn.value, 1))
+        seq = np.zeros(max(nb.value, 1), dtype=np.uint8)
+        qual = np.zeros(max(nb.value, 1), dtype=np.uint8)
+        lens = np.zeros(max(n.value, 1), dtype=np.int32)
+        check(lib().mh_fastq_parse(self.h, m, names, len(names), _ptr(seq), _ptr(qual), len(seq),
+                                   _ptr(lens), len(lens), ctypes.byref(n), ctypes.byref(nb),
+                                   ctypes.byref(nn)), 'mh_fastq_parse')
+        qn = names.raw[:nn.value].decode().split('\n')[:n.value]
+        out_s, out_q, at = [], [], 0
+        for L in lens[:n.value].tolist():
+            out_s.append(seq[at:at + L].tobytes())
+            out_q.append(qual[at:at + L].tobytes())
+            at += L
+        return qn, out_s, out_q
 
     def close(self):
         if getattr(self, 'h', None):

@@ -10,7 +10,7 @@ set -e -o pipefail
 R=$GRAFT_REPO_ROOT
 WHAT=${1:-all}
 O=$R/gpurun_out/r04
-mkdir -p $O/c2 $O/c3 $O/c4 $O/c5
+mkdir -p $O/c2 $O/c3 $O/c4 $O/c4all $O/c5
 cd $R
 if [ "$WHAT" = c2 ] || [ "$WHAT" = all ]; then
   timeout -k 10 500 python3 bench.py --breakdown > $O/c2/bench.json 2> $O/c2/bench.err
@@ -37,6 +37,10 @@ fi
 if [ "$WHAT" = c5 ] || [ "$WHAT" = all ]; then
   timeout -k 10 400 python3 bench.py --unpaired --read-len 300 --pairs 2000000 --steps 10 --warmup 2 \
       > $O/c5/bench.json 2> $O/c5/bench.err
+fi
+if [ "$WHAT" = c4all ] || [ "$WHAT" = all ]; then
+  timeout -k 10 500 python3 bench.py --genomes all --pairs 5000000 --steps 3 --warmup 1 --breakdown \
+      > $O/c4all/bench.json 2> $O/c4all/bench.err
 fi
 if [ "$WHAT" = c4 ] || [ "$WHAT" = all ]; then
   timeout -k 10 400 python3 bench.py --genomes hiv --pairs 5000000 --steps 3 --warmup 1 --breakdown > $O/c4/bench.json 2> $O/c4/bench.err

@@ -207,3 +207,68 @@ def test_parallel_gunzip_matches_serial(tmp_path):
         fq = _native.Fastq(str(path))
         assert fq.view().tobytes() == gzip.decompress(blob)
         fq.close()
+
+
+def _py_reads(text, paired):
+    """The loader's reading of FASTQ text (mh_api.cpp index_fastq and
+    qname_span): blank lines skipped where a record starts, '\\r' before
+    '\\n' dropped, QNAME = header up to the first blank (bowtie2), '/1' '/2'
+    dropped for mates, QUAL padded with 'I' / cut to the SEQ length."""
+    lines = text.split(b'\n')
+    if lines and lines[-1] == b'':
+        lines = lines[:-1]
+    lines = [ln[:-1] if ln.endswith(b'\r') else ln for ln in lines]
+    out, k = [], 0
+    while k < len(lines):
+        if lines[k] == b'':
+            k += 1
+            continue
+        h, seq, qual = lines[k], lines[k + 1], lines[k + 3]
+        a = 1 if h[:1] == b'@' else 0
+        while a < len(h) and h[a:a + 1] in (b' ', b'\t'):
+            a += 1
+        b = a
+        while b < len(h) and h[b:b + 1] not in (b' ', b'\t', b'\r'):
+            b += 1
+        name = h[a:b]
+        if paired and len(name) > 2 and name[-2:-1] == b'/' and name[-1:] in (b'1', b'2'):
+            name = name[:-2]
+        q = (qual + b'I' * len(seq))[:len(seq)]
+        out.append((name.decode(), seq, q))
+        k += 4
+    return out
+
+
+@pytest.mark.parametrize('variant', ['plain', 'crlf', 'slash', 'blank_and_short_qual'])
+def test_host_parse_matches_the_loader_rules(tmp_path, variant):
+    """mh_fastq_parse: the host half of the loader (records, bowtie2 QNAMEs,
+    SEQ / QUAL, mates interleaved) against a Python restatement, on R1 / R2
+    texts with CRLF line ends, '/1' '/2' name suffixes, blank lines between
+    records and qualities shorter than the read."""
+    r1 = _records(300, 1, 11, crlf=variant == 'crlf')
+    r2 = _records(300, 2, 12, crlf=variant == 'crlf')
+    if variant == 'slash':
+        r1 = [r.replace(b' 1:N', b'/1 1:N') for r in r1]
+        r2 = [r.replace(b' 2:N', b'/2 2:N') for r in r2]
+    if variant == 'blank_and_short_qual':
+        r1[10] = b'\n' + r1[10]
+        parts = r2[20].split(b'\n')
+        parts[3] = parts[3][:-5]
+        r2[20] = b'\n'.join(parts)
+    paths = []
+    for k, rs in enumerate((r1, r2)):
+        p = tmp_path / ('R%d.fastq.gz' % (k + 1))
+        p.write_bytes(_gz_members(b''.join(rs), 5000))
+        paths.append(str(p))
+    a, b = _native.Fastq(paths[0]), _native.Fastq(paths[1])
+    names, seqs, quals = a.parse(b)
+    want1, want2 = _py_reads(b''.join(r1), True), _py_reads(b''.join(r2), True)
+    want = [x for pair in zip(want1, want2) for x in pair]
+    assert names == [w[0] for w in want]
+    assert seqs == [w[1] for w in want]
+    assert quals == [w[2] for w in want]
+    un_names, un_seqs, _ = a.parse()
+    assert un_names[:3] == [w[0] for w in _py_reads(b''.join(r1), False)][:3]
+    assert len(un_seqs) == 300
+    a.close()
+    b.close()
