@@ -2237,162 +2237,109 @@ __device__ void tally_flush(const PairArgs &A, TallyLds *T)
     }
 }
 
-// One wave per block of PAIR_UNITS units.  The block's slots (every read's
-// first n_cand of its MAXCAND) are copied to LDS with coalesced dword loads,
-// each lane pairs its unit from LDS, and the records go back through LDS to
-// coalesced dword stores: the slot array is read, and the record array
-// written, as two streams instead of 52- and 88-byte structs per lane.
-constexpr int PAIR_UNITS = 64;
-constexpr int SLOT_WORDS = (int)(sizeof(Slot) / 4);
-constexpr int REC_WORDS = (int)(sizeof(Rec) / 4);
-static_assert(sizeof(Slot) % 4 == 0 && sizeof(Rec) % 4 == 0, "word-sized records");
-
-__device__ __forceinline__ void pair_unit(const PairArgs &A, TallyLds *T, const Slot *ls,
-                                          const int32_t *lnc, int64_t u, int l, Rec *lrec)
+__global__ __launch_bounds__(256) void k_pair(PairArgs A)
 {
-    if (!A.paired) {
-        MateView mv;
-        mv.s = ls + (size_t)l * MAXCAND;
-        mv.n = lnc[l];
-        mv.best = -1;
-        int bs = 0;
-        for (int c = 0; c < mv.n; ++c) {
-            const int v = mv.s[c].valid, sc = mv.s[c].score;
-            if (v && (mv.best < 0 || sc > bs)) { mv.best = c; bs = sc; }
-        }
-        Rec o;
-        clear_rec(o);
-        o.yf = A.yf[u];
-        o.yt = 3;
-        if (mv.best >= 0) {
-            fill_aligned(A, o, mv, mv.best, A.R.len[u]);
-            o.flag = o.rev ? 0x10 : 0;
-        } else {
-            o.flag = 0x4;
-        }
-        lrec[l] = o;
-        tally(A, T, o, u);
-        return;
-    }
-    const int64_t r1 = 2 * u, r2 = 2 * u + 1;
-    MateView m1, m2;
-    m1.s = ls + (size_t)(2 * l) * MAXCAND;
-    m2.s = ls + (size_t)(2 * l + 1) * MAXCAND;
-    m1.n = lnc[2 * l];
-    m2.n = lnc[2 * l + 1];
-    for (MateView *mv : {&m1, &m2}) {
-        mv->best = -1;
-        int bs = 0;
-        for (int c = 0; c < mv->n; ++c) {
-            const int v = mv->s[c].valid, sc = mv->s[c].score;
-            if (v && (mv->best < 0 || sc > bs)) { mv->best = c; bs = sc; }
-        }
-    }
-    Rec o1, o2;
-    clear_rec(o1);
-    clear_rec(o2);
-    o1.yf = A.yf[r1];
-    o2.yf = A.yf[r2];
-    int c1 = m1.best, c2 = m2.best, conc = 0;
-    long long best_sum = -9223372036854775807ll - 1;
-    for (int x = 0; x < m1.n; ++x) {
-        const Slot sx = m1.s[x];
-        if (!sx.valid) continue;
-        for (int y = 0; y < m2.n; ++y) {
-            const Slot sy = m2.s[y];
-            if (!sy.valid) continue;
-            if (!concordant(sx, sy, A.maxins)) continue;
-            const long long sum = (long long)sx.score + sy.score;
-            if (sum > best_sum) { best_sum = sum; c1 = x; c2 = y; conc = 1; }
-        }
-    }
-    const int al1 = c1 >= 0, al2 = c2 >= 0;
-    if (al1) fill_aligned(A, o1, m1, c1, A.R.len[r1]);
-    if (al2) fill_aligned(A, o2, m2, c2, A.R.len[r2]);
-    int f1 = 0x1 | 0x40, f2 = 0x1 | 0x80;
-    if (conc) { f1 |= 0x2; f2 |= 0x2; }
-    if (!al1) { f1 |= 0x4; f2 |= 0x8; }
-    if (!al2) { f2 |= 0x4; f1 |= 0x8; }
-    if (al1 && o1.rev) { f1 |= 0x10; f2 |= 0x20; }
-    if (al2 && o2.rev) { f2 |= 0x10; f1 |= 0x20; }
-    o1.flag = f1;
-    o2.flag = f2;
-    const int yt = conc ? 0 : (al1 && al2) ? 1 : 2;
-    o1.yt = o2.yt = yt;
-    if (al1 && al2) {
-        o1.ys = o2.score;
-        o2.ys = o1.score;
-        if (o1.ref == o2.ref) {
-            o1.rnext = o2.rnext = -1;
-            const Slot a = m1.s[c1], b = m2.s[c2];
-            const int lo = a.pos < b.pos ? a.pos : b.pos;
-            const int hi = a.end > b.end ? a.end : b.end;
-            const int t = hi - lo;
-            const bool first1 = a.pos <= b.pos;
-            o1.tlen = first1 ? t : -t;
-            o2.tlen = first1 ? -t : t;
-        } else {
-            o1.rnext = o2.ref;
-            o2.rnext = o1.ref;
-        }
-        o1.pnext = o2.sam_pos;
-        o2.pnext = o1.sam_pos;
-    } else if (al1 || al2) {
-        Rec &Al = al1 ? o1 : o2;
-        Rec &Un = al1 ? o2 : o1;
-        Un.sam_ref = Al.sam_ref;
-        Un.sam_pos = Al.sam_pos;
-        Al.rnext = Un.rnext = -1;
-        Al.pnext = Al.sam_pos;
-        Un.pnext = Al.sam_pos;
-        Un.ys = Al.score;
-    }
-    lrec[2 * l] = o1;
-    lrec[2 * l + 1] = o2;
-    tally(A, T, o1, r1);
-    tally(A, T, o2, r2);
-}
-
-__global__ __launch_bounds__(64) void k_pair(PairArgs A)
-{
-    __shared__ uint32_t s_slot[2 * PAIR_UNITS * MAXCAND * SLOT_WORDS];
-    __shared__ uint32_t s_rec[2 * PAIR_UNITS * REC_WORDS];
-    __shared__ int32_t s_nc[2 * PAIR_UNITS];
     __shared__ TallyLds sT;
     TallyLds *T = (A.n_refs <= TALLY_LDS_REFS && A.R.n < INT32_MAX) ? &sT : nullptr;
-    const int lane = threadIdx.x;
     if (T) {
-        for (int r = lane; r < TALLY_LDS_REFS; r += 64) {
+        for (int r = threadIdx.x; r < TALLY_LDS_REFS; r += blockDim.x) {
             T->lines[r] = T->filt[r] = T->mapped[r] = 0;
             T->first[r] = T->firstm[r] = INT32_MAX;
         }
-        if (lane == 0) { T->unmapped = T->star = 0; T->star_first = INT32_MAX; }
+        if (threadIdx.x == 0) { T->unmapped = T->star = 0; T->star_first = INT32_MAX; }
         __syncthreads();
     }
-    const int per = A.paired ? 2 : 1;
     const int64_t units = A.paired ? A.R.n / 2 : A.R.n;
-    for (int64_t u0 = (int64_t)blockIdx.x * PAIR_UNITS; u0 < units; u0 += (int64_t)gridDim.x * PAIR_UNITS) {
-        const int nu = (int)(units - u0 < PAIR_UNITS ? units - u0 : PAIR_UNITS);
-        const int nr = per * nu;
-        const int64_t r0 = per * u0;
-        for (int k = lane; k < nr; k += 64) s_nc[k] = A.n_cand[r0 + k];
-        __syncthreads();
-        // the block's slots, word by word; words of slots past a read's
-        // candidates are not loaded
-        const uint32_t *g = (const uint32_t *)(A.slot + r0 * MAXCAND);
-        const int words = nr * MAXCAND * SLOT_WORDS;
-        for (int w = lane; w < words; w += 64) {
-            const int rd = w / (MAXCAND * SLOT_WORDS);
-            const int c = (w - rd * MAXCAND * SLOT_WORDS) / SLOT_WORDS;
-            if (c < s_nc[rd]) s_slot[w] = __builtin_nontemporal_load(g + w);
+    // every thread runs the same trip count so the final barrier is uniform
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t trips = (units + stride - 1) / stride;
+    for (int64_t it = 0; it < trips; ++it) {
+        const int64_t u = it * stride + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (u >= units) continue;
+        if (!A.paired) {
+            MateView mv;
+            load_mate(A, u, mv);
+            Rec o;
+            clear_rec(o);
+            o.yf = A.yf[u];
+            o.yt = 3;
+            if (mv.best >= 0) {
+                fill_aligned(A, o, mv, mv.best, A.R.len[u]);
+                o.flag = o.rev ? 0x10 : 0;
+            } else {
+                o.flag = 0x4;
+            }
+            A.rec[u] = o;
+            tally(A, T, o, u);
+            continue;
         }
-        __syncthreads();
-        if (lane < nu)
-            pair_unit(A, T, (const Slot *)s_slot, s_nc, u0 + lane, lane, (Rec *)s_rec);
-        __syncthreads();
-        uint32_t *gr = (uint32_t *)(A.rec + r0);
-        for (int w = lane; w < nr * REC_WORDS; w += 64) gr[w] = s_rec[w];
-        __syncthreads();
+        const int64_t r1 = 2 * u, r2 = 2 * u + 1;
+        MateView m1, m2;
+        load_mate(A, r1, m1);
+        load_mate(A, r2, m2);
+        Rec o1, o2;
+        clear_rec(o1);
+        clear_rec(o2);
+        o1.yf = A.yf[r1];
+        o2.yf = A.yf[r2];
+        int c1 = m1.best, c2 = m2.best, conc = 0;
+        long long best_sum = -9223372036854775807ll - 1;
+        for (int x = 0; x < m1.n; ++x) {
+            const Slot sx = m1.s[x];
+            if (!sx.valid) continue;
+            for (int y = 0; y < m2.n; ++y) {
+                const Slot sy = m2.s[y];
+                if (!sy.valid) continue;
+                if (!concordant(sx, sy, A.maxins)) continue;
+                const long long s = (long long)sx.score + sy.score;
+                if (s > best_sum) { best_sum = s; c1 = x; c2 = y; conc = 1; }
+            }
+        }
+        const int al1 = c1 >= 0, al2 = c2 >= 0;
+        if (al1) fill_aligned(A, o1, m1, c1, A.R.len[r1]);
+        if (al2) fill_aligned(A, o2, m2, c2, A.R.len[r2]);
+        int f1 = 0x1 | 0x40, f2 = 0x1 | 0x80;
+        if (conc) { f1 |= 0x2; f2 |= 0x2; }
+        if (!al1) { f1 |= 0x4; f2 |= 0x8; }
+        if (!al2) { f2 |= 0x4; f1 |= 0x8; }
+        if (al1 && o1.rev) { f1 |= 0x10; f2 |= 0x20; }
+        if (al2 && o2.rev) { f2 |= 0x10; f1 |= 0x20; }
+        o1.flag = f1;
+        o2.flag = f2;
+        const int yt = conc ? 0 : (al1 && al2) ? 1 : 2;
+        o1.yt = o2.yt = yt;
+        if (al1 && al2) {
+            o1.ys = o2.score;
+            o2.ys = o1.score;
+            if (o1.ref == o2.ref) {
+                o1.rnext = o2.rnext = -1;
+                const Slot a = m1.s[c1], b = m2.s[c2];
+                const int lo = a.pos < b.pos ? a.pos : b.pos;
+                const int hi = a.end > b.end ? a.end : b.end;
+                const int t = hi - lo;
+                const bool first1 = a.pos <= b.pos;
+                o1.tlen = first1 ? t : -t;
+                o2.tlen = first1 ? -t : t;
+            } else {
+                o1.rnext = o2.ref;
+                o2.rnext = o1.ref;
+            }
+            o1.pnext = o2.sam_pos;
+            o2.pnext = o1.sam_pos;
+        } else if (al1 || al2) {
+            Rec &Al = al1 ? o1 : o2;
+            Rec &Un = al1 ? o2 : o1;
+            Un.sam_ref = Al.sam_ref;
+            Un.sam_pos = Al.sam_pos;
+            Al.rnext = Un.rnext = -1;
+            Al.pnext = Al.sam_pos;
+            Un.pnext = Al.sam_pos;
+            Un.ys = Al.score;
+        }
+        A.rec[r1] = o1;
+        A.rec[r2] = o2;
+        tally(A, T, o1, r1);
+        tally(A, T, o2, r2);
     }
     if (T) {
         __syncthreads();
@@ -2580,8 +2527,8 @@ int run_map(Ctx &c, const mh_params &par)
         const int64_t units = c.reads.paired ? n / 2 : n;
         PairArgs pa{c.reads, c.len_tab, M.slot, M.n_cand, M.yf, M.pool, M.rec, M.ref_stats,
                     M.n_refs, par.mode == MH_LOCAL, par.maxins, c.reads.paired};
-        int64_t pblocks = (units + PAIR_UNITS - 1) / PAIR_UNITS;
-        if (pblocks > 8192) pblocks = 8192;
+        int64_t pblocks = (units + 255) / 256;
+        if (pblocks > 1 << 16) pblocks = 1 << 16;
         if (pblocks < 1) pblocks = 1;
         for (int attempt = 0; attempt < 2; ++attempt) {
             // counters: [0] work items, [2] pool overflow, [3] fast path,
@@ -2607,7 +2554,7 @@ int run_map(Ctx &c, const mh_params &par)
             }
             pa.pool = M.pool;
             const int pp = prof_begin(c, "k_pair");
-            hipLaunchKernelGGL(k_pair, dim3((unsigned)pblocks), dim3(64), 0, s, pa);
+            hipLaunchKernelGGL(k_pair, dim3((unsigned)pblocks), dim3(256), 0, s, pa);
             prof_end(c, pp);
             MH_HIP(hipGetLastError());
             int32_t ctr[5];
