@@ -319,7 +319,7 @@ def read_pmc_traffic(kernel, pairs, stage='remap'):
     gfx950 rule; profiles/collect_pmc_stages.sh), when it was measured on the
     same per-GPU pair count."""
     if stage == 'remap':
-        path = os.path.join(REPO, 'profiles', 'r03', 'c2', 'pmc_traffic.json')
+        path = os.path.join(REPO, 'profiles', 'r04', 'c2', 'pmc_traffic.json')
     else:
         path = os.path.join(REPO, 'profiles', 'pmc_traffic_{}.json'.format(stage))
     try:
@@ -339,11 +339,11 @@ VALU_ISSUE_CYCLES = 2      # MI355X_MICROARCH.md: a wave64 VALU instruction issu
 def read_valu_issue(kernel, pairs, avg_launch_ms):
     """Issue-side roofline of `kernel` (it is bound by integer VALU issue and
     its dependency chain, not HBM): VALU wave-instructions per launch from the
-    committed SQ_INSTS_VALU pass (profiles/r03/c2/sq_issue.json, same
+    committed SQ_INSTS_VALU pass (profiles/r04/c2/sq_issue.json, same
     per-GPU pair count; the mate-rescue DP launch, the one after k_rescue, is
     left out), over this run's average launch time, against 1024 SIMDs x the
     measured clock / VALU_ISSUE_CYCLES."""
-    path = os.path.join(REPO, 'profiles', 'r03', 'c2', 'sq_issue.json')
+    path = os.path.join(REPO, 'profiles', 'r04', 'c2', 'sq_issue.json')
     try:
         with open(path) as f:
             every = json.load(f)['dispatches']
@@ -357,7 +357,7 @@ def read_valu_issue(kernel, pairs, avg_launch_ms):
         peak = 1024 * clk / VALU_ISSUE_CYCLES
         return {'unit': 'G wave-instr/s', 'valu_insts_per_launch': insts, 'achieved': round(achieved, 1),
                 'peak': round(peak, 1), 'frac': round(achieved / peak, 4), 'clock_ghz': round(clk, 3),
-                'source': 'profiles/r03/c2/sq_issue.json (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)'}
+                'source': 'profiles/r04/c2/sq_issue.json (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)'}
     except (OSError, KeyError, ValueError):
         return None
 

@@ -169,12 +169,16 @@ static int prepare_len_tab(Ctx &c, const mh_params &par)
 // every byte it keeps; a std::vector's value-initialisation of a GB buffer
 // is a serial memset the ingest does not need).
 struct Bytes {
-    std::unique_ptr<uint8_t[]> p;
+    std::unique_ptr<char[], BigDeleter> p{nullptr, BigDeleter{}};
     size_t n = 0;
-    void alloc(size_t k) { p.reset(new uint8_t[k > 0 ? k : 1]); n = k; }
+    void alloc(size_t k)
+    {
+        p = std::unique_ptr<char[], BigDeleter>(big_alloc(k > 0 ? k : 1), BigDeleter{k > 0 ? k : 1});
+        n = k;
+    }
     void assign(const uint8_t *a, const uint8_t *b) { alloc((size_t)(b - a)); if (b > a) std::memcpy(p.get(), a, n); }
-    uint8_t *data() { return p.get(); }
-    const uint8_t *data() const { return p.get(); }
+    uint8_t *data() { return (uint8_t *)p.get(); }
+    const uint8_t *data() const { return (const uint8_t *)p.get(); }
     size_t size() const { return n; }
 };
 

@@ -4,6 +4,7 @@
 // library without its header) decodes ~3x faster than zlib's inflate and is
 // used when present; zlib otherwise.  Host code only.
 #include <dlfcn.h>
+#include <sys/mman.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -263,6 +264,24 @@ int gunzip_members(const LdApi &api, const uint8_t *src, int64_t len, Buf &out, 
 }
 
 }  // namespace
+
+constexpr size_t BIG = (size_t)32 << 20;
+
+char *big_alloc(size_t n)
+{
+    if (n < BIG) return new char[n > 0 ? n : 1];
+    void *p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) throw std::bad_alloc();
+    madvise(p, n, MADV_HUGEPAGE);
+    return (char *)p;
+}
+
+void big_free(char *p, size_t n)
+{
+    if (!p) return;
+    if (n < BIG) delete[] p;
+    else munmap(p, n);
+}
 
 bool gunzip_fast_available() { return ld_api().ok; }
 

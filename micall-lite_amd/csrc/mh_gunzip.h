@@ -10,6 +10,18 @@
 
 namespace mh {
 
+// Large host buffers: anonymous mappings with transparent huge pages asked
+// for (the box's THP mode is "madvise"), so filling and freeing a GB-sized
+// text faults and frees 2 MiB pages instead of half a million 4 KiB ones.
+// Small ones come from the heap.  Contents are not initialised.
+char *big_alloc(size_t n);
+void big_free(char *p, size_t n);
+
+struct BigDeleter {
+    size_t n = 0;
+    void operator()(char *p) const { big_free(p, n); }
+};
+
 // A growable byte buffer whose new bytes are not zero-filled (a GB-sized
 // std::string::resize is a serial memset before the threads that fill it
 // can start; here the pages are first touched by the threads that write
@@ -25,7 +37,7 @@ class TextBuf {
     void reserve(size_t k)
     {
         if (k <= cap_) return;
-        std::unique_ptr<char[]> q(new char[k]);
+        std::unique_ptr<char[], BigDeleter> q(big_alloc(k), BigDeleter{k});
         if (n_) memcpy(q.get(), p_.get(), n_);
         p_.swap(q);
         cap_ = k;
@@ -47,7 +59,7 @@ class TextBuf {
     void swap(TextBuf &o) { p_.swap(o.p_); std::swap(n_, o.n_); std::swap(cap_, o.cap_); }
 
   private:
-    std::unique_ptr<char[]> p_;
+    std::unique_ptr<char[], BigDeleter> p_{nullptr, BigDeleter{}};
     size_t n_ = 0, cap_ = 0;
 };
 

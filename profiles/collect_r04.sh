@@ -13,7 +13,7 @@ O=$R/gpurun_out/r04
 mkdir -p $O/c2 $O/c3 $O/c4 $O/c4all $O/c5
 cd $R
 if [ "$WHAT" = c2 ] || [ "$WHAT" = all ]; then
-  timeout -k 10 500 python3 bench.py --breakdown > $O/c2/bench.json 2> $O/c2/bench.err
+  timeout -k 10 500 python3 bench.py --steps 20 --warmup 3 > $O/c2/bench.json 2> $O/c2/bench.err
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/c2/prof -o run \
       -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $O/c2/bench_under_rocprof.json 2> $O/c2/prof.err
