@@ -656,7 +656,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     for (auto &ix : c->cache) free_index(ix);   // c->index only views one of these
     free_index(c->small);
     MapState &M = c->map;
-    hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work); hipFree(M.rwork); hipFree(M.slot);
+    hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work); hipFree(M.rwork); hipFree(M.skey); hipFree(M.sinfo);
     hipFree(M.pool); hipFree(M.pool_used); hipFree(M.rec); hipFree(M.counters); hipFree(M.ref_stats);
     RowState &R = c->rows;
     hipFree(R.flag); hipFree(R.ref); hipFree(R.pos); hipFree(R.cig_off); hipFree(R.n_cigar);

@@ -265,14 +265,16 @@ int gunzip_members(const LdApi &api, const uint8_t *src, int64_t len, Buf &out, 
 
 }  // namespace
 
-constexpr size_t BIG = (size_t)32 << 20;
+constexpr size_t BIG = (size_t)4 << 20;
 
 char *big_alloc(size_t n)
 {
     if (n < BIG) return new char[n > 0 ? n : 1];
     void *p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (p == MAP_FAILED) throw std::bad_alloc();
-    madvise(p, n, MADV_HUGEPAGE);
+    // MICALL_NO_THP=1: 4 KiB pages (for A/B timing)
+    static const bool thp = !(getenv("MICALL_NO_THP") && *getenv("MICALL_NO_THP") == '1');
+    if (thp) madvise(p, n, MADV_HUGEPAGE);
     return (char *)p;
 }
 

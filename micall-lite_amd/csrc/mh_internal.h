@@ -93,10 +93,23 @@ struct Cand {
     int32_t strand, ref, center, support;
 };
 
-// Result of one banded extension (one candidate of one read).
+// Result of one banded extension (one candidate of one read), as k_dp
+// builds it in registers.
 struct Slot {
     int32_t valid, strand, ref, pos, end, score, xm, xo, xg, nm, n_cigar, cig_off;
     int32_t maxm;   // longest M run of the CIGAR (remap.py:500-506 filter), from the traceback
+};
+
+// In HBM a slot is split in two arrays: the 16-B key that pairing, mate
+// rescue and the best-candidate choice compare (a read's MAXCAND keys are
+// one 64-B line), and the 32-B statistics only the chosen candidate's
+// record copies.
+struct alignas(16) SlotKey {
+    int32_t rs;      // ref << 1 | strand; -1 when the extension found no alignment
+    int32_t pos, end, score;
+};
+struct alignas(16) SlotInfo {
+    int32_t xm, xo, xg, nm, n_cigar, cig_off, maxm, pad;
 };
 
 // Final per-read SAM record (mh_aln without the inline CIGAR).
@@ -115,7 +128,8 @@ struct MapState {
     int32_t *yf = nullptr;       // n_reads
     int32_t *work = nullptr;     // slot ids to extend
     int32_t *rwork = nullptr;    // slot ids of mate-rescue candidates (one per pair at most)
-    Slot *slot = nullptr;        // n_reads * MAXCAND
+    SlotKey *skey = nullptr;     // n_reads * MAXCAND
+    SlotInfo *sinfo = nullptr;   // n_reads * MAXCAND
     uint32_t *pool = nullptr;    // CIGAR ops of all slots
     int64_t pool_cap = 0;
     unsigned long long *pool_used = nullptr;  // words claimed (demand; may exceed pool_cap)

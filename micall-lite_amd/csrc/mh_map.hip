@@ -654,7 +654,8 @@ struct DpArgs {
     const Cand *cand;
     const int32_t *work;
     const int32_t *counters;  // [0] = number of work items
-    Slot *slot;
+    SlotKey *skey;
+    SlotInfo *sinfo;
     uint32_t *pool;
     unsigned long long *pool_used;  // words claimed so far (64-bit: never wraps)
     int32_t *pool_ctr;        // [1] overflow, [2] fast-path extensions
@@ -1655,7 +1656,10 @@ __device__ void post_ext(const DpArgs &A, const XItem &it, const XView &X, int b
             }
         }
     }
-    if (lane == 0) A.slot[it.sid] = out;
+    if (lane == 0) {
+        A.skey[it.sid] = SlotKey{out.valid ? (out.ref << 1 | out.strand) : -1, out.pos, out.end, out.score};
+        A.sinfo[it.sid] = SlotInfo{out.xm, out.xo, out.xg, out.nm, out.n_cigar, out.cig_off, out.maxm, 0};
+    }
     wave_sync();
 }
 
@@ -1828,7 +1832,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
 struct RescueArgs {
     DevReads R;
     DevIndex I;
-    const Slot *slot;
+    const SlotKey *skey;
     int32_t *n_cand;
     const int32_t *yf;
     Cand *cand;
@@ -1852,12 +1856,12 @@ __device__ __forceinline__ uint32_t compact16(uint32_t x)
     return (x | (x >> 8)) & 0x0000ffffu;
 }
 
-__device__ __forceinline__ int best_slot(const Slot *sl, int n)
+__device__ __forceinline__ int best_slot(const SlotKey *sl, int n)
 {
     int best = -1, bs = 0;
     for (int c = 0; c < n; ++c) {
-        const int v = sl[c].valid, sc = sl[c].score;
-        if (v && (best < 0 || sc > bs)) { best = c; bs = sc; }
+        const SlotKey k = sl[c];
+        if (k.rs >= 0 && (best < 0 || k.score > bs)) { best = c; bs = k.score; }
     }
     return best;
 }
@@ -1888,19 +1892,19 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
         int64_t t_off = 0, r_off = 0;   // the mate's and the reference's (loaded lane-parallel here)
         if (u < units) {
             const int64_t r1 = 2 * u, r2 = r1 + 1;
-            const int b1 = best_slot(A.slot + r1 * MAXCAND, A.n_cand[r1]);
-            const int b2 = best_slot(A.slot + r2 * MAXCAND, A.n_cand[r2]);
+            const int b1 = best_slot(A.skey + r1 * MAXCAND, A.n_cand[r1]);
+            const int b2 = best_slot(A.skey + r2 * MAXCAND, A.n_cand[r2]);
             if ((b1 >= 0) != (b2 >= 0)) {
                 const int64_t an = b1 >= 0 ? r1 : r2, tg = b1 >= 0 ? r2 : r1;
                 if (A.yf[tg] == 0 && A.R.len[tg] > 0) {
-                    const Slot s = A.slot[an * MAXCAND + (b1 >= 0 ? b1 : b2)];
+                    const SlotKey s = A.skey[an * MAXCAND + (b1 >= 0 ? b1 : b2)];
                     need = 1;
                     tgt_mate = b1 >= 0 ? 1 : 0;
-                    a_ref = s.ref; a_strand = s.strand; a_pos = s.pos; a_end = s.end;
+                    a_ref = s.rs >> 1; a_strand = s.rs & 1; a_pos = s.pos; a_end = s.end;
                     t_len = A.R.len[tg];
                     t_off = A.R.off[tg];
-                    r_len = A.I.ref_len[s.ref];
-                    r_off = A.I.ref_off[s.ref];
+                    r_len = A.I.ref_len[a_ref];
+                    r_off = A.I.ref_off[a_ref];
                 }
             }
         }
@@ -2097,7 +2101,8 @@ __device__ int mapq_v2(int local, int perfect, int minsc, int best, int has_sec,
 struct PairArgs {
     DevReads R;
     const int32_t *len_tab;
-    const Slot *slot;
+    const SlotKey *skey;
+    const SlotInfo *sinfo;
     const int32_t *n_cand;
     const int32_t *yf;
     const uint32_t *pool;
@@ -2109,30 +2114,31 @@ struct PairArgs {
     int paired;
 };
 
+// A read's candidates: its keys in registers (one 16-B load each, the
+// read's MAXCAND keys are one 64-B line), invalid ones and those past
+// n_cand as rs = -1.
 struct MateView {
-    const Slot *s;   // this read's MAXCAND slots in global memory (L2-hot after k_dp)
-    int n;
+    SlotKey k[MAXCAND];
+    int64_t base;    // slot id of candidate 0
     int best;
+    SlotKey bk;      // k[best] (copied when chosen: a run-time index into k would
+                     // put the view in scratch memory)
 };
 
 __device__ __forceinline__ void load_mate(const PairArgs &A, int64_t r, MateView &mv)
 {
-    mv.s = A.slot + r * MAXCAND;
-    mv.n = A.n_cand[r];
+    mv.base = r * MAXCAND;
+    const int n = A.n_cand[r];
     mv.best = -1;
-    int bs = 0;
-    for (int c = 0; c < mv.n; ++c) {
-        const int v = mv.s[c].valid, sc = mv.s[c].score;
-        if (v && (mv.best < 0 || sc > bs)) { mv.best = c; bs = sc; }
+    mv.bk = SlotKey{-1, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < MAXCAND; ++c) {
+        mv.k[c] = c < n ? A.skey[mv.base + c] : SlotKey{-1, 0, 0, 0};
+        if (mv.k[c].rs >= 0 && (mv.best < 0 || mv.k[c].score > mv.bk.score)) { mv.best = c; mv.bk = mv.k[c]; }
     }
 }
 
-__device__ __forceinline__ bool same_place(const Slot &x, const Slot &y)
-{
-    return x.strand == y.strand && x.ref == y.ref && x.pos == y.pos;
-}
-
-__device__ void clear_rec(Rec &o)
+__device__ __forceinline__ void clear_rec(Rec &o)
 {
     o.ref = -1; o.pos = 0; o.rev = 0; o.score = 0; o.secbest = I32MIN; o.flag = 0; o.mapq = 0;
     o.rnext = -2; o.pnext = 0; o.tlen = 0; o.sam_ref = -1; o.sam_pos = 0; o.xm = 0; o.xo = 0;
@@ -2140,32 +2146,35 @@ __device__ void clear_rec(Rec &o)
     o.maxm = 0;
 }
 
-__device__ void fill_aligned(const PairArgs &A, Rec &o, const MateView &mv, int chosen, int m)
+__device__ __forceinline__ void fill_aligned(const PairArgs &A, Rec &o, const MateView &mv, int chosen,
+                                             const SlotKey &a, int m)
 {
-    const Slot a = mv.s[chosen];
-    o.ref = a.ref; o.pos = a.pos; o.rev = a.strand; o.score = a.score;
+    o.ref = a.rs >> 1; o.pos = a.pos; o.rev = a.rs & 1; o.score = a.score;
     int sec = 0, has = 0;
-    for (int c = 0; c < mv.n; ++c) {
-        if (c == chosen) continue;
-        const Slot b = mv.s[c];
-        if (!b.valid || same_place(b, a)) continue;
+#pragma unroll
+    for (int c = 0; c < MAXCAND; ++c) {
+        const SlotKey b = mv.k[c];
+        // same place: strand, reference and position
+        if (c == chosen || b.rs < 0 || (b.rs == a.rs && b.pos == a.pos)) continue;
         if (!has || b.score > sec) { sec = b.score; has = 1; }
     }
     o.secbest = has ? sec : I32MIN;
     o.mapq = mapq_v2(A.local, A.local ? 2 * m : 0, A.len_tab[(MAXLEN + 1) + m], a.score, has, sec);
-    o.xm = a.xm; o.xo = a.xo; o.xg = a.xg; o.nm = a.nm;
-    o.n_cigar = a.n_cigar;
-    o.cig_off = a.cig_off;
-    o.maxm = a.maxm;
-    o.sam_ref = a.ref;
+    const SlotInfo f = A.sinfo[mv.base + chosen];
+    o.xm = f.xm; o.xo = f.xo; o.xg = f.xg; o.nm = f.nm;
+    o.n_cigar = f.n_cigar;
+    o.cig_off = f.cig_off;
+    o.maxm = f.maxm;
+    o.sam_ref = o.ref;
     o.sam_pos = a.pos + 1;
 }
 
-__device__ __forceinline__ bool concordant(const Slot &x, const Slot &y, int maxins)
+__device__ __forceinline__ bool concordant(const SlotKey &x, const SlotKey &y, int maxins)
 {
-    if (x.ref != y.ref || x.strand == y.strand) return false;
-    const Slot &fw = x.strand == 0 ? x : y;
-    const Slot &rv = x.strand == 0 ? y : x;
+    // same reference, opposite strands
+    if ((x.rs ^ y.rs) != 1) return false;
+    const SlotKey &fw = (x.rs & 1) == 0 ? x : y;
+    const SlotKey &rv = (x.rs & 1) == 0 ? y : x;
     const int lo = fw.pos < rv.pos ? fw.pos : rv.pos;
     const int hi = fw.end > rv.end ? fw.end : rv.end;
     if (hi - lo > maxins) return false;
@@ -2185,7 +2194,7 @@ struct TallyLds {
     int star_first;
 };
 
-__device__ void tally(const PairArgs &A, TallyLds *T, const Rec &o, int64_t row)
+__device__ __forceinline__ void tally(const PairArgs &A, TallyLds *T, const Rec &o, int64_t row)
 {
     const int n = A.n_refs;
     if (T) {
@@ -2264,7 +2273,7 @@ __global__ __launch_bounds__(256) void k_pair(PairArgs A)
             o.yf = A.yf[u];
             o.yt = 3;
             if (mv.best >= 0) {
-                fill_aligned(A, o, mv, mv.best, A.R.len[u]);
+                fill_aligned(A, o, mv, mv.best, mv.bk, A.R.len[u]);
                 o.flag = o.rev ? 0x10 : 0;
             } else {
                 o.flag = 0x4;
@@ -2283,21 +2292,24 @@ __global__ __launch_bounds__(256) void k_pair(PairArgs A)
         o1.yf = A.yf[r1];
         o2.yf = A.yf[r2];
         int c1 = m1.best, c2 = m2.best, conc = 0;
+        SlotKey k1 = m1.bk, k2 = m2.bk;
         long long best_sum = -9223372036854775807ll - 1;
-        for (int x = 0; x < m1.n; ++x) {
-            const Slot sx = m1.s[x];
-            if (!sx.valid) continue;
-            for (int y = 0; y < m2.n; ++y) {
-                const Slot sy = m2.s[y];
-                if (!sy.valid) continue;
+#pragma unroll
+        for (int x = 0; x < MAXCAND; ++x) {
+            const SlotKey sx = m1.k[x];
+            if (sx.rs < 0) continue;
+#pragma unroll
+            for (int y = 0; y < MAXCAND; ++y) {
+                const SlotKey sy = m2.k[y];
+                if (sy.rs < 0) continue;
                 if (!concordant(sx, sy, A.maxins)) continue;
                 const long long s = (long long)sx.score + sy.score;
-                if (s > best_sum) { best_sum = s; c1 = x; c2 = y; conc = 1; }
+                if (s > best_sum) { best_sum = s; c1 = x; c2 = y; k1 = sx; k2 = sy; conc = 1; }
             }
         }
         const int al1 = c1 >= 0, al2 = c2 >= 0;
-        if (al1) fill_aligned(A, o1, m1, c1, A.R.len[r1]);
-        if (al2) fill_aligned(A, o2, m2, c2, A.R.len[r2]);
+        if (al1) fill_aligned(A, o1, m1, c1, k1, A.R.len[r1]);
+        if (al2) fill_aligned(A, o2, m2, c2, k2, A.R.len[r2]);
         int f1 = 0x1 | 0x40, f2 = 0x1 | 0x80;
         if (conc) { f1 |= 0x2; f2 |= 0x2; }
         if (!al1) { f1 |= 0x4; f2 |= 0x8; }
@@ -2313,7 +2325,7 @@ __global__ __launch_bounds__(256) void k_pair(PairArgs A)
             o2.ys = o1.score;
             if (o1.ref == o2.ref) {
                 o1.rnext = o2.rnext = -1;
-                const Slot a = m1.s[c1], b = m2.s[c2];
+                const SlotKey &a = k1, &b = k2;
                 const int lo = a.pos < b.pos ? a.pos : b.pos;
                 const int hi = a.end > b.end ? a.end : b.end;
                 const int t = hi - lo;
@@ -2327,14 +2339,17 @@ __global__ __launch_bounds__(256) void k_pair(PairArgs A)
             o1.pnext = o2.sam_pos;
             o2.pnext = o1.sam_pos;
         } else if (al1 || al2) {
-            Rec &Al = al1 ? o1 : o2;
-            Rec &Un = al1 ? o2 : o1;
-            Un.sam_ref = Al.sam_ref;
-            Un.sam_pos = Al.sam_pos;
-            Al.rnext = Un.rnext = -1;
-            Al.pnext = Al.sam_pos;
-            Un.pnext = Al.sam_pos;
-            Un.ys = Al.score;
+            // the aligned mate's place for both (no run-time reference to
+            // one of the two records: that puts both in scratch memory)
+            const int sref = al1 ? o1.sam_ref : o2.sam_ref;
+            const int spos = al1 ? o1.sam_pos : o2.sam_pos;
+            const int ascore = al1 ? o1.score : o2.score;
+            o1.sam_ref = o2.sam_ref = sref;
+            o1.sam_pos = o2.sam_pos = spos;
+            o1.rnext = o2.rnext = -1;
+            o1.pnext = o2.pnext = spos;
+            if (al1) o2.ys = ascore;
+            else o1.ys = ascore;
         }
         A.rec[r1] = o1;
         A.rec[r2] = o2;
@@ -2362,14 +2377,15 @@ static int ensure_map_buffers(Ctx &c)
     const int64_t n = c.reads.n;
     if (M.cap_reads < n || M.cand == nullptr) {
         hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work);
-        hipFree(M.rwork); hipFree(M.slot); hipFree(M.rec);
+        hipFree(M.rwork); hipFree(M.skey); hipFree(M.sinfo); hipFree(M.rec);
         const int64_t cap = n > 0 ? n : 1;
         MH_HIP(hipMalloc(&M.cand, sizeof(Cand) * cap * MAXCAND));
         MH_HIP(hipMalloc(&M.n_cand, sizeof(int32_t) * cap));
         MH_HIP(hipMalloc(&M.yf, sizeof(int32_t) * cap));
         MH_HIP(hipMalloc(&M.work, sizeof(int32_t) * cap * MAXCAND));
         MH_HIP(hipMalloc(&M.rwork, sizeof(int32_t) * (cap / 2 + 1)));
-        MH_HIP(hipMalloc(&M.slot, sizeof(Slot) * cap * MAXCAND));
+        MH_HIP(hipMalloc(&M.skey, sizeof(SlotKey) * cap * MAXCAND));
+        MH_HIP(hipMalloc(&M.sinfo, sizeof(SlotInfo) * cap * MAXCAND));
         MH_HIP(hipMalloc(&M.rec, sizeof(Rec) * cap));
         M.cap_reads = cap;
     }
@@ -2483,7 +2499,7 @@ int run_map(Ctx &c, const mh_params &par)
         if (wave_lds > 160 * 1024) { set_error("mh_map: reads too long for LDS"); return -3; }
         auto launch_dp = [&](const int32_t *work, const int32_t *count, int32_t *queue,
                              int64_t max_items, const char *name) -> int {
-            DpArgs da{c.reads, c.index, c.len_tab, M.cand, work, count, M.slot, M.pool,
+            DpArgs da{c.reads, c.index, c.len_tab, M.cand, work, count, M.skey, M.sinfo, M.pool,
                       M.pool_used, M.counters + 1, queue, M.pool_cap, rows_pad, wave_lds,
                       par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext,
                       par.rdg_ext};
@@ -2525,7 +2541,7 @@ int run_map(Ctx &c, const mh_params &par)
             return 0;
         };
         const int64_t units = c.reads.paired ? n / 2 : n;
-        PairArgs pa{c.reads, c.len_tab, M.slot, M.n_cand, M.yf, M.pool, M.rec, M.ref_stats,
+        PairArgs pa{c.reads, c.len_tab, M.skey, M.sinfo, M.n_cand, M.yf, M.pool, M.rec, M.ref_stats,
                     M.n_refs, par.mode == MH_LOCAL, par.maxins, c.reads.paired};
         int64_t pblocks = (units + 255) / 256;
         if (pblocks > 1 << 16) pblocks = 1 << 16;
@@ -2542,7 +2558,7 @@ int run_map(Ctx &c, const mh_params &par)
             if (int st = launch_seed()) return st;
             if (int st = launch_dp(M.work, M.counters, M.counters + 5, n * 2, "k_dp")) return st;
             if (c.reads.paired && units > 0) {
-                RescueArgs ra{c.reads, c.index, M.slot, M.n_cand, M.yf, M.cand, M.rwork,
+                RescueArgs ra{c.reads, c.index, M.skey, M.n_cand, M.yf, M.cand, M.rwork,
                               M.counters + 4, par.maxins};
                 int64_t rblocks = (units + 255) / 256;
                 if (rblocks > 4096) rblocks = 4096;
