@@ -2463,13 +2463,24 @@ int mh_levenshtein_batch(int count, const char *const *a, const char *const *b, 
     if (count < 0 || (count > 0 && (!a || !b || !out))) return -3;
     for (int t = 0; t < count; ++t)
         if (!a[t] || !b[t]) return -3;
-    // one pair per thread: the pairs of a consensus-distance filter are few and long
+    // one pair per thread: the pairs of a consensus-distance filter are few and
+    // long, so they are taken longest first (cost |a| * |b|) to balance the threads
     const int threads = count < 16 ? count : 16;
+    std::vector<int> order((size_t)count);
+    std::vector<double> cost((size_t)count);
+    for (int t = 0; t < count; ++t) {
+        order[(size_t)t] = t;
+        cost[(size_t)t] = (double)std::strlen(a[t]) * (double)std::strlen(b[t]);
+    }
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cost[(size_t)x] > cost[(size_t)y]; });
     std::vector<std::thread> pool;
     std::atomic<int> next(0);
     for (int w = 0; w < threads; ++w)
         pool.emplace_back([&]() {
-            for (int t = next++; t < count; t = next++) out[t] = mh_levenshtein(a[t], b[t]);
+            for (int i = next++; i < count; i = next++) {
+                const int t = order[(size_t)i];
+                out[t] = mh_levenshtein(a[t], b[t]);
+            }
         });
     for (auto &th : pool) th.join();
     return 0;
@@ -2490,32 +2501,45 @@ int mh_levenshtein(const char *a, const char *b)
     const size_t nb = (m + 63) / 64;
     const size_t pad = nb * 64 - m;
     const uint64_t padmask = pad ? ~0ull << (64 - pad) : 0;   // padded rows of the last block
-    std::vector<uint64_t> peq(nb * 256, 0);
-    for (size_t c = 0; c < 256; ++c) peq[(nb - 1) * 256 + c] = padmask;
-    for (size_t i = 0; i < m; ++i) peq[(i / 64) * 256 + (unsigned char)a[i]] |= 1ull << (i % 64);
+    // a's alphabet compacted: symbol s's match vectors are peq[s * nb ..], one
+    // contiguous row per symbol; characters a does not hold map to the last
+    // symbol, which matches only the padded rows
+    uint8_t sym[256];
+    int ns = 0;
+    std::memset(sym, 0xff, sizeof(sym));
+    for (size_t i = 0; i < m; ++i) {
+        const unsigned char ch = (unsigned char)a[i];
+        if (sym[ch] == 0xff) sym[ch] = (uint8_t)ns++;
+    }
+    const int none = ns++;
+    for (int ch = 0; ch < 256; ++ch) if (sym[ch] == 0xff) sym[ch] = (uint8_t)none;
+    std::vector<uint64_t> peq((size_t)ns * nb, 0);
+    for (int s = 0; s < ns; ++s) peq[(size_t)s * nb + nb - 1] = padmask;
+    for (size_t i = 0; i < m; ++i) peq[(size_t)sym[(unsigned char)a[i]] * nb + i / 64] |= 1ull << (i % 64);
     std::vector<uint64_t> P(nb, ~0ull), M(nb, 0);   // vertical deltas +1 / -1 (D[i][0] = i)
+    uint64_t *Pp = P.data(), *Mp = M.data();
     long long score = (long long)(nb * 64);         // D[bottom row][0]
     for (size_t j = 0; j < n; ++j) {
-        const uint64_t *eqc = &peq[(unsigned char)b[j]];
-        int hin = 1;                                 // D[0][j+1] - D[0][j] = +1 (global)
+        const uint64_t *eqc = &peq[(size_t)sym[(unsigned char)b[j]] * nb];
+        // horizontal delta into the block's top row as two bits (+1: hp, -1: hn);
+        // D[0][j+1] - D[0][j] = +1 (global)
+        uint64_t hp = 1, hn = 0;
         for (size_t k = 0; k < nb; ++k) {
-            uint64_t Eq = eqc[k * 256];
-            const uint64_t Pv = P[k], Mv = M[k];
-            const uint64_t Xv = Eq | Mv;
-            if (hin < 0) Eq |= 1ull;
+            const uint64_t Pv = Pp[k], Mv = Mp[k];
+            const uint64_t Xv = eqc[k] | Mv;
+            const uint64_t Eq = eqc[k] | hn;
             const uint64_t Xh = (((Eq & Pv) + Pv) ^ Pv) | Eq;
             uint64_t Ph = Mv | ~(Xh | Pv);
             uint64_t Mh = Pv & Xh;
-            const int hout = (Ph >> 63) ? 1 : ((Mh >> 63) ? -1 : 0);
-            Ph <<= 1;
-            Mh <<= 1;
-            if (hin < 0) Mh |= 1ull;
-            else if (hin > 0) Ph |= 1ull;
-            P[k] = Mh | ~(Xv | Ph);
-            M[k] = Ph & Xv;
-            hin = hout;
+            const uint64_t op = Ph >> 63, on = Mh >> 63;
+            Ph = (Ph << 1) | hp;
+            Mh = (Mh << 1) | hn;
+            Pp[k] = Mh | ~(Xv | Ph);
+            Mp[k] = Ph & Xv;
+            hp = op;
+            hn = on;
         }
-        score += hin;
+        score += (long long)hp - (long long)hn;
     }
     // D[m][n] = D[bottom][n] - (deltas of the padded rows in the last column)
     score -= (long long)__builtin_popcountll(P[nb - 1] & padmask) -

@@ -76,3 +76,22 @@ def test_levenshtein_bit_parallel_matches_dp(native):
                 b = ''.join(rng.choice(alphabet) for _ in range(lb))
             assert native.levenshtein(a, b) == oracle.levenshtein(a, b), (la, len(b))
             assert native.levenshtein(b, a) == oracle.levenshtein(a, b), (la, len(b))
+
+
+def test_levenshtein_batch_keeps_pair_order():
+    """mh_levenshtein_batch runs its pairs longest first over host threads;
+    each result still lands at its pair's index, and characters of b that a
+    does not hold (mapped to one no-match symbol) count as mismatches."""
+    import random
+
+    from micall_amd import _native
+    rng = random.Random(11)
+    pairs = []
+    for _ in range(40):
+        la, lb = rng.randint(0, 400), rng.randint(0, 400)
+        pairs.append((''.join(rng.choice('ACGT') for _ in range(la)),
+                      ''.join(rng.choice('ACGTNxyz-') for _ in range(lb))))
+    got = _native.levenshtein_many(pairs)
+    assert got == [_native.levenshtein(a, b) for a, b in pairs]
+    import oracle
+    assert got[:8] == [oracle.levenshtein(a, b) for a, b in pairs[:8]]
