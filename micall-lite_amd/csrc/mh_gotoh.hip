@@ -73,10 +73,12 @@ struct GotohArgs {
     int *result;                  // [0] status, [1] score, [2] length
 };
 
-// the strips of a batch, in ticket order (alignment-major)
+// the strips of a batch, in ticket order (alignment-major, the alignments
+// longest critical path first)
 struct GotohStrips {
     const GotohArgs *args;
-    const int *first;             // per alignment: its first ticket; [count] = total
+    const int *first;             // per rank: the first ticket of that alignment; [count] = total
+    const int *order;             // per rank: the alignment (index into args)
     int count;
     int *ticket;                  // [0] fwd, [1] bwd
     // diagnostics (MH_GOTOH_STAMPS=path, else null): per ticket and block,
@@ -191,7 +193,7 @@ __device__ __forceinline__ void strip_of(const GotohStrips &S, int u, int &t, in
         const int mid = (lo + hi) >> 1;
         if (S.first[mid] <= u) lo = mid; else hi = mid;
     }
-    t = lo;
+    t = S.order[lo];
     q = u - S.first[lo];
 }
 
@@ -747,11 +749,21 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
         }
         work[t + 1] = work[t] + gotoh_work_bytes(ms[t], ns[t]);
     }
-    // strips in ticket order: every alignment's, alignment by alignment
+    // strips in ticket order: every alignment's, alignment by alignment, the
+    // longest critical path first (an alignment takes about (n + m) / 32
+    // blocks of steps: n columns, plus two blocks of lag per strip of 64
+    // rows), so the few long ones start at once and the many short ones fill
+    // the GPU around them instead of leaving the long ones to run alone at
+    // the end
+    std::vector<int> order(count);
+    for (int t = 0; t < count; ++t) order[t] = t;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int x, int y) { return ms[x] + ns[x] > ms[y] + ns[y]; });
     std::vector<int> first(count + 1, 0);
-    for (int t = 0; t < count; ++t) first[t + 1] = first[t] + (ms[t] + 1 + 63) / 64;
+    for (int r = 0; r < count; ++r) first[r + 1] = first[r] + (ms[order[r]] + 1 + 63) / 64;
     const size_t sz_mat = align16(sizeof(int) * L * L), sz_args = align16(sizeof(GotohArgs) * count);
-    const size_t sz_first = align16(sizeof(int) * (count + 1)) + 16;   // + the two ticket counters
+    const size_t sz_order = align16(sizeof(int) * count);
+    const size_t sz_first = align16(sizeof(int) * (count + 1)) + sz_order + 16;   // + order, the two ticket counters
     // device buffer: [io blocks][matrix][arguments][strip table, tickets][work blocks]
     const size_t off_mat = io[count], off_args = off_mat + sz_mat, off_first = off_args + sz_args,
                  off_work = off_first + sz_first;
@@ -816,9 +828,12 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     MH_HIP(hipMemcpyAsync(d + off_args, args.data(), sizeof(GotohArgs) * count,
                           hipMemcpyHostToDevice, st));
     MH_HIP(hipMemcpyAsync(d + off_first, first.data(), sizeof(int) * (count + 1), hipMemcpyHostToDevice, st));
+    const size_t off_order = off_first + align16(sizeof(int) * (count + 1));
+    MH_HIP(hipMemcpyAsync(d + off_order, order.data(), sizeof(int) * count, hipMemcpyHostToDevice, st));
     GotohStrips S;
     S.args = (const GotohArgs *)(d + off_args);
     S.first = (const int *)(d + off_first);
+    S.order = (const int *)(d + off_order);
     S.count = count;
     S.ticket = (int *)(d + off_first + sz_first - 16);
     const int strips = first[count];
