@@ -225,13 +225,11 @@ def write_fastq_gz(pairs, path1, path2, threads=16, single=False):
     def member(chunk):
         c = zlib.compressobj(1, zlib.DEFLATED, 31)
         return c.compress(chunk) + c.flush()
-    if single:
-        threads = 1
     for mate, path in ((1, path1), (2, path2)):
         r, q = pairs['r%d' % mate], pairs['q%d' % mate]
         recs = [b'%s\n%s\n+\n%s\n' % (synth.read_name(pairs['block'], i, mate).encode(),
                                       r[i].tobytes(), q[i].tobytes()) for i in range(pairs['n'])]
-        step = -(-len(recs) // (threads * 4))
+        step = len(recs) if single else -(-len(recs) // (threads * 4))
         chunks = [b''.join(recs[k:k + step]) for k in range(0, len(recs), step)]
         del recs
         with ThreadPoolExecutor(threads) as ex, open(path, 'wb') as f:
@@ -515,16 +513,35 @@ def bench_censor(args):
     rng = random.Random(SEED)
     bad = sorted({(str(1101 + t), c) for t in range(8) for c in range(1, READ_LEN + 1)
                   if rng.random() < 0.02})
-    ctx = _native.Context(0)
+    from micall_amd import censor_fastq, session
+    tmp = tempfile.mkdtemp(prefix='bench_fq_')
+    p1, p2 = os.path.join(tmp, 'R1.fastq.gz'), os.path.join(tmp, 'R2.fastq.gz')
+    with open(p1, 'wb') as f:
+        f.write(gz1)
+    with open(p2, 'wb') as f:
+        f.write(gz2)
+    pout = os.path.join(tmp, 'R1.censor.fastq.gz')
+    rows = [{'tile': t, 'cycle': str(c)} for t, c in bad]
+
+    def censor_file():
+        # the drop-in as bin/micall calls it: file handles in and out
+        with open(p1, 'rb') as src, open(pout, 'wb') as dst:
+            censor_fastq.censor(src, iter(rows), dst, use_gzip=True)
+
+    ctx = session.context()
     for _ in range(args.warmup):
-        ctx.censor_fastq(gz1, bad, True, True)
+        censor_file()
     ctx.profile(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out, n_bases, total = ctx.censor_fastq(gz1, bad, True, True)
+        censor_file()
     elapsed = time.perf_counter() - t0
     host_ms = ctx.censor_timing()
     k_ms, k_n = ctx.profile_get('k_censor')
+    # the in-memory entry (bytes in, bytes out: mh_censor_fastq) for comparison
+    t3 = time.perf_counter()
+    out, n_bases, total = ctx.censor_fastq(gz1, bad, True, True)
+    mem_s = time.perf_counter() - t3
     # k_censor runs once per inflated piece (~32 MB of FASTQ): account per
     # file.  Algorithmic bytes: read and write every base and quality byte
     # once (the kernel censors in place), 16 B of spans per record.
@@ -538,15 +555,11 @@ def bench_censor(args):
     except (OSError, KeyError, ValueError):
         pmc_launches = 1
     # FASTQ ingest of the pair (what prelim_map does first)
-    tmp = tempfile.mkdtemp(prefix='bench_fq_')
-    p1, p2 = os.path.join(tmp, 'R1.fastq.gz'), os.path.join(tmp, 'R2.fastq.gz')
-    with open(p1, 'wb') as f:
-        f.write(gz1)
-    with open(p2, 'wb') as f:
-        f.write(gz2)
     t1 = time.perf_counter()
     ctx.reads_load_fastq(p1, p2)
     ingest_s = time.perf_counter() - t1
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
     sample = min(20000, args.pairs)
     stext = b'\n'.join(raw1.split(b'\n', 4 * sample)[:4 * sample]) + b'\n'
     t2 = time.perf_counter()
@@ -565,6 +578,9 @@ def bench_censor(args):
         'host_ms_last_step': {'gunzip_split': round(host_ms[0], 1),
                               'device_call': round(host_ms[1], 1),
                               'rewrite_gzip': round(host_ms[2], 1)},
+        'what': 'censor_fastq.censor() drop-in, file to file (single-member gzip R1 in, gzip out '
+                'written with pwrite); in_memory_s: mh_censor_fastq on the same bytes in memory',
+        'in_memory_s': round(mem_s, 3),
         'ingest_pair_s': round(ingest_s, 3),
         'ingest_reads_per_s': round(2 * args.pairs / ingest_s, 1),
         'roofline': {'kernel': 'k_censor', 'bound': 'hbm', 'achieved': round(achieved, 3),

@@ -32,7 +32,8 @@
  *          -> mh_sam2aln_csv, mh_sam2aln_output;
  *   5. (the stage before) censor_fastq.censor's per-base
  *      Python loop, micall/core/censor_fastq.py:32-102
- *          -> mh_censor_fastq, mh_censor_output;
+ *          -> mh_censor_fastq / mh_censor_staged, mh_censor_output /
+ *             mh_censor_write;
  *   6. (the stage after sam2aln) aln2counts' per-read loops,
  *      SequenceReport._count_reads (micall/core/aln2counts.py:115-172) and
  *      InsertionWriter.write (:748-811)
@@ -357,7 +358,18 @@ int mh_sam2aln_timing(mh_ctx *ctx, double *ms5);
 int mh_censor_fastq(mh_ctx *ctx, const uint8_t *src, int64_t len, int src_gzip, int n_bad,
                     const char *const *tiles, const int32_t *cycles, int dst_gzip,
                     int64_t *base_count, int64_t *score_sum);
+/* The same on the text a staged FASTQ holds (mh_fastq_open_part: the whole
+ * file, or a rank's block of records of a sharded job; gzip already
+ * inflated).  The text is taken (the handle keeps an empty one).
+ * *out_bytes = size of the censored output held for mh_censor_output /
+ * mh_censor_write. */
+int mh_censor_staged(mh_ctx *ctx, mh_fastq *fq, int n_bad, const char *const *tiles,
+                     const int32_t *cycles, int dst_gzip, int64_t *out_bytes,
+                     int64_t *base_count, int64_t *score_sum);
 int mh_censor_output(mh_ctx *ctx, char *buf, size_t cap, size_t *used);
+/* The held censored output written to fd at offset (pwrite; the descriptor's
+ * own offset is not used); *written = its size.  The output is released. */
+int mh_censor_write(mh_ctx *ctx, int fd, int64_t offset, int64_t *written);
 /* Host wall ms of the last call: [0] gunzip + record split, [1] upload +
  * k_censor + download, [2] rewrite + gzip. */
 int mh_censor_timing(mh_ctx *ctx, double *ms3);

@@ -1,32 +1,40 @@
 // mh_censor.hip -- censor_fastq.censor (micall/core/censor_fastq.py:32-102)
-// on gfx950, behind mh_censor_fastq / mh_censor_output:
-//   host      gunzip (multi-member): libdeflate on the whole file when the
-//             system has it, else streaming zlib (a producer thread inflates
-//             ~32 MB chunks while the whole records of the chunks already
-//             there are censored); records split in parallel,
-//             tile + read direction from each header exactly as :59-63 parse
-//             them, bad (tile, cycle) set from the caller
+// on gfx950, behind mh_censor_fastq / mh_censor_staged / mh_censor_output /
+// mh_censor_write:
+//   host      the FASTQ text: gunzipped from a buffer (libdeflate, else
+//             zlib) or taken from a staged FASTQ (mh_fastq_open_part: the
+//             file mmap'd, its gzip members inflated in parallel), into a
+//             buffer that is not zero-filled; line starts found in parallel
+//             (memchr, two passes: counts, then positions); records parsed
+//             in parallel, tile + read direction from each header exactly as
+//             :59-63 parse them, bad (tile, cycle) set from the caller
 //   k_censor  one wave64 per read: the bases / qualities of bad cycles
 //             become 'N' / '#' in place, the trailing run of bad cycles is
 //             dropped (the reference only flushes pending Ns before a good
 //             cycle, :66-74, :78-90), and every quality score is summed for
 //             the summary (:80-82) -- per-block sums, one atomic per block
-//   host      records rewritten (header and '+' lines verbatim), optional
-//             gzip as independent deflate members compressed in parallel
+//   host      records rewritten (header and '+' lines verbatim) and, for
+//             gzip output, compressed, in blocks of ~8 MB of records on
+//             every host thread (one gzip member per block: the member
+//             boundaries depend on the input only, not on the thread count);
+//             the output is written with pwrite (mh_censor_write) or copied
+//             out (mh_censor_output)
+#include <sys/types.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
-#include <condition_variable>
-#include <deque>
-#include <mutex>
 #include <cstring>
 #include <functional>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <vector>
 
+#include "mh_fastq.h"
 #include "mh_gunzip.h"
 #include "mh_internal.h"
 
@@ -35,18 +43,17 @@ namespace mh {
 int s2a_threads();   // mh_s2a_host.cpp: host worker count
 
 struct CensorState {
-    std::string text;                       // the FASTQ (censored in place)
-    // per record: spans into text
-    std::vector<int64_t> h0, s0, o0, q0;    // header, seq, '+' line, qual starts
-    std::vector<int32_t> hl, sl, ol, ql;    // line lengths incl. their newline (h, o) /
-                                            // stripped lengths (s, q)
+    TextBuf text;                           // the FASTQ (censored in place)
+    // per record: line starts (header, seq, '+', qual); the header line is
+    // [h0, s0), the '+' line [o0, q0), both with their newline
+    std::vector<int64_t> h0, s0, o0, q0;
+    std::vector<int32_t> sl, ql;            // seq / qual lengths, trailing whitespace stripped
     std::vector<int32_t> tile, sign;        // tile id (-1: no bad cycle) / +1, -1
     std::vector<int32_t> keep;              // 2 per record: kept seq / qual length
     int64_t base_count = 0, score_sum = 0;
-    int64_t rec_base = 0;                   // records before this piece (messages)
-    std::string out;
+    TextBuf out;                            // the censored file (gzip members or text)
     double t_host_in = 0, t_device = 0, t_host_out = 0;
-    // device buffers, grown on demand and kept between pieces and calls
+    // device buffers, grown on demand and kept between calls
     uint8_t *d_text = nullptr;
     int64_t *d_s0 = nullptr, *d_q0 = nullptr;
     int32_t *d_sl = nullptr, *d_ql = nullptr, *d_tile = nullptr, *d_sign = nullptr, *d_keep = nullptr;
@@ -79,6 +86,11 @@ void censor_free(Ctx &c)
     if (c.censor) censor_free_device(*c.censor);
     delete c.censor;
     c.censor = nullptr;
+}
+
+static double ms_since(std::chrono::steady_clock::time_point t0)
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // ---------------------------------------------------------------------------
@@ -148,119 +160,116 @@ __global__ __launch_bounds__(256) void k_censor(CensorArgs A)
     }
 }
 
+
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
-// gzip of `in` as independent members of `block` bytes, compressed in parallel
-static int gzip_parallel(const std::string &in, std::string &out, int level)
-{
-    const int64_t block = 8 << 20;
-    const int64_t nblk = std::max<int64_t>(1, ((int64_t)in.size() + block - 1) / block);
-    std::vector<std::string> parts((size_t)nblk);
-    std::vector<int> err((size_t)nblk, 0);
-    const int nt = (int)std::min<int64_t>(s2a_threads(), nblk);
-    cz_parallel(nt, [&](int t) {
-        for (int64_t b = t; b < nblk; b += nt) {
-            const int64_t a = b * block, e = std::min<int64_t>((int64_t)in.size(), a + block);
-            if (gzip_member(in.data() + a, (size_t)(e - a), parts[b], level)) err[b] = 1;
-        }
-    });
-    for (int e : err) if (e) { set_error("censor: deflate failed"); return -2; }
-    size_t total = 0;
-    for (auto &p : parts) total += p.size();
-    out.clear();
-    out.reserve(total);
-    for (auto &p : parts) out += p;
-    return 0;
-}
-
 static inline bool py_space(unsigned char c)
 {
     return c == ' ' || (c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x1f);
 }
 
+using TileMap = std::unordered_map<std::string_view, int>;
+
 // records of the FASTQ text: 4 lines each (itertools.zip_longest, :57)
-static int split_records(CensorState &C, const std::unordered_map<std::string, int> &tiles)
+static int split_records(CensorState &C, const TileMap &tiles)
 {
-    const std::string &T = C.text;
-    const int64_t n = (int64_t)T.size();
-    // line starts, in parallel chunks
-    const int nt = s2a_threads();
-    std::vector<std::vector<int64_t>> ls(nt);
+    const char *T = C.text.data();
+    const int64_t n = (int64_t)C.text.size();
+    const int nt = std::max(1, std::min<int>(s2a_threads(), (int)(n >> 20) + 1));
+    // newlines per chunk, then every line start at its place: 0, and the byte
+    // after every newline that is not the text's last byte
+    std::vector<int64_t> cnt((size_t)nt + 1, 0);
+    auto chunk = [&](int t, int64_t &a, int64_t &b) { a = n * t / nt; b = n * (t + 1) / nt; };
     cz_parallel(nt, [&](int t) {
-        const int64_t a = n * t / nt, b = n * (t + 1) / nt;
-        for (int64_t i = a; i < b; ++i)
-            if (T[i] == '\n' && i + 1 < n) ls[t].push_back(i + 1);
+        int64_t a, b, k = 0;
+        chunk(t, a, b);
+        for (const char *p = T + a, *e = T + b; p < e;) {
+            const char *q = (const char *)memchr(p, '\n', (size_t)(e - p));
+            if (!q) break;
+            ++k;
+            p = q + 1;
+        }
+        cnt[(size_t)t + 1] = k;
     });
-    std::vector<int64_t> starts;
-    if (n > 0) starts.push_back(0);
-    for (auto &v : ls) starts.insert(starts.end(), v.begin(), v.end());
-    const int64_t nl = (int64_t)starts.size();
+    for (int t = 0; t < nt; ++t) cnt[(size_t)t + 1] += cnt[(size_t)t];
+    const int64_t nl = n == 0 ? 0 : 1 + cnt[(size_t)nt] - (T[n - 1] == '\n' ? 1 : 0);
     if (nl % 4) {
-        set_error("censor: FASTQ has %lld lines, not a multiple of 4",
-                  (long long)(nl + 4 * C.rec_base));
+        set_error("censor: FASTQ has %lld lines, not a multiple of 4", (long long)nl);
         return -3;
     }
+    std::unique_ptr<int64_t[]> starts(new int64_t[(size_t)std::max<int64_t>(nl, 1)]);
+    if (nl) starts[0] = 0;
+    cz_parallel(nt, [&](int t) {
+        int64_t a, b, k = 1 + cnt[(size_t)t];
+        chunk(t, a, b);
+        for (const char *p = T + a, *e = T + b; p < e;) {
+            const char *q = (const char *)memchr(p, '\n', (size_t)(e - p));
+            if (!q) break;
+            const int64_t at = (int64_t)(q - T) + 1;
+            if (at < n) starts[(size_t)k++] = at;
+            p = q + 1;
+        }
+    });
     const int64_t nr = nl / 4;
     C.h0.resize(nr); C.s0.resize(nr); C.o0.resize(nr); C.q0.resize(nr);
-    C.hl.resize(nr); C.sl.resize(nr); C.ol.resize(nr); C.ql.resize(nr);
-    C.tile.resize(nr); C.sign.resize(nr);
-    std::vector<int> bad(nt, 0);
-    std::vector<int64_t> bad_rec(nt, -1);
-    auto line_end = [&](int64_t k) { return k + 1 < nl ? starts[k + 1] : n; };   // after '\n'
-    cz_parallel(nt, [&](int t) {
-        for (int64_t r = nr * t / nt; r < nr * (t + 1) / nt; ++r) {
+    C.sl.resize(nr); C.ql.resize(nr); C.tile.resize(nr); C.sign.resize(nr);
+    const int rt = std::max(1, std::min<int>(nt, (int)(nr >> 12) + 1));
+    std::vector<int> bad((size_t)rt, 0);
+    std::vector<int64_t> bad_rec((size_t)rt, -1);
+    auto line_end = [&](int64_t k) { return k + 1 < nl ? starts[(size_t)k + 1] : n; };   // after '\n'
+    auto stripped = [&](int64_t a, int64_t e) {
+        while (e > a && py_space((unsigned char)T[e - 1])) --e;
+        return (int32_t)(e - a);
+    };
+    cz_parallel(rt, [&](int t) {
+        for (int64_t r = nr * t / rt; r < nr * (t + 1) / rt; ++r) {
             const int64_t k = 4 * r;
-            const int64_t ha = starts[k], he = line_end(k);
-            C.h0[r] = ha; C.hl[r] = (int32_t)(he - ha);
-            C.o0[r] = starts[k + 2]; C.ol[r] = (int32_t)(line_end(k + 2) - starts[k + 2]);
-            auto stripped = [&](int64_t a, int64_t e) {
-                while (e > a && py_space((unsigned char)T[e - 1])) --e;
-                return (int32_t)(e - a);
-            };
-            C.s0[r] = starts[k + 1]; C.sl[r] = stripped(starts[k + 1], line_end(k + 1));
-            C.q0[r] = starts[k + 3]; C.ql[r] = stripped(starts[k + 3], line_end(k + 3));
+            const int64_t ha = starts[(size_t)k], he = starts[(size_t)k + 1];
+            C.h0[r] = ha;
+            C.s0[r] = he;
+            C.o0[r] = starts[(size_t)k + 2];
+            C.q0[r] = starts[(size_t)k + 3];
+            C.sl[r] = stripped(he, C.o0[r]);
+            C.ql[r] = stripped(C.q0[r], line_end(k + 3));
             // ident.split(' ') -> fields[0].split(':')[4] (tile),
             // fields[1].split(':')[0] (read direction); the line keeps its '\n'
-            const char *h = T.data() + ha;
+            const char *h = T + ha;
             const int64_t hn = he - ha;
-            int64_t sp = 0;
-            while (sp < hn && h[sp] != ' ') ++sp;
-            if (sp >= hn) { bad[t] = 1; bad_rec[t] = r; break; }
+            const char *spp = (const char *)memchr(h, ' ', (size_t)hn);
+            if (!spp) { bad[(size_t)t] = 1; bad_rec[(size_t)t] = r; break; }
+            const int64_t sp = spp - h;
             int64_t f = 0, colon = 0;
             while (f < sp && colon < 4) { if (h[f] == ':') ++colon; ++f; }
-            if (colon < 4) { bad[t] = 2; bad_rec[t] = r; break; }
+            if (colon < 4) { bad[(size_t)t] = 2; bad_rec[(size_t)t] = r; break; }
             int64_t g = f;
             while (g < sp && h[g] != ':') ++g;
-            const std::string tl(h + f, (size_t)(g - f));
             int64_t d = sp + 1, de = d;
             while (de < hn && h[de] != ' ' && h[de] != ':') ++de;
-            const bool fwd = de - d == 1 && h[d] == '1';
-            C.sign[r] = fwd ? 1 : -1;
-            auto it = tiles.find(tl);
+            C.sign[r] = (de - d == 1 && h[d] == '1') ? 1 : -1;
+            auto it = tiles.find(std::string_view(h + f, (size_t)(g - f)));
             C.tile[r] = it == tiles.end() ? -1 : it->second;
         }
     });
-    for (int t = 0; t < nt; ++t)
-        if (bad[t]) {
-            set_error(bad[t] == 1 ? "censor: header of record %lld has no space (ValueError)"
-                                  : "censor: header of record %lld has no tile field (IndexError)",
-                      (long long)(bad_rec[t] + 1 + C.rec_base));
+    for (int t = 0; t < rt; ++t)
+        if (bad[(size_t)t]) {
+            set_error(bad[(size_t)t] == 1 ? "censor: header of record %lld has no space (ValueError)"
+                                          : "censor: header of record %lld has no tile field (IndexError)",
+                      (long long)(bad_rec[(size_t)t] + 1));
             return -3;
         }
     return 0;
 }
 
-static int censor_run(Ctx &c, CensorState &C, CensorState &D, int n_bad,
-                      const char *const *tiles, const int32_t *cycles)
+// k_censor over the records: the text up, censored in place, down again
+static int censor_run(Ctx &c, CensorState &C, const TileMap &tid, int n_bad, const char *const *tiles,
+                      const int32_t *cycles)
 {
     const int64_t nr = (int64_t)C.h0.size();
     C.keep.assign(2 * (size_t)nr, 0);
     C.base_count = C.score_sum = 0;
     if (nr == 0) return 0;
-    // bad-cycle bitmaps per bad tile id, over the cycles of this piece's reads
-    std::unordered_map<std::string, int> tid;
-    for (int k = 0; k < n_bad; ++k) tid.emplace(tiles[k], (int)tid.size());
+    // bad-cycle bitmaps per bad tile id, over the cycles of the reads
     int maxc = 1;
     for (int64_t r = 0; r < nr; ++r) maxc = std::max(maxc, std::max(C.sl[r], C.ql[r]));
     const int words = (2 * maxc + 1 + 31) / 32;
@@ -269,7 +278,7 @@ static int censor_run(Ctx &c, CensorState &C, CensorState &D, int n_bad,
         const int c0 = cycles[k];
         if (c0 < -maxc || c0 > maxc) continue;
         const int b = c0 + maxc;
-        bm[(size_t)tid[tiles[k]] * words + (b >> 5)] |= 1u << (b & 31);
+        bm[(size_t)tid.at(std::string_view(tiles[k])) * words + (b >> 5)] |= 1u << (b & 31);
     }
     hipStream_t s = c.stream;
     int st = 0;
@@ -277,6 +286,7 @@ static int censor_run(Ctx &c, CensorState &C, CensorState &D, int n_bad,
         if (e != hipSuccess && !st) st = hip_fail(e, what);
         return st == 0;
     };
+    CensorState &D = C;
     if ((int64_t)C.text.size() + 1 > D.cap_text) {
         hipFree(D.d_text);
         D.d_text = nullptr;
@@ -322,7 +332,7 @@ static int censor_run(Ctx &c, CensorState &C, CensorState &D, int n_bad,
         H(hipGetLastError(), "k_censor");
     }
     unsigned long long sums[2] = {0, 0};
-    H(hipMemcpyAsync(&C.text[0], D.d_text, C.text.size(), hipMemcpyDeviceToHost, s), "D2H");
+    H(hipMemcpyAsync(C.text.data(), D.d_text, C.text.size(), hipMemcpyDeviceToHost, s), "D2H");
     H(hipMemcpyAsync(C.keep.data(), D.d_keep, 8 * nr, hipMemcpyDeviceToHost, s), "D2H");
     H(hipMemcpyAsync(sums, D.d_sums, 16, hipMemcpyDeviceToHost, s), "D2H");
     H(hipStreamSynchronize(s), "sync");
@@ -333,141 +343,96 @@ static int censor_run(Ctx &c, CensorState &C, CensorState &D, int n_bad,
     return 0;
 }
 
-static void censor_write(CensorState &C)
+// The censored records, rewritten (header and '+' lines verbatim, seq and
+// qual cut to their kept length, each line ending in '\n') and, for gzip,
+// deflated, in blocks of records of about CENSOR_BLOCK input bytes, one gzip
+// member per block; the blocks are made by every host thread in turn and
+// placed into C.out by their precomputed offsets.
+constexpr int64_t CENSOR_BLOCK = (int64_t)8 << 20;
+
+static int censor_emit(CensorState &C, int dst_gzip)
 {
     const int64_t nr = (int64_t)C.h0.size();
-    const int nt = s2a_threads();
-    std::vector<std::string> piece(nt);
-    cz_parallel(nt, [&](int t) {
-        std::string &o = piece[t];
-        for (int64_t r = nr * t / nt; r < nr * (t + 1) / nt; ++r) {
-            o.append(C.text, (size_t)C.h0[r], (size_t)C.hl[r]);
-            o.append(C.text, (size_t)C.s0[r], (size_t)C.keep[2 * r]);
-            o.push_back('\n');
-            o.append(C.text, (size_t)C.o0[r], (size_t)C.ol[r]);
-            o.append(C.text, (size_t)C.q0[r], (size_t)C.keep[2 * r + 1]);
-            o.push_back('\n');
+    const int64_t n = (int64_t)C.text.size();
+    std::vector<int64_t> bstart{0};
+    for (int64_t r = 0, base = 0; r < nr; ++r) {
+        if (C.h0[r] - base >= CENSOR_BLOCK) { bstart.push_back(r); base = C.h0[r]; }
+    }
+    if (nr > 0) bstart.push_back(nr);
+    const int64_t nb = (int64_t)bstart.size() - 1;
+    if (nb <= 0) {
+        C.out.clear();
+        if (dst_gzip) {   // an empty FASTQ still makes one (empty) gzip member
+            if (gzip_member("", 0, C.out, 1)) { set_error("censor: deflate failed"); return -2; }
+        }
+        return 0;
+    }
+    std::vector<TextBuf> part((size_t)nb);
+    std::atomic<int64_t> next(0);
+    std::atomic<int> err(0);
+    const int nt = std::max(1, std::min<int>(s2a_threads(), (int)nb));
+    const char *T = C.text.data();
+    cz_parallel(nt, [&](int) {
+        TextBuf raw;
+        for (int64_t b; (b = next.fetch_add(1)) < nb;) {
+            const int64_t r0 = bstart[(size_t)b], r1 = bstart[(size_t)b + 1];
+            const int64_t in_end = r1 < nr ? C.h0[r1] : n;
+            TextBuf &dst = dst_gzip ? raw : part[(size_t)b];
+            dst.resize((size_t)(in_end - C.h0[r0] + 2 * (r1 - r0)));
+            char *o = dst.data();
+            for (int64_t r = r0; r < r1; ++r) {
+                const size_t hl = (size_t)(C.s0[r] - C.h0[r]), pl = (size_t)(C.q0[r] - C.o0[r]);
+                const size_t ks = (size_t)C.keep[2 * r], kq = (size_t)C.keep[2 * r + 1];
+                memcpy(o, T + C.h0[r], hl); o += hl;
+                memcpy(o, T + C.s0[r], ks); o += ks;
+                *o++ = '\n';
+                memcpy(o, T + C.o0[r], pl); o += pl;
+                memcpy(o, T + C.q0[r], kq); o += kq;
+                *o++ = '\n';
+            }
+            dst.resize((size_t)(o - dst.data()));
+            if (dst_gzip && gzip_member(raw.data(), raw.size(), part[(size_t)b], 1)) err = 1;
         }
     });
-    size_t total = 0;
-    for (auto &p : piece) total += p.size();
-    C.out.clear();
-    C.out.reserve(total);
-    for (auto &p : piece) C.out += p;
-}
-
-// One piece of whole records: split, censor on the device, rewrite, deflate;
-// the output and the sums go to C.
-static int censor_piece(Ctx &c, CensorState &C, std::string &&text,
-                        const std::unordered_map<std::string, int> &tid, int n_bad,
-                        const char *const *tiles, const int32_t *cycles, int dst_gzip)
-{
-    CensorState P;
-    P.text.swap(text);
-    P.rec_base = C.rec_base;
-    if (int st = split_records(P, tid)) return st;
-    C.rec_base += (int64_t)P.h0.size();
-    auto t0 = std::chrono::steady_clock::now();
-    if (int st = censor_run(c, P, C, n_bad, tiles, cycles)) return st;
-    C.t_device += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    censor_write(P);
-    std::string().swap(P.text);
-    if (dst_gzip) {
-        std::string z;
-        if (int st = gzip_parallel(P.out, z, 1)) return st;
-        C.out += z;
-    } else {
-        C.out += P.out;
-    }
-    C.base_count += P.base_count;
-    C.score_sum += P.score_sum;
+    if (err) { set_error("censor: deflate failed"); return -2; }
+    std::vector<size_t> off((size_t)nb + 1, 0);
+    for (int64_t b = 0; b < nb; ++b) off[(size_t)b + 1] = off[(size_t)b] + part[(size_t)b].size();
+    C.out.resize(off[(size_t)nb]);
+    next = 0;
+    cz_parallel(nt, [&](int) {
+        for (int64_t b; (b = next.fetch_add(1)) < nb;) {
+            memcpy(C.out.data() + off[(size_t)b], part[(size_t)b].data(), part[(size_t)b].size());
+            part[(size_t)b].release();
+        }
+    });
     return 0;
 }
 
-// Streaming inflate: a producer thread inflates the gzip input (multi-member)
-// into ~32 MB chunks while the caller censors the records of the chunks
-// already there (serial inflate is this stage's bound).
-struct InflateQueue {
-    std::mutex m;
-    std::condition_variable cv;
-    std::deque<std::string> q;
-    bool done = false;
-    int err = 0;
-    std::string msg;
-};
-
-static void inflate_producer(const uint8_t *src, int64_t len, InflateQueue &Q)
+// one FASTQ text (moved into C.text) through split, k_censor and the rewrite
+static int censor_text(Ctx &c, CensorState &C, int n_bad, const char *const *tiles,
+                       const int32_t *cycles, int dst_gzip, std::chrono::steady_clock::time_point t0)
 {
-    const size_t chunk = 32u << 20;
-    auto push = [&](std::string &&piece) {
-        std::unique_lock<std::mutex> lk(Q.m);
-        Q.cv.wait(lk, [&] { return Q.q.size() < 4; });
-        Q.q.push_back(std::move(piece));
-        Q.cv.notify_all();
-    };
-    auto finish = [&](int err, const char *msg) {
-        std::lock_guard<std::mutex> lk(Q.m);
-        Q.err = err;
-        if (msg) Q.msg = msg;
-        Q.done = true;
-        Q.cv.notify_all();
-    };
-    if (len == 0) { finish(0, nullptr); return; }
-    z_stream z{};
-    if (inflateInit2(&z, 15 + 32) != Z_OK) { finish(1, "censor: zlib init"); return; }
-    std::string cur;
-    cur.reserve(chunk + (4u << 20));
-    std::vector<char> buf(4u << 20);
-    int64_t pos = 0;
-    bool ended = false;
-    for (;;) {
-        if (z.avail_in == 0) {
-            if (pos >= len) break;
-            const int64_t take = std::min<int64_t>(len - pos, 1 << 30);
-            z.next_in = (Bytef *)(src + pos);
-            z.avail_in = (uInt)take;
-            pos += take;
-        }
-        z.next_out = (Bytef *)buf.data();
-        z.avail_out = (uInt)buf.size();
-        const int st = inflate(&z, Z_NO_FLUSH);
-        cur.append(buf.data(), buf.size() - z.avail_out);
-        if (cur.size() >= chunk) {
-            push(std::move(cur));
-            cur = std::string();
-            cur.reserve(chunk + (4u << 20));
-        }
-        if (st == Z_STREAM_END) {
-            ended = true;
-            if (z.avail_in == 0 && pos >= len) break;
-            inflateReset(&z);          // GzipFile reads concatenated members
-            ended = false;
-            continue;
-        }
-        if (st != Z_OK && !(st == Z_BUF_ERROR && z.avail_in == 0)) {
-            inflateEnd(&z);
-            finish(1, "censor: not a valid gzip stream");
-            return;
-        }
-    }
-    inflateEnd(&z);
-    if (!ended) { finish(1, "censor: truncated gzip stream"); return; }
-    if (!cur.empty()) push(std::move(cur));
-    finish(0, nullptr);
+    TileMap tid;
+    for (int k = 0; k < n_bad; ++k) tid.emplace(std::string_view(tiles[k]), (int)tid.size());
+    if (int st = split_records(C, tid)) return st;
+    C.t_host_in = ms_since(t0);
+    const auto t1 = std::chrono::steady_clock::now();
+    if (int st = censor_run(c, C, tid, n_bad, tiles, cycles)) return st;
+    C.t_device = ms_since(t1);
+    const auto t2 = std::chrono::steady_clock::now();
+    const int st = censor_emit(C, dst_gzip);
+    C.t_host_out = ms_since(t2);
+    // the text and record tables are not needed past the call: freed on a
+    // detached thread (a GB-sized free is tens of ms)
+    auto *old = new TextBuf();
+    old->swap(C.text);
+    std::thread([old]() { delete old; }).detach();
+    return st;
 }
 
-// end of the last whole record (4 lines) in t, from its start
-static size_t last_record_end(const std::string &t)
+static bool censor_args_ok(mh_ctx *ctx, int n_bad, const char *const *tiles, const int32_t *cycles)
 {
-    size_t cut = 0, at = 0;
-    int lines = 0;
-    for (;;) {
-        const void *nl = memchr(t.data() + at, '\n', t.size() - at);
-        if (!nl) break;
-        at = (size_t)((const char *)nl - t.data()) + 1;
-        if (++lines == 4) { lines = 0; cut = at; }
-    }
-    return cut;
+    return ctx && n_bad >= 0 && (!n_bad || (tiles && cycles));
 }
 
 }  // namespace mh
@@ -478,115 +443,47 @@ extern "C" int mh_censor_fastq(mh_ctx *ctx, const uint8_t *src, int64_t len, int
                                int n_bad, const char *const *tiles, const int32_t *cycles,
                                int dst_gzip, int64_t *base_count, int64_t *score_sum)
 {
-    if (!ctx || (len && !src) || len < 0 || n_bad < 0 || (n_bad && (!tiles || !cycles))) return -3;
+    if (!censor_args_ok(ctx, n_bad, tiles, cycles) || (len && !src) || len < 0) return -3;
     Ctx &c = *ctx_of(ctx);
     MH_HIP(hipSetDevice(c.device));
     if (!c.censor) c.censor = new CensorState();
     CensorState &C = *c.censor;
     C.out.clear();
     C.base_count = C.score_sum = 0;
-    C.rec_base = 0;
     C.t_host_in = C.t_device = C.t_host_out = 0;
-    std::unordered_map<std::string, int> tid;
-    for (int k = 0; k < n_bad; ++k) tid.emplace(tiles[k], (int)tid.size());
-    auto t0 = std::chrono::steady_clock::now();
-    int pieces = 0;
-    if (!src_gzip) {
-        std::string text((const char *)src, (size_t)len);
-        if (len) {
-            if (int st = censor_piece(c, C, std::move(text), tid, n_bad, tiles, cycles, dst_gzip))
-                return st;
-            ++pieces;
-        }
-    } else if (gunzip_fast_available()) {
-        // libdeflate decodes the whole file faster than the streaming zlib
-        // producer below can overlap it with the rest
-        std::string text, why;
-        if (gunzip_buffer(src, len, text, why)) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (src_gzip) {
+        std::string why;
+        if (gunzip_buffer(src, len, C.text, why)) {
             set_error("censor: %s", why.c_str());
             return -3;
         }
-        C.t_host_in = std::chrono::duration<double, std::milli>(
-                          std::chrono::steady_clock::now() - t0).count();
-        if (!text.empty()) {
-            if (int st = censor_piece(c, C, std::move(text), tid, n_bad, tiles, cycles, dst_gzip))
-                return st;
-            ++pieces;
-        }
     } else {
-        InflateQueue Q;
-        std::thread producer(inflate_producer, src, len, std::ref(Q));
-        std::string carry;
-        int st = 0;
-        for (;;) {
-            std::string chunk;
-            bool last = false;
-            {
-                std::unique_lock<std::mutex> lk(Q.m);
-                Q.cv.wait(lk, [&] { return !Q.q.empty() || Q.done; });
-                if (!Q.q.empty()) {
-                    chunk = std::move(Q.q.front());
-                    Q.q.pop_front();
-                    Q.cv.notify_all();
-                } else {
-                    last = true;
-                    if (Q.err) {
-                        set_error("%s", Q.msg.c_str());
-                        st = -3;
-                    }
-                }
-            }
-            if (st) break;
-            if (last) {
-                C.t_host_in = std::chrono::duration<double, std::milli>(
-                                  std::chrono::steady_clock::now() - t0).count();
-                // a trailing partial record (or one without its last newline)
-                if (!carry.empty()) {
-                    st = censor_piece(c, C, std::move(carry), tid, n_bad, tiles, cycles, dst_gzip);
-                    ++pieces;
-                }
-                break;
-            }
-            carry += chunk;
-            std::string().swap(chunk);
-            const size_t cut = last_record_end(carry);
-            if (cut == 0) continue;
-            std::string rest(carry, cut);
-            carry.resize(cut);
-            st = censor_piece(c, C, std::move(carry), tid, n_bad, tiles, cycles, dst_gzip);
-            ++pieces;
-            carry.swap(rest);
-            if (st) break;
-        }
-        if (st) {
-            // drain the producer before leaving
-            {
-                std::unique_lock<std::mutex> lk(Q.m);
-                Q.q.clear();
-                Q.cv.notify_all();
-            }
-            for (;;) {
-                std::unique_lock<std::mutex> lk(Q.m);
-                if (Q.done) break;
-                Q.cv.wait(lk, [&] { return !Q.q.empty() || Q.done; });
-                Q.q.clear();
-                Q.cv.notify_all();
-            }
-            producer.join();
-            C.out.clear();
-            return st;
-        }
-        producer.join();
+        C.text.assign((const char *)src, (size_t)len);
     }
-    if (!pieces && dst_gzip) {
-        // an empty FASTQ still makes one (empty) gzip member
-        if (int st = gzip_parallel(std::string(), C.out, 1)) return st;
-    }
-    const double total = std::chrono::duration<double, std::milli>(
-                             std::chrono::steady_clock::now() - t0).count();
-    if (!src_gzip) C.t_host_in = 0;
-    if (!C.t_host_in) C.t_host_in = 0;
-    C.t_host_out = total - C.t_host_in;
+    if (int st = censor_text(c, C, n_bad, tiles, cycles, dst_gzip, t0)) { C.out.clear(); return st; }
+    if (base_count) *base_count = C.base_count;
+    if (score_sum) *score_sum = C.score_sum;
+    return 0;
+}
+
+extern "C" int mh_censor_staged(mh_ctx *ctx, mh_fastq *fq, int n_bad, const char *const *tiles,
+                                const int32_t *cycles, int dst_gzip, int64_t *out_bytes,
+                                int64_t *base_count, int64_t *score_sum)
+{
+    if (!censor_args_ok(ctx, n_bad, tiles, cycles) || !fq) return -3;
+    Ctx &c = *ctx_of(ctx);
+    MH_HIP(hipSetDevice(c.device));
+    if (!c.censor) c.censor = new CensorState();
+    CensorState &C = *c.censor;
+    C.out.clear();
+    C.base_count = C.score_sum = 0;
+    C.t_host_in = C.t_device = C.t_host_out = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    TextBuf text = take_fastq_text(fq);
+    C.text.swap(text);
+    if (int st = censor_text(c, C, n_bad, tiles, cycles, dst_gzip, t0)) { C.out.clear(); return st; }
+    if (out_bytes) *out_bytes = (int64_t)C.out.size();
     if (base_count) *base_count = C.base_count;
     if (score_sum) *score_sum = C.score_sum;
     return 0;
@@ -601,8 +498,30 @@ extern "C" int mh_censor_output(mh_ctx *ctx, char *buf, size_t cap, size_t *used
     *used = C.out.size();
     if (!buf) return 0;
     if (cap < C.out.size()) { set_error("mh_censor_output: buffer too small"); return -2; }
-    memcpy(buf, C.out.data(), C.out.size());
-    std::string().swap(C.out);
+    if (C.out.size()) memcpy(buf, C.out.data(), C.out.size());
+    C.out.release();
+    return 0;
+}
+
+extern "C" int mh_censor_write(mh_ctx *ctx, int fd, int64_t offset, int64_t *written)
+{
+    if (!ctx || fd < 0 || offset < 0) return -3;
+    Ctx &c = *ctx_of(ctx);
+    if (!c.censor) { set_error("mh_censor_write: no censor results"); return -3; }
+    CensorState &C = *c.censor;
+    const char *p = C.out.data();
+    size_t left = C.out.size();
+    int64_t pos = offset;
+    while (left > 0) {
+        const ssize_t w = pwrite(fd, p, left, (off_t)pos);
+        if (w <= 0) {
+            set_error("mh_censor_write: write failed (%s)", strerror(errno ? errno : EIO));
+            return -4;
+        }
+        p += w; left -= (size_t)w; pos += w;
+    }
+    if (written) *written = pos - offset;
+    C.out.release();
     return 0;
 }
 

@@ -217,6 +217,25 @@ int gunzip_members(const LdApi &api, const uint8_t *src, int64_t len, Buf &out, 
         for (auto &v : part) cand.insert(cand.end(), v.begin(), v.end());
     }
     if (cand.empty() || cand[0] != 0) return -1;
+    {
+        // header-shaped bytes inside compressed data are common (a few per
+        // 16 MB): a candidate after the first must also start decoding (its
+        // first 16 KB of output), else it is dropped here instead of splitting
+        // a member into spans that fail to decode.  A single member (as
+        // bcl2fastq writes it) is left with one candidate and decoded serially
+        // by the caller.
+        std::vector<char> keep(cand.size(), 1);
+        std::atomic<size_t> next(1);
+        run_threads(std::min<int>(threads, (int)cand.size()), [&](int) {
+            for (size_t j; (j = next.fetch_add(1)) < cand.size();)
+                keep[j] = gzip_member_probe(src + cand[j], len - cand[j], 16384);
+        });
+        size_t w = 0;
+        for (size_t j = 0; j < cand.size(); ++j)
+            if (keep[j]) cand[w++] = cand[j];
+        cand.resize(w);
+        if (cand.size() < 2) return -2;   // one member
+    }
     cand.push_back(len);
     // spans [cand[j], cand[j + 1]) and their sizes, merging spans whose
     // decode failed until every span is one whole member
@@ -335,6 +354,12 @@ bool gzip_member_probe(const uint8_t *src, int64_t len, size_t probe)
     return ok;
 }
 
+static bool getenv_flag(const char *name)
+{
+    const char *e = getenv(name);
+    return e && *e == '1';
+}
+
 int gunzip_threads()
 {
     const char *e = getenv("OMP_NUM_THREADS");
@@ -356,6 +381,11 @@ int gunzip_any(const uint8_t *src, int64_t len, Buf &out, std::string &why)
         int st = -1;
         try {
             st = gunzip_members(api, src, len, out, gunzip_threads());
+            // one member: its deflate blocks found and inflated in parallel
+            if (st == -2 && !getenv_flag("MICALL_SERIAL_INFLATE")) {
+                Buf().swap(out);
+                st = gunzip_single_parallel(src, len, out, gunzip_threads());
+            }
         } catch (const std::exception &) {   // bad_alloc / length_error: decode serially
             st = -1;
         }
@@ -381,7 +411,8 @@ int gunzip_buffer(const uint8_t *src, int64_t len, TextBuf &out, std::string &wh
     return gunzip_any(src, len, out, why);
 }
 
-int gzip_member(const char *src, size_t len, std::string &out, int level)
+template <class Buf>
+static int gzip_member_any(const char *src, size_t len, Buf &out, int level)
 {
     const LdApi &api = ld_api();
     if (api.c_ok) {
@@ -404,6 +435,16 @@ int gzip_member(const char *src, size_t len, std::string &out, int level)
     out.resize(out.size() - z.avail_out);
     deflateEnd(&z);
     return st == Z_STREAM_END ? 0 : -2;
+}
+
+int gzip_member(const char *src, size_t len, std::string &out, int level)
+{
+    return gzip_member_any(src, len, out, level);
+}
+
+int gzip_member(const char *src, size_t len, TextBuf &out, int level)
+{
+    return gzip_member_any(src, len, out, level);
 }
 
 }  // namespace mh

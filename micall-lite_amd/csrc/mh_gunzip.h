@@ -72,6 +72,11 @@ bool gunzip_fast_available();
 // One gzip member of src[0 .. len) at `level` (libdeflate when present);
 // 0, or -2 when compression fails.
 int gzip_member(const char *src, size_t len, std::string &out, int level);
+int gzip_member(const char *src, size_t len, TextBuf &out, int level);
+// One gzip member (the whole of src) inflated by `threads` host threads
+// (mh_pinflate.cpp); -1 when it cannot be (the caller inflates serially).
+template <class Buf>
+int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int threads);
 // crc32 (zlib's polynomial; libdeflate's PCLMUL code when present)
 uint32_t crc32_update(uint32_t crc, const void *p, size_t n);
 // crc32 of A then B from crc32(A), crc32(B) and the length of B

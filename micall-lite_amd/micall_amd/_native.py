@@ -121,8 +121,11 @@ def _declare(L):
         'mh_censor_fastq': ([_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                              ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_int, _I64P, _I64P],
                             ctypes.c_int),
+        'mh_censor_staged': ([_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_int,
+                              _I64P, _I64P, _I64P], ctypes.c_int),
         'mh_censor_output': ([_P, ctypes.c_char_p, ctypes.c_size_t,
                               ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        'mh_censor_write': ([_P, ctypes.c_int, ctypes.c_int64, _I64P], ctypes.c_int),
         'mh_censor_timing': ([_P, _P], ctypes.c_int),
         'mh_a2c_load_csv': ([_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p,
                              _I64P], ctypes.c_int),
@@ -264,22 +267,48 @@ class Context:
         del cbuf
         return buf.decode()
 
+    @staticmethod
+    def _bad_cycle_args(bad_cycles):
+        tiles = (ctypes.c_char_p * max(len(bad_cycles), 1))(*[t.encode() for t, _ in bad_cycles])
+        cycles = np.array([c for _, c in bad_cycles] or [0], dtype=np.int32)
+        return tiles, cycles
+
     def censor_fastq(self, data, bad_cycles, src_gzip, dst_gzip):
         """mh_censor_fastq: (censored bytes, base_count, score_sum) for FASTQ
         bytes and [(tile, cycle)] bad cycles."""
-        tiles = (ctypes.c_char_p * max(len(bad_cycles), 1))(*[t.encode() for t, _ in bad_cycles])
-        cycles = np.array([c for _, c in bad_cycles] or [0], dtype=np.int32)
+        tiles, cycles = self._bad_cycle_args(bad_cycles)
         bc, ss = ctypes.c_int64(), ctypes.c_int64()
-        check(lib().mh_censor_fastq(self.h, bytes(data), len(data), int(src_gzip), len(bad_cycles),
+        src = data if isinstance(data, bytes) else bytes(data)
+        check(lib().mh_censor_fastq(self.h, src, len(src), int(src_gzip), len(bad_cycles),
                                     tiles, _ptr(cycles), int(dst_gzip), ctypes.byref(bc),
                                     ctypes.byref(ss)), 'mh_censor_fastq')
+        return self.censor_output(), bc.value, ss.value
+
+    def censor_staged(self, fq, bad_cycles, dst_gzip):
+        """mh_censor_staged on a staged FASTQ's text (taken from the handle):
+        (output bytes held, base_count, score_sum)."""
+        tiles, cycles = self._bad_cycle_args(bad_cycles)
+        nb, bc, ss = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(lib().mh_censor_staged(self.h, fq.h, len(bad_cycles), tiles, _ptr(cycles), int(dst_gzip),
+                                     ctypes.byref(nb), ctypes.byref(bc), ctypes.byref(ss)),
+              'mh_censor_staged')
+        return nb.value, bc.value, ss.value
+
+    def censor_output(self):
+        """The held censored output as a bytearray (then released)."""
         used = ctypes.c_size_t()
         check(lib().mh_censor_output(self.h, None, 0, ctypes.byref(used)), 'mh_censor_output')
         buf = bytearray(used.value)
         cbuf = (ctypes.c_char * max(len(buf), 1)).from_buffer(buf) if buf else None
         check(lib().mh_censor_output(self.h, cbuf, len(buf), ctypes.byref(used)), 'mh_censor_output')
         del cbuf
-        return bytes(buf), bc.value, ss.value
+        return buf
+
+    def censor_write(self, fd, offset):
+        """The held censored output written to fd at offset (then released)."""
+        n = ctypes.c_int64()
+        check(lib().mh_censor_write(self.h, int(fd), int(offset), ctypes.byref(n)), 'mh_censor_write')
+        return n.value
 
     def censor_timing(self):
         out = np.zeros(3, dtype=np.float64)

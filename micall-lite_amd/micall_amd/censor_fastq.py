@@ -62,7 +62,29 @@ def censor(src, bad_cycles_reader, dest, use_gzip=True, summary_file=None):
 
 
 def _censor_whole(src, bad_cycles, dest, use_gzip):
-    """The whole file by one process."""
+    """The whole file by one process: straight from the source file to the
+    destination file when both are plain binary files (the source mmap'd
+    and its gzip members inflated in parallel, the output written with
+    pwrite at dest's position), else through bytes."""
+    import io
+    from . import _native
+    plain = isinstance(src, (io.BufferedReader, io.FileIO)) and isinstance(dest, (io.BufferedWriter,
+                                                                                   io.BufferedRandom,
+                                                                                   io.FileIO))
+    fd = _binary_fd(src) if plain else None
+    out_fd = _binary_fd(dest) if plain else None
+    if (fd is not None and out_fd is not None and src.tell() == 0 and
+            _is_gzip_file(fd) == bool(use_gzip)):
+        ctx = session.context()
+        fq = _native.Fastq(fd=fd)
+        try:
+            n, base_count, score_sum = ctx.censor_staged(fq, bad_cycles, use_gzip)
+        finally:
+            fq.close()
+        shared = sharded_io.SharedOutput(None, dest, binary=True)
+        ctx.censor_write(out_fd, int(shared.place([n])[0]))
+        shared.finish()
+        return base_count, score_sum
     data = src.read()
     text_mode = isinstance(data, str)
     if text_mode:
@@ -78,14 +100,19 @@ def _censor_block(sh, fd, bad_cycles, dest, use_gzip):
     """This rank's block of records, censored and written at its offset."""
     st = sharded_io.stage_fastq(sh, [(None, fd)], strict=True)
     fq = st['frames'][0].fq
-    text = fq.view().tobytes()
-    fq.close()
-    out, base_count, score_sum = session.context().censor_fastq(
-        text, bad_cycles, src_gzip=False, dst_gzip=use_gzip)
+    ctx = session.context()
+    try:
+        n, base_count, score_sum = ctx.censor_staged(fq, bad_cycles, use_gzip)
+    finally:
+        fq.close()
     if sh.rank == 0:
         dest.flush()
     shared = sharded_io.SharedOutput(sh, dest, binary=True)
-    shared.write_bytes([out])
+    if shared.direct:
+        off = int(shared.place([n])[0])
+        ctx.censor_write(shared.fd, off)
+    else:
+        shared.write_bytes([ctx.censor_output()])
     shared.finish()
     sums = sh.sum_i64([base_count, score_sum])
     return int(sums[0]), int(sums[1])

@@ -272,3 +272,51 @@ def test_host_parse_matches_the_loader_rules(tmp_path, variant):
     assert len(un_seqs) == 300
     a.close()
     b.close()
+
+
+def _pinflate_run(path, env_extra):
+    """Stage a FASTQ in a child process with MH_PINFLATE_TRACE: (text sha, stderr)."""
+    import subprocess
+    import sys
+    code = ('import hashlib, sys; sys.path[:0] = [%r]\n'
+            'from micall_amd import _native\n'
+            'fq = _native.Fastq(path=%r)\n'
+            'print(hashlib.sha256(fq.view().tobytes()).hexdigest())\n'
+            % (os.path.dirname(os.path.dirname(os.path.abspath(_native.__file__))), path))
+    env = dict(os.environ, MH_PINFLATE_TRACE='1', OMP_NUM_THREADS='4', **env_extra)
+    out = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, env=env, timeout=300)
+    assert out.returncode == 0, out.stderr
+    return out.stdout.strip(), out.stderr
+
+
+@pytest.mark.parametrize('level,nul', [(1, False), (6, False), (9, True)])
+def test_single_member_parallel_inflate(tmp_path, level, nul):
+    """One gzip member (as bcl2fastq writes it) of > 8 MB is inflated by
+    several threads (mh_pinflate.cpp: block starts found by header search,
+    spans decoded with a zero window, window-derived bytes resolved from
+    base-255 offset windows, CRC-32 checked) and gives the bytes of a plain
+    inflate; a file holding NUL bytes (which the zero window cannot tell from
+    window bytes) too."""
+    import hashlib
+    import numpy as np
+    rng = np.random.default_rng(level)
+    n = 90000 if level == 1 else 60000
+    bases = np.frombuffer(b'ACGT', dtype=np.uint8)[rng.integers(0, 4, (n, 151))]
+    quals = (rng.integers(0, 40, (n, 151)) + 33).astype(np.uint8)
+    if nul:
+        quals[::997, 7] = 0
+    lines = []
+    for i in range(n):
+        lines.append(b'@M01:1:FC:1:%d:%d:%d 1:N:0:1\n' % (1101 + i % 4, i, i))
+        lines.append(bases[i].tobytes() + b'\n+\n' + quals[i].tobytes() + b'\n')
+    text = b''.join(lines)
+    path = str(tmp_path / 'R1.fastq.gz')
+    with gzip.GzipFile(path, 'wb', compresslevel=level) as f:    # FNAME in the header
+        f.write(text)
+    assert os.path.getsize(path) > (8 << 20)
+    want = hashlib.sha256(text).hexdigest()
+    got, err = _pinflate_run(path, {})
+    assert got == want
+    assert 'pinflate crc' in err, err[-2000:]
+    got, err = _pinflate_run(path, {'MICALL_SERIAL_INFLATE': '1'})
+    assert got == want and 'pinflate' not in err
