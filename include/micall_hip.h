@@ -338,6 +338,13 @@ int mh_sam2aln_csv(mh_ctx *ctx, const char *text, int64_t len, int q_cutoff, dou
  * insert.csv, 2 = failed.csv (DictWriter, '\n' line ends, with header).
  * buf NULL: only *used = bytes needed. */
 int mh_sam2aln_output(mh_ctx *ctx, int which, char *buf, size_t cap, size_t *used);
+/* mh_sam2aln_csv on the whole of a regular file (fd, mmap'd from offset 0):
+ * 0, or 1 when the file holds '\r' (a text-mode read would translate it;
+ * the caller reads the file itself), or an error. */
+int mh_sam2aln_file(mh_ctx *ctx, int fd, int q_cutoff, double max_prop_n, int64_t *n_units);
+/* Output `which` (as mh_sam2aln_output) written to fd at offset with
+ * pwrite (the descriptor's own offset is not used); *written = its size. */
+int mh_sam2aln_write(mh_ctx *ctx, int which, int fd, int64_t offset, int64_t *written);
 /* out[0] pairs, out[1] pairs merged on the device, out[2] distinct merged
  * sequences, out[3] failed pairs. */
 int mh_sam2aln_stats(mh_ctx *ctx, int64_t *out4);

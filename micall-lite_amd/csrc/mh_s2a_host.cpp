@@ -9,6 +9,8 @@
 // for any thread count.
 #include <algorithm>
 #include <charconv>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -142,7 +144,7 @@ static int8_t cigar_ops(const char *c, size_t n, int64_t L, std::vector<uint32_t
 struct Part {
     const char *beg = nullptr, *end = nullptr;
     int64_t rows = 0;
-    std::string qpool, cpool, seq, qual;
+    TextBuf qpool, cpool, seq, qual;
     std::vector<int64_t> qoff, coff, soff;
     std::vector<int32_t> qlen, clen, slen, flag, pos, cig_off, n_cig, rid;
     std::vector<uint64_t> qhash;
@@ -164,6 +166,19 @@ static void parse_part(Part &P, const int *col)
     const char *p = P.beg;
     int need = 0;
     for (int k = 0; k < 11; ++k) need = std::max(need, col[k] + 1);
+    {   // upper bounds from the part's bytes (a row's seq and qual are under
+        // half its bytes each; C2 rows are ~600 bytes): no regrowth copies
+        const size_t bytes = (size_t)(P.end - P.beg);
+        P.seq.reserve(bytes / 2 + 64);
+        P.qual.reserve(bytes / 2 + 64);
+        P.qpool.reserve(bytes / 4 + 64);
+        P.cpool.reserve(bytes / 8 + 64);
+        const size_t rows = bytes / 256 + 16;
+        P.qoff.reserve(rows); P.coff.reserve(rows); P.soff.reserve(rows); P.qlen.reserve(rows);
+        P.clen.reserve(rows); P.slen.reserve(rows); P.flag.reserve(rows); P.pos.reserve(rows);
+        P.cig_off.reserve(rows); P.n_cig.reserve(rows); P.rid.reserve(rows); P.qhash.reserve(rows);
+        P.cstate.reserve(rows); P.qshort.reserve(rows);
+    }
     while (p < P.end) {
         if (!record_views(p, P.end, f, scratch)) {
             P.err = 1; P.err_row = P.rows; P.err_msg = "more than 64 columns";
@@ -205,7 +220,12 @@ static void parse_part(Part &P, const int *col)
         P.seq.append(sq.p, sq.n);
         P.qshort.push_back(ql.n < sq.n);
         if (ql.n >= sq.n) P.qual.append(ql.p, sq.n);
-        else { P.qual.append(ql.p, ql.n); P.qual.append(sq.n - ql.n, '!'); }
+        else {
+            P.qual.append(ql.p, ql.n);
+            const size_t at = P.qual.size();
+            P.qual.resize(at + (sq.n - ql.n));
+            memset(P.qual.data() + at, '!', sq.n - ql.n);
+        }
         ++P.rows;
     }
 }
@@ -244,8 +264,18 @@ static int row_error(const S2AState &S, int64_t r)
     return 0;
 }
 
+// MH_S2A_TRACE=1: phase times of s2a_parse to stderr
+static void s2a_mark(std::chrono::steady_clock::time_point t0, const char *what)
+{
+    static const bool on = getenv("MH_S2A_TRACE") && *getenv("MH_S2A_TRACE") == '1';
+    if (on)
+        fprintf(stderr, "s2a_parse %s %.1f ms\n", what,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+}
+
 int s2a_parse(S2AState &S, const char *text, int64_t len)
 {
+    const auto tp = std::chrono::steady_clock::now();
     const char *p = text, *end = text + len;
     std::vector<std::string> head;
     if (!csv_record(p, end, head)) {
@@ -289,7 +319,9 @@ int s2a_parse(S2AState &S, const char *text, int64_t len)
     }
     std::vector<Part> parts(nt);
     for (int t = 0; t < nt; ++t) { parts[t].beg = cut[t]; parts[t].end = cut[t + 1]; }
+    s2a_mark(tp, "split");
     parallel_for(nt, [&](int t) { parse_part(parts[t], col); });
+    s2a_mark(tp, "parts");
     int64_t base = 0;
     for (auto &P : parts) {
         if (P.err) {
@@ -351,7 +383,11 @@ int s2a_parse(S2AState &S, const char *text, int64_t len)
             qhash[b + i] = P.qhash[i];
         }
     });
-    parts.clear();
+    {   // the parts' buffers freed off the clock (GB-sized frees take tens of ms)
+        auto *old = new std::vector<Part>(std::move(parts));
+        std::thread([old]() { delete old; }).detach();
+    }
+    s2a_mark(tp, "concat");
     // ---- matchmaker (sam2aln.py:291-312): open addressing on qname ----
     uint64_t cap = 1024;
     while (cap < (uint64_t)(2 * nr + 2)) cap <<= 1;
@@ -388,6 +424,7 @@ int s2a_parse(S2AState &S, const char *text, int64_t len)
         }
     }
     for (auto &o : pend) if (o.second) { S.u1.push_back(o.first); S.u2.push_back(-1); }
+    s2a_mark(tp, "matchmaker");
     // ---- parse_sam's early causes and the rname order ----
     const int64_t nu = (int64_t)S.u1.size();
     S.ucause.assign(nu, -1);
@@ -414,6 +451,7 @@ int s2a_parse(S2AState &S, const char *text, int64_t len)
                 if (int st = row_error(S, r2)) return st;
         }
     }
+    s2a_mark(tp, "causes");
     return 0;
 }
 
@@ -445,26 +483,25 @@ static void parallel_sort(std::vector<int64_t> &v, Cmp cmp, int nt)
     }
 }
 
-// concatenates what fn(t, range) writes for nt ranges of [0, n)
-static void parallel_text(int64_t n, int nt, std::string &out,
+// the pieces fn(t, range) writes for nt ranges of [0, n), appended in order
+using Pieces = std::vector<std::string>;
+static void parallel_text(int64_t n, int nt, Pieces &out,
                           const std::function<void(std::string &, int64_t, int64_t)> &fn)
 {
     if (n < 4096) nt = 1;
     std::vector<std::string> piece(nt);
     parallel_for(nt, [&](int t) { fn(piece[t], n * t / nt, n * (t + 1) / nt); });
-    size_t total = out.size();
-    for (auto &x : piece) total += x.size();
-    out.reserve(total);
-    for (auto &x : piece) out += x;
+    for (auto &x : piece)
+        if (!x.empty()) out.push_back(std::move(x));
 }
 
 // aligned.csv (sam2aln.py:459-478): per rname in first-seen order, the
 // distinct merged sequences sorted by (count, gap prefix, sequence), all
 // descending; seq written without its leading / trailing gaps
-static void s2a_aligned(const S2AState &S, std::string &out)
+static void s2a_aligned(const S2AState &S, Pieces &out)
 {
     const int nt = s2a_threads();
-    out = "refname,qcut,rank,count,offset,seq\n";
+    out.assign(1, "refname,qcut,rank,count,offset,seq\n");
     const int nn = (int)S.names.size();
     std::vector<int32_t> mref(S.n_merge);
     for (int64_t u = 0; u < (int64_t)S.u1.size(); ++u)
@@ -511,9 +548,9 @@ static void s2a_aligned(const S2AState &S, std::string &out)
 
 // insert.csv rows of parse_sam (sam2aln.py:357-380): every I op of the
 // mates of a unit that reached apply_cigar, at pos - 1 + read offset
-static void s2a_inserts(const S2AState &S, std::string &out)
+static void s2a_inserts(const S2AState &S, Pieces &out)
 {
-    out = "qname,fwd_rev,refname,pos,insert,qual\n";
+    out.assign(1, "qname,fwd_rev,refname,pos,insert,qual\n");
     parallel_text((int64_t)S.u1.size(), s2a_threads(), out, [&](std::string &o, int64_t a, int64_t b) {
         for (int64_t u = a; u < b; ++u) {
             if (S.ucause[u] >= 0) continue;
@@ -544,9 +581,9 @@ static void s2a_inserts(const S2AState &S, std::string &out)
     });
 }
 
-static void s2a_failed(const S2AState &S, std::string &out)
+static void s2a_failed(const S2AState &S, Pieces &out)
 {
-    out = "qname,cause\n";
+    out.assign(1, "qname,cause\n");
     parallel_text((int64_t)S.u1.size(), s2a_threads(), out, [&](std::string &o, int64_t a, int64_t b) {
         for (int64_t u = a; u < b; ++u) {
             int cause = S.ucause[u];
@@ -561,7 +598,7 @@ static void s2a_failed(const S2AState &S, std::string &out)
     });
 }
 
-int s2a_format(const S2AState &S, int which, std::string &out)
+int s2a_format(const S2AState &S, int which, std::vector<std::string> &out)
 {
     if (which == 0) s2a_aligned(S, out);
     else if (which == 1) s2a_inserts(S, out);

@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "mh_gunzip.h"
 #include "mh_internal.h"
 
 namespace mh {
@@ -22,10 +23,10 @@ enum { CIG_OK = 0, CIG_STAR = 1, CIG_INVALID = 2, CIG_UNSUPPORTED = 3, CIG_LONG 
 struct S2AState {
     // ---- rows of the last remap.csv (host) ----
     int64_t n_rows = 0;
-    std::string qpool;                  // qnames back to back
+    TextBuf qpool;                      // qnames back to back (not zero-filled)
     std::vector<int64_t> qoff;
     std::vector<int32_t> qlen;
-    std::string cpool;                  // CIGAR texts (for error messages)
+    TextBuf cpool;                      // CIGAR texts (for error messages)
     std::vector<int64_t> coff;
     std::vector<int32_t> clen;
     std::vector<int8_t> cstate;         // CIG_*
@@ -33,7 +34,7 @@ struct S2AState {
     std::vector<std::string> rnames;
     std::vector<int32_t> flag, pos;     // pos INT32_MIN: not an integer
     std::vector<uint8_t> qshort;        // qual shorter than seq
-    std::string seq, qual;              // concatenated, qual padded to seq length
+    TextBuf seq, qual;                  // concatenated, qual padded to seq length
     std::vector<int64_t> soff;
     std::vector<int32_t> slen;
     std::vector<int32_t> cig_off, n_cig;
@@ -61,7 +62,7 @@ struct S2AState {
     std::vector<int64_t> uniq_off;      // offsets into gathered
     std::string gathered;               // bodies of the distinct sequences
     // ---- formatted outputs (cached between the size query and the copy) ----
-    std::string out_cache[3];
+    std::vector<std::string> out_cache[3];   // the text as pieces, in order
     int out_valid = 0;
     // ---- host timings of the last call (ms) ----
     double t_parse = 0, t_device = 0, t_format[3] = {0, 0, 0};
@@ -69,7 +70,7 @@ struct S2AState {
 
 // host half
 int s2a_parse(S2AState &S, const char *text, int64_t len);
-int s2a_format(const S2AState &S, int which, std::string &out);
+int s2a_format(const S2AState &S, int which, std::vector<std::string> &out);
 int s2a_threads();
 // device half
 int s2a_run(Ctx &c, S2AState &S, double max_prop_n);

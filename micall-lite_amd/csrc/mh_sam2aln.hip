@@ -18,9 +18,17 @@
 //   k_s2a_gather  distinct sequences copied out for the host's sort
 // Bit-for-bit specification: the reference itself (tests/golden/e2e/*/aligned.csv
 // etc. were produced by running micall.core.sam2aln on the same remap.csv).
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mh_sam2aln.h"
@@ -399,7 +407,8 @@ static int s2a_upload(T *&dst, const std::vector<T> &v, hipStream_t s)
     return 0;
 }
 
-static int s2a_upload_bytes(uint8_t *&dst, const std::string &v, hipStream_t s)
+template <class Bytes>
+static int s2a_upload_bytes(uint8_t *&dst, const Bytes &v, hipStream_t s)
 {
     hipFree(dst);
     dst = nullptr;
@@ -577,7 +586,7 @@ extern "C" int mh_sam2aln_csv(mh_ctx *ctx, const char *text, int64_t len, int q_
     S.q_cutoff = q_cutoff;
     S.n_merge = S.n_unique = 0;
     S.res.clear();
-    for (auto &o : S.out_cache) o.clear();
+    for (auto &o : S.out_cache) std::vector<std::string>().swap(o);
     S.out_valid = 0;
     auto t0 = std::chrono::steady_clock::now();
     if (int st = s2a_parse(S, text ? text : "", len)) {
@@ -596,13 +605,68 @@ extern "C" int mh_sam2aln_csv(mh_ctx *ctx, const char *text, int64_t len, int q_
     return 0;
 }
 
+extern "C" int mh_sam2aln_file(mh_ctx *ctx, int fd, int q_cutoff, double max_prop_n, int64_t *n_units)
+{
+    if (!ctx || fd < 0) return -3;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) { set_error("mh_sam2aln_file: not a regular file"); return -3; }
+    const size_t len = (size_t)st.st_size;
+    void *m = nullptr;
+    if (len > 0) {
+        m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) { set_error("mh_sam2aln_file: mmap failed (%s)", strerror(errno)); return -3; }
+    }
+    const char *text = (const char *)m;
+    // text-mode reads turn "\r\n" and "\r" into "\n": such a file goes through
+    // the caller's own read instead.  (The scan runs on every parse thread,
+    // which also faults the mapping in in parallel.)
+    if (len) {
+        const int nt = std::max(1, std::min<int>(s2a_threads(), (int)(len >> 20) + 1));
+        std::vector<char> cr((size_t)nt, 0);
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t]() {
+                const size_t a = len * (size_t)t / (size_t)nt, b = len * (size_t)(t + 1) / (size_t)nt;
+                cr[(size_t)t] = memchr(text + a, '\r', b - a) != nullptr;
+            });
+        for (auto &x : th) x.join();
+        for (char c : cr)
+            if (c) { munmap(m, len); return 1; }
+    }
+    const int rc = mh_sam2aln_csv(ctx, text, (int64_t)len, q_cutoff, max_prop_n, n_units);
+    if (m) munmap(m, len);
+    return rc;
+}
+
+extern "C" int mh_sam2aln_write(mh_ctx *ctx, int which, int fd, int64_t offset, int64_t *written)
+{
+    size_t used = 0;
+    if (int st = mh_sam2aln_output(ctx, which, nullptr, 0, &used)) return st;
+    if (fd < 0 || offset < 0) return -3;
+    S2AState &S = *ctx_of(ctx)->s2a;
+    int64_t pos = offset;
+    for (const std::string &piece : S.out_cache[which]) {
+        const char *p = piece.data();
+        size_t left = piece.size();
+        while (left > 0) {
+            const ssize_t w = pwrite(fd, p, left, (off_t)pos);
+            if (w <= 0) { set_error("mh_sam2aln_write: write failed (%s)", strerror(errno ? errno : EIO)); return -4; }
+            p += w; left -= (size_t)w; pos += w;
+        }
+    }
+    if (written) *written = pos - offset;
+    std::vector<std::string>().swap(S.out_cache[which]);
+    S.out_valid &= ~(1 << which);
+    return 0;
+}
+
 extern "C" int mh_sam2aln_output(mh_ctx *ctx, int which, char *buf, size_t cap, size_t *used)
 {
     if (!ctx || which < 0 || which > 2 || !used) return -3;
     Ctx &c = *ctx_of(ctx);
     if (!c.s2a) { set_error("mh_sam2aln_output: no sam2aln results"); return -3; }
     S2AState &S = *c.s2a;
-    std::string &out = S.out_cache[which];
+    std::vector<std::string> &out = S.out_cache[which];
     if (!(S.out_valid & (1 << which))) {
         auto t0 = std::chrono::steady_clock::now();
         s2a_format(S, which, out);
@@ -610,11 +674,13 @@ extern "C" int mh_sam2aln_output(mh_ctx *ctx, int which, char *buf, size_t cap, 
                                 std::chrono::steady_clock::now() - t0).count();
         S.out_valid |= 1 << which;
     }
-    *used = out.size();
+    size_t total = 0;
+    for (const std::string &p : out) total += p.size();
+    *used = total;
     if (!buf) return 0;
-    if (cap < out.size()) { set_error("mh_sam2aln_output: buffer too small"); return -2; }
-    memcpy(buf, out.data(), out.size());
-    std::string().swap(out);          // handed over: free the cached text
+    if (cap < total) { set_error("mh_sam2aln_output: buffer too small"); return -2; }
+    for (const std::string &p : out) { memcpy(buf, p.data(), p.size()); buf += p.size(); }
+    std::vector<std::string>().swap(out);   // handed over: free the cached text
     S.out_valid &= ~(1 << which);
     return 0;
 }

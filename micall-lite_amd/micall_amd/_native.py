@@ -116,6 +116,8 @@ def _declare(L):
                             _I64P], ctypes.c_int),
         'mh_sam2aln_output': ([_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
                                ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        'mh_sam2aln_file': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_double, _I64P], ctypes.c_int),
+        'mh_sam2aln_write': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _I64P], ctypes.c_int),
         'mh_sam2aln_stats': ([_P, _P], ctypes.c_int),
         'mh_sam2aln_timing': ([_P, _P], ctypes.c_int),
         'mh_censor_fastq': ([_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
@@ -253,6 +255,31 @@ class Context:
         n = ctypes.c_int64()
         check(lib().mh_sam2aln_csv(self.h, data, len(data), int(q_cutoff), float(max_prop_n),
                                    ctypes.byref(n)), 'mh_sam2aln_csv')
+        return n.value
+
+    def sam2aln_file(self, fd, q_cutoff=15, max_prop_n=0.5):
+        """mh_sam2aln_file on the whole regular file fd (mmap'd): the number of
+        matchmaker pairs, or None when the file holds '\r' (read it in text
+        mode and use sam2aln_csv)."""
+        n = ctypes.c_int64()
+        st = lib().mh_sam2aln_file(self.h, int(fd), int(q_cutoff), float(max_prop_n), ctypes.byref(n))
+        if st == 1:
+            return None
+        check(st, 'mh_sam2aln_file')
+        return n.value
+
+    def sam2aln_size(self, which):
+        """Bytes of output 'aligned' | 'insert' | 'failed' (formats it)."""
+        w = {'aligned': 0, 'insert': 1, 'failed': 2}[which]
+        used = ctypes.c_size_t()
+        check(lib().mh_sam2aln_output(self.h, w, None, 0, ctypes.byref(used)), 'mh_sam2aln_output')
+        return used.value
+
+    def sam2aln_write(self, which, fd, offset):
+        """Output `which` written to fd at offset (pwrite); bytes written."""
+        w = {'aligned': 0, 'insert': 1, 'failed': 2}[which]
+        n = ctypes.c_int64()
+        check(lib().mh_sam2aln_write(self.h, w, int(fd), int(offset), ctypes.byref(n)), 'mh_sam2aln_write')
         return n.value
 
     def sam2aln_output(self, which):

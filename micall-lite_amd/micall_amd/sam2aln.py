@@ -27,14 +27,31 @@ def sam2aln(remap_csv, aligned_csv, insert_csv=None, failed_csv=None, nthreads=N
     with session.writer_stage(aligned_csv, insert_csv, failed_csv) as stage:
         if not stage.active:
             return
-        text = session.read_text(remap_csv)
         ctx = session.context()
-        ctx.sam2aln_csv(text, q_cutoff=SAM2ALN_Q_CUTOFFS[0], max_prop_n=MAX_PROP_N)
-        if insert_csv:
-            insert_csv.write(ctx.sam2aln_output('insert'))
-        if failed_csv:
-            failed_csv.write(ctx.sam2aln_output('failed'))
-        aligned_csv.write(ctx.sam2aln_output('aligned'))
+        fd = session.readable_fd(remap_csv)
+        done = None
+        if fd is not None:   # the file mmap'd by the library (no '\r' in it)
+            done = ctx.sam2aln_file(fd, q_cutoff=SAM2ALN_Q_CUTOFFS[0], max_prop_n=MAX_PROP_N)
+            if done is not None:
+                remap_csv.seek(0, 2)     # consumed, as the reference's DictReader leaves it
+        if done is None:
+            text = session.read_text(remap_csv)
+            ctx.sam2aln_csv(text, q_cutoff=SAM2ALN_Q_CUTOFFS[0], max_prop_n=MAX_PROP_N)
+        for which, handle in (('insert', insert_csv), ('failed', failed_csv), ('aligned', aligned_csv)):
+            if handle:
+                _write_output(ctx, which, handle)
+
+
+def _write_output(ctx, which, handle):
+    """One output: written by the library at the handle's position when it is
+    a plain file (pwrite), else through the handle."""
+    from .sharded_io import SharedOutput
+    out = SharedOutput(None, handle)
+    if out.direct:
+        ctx.sam2aln_write(which, out.fd, int(out.place([ctx.sam2aln_size(which)])[0]))
+        out.finish()
+    else:
+        handle.write(ctx.sam2aln_output(which))
 
 
 def parseArgs():

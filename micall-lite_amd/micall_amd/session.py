@@ -172,6 +172,25 @@ def read_text(handle):
     return handle.read()
 
 
+def readable_fd(handle):
+    """The descriptor of an open text file whose whole content the native
+    parsers may read straight from the file: nothing read from it yet,
+    UTF-8 / ASCII, a regular file (what read_text would hand over as raw
+    bytes); else None."""
+    import stat
+    raw = getattr(handle, 'buffer', None)
+    enc = (getattr(handle, 'encoding', '') or '').lower().replace('-', '')
+    if raw is None or enc not in ('utf8', 'ascii') or getattr(handle, 'newlines', None) is not None:
+        return None
+    try:
+        if handle.tell() != 0:
+            return None
+        fd = handle.fileno()
+        return fd if stat.S_ISREG(os.fstat(fd).st_mode) else None
+    except (OSError, ValueError, AttributeError):
+        return None
+
+
 def write_bytes(handle, data):
     """Write ASCII bytes to an open text file (through its binary buffer when
     it is a UTF-8 / ASCII file that writes '\n' as is), or to a binary one."""
