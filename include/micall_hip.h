@@ -396,6 +396,9 @@ int mh_censor_timing(mh_ctx *ctx, double *ms3);
  * 0..2^28 and counts outside 0..2^32-1.  *n_groups = number of groups. */
 int mh_a2c_load_csv(mh_ctx *ctx, int slot, const char *text, int64_t len,
                     const char *codon_chars, int64_t *n_groups);
+/* mh_a2c_load_csv on the whole of a regular file (fd, mmap'd): 0, or 1 when
+ * the file holds '\r' (the caller reads it in text mode instead). */
+int mh_a2c_load_file(mh_ctx *ctx, int slot, int fd, const char *codon_chars, int64_t *n_groups);
 /* The same from rows in memory: row r's seq is pool[seq_off[r] ..
  * seq_off[r] + seq_len[r]); group g = rows group_first[g] ..
  * group_first[g + 1] - 1 (group names are empty). */
@@ -422,6 +425,12 @@ int mh_a2c_inserts(mh_ctx *ctx, int slot, int64_t g, int frame, int n_ranges,
                    const int32_t *left, const int32_t *right, int64_t *n_entries);
 int mh_a2c_insert_entries(mh_ctx *ctx, int slot, int32_t *range, int64_t *count,
                           uint32_t *first, char *aminos, size_t cap, size_t *used);
+/* The insertion report rows (aln2counts InsertionWriter.write) of the last
+ * mh_a2c_inserts: per entry, lead + (left[range] + 1) + ',' + its amino-acid
+ * string + ',' + its count + ',' + target[range] (blank for INT32_MIN) +
+ * eol.  buf NULL: formats and sets *used; then copies into buf. */
+int mh_a2c_insert_rows(mh_ctx *ctx, int slot, const char *lead, int n_ranges, const int32_t *left,
+                       const int32_t *target, const char *eol, char *buf, size_t cap, size_t *used);
 /* Host wall ms: [0] parse of the last load, [1] its upload + k_a2c_count +
  * fetch, [2] mh_a2c_inserts since the last call of this function. */
 int mh_a2c_timing(mh_ctx *ctx, int slot, double *ms3);

@@ -40,6 +40,7 @@
 #include <thread>
 #include <vector>
 
+#include "mh_gunzip.h"
 #include "mh_internal.h"
 #include "mh_sam2aln.h"
 #include "mh_text.h"
@@ -104,6 +105,7 @@ struct A2CState {
     // insertion strings of the last mh_a2c_inserts, in (range, first row) order
     std::vector<A2CEntry> entries;
     std::string aminos;                       // one line per entry
+    std::string ins_rows;                     // mh_a2c_insert_rows text (size query, then copy)
     double t_parse = 0, t_count = 0, t_ins = 0;
 };
 
@@ -756,6 +758,17 @@ extern "C" int mh_a2c_load_csv(mh_ctx *ctx, int slot, const char *text, int64_t 
     return 0;
 }
 
+extern "C" int mh_a2c_load_file(mh_ctx *ctx, int slot, int fd, const char *codon_chars, int64_t *n_groups)
+{
+    if (!ctx || fd < 0) return -3;
+    const char *text = nullptr;
+    size_t len = 0;
+    if (int st = map_text_file(fd, &text, &len)) return st;
+    const int rc = mh_a2c_load_csv(ctx, slot, text, (int64_t)len, codon_chars, n_groups);
+    unmap_text_file(text, len);
+    return rc;
+}
+
 extern "C" int mh_a2c_load_rows(mh_ctx *ctx, int slot, int64_t n_rows, const char *pool,
                                 int64_t pool_len, const int64_t *seq_off, const int32_t *seq_len,
                                 const int64_t *offset, const int64_t *count, int64_t n_groups,
@@ -1015,6 +1028,54 @@ extern "C" int mh_a2c_insert_entries(mh_ctx *ctx, int slot, int32_t *range, int6
         if (cap < S.aminos.size()) { set_error("mh_a2c_insert_entries: buffer too small"); return -2; }
         memcpy(aminos, S.aminos.data(), S.aminos.size());
     }
+    return 0;
+}
+
+extern "C" int mh_a2c_insert_rows(mh_ctx *ctx, int slot, const char *lead, int n_ranges,
+                                  const int32_t *left, const int32_t *target, const char *eol,
+                                  char *buf, size_t cap, size_t *used)
+{
+    if (!ctx || slot < 0 || slot >= A2C_SLOTS || !lead || !eol || !used || n_ranges < 0 ||
+        (n_ranges && (!left || !target)))
+        return -3;
+    Ctx &c = *ctx_of(ctx);
+    A2CState &S = *a2c_state(c, slot);
+    if (!buf) {
+        // InsertionWriter.write's rows: lead, left codon + 1, the amino-acid
+        // string, its count, the coordinate position (blank when none)
+        std::string &o = S.ins_rows;
+        o.clear();
+        const size_t ll = strlen(lead), el = strlen(eol);
+        o.reserve(S.entries.size() * (ll + el + 24) + S.aminos.size());
+        const char *am = S.aminos.data(), *am_end = am + S.aminos.size();
+        char num[24];
+        auto put = [&](long long v) {
+            auto r = std::to_chars(num, num + sizeof num, v);
+            o.append(num, (size_t)(r.ptr - num));
+        };
+        for (size_t k = 0; k < S.entries.size(); ++k) {
+            const char *nl = (const char *)memchr(am, '\n', (size_t)(am_end - am));
+            if (!nl) { set_error("mh_a2c_insert_rows: entry strings out of step"); return -3; }
+            const int r = S.entries[k].range;
+            if (r < 0 || r >= n_ranges) { set_error("mh_a2c_insert_rows: range %d out of %d", r, n_ranges); return -3; }
+            o.append(lead, ll);
+            put((long long)left[r] + 1);
+            o.push_back(',');
+            o.append(am, (size_t)(nl - am));
+            o.push_back(',');
+            put((long long)S.entries[k].count);
+            o.push_back(',');
+            if (target[r] != INT32_MIN) put(target[r]);
+            o.append(eol, el);
+            am = nl + 1;
+        }
+        *used = o.size();
+        return 0;
+    }
+    *used = S.ins_rows.size();
+    if (cap < S.ins_rows.size()) { set_error("mh_a2c_insert_rows: buffer too small"); return -2; }
+    memcpy(buf, S.ins_rows.data(), S.ins_rows.size());
+    std::string().swap(S.ins_rows);
     return 0;
 }
 

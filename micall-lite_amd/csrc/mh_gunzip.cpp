@@ -5,6 +5,8 @@
 // used when present; zlib otherwise.  Host code only.
 #include <dlfcn.h>
 #include <sys/mman.h>
+#include <cerrno>
+#include <sys/stat.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -20,6 +22,9 @@
 #include "mh_gunzip.h"
 
 namespace mh {
+
+void set_error(const char *fmt, ...);   // mh_api.cpp
+int gunzip_threads();
 
 namespace {
 
@@ -305,6 +310,38 @@ void big_free(char *p, size_t n)
 }
 
 bool gunzip_fast_available() { return ld_api().ok; }
+
+int map_text_file(int fd, const char **text, size_t *len)
+{
+    *text = nullptr;
+    *len = 0;
+    struct stat st;
+    if (fd < 0 || fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
+        set_error("map_text_file: not a regular file");
+        return -3;
+    }
+    const size_t n = (size_t)st.st_size;
+    if (n == 0) return 0;
+    void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (m == MAP_FAILED) { set_error("map_text_file: mmap failed (%s)", strerror(errno)); return -3; }
+    const char *t = (const char *)m;
+    const int nt = std::max(1, std::min<int>(gunzip_threads(), (int)(n >> 20) + 1));
+    std::vector<char> cr((size_t)nt, 0);
+    run_threads(nt, [&](int k) {
+        const size_t a = n * (size_t)k / (size_t)nt, b = n * (size_t)(k + 1) / (size_t)nt;
+        cr[(size_t)k] = memchr(t + a, '\r', b - a) != nullptr;
+    });
+    for (char c : cr)
+        if (c) { munmap(m, n); return 1; }
+    *text = t;
+    *len = n;
+    return 0;
+}
+
+void unmap_text_file(const char *text, size_t len)
+{
+    if (text && len) munmap((void *)text, len);
+}
 
 uint32_t crc32_update(uint32_t crc, const void *p, size_t n)
 {

@@ -73,6 +73,13 @@ bool gunzip_fast_available();
 // 0, or -2 when compression fails.
 int gzip_member(const char *src, size_t len, std::string &out, int level);
 int gzip_member(const char *src, size_t len, TextBuf &out, int level);
+// The whole regular file fd mapped read-only for a native parser: 0, 1
+// when it holds '\r' (a text-mode read would translate it: the caller reads
+// it itself; nothing stays mapped), or -3 (error set).  The '\r' scan runs
+// on many threads, which also faults the mapping in in parallel.
+int map_text_file(int fd, const char **text, size_t *len);
+void unmap_text_file(const char *text, size_t len);
+
 // One gzip member (the whole of src) inflated by `threads` host threads
 // (mh_pinflate.cpp); -1 when it cannot be (the caller inflates serially).
 template <class Buf>

@@ -31,6 +31,7 @@
 #include <thread>
 #include <vector>
 
+#include "mh_gunzip.h"
 #include "mh_sam2aln.h"
 
 namespace mh {
@@ -608,33 +609,11 @@ extern "C" int mh_sam2aln_csv(mh_ctx *ctx, const char *text, int64_t len, int q_
 extern "C" int mh_sam2aln_file(mh_ctx *ctx, int fd, int q_cutoff, double max_prop_n, int64_t *n_units)
 {
     if (!ctx || fd < 0) return -3;
-    struct stat st;
-    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) { set_error("mh_sam2aln_file: not a regular file"); return -3; }
-    const size_t len = (size_t)st.st_size;
-    void *m = nullptr;
-    if (len > 0) {
-        m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE, fd, 0);
-        if (m == MAP_FAILED) { set_error("mh_sam2aln_file: mmap failed (%s)", strerror(errno)); return -3; }
-    }
-    const char *text = (const char *)m;
-    // text-mode reads turn "\r\n" and "\r" into "\n": such a file goes through
-    // the caller's own read instead.  (The scan runs on every parse thread,
-    // which also faults the mapping in in parallel.)
-    if (len) {
-        const int nt = std::max(1, std::min<int>(s2a_threads(), (int)(len >> 20) + 1));
-        std::vector<char> cr((size_t)nt, 0);
-        std::vector<std::thread> th;
-        for (int t = 0; t < nt; ++t)
-            th.emplace_back([&, t]() {
-                const size_t a = len * (size_t)t / (size_t)nt, b = len * (size_t)(t + 1) / (size_t)nt;
-                cr[(size_t)t] = memchr(text + a, '\r', b - a) != nullptr;
-            });
-        for (auto &x : th) x.join();
-        for (char c : cr)
-            if (c) { munmap(m, len); return 1; }
-    }
+    const char *text = nullptr;
+    size_t len = 0;
+    if (int st = map_text_file(fd, &text, &len)) return st;
     const int rc = mh_sam2aln_csv(ctx, text, (int64_t)len, q_cutoff, max_prop_n, n_units);
-    if (m) munmap(m, len);
+    unmap_text_file(text, len);
     return rc;
 }
 

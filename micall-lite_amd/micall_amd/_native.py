@@ -129,6 +129,10 @@ def _declare(L):
                               ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         'mh_censor_write': ([_P, ctypes.c_int, ctypes.c_int64, _I64P], ctypes.c_int),
         'mh_censor_timing': ([_P, _P], ctypes.c_int),
+        'mh_a2c_load_file': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _I64P], ctypes.c_int),
+        'mh_a2c_insert_rows': ([_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, _P, _P, ctypes.c_char_p,
+                                ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)],
+                               ctypes.c_int),
         'mh_a2c_load_csv': ([_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p,
                              _I64P], ctypes.c_int),
         'mh_a2c_load_rows': ([_P, ctypes.c_int, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64,
@@ -351,6 +355,34 @@ class Context:
         check(lib().mh_a2c_load_csv(self.h, slot, data, len(data), codon_chars, ctypes.byref(n)),
               'mh_a2c_load_csv')
         return n.value
+
+    def a2c_load_file(self, slot, fd, codon_chars):
+        """mh_a2c_load_file on the whole regular file fd (mmap'd): number of
+        groups, or None when it holds '\r' (read it in text mode instead)."""
+        n = ctypes.c_int64()
+        st = lib().mh_a2c_load_file(self.h, slot, int(fd), codon_chars, ctypes.byref(n))
+        if st == 1:
+            return None
+        check(st, 'mh_a2c_load_file')
+        return n.value
+
+    def a2c_inserts_text(self, slot, g, frame, lefts, rights, lead, targets, eol):
+        """mh_a2c_inserts then mh_a2c_insert_rows: the insertion report rows
+        as text ('' when there are none)."""
+        lo = np.array(list(lefts) or [0], dtype=np.int32)
+        hi = np.array(list(rights) or [0], dtype=np.int32)
+        n = ctypes.c_int64()
+        check(lib().mh_a2c_inserts(self.h, slot, g, frame, len(lefts), _ptr(lo), _ptr(hi),
+                                   ctypes.byref(n)), 'mh_a2c_inserts')
+        if n.value == 0:
+            return ''
+        tg = np.array([INT32_MIN if t is None else t for t in targets] or [0], dtype=np.int32)
+        used = ctypes.c_size_t()
+        args = (self.h, slot, lead.encode(), len(lefts), _ptr(lo), _ptr(tg), eol.encode())
+        check(lib().mh_a2c_insert_rows(*args, None, 0, ctypes.byref(used)), 'mh_a2c_insert_rows')
+        buf = ctypes.create_string_buffer(max(used.value, 1))
+        check(lib().mh_a2c_insert_rows(*args, buf, len(buf), ctypes.byref(used)), 'mh_a2c_insert_rows')
+        return buf.raw[:used.value].decode()
 
     def a2c_load_rows(self, slot, seqs, offsets, counts, group_first, codon_chars):
         """mh_a2c_load_rows from lists: seq strings, offsets, counts and the

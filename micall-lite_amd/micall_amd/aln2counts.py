@@ -669,26 +669,25 @@ class InsertionWriter(object):
         """The reads of this run are run g of the device table `slot`."""
         self._source = (ctx, slot, g)
 
-    def _count(self, ranges, reading_frame):
-        """[(range number, count, first row, amino-acid string)] on the device."""
-        source = self._source
-        if source is None:
-            if not self.nuc_seqs:
-                return []
-            reads = list(self.nuc_seqs)
-            ctx = session.context()
-            ctx.a2c_load_rows(SLOT_INSERTS, reads, [0] * len(reads),
-                              [self.nuc_seqs[r] for r in reads], [0, len(reads)], _CODON_CHARS)
-            source = (ctx, SLOT_INSERTS, 0)
-        ctx, slot, g = source
-        return ctx.a2c_inserts(slot, g, reading_frame, [r[0] for r in ranges],
-                               [r[1] for r in ranges])
+    def _source_of(self):
+        """(ctx, slot, group) of the reads to count insertions over."""
+        if self._source is not None:
+            return self._source
+        if not self.nuc_seqs:
+            return None
+        reads = list(self.nuc_seqs)
+        ctx = session.context()
+        ctx.a2c_load_rows(SLOT_INSERTS, reads, [0] * len(reads),
+                          [self.nuc_seqs[r] for r in reads], [0, len(reads)], _CODON_CHARS)
+        return ctx, SLOT_INSERTS, 0
 
     def write(self, inserts, region, reading_frame=0, report_aminos=()):
         """Rows for each run of inserted consensus codons: the 1-based left
         codon, each amino-acid string with its count, and the coordinate
         position the run precedes.  Runs placed before coordinate position 1
-        or past the end are skipped when report_aminos is given."""
+        or past the end are skipped when report_aminos is given.  The strings
+        are counted and the rows formatted by the library (mh_a2c_inserts,
+        mh_a2c_insert_rows)."""
         if len(inserts) == 0:
             return
         before = {}
@@ -702,21 +701,18 @@ class InsertionWriter(object):
                 if not report_aminos or target.get(r[0]) not in (1, None)]
         if not kept:
             return
-        found = self._count(kept, reading_frame)
-        if not found:
+        source = self._source_of()
+        if source is None:
             return
         # the leading text columns go through the csv module (quoting); the
         # rest are numbers and amino-acid letters, which never need quotes
         lead = io.StringIO()
         csv.writer(lead, lineterminator='').writerow([self.seed, region, self.qcut, ''])
-        lead = lead.getvalue()
-        rows = []
-        for k, count, _first, aminos in found:
-            left = kept[k][0]
-            pos = target.get(left)
-            rows.append('%s%d,%s,%d,%s%s' % (lead, left + 1, aminos, count,
-                                             '' if pos is None else pos, os.linesep))
-        self._file.write(''.join(rows))
+        ctx, slot, g = source
+        text = ctx.a2c_inserts_text(slot, g, reading_frame, [r[0] for r in kept], [r[1] for r in kept],
+                                    lead.getvalue(), [target.get(r[0]) for r in kept], os.linesep)
+        if text:
+            self._file.write(text)
 
 
 def format_cutoff(cutoff):
@@ -766,7 +762,15 @@ def _aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv, fail
     if source:
         report.enable_callback(callback, os.stat(source).st_size)
     ctx = session.context()
-    for g in range(ctx.a2c_load_csv(SLOT_REPORT, session.read_text(aligned_csv), _CODON_CHARS)):
+    fd = session.readable_fd(aligned_csv)
+    groups = None
+    if fd is not None:   # the file mmap'd by the library (no '\r' in it)
+        groups = ctx.a2c_load_file(SLOT_REPORT, fd, _CODON_CHARS)
+        if groups is not None:
+            aligned_csv.seek(0, 2)
+    if groups is None:
+        groups = ctx.a2c_load_csv(SLOT_REPORT, session.read_text(aligned_csv), _CODON_CHARS)
+    for g in range(groups):
         report._read_group(ctx, SLOT_REPORT, g)
         for step in per_run:
             step()
