@@ -693,6 +693,104 @@ def bench_aln2counts(args):
     print(json.dumps(out))
 
 
+def bench_chain(args):
+    """bin/micall's per-sample chain (bin/micall:116-188) file to file with
+    the drop-ins, on the C2 input as a raw MiSeq pair arrives (each FASTQ one
+    gzip member): censor R1, censor R2 (2 % bad tile-cycles) -> prelim_map
+    -> remap -> sam2aln -> aln2counts, every output to a file.  One line:
+    reads/s through the whole chain and seconds per stage."""
+    import csv
+    import io
+    import shutil
+    import tempfile
+    import random
+    from micall_amd import (aln2counts, censor_fastq, prelim_map, remap, sam2aln, session, synth)
+    work = tempfile.mkdtemp(prefix='bench_chain_')
+    r1, r2 = os.path.join(work, 'R1.fastq.gz'), os.path.join(work, 'R2.fastq.gz')
+    pairs = synth.make_pairs(args.pairs, genomes=bench_genomes('pol'), genome_seed=SEED,
+                             read_seed=SEED, block=0)
+    write_fastq_gz(pairs, r1, r2, single=True)
+    del pairs
+    rng = random.Random(SEED)
+    bad = [{'tile': str(1101 + t), 'cycle': str(sign * c)} for t in range(8) for sign in (1, -1)
+           for c in range(1, READ_LEN + 1) if rng.random() < 0.02]
+    P = {k: os.path.join(work, k) for k in ('c1.fastq.gz', 'c2.fastq.gz', 'prelim.csv', 'remap.csv',
+                                            'align.csv', 'nuc.csv', 'amino.csv', 'insert.csv',
+                                            'conseq.csv', 'remap_counts.csv')}
+
+    lib = {}
+    gap = float(os.environ.get('MICALL_CHAIN_GAP_S', '0'))   # diagnostics: idle seconds between stages
+
+    def run():
+        times = {}
+        t = time.perf_counter()
+        for src, dst in ((r1, P['c1.fastq.gz']), (r2, P['c2.fastq.gz'])):
+            with open(src, 'rb') as f, open(dst, 'wb') as g:
+                censor_fastq.censor(f, iter(bad), g, use_gzip=True)
+        times['censor'] = time.perf_counter() - t
+        time.sleep(gap)
+        t = time.perf_counter()
+        session.context().phase_times(reset=True)
+        with open(P['prelim.csv'], 'w') as f:
+            prelim_map.prelim_map(P['c1.fastq.gz'], P['c2.fastq.gz'], f, gzip=True)
+        times['prelim_map'] = time.perf_counter() - t
+        time.sleep(gap)
+        lib['prelim_map'] = {k: round(v / 1e3, 4) for k, v in session.context().phase_times(reset=True).items()}
+        t = time.perf_counter()
+        with open(P['prelim.csv']) as pre, open(P['remap.csv'], 'w') as out, \
+                open(P['remap_counts.csv'], 'w') as counts:
+            remap.remap(P['c1.fastq.gz'], P['c2.fastq.gz'], pre, out, counts, gzip=True)
+        times['remap'] = time.perf_counter() - t
+        time.sleep(gap)
+        lib['remap'] = {k: round(v / 1e3, 4) for k, v in session.context().phase_times(reset=True).items()}
+        lib['prelim_source'] = session.stats.get('prelim_source')
+        t = time.perf_counter()
+        with open(P['remap.csv']) as rc, open(P['align.csv'], 'w') as al:
+            sam2aln.sam2aln(rc, al)
+        times['sam2aln'] = time.perf_counter() - t
+        time.sleep(gap)
+        t = time.perf_counter()
+        with open(P['align.csv']) as al, open(P['nuc.csv'], 'w') as nuc, \
+                open(P['amino.csv'], 'w') as amino, open(P['insert.csv'], 'w') as ins, \
+                open(P['conseq.csv'], 'w') as conseq:
+            aln2counts.aln2counts(al, nuc, amino, ins, conseq)
+        times['aln2counts'] = time.perf_counter() - t
+        return times
+
+    for _ in range(args.warmup):
+        run()
+    runs = [run() for _ in range(max(args.steps, 1))]
+    if os.environ.get('MICALL_CHAIN_PROFILE'):   # diagnostics: cProfile of one more run to stderr
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        run()
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats('cumulative').print_stats(60)
+    best = min(runs, key=lambda r: sum(r.values()))
+    total = sum(best.values())
+    sizes = {k: os.path.getsize(v) for k, v in P.items()}
+    sizes['R1.fastq.gz'], sizes['R2.fastq.gz'] = os.path.getsize(r1), os.path.getsize(r2)
+    shutil.rmtree(work, ignore_errors=True)
+    out = {
+        'metric': 'bin/micall per-sample chain reads/sec (raw FASTQ.gz pair -> nuc/amino/conseq)',
+        'value': round(2 * args.pairs / total, 1), 'unit': 'reads/s', 'n_gpus': 1,
+        'steps': len(runs), 'warmup': args.warmup, 'ms_per_step': round(1e3 * total, 1),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8',
+        'data': 'synthetic',
+        'config': {'workload': 'C2 input (1M synthetic 2x251 HIV-1 pol pairs), each FASTQ one gzip '
+                               'member; 2 % bad tile-cycles; censor R1 + R2, prelim_map, remap, '
+                               'sam2aln, aln2counts, drop-ins file to file',
+                   'pairs': args.pairs, 'bad_cycles': len(bad)},
+        'stages_s': {k: round(v, 3) for k, v in best.items()},
+        'all_runs_s': [round(sum(r.values()), 3) for r in runs],
+        'library_phases_s_last_run': lib,
+        'bytes': sizes,
+    }
+    print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split('\n\n')[0])
     ap.add_argument('--gpus', type=int, default=1)
@@ -723,7 +821,7 @@ def main():
                          '(as a parallel gzip writes it) or one member (as bcl2fastq does)')
     ap.add_argument('--breakdown', action='store_true',
                     help='time each pipeline stage (synchronising) and print it to stderr')
-    ap.add_argument('--stage', choices=('remap', 'sam2aln', 'censor', 'aln2counts'), default='remap',
+    ap.add_argument('--stage', choices=('remap', 'sam2aln', 'censor', 'aln2counts', 'chain'), default='remap',
                     help='remap: the headline hot path (default); sam2aln: the next stage '
                          '(SURVEY.md 8(f)) over the remap.csv of one C2 pass; censor: the '
                          'stage before (FASTQ censor of the C2 reads) plus the FASTQ ingest')
@@ -734,6 +832,8 @@ def main():
         return bench_aln2counts(args)
     if args.stage == 'censor':
         return bench_censor(args)
+    if args.stage == 'chain':
+        return bench_chain(args)
 
     import torch
     import torch.distributed as dist

@@ -201,6 +201,9 @@ int mh_retry_counts(mh_ctx *ctx, int64_t *out4);
 int mh_test_set_gotoh_wait(mh_ctx *ctx, int64_t ticks);
 /* The 20 int32 header fields of mh_aln (no CIGAR) for reads [first, first+n). */
 int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20);
+/* Fields [field0, field0 + nfields) of records [first, first + n) (the
+ * mh_recs_fetch field order), nfields int32 per record. */
+int mh_recs_fetch_fields(mh_ctx *ctx, int64_t first, int64_t n, int field0, int nfields, int32_t *out);
 /* SAM text for reads order[first .. first+n) (order NULL: reads first ..
  * first+n-1): style 0 = tab-separated SAM with
  * optional tags, style 1 = the 11 CSV columns prelim.csv / remap.csv hold

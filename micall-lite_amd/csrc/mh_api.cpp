@@ -1186,6 +1186,21 @@ int mh_recs_fetch(mh_ctx *ctx, int64_t first, int64_t n, int32_t *out20)
     return 0;
 }
 
+int mh_recs_fetch_fields(mh_ctx *ctx, int64_t first, int64_t n, int field0, int nfields, int32_t *out)
+{
+    if (!ctx || (n > 0 && !out) || field0 < 0 || nfields < 1 || field0 + nfields > 20) return -3;
+    CtxEx *c = X(ctx);
+    MapState &M = c->map;
+    if (!M.valid) { set_error("no mapping results (call mh_map)"); return -3; }
+    if (first < 0 || n < 0 || first + n > M.n_reads) { set_error("record range out of bounds"); return -3; }
+    MH_HIP(hipSetDevice(c->device));
+    if (n == 0) return 0;
+    MH_HIP(hipMemcpy2DAsync(out, sizeof(int32_t) * nfields, (const int32_t *)(M.rec + first) + field0, sizeof(Rec),
+                            sizeof(int32_t) * nfields, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    MH_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
 // decimal text of v appended to out (no locale, no allocation)
 // decimal text of v at o; returns the end
 static inline char *put_int(char *o, int64_t v)

@@ -71,6 +71,8 @@ def _declare(L):
         'mh_alns_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
         'mh_map_counts': ([_P, _P, _P, _P, _P, _P, _I64P, _I64P, _I64P], ctypes.c_int),
         'mh_map_stats': ([_P, _P], ctypes.c_int),
+        'mh_recs_fetch_fields': ([_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _P],
+                                 ctypes.c_int),
         'mh_recs_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
         'mh_test_set_capacities': ([_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                     ctypes.c_int64], ctypes.c_int),
@@ -662,6 +664,19 @@ class Context:
             n = self.reads_count()[0] - first
         out = np.zeros((max(n, 1), 20), dtype=np.int32)
         check(lib().mh_recs_fetch(self.h, first, n, _ptr(out)), 'mh_recs_fetch')
+        return out[:n]
+
+    def rec_fields(self, names, first=0, n=None):
+        """(n, len(names)) int32 of consecutive ALN_FIELDS columns of the
+        records (one strided copy; names must be adjacent in ALN_FIELDS)."""
+        if n is None:
+            n = self.reads_count()[0] - first
+        idx = [ALN_FIELDS.index(k) for k in names]
+        if idx != list(range(idx[0], idx[0] + len(idx))):
+            raise ValueError('rec_fields: columns must be adjacent')
+        out = np.empty((max(n, 1), len(idx)), dtype=np.int32)
+        check(lib().mh_recs_fetch_fields(self.h, first, n, idx[0], len(idx), _ptr(out)),
+              'mh_recs_fetch_fields')
         return out[:n]
 
     def format_rows(self, style, first=0, n=None, order=None):

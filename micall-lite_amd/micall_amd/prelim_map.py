@@ -80,7 +80,7 @@ def prelim_map(fastq1, fastq2, prelim_csv,
     ctx.index_build(names, [seeds[n] for n in names], E2E_SEEDLEN)
     ctx.map(_native.params(_native.E2E, rdg=(rdgopen, READ_GAP_EXTEND),
                            rfg=(rfgopen, REF_GAP_EXTEND), maxins=MAXINS))
-    sam_ref = ctx.recs()[:, _native.ALN_FIELDS.index('sam_ref')]
+    sam_ref = ctx.rec_fields(('sam_ref',))[:, 0]
     header = (','.join(FIELDNAMES) + os.linesep).encode()
     if session.is_writer():
         session.write_bytes(prelim_csv, header)

@@ -72,22 +72,29 @@ def _sam_fields(ctx, rows):
     return [line.split('\t') for line in text.split('\n')[:-1]]
 
 
-def _unmapped_text(ctx, recs):
+def _flags(ctx):
+    """(flag, rnext) of the resident records (one strided copy of three
+    adjacent fields, not the whole records)."""
+    a = ctx.rec_fields(('flag', 'mapq', 'rnext'))
+    return a[:, 0], a[:, 2]
+
+
+def _unmapped_text(ctx):
     """FASTQ text of the unmapped lines of the last pass, R1 and R2 apart
     (remap.py:743-753)."""
     out = ([], [])
-    for fields in _sam_fields(ctx, np.nonzero(recs[:, F['flag']] & _UNMAPPED)[0]):
+    for fields in _sam_fields(ctx, np.nonzero(_flags(ctx)[0] & _UNMAPPED)[0]):
         out[0 if is_first_read(fields[1]) else 1].append('@{0[0]}\n{0[9]}\n+\n{0[10]}\n'.format(fields))
     return ''.join(out[0]).encode(), ''.join(out[1]).encode()
 
 
-def _write_unmapped(ctx, recs, outs):
+def _write_unmapped(ctx, outs):
     """Append the last pass's unmapped reads to the unmapped FASTQs (every
     rank's, in rank order, in a sharded run).  outs: the SharedOutput of
     unmapped1 and unmapped2 (None where not requested)."""
     if not any(outs):
         return
-    texts = _unmapped_text(ctx, recs)
+    texts = _unmapped_text(ctx)
     for out, text in zip(outs, texts):
         if out is not None:
             out.write_bytes([text])
@@ -195,15 +202,17 @@ class MixedReferenceSplit(object):
         return False
 
 
-def split_mixed_references(ctx, recs):
+def split_mixed_references(ctx):
     """MixedReferenceSplit over the resident records of the last pass:
-    returns (record indices that stay in remap.csv, splits).  Only records
-    whose RNEXT names another reference with both mates mapped are turned
-    into text; every other record passes."""
-    candidate = (recs[:, F['rnext']] >= 0) & ((recs[:, F['flag']] & (_UNMAPPED |
-                                                                       _MATE_UNMAPPED)) == 0)
-    split = MixedReferenceSplit()
+    returns (record indices that stay in remap.csv -- None when that is every
+    record --, splits).  Only records whose RNEXT names another reference
+    with both mates mapped are turned into text; every other record passes."""
+    flag, rnext = _flags(ctx)
+    candidate = (rnext >= 0) & ((flag & (_UNMAPPED | _MATE_UNMAPPED)) == 0)
     rows = np.flatnonzero(candidate)
+    if len(rows) == 0:
+        return None, {}
+    split = MixedReferenceSplit()
     for fields in _sam_fields(ctx, rows):
         split.feed(fields)      # never passes: RNEXT is a name, both mates mapped
     return np.flatnonzero(~candidate), split.splits
@@ -262,7 +271,7 @@ def remap(fastq1, fastq2, prelim_csv, remap_csv, remap_counts_csv=None, remap_co
     rows_out = sharded_io.SharedOutput(sh, remap_csv)
     unmapped_outs = [sharded_io.SharedOutput(sh, h) if h else None for h in (unmapped1, unmapped2)]
     if run.mapped_to is not None:
-        _write_unmapped(ctx, ctx.recs(), unmapped_outs)
+        _write_unmapped(ctx, unmapped_outs)
     if new_counts:
         unmapped_count += _write_remap_rows(ctx, run, conseqs, new_counts, rows_out,
                                             unmapped_outs, sh)
@@ -303,8 +312,9 @@ def _write_remap_rows(ctx, run, conseqs, new_counts, rows_out, unmapped_outs, sh
     split (rank order, then each rank's order), every rank taking part in
     each one (with its own split pairs, possibly none), and the rows and
     unmapped reads land in rank order."""
-    keep_rows, splits = split_mixed_references(ctx, ctx.recs())
-    rows_out.write_rows(ctx, 1, keep_rows, [0, len(keep_rows)])
+    keep_rows, splits = split_mixed_references(ctx)
+    n_keep = ctx.reads_count()[0] if keep_rows is None else len(keep_rows)
+    rows_out.write_rows(ctx, 1, keep_rows, [0, n_keep])
     order = list(splits)
     if shard is not None:
         order = []
@@ -325,7 +335,7 @@ def _write_remap_rows(ctx, run, conseqs, new_counts, rows_out, unmapped_outs, sh
         counts, unmapped = run.map_to_reference({name: conseqs[name]})
         extra_unmapped += unmapped
         new_counts.update(counts)
-        _write_unmapped(ctx, ctx.recs(), unmapped_outs)
+        _write_unmapped(ctx, unmapped_outs)
         rows_out.write_rows(ctx, 1, None, [0, len(seqs)])
     return extra_unmapped
 
