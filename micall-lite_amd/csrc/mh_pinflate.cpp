@@ -9,20 +9,20 @@
 //      its byte offset -- every bit position whose header (RFC 1951 3.2.7)
 //      parses into complete code-length and literal/length codes with an
 //      end-of-block code, then confirmed by decoding two blocks;
-//   2. decode: every span inflated (zlib, raw) from its start to the next
-//      span's start with a dictionary of 32 KiB of zero bytes in place of
-//      the unknown window: the bytes copied out of that window come out as
-//      NUL, which FASTQ text never holds, so everything past a span's last
-//      NUL is exact; a span must end exactly on the next one's start (else
-//      the start was false and the caller decodes serially);
-//   3. resolve: each span's bytes up to its last NUL decoded twice more,
-//      with windows whose bytes spell each window offset in base 255, so
-//      every window-derived byte knows which window byte it copies; they are
-//      replaced from the true window (the 32 KiB before the span) -- the last
-//      32 KiB of every span in order, as each is the next span's window, then
-//      everything else at once.  (Back-references keep window bytes alive
-//      through most of a span of FASTQ: re-decoding the dirty part in order
-//      with the true window would be nearly serial.)
+//   2. decode: every span after the first inflated twice (zlib, raw) from
+//      its start to the next span's start, in place of the unknown window
+//      once with window bytes W1[i] = i % 255 + 1 and once with W2[i] =
+//      (i / 255 + i % 255 + 1) % 255 + 1: a byte of the data comes out the
+//      same in both, a byte copied out of the window at offset i comes out
+//      as W1[i] / W2[i], which always differ and give i back; a span must
+//      end exactly on the next one's start (else the start was false and the
+//      caller decodes serially);
+//   3. resolve: every window-derived byte replaced from the true window (the
+//      32 KiB before its span) -- the last 32 KiB of every span in order, as
+//      each is the next span's window, then everything else at once.  (Back-
+//      references keep window bytes alive through most of a span of FASTQ,
+//      so decoding the span again once its window is known would be nearly
+//      serial.)
 //   4. check: the whole output's CRC-32 and size against the gzip trailer.
 //
 // Any failure returns -1 and the caller inflates serially, so the result is
@@ -209,26 +209,6 @@ int inflate_to(const uint8_t *p, int64_t nbytes, int64_t bit, const uint8_t *dic
     }
 }
 
-// Exactly n output bytes from `bit` with dictionary dict into dst.
-bool inflate_prefix(const uint8_t *p, int64_t nbytes, int64_t bit, const uint8_t *dict, int dlen,
-                    char *dst, size_t n)
-{
-    Span s;
-    if (!s.start(p, nbytes, bit, dict, dlen)) return false;
-    size_t used = 0;
-    while (used < n) {
-        s.refill();
-        s.z.next_out = (Bytef *)dst + used;
-        s.z.avail_out = (uInt)std::min<size_t>(n - used, (size_t)1 << 30);
-        const uInt before = s.z.avail_out;
-        const int st = inflate(&s.z, Z_NO_FLUSH);
-        used += before - s.z.avail_out;
-        if (used >= n) break;
-        if (st != Z_OK) return false;         // the stream ended or broke short of n
-    }
-    return true;
-}
-
 void threads_run(int nt, const std::function<void(int)> &fn)
 {
     if (nt <= 1) { fn(0); return; }
@@ -303,72 +283,83 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
     const int K = (int)st.size();
     mark("search");
     if (K < 2) return -1;
-    // 2. every span with a window of zeros
-    std::vector<TextBuf> part((size_t)K);
-    std::vector<int64_t> end((size_t)K, -1);
-    std::atomic<int> bad(0);
-    threads_run(K, [&](int k) {
-        part[(size_t)k].resize((size_t)std::max<int64_t>(1 << 20, ((k + 1 < K ? st[k + 1] : dend * 8) - st[k]) / 2));
-        if (inflate_to(src, dend, st[k], k ? zeros.data() : nullptr, k ? WIN : 0, k + 1 < K ? st[k + 1] : -1,
-                       part[(size_t)k], &end[(size_t)k]))
-            bad = 1;
-    });
-    mark("decode");
-    if (bad || (end[(size_t)K - 1] + 7) / 8 != dend) return -1;
-    std::vector<size_t> off((size_t)K + 1, 0), dirty((size_t)K, 0);
-    for (int k = 0; k < K; ++k) {
-        off[(size_t)k + 1] = off[(size_t)k] + part[(size_t)k].size();
-        if (k) {
-            const char *b = part[(size_t)k].data();
-            const void *z = memrchr(b, 0, part[(size_t)k].size());
-            dirty[(size_t)k] = z ? (size_t)((const char *)z - b) + 1 : 0;
-        }
+    // 2. every span after the first decoded twice, with windows whose bytes
+    // spell each window offset i: W1[i] = i % 255 + 1 and W2[i] = (i / 255 +
+    // i % 255 + 1) % 255 + 1.  A byte of the data comes out the same in both
+    // decodes; a byte copied from window offset i comes out as W1[i] and
+    // W2[i], which always differ (i / 255 <= 128) and together give i back.
+    std::vector<uint8_t> w1(WIN), w2(WIN);
+    for (int i = 0; i < WIN; ++i) {
+        w1[(size_t)i] = (uint8_t)(i % 255 + 1);
+        w2[(size_t)i] = (uint8_t)((i / 255 + i % 255 + 1) % 255 + 1);
     }
-    if ((uint32_t)off[(size_t)K] != isize) return -1;
-    out.resize(off[(size_t)K]);
-    char *o = &out[0];
-    threads_run(std::min(K, threads), [&](int t) {
-        for (int k = t; k < K; k += std::min(K, threads)) {
-            memcpy(o + off[(size_t)k], part[(size_t)k].data(), part[(size_t)k].size());
-            part[(size_t)k].release();
-        }
-    });
-    mark("place");
-    // 3. the dirty bytes' window offsets: each span's dirty prefix decoded
-    // twice more with windows whose bytes spell the offset (lo: i % 255 + 1,
-    // hi: i / 255 + 1; never 0, so a byte that is NUL in all three decodes is
-    // a NUL of the data), then every dirty byte replaced by the window byte
-    // it copies -- first the last 32 KiB of every span in order (they are
-    // the next span's window), then the rest of every span at once
-    std::vector<TextBuf> lo((size_t)K), hi((size_t)K);
-    std::vector<int> win((size_t)K, 0);
-    std::vector<uint8_t> wlo(WIN), whi(WIN);
-    for (int k = 1; k < K; ++k) win[(size_t)k] = (int)std::min<size_t>(WIN, off[(size_t)k]);
+    std::vector<TextBuf> p1((size_t)K), p2((size_t)K);
+    std::vector<int64_t> e1((size_t)K, -1), e2((size_t)K, -1);
+    std::atomic<int> bad(0);
     {
-        std::vector<std::pair<int, int>> jobs;   // (span, 0 lo / 1 hi)
-        for (int k = 1; k < K; ++k)
-            if (dirty[(size_t)k]) { jobs.emplace_back(k, 0); jobs.emplace_back(k, 1); }
+        std::vector<std::pair<int, int>> jobs{{0, 1}};   // (span, window 1 / 2)
+        for (int k = 1; k < K; ++k) { jobs.emplace_back(k, 1); jobs.emplace_back(k, 2); }
         std::atomic<size_t> next(0);
         threads_run(std::min<int>((int)jobs.size(), threads), [&](int) {
-            std::vector<uint8_t> dict(WIN);
             for (size_t j; (j = next.fetch_add(1)) < jobs.size();) {
-                const int k = jobs[j].first, w = win[(size_t)k];
-                for (int i = 0; i < w; ++i) dict[(size_t)i] = (uint8_t)(jobs[j].second ? i / 255 + 1 : i % 255 + 1);
-                TextBuf &dst = jobs[j].second ? hi[(size_t)k] : lo[(size_t)k];
-                dst.resize(dirty[(size_t)k]);
-                if (!inflate_prefix(src, dend, st[k], dict.data(), w, dst.data(), dirty[(size_t)k])) bad = 1;
+                const int k = jobs[j].first, which = jobs[j].second;
+                TextBuf &dst = which == 1 ? p1[(size_t)k] : p2[(size_t)k];
+                dst.resize((size_t)std::max<int64_t>(1 << 20, ((k + 1 < K ? st[k + 1] : dend * 8) - st[k]) / 2));
+                const uint8_t *dict = k == 0 ? nullptr : which == 1 ? w1.data() : w2.data();
+                if (inflate_to(src, dend, st[k], dict, k ? WIN : 0, k + 1 < K ? st[k + 1] : -1, dst,
+                               which == 1 ? &e1[(size_t)k] : &e2[(size_t)k]))
+                    bad = 1;
             }
         });
     }
-    if (bad) return -1;
+    mark("decode");
+    if (bad || (e1[(size_t)K - 1] + 7) / 8 != dend) return -1;
+    std::vector<size_t> off((size_t)K + 1, 0), dirty((size_t)K, 0);
+    for (int k = 0; k < K; ++k) {
+        if (k && (e1[(size_t)k] != e2[(size_t)k] || p1[(size_t)k].size() != p2[(size_t)k].size())) return -1;
+        off[(size_t)k + 1] = off[(size_t)k] + p1[(size_t)k].size();
+    }
+    // the first span's output must hold a whole window
+    if ((uint32_t)off[(size_t)K] != isize || off[1] < (size_t)WIN) return -1;
+    out.resize(off[(size_t)K]);
+    char *o = &out[0];
+    {
+        std::atomic<int> next(0);
+        threads_run(std::min(K, threads), [&](int) {
+            for (int k; (k = next.fetch_add(1)) < K;) {
+                const char *a1 = p1[(size_t)k].data(), *a2 = k ? p2[(size_t)k].data() : nullptr;
+                const size_t n = p1[(size_t)k].size();
+                memcpy(o + off[(size_t)k], a1, n);
+                if (k) {   // the last window-derived byte: the end of the dirty prefix
+                    size_t i = n;
+                    while (i >= 8) {
+                        uint64_t x, y;
+                        memcpy(&x, a1 + i - 8, 8);
+                        memcpy(&y, a2 + i - 8, 8);
+                        if (x != y) break;
+                        i -= 8;
+                    }
+                    while (i > 0 && a1[i - 1] == a2[i - 1]) --i;
+                    dirty[(size_t)k] = i;
+                }
+                p1[(size_t)k].release();
+            }
+        });
+    }
+    mark("place");
+    // 3. every window-derived byte replaced by the window byte it copies:
+    // the last 32 KiB of every span in order (they are the next span's
+    // window), then the rest of every span at once
     auto resolve = [&](int k, size_t i0, size_t i1) {
         char *span = o + off[(size_t)k];
-        const char *wb = o + off[(size_t)k] - win[(size_t)k];
-        const uint8_t *L = (const uint8_t *)lo[(size_t)k].data(), *H = (const uint8_t *)hi[(size_t)k].data();
+        const char *wb = o + off[(size_t)k] - WIN;
+        const uint8_t *B = (const uint8_t *)p2[(size_t)k].data();
         for (size_t i = i0; i < i1; ++i) {
-            if (span[i] != 0 || L[i] == 0) continue;      // exact, or a NUL of the data
-            const int idx = (H[i] - 1) * 255 + (L[i] - 1);
-            if (idx >= win[(size_t)k]) { bad = 1; return; }
+            const int a1 = (uint8_t)span[i], a2 = B[i];
+            if (a1 == a2) continue;                        // a byte of the data
+            const int r = a1 - 1, q = (a2 - r - 2 + 2 * 255) % 255;
+            const int idx = 255 * q + r;
+            if (a1 == 0 || idx >= WIN) { bad = 1; return; }
             span[i] = wb[idx];
         }
     };
@@ -384,8 +375,7 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
                 const size_t n = off[(size_t)k + 1] - off[(size_t)k];
                 const size_t t0 = n > (size_t)WIN ? n - WIN : 0;
                 resolve(k, 0, std::min(dirty[(size_t)k], t0));
-                lo[(size_t)k].release();
-                hi[(size_t)k].release();
+                p2[(size_t)k].release();
             }
         });
     }
