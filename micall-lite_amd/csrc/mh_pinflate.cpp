@@ -209,13 +209,28 @@ int inflate_to(const uint8_t *p, int64_t nbytes, int64_t bit, const uint8_t *dic
     }
 }
 
-void threads_run(int nt, const std::function<void(int)> &fn)
+// fn(t) on nt threads; an exception in a worker (an allocation failure)
+// ends that worker and makes the call return false, so the caller falls
+// back to the serial inflate instead of the process terminating
+bool threads_run(int nt, const std::function<void(int)> &fn)
 {
-    if (nt <= 1) { fn(0); return; }
+    std::atomic<int> failed(0);
+    auto guarded = [&](int t) {
+        try {
+            fn(t);
+        } catch (...) {
+            failed = 1;
+        }
+    };
+    if (nt <= 1) {
+        guarded(0);
+        return !failed;
+    }
     std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(fn, t);
-    fn(0);
+    for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    guarded(0);
     for (auto &x : th) x.join();
+    return !failed;
 }
 
 inline uint32_t rd32(const uint8_t *p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
@@ -264,7 +279,7 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
     std::vector<int64_t> found((size_t)T, -1);
     found[0] = d0 * 8;
     std::vector<uint8_t> zeros(WIN, 0);
-    threads_run(T - 1, [&](int i) {
+    const bool ok_search = threads_run(T - 1, [&](int i) {
         const int t = i + 1;
         const int64_t a = d0 + (dend - d0) * t / T, b = d0 + (dend - d0) * (t + 1) / T;
         TextBuf probe;
@@ -278,6 +293,7 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
             }
         }
     });
+    if (!ok_search) return -1;
     std::vector<int64_t> st;
     for (int64_t f : found) if (f >= 0) st.push_back(f);
     const int K = (int)st.size();
@@ -300,7 +316,7 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
         std::vector<std::pair<int, int>> jobs{{0, 1}};   // (span, window 1 / 2)
         for (int k = 1; k < K; ++k) { jobs.emplace_back(k, 1); jobs.emplace_back(k, 2); }
         std::atomic<size_t> next(0);
-        threads_run(std::min<int>((int)jobs.size(), threads), [&](int) {
+        if (!threads_run(std::min<int>((int)jobs.size(), threads), [&](int) {
             for (size_t j; (j = next.fetch_add(1)) < jobs.size();) {
                 const int k = jobs[j].first, which = jobs[j].second;
                 TextBuf &dst = which == 1 ? p1[(size_t)k] : p2[(size_t)k];
@@ -310,7 +326,8 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
                                which == 1 ? &e1[(size_t)k] : &e2[(size_t)k]))
                     bad = 1;
             }
-        });
+        }))
+            bad = 1;
     }
     mark("decode");
     if (bad || (e1[(size_t)K - 1] + 7) / 8 != dend) return -1;
