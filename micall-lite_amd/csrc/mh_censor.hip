@@ -27,7 +27,9 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <exception>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -72,13 +74,26 @@ static void censor_free_device(CensorState &C)
     C.cap_text = C.cap_rec = C.cap_bad = 0;
 }
 
+// fn(t) on nt threads; the first exception a worker throws (an allocation
+// failure) is rethrown here once every worker has ended
 static void cz_parallel(int nt, const std::function<void(int)> &fn)
 {
     if (nt <= 1) { fn(0); return; }
+    std::exception_ptr err;
+    std::mutex mu;
+    auto guarded = [&](int t) {
+        try {
+            fn(t);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = std::current_exception();
+        }
+    };
     std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(fn, t);
-    fn(0);
+    for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    guarded(0);
     for (auto &x : th) x.join();
+    if (err) std::rethrow_exception(err);
 }
 
 void censor_free(Ctx &c)
@@ -430,6 +445,19 @@ static int censor_text(Ctx &c, CensorState &C, int n_bad, const char *const *til
     return st;
 }
 
+// censor_text with an allocation failure (here or in a worker) as status -2
+static int censor_text_guarded(Ctx &c, CensorState &C, int n_bad, const char *const *tiles,
+                               const int32_t *cycles, int dst_gzip,
+                               std::chrono::steady_clock::time_point t0)
+{
+    try {
+        return censor_text(c, C, n_bad, tiles, cycles, dst_gzip, t0);
+    } catch (const std::exception &e) {
+        set_error("censor: out of memory (%s)", e.what());
+        return -2;
+    }
+}
+
 static bool censor_args_ok(mh_ctx *ctx, int n_bad, const char *const *tiles, const int32_t *cycles)
 {
     return ctx && n_bad >= 0 && (!n_bad || (tiles && cycles));
@@ -459,9 +487,14 @@ extern "C" int mh_censor_fastq(mh_ctx *ctx, const uint8_t *src, int64_t len, int
             return -3;
         }
     } else {
-        C.text.assign((const char *)src, (size_t)len);
+        try {
+            C.text.assign((const char *)src, (size_t)len);
+        } catch (const std::exception &) {
+            set_error("censor: out of memory");
+            return -2;
+        }
     }
-    if (int st = censor_text(c, C, n_bad, tiles, cycles, dst_gzip, t0)) { C.out.clear(); return st; }
+    if (int st = censor_text_guarded(c, C, n_bad, tiles, cycles, dst_gzip, t0)) { C.out.clear(); return st; }
     if (base_count) *base_count = C.base_count;
     if (score_sum) *score_sum = C.score_sum;
     return 0;
@@ -482,7 +515,7 @@ extern "C" int mh_censor_staged(mh_ctx *ctx, mh_fastq *fq, int n_bad, const char
     const auto t0 = std::chrono::steady_clock::now();
     TextBuf text = take_fastq_text(fq);
     C.text.swap(text);
-    if (int st = censor_text(c, C, n_bad, tiles, cycles, dst_gzip, t0)) { C.out.clear(); return st; }
+    if (int st = censor_text_guarded(c, C, n_bad, tiles, cycles, dst_gzip, t0)) { C.out.clear(); return st; }
     if (out_bytes) *out_bytes = (int64_t)C.out.size();
     if (base_count) *base_count = C.base_count;
     if (score_sum) *score_sum = C.score_sum;

@@ -13,7 +13,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -37,13 +39,26 @@ int s2a_threads()
     return n > 16 ? 16 : n;
 }
 
+// fn(t) on nt threads; the first exception a worker throws (an allocation
+// failure) is rethrown here once every worker has ended
 static void parallel_for(int nt, const std::function<void(int)> &fn)
 {
     if (nt <= 1) { fn(0); return; }
+    std::exception_ptr err;
+    std::mutex mu;
+    auto guarded = [&](int t) {
+        try {
+            fn(t);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = std::current_exception();
+        }
+    };
     std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(fn, t);
-    fn(0);
+    for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    guarded(0);
     for (auto &x : th) x.join();
+    if (err) std::rethrow_exception(err);
 }
 
 struct FieldRef {

@@ -590,9 +590,16 @@ extern "C" int mh_sam2aln_csv(mh_ctx *ctx, const char *text, int64_t len, int q_
     for (auto &o : S.out_cache) std::vector<std::string>().swap(o);
     S.out_valid = 0;
     auto t0 = std::chrono::steady_clock::now();
-    if (int st = s2a_parse(S, text ? text : "", len)) {
+    int pst = 0;
+    try {
+        pst = s2a_parse(S, text ? text : "", len);
+    } catch (const std::exception &e) {
+        set_error("remap csv: out of memory (%s)", e.what());
+        pst = -2;
+    }
+    if (pst) {
         S.u1.clear();
-        return st;
+        return pst;
     }
     auto t1 = std::chrono::steady_clock::now();
     if (int st = s2a_run(c, S, max_prop_n)) {
@@ -648,7 +655,13 @@ extern "C" int mh_sam2aln_output(mh_ctx *ctx, int which, char *buf, size_t cap, 
     std::vector<std::string> &out = S.out_cache[which];
     if (!(S.out_valid & (1 << which))) {
         auto t0 = std::chrono::steady_clock::now();
-        s2a_format(S, which, out);
+        try {
+            s2a_format(S, which, out);
+        } catch (const std::exception &e) {
+            std::vector<std::string>().swap(out);
+            set_error("mh_sam2aln_output: out of memory (%s)", e.what());
+            return -2;
+        }
         S.t_format[which] = std::chrono::duration<double, std::milli>(
                                 std::chrono::steady_clock::now() - t0).count();
         S.out_valid |= 1 << which;
