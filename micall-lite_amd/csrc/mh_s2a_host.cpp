@@ -8,6 +8,7 @@
 // Threads: min(16, hardware threads, OMP_NUM_THREADS); output is identical
 // for any thread count.
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <chrono>
 #include <cstdio>
@@ -535,10 +536,29 @@ static void s2a_aligned(const S2AState &S, Pieces &out)
         if (c != 0) return c > 0;
         return lx > ly;
     };
+    // the order of cmp in two passes: by (count, offset) -- one 64-bit key,
+    // cheap to compare -- then each run of equal keys by its sequence, the
+    // runs sorted in parallel (no serial merge of memcmp comparisons)
+    std::vector<uint64_t> key((size_t)S.n_unique);
+    parallel_for(nt, [&](int t) {
+        for (int64_t k = S.n_unique * t / nt; k < S.n_unique * (t + 1) / nt; ++k)
+            key[(size_t)k] = (uint64_t)(uint32_t)S.uniq[2 * k + 1] << 32 |
+                             (uint32_t)(S.res[4 * S.uniq[2 * k] + 1] ^ (int32_t)0x80000000);
+    });
+    auto by_key = [&](int64_t x, int64_t y) { return key[(size_t)x] > key[(size_t)y]; };
     for (int r = 0; r < nn; ++r) {
         auto &v = by[r];
         if (v.empty()) continue;
-        parallel_sort(v, cmp, nt);
+        parallel_sort(v, by_key, nt);
+        std::vector<size_t> runs{0};
+        for (size_t i = 1; i < v.size(); ++i)
+            if (key[(size_t)v[i]] != key[(size_t)v[i - 1]]) runs.push_back(i);
+        runs.push_back(v.size());
+        std::atomic<size_t> next_run(0);
+        parallel_for(nt, [&](int) {
+            for (size_t j; (j = next_run.fetch_add(1)) + 1 < runs.size();)
+                if (runs[j + 1] - runs[j] > 1) std::sort(v.begin() + runs[j], v.begin() + runs[j + 1], cmp);
+        });
         std::string ref;
         csv_field(ref, S.names[r].data(), S.names[r].size());
         parallel_text((int64_t)v.size(), nt, out, [&](std::string &o, int64_t a, int64_t b) {
