@@ -104,22 +104,25 @@ def grouped_segments(sam_ref, n_refs, sh=None):
     every group, possibly empty: written segment-major, a group holds the
     rows of rank 0, then rank 1, ... -- the ranks hold consecutive blocks of
     the FASTQ, so that is FASTQ order, as on one GPU."""
-    sam_ref = np.asarray(sam_ref, dtype=np.int64)
-    key = np.where(sam_ref < 0, n_refs, sam_ref)
+    sam_ref = np.asarray(sam_ref)
+    # rname ids are small: a stable argsort of int16 keys is numpy's radix sort
+    kt = np.int16 if n_refs < np.iinfo(np.int16).max else np.int64
+    key = np.where(sam_ref < 0, n_refs, sam_ref).astype(kt)
+    by_key = np.argsort(key, kind='stable').astype(np.int64)
+    counts = np.bincount(key, minlength=n_refs + 1)
+    starts = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     first = np.full(n_refs + 1, -1, dtype=np.int64)
-    if len(key):
-        k_vals, k_first = np.unique(key, return_index=True)
-        first[k_vals] = k_first + (sh.read_base if sh is not None else 0)
+    present = counts > 0
+    # a stable sort keeps each key's rows in output order: its first row first
+    first[present] = by_key[starts[:-1][present]] + (sh.read_base if sh is not None else 0)
     if sh is not None:
         first = sh.min_i64(first)
     groups = [g for g in np.argsort(np.where(first < 0, np.iinfo(np.int64).max, first),
                                     kind='stable') if first[g] >= 0]
-    rank_of = np.full(n_refs + 1, len(groups), dtype=np.int64)
-    rank_of[groups] = np.arange(len(groups))
-    order = np.argsort(rank_of[key], kind='stable').astype(np.int64)
-    bounds = np.searchsorted(rank_of[key][order], np.arange(len(groups) + 1)).astype(np.int64)
     if len(groups) == 0:
-        bounds = np.zeros(2, dtype=np.int64)
+        return np.zeros(0, dtype=np.int64), np.zeros(2, dtype=np.int64)
+    order = np.concatenate([by_key[starts[g]:starts[g + 1]] for g in groups]).astype(np.int64)
+    bounds = np.concatenate([[0], np.cumsum([counts[g] for g in groups])]).astype(np.int64)
     return order, bounds
 
 
