@@ -272,33 +272,73 @@ static uint64_t signature(int n, const char *const *seqs, int seedlen)
     return mix64(h, (uint64_t)n);
 }
 
+static void par_for(int nt, const std::function<void(int)> &fn);
+int s2a_threads();   // mh_s2a_host.cpp: host worker count
+
 static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int seedlen)
 {
     struct E { uint64_t key; int32_t ref, pos; };
-    std::vector<uint8_t> codes;
     std::vector<int64_t> ref_off(n_refs);
     std::vector<int32_t> ref_len(n_refs);
-    std::vector<E> ent;
+    int64_t total_len = 0;
     for (int r = 0; r < n_refs; ++r) {
-        const int L = (int)std::strlen(seqs[r]);
-        ref_off[r] = (int64_t)codes.size();
-        ref_len[r] = L;
-        uint64_t key = 0;
-        int last_n = -1;
-        for (int p = 0; p < L; ++p) {
-            const uint8_t c = code_of(seqs[r][p]);
-            codes.push_back(c);
-            if (c > 3) last_n = p;
-            // little-endian 2-bit packing: base x of the window at bits 2x+1:2x
-            key = (key >> 2) | ((uint64_t)(c & 3) << (2 * (seedlen - 1)));
-            if (p >= seedlen - 1 && last_n <= p - seedlen) ent.push_back({key, r, p - seedlen + 1});
-        }
+        ref_len[r] = (int)std::strlen(seqs[r]);
+        ref_off[r] = total_len;
+        total_len += ref_len[r];
     }
-    std::sort(ent.begin(), ent.end(), [](const E &a, const E &b) {
+    std::vector<uint8_t> codes((size_t)total_len);
+    // every reference's seeds by its own thread (references are independent),
+    // then concatenated in reference order
+    const int nt = std::max(1, std::min<int>(s2a_threads(), n_refs));
+    std::vector<std::vector<E>> per(n_refs);
+    {
+        std::atomic<int> next(0);
+        par_for(nt, [&](int) {
+            for (int r; (r = next.fetch_add(1)) < n_refs;) {
+                const int L = ref_len[r];
+                uint8_t *cr = codes.data() + ref_off[r];
+                std::vector<E> &v = per[r];
+                v.reserve(L > seedlen ? (size_t)(L - seedlen + 1) : 0);
+                uint64_t key = 0;
+                int last_n = -1;
+                for (int p = 0; p < L; ++p) {
+                    const uint8_t c = code_of(seqs[r][p]);
+                    cr[p] = c;
+                    if (c > 3) last_n = p;
+                    // little-endian 2-bit packing: base x of the window at bits 2x+1:2x
+                    key = (key >> 2) | ((uint64_t)(c & 3) << (2 * (seedlen - 1)));
+                    if (p >= seedlen - 1 && last_n <= p - seedlen) v.push_back({key, r, p - seedlen + 1});
+                }
+            }
+        });
+    }
+    std::vector<E> ent;
+    {
+        size_t n = 0;
+        for (auto &v : per) n += v.size();
+        ent.reserve(n);
+        for (auto &v : per) { ent.insert(ent.end(), v.begin(), v.end()); std::vector<E>().swap(v); }
+    }
+    auto less = [](const E &a, const E &b) {
         if (a.key != b.key) return a.key < b.key;
         if (a.ref != b.ref) return a.ref < b.ref;
         return a.pos < b.pos;
-    });
+    };
+    {   // sorted in parallel chunks, then merged pairwise (a total order: the
+        // result is the one std::sort gives)
+        const int ns = ent.size() < 65536 ? 1 : s2a_threads();
+        std::vector<size_t> b((size_t)ns + 1);
+        for (int t = 0; t <= ns; ++t) b[(size_t)t] = ent.size() * (size_t)t / (size_t)ns;
+        par_for(ns, [&](int t) { std::sort(ent.begin() + b[(size_t)t], ent.begin() + b[(size_t)t + 1], less); });
+        for (int w = 1; w < ns; w *= 2) {
+            std::vector<std::pair<int, int>> jobs;
+            for (int t = 0; t + w < ns; t += 2 * w) jobs.push_back({t, std::min(t + 2 * w, ns)});
+            par_for((int)jobs.size(), [&](int j) {
+                const int a = jobs[(size_t)j].first, m = a + w, z = jobs[(size_t)j].second;
+                std::inplace_merge(ent.begin() + b[(size_t)a], ent.begin() + b[(size_t)m], ent.begin() + b[(size_t)z], less);
+            });
+        }
+    }
     size_t nkeys = 0;
     for (size_t i = 0; i < ent.size(); ++i) if (i == 0 || ent[i].key != ent[i - 1].key) ++nkeys;
     uint64_t cap = 1024;
