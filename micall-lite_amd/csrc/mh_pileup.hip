@@ -280,7 +280,7 @@ __device__ __forceinline__ int wave_max_all(int v)
 // 6 waves per SIMD: at most 80 VGPRs, so 24 waves stay resident per CU
 // (pile_geometry); k_pileup<0> keeps 2 VGPRs in scratch (12 B per lane)
 template <int SRC>
-__global__ __launch_bounds__(1024, 5) void k_pileup(PileArgs A)
+__global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;

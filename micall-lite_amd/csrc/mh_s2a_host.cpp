@@ -404,85 +404,42 @@ int s2a_parse(S2AState &S, const char *text, int64_t len)
         std::thread([old]() { delete old; }).detach();
     }
     s2a_mark(tp, "concat");
-    // ---- matchmaker (sam2aln.py:291-312) ----
-    // A row pairs with the pending row of its qname seen before it, and the
-    // pair leaves the table (a third row of the qname waits for a fourth);
-    // units come in the order of their second row, then the rows left
-    // waiting in row order.  Rows of one qname share a hash, so the rows are
-    // split by hash into buckets matched in parallel (each in row order,
-    // open addressing with tombstones as a serial pass would), and a last
-    // pass over the rows emits the units in that order.
-    enum : int8_t { ROLE_PENDING = 0, ROLE_FIRST = 1, ROLE_SECOND = 2 };
-    std::vector<int8_t> role((size_t)nr, ROLE_PENDING);
-    std::vector<int64_t> partner((size_t)nr, -1);
+    // ---- matchmaker (sam2aln.py:291-312): open addressing on qname ----
+    uint64_t cap = 1024;
+    while (cap < (uint64_t)(2 * nr + 2)) cap <<= 1;
+    std::vector<int64_t> slot_row(cap, -1);   // row waiting for its mate
+    std::vector<int64_t> pend_of_row(nr, -1);
+    std::vector<std::pair<int64_t, bool>> pend;
+    pend.reserve((size_t)nr);
+    S.u1.clear(); S.u2.clear();
+    S.u1.reserve((size_t)nr / 2 + 1); S.u2.reserve((size_t)nr / 2 + 1);
     auto same = [&](int64_t a, int64_t b) {
         return S.qlen[a] == S.qlen[b] &&
                memcmp(S.qpool.data() + S.qoff[a], S.qpool.data() + S.qoff[b], (size_t)S.qlen[a]) == 0;
     };
-    {
-        // buckets by the hash's top bits (MH_S2A_BUCKETS=1 / 64: the serial
-        // order / the parallel split at any size, for the equivalence test)
-        int nb = nr < 65536 ? 1 : 64;
-        if (const char *e = getenv("MH_S2A_BUCKETS")) nb = atoi(e) == 1 ? 1 : 64;
-        auto bucket = [&](int64_t r) { return nb == 1 ? 0 : (int)(qhash[r] >> 58); };
-        const int ct = std::max(1, std::min<int>(s2a_threads(), (int)(nr >> 14) + 1));
-        // rows of each bucket in row order: per-chunk counts, prefix, scatter
-        std::vector<int64_t> cnt((size_t)ct * nb, 0);
-        parallel_for(ct, [&](int t) {
-            for (int64_t r = nr * t / ct; r < nr * (t + 1) / ct; ++r) ++cnt[(size_t)t * nb + bucket(r)];
-        });
-        std::vector<int64_t> bstart((size_t)nb + 1, 0), at((size_t)ct * nb, 0);
-        {
-            int64_t run = 0;
-            for (int g = 0; g < nb; ++g) {
-                bstart[(size_t)g] = run;
-                for (int t = 0; t < ct; ++t) { at[(size_t)t * nb + g] = run; run += cnt[(size_t)t * nb + g]; }
-            }
-            bstart[(size_t)nb] = run;
+    for (int64_t r = 0; r < nr; ++r) {
+        uint64_t s = qhash[r] & (cap - 1);
+        int64_t hit = -1;
+        uint64_t tomb = ~0ull;
+        while (slot_row[s] != -1) {
+            const int64_t o = slot_row[s];
+            if (o == -2) { if (tomb == ~0ull) tomb = s; }
+            else if (qhash[o] == qhash[r] && same(o, r)) { hit = (int64_t)s; break; }
+            s = (s + 1) & (cap - 1);
         }
-        std::vector<int64_t> rows((size_t)std::max<int64_t>(nr, 1));
-        parallel_for(ct, [&](int t) {
-            std::vector<int64_t> pos(at.begin() + (size_t)t * nb, at.begin() + (size_t)(t + 1) * nb);
-            for (int64_t r = nr * t / ct; r < nr * (t + 1) / ct; ++r) rows[(size_t)pos[(size_t)bucket(r)]++] = r;
-        });
-        std::atomic<int> next(0);
-        parallel_for(std::min(ct, nb), [&](int) {
-            std::vector<int64_t> slot_row;
-            for (int g; (g = next.fetch_add(1)) < nb;) {
-                const int64_t g0 = bstart[(size_t)g], g1 = bstart[(size_t)g + 1];
-                uint64_t cap = 1024;
-                while (cap < (uint64_t)(2 * (g1 - g0) + 2)) cap <<= 1;
-                slot_row.assign(cap, -1);   // row waiting for its mate; -2 tombstone
-                for (int64_t i = g0; i < g1; ++i) {
-                    const int64_t r = rows[(size_t)i];
-                    uint64_t sl = qhash[r] & (cap - 1);
-                    int64_t hit = -1;
-                    uint64_t tomb = ~0ull;
-                    while (slot_row[sl] != -1) {
-                        const int64_t o = slot_row[sl];
-                        if (o == -2) { if (tomb == ~0ull) tomb = sl; }
-                        else if (qhash[o] == qhash[r] && same(o, r)) { hit = (int64_t)sl; break; }
-                        sl = (sl + 1) & (cap - 1);
-                    }
-                    if (hit >= 0) {
-                        const int64_t o = slot_row[hit];
-                        role[(size_t)o] = ROLE_FIRST;
-                        role[(size_t)r] = ROLE_SECOND;
-                        partner[(size_t)r] = o;
-                        slot_row[hit] = -2;
-                    } else {
-                        slot_row[tomb != ~0ull ? tomb : sl] = r;
-                    }
-                }
-            }
-        });
+        if (hit >= 0) {
+            const int64_t o = slot_row[hit];
+            pend[pend_of_row[o]].second = false;
+            S.u1.push_back(o);
+            S.u2.push_back(r);
+            slot_row[hit] = -2;   // tombstone
+        } else {
+            slot_row[tomb != ~0ull ? tomb : s] = r;
+            pend_of_row[r] = (int64_t)pend.size();
+            pend.push_back({r, true});
+        }
     }
-    S.u1.clear(); S.u2.clear();
-    S.u1.reserve((size_t)nr / 2 + 1); S.u2.reserve((size_t)nr / 2 + 1);
-    for (int64_t r = 0; r < nr; ++r)
-        if (role[(size_t)r] == ROLE_SECOND) { S.u1.push_back(partner[(size_t)r]); S.u2.push_back(r); }
-    for (int64_t r = 0; r < nr; ++r)
-        if (role[(size_t)r] == ROLE_PENDING) { S.u1.push_back(r); S.u2.push_back(-1); }
+    for (auto &o : pend) if (o.second) { S.u1.push_back(o.first); S.u2.push_back(-1); }
     s2a_mark(tp, "matchmaker");
     // ---- parse_sam's early causes and the rname order ----
     const int64_t nu = (int64_t)S.u1.size();

@@ -106,31 +106,3 @@ def test_sam2aln_rejects_bad_cigar_like_the_reference(ctx):
         ctx.sam2aln_csv(text)
     with pytest.raises(RuntimeError, match='too long'):
         ctx.sam2aln_csv(text.replace('3H3M', '4M'))
-
-
-def test_sam2aln_matchmaker_buckets_match_serial_order(ctx, monkeypatch):
-    """The matchmaker splits rows into hash buckets matched in parallel
-    (mh_s2a_host.cpp) once a file has 64 k rows; forced here at a small size
-    (MH_S2A_BUCKETS=64) against the one-bucket serial order and the oracle,
-    on rows shuffled so mates sit far apart, with qnames seen three and four
-    times (a third row waits for a fourth, sam2aln.py:291-312) and mates
-    that never come."""
-    text = _synthetic_remap_csv(ctx, 1500, 53)
-    rows = list(csv.reader(io.StringIO(text)))
-    head, body = rows[0], rows[1:]
-    rng = np.random.default_rng(5)
-    body = [body[i] for i in rng.permutation(len(body))]
-    extra = [list(r) for r in body[:300]]               # third and fourth rows of 300 qnames
-    lone = [[r[0] + 'lone'] + r[1:] for r in body[300:420]]   # mates that never come
-    body = body + extra[:150] + lone + extra[150:] + [list(r) for r in body[:150]]
-    out = io.StringIO()
-    csv.writer(out, lineterminator='\n').writerows([head] + body)
-    text = out.getvalue()
-    want = og_sam2aln.sam2aln(text)
-    for buckets in ('1', '64'):
-        monkeypatch.setenv('MH_S2A_BUCKETS', buckets)
-        got = _device(ctx, text)
-        assert got[0] == want[0], buckets
-        assert got[1] == want[1], buckets
-        assert got[2] == want[2], buckets
-    assert 'unmatched' in want[2]
