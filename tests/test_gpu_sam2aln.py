@@ -106,3 +106,24 @@ def test_sam2aln_rejects_bad_cigar_like_the_reference(ctx):
         ctx.sam2aln_csv(text)
     with pytest.raises(RuntimeError, match='too long'):
         ctx.sam2aln_csv(text.replace('3H3M', '4M'))
+
+
+def test_sam2aln_matchmaker_order_vs_oracle(ctx):
+    """The matchmaker (sam2aln.py:291-312) on rows shuffled so mates sit far
+    apart, with qnames seen three and four times (a third row waits for a
+    fourth) and mates that never come: byte-identical to the oracle."""
+    text = _synthetic_remap_csv(ctx, 1500, 53)
+    rows = list(csv.reader(io.StringIO(text)))
+    head, body = rows[0], rows[1:]
+    rng = np.random.default_rng(5)
+    body = [body[i] for i in rng.permutation(len(body))]
+    extra = [list(r) for r in body[:300]]                     # third and fourth rows of 300 qnames
+    lone = [[r[0] + 'lone'] + r[1:] for r in body[300:420]]   # mates that never come
+    body = body + extra[:150] + lone + extra[150:] + [list(r) for r in body[:150]]
+    out = io.StringIO()
+    csv.writer(out, lineterminator='\n').writerows([head] + body)
+    text = out.getvalue()
+    want = og_sam2aln.sam2aln(text)
+    got = _device(ctx, text)
+    assert got == tuple(want) or list(got) == list(want)
+    assert 'unmatched' in want[2]
