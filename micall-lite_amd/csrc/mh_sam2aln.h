@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "mh_gunzip.h"
@@ -55,12 +56,13 @@ struct S2AState {
             *d_ctr = nullptr;
     uint32_t *d_cig = nullptr;
     uint64_t *d_h = nullptr, *d_tkey = nullptr;
+    std::unordered_map<const void *, size_t> dcap;   // bytes allocated behind each device pointer (grow-only)
     // ---- results of the device pass ----
     int64_t n_merge = 0, n_unique = 0;
     std::vector<int32_t> res;           // per merge unit: status, offset, body_len, strip_len
     std::vector<int32_t> uniq;          // rep merge unit, count
     std::vector<int64_t> uniq_off;      // offsets into gathered
-    std::string gathered;               // bodies of the distinct sequences
+    TextBuf gathered;                   // bodies of the distinct sequences (not zero-filled)
     // ---- formatted outputs (cached between the size query and the copy) ----
     std::vector<std::string> out_cache[3];   // the text as pieces, in order
     int out_valid = 0;

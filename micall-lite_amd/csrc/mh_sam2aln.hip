@@ -49,6 +49,7 @@ static void s2a_free_device(S2AState &S)
         S.d_uniq = S.d_ctr = nullptr;
     S.d_cig = nullptr;
     S.d_h = S.d_tkey = nullptr;
+    S.dcap.clear();
 }
 
 void s2a_free(Ctx &c)
@@ -397,23 +398,34 @@ __global__ __launch_bounds__(256) void k_s2a_gather(const int32_t *uniq, const i
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
+// a device buffer of at least `bytes` behind p: kept between calls and
+// reallocated only to grow (a hipFree waits for the device, and large
+// allocations map pages: both once per size, not once per call)
 template <class T>
-static int s2a_upload(T *&dst, const std::vector<T> &v, hipStream_t s)
+static int dev_reserve(S2AState &S, T *&p, size_t bytes)
 {
-    hipFree(dst);
-    dst = nullptr;
-    const size_t n = v.size() > 0 ? v.size() : 1;
-    MH_HIP(hipMalloc(&dst, sizeof(T) * n));
+    size_t &cap = S.dcap[(const void *)&p];
+    if (p && cap >= bytes) return 0;
+    hipFree(p);
+    p = nullptr;
+    cap = 0;
+    MH_HIP(hipMalloc(&p, bytes > 0 ? bytes : 1));
+    cap = bytes;
+    return 0;
+}
+
+template <class T>
+static int s2a_upload(S2AState &S, T *&dst, const std::vector<T> &v, hipStream_t s)
+{
+    if (int st = dev_reserve(S, dst, sizeof(T) * v.size())) return st;
     if (!v.empty()) MH_HIP(hipMemcpyAsync(dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s));
     return 0;
 }
 
 template <class Bytes>
-static int s2a_upload_bytes(uint8_t *&dst, const Bytes &v, hipStream_t s)
+static int s2a_upload_bytes(S2AState &S, uint8_t *&dst, const Bytes &v, hipStream_t s)
 {
-    hipFree(dst);
-    dst = nullptr;
-    MH_HIP(hipMalloc(&dst, v.size() > 0 ? v.size() : 1));
+    if (int st = dev_reserve(S, dst, v.size())) return st;
     if (!v.empty()) MH_HIP(hipMemcpyAsync(dst, v.data(), v.size(), hipMemcpyHostToDevice, s));
     return 0;
 }
@@ -469,31 +481,27 @@ int s2a_run(Ctx &c, S2AState &S, double max_prop_n)
         set_error("sam2aln: reference span %d too long for LDS", span_cap);
         return -3;
     }
-    if (int st = s2a_upload_bytes(S.d_seq, S.seq, s)) return st;
-    if (int st = s2a_upload_bytes(S.d_qual, S.qual, s)) return st;
-    if (int st = s2a_upload(S.d_soff, S.soff, s)) return st;
-    if (int st = s2a_upload(S.d_pos, S.pos, s)) return st;
-    if (int st = s2a_upload(S.d_cigoff, S.cig_off, s)) return st;
-    if (int st = s2a_upload(S.d_ncig, S.n_cig, s)) return st;
-    if (int st = s2a_upload(S.d_cig, S.cig, s)) return st;
-    if (int st = s2a_upload(S.d_units, mu, s)) return st;
-    if (int st = s2a_upload(S.d_uref, mref, s)) return st;
-    if (int st = s2a_upload(S.d_slot, slot, s)) return st;
+    if (int st = s2a_upload_bytes(S, S.d_seq, S.seq, s)) return st;
+    if (int st = s2a_upload_bytes(S, S.d_qual, S.qual, s)) return st;
+    if (int st = s2a_upload(S, S.d_soff, S.soff, s)) return st;
+    if (int st = s2a_upload(S, S.d_pos, S.pos, s)) return st;
+    if (int st = s2a_upload(S, S.d_cigoff, S.cig_off, s)) return st;
+    if (int st = s2a_upload(S, S.d_ncig, S.n_cig, s)) return st;
+    if (int st = s2a_upload(S, S.d_cig, S.cig, s)) return st;
+    if (int st = s2a_upload(S, S.d_units, mu, s)) return st;
+    if (int st = s2a_upload(S, S.d_uref, mref, s)) return st;
+    if (int st = s2a_upload(S, S.d_slot, slot, s)) return st;
     const int64_t nm = S.n_merge;
-    hipFree(S.d_out); hipFree(S.d_res); hipFree(S.d_h); hipFree(S.d_ctr);
-    hipFree(S.d_tkey); hipFree(S.d_tcnt); hipFree(S.d_trep); hipFree(S.d_uniq);
-    S.d_out = nullptr; S.d_res = nullptr; S.d_h = nullptr; S.d_ctr = nullptr;
-    S.d_tkey = nullptr; S.d_tcnt = nullptr; S.d_trep = nullptr; S.d_uniq = nullptr;
-    MH_HIP(hipMalloc(&S.d_out, total > 0 ? total : 1));
-    MH_HIP(hipMalloc(&S.d_res, sizeof(int32_t) * 4 * nm));
-    MH_HIP(hipMalloc(&S.d_h, sizeof(uint64_t) * 2 * nm));
-    MH_HIP(hipMalloc(&S.d_ctr, sizeof(int32_t) * 4));
     uint64_t tsize = 1024;
     while (tsize < (uint64_t)(2 * nm)) tsize <<= 1;
-    MH_HIP(hipMalloc(&S.d_tkey, sizeof(uint64_t) * tsize));
-    MH_HIP(hipMalloc(&S.d_tcnt, sizeof(int32_t) * tsize));
-    MH_HIP(hipMalloc(&S.d_trep, sizeof(int32_t) * tsize));
-    MH_HIP(hipMalloc(&S.d_uniq, sizeof(int32_t) * 2 * nm));
+    if (int st = dev_reserve(S, S.d_out, total > 0 ? (size_t)total : 1)) return st;
+    if (int st = dev_reserve(S, S.d_res, sizeof(int32_t) * 4 * nm)) return st;
+    if (int st = dev_reserve(S, S.d_h, sizeof(uint64_t) * 2 * nm)) return st;
+    if (int st = dev_reserve(S, S.d_ctr, sizeof(int32_t) * 4)) return st;
+    if (int st = dev_reserve(S, S.d_tkey, sizeof(uint64_t) * tsize)) return st;
+    if (int st = dev_reserve(S, S.d_tcnt, sizeof(int32_t) * tsize)) return st;
+    if (int st = dev_reserve(S, S.d_trep, sizeof(int32_t) * tsize)) return st;
+    if (int st = dev_reserve(S, S.d_uniq, sizeof(int32_t) * 2 * nm)) return st;
     MH_HIP(hipMemsetAsync(S.d_ctr, 0, sizeof(int32_t) * 4, s));
     MH_HIP(hipMemsetAsync(S.d_tkey, 0, sizeof(uint64_t) * tsize, s));
     MH_HIP(hipMemsetAsync(S.d_tcnt, 0, sizeof(int32_t) * tsize, s));
@@ -554,12 +562,10 @@ int s2a_run(Ctx &c, S2AState &S, double max_prop_n)
         g += S.res[4 * (int64_t)S.uniq[2 * k] + 2];
     }
     S.uniq_off[S.n_unique] = g;
-    S.gathered.assign((size_t)g, '\0');
+    S.gathered.resize((size_t)g);
     if (S.n_unique && g) {
-        if (int st = s2a_upload(S.d_goff, S.uniq_off, s)) return st;
-        hipFree(S.d_gather);
-        S.d_gather = nullptr;
-        MH_HIP(hipMalloc(&S.d_gather, (size_t)g));
+        if (int st = s2a_upload(S, S.d_goff, S.uniq_off, s)) return st;
+        if (int st = dev_reserve(S, S.d_gather, (size_t)g)) return st;
         int64_t gb = (S.n_unique + 3) / 4;
         if (gb > 256 * 64) gb = 256 * 64;
         hipLaunchKernelGGL(k_s2a_gather, dim3((unsigned)gb), dim3(256), 0, s, S.d_uniq, S.d_goff,
