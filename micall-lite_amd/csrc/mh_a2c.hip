@@ -38,6 +38,7 @@
 #include <functional>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "mh_gunzip.h"
@@ -106,6 +107,7 @@ struct A2CState {
     std::vector<A2CEntry> entries;
     std::string aminos;                       // one line per entry
     std::string ins_rows;                     // mh_a2c_insert_rows text (size query, then copy)
+    std::unordered_map<const void *, size_t> dcap;   // bytes behind each device pointer (grow-only)
     double t_parse = 0, t_count = 0, t_ins = 0;
 };
 
@@ -337,6 +339,7 @@ static void a2c_free_device(A2CState &S)
     S.d_bin_rows = nullptr;
     S.d_chunks = nullptr;
     S.d_cnt = S.d_first = nullptr;
+    S.dcap.clear();
 }
 
 static void a2c_parallel_for(int nt, const std::function<void(int)> &fn)
@@ -559,9 +562,23 @@ static int a2c_layout(A2CState &S, std::vector<int32_t> &bin_rows, std::vector<A
 }
 
 template <class T>
-static int a2c_upload(T *&dst, const T *src, size_t n, hipStream_t s)
+static int a2c_reserve(A2CState &S, T *&p, size_t bytes)
 {
-    MH_HIP(hipMalloc(&dst, sizeof(T) * (n ? n : 1)));
+    // kept between calls, reallocated only to grow (hipFree waits for the device)
+    size_t &cap = S.dcap[(const void *)&p];
+    if (p && cap >= bytes) return 0;
+    hipFree(p);
+    p = nullptr;
+    cap = 0;
+    MH_HIP(hipMalloc(&p, bytes > 0 ? bytes : 1));
+    cap = bytes;
+    return 0;
+}
+
+template <class T>
+static int a2c_upload(A2CState &S, T *&dst, const T *src, size_t n, hipStream_t s)
+{
+    if (int st = a2c_reserve(S, dst, sizeof(T) * n)) return st;
     if (n) MH_HIP(hipMemcpyAsync(dst, src, sizeof(T) * n, hipMemcpyHostToDevice, s));
     return 0;
 }
@@ -573,16 +590,15 @@ static int a2c_count(Ctx &c, A2CState &S, const char *text, int64_t text_len)
     std::vector<A2CChunk> chunks;
     if (int st = a2c_layout(S, bin_rows, chunks)) return st;
     hipStream_t s = c.stream;
-    a2c_free_device(S);
-    if (int st = a2c_upload(S.d_text, (const uint8_t *)text, (size_t)text_len, s)) return st;
-    if (int st = a2c_upload(S.d_rows, S.rows.data(), S.rows.size(), s)) return st;
-    if (int st = a2c_upload(S.d_bin_rows, bin_rows.data(), bin_rows.size(), s)) return st;
-    if (int st = a2c_upload(S.d_chunks, chunks.data(), chunks.size(), s)) return st;
-    if (int st = a2c_upload(S.d_code, S.code, 512, s)) return st;
-    if (int st = a2c_upload(S.d_cls, S.cls, 256, s)) return st;
+    if (int st = a2c_upload(S, S.d_text, (const uint8_t *)text, (size_t)text_len, s)) return st;
+    if (int st = a2c_upload(S, S.d_rows, S.rows.data(), S.rows.size(), s)) return st;
+    if (int st = a2c_upload(S, S.d_bin_rows, bin_rows.data(), bin_rows.size(), s)) return st;
+    if (int st = a2c_upload(S, S.d_chunks, chunks.data(), chunks.size(), s)) return st;
+    if (int st = a2c_upload(S, S.d_code, S.code, 512, s)) return st;
+    if (int st = a2c_upload(S, S.d_cls, S.cls, 256, s)) return st;
     const size_t cells = (size_t)S.n_bins * A2C_CELLS;
-    MH_HIP(hipMalloc(&S.d_cnt, sizeof(uint32_t) * (cells ? cells : 1)));
-    MH_HIP(hipMalloc(&S.d_first, sizeof(uint32_t) * (cells ? cells : 1)));
+    if (int st = a2c_reserve(S, S.d_cnt, sizeof(uint32_t) * cells)) return st;
+    if (int st = a2c_reserve(S, S.d_first, sizeof(uint32_t) * cells)) return st;
     if (cells) {
         MH_HIP(hipMemsetAsync(S.d_cnt, 0, sizeof(uint32_t) * cells, s));
         MH_HIP(hipMemsetAsync(S.d_first, 0xff, sizeof(uint32_t) * cells, s));
