@@ -40,6 +40,7 @@ typedef void (*lc_free_t)(Lc *);
 typedef size_t (*lc_gzip_t)(Lc *, const void *, size_t, void *, size_t);
 typedef size_t (*lc_bound_t)(Lc *, size_t);
 typedef uint32_t (*l_crc32_t)(uint32_t, const void *, size_t);
+typedef int (*ld_raw_ex_t)(Ld *, const void *, size_t, void *, size_t, size_t *, size_t *);
 
 struct LdApi {
     ld_alloc_t alloc = nullptr;
@@ -50,6 +51,7 @@ struct LdApi {
     lc_gzip_t c_gzip = nullptr;
     lc_bound_t c_bound = nullptr;
     l_crc32_t crc32 = nullptr;
+    ld_raw_ex_t raw = nullptr;
     bool ok = false, c_ok = false;
 };
 
@@ -71,6 +73,7 @@ const LdApi &ld_api()
         api.c_bound = (lc_bound_t)dlsym(h, "libdeflate_gzip_compress_bound");
         api.c_ok = api.c_alloc && api.c_free && api.c_gzip && api.c_bound;
         api.crc32 = (l_crc32_t)dlsym(h, "libdeflate_crc32");
+        api.raw = (ld_raw_ex_t)dlsym(h, "libdeflate_deflate_decompress_ex");
     });
     return api;
 }
@@ -288,6 +291,23 @@ int gunzip_members(const LdApi &api, const uint8_t *src, int64_t len, Buf &out, 
 }
 
 }  // namespace
+
+void *ld_raw_alloc()
+{
+    const LdApi &api = ld_api();
+    return api.ok && api.raw ? (void *)api.alloc() : nullptr;
+}
+
+void ld_raw_free(void *d)
+{
+    if (d) ld_api().free_((Ld *)d);
+}
+
+int ld_raw_inflate(void *d, const uint8_t *in, size_t n, char *out, size_t cap, size_t *in_used,
+                   size_t *out_used)
+{
+    return ld_api().raw((Ld *)d, in, n, out, cap, in_used, out_used);
+}
 
 constexpr size_t BIG = (size_t)4 << 20;
 

@@ -84,6 +84,13 @@ void unmap_text_file(const char *text, size_t len);
 // (mh_pinflate.cpp); -1 when it cannot be (the caller inflates serially).
 template <class Buf>
 int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int threads);
+// Raw DEFLATE (RFC 1951) through libdeflate: ld_raw_alloc() is nullptr when
+// libdeflate is absent.  ld_raw_inflate decodes in[0 .. n) up to the end of
+// its final block: 0 (*in_used, *out_used set), 1 bad data, 3 out of space.
+void *ld_raw_alloc();
+void ld_raw_free(void *d);
+int ld_raw_inflate(void *d, const uint8_t *in, size_t n, char *out, size_t cap, size_t *in_used,
+                   size_t *out_used);
 // crc32 (zlib's polynomial; libdeflate's PCLMUL code when present)
 uint32_t crc32_update(uint32_t crc, const void *p, size_t n);
 // crc32 of A then B from crc32(A), crc32(B) and the length of B

@@ -9,8 +9,11 @@
 //      its byte offset -- every bit position whose header (RFC 1951 3.2.7)
 //      parses into complete code-length and literal/length codes with an
 //      end-of-block code, then confirmed by decoding two blocks;
-//   2. decode: every span after the first inflated twice (zlib, raw) from
-//      its start to the next span's start, in place of the unknown window
+//   2. decode: every span after the first inflated twice from its start to
+//      the next span's start (libdeflate when present: the span's bits are
+//      laid out byte-aligned behind a stored block holding the window and
+//      closed by an empty final block; zlib with inflatePrime and
+//      inflateSetDictionary otherwise), in place of the unknown window
 //      once with window bytes W1[i] = i % 255 + 1 and once with W2[i] =
 //      (i / 255 + i % 255 + 1) % 255 + 1: a byte of the data comes out the
 //      same in both, a byte copied out of the window at offset i comes out
@@ -233,6 +236,49 @@ bool threads_run(int nt, const std::function<void(int)> &fn)
     return !failed;
 }
 
+// The DEFLATE bits [b0, b1) of src, byte-aligned, into in[pre ..) (the
+// caller fills in[0 .. pre)); with `close`, followed by a final empty stored
+// block (BFINAL 1, BTYPE 00, LEN 0) so that a decoder stops at b1.
+bool lay_out_span(const uint8_t *src, int64_t len, int64_t b0, int64_t b1, bool close, size_t pre,
+                  TextBuf &in)
+{
+    const int64_t nbits = b1 - b0, nb = (nbits + 7) / 8;
+    if (nbits <= 0 || (b1 + 7) / 8 > len) return false;
+    in.resize(pre + (size_t)nb + (close ? 5 : 0));
+    uint8_t *o = (uint8_t *)in.data() + pre;
+    const uint8_t *p = src + (b0 >> 3);
+    const int r = (int)(b0 & 7);
+    const int64_t avail = len - (b0 >> 3);   // readable bytes from p
+    int64_t j = 0;
+    if (r == 0) {
+        memcpy(o, p, (size_t)nb);
+        j = nb;
+    } else {
+        for (; j + 8 < nb && j + 9 <= avail; j += 8) {
+            uint64_t x;
+            memcpy(&x, p + j, 8);
+            const uint64_t y = (x >> r) | ((uint64_t)p[j + 8] << (64 - r));
+            memcpy(o + j, &y, 8);
+        }
+        for (; j < nb; ++j)
+            o[j] = (uint8_t)((p[j] >> r) | (j + 1 < avail ? p[j + 1] << (8 - r) : 0));
+    }
+    const int tail = (int)(nbits & 7);
+    if (!close) return true;
+    // the closing block's 3 header bits at bit nbits, then LEN 0 / NLEN 0xffff
+    int64_t at = nb;
+    if (tail) {
+        o[nb - 1] &= (uint8_t)((1u << tail) - 1);
+        if (tail <= 5) o[nb - 1] |= (uint8_t)(1u << tail);
+        else { o[nb - 1] |= (uint8_t)(1u << tail); o[at++] = 0; }   // BTYPE spills into a new byte
+    } else {
+        o[at++] = 1;
+    }
+    o[at++] = 0; o[at++] = 0; o[at++] = 0xff; o[at++] = 0xff;
+    in.resize(pre + (size_t)at);
+    return true;
+}
+
 inline uint32_t rd32(const uint8_t *p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
 
 // end of the gzip header at src (RFC 1952), or -1
@@ -310,9 +356,66 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
         w2[(size_t)i] = (uint8_t)((i / 255 + i % 255 + 1) % 255 + 1);
     }
     std::vector<TextBuf> p1((size_t)K), p2((size_t)K);
-    std::vector<int64_t> e1((size_t)K, -1), e2((size_t)K, -1);
+    std::vector<size_t> skip((size_t)K, 0);   // bytes of p1 / p2 before the span's data
     std::atomic<int> bad(0);
-    {
+    // MICALL_ZLIB_SPANS=1: the zlib span decode even when libdeflate is present
+    static const bool zlib_spans = getenv("MICALL_ZLIB_SPANS") && *getenv("MICALL_ZLIB_SPANS") == '1';
+    void *probe_ld = zlib_spans ? nullptr : ld_raw_alloc();
+    if (probe_ld) {
+        ld_raw_free(probe_ld);
+        // libdeflate (raw, no dictionary or bit-offset API): each span is
+        // re-laid out byte-aligned behind a stored block holding the window
+        // (so back-references reach it), and a final empty stored block is
+        // put where the next span starts, so the decode ends there
+        std::atomic<int> next(0);
+        if (!threads_run(std::min(K, threads), [&](int) {
+            void *d = ld_raw_alloc();
+            if (!d) { bad = 1; return; }
+            TextBuf in;
+            for (int k; (k = next.fetch_add(1)) < K;) {
+                const bool last = k + 1 == K;
+                const int64_t b0 = st[(size_t)k], b1 = last ? dend * 8 : st[(size_t)k + 1];
+                const size_t pre = k ? 5 + WIN : 0;
+                if (!lay_out_span(src, len, b0, b1, !last, pre, in)) { bad = 1; break; }
+                for (int which = 1; which <= (k ? 2 : 1); ++which) {
+                    if (k) {
+                        uint8_t *w = (uint8_t *)in.data();
+                        w[0] = 0; w[1] = 0x00; w[2] = 0x80; w[3] = 0xff; w[4] = 0x7f;   // LEN 32768
+                        memcpy(w + 5, which == 1 ? w1.data() : w2.data(), WIN);
+                    }
+                    TextBuf &dst = which == 1 ? p1[(size_t)k] : p2[(size_t)k];
+                    size_t cap = (size_t)WIN + (size_t)((b1 - b0) / 8) * 6 + ((size_t)1 << 20);
+                    for (;;) {
+                        dst.resize(cap);
+                        size_t in_used = 0, out_used = 0;
+                        const int r = ld_raw_inflate(d, (const uint8_t *)in.data(), in.size(), dst.data(),
+                                                     cap, &in_used, &out_used);
+                        if (r == 3) { cap *= 2; continue; }
+                        // the last span ends inside its last byte: libdeflate may
+                        // leave that byte uncounted
+                        const size_t unread = in.size() - std::min(in_used, in.size());
+                        if (r != 0 || unread > (last ? 1u : 0u) || out_used < (k ? (size_t)WIN : 0)) {
+                            if (trace)
+                                fprintf(stderr, "pinflate span %d rc %d in %zu of %zu out %zu\n", k, r, in_used,
+                                        in.size(), out_used);
+                            bad = 1;
+                            break;
+                        }
+                        dst.resize(out_used);
+                        break;
+                    }
+                    if (bad) break;
+                }
+                skip[(size_t)k] = k ? WIN : 0;
+                if (bad) break;
+            }
+            ld_raw_free(d);
+        }))
+            bad = 1;
+        mark("decode");
+        if (bad) return -1;
+    } else {
+        std::vector<int64_t> e1((size_t)K, -1), e2((size_t)K, -1);
         std::vector<std::pair<int, int>> jobs{{0, 1}};   // (span, window 1 / 2)
         for (int k = 1; k < K; ++k) { jobs.emplace_back(k, 1); jobs.emplace_back(k, 2); }
         std::atomic<size_t> next(0);
@@ -328,13 +431,15 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
             }
         }))
             bad = 1;
+        mark("decode");
+        if (bad || (e1[(size_t)K - 1] + 7) / 8 != dend) return -1;
+        for (int k = 1; k < K; ++k)
+            if (e1[(size_t)k] != e2[(size_t)k]) return -1;
     }
-    mark("decode");
-    if (bad || (e1[(size_t)K - 1] + 7) / 8 != dend) return -1;
     std::vector<size_t> off((size_t)K + 1, 0), dirty((size_t)K, 0);
     for (int k = 0; k < K; ++k) {
-        if (k && (e1[(size_t)k] != e2[(size_t)k] || p1[(size_t)k].size() != p2[(size_t)k].size())) return -1;
-        off[(size_t)k + 1] = off[(size_t)k] + p1[(size_t)k].size();
+        if (k && p1[(size_t)k].size() != p2[(size_t)k].size()) return -1;
+        off[(size_t)k + 1] = off[(size_t)k] + p1[(size_t)k].size() - skip[(size_t)k];
     }
     // the first span's output must hold a whole window
     if ((uint32_t)off[(size_t)K] != isize || off[1] < (size_t)WIN) return -1;
@@ -344,8 +449,9 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
         std::atomic<int> next(0);
         threads_run(std::min(K, threads), [&](int) {
             for (int k; (k = next.fetch_add(1)) < K;) {
-                const char *a1 = p1[(size_t)k].data(), *a2 = k ? p2[(size_t)k].data() : nullptr;
-                const size_t n = p1[(size_t)k].size();
+                const char *a1 = p1[(size_t)k].data() + skip[(size_t)k];
+                const char *a2 = k ? p2[(size_t)k].data() + skip[(size_t)k] : nullptr;
+                const size_t n = p1[(size_t)k].size() - skip[(size_t)k];
                 memcpy(o + off[(size_t)k], a1, n);
                 if (k) {   // the last window-derived byte: the end of the dirty prefix
                     size_t i = n;
@@ -367,17 +473,29 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
     // 3. every window-derived byte replaced by the window byte it copies:
     // the last 32 KiB of every span in order (they are the next span's
     // window), then the rest of every span at once
+    // window offset of each (W1, W2) byte pair, 0xffff where none
+    std::vector<uint16_t> at_of(65536, 0xffff);
+    for (int i = 0; i < WIN; ++i) at_of[(size_t)w1[(size_t)i] << 8 | w2[(size_t)i]] = (uint16_t)i;
     auto resolve = [&](int k, size_t i0, size_t i1) {
         char *span = o + off[(size_t)k];
         const char *wb = o + off[(size_t)k] - WIN;
-        const uint8_t *B = (const uint8_t *)p2[(size_t)k].data();
-        for (size_t i = i0; i < i1; ++i) {
-            const int a1 = (uint8_t)span[i], a2 = B[i];
-            if (a1 == a2) continue;                        // a byte of the data
-            const int r = a1 - 1, q = (a2 - r - 2 + 2 * 255) % 255;
-            const int idx = 255 * q + r;
-            if (a1 == 0 || idx >= WIN) { bad = 1; return; }
-            span[i] = wb[idx];
+        const uint8_t *B = (const uint8_t *)p2[(size_t)k].data() + skip[(size_t)k];
+        const uint16_t *T = at_of.data();
+        for (size_t i = i0; i < i1;) {
+            if (i + 8 <= i1) {                             // 8 bytes of the data
+                uint64_t x, y;
+                memcpy(&x, span + i, 8);
+                memcpy(&y, B + i, 8);
+                if (x == y) { i += 8; continue; }
+            }
+            const size_t e = std::min(i + 8, i1);
+            for (; i < e; ++i) {
+                const int a1 = (uint8_t)span[i], a2 = B[i];
+                if (a1 == a2) continue;                    // a byte of the data
+                const int idx = T[a1 << 8 | a2];
+                if (idx == 0xffff) { bad = 1; return; }
+                span[i] = wb[idx];
+            }
         }
     };
     for (int k = 1; k < K; ++k) {   // the tails, in order

@@ -320,3 +320,32 @@ def test_single_member_parallel_inflate(tmp_path, level, nul):
     assert 'pinflate crc' in err, err[-2000:]
     got, err = _pinflate_run(path, {'MICALL_SERIAL_INFLATE': '1'})
     assert got == want and 'pinflate' not in err
+
+
+def test_single_member_parallel_inflate_high_ratio(tmp_path):
+    """A member that compresses ~7:1 (reads drawn from a small pool): each
+    span's decode outgrows the output size first guessed for it and is run
+    again with a larger buffer; the bytes still equal a plain inflate's, and
+    the zlib span decode (MICALL_ZLIB_SPANS=1) gives the same."""
+    import hashlib
+    import numpy as np
+    rng = np.random.default_rng(3)
+    pool_b = np.frombuffer(b'ACGT', dtype=np.uint8)[rng.integers(0, 4, (64, 151))]
+    pool_q = (rng.integers(30, 41, (64, 151)) + 33).astype(np.uint8)
+    n = 190000
+    pick_b, pick_q = rng.integers(0, 64, n), rng.integers(0, 64, n)
+    lines = []
+    for i in range(n):
+        lines.append(b'@M01:1:FC:1:%d:%d:%d 1:N:0:1\n' % (1101 + i % 4, i % 50, i % 70))
+        lines.append(pool_b[pick_b[i]].tobytes() + b'\n+\n' + pool_q[pick_q[i]].tobytes() + b'\n')
+    text = b''.join(lines)
+    path = str(tmp_path / 'R1.fastq.gz')
+    with gzip.GzipFile(path, 'wb', compresslevel=6) as f:
+        f.write(text)
+    assert os.path.getsize(path) > (8 << 20)
+    assert len(text) > 6 * os.path.getsize(path)
+    want = hashlib.sha256(text).hexdigest()
+    for extra in ({}, {'MICALL_ZLIB_SPANS': '1'}):
+        got, err = _pinflate_run(path, extra)
+        assert got == want
+        assert 'pinflate crc' in err, err[-2000:]
