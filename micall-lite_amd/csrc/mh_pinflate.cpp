@@ -39,6 +39,7 @@
 #include <atomic>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -445,92 +446,105 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
     if ((uint32_t)off[(size_t)K] != isize || off[1] < (size_t)WIN) return -1;
     out.resize(off[(size_t)K]);
     char *o = &out[0];
-    {
-        std::atomic<int> next(0);
-        threads_run(std::min(K, threads), [&](int) {
-            for (int k; (k = next.fetch_add(1)) < K;) {
-                const char *a1 = p1[(size_t)k].data() + skip[(size_t)k];
-                const char *a2 = k ? p2[(size_t)k].data() + skip[(size_t)k] : nullptr;
-                const size_t n = p1[(size_t)k].size() - skip[(size_t)k];
-                memcpy(o + off[(size_t)k], a1, n);
-                if (k) {   // the last window-derived byte: the end of the dirty prefix
-                    size_t i = n;
-                    while (i >= 8) {
-                        uint64_t x, y;
-                        memcpy(&x, a1 + i - 8, 8);
-                        memcpy(&y, a2 + i - 8, 8);
-                        if (x != y) break;
-                        i -= 8;
-                    }
-                    while (i > 0 && a1[i - 1] == a2[i - 1]) --i;
-                    dirty[(size_t)k] = i;
-                }
-                p1[(size_t)k].release();
-            }
-        });
-    }
-    mark("place");
-    // 3. every window-derived byte replaced by the window byte it copies:
-    // the last 32 KiB of every span in order (they are the next span's
-    // window), then the rest of every span at once
-    // window offset of each (W1, W2) byte pair, 0xffff where none
-    std::vector<uint16_t> at_of(65536, 0xffff);
+    // 3. the output placed with every window-derived byte replaced by the
+    // window byte it copies: the end of each span's dirty prefix (its last
+    // window-derived byte) first; then the last 32 KiB of every span in
+    // order (each is the next span's window); then the rest of every span
+    // at once, each span's CRC-32 taken while it is in cache
+    std::vector<uint16_t> at_of(65536, 0xffff);   // window offset of a (W1, W2) byte pair
     for (int i = 0; i < WIN; ++i) at_of[(size_t)w1[(size_t)i] << 8 | w2[(size_t)i]] = (uint16_t)i;
-    auto resolve = [&](int k, size_t i0, size_t i1) {
-        char *span = o + off[(size_t)k];
+    auto span_len = [&](int k) { return off[(size_t)k + 1] - off[(size_t)k]; };
+    auto tail0 = [&](int k) { return span_len(k) > (size_t)WIN ? span_len(k) - WIN : (size_t)0; };
+    // bytes [i0, i1) of span k into place
+    auto place = [&](int k, size_t i0, size_t i1) {
+        if (i0 >= i1) return;
+        char *dst = o + off[(size_t)k];
+        const char *A = p1[(size_t)k].data() + skip[(size_t)k];
+        const size_t d = std::min(std::max(dirty[(size_t)k], i0), i1);   // clean from d on
+        if (d < i1) memcpy(dst + d, A + d, i1 - d);
+        if (i0 >= d) return;
         const char *wb = o + off[(size_t)k] - WIN;
         const uint8_t *B = (const uint8_t *)p2[(size_t)k].data() + skip[(size_t)k];
         const uint16_t *T = at_of.data();
-        for (size_t i = i0; i < i1;) {
-            if (i + 8 <= i1) {                             // 8 bytes of the data
+        for (size_t i = i0; i < d;) {
+            if (i + 8 <= d) {                              // 8 bytes of the data
                 uint64_t x, y;
-                memcpy(&x, span + i, 8);
+                memcpy(&x, A + i, 8);
                 memcpy(&y, B + i, 8);
-                if (x == y) { i += 8; continue; }
+                if (x == y) { memcpy(dst + i, &x, 8); i += 8; continue; }
             }
-            const size_t e = std::min(i + 8, i1);
+            const size_t e = std::min(i + 8, d);
             for (; i < e; ++i) {
-                const int a1 = (uint8_t)span[i], a2 = B[i];
-                if (a1 == a2) continue;                    // a byte of the data
+                const int a1 = (uint8_t)A[i], a2 = B[i];
+                if (a1 == a2) { dst[i] = (char)a1; continue; }   // a byte of the data
                 const int idx = T[a1 << 8 | a2];
                 if (idx == 0xffff) { bad = 1; return; }
-                span[i] = wb[idx];
+                dst[i] = wb[idx];
             }
         }
     };
-    for (int k = 1; k < K; ++k) {   // the tails, in order
-        const size_t n = off[(size_t)k + 1] - off[(size_t)k];
-        const size_t t0 = n > (size_t)WIN ? n - WIN : 0;
-        if (dirty[(size_t)k] > t0) resolve(k, t0, dirty[(size_t)k]);
-    }
     {
         std::atomic<int> next(1);
         threads_run(std::min(K, threads), [&](int) {
             for (int k; (k = next.fetch_add(1)) < K;) {
-                const size_t n = off[(size_t)k + 1] - off[(size_t)k];
-                const size_t t0 = n > (size_t)WIN ? n - WIN : 0;
-                resolve(k, 0, std::min(dirty[(size_t)k], t0));
-                p2[(size_t)k].release();
+                const char *a1 = p1[(size_t)k].data() + skip[(size_t)k];
+                const char *a2 = p2[(size_t)k].data() + skip[(size_t)k];
+                size_t i = span_len(k);
+                while (i >= 8) {
+                    uint64_t x, y;
+                    memcpy(&x, a1 + i - 8, 8);
+                    memcpy(&y, a2 + i - 8, 8);
+                    if (x != y) break;
+                    i -= 8;
+                }
+                while (i > 0 && a1[i - 1] == a2[i - 1]) --i;
+                dirty[(size_t)k] = i;
             }
         });
     }
-    mark("fix");
+    mark("dirty");
+    for (int k = 0; k < K; ++k) place(k, tail0(k), span_len(k));   // the tails, in order
+    // the rest in pieces of about 4 MiB (a piece reads only its span's
+    // window, which is in place), each piece's CRC-32 taken while in cache
+    struct Piece { int k; size_t a, b; };
+    std::vector<Piece> pieces;
+    for (int k = 0; k < K; ++k) {
+        const size_t n = span_len(k), t0 = tail0(k);
+        const size_t np = std::max<size_t>(1, n >> 22);
+        for (size_t j = 0; j < np; ++j) {
+            const size_t a = n * j / np, b = j + 1 < np ? n * (j + 1) / np : n;
+            pieces.push_back({k, a, b});
+        }
+        (void)t0;
+    }
+    std::vector<uint32_t> crc(pieces.size(), 0);
+    {
+        std::atomic<size_t> next(0);
+        threads_run(std::min<int>((int)pieces.size(), threads), [&](int) {
+            for (size_t j; (j = next.fetch_add(1)) < pieces.size();) {
+                const Piece &pc = pieces[j];
+                place(pc.k, pc.a, std::min(pc.b, tail0(pc.k)));
+                crc[j] = crc32_update(0, o + off[(size_t)pc.k] + pc.a, pc.b - pc.a);
+            }
+        });
+    }
+    mark("place");
+    {   // the decodes freed on a detached thread
+        auto hold = std::make_shared<std::pair<std::vector<TextBuf>, std::vector<TextBuf>>>(std::move(p1),
+                                                                                       std::move(p2));
+        std::thread([hold]() { hold->first.clear(); hold->second.clear(); }).detach();
+    }
+    mark("free");
     if (trace) {
         size_t d = 0;
         for (size_t x : dirty) d += x;
         fprintf(stderr, "pinflate spans %d dirty bytes %zu\n", K, d);
     }
     if (bad) return -1;
-    // 4. CRC-32 of the whole output, in parallel pieces
-    const size_t total = off[(size_t)K];
-    const int P = std::max(1, std::min<int>(threads, (int)(total >> 22) + 1));
-    std::vector<uint32_t> crc((size_t)P, 0);
-    threads_run(P, [&](int t) {
-        const size_t a = total * t / P, b = total * (t + 1) / P;
-        crc[(size_t)t] = crc32_update(0, o + a, b - a);
-    });
+    // 4. the CRC-32 of the whole output against the trailer
     uint32_t all = 0;
-    for (int t = 0; t < P; ++t) all = crc32_join(all, crc[(size_t)t], (int64_t)(total * (t + 1) / P - total * t / P));
+    for (size_t j = 0; j < pieces.size(); ++j)
+        all = crc32_join(all, crc[j], (int64_t)(pieces[j].b - pieces[j].a));
     mark("crc");
     return all == crc_want ? 0 : -1;
 }

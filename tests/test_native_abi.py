@@ -95,3 +95,17 @@ def test_levenshtein_batch_keeps_pair_order():
     assert got == [_native.levenshtein(a, b) for a, b in pairs]
     import oracle
     assert got[:8] == [oracle.levenshtein(a, b) for a, b in pairs[:8]]
+
+
+def test_crc32_combine_matches_zlib(native):
+    """mh_crc32_combine (the CRC-32 of A ++ B from crc(A), crc(B), |B|; the
+    shift by |B| bytes as products of precomputed x^(2^k) mod P) equals
+    zlib.crc32 of the concatenation, empty and odd lengths included."""
+    import random
+    import zlib
+    rng = random.Random(5)
+    for _ in range(300):
+        a = rng.randbytes(rng.randint(0, 3000))
+        b = rng.randbytes(rng.choice([0, 1, 2, 7, 8, 100, 4095, 70000]))
+        got = native.crc32_combine(zlib.crc32(a), zlib.crc32(b), len(b))
+        assert got == zlib.crc32(a + b)
