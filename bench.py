@@ -722,6 +722,13 @@ def bench_chain(args):
     gap = float(os.environ.get('MICALL_CHAIN_GAP_S', '0'))   # diagnostics: idle seconds between stages
 
     def run():
+        # bin/micall writes each sample's outputs into a fresh directory:
+        # the previous run's outputs are removed, untimed, so that opening
+        # them does not truncate 2.4 GB of files (an ext4 / overlay truncate
+        # also makes close() flush the file: 0.3 s + 0.3 s on the box)
+        for path in P.values():
+            if os.path.exists(path):
+                os.unlink(path)
         times = {}
         t = time.perf_counter()
         for src, dst in ((r1, P['c1.fastq.gz']), (r2, P['c2.fastq.gz'])):
