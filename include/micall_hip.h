@@ -346,7 +346,9 @@ int mh_sam2aln_output(mh_ctx *ctx, int which, char *buf, size_t cap, size_t *use
  * the caller reads the file itself), or an error. */
 int mh_sam2aln_file(mh_ctx *ctx, int fd, int q_cutoff, double max_prop_n, int64_t *n_units);
 /* Output `which` (as mh_sam2aln_output) written to fd at offset with
- * pwrite (the descriptor's own offset is not used); *written = its size. */
+ * pwrite (the descriptor's own offset is not used); *written = its size.
+ * Not sized before (no mh_sam2aln_output size query), it is formatted and
+ * written in one pass, the writes overlapping the formatting. */
 int mh_sam2aln_write(mh_ctx *ctx, int which, int fd, int64_t offset, int64_t *written);
 /* out[0] pairs, out[1] pairs merged on the device, out[2] distinct merged
  * sequences, out[3] failed pairs. */

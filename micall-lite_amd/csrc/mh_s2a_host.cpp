@@ -8,6 +8,9 @@
 // Threads: min(16, hardware threads, OMP_NUM_THREADS); output is identical
 // for any thread count.
 #include <algorithm>
+#include <memory>
+#include <cerrno>
+#include <unistd.h>
 #include <atomic>
 #include <charconv>
 #include <chrono>
@@ -501,23 +504,96 @@ static void parallel_sort(std::vector<int64_t> &v, Cmp cmp, int nt)
 
 // the pieces fn(t, range) writes for nt ranges of [0, n), appended in order
 using Pieces = std::vector<std::string>;
-static void parallel_text(int64_t n, int nt, Pieces &out,
+
+// Where an output's text goes, in order: collected as pieces (out), or
+// written to fd from pos (pwrite) as each piece is finished.
+struct TextSink {
+    Pieces *out = nullptr;
+    int fd = -1;
+    int64_t pos = 0;
+    int err = 0;    // errno of a failed write
+    void put(std::string &s)
+    {
+        if (out) {
+            if (!s.empty()) out->push_back(std::move(s));
+            return;
+        }
+        const char *p = s.data();
+        size_t left = s.size();
+        while (left > 0 && !err) {
+            const ssize_t w = pwrite(fd, p, left, (off_t)pos);
+            if (w <= 0) { err = errno ? errno : EIO; break; }
+            p += (size_t)w;
+            left -= (size_t)w;
+            pos += w;
+        }
+        std::string().swap(s);
+    }
+};
+
+// fn(text, a, b) formats items [a, b) of n.  Collected: one piece per
+// thread.  Streamed: jobs of STREAM_ROWS items on nt - 1 formatting threads
+// while this thread writes the finished jobs in order, so the writing of a
+// GB-sized output overlaps its formatting.
+constexpr int64_t STREAM_ROWS = 4096;
+static void parallel_text(int64_t n, int nt, TextSink &sink,
                           const std::function<void(std::string &, int64_t, int64_t)> &fn)
 {
     if (n < 4096) nt = 1;
-    std::vector<std::string> piece(nt);
-    parallel_for(nt, [&](int t) { fn(piece[t], n * t / nt, n * (t + 1) / nt); });
-    for (auto &x : piece)
-        if (!x.empty()) out.push_back(std::move(x));
+    if (sink.out) {
+        std::vector<std::string> piece(nt);
+        parallel_for(nt, [&](int t) { fn(piece[t], n * t / nt, n * (t + 1) / nt); });
+        for (auto &x : piece) sink.put(x);
+        return;
+    }
+    const int64_t nj = (n + STREAM_ROWS - 1) / STREAM_ROWS;
+    if (nt <= 1 || nj <= 1) {
+        std::string one;
+        fn(one, 0, n);
+        sink.put(one);
+        return;
+    }
+    std::vector<std::string> buf((size_t)nj);
+    std::unique_ptr<std::atomic<int>[]> done(new std::atomic<int>[(size_t)nj]);
+    for (int64_t j = 0; j < nj; ++j) done[j].store(0);
+    std::atomic<int64_t> next(0);
+    std::atomic<int> failed(0);
+    std::exception_ptr exc;
+    std::mutex mu;
+    auto work = [&]() {
+        try {
+            for (int64_t j; !failed && (j = next.fetch_add(1)) < nj;) {
+                fn(buf[(size_t)j], j * STREAM_ROWS, std::min(n, (j + 1) * STREAM_ROWS));
+                done[j].store(1, std::memory_order_release);
+            }
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!exc) exc = std::current_exception();
+            failed = 1;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::max(1, nt - 1); ++t) th.emplace_back(work);
+    for (int64_t j = 0; j < nj && !failed && !sink.err; ++j) {
+        while (!done[j].load(std::memory_order_acquire) && !failed) std::this_thread::yield();
+        if (failed) break;
+        sink.put(buf[(size_t)j]);
+    }
+    failed = 1;   // a write error: the formatters stop at their next job
+    for (auto &x : th) x.join();
+    if (exc) std::rethrow_exception(exc);
 }
 
 // aligned.csv (sam2aln.py:459-478): per rname in first-seen order, the
 // distinct merged sequences sorted by (count, gap prefix, sequence), all
 // descending; seq written without its leading / trailing gaps
-static void s2a_aligned(const S2AState &S, Pieces &out)
+static void s2a_aligned(const S2AState &S, TextSink &out)
 {
     const int nt = s2a_threads();
-    out.assign(1, "refname,qcut,rank,count,offset,seq\n");
+    {
+        std::string head("refname,qcut,rank,count,offset,seq\n");
+        out.put(head);
+    }
     const int nn = (int)S.names.size();
     std::vector<int32_t> mref(S.n_merge);
     for (int64_t u = 0; u < (int64_t)S.u1.size(); ++u)
@@ -561,7 +637,9 @@ static void s2a_aligned(const S2AState &S, Pieces &out)
         });
         std::string ref;
         csv_field(ref, S.names[r].data(), S.names[r].size());
+        const size_t row_guess = ref.size() + 40 + (S.n_unique ? (size_t)(S.gathered.size() / S.n_unique) : 0);
         parallel_text((int64_t)v.size(), nt, out, [&](std::string &o, int64_t a, int64_t b) {
+            o.reserve(o.size() + (size_t)(b - a) * row_guess);
             for (int64_t rank = a; rank < b; ++rank) {
                 const int64_t k = v[rank], rep = S.uniq[2 * k];
                 o += ref;
@@ -583,9 +661,12 @@ static void s2a_aligned(const S2AState &S, Pieces &out)
 
 // insert.csv rows of parse_sam (sam2aln.py:357-380): every I op of the
 // mates of a unit that reached apply_cigar, at pos - 1 + read offset
-static void s2a_inserts(const S2AState &S, Pieces &out)
+static void s2a_inserts(const S2AState &S, TextSink &out)
 {
-    out.assign(1, "qname,fwd_rev,refname,pos,insert,qual\n");
+    {
+        std::string head("qname,fwd_rev,refname,pos,insert,qual\n");
+        out.put(head);
+    }
     parallel_text((int64_t)S.u1.size(), s2a_threads(), out, [&](std::string &o, int64_t a, int64_t b) {
         for (int64_t u = a; u < b; ++u) {
             if (S.ucause[u] >= 0) continue;
@@ -616,9 +697,12 @@ static void s2a_inserts(const S2AState &S, Pieces &out)
     });
 }
 
-static void s2a_failed(const S2AState &S, Pieces &out)
+static void s2a_failed(const S2AState &S, TextSink &out)
 {
-    out.assign(1, "qname,cause\n");
+    {
+        std::string head("qname,cause\n");
+        out.put(head);
+    }
     parallel_text((int64_t)S.u1.size(), s2a_threads(), out, [&](std::string &o, int64_t a, int64_t b) {
         for (int64_t u = a; u < b; ++u) {
             int cause = S.ucause[u];
@@ -633,12 +717,30 @@ static void s2a_failed(const S2AState &S, Pieces &out)
     });
 }
 
+static void s2a_emit(const S2AState &S, int which, TextSink &sink)
+{
+    if (which == 0) s2a_aligned(S, sink);
+    else if (which == 1) s2a_inserts(S, sink);
+    else s2a_failed(S, sink);
+}
+
 int s2a_format(const S2AState &S, int which, std::vector<std::string> &out)
 {
-    if (which == 0) s2a_aligned(S, out);
-    else if (which == 1) s2a_inserts(S, out);
-    else s2a_failed(S, out);
+    out.clear();
+    TextSink sink;
+    sink.out = &out;
+    s2a_emit(S, which, sink);
     return 0;
+}
+
+int s2a_format_write(const S2AState &S, int which, int fd, int64_t offset, int64_t *written)
+{
+    TextSink sink;
+    sink.fd = fd;
+    sink.pos = offset;
+    s2a_emit(S, which, sink);
+    if (written) *written = sink.pos - offset;
+    return sink.err;
 }
 
 }  // namespace mh

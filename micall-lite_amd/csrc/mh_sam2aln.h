@@ -73,6 +73,8 @@ struct S2AState {
 // host half
 int s2a_parse(S2AState &S, const char *text, int64_t len);
 int s2a_format(const S2AState &S, int which, std::vector<std::string> &out);
+// the same text written to fd from offset while it is formatted; 0 or errno
+int s2a_format_write(const S2AState &S, int which, int fd, int64_t offset, int64_t *written);
 int s2a_threads();
 // device half
 int s2a_run(Ctx &c, S2AState &S, double max_prop_n);

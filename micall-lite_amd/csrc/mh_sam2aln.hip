@@ -632,9 +632,28 @@ extern "C" int mh_sam2aln_file(mh_ctx *ctx, int fd, int q_cutoff, double max_pro
 
 extern "C" int mh_sam2aln_write(mh_ctx *ctx, int which, int fd, int64_t offset, int64_t *written)
 {
+    if (!ctx || which < 0 || which > 2 || fd < 0 || offset < 0) return -3;
+    Ctx &c = *ctx_of(ctx);
+    if (!c.s2a) { set_error("mh_sam2aln_write: no sam2aln results"); return -3; }
+    if (!(c.s2a->out_valid & (1 << which))) {
+        // not formatted yet (no size query before): formatted and written
+        // together, the writes overlapping the formatting
+        S2AState &S = *c.s2a;
+        auto t0 = std::chrono::steady_clock::now();
+        int err = 0;
+        try {
+            err = s2a_format_write(S, which, fd, offset, written);
+        } catch (const std::exception &e) {
+            set_error("mh_sam2aln_write: out of memory (%s)", e.what());
+            return -2;
+        }
+        S.t_format[which] = std::chrono::duration<double, std::milli>(
+                                std::chrono::steady_clock::now() - t0).count();
+        if (err) { set_error("mh_sam2aln_write: write failed (%s)", strerror(err)); return -4; }
+        return 0;
+    }
     size_t used = 0;
     if (int st = mh_sam2aln_output(ctx, which, nullptr, 0, &used)) return st;
-    if (fd < 0 || offset < 0) return -3;
     S2AState &S = *ctx_of(ctx)->s2a;
     int64_t pos = offset;
     for (const std::string &piece : S.out_cache[which]) {

@@ -48,7 +48,8 @@ def _write_output(ctx, which, handle):
     from .sharded_io import SharedOutput
     out = SharedOutput(None, handle)
     if out.direct:
-        ctx.sam2aln_write(which, out.fd, int(out.place([ctx.sam2aln_size(which)])[0]))
+        # formatted and written together (pwrite from the handle's position)
+        out.end += ctx.sam2aln_write(which, out.fd, int(out.end))
         out.finish()
     else:
         handle.write(ctx.sam2aln_output(which))
