@@ -382,6 +382,14 @@ int mh_censor_output(mh_ctx *ctx, char *buf, size_t cap, size_t *used);
 /* The held censored output written to fd at offset (pwrite; the descriptor's
  * own offset is not used); *written = its size.  The output is released. */
 int mh_censor_write(mh_ctx *ctx, int fd, int64_t offset, int64_t *written);
+/* mh_censor_staged, the output written to fd from offset (pwrite) while it
+ * is made: each gzip member (or text block) as soon as it and those before
+ * it are done; *written = bytes written.  Nothing is kept for
+ * mh_censor_output / mh_censor_write.  Replaces the same censor_fastq.py:
+ * 32-102 call as mh_censor_staged + mh_censor_write. */
+int mh_censor_staged_write(mh_ctx *ctx, mh_fastq *fq, int n_bad, const char *const *tiles,
+                           const int32_t *cycles, int dst_gzip, int fd, int64_t offset,
+                           int64_t *written, int64_t *base_count, int64_t *score_sum);
 /* Host wall ms of the last call: [0] gunzip + record split, [1] upload +
  * k_censor + download, [2] rewrite + gzip. */
 int mh_censor_timing(mh_ctx *ctx, double *ms3);

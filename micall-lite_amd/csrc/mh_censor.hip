@@ -25,10 +25,12 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <cstring>
 #include <exception>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <string_view>
@@ -54,6 +56,11 @@ struct CensorState {
     std::vector<int32_t> keep;              // 2 per record: kept seq / qual length
     int64_t base_count = 0, score_sum = 0;
     TextBuf out;                            // the censored file (gzip members or text)
+    // set: the blocks are written to sink_fd from sink_pos as they are made
+    // (mh_censor_staged_write) instead of collected in out
+    int sink_fd = -1;
+    int64_t sink_pos = 0;
+    int sink_err = 0;
     double t_host_in = 0, t_device = 0, t_host_out = 0;
     // device buffers, grown on demand and kept between calls
     uint8_t *d_text = nullptr;
@@ -380,16 +387,50 @@ static int censor_emit(CensorState &C, int dst_gzip)
         if (dst_gzip) {   // an empty FASTQ still makes one (empty) gzip member
             if (gzip_member("", 0, C.out, 1)) { set_error("censor: deflate failed"); return -2; }
         }
+        if (C.sink_fd >= 0 && C.out.size()) {
+            const ssize_t w = pwrite(C.sink_fd, C.out.data(), C.out.size(), (off_t)C.sink_pos);
+            if (w != (ssize_t)C.out.size()) {
+                set_error("censor: write failed (%s)", strerror(errno ? errno : EIO));
+                return -4;
+            }
+            C.sink_pos += w;
+            C.out.clear();
+        }
         return 0;
     }
     std::vector<TextBuf> part((size_t)nb);
     std::atomic<int64_t> next(0);
     std::atomic<int> err(0);
-    const int nt = std::max(1, std::min<int>(s2a_threads(), (int)nb));
     const char *T = C.text.data();
-    cz_parallel(nt, [&](int) {
+    const bool stream = C.sink_fd >= 0;
+    // streamed: thread 0 writes the blocks in order as the others finish them
+    const int nt = std::max(stream ? 2 : 1, std::min<int>(s2a_threads(), (int)nb + (stream ? 1 : 0)));
+    std::unique_ptr<std::atomic<int>[]> done(new std::atomic<int>[(size_t)nb]);
+    for (int64_t b = 0; b < nb; ++b) done[b].store(0);
+    std::atomic<int> dead(0);   // a block maker failed: the writer stops waiting
+    auto write_blocks = [&]() {
+        for (int64_t b = 0; b < nb; ++b) {
+            while (!done[b].load(std::memory_order_acquire) && !dead) std::this_thread::yield();
+            if (dead || err) return;
+            const char *p = part[(size_t)b].data();
+            size_t left = part[(size_t)b].size();
+            while (left > 0) {
+                const ssize_t w = pwrite(C.sink_fd, p, left, (off_t)C.sink_pos);
+                if (w <= 0) { C.sink_err = errno ? errno : EIO; dead = 1; return; }
+                p += w; left -= (size_t)w; C.sink_pos += w;
+            }
+            part[(size_t)b].release();
+        }
+    };
+    cz_parallel(nt, [&](int t) {
+        if (stream && t == 0) { write_blocks(); return; }
         TextBuf raw;
-        for (int64_t b; (b = next.fetch_add(1)) < nb;) {
+        struct Dead {   // a throw out of a block maker releases the writer
+            std::atomic<int> &d;
+            bool ok = false;
+            ~Dead() { if (!ok) d = 1; }
+        } guard{dead};
+        for (int64_t b; !dead && (b = next.fetch_add(1)) < nb;) {
             const int64_t r0 = bstart[(size_t)b], r1 = bstart[(size_t)b + 1];
             const int64_t in_end = r1 < nr ? C.h0[r1] : n;
             TextBuf &dst = dst_gzip ? raw : part[(size_t)b];
@@ -406,10 +447,16 @@ static int censor_emit(CensorState &C, int dst_gzip)
                 *o++ = '\n';
             }
             dst.resize((size_t)(o - dst.data()));
-            if (dst_gzip && gzip_member(raw.data(), raw.size(), part[(size_t)b], 1)) err = 1;
+            if (dst_gzip && gzip_member(raw.data(), raw.size(), part[(size_t)b], 1)) { err = 1; dead = 1; }
+            done[b].store(1, std::memory_order_release);
         }
+        guard.ok = true;
     });
     if (err) { set_error("censor: deflate failed"); return -2; }
+    if (stream) {
+        if (C.sink_err) { set_error("censor: write failed (%s)", strerror(C.sink_err)); return -4; }
+        return 0;
+    }
     std::vector<size_t> off((size_t)nb + 1, 0);
     for (int64_t b = 0; b < nb; ++b) off[(size_t)b + 1] = off[(size_t)b] + part[(size_t)b].size();
     C.out.resize(off[(size_t)nb]);
@@ -517,6 +564,33 @@ extern "C" int mh_censor_staged(mh_ctx *ctx, mh_fastq *fq, int n_bad, const char
     C.text.swap(text);
     if (int st = censor_text_guarded(c, C, n_bad, tiles, cycles, dst_gzip, t0)) { C.out.clear(); return st; }
     if (out_bytes) *out_bytes = (int64_t)C.out.size();
+    if (base_count) *base_count = C.base_count;
+    if (score_sum) *score_sum = C.score_sum;
+    return 0;
+}
+
+extern "C" int mh_censor_staged_write(mh_ctx *ctx, mh_fastq *fq, int n_bad, const char *const *tiles,
+                                      const int32_t *cycles, int dst_gzip, int fd, int64_t offset,
+                                      int64_t *written, int64_t *base_count, int64_t *score_sum)
+{
+    if (!censor_args_ok(ctx, n_bad, tiles, cycles) || !fq || fd < 0 || offset < 0) return -3;
+    Ctx &c = *ctx_of(ctx);
+    MH_HIP(hipSetDevice(c.device));
+    if (!c.censor) c.censor = new CensorState();
+    CensorState &C = *c.censor;
+    C.out.clear();
+    C.base_count = C.score_sum = 0;
+    C.t_host_in = C.t_device = C.t_host_out = 0;
+    C.sink_fd = fd;
+    C.sink_pos = offset;
+    C.sink_err = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    TextBuf text = take_fastq_text(fq);
+    C.text.swap(text);
+    const int st = censor_text_guarded(c, C, n_bad, tiles, cycles, dst_gzip, t0);
+    C.sink_fd = -1;
+    if (st) return st;
+    if (written) *written = C.sink_pos - offset;
     if (base_count) *base_count = C.base_count;
     if (score_sum) *score_sum = C.score_sum;
     return 0;

@@ -127,6 +127,8 @@ def _declare(L):
                             ctypes.c_int),
         'mh_censor_staged': ([_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_int,
                               _I64P, _I64P, _I64P], ctypes.c_int),
+        'mh_censor_staged_write': ([_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int64, _I64P, _I64P, _I64P], ctypes.c_int),
         'mh_censor_output': ([_P, ctypes.c_char_p, ctypes.c_size_t,
                               ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         'mh_censor_write': ([_P, ctypes.c_int, ctypes.c_int64, _I64P], ctypes.c_int),
@@ -326,6 +328,17 @@ class Context:
                                      ctypes.byref(nb), ctypes.byref(bc), ctypes.byref(ss)),
               'mh_censor_staged')
         return nb.value, bc.value, ss.value
+
+    def censor_staged_write(self, fq, bad_cycles, dst_gzip, fd, offset):
+        """mh_censor_staged_write: the censored output written to fd from
+        offset while it is made: (bytes written, base_count, score_sum)."""
+        tiles, cycles = self._bad_cycle_args(bad_cycles)
+        nw, bc, ss = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(lib().mh_censor_staged_write(self.h, fq.h, len(bad_cycles), tiles, _ptr(cycles), int(dst_gzip),
+                                           int(fd), int(offset), ctypes.byref(nw), ctypes.byref(bc),
+                                           ctypes.byref(ss)),
+              'mh_censor_staged_write')
+        return nw.value, bc.value, ss.value
 
     def censor_output(self):
         """The held censored output as a bytearray (then released)."""

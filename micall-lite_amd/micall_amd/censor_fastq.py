@@ -77,12 +77,14 @@ def _censor_whole(src, bad_cycles, dest, use_gzip):
             _is_gzip_file(fd) == bool(use_gzip)):
         ctx = session.context()
         fq = _native.Fastq(fd=fd)
+        shared = sharded_io.SharedOutput(None, dest, binary=True)
         try:
-            n, base_count, score_sum = ctx.censor_staged(fq, bad_cycles, use_gzip)
+            # each gzip member written as soon as it is made
+            n, base_count, score_sum = ctx.censor_staged_write(fq, bad_cycles, use_gzip, out_fd,
+                                                               int(shared.end))
         finally:
             fq.close()
-        shared = sharded_io.SharedOutput(None, dest, binary=True)
-        ctx.censor_write(out_fd, int(shared.place([n])[0]))
+        shared.end += n
         shared.finish()
         return base_count, score_sum
     data = src.read()
