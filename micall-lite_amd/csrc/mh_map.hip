@@ -124,7 +124,10 @@ __device__ __forceinline__ Cand ldc_cand(const Cand *p)
 }
 
 // ---------------------------------------------------------------------------
-// k_pack_reads: one wave per read, one lane per 32-base chunk
+// k_pack_reads: one wave per read, one lane per base, 64 bases a step: the
+// loads of seq and qual are coalesced, and the 2-bit words and N masks are
+// assembled from three ballots (code bit 0, code bit 1, N) instead of a lane
+// walking 32 bytes of its own
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t base_code(uint8_t c, uint32_t &isn)
 {
@@ -137,6 +140,17 @@ __device__ __forceinline__ uint32_t base_code(uint8_t c, uint32_t &isn)
     }
 }
 
+// the 16 low bits of x to the even bit positions
+__device__ __forceinline__ uint32_t spread16(uint32_t x)
+{
+    x &= 0xffffu;
+    x = (x | (x << 8)) & 0x00ff00ffu;
+    x = (x | (x << 4)) & 0x0f0f0f0fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+
 __global__ __launch_bounds__(256) void k_pack_reads(DevReads R, const uint8_t *__restrict__ seq,
                                                     const uint8_t *__restrict__ qual,
                                                     const int64_t *__restrict__ src_off)
@@ -147,21 +161,24 @@ __global__ __launch_bounds__(256) void k_pack_reads(DevReads R, const uint8_t *_
     for (int64_t r = wave; r < R.n; r += nwaves) {
         const int m = R.len[r];
         const int64_t so = src_off[r], dofs = R.off[r];
-        const int chunks = (m + 31) >> 5;
-        if (lane < chunks) {
-            uint32_t w0 = 0, w1 = 0, nm = 0;
-            for (int x = 0; x < 32; ++x) {
-                const int b = lane * 32 + x;
-                if (b >= m) break;
-                uint32_t isn;
-                const uint32_t c = base_code(seq[so + b], isn);
-                if (x < 16) w0 |= c << (2 * x); else w1 |= c << (2 * (x - 16));
-                nm |= isn << x;
+        const int words = 2 * ((m + 31) >> 5);   // 16-base words the read's slot holds
+        for (int g = 0; 64 * g < m; ++g) {
+            const int b = 64 * g + lane;
+            uint32_t c = 0, isn = 0;
+            if (b < m) {
+                c = base_code(seq[so + b], isn);
                 R.qual[dofs + b] = qual[so + b];
             }
-            R.seq2[(dofs >> 4) + 2 * lane] = w0;
-            R.seq2[(dofs >> 4) + 2 * lane + 1] = w1;
-            R.nmask[(dofs >> 5) + lane] = nm;
+            const uint64_t b0 = __builtin_amdgcn_ballot_w64((c & 1u) != 0);
+            const uint64_t b1 = __builtin_amdgcn_ballot_w64((c & 2u) != 0);
+            const uint64_t bn = __builtin_amdgcn_ballot_w64(isn != 0);
+            if (lane < 4 && 4 * g + lane < words) {
+                const int sh = 16 * lane;
+                R.seq2[(dofs >> 4) + 4 * g + lane] =
+                    spread16((uint32_t)(b0 >> sh)) | (spread16((uint32_t)(b1 >> sh)) << 1);
+            } else if (lane >= 4 && lane < 6 && 4 * g + 2 * (lane - 4) < words) {   // 32-base N words
+                R.nmask[(dofs >> 5) + 2 * g + (lane - 4)] = (uint32_t)(bn >> (32 * (lane - 4)));
+            }
         }
     }
 }
