@@ -65,6 +65,25 @@ def make_reads(pairs, block, read_len=READ_LEN, paired=True, genomes='pol'):
     return reads, quals
 
 
+def cgroup_throttle():
+    """(nr_throttled, throttled ms) of this cgroup's CPU quota so far, or
+    None: a bench leg reports the difference, the time its threads stood
+    still because the process had used up its quota for the period."""
+    try:
+        with open('/sys/fs/cgroup/cpu.stat') as f:
+            kv = dict(line.split() for line in f if line.strip())
+        return int(kv['nr_throttled']), int(kv['throttled_usec']) / 1e3
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def throttle_since(before):
+    after = cgroup_throttle()
+    if before is None or after is None:
+        return None
+    return {'periods': after[0] - before[0], 'ms': round(after[1] - before[1], 1)}
+
+
 def host_cpus():
     """The host CPUs as this process sees them: every CPU it may run on
     (sched_getaffinity: all host cores, 256 on the GPU box), the launcher's
@@ -267,6 +286,7 @@ def end_to_end(n_pairs, workdir, single_member=False):
     session.reset()
     prelim_path = os.path.join(workdir, 'prelim.csv')
     remap_path = os.path.join(workdir, 'remap.csv')
+    thr0 = cgroup_throttle()
     with PhaseClock() as clock:
         t0 = time.perf_counter()
         with open(prelim_path, 'w') as f:
@@ -295,6 +315,7 @@ def end_to_end(n_pairs, workdir, single_member=False):
     out = {'value': round(2 * n_pairs / (t2 - t0), 1), 'unit': 'reads/s',
            'seconds': round(t2 - t0, 3), 'prelim_map_s': round(t1 - t0, 3),
            'remap_s': round(t2 - t1, 3), 'index_build_cold_ms': round(index_cold_ms, 2),
+           'cgroup_throttled': throttle_since(thr0),
            'phases_s': {k: round(v, 4) for k, v in phases.items()},
            'prelim_source': session.stats.get('prelim_source'),
            'fastq_gz_bytes': sizes, 'fastq_gz_members': 'one' if single_member else 'many (64 per file)',
@@ -721,6 +742,8 @@ def bench_chain(args):
     lib = {}
     gap = float(os.environ.get('MICALL_CHAIN_GAP_S', '0'))   # diagnostics: idle seconds between stages
 
+    throttled = []
+
     def run():
         # bin/micall writes each sample's outputs into a fresh directory:
         # the previous run's outputs are removed, untimed, so that opening
@@ -730,6 +753,7 @@ def bench_chain(args):
             if os.path.exists(path):
                 os.unlink(path)
         times = {}
+        thr = cgroup_throttle()
         t = time.perf_counter()
         for src, dst in ((r1, P['c1.fastq.gz']), (r2, P['c2.fastq.gz'])):
             with open(src, 'rb') as f, open(dst, 'wb') as g:
@@ -764,6 +788,7 @@ def bench_chain(args):
                 open(P['conseq.csv'], 'w') as conseq:
             aln2counts.aln2counts(al, nuc, amino, ins, conseq)
         times['aln2counts'] = time.perf_counter() - t
+        throttled.append(throttle_since(thr))
         return times
 
     for _ in range(args.warmup):
@@ -795,6 +820,7 @@ def bench_chain(args):
         'stages_s': {k: round(v, 3) for k, v in best.items()},
         'all_runs_s': [round(sum(r.values()), 3) for r in runs],
         'library_phases_s_last_run': lib,
+        'cgroup_throttled_per_run': throttled[args.warmup:args.warmup + len(runs)],
         'bytes': sizes,
     }
     print(json.dumps(out))

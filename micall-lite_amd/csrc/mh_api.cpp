@@ -277,6 +277,14 @@ int s2a_threads();   // mh_s2a_host.cpp: host worker count
 
 static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int seedlen)
 {
+    // MH_INDEX_TRACE=1: phase times to stderr
+    static const bool trace = getenv("MH_INDEX_TRACE") && *getenv("MH_INDEX_TRACE") == '1';
+    const auto tb = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        if (trace)
+            fprintf(stderr, "index %s %.2f ms\n", what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
+    };
     struct E { uint64_t key; int32_t ref, pos; };
     std::vector<int64_t> ref_off(n_refs);
     std::vector<int32_t> ref_len(n_refs);
@@ -291,9 +299,12 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     // then concatenated in reference order
     const int nt = std::max(1, std::min<int>(s2a_threads(), n_refs));
     std::vector<std::vector<E>> per(n_refs);
+    mark("pre");
+    std::vector<double> t_start((size_t)nt, 0.0);
     {
         std::atomic<int> next(0);
-        par_for(nt, [&](int) {
+        par_for(nt, [&](int t) {
+            t_start[(size_t)t] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count();
             for (int r; (r = next.fetch_add(1)) < n_refs;) {
                 const int L = ref_len[r];
                 uint8_t *cr = codes.data() + ref_off[r];
@@ -312,6 +323,12 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
             }
         });
     }
+    if (trace) {
+        double mx = 0;
+        for (double x : t_start) mx = std::max(mx, x);
+        fprintf(stderr, "index thread starts: last at %.2f ms\n", mx);
+    }
+    mark("seeds");
     std::vector<E> ent;
     {
         size_t n = 0;
@@ -339,6 +356,7 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
             });
         }
     }
+    mark("sort");
     size_t nkeys = 0;
     for (size_t i = 0; i < ent.size(); ++i) if (i == 0 || ent[i].key != ent[i - 1].key) ++nkeys;
     uint64_t cap = 1024;
@@ -357,6 +375,7 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
         i = j;
     }
     for (size_t i = 0; i < ent.size(); ++i) hits[i] = make_int2(ent[i].ref, ent[i].pos);
+    mark("hash");
     ix.n_refs = n_refs;
     ix.seedlen = seedlen;
     ix.total = (int64_t)codes.size();
@@ -392,8 +411,10 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
         MH_HIP(hipMalloc(&ix.blob, total));
         ix.cap_blob = (int64_t)total;
     }
+    mark("planes+alloc");
     std::vector<uint8_t> stage(total);
     for (int x = 0; x < 10; ++x) if (sz[x]) std::memcpy(stage.data() + at[x], src[x], sz[x]);
+    mark("stage");
     uint8_t *d = (uint8_t *)ix.blob;
     ix.codes = d + at[0];
     ix.ref_off = (int64_t *)(d + at[1]);
@@ -407,6 +428,7 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     ix.cplane = (uint32_t *)(d + at[9]);
     // callers synchronise the context stream first (mh_index_build)
     MH_HIP(hipMemcpy(ix.blob, stage.data(), total, hipMemcpyHostToDevice));
+    mark("upload");
     return 0;
 }
 

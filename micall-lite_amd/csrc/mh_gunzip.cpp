@@ -325,8 +325,18 @@ char *big_alloc(size_t n)
 void big_free(char *p, size_t n)
 {
     if (!p) return;
-    if (n < BIG) delete[] p;
-    else munmap(p, n);
+    if (n < BIG) { delete[] p; return; }
+    // The pages are given back by MADV_DONTNEED in 8 MiB pieces first, and
+    // the emptied mapping is unmapped after.  A GB-sized munmap on a detached
+    // thread holds the process's mmap lock for writing for tens of ms, and
+    // every thread creation meanwhile (its stack is an mmap) waits for it.
+    // MICALL_PLAIN_MUNMAP=1: one munmap (for A/B timing).
+    static const bool plain = getenv("MICALL_PLAIN_MUNMAP") && *getenv("MICALL_PLAIN_MUNMAP") == '1';
+    if (!plain && n >= ((size_t)64 << 20)) {
+        const size_t piece = (size_t)8 << 20;
+        for (size_t at = 0; at < n; at += piece) madvise(p + at, std::min(piece, n - at), MADV_DONTNEED);
+    }
+    munmap(p, n);
 }
 
 bool gunzip_fast_available() { return ld_api().ok; }
