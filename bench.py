@@ -66,9 +66,11 @@ def make_reads(pairs, block, read_len=READ_LEN, paired=True, genomes='pol'):
 
 
 def cgroup_throttle():
-    """(nr_throttled, throttled ms) of this cgroup's CPU quota so far, or
-    None: a bench leg reports the difference, the time its threads stood
-    still because the process had used up its quota for the period."""
+    """(nr_throttled, throttled_usec / 1e3) of this cgroup's CPU quota so
+    far, or None: a bench leg reports the difference, the periods in which
+    its threads stood still because the cgroup had used up its quota (the
+    kernel's throttled time is summed over CPUs, so it can exceed the wall
+    time of the leg)."""
     try:
         with open('/sys/fs/cgroup/cpu.stat') as f:
             kv = dict(line.split() for line in f if line.strip())
@@ -81,7 +83,7 @@ def throttle_since(before):
     after = cgroup_throttle()
     if before is None or after is None:
         return None
-    return {'periods': after[0] - before[0], 'ms': round(after[1] - before[1], 1)}
+    return {'periods': after[0] - before[0], 'cpu_ms': round(after[1] - before[1], 1)}
 
 
 def host_cpus():
