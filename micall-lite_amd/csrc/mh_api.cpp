@@ -592,10 +592,26 @@ static int index_fastq(Fastq &fq, const char *path, int64_t *newlines)
         }
     });
     std::vector<int64_t> nlpos;
-    size_t nn = 0;
-    for (auto &v : ls) nn += v.size();
-    nlpos.reserve(nn);
-    for (auto &v : ls) nlpos.insert(nlpos.end(), v.begin(), v.end());
+    std::vector<size_t> at((size_t)nt + 1, 0);
+    for (int t = 0; t < nt; ++t) at[(size_t)t + 1] = at[(size_t)t] + ls[(size_t)t].size();
+    nlpos.resize(at[(size_t)nt]);
+    std::vector<int64_t> before((size_t)nt, -1);   // the last newline before part t
+    for (int t = 1; t < nt; ++t)
+        before[(size_t)t] = ls[(size_t)t - 1].empty() ? before[(size_t)t - 1] : ls[(size_t)t - 1].back();
+    std::atomic<int> blank(0);   // an empty line (or one holding only '\r') anywhere
+    par_for(nt, [&](int t) {
+        const auto &v = ls[(size_t)t];
+        if (!v.empty()) std::memcpy(nlpos.data() + at[(size_t)t], v.data(), sizeof(int64_t) * v.size());
+        int64_t prev = before[(size_t)t];
+        bool b = false;
+        for (int64_t x : v) {
+            const int64_t st = prev + 1;
+            if (x == st || (x == st + 1 && D[st] == '\r')) b = true;
+            prev = x;
+        }
+        if (b) blank = 1;
+    });
+    std::vector<std::vector<int64_t>>().swap(ls);
     if (newlines) *newlines = (int64_t)nlpos.size();
     // line k spans [start_k, end_k) without '\n' / trailing '\r'
     const int64_t nl = (int64_t)nlpos.size() + (nlpos.empty() || nlpos.back() + 1 < n ? 1 : 0);
@@ -605,21 +621,29 @@ static int index_fastq(Fastq &fq, const char *path, int64_t *newlines)
         if (e > lstart(k) && D[e - 1] == '\r') --e;
         return e;
     };
-    std::vector<int64_t> rec;   // first line of each record
-    rec.reserve((size_t)(nl / 4 + 1));
-    for (int64_t k = 0; k < nl;) {
-        if (lend(k) == lstart(k)) { ++k; continue; }
-        if (k + 3 >= nl) { set_error("truncated FASTQ record in %s", path); return -3; }
-        rec.push_back(k);
-        k += 4;
+    // first line of each record: every fourth line when no line is empty
+    // (the last line, after the final newline, is checked on its own)
+    std::vector<int64_t> rec;
+    const bool tail_blank = nl > (int64_t)nlpos.size() && lend(nl - 1) == lstart(nl - 1);
+    const bool simple = !blank && !tail_blank;
+    if (simple) {
+        if (nl % 4) { set_error("truncated FASTQ record in %s", path); return -3; }
+    } else {
+        rec.reserve((size_t)(nl / 4 + 1));
+        for (int64_t k = 0; k < nl;) {
+            if (lend(k) == lstart(k)) { ++k; continue; }
+            if (k + 3 >= nl) { set_error("truncated FASTQ record in %s", path); return -3; }
+            rec.push_back(k);
+            k += 4;
+        }
     }
-    const int64_t nr = (int64_t)rec.size();
+    const int64_t nr = simple ? nl / 4 : (int64_t)rec.size();
     fq.name_at.resize(nr); fq.seq_at.resize(nr); fq.qual_at.resize(nr);
     fq.name_len.resize(nr); fq.len.resize(nr); fq.qual_len.resize(nr);
     std::atomic<int64_t> too_long(-1);
     par_for(nt, [&](int t) {
         for (int64_t r = nr * t / nt; r < nr * (t + 1) / nt; ++r) {
-            const int64_t k = rec[r];
+            const int64_t k = simple ? 4 * r : rec[r];
             fq.name_at[r] = lstart(k);
             fq.name_len[r] = (int32_t)(lend(k) - lstart(k));
             const int64_t L = lend(k + 1) - lstart(k + 1);

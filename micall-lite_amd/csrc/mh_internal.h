@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "micall_hip.h"
+#include "mh_gunzip.h"
 
 namespace mh {
 
@@ -227,7 +228,7 @@ int run_gotoh_batch(struct Ctx &c, int count, const char *const *s1, const char 
 // Read names (QNAMEs) in one byte pool: name r is bytes off[r] .. off[r + 1]
 // (one allocation for millions of names instead of one string each).
 struct NameTable {
-    std::string pool;
+    TextBuf pool;   // not zero-filled when sized (the names are copied in by many threads)
     std::vector<int64_t> off{0};
     size_t size() const { return off.size() - 1; }
     std::string_view operator[](size_t r) const

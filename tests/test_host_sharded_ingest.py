@@ -349,3 +349,24 @@ def test_single_member_parallel_inflate_high_ratio(tmp_path):
         got, err = _pinflate_run(path, extra)
         assert got == want
         assert 'pinflate crc' in err, err[-2000:]
+
+
+@pytest.mark.parametrize('tail,ok', [(b'', True), (b'\n', True), (b'\n\n', True), (b'\r\n', True),
+                                     (b'@extra\n', False), (b'@extra', False)])
+def test_host_parse_record_framing_tail(tmp_path, tail, ok):
+    """index_fastq's framing at the end of the text: trailing empty lines
+    (or '\\r' alone) are skipped, a partial record is an error, whichever of
+    its two paths (every fourth line when no line is empty, else the
+    line-by-line walk) runs."""
+    text = b''.join(_records(40, 1, 5)) + tail
+    p = tmp_path / 'R1.fastq'
+    p.write_bytes(text)
+    if ok:
+        fq = _native.Fastq(str(p))
+        names, seqs, _ = fq.parse()
+        assert len(seqs) == 40 and names[0] == _py_reads(text, False)[0][0]
+        fq.close()
+    else:
+        with pytest.raises(Exception, match='truncated'):
+            fq = _native.Fastq(str(p))
+            fq.parse()
