@@ -501,6 +501,17 @@ static inline void qname_span(const char *h, size_t n, bool paired, size_t *at, 
     size_t a = (n && h[0] == '@') ? 1 : 0;
     while (a < n && (h[a] == ' ' || h[a] == '\t')) ++a;
     size_t b = a;
+    // 8 bytes at a time while none of them is <= ' ' (space, tab and '\r'
+    // all are): the classic has-less-than test, exact for bytes < 0x80 and
+    // never missing a small byte (a byte >= 0x80 only sends the word to the
+    // byte-wise loop)
+    constexpr uint64_t ONES = 0x0101010101010101ull, HIGH = 0x8080808080808080ull;
+    while (b + 8 <= n) {
+        uint64_t w;
+        std::memcpy(&w, h + b, 8);
+        if (((w - ONES * 0x21) | w) & HIGH) break;
+        b += 8;
+    }
     while (b < n && h[b] != ' ' && h[b] != '\t' && h[b] != '\r') ++b;
     if (paired && b - a > 2 && h[b - 2] == '/' && (h[b - 1] == '1' || h[b - 1] == '2')) b -= 2;
     *at = a;
@@ -861,6 +872,7 @@ static int host_reads_from(Fastq &a, Fastq *b, int64_t a0, int64_t a1, int64_t b
         h.len[i] = f.len[(mate2 ? b0 : a0) + i / per];
         total += h.len[i];
     }
+    const auto t_setup = std::chrono::steady_clock::now();
     h.seq.alloc((size_t)total);
     h.qual.alloc((size_t)total);
     const auto tn = std::chrono::steady_clock::now();
@@ -870,7 +882,9 @@ static int host_reads_from(Fastq &a, Fastq *b, int64_t a0, int64_t a1, int64_t b
     std::vector<int64_t> nstart((size_t)n);
     const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 14) + 1));
     std::vector<int64_t> tsum(nt + 1, 0);
+    std::vector<double> t_go((size_t)nt, 0.0), t_end((size_t)nt, 0.0);
     par_for(nt, [&](int t) {
+        t_go[(size_t)t] = ms_since(tn);
         int64_t sum = 0;
         for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
             const bool mate2 = paired && (i & 1);
@@ -883,7 +897,19 @@ static int host_reads_from(Fastq &a, Fastq *b, int64_t a0, int64_t a1, int64_t b
             sum += (int64_t)len;
         }
         tsum[t + 1] = sum;
+        t_end[(size_t)t] = ms_since(tn);
     });
+    const double names_pass1 = ms_since(tn);
+    if (getenv("MH_INGEST_TRACE")) {
+        double g = 0, e = 0, w = 0;
+        for (int t = 0; t < nt; ++t) {
+            g = std::max(g, t_go[(size_t)t]);
+            e = std::max(e, t_end[(size_t)t]);
+            w = std::max(w, t_end[(size_t)t] - t_go[(size_t)t]);
+        }
+        fprintf(stderr, "ingest: name spans: last start %.1f ms, last end %.1f ms, longest %.1f ms (%d threads)\n",
+                g, e, w, nt);
+    }
     for (int t = 0; t < nt; ++t) tsum[t + 1] += tsum[t];
     names.pool.resize((size_t)tsum[nt]);
     par_for(nt, [&](int t) {
@@ -899,6 +925,9 @@ static int host_reads_from(Fastq &a, Fastq *b, int64_t a0, int64_t a1, int64_t b
     });
     names.off[0] = 0;
     *names_ms = ms_since(tn);
+    if (getenv("MH_INGEST_TRACE"))
+        fprintf(stderr, "ingest: names setup %.1f ms, spans %.1f ms, copies to %.1f ms\n", ms_since(t_setup) - ms_since(tn),
+                names_pass1, *names_ms);
     const auto tc = std::chrono::steady_clock::now();
     par_for(nt, [&](int t) {
         for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
