@@ -219,7 +219,33 @@ struct CtxEx : Ctx {
     // segment bound in their concatenation, kept for mh_write_segments
     std::vector<TextBuf> seg_chunks;
     std::vector<int64_t> seg_at;
+    // device buffers of the reads (both DevReads) and the upload staging,
+    // kept between loads and grown only: bytes behind each pointer
+    std::unordered_map<const void *, size_t> rcap;
+    uint8_t *stage_seq = nullptr, *stage_qual = nullptr;
+    int64_t *stage_off = nullptr;
 };
+
+// p sized to at least `need` bytes: kept when it already is, else freed and
+// allocated again (cap: CtxEx::rcap)
+template <class T>
+static hipError_t grow_dev(CtxEx &c, T *&p, size_t need)
+{
+    if (need == 0) need = 1;
+    if (p) {
+        auto it = c.rcap.find((const void *)p);
+        if (it != c.rcap.end() && it->second >= need) return hipSuccess;
+        if (it != c.rcap.end()) c.rcap.erase(it);
+        hipFree(p);
+        p = nullptr;
+    }
+    void *q = nullptr;
+    const hipError_t e = hipMalloc(&q, need);
+    if (e != hipSuccess) return e;
+    p = (T *)q;
+    c.rcap[(const void *)q] = need;
+    return hipSuccess;
+}
 
 static void free_index(DevIndex &ix)
 {
@@ -456,32 +482,31 @@ static int load_reads(CtxEx &c, DevReads &dst, HostReads &host, int64_t n, int p
         off[r] = total;
         total += ((int64_t)lens[r] + 31) / 32 * 32;
     }
-    free_reads(dst);
+    // the device buffers of the last load are reused when large enough
+    // (a chain of samples in one process frees and maps GBs otherwise)
+    MH_HIP(hipStreamSynchronize(c.stream));   // nothing may still read the old reads
     dst.n = n;
     dst.paired = paired;
     dst.max_len = max_len;
     dst.total_bases = total;
-    MH_HIP(hipMalloc(&dst.seq2, sizeof(uint32_t) * (total / 16 + 8)));
-    MH_HIP(hipMalloc(&dst.nmask, sizeof(uint32_t) * (total / 32 + 8)));
-    MH_HIP(hipMalloc(&dst.qual, total + 64));
-    MH_HIP(hipMalloc(&dst.off, sizeof(int64_t) * (n > 0 ? n : 1)));
-    MH_HIP(hipMalloc(&dst.len, sizeof(int32_t) * (n > 0 ? n : 1)));
+    MH_HIP(grow_dev(c, dst.seq2, sizeof(uint32_t) * (total / 16 + 8)));
+    MH_HIP(grow_dev(c, dst.nmask, sizeof(uint32_t) * (total / 32 + 8)));
+    MH_HIP(grow_dev(c, dst.qual, (size_t)total + 64));
+    MH_HIP(grow_dev(c, dst.off, sizeof(int64_t) * (n > 0 ? n : 1)));
+    MH_HIP(grow_dev(c, dst.len, sizeof(int32_t) * (n > 0 ? n : 1)));
     MH_HIP(hipMemsetAsync(dst.seq2, 0, sizeof(uint32_t) * (total / 16 + 8), c.stream));
     MH_HIP(hipMemsetAsync(dst.nmask, 0, sizeof(uint32_t) * (total / 32 + 8), c.stream));
     if (n > 0) {
         MH_HIP(hipMemcpyAsync(dst.off, off.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, c.stream));
         MH_HIP(hipMemcpyAsync(dst.len, lens, sizeof(int32_t) * n, hipMemcpyHostToDevice, c.stream));
-        uint8_t *dseq = nullptr, *dqual = nullptr;
-        int64_t *doff = nullptr;
-        MH_HIP(hipMalloc(&dseq, src_total + 1));
-        MH_HIP(hipMalloc(&dqual, src_total + 1));
-        MH_HIP(hipMalloc(&doff, sizeof(int64_t) * n));
-        MH_HIP(hipMemcpyAsync(dseq, seq, src_total, hipMemcpyHostToDevice, c.stream));
-        MH_HIP(hipMemcpyAsync(dqual, qual, src_total, hipMemcpyHostToDevice, c.stream));
-        MH_HIP(hipMemcpyAsync(doff, offsets, sizeof(int64_t) * n, hipMemcpyHostToDevice, c.stream));
-        MH_HIP(launch_pack_reads(dst, dseq, dqual, doff, c.stream));
+        MH_HIP(grow_dev(c, c.stage_seq, (size_t)src_total + 1));
+        MH_HIP(grow_dev(c, c.stage_qual, (size_t)src_total + 1));
+        MH_HIP(grow_dev(c, c.stage_off, sizeof(int64_t) * (size_t)n));
+        MH_HIP(hipMemcpyAsync(c.stage_seq, seq, src_total, hipMemcpyHostToDevice, c.stream));
+        MH_HIP(hipMemcpyAsync(c.stage_qual, qual, src_total, hipMemcpyHostToDevice, c.stream));
+        MH_HIP(hipMemcpyAsync(c.stage_off, offsets, sizeof(int64_t) * n, hipMemcpyHostToDevice, c.stream));
+        MH_HIP(launch_pack_reads(dst, c.stage_seq, c.stage_qual, c.stage_off, c.stream));
         MH_HIP(hipStreamSynchronize(c.stream));
-        hipFree(dseq); hipFree(dqual); hipFree(doff);
     }
     if (adopt) {
         host = std::move(*adopt);
@@ -750,6 +775,7 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipStreamSynchronize(c->stream);
     free_reads(c->reads);
     free_reads(c->rows.reads);
+    hipFree(c->stage_seq); hipFree(c->stage_qual); hipFree(c->stage_off);
     for (auto &ix : c->cache) free_index(ix);   // c->index only views one of these
     free_index(c->small);
     MapState &M = c->map;
