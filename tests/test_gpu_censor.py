@@ -67,3 +67,34 @@ def test_censor_large_vs_oracle():
                         use_gzip=True, summary_file=summary)
     assert gzip.decompress(dest.getvalue()) == want
     assert summary.getvalue() == 'avg_quality,base_count\n{},{}\n'.format(repr(total / n), n)
+
+
+@pytest.mark.parametrize('use_gzip', [True, False])
+def test_censor_file_to_file_streamed(tmp_path, use_gzip):
+    """The drop-in on real files (bin/micall's call): the source mmap'd and
+    each output block written with pwrite as it is made
+    (mh_censor_staged_write), at the handle's position (bytes already
+    written through the handle are kept), for a file large enough to make
+    many blocks and for an empty one."""
+    import random
+    rng = random.Random(11)
+    bad = {(str(1101 + t), c) for t in range(4) for c in rng.sample(range(1, 151), 6)}
+    recs = []
+    for i in range(120000):
+        seq = ''.join(rng.choice('ACGT') for _ in range(150))
+        recs.append('@M1:2:F:1:{}:{}:{} 1:N:0:1\n{}\n+\n{}\n'.format(1101 + i % 4, i, i, seq, 'F' * 150))
+    data = ''.join(recs).encode()
+    want, n, total = og_censor.censor_bytes(data, bad)
+    for payload, expect in ((data, want), (b'', b'')):
+        src_path, dst_path = tmp_path / 'in.fastq', tmp_path / 'out.fastq'
+        src_path.write_bytes(gzip.compress(payload, 1) if use_gzip else payload)
+        lead = b'lead bytes\n'
+        with open(src_path, 'rb') as src, open(dst_path, 'wb') as dst:
+            dst.write(lead)
+            censor_fastq.censor(src, [dict(tile=t, cycle=str(c)) for t, c in sorted(bad)], dst,
+                                use_gzip=use_gzip)
+            dst.write(b'tail')
+        out = dst_path.read_bytes()
+        assert out.startswith(lead) and out.endswith(b'tail')
+        body = out[len(lead):-4]
+        assert (gzip.decompress(body) if use_gzip else body) == expect

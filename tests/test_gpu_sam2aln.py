@@ -129,3 +129,41 @@ def test_sam2aln_matchmaker_order_vs_oracle(ctx):
     assert got[1] == want[1]
     assert got[2] == want[2]
     assert 'unmatched' in want[2]
+
+
+@pytest.mark.parametrize('case', E2E)
+def test_sam2aln_drop_in_on_files_streamed(tmp_path, case):
+    """The drop-in on real files, as bin/micall calls it: remap.csv mmap'd,
+    every output formatted and written in one pass (mh_sam2aln_write
+    without a size query) at the handle's position, after what the caller
+    had written through the handle."""
+    d = os.path.join(GOLDEN, 'e2e', case)
+    rp = tmp_path / 'remap.csv'
+    rp.write_text(_gz(os.path.join(d, 'remap.csv.gz')))
+    outs = {k: tmp_path / (k + '.csv') for k in ('aligned', 'insert', 'failed')}
+    with open(rp) as remap, open(outs['aligned'], 'w') as al, open(outs['insert'], 'w') as ins, \
+            open(outs['failed'], 'w') as fa:
+        for h in (al, ins, fa):
+            h.write('lead\n')
+        s2a.sam2aln(remap, al, ins, fa)
+        for h in (al, ins, fa):
+            h.write('tail\n')
+    for k, p in outs.items():
+        assert p.read_text() == 'lead\n' + _gz(os.path.join(d, k + '.csv.gz')) + 'tail\n'
+
+
+def test_sam2aln_streamed_write_matches_collected(ctx, tmp_path):
+    """Many formatting jobs (more rows than one 4096-row job): the streamed
+    file output equals the collected text, byte for byte."""
+    text = _synthetic_remap_csv(ctx, 20000, 7)
+    al_want, ins_want, fa_want = _device(ctx, text)
+    assert al_want.count('\n') > 3 * 4096
+    rp = tmp_path / 'remap.csv'
+    rp.write_text(text)
+    outs = {k: tmp_path / (k + '.csv') for k in ('aligned', 'insert', 'failed')}
+    with open(rp) as remap, open(outs['aligned'], 'w') as al, open(outs['insert'], 'w') as ins, \
+            open(outs['failed'], 'w') as fa:
+        s2a.sam2aln(remap, al, ins, fa)
+    assert outs['aligned'].read_text() == al_want
+    assert outs['insert'].read_text() == ins_want
+    assert outs['failed'].read_text() == fa_want
