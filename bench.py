@@ -104,22 +104,22 @@ def host_cpus():
             'share_threads': share, 'cgroup_cpu_quota': quota}
 
 
-def cpu_baseline(sample_pairs):
+def cpu_baseline(reads, quals):
     """The CPU oracle's step (C restatement: og_map + og_rows_from_alns +
     og_pileup_mt, OpenMP over read pairs; O(reference length) consensus in
-    Python) on a bounded sample of the same workload, on every host core
-    (sched_getaffinity) and again on the box's CPU share (OMP_NUM_THREADS).
-    The reads are packed before the clock starts, so the timed region holds
-    no per-read Python: the device-resident step's CPU equivalent."""
+    Python) on a bounded sample of the same workload -- the first pairs of
+    the bench's own input -- on every host core (sched_getaffinity) and again
+    on the box's CPU share (OMP_NUM_THREADS).  The reads are packed before
+    the clock starts, so the timed region holds no per-read Python: the
+    device-resident step's CPU equivalent.  Returns (baseline dict, the
+    oracle's records and consensus of the last run for the parity leg)."""
     import cpu_pipeline
     from micall_amd import projects
     cfg = projects.load_default()
     seed_set = cfg.seed_sequences()
     groups = {k: cfg.getSeedGroup(k) for k in seed_set}
-    reads, quals = make_reads(sample_pairs, block=0)
-    prep = cpu_pipeline.Prepared([r.tobytes().decode() for r in reads],
-                                 [q.tobytes().decode() for q in quals], True)
-    del reads, quals
+    sample_pairs = reads.shape[0] // 2
+    prep = cpu_pipeline.Prepared.from_arrays(reads, quals, True)
     cpus = host_cpus()
     runs = {}
     for threads in sorted({cpus['sched_getaffinity'], cpus['share_threads']}, reverse=True):
@@ -131,12 +131,103 @@ def cpu_baseline(sample_pairs):
             'kind': 'port', 'host_cpus': cpus,
             'runs': {str(t): {'seconds': round(s, 3), 'value': round(2 * sample_pairs / s, 1)}
                      for t, s in sorted(runs.items())},
-            'sample': '{} synthetic pairs (first block of the bench input): prelim e2e pass over '
+            'sample': 'the first {} pairs of the bench input: prelim e2e pass over '
                       '74 seeds + 1 local remap pass + 2 pileups/consensus, oracle C restatement '
                       '(og_map, og_pileup_mt) with OpenMP over pairs, timed on all {} host cores '
                       '({:.1f} s) and on the {}-thread CPU share ({:.1f} s); value is the faster; '
                       'reads packed before timing'.format(
-                          sample_pairs, allc, runs[allc], share, runs[share])}
+                          sample_pairs, allc, runs[allc], share, runs[share])}, prep.result
+
+
+def record_mismatches(dev, ref):
+    """Indices of the records that differ between two arrays of alignment
+    records (every field, and the CIGAR words up to n_cigar)."""
+    from micall_amd import _native
+    assert len(dev) == len(ref), (len(dev), len(ref))
+    same = np.ones(len(ref), dtype=bool)
+    for f in _native.ALN_FIELDS:
+        same &= dev[f] == ref[f]
+    live = np.arange(ref['cigar'].shape[1])[None, :] < ref['n_cigar'][:, None]
+    same &= np.all((dev['cigar'] == ref['cigar']) | ~live, axis=1)
+    return np.flatnonzero(~same)
+
+
+def parity_check(ctx, pipe, sample, paired, baseline_result=None, device_index=0):
+    """Parity at configuration size (untimed, after the timed steps): the
+    device's alignment records of the bench's own run for its first units
+    against the CPU oracle's (og_map) on the same reads, byte for byte.
+    A record depends on its read (pair) and the references only, so the
+    first units of the 1M-pair run must equal the oracle's on those units.
+
+      prelim   an end-to-end pass over the 74 seeds on the resident reads
+               (what every step's prelim pass computes);
+      remap    the last step's --local pass, against the consensus set it
+               mapped to (pipe.mapped_to), vs og_map against the same set;
+      consensus  (with the CPU baseline's run of the same sample) the
+               sample alone through the device pipeline on a new context:
+               its prelim consensus and final consensus against the oracle
+               step's (cpu_pipeline.timed_step).
+
+    Consumers of these records in the reference: remap.py:474-541 (seed
+    selection and the consensus), prelim_map.py:134-151 (prelim.csv)."""
+    import cpu_pipeline
+    import oracle
+    from micall_amd import _native
+    from micall_amd.pipeline import RemapPipeline
+    t0 = time.perf_counter()
+    reads, quals = sample
+    n = reads.shape[0]
+    threads = host_cpus()['share_threads']
+    out = {'units_checked': n // 2 if paired else n, 'reads_checked': n,
+           'unit': 'pairs' if paired else 'reads'}
+    # the last step's remap pass: its records are still the context's
+    mapped_to = dict(pipe.mapped_to or {})
+    if mapped_to:
+        dev = ctx.fetch(0, n)
+        ref = cpu_pipeline.map_arrays(list(mapped_to.values()), oracle.LOCAL, reads, quals, paired,
+                                      threads)
+        bad = record_mismatches(dev, ref)
+        out['remap'] = {'references': list(mapped_to), 'record_mismatches': int(len(bad)),
+                        'first_mismatches': bad[:8].tolist(),
+                        'mapped_reads': int(((ref['flag'] & 4) == 0).sum())}
+        del dev, ref
+    names = list(pipe.seed_set)
+    ctx.index_build(names, [pipe.seed_set[k] for k in names], 22)
+    ctx.map(pipe._params(_native.E2E))
+    dev = ctx.fetch(0, n)
+    if baseline_result is not None and baseline_result['prelim_names'] == names:
+        ref = baseline_result['prelim']
+    else:
+        ref = cpu_pipeline.map_arrays([pipe.seed_set[k] for k in names], oracle.E2E, reads, quals,
+                                      paired, threads)
+    bad = record_mismatches(dev, ref)
+    out['prelim'] = {'record_mismatches': int(len(bad)), 'first_mismatches': bad[:8].tolist(),
+                     'mapped_reads': int(((ref['flag'] & 4) == 0).sum())}
+    del dev, ref
+    if baseline_result is not None:
+        c2 = _native.Context(device_index)
+        try:
+            c2.reads_load_fixed(reads, quals, paired)
+            p2 = RemapPipeline(c2)
+            final, _counts, _unm = p2.run(float(n), max_iterations=1)
+            out['consensus'] = {
+                'prelim_equal': p2.mapped_to == baseline_result['prelim_conseqs'] and
+                list(p2.mapped_to or {}) == baseline_result['remap_names'],
+                'final_equal': final == baseline_result['conseqs'],
+                'references': sorted(final)}
+            if out['consensus']['prelim_equal'] and baseline_result['remap'] is not None:
+                bad = record_mismatches(c2.fetch(), baseline_result['remap'])
+                out['consensus']['sample_remap_record_mismatches'] = int(len(bad))
+        finally:
+            c2.close()
+    out['record_mismatches'] = out['prelim']['record_mismatches'] + \
+        out.get('remap', {}).get('record_mismatches', 0)
+    out['pairs_checked'] = out['units_checked'] if paired else None
+    out['consensus_equal'] = (out['consensus']['prelim_equal'] and out['consensus']['final_equal']
+                              if 'consensus' in out else None)
+    out['seconds'] = round(time.perf_counter() - t0, 2)
+    out['oracle_threads'] = threads
+    return out
 
 
 def cpu_end_to_end(sample_pairs, workdir):
@@ -851,6 +942,9 @@ def main():
     ap.add_argument('--cpu-e2e-sample', type=int, default=20000,
                     help='pairs for the CPU end-to-end baseline (file to file)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-parity', action='store_true',
+                    help='skip the parity leg (device records of the first --cpu-sample units '
+                         'against the CPU oracle, after timing)')
     ap.add_argument('--no-e2e', action='store_true',
                     help='skip the end-to-end (file to file) leg of the default C2 run')
     ap.add_argument('--e2e-gzip', choices=('members', 'single'), default='members',
@@ -899,6 +993,13 @@ def main():
     L = args.read_len
     reads, quals = make_reads(args.pairs, block=rank, read_len=L, paired=paired, genomes=args.genomes)
     ctx.reads_load_fixed(reads, quals, paired)
+    # the first units of this rank's input, kept for the CPU baseline and
+    # the parity leg (rank 0; N = 1 checks 200k pairs, N > 1 a 20k sample)
+    sample = None
+    if rank == 0 and (not args.no_parity or (world == 1 and not args.no_cpu_baseline)):
+        k = min(args.cpu_sample if world == 1 else min(args.cpu_sample, 20000), args.pairs)
+        k *= 2 if paired else 1
+        sample = (reads[:k].copy(), quals[:k].copy())
     del reads, quals
     shard = Shard(rank, world, read_base=rank * (1 if args.unpaired else 2) * args.pairs, device=device) if world > 1 else None
     pipe = RemapPipeline(ctx, shard=shard)
@@ -964,10 +1065,15 @@ def main():
     cells = (ext - fast) * L * 31
     dp_ms = kernels['k_dp'][0] + kernels['k_dp_rescue'][0]
 
+    parity = None
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline and paired and L == READ_LEN and args.genomes == 'pol':
-            cpu = cpu_baseline(args.cpu_sample)
+        cpu = cpu_result = None
+        if (world == 1 and not args.no_cpu_baseline and paired and L == READ_LEN and
+                args.genomes == 'pol' and sample is not None):
+            cpu, cpu_result = cpu_baseline(*sample)
+        if sample is not None and not args.no_parity:
+            parity = parity_check(ctx, pipe, sample, paired, cpu_result, device.index)
+            del cpu_result
         e2e = None
         if (world == 1 and not args.no_e2e and paired and L == READ_LEN and args.genomes == 'pol'
                 and args.iterations == 1 and not args.force_iterations):
@@ -1020,6 +1126,7 @@ def main():
                    'cells_per_step': cells // max(args.steps, 1),
                    'gcups': round(cells / (dp_ms / 1e3) / 1e9, 1) if dp_ms > 0 else None},
             'cpu_baseline': cpu,
+            'parity': parity,
             'end_to_end': e2e,
             'result': {'remap_iterations_run': len(pipe.log),
                        'conseqs': {k: len(v) for k, v in conseqs.items()},
@@ -1030,8 +1137,10 @@ def main():
             print(json.dumps({'stage_ms_per_step': {k: round(v[0] * 1e3 / (args.steps + args.warmup), 3)
                                                     for k, v in stages.items() if not k.startswith('_')},
                               'map_stats': stages.get('_map_stats')}), file=sys.stderr)
+    del sample
     ctx.close()
     if world > 1:
+        dist.barrier()     # rank 0's untimed legs (parity) end before the group does
         dist.destroy_process_group()
 
 

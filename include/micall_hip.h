@@ -124,6 +124,33 @@ int mh_reads_count(mh_ctx *ctx, int64_t *n_reads, int *paired);
  * wall time (microseconds). */
 typedef struct mh_fastq mh_fastq;
 int mh_fastq_open_part(const char *path, int fd, int part, int parts, mh_fastq **out, int64_t *info);
+/* The ranks' test for a single gzip member: info[3] = is gzip, file size,
+ * 1 if a gzip member starts inside part `part`'s byte range (past offset
+ * 0).  Scans 1/parts of the file; no decode. */
+int mh_fastq_scan_part(const char *path, int fd, int part, int parts, int64_t *info);
+/* Part `part` of `parts` of a FASTQ file that is one gzip member (bcl2fastq's
+ * layout), decoded without any other part's bytes (the reference reads the
+ * file once per pass, prelim_map.py:114-134; censor_fastq.py:58-96):
+ *   open    info[7]: this part's first deflate block start (bit; -1 if its
+ *           share of the compressed bytes holds none: not splittable), the
+ *           stream's end bit, the trailer's CRC-32 and size, spans, file
+ *           size, microseconds;
+ *   decode  up to end_bit (the next part's first block start, or the
+ *           stream's end bit for the last part); info[2]: text bytes (-1:
+ *           not decodable this way), microseconds;
+ *   tail    with `window` = the previous part's last 32768 text bytes (NULL
+ *           for part 0), this part's last 32768 text bytes into tail[32768]
+ *           (the next part's window);
+ *   finish  the rest of the text resolved; info[11]: the mh_fastq_open_part
+ *           fields with mode 3 and file offsets c0 / c1 as given, then the
+ *           CRC-32 of this part's text (the caller checks the combined CRC
+ *           and size against the trailer).
+ * Each returns 0, -1 (not resolvable: fall back), -2 out of memory, -3 bad
+ * arguments. */
+int mh_fastq_member_open(const char *path, int fd, int part, int parts, mh_fastq **out, int64_t *info);
+int mh_fastq_member_decode(mh_fastq *fq, int64_t end_bit, int64_t *info);
+int mh_fastq_member_tail(mh_fastq *fq, const char *window, char *tail);
+int mh_fastq_member_finish(mh_fastq *fq, const char *window, int64_t c0, int64_t c1, int64_t *info);
 /* Record starts of the held text, a record being four lines: line0 = lines
  * of the file before its first byte, starts_line = 1 if that byte starts a
  * line.  out[5]: offset of the first record start (the size if none),

@@ -20,6 +20,7 @@
 #include <string>
 #include <condition_variable>
 #include <deque>
+#include <exception>
 #include <mutex>
 #include <functional>
 #include <string_view>
@@ -554,13 +555,33 @@ struct Fastq {
 
 int s2a_threads();   // mh_s2a_host.cpp: host worker count
 
+// fn(0) .. fn(nt-1) on nt threads (the caller's is thread 0).  An
+// exception on any thread (bad_alloc from a text buffer) is kept, every
+// thread is joined, then the first one is rethrown on the caller's thread:
+// none escapes a std::thread (that would terminate the process).
 static void par_for(int nt, const std::function<void(int)> &fn)
 {
     if (nt <= 1) { fn(0); return; }
+    std::mutex mu;
+    std::exception_ptr first;
+    auto guarded = [&](int t) {
+        try {
+            fn(t);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!first) first = std::current_exception();
+        }
+    };
     std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(fn, t);
-    fn(0);
+    th.reserve((size_t)nt - 1);
+    try {
+        for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    } catch (...) {           // thread creation failed: run the rest here
+        for (int t = (int)th.size() + 1; t < nt; ++t) guarded(t);
+    }
+    guarded(0);
     for (auto &x : th) x.join();
+    if (first) std::rethrow_exception(first);
 }
 
 // The whole (gzip or plain) file; every concatenated gzip member is decoded
@@ -1580,10 +1601,36 @@ static int write_pieces(int fd, std::vector<WritePiece> pieces)
 // host thread, in order.  With segment row bounds seg_rows[0 .. n_seg]
 // (relative to `first`, ascending), *seg_at gets the byte offset in the
 // concatenated text at which each bound row starts.
+static int format_chunks_unguarded(CtxEx *c, int style, const int64_t *order, int64_t first,
+                                   int64_t n, const char *const *refnames,
+                                   std::vector<TextBuf> &chunks, int n_seg,
+                                   const int64_t *seg_rows, std::vector<int64_t> *seg_at);
+
+// format_chunks_unguarded with an allocation failure on any formatting
+// thread (par_for rethrows it here) reported as -2, not thrown across the ABI
 static int format_chunks(CtxEx *c, int style, const int64_t *order, int64_t first, int64_t n,
                          const char *const *refnames, std::vector<TextBuf> &chunks,
                          int n_seg = 0, const int64_t *seg_rows = nullptr,
                          std::vector<int64_t> *seg_at = nullptr)
+{
+    try {
+        return format_chunks_unguarded(c, style, order, first, n, refnames, chunks, n_seg, seg_rows,
+                                       seg_at);
+    } catch (const std::bad_alloc &) {
+        chunks.clear();
+        set_error("row formatting: out of memory");
+        return -2;
+    } catch (const std::exception &e) {
+        chunks.clear();
+        set_error("row formatting: %s", e.what());
+        return -2;
+    }
+}
+
+static int format_chunks_unguarded(CtxEx *c, int style, const int64_t *order, int64_t first,
+                                   int64_t n, const char *const *refnames,
+                                   std::vector<TextBuf> &chunks, int n_seg,
+                                   const int64_t *seg_rows, std::vector<int64_t> *seg_at)
 {
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<Rec> rec;
@@ -1690,37 +1737,60 @@ static int format_write_stream(CtxEx *c, int style, const int64_t *order, int64_
     std::atomic<int> finished(0);
     std::atomic<double> fmt_end(0.0);
     std::vector<std::thread> fmt;
+    // a formatter that throws (bad_alloc from a row buffer) stores the
+    // exception and raises `failed`; the writer stops waiting on it, every
+    // thread is joined, and the exception is rethrown to mh_write_rows_crc
+    std::exception_ptr err;
+    std::atomic<bool> failed(false);
+    auto fail = [&](std::exception_ptr e) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = e;
+            failed.store(true);
+        }
+        next.store(nch);        // no formatter starts another chunk
+        cv.notify_all();
+    };
     auto worker = [&]() {
-        std::string tmp;
-        for (int64_t k; (k = next.fetch_add(1)) < nch;) {
-            const int64_t k0 = n * k / nch, k1 = n * (k + 1) / nch;
-            TextBuf &out = buf[(size_t)k];
-            out.resize((size_t)(k1 - k0) * row_max + 1);
-            size_t used = 0;
-            for (int64_t j = k0; j < k1; ++j) {
-                const int64_t r = order ? order[first + j] : first + j;
-                format_row(c, style, order ? rec[r] : rec[j], r, pool.data(), refnames, rn_len.data(),
-                           out, used, tmp);
+        try {
+            std::string tmp;
+            for (int64_t k; (k = next.fetch_add(1)) < nch;) {
+                const int64_t k0 = n * k / nch, k1 = n * (k + 1) / nch;
+                TextBuf &out = buf[(size_t)k];
+                out.resize((size_t)(k1 - k0) * row_max + 1);
+                size_t used = 0;
+                for (int64_t j = k0; j < k1; ++j) {
+                    const int64_t r = order ? order[first + j] : first + j;
+                    format_row(c, style, order ? rec[r] : rec[j], r, pool.data(), refnames, rn_len.data(),
+                               out, used, tmp);
+                }
+                out.resize(used);
+                if (crc_out) crc[(size_t)k] = crc32_update(0, out.data(), used);
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    done[k].store(1);
+                }
+                cv.notify_all();
             }
-            out.resize(used);
-            if (crc_out) crc[(size_t)k] = crc32_update(0, out.data(), used);
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                done[k].store(1);
-            }
-            cv.notify_all();
+        } catch (...) {
+            fail(std::current_exception());
         }
         if (finished.fetch_add(1) + 1 == nf) fmt_end.store(ms_since(t0));
     };
-    for (int t = 0; t < nf; ++t) fmt.emplace_back(worker);
+    try {
+        for (int t = 0; t < nf; ++t) fmt.emplace_back(worker);
+    } catch (...) {
+        fail(std::current_exception());
+    }
     int bad = 0;
     int64_t pos = offset;
     uint32_t total_crc = 0;
-    for (int64_t k = 0; k < nch; ++k) {
+    for (int64_t k = 0; k < nch && !failed.load(); ++k) {
         {
             std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return done[k].load() != 0; });
+            cv.wait(lk, [&] { return done[k].load() != 0 || failed.load(); });
         }
+        if (failed.load()) break;
         const char *p = buf[(size_t)k].data();
         size_t left = buf[(size_t)k].size();
         if (crc_out) total_crc = crc32_join(total_crc, crc[(size_t)k], (int64_t)left);
@@ -1732,6 +1802,7 @@ static int format_write_stream(CtxEx *c, int style, const int64_t *order, int64_
         buf[(size_t)k].release();
     }
     for (auto &t : fmt) t.join();
+    if (err) std::rethrow_exception(err);
     // the formatting (overlapped with the first writes), then the write tail
     const double all_ms = ms_since(t0), f_ms = fmt_end.load();
     c->phase_ms[MH_PHASE_FORMAT] += f_ms;
@@ -1761,6 +1832,9 @@ int mh_write_rows_crc(mh_ctx *ctx, int style, const int64_t *order, int64_t firs
     } catch (const std::bad_alloc &) {
         set_error("mh_write_rows: out of memory");
         return -2;
+    } catch (const std::exception &e) {
+        set_error("mh_write_rows: %s", e.what());
+        return -2;
     }
 }
 
@@ -1771,6 +1845,12 @@ int mh_format_segments(mh_ctx *ctx, int style, const int64_t *order, int64_t n,
     if (!ctx || !refnames || (style != 0 && style != 1) || n < 0 || n_seg < 1 || !seg_rows ||
         !seg_bytes) {
         set_error("mh_format_segments: bad arguments");
+        return -3;
+    }
+    // the bounds cover rows 0 .. n exactly: every formatted byte belongs
+    // to one segment (mh_write_segments indexes seg_at by segment)
+    if (seg_rows[0] != 0 || seg_rows[n_seg] != n) {
+        set_error("mh_format_segments: segment bounds must start at row 0 and end at row n");
         return -3;
     }
     for (int k = 0; k < n_seg; ++k)

@@ -13,8 +13,14 @@
 //     a false one fails to decode), so the ranges of consecutive ranks meet
 //     exactly;
 //   * a plain file: the byte range itself;
-//   * anything else (one gzip member, as bcl2fastq writes it): the whole file
-//     (mode 0), and the rank keeps its records by count.
+//   * one gzip member (as bcl2fastq writes it; mh_fastq_scan_part finds no
+//     member start in any rank's range): the deflate bits from the first
+//     block start in the rank's share of the compressed bytes to the next
+//     rank's (mh_fastq_member_*, mh_pinflate.cpp), decoded without the
+//     window the rank before holds, which then arrives through the caller's
+//     rank-order chain of 32 KiB messages (mode 3);
+//   * anything else: the whole file (mode 0), and the rank keeps its records
+//     by count.
 //
 // The text a rank holds then starts and ends mid-record.  mh_fastq_frame
 // locates its record starts from the number of lines before it (a record is
@@ -50,12 +56,6 @@ int s2a_threads();
 }
 
 using namespace mh;
-
-struct mh_fastq {
-    TextBuf data;                  // the held text
-    std::vector<int64_t> rec;      // byte offsets of its record starts (mh_fastq_frame)
-    bool framed = false;
-};
 
 namespace {
 
@@ -104,10 +104,11 @@ int view_file(const char *path, int fd_in, FileView &v)
     return rc;
 }
 
-// the first offset in [from, size) where a gzip member starts (probed), or size
-int64_t next_member(const FileView &v, int64_t from)
+// the first offset in [from, to) where a gzip member starts (probed), or
+// v.size (to < 0: to the end of the file)
+int64_t next_member(const FileView &v, int64_t from, int64_t to = -1)
 {
-    const uint8_t *p = v.p + from, *e = v.p + v.size;
+    const uint8_t *p = v.p + from, *e = v.p + (to < 0 ? v.size : std::min(to, v.size));
     while (p < e) {
         p = (const uint8_t *)memchr(p, 0x1f, (size_t)(e - p));
         if (!p) break;
@@ -142,6 +143,52 @@ int64_t cut_at(const FileView &v, int64_t x)
 double ms_since(std::chrono::steady_clock::time_point t)
 {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+}  // namespace
+
+struct mh_fastq {
+    TextBuf data;                  // the held text
+    std::vector<int64_t> rec;      // byte offsets of its record starts (mh_fastq_frame)
+    bool framed = false;
+    // one part of a single gzip member (mh_fastq_member_*): the file's view
+    // and the part's decode state until mh_fastq_member_finish
+    std::unique_ptr<FileView> view;
+    MemberPart *member = nullptr;
+    int part = 0, parts = 1;
+    double member_ms = 0;
+    ~mh_fastq() { if (member) member_part_free(member); }
+};
+
+namespace {
+
+// newlines of d on host threads; info[3..6] of the open_part layout
+void text_info(const TextBuf &d, int64_t *info)
+{
+    const int64_t n = (int64_t)d.size();
+    const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 22) + 1));
+    std::vector<int64_t> cnt(nt, 0);
+    std::vector<std::thread> th;
+    auto count = [&](int t) {
+        const char *a = d.data() + n * t / nt, *b = d.data() + n * (t + 1) / nt;
+        int64_t k = 0;
+        while (a < b) {
+            const char *q = (const char *)memchr(a, '\n', (size_t)(b - a));
+            if (!q) break;
+            ++k;
+            a = q + 1;
+        }
+        cnt[t] = k;
+    };
+    for (int t = 1; t < nt; ++t) th.emplace_back(count, t);
+    count(0);
+    for (auto &x : th) x.join();
+    int64_t nl = 0;
+    for (int64_t k : cnt) nl += k;
+    info[3] = n;
+    info[4] = nl;
+    info[5] = n > 0 && d[n - 1] == '\n';
+    info[6] = n > 0 && d[0] == '\n';
 }
 
 }  // namespace
@@ -182,35 +229,10 @@ int mh_fastq_open_part(const char *path, int fd, int part, int parts, mh_fastq *
         } else if (c1 > c0) {
             fq->data.assign((const char *)v.p + c0, (size_t)(c1 - c0));
         }
-        const TextBuf &d = fq->data;
-        const int64_t n = (int64_t)d.size();
-        // newlines, counted on host threads
-        const int nt = std::max(1, std::min(s2a_threads(), (int)(n >> 22) + 1));
-        std::vector<int64_t> cnt(nt, 0);
-        std::vector<std::thread> th;
-        auto count = [&](int t) {
-            const char *a = d.data() + n * t / nt, *b = d.data() + n * (t + 1) / nt;
-            int64_t k = 0;
-            while (a < b) {
-                const char *q = (const char *)memchr(a, '\n', (size_t)(b - a));
-                if (!q) break;
-                ++k;
-                a = q + 1;
-            }
-            cnt[t] = k;
-        };
-        for (int t = 1; t < nt; ++t) th.emplace_back(count, t);
-        count(0);
-        for (auto &x : th) x.join();
-        int64_t nl = 0;
-        for (int64_t k : cnt) nl += k;
         info[0] = mode;
         info[1] = c0;
         info[2] = c1;
-        info[3] = n;
-        info[4] = nl;
-        info[5] = n > 0 && d[n - 1] == '\n';
-        info[6] = n > 0 && d[0] == '\n';
+        text_info(fq->data, info);
         info[7] = c1 - c0;
         info[8] = v.size;
         info[9] = (int64_t)(ms_since(t0) * 1000.0);   // microseconds
@@ -221,6 +243,133 @@ int mh_fastq_open_part(const char *path, int fd, int part, int parts, mh_fastq *
         return -2;
     } catch (const std::exception &e) {
         set_error("mh_fastq_open_part: %s", e.what());
+        return -4;
+    }
+}
+
+int mh_fastq_scan_part(const char *path, int fd, int part, int parts, int64_t *info)
+{
+    if (!info || (!path && fd < 0) || parts < 1 || part < 0 || part >= parts) {
+        set_error("mh_fastq_scan_part: bad arguments");
+        return -3;
+    }
+    try {
+        FileView v;
+        if (int st = view_file(path, fd, v)) return st;
+        const bool gz = v.size >= 2 && v.p[0] == 0x1f && v.p[1] == 0x8b;
+        const int64_t lo = v.size * part / parts, hi = v.size * (part + 1) / parts;
+        info[0] = gz;
+        info[1] = v.size;
+        // a member start inside this part's byte range (past offset 0, the
+        // file's first member): the scan covers 1/parts of the file
+        info[2] = gz && hi > std::max<int64_t>(lo, 1) && next_member(v, std::max<int64_t>(lo, 1), hi) < hi;
+        return 0;
+    } catch (const std::bad_alloc &) {
+        set_error("mh_fastq_scan_part: out of memory");
+        return -2;
+    } catch (const std::exception &e) {
+        set_error("mh_fastq_scan_part: %s", e.what());
+        return -4;
+    }
+}
+
+int mh_fastq_member_open(const char *path, int fd, int part, int parts, mh_fastq **out, int64_t *info)
+{
+    if (!out || !info || (!path && fd < 0) || parts < 1 || part < 0 || part >= parts) {
+        set_error("mh_fastq_member_open: bad arguments");
+        return -3;
+    }
+    *out = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        std::unique_ptr<mh_fastq> fq(new mh_fastq());
+        fq->view.reset(new FileView());
+        if (int st = view_file(path, fd, *fq->view)) return st;
+        const FileView &v = *fq->view;
+        for (int k = 0; k < 5; ++k) info[k] = -1;
+        info[5] = v.size;
+        if (v.size >= 2 && v.p[0] == 0x1f && v.p[1] == 0x8b)
+            fq->member = member_part_open(v.p, v.size, part, parts, s2a_threads(), info);
+        if (!fq->member) info[0] = -1;
+        fq->part = part;
+        fq->parts = parts;
+        fq->member_ms = ms_since(t0);
+        info[6] = (int64_t)(fq->member_ms * 1000.0);
+        *out = fq.release();
+        return 0;
+    } catch (const std::bad_alloc &) {
+        set_error("mh_fastq_member_open: out of memory");
+        return -2;
+    } catch (const std::exception &e) {
+        set_error("mh_fastq_member_open: %s", e.what());
+        return -4;
+    }
+}
+
+int mh_fastq_member_decode(mh_fastq *fq, int64_t end_bit, int64_t *info)
+{
+    if (!fq || !info || !fq->member) { set_error("mh_fastq_member_decode: bad arguments"); return -3; }
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        info[0] = -1;
+        if (member_part_decode(fq->member, end_bit, fq->part > 0, s2a_threads()) == 0 &&
+            member_part_place(fq->member, fq->data, s2a_threads()) == 0)
+            info[0] = (int64_t)fq->data.size();
+        fq->member_ms += ms_since(t0);
+        info[1] = (int64_t)(ms_since(t0) * 1000.0);
+        return 0;
+    } catch (const std::bad_alloc &) {
+        set_error("mh_fastq_member_decode: out of memory");
+        return -2;
+    } catch (const std::exception &e) {
+        set_error("mh_fastq_member_decode: %s", e.what());
+        return -4;
+    }
+}
+
+int mh_fastq_member_tail(mh_fastq *fq, const char *window, char *tail)
+{
+    if (!fq || !tail || !fq->member || (fq->part > 0 && !window)) {
+        set_error("mh_fastq_member_tail: bad arguments");
+        return -3;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    const int st = member_part_tail(fq->member, fq->data, window, tail);
+    fq->member_ms += ms_since(t0);
+    if (st) { set_error("mh_fastq_member_tail: the window does not resolve this part"); return -1; }
+    return 0;
+}
+
+int mh_fastq_member_finish(mh_fastq *fq, const char *window, int64_t c0, int64_t c1, int64_t *info)
+{
+    if (!fq || !info || !fq->member || (fq->part > 0 && !window)) {
+        set_error("mh_fastq_member_finish: bad arguments");
+        return -3;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        uint32_t crc = 0;
+        const int st = member_part_finish(fq->member, fq->data, window, s2a_threads(), &crc);
+        member_part_free(fq->member);
+        fq->member = nullptr;
+        const int64_t size = fq->view ? fq->view->size : 0;
+        fq->view.reset();
+        if (st) { set_error("mh_fastq_member_finish: the window does not resolve this part"); return -1; }
+        info[0] = 3;
+        info[1] = c0;
+        info[2] = c1;
+        text_info(fq->data, info);
+        info[7] = c1 - c0;
+        info[8] = size;
+        fq->member_ms += ms_since(t0);
+        info[9] = (int64_t)(fq->member_ms * 1000.0);
+        info[10] = crc;
+        return 0;
+    } catch (const std::bad_alloc &) {
+        set_error("mh_fastq_member_finish: out of memory");
+        return -2;
+    } catch (const std::exception &e) {
+        set_error("mh_fastq_member_finish: %s", e.what());
         return -4;
     }
 }

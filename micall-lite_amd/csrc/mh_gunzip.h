@@ -84,6 +84,27 @@ void unmap_text_file(const char *text, size_t len);
 // (mh_pinflate.cpp); -1 when it cannot be (the caller inflates serially).
 template <class Buf>
 int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int threads);
+// One part of one gzip member for a job of `parts` ranks (mh_pinflate.cpp):
+// open finds the part's span starts (info: [0] its first block start bit or
+// -1, [1] the deflate stream's end bit, [2] trailer CRC-32, [3] trailer size,
+// [4] spans); decode inflates them up to end_bit (the next part's first
+// start, or the stream's end), span 0 with an unknown window unless part 0;
+// place lays the text out in `out` (window-derived bytes symbolic); tail
+// resolves the last 32 KiB from the window (the previous part's last 32 KiB;
+// NULL for part 0) and copies them out; finish resolves the rest and gives
+// the CRC-32 of the part's text.  Each returns 0 or -1 (not decodable this
+// way: the caller falls back).
+struct MemberPart;
+MemberPart *member_part_open(const uint8_t *src, int64_t len, int part, int parts, int threads,
+                             int64_t *info);
+int member_part_decode(MemberPart *m, int64_t end_bit, bool windowed, int threads);
+template <class Buf>
+int member_part_place(MemberPart *m, Buf &out, int threads);
+template <class Buf>
+int member_part_tail(MemberPart *m, Buf &out, const char *window, char *tail);
+template <class Buf>
+int member_part_finish(MemberPart *m, Buf &out, const char *window, int threads, uint32_t *crc);
+void member_part_free(MemberPart *m);
 // Raw DEFLATE (RFC 1951) through libdeflate: ld_raw_alloc() is nullptr when
 // libdeflate is absent.  ld_raw_inflate decodes in[0 .. n) up to the end of
 // its final block: 0 (*in_used, *out_used set), 1 bad data, 3 out of space.

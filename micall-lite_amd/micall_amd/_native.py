@@ -152,6 +152,13 @@ def _declare(L):
         'mh_a2c_timing': ([_P, ctypes.c_int, _P], ctypes.c_int),
         'mh_fastq_open_part': ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 ctypes.POINTER(_P), _I64P], ctypes.c_int),
+        'mh_fastq_scan_part': ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64P],
+                               ctypes.c_int),
+        'mh_fastq_member_open': ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(_P), _I64P], ctypes.c_int),
+        'mh_fastq_member_decode': ([_P, ctypes.c_int64, _I64P], ctypes.c_int),
+        'mh_fastq_member_tail': ([_P, _P, _P], ctypes.c_int),
+        'mh_fastq_member_finish': ([_P, _P, ctypes.c_int64, ctypes.c_int64, _I64P], ctypes.c_int),
         'mh_fastq_frame': ([_P, ctypes.c_int64, ctypes.c_int, _I64P], ctypes.c_int),
         'mh_fastq_record_offset': ([_P, ctypes.c_int64, _I64P], ctypes.c_int),
         'mh_fastq_splice': ([_P, ctypes.c_int64, ctypes.c_int64, _P, ctypes.c_int64, _P,
@@ -966,14 +973,64 @@ class Fastq:
     INFO = ('mode', 'c0', 'c1', 'bytes', 'newlines', 'ends_nl', 'starts_nl', 'file_bytes_read',
             'file_size', 'decode_us')
 
-    def __init__(self, path=None, fd=-1, part=0, parts=1):
+    MEMBER_WINDOW = 32768
+    MEMBER_INFO = ('first_bit', 'end_bit', 'crc', 'isize', 'spans', 'file_size', 'open_us')
+
+    def __init__(self, path=None, fd=-1, part=0, parts=1, member=False):
+        """member=False: mh_fastq_open_part (this part's text, decoded).
+        member=True: mh_fastq_member_open -- part `part` of one gzip member,
+        searched but not decoded yet; info holds MEMBER_INFO, and the text
+        comes from member_decode / member_tail / member_finish."""
         h = ctypes.c_void_p()
         info = np.zeros(10, dtype=np.int64)
-        check(lib().mh_fastq_open_part(path.encode() if path else None, int(fd), int(part),
-                                       int(parts), ctypes.byref(h), info.ctypes.data_as(_I64P)),
-              'mh_fastq_open_part')
+        fn = 'mh_fastq_member_open' if member else 'mh_fastq_open_part'
+        check(getattr(lib(), fn)(path.encode() if path else None, int(fd), int(part), int(parts),
+                                 ctypes.byref(h), info.ctypes.data_as(_I64P)), fn)
         self.h = h
-        self.info = dict(zip(self.INFO, (int(x) for x in info)))
+        self.info = dict(zip(self.MEMBER_INFO if member else self.INFO, (int(x) for x in info)))
+        self.info_member = self.info if member else None
+
+    @staticmethod
+    def scan_part(path=None, fd=-1, part=0, parts=1):
+        """(is gzip, file size, a gzip member starts in this part's byte
+        range past offset 0): mh_fastq_scan_part."""
+        info = np.zeros(3, dtype=np.int64)
+        check(lib().mh_fastq_scan_part(path.encode() if path else None, int(fd), int(part), int(parts),
+                                       info.ctypes.data_as(_I64P)), 'mh_fastq_scan_part')
+        return bool(info[0]), int(info[1]), bool(info[2])
+
+    def member_decode(self, end_bit):
+        """Decode this member part up to end_bit: its text bytes, or -1."""
+        info = np.zeros(2, dtype=np.int64)
+        check(lib().mh_fastq_member_decode(self.h, int(end_bit), info.ctypes.data_as(_I64P)),
+              'mh_fastq_member_decode')
+        self.info['decode_us'] = int(info[1])
+        return int(info[0])
+
+    def member_tail(self, window):
+        """This part's last 32 KiB of text resolved from `window` (the part
+        before's tail; None for part 0), or None when it does not resolve."""
+        tail = np.zeros(self.MEMBER_WINDOW, dtype=np.uint8)
+        w = None if window is None else np.frombuffer(bytes(window), dtype=np.uint8)
+        st = lib().mh_fastq_member_tail(self.h, None if w is None else _ptr(w), _ptr(tail))
+        if st == -1:
+            return None
+        check(st, 'mh_fastq_member_tail')
+        return tail
+
+    def member_finish(self, window, c0, c1):
+        """Resolve the rest of the text; info becomes the open_part fields
+        (mode 3) plus 'crc' of this part's text.  False when it does not
+        resolve."""
+        info = np.zeros(11, dtype=np.int64)
+        w = None if window is None else np.frombuffer(bytes(window), dtype=np.uint8)
+        st = lib().mh_fastq_member_finish(self.h, None if w is None else _ptr(w), int(c0), int(c1),
+                                          info.ctypes.data_as(_I64P))
+        if st == -1:
+            return False
+        check(st, 'mh_fastq_member_finish')
+        self.info = dict(zip(self.INFO + ('crc',), (int(x) for x in info)))
+        return True
 
     def frame(self, line0, starts_line):
         """(first record offset, record starts, first record's file line,

@@ -3,15 +3,24 @@ Host-side mirror of micall/core/parse_interop.py: the Illumina InterOp
 ErrorMetricsOut.bin reader and the phiX error-rate CSV writer that feed the
 censor stage (bin/micall:101-106).  Byte parsing of a few kB; no device work.
 
-    read_records    parse_interop.py:13-38
-    read_errors     parse_interop.py:41-69
-    write_phix_csv  parse_interop.py:72-139 (with _yield_cycles, :72-91)
+    read_records    parse_interop.py:14-40
+    read_errors     parse_interop.py:43-72
+    write_phix_csv  parse_interop.py:98-139 (cycle renumbering :75-95)
+
+write_phix_csv's behaviour, restated: records are ordered by (tile, cycle,
+rate).  With read lengths [forward, index..., reverse], cycles up to the
+forward length are forward cycles, cycles from sum(lengths[:-1]) + 1 on are
+reverse cycles renumbered -1, -2, ..., and the index cycles between are
+dropped.  Each (tile, direction) lane is written in order with a blank row
+(tile and cycle only) for every cycle the records skip, counted from the
+lane's start; a record whose cycle does not advance (a duplicate) still
+takes the next slot.  With read lengths, the lane is then padded with blank
+rows to the read's length.  summary gets the mean rate of the written
+records per direction.
 """
 import csv
-import math
 import os
 import sys
-from itertools import groupby
 from struct import unpack
 
 
@@ -21,14 +30,15 @@ def read_records(data_file, min_version):
     if version < min_version:
         raise IOError('File version {} is less than minimum version {} in {}.'.format(
             version, min_version, data_file.name))
-    while True:
-        data = data_file.read(record_length)
-        if not data:
-            return
-        if len(data) < record_length:
-            raise IOError('Partial record of length {} found in {}.'.format(len(data),
-                                                                           data_file.name))
-        yield data
+    if record_length == 0:     # every read of 0 bytes comes back empty: no records
+        return
+    body = memoryview(data_file.read())
+    whole = len(body) - len(body) % record_length
+    for at in range(0, whole, record_length):
+        yield bytes(body[at:at + record_length])
+    if len(body) > whole:
+        raise IOError('Partial record of length {} found in {}.'.format(len(body) - whole,
+                                                                       data_file.name))
 
 
 _ERROR_FIELDS = ('lane', 'tile', 'cycle', 'error_rate', 'num_0_errors', 'num_1_error',
@@ -42,17 +52,40 @@ def read_errors(data_file):
         yield dict(zip(_ERROR_FIELDS, unpack('<HHHfLLLLL', data[:30])))
 
 
-def _cycles(records, read_lengths):
-    """(tile, cycle, error_rate) sorted; reverse-read cycles renumbered
-    -1, -2, ... and index-read cycles dropped."""
-    rows = sorted((r['tile'], r['cycle'], r['error_rate']) for r in records)
-    last_forward = read_lengths[0] if read_lengths else sys.maxsize
-    first_reverse = sum(read_lengths[:-1]) + 1 if read_lengths else sys.maxsize
-    for tile, cycle, rate in rows:
-        if cycle >= first_reverse:
-            yield tile, first_reverse - cycle - 1, rate
-        elif cycle <= last_forward:
-            yield tile, cycle, rate
+def _lanes(records, read_lengths):
+    """{(tile, +1 | -1): [(cycle number within the read, rate), ...]} in
+    (tile, cycle, rate) order; index-read cycles left out."""
+    if read_lengths:
+        forward_end, reverse_start = read_lengths[0], sum(read_lengths[:-1]) + 1
+    else:
+        forward_end = reverse_start = sys.maxsize
+    lanes = {}
+    for tile, cycle, rate in sorted((r['tile'], r['cycle'], r['error_rate']) for r in records):
+        if cycle >= reverse_start:
+            lanes.setdefault((tile, -1), []).append((cycle - reverse_start + 1, rate))
+        elif cycle <= forward_end:
+            lanes.setdefault((tile, 1), []).append((cycle, rate))
+    return lanes
+
+
+def _phix_rows(records, read_lengths, totals):
+    """The CSV rows of write_phix_csv; totals[direction] = [sum, count] of
+    the record rates written."""
+    lanes = _lanes(records, read_lengths)
+    rows = []
+    for tile, direction in sorted(lanes, key=lambda key: (key[0], -key[1])):
+        slot = 0
+        acc = totals[direction]
+        for number, rate in lanes[tile, direction]:
+            rows.extend((tile, direction * blank) for blank in range(slot + 1, number))
+            rows.append((tile, direction * number, rate))
+            slot = max(slot + 1, number)
+            acc[0] += rate
+            acc[1] += 1
+        if read_lengths:
+            length = read_lengths[0] if direction == 1 else read_lengths[-1]
+            rows.extend((tile, direction * blank) for blank in range(slot + 1, length + 1))
+    return rows
 
 
 def write_phix_csv(out_file, records, read_lengths=None, summary=None):
@@ -66,28 +99,13 @@ def write_phix_csv(out_file, records, read_lengths=None, summary=None):
 
 
 def _write_phix_csv(out_file, records, read_lengths, summary):
+    totals = {1: [0.0, 0], -1: [0.0, 0]}
+    rows = _phix_rows(records, read_lengths, totals)
     writer = csv.writer(out_file, lineterminator=os.linesep)
     writer.writerow(['tile', 'cycle', 'errorrate'])
-    sums, counts = [0.0, 0.0], [0, 0]
-    for (tile, sign), group in groupby(_cycles(records, read_lengths),
-                                       lambda r: (r[0], int(math.copysign(1, r[1])))):
-        prev = 0
-        last = None
-        for last in group:
-            prev += sign
-            while prev * sign < last[1] * sign:
-                writer.writerow((last[0], prev))
-                prev += sign
-            writer.writerow(last)
-            k = (sign + 1) // 2
-            sums[k] += last[2]
-            counts[k] += 1
-        if read_lengths:
-            end = read_lengths[0] if sign == 1 else -read_lengths[-1]
-            while prev * sign < end * sign:
-                prev += sign
-                writer.writerow((last[0], prev))
-    if counts[1] > 0 and summary is not None:
-        summary['error_rate_fwd'] = sums[1] / counts[1]
-    if counts[0] > 0 and summary is not None:
-        summary['error_rate_rev'] = sums[0] / counts[0]
+    writer.writerows(rows)
+    if summary is not None:
+        for direction, key in ((1, 'error_rate_fwd'), (-1, 'error_rate_rev')):
+            total, count = totals[direction]
+            if count:
+                summary[key] = total / count

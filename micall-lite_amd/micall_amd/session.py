@@ -12,11 +12,17 @@ WORLD_SIZE > 1 in the environment, in which case the group is initialised
 here over MICALL_DIST_BACKEND, default nccl = RCCL), every rank keeps its
 own contiguous block of read pairs resident (mh_reads_load_fastq_part) and
 the drop-ins exchange counters through pipeline.Shard.  Every rank opens the
-same paths and then calls the drop-ins with the same arguments; rank 0
-writes the output files, in the order a single GPU writes them (each drop-in
-starts with a barrier, so no rank's open can truncate what rank 0 wrote).
+same paths and then calls the drop-ins with the same arguments.  The large
+outputs (prelim.csv, remap.csv, the censored FASTQs, the unmapped FASTQs)
+are written by every rank: each `pwrite`s its own rows at offsets
+all-gathered from every rank's byte counts, so the file holds the rows in
+the order a single GPU writes them (sharded_io.py).  The small reports
+(remap_counts.csv, remap_conseq.csv, the InterOp CSVs) are written by rank
+0 (writer_stage).  Each drop-in starts with a barrier, so no rank's open can
+truncate what another rank wrote.
 """
 import os
+import time
 
 from . import _native
 
@@ -219,6 +225,24 @@ def _file_identity(handle):
     return st.st_dev, st.st_ino, st.st_size, st.st_mtime_ns, st.st_ctime_ns
 
 
+def _wait_past(ctime_ns, limit_s=0.05):
+    """Return once the kernel's coarse clock, which stamps file changes, has
+    moved past `ctime_ns` (at most one timer tick, a few ms).  A later
+    rewrite of the file then gets a newer ctime, so an unchanged identity
+    proves unchanged content: a same-size rewrite inside the tick of our
+    last write cannot pass for our file.  False when that could not be
+    established (the identity alone is then not trusted)."""
+    clock = getattr(time, 'CLOCK_REALTIME_COARSE', None)
+    if clock is None:
+        return False
+    deadline = time.monotonic() + limit_s
+    while time.clock_gettime_ns(clock) <= ctime_ns:
+        if time.monotonic() >= deadline:
+            return False
+        time.sleep(0.0005)
+    return True
+
+
 def prelim_written(ctx, handle, seed_names, checksum=None):
     """Record that prelim_map() wrote `handle` from the device records that
     are resident now (ctx.map_serial) for these seeds: the file's identity
@@ -226,13 +250,15 @@ def prelim_written(ctx, handle, seed_names, checksum=None):
     formatted (no read-back)."""
     global _prelim
     ident = None
+    settled = False
     if is_writer():
         try:
             handle.flush()
         except (AttributeError, OSError, ValueError):
             pass
         ident = _file_identity(handle)
-    _prelim = dict(identity=ident, checksum=checksum, serial=ctx.map_serial, key=_key,
+        settled = ident is not None and _wait_past(ident[4])
+    _prelim = dict(identity=ident, settled=settled, checksum=checksum, serial=ctx.map_serial, key=_key,
                    seeds=list(seed_names))
 
 
@@ -250,7 +276,7 @@ def prelim_resident(ctx, handle, seed_names):
     if ok and is_writer():
         ident = _file_identity(handle)
         ok = ident is not None and p['identity'] is not None
-        if ok and ident != p['identity']:
+        if ok and (ident != p['identity'] or not p['settled']):
             ok = False
             want = p['checksum']
             if want is not None and ident[2] == want[1] and ident[:2] == p['identity'][:2]:

@@ -6,13 +6,15 @@ file from its one process (prelim_map.py:114-151, remap.py:612-658,
 censor_fastq.py:58-96).  In a job of W ranks each rank here
 
   * reads its 1/W share of every FASTQ file (`stage_fastq`): the gzip members
-    that start in its byte range (a plain file: the byte range), frames the
-    text into four-line records from the line counts of the ranks before it,
-    passes the bytes in front of its first record to the rank before, and, for
-    a pair of files, exchanges whole records so that its R1 and R2 blocks hold
-    the same reads.  A file that cannot be split that way (one gzip member, as
-    bcl2fastq writes it; a blank line where a record starts) is decoded whole
-    by every rank, which keeps its records by count -- the round-3 behaviour;
+    that start in its byte range (a plain file: the byte range; a file that is
+    one gzip member, as bcl2fastq writes it: the deflate blocks that start in
+    its share of the compressed bytes, `_open_members`), frames the text into
+    four-line records from the line counts of the ranks before it, passes the
+    bytes in front of its first record to the rank before, and, for a pair of
+    files, exchanges whole records so that its R1 and R2 blocks hold the same
+    reads.  A file that cannot be split (a blank line where a record starts;
+    a member with no block start in some rank's share) is decoded whole by
+    every rank, which keeps its records by count;
   * writes its own rows of every output file (`SharedOutput`) with pwrite at
     offsets computed from the all-gathered segment sizes, so the file holds
     the rows in single-GPU order (segment 0 of rank 0, rank 1, ..., then
@@ -86,6 +88,97 @@ class _Frame:
         self.fq, self.first, self.count, self.total, self.lines = fq, first, count, total, lines
 
 
+def _open_members(sh, sources):
+    """Each source file one gzip member: this rank's part of each, decoded
+    from its own share of the compressed bytes (mh_fastq_member_*).
+
+    1. every rank finds the first deflate block start in its share (rank 0:
+       the stream's start) and the ranks all-gather them: rank r decodes up
+       to rank r + 1's start, on its threads, with the window it lacks (the
+       last 32 KiB of rank r - 1's text) left symbolic;
+    2. the windows travel in rank order: rank r receives rank r - 1's
+       resolved last 32 KiB of every file (one message), resolves its own
+       last 32 KiB with it and sends them on to rank r + 1 (W - 1 messages
+       of 32 KiB per file in all);
+    3. every rank resolves the rest of its text in parallel and all-gathers
+       the CRC-32 and size of its text: combined in rank order they must
+       equal the gzip trailer's.
+
+    Returns [Fastq or None] per source; None (on every rank) for a file that
+    cannot be split this way (the caller then decodes it whole)."""
+    W, r = sh.world, sh.rank
+    n = len(sources)
+
+    def each(fn, items):
+        if len(items) <= 1:
+            return [fn(x) for x in items]
+        with ThreadPoolExecutor(len(items)) as ex:
+            return list(ex.map(fn, items))
+    fqs = _checked(sh, lambda: each(lambda src: _native.Fastq(src[0], src[1] if src[1] is not None
+                                                               else -1, r, W, member=True), sources))
+    starts = sh._gather_sizes([fq.info['first_bit'] for fq in fqs])        # [rank, source]
+    ok = [bool((starts[:, k] >= 0).all()) and bool((np.diff(starts[:, k]) > 0).all()) for k in range(n)]
+
+    def decode(k):
+        if not ok[k]:
+            return -1
+        end = int(starts[r + 1, k]) if r + 1 < W else fqs[k].info['end_bit']
+        return fqs[k].member_decode(end)
+    sizes = _checked(sh, lambda: each(decode, list(range(n))))
+    good = sh._gather_sizes([1 if sz >= 0 else 0 for sz in sizes]).min(axis=0)
+    live = [k for k in range(n) if ok[k] and good[k]]
+    windows = {k: None for k in live}
+    resolved = {k: True for k in live}
+    if live:
+        torch, dist = sh.torch, sh.dist
+        dev = sh._text_device()
+        win = _native.Fastq.MEMBER_WINDOW
+        if r > 0:
+            t = torch.empty(win * len(live), dtype=torch.uint8, device=dev)
+            dist.recv(t, src=r - 1)
+            got = t.cpu().numpy()
+            for j, k in enumerate(live):
+                windows[k] = got[j * win:(j + 1) * win].tobytes()
+        tails = []
+        for k in live:
+            try:
+                tail = fqs[k].member_tail(windows[k])
+            except _native.NativeError:
+                tail = None
+            if tail is None:          # sent on anyway (the chain must not stall); the CRC check fails
+                resolved[k] = False
+                tail = np.zeros(win, dtype=np.uint8)
+            tails.append(tail)
+        if r + 1 < W:
+            dist.send(torch.from_numpy(np.concatenate(tails)).to(dev), dst=r + 1)
+
+    def finish(k):
+        if k not in resolved or not resolved[k]:
+            return False
+        c0 = 0 if r == 0 else int(starts[r, k]) // 8
+        c1 = fqs[k].info['file_size'] if r + 1 == W else int(starts[r + 1, k]) // 8
+        return fqs[k].member_finish(windows[k], c0, c1)
+    done = _checked(sh, lambda: each(finish, list(range(n))))
+    rows = sh._gather_sizes([v for k in range(n) for v in (
+        1 if done[k] else 0, fqs[k].info.get('crc', 0) if done[k] else 0,
+        fqs[k].info.get('bytes', 0) if done[k] else 0)]).reshape(W, n, 3)
+    out = []
+    for k in range(n):
+        fine = bool(rows[:, k, 0].all())
+        if fine:
+            crc, total = 0, 0
+            for q in range(W):
+                crc = _native.crc32_combine(crc, int(rows[q, k, 1]), int(rows[q, k, 2]))
+                total += int(rows[q, k, 2])
+            fine = crc == fqs[k].info_member['crc'] and (total & 0xffffffff) == fqs[k].info_member['isize']
+        if not fine:
+            fqs[k].close()
+            out.append(None)
+        else:
+            out.append(fqs[k])
+    return out
+
+
 def _open_all(sh, sources, part, parts):
     def one(src):
         path, fd = src
@@ -105,7 +198,7 @@ def _frame_sharded(sh, fq, strict):
     rows = sh._gather_sizes([inf['mode'], inf['c0'], inf['c1'], inf['bytes'], inf['newlines'],
                              inf['ends_nl'], inf['starts_nl'], inf['file_size']])
     mode, c0, c1, nbytes, nl, ends_nl, starts_nl, size = (rows[:, k] for k in range(8))
-    chain = (all(m in (1, 2) for m in mode) and c0[0] == 0 and c1[W - 1] == size[0] and
+    chain = (all(m in (1, 2, 3) for m in mode) and c0[0] == 0 and c1[W - 1] == size[0] and
              all(c1[k] == c0[k + 1] for k in range(W - 1)))
     if not chain:
         return None
@@ -202,12 +295,35 @@ def stage_fastq(sh, sources, strict=False):
     when the ingest should fall back to the whole-file loader
     (mh_reads_load_fastq_part)."""
     W, r = sh.world, sh.rank
-    fqs = _checked(sh, lambda: _open_all(sh, sources, r, W))
-    frames = [_checked(sh, lambda fq=fq: _frame_sharded(sh, fq, strict)) for fq in fqs]
-    IO_STATS['fastq_file_bytes'] += sum(fq.info['file_bytes_read'] for fq in fqs)
+    n = len(sources)
+    # which files are one gzip member: no rank finds a member start in its
+    # byte range (each scans 1/W of the file)
+    scans = _checked(sh, lambda: [_native.Fastq.scan_part(p, fd if fd is not None else -1, r, W)
+                                  for p, fd in sources])
+    flags = sh._gather_sizes([v for gz, _size, found in scans for v in (int(gz), int(found))])
+    single = [bool(flags[0, 2 * k]) and not flags[:, 2 * k + 1].any() for k in range(n)]
+    fqs = [None] * n
+    tried_member = [k for k in range(n) if single[k]]
+    if tried_member:
+        for k, fq in zip(tried_member, _open_members(sh, [sources[k] for k in tried_member])):
+            fqs[k] = fq
+            if fq is not None:
+                IO_STATS['fastq_file_bytes'] += fq.info['file_bytes_read']
+    split = [k for k in range(n) if not single[k]]
+    if split:
+        opened = _checked(sh, lambda: _open_all(sh, [sources[k] for k in split], r, W))
+        for k, fq in zip(split, opened):
+            fqs[k] = fq
+            IO_STATS['fastq_file_bytes'] += fq.info['file_bytes_read']
+    # a single member that could not be split is read whole below (no
+    # member-range decode first)
+    frames = [None if fq is None else _checked(sh, lambda fq=fq: _frame_sharded(sh, fq, strict))
+              for fq in fqs]
+    member_split = any(f is not None and single[k] for k, f in enumerate(frames))
     if all(f is None for f in frames):
         for fq in fqs:
-            fq.close()
+            if fq is not None:
+                fq.close()
         if not strict:
             return None            # every rank reads the files whole (the part loader)
         fqs = _checked(sh, lambda: _open_all(sh, sources, 0, 1))
@@ -217,7 +333,8 @@ def stage_fastq(sh, sources, strict=False):
     else:
         for k, f in enumerate(frames):
             if f is None:          # this one is read whole, its partner split
-                fqs[k].close()
+                if fqs[k] is not None:
+                    fqs[k].close()
                 whole = _checked(sh, lambda k=k: _open_all(sh, [sources[k]], 0, 1)[0])
                 IO_STATS['fastq_file_bytes'] += whole.info['file_bytes_read']
                 frames[k] = _frame_whole(whole, strict)
@@ -226,7 +343,7 @@ def stage_fastq(sh, sources, strict=False):
                         if f2 is not None:
                             f2.fq.close()
                     return None
-        mode = 'members'
+        mode = 'member-part' if member_split else 'members'
     totals = [f.total for f in frames]
     if len(set(totals)) != 1:
         raise _native.NativeError('paired FASTQ files hold {} and {} reads'.format(*totals))

@@ -139,7 +139,10 @@ def run_step(seed_set, all_seeds, seed_groups, seqs, quals, paired=True, nthread
 # before the clock starts.
 # ---------------------------------------------------------------------------
 class Prepared:
-    """Reads packed once into the buffers og_map / og_rows_from_alns take."""
+    """Reads packed once into the buffers og_map / og_rows_from_alns take.
+    Each mapping pass of timed_step has its own record buffer (alns: the
+    prelim pass, alns2: the remap pass), so both stay readable afterwards
+    (bench.py's parity leg compares them with the device's records)."""
 
     def __init__(self, seqs, quals, paired):
         self.n = len(seqs)
@@ -153,10 +156,31 @@ class Prepared:
             pos += len(s)
         self.sbuf = ''.join(seqs).encode()
         self.qbuf = ''.join(quals).encode()
-        self.seq_out = ctypes.create_string_buffer(max(pos, 1))
-        self.qual_out = ctypes.create_string_buffer(max(pos, 1))
+        self._buffers(pos)
+
+    @classmethod
+    def from_arrays(cls, reads, quals, paired):
+        """(n, L) uint8 read / quality arrays (mates interleaved when
+        paired), without a per-read Python loop."""
+        self = cls.__new__(cls)
+        n, L = reads.shape
+        self.n, self.paired = n, paired
+        self.offs = (ctypes.c_int64 * max(n, 1)).from_buffer_copy(
+            (np.arange(max(n, 1), dtype=np.int64) * L).tobytes())
+        self.lens = (ctypes.c_int32 * max(n, 1)).from_buffer_copy(
+            np.full(max(n, 1), L, dtype=np.int32).tobytes())
+        self.sbuf = np.ascontiguousarray(reads).tobytes()
+        self.qbuf = np.ascontiguousarray(quals).tobytes()
+        self._buffers(n * L)
+        return self
+
+    def _buffers(self, total):
+        self.seq_out = ctypes.create_string_buffer(max(total, 1))
+        self.qual_out = ctypes.create_string_buffer(max(total, 1))
         self.rows = (oracle.OgRow * max(self.n, 1))()
         self.alns = (oracle.OgAln * max(self.n, 1))()
+        self.alns2 = (oracle.OgAln * max(self.n, 1))()
+        self.result = None
 
 
 def _declare_fast(L):
@@ -170,17 +194,25 @@ def _declare_fast(L):
     L._fast_declared = True
 
 
-def _map_fast(prep, ix, mode, nthreads):
+def _map_fast(prep, ix, mode, nthreads, out):
     st = oracle.lib().og_map(ix.handle, ctypes.byref(oracle.params(mode)), prep.n, int(prep.paired),
-                             prep.sbuf, prep.qbuf, prep.offs, prep.lens, prep.alns, nthreads)
+                             prep.sbuf, prep.qbuf, prep.offs, prep.lens, out, nthreads)
     if st:
         raise RuntimeError('og_map status %d' % st)
-    return np.frombuffer(prep.alns, dtype=_ALN_DTYPE, count=prep.n)
+    return np.frombuffer(out, dtype=_ALN_DTYPE, count=prep.n)
 
 
-def _pileup_fast(prep, recs, n_refs, ref_lens, nthreads, q=20):
+def map_arrays(refseqs, mode, reads, quals, paired, nthreads=0):
+    """og_map of (n, L) read / quality arrays against refseqs: the records
+    as a numpy array of _ALN_DTYPE (the device's ALN_DTYPE layout)."""
+    prep = Prepared.from_arrays(reads, quals, paired)
+    ix = oracle.Index(list(refseqs), oracle.seed_len(mode))
+    return _map_fast(prep, ix, mode, nthreads, prep.alns).copy()
+
+
+def _pileup_fast(prep, alns, recs, n_refs, ref_lens, nthreads, q=20):
     L = oracle.lib()
-    L.og_rows_from_alns(prep.alns, prep.n, prep.sbuf, prep.qbuf, prep.offs, prep.lens,
+    L.og_rows_from_alns(alns, prep.n, prep.sbuf, prep.qbuf, prep.offs, prep.lens,
                         prep.seq_out, prep.qual_out, prep.rows, nthreads)
     sam_ref = recs['sam_ref']
     if prep.paired:
@@ -219,7 +251,7 @@ def timed_step(seed_set, all_seeds, seed_groups, prep, nthreads, count_threshold
     t0 = time.perf_counter()
     names = list(seed_set)
     ix = oracle.Index([seed_set[k] for k in names], 22)
-    recs = _map_fast(prep, ix, oracle.E2E, nthreads)
+    recs = _map_fast(prep, ix, oracle.E2E, nthreads, prep.alns)
     sam_ref = recs['sam_ref']
     mapped = (recs['flag'] & 4) == 0
     longest_m = _longest_m(recs)
@@ -236,17 +268,21 @@ def timed_step(seed_set, all_seeds, seed_groups, prep, nthreads, count_threshold
         if f > best:
             refgroups[seed_groups[name]] = (name, f)
     seed_counts = {r: c for r, c in refgroups.values()}
-    pile = _pileup_fast(prep, recs, len(names), [len(seed_set[k]) for k in names], nthreads)
+    pile = _pileup_fast(prep, prep.alns, recs, len(names), [len(seed_set[k]) for k in names], nthreads)
     order = sorted((r for r in range(len(names)) if pile[2][r] >= 0), key=lambda r: first[names[r]])
     conseqs = {k: v for k, v in _conseqs(names, all_seeds, pile, order).items() if k in seed_counts}
+    prelim_conseqs, cn, recs2 = dict(conseqs), [], None
     if conseqs:
         cn = list(conseqs)
         ix2 = oracle.Index([conseqs[k] for k in cn], 20)
-        recs2 = _map_fast(prep, ix2, oracle.LOCAL, nthreads)
-        pile2 = _pileup_fast(prep, recs2, len(cn), [len(conseqs[k]) for k in cn], nthreads)
+        recs2 = _map_fast(prep, ix2, oracle.LOCAL, nthreads, prep.alns2)
+        pile2 = _pileup_fast(prep, prep.alns2, recs2, len(cn), [len(conseqs[k]) for k in cn], nthreads)
         order2 = sorted((r for r in range(len(cn)) if pile2[2][r] >= 0), key=lambda r: pile2[2][r])
         conseqs = _conseqs(cn, all_seeds, pile2, order2)
-    return conseqs, time.perf_counter() - t0
+    secs = time.perf_counter() - t0
+    prep.result = dict(prelim=recs, prelim_names=names, prelim_conseqs=prelim_conseqs,
+                       remap=recs2, remap_names=cn, conseqs=conseqs)
+    return conseqs, secs
 
 
 _ALN_DTYPE = np.dtype([(name, np.int32) for name, _ in oracle.OgAln._fields_[:-1]] +

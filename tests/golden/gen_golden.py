@@ -719,6 +719,78 @@ def gen_censor():
     print('censor: {} bad cycles, {} scenarios'.format(bad.getvalue().count('\n') - 1, len(cases)))
 
 
+def gen_interop_edge():
+    """Edge cases of the reference's write_phix_csv and report_bad_cycles:
+    duplicate (tile, cycle) records, cycle 0, gaps at a lane's start and end,
+    index cycles, lanes with only one direction, blank and bad rates inside
+    a run, a tile that comes back after another, rates that are not
+    numbers after the first bad cycle; plus seeded random tables.
+    tests/golden/censor/interop_edge.json."""
+    import random
+    refharness.setup()
+    from micall.core.filter_quality import report_bad_cycles
+    from micall.core.parse_interop import write_phix_csv
+
+    def rec(tile, cycle, rate):
+        return dict(lane=1, tile=tile, cycle=cycle, error_rate=rate)
+    phix = [
+        ('dups_and_gaps', [rec(1101, 3, 0.5), rec(1101, 3, 0.25), rec(1101, 5, 1.0),
+                           rec(1101, 5, 1.0), rec(1101, 6, 2.0), rec(1101, 22, 0.5),
+                           rec(1101, 27, 8.0)], [6, 2, 2, 6]),
+        ('cycle_zero', [rec(1102, 0, 0.5), rec(1102, 1, 0.5), rec(1102, 4, 0.75)], [4, 4]),
+        ('reverse_only', [rec(1103, 9, 0.5), rec(1103, 12, 0.75), rec(1101, 11, 9.5)], [4, 4, 4]),
+        ('index_only', [rec(1101, 5, 0.5), rec(1101, 6, 0.5)], [4, 4, 4]),
+        ('no_index', [rec(2101, c, 0.125 * c) for c in (1, 2, 4, 5, 8)], [4, 4]),
+        ('short_lengths', [rec(1101, c, 1.5) for c in range(1, 12)], [3, 2, 3]),
+        ('empty', [], [5, 5]),
+    ]
+    rng = random.Random(11)
+    for k in range(6):
+        lengths = [rng.randint(3, 12), rng.randint(0, 3), rng.randint(3, 12)]
+        if k % 2:
+            lengths = [lengths[0], lengths[1], lengths[1], lengths[2]]
+        recs = [rec(rng.choice((1101, 1102, 2101)), rng.randint(0, sum(lengths) + 2),
+                    rng.choice((0.1, 0.5, 2.0, 7.5, 12.0))) for _ in range(rng.randint(5, 40))]
+        phix.append(('random%d' % k, recs, lengths))
+    phix_out = []
+    for name, recs, lengths in phix:
+        out, summary = io.StringIO(), {}
+        write_phix_csv(out, iter([dict(r) for r in recs]), lengths, summary)
+        phix_out.append(dict(name=name, records=recs, read_lengths=lengths, csv=out.getvalue(),
+                             summary=summary))
+    quality = [
+        ('blank_mid_run', 'tile,cycle,errorrate\n1101,1,0.5\n1101,2,\n1101,3,0.5\n1101,-1,0.5\n'
+                          '1101,-2,9.0\n1101,-3,0.1\n'),
+        ('tile_returns', 'tile,cycle,errorrate\n1101,1,8.0\n1101,2,0.5\n1102,1,0.5\n1102,2,7.5\n'
+                         '1101,1,0.5\n1101,2,7.49\n1101,3,7.5\n'),
+        ('direction_flips', 'tile,cycle,errorrate\n1101,1,0.5\n1101,-1,8.0\n1101,2,0.5\n'
+                            '1101,-2,0.5\n1101,0,9.0\n'),
+        ('missing_column', 'tile,cycle,errorrate\n1101,1,0.5\n1101,2\n1101,3,0.5\n'),
+        ('not_a_number_after_bad', 'tile,cycle,errorrate\n1101,1,8.0\n1101,2,oops\n1101,3,0.5\n'),
+        ('all_good', 'tile,cycle,errorrate\n1101,1,0.5\n1101,-1,0.5\n'),
+        ('header_only', 'tile,cycle,errorrate\n'),
+    ]
+    for k in range(6):
+        lines = ['tile,cycle,errorrate']
+        for _ in range(rng.randint(3, 30)):
+            rate = rng.choice(('0.5', '1.0', '', '7.5', '7.4', '12'))
+            lines.append('{},{},{}'.format(rng.choice((1101, 1102)), rng.choice((1, 2, -1, -2, 3)),
+                                           rate))
+        quality.append(('random%d' % k, '\n'.join(lines) + '\n'))
+    quality_out = []
+    for name, text in quality:
+        bad, tiles = io.StringIO(), io.StringIO()
+        report_bad_cycles(io.StringIO(text), bad, tiles)
+        quality_out.append(dict(name=name, quality_csv=text, bad_cycles_csv=bad.getvalue(),
+                                bad_tiles_csv=tiles.getvalue()))
+    path = os.path.join(HERE, 'censor', 'interop_edge.json')
+    with open(path, 'w') as f:
+        json.dump(dict(source='reference micall.core parse_interop.write_phix_csv / '
+                              'filter_quality.report_bad_cycles outputs',
+                       phix=phix_out, quality=quality_out), f, indent=0)
+    print('interop_edge: {} phix tables, {} quality tables'.format(len(phix_out), len(quality_out)))
+
+
 def _error_metrics(lengths, tiles, bad, seed):
     """A version-3 ErrorMetricsOut.bin: every (tile, cycle) of the run, the
     (tile, run cycle) pairs in `bad` at an error rate >= 7.5.  A bad cycle

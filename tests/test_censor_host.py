@@ -46,6 +46,43 @@ def test_report_bad_cycles_matches_reference():
     assert tiles.getvalue() == G['bad_tiles_csv']
 
 
+EDGE = json.load(open(os.path.join(CDIR, 'interop_edge.json')))
+
+
+@pytest.mark.parametrize('case', EDGE['phix'], ids=lambda c: c['name'])
+def test_phix_csv_edge_cases_match_reference(case):
+    """Duplicates, cycle 0, gaps at lane ends, index cycles, one-direction
+    lanes, random tables: write_phix_csv's rows and summary as the
+    reference wrote them (gen_golden.py interop_edge)."""
+    out, summary = io.StringIO(), {}
+    parse_interop.write_phix_csv(out, iter([dict(r) for r in case['records']]),
+                                 case['read_lengths'], summary)
+    assert out.getvalue() == case['csv']
+    assert summary == case['summary']
+
+
+@pytest.mark.parametrize('case', EDGE['quality'], ids=lambda c: c['name'])
+def test_bad_cycles_edge_cases_match_reference(case):
+    """Blank rates inside a run, a tile that comes back, direction flips,
+    rows missing the rate column, unparsable rates after the first bad one."""
+    bad, tiles = io.StringIO(), io.StringIO()
+    filter_quality.report_bad_cycles(io.StringIO(case['quality_csv']), bad, tiles)
+    assert bad.getvalue() == case['bad_cycles_csv']
+    assert tiles.getvalue() == case['bad_tiles_csv']
+
+
+def test_read_records_zero_length_and_stream():
+    """A zero record length yields nothing (the reference's read(0) loop
+    stops at once); whole records come out in order before a partial one
+    raises."""
+    assert list(parse_interop.read_records(_Named(bytes([3, 0]) + b'xyz'), 3)) == []
+    got = []
+    with pytest.raises(IOError, match='Partial record of length 2'):
+        for rec in parse_interop.read_records(_Named(bytes([3, 3]) + b'abcdefgh'), 3):
+            got.append(rec)
+    assert got == [b'abc', b'def']
+
+
 @pytest.mark.parametrize('k', range(len(G['cases'])))
 def test_oracle_censor_scenarios(k):
     case = G['cases'][k]

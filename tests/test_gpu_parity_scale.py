@@ -1,0 +1,115 @@
+"""GPU parity at configuration scale: 100k read pairs (or unpaired reads) of
+each read shape the BASELINE configs use, through the device pipeline, every
+alignment record compared byte for byte with the CPU oracle's (og_map) on
+the same reads, and the consensus compared with the oracle step's
+(oracle/cpu_pipeline.timed_step).
+
+    pol_2x251        C2 / C3: 2x251 HIV-1 pol pairs
+    hiv_mixed_2x251  C4: 2x251 pairs over the HIV-1 seeds (several seed
+                     groups, so several consensus references)
+    unpaired_1x300   C5: unpaired 1x300 pol reads
+
+At this size the paths only large batches take run: the DP work queue past
+its first chunk of blocks, CIGAR-pool growth under load, the full k_seed
+grid, k_pair's tally flushes over many blocks.  Reference consumers of the
+records: remap.py:474-541, prelim_map.py:134-151."""
+import os
+
+import numpy as np
+import pytest
+
+import cpu_pipeline
+import oracle
+from micall_amd import _native, projects, synth
+from micall_amd.pipeline import RemapPipeline
+
+pytestmark = pytest.mark.gpu
+
+UNITS = 100000
+SEED = 20261015
+CFG = projects.load_default()
+SEEDS = CFG.seed_sequences()
+
+
+def _threads():
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get('OMP_NUM_THREADS', '')
+    return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
+
+
+def _genomes(which, read_len):
+    if which == 'pol':
+        return {'HIV1B-pol-seed': SEEDS['HIV1B-pol-seed']}
+    return {k: v for k, v in SEEDS.items()
+            if k.startswith('HIV') and len(v) >= max(260, read_len + 9)}
+
+
+def _reads(which, read_len, paired):
+    d = synth.make_pairs(UNITS, genomes=_genomes(which, read_len), genome_seed=SEED,
+                         read_seed=SEED + 7, read_len=read_len, paired=paired)
+    if not paired:
+        return d['r1'], d['q1']
+    reads = np.stack([d['r1'], d['r2']], axis=1).reshape(2 * UNITS, read_len)
+    quals = np.stack([d['q1'], d['q2']], axis=1).reshape(2 * UNITS, read_len)
+    return reads, quals
+
+
+def _assert_records_equal(dev, ref, what):
+    assert len(dev) == len(ref)
+    same = np.ones(len(ref), dtype=bool)
+    for f in _native.ALN_FIELDS:
+        same &= dev[f] == ref[f]
+    live = np.arange(ref['cigar'].shape[1])[None, :] < ref['n_cigar'][:, None]
+    same &= np.all((dev['cigar'] == ref['cigar']) | ~live, axis=1)
+    bad = np.flatnonzero(~same)
+    if len(bad):
+        i = int(bad[0])
+        diff = {f: (int(dev[i][f]), int(ref[i][f])) for f in _native.ALN_FIELDS
+                if dev[i][f] != ref[i][f]}
+        pytest.fail('{}: {} of {} records differ; first {} {}'.format(what, len(bad), len(ref), i,
+                                                                      diff or 'CIGAR'))
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    c = _native.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize('which,read_len,paired', [('pol', 251, True), ('hiv', 251, True),
+                                                   ('pol', 300, False)],
+                         ids=['pol_2x251', 'hiv_mixed_2x251', 'unpaired_1x300'])
+def test_records_and_consensus_at_scale(ctx, which, read_len, paired):
+    reads, quals = _reads(which, read_len, paired)
+    threads = _threads()
+    ctx.reads_load_fixed(reads, quals, paired)
+    pipe = RemapPipeline(ctx)
+    final, _counts, _unm = pipe.run(2.0 * UNITS, max_iterations=1)
+    mapped_to = dict(pipe.mapped_to)
+    assert mapped_to, 'no seed selected: the test would check nothing'
+    # the --local pass against the consensus set of the prelim pass
+    ref = cpu_pipeline.map_arrays(list(mapped_to.values()), oracle.LOCAL, reads, quals, paired,
+                                  threads)
+    _assert_records_equal(ctx.fetch(), ref, 'remap --local')
+    assert ((ref['flag'] & 4) == 0).mean() > 0.5
+    # the end-to-end prelim pass over every seed
+    names = list(SEEDS)
+    ctx.index_build(names, [SEEDS[k] for k in names], 22)
+    ctx.map(pipe._params(_native.E2E))
+    ref = cpu_pipeline.map_arrays([SEEDS[k] for k in names], oracle.E2E, reads, quals, paired,
+                                  threads)
+    _assert_records_equal(ctx.fetch(), ref, 'prelim end-to-end')
+    # the consensus: the oracle's step on the same reads (its pileup is
+    # og_pileup, its consensus oracle.counts_to_conseqs)
+    prep = cpu_pipeline.Prepared.from_arrays(reads, quals, paired)
+    cpu_final, _ = cpu_pipeline.timed_step(SEEDS, CFG.all_region_sequences(),
+                                           {k: CFG.getSeedGroup(k) for k in SEEDS}, prep, threads)
+    res = prep.result
+    assert mapped_to == res['prelim_conseqs']
+    assert list(mapped_to) == res['remap_names']
+    if len(mapped_to) < 2:
+        # one consensus: no distance filter on either side
+        assert final == cpu_final
+    if which == 'hiv':
+        assert len(mapped_to) >= 3, sorted(mapped_to)

@@ -48,6 +48,21 @@ def _records(n, mate, seed, crlf=False, fake_header_at=None):
     return out
 
 
+def _records_fast(n, mate, seed):
+    """n FASTQ records of 151 nt (vectorised: the > 8 MB single-member cases)."""
+    rng = np.random.default_rng(seed)
+    bases = np.frombuffer(b'ACGTN', dtype=np.uint8)[rng.choice(5, size=(n, 151), p=[.3, .2, .2, .29, .01])]
+    quals = np.frombuffer(b'#,:AFG', dtype=np.uint8)[rng.choice(6, size=(n, 151),
+                                                                 p=[.02, .02, .06, .1, .2, .6])]
+    return [b'@M00:1:FC:1:%d:%d:%d %d:N:0:1\n%s\n+\n%s\n' % (1101 + i % 3, i, 7 * i, mate,
+                                                              bases[i].tobytes(), quals[i].tobytes())
+            for i in range(n)]
+
+
+MODES = {None: 0, 'members': 1, 'member-part': 2, 'whole': 3}
+BIG = 80000
+
+
 def _gz_members(data, member_bytes, level=1, stored_member=None):
     out, k = [], 0
     for at in range(0, len(data), member_bytes):
@@ -61,6 +76,22 @@ def _gz_members(data, member_bytes, level=1, stored_member=None):
 def _make_case(d, case):
     """Write the case's files; returns (paths, [records per file])."""
     n = 700
+    if case.startswith('big'):
+        n = BIG
+        recs = [_records_fast(n, 1, 1), _records_fast(n, 2, 2)]
+        if case == 'big_unpaired':
+            recs = recs[:1]
+        paths = []
+        for k, rs in enumerate(recs):
+            p = os.path.join(d, 'R%d.fastq.gz' % (k + 1))
+            with open(p, 'wb') as f:
+                # one member, as bcl2fastq writes it; big6: zlib level 6
+                # (bigger blocks), else level 1; big_stored: stored blocks only
+                # (no block start to find: read whole)
+                lvl = 6 if case == 'big6' else 0 if case == 'big_stored' else 1
+                f.write(gzip.compress(b''.join(rs), lvl))
+            paths.append(p)
+        return paths, recs
     recs = [_records(n, 1, 1, crlf=case == 'crlf'), _records(n, 2, 2, crlf=case == 'crlf')]
     if case == 'unpaired':
         recs = recs[:1]
@@ -91,6 +122,10 @@ def _make_case(d, case):
 
 def _worker(rank, world, port, d, case, strict):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    if case.startswith('big'):
+        # spans of 1 MiB: several per rank, so that spans after a rank's
+        # first copy window bytes that are still symbolic
+        os.environ['MH_PINFLATE_SPAN_MIN'] = str(1 << 20)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         paths, recs = _make_case(d, case) if rank == 0 else (None, None)
@@ -104,6 +139,7 @@ def _worker(rank, world, port, d, case, strict):
         result = dict(rank=rank)
         if st is None:
             result['fallback'] = True
+            result['file_bytes'] = sharded_io.IO_STATS['fastq_file_bytes']
         else:
             first, units = st['first'], st['units']
             for k, f in enumerate(st['frames']):
@@ -119,7 +155,7 @@ def _worker(rank, world, port, d, case, strict):
                           file_size=sum(os.path.getsize(p) for p in paths))
         np.save(os.path.join(d, 'rank%d.npy' % rank), np.array([
             result.get('fallback', False), result.get('first', -1), result.get('units', -1),
-            result.get('mode') == 'members', result.get('file_bytes', 0),
+            MODES[result.get('mode')], result.get('file_bytes', 0),
             result.get('file_size', 0)], dtype=np.int64))
     finally:
         dist.destroy_process_group()
@@ -149,7 +185,7 @@ def test_split_blocks_tile_the_file(tmp_path, world, case):
     firsts, units = [int(r[1]) for r in res], [int(r[2]) for r in res]
     assert firsts[0] == 0 and all(firsts[k] + units[k] == firsts[k + 1] for k in range(world - 1))
     assert firsts[-1] + units[-1] == 700
-    assert all(r[3] for r in res)                    # split, not read whole
+    assert all(r[3] == MODES['members'] for r in res)    # split, not read whole
     # each rank decoded about its share of the files (members are whole units)
     size = int(res[0][5])
     for r in res:
@@ -164,6 +200,40 @@ def test_mixed_split_and_whole_files(tmp_path, world):
     res = _run(tmp_path, world, 'mixed')
     assert not any(r[0] for r in res)
     assert sum(int(r[2]) for r in res) == 700
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('world,case,strict', [(2, 'big', False), (3, 'big', False), (2, 'big6', False),
+                                               (3, 'big_unpaired', False), (3, 'big', True)])
+def test_single_member_split_by_rank(tmp_path, world, case, strict):
+    """Each FASTQ one gzip member of > 8 MB (bcl2fastq's layout): every rank
+    decodes only the deflate blocks that start in its share of the
+    compressed bytes, the windows it lacks arrive by the rank-order chain,
+    and the combined CRC-32 matches the trailer (sharded_io._open_members).
+    The blocks tile the file in rank order with the serial decode's bytes
+    (checked per record in _worker), and no rank reads more than 3/4 (W=2)
+    or 3/5 (W=3) of the compressed bytes."""
+    res = _run(tmp_path, world, case, strict=strict)
+    assert not any(r[0] for r in res)
+    assert all(r[3] == MODES['member-part'] for r in res)
+    firsts, units = [int(r[1]) for r in res], [int(r[2]) for r in res]
+    assert firsts[0] == 0 and all(firsts[k] + units[k] == firsts[k + 1] for k in range(world - 1))
+    assert firsts[-1] + units[-1] == BIG
+    size = int(res[0][5])
+    assert size > (8 << 20) * (1 if case == 'big_unpaired' else 2)
+    for r in res:
+        assert 0 < r[4] <= size * (3 / 4 if world == 2 else 3 / 5), (r[4], size)
+
+
+@pytest.mark.timeout(300)
+def test_single_member_without_block_starts_is_read_whole(tmp_path):
+    """A member of stored blocks only has no block start to split at: the
+    ranks agree to read it whole (strict framing: records split by count),
+    having decoded nothing before."""
+    res = _run(tmp_path, 2, 'big_stored', strict=True)
+    assert not any(r[0] for r in res)
+    assert all(r[3] == MODES['whole'] for r in res)
+    assert [int(r[2]) for r in res] == [BIG // 2, BIG - BIG // 2]
 
 
 @pytest.mark.timeout(300)
