@@ -325,51 +325,161 @@ class PhaseClock:
         return False
 
 
-def write_fastq_gz(pairs, path1, path2, threads=16, single=False):
-    """The pairs as gzip FASTQ files (independent gzip members compressed on
-    `threads` threads; a multi-member file is one valid gzip stream).  With
-    single=True each file is one gzip member, as bcl2fastq writes it (its
-    inflate cannot be split across threads)."""
+class Job:
+    """This process's place in the bench job and the collectives the
+    file-to-file legs use: rank, world, and a barrier / gathers over the
+    initialised torch.distributed group (through the drop-ins' own
+    pipeline.Shard, so the legs run the sharded code paths a torchrun'd
+    bin/micall runs).  world == 1 without a group."""
+
+    def __init__(self, shard=None):
+        import torch.distributed as dist
+        from micall_amd import session
+        if shard is None and dist.is_available() and dist.is_initialized():
+            shard = session.shard()
+        self.shard = shard
+        self.rank = self.shard.rank if self.shard else 0
+        self.world = self.shard.world if self.shard else 1
+
+    def barrier(self):
+        if self.shard:
+            self.shard.barrier()
+
+    def gather(self, values):
+        """int64 values of every rank: array [world, len(values)]."""
+        if not self.shard:
+            return np.asarray([values], dtype=np.int64)
+        return self.shard._gather_sizes(values)
+
+    def max_seconds(self, secs):
+        """max over ranks of a duration (microsecond resolution)."""
+        return float(self.gather([int(round(secs * 1e6))])[:, 0].max()) / 1e6
+
+    def per_rank_seconds(self, secs):
+        return [round(float(x) / 1e6, 4) for x in self.gather([int(round(secs * 1e6))])[:, 0]]
+
+    def shared_dir(self, prefix):
+        """A fresh directory every rank of the job uses (rank 0 makes it)."""
+        import tempfile
+        path = tempfile.mkdtemp(prefix=prefix).encode() if self.rank == 0 else b''
+        if self.shard:
+            path = self.shard.all_gather_bytes(path)[0]
+        return path.decode()
+
+
+def _fastq_records(pairs, mate):
+    from micall_amd import synth
+    r, q = pairs['r%d' % mate], pairs['q%d' % mate]
+    return [b'%s\n%s\n+\n%s\n' % (synth.read_name(pairs['block'], i, mate).encode(), r[i].tobytes(),
+                                  q[i].tobytes()) for i in range(pairs['n'])]
+
+
+def write_fastq_gz(pairs, path1, path2, threads=16, single=False, job=None):
+    """The pairs as gzip FASTQ files.  One process: independent gzip members
+    compressed on `threads` threads (a multi-member file is one valid gzip
+    stream), or with single=True one gzip member, as bcl2fastq writes it
+    (one deflate stream over the whole text).
+
+    Under a job of W ranks each rank passes its own block of pairs and the
+    file holds the blocks in rank order: its members (many), or (single)
+    one gzip member whose deflate stream each rank writes for its block --
+    one stream per rank, primed with the last 32 KiB of the block before
+    (so back-references cross the rank boundaries, as pigz writes a single
+    member) and ended with a sync flush -- between rank 0's gzip header and
+    a trailer carrying the CRC-32 and size of the whole text.  Every rank
+    pwrites its bytes at offsets all-gathered from the sizes."""
     import zlib
     from concurrent.futures import ThreadPoolExecutor
-    from micall_amd import synth
+    from micall_amd import _native
+    world = job.world if job else 1
+    rank = job.rank if job else 0
 
     def member(chunk):
         c = zlib.compressobj(1, zlib.DEFLATED, 31)
         return c.compress(chunk) + c.flush()
     for mate, path in ((1, path1), (2, path2)):
-        r, q = pairs['r%d' % mate], pairs['q%d' % mate]
-        recs = [b'%s\n%s\n+\n%s\n' % (synth.read_name(pairs['block'], i, mate).encode(),
-                                      r[i].tobytes(), q[i].tobytes()) for i in range(pairs['n'])]
-        step = len(recs) if single else -(-len(recs) // (threads * 4))
-        chunks = [b''.join(recs[k:k + step]) for k in range(0, len(recs), step)]
-        del recs
-        with ThreadPoolExecutor(threads) as ex, open(path, 'wb') as f:
-            for blob in ex.map(member, chunks):
-                f.write(blob)
+        recs = _fastq_records(pairs, mate)
+        if not single:
+            step = -(-len(recs) // (threads * 4))
+            chunks = [b''.join(recs[k:k + step]) for k in range(0, len(recs), step)]
+            del recs
+            with ThreadPoolExecutor(threads) as ex:
+                blob = b''.join(ex.map(member, chunks))
+            head, tail = b'', b''
+        elif world == 1:
+            blob = member(b''.join(recs))
+            del recs
+            head, tail = b'', b''
+        else:
+            text = b''.join(recs)
+            del recs
+            before = job.shard.all_gather_bytes(text[-32768:])
+            zdict = before[rank - 1] if rank > 0 else None
+            c = (zlib.compressobj(1, zlib.DEFLATED, -15, zdict=zdict) if zdict else
+                 zlib.compressobj(1, zlib.DEFLATED, -15))
+            blob = c.compress(text) + c.flush(zlib.Z_FINISH if rank == world - 1 else zlib.Z_SYNC_FLUSH)
+            facts = job.gather([zlib.crc32(text), len(text)])
+            del text
+            crc = 0
+            for k in range(world):
+                crc = _native.crc32_combine(crc, int(facts[k, 0]), int(facts[k, 1]))
+            size = int(facts[:, 1].sum())
+            head = b'\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\x03' if rank == 0 else b''
+            tail = (crc.to_bytes(4, 'little') + (size & 0xffffffff).to_bytes(4, 'little')
+                    if rank == world - 1 else b'')
+        data = head + blob + tail
+        if world == 1:
+            with open(path, 'wb') as f:
+                f.write(data)
+            continue
+        lens = job.gather([len(data)])[:, 0]
+        if rank == 0:
+            with open(path, 'wb') as f:
+                f.truncate(int(lens.sum()))
+        job.barrier()
+        fd = os.open(path, os.O_WRONLY)
+        try:
+            at, mv = int(lens[:rank].sum()), memoryview(data)
+            while len(mv):
+                n = os.pwrite(fd, mv, at)
+                at += n
+                mv = mv[n:]
+        finally:
+            os.close(fd)
+        job.barrier()
 
 
-def end_to_end(n_pairs, workdir, single_member=False):
+def end_to_end(n_pairs, workdir, single_member=False, job=None):
     """The file-to-file path bin/micall runs (prelim_map() then remap(), the
     drop-ins) on the C2 input written as gzip FASTQ: ingest (gunzip + parse
     + H2D + 2-bit packing), the cold 74-seed index, the prelim pass and
     prelim.csv text, remap's prelim.csv parse, one remap pass, remap.csv
     text.  A new device context is used, so nothing is cached from the
-    device-resident bench.  Returns the result dict (reads/s over the whole
-    call sequence, seconds per part)."""
+    device-resident bench.
+
+    Under a job of W ranks (torchrun) the files hold every rank's block of
+    n_pairs pairs (written untimed, in rank order) and every rank calls the
+    drop-ins with the same paths, as a torchrun'd bin/micall does: each
+    reads its share of the FASTQ, maps its block and writes its own rows;
+    the time is the max over ranks.  Returns the result dict (reads/s over
+    the whole job, seconds per part)."""
     import io
-    from micall_amd import _native, prelim_map, remap, session, synth
+    from micall_amd import _native, prelim_map, remap, session, sharded_io, synth
+    world = job.world if job else 1
+    rank = job.rank if job else 0
     r1 = os.path.join(workdir, 'R1.fastq.gz')
     r2 = os.path.join(workdir, 'R2.fastq.gz')
     pairs = synth.make_pairs(n_pairs, genomes=bench_genomes('pol'), genome_seed=SEED,
-                             read_seed=SEED, block=0)
-    write_fastq_gz(pairs, r1, r2, single=single_member)
+                             read_seed=SEED, block=rank)
+    t_write = time.perf_counter()
+    write_fastq_gz(pairs, r1, r2, single=single_member, job=job)
+    t_write = time.perf_counter() - t_write
     del pairs
     sizes = os.path.getsize(r1) + os.path.getsize(r2)
     # cold index build alone, on its own context
     from micall_amd import projects
     seeds = projects.load_default().seed_sequences()
-    probe = _native.Context(0)
+    probe = _native.Context(session._device_index())
     probe.sync()
     t = time.perf_counter()
     probe.index_build(list(seeds), list(seeds.values()), 22)
@@ -377,9 +487,12 @@ def end_to_end(n_pairs, workdir, single_member=False):
     index_cold_ms = 1e3 * (time.perf_counter() - t)
     probe.close()
     session.reset()
+    sharded_io.reset_stats()
     prelim_path = os.path.join(workdir, 'prelim.csv')
     remap_path = os.path.join(workdir, 'remap.csv')
     thr0 = cgroup_throttle()
+    if job:
+        job.barrier()
     with PhaseClock() as clock:
         t0 = time.perf_counter()
         with open(prelim_path, 'w') as f:
@@ -392,6 +505,17 @@ def end_to_end(n_pairs, workdir, single_member=False):
         t2 = time.perf_counter()
     lib_rem = session.context().phase_times(reset=True)
     session.context().sync()
+    io_stats = dict(sharded_io.IO_STATS)
+    if job:
+        job.barrier()
+        secs = job.max_seconds(t2 - t0)
+        per_rank = job.per_rank_seconds(t2 - t0)
+        pre_s = job.max_seconds(t1 - t0)
+        rem_s = job.max_seconds(t2 - t1)
+        rank_io = job.gather([io_stats['fastq_file_bytes'], io_stats['fastq_text_bytes'],
+                              io_stats['written_bytes']])
+    else:
+        secs, per_rank, pre_s, rem_s, rank_io = t2 - t0, None, t1 - t0, t2 - t1, None
     ph = {k: v for k, v in clock.acc.items()}
     phases = {'inflate': lib_pre['inflate'] / 1e3, 'parse': lib_pre['parse'] / 1e3,
               'upload_pack': lib_pre['upload'] / 1e3,
@@ -405,23 +529,38 @@ def end_to_end(n_pairs, workdir, single_member=False):
               'map_remap': ph.get('map_remap', 0.0),
               'remap_csv_format': lib_rem['format'] / 1e3, 'remap_csv_write': lib_rem['write'] / 1e3}
     phases['other'] = (t2 - t0) - sum(phases.values())
-    out = {'value': round(2 * n_pairs / (t2 - t0), 1), 'unit': 'reads/s',
-           'seconds': round(t2 - t0, 3), 'prelim_map_s': round(t1 - t0, 3),
-           'remap_s': round(t2 - t1, 3), 'index_build_cold_ms': round(index_cold_ms, 2),
+    layout = ('one gzip member per file' + (' (one deflate stream per rank block, primed with the '
+                                            'block before\'s last 32 KiB)' if world > 1 else '')
+              if single_member else 'many members ({} per file)'.format(64 * world))
+    out = {'value': round(2 * n_pairs * world / secs, 1), 'unit': 'reads/s', 'n_gpus': world,
+           'seconds': round(secs, 3), 'prelim_map_s': round(pre_s, 3),
+           'remap_s': round(rem_s, 3), 'index_build_cold_ms': round(index_cold_ms, 2),
            'cgroup_throttled': throttle_since(thr0),
            'phases_s': {k: round(v, 4) for k, v in phases.items()},
            'prelim_source': session.stats.get('prelim_source'),
-           'fastq_gz_bytes': sizes, 'fastq_gz_members': 'one' if single_member else 'many (64 per file)',
+           'fastq_gz_bytes': sizes, 'fastq_gz_members': layout,
+           'fastq_write_untimed_s': round(t_write, 2),
            'prelim_csv_bytes': os.path.getsize(prelim_path),
            'remap_csv_bytes': os.path.getsize(remap_path),
            'remap_counts': counts.getvalue().strip().split('\n')[-3:],
            'what': 'prelim_map() + remap() drop-ins file to file on {} pairs of gzip FASTQ '
-                   '(C2 input): ingest, cold 74-seed index, prelim pass, prelim.csv write, '
+                   '(C2 input{}): ingest, cold 74-seed index, prelim pass, prelim.csv write, '
                    'remap pass(es) by the reference\'s stopping rules, remap.csv write; '
-                   'new device context'.format(n_pairs)}
+                   'new device context'.format(n_pairs * world,
+                                               '' if world == 1 else ', {} pairs per rank'.format(n_pairs))}
+    if job and world > 1:
+        out['per_rank_seconds'] = per_rank
+        out['per_rank_io'] = {'fastq_file_bytes': rank_io[:, 0].tolist(),
+                              'fastq_text_bytes': rank_io[:, 1].tolist(),
+                              'written_bytes': rank_io[:, 2].tolist(),
+                              'fastq_mode': io_stats['fastq_mode']}
+        out['phases_s_rank0'] = out.pop('phases_s')
     session.reset()
-    for p in (r1, r2, prelim_path, remap_path):
-        os.remove(p)
+    if job:
+        job.barrier()
+    if rank == 0:
+        for p in (r1, r2, prelim_path, remap_path):
+            os.remove(p)
     return out
 
 
@@ -807,23 +946,55 @@ def bench_aln2counts(args):
     print(json.dumps(out))
 
 
+def _init_job(args):
+    """torch.distributed for a leg run under torchrun (WORLD_SIZE > 1): the
+    device of this rank (RCCL), or device LOCAL_RANK % devices with
+    MICALL_BENCH_BACKEND=gloo (several ranks on one GPU, tests only).  The
+    drop-ins' session uses the same device.  Returns (world, rank, device)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        print('warning: --gpus {} but WORLD_SIZE {}'.format(args.gpus, world), file=sys.stderr)
+    backend = os.environ.get('MICALL_BENCH_BACKEND', 'nccl')
+    ndev = torch.cuda.device_count()
+    device = torch.device('cuda', local if backend == 'nccl' else local % max(ndev, 1))
+    torch.cuda.set_device(device)
+    os.environ['MICALL_HIP_DEVICE'] = str(device.index)
+    if world > 1 and not dist.is_initialized():
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=device)
+        else:
+            dist.init_process_group(backend)
+    return world, rank, device, backend
+
+
 def bench_chain(args):
     """bin/micall's per-sample chain (bin/micall:116-188) file to file with
     the drop-ins, on the C2 input as a raw MiSeq pair arrives (each FASTQ one
     gzip member): censor R1, censor R2 (2 % bad tile-cycles) -> prelim_map
     -> remap -> sam2aln -> aln2counts, every output to a file.  One line:
-    reads/s through the whole chain and seconds per stage."""
-    import csv
-    import io
+    reads/s through the whole chain and seconds per stage.
+
+    Under torchrun every rank holds --pairs pairs of the files (written
+    untimed, in rank order) and runs the chain on the same paths, as a
+    torchrun'd bin/micall does (python -m micall_amd.run_micall); each
+    stage's time is the max over ranks.  The line reports the run with the
+    median total (every run listed)."""
     import shutil
-    import tempfile
     import random
-    from micall_amd import (aln2counts, censor_fastq, prelim_map, remap, sam2aln, session, synth)
-    work = tempfile.mkdtemp(prefix='bench_chain_')
+    import torch.distributed as dist
+    world, rank, device, backend = _init_job(args)
+    from micall_amd import (aln2counts, censor_fastq, prelim_map, remap, sam2aln, session, sharded_io,
+                            synth)
+    job = Job()
+    work = job.shared_dir('bench_chain_')
     r1, r2 = os.path.join(work, 'R1.fastq.gz'), os.path.join(work, 'R2.fastq.gz')
     pairs = synth.make_pairs(args.pairs, genomes=bench_genomes('pol'), genome_seed=SEED,
-                             read_seed=SEED, block=0)
-    write_fastq_gz(pairs, r1, r2, single=True)
+                             read_seed=SEED, block=rank)
+    write_fastq_gz(pairs, r1, r2, single=True, job=job)
     del pairs
     rng = random.Random(SEED)
     bad = [{'tile': str(1101 + t), 'cycle': str(sign * c)} for t in range(8) for sign in (1, -1)
@@ -834,39 +1005,47 @@ def bench_chain(args):
 
     lib = {}
     gap = float(os.environ.get('MICALL_CHAIN_GAP_S', '0'))   # diagnostics: idle seconds between stages
-
     throttled = []
+    io = []
 
     def run():
         # bin/micall writes each sample's outputs into a fresh directory:
         # the previous run's outputs are removed, untimed, so that opening
         # them does not truncate 2.4 GB of files (an ext4 / overlay truncate
         # also makes close() flush the file: 0.3 s + 0.3 s on the box)
-        for path in P.values():
-            if os.path.exists(path):
-                os.unlink(path)
-        times = {}
+        if rank == 0:
+            for path in P.values():
+                if os.path.exists(path):
+                    os.unlink(path)
+        job.barrier()
+        times, stats = {}, {}
         thr = cgroup_throttle()
+        sharded_io.reset_stats()
         t = time.perf_counter()
         for src, dst in ((r1, P['c1.fastq.gz']), (r2, P['c2.fastq.gz'])):
             with open(src, 'rb') as f, open(dst, 'wb') as g:
                 censor_fastq.censor(f, iter(bad), g, use_gzip=True)
         times['censor'] = time.perf_counter() - t
+        stats['censor'] = dict(sharded_io.IO_STATS)
         time.sleep(gap)
+        sharded_io.reset_stats()
         t = time.perf_counter()
         session.context().phase_times(reset=True)
         with open(P['prelim.csv'], 'w') as f:
             prelim_map.prelim_map(P['c1.fastq.gz'], P['c2.fastq.gz'], f, gzip=True)
             lib['prelim_map_call_s'] = round(time.perf_counter() - t, 4)
         times['prelim_map'] = time.perf_counter() - t
+        stats['prelim_map'] = dict(sharded_io.IO_STATS)
         time.sleep(gap)
         lib['prelim_map'] = {k: round(v / 1e3, 4) for k, v in session.context().phase_times(reset=True).items()}
+        sharded_io.reset_stats()
         t = time.perf_counter()
         with open(P['prelim.csv']) as pre, open(P['remap.csv'], 'w') as out, \
                 open(P['remap_counts.csv'], 'w') as counts:
             remap.remap(P['c1.fastq.gz'], P['c2.fastq.gz'], pre, out, counts, gzip=True)
             lib['remap_call_s'] = round(time.perf_counter() - t, 4)
         times['remap'] = time.perf_counter() - t
+        stats['remap'] = dict(sharded_io.IO_STATS)
         time.sleep(gap)
         lib['remap'] = {k: round(v / 1e3, 4) for k, v in session.context().phase_times(reset=True).items()}
         lib['prelim_source'] = session.stats.get('prelim_source')
@@ -882,12 +1061,19 @@ def bench_chain(args):
             aln2counts.aln2counts(al, nuc, amino, ins, conseq)
         times['aln2counts'] = time.perf_counter() - t
         throttled.append(throttle_since(thr))
-        return times
+        io.append(stats)
+        # the job's time per stage: the slowest rank's
+        names = list(times)
+        us = job.gather([int(round(times[k] * 1e6)) for k in names] +
+                        [int(round(sum(times.values()) * 1e6))])
+        return {'stages': {k: float(us[:, j].max()) / 1e6 for j, k in enumerate(names)},
+                'total': float(us[:, -1].max()) / 1e6,
+                'per_rank_total': [round(float(x) / 1e6, 3) for x in us[:, -1]]}
 
     for _ in range(args.warmup):
         run()
     runs = [run() for _ in range(max(args.steps, 1))]
-    if os.environ.get('MICALL_CHAIN_PROFILE'):   # diagnostics: cProfile of one more run to stderr
+    if os.environ.get('MICALL_CHAIN_PROFILE') and world == 1:   # diagnostics: cProfile of one more run
         import cProfile
         import pstats
         pr = cProfile.Profile()
@@ -895,28 +1081,81 @@ def bench_chain(args):
         run()
         pr.disable()
         pstats.Stats(pr, stream=sys.stderr).sort_stats('cumulative').print_stats(60)
-    best = min(runs, key=lambda r: sum(r.values()))
-    total = sum(best.values())
+    order = sorted(range(len(runs)), key=lambda k: runs[k]['total'])
+    med = runs[order[(len(runs) - 1) // 2]]       # the median run (the lower one of an even count)
+    total = med['total']
     sizes = {k: os.path.getsize(v) for k, v in P.items()}
     sizes['R1.fastq.gz'], sizes['R2.fastq.gz'] = os.path.getsize(r1), os.path.getsize(r2)
-    shutil.rmtree(work, ignore_errors=True)
-    out = {
-        'metric': 'bin/micall per-sample chain reads/sec (raw FASTQ.gz pair -> nuc/amino/conseq)',
-        'value': round(2 * args.pairs / total, 1), 'unit': 'reads/s', 'n_gpus': 1,
-        'steps': len(runs), 'warmup': args.warmup, 'ms_per_step': round(1e3 * total, 1),
-        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8',
-        'data': 'synthetic',
-        'config': {'workload': 'C2 input (1M synthetic 2x251 HIV-1 pol pairs), each FASTQ one gzip '
-                               'member; 2 % bad tile-cycles; censor R1 + R2, prelim_map, remap, '
-                               'sam2aln, aln2counts, drop-ins file to file',
-                   'pairs': args.pairs, 'bad_cycles': len(bad)},
-        'stages_s': {k: round(v, 3) for k, v in best.items()},
-        'all_runs_s': [round(sum(r.values()), 3) for r in runs],
-        'library_phases_s_last_run': lib,
-        'cgroup_throttled_per_run': throttled[args.warmup:args.warmup + len(runs)],
-        'bytes': sizes,
-    }
-    print(json.dumps(out))
+    rank_io = {}
+    last = io[-1]
+    for stage in ('censor', 'prelim_map', 'remap'):
+        g = job.gather([last[stage]['fastq_file_bytes'], last[stage]['fastq_text_bytes'],
+                        last[stage]['written_bytes']])
+        rank_io[stage] = {'fastq_file_bytes': g[:, 0].tolist(), 'fastq_text_bytes': g[:, 1].tolist(),
+                          'written_bytes': g[:, 2].tolist(), 'fastq_mode': last[stage]['fastq_mode']}
+    job.barrier()
+    if rank == 0:
+        shutil.rmtree(work, ignore_errors=True)
+        out = {
+            'metric': 'bin/micall per-sample chain reads/sec (raw FASTQ.gz pair -> nuc/amino/conseq)',
+            'value': round(2 * args.pairs * world / total, 1), 'unit': 'reads/s', 'n_gpus': world,
+            'steps': len(runs), 'warmup': args.warmup, 'ms_per_step': round(1e3 * total, 1),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8',
+            'data': 'synthetic',
+            'config': {'workload': 'C2 input ({} synthetic 2x251 HIV-1 pol pairs per GPU), each FASTQ '
+                                   'one gzip member; 2 % bad tile-cycles; censor R1 + R2, prelim_map, '
+                                   'remap, sam2aln, aln2counts, drop-ins file to file'.format(args.pairs),
+                       'pairs': args.pairs * world, 'pairs_per_gpu': args.pairs, 'bad_cycles': len(bad),
+                       'parallelism': 'dp{}{}'.format(world, '' if world == 1 else ' ({}; every rank runs '
+                                                       'the chain on the shared files)'.format(
+                                                           'RCCL' if backend == 'nccl' else backend))},
+            'reported_run': 'median of {} runs by total time (the slowest rank\'s per stage)'.format(len(runs)),
+            'stages_s': {k: round(v, 3) for k, v in med['stages'].items()},
+            'all_runs_s': [round(r['total'], 3) for r in runs],
+            'per_rank_total_s': med['per_rank_total'] if world > 1 else None,
+            'per_rank_io_last_run': rank_io if world > 1 else None,
+            'library_phases_s_last_run_rank0': lib,
+            'cgroup_throttled_per_run': throttled[args.warmup:args.warmup + len(runs)],
+            'bytes': sizes,
+        }
+        print(json.dumps(out))
+    session.reset()
+    if world > 1:
+        job.barrier()
+        dist.destroy_process_group()
+
+
+def run_end_to_end(args):
+    """The end_to_end legs of the default line, on every rank: the C2 input
+    as many gzip members per file and as one member (bcl2fastq's layout),
+    each file to file through the drop-ins; at N = 1 also the CPU
+    file-to-file baseline on a bounded sample.  Skipped (with the reason)
+    when the scratch file system cannot hold the files."""
+    import shutil
+    job = Job()
+    layouts = ('members', 'single') if args.e2e_gzip == 'both' else (args.e2e_gzip,)
+    work = job.shared_dir('micall_e2e_')
+    out = {}
+    try:
+        # FASTQ (~0.6 GB) + prelim.csv and remap.csv (~1.2 GB each) per 1M pairs
+        need = 3.2e9 * args.pairs / 1e6 * job.world
+        free = shutil.disk_usage(work).free
+        if free < 1.5 * need:
+            skip = {'skipped': 'scratch file system {} has {:.1f} GB free, the files need '
+                               '{:.1f} GB'.format(work, free / 1e9, need / 1e9)}
+            return {k: skip for k in layouts}
+        for layout in layouts:
+            out[layout] = end_to_end(args.pairs, work, single_member=layout == 'single', job=job)
+        if job.world == 1 and not args.no_cpu_baseline and 'members' in out:
+            out['members']['cpu_baseline'] = cpu_end_to_end(args.cpu_e2e_sample, work)
+            for layout in out:
+                out[layout]['vs_cpu'] = round(out[layout]['value'] /
+                                              out['members']['cpu_baseline']['value'], 2)
+    finally:
+        job.barrier()
+        if job.rank == 0:
+            shutil.rmtree(work, ignore_errors=True)
+    return out
 
 
 def main():
@@ -947,9 +1186,10 @@ def main():
                          'against the CPU oracle, after timing)')
     ap.add_argument('--no-e2e', action='store_true',
                     help='skip the end-to-end (file to file) leg of the default C2 run')
-    ap.add_argument('--e2e-gzip', choices=('members', 'single'), default='members',
+    ap.add_argument('--e2e-gzip', choices=('members', 'single', 'both'), default='both',
                     help='gzip layout of the end-to-end FASTQ input: 64 members per file '
-                         '(as a parallel gzip writes it) or one member (as bcl2fastq does)')
+                         '(as a parallel gzip writes it), one member (as bcl2fastq does), or '
+                         'both legs (the default line carries both)')
     ap.add_argument('--breakdown', action='store_true',
                     help='time each pipeline stage (synchronising) and print it to stderr')
     ap.add_argument('--stage', choices=('remap', 'sam2aln', 'censor', 'aln2counts', 'chain'), default='remap',
@@ -971,22 +1211,7 @@ def main():
     from micall_amd import _native
     from micall_amd.pipeline import RemapPipeline, Shard
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world != args.gpus:
-        print('warning: --gpus {} but WORLD_SIZE {}'.format(args.gpus, world), file=sys.stderr)
-    # MICALL_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on
-    # one GPU (tests only; the measured multi-GPU runs use RCCL)
-    backend = os.environ.get('MICALL_BENCH_BACKEND', 'nccl')
-    ndev = torch.cuda.device_count()
-    device = torch.device('cuda', local if backend == 'nccl' else local % max(ndev, 1))
-    torch.cuda.set_device(device)
-    if world > 1:
-        if backend == 'nccl':
-            dist.init_process_group('nccl', device_id=device)
-        else:
-            dist.init_process_group(backend)
+    world, rank, device, backend = _init_job(args)
 
     ctx = _native.Context(device.index)
     paired = not args.unpaired
@@ -1065,6 +1290,12 @@ def main():
     cells = (ext - fast) * L * 31
     dp_ms = kernels['k_dp'][0] + kernels['k_dp_rescue'][0]
 
+    # the file-to-file legs (every rank: under torchrun they are the sharded
+    # drop-ins over files holding every rank's block)
+    e2e_legs = {}
+    if (not args.no_e2e and paired and L == READ_LEN and args.genomes == 'pol'
+            and args.iterations == 1 and not args.force_iterations):
+        e2e_legs = run_end_to_end(args)
     parity = None
     if rank == 0:
         cpu = cpu_result = None
@@ -1074,15 +1305,6 @@ def main():
         if sample is not None and not args.no_parity:
             parity = parity_check(ctx, pipe, sample, paired, cpu_result, device.index)
             del cpu_result
-        e2e = None
-        if (world == 1 and not args.no_e2e and paired and L == READ_LEN and args.genomes == 'pol'
-                and args.iterations == 1 and not args.force_iterations):
-            import tempfile
-            with tempfile.TemporaryDirectory(prefix='micall_e2e_') as work:
-                e2e = end_to_end(args.pairs, work, single_member=args.e2e_gzip == 'single')
-                if not args.no_cpu_baseline:
-                    e2e['cpu_baseline'] = cpu_end_to_end(args.cpu_e2e_sample, work)
-                    e2e['vs_cpu'] = round(e2e['value'] / e2e['cpu_baseline']['value'], 2)
         if cpu is not None:
             cpu['device_resident_vs_cpu'] = round(value / cpu['value'], 1)
         out = {
@@ -1127,7 +1349,8 @@ def main():
                    'gcups': round(cells / (dp_ms / 1e3) / 1e9, 1) if dp_ms > 0 else None},
             'cpu_baseline': cpu,
             'parity': parity,
-            'end_to_end': e2e,
+            'end_to_end': e2e_legs.get('members'),
+            'end_to_end_single_member': e2e_legs.get('single'),
             'result': {'remap_iterations_run': len(pipe.log),
                        'conseqs': {k: len(v) for k, v in conseqs.items()},
                        'mapped_lines': dict(new_counts)},

@@ -108,11 +108,13 @@ int view_file(const char *path, int fd_in, FileView &v)
 // v.size (to < 0: to the end of the file)
 int64_t next_member(const FileView &v, int64_t from, int64_t to = -1)
 {
+    // candidates start before `to`; the probe may read on to the file's end
     const uint8_t *p = v.p + from, *e = v.p + (to < 0 ? v.size : std::min(to, v.size));
+    const uint8_t *end = v.p + v.size;
     while (p < e) {
         p = (const uint8_t *)memchr(p, 0x1f, (size_t)(e - p));
         if (!p) break;
-        if (gzip_header_at(p, e - p) && gzip_member_probe(p, e - p, 1 << 16)) return p - v.p;
+        if (gzip_header_at(p, end - p) && gzip_member_probe(p, end - p, 1 << 16)) return p - v.p;
         ++p;
     }
     return v.size;

@@ -440,3 +440,21 @@ def test_host_parse_record_framing_tail(tmp_path, tail, ok):
         with pytest.raises(Exception, match='truncated'):
             fq = _native.Fastq(str(p))
             fq.parse()
+
+
+def test_member_scan_near_range_ends(tmp_path):
+    """mh_fastq_scan_part: a member that starts just before the end of a
+    part's byte range is found (its header probe reads past the range), so a
+    file of one member per rank -- the censor's output -- is split by
+    member, not taken for a single member."""
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, 300000, dtype=np.uint8).tobytes()
+    blob = b''.join(_gz_members(data[a:b], b - a + 1) for a, b in ((0, 99000), (99000, 199000),
+                                                                   (199000, 300000)))
+    path = tmp_path / 'three.gz'
+    path.write_bytes(blob)
+    found = [_native.Fastq.scan_part(str(path), -1, r, 3)[2] for r in range(3)]
+    assert found[:2] == [True, True] and found[2] is False
+    single = tmp_path / 'one.gz'
+    single.write_bytes(gzip.compress(data, 1))
+    assert not any(_native.Fastq.scan_part(str(single), -1, r, 3)[2] for r in range(3))
