@@ -848,11 +848,21 @@ struct XView {
     uint8_t *rowk;    // rows: band lane of the M cell of each row, 255 none
 };
 
-__host__ __device__ constexpr int xview_rows(int rows_pad) { return rows_pad > 256 ? rows_pad : 256; }
+// rows of the tables: a one-round staging (rows_pad <= 256 or <= 320, see
+// stage_raw) writes all of its rows unguarded
+__host__ __device__ constexpr int xview_rows(int rows_pad)
+{
+    return rows_pad <= 256 ? 256 : rows_pad <= 320 ? 320 : rows_pad;
+}
+
+__host__ __device__ constexpr int xview_tab_words(int rows_pad)
+{
+    return xview_rows(rows_pad) > RUNS_CAP ? xview_rows(rows_pad) : RUNS_CAP;
+}
 
 __host__ __device__ constexpr int xview_bytes(int rows_pad)
 {
-    return (4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP) + 3 * xview_rows(rows_pad) + 64 + 15) & ~15;
+    return (4 * xview_tab_words(rows_pad) + 3 * xview_rows(rows_pad) + 64 + 15) & ~15;
 }
 
 __device__ __forceinline__ XView xview(unsigned char *base, int rows_pad, int h)
@@ -861,7 +871,7 @@ __device__ __forceinline__ XView xview(unsigned char *base, int rows_pad, int h)
     const int rows = xview_rows(rows_pad);
     XView X;
     X.tab = (uint32_t *)p;
-    p += 4 * (rows_pad > RUNS_CAP ? rows_pad : RUNS_CAP);
+    p += 4 * xview_tab_words(rows_pad);
     X.refw = p;
     p += rows + 64;
     X.rdc = p;
@@ -1156,18 +1166,36 @@ __device__ __forceinline__ void stage_ref(const DpArgs &A, const XItem &it, cons
     }
 }
 
-// rows_pad <= 256: one round, whose loads k_dp issues an item ahead
+// Reads of more than one round (rows_pad > 320) load and store 256 rows and
+// 320 reference bytes per round (stage_ext)
 constexpr int STAGE_ROWS = 256;
 
-// Reads of one round (rows_pad <= 256) are staged in two halves: k_dp issues
-// the next item's raw bytes into a per-wave raw area by LDS-DMA
-// (global_load_lds_dword: no VGPR destination, so nothing in the compiler's
-// waits depends on them) before the current item's DP and traceback, and
-// builds the tables from the raw area when the item's turn comes.  Raw area
-// (RAW_BYTES): [0, 256) qualities; [256, 512) the 2-bit words (lanes 0-15)
-// and N-mask words (lanes 16-23) of the read; [512, 1024) 128 dwords of
-// reference codes from the aligned dword below the window's first byte.
-constexpr int RAW_BYTES = 1024;
+// Reads of one round (rows_pad <= ROUND, 256 or 320) are staged in two
+// halves: k_dp issues the next item's raw bytes into a per-wave raw area by
+// LDS-DMA (global_load_lds_dword: no VGPR destination, so nothing in the
+// compiler's waits depends on them) before the current item's DP and
+// traceback, and builds the tables from the raw area when the item's turn
+// comes.  Raw area (RawLayout<ROUND>): the qualities (one dword per lane per
+// 256 rows); the 2-bit words (16 bases each, lanes 0 .. ROUND/16 - 1) and
+// N-mask words (32 bases each, the next ROUND/32 lanes) of the read; 128
+// dwords of reference codes from the aligned dword below the window's first
+// byte (the window is rows_pad + XREFW_PAD <= 368 bytes).
+template <int ROUND>
+struct RawLayout {
+    static constexpr int QUAL = ROUND <= 256 ? 256 : 512;   // quality bytes
+    static constexpr int WORDS = QUAL;                      // offset of the read's words
+    static constexpr int NSEQ = ROUND / 16;                 // lanes loading 2-bit words
+    static constexpr int NMASK = ROUND / 32;                // lanes loading N-mask words
+    static constexpr int REF = WORDS + 256;                 // offset of the reference dwords
+    static constexpr int BYTES = REF + 512;
+    static constexpr int ROW_ROUNDS = ROUND / 64;           // rows per lane
+    static constexpr int REF_ROUNDS = ROUND <= 256 ? 5 : 6; // reference bytes per lane
+};
+
+__host__ __device__ constexpr int raw_bytes(int rows_pad)
+{
+    return rows_pad <= 256 ? RawLayout<256>::BYTES : rows_pad <= 320 ? RawLayout<320>::BYTES : 0;
+}
 
 // s_waitcnt vmcnt(0): every vector memory operation of the wave, the
 // LDS-DMA of stage_dma included, has completed
@@ -1178,18 +1206,24 @@ __device__ __forceinline__ void dma4(const void *g, unsigned char *lds)
     __builtin_amdgcn_global_load_lds((const void *)g, (__attribute__((address_space(3))) void *)lds, 4, 0, 0);
 }
 
+template <int ROUND>
 __device__ __forceinline__ void stage_dma(const DpArgs &A, const XItem &x, unsigned char *raw, int lane)
 {
-    // qualities: lane l the bytes 4l .. 4l+3 of the read (a lane past the
-    // read re-reads its first dword)
-    const int64_t q = x.roff + (4 * lane < x.m ? 4 * lane : 0);
-    dma4(A.R.qual + q, raw);
+    using RL = RawLayout<ROUND>;
+    // qualities: lane l the bytes 4l .. 4l+3 of each 256 rows of the read (a
+    // lane past the read re-reads its first dword)
+#pragma unroll
+    for (int k = 0; k < RL::QUAL / 256; ++k) {
+        const int b = 256 * k + 4 * lane;
+        dma4(A.R.qual + x.roff + (b < x.m ? b : 0), raw + 256 * k);
+    }
     // 2-bit words (16 bases each) and N-mask words (32 bases each); roff is a
     // multiple of 32
     const int64_t sw = x.roff >> 4, nw = x.roff >> 5;
-    const uint32_t *sp = A.R.seq2 + sw + (16 * lane < x.m && lane < 16 ? lane : 0);
-    const uint32_t *np = A.R.nmask + nw + (lane >= 16 && lane < 24 && 32 * (lane - 16) < x.m ? lane - 16 : 0);
-    dma4(lane < 16 ? (const void *)sp : (const void *)np, raw + 256);
+    const int nl = lane - RL::NSEQ;
+    const uint32_t *sp = A.R.seq2 + sw + (16 * lane < x.m && lane < RL::NSEQ ? lane : 0);
+    const uint32_t *np = A.R.nmask + nw + (nl >= 0 && nl < RL::NMASK && 32 * nl < x.m ? nl : 0);
+    dma4(lane < RL::NSEQ ? (const void *)sp : (const void *)np, raw + RL::WORDS);
     // reference codes: dwords from the aligned dword at or below gref + d0,
     // clamped into the code array (bytes off the reference are masked later)
     const int64_t a0 = (x.gref + x.d0) & ~(int64_t)3;
@@ -1198,23 +1232,25 @@ __device__ __forceinline__ void stage_dma(const DpArgs &A, const XItem &x, unsig
     for (int k = 0; k < 2; ++k) {
         int64_t a = a0 + 4 * (64 * k + lane);
         a = a < 0 ? 0 : (a > last ? last : a);
-        dma4(A.I.codes + a, raw + 512 + 256 * k);
+        dma4(A.I.codes + a, raw + RL::REF + 256 * k);
     }
 }
 
 // the tables of an item whose raw bytes stage_dma brought in (after a wait
 // for the wave's vector memory operations)
-template <int LOCAL>
+template <int LOCAL, int ROUND>
 __device__ __forceinline__ void stage_raw(const DpArgs &A, const XItem &it, const XView &X,
                                           const unsigned char *raw, int lane)
 {
+    using RL = RawLayout<ROUND>;
+    constexpr int NR = RL::ROW_ROUNDS, NX = RL::REF_ROUNDS;
     const int m = it.m;
-    const uint32_t *sw = (const uint32_t *)(raw + 256), *nw = sw + 16;
+    const uint32_t *sw = (const uint32_t *)(raw + RL::WORDS), *nw = sw + RL::NSEQ;
     // every LDS read first (no branches: rows past the read read base 0)
-    int b[4];
-    uint32_t nmw[4], sqw[4], qv[4], gv[5];
+    int b[NR];
+    uint32_t nmw[NR], sqw[NR], qv[NR], gv[NX];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < NR; ++u) {
         const int i = 64 * u + lane;
         b[u] = i < m ? (it.strand ? m - 1 - i : i) : 0;
         nmw[u] = nw[b[u] >> 5];
@@ -1223,16 +1259,16 @@ __device__ __forceinline__ void stage_raw(const DpArgs &A, const XItem &it, cons
     }
     const int sh = (int)((it.gref + it.d0) & 3);
 #pragma unroll
-    for (int u = 0; u < 5; ++u) gv[u] = raw[512 + sh + 64 * u + lane];
+    for (int u = 0; u < NX; ++u) gv[u] = raw[RL::REF + sh + 64 * u + lane];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {   // rows 0 .. 255 (the tables hold 256)
+    for (int u = 0; u < NR; ++u) {   // rows 0 .. ROUND - 1 (the tables hold them)
         const int i = 64 * u + lane;
         uint32_t c = ((nmw[u] >> (b[u] & 31)) & 1) ? 4u : ((sqw[u] >> (2 * (b[u] & 15))) & 3u);
         if (it.strand && c < 4) c = 3 - c;
         put_row<LOCAL>(X, i, i < m, c, (int)qv[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 5; ++u) {   // reference bytes 0 .. 319 (the window holds 320)
+    for (int u = 0; u < NX; ++u) {   // reference bytes 0 .. 64 NX - 1 (the window holds rows + 64)
         const int x = 64 * u + lane, j = it.d0 + x;
         const uint32_t g = (j >= 0 && j < it.reflen) ? gv[u] : 4u;
         X.refw[x] = (uint8_t)(g * 4);
@@ -1699,7 +1735,7 @@ __device__ void finish_ext(const DpArgs &A, const XItem &it, const XView &X, con
 // whole wave); an item that needs the DP waits in half 0 until a second one
 // fills half 1, then both run through the rows together.  A last waiting
 // item runs with half 1 repeating it.
-template <int LOCAL, int ONE_ROUND>
+template <int LOCAL, int ROUND>
 __global__ __launch_bounds__(256) void k_dp(DpArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1710,7 +1746,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     uint32_t *bits = (uint32_t *)wbase;                       // rows_pad/8 * 64: 4 bits/cell
     unsigned char *xbase = wbase + (size_t)32 * A.rows_pad;
     const XView X0 = xview(xbase, A.rows_pad, 0), X1 = xview(xbase, A.rows_pad, 1);
-    unsigned char *raw = xbase + 2 * xview_bytes(A.rows_pad);   // RAW_BYTES (reads of one round)
+    unsigned char *raw = xbase + 2 * xview_bytes(A.rows_pad);   // RawLayout<ROUND> (reads of one round)
     const int n_work = A.counters[0];
     const int gmin = A.oeI < A.oeD ? A.oeI : A.oeD;
 
@@ -1731,7 +1767,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     // global round trip between items.
     constexpr int QCH = DP_QUEUE_CHUNK;
     const int gwaves = gridDim.x * wpb;
-    constexpr bool one_round = ONE_ROUND;   // rows_pad <= STAGE_ROWS
+    constexpr bool one_round = ROUND > 0;   // rows_pad <= ROUND
     int cA = (blockIdx.x * wpb + wv) * QCH, cB = 0, qv = 0, p = 0;
     auto grab = [&]() {   // lane 0: the base of a later chunk (in flight until read)
         if (lane == 0) qv = atomicAdd(A.queue, QCH) + gwaves * QCH;
@@ -1759,7 +1795,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         x.reflen = ldc(&A.I.ref_len[cd.ref]);
         x.gref = ldc(&A.I.ref_off[cd.ref]);
         x.hb = ldc(&A.len_tab[3 * (MAXLEN + 1) + m]);
-        if (one_round) stage_dma(A, x, raw, lane);
+        if (one_round) stage_dma<ROUND ? ROUND : 256>(A, x, raw, lane);
         return x;
     };
     if (w < n_work) {
@@ -1783,7 +1819,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         const XView X = h ? X1 : X0;
         if (one_round) {
             if (!landed) vm_wait();   // (after a pending item: nothing ran to cover them)
-            stage_raw<LOCAL>(A, it, X, raw, lane);
+            stage_raw<LOCAL, ROUND ? ROUND : 256>(A, it, X, raw, lane);
         } else {
             stage_ext<LOCAL>(A, it, X, lane);
         }
@@ -2506,23 +2542,29 @@ int run_map(Ctx &c, const mh_params &par)
         };
 
         const int rows_pad = ((c.reads.max_len + 7) / 8) * 8;
-        // traceback bits 32 B per row, then the tables of the wave's two extensions
-        const int wave_lds = 32 * rows_pad + 2 * xview_bytes(rows_pad) +
-                             (rows_pad <= STAGE_ROWS ? RAW_BYTES : 0);
-        // one wave per workgroup: the CU then packs floor(160 KiB / wave_lds)
-        // waves (15 at 251-nt reads) with no workgroup rounding loss
-        int wpb = DP_WAVES_PER_BLOCK;
-        while (wpb > 1 && wpb * wave_lds > 160 * 1024) --wpb;
+        // traceback bits 32 B per row, the tables of the wave's two
+        // extensions, the raw area of a one-round staging
+        const int wave_lds = 32 * rows_pad + 2 * xview_bytes(rows_pad) + raw_bytes(rows_pad);
         if (wave_lds > 160 * 1024) { set_error("mh_map: reads too long for LDS"); return -3; }
+        // waves per workgroup: the most that keeps the CU's resident waves,
+        // floor(160 KiB / (wpb wave_lds)) wpb, at its maximum (at 251-nt reads
+        // all of 1 .. 4 give 12; at 300-nt reads 4 would leave 8 of 10)
+        int wpb = 1;
+        for (int w = DP_WAVES_PER_BLOCK; w >= 1; --w)
+            if ((160 * 1024 / (w * wave_lds)) * w > (160 * 1024 / (wpb * wave_lds)) * wpb ||
+                ((160 * 1024 / (w * wave_lds)) * w == (160 * 1024 / (wpb * wave_lds)) * wpb && w > wpb))
+                wpb = w;
         auto launch_dp = [&](const int32_t *work, const int32_t *count, int32_t *queue,
                              int64_t max_items, const char *name) -> int {
             DpArgs da{c.reads, c.index, c.len_tab, M.cand, work, count, M.skey, M.sinfo, M.pool,
                       M.pool_used, M.counters + 1, queue, M.pool_cap, rows_pad, wave_lds,
                       par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext,
                       par.rdg_ext};
-            const bool one = rows_pad <= STAGE_ROWS;
-            const void *kf = par.mode == MH_LOCAL ? (one ? (const void *)k_dp<1, 1> : (const void *)k_dp<1, 0>)
-                                                  : (one ? (const void *)k_dp<0, 1> : (const void *)k_dp<0, 0>);
+            const int round = rows_pad <= 256 ? 256 : rows_pad <= 320 ? 320 : 0;
+            const void *kf =
+                par.mode == MH_LOCAL
+                    ? (round == 256 ? (const void *)k_dp<1, 256> : round ? (const void *)k_dp<1, 320> : (const void *)k_dp<1, 0>)
+                    : (round == 256 ? (const void *)k_dp<0, 256> : round ? (const void *)k_dp<0, 320> : (const void *)k_dp<0, 0>);
             // the waves that fit at once (the queue balances them), no more
             // than the items need
             const auto okey = std::make_pair(kf, wpb * wave_lds);
@@ -2542,16 +2584,16 @@ int run_map(Ctx &c, const mh_params &par)
             if (dblocks > DP_MAX_BLOCKS) dblocks = DP_MAX_BLOCKS;
             if (dblocks < 1) dblocks = 1;
             const int pd = prof_begin(c, name);
+            const dim3 grid((unsigned)dblocks), block(64 * wpb);
+            const size_t lds = (size_t)wpb * wave_lds;
             if (par.mode == MH_LOCAL) {
-                if (one)
-                    hipLaunchKernelGGL((k_dp<1, 1>), dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
-                else
-                    hipLaunchKernelGGL((k_dp<1, 0>), dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
+                if (round == 256) hipLaunchKernelGGL((k_dp<1, 256>), grid, block, lds, s, da);
+                else if (round) hipLaunchKernelGGL((k_dp<1, 320>), grid, block, lds, s, da);
+                else hipLaunchKernelGGL((k_dp<1, 0>), grid, block, lds, s, da);
             } else {
-                if (one)
-                    hipLaunchKernelGGL((k_dp<0, 1>), dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
-                else
-                    hipLaunchKernelGGL((k_dp<0, 0>), dim3((unsigned)dblocks), dim3(64 * wpb), wpb * wave_lds, s, da);
+                if (round == 256) hipLaunchKernelGGL((k_dp<0, 256>), grid, block, lds, s, da);
+                else if (round) hipLaunchKernelGGL((k_dp<0, 320>), grid, block, lds, s, da);
+                else hipLaunchKernelGGL((k_dp<0, 0>), grid, block, lds, s, da);
             }
             prof_end(c, pd);
             MH_HIP(hipGetLastError());

@@ -292,7 +292,7 @@ static void s2a_mark(std::chrono::steady_clock::time_point t0, const char *what)
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
-int s2a_parse(S2AState &S, const char *text, int64_t len)
+int s2a_parse(S2AState &S, const char *text, int64_t len, int64_t body_lo, int64_t body_hi)
 {
     const auto tp = std::chrono::steady_clock::now();
     const char *p = text, *end = text + len;
@@ -300,6 +300,14 @@ int s2a_parse(S2AState &S, const char *text, int64_t len)
     if (!csv_record(p, end, head)) {
         set_error("remap csv: empty");
         return -3;
+    }
+    if (body_lo >= 0) {       // one part of the body: records [body_lo, body_hi)
+        if (body_lo < p - text || body_hi < body_lo || body_hi > len) {
+            set_error("remap csv: bad part bounds");
+            return -3;
+        }
+        p = text + body_lo;
+        end = text + body_hi;
     }
     const char *want[11] = {"qname", "flag", "rname", "pos", "mapq", "cigar", "rnext", "pnext",
                             "tlen", "seq", "qual"};
@@ -661,14 +669,14 @@ static void s2a_aligned(const S2AState &S, TextSink &out)
 
 // insert.csv rows of parse_sam (sam2aln.py:357-380): every I op of the
 // mates of a unit that reached apply_cigar, at pos - 1 + read offset
-static void s2a_inserts(const S2AState &S, TextSink &out)
+static void s2a_inserts(const S2AState &S, TextSink &out, int64_t u0, int64_t u1, bool head_row)
 {
-    {
+    if (head_row) {
         std::string head("qname,fwd_rev,refname,pos,insert,qual\n");
         out.put(head);
     }
-    parallel_text((int64_t)S.u1.size(), s2a_threads(), out, [&](std::string &o, int64_t a, int64_t b) {
-        for (int64_t u = a; u < b; ++u) {
+    parallel_text(u1 - u0, s2a_threads(), out, [&](std::string &o, int64_t a, int64_t b) {
+        for (int64_t u = u0 + a; u < u0 + b; ++u) {
             if (S.ucause[u] >= 0) continue;
             const int64_t r1 = S.u1[u];
             for (int k = 0; k < (S.upaired[u] ? 2 : 1); ++k) {
@@ -697,14 +705,14 @@ static void s2a_inserts(const S2AState &S, TextSink &out)
     });
 }
 
-static void s2a_failed(const S2AState &S, TextSink &out)
+static void s2a_failed(const S2AState &S, TextSink &out, int64_t u0, int64_t u1, bool head_row)
 {
-    {
+    if (head_row) {
         std::string head("qname,cause\n");
         out.put(head);
     }
-    parallel_text((int64_t)S.u1.size(), s2a_threads(), out, [&](std::string &o, int64_t a, int64_t b) {
-        for (int64_t u = a; u < b; ++u) {
+    parallel_text(u1 - u0, s2a_threads(), out, [&](std::string &o, int64_t a, int64_t b) {
+        for (int64_t u = u0 + a; u < u0 + b; ++u) {
             int cause = S.ucause[u];
             if (cause < 0 && S.res[4 * S.merge_of_unit[u]] == S2A_MANYNS) cause = S2A_MANYNS;
             if (cause < 0) continue;
@@ -719,9 +727,21 @@ static void s2a_failed(const S2AState &S, TextSink &out)
 
 static void s2a_emit(const S2AState &S, int which, TextSink &sink)
 {
+    const int64_t nu = (int64_t)S.u1.size();
     if (which == 0) s2a_aligned(S, sink);
-    else if (which == 1) s2a_inserts(S, sink);
-    else s2a_failed(S, sink);
+    else if (which == 1) s2a_inserts(S, sink, 0, nu, true);
+    else s2a_failed(S, sink, 0, nu, true);
+}
+
+int s2a_format_units(const S2AState &S, int which, int64_t u0, int64_t u1, bool head_row,
+                     std::vector<std::string> &out)
+{
+    out.clear();
+    TextSink sink;
+    sink.out = &out;
+    if (which == 1) s2a_inserts(S, sink, u0, u1, head_row);
+    else s2a_failed(S, sink, u0, u1, head_row);
+    return 0;
 }
 
 int s2a_format(const S2AState &S, int which, std::vector<std::string> &out)

@@ -21,6 +21,9 @@ enum { S2A_OK = 0, S2A_UNMATCHED = 1, S2A_BADCIGAR = 2, S2A_2REFS = 3, S2A_MANYN
 enum { CIG_OK = 0, CIG_STAR = 1, CIG_INVALID = 2, CIG_UNSUPPORTED = 3, CIG_LONG = 4,
        CIG_SHORT = 5 };
 
+struct S2AShard;                 // sam2aln split over the ranks of a job (mh_s2a_shard.cpp)
+void s2a_shard_free(S2AShard *sh);
+
 struct S2AState {
     // ---- rows of the last remap.csv (host) ----
     int64_t n_rows = 0;
@@ -68,10 +71,17 @@ struct S2AState {
     int out_valid = 0;
     // ---- host timings of the last call (ms) ----
     double t_parse = 0, t_device = 0, t_format[3] = {0, 0, 0};
+    // ---- this rank's part of a sharded sam2aln ----
+    S2AShard *shard = nullptr;
+    ~S2AState() { if (shard) s2a_shard_free(shard); }
 };
 
-// host half
-int s2a_parse(S2AState &S, const char *text, int64_t len);
+// host half: the header row of text, then its records (body_lo >= 0: only
+// the records in bytes [body_lo, body_hi) of text, both record boundaries)
+int s2a_parse(S2AState &S, const char *text, int64_t len, int64_t body_lo = -1, int64_t body_hi = -1);
+// insert.csv (which 1) or failed.csv (2) rows of units [u0, u1)
+int s2a_format_units(const S2AState &S, int which, int64_t u0, int64_t u1, bool head_row,
+                     std::vector<std::string> &out);
 int s2a_format(const S2AState &S, int which, std::vector<std::string> &out);
 // the same text written to fd from offset while it is formatted; 0 or errno
 int s2a_format_write(const S2AState &S, int which, int fd, int64_t offset, int64_t *written);

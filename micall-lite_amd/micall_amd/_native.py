@@ -121,6 +121,21 @@ def _declare(L):
         'mh_sam2aln_file': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_double, _I64P], ctypes.c_int),
         'mh_sam2aln_write': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _I64P], ctypes.c_int),
         'mh_sam2aln_stats': ([_P, _P], ctypes.c_int),
+        'mh_sam2aln_part': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                             _I64P], ctypes.c_int),
+        'mh_sam2aln_part_units': ([_P, _P, _P], ctypes.c_int),
+        'mh_sam2aln_part_names': ([_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                                   _I64P], ctypes.c_int),
+        'mh_sam2aln_part_set_names': ([_P, _P, ctypes.c_int], ctypes.c_int),
+        'mh_sam2aln_records': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64P, ctypes.POINTER(_P)],
+                               ctypes.c_int),
+        'mh_sam2aln_records_merge': ([_P, ctypes.c_int, _P, ctypes.c_int64], ctypes.c_int),
+        'mh_sam2aln_splitters': ([_P, _P, ctypes.c_int64, ctypes.c_int], ctypes.c_int),
+        'mh_sam2aln_range_counts': ([_P, ctypes.c_int, _I64P], ctypes.c_int),
+        'mh_sam2aln_range_text': ([_P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), _I64P, _I64P,
+                                   ctypes.POINTER(_P)], ctypes.c_int),
+        'mh_sam2aln_part_text': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64P, ctypes.POINTER(_P)],
+                                 ctypes.c_int),
         'mh_sam2aln_timing': ([_P, _P], ctypes.c_int),
         'mh_censor_fastq': ([_P, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                              ctypes.POINTER(ctypes.c_char_p), _P, ctypes.c_int, _I64P, _I64P],
@@ -282,6 +297,96 @@ class Context:
             return None
         check(st, 'mh_sam2aln_file')
         return n.value
+
+    # ---- sam2aln split over the ranks of a job (mh_s2a_shard.cpp) ----
+    def sam2aln_part(self, fd, part, parts, q_cutoff=15, max_prop_n=0.5):
+        """This rank's records of remap.csv (file fd) parsed and merged:
+        dict(units, pair_units, names, distinct, bytes, file_bytes), or None
+        when the file cannot be split by lines ('\r' or a quoted field)."""
+        info = np.zeros(6, dtype=np.int64)
+        st = lib().mh_sam2aln_part(self.h, int(fd), int(part), int(parts), int(q_cutoff),
+                                   float(max_prop_n), info.ctypes.data_as(_I64P))
+        if st == 1:
+            return None
+        check(st, 'mh_sam2aln_part')
+        return dict(zip(('units', 'pair_units', 'names', 'distinct', 'bytes', 'file_bytes'),
+                        (int(x) for x in info)))
+
+    def sam2aln_part_units(self, n_units):
+        """(qname hash, leftover?) of every unit of this rank's part."""
+        h = np.zeros(max(n_units, 1), dtype=np.uint64)
+        left = np.zeros(max(n_units, 1), dtype=np.uint8)
+        check(lib().mh_sam2aln_part_units(self.h, _ptr(h), _ptr(left)), 'mh_sam2aln_part_units')
+        return h[:n_units], left[:n_units].astype(bool)
+
+    def sam2aln_part_names(self, n_names):
+        """(reference names of this part in first-seen order, first unit of each)."""
+        used = ctypes.c_size_t()
+        check(lib().mh_sam2aln_part_names(self.h, None, 0, ctypes.byref(used), None),
+              'mh_sam2aln_part_names')
+        buf = ctypes.create_string_buffer(max(used.value, 1))
+        first = np.zeros(max(n_names, 1), dtype=np.int64)
+        check(lib().mh_sam2aln_part_names(self.h, buf, len(buf), ctypes.byref(used),
+                                          first.ctypes.data_as(_I64P)), 'mh_sam2aln_part_names')
+        names = buf.raw[:used.value].decode().split('\n')[:n_names]
+        return names, first[:n_names]
+
+    def sam2aln_part_set_names(self, gids):
+        g = np.ascontiguousarray(gids, dtype=np.int32)
+        check(lib().mh_sam2aln_part_set_names(self.h, _ptr(g), len(g)), 'mh_sam2aln_part_set_names')
+
+    def _held_view(self, ptr, n):
+        if n <= 0 or not ptr:
+            return np.zeros(0, dtype=np.uint8)
+        return np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(ptr))
+
+    def sam2aln_records(self, step, parts, per_name=0):
+        """step 0: this part's distinct sequences bucketed by owner rank;
+        1: samples of the owner's sorted records; 2: the owner's records
+        bucketed by range rank.  Returns (uint8 view of the library's buffer,
+        valid until the next call, per-destination sizes)."""
+        sizes = np.zeros(max(parts, 1), dtype=np.int64)
+        ptr = ctypes.c_void_p()
+        check(lib().mh_sam2aln_records(self.h, int(step), int(parts), int(per_name),
+                                       sizes.ctypes.data_as(_I64P), ctypes.byref(ptr)), 'mh_sam2aln_records')
+        n = int(sizes[0]) if step == 1 else int(sizes.sum())
+        return self._held_view(ptr.value, n), (sizes[:1] if step == 1 else sizes)
+
+    def sam2aln_records_merge(self, stage, data):
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        check(lib().mh_sam2aln_records_merge(self.h, int(stage), _ptr(d), len(d)), 'mh_sam2aln_records_merge')
+
+    def sam2aln_splitters(self, data, parts):
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        check(lib().mh_sam2aln_splitters(self.h, _ptr(d), len(d), int(parts)), 'mh_sam2aln_splitters')
+
+    def sam2aln_range_counts(self, n_names):
+        out = np.zeros(max(n_names, 1), dtype=np.int64)
+        check(lib().mh_sam2aln_range_counts(self.h, int(n_names), out.ctypes.data_as(_I64P)),
+              'mh_sam2aln_range_counts')
+        return out[:n_names]
+
+    def sam2aln_range_text(self, names, base):
+        """aligned.csv rows of this rank's ranges: (uint8 view, bytes per name)."""
+        arr = (ctypes.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+        b = np.ascontiguousarray(base, dtype=np.int64)
+        seg = np.zeros(max(len(names), 1), dtype=np.int64)
+        ptr = ctypes.c_void_p()
+        check(lib().mh_sam2aln_range_text(self.h, len(names), arr, b.ctypes.data_as(_I64P),
+                                          seg.ctypes.data_as(_I64P), ctypes.byref(ptr)),
+              'mh_sam2aln_range_text')
+        seg = seg[:len(names)]
+        return self._held_view(ptr.value, int(seg.sum())), seg
+
+    def sam2aln_part_text(self, which, seg, head=False):
+        """insert.csv ('insert') or failed.csv ('failed') rows of this part's
+        pair units (seg 0) or leftover units (seg 1), as bytes."""
+        w = {'insert': 1, 'failed': 2}[which]
+        n = ctypes.c_int64()
+        ptr = ctypes.c_void_p()
+        check(lib().mh_sam2aln_part_text(self.h, w, int(seg), int(bool(head)), ctypes.byref(n),
+                                         ctypes.byref(ptr)), 'mh_sam2aln_part_text')
+        return self._held_view(ptr.value, n.value).tobytes()
 
     def sam2aln_size(self, which):
         """Bytes of output 'aligned' | 'insert' | 'failed' (formats it)."""

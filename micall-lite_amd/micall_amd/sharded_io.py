@@ -80,6 +80,57 @@ def _p2p(sh, sends, recv_sizes):
     return {peer: t.cpu().numpy().tobytes() for peer, t in bufs.items()}
 
 
+def all_to_all_bytes(sh, data, sizes):
+    """Every rank sends sizes[d] bytes of data (laid out by destination) to
+    rank d; returns the bytes received, in source-rank order (uint8)."""
+    torch, dist = sh.torch, sh.dist
+    sizes = np.asarray(sizes, dtype=np.int64)
+    matrix = sh._gather_sizes(sizes)                     # [sender, receiver]
+    recv = [int(matrix[s, sh.rank]) for s in range(sh.world)]
+    if int(matrix.sum()) == 0:
+        return np.zeros(0, dtype=np.uint8)
+    dev = sh._text_device()
+    src = np.ascontiguousarray(data, dtype=np.uint8)
+    inp = torch.from_numpy(src) if dev.type == 'cpu' else torch.from_numpy(src).to(dev)
+    out = torch.empty(sum(recv), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(out, inp, recv, [int(x) for x in sizes])
+    return out.cpu().numpy()
+
+
+def qname_conflict(sh, hashes, leftover):
+    """True on every rank when some qname that is left unpaired on one rank
+    also has rows on another (then the ranks' matchmaker order is not the
+    reference's over the whole file).  Each (qname hash, rank, leftover)
+    goes to the rank that owns the hash, which looks for hashes held by two
+    ranks with a leftover among them."""
+    W = sh.world
+    h = np.asarray(hashes, dtype=np.uint64)
+    owner = (h % np.uint64(W)).astype(np.int64)
+    order = np.argsort(owner, kind='stable')
+    rec = np.empty((len(h), 2), dtype=np.int64)
+    rec[:, 0] = h.view(np.int64)
+    rec[:, 1] = (sh.rank << 1) | np.asarray(leftover, dtype=np.int64)
+    rec = np.ascontiguousarray(rec[order])
+    sizes = np.bincount(owner, minlength=W).astype(np.int64) * 16
+    got = all_to_all_bytes(sh, rec.view(np.uint8).reshape(-1), sizes).view(np.int64).reshape(-1, 2)
+    bad = False
+    if len(got):
+        o = np.lexsort((got[:, 1], got[:, 0]))
+        hv, fl = got[o, 0], got[o, 1]
+        start = np.r_[True, hv[1:] != hv[:-1]]
+        gid = np.cumsum(start) - 1
+        ng = int(gid[-1]) + 1
+        rk = fl >> 1
+        rmin = np.full(ng, np.iinfo(np.int64).max)
+        rmax = np.full(ng, -1)
+        np.minimum.at(rmin, gid, rk)
+        np.maximum.at(rmax, gid, rk)
+        left = np.zeros(ng, dtype=bool)
+        np.logical_or.at(left, gid, (fl & 1) == 1)
+        bad = bool(np.any((rmin != rmax) & left))
+    return bool(sh.sum_i64([1 if bad else 0])[0])
+
+
 # ---- FASTQ staging -------------------------------------------------------------
 class _Frame:
     """One file's framing on this rank after the boundary exchange."""

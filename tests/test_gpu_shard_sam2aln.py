@@ -1,0 +1,88 @@
+"""sam2aln split over the ranks of a job:
+2 and 3 ranks on the test box's one GPU (gloo; RCCL on the driver's nodes
+through the same calls) each parse their share of remap.csv, merge their
+pairs on the device, count the distinct merged sequences by hash owner and
+sort them across the ranks (micall_amd.sam2aln._sam2aln_sharded,
+csrc/mh_s2a_shard.cpp).  aligned.csv, insert.csv and failed.csv must be
+byte-equal to the reference's sam2aln() on the same remap.csv: every e2e
+case (tests/golden/e2e/*) and every reference call and edge-case text of
+tests/golden/sam2aln_e2e.json.  Reference: sam2aln.py:395-478 (its own
+pool splits parse_sam over pairs, :411-424)."""
+import gzip
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, 'golden')
+WORKER = os.path.join(HERE, 'gpu_s2a_worker.py')
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _gz(path):
+    with gzip.open(path, 'rt') as f:
+        return f.read()
+
+
+def _cases(root):
+    """case name -> {'remap.csv': text, output name: expected text or None}"""
+    out = {}
+    for case in sorted(os.listdir(os.path.join(GOLDEN, 'e2e'))):
+        d = os.path.join(GOLDEN, 'e2e', case)
+        out['e2e_' + case] = {'remap.csv': _gz(os.path.join(d, 'remap.csv.gz')),
+                              'aligned.csv': _gz(os.path.join(d, 'aligned.csv.gz')),
+                              'insert.csv': _gz(os.path.join(d, 'insert.csv.gz')),
+                              'failed.csv': _gz(os.path.join(d, 'failed.csv.gz'))}
+    for k, c in enumerate(json.load(open(os.path.join(GOLDEN, 'sam2aln_e2e.json')))['cases']):
+        out['call%02d' % k] = {'remap.csv': c['remap_csv'], 'aligned.csv': c['aligned'],
+                               'insert.csv': c['insert'], 'failed.csv': c['failed']}
+    for name, files in out.items():
+        os.makedirs(os.path.join(root, name))
+        with open(os.path.join(root, name, 'remap.csv'), 'w') as f:
+            f.write(files['remap.csv'])
+    return out
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('world', [2, 3])
+def test_sharded_sam2aln_matches_reference(tmp_path, world):
+    root = str(tmp_path / 'cases')
+    os.makedirs(root)
+    cases = _cases(root)
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_port()), WORLD_SIZE=str(world),
+               MICALL_DIST_BACKEND='gloo', MICALL_HIP_DEVICE='0')
+    procs = [subprocess.Popen([sys.executable, WORKER, '--cases', root],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r))) for r in range(world)]
+    try:
+        codes = [p.wait(timeout=800) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert codes == [0] * world, codes
+    stats = [json.load(open(os.path.join(root, 'rank%d.json' % r))) for r in range(world)]
+    for name, files in cases.items():
+        for out in ('aligned.csv', 'insert.csv', 'failed.csv'):
+            if files[out] is None:
+                continue
+            got = open(os.path.join(root, name, out)).read()
+            assert got == files[out], (name, out)
+    # the e2e cases (mates in adjacent rows) run split: every rank parsed a
+    # share of remap.csv, none the whole file
+    for name in cases:
+        if not name.startswith('e2e_'):
+            continue
+        assert all(s[name].get('mode') == 'sharded' for s in stats), (name, [s[name] for s in stats])
+        parsed = [s[name]['bytes'] for s in stats]
+        assert sum(parsed) > 0 and max(parsed) < stats[0][name]['file_bytes'], (name, parsed)
