@@ -232,6 +232,21 @@ static std::pair<const char *, size_t> qname_at(const char *t, int64_t a, int64_
     return {p, (size_t)((c ? c : le) - p)};
 }
 
+// true when no line end of [a, e) lies inside quotes (and the quotes
+// balance): every line holds an even number of '"'
+static bool even_quote_lines(const char *a, const char *e)
+{
+    bool open = false;
+    const char *q = a;
+    for (const char *x = (const char *)memchr(a, '"', (size_t)(e - a)); x;
+         x = (const char *)memchr(q, '"', (size_t)(e - q))) {
+        if (open && memchr(q, '\n', (size_t)(x - q))) return false;
+        open = !open;
+        q = x + 1;
+    }
+    return !open;
+}
+
 // The cut between part k - 1 and part k: the record start at or after the
 // even split of the body; when the rows either side of it have one qname
 // (the two mates of a pair, written one after the other) it moves past the
@@ -543,20 +558,25 @@ extern "C" int mh_sam2aln_part(mh_ctx *ctx, int fd, int part, int parts, int q_c
         S.res.clear();
         for (auto &o : S.out_cache) std::vector<std::string>().swap(o);
         S.out_valid = 0;
-        // the header row, the qname column; a quoted field anywhere means a
-        // record may span lines: not split
+        // the header row and the qname column
         const char *p = text, *end = text + len;
         std::vector<std::string> head;
         if (!csv_record(p, end, head)) { set_error("remap csv: empty"); return -3; }
         int qcol = -1;
         for (size_t k = 0; k < head.size(); ++k) if (head[k] == "qname") qcol = (int)k;
-        if (qcol < 0 || memchr(text, '"', len)) return 1;
+        if (qcol < 0) return 1;
         const int64_t lo = p - text, hi = (int64_t)len;
         S2AShard &H = s2a_shard(S);
         H.part = part;
         H.parts = parts;
         H.b0 = s2a_cut(text, lo, hi, part, parts, qcol);
         H.b1 = s2a_cut(text, lo, hi, part + 1, parts, qcol);
+        // the cuts are record starts when no quoted field holds a line end
+        // (csv quotes a quality string with '"' or ',' in it, never across
+        // lines in remap.csv): every line of this part has an even number of
+        // quote characters, else the part is not split (the caller's ranks
+        // agree on it)
+        if (!even_quote_lines(text + H.b0, text + H.b1)) return 1;
         const auto t0 = std::chrono::steady_clock::now();
         if (int st = s2a_parse(S, text, (int64_t)len, H.b0, H.b1)) return st;
         const auto t1 = std::chrono::steady_clock::now();

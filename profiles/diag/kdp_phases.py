@@ -1,11 +1,11 @@
 """Throwaway k_dp phase clock: copies micall-lite_amd/csrc to
-variants/phases/src, inserts s_memtime stamps around the phases of k_dp's
+_ab/phases/src, inserts s_memtime stamps around the phases of k_dp's
 item loop (staging, fast-path attempt, DP rows, finish of fast items, finish
 of DP pairs, the tail), sums the wave cycles per phase and mode in a device
 array, and prints them to stderr after every mh_map pass.  Builds
-variants/phases/libmicall_hip.so; run with MICALL_HIP_LIB pointing at it.
+_ab/phases/libmicall_hip.so; run with MICALL_HIP_LIB pointing at it.
 
-    python profiles/diag/kdp_phases.py && make -C variants/phases/src -j8 \
+    python profiles/diag/kdp_phases.py && make -C _ab/phases/src -j8 \
         OUTDIR=.. OBJDIR=_obj
 """
 import os
@@ -14,7 +14,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SRC = os.path.join(ROOT, 'micall-lite_amd', 'csrc')
-DST = os.path.join(ROOT, 'variants', 'phases', 'src')
+DST = os.path.join(ROOT, '_ab', 'phases', 'src')
 
 
 def sub(text, old, new, count=1):
@@ -34,9 +34,9 @@ def main():
     open(os.path.join(DST, 'Makefile'), 'w').write(mk)
     p = os.path.join(DST, 'mh_map.hip')
     t = open(p).read()
-    t = sub(t, 'template <int LOCAL, int ONE_ROUND>\n__global__ __launch_bounds__(256) void k_dp(DpArgs A)',
+    t = sub(t, 'template <int LOCAL, int ROUND>\n__global__ __launch_bounds__(256) void k_dp(DpArgs A)',
             '__device__ unsigned long long g_ph[2][8];\n'
-            'template <int LOCAL, int ONE_ROUND>\n__global__ __launch_bounds__(256) void k_dp(DpArgs A)')
+            'template <int LOCAL, int ROUND>\n__global__ __launch_bounds__(256) void k_dp(DpArgs A)')
     t = sub(t, '    bool pend = false;     // half 0 holds an item waiting for the DP\n',
             '    bool pend = false;     // half 0 holds an item waiting for the DP\n'
             '    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};\n'
