@@ -35,6 +35,7 @@
 #include <chrono>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <functional>
 #include <string>
 #include <thread>
@@ -109,6 +110,11 @@ struct A2CState {
     std::string ins_rows;                     // mh_a2c_insert_rows text (size query, then copy)
     std::unordered_map<const void *, size_t> dcap;   // bytes behind each device pointer (grow-only)
     double t_parse = 0, t_count = 0, t_ins = 0;
+    // a part of aligned.csv held between mh_a2c_part_open and _count (mapped)
+    const char *part_text = nullptr;
+    size_t part_len = 0;
+    int64_t part_b0 = 0, part_b1 = 0;         // the part's bytes of the text
+    std::vector<int64_t> part_first;          // local groups' first rows (+ end)
 };
 
 // ---------------------------------------------------------------------------
@@ -507,15 +513,23 @@ static void a2c_parse_quoted(A2CPart &P, const int *col, int need, const uint8_t
 }
 
 // Per-group codon extents, bins, bin row lists and chunks.
-static int a2c_layout(A2CState &S, std::vector<int32_t> &bin_rows, std::vector<A2CChunk> &chunks)
+// preset: g_ncod and every row's `local` were set by the caller (a part of
+// a sharded job: the job's codon extents and row numbers within the group)
+static int a2c_layout(A2CState &S, std::vector<int32_t> &bin_rows, std::vector<A2CChunk> &chunks,
+                      bool preset = false)
 {
     const int64_t ng = (int64_t)S.g_first.size() - 1;
-    S.g_ncod.assign(3 * ng, 0);
+    if (!preset) S.g_ncod.assign(3 * ng, 0);
     S.g_bin0.assign(ng + 1, 0);
     if (S.n_rows >= INT32_MAX) { set_error("aln2counts: more than 2**31 rows"); return -3; }
     for (int64_t g = 0; g < ng; ++g) {
-        uint64_t total = 0;
         int32_t *nc = &S.g_ncod[3 * g];
+        if (preset) {
+            const int top = std::max(nc[0], std::max(nc[1], nc[2]));
+            S.g_bin0[g + 1] = S.g_bin0[g] + (top + A2C_W - 1) / A2C_W;
+            continue;
+        }
+        uint64_t total = 0;
         for (int64_t r = S.g_first[g]; r < S.g_first[g + 1]; ++r) {
             A2CRow &R = S.rows[r];
             R.local = (uint32_t)(r - S.g_first[g]);
@@ -584,11 +598,11 @@ static int a2c_upload(A2CState &S, T *&dst, const T *src, size_t n, hipStream_t 
 }
 
 // upload the rows, count every group on the device, fetch the counters
-static int a2c_count(Ctx &c, A2CState &S, const char *text, int64_t text_len)
+static int a2c_count(Ctx &c, A2CState &S, const char *text, int64_t text_len, bool preset = false)
 {
     std::vector<int32_t> bin_rows;
     std::vector<A2CChunk> chunks;
-    if (int st = a2c_layout(S, bin_rows, chunks)) return st;
+    if (int st = a2c_layout(S, bin_rows, chunks, preset)) return st;
     hipStream_t s = c.stream;
     if (int st = a2c_upload(S, S.d_text, (const uint8_t *)text, (size_t)text_len, s)) return st;
     if (int st = a2c_upload(S, S.d_rows, S.rows.data(), S.rows.size(), s)) return st;
@@ -624,7 +638,8 @@ static int a2c_count(Ctx &c, A2CState &S, const char *text, int64_t text_len)
     return 0;
 }
 
-static int a2c_parse_csv(A2CState &S, const char *text, int64_t len, bool &use_pool)
+static int a2c_parse_csv(A2CState &S, const char *text, int64_t len, bool &use_pool,
+                         int64_t body_lo = -1, int64_t body_hi = -1)
 {
     const char *p = text, *end = text + len;
     std::vector<std::string> head;
@@ -635,6 +650,10 @@ static int a2c_parse_csv(A2CState &S, const char *text, int64_t len, bool &use_p
     S.pool.clear();
     use_pool = false;
     if (!csv_record(p, end, head)) return 0;             // empty file: no rows
+    if (body_lo >= 0) {      // one part of the body: the records of [body_lo, body_hi)
+        p = text + std::max<int64_t>(body_lo, p - text);
+        end = text + std::max<int64_t>(body_hi, p - text);
+    }
     static const char *const want[N_COLS] = {"refname", "qcut", "count", "offset", "seq"};
     int col[N_COLS];
     int need = 0;
@@ -722,6 +741,7 @@ void a2c_free(Ctx &c)
     if (!c.a2c) return;
     for (int k = 0; k < A2C_SLOTS; ++k)
         if (c.a2c[k]) {
+            if (c.a2c[k]->part_text) unmap_text_file(c.a2c[k]->part_text, c.a2c[k]->part_len);
             a2c_free_device(*c.a2c[k]);
             delete c.a2c[k];
         }
@@ -752,6 +772,10 @@ extern "C" int mh_a2c_load_csv(mh_ctx *ctx, int slot, const char *text, int64_t 
     MH_HIP(hipSetDevice(c.device));
     A2CState &S = *a2c_state(c, slot);
     a2c_clear_inserts(S);
+    if (S.part_text) {       // a part left open by a sharded load that fell back
+        unmap_text_file(S.part_text, S.part_len);
+        S.part_text = nullptr;
+    }
     auto t0 = std::chrono::steady_clock::now();
     if (int st = a2c_tables(S, codon_chars)) return st;
     bool use_pool = false;
@@ -1104,5 +1128,283 @@ extern "C" int mh_a2c_timing(mh_ctx *ctx, int slot, double *ms3)
     ms3[1] = S.t_count;
     ms3[2] = S.t_ins;
     S.t_ins = 0;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// aln2counts split over the ranks of a job.  The reference counts every row
+// of aligned.csv into per-(refname, qcut) Counters (aln2counts.py:115-172),
+// in file order; the counts are sums and the first row a Counter saw is a
+// minimum, so rank r counts the rows in its share of the file's bytes and
+// the caller adds the ranks' counters up (and takes the minimum of their
+// first rows): mh_a2c_part_open parses the share, mh_a2c_part_groups reports
+// its runs of (refname, qcut), mh_a2c_part_count lays out the job's groups
+// (codon extents, row numbers within a group from the ranks before) and
+// counts, mh_a2c_part_counters hands the counters out and takes the sums
+// back.  The insertion strings of InsertionWriter.write (:786-795) are the
+// same kind of reduction: mh_a2c_insert_export / mh_a2c_insert_merge.
+// ---------------------------------------------------------------------------
+static int64_t a2c_line_start(const char *t, int64_t lo, int64_t hi, int64_t x)
+{
+    if (x <= lo) return lo;
+    if (x >= hi) return hi;
+    if (t[x - 1] == '\n') return x;
+    const char *q = (const char *)memchr(t + x, '\n', (size_t)(hi - x));
+    return q ? (q - t) + 1 : hi;
+}
+
+extern "C" int mh_a2c_part_open(mh_ctx *ctx, int slot, int fd, int part, int parts,
+                                const char *codon_chars, int64_t *info3)
+{
+    if (!ctx || slot < 0 || slot >= A2C_SLOTS || fd < 0 || parts < 1 || part < 0 || part >= parts ||
+        !info3)
+        return -3;
+    Ctx &c = *ctx_of(ctx);
+    MH_HIP(hipSetDevice(c.device));
+    A2CState &S = *a2c_state(c, slot);
+    a2c_clear_inserts(S);
+    if (S.part_text) { unmap_text_file(S.part_text, S.part_len); S.part_text = nullptr; }
+    if (int st = a2c_tables(S, codon_chars)) return st;
+    const char *text = nullptr;
+    size_t len = 0;
+    if (int st = map_text_file(fd, &text, &len)) return st;   // 1: '\r' in it
+    auto t0 = std::chrono::steady_clock::now();
+    const char *p = text, *end = text + len;
+    std::vector<std::string> head;
+    int64_t lo = 0, hi = (int64_t)len;
+    if (csv_record(p, end, head)) lo = p - text;
+    const int64_t b0 = a2c_line_start(text, lo, hi, lo + (hi - lo) * part / parts);
+    const int64_t b1 = a2c_line_start(text, lo, hi, lo + (hi - lo) * (part + 1) / parts);
+    // a quoted field (a refname with a comma) is parsed on one thread into a
+    // pool; the split is kept to unquoted files
+    if (memchr(text + b0, '"', (size_t)(b1 - b0))) { unmap_text_file(text, len); return 1; }
+    bool use_pool = false;
+    int st = 0;
+    try {
+        st = a2c_parse_csv(S, text, (int64_t)len, use_pool, b0, b1);
+    } catch (const std::exception &e) {
+        set_error("aligned csv: out of memory (%s)", e.what());
+        st = -2;
+    }
+    if (st || use_pool) {
+        unmap_text_file(text, len);
+        S.rows.clear();
+        S.g_first.assign(1, 0);
+        return st ? st : 1;
+    }
+    S.part_text = text;
+    S.part_len = len;
+    S.part_b0 = b0;
+    S.part_b1 = b1;
+    S.part_first = S.g_first;
+    S.t_parse = ms_since(t0);
+    info3[0] = S.n_rows;
+    info3[1] = (int64_t)S.g_first.size() - 1;
+    info3[2] = b1 - b0;
+    return 0;
+}
+
+extern "C" int mh_a2c_part_groups(mh_ctx *ctx, int slot, char *keys, size_t cap, size_t *used,
+                                  int64_t *rows, int32_t *ncod3, int64_t *total)
+{
+    if (!ctx || slot < 0 || slot >= A2C_SLOTS || !used) return -3;
+    Ctx &c = *ctx_of(ctx);
+    A2CState &S = *a2c_state(c, slot);
+    const int64_t ng = (int64_t)S.part_first.size() - 1;
+    size_t need = 0;
+    for (int64_t g = 0; g < ng; ++g) need += S.g_ref[g].size() + S.g_qcut[g].size() + 2;
+    *used = need;
+    if (!keys) return 0;
+    if (cap < need || !rows || !ncod3 || !total) { set_error("mh_a2c_part_groups: buffer too small"); return -2; }
+    for (int64_t g = 0; g < ng; ++g) {
+        memcpy(keys, S.g_ref[g].data(), S.g_ref[g].size());
+        keys += S.g_ref[g].size();
+        *keys++ = '\x1f';
+        memcpy(keys, S.g_qcut[g].data(), S.g_qcut[g].size());
+        keys += S.g_qcut[g].size();
+        *keys++ = '\n';
+        int32_t nc[3] = {0, 0, 0};
+        uint64_t tot = 0;
+        for (int64_t r = S.part_first[g]; r < S.part_first[g + 1]; ++r) {
+            const A2CRow &R = S.rows[r];
+            tot += R.cnt;
+            const int l = R.off / 3;
+            for (int f = 0; f < 3; ++f) {
+                const int h = (f + R.off + R.len + 2) / 3;
+                if (h > l && h > nc[f]) nc[f] = h;
+            }
+        }
+        rows[g] = S.part_first[g + 1] - S.part_first[g];
+        for (int f = 0; f < 3; ++f) ncod3[3 * g + f] = nc[f];
+        total[g] = (int64_t)tot;
+    }
+    return 0;
+}
+
+extern "C" int mh_a2c_part_count(mh_ctx *ctx, int slot, int64_t n_groups, const char *keys,
+                                 const int64_t *gid, const int32_t *ncod3, const int64_t *row_base,
+                                 int64_t *cells)
+{
+    if (!ctx || slot < 0 || slot >= A2C_SLOTS || n_groups < 0 || (n_groups && (!keys || !ncod3)) ||
+        !cells)
+        return -3;
+    Ctx &c = *ctx_of(ctx);
+    MH_HIP(hipSetDevice(c.device));
+    A2CState &S = *a2c_state(c, slot);
+    if (!S.part_text) { set_error("mh_a2c_part_count: no part open"); return -3; }
+    const int64_t nl = (int64_t)S.part_first.size() - 1;
+    if (nl && (!gid || !row_base)) return -3;
+    for (int64_t k = 0; k < nl; ++k)
+        if (gid[k] < 0 || gid[k] >= n_groups || (k && gid[k] <= gid[k - 1])) {
+            set_error("mh_a2c_part_count: group ids out of order");
+            return -3;
+        }
+    // the job's groups, this part's rows in them (global row numbers within
+    // a group for the first-row counters)
+    std::vector<std::string> ref, qcut;
+    const char *p = keys;
+    for (int64_t g = 0; g < n_groups; ++g) {
+        const char *us = strchr(p, '\x1f'), *nlp = us ? strchr(us, '\n') : nullptr;
+        if (!us || !nlp) { set_error("mh_a2c_part_count: malformed group keys"); return -3; }
+        ref.emplace_back(p, (size_t)(us - p));
+        qcut.emplace_back(us + 1, (size_t)(nlp - us - 1));
+        p = nlp + 1;
+    }
+    std::vector<int64_t> first((size_t)n_groups + 1, 0);
+    {
+        int64_t k = 0, at = 0;
+        for (int64_t g = 0; g < n_groups; ++g) {
+            first[(size_t)g] = at;
+            if (k < nl && gid[k] == g) {
+                for (int64_t r = S.part_first[k]; r < S.part_first[k + 1]; ++r)
+                    S.rows[r].local = (uint32_t)(row_base[k] + (r - S.part_first[k]));
+                at = S.part_first[k + 1];
+                ++k;
+            }
+        }
+        first[(size_t)n_groups] = at;
+    }
+    S.g_first.swap(first);
+    S.g_ref.swap(ref);
+    S.g_qcut.swap(qcut);
+    S.g_ncod.assign(ncod3, ncod3 + 3 * n_groups);
+    auto t1 = std::chrono::steady_clock::now();
+    int st = 0;
+    try {
+        // only the part's bytes go to the device: row offsets from b0
+        for (A2CRow &R : S.rows) R.soff -= S.part_b0;
+        st = a2c_count(c, S, S.part_text + S.part_b0, S.part_b1 - S.part_b0, true);
+    } catch (const std::exception &e) {
+        set_error("aln2counts: out of memory (%s)", e.what());
+        st = -2;
+    }
+    unmap_text_file(S.part_text, S.part_len);
+    S.part_text = nullptr;
+    S.part_len = 0;
+    if (st) {
+        S.rows.clear();
+        S.g_first.assign(1, 0);
+        return st;
+    }
+    S.t_count = ms_since(t1);
+    *cells = (int64_t)S.h_cnt.size();
+    return 0;
+}
+
+extern "C" int mh_a2c_part_counters(mh_ctx *ctx, int slot, int set, uint32_t *cnt, uint32_t *first)
+{
+    if (!ctx || slot < 0 || slot >= A2C_SLOTS || !cnt || !first) return -3;
+    Ctx &c = *ctx_of(ctx);
+    A2CState &S = *a2c_state(c, slot);
+    const size_t n = S.h_cnt.size();
+    if (set) {
+        memcpy(S.h_cnt.data(), cnt, 4 * n);
+        memcpy(S.h_first.data(), first, 4 * n);
+    } else {
+        memcpy(cnt, S.h_cnt.data(), 4 * n);
+        memcpy(first, S.h_first.data(), 4 * n);
+    }
+    return 0;
+}
+
+// insertion entries on the wire: range, first row, codons, string length,
+// count, then the string, padded to 8
+struct A2CWireEntry {
+    int32_t range;
+    uint32_t first;
+    int32_t n_codons;
+    int32_t slen;
+    unsigned long long count;
+};
+
+extern "C" int mh_a2c_insert_export(mh_ctx *ctx, int slot, uint8_t *buf, size_t cap, size_t *used)
+{
+    if (!ctx || slot < 0 || slot >= A2C_SLOTS || !used) return -3;
+    Ctx &c = *ctx_of(ctx);
+    A2CState &S = *a2c_state(c, slot);
+    size_t need = 0;
+    const char *am = S.aminos.data(), *am_end = am + S.aminos.size();
+    std::vector<std::pair<const char *, size_t>> str;
+    for (size_t k = 0; k < S.entries.size(); ++k) {
+        const char *nl = (const char *)memchr(am, '\n', (size_t)(am_end - am));
+        if (!nl) { set_error("mh_a2c_insert_export: entry strings out of step"); return -3; }
+        str.emplace_back(am, (size_t)(nl - am));
+        need += sizeof(A2CWireEntry) + ((str.back().second + 7) & ~(size_t)7);
+        am = nl + 1;
+    }
+    *used = need;
+    if (!buf) return 0;
+    if (cap < need) { set_error("mh_a2c_insert_export: buffer too small"); return -2; }
+    memset(buf, 0, need);
+    for (size_t k = 0; k < S.entries.size(); ++k) {
+        const A2CEntry &e = S.entries[k];
+        A2CWireEntry w{e.range, e.first, e.n_codons, (int32_t)str[k].second, e.count};
+        memcpy(buf, &w, sizeof w);
+        memcpy(buf + sizeof w, str[k].first, str[k].second);
+        buf += sizeof w + ((str[k].second + 7) & ~(size_t)7);
+    }
+    return 0;
+}
+
+// every rank's entries of one insertion call: equal (range, string) added
+// up, the first row the least, in (range, first row) order
+extern "C" int mh_a2c_insert_merge(mh_ctx *ctx, int slot, const uint8_t *buf, int64_t len,
+                                   int64_t *n_entries)
+{
+    if (!ctx || slot < 0 || slot >= A2C_SLOTS || (!buf && len) || len < 0) return -3;
+    Ctx &c = *ctx_of(ctx);
+    A2CState &S = *a2c_state(c, slot);
+    std::map<std::pair<int32_t, std::string>, A2CEntry> merged;
+    int64_t at = 0;
+    while (at < len) {
+        if (len - at < (int64_t)sizeof(A2CWireEntry)) { set_error("mh_a2c_insert_merge: malformed"); return -3; }
+        A2CWireEntry w;
+        memcpy(&w, buf + at, sizeof w);
+        const int64_t sz = (int64_t)(sizeof w + (((size_t)w.slen + 7) & ~(size_t)7));
+        if (w.slen < 0 || len - at < sz) { set_error("mh_a2c_insert_merge: malformed"); return -3; }
+        std::string key((const char *)buf + at + sizeof w, (size_t)w.slen);
+        auto it = merged.find({w.range, key});
+        if (it == merged.end()) {
+            merged.emplace(std::make_pair(w.range, std::move(key)), A2CEntry{w.range, w.first, w.n_codons, 0, w.count});
+        } else {
+            it->second.count += w.count;
+            it->second.first = std::min(it->second.first, w.first);
+        }
+        at += sz;
+    }
+    std::vector<std::pair<const std::string *, A2CEntry>> v;
+    for (auto &kv : merged) v.push_back({&kv.first.second, kv.second});
+    std::sort(v.begin(), v.end(), [](const auto &x, const auto &y) {
+        return x.second.range != y.second.range ? x.second.range < y.second.range
+                                                : x.second.first < y.second.first;
+    });
+    S.entries.clear();
+    S.aminos.clear();
+    for (auto &x : v) {
+        S.entries.push_back(x.second);
+        S.aminos += *x.first;
+        S.aminos.push_back('\n');
+    }
+    if (n_entries) *n_entries = (int64_t)S.entries.size();
     return 0;
 }

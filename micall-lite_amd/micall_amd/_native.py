@@ -121,6 +121,16 @@ def _declare(L):
         'mh_sam2aln_file': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_double, _I64P], ctypes.c_int),
         'mh_sam2aln_write': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _I64P], ctypes.c_int),
         'mh_sam2aln_stats': ([_P, _P], ctypes.c_int),
+        'mh_a2c_part_open': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                              _I64P], ctypes.c_int),
+        'mh_a2c_part_groups': ([_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                                ctypes.POINTER(ctypes.c_size_t), _I64P, _P, _I64P], ctypes.c_int),
+        'mh_a2c_part_count': ([_P, ctypes.c_int, ctypes.c_int64, ctypes.c_char_p, _I64P, _P, _I64P, _I64P],
+                              ctypes.c_int),
+        'mh_a2c_part_counters': ([_P, ctypes.c_int, ctypes.c_int, _P, _P], ctypes.c_int),
+        'mh_a2c_insert_export': ([_P, ctypes.c_int, _P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)],
+                                 ctypes.c_int),
+        'mh_a2c_insert_merge': ([_P, ctypes.c_int, _P, ctypes.c_int64, _I64P], ctypes.c_int),
         'mh_sam2aln_part': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                              _I64P], ctypes.c_int),
         'mh_sam2aln_part_units': ([_P, _P, _P], ctypes.c_int),
@@ -510,6 +520,93 @@ class Context:
         buf = ctypes.create_string_buffer(max(used.value, 1))
         check(lib().mh_a2c_insert_rows(*args, buf, len(buf), ctypes.byref(used)), 'mh_a2c_insert_rows')
         return buf.raw[:used.value].decode()
+
+    def _a2c_insert_rows(self, slot, lefts, lead, targets, eol):
+        lo = np.array(list(lefts) or [0], dtype=np.int32)
+        tg = np.array([INT32_MIN if t is None else t for t in targets] or [0], dtype=np.int32)
+        used = ctypes.c_size_t()
+        args = (self.h, slot, lead.encode(), len(lefts), _ptr(lo), _ptr(tg), eol.encode())
+        check(lib().mh_a2c_insert_rows(*args, None, 0, ctypes.byref(used)), 'mh_a2c_insert_rows')
+        buf = ctypes.create_string_buffer(max(used.value, 1))
+        check(lib().mh_a2c_insert_rows(*args, buf, len(buf), ctypes.byref(used)), 'mh_a2c_insert_rows')
+        return buf.raw[:used.value].decode()
+
+    # ---- aln2counts split over the ranks of a job (mh_a2c_part_*) ----
+    def a2c_part_open(self, slot, fd, part, parts, codon_chars):
+        """Parse this rank's share of aligned.csv (file fd): dict(rows,
+        groups, bytes), or None when the file is not split ('\r' or quotes)."""
+        info = np.zeros(3, dtype=np.int64)
+        st = lib().mh_a2c_part_open(self.h, slot, int(fd), int(part), int(parts), codon_chars,
+                                    info.ctypes.data_as(_I64P))
+        if st == 1:
+            return None
+        check(st, 'mh_a2c_part_open')
+        return dict(rows=int(info[0]), groups=int(info[1]), bytes=int(info[2]))
+
+    def a2c_part_groups(self, slot, n):
+        """This part's runs of (refname, qcut): (key bytes 'ref\x1fqcut\n'
+        joined, rows, codon extents [n, 3], count totals)."""
+        used = ctypes.c_size_t()
+        check(lib().mh_a2c_part_groups(self.h, slot, None, 0, ctypes.byref(used), None, None, None),
+              'mh_a2c_part_groups')
+        buf = ctypes.create_string_buffer(max(used.value, 1))
+        rows = np.zeros(max(n, 1), dtype=np.int64)
+        ncod = np.zeros((max(n, 1), 3), dtype=np.int32)
+        total = np.zeros(max(n, 1), dtype=np.int64)
+        check(lib().mh_a2c_part_groups(self.h, slot, buf, len(buf), ctypes.byref(used),
+                                       rows.ctypes.data_as(_I64P), _ptr(ncod), total.ctypes.data_as(_I64P)),
+              'mh_a2c_part_groups')
+        return buf.raw[:used.value], rows[:n], ncod[:n], total[:n]
+
+    def a2c_part_count(self, slot, keys, gid, ncod, row_base):
+        """Count this part's rows into the job's groups (keys joined as
+        a2c_part_groups gives them); returns the counter cells."""
+        g = np.ascontiguousarray(gid, dtype=np.int64)
+        nc = np.ascontiguousarray(ncod, dtype=np.int32)
+        rb = np.ascontiguousarray(row_base, dtype=np.int64)
+        cells = ctypes.c_int64()
+        n_groups = keys.count(b'\n')
+        check(lib().mh_a2c_part_count(self.h, slot, n_groups, keys, g.ctypes.data_as(_I64P), _ptr(nc),
+                                      rb.ctypes.data_as(_I64P), ctypes.byref(cells)), 'mh_a2c_part_count')
+        return cells.value
+
+    def a2c_part_counters(self, slot, cells, values=None):
+        """The counters (count, first row) of the slot, or set them."""
+        if values is not None:
+            c = np.ascontiguousarray(values[0], dtype=np.uint32)
+            f = np.ascontiguousarray(values[1], dtype=np.uint32)
+            check(lib().mh_a2c_part_counters(self.h, slot, 1, _ptr(c), _ptr(f)), 'mh_a2c_part_counters')
+            return None
+        c = np.zeros(max(cells, 1), dtype=np.uint32)
+        f = np.zeros(max(cells, 1), dtype=np.uint32)
+        check(lib().mh_a2c_part_counters(self.h, slot, 0, _ptr(c), _ptr(f)), 'mh_a2c_part_counters')
+        return c[:cells], f[:cells]
+
+    def a2c_inserts_local(self, slot, g, frame, lefts, rights):
+        """mh_a2c_inserts over this rank's rows of group g, then the entries
+        as bytes (mh_a2c_insert_export)."""
+        lo = np.array(list(lefts) or [0], dtype=np.int32)
+        hi = np.array(list(rights) or [0], dtype=np.int32)
+        n = ctypes.c_int64()
+        check(lib().mh_a2c_inserts(self.h, slot, g, frame, len(lefts), _ptr(lo), _ptr(hi),
+                                   ctypes.byref(n)), 'mh_a2c_inserts')
+        used = ctypes.c_size_t()
+        check(lib().mh_a2c_insert_export(self.h, slot, None, 0, ctypes.byref(used)), 'mh_a2c_insert_export')
+        buf = np.zeros(max(used.value, 1), dtype=np.uint8)
+        check(lib().mh_a2c_insert_export(self.h, slot, _ptr(buf), len(buf), ctypes.byref(used)),
+              'mh_a2c_insert_export')
+        return buf[:used.value].tobytes()
+
+    def a2c_inserts_merged_text(self, slot, entries, lefts, lead, targets, eol):
+        """Every rank's entries merged (mh_a2c_insert_merge), then the rows
+        as text ('' when there are none)."""
+        d = np.frombuffer(entries, dtype=np.uint8) if entries else np.zeros(1, dtype=np.uint8)
+        n = ctypes.c_int64()
+        check(lib().mh_a2c_insert_merge(self.h, slot, _ptr(d), len(entries), ctypes.byref(n)),
+              'mh_a2c_insert_merge')
+        if n.value == 0:
+            return ''
+        return self._a2c_insert_rows(slot, lefts, lead, targets, eol)
 
     def a2c_load_rows(self, slot, seqs, offsets, counts, group_first, codon_chars):
         """mh_a2c_load_rows from lists: seq strings, offsets, counts and the

@@ -45,6 +45,7 @@ from collections import Counter, namedtuple
 
 import numpy as np
 
+from . import _native
 from . import projects as project_config
 from . import session
 from .translation import AMBIG, codon_chars, translate
@@ -709,8 +710,17 @@ class InsertionWriter(object):
         lead = io.StringIO()
         csv.writer(lead, lineterminator='').writerow([self.seed, region, self.qcut, ''])
         ctx, slot, g = source
-        text = ctx.a2c_inserts_text(slot, g, reading_frame, [r[0] for r in kept], [r[1] for r in kept],
-                                    lead.getvalue(), [target.get(r[0]) for r in kept], os.linesep)
+        lefts, rights = [r[0] for r in kept], [r[1] for r in kept]
+        targets = [target.get(r[0]) for r in kept]
+        if _SHARD is not None and slot == SLOT_REPORT:
+            # every rank's strings over its own rows, added up (the first
+            # rows are the job's row numbers within the group)
+            mine = ctx.a2c_inserts_local(slot, g, reading_frame, lefts, rights)
+            text = ctx.a2c_inserts_merged_text(slot, b''.join(_SHARD.all_gather_bytes(mine)), lefts,
+                                               lead.getvalue(), targets, os.linesep)
+        else:
+            text = ctx.a2c_inserts_text(slot, g, reading_frame, lefts, rights, lead.getvalue(), targets,
+                                        os.linesep)
         if text:
             self._file.write(text)
 
@@ -720,23 +730,103 @@ def format_cutoff(cutoff):
     return cutoff if cutoff == MAX_CUTOFF else '%.3f' % cutoff
 
 
+SHARD_STATS = {}   # how the last sharded call ran (tests): rows and bytes this rank parsed
+_SHARD = None      # the job's Shard while a sharded aln2counts runs (InsertionWriter.write)
+
+
 def aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv,
                failed_align_csv=None, nuc_variants_csv=None, callback=None,
                coverage_summary_csv=None, json=None):
     """aligned.csv -> nucleotide, amino-acid, insertion, consensus (and the
     optional failure, variant and coverage) reports; every argument is an
-    open file except json, a project-file path (None: the default).  In a
-    sharded job rank 0 computes and writes while the other ranks wait
-    (session.writer_stage)."""
-    with session.writer_stage(nuc_csv, amino_csv, coord_ins_csv, conseq_csv, failed_align_csv,
-                              nuc_variants_csv, coverage_summary_csv) as stage:
-        if stage.active:
-            _aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv,
-                        failed_align_csv, nuc_variants_csv, callback, coverage_summary_csv, json)
+    open file except json, a project-file path (None: the default).
+
+    In a sharded job the counting is split: every rank counts the rows in
+    its share of aligned.csv and the ranks add their counters up
+    (_load_sharded); every rank then builds the same reports from the
+    job's counters, and rank 0 writes them (session.writer_stage).  The
+    insertion strings are counted the same way (InsertionWriter.write).
+    When aligned.csv cannot be split (not a plain file on every rank, '\r'
+    or quoted fields), rank 0 computes alone while the others wait."""
+    global _SHARD
+    sh = session.shard()
+    SHARD_STATS.clear()
+    handles = (nuc_csv, amino_csv, coord_ins_csv, conseq_csv, failed_align_csv, nuc_variants_csv,
+               coverage_summary_csv)
+    with session.writer_stage(*handles) as stage:
+        groups = _load_sharded(sh, aligned_csv) if sh is not None else None
+        if groups is None:
+            if stage.active:
+                _aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv,
+                            failed_align_csv, nuc_variants_csv, callback, coverage_summary_csv, json)
+            return
+        # every rank builds the reports; the others' go nowhere
+        outs = handles if stage.active else tuple(None if h is None else io.StringIO() for h in handles)
+        _SHARD = sh
+        try:
+            _aln2counts(aligned_csv, outs[0], outs[1], outs[2], outs[3], outs[4], outs[5],
+                        callback if stage.active else None, outs[6], json, groups=groups)
+        finally:
+            _SHARD = None
+
+
+def _load_sharded(sh, aligned_csv):
+    """This rank's share of aligned.csv counted into the job's groups, the
+    counters added up over the ranks: the number of (refname, qcut) groups,
+    or None (on every rank) when the file is not split."""
+    from .sharded_io import _agree_ok, _checked
+    ctx = session.context()
+    fd = session.readable_fd(aligned_csv)
+    if not _agree_ok(sh, fd is not None):
+        return None
+    part = _checked(sh, lambda: ctx.a2c_part_open(SLOT_REPORT, fd, sh.rank, sh.world, _CODON_CHARS))
+    if not _agree_ok(sh, part is not None):
+        return None
+    aligned_csv.seek(0, 2)    # consumed, as the reference's DictReader leaves it
+    keys, rows, ncod, total = ctx.a2c_part_groups(SLOT_REPORT, part['groups'])
+    all_keys = sh.all_gather_bytes(keys)
+    all_meta = sh.all_gather_bytes(np.concatenate([rows, ncod.reshape(-1), total]).astype(np.int64).tobytes())
+    # the job's groups: runs of equal keys in rank order (a run can go on
+    # across the ranks' cuts)
+    g_keys, g_ncod, g_total, g_rows = [], [], [], []
+    mine_gid, mine_base = [], []
+    for r in range(sh.world):
+        ks = all_keys[r].split(b'\n')[:-1] if all_keys[r] else []
+        meta = np.frombuffer(all_meta[r], dtype=np.int64)
+        n = len(ks)
+        rr, nc, tt = meta[:n], meta[n:4 * n].reshape(n, 3), meta[4 * n:5 * n]
+        for k in range(n):
+            if k == 0 and g_keys and g_keys[-1] == ks[k]:
+                g = len(g_keys) - 1
+                g_ncod[g] = np.maximum(g_ncod[g], nc[k])
+            else:
+                g = len(g_keys)
+                g_keys.append(ks[k])
+                g_ncod.append(nc[k].copy())
+                g_total.append(0)
+                g_rows.append(0)
+            if r == sh.rank:
+                mine_gid.append(g)
+                mine_base.append(g_rows[g])
+            g_total[g] += int(tt[k])
+            g_rows[g] += int(rr[k])
+    for g, t in enumerate(g_total):
+        if t > 0xffffffff:
+            raise _native.NativeError('aln2counts: the counts of group %d add up to more than 2**32-1' % g)
+    cells = ctx.a2c_part_count(SLOT_REPORT, b''.join(k + b'\n' for k in g_keys), mine_gid,
+                               np.array(g_ncod, dtype=np.int32).reshape(-1, 3), mine_base)
+    cnt, first = ctx.a2c_part_counters(SLOT_REPORT, cells)
+    total_cnt = sh.sum_i64(cnt.astype(np.int64))
+    first64 = np.where(first == np.uint32(0xffffffff), -1, first.astype(np.int64))
+    least = sh.min_i64(first64)
+    ctx.a2c_part_counters(SLOT_REPORT, cells, (total_cnt.astype(np.uint32),
+                                               np.where(least < 0, 0xffffffff, least).astype(np.uint32)))
+    SHARD_STATS.update(mode='sharded', rows=part['rows'], bytes=part['bytes'])
+    return len(g_keys)
 
 
 def _aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv, failed_align_csv,
-                nuc_variants_csv, callback, coverage_summary_csv, json):
+                nuc_variants_csv, callback, coverage_summary_csv, json, groups=None):
     projects = (project_config.ProjectConfig.loadDefault() if json is None
                 else project_config.ProjectConfig.loadCustom(json))
     report = SequenceReport(InsertionWriter(coord_ins_csv), projects, CONSEQ_MIXTURE_CUTOFFS)
@@ -762,14 +852,14 @@ def _aln2counts(aligned_csv, nuc_csv, amino_csv, coord_ins_csv, conseq_csv, fail
     if source:
         report.enable_callback(callback, os.stat(source).st_size)
     ctx = session.context()
-    fd = session.readable_fd(aligned_csv)
-    groups = None
-    if fd is not None:   # the file mmap'd by the library (no '\r' in it)
-        groups = ctx.a2c_load_file(SLOT_REPORT, fd, _CODON_CHARS)
-        if groups is not None:
-            aligned_csv.seek(0, 2)
-    if groups is None:
-        groups = ctx.a2c_load_csv(SLOT_REPORT, session.read_text(aligned_csv), _CODON_CHARS)
+    if groups is None:           # not loaded by the ranks of a sharded job
+        fd = session.readable_fd(aligned_csv)
+        if fd is not None:   # the file mmap'd by the library (no '\r' in it)
+            groups = ctx.a2c_load_file(SLOT_REPORT, fd, _CODON_CHARS)
+            if groups is not None:
+                aligned_csv.seek(0, 2)
+        if groups is None:
+            groups = ctx.a2c_load_csv(SLOT_REPORT, session.read_text(aligned_csv), _CODON_CHARS)
     for g in range(groups):
         report._read_group(ctx, SLOT_REPORT, g)
         for step in per_run:
