@@ -385,6 +385,63 @@ int mh_sam2aln_stats(mh_ctx *ctx, int64_t *out4);
  * outputs (0 until formatted). */
 int mh_sam2aln_timing(mh_ctx *ctx, double *ms5);
 
+/* ---- sam2aln split over the ranks of a job (same reference call,
+ * sam2aln.py:395-478; the bytes move between ranks through the caller's
+ * collectives, torch.distributed in sam2aln._sam2aln_sharded).  Rank `part`
+ * of `parts`:
+ *   mh_sam2aln_part       parses its share of remap.csv (fd, mmap'd): the
+ *                         record at or after byte part/parts of the body, a
+ *                         cut between the two rows of one qname moved past
+ *                         the second, and merges its pairs on its device.
+ *                         0, or 1 = not split (a line with an odd number of
+ *                         '"', no qname column, '\r' in the file: every rank
+ *                         gets 1 and the caller runs mh_sam2aln_file on one).
+ *                         info[0..5] = units, pair units, reference names,
+ *                         distinct merged sequences, share bytes, file bytes.
+ *   mh_sam2aln_part_units qname hash (n = info[0]) and leftover flag per
+ *                         unit: the caller checks that no leftover qname
+ *                         has rows on two ranks (matchmaker, :291-312, pairs
+ *                         across the whole file), else falls back.
+ *   mh_sam2aln_part_names this rank's reference names ('\n' after each) and
+ *                         the first unit of each; _set_names gives each its
+ *                         job-wide id (the names in first-appearance order,
+ *                         the order of groups in aligned.csv, :449-478).
+ *   mh_sam2aln_records    step 0: distinct sequences as records, one buffer
+ *                         per owner rank (hash % parts), sizes[parts];
+ *                         step 1: up to per_name evenly spaced records of
+ *                         every name of the owner's merged order, sizes[1];
+ *                         step 2 (after mh_sam2aln_splitters): the owner's
+ *                         records to the rank of their range, sizes[parts].
+ *                         *data = the concatenated buffers (valid until the
+ *                         next call on ctx).
+ *   mh_sam2aln_records_merge  stage 0: the records every rank sent this
+ *                         owner, equal ones added up (:446-452), sorted as
+ *                         aligned.csv lists them (:466-470); stage 1: the
+ *                         records of this rank's ranges, sorted.
+ *   mh_sam2aln_splitters  all ranks' samples -> the splitters of each name.
+ *   mh_sam2aln_range_counts   rows of this rank's range per job-wide name.
+ *   mh_sam2aln_range_text aligned.csv rows of this rank's range (:471-478),
+ *                         one segment per name, row numbers ("rank" column)
+ *                         from base[name] (the rows of ranks before it).
+ *   mh_sam2aln_part_text  insert.csv (which 1) / failed.csv (which 2) rows
+ *                         of this rank's pair units (seg 0) or leftover
+ *                         units (seg 1), with the header when head != 0; the
+ *                         caller writes segments segment-major by rank. */
+int mh_sam2aln_part(mh_ctx *ctx, int fd, int part, int parts, int q_cutoff, double max_prop_n,
+                    int64_t *info);
+int mh_sam2aln_part_units(mh_ctx *ctx, uint64_t *qhash, uint8_t *leftover);
+int mh_sam2aln_part_names(mh_ctx *ctx, char *buf, size_t cap, size_t *used, int64_t *first_unit);
+int mh_sam2aln_part_set_names(mh_ctx *ctx, const int32_t *gid, int n);
+int mh_sam2aln_records(mh_ctx *ctx, int step, int parts, int per_name, int64_t *sizes,
+                       const uint8_t **data);
+int mh_sam2aln_records_merge(mh_ctx *ctx, int stage, const uint8_t *data, int64_t len);
+int mh_sam2aln_splitters(mh_ctx *ctx, const uint8_t *data, int64_t len, int parts);
+int mh_sam2aln_range_counts(mh_ctx *ctx, int n_names, int64_t *counts);
+int mh_sam2aln_range_text(mh_ctx *ctx, int n_names, const char *const *names, const int64_t *base,
+                          int64_t *seg_bytes, const uint8_t **data);
+int mh_sam2aln_part_text(mh_ctx *ctx, int which, int seg, int head, int64_t *bytes,
+                         const uint8_t **data);
+
 /* ---- censor: replaces censor_fastq.censor (censor_fastq.py:32-102) ---- */
 /* One FASTQ file (src, gzip when src_gzip) censored on the device: bases /
  * qualities at the bad (tile, cycle) pairs (tiles[k], cycles[k]; negative
@@ -474,6 +531,44 @@ int mh_a2c_insert_rows(mh_ctx *ctx, int slot, const char *lead, int n_ranges, co
 /* Host wall ms: [0] parse of the last load, [1] its upload + k_a2c_count +
  * fetch, [2] mh_a2c_inserts since the last call of this function. */
 int mh_a2c_timing(mh_ctx *ctx, int slot, double *ms3);
+
+/* ---- aln2counts counting split over the ranks of a job (the same
+ * aln2counts.py:115-172 loops; the counters are sums and a first row is a
+ * minimum, so each rank counts its share and the caller reduces them) ----
+ *   mh_a2c_part_open     rank `part` of `parts` parses the rows of its share
+ *                        of aligned.csv (fd, mmap'd; cuts at line starts).
+ *                        0, or 1 = not split (a quoted field in the share or
+ *                        '\r' in the file: the caller loads it whole).
+ *                        info3 = rows, local groups, share bytes.
+ *   mh_a2c_part_groups   its runs of (refname, qcut): keys "refname\x1fqcut\n"
+ *                        each (keys NULL: *used only), rows, the codon
+ *                        extent of frames 0..2 (ncod3[3 g + f]) and the
+ *                        summed count of each.
+ *   mh_a2c_part_count    the job's groups (n_groups keys as above, the codon
+ *                        extents the maximum over ranks), gid[k] = the job
+ *                        group of local run k (increasing), row_base[k] = rows
+ *                        of that group on the ranks before; counts on the
+ *                        device.  *cells = counter cells (aa + nuc, all
+ *                        groups and frames), as mh_a2c_counts lays them out.
+ *   mh_a2c_part_counters set 0: copies the cells' counts and first rows out;
+ *                        set 1: takes the reduced ones (counts summed, first
+ *                        rows the minimum) back, after which mh_a2c_group /
+ *                        mh_a2c_counts read the job's counters.
+ *   mh_a2c_insert_export the entries of the last mh_a2c_inserts as bytes
+ *                        (buf NULL: *used only);
+ *   mh_a2c_insert_merge  every rank's exports of one call concatenated:
+ *                        equal (range, string) added up, first row the least,
+ *                        in (range, first row) order (InsertionWriter.write,
+ *                        :779-795), for mh_a2c_insert_entries / _rows. */
+int mh_a2c_part_open(mh_ctx *ctx, int slot, int fd, int part, int parts, const char *codon_chars,
+                     int64_t *info3);
+int mh_a2c_part_groups(mh_ctx *ctx, int slot, char *keys, size_t cap, size_t *used, int64_t *rows,
+                       int32_t *ncod3, int64_t *total);
+int mh_a2c_part_count(mh_ctx *ctx, int slot, int64_t n_groups, const char *keys, const int64_t *gid,
+                      const int32_t *ncod3, const int64_t *row_base, int64_t *cells);
+int mh_a2c_part_counters(mh_ctx *ctx, int slot, int set, uint32_t *cnt, uint32_t *first);
+int mh_a2c_insert_export(mh_ctx *ctx, int slot, uint8_t *buf, size_t cap, size_t *used);
+int mh_a2c_insert_merge(mh_ctx *ctx, int slot, const uint8_t *buf, int64_t len, int64_t *n_entries);
 
 /* ---- Gotoh: replaces _gotoh2.align (_gotoh2.c:544-607) ---------------- */
 /* seq1/seq2 already cleaned (gotoh2.py:70-72).  out1/out2 need
