@@ -296,6 +296,10 @@ static inline int imax(int a, int b) { return a > b ? a : b; }
 
 enum { FAIL_NONE = 0, FAIL_SCORE = 1, FAIL_NCEIL = 2, FAIL_OTHER = 3 };
 
+#ifdef OG_ROW_PROBE
+void og_row_probe(int W, const int *H1, const int *H, int oeD, int exD);
+#endif
+
 static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *rd,
                       const uint8_t *qv, int m, const cand_t *cd, uint8_t *bits,
                       uint8_t *ops, caln_t *out)
@@ -352,6 +356,10 @@ static void dp_extend(const og_index *ix, const og_params *par, const uint8_t *r
             bits[(size_t)i * OG_BAND + k] = (uint8_t)(src | (eb[k] << 2) | (fb << 3));
             if ((local || i == m - 1) && H[k] > best) { best = H[k]; bi = i; bk = k; }
         }
+#ifdef OG_ROW_PROBE
+        /* diagnostics build only (profiles/diag/lazy_f_probe.py) */
+        if (gap_ok) og_row_probe(W, H1, H, oeD, exD);
+#endif
         memcpy(Hp, H, sizeof(Hp));
         memcpy(Ep, E, sizeof(Ep));
     }
