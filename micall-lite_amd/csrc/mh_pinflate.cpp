@@ -669,9 +669,13 @@ int gunzip_single_parallel(const uint8_t *src, int64_t len, Buf &out, int thread
     const int64_t dend = len - 8;             // the deflate stream ends before the trailer
     const uint32_t crc_want = rd32(src + len - 8), isize = rd32(src + len - 4);
     // the two decodes of every span and the text are held at once (about
-    // 3x the text): leave this to the serial inflate when memory is short
+    // 3x the text; a span of FASTQ stays window-dependent nearly to its end,
+    // 63.0 of 63.0 MB in a C2-like file, so plane 2 cannot be cut short):
+    // leave this to the serial inflate when memory is short.  The trailer's
+    // size is mod 2^32; FASTQ inflates about 4x, so that bounds it too.
     const int64_t avail = mem_available();
-    if (avail >= 0 && 3 * (int64_t)isize > avail / 2) return -1;
+    const int64_t text = std::max<int64_t>((int64_t)isize, 4 * (dend - d0));
+    if (avail >= 0 && 3 * text > avail / 2) return -1;
     const int64_t span_min = span_min_bytes();
     const int T = (int)std::min<int64_t>(threads, (dend - d0) / span_min);
     if (T < 2) return -1;
