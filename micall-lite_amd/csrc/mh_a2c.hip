@@ -188,6 +188,8 @@ __global__ __launch_bounds__(256) void k_a2c_count(A2CCountArgs A)
 struct A2CInsArgs {
     const uint8_t *text;
     const A2CRow *rows;      // the rows of one group
+    uint32_t row0;           // rows[0].local: a first-row number minus row0 indexes rows
+                             // (a rank's part of a group starts at the ranks before's rows)
     const int8_t *code;
     const uint8_t *cls;
     const int32_t *left, *right;
@@ -293,7 +295,7 @@ __global__ __launch_bounds__(256) void k_a2c_ins_verify(A2CInsArgs A)
     if (!h) return;
     const int rg = (int)(p / A.n_rows);
     const int64_t s = a2c_find(A, h);
-    const A2CRow R = A.rows[p % A.n_rows], F = A.rows[A.tfirst[s]];
+    const A2CRow R = A.rows[p % A.n_rows], F = A.rows[A.tfirst[s] - A.row0];
     int lo = 0, n = 0, flo = 0, fn = 0;
     bool same = A.trange[s] == rg && a2c_slice(A, R, rg, lo, n) && a2c_slice(A, F, rg, flo, fn) &&
                 n == fn;
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(256) void k_a2c_ins_compact(A2CInsArgs A)
     e.first = A.tfirst[s];
     e.count = A.tcnt[s];
     int lo = 0, n = 0;
-    a2c_slice(A, A.rows[e.first], e.range, lo, n);
+    a2c_slice(A, A.rows[e.first - A.row0], e.range, lo, n);
     e.lo = lo;
     e.n_codons = n;
     A.entries[atomicAdd(&A.ctr[2], 1ull)] = e;
@@ -326,7 +328,7 @@ __global__ __launch_bounds__(256) void k_a2c_ins_gather(A2CInsArgs A, const A2CE
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= n_ent) return;
     const A2CEntry e = ent[k];
-    const uint8_t *s = A.text + A.rows[e.first].soff;
+    const uint8_t *s = A.text + A.rows[e.first - A.row0].soff;
     char *o = out + eoff[k];
     for (int c = 0; c < e.n_codons; ++c) o[c] = c_a2c_codes[a2c_codon(A, s, e.lo + 3 * c)];
     o[e.n_codons] = '\n';
@@ -966,6 +968,7 @@ extern "C" int mh_a2c_inserts(mh_ctx *ctx, int slot, int64_t g, int frame, int n
     if (e != hipSuccess) { fail(e, "mh_a2c_inserts alloc"); goto done; }
     a.text = S.d_text;
     a.rows = S.d_rows + S.g_first[g];
+    a.row0 = S.rows[(size_t)S.g_first[g]].local;
     a.code = S.d_code;
     a.cls = S.d_cls;
     a.left = d_lr;

@@ -715,7 +715,8 @@ class InsertionWriter(object):
         if _SHARD is not None and slot == SLOT_REPORT:
             # every rank's strings over its own rows, added up (the first
             # rows are the job's row numbers within the group)
-            mine = ctx.a2c_inserts_local(slot, g, reading_frame, lefts, rights)
+            from .sharded_io import _checked
+            mine = _checked(_SHARD, lambda: ctx.a2c_inserts_local(slot, g, reading_frame, lefts, rights))
             text = ctx.a2c_inserts_merged_text(slot, b''.join(_SHARD.all_gather_bytes(mine)), lefts,
                                                lead.getvalue(), targets, os.linesep)
         else:

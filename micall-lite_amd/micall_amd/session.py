@@ -22,6 +22,7 @@ the order a single GPU writes them (sharded_io.py).  The small reports
 truncate what another rank wrote.
 """
 import os
+import sys
 import time
 
 from . import _native
@@ -151,6 +152,13 @@ class writer_stage:
                 if flush is not None and not getattr(h, 'closed', False):
                     flush()
         if self.sh is not None:
+            if exc_type is not None:
+                # shown here: a rank that fails between the stage's
+                # collectives leaves the others waiting in one of them
+                import traceback
+                sys.stderr.write('rank {}: the stage failed\n{}'.format(
+                    self.sh.rank, ''.join(traceback.format_exception(exc_type, exc, tb))))
+                sys.stderr.flush()
             failed = int(self.sh.sum_i64([1 if exc_type is not None else 0])[0])
             if failed and exc_type is None:
                 raise RuntimeError('the stage failed on rank 0 of the sharded job')

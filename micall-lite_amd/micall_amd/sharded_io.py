@@ -54,7 +54,7 @@ def _checked(sh, fn):
     if not _agree_ok(sh, err is None):
         if err is not None:
             raise err
-        raise _native.NativeError('a FASTQ read failed on another rank of the job')
+        raise _native.NativeError('the call failed on another rank of the job')
     return out
 
 

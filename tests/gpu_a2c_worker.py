@@ -11,6 +11,7 @@ import io
 import json
 import os
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, 'micall-lite_amd'))
@@ -21,9 +22,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--cases', required=True)
     args = ap.parse_args()
+    if os.environ.get('MICALL_TEST_STACKS') == '1':
+        import faulthandler
+        faulthandler.dump_traceback_later(60, repeat=True)
     from micall_amd import aln2counts as a2c
     from micall_amd import session
     sh = session.shard()
+    t0 = time.time()
     stats = {}
     for case in sorted(os.listdir(args.cases)):
         d = os.path.join(args.cases, case)
@@ -47,6 +52,7 @@ def main():
         for h in handles.values():
             h.close()
         stats[case] = dict(a2c.SHARD_STATS)
+        print('rank %d %s %.1f s' % (sh.rank, case, time.time() - t0), file=sys.stderr, flush=True)
     with open(os.path.join(args.cases, 'rank%d.json' % sh.rank), 'w') as f:
         json.dump(stats, f)
     import torch.distributed as dist
