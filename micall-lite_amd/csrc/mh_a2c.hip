@@ -111,8 +111,9 @@ struct A2CState {
     std::unordered_map<const void *, size_t> dcap;   // bytes behind each device pointer (grow-only)
     double t_parse = 0, t_count = 0, t_ins = 0;
     // a part of aligned.csv held between mh_a2c_part_open and _count (mapped)
-    const char *part_text = nullptr;
+    const char *part_text = nullptr;          // (null for an empty file)
     size_t part_len = 0;
+    bool part_open = false;                   // mh_a2c_part_open done, not counted yet
     int64_t part_b0 = 0, part_b1 = 0;         // the part's bytes of the text
     std::vector<int64_t> part_first;          // local groups' first rows (+ end)
 };
@@ -777,6 +778,7 @@ extern "C" int mh_a2c_load_csv(mh_ctx *ctx, int slot, const char *text, int64_t 
     if (S.part_text) {       // a part left open by a sharded load that fell back
         unmap_text_file(S.part_text, S.part_len);
         S.part_text = nullptr;
+        S.part_open = false;
     }
     auto t0 = std::chrono::steady_clock::now();
     if (int st = a2c_tables(S, codon_chars)) return st;
@@ -1167,6 +1169,7 @@ extern "C" int mh_a2c_part_open(mh_ctx *ctx, int slot, int fd, int part, int par
     A2CState &S = *a2c_state(c, slot);
     a2c_clear_inserts(S);
     if (S.part_text) { unmap_text_file(S.part_text, S.part_len); S.part_text = nullptr; }
+    S.part_open = false;
     if (int st = a2c_tables(S, codon_chars)) return st;
     const char *text = nullptr;
     size_t len = 0;
@@ -1197,6 +1200,7 @@ extern "C" int mh_a2c_part_open(mh_ctx *ctx, int slot, int fd, int part, int par
     }
     S.part_text = text;
     S.part_len = len;
+    S.part_open = true;
     S.part_b0 = b0;
     S.part_b1 = b1;
     S.part_first = S.g_first;
@@ -1254,7 +1258,7 @@ extern "C" int mh_a2c_part_count(mh_ctx *ctx, int slot, int64_t n_groups, const 
     Ctx &c = *ctx_of(ctx);
     MH_HIP(hipSetDevice(c.device));
     A2CState &S = *a2c_state(c, slot);
-    if (!S.part_text) { set_error("mh_a2c_part_count: no part open"); return -3; }
+    if (!S.part_open) { set_error("mh_a2c_part_count: no part open"); return -3; }
     const int64_t nl = (int64_t)S.part_first.size() - 1;
     if (nl && (!gid || !row_base)) return -3;
     for (int64_t k = 0; k < nl; ++k)
@@ -1304,6 +1308,7 @@ extern "C" int mh_a2c_part_count(mh_ctx *ctx, int slot, int64_t n_groups, const 
     unmap_text_file(S.part_text, S.part_len);
     S.part_text = nullptr;
     S.part_len = 0;
+    S.part_open = false;
     if (st) {
         S.rows.clear();
         S.g_first.assign(1, 0);
