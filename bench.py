@@ -564,13 +564,31 @@ def end_to_end(n_pairs, workdir, single_member=False, job=None):
     return out
 
 
+def latest_profile(*parts):
+    """The newest committed round's copy of a profile summary
+    (profiles/rNN/...), or None."""
+    base = os.path.join(REPO, 'profiles')
+    try:
+        rounds = sorted((d for d in os.listdir(base) if len(d) == 3 and d[0] == 'r' and d[1:].isdigit()),
+                        reverse=True)
+    except OSError:
+        return None
+    for d in rounds:
+        path = os.path.join(base, d, *parts)
+        if os.path.exists(path):
+            return path
+    return None
+
+
 def read_pmc_traffic(kernel, pairs, stage='remap'):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC
     summary of this stage (separate --pmc passes, FETCH_SIZE doubled per the
     gfx950 rule; profiles/collect_pmc_stages.sh), when it was measured on the
     same per-GPU pair count."""
     if stage == 'remap':
-        path = os.path.join(REPO, 'profiles', 'r04', 'c2', 'pmc_traffic.json')
+        path = latest_profile('c2', 'pmc_traffic.json')
+        if path is None:
+            return None
     else:
         path = os.path.join(REPO, 'profiles', 'pmc_traffic_{}.json'.format(stage))
     try:
@@ -590,11 +608,13 @@ VALU_ISSUE_CYCLES = 2      # MI355X_MICROARCH.md: a wave64 VALU instruction issu
 def read_valu_issue(kernel, pairs, avg_launch_ms):
     """Issue-side roofline of `kernel` (it is bound by integer VALU issue and
     its dependency chain, not HBM): VALU wave-instructions per launch from the
-    committed SQ_INSTS_VALU pass (profiles/r04/c2/sq_issue.json, same
+    committed SQ_INSTS_VALU pass (profiles/rNN/c2/sq_issue.json, the newest; same
     per-GPU pair count; the mate-rescue DP launch, the one after k_rescue, is
     left out), over this run's average launch time, against 1024 SIMDs x the
     measured clock / VALU_ISSUE_CYCLES."""
-    path = os.path.join(REPO, 'profiles', 'r04', 'c2', 'sq_issue.json')
+    path = latest_profile('c2', 'sq_issue.json')
+    if path is None:
+        return None
     try:
         with open(path) as f:
             every = json.load(f)['dispatches']
@@ -608,7 +628,7 @@ def read_valu_issue(kernel, pairs, avg_launch_ms):
         peak = 1024 * clk / VALU_ISSUE_CYCLES
         return {'unit': 'G wave-instr/s', 'valu_insts_per_launch': insts, 'achieved': round(achieved, 1),
                 'peak': round(peak, 1), 'frac': round(achieved / peak, 4), 'clock_ghz': round(clk, 3),
-                'source': 'profiles/r04/c2/sq_issue.json (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)'}
+                'source': os.path.relpath(path, REPO) + ' (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)'}
     except (OSError, KeyError, ValueError):
         return None
 
