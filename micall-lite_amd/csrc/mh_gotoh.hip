@@ -55,6 +55,8 @@ constexpr size_t TB_LDS = (size_t)TB * TB + 2 * TB;   // window + both sequences
 
 __host__ __device__ inline size_t gotoh_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+typedef unsigned int g4u __attribute__((ext_vector_type(4)));
+
 struct GotohArgs {
     const int8_t *a;      // seq1 codes, m
     const int8_t *b;      // seq2 codes, n
@@ -341,8 +343,29 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
     int Rdg = G_HUGE;
     int abcp = 0;                             // abc of (i, j - 1), stored this step
     int pR = 0, pP = 0;                       // lanes 32..63: lane 63's R, P at the block's steps
+    // !PL: a block's 32 profile bytes of this lane come from 9 aligned dwords
+    // loaded one block ahead through a buffer resource and realigned once per
+    // block (a byte load per step was a FLAT load, and its wait, vmcnt(0),
+    // also waited for every plane store before it)
+    const __amdgpu_buffer_rsrc_t rprof = brsrc(PL ? nullptr : (const void *)uni(A.prof),
+                                               PL ? 0u : (uint32_t)(L * PW));
+    const uint32_t pa = (uint32_t)prow & ~3u, psh = (uint32_t)prow & 3u;
+    g4u nx0 = {0, 0, 0, 0}, nx1 = {0, 0, 0, 0};
+    uint32_t nx2 = 0;
+    auto prof_fetch = [&](int tb) {
+        nx0 = __builtin_amdgcn_raw_buffer_load_b128(rprof, pa + (uint32_t)tb, 0, 0);
+        nx1 = __builtin_amdgcn_raw_buffer_load_b128(rprof, pa + (uint32_t)tb + 16u, 0, 0);
+        nx2 = __builtin_amdgcn_raw_buffer_load_b32(rprof, pa + (uint32_t)tb + 32u, 0, 0);
+    };
+    if (!PL) prof_fetch(0);
     for (int t0 = 0; t0 <= n + 64; t0 += GBLK) {
         stamp(S, 0, u, t0 / GBLK, 0);
+        uint32_t pb[8];                           // !PL: profile bytes t0 .. t0 + 31 of this lane
+        if (!PL) {
+            const uint32_t c[9] = {nx0.x, nx0.y, nx0.z, nx0.w, nx1.x, nx1.y, nx1.z, nx1.w, nx2};
+            for (int x = 0; x < 8; ++x) pb[x] = __builtin_amdgcn_alignbyte(c[x + 1], c[x], psh);
+            if (t0 + GBLK <= n + 64) prof_fetch(t0 + GBLK);
+        }
         int aR = 0, aP = G_INF;
         if (consume && t0 <= n) {
             // this block of the row above: poll its cells until they carry
@@ -372,12 +395,18 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
         const int j0 = t0 - lane;
         // LEFT: a lane may be at column 0; RIGHT: at column n or past it
         // PRED: a lane's column may lie off the grid (its store is dropped)
-        auto step = [&](auto leftc, auto rightc, auto tlc, auto predc, int q) {
+        // the score of step q: q a constant (the unrolled blocks) from the
+        // realigned dwords, else (short rows) a load
+        auto score = [&](auto qc) {
+            constexpr int Q = decltype(qc)::value;
+            if constexpr (PL) return (int)prof[pbase + Q];
+            else return (int)__builtin_amdgcn_sbfe(pb[Q >> 2], 8u * (Q & 3), 8u);
+        };
+        auto step = [&](auto leftc, auto rightc, auto tlc, auto predc, int q, int sc) {
             constexpr bool LEFT = decltype(leftc)::value, RIGHT = decltype(rightc)::value;
             constexpr bool TL = decltype(tlc)::value, PRED = LEFT || RIGHT || decltype(predc)::value;
             const int j = j0 + q;
             const int2 bd = brd[q];
-            const int sc = prof[pbase + q];
             const int Rup = __builtin_amdgcn_update_dpp(bd.x, Rme, 0x138, 0xF, 0xF, false);
             const int Pup = __builtin_amdgcn_update_dpp(bd.y, Pme, 0x138, 0xF, 0xF, false);
             const int dg = Rdg - sc;
@@ -433,22 +462,22 @@ __global__ __launch_bounds__(64) void k_gotoh_fwd(GotohStrips S)
         constexpr std::false_type N{};
         if (right && left) {   // n < 64 + GBLK - 1: short rows
             if (tl) {
-                for (int q = 0; q < GBLK; ++q) step(Y, Y, Y, N, q);
+                for (int q = 0; q < GBLK; ++q) step(Y, Y, Y, N, q, prof[pbase + q]);
             } else {
-                for (int q = 0; q < GBLK; ++q) step(Y, Y, N, N, q);
+                for (int q = 0; q < GBLK; ++q) step(Y, Y, N, N, q, prof[pbase + q]);
             }
         } else if (right) {
-            if (tl) unroll<GBLK>([&](auto qc) { step(N, Y, Y, N, decltype(qc)::value); });
-            else unroll<GBLK>([&](auto qc) { step(N, Y, N, N, decltype(qc)::value); });
+            if (tl) unroll<GBLK>([&](auto qc) { step(N, Y, Y, N, decltype(qc)::value, score(qc)); });
+            else unroll<GBLK>([&](auto qc) { step(N, Y, N, N, decltype(qc)::value, score(qc)); });
         } else if (left) {
             // a middle strip of a global alignment: column 0 comes out of
             // the huge start values, only the stores test their column
-            if (tl) unroll<GBLK>([&](auto qc) { step(Y, N, Y, N, decltype(qc)::value); });
-            else if (glob) unroll<GBLK>([&](auto qc) { step(N, N, N, Y, decltype(qc)::value); });
-            else unroll<GBLK>([&](auto qc) { step(Y, N, N, N, decltype(qc)::value); });
+            if (tl) unroll<GBLK>([&](auto qc) { step(Y, N, Y, N, decltype(qc)::value, score(qc)); });
+            else if (glob) unroll<GBLK>([&](auto qc) { step(N, N, N, Y, decltype(qc)::value, score(qc)); });
+            else unroll<GBLK>([&](auto qc) { step(Y, N, N, N, decltype(qc)::value, score(qc)); });
         } else {
-            if (tl) unroll<GBLK>([&](auto qc) { step(N, N, Y, N, decltype(qc)::value); });
-            else unroll<GBLK>([&](auto qc) { step(N, N, N, N, decltype(qc)::value); });
+            if (tl) unroll<GBLK>([&](auto qc) { step(N, N, Y, N, decltype(qc)::value, score(qc)); });
+            else unroll<GBLK>([&](auto qc) { step(N, N, N, N, decltype(qc)::value, score(qc)); });
         }
         // the strip's last row (lane 63 at column t - 63) to the strip below
         const int jp = t0 + lane - (64 - GBLK) - 63;

@@ -38,4 +38,5 @@ for _ in range(steps):
 ctx.sync()
 pr.disable()
 st = pstats.Stats(pr)
-st.sort_stats('tottime').print_stats(30)
+st.sort_stats('tottime').print_stats(40)
+st.sort_stats('cumulative').print_stats(60)

@@ -413,6 +413,27 @@ def test_gotoh_pol_sized(ctx):
 
 
 @pytest.mark.parametrize('is_global', [True, False])
+def test_gotoh_profile_in_global_memory(ctx, is_global):
+    """A batch whose longest seq2 makes the score profile too large for LDS
+    (5 x 14k bytes > 64 KiB: k_gotoh_fwd<false> streams each lane's profile
+    bytes from global memory, realigned per block of 32 columns) holding
+    pairs of every block kind -- long rows, rows shorter than one block,
+    seq1 shorter than a strip -- all equal to the oracle."""
+    rng = np.random.default_rng(23)
+    mat, alpha = [5, -4, -4, -4, 0, -4, 5, -4, -4, 0, -4, -4, 5, -4, 0, -4, -4, -4, 5, 0,
+                  0, 0, 0, 0, 0], 'ACGT?'
+    rand = lambda k: ''.join(rng.choice(list('ACGT'), size=k))
+    long2 = ''.join(synth.sample_genome(POL, rng, 0.05, 0.01).tobytes().decode() for _ in range(5))[:14000]
+    pairs = [(long2[2000:2700], long2),                          # 700 x 14,000
+             (POL[:130], long2[:90]),                            # n < one block past the skew
+             (rand(40), long2[5000:5450]),                       # m < one strip
+             (long2[9000:9300] + rand(20), long2[8900:13950])]
+    got = ctx.gotoh_align_many(pairs, 15, 3, is_global, alpha, mat)
+    for (a, b), g in zip(pairs, got):
+        assert g == oracle.gotoh_align(a, b, 15, 3, is_global, alpha, mat)
+
+
+@pytest.mark.parametrize('is_global', [True, False])
 def test_gotoh_long_seq1_global_memory_variant(ctx, is_global):
     """seq1 too long for the rolling diagonals in LDS (k_gotoh<false>: they
     stay in global memory), in a batch with a short pair, and a batch of
