@@ -75,13 +75,13 @@ struct GotohArgs {
     int *result;                  // [0] status, [1] score, [2] length
 };
 
-// the strips of a batch, in ticket order (alignment-major, the alignments
-// longest critical path first)
+// the strips of a batch in ticket order: tick[u] = (alignment, the strip's
+// index in the pass's dependency order), longest remaining critical path
+// first (see mh_gotoh_align_batch)
 struct GotohStrips {
     const GotohArgs *args;
-    const int *first;             // per rank: the first ticket of that alignment; [count] = total
-    const int *order;             // per rank: the alignment (index into args)
-    int count;
+    const int2 *tick;
+    int strips;
     int *ticket;                  // [0] fwd, [1] bwd
     // diagnostics (MH_GOTOH_STAMPS=path, else null): per ticket and block,
     // the shader clock before and after the block's wait, fwd then bwd
@@ -98,7 +98,7 @@ __device__ __forceinline__ void stamp(const GotohStrips &S, int pass, int u, int
     if (S.stamps == nullptr || blk >= S.stamp_blocks) return;
     const unsigned long long now = clock64();
     if (threadIdx.x == 0)
-        S.stamps[(((size_t)pass * S.first[S.count] + u) * S.stamp_blocks + blk) * 2 + which] = now;
+        S.stamps[(((size_t)pass * S.strips + u) * S.stamp_blocks + blk) * 2 + which] = now;
 }
 
 __device__ __forceinline__ int gmin(int x, int y) { return x <= y ? x : y; }
@@ -187,16 +187,12 @@ __device__ __forceinline__ void dev_store(T *p, T v)
     __hip_atomic_store((__attribute__((address_space(1))) T *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// the strip of ticket u: (alignment, index in ticket order)
+// the strip of ticket u: (alignment, index in the pass's dependency order)
 __device__ __forceinline__ void strip_of(const GotohStrips &S, int u, int &t, int &q)
 {
-    int lo = 0, hi = S.count;   // first[lo] <= u < first[hi]
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (S.first[mid] <= u) lo = mid; else hi = mid;
-    }
-    t = S.order[lo];
-    q = u - S.first[lo];
+    const int2 x = S.tick[u];
+    t = __builtin_amdgcn_readfirstlane(x.x);
+    q = __builtin_amdgcn_readfirstlane(x.y);
 }
 
 // A boundary cell of the forward pass as one 64-bit word written by one
@@ -778,21 +774,35 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
         }
         work[t + 1] = work[t] + gotoh_work_bytes(ms[t], ns[t]);
     }
-    // strips in ticket order: every alignment's, alignment by alignment, the
-    // longest critical path first (an alignment takes about (n + m) / 32
-    // blocks of steps: n columns, plus two blocks of lag per strip of 64
-    // rows), so the few long ones start at once and the many short ones fill
-    // the GPU around them instead of leaving the long ones to run alone at
-    // the end
-    std::vector<int> order(count);
-    for (int t = 0; t < count; ++t) order[t] = t;
-    std::stable_sort(order.begin(), order.end(),
-                     [&](int x, int y) { return ms[x] + ns[x] > ms[y] + ns[y]; });
-    std::vector<int> first(count + 1, 0);
-    for (int r = 0; r < count; ++r) first[r + 1] = first[r] + (ms[order[r]] + 1 + 63) / 64;
+    // strips in ticket order, the longest remaining critical path first:
+    // strip q of an alignment (q-th in its pass's dependency order) still has
+    // (strips - 1 - q) strips after it, each starting about GLAG steps after
+    // the one before (the 64-lane skew plus a block), and then its own n + 64
+    // steps.  A strip's predecessor always has the longer path, so it holds
+    // a lower ticket (every wait is for a strip already started), and a
+    // resident wave rarely waits: the strips that can run next across all the
+    // alignments are the ones handed out (alignment-major tickets left the
+    // later strips of a long alignment resident and idle, ~half the waves)
+    constexpr int64_t GLAG = 128;
+    std::vector<int2> tick;
+    std::vector<int64_t> key;
+    for (int t = 0; t < count; ++t) {
+        const int nsx = (ms[t] + 1 + 63) / 64;
+        for (int q = 0; q < nsx; ++q) {
+            tick.push_back(make_int2(t, q));
+            key.push_back((int64_t)(nsx - 1 - q) * GLAG + ns[t] + 64);
+        }
+    }
+    {
+        std::vector<int> idx(tick.size());
+        for (size_t x = 0; x < idx.size(); ++x) idx[x] = (int)x;
+        std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return key[(size_t)x] > key[(size_t)y]; });
+        std::vector<int2> sorted(tick.size());
+        for (size_t x = 0; x < idx.size(); ++x) sorted[x] = tick[(size_t)idx[x]];
+        tick.swap(sorted);
+    }
     const size_t sz_mat = align16(sizeof(int) * L * L), sz_args = align16(sizeof(GotohArgs) * count);
-    const size_t sz_order = align16(sizeof(int) * count);
-    const size_t sz_first = align16(sizeof(int) * (count + 1)) + sz_order + 16;   // + order, the two ticket counters
+    const size_t sz_first = align16(sizeof(int2) * tick.size()) + 16;   // the ticket table, the two ticket counters
     // device buffer: [io blocks][matrix][arguments][strip table, tickets][work blocks]
     const size_t off_mat = io[count], off_args = off_mat + sz_mat, off_first = off_args + sz_args,
                  off_work = off_first + sz_first;
@@ -856,16 +866,13 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     MH_HIP(hipMemcpyAsync(d + off_mat, matrix, sizeof(int) * L * L, hipMemcpyHostToDevice, st));
     MH_HIP(hipMemcpyAsync(d + off_args, args.data(), sizeof(GotohArgs) * count,
                           hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(d + off_first, first.data(), sizeof(int) * (count + 1), hipMemcpyHostToDevice, st));
-    const size_t off_order = off_first + align16(sizeof(int) * (count + 1));
-    MH_HIP(hipMemcpyAsync(d + off_order, order.data(), sizeof(int) * count, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(d + off_first, tick.data(), sizeof(int2) * tick.size(), hipMemcpyHostToDevice, st));
+    const int strips = (int)tick.size();
     GotohStrips S;
     S.args = (const GotohArgs *)(d + off_args);
-    S.first = (const int *)(d + off_first);
-    S.order = (const int *)(d + off_order);
-    S.count = count;
+    S.tick = (const int2 *)(d + off_first);
+    S.strips = strips;
     S.ticket = (int *)(d + off_first + sz_first - 16);
-    const int strips = first[count];
     S.stamps = nullptr;
     S.stamp_blocks = 0;
     S.wait_ticks = wait_ticks;
