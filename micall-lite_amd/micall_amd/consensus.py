@@ -217,9 +217,15 @@ def counts_to_conseqs(pile, order, seeds=None):
 
 
 def extract_relevant_seed(aligned_conseq, aligned_seed):
-    """remap.extract_relevant_seed (remap.py:129-138)."""
-    match = re.match('-*([^-](.*[^-])?)', aligned_conseq)
-    return aligned_seed[match.start(1):match.end(1)].replace('-', '')
+    """remap.extract_relevant_seed (remap.py:129-138): the seed under the
+    consensus from its first to its last non-gap column, gaps removed."""
+    start = len(aligned_conseq) - len(aligned_conseq.lstrip('-'))
+    end = len(aligned_conseq.rstrip('-'))
+    if start >= end:
+        # no non-gap column: the reference's match is None (AttributeError)
+        match = re.match('-*([^-](.*[^-])?)', aligned_conseq)
+        return aligned_seed[match.start(1):match.end(1)].replace('-', '')
+    return aligned_seed[start:end].replace('-', '')
 
 
 def clean_sequence(seq, alphabet=HYPHY_NUC_ALPHABET):
@@ -247,13 +253,16 @@ def filter_conseqs(ctx, pile, order, new_conseqs, seeds, filter_coverage, distan
     for name in names:
         conseq = new_conseqs[name]
         keep = pile.position_sums(index[name], seeds.get(name), len(conseq)) >= filter_coverage
-        covered = ''.join(c for c, k in zip(conseq, keep) if k)
+        covered = np.frombuffer(conseq.encode(), dtype=np.uint8)[keep[:len(conseq)]].tobytes().decode()
         if covered:
             relevant[name] = covered
     jobs = [(name, seed_name) for name in names if name in relevant for seed_name in names]
+    # each sequence cleaned once (K seeds, K consensuses; not K x K times)
+    clean_seed = {n: clean_sequence(seeds[n]) for n in names}
+    clean_rel = {n: clean_sequence(relevant[n]) for n in relevant}
     aligned = ctx.gotoh_align_many(
-        [(clean_sequence(seeds[seed_name]), clean_sequence(relevant[name]))
-         for name, seed_name in jobs], FILTER_GOP, FILTER_GEP, True, HYPHY_NUC_ALPHABET, HYPHY_NUC)
+        [(clean_seed[seed_name], clean_rel[name]) for name, seed_name in jobs],
+        FILTER_GOP, FILTER_GEP, True, HYPHY_NUC_ALPHABET, HYPHY_NUC)
     for result in aligned:
         if isinstance(result, Exception):
             raise result
