@@ -35,6 +35,12 @@
 // Bit-for-bit specification: oracle/og_gotoh.c.
 #include <limits.h>
 
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <thread>
+#include <system_error>
+#include <algorithm>
 #include <mutex>
 #include <type_traits>
 #include <utility>
@@ -715,10 +721,30 @@ static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 // Per alignment: an "io" block (codes, strings, output strings, result: what
 // crosses PCIe) and a "work" block (diagonal buffers, last row / column and
 // the three tie planes, zeroed on the device).
-static size_t gotoh_io_bytes(int m, int n, int L)
+static size_t gotoh_in_bytes(int m, int n, int L)     // codes, text, score profile (uploaded)
 {
-    return align16(m + 8) + align16(n + 8) + align16(m + 1) + align16(n + 1) +
-           2 * align16(m + n + 1) + 64 + (size_t)L * prof_width(n);
+    return align16(m + 8) + align16(n + 8) + align16(m + 1) + align16(n + 1) + (size_t)L * prof_width(n);
+}
+
+static size_t gotoh_out_bytes(int m, int n)            // aligned strings, result (fetched)
+{
+    return 2 * align16(m + n + 1) + 64;
+}
+
+// fn(t) for t = 0 .. count - 1 on up to 16 host threads
+static void gotoh_par(int count, const std::function<void(int)> &fn)
+{
+    const int nt = std::max(1, std::min({count, 16, (int)std::thread::hardware_concurrency()}));
+    std::atomic<int> next(0);
+    auto run = [&]() { for (int t; (t = next.fetch_add(1)) < count;) fn(t); };
+    std::vector<std::thread> th;
+    try {
+        for (int k = 1; k < nt; ++k) th.emplace_back(run);
+    } catch (const std::system_error &) {
+        // fewer threads: the ones started and this one share the work
+    }
+    run();
+    for (auto &x : th) x.join();
 }
 
 static size_t gotoh_work_bytes(int m, int n)
@@ -749,20 +775,28 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     if (mat_max > 127) { set_error("mh_gotoh_align: scores outside -127..127"); return -3; }
     if (gop < 0 || gep < 0 || gop > (1 << 16) || gep > (1 << 16)) { set_error("mh_gotoh_align: bad gap penalties"); return -3; }
     std::vector<int> ms(count), ns(count);
-    std::vector<size_t> io(count + 1, 0), work(count + 1, 0);
-    for (int t = 0; t < count; ++t) {
+    std::vector<size_t> io(count + 1, 0), oo(count + 1, 0), work(count + 1, 0);
+    for (int t = 0; t < count; ++t)
         if (!s1[t] || !s2[t] || !out1[t] || !out2[t]) { set_error("mh_gotoh_align: null argument"); return -3; }
+    // lengths and the alphabet check of every alignment on host threads; the
+    // first offending character (by alignment, then position) is reported
+    std::vector<int> badc(count, -1);
+    gotoh_par(count, [&](int t) {
         ms[t] = (int)strlen(s1[t]);
         ns[t] = (int)strlen(s2[t]);
+        for (int i = 0; i < ms[t] && badc[t] < 0; ++i)
+            if (code[(unsigned char)s1[t][i]] < 0) badc[t] = (unsigned char)s1[t][i];
+        for (int j = 0; j < ns[t] && badc[t] < 0; ++j)
+            if (code[(unsigned char)s2[t][j]] < 0) badc[t] = (unsigned char)s2[t][j];
+    });
+    for (int t = 0; t < count; ++t) {
         if (ms[t] == 0 || ns[t] == 0 || cap[t] < ms[t] + ns[t] + 1) {
             set_error("mh_gotoh_align: bad arguments (alignment %d)", t);
             return -3;
         }
-        for (int i = 0; i < ms[t]; ++i)
-            if (code[(unsigned char)s1[t][i]] < 0) { set_error("mh_gotoh_align: '%c' not in alphabet", s1[t][i]); return -3; }
-        for (int j = 0; j < ns[t]; ++j)
-            if (code[(unsigned char)s2[t][j]] < 0) { set_error("mh_gotoh_align: '%c' not in alphabet", s2[t][j]); return -3; }
-        io[t + 1] = io[t] + gotoh_io_bytes(ms[t], ns[t], L);
+        if (badc[t] >= 0) { set_error("mh_gotoh_align: '%c' not in alphabet", badc[t]); return -3; }
+        io[t + 1] = io[t] + gotoh_in_bytes(ms[t], ns[t], L);
+        oo[t + 1] = oo[t] + gotoh_out_bytes(ms[t], ns[t]);
         // boundary cells carry R and P in 26 bits (k_gotoh_fwd rp_pack)
         if ((int64_t)(ms[t] + ns[t] + 2) * (mat_max + gop + gep + 1) >= ((int64_t)1 << 24)) {
             set_error("mh_gotoh_align: alignment %d too long for the score range", t);
@@ -803,8 +837,9 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     }
     const size_t sz_mat = align16(sizeof(int) * L * L), sz_args = align16(sizeof(GotohArgs) * count);
     const size_t sz_first = align16(sizeof(int2) * tick.size()) + 16;   // the ticket table, the two ticket counters
-    // device buffer: [io blocks][matrix][arguments][strip table, tickets][work blocks]
-    const size_t off_mat = io[count], off_args = off_mat + sz_mat, off_first = off_args + sz_args,
+    // device buffer: [in blocks][out blocks][matrix][arguments][strip table, tickets][work blocks]
+    const size_t off_out = io[count];
+    const size_t off_mat = off_out + oo[count], off_args = off_mat + sz_mat, off_first = off_args + sz_args,
                  off_work = off_first + sz_first;
     const size_t total = off_work + work[count] + 256;
     std::lock_guard<std::mutex> guard(c.gotoh_mutex);   // the scratch is per context
@@ -816,17 +851,22 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
         c.gotoh_cap = total;
     }
     char *d = c.gotoh_buf;
-    std::vector<char> img(io[count], 0);   // host image of the io blocks
+    // host images of the in blocks (uploaded) and the out blocks (fetched),
+    // each alignment's part built by one host thread
+    std::unique_ptr<char[]> img(new char[io[count] + 16]);
+    std::unique_ptr<char[]> oimg(new char[oo[count] + 16]);
     std::vector<GotohArgs> args(count);
-    for (int t = 0; t < count; ++t) {
+    gotoh_par(count, [&](int t) {
         const int m = ms[t], n = ns[t];
-        size_t o = io[t], w = off_work + work[t];
+        size_t o = io[t], q = off_out + oo[t], w = off_work + work[t];
+        memset(&img[o], 0, io[t + 1] - io[t]);
         auto take_io = [&](size_t sz) { const size_t at = o; o += align16(sz); return at; };
+        auto take_out = [&](size_t sz) { const size_t at = q; q += align16(sz); return at; };
         auto take_w = [&](size_t sz) { char *at = d + w; w += align16(sz); return at; };
         GotohArgs &A = args[t];
         const size_t oa = take_io(m + 8), ob = take_io(n + 8), o1 = take_io(m + 1),
-                     o2 = take_io(n + 1), oo1 = take_io(m + n + 1), oo2 = take_io(m + n + 1),
-                     ores = take_io(64), oprof = take_io((size_t)L * prof_width(n));
+                     o2 = take_io(n + 1), oprof = take_io((size_t)L * prof_width(n));
+        const size_t oo1 = take_out(m + n + 1), oo2 = take_out(m + n + 1), ores = take_out(64);
         A.lastcol = (int *)take_w(sizeof(int) * (m + 2));
         A.lastrow = (int *)take_w(sizeof(int) * (n + 2));
         const size_t cells = (size_t)(m + 2) * (n + 2);
@@ -858,11 +898,12 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
         A.result = (int *)(d + ores);
         A.m = m; A.n = n; A.L = L; A.mat = (const int *)(d + off_mat);
         A.u = gep; A.v = gop; A.is_global = is_global ? 1 : 0;
-    }
+    });
     hipStream_t st = c.stream;
     MH_HIP(hipMemsetAsync(d + off_work, 0, work[count], st));
     MH_HIP(hipMemsetAsync(d + off_first, 0, sz_first, st));
-    MH_HIP(hipMemcpyAsync(d, img.data(), io[count], hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemsetAsync(d + off_out, 0, oo[count], st));
+    MH_HIP(hipMemcpyAsync(d, img.get(), io[count], hipMemcpyHostToDevice, st));
     MH_HIP(hipMemcpyAsync(d + off_mat, matrix, sizeof(int) * L * L, hipMemcpyHostToDevice, st));
     MH_HIP(hipMemcpyAsync(d + off_args, args.data(), sizeof(GotohArgs) * count,
                           hipMemcpyHostToDevice, st));
@@ -905,7 +946,7 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
                        (const GotohArgs *)(d + off_args));
     prof_end(c, pg);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(img.data(), d, io[count], hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(oimg.get(), d + off_out, oo[count], hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "k_gotoh");
     if (S.stamps) {   // header: strips, blocks per strip; then fwd and bwd stamps
@@ -922,12 +963,12 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     for (int t = 0; t < count; ++t) {
         const GotohArgs &A = args[t];
         int res[3];
-        memcpy(res, &img[(const char *)A.result - d], sizeof(res));
+        memcpy(res, &oimg[(const char *)A.result - d - off_out], sizeof(res));
         if (res[0] == -4) { set_error("k_gotoh: a strip's wait for its neighbour timed out (alignment %d)", t); return -4; }
         status[t] = res[0] ? -1 : 0;
         score[t] = res[1];
         const int len = res[0] ? 0 : res[2];
-        const char *t1 = &img[A.out1 - d], *t2 = &img[A.out2 - d];
+        const char *t1 = &oimg[A.out1 - d - off_out], *t2 = &oimg[A.out2 - d - off_out];
         for (int k = 0; k < len; ++k) { out1[t][k] = t1[len - 1 - k]; out2[t][k] = t2[len - 1 - k]; }
         out1[t][len] = out2[t][len] = '\0';
     }
