@@ -286,7 +286,17 @@ static uint64_t signature(int n, const char *const *seqs, int seedlen)
     for (int r = 0; r < n; ++r) {
         const size_t len = std::strlen(seqs[r]);
         h = mix64(h, (uint64_t)len);
+        // four independent chains over 32-byte steps (the 74 seeds are
+        // 0.74 MB, hashed on every prelim pass), folded in order
+        uint64_t q[4] = {h, h ^ 1, h ^ 2, h ^ 3};
         size_t i = 0;
+        for (; i + 32 <= len; i += 32)
+            for (int k = 0; k < 4; ++k) {
+                uint64_t w;
+                std::memcpy(&w, seqs[r] + i + 8 * k, 8);
+                q[k] = mix64(q[k], w);
+            }
+        h = mix64(mix64(mix64(mix64(h, q[0]), q[1]), q[2]), q[3]);
         for (; i + 8 <= len; i += 8) {
             uint64_t w;
             std::memcpy(&w, seqs[r] + i, 8);
