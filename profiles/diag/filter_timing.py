@@ -49,4 +49,20 @@ for rep in range(reps):
                       'clean_ms': round(1e3 * (t1 - t0), 1), 'gotoh_ms': round(1e3 * (t2 - t1), 1),
                       'extract_ms': round(1e3 * (t3 - t2), 1), 'lev_ms': round(1e3 * (t4 - t3), 1),
                       'dist_sum': int(sum(d))}), flush=True)
+# what exact length bounds could skip (d >= len(relevant) - len(seed) before
+# the alignment, d >= |len(relevant seed) - len(relevant)| after it): pairs
+# whose bound exceeds the name's nearest other seed's distance
+best = {}
+for (n, s), dist in zip(jobs, d):
+    if s != n:
+        best[n] = min(best.get(n, 1 << 60), dist)
+pre = [(n, s) for (n, s), (a, b) in zip(jobs, inputs) if s != n and len(b) - len(a) > best[n]]
+post = [(n, s) for (n, s), (rs, c) in zip(jobs, lev_in) if s != n and abs(len(rs) - len(c)) > best[n]]
+cells = {(n, s): len(a) * len(b) for (n, s), (a, b) in zip(jobs, inputs)}
+lcells = {(n, s): len(a) * len(b) for (n, s), (a, b) in zip(jobs, lev_in)}
+print(json.dumps({'prune_before_alignment': len(pre),
+                  'gotoh_cells_G_skipped': round(sum(cells[k] for k in pre) / 1e9, 2),
+                  'lev_cells_G_skipped_with_it': round(sum(lcells[k] for k in pre) / 1e9, 2),
+                  'prune_after_alignment': len(post),
+                  'lev_cells_G_skipped': round(sum(lcells[k] for k in post) / 1e9, 2)}), flush=True)
 ctx.close()

@@ -1,0 +1,103 @@
+"""consensus.filter_conseqs computes an edit distance only where it can
+decide (the own seed, then the other seeds whose length bound does not
+exceed the nearest one found).  Its decisions and its distance report must
+equal the reference's loop over every seed (remap.py:242-262: the first
+other seed in name order with the smallest distance), on sets built to
+prune (lengths far apart) and to tie (copies of one sequence).  CPU: the
+alignments come from the oracle's Gotoh (test infrastructure) through a
+stand-in context; the edit distances from the library's host batch."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from micall_amd import _native
+from micall_amd.consensus import (FILTER_GEP, FILTER_GOP, HYPHY_NUC, HYPHY_NUC_ALPHABET,
+                                  clean_sequence, extract_relevant_seed, filter_conseqs)
+
+
+class _OracleAligner:
+    def gotoh_align_many(self, pairs, gop, gep, is_global, alphabet, matrix):
+        return [oracle.gotoh_align(a, b, gop, gep, is_global, alphabet, list(matrix)) for a, b in pairs]
+
+
+class _FullCoverage:
+    def __init__(self, names):
+        self.refnames = list(names)
+
+    def position_sums(self, r, seed, length):
+        return np.full(length, 100, dtype=np.int64)
+
+
+def _reference_loop(new_conseqs, seeds):
+    """remap.py:231-262 over every seed (no pruning), oracle Levenshtein."""
+    report, kept = {}, {}
+    for name in sorted(new_conseqs):
+        relevant = new_conseqs[name]
+        seed_dist = other_dist = other_seed = None
+        for seed_name in sorted(new_conseqs):
+            a_seed, a_conseq, _ = oracle.gotoh_align(
+                clean_sequence(seeds[seed_name]), clean_sequence(relevant), FILTER_GOP, FILTER_GEP,
+                True, HYPHY_NUC_ALPHABET, HYPHY_NUC)
+            d = oracle.levenshtein(extract_relevant_seed(a_conseq, a_seed), relevant)
+            if seed_name == name:
+                seed_dist = d
+            elif other_dist is None or d < other_dist:
+                other_seed, other_dist = seed_name, d
+        if seed_dist <= other_dist:
+            kept[name] = relevant
+        report[name] = dict(seed_dist=seed_dist, other_dist=other_dist, other_seed=other_seed)
+    return kept, report
+
+
+def _mutate(rng, s, rate):
+    return ''.join(rng.choice('ACGT') if rng.random() < rate else c for c in s)
+
+
+@pytest.mark.parametrize('seed', range(6))
+def test_pruned_filter_equals_the_full_loop(seed):
+    rng = random.Random(seed)
+    base = ''.join(rng.choice('ACGT') for _ in range(900))
+    seeds = {
+        'A-long': base + ''.join(rng.choice('ACGT') for _ in range(600)),
+        'B-short': base[100:220],
+        'C-mid': _mutate(rng, base[:700], 0.05),
+        'D-copy': base[:700],          # two seeds at one distance: ties
+        'E-copy': base[:700],
+        'F-tiny': base[400:430],
+    }
+    names = sorted(seeds)
+    new_conseqs = {n: _mutate(rng, seeds[n], 0.08) for n in names}
+    order = list(range(len(names)))
+    report = {}
+    kept = filter_conseqs(_OracleAligner(), _FullCoverage(names), order, new_conseqs, seeds, 1,
+                          report)
+    want_kept, want_report = _reference_loop(new_conseqs, seeds)
+    assert report == want_report
+    assert kept == want_kept
+
+
+def test_the_bound_skips_work():
+    """The long consensus against the short seeds: those distances are not
+    computed (their bound exceeds the nearest other seed's distance)."""
+    rng = random.Random(11)
+    base = ''.join(rng.choice('ACGT') for _ in range(1500))
+    seeds = {'long': base, 'long2': _mutate(rng, base, 0.05), 'short': base[:80], 'short2': base[700:760]}
+    new_conseqs = {n: _mutate(rng, s, 0.03) for n, s in seeds.items()}
+    names = sorted(seeds)
+    calls = []
+    real = _native.levenshtein_many
+
+    def counted(pairs):
+        calls.append(len(pairs))
+        return real(pairs)
+    _native.levenshtein_many = counted
+    try:
+        report = {}
+        filter_conseqs(_OracleAligner(), _FullCoverage(names), list(range(4)), new_conseqs, seeds, 1,
+                       report)
+    finally:
+        _native.levenshtein_many = real
+    assert sum(calls) < len(names) * len(names)
+    assert report == _reference_loop(new_conseqs, seeds)[1]
