@@ -266,31 +266,16 @@ def filter_conseqs(ctx, pile, order, new_conseqs, seeds, filter_coverage, distan
     for result in aligned:
         if isinstance(result, Exception):
             raise result
-    # edit distances, exact where they can decide: every name's own seed and
-    # its other seed with the smallest length bound first; then only the
-    # other seeds whose bound |len(relevant seed) - len(relevant)| (a lower
-    # bound of the edit distance) does not exceed the nearest one found, as
-    # a larger distance is neither the minimum nor its first occurrence
-    rel_seed = [extract_relevant_seed(a_conseq, a_seed) for (a_seed, a_conseq, _score) in aligned]
-    bound = [abs(len(rs) - len(relevant[name])) for (name, _seed), rs in zip(jobs, rel_seed)]
-    first = {}
-    for k, (name, seed_name) in enumerate(jobs):
-        if seed_name != name and (name not in first or bound[k] < bound[first[name]]):
-            first[name] = k
-    todo = [k for k, (name, seed_name) in enumerate(jobs) if seed_name == name or first.get(name) == k]
-    dist = dict(zip(todo, _native.levenshtein_many([(rel_seed[k], relevant[jobs[k][0]]) for k in todo])))
-    nearest = {}
-    for k in todo:
-        name, seed_name = jobs[k]
-        if seed_name != name:
-            nearest[name] = dist[k]
-    rest = [k for k, (name, seed_name) in enumerate(jobs)
-            if k not in dist and bound[k] <= nearest[name]]
-    dist.update(zip(rest, _native.levenshtein_many([(rel_seed[k], relevant[jobs[k][0]]) for k in rest])))
+    # every distance in one host batch: an exact length bound could skip 43 %
+    # of the cells at C4-all size, but in two dependent batches each is as
+    # long as its longest pair, and the two took 31 ms against 24 ms
+    # (profiles/diag/filter_timing.py, lev_pruned_ms)
+    dists = _native.levenshtein_many(
+        [(extract_relevant_seed(a_conseq, a_seed), relevant[name])
+         for (name, _seed), (a_seed, a_conseq, _score) in zip(jobs, aligned)])
     per_name = {}
-    for k, (name, seed_name) in enumerate(jobs):
-        if k in dist:
-            per_name.setdefault(name, []).append((seed_name, dist[k]))
+    for (name, seed_name), d in zip(jobs, dists):
+        per_name.setdefault(name, []).append((seed_name, d))
     filtered = {}
     for name in names:
         if name not in relevant:

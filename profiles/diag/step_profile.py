@@ -18,8 +18,9 @@ from micall_amd.pipeline import RemapPipeline  # noqa: E402
 
 pairs = int(sys.argv[1]) if len(sys.argv) > 1 else 1000000
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+genomes = sys.argv[3] if len(sys.argv) > 3 else 'pol'
 ctx = _native.Context(0)
-reads, quals = bench.make_reads(pairs, block=0)
+reads, quals = bench.make_reads(pairs, block=0, genomes=genomes)
 ctx.reads_load_fixed(reads, quals, True)
 del reads, quals
 pipe = RemapPipeline(ctx)

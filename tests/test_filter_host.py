@@ -1,9 +1,8 @@
-"""consensus.filter_conseqs computes an edit distance only where it can
-decide (the own seed, then the other seeds whose length bound does not
-exceed the nearest one found).  Its decisions and its distance report must
-equal the reference's loop over every seed (remap.py:242-262: the first
-other seed in name order with the smallest distance), on sets built to
-prune (lengths far apart) and to tie (copies of one sequence).  CPU: the
+"""consensus.filter_conseqs (one Gotoh batch, one edit-distance batch, each
+sequence cleaned once) against the reference's loop over every seed
+(remap.py:231-262: the first other seed in name order with the smallest
+distance) on sets with lengths far apart and with ties (copies of one
+sequence): the same decisions and distance report.  CPU: the
 alignments come from the oracle's Gotoh (test infrastructure) through a
 stand-in context; the edit distances from the library's host batch."""
 import random
@@ -12,7 +11,6 @@ import numpy as np
 import pytest
 
 import oracle
-from micall_amd import _native
 from micall_amd.consensus import (FILTER_GEP, FILTER_GOP, HYPHY_NUC, HYPHY_NUC_ALPHABET,
                                   clean_sequence, extract_relevant_seed, filter_conseqs)
 
@@ -76,28 +74,3 @@ def test_pruned_filter_equals_the_full_loop(seed):
     want_kept, want_report = _reference_loop(new_conseqs, seeds)
     assert report == want_report
     assert kept == want_kept
-
-
-def test_the_bound_skips_work():
-    """The long consensus against the short seeds: those distances are not
-    computed (their bound exceeds the nearest other seed's distance)."""
-    rng = random.Random(11)
-    base = ''.join(rng.choice('ACGT') for _ in range(1500))
-    seeds = {'long': base, 'long2': _mutate(rng, base, 0.05), 'short': base[:80], 'short2': base[700:760]}
-    new_conseqs = {n: _mutate(rng, s, 0.03) for n, s in seeds.items()}
-    names = sorted(seeds)
-    calls = []
-    real = _native.levenshtein_many
-
-    def counted(pairs):
-        calls.append(len(pairs))
-        return real(pairs)
-    _native.levenshtein_many = counted
-    try:
-        report = {}
-        filter_conseqs(_OracleAligner(), _FullCoverage(names), list(range(4)), new_conseqs, seeds, 1,
-                       report)
-    finally:
-        _native.levenshtein_many = real
-    assert sum(calls) < len(names) * len(names)
-    assert report == _reference_loop(new_conseqs, seeds)[1]
