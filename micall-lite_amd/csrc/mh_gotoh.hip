@@ -56,8 +56,11 @@ enum { GA = 1, GB = 2, GC = 4, GD = 8, GE_ = 16, GF = 32, GG = 64 };
 constexpr int GOTOH_THREADS = 1024;        // k_gotoh_tb
 constexpr int GBLK = 32;                   // boundary columns published / awaited at a time
 constexpr uint32_t GOOB = 0x80000000u;     // a buffer offset past every plane (planes < 2 GiB)
-constexpr int TB = 128;                                // traceback window (diagonals x rows)
-constexpr size_t TB_LDS = (size_t)TB * TB + 2 * TB;   // window + both sequences' characters
+// traceback window: TBD anti-diagonals x TBR rows (a window twice as deep
+// in diagonals, for the mostly diagonal paths, measured no faster: the walk
+// is bound by its serial LDS reads, not by the window loads)
+constexpr int TBD = 128, TBR = 128;
+constexpr size_t TB_LDS = (size_t)TBD * TBR + TBR + TBD;   // window + both sequences' characters
 
 __host__ __device__ inline size_t gotoh_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -628,14 +631,14 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh_tb(const GotohArgs *bat
     const int gabort = A.flags[0];
     // ---- phase 3: traceback ----
     // The walk is serial, so it never waits on global memory: the block
-    // stages a TB x TB window of abc (diagonals s0 .. s0-TB+1, rows
-    // ii .. ii-TB+1 of the current cell (ii, jj), which holds every cell the
-    // path can reach before it leaves the window) and the TB characters of
+    // stages a TBD x TBR window of abc (diagonals s0 .. s0-TBD+1, rows
+    // ii .. ii-TBR+1 of the current cell (ii, jj), which holds every cell the
+    // path can reach before it leaves the window) and the TBR / TBD characters of
     // each sequence before ii / jj into LDS; thread 0 walks the window and
     // writes the output characters; repeat.  The gap runs at both ends are
     // written by the whole block.
     uint8_t *win = gsm;
-    char *wc1 = (char *)win + TB * TB, *wc2 = wc1 + TB;
+    char *wc1 = (char *)win + TBD * TBR, *wc2 = wc1 + TBR;
     __shared__ unsigned long long tb_key;
     __shared__ int tb_ii, tb_jj, tb_len, tb_status;
     if (threadIdx.x == 0) tb_key = ~0ull;
@@ -659,7 +662,13 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh_tb(const GotohArgs *bat
         if (x >= 1 && x <= m + 1) { ii = x - 1; jj = n; }
         else if (x > m + 1) { ii = m; jj = x - m - 2; }
     }
-    char *r1 = A.out1, *r2 = A.out2;   // built back to front, reversed by the host
+    // built back to front, reversed by the host; global (not flat) stores:
+    // a flat store counts in lgkmcnt too, so the walk's next LDS read of the
+    // window waited for the last step's two output stores
+    typedef __attribute__((address_space(1))) char gchar;
+    typedef const __attribute__((address_space(1))) uint8_t gbyte;
+    gchar *r1 = (gchar *)A.out1, *r2 = (gchar *)A.out2;
+    gbyte *bits = (gbyte *)A.bits;
     // end gaps: seq1 past ii, then seq2 past jj
     for (int x = threadIdx.x; x < m - ii; x += blockDim.x) { r1[x] = A.s1[m - 1 - x]; r2[x] = '-'; }
     for (int x = threadIdx.x; x < n - jj; x += blockDim.x) {
@@ -672,15 +681,15 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh_tb(const GotohArgs *bat
         const int i0 = tb_ii, j0 = tb_jj;
         if (i0 <= 0 || j0 <= 0 || tb_status) break;
         const int s0 = i0 + j0;
-        for (int x = threadIdx.x; x < TB * TB; x += blockDim.x) {
-            const int t = x / TB, r = x % TB;
+        for (int x = threadIdx.x; x < TBD * TBR; x += blockDim.x) {
+            const int t = x / TBR, r = x % TBR;
             const int sd = s0 - t, i = i0 - r, j = sd - i;
             uint8_t vv = 0;
-            if (i >= 1 && j >= 1 && j <= n) vv = A.bits[dbase(sd, m, n) + i];   // (r <= t on the path)
+            if (i >= 1 && j >= 1 && j <= n) vv = bits[dbase(sd, m, n) + i];   // (r <= t on the path)
             win[x] = vv;
         }
-        for (int x = threadIdx.x; x < TB; x += blockDim.x) {
-            wc1[x] = i0 - 1 - x >= 0 ? A.s1[i0 - 1 - x] : 0;
+        for (int x = threadIdx.x; x < TBD; x += blockDim.x) {
+            if (x < TBR) wc1[x] = i0 - 1 - x >= 0 ? A.s1[i0 - 1 - x] : 0;
             wc2[x] = j0 - 1 - x >= 0 ? A.s2[j0 - 1 - x] : 0;
         }
         __syncthreads();
@@ -688,8 +697,8 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh_tb(const GotohArgs *bat
             int i = i0, j = j0, len = tb_len, status = 0;
             while (i > 0 && j > 0) {
                 const int t = s0 - (i + j), r = i0 - i, c = j0 - j;
-                if (t >= TB || r >= TB || c >= TB) break;
-                const uint8_t x = win[t * TB + r];
+                if (t >= TBD || r >= TBR || c >= TBD) break;
+                const uint8_t x = win[t * TBR + r];
                 if (x & GA) { r1[len] = wc1[r]; r2[len] = '-'; --i; }
                 else if (x & GB) { r1[len] = '-'; r2[len] = wc2[c]; --j; }
                 else if (x & GC) { r1[len] = wc1[r]; r2[len] = wc2[c]; --i; --j; }
