@@ -812,6 +812,9 @@ int mh_ctx_destroy(mh_ctx *ctx)
     MapState &M = c->map;
     hipFree(M.cand); hipFree(M.n_cand); hipFree(M.yf); hipFree(M.work); hipFree(M.rwork); hipFree(M.skey); hipFree(M.sinfo);
     hipFree(M.pool); hipFree(M.pool_used); hipFree(M.rec); hipFree(M.counters); hipFree(M.ref_stats);
+    if (M.stats_pin) hipHostFree(M.stats_pin);
+    M.stats_pin = nullptr;
+    M.stats_pin_cap = 0;
     RowState &R = c->rows;
     hipFree(R.flag); hipFree(R.ref); hipFree(R.pos); hipFree(R.cig_off); hipFree(R.n_cigar);
     hipFree(R.cigar); hipFree(R.units);
@@ -822,6 +825,10 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipFree(P.tok_slot); hipFree(P.tok_cnt); hipFree(P.tok_used); hipFree(P.tok_meta);
     hipFree(P.tok_bytes);
     hipFree(P.ev_counters);
+    if (P.land) hipHostFree(P.land);
+    P.land = nullptr;
+    P.land_cap = 0;
+    P.land_ok = false;
     hipFree(P.ins_scratch);
     hipFree(P.sel);
     hipFree(P.win_map);
@@ -2520,8 +2527,29 @@ int mh_pileup(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *
     c->pile.n_refs = n_refs;
     c->pile.cap = cap;
     c->pile.ref_lens.assign(ref_lens, ref_lens + n_refs);
+    c->pile.land_ok = false;
     int st = run_pileup(*c, source, q_cutoff);
-    if (st == 0) MH_HIP(hipStreamSynchronize(c->stream));
+    if (st == 0) {
+        PileState &P = c->pile;
+        const size_t nr = (size_t)P.n_refs, need = 16 * nr + 4 * nr + 64;
+        if (P.land_cap < need) {
+            if (P.land) hipHostFree(P.land);
+            P.land = nullptr;
+            P.land_cap = 0;
+            if (hipHostMalloc((void **)&P.land, need, hipHostMallocDefault) == hipSuccess) P.land_cap = need;
+            else P.land = nullptr;
+        }
+        if (P.land && P.read_counts && P.first_unit && P.max_pos) {
+            bool ok = hipMemcpyAsync(P.land, P.read_counts, 8 * nr, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+                      hipMemcpyAsync(P.land + 8 * nr, P.first_unit, 8 * nr, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+                      hipMemcpyAsync(P.land + 16 * nr, P.max_pos, 4 * nr, hipMemcpyDeviceToHost, c->stream) == hipSuccess;
+            if (ok && P.ev_counters)
+                ok = hipMemcpyAsync(P.land + ((20 * nr + 7) & ~(size_t)7), P.ev_counters, 32,
+                                    hipMemcpyDeviceToHost, c->stream) == hipSuccess;
+            P.land_ok = ok;
+        }
+        MH_HIP(hipStreamSynchronize(c->stream));
+    }
     prof_flush(*c);
     return st;
 }
@@ -2537,7 +2565,10 @@ static int aggregate_tokens(CtxEx &c)
     c.tok_ref.clear(); c.tok_pos.clear(); c.tok_off.clear(); c.tok_len.clear();
     c.tok_count.clear(); c.tok_pool.clear();
     int64_t ctr[4] = {0, 0, 0, 0};
-    if (P.ev_counters) MH_HIP(copy_sync(c, ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
+    if (P.ev_counters && P.land_ok)   // landed behind mh_pileup
+        std::memcpy(ctr, P.land + ((20 * (size_t)P.n_refs + 7) & ~(size_t)7), sizeof(ctr));
+    else if (P.ev_counters)
+        MH_HIP(copy_sync(c, ctr, P.ev_counters, sizeof(ctr), hipMemcpyDeviceToHost));
     const int64_t ne = ctr[0];
     if (ne > 0) {
         // distinct (ref, pos, token) keys and their counts come from the
@@ -2639,6 +2670,12 @@ int mh_pileup_fetch(mh_ctx *ctx, int32_t *dense, uint8_t *nflag, uint8_t *dflag,
     if (!P.dense) { set_error("no pileup (call mh_pileup)"); return -3; }
     MH_HIP(hipSetDevice(c->device));
     const size_t cells = (size_t)P.n_refs * P.cap, nr = (size_t)P.n_refs;
+    if (!dense && !nflag && !dflag && P.land_ok) {   // the scalars, landed behind mh_pileup
+        if (read_counts) std::memcpy(read_counts, P.land, 8 * nr);
+        if (first_unit) std::memcpy(first_unit, P.land + 8 * nr, 8 * nr);
+        if (max_pos) std::memcpy(max_pos, P.land + 16 * nr, 4 * nr);
+        return 0;
+    }
     const FetchPart parts[6] = {{P.dense, sizeof(int32_t) * 4 * cells, dense},
                                 {P.nflag, cells, nflag},
                                 {P.dflag, cells, dflag},

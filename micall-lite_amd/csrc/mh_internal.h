@@ -147,6 +147,11 @@ struct MapState {
     // host copy of ref_stats (5 * n_refs + 3), filled on first use after a
     // mapping pass: mh_map_counts and the pileup's window choice share it
     std::vector<int64_t> stats_host;
+    // pinned landing area of ref_stats, copied at the end of each pass (mh_map
+    // synchronises anyway), so mh_map_counts needs no round trip of its own
+    int64_t *stats_pin = nullptr;
+    size_t stats_pin_cap = 0;
+    bool stats_pin_ready = false;
     // k_dp launch shapes already sized: (kernel, LDS bytes) -> blocks per CU
     // that fit (the occupancy query is a host call worth skipping per launch)
     std::map<std::pair<const void *, int>, int> dp_occ;
@@ -182,6 +187,12 @@ struct PileState {
     int64_t alloc_cells = 0;
     int alloc_refs = 0;
     int64_t gen = 0;                // bumped by every mh_pileup / mh_pileup_import
+    // pinned landing of the per-reference scalars (read_counts, first_unit,
+    // max_pos) and ev_counters, copied behind mh_pileup's kernels so the
+    // fetches after it need no round trip; cleared by anything that changes them
+    char *land = nullptr;
+    size_t land_cap = 0;
+    bool land_ok = false;
     std::vector<int32_t> ref_lens;  // host copy (sizes the LDS window)
     int32_t *sel = nullptr;         // references of a multi-GPU exchange
     int sel_cap = 0;

@@ -18,6 +18,8 @@
 //                 k_dp again over those candidates
 //   k_pair        one thread per pair: concordance, flags, MAPQ, SAM fields,
 //                 per-reference line tallies
+#include <cstring>
+
 #include "mh_internal.h"
 
 namespace mh {
@@ -2490,9 +2492,16 @@ const int64_t *map_stats_host(Ctx &c)
     MapState &M = c.map;
     if (!M.stats_host_valid) {
         M.stats_host.resize(5 * (size_t)M.n_refs + 3);
-        if (hipMemcpyAsync(M.stats_host.data(), M.ref_stats, sizeof(int64_t) * M.stats_host.size(),
-                           hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
-            hipStreamSynchronize(c.stream) != hipSuccess) {
+        const size_t bytes = sizeof(int64_t) * M.stats_host.size();
+        if (M.stats_pin_ready) {   // copied at the end of the pass: done by now or at this sync
+            if (hipStreamSynchronize(c.stream) != hipSuccess) {
+                set_error("map_stats_host: copy failed");
+                return nullptr;
+            }
+            std::memcpy(M.stats_host.data(), M.stats_pin, bytes);
+        } else if (hipMemcpyAsync(M.stats_host.data(), M.ref_stats, bytes, hipMemcpyDeviceToHost,
+                                  c.stream) != hipSuccess ||
+                   hipStreamSynchronize(c.stream) != hipSuccess) {
             set_error("map_stats_host: copy failed");
             return nullptr;
         }
@@ -2504,6 +2513,7 @@ const int64_t *map_stats_host(Ctx &c)
 int run_map(Ctx &c, const mh_params &par)
 {
     c.map.stats_host_valid = false;
+    c.map.stats_pin_ready = false;
     if (c.index.n_refs <= 0 || c.index.hkey == nullptr) {
         set_error("mh_map: no reference index (call mh_index_build first)");
         return -3;
@@ -2663,6 +2673,20 @@ int run_map(Ctx &c, const mh_params &par)
     }
     hipLaunchKernelGGL(k_fix_first, dim3(8), dim3(256), 0, s, M.ref_stats, M.n_refs);
     MH_HIP(hipGetLastError());
+    {   // the tallies to pinned memory behind the pass (mh_map's sync covers it)
+        const size_t bytes = sizeof(int64_t) * (5 * (size_t)M.n_refs + 3);
+        if (M.stats_pin_cap < bytes) {
+            if (M.stats_pin) hipHostFree(M.stats_pin);
+            M.stats_pin = nullptr;
+            M.stats_pin_cap = 0;
+            if (hipHostMalloc(&M.stats_pin, bytes, hipHostMallocDefault) == hipSuccess)
+                M.stats_pin_cap = bytes;
+            else
+                M.stats_pin = nullptr;   // map_stats_host copies on demand instead
+        }
+        if (M.stats_pin && hipMemcpyAsync(M.stats_pin, M.ref_stats, bytes, hipMemcpyDeviceToHost, s) == hipSuccess)
+            M.stats_pin_ready = true;
+    }
     M.valid = true;
     return 0;
 }

@@ -1429,6 +1429,7 @@ extern "C" int mh_pileup_import(mh_ctx *ctx, int n_sel, const int32_t *sel, cons
     PileState &P = c.pile;
     if (!P.dense) { set_error("no pileup to import into"); return -3; }
     MH_HIP(hipSetDevice(c.device));
+    P.land_ok = false;   // the scalars change
     int32_t *dsel = nullptr;
     if (int st = upload_sel(c, n_sel, sel, &dsel)) return st;
     hipLaunchKernelGGL(k_pile_import, dim3(64, n_sel > 0 ? n_sel : 1), dim3(256), 0, c.stream,
@@ -1541,5 +1542,6 @@ extern "C" int mh_pileup_events_import(mh_ctx *ctx, int parts, const int64_t *n_
     MH_HIP(hipMemcpyAsync(P.ev_counters, ctr, sizeof(ctr), hipMemcpyHostToDevice, c.stream));
     MH_HIP(hipStreamSynchronize(c.stream));
     ++P.gen;   // the aggregated tokens are recomputed from the new events
+    P.land_ok = false;   // ev_counters change
     return 0;
 }
