@@ -827,6 +827,9 @@ int mh_ctx_destroy(mh_ctx *ctx)
     hipFree(P.ev_counters);
     if (P.land) hipHostFree(P.land);
     P.land = nullptr;
+    if (P.tok_pin) hipHostFree(P.tok_pin);
+    P.tok_pin = nullptr;
+    P.tok_pin_cap = 0;
     P.land_cap = 0;
     P.land_ok = false;
     hipFree(P.ins_scratch);
@@ -2575,7 +2578,7 @@ static int aggregate_tokens(CtxEx &c)
         // device (run_token_aggregate); only their order is fixed here
         std::vector<int32_t> meta;
         std::string bytes;
-        if (int st = run_token_aggregate(c, ne, meta, bytes)) return st;
+        if (int st = run_token_aggregate(c, ne, ctr[1], meta, bytes)) return st;
         struct Key { int32_t ref, pos, off, len; int64_t count; };
         const size_t nd = meta.size() / 5;
         std::vector<Key> uniq(nd);

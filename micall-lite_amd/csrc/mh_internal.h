@@ -214,6 +214,8 @@ struct PileState {
     int32_t *tok_meta = nullptr;    // gather: per distinct key (ref, pos, off, len, count)
     char *tok_bytes = nullptr;
     int64_t tok_meta_cap = 0, tok_bytes_cap = 0;
+    char *tok_pin = nullptr;        // pinned staging of the gather's first round trip
+    size_t tok_pin_cap = 0;
 };
 
 // ---- kernels' host-side launchers (defined in the .hip files) ----------
@@ -226,8 +228,8 @@ const int64_t *map_stats_host(struct Ctx &c);
 int run_pileup(struct Ctx &c, int source, int q_cutoff);
 // distinct (ref, pos, token) keys of the last pileup's events with their
 // counts, aggregated on the device; tokens concatenated in `bytes` at `off`
-int run_token_aggregate(struct Ctx &c, int64_t n_events, std::vector<int32_t> &meta,
-                        std::string &bytes);
+int run_token_aggregate(struct Ctx &c, int64_t n_events, int64_t pool_used,
+                        std::vector<int32_t> &meta, std::string &bytes);
 int run_gotoh(struct Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_global,
               const char *alphabet, const int *matrix, char *out1, char *out2, int cap,
               int *score);

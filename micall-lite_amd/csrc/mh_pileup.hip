@@ -10,6 +10,8 @@
 // The refmap of the reference is order-independent except for its key
 // order, which is recovered from first_unit (atomicMin), so results are
 // deterministic.  Bit-for-bit specification: oracle/og_pileup.c.
+#include <cstring>
+
 #include "mh_internal.h"
 
 namespace mh {
@@ -1230,7 +1232,8 @@ __global__ void k_tok_gather(const int32_t *ev, const char *pool, const int32_t 
     }
 }
 
-int run_token_aggregate(Ctx &c, int64_t ne, std::vector<int32_t> &meta, std::string &bytes)
+int run_token_aggregate(Ctx &c, int64_t ne, int64_t pool_used, std::vector<int32_t> &meta,
+                        std::string &bytes)
 {
     PileState &P = c.pile;
     hipStream_t s = c.stream;
@@ -1248,6 +1251,26 @@ int run_token_aggregate(Ctx &c, int64_t ne, std::vector<int32_t> &meta, std::str
         MH_HIP(hipMalloc(&P.tok_used, sizeof(int32_t) * (cap + 1)));
         P.tok_cap = cap;
     }
+    // room for every event to be a distinct key, and the overflow flag after it
+    if (P.tok_meta_cap < ne) {
+        hipFree(P.tok_meta);
+        P.tok_meta = nullptr;
+        P.tok_meta_cap = 0;
+        MH_HIP(hipMalloc(&P.tok_meta, sizeof(int32_t) * (5 * (size_t)ne + 1)));
+        P.tok_meta_cap = ne;
+    }
+    int32_t *ovf = P.tok_meta + 5 * (size_t)P.tok_meta_cap;
+    // the distinct keys' bytes are a subset of the events' pool: sized by it,
+    // the gather cannot overflow (a test may impose less, to run the retry)
+    const int64_t want = c.test_caps.token_bytes > 0 ? c.test_caps.token_bytes
+                                                     : std::max<int64_t>(pool_used, 64);
+    if (P.tok_bytes_cap < want || (c.test_caps.token_bytes > 0 && P.tok_bytes_cap != want)) {
+        hipFree(P.tok_bytes);
+        P.tok_bytes = nullptr;
+        P.tok_bytes_cap = 0;
+        MH_HIP(hipMalloc(&P.tok_bytes, (size_t)want));
+        P.tok_bytes_cap = want;
+    }
     int32_t *slotid = P.tok_slot + cap, *eslot = P.tok_slot + 2 * cap;
     MH_HIP(hipMemsetAsync(P.tok_slot, 0, sizeof(int32_t) * cap, s));
     MH_HIP(hipMemsetAsync(P.tok_cnt, 0, sizeof(uint32_t) * cap, s));
@@ -1262,45 +1285,45 @@ int run_token_aggregate(Ctx &c, int64_t ne, std::vector<int32_t> &meta, std::str
     hipLaunchKernelGGL(k_tok_count, dim3((unsigned)cblocks), dim3(1024), 0, s, eslot, ne, slotid,
                        P.tok_used, P.tok_cnt);
     MH_HIP(hipGetLastError());
-    int32_t nd = 0;
-    MH_HIP(hipMemcpyAsync(&nd, P.tok_used, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    MH_HIP(hipStreamSynchronize(s));
-    if (nd <= 0) return 0;
-    // the tokens of the distinct keys: at most every event's bytes; usually few
+    // one round trip in the common case: the key count, the overflow flag, the
+    // first keys and the first bytes, through pinned memory
+    const int64_t K = std::min<int64_t>(ne, 4096), B = std::min<int64_t>(P.tok_bytes_cap, 64 << 10);
+    const size_t pin_need = 16 + 20 * (size_t)K + (size_t)B;
+    if (P.tok_pin_cap < pin_need) {
+        if (P.tok_pin) hipHostFree(P.tok_pin);
+        P.tok_pin = nullptr;
+        P.tok_pin_cap = 0;
+        MH_HIP(hipHostMalloc((void **)&P.tok_pin, pin_need, hipHostMallocDefault));
+        P.tok_pin_cap = pin_need;
+    }
     for (int attempt = 0; attempt < 2; ++attempt) {
-        if (P.tok_meta_cap < nd) {
-            hipFree(P.tok_meta);
-            P.tok_meta = nullptr;
-            MH_HIP(hipMalloc(&P.tok_meta, sizeof(int32_t) * 5 * (size_t)nd + sizeof(int32_t)));
-            P.tok_meta_cap = nd;
-        }
-        // first attempt: 64 bytes per distinct key (or what a test imposes)
-        const int64_t want = c.test_caps.token_bytes > 0 ? c.test_caps.token_bytes : 64 * (int64_t)nd;
-        if (attempt == 0 && (P.tok_bytes_cap < want || (c.test_caps.token_bytes > 0 && P.tok_bytes_cap != want))) {
-            hipFree(P.tok_bytes);
-            P.tok_bytes = nullptr;
-            P.tok_bytes_cap = 0;
-            MH_HIP(hipMalloc(&P.tok_bytes, (size_t)want));
-            P.tok_bytes_cap = want;
-        }
-        int32_t *ovf = P.tok_meta + 5 * (size_t)nd;
         MH_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), s));
         hipLaunchKernelGGL(k_tok_gather, dim3(1), dim3(64), 0, s, P.ev, P.ev_pool, P.tok_slot,
                            P.tok_cnt, P.tok_used, P.tok_meta, P.tok_bytes, P.tok_bytes_cap, ovf);
         MH_HIP(hipGetLastError());
-        meta.resize(5 * (size_t)nd + 1);
-        MH_HIP(hipMemcpyAsync(meta.data(), P.tok_meta, sizeof(int32_t) * meta.size(),
-                              hipMemcpyDeviceToHost, s));
+        MH_HIP(hipMemcpyAsync(P.tok_pin, P.tok_used, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        MH_HIP(hipMemcpyAsync(P.tok_pin + 4, ovf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        MH_HIP(hipMemcpyAsync(P.tok_pin + 16, P.tok_meta, 20 * (size_t)K, hipMemcpyDeviceToHost, s));
+        MH_HIP(hipMemcpyAsync(P.tok_pin + 16 + 20 * (size_t)K, P.tok_bytes, (size_t)B, hipMemcpyDeviceToHost, s));
         MH_HIP(hipStreamSynchronize(s));
+        int32_t nd = 0, of = 0;
+        std::memcpy(&nd, P.tok_pin, 4);
+        std::memcpy(&of, P.tok_pin + 4, 4);
+        if (nd <= 0) return 0;
+        meta.resize(5 * (size_t)nd);
+        std::memcpy(meta.data(), P.tok_pin + 16, 20 * (size_t)std::min<int64_t>(nd, K));
+        if (nd > K)   // more keys than the first round brought
+            MH_HIP(copy_sync(c, meta.data() + 5 * (size_t)K, P.tok_meta + 5 * (size_t)K,
+                             20 * (size_t)(nd - K), hipMemcpyDeviceToHost));
         const int64_t total = (int64_t)meta[5 * (size_t)(nd - 1) + 2] + meta[5 * (size_t)(nd - 1) + 3];
-        if (!meta.back()) {
-            meta.pop_back();
+        if (!of) {
             bytes.resize((size_t)total);
-            if (total > 0)
-                MH_HIP(copy_sync(c, &bytes[0], P.tok_bytes, (size_t)total, hipMemcpyDeviceToHost));
+            if (total > 0) std::memcpy(&bytes[0], P.tok_pin + 16 + 20 * (size_t)K, (size_t)std::min(total, B));
+            if (total > B)
+                MH_HIP(copy_sync(c, &bytes[(size_t)B], P.tok_bytes + B, (size_t)(total - B), hipMemcpyDeviceToHost));
             return 0;
         }
-        // longer tokens than 64 bytes on average: room for all of them
+        // longer tokens than the room a test imposed: room for all of them
         ++c.retries[RETRY_TOKEN_BYTES];
         hipFree(P.tok_bytes);
         P.tok_bytes = nullptr;
