@@ -1044,9 +1044,11 @@ class Context:
         check(lib().mh_pileup_events(self.h, _ptr(eref), _ptr(epos), _ptr(eoff), _ptr(elen),
                                      _ptr(ecnt), pool), 'mh_pileup_events')
         raw = pool.raw
-        # (ref, pos, token, number of merged pairs with that token)
-        events = [(int(eref[e]), int(epos[e]), raw[eoff[e]:eoff[e] + elen[e]].decode(),
-                   int(ecnt[e])) for e in range(ne)]
+        # (ref, pos, token, number of merged pairs with that token); the
+        # arrays as lists first (a numpy scalar per field costs ~100 ns)
+        events = [(r, p, raw[o:o + ln].decode(), k) for r, p, o, ln, k in
+                  zip(eref[:ne].tolist(), epos[:ne].tolist(), eoff[:ne].tolist(), elen[:ne].tolist(),
+                      ecnt[:ne].tolist())]
         return dict(dense=dense[:n], nflag=nflag[:n], dflag=dflag[:n], read_counts=rc[:n],
                     first_unit=fu[:n], max_pos=mp[:n], events=events, cap=cap)
 
