@@ -373,17 +373,14 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
         ent.reserve(n);
         for (auto &v : per) { ent.insert(ent.end(), v.begin(), v.end()); std::vector<E>().swap(v); }
     }
-    auto less = [](const E &a, const E &b) {
-        if (a.key != b.key) return a.key < b.key;
-        if (a.ref != b.ref) return a.ref < b.ref;
-        return a.pos < b.pos;
-    };
-    {   // sorted in parallel chunks, then merged pairwise (a total order: the
-        // result is the one std::sort gives)
+    // (key, ref, pos) order: the entries come in (ref, pos) order, so a stable
+    // sort by key alone gives it with a cheaper comparison
+    auto less = [](const E &a, const E &b) { return a.key < b.key; };
+    {   // stable-sorted in parallel chunks, then merged pairwise (stable)
         const int ns = ent.size() < 65536 ? 1 : s2a_threads();
         std::vector<size_t> b((size_t)ns + 1);
         for (int t = 0; t <= ns; ++t) b[(size_t)t] = ent.size() * (size_t)t / (size_t)ns;
-        par_for(ns, [&](int t) { std::sort(ent.begin() + b[(size_t)t], ent.begin() + b[(size_t)t + 1], less); });
+        par_for(ns, [&](int t) { std::stable_sort(ent.begin() + b[(size_t)t], ent.begin() + b[(size_t)t + 1], less); });
         for (int w = 1; w < ns; w *= 2) {
             std::vector<std::pair<int, int>> jobs;
             for (int t = 0; t + w < ns; t += 2 * w) jobs.push_back({t, std::min(t + 2 * w, ns)});
