@@ -34,6 +34,7 @@
 #include <mutex>
 #include <string>
 #include <string_view>
+#include <system_error>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -97,7 +98,11 @@ static void cz_parallel(int nt, const std::function<void(int)> &fn)
         }
     };
     std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    try {
+        for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    } catch (const std::system_error &) {   // no more threads: the rest run here
+        for (int t = (int)th.size() + 1; t < nt; ++t) guarded(t);
+    }
     guarded(0);
     for (auto &x : th) x.join();
     if (err) std::rethrow_exception(err);

@@ -43,6 +43,7 @@
 #include <functional>
 #include <memory>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -182,7 +183,11 @@ void text_info(const TextBuf &d, int64_t *info)
         }
         cnt[t] = k;
     };
-    for (int t = 1; t < nt; ++t) th.emplace_back(count, t);
+    try {
+        for (int t = 1; t < nt; ++t) th.emplace_back(count, t);
+    } catch (const std::system_error &) {   // no more threads: the rest run here
+        for (int t = (int)th.size() + 1; t < nt; ++t) count(t);
+    }
     count(0);
     for (auto &x : th) x.join();
     int64_t nl = 0;

@@ -40,6 +40,7 @@
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -231,7 +232,11 @@ bool threads_run(int nt, const std::function<void(int)> &fn)
         return !failed;
     }
     std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    try {
+        for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    } catch (const std::system_error &) {   // no more threads: the rest run here
+        for (int t = (int)th.size() + 1; t < nt; ++t) guarded(t);
+    }
     guarded(0);
     for (auto &x : th) x.join();
     return !failed;

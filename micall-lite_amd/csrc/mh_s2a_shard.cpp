@@ -39,6 +39,7 @@
 #include <functional>
 #include <mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -127,7 +128,11 @@ void run_threads(int nt, const std::function<void(int)> &fn)
         }
     };
     std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    try {
+        for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    } catch (const std::system_error &) {   // no more threads: the rest run here
+        for (int t = (int)th.size() + 1; t < nt; ++t) guarded(t);
+    }
     guarded(0);
     for (auto &x : th) x.join();
     if (err) std::rethrow_exception(err);
