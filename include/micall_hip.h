@@ -587,12 +587,26 @@ int mh_gotoh_align_batch(mh_ctx *ctx, int count, const char *const *seq1,
                          const char *alphabet, const int *matrix, char *const *out1,
                          char *const *out2, const int *cap, int *score, int *status);
 
+/* The consensus-distance filter's edit distances (remap.py:247-251) as one
+ * device batch: alignment t is mh_gotoh_align_batch's (seq1[t], seq2[t])
+ * and dist[t] = Levenshtein.distance(extract_relevant_seed(aligned seq2,
+ * aligned seq1), text[t]) (remap.py:129-138, :251), computed on the device
+ * from the alignment (k_lev_prep, k_lev); only the distances are fetched.
+ * status[t] = 0, -1 where the traceback fails, or -2 where the aligned
+ * seq2 has no non-gap column (the reference's match is None); score[t] is
+ * the alignment score.  Replaces remap.py:249-251's per-pair aligner.align +
+ * extract_relevant_seed + Levenshtein.distance calls. */
+int mh_gotoh_distance_batch(mh_ctx *ctx, int count, const char *const *seq1,
+                            const char *const *seq2, const char *const *text, int gop, int gep,
+                            int is_global, const char *alphabet, const int *matrix, int *dist,
+                            int *score, int *status);
+
 /* Per-kernel device time measured with HIP events on the context's stream
  * (k_seed, k_dp, k_pair, k_pileup).  mh_profile(ctx, 1) enables and resets. */
 int mh_profile(mh_ctx *ctx, int enable);
 int mh_profile_get(mh_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 
-/* Unit-cost edit distance (Levenshtein.distance, remap.py:250). */
+/* Unit-cost edit distance (Levenshtein.distance, remap.py:251). */
 int mh_levenshtein(const char *a, const char *b);
 /* out[t] = mh_levenshtein(a[t], b[t]) for count pairs, on host threads. */
 int mh_levenshtein_batch(int count, const char *const *a, const char *const *b, int *out);

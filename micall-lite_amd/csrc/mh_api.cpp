@@ -2741,6 +2741,19 @@ int mh_gotoh_align_batch(mh_ctx *ctx, int count, const char *const *seq1,
                            out2, cap, score, status);
 }
 
+int mh_gotoh_distance_batch(mh_ctx *ctx, int count, const char *const *seq1, const char *const *seq2,
+                            const char *const *text, int gop, int gep, int is_global,
+                            const char *alphabet, const int *matrix, int *dist, int *score, int *status)
+{
+    if (!ctx || count < 0 || (count > 0 && (!seq1 || !seq2 || !text || !dist || !score || !status)) ||
+        !alphabet || !matrix)
+        return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    return run_gotoh_distance_batch(*c, count, seq1, seq2, text, gop, gep, is_global, alphabet, matrix,
+                                    dist, score, status);
+}
+
 int mh_levenshtein_batch(int count, const char *const *a, const char *const *b, int *out)
 {
     if (count < 0 || (count > 0 && (!a || !b || !out))) return -3;

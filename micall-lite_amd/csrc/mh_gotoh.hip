@@ -725,6 +725,197 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh_tb(const GotohArgs *bat
     }
 }
 
+// ---------------------------------------------------------------------------
+// The distance filter's edit distances on the device (remap.py:249-251):
+// Levenshtein.distance(extract_relevant_seed(aligned_conseq, aligned_seed),
+// relevant) for every alignment of the batch, straight from k_gotoh_tb's
+// output (nothing is fetched but one distance per alignment).
+//
+// The aligned strings are stored back to front, and an edit distance is the
+// same for both strings reversed, so the pattern is taken as it lies: seq1's
+// characters over the span of seq2's non-gap columns, gaps dropped
+// (k_lev_prep), and the text (relevant) is uploaded reversed.  k_lev runs the
+// bit-parallel recurrence of Myers / Hyyro (as mh_levenshtein on the host):
+// pattern rows in 64-row blocks, one block per lane, 64 blocks per strip,
+// one wave per strip; lane l is at column t - l at step t, so the horizontal
+// delta into its block's top row is the lane above's output of the step
+// before, one DPP lane shift.  A strip's last lane hands its bottom deltas
+// to the next strip through global memory in blocks of GBLK columns, each
+// word carrying a tag bit, and strips are taken by ticket in their
+// dependency order (as k_gotoh_fwd's).  The last block is padded to 64 rows
+// that match every character; their vertical deltas in the last column are
+// taken off the bottom score at the end.
+// ---------------------------------------------------------------------------
+struct LevArgs {
+    const char *o1, *o2;   // k_gotoh_tb's aligned seq1 / seq2 (reversed)
+    const int *result;     // k_gotoh_tb's [status, score, length]
+    const uint8_t *text;   // the second string, reversed (n bytes)
+    int n;
+    uint8_t *pcode;        // the pattern's codes (<= m + 64 bytes)
+    int *bnd;              // (strips - 1) x n boundary words: delta bits | 4
+    int *meta;             // [0] pattern length, [1] status
+    int *res;              // [0] status, [1] score, [2] distance
+};
+
+struct LevBatch {
+    const LevArgs *args;
+    const int2 *tick;      // (alignment, strip) in ticket order
+    int strips;
+    int *ticket;
+    const uint8_t *lut;    // character -> 1 + alphabet code, 0 (none)
+    int ncodes;            // alphabet size + 1
+    int *flags;            // [0] a wait timed out
+    unsigned long long wait_ticks;
+};
+
+constexpr int LEV_STRIP_ROWS = 64 * 64;
+
+// One wave per alignment: the span of seq2's non-gap columns, and seq1's
+// characters over it without gaps, as codes.
+__global__ __launch_bounds__(64) void k_lev_prep(LevBatch B)
+{
+    const LevArgs A = B.args[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int status = A.result[0], score = A.result[1], len = A.result[2];
+    typedef const __attribute__((address_space(1))) char gcc;
+    const gcc *o1 = (const gcc *)A.o1, *o2 = (const gcc *)A.o2;
+    int lo = len, hi = -1;
+    if (status == 0) {
+        for (int k0 = 0; k0 < len; k0 += 64) {
+            const int k = k0 + lane;
+            const uint64_t b = __builtin_amdgcn_ballot_w64(k < len && o2[k] != '-');
+            if (b) { lo = k0 + __builtin_ctzll(b); break; }
+        }
+        for (int k0 = len - 1; k0 >= 0; k0 -= 64) {
+            const int k = k0 - lane;
+            const uint64_t b = __builtin_amdgcn_ballot_w64(k >= 0 && o2[k] != '-');
+            if (b) { hi = k0 - __builtin_ctzll(b); break; }
+        }
+    }
+    int base = 0;
+    if (status == 0 && lo <= hi) {
+        const uint64_t below = lane ? ~0ull >> (64 - lane) : 0ull;
+        for (int k0 = lo; k0 <= hi; k0 += 64) {
+            const int k = k0 + lane;
+            const char c = k <= hi ? o1[k] : '-';
+            const uint64_t b = __builtin_amdgcn_ballot_w64(c != '-');
+            if (c != '-') A.pcode[base + __builtin_popcountll(b & below)] = B.lut[(uint8_t)c];
+            base += __builtin_popcountll(b);
+        }
+    }
+    if (lane == 0) {
+        // -2: no non-gap column (extract_relevant_seed's match is None)
+        const int st = status == -4 ? -4 : status ? -1 : lo > hi ? -2 : 0;
+        A.meta[0] = base;
+        A.meta[1] = st;
+        A.res[0] = st;
+        A.res[1] = score;
+        A.res[2] = base == 0 ? A.n : A.n == 0 ? base : -1;
+    }
+}
+
+// the Myers / Hyyro step of one 64-row block at one column: eq the block's
+// match bits for the column's character, (hp, hn) the horizontal delta into
+// its top row; returns the delta out of its bottom row (bit 0: +1, bit 1: -1)
+__device__ __forceinline__ int lev_step(uint64_t eq, int hin, uint64_t &Pv, uint64_t &Mv)
+{
+    const uint64_t hp = (uint64_t)(hin & 1), hn = (uint64_t)((hin >> 1) & 1);
+    const uint64_t Xv = eq | Mv;
+    const uint64_t Eq = eq | hn;
+    const uint64_t Xh = (((Eq & Pv) + Pv) ^ Pv) | Eq;
+    uint64_t Ph = Mv | ~(Xh | Pv);
+    uint64_t Mh = Pv & Xh;
+    const int out = (int)(Ph >> 63) | (int)(Mh >> 63) << 1;
+    Ph = (Ph << 1) | hp;
+    Mh = (Mh << 1) | hn;
+    Pv = Mh | ~(Xv | Ph);
+    Mv = Ph & Xv;
+    return out;
+}
+
+__global__ __launch_bounds__(64) void k_lev(LevBatch B)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lsm[];
+    uint64_t *peq = (uint64_t *)lsm;                  // [code][lane]
+    uint8_t *lut = lsm + (size_t)B.ncodes * 64 * 8;   // 256 bytes
+    const int lane = threadIdx.x;
+    __shared__ int tk;
+    if (lane == 0) tk = atomicAdd(B.ticket, 1);
+    for (int x = lane; x < 256; x += 64) lut[x] = B.lut[x];
+    __syncthreads();
+    const int u = tk;
+    if (u >= B.strips) return;
+    int t, s;
+    {
+        const int2 x = B.tick[u];
+        t = __builtin_amdgcn_readfirstlane(x.x);
+        s = __builtin_amdgcn_readfirstlane(x.y);
+    }
+    const LevArgs A = B.args[t];
+    const int mlen = __builtin_amdgcn_readfirstlane(A.meta[0]);
+    const int st = __builtin_amdgcn_readfirstlane(A.meta[1]);
+    const int n = A.n;
+    if (st != 0 || mlen == 0 || n == 0) return;   // k_lev_prep wrote the result
+    const int nb = (mlen + 63) / 64, nstr = (nb + 63) / 64;
+    if (s >= nstr) return;
+    const bool last = s == nstr - 1;
+    const int b = 64 * s + lane;                      // this lane's block
+    const bool blk = b < nb;
+    const int lastw = (nb - 1 - 64 * s) < 63 ? nb - 1 - 64 * s : 63;
+    const int pad = nb * 64 - mlen;
+    const uint64_t padmask = (b == nb - 1 && pad) ? ~0ull << (64 - pad) : 0ull;
+    // match bits of this lane's block, one word per code (lane-private column)
+    for (int c = 0; c < B.ncodes; ++c) peq[c * 64 + lane] = padmask;
+    if (blk) {
+        const int r_end = mlen - 64 * b < 64 ? mlen - 64 * b : 64;
+        for (int r = 0; r < r_end; ++r) peq[A.pcode[64 * b + r] * 64 + lane] |= 1ull << r;
+    }
+    uint64_t Pv = ~0ull, Mv = 0;
+    int cc = 0, hout = 0, acc = 0, pr = 0;
+    const int *prev = s > 0 ? A.bnd + (size_t)(s - 1) * n : nullptr;
+    int *mine = last ? nullptr : A.bnd + (size_t)s * n;
+    const int steps = n + (last ? lastw : 63);
+    typedef const __attribute__((address_space(1))) uint8_t gbyte;
+    const gbyte *text = (const gbyte *)A.text;
+    // the next block's text codes and boundary words, loaded one block ahead
+    int cw_next = lane < GBLK && lane < n ? lut[text[lane]] : 0;
+    int bw_next = prev && lane < GBLK && lane < n ? dev_load(prev + lane) : 0;
+    for (int t0 = 0; t0 < steps; t0 += GBLK) {
+        const int cw = cw_next;
+        int bw = bw_next;
+        const bool need = lane < GBLK && t0 + lane < n;
+        if (prev && __builtin_amdgcn_ballot_w64(need && !(bw & 4)))
+            bw = poll_block(prev + t0, lane, need, [](int v) { return (v & 4) != 0; }, B.flags, B.wait_ticks);
+        const int t1 = t0 + GBLK + lane;
+        cw_next = lane < GBLK && t1 < n ? lut[text[t1]] : 0;
+        bw_next = prev && lane < GBLK && t1 < n ? dev_load(prev + t1) : 0;
+        unroll<GBLK>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const int j = t0 + q - lane;
+            cc = from_prev_lane(__builtin_amdgcn_readlane(cw, q), cc);
+            const int h0 = prev ? (__builtin_amdgcn_readlane(bw, q) & 3) : 1;
+            const int hin = from_prev_lane(h0, hout);
+            const uint64_t eq = peq[cc * 64 + lane];
+            if (blk && j >= 0 && j < n) {
+                hout = lev_step(eq, hin, Pv, Mv);
+                if (last && lane == lastw) acc += (hout & 1) - (hout >> 1);
+            } else {
+                hout = 0;
+            }
+            if (!last) pr = shift_in63(hout, pr);
+        });
+        if (!last) {
+            // lanes 64 - GBLK .. 63 hold lane 63's outputs of the block's steps
+            const int col = t0 + (lane - (64 - GBLK)) - 63;
+            if (lane >= 64 - GBLK && col >= 0 && col < n) dev_store(mine + col, (pr & 3) | 4);
+        }
+    }
+    if (last && lane == lastw) {
+        const int corr = __builtin_popcountll(Pv & padmask) - __builtin_popcountll(Mv & padmask);
+        A.res[2] = nb * 64 + acc - corr;
+    }
+}
+
 static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // Per alignment: an "io" block (codes, strings, output strings, result: what
@@ -768,11 +959,16 @@ static size_t gotoh_work_bytes(int m, int n)
 // alignment must not pin device memory for the rest of the session).
 constexpr size_t GOTOH_KEEP_BYTES = (size_t)1 << 30;
 
+// lev_text non-null: the filter's edit distances instead of the aligned
+// strings (out1 / out2 / cap unused): lev_dist[t] = the distance between
+// alignment t's relevant seed and lev_text[t] (status -2: no non-gap column)
 static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char *const *s2, int gop,
                             int gep, int is_global, const char *alphabet, const int *matrix,
                             char *const *out1, char *const *out2, const int *cap, int *score,
-                            int *status, unsigned long long wait_ticks)
+                            int *status, unsigned long long wait_ticks, const char *const *lev_text,
+                            int *lev_dist)
 {
+    const bool lev = lev_text != nullptr;
     const int L = (int)strlen(alphabet);
     if (count < 0 || L == 0 || L > 64) { set_error("mh_gotoh_align: bad arguments"); return -3; }
     if (count == 0) return 0;
@@ -783,28 +979,32 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     for (int x = 0; x < L * L; ++x) mat_max = std::max<int64_t>(mat_max, std::abs((int64_t)matrix[x]));
     if (mat_max > 127) { set_error("mh_gotoh_align: scores outside -127..127"); return -3; }
     if (gop < 0 || gep < 0 || gop > (1 << 16) || gep > (1 << 16)) { set_error("mh_gotoh_align: bad gap penalties"); return -3; }
-    std::vector<int> ms(count), ns(count);
+    std::vector<int> ms(count), ns(count), nt(count, 0), lstr(count, 0);
     std::vector<size_t> io(count + 1, 0), oo(count + 1, 0), work(count + 1, 0);
     for (int t = 0; t < count; ++t)
-        if (!s1[t] || !s2[t] || !out1[t] || !out2[t]) { set_error("mh_gotoh_align: null argument"); return -3; }
+        if (!s1[t] || !s2[t] || (lev ? !lev_text[t] : !out1[t] || !out2[t])) {
+            set_error("mh_gotoh_align: null argument");
+            return -3;
+        }
     // lengths and the alphabet check of every alignment on host threads; the
     // first offending character (by alignment, then position) is reported
     std::vector<int> badc(count, -1);
     gotoh_par(count, [&](int t) {
         ms[t] = (int)strlen(s1[t]);
         ns[t] = (int)strlen(s2[t]);
+        if (lev) nt[t] = (int)strlen(lev_text[t]);
         for (int i = 0; i < ms[t] && badc[t] < 0; ++i)
             if (code[(unsigned char)s1[t][i]] < 0) badc[t] = (unsigned char)s1[t][i];
         for (int j = 0; j < ns[t] && badc[t] < 0; ++j)
             if (code[(unsigned char)s2[t][j]] < 0) badc[t] = (unsigned char)s2[t][j];
     });
     for (int t = 0; t < count; ++t) {
-        if (ms[t] == 0 || ns[t] == 0 || cap[t] < ms[t] + ns[t] + 1) {
+        if (ms[t] == 0 || ns[t] == 0 || (!lev && cap[t] < ms[t] + ns[t] + 1)) {
             set_error("mh_gotoh_align: bad arguments (alignment %d)", t);
             return -3;
         }
         if (badc[t] >= 0) { set_error("mh_gotoh_align: '%c' not in alphabet", badc[t]); return -3; }
-        io[t + 1] = io[t] + gotoh_in_bytes(ms[t], ns[t], L);
+        io[t + 1] = io[t] + gotoh_in_bytes(ms[t], ns[t], L) + (lev ? align16((size_t)nt[t] + 16) : 0);
         oo[t + 1] = oo[t] + gotoh_out_bytes(ms[t], ns[t]);
         // boundary cells carry R and P in 26 bits (k_gotoh_fwd rp_pack)
         if ((int64_t)(ms[t] + ns[t] + 2) * (mat_max + gop + gep + 1) >= ((int64_t)1 << 24)) {
@@ -815,7 +1015,11 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
             set_error("mh_gotoh_align: alignment %d too large (%d x %d)", t, ms[t], ns[t]);
             return -3;
         }
-        work[t + 1] = work[t] + gotoh_work_bytes(ms[t], ns[t]);
+        // the pattern is at most seq1 long: its strips of LEV_STRIP_ROWS rows
+        lstr[t] = (ms[t] + LEV_STRIP_ROWS - 1) / LEV_STRIP_ROWS;
+        work[t + 1] = work[t] + gotoh_work_bytes(ms[t], ns[t]) +
+                      (lev ? align16((size_t)ms[t] + 64) + align16(sizeof(int) * (size_t)(lstr[t] - 1) * nt[t]) + 16
+                           : 0);
     }
     // strips in ticket order, the longest remaining critical path first:
     // strip q of an alignment (q-th in its pass's dependency order) still has
@@ -844,12 +1048,34 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
         for (size_t x = 0; x < idx.size(); ++x) sorted[x] = tick[(size_t)idx[x]];
         tick.swap(sorted);
     }
+    // the edit distances' strips, in the same critical-path order
+    std::vector<int2> ltick;
+    if (lev) {
+        std::vector<int64_t> lkey;
+        for (int t = 0; t < count; ++t)
+            for (int q = 0; q < lstr[t]; ++q) {
+                ltick.push_back(make_int2(t, q));
+                lkey.push_back((int64_t)(lstr[t] - 1 - q) * GLAG + nt[t] + 64);
+            }
+        std::vector<int> idx(ltick.size());
+        for (size_t x = 0; x < idx.size(); ++x) idx[x] = (int)x;
+        std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return lkey[(size_t)x] > lkey[(size_t)y]; });
+        std::vector<int2> sorted(ltick.size());
+        for (size_t x = 0; x < idx.size(); ++x) sorted[x] = ltick[(size_t)idx[x]];
+        ltick.swap(sorted);
+    }
     const size_t sz_mat = align16(sizeof(int) * L * L), sz_args = align16(sizeof(GotohArgs) * count);
     const size_t sz_first = align16(sizeof(int2) * tick.size()) + 16;   // the ticket table, the two ticket counters
-    // device buffer: [in blocks][out blocks][matrix][arguments][strip table, tickets][work blocks]
+    // edit distances: [LevArgs][lut][strip table][ticket, flags][results]
+    const size_t sz_lev = lev ? align16(sizeof(LevArgs) * count) + 256 + align16(sizeof(int2) * ltick.size()) + 16 +
+                                    align16((size_t)16 * count)
+                              : 0;
+    // device buffer: [in blocks][out blocks][matrix][arguments][strip table, tickets][edit distances][work blocks]
     const size_t off_out = io[count];
     const size_t off_mat = off_out + oo[count], off_args = off_mat + sz_mat, off_first = off_args + sz_args,
-                 off_work = off_first + sz_first;
+                 off_lev = off_first + sz_first, off_work = off_lev + sz_lev;
+    const size_t off_lut = off_lev + align16(sizeof(LevArgs) * count), off_ltick = off_lut + 256,
+                 off_lctr = off_ltick + align16(sizeof(int2) * ltick.size()), off_lres = off_lctr + 16;
     const size_t total = off_work + work[count] + 256;
     std::lock_guard<std::mutex> guard(c.gotoh_mutex);   // the scratch is per context
     if (c.gotoh_cap < total) {
@@ -865,6 +1091,7 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     std::unique_ptr<char[]> img(new char[io[count] + 16]);
     std::unique_ptr<char[]> oimg(new char[oo[count] + 16]);
     std::vector<GotohArgs> args(count);
+    std::vector<LevArgs> largs(lev ? count : 0);
     gotoh_par(count, [&](int t) {
         const int m = ms[t], n = ns[t];
         size_t o = io[t], q = off_out + oo[t], w = off_work + work[t];
@@ -907,6 +1134,21 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
         A.result = (int *)(d + ores);
         A.m = m; A.n = n; A.L = L; A.mat = (const int *)(d + off_mat);
         A.u = gep; A.v = gop; A.is_global = is_global ? 1 : 0;
+        if (lev) {
+            LevArgs &E = largs[t];
+            const int nx = nt[t];
+            const size_t otx = take_io((size_t)nx + 16);
+            for (int j = 0; j < nx; ++j) img[otx + j] = lev_text[t][nx - 1 - j];
+            E.o1 = A.out1;
+            E.o2 = A.out2;
+            E.result = A.result;
+            E.text = (const uint8_t *)(d + otx);
+            E.n = nx;
+            E.pcode = (uint8_t *)take_w((size_t)m + 64);
+            E.bnd = (int *)take_w(sizeof(int) * (size_t)(lstr[t] - 1) * nx);
+            E.meta = (int *)take_w(16);
+            E.res = (int *)(d + off_lres + (size_t)16 * t);
+        }
     });
     hipStream_t st = c.stream;
     MH_HIP(hipMemsetAsync(d + off_work, 0, work[count], st));
@@ -917,6 +1159,14 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     MH_HIP(hipMemcpyAsync(d + off_args, args.data(), sizeof(GotohArgs) * count,
                           hipMemcpyHostToDevice, st));
     MH_HIP(hipMemcpyAsync(d + off_first, tick.data(), sizeof(int2) * tick.size(), hipMemcpyHostToDevice, st));
+    if (lev) {
+        uint8_t lut[256];
+        for (int k = 0; k < 256; ++k) lut[k] = (uint8_t)(code[k] + 1);
+        MH_HIP(hipMemsetAsync(d + off_lctr, 0, 16, st));
+        MH_HIP(hipMemcpyAsync(d + off_lev, largs.data(), sizeof(LevArgs) * count, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(d + off_lut, lut, 256, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(d + off_ltick, ltick.data(), sizeof(int2) * ltick.size(), hipMemcpyHostToDevice, st));
+    }
     const int strips = (int)tick.size();
     GotohStrips S;
     S.args = (const GotohArgs *)(d + off_args);
@@ -954,8 +1204,31 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     hipLaunchKernelGGL(k_gotoh_tb, dim3((unsigned)count), dim3(GOTOH_THREADS), TB_LDS, st,
                        (const GotohArgs *)(d + off_args));
     prof_end(c, pg);
+    std::vector<int> lres(lev ? 4 * (size_t)count : 0);
+    int lflag = 0;
+    if (lev) {
+        LevBatch LB;
+        LB.args = (const LevArgs *)(d + off_lev);
+        LB.tick = (const int2 *)(d + off_ltick);
+        LB.strips = (int)ltick.size();
+        LB.ticket = (int *)(d + off_lctr);
+        LB.flags = (int *)(d + off_lctr + 4);
+        LB.lut = (const uint8_t *)(d + off_lut);
+        LB.ncodes = L + 1;
+        LB.wait_ticks = wait_ticks;
+        const int pl = prof_begin(c, "k_lev");
+        hipLaunchKernelGGL(k_lev_prep, dim3((unsigned)count), dim3(64), 0, st, LB);
+        if (LB.strips > 0)
+            hipLaunchKernelGGL(k_lev, dim3((unsigned)LB.strips), dim3(64), (size_t)LB.ncodes * 64 * 8 + 256, st, LB);
+        prof_end(c, pl);
+    }
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(oimg.get(), d + off_out, oo[count], hipMemcpyDeviceToHost, st);
+    if (lev) {
+        if (e == hipSuccess) e = hipMemcpyAsync(lres.data(), d + off_lres, sizeof(int) * lres.size(), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&lflag, d + off_lctr + 4, sizeof(int), hipMemcpyDeviceToHost, st);
+    } else if (e == hipSuccess) {
+        e = hipMemcpyAsync(oimg.get(), d + off_out, oo[count], hipMemcpyDeviceToHost, st);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "k_gotoh");
     if (S.stamps) {   // header: strips, blocks per strip; then fwd and bwd stamps
@@ -969,7 +1242,19 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
             fclose(f);
         }
     }
-    for (int t = 0; t < count; ++t) {
+    if (lev) {
+        for (int t = 0; t < count; ++t) {
+            const int *r = &lres[(size_t)4 * t];
+            if (r[0] == -4 || lflag) {
+                set_error("k_gotoh: a strip's wait for its neighbour timed out (alignment %d)", t);
+                return -4;
+            }
+            status[t] = r[0];
+            score[t] = r[1];
+            lev_dist[t] = r[0] ? 0 : r[2];
+        }
+    }
+    for (int t = 0; t < count && !lev; ++t) {
         const GotohArgs &A = args[t];
         int res[3];
         memcpy(res, &oimg[(const char *)A.result - d - off_out], sizeof(res));
@@ -1002,11 +1287,28 @@ int run_gotoh_batch(Ctx &c, int count, const char *const *s1, const char *const 
                                          ? (unsigned long long)c.test_caps.gotoh_wait_ticks
                                          : GWAIT_TICKS;
     int st = gotoh_batch_once(c, count, s1, s2, gop, gep, is_global, alphabet, matrix, out1, out2,
-                              cap, score, status, first);
+                              cap, score, status, first, nullptr, nullptr);
     if (st != -4) return st;
     ++c.retries[RETRY_GOTOH_WAIT];
     return gotoh_batch_once(c, count, s1, s2, gop, gep, is_global, alphabet, matrix, out1, out2,
-                            cap, score, status, GWAIT_TICKS);
+                            cap, score, status, GWAIT_TICKS, nullptr, nullptr);
+}
+
+// The batch's alignments reduced on the device to the filter's edit
+// distances (k_lev_prep, k_lev); the same timeout-and-retry as above.
+int run_gotoh_distance_batch(Ctx &c, int count, const char *const *s1, const char *const *s2,
+                             const char *const *text, int gop, int gep, int is_global,
+                             const char *alphabet, const int *matrix, int *dist, int *score, int *status)
+{
+    const unsigned long long first = c.test_caps.gotoh_wait_ticks > 0
+                                         ? (unsigned long long)c.test_caps.gotoh_wait_ticks
+                                         : GWAIT_TICKS;
+    int st = gotoh_batch_once(c, count, s1, s2, gop, gep, is_global, alphabet, matrix, nullptr, nullptr,
+                              nullptr, score, status, first, text, dist);
+    if (st != -4) return st;
+    ++c.retries[RETRY_GOTOH_WAIT];
+    return gotoh_batch_once(c, count, s1, s2, gop, gep, is_global, alphabet, matrix, nullptr, nullptr,
+                            nullptr, score, status, GWAIT_TICKS, text, dist);
 }
 
 int run_gotoh(Ctx &c, const char *s1, const char *s2, int gop, int gep, int is_global,

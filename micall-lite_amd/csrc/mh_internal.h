@@ -237,6 +237,10 @@ int run_gotoh_batch(struct Ctx &c, int count, const char *const *s1, const char 
                     int gop, int gep, int is_global, const char *alphabet, const int *matrix,
                     char *const *out1, char *const *out2, const int *cap, int *score,
                     int *status);
+int run_gotoh_distance_batch(struct Ctx &c, int count, const char *const *s1, const char *const *s2,
+                             const char *const *text, int gop, int gep, int is_global,
+                             const char *alphabet, const int *matrix, int *dist, int *score,
+                             int *status);
 
 // Read names (QNAMEs) in one byte pool: name r is bytes off[r] .. off[r + 1]
 // (one allocation for millions of names instead of one string each).

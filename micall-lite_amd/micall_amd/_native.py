@@ -109,6 +109,8 @@ def _declare(L):
         'mh_gotoh_align_batch': ([_P, ctypes.c_int, _P, _P, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_int, ctypes.c_char_p, _P, _P, _P, _P, _P, _P],
                                  ctypes.c_int),
+        'mh_gotoh_distance_batch': ([_P, ctypes.c_int, _P, _P, _P, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_char_p, _P, _P, _P, _P], ctypes.c_int),
         'mh_levenshtein_batch': ([ctypes.c_int, _P, _P, _P], ctypes.c_int),
         'mh_pileup_event_bytes': ([_P, _P, _P], ctypes.c_int),
         'mh_pileup_events_export': ([_P, _P, _P], ctypes.c_int),
@@ -1152,6 +1154,40 @@ class Context:
               'mh_gotoh_align_batch')
         return [RuntimeError('Traceback failed, try local alignment') if status[t] else
                 (o1[t].value.decode(), o2[t].value.decode(), int(score[t])) for t in range(n)]
+
+    def gotoh_distance_many(self, triples, gop, gep, is_global, alphabet, matrix):
+        """The consensus-distance filter's edit distances (remap.py:249-251)
+        for [(seq1, seq2, text)]: Levenshtein distance between text and the
+        part of seq1 under seq2's aligned span (extract_relevant_seed), each
+        alignment as gotoh_align_many's, all reduced on the device
+        (mh_gotoh_distance_batch).  A pair whose traceback fails gives
+        RuntimeError in its place; one whose aligned seq2 has no non-gap
+        column AttributeError, as the reference's re.match gives None."""
+        n = len(triples)
+        if n == 0:
+            return []
+        s1 = (ctypes.c_char_p * n)(*[a.encode() for a, _, _ in triples])
+        s2 = (ctypes.c_char_p * n)(*[b.encode() for _, b, _ in triples])
+        tx = (ctypes.c_char_p * n)(*[c.encode() for _, _, c in triples])
+        dist = np.zeros(n, dtype=np.int32)
+        score = np.zeros(n, dtype=np.int32)
+        status = np.zeros(n, dtype=np.int32)
+        mat = np.ascontiguousarray(matrix, dtype=np.int32)
+        check(lib().mh_gotoh_distance_batch(self.h, n, ctypes.cast(s1, ctypes.c_void_p),
+                                            ctypes.cast(s2, ctypes.c_void_p),
+                                            ctypes.cast(tx, ctypes.c_void_p), gop, gep, int(is_global),
+                                            alphabet.encode(), _ptr(mat), _ptr(dist), _ptr(score),
+                                            _ptr(status)),
+              'mh_gotoh_distance_batch')
+        out = []
+        for t in range(n):
+            if status[t] == -1:
+                out.append(RuntimeError('Traceback failed, try local alignment'))
+            elif status[t]:
+                out.append(AttributeError("'NoneType' object has no attribute 'start'"))
+            else:
+                out.append(int(dist[t]))
+        return out
 
 
 def _plain_fd(handle):

@@ -242,9 +242,9 @@ def filter_conseqs(ctx, pile, order, new_conseqs, seeds, filter_coverage, distan
     the edit distance to the part of each seed they cover decides: a
     consensus stays when its own seed is no farther than the nearest other
     one.  If none stays, the one with the most merged pairs does.  All the
-    K x K alignments are one device launch (mh_gotoh_align_batch), the edit
-    distances one host call spread over threads."""
-    from . import _native
+    K x K alignments and their edit distances are one device batch
+    (mh_gotoh_distance_batch): the relevant seed is cut from each alignment
+    and measured on the device, and only the distances come back."""
     if not seeds or len(new_conseqs) < 2:
         return new_conseqs
     index = {pile.refnames[r]: r for r in order}
@@ -260,19 +260,15 @@ def filter_conseqs(ctx, pile, order, new_conseqs, seeds, filter_coverage, distan
     # each sequence cleaned once (K seeds, K consensuses; not K x K times)
     clean_seed = {n: clean_sequence(seeds[n]) for n in names}
     clean_rel = {n: clean_sequence(relevant[n]) for n in relevant}
-    aligned = ctx.gotoh_align_many(
-        [(clean_seed[seed_name], clean_rel[name]) for name, seed_name in jobs],
+    # every distance in one batch: an exact length bound could skip 43 % of
+    # the cells at C4-all size, but in two dependent batches each is as long
+    # as its longest pair (profiles/diag/filter_timing.py, lev_pruned_ms)
+    dists = ctx.gotoh_distance_many(
+        [(clean_seed[seed_name], clean_rel[name], relevant[name]) for name, seed_name in jobs],
         FILTER_GOP, FILTER_GEP, True, HYPHY_NUC_ALPHABET, HYPHY_NUC)
-    for result in aligned:
+    for result in dists:
         if isinstance(result, Exception):
             raise result
-    # every distance in one host batch: an exact length bound could skip 43 %
-    # of the cells at C4-all size, but in two dependent batches each is as
-    # long as its longest pair, and the two took 31 ms against 24 ms
-    # (profiles/diag/filter_timing.py, lev_pruned_ms)
-    dists = _native.levenshtein_many(
-        [(extract_relevant_seed(a_conseq, a_seed), relevant[name])
-         for (name, _seed), (a_seed, a_conseq, _score) in zip(jobs, aligned)])
     per_name = {}
     for (name, seed_name), d in zip(jobs, dists):
         per_name.setdefault(name, []).append((seed_name, d))

@@ -117,7 +117,7 @@ def gotoh_align(seq1, seq2, gop, gep, is_global, alphabet, matrix):
 
 
 def levenshtein(a, b):
-    """Unit-cost edit distance (Levenshtein.distance at remap.py:250)."""
+    """Unit-cost edit distance (Levenshtein.distance at remap.py:251)."""
     return lib().og_levenshtein(a.encode(), b.encode())
 
 

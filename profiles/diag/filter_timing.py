@@ -1,7 +1,9 @@
 """profiles/diag/filter_timing.py -- where the consensus-distance filter's
 time goes when the consensuses are long (C4 'all': 24 consensuses up to
 SARS-CoV-2's 30 kb): the K x K Gotoh batch on the device, the relevant-seed
-extraction, and the K x K edit distances.  Consensuses are the seeds with
+extraction, and the K x K edit distances on the host, against the one
+device batch the filter now makes of all three (device_batch_ms, checked
+equal).  Consensuses are the seeds with
 10 % substitutions (the bench's sample genomes).
     python3 profiles/diag/filter_timing.py [repeats]"""
 import json
@@ -57,7 +59,13 @@ for rep in range(reps):
     rest = [k for k, (n, s) in enumerate(jobs) if k not in dist and bound[k] <= near[n]]
     dist.update(zip(rest, _native.levenshtein_many([lev_in[k] for k in rest])))
     t6 = time.perf_counter()
-    print(json.dumps({'rep': rep, 'pairs': len(jobs),
+    # the filter's own call: alignments, relevant seeds and distances in one
+    # device batch (mh_gotoh_distance_batch)
+    dd = ctx.gotoh_distance_many([(a, b, cons[n]) for (a, b), (n, _s) in zip(inputs, jobs)],
+                                 FILTER_GOP, FILTER_GEP, True, HYPHY_NUC_ALPHABET, HYPHY_NUC)
+    t7 = time.perf_counter()
+    assert dd == d, 'device distances differ from the host ones'
+    print(json.dumps({'rep': rep, 'pairs': len(jobs), 'device_batch_ms': round(1e3 * (t7 - t6), 1),
                       'gotoh_cells_G': round(sum(len(a) * len(b) for a, b in inputs) / 1e9, 2),
                       'lev_cells_G': round(sum(len(a) * len(b) for a, b in lev_in) / 1e9, 2),
                       'clean_ms': round(1e3 * (t1 - t0), 1), 'gotoh_ms': round(1e3 * (t2 - t1), 1),

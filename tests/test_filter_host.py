@@ -1,10 +1,11 @@
-"""consensus.filter_conseqs (one Gotoh batch, one edit-distance batch, each
-sequence cleaned once) against the reference's loop over every seed
+"""consensus.filter_conseqs (one batch of alignments and edit distances,
+each sequence cleaned once) against the reference's loop over every seed
 (remap.py:231-262: the first other seed in name order with the smallest
 distance) on sets with lengths far apart and with ties (copies of one
 sequence): the same decisions and distance report.  CPU: the
-alignments come from the oracle's Gotoh (test infrastructure) through a
-stand-in context; the edit distances from the library's host batch."""
+distances come from the oracle's Gotoh and Levenshtein (test
+infrastructure) through a stand-in context; tests/test_gpu_parity.py holds
+the device batch to the same oracle."""
 import random
 
 import numpy as np
@@ -16,8 +17,14 @@ from micall_amd.consensus import (FILTER_GEP, FILTER_GOP, HYPHY_NUC, HYPHY_NUC_A
 
 
 class _OracleAligner:
-    def gotoh_align_many(self, pairs, gop, gep, is_global, alphabet, matrix):
-        return [oracle.gotoh_align(a, b, gop, gep, is_global, alphabet, list(matrix)) for a, b in pairs]
+    """Stands in for the context's gotoh_distance_many (the device batch):
+    the oracle's alignment, relevant seed and edit distance per triple."""
+    def gotoh_distance_many(self, triples, gop, gep, is_global, alphabet, matrix):
+        out = []
+        for a, b, text in triples:
+            a_seed, a_conseq, _ = oracle.gotoh_align(a, b, gop, gep, is_global, alphabet, list(matrix))
+            out.append(oracle.levenshtein(extract_relevant_seed(a_conseq, a_seed), text))
+        return out
 
 
 class _FullCoverage:

@@ -433,6 +433,56 @@ def test_gotoh_profile_in_global_memory(ctx, is_global):
         assert g == oracle.gotoh_align(a, b, 15, 3, is_global, alpha, mat)
 
 
+def _filter_distance_oracle(seq1, seq2, text, alpha, mat):
+    from micall_amd.consensus import extract_relevant_seed
+    a_seed, a_conseq, _ = oracle.gotoh_align(seq1, seq2, 15, 3, True, alpha, mat)
+    return oracle.levenshtein(extract_relevant_seed(a_conseq, a_seed), text)
+
+
+def test_gotoh_distance_batch(ctx):
+    """mh_gotoh_distance_batch (the filter's alignment, relevant seed and
+    edit distance on the device, remap.py:249-251) against the oracle's
+    Gotoh + extract_relevant_seed + Levenshtein: patterns of one block, of
+    exactly 64 blocks (one strip), one row into a second strip and three
+    strips (the strips hand their bottom deltas on through global memory),
+    texts shorter than a block of columns, with characters outside the
+    alphabet, empty, and the filter's own shape (a seed against a mutated
+    part of itself and against an unrelated seed)."""
+    rng = np.random.default_rng(31)
+    mat, alpha = [5, -4, -4, -4, 0, -4, 5, -4, -4, 0, -4, -4, 5, -4, 0, -4, -4, -4, 5, 0,
+                  0, 0, 0, 0, 0], 'ACGT?'
+    rand = lambda k: ''.join(rng.choice(list('ACGT'), size=k))
+    mut = lambda x, r: synth.sample_genome(x, rng, r, r / 10).tobytes().decode()
+    long1 = ''.join(mut(POL, 0.05) for _ in range(4))[:9000]
+    triples = [
+        (POL, mut(POL, 0.1)[200:2900], None),              # the filter's shape
+        (POL, mut(SEEDS['HIV1B-env-seed'], 0.05)[:1500], None),
+        (rand(30), rand(25), None),                         # one block
+        (long1[:4096], mut(long1[:4096], 0.05), None),      # exactly one strip
+        (long1[:4097], mut(long1[:4097], 0.05), None),      # one row into strip 2
+        (long1, mut(long1, 0.08)[100:8700], None),          # three strips
+        (long1[3000:3900], mut(long1[3000:3900], 0.1)[:20], None),   # text < 32 columns
+        (POL[:700].replace('A', '?', 9), POL[100:600], 'xx' + POL[100:600].lower()[:50] + '-N?'),
+        (POL[:500], POL[50:400], ''),                        # empty text
+    ]
+    jobs = [(a, b, b if t is None else t) for a, b, t in triples]
+    got = ctx.gotoh_distance_many(jobs, 15, 3, True, alpha, mat)
+    for (a, b, t), g in zip(jobs, got):
+        assert g == _filter_distance_oracle(a, b, t, alpha, mat), (len(a), len(b), len(t))
+
+
+def test_gotoh_distance_batch_no_nongap_column(ctx):
+    """An aligned seq2 that is all gap characters ('-' in the alphabet) has
+    no relevant span: AttributeError, as the reference's re.match gives
+    None; the other pairs of the batch are unaffected."""
+    mat = [5, -4, -4, -4, 0, -4, 5, -4, -4, 0, -4, -4, 5, -4, 0, -4, -4, -4, 5, 0,
+           0, 0, 0, 0, 0]
+    got = ctx.gotoh_distance_many([(POL[:80], '---', 'ACG'), (POL[:80], POL[10:60], POL[10:60])],
+                                  15, 3, True, 'ACGT-', mat)
+    assert isinstance(got[0], AttributeError)
+    assert got[1] == _filter_distance_oracle(POL[:80], POL[10:60], POL[10:60], 'ACGT-', mat)
+
+
 @pytest.mark.parametrize('is_global', [True, False])
 def test_gotoh_long_seq1_global_memory_variant(ctx, is_global):
     """seq1 too long for the rolling diagonals in LDS (k_gotoh<false>: they
