@@ -871,7 +871,6 @@ __global__ __launch_bounds__(64) void k_lev(LevBatch B)
         for (int r = 0; r < r_end; ++r) peq[A.pcode[64 * b + r] * 64 + lane] |= 1ull << r;
     }
     uint64_t Pv = ~0ull, Mv = 0;
-    int cc = 0, hout = 0, acc = 0, pr = 0;
     const int *prev = s > 0 ? A.bnd + (size_t)(s - 1) * n : nullptr;
     int *mine = last ? nullptr : A.bnd + (size_t)s * n;
     const int steps = n + (last ? lastw : 63);
@@ -879,7 +878,13 @@ __global__ __launch_bounds__(64) void k_lev(LevBatch B)
     const gbyte *text = (const gbyte *)A.text;
     // the next block's text codes and boundary words, loaded one block ahead
     int cw_next = lane < GBLK && lane < n ? lut[text[lane]] : 0;
-    int bw_next = prev && lane < GBLK && lane < n ? dev_load(prev + lane) : 0;
+    // (strip 0: every column's delta into row 0 is +1)
+    int bw_next = !prev ? 1 : lane < GBLK && lane < n ? dev_load(prev + lane) : 0;
+    // cc: the code of this lane's column; eqn: the match bits of the next
+    // step, read from LDS a step ahead (the column's code is known then)
+    int cc = lane == 0 ? __builtin_amdgcn_readlane(cw_next, 0) : 0;
+    uint64_t eqn = peq[cc * 64 + lane];
+    int hout = 0, acc = 0, pr = 0;
     for (int t0 = 0; t0 < steps; t0 += GBLK) {
         const int cw = cw_next;
         int bw = bw_next;
@@ -888,28 +893,46 @@ __global__ __launch_bounds__(64) void k_lev(LevBatch B)
             bw = poll_block(prev + t0, lane, need, [](int v) { return (v & 4) != 0; }, B.flags, B.wait_ticks);
         const int t1 = t0 + GBLK + lane;
         cw_next = lane < GBLK && t1 < n ? lut[text[t1]] : 0;
-        bw_next = prev && lane < GBLK && t1 < n ? dev_load(prev + t1) : 0;
-        unroll<GBLK>([&](auto qc) {
-            constexpr int q = decltype(qc)::value;
-            const int j = t0 + q - lane;
-            cc = from_prev_lane(__builtin_amdgcn_readlane(cw, q), cc);
-            const int h0 = prev ? (__builtin_amdgcn_readlane(bw, q) & 3) : 1;
-            const int hin = from_prev_lane(h0, hout);
-            const uint64_t eq = peq[cc * 64 + lane];
-            if (blk && j >= 0 && j < n) {
-                hout = lev_step(eq, hin, Pv, Mv);
-                if (last && lane == lastw) acc += (hout & 1) - (hout >> 1);
-            } else {
-                hout = 0;
-            }
-            if (!last) pr = shift_in63(hout, pr);
-        });
+        bw_next = !prev ? 1 : lane < GBLK && t1 < n ? dev_load(prev + t1) : 0;
+        // A block where some lane is off its columns (the first 64 steps,
+        // the last ones) keeps such a lane's state as it is; elsewhere every
+        // lane steps (a lane past the pattern only feeds lanes past it, and
+        // a lane's output only reaches the next lane at the same column, so
+        // off-grid outputs never meet on-grid cells).
+        auto block = [&](auto edge_c) {
+            constexpr bool EDGE = decltype(edge_c)::value;
+            unroll<GBLK>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                const uint64_t eq = eqn;
+                const int nx = q + 1 < GBLK ? __builtin_amdgcn_readlane(cw, q + 1 < GBLK ? q + 1 : 0)
+                                            : __builtin_amdgcn_readlane(cw_next, 0);
+                cc = from_prev_lane(nx, cc);
+                eqn = peq[cc * 64 + lane];
+                const int h0 = __builtin_amdgcn_readlane(bw, q) & 3;
+                const int hin = from_prev_lane(h0, hout);
+                if constexpr (EDGE) {
+                    uint64_t nP = Pv, nM = Mv;
+                    hout = lev_step(eq, hin, nP, nM);
+                    const bool act = blk && (uint32_t)(t0 + q - lane) < (uint32_t)n;
+                    Pv = act ? nP : Pv;
+                    Mv = act ? nM : Mv;
+                    acc += act ? (hout & 1) - (hout >> 1) : 0;
+                } else {
+                    hout = lev_step(eq, hin, Pv, Mv);
+                    acc += (hout & 1) - (hout >> 1);
+                }
+                pr = shift_in63(hout, pr);
+            });
+        };
+        if (t0 < 64 || t0 + GBLK > n) block(std::true_type{});
+        else block(std::false_type{});
         if (!last) {
             // lanes 64 - GBLK .. 63 hold lane 63's outputs of the block's steps
             const int col = t0 + (lane - (64 - GBLK)) - 63;
             if (lane >= 64 - GBLK && col >= 0 && col < n) dev_store(mine + col, (pr & 3) | 4);
         }
     }
+    // lane lastw of the last strip: the bottom row's score
     if (last && lane == lastw) {
         const int corr = __builtin_popcountll(Pv & padmask) - __builtin_popcountll(Mv & padmask);
         A.res[2] = nb * 64 + acc - corr;
