@@ -940,9 +940,92 @@ __device__ __forceinline__ void half_max64(long long v, int lane, long long &k0,
 // (tests/test_gpu_parity.py runs both and compares them with the oracle,
 // og_mapper.c:dp_extend).
 // ---------------------------------------------------------------------------
+// Local mode, up to three non-matches on the seeded diagonal (rows x_t,
+// each scoring s_t): the crude bound Gb prices a gapped path as matching
+// every row, and fails as soon as two non-matches cost more than one gap.
+// A gapped path P over rows [a, b] scores at most the seeded diagonal's sum
+// over [a, b] (<= S, and <= U(r, kb) when P ends at (r, kb)) plus, per row it
+// spends off that diagonal, e(i) = ma - s(i, kb) at a non-match row and at
+// most 0 elsewhere (a row on another diagonal scores <= ma; an inserted row
+// 0 before its gap's extension, which the gap's cost holds), minus its gaps.
+// With two or more gaps P gains at most G = sum(ma - s_t) - 2 gmin; with one
+// gap its off-diagonal rows are one interval at an end of [a, b] on one
+// diagonal k (plus the inserted rows of the gap), costing the gap
+// oe + ex (|k - kb| - 1) at least, and a row of the interval where k does
+// not match the read loses ma there (e <= 0 - ma, or 0 - ma inserted).
+// The interval's best sum starts and ends at non-match rows, so it is
+// enough that for every other live diagonal k and every run x_j .. x_l
+// (j < l) of the non-match rows,
+//     sum_{t=j..l} (ma - s_t) - ma * (non-matches of k strictly inside, x_t
+//     excluded) < the gap's cost to k,
+// and G < 2 gmin.  Then no gapped cell reaches its diagonal's ungapped
+// value, so (A) and (C) hold without Gb.  One wave, lane = diagonal as (B).
+template <int LOCAL>
+__device__ bool ungapped_wide(const XView &X, int m, int lane, int hb, int nm, uint32_t xm0, uint32_t xm1,
+                              int oeI, int exI, int oeD, int exD)
+{
+    const uint32_t *tab = X.tab;
+    const uint8_t *refw = X.refw, *rdc = X.rdc;
+    const int ma = 2;
+    const int kb = XCENTER;
+    const int gmin = oeI < oeD ? oeI : oeD;
+    // the non-match rows in order (lane L holds rows 4L .. 4L+3 in xm0 and
+    // 256 + 4L .. in xm1, one bit per byte)
+    int xs[3] = {0, 0, 0}, es[3] = {0, 0, 0};
+    int G = 0;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        if (t < nm) {
+            const int f = xm0 ? 4 * lane + (__builtin_ctz(xm0) >> 3)
+                              : xm1 ? 256 + 4 * lane + (__builtin_ctz(xm1) >> 3) : INT32_MAX;
+            const int x = __builtin_amdgcn_readfirstlane(wave_min(f));
+            if (f == x) {
+                if (xm0) xm0 &= xm0 - 1;
+                else xm1 &= xm1 - 1;
+            }
+            xs[t] = x;
+            es[t] = ma - ((int)__builtin_amdgcn_ubfe(tab[x], (uint32_t)refw[x + kb], 4) - 8);
+            G += es[t];
+            if (es[t] >= gmin) return false;
+        }
+    }
+    if (G >= 2 * gmin) return false;
+    if (nm <= 1) return true;   // one gap already costs more than the one non-match
+    const int x0 = xs[0], x1 = xs[1], xl = xs[nm - 1];
+    // this lane's diagonal: its non-matches in (x0, x1) and (x1, x2)
+    const int kl = lane - 16;
+    const bool other = kl >= XCENTER - hb && kl <= XCENTER + hb && kl != kb;
+    const int kr = other ? kl : 0;
+    const uint8_t *rp = refw + (kr & ~3);
+    const uint32_t sh = (uint32_t)(kr & 3);
+    int c1 = 0, c2 = 0;
+    for (int i = (x0 + 1) & ~3; i < xl; i += 4) {
+        const uint32_t rd = *(const uint32_t *)(rdc + i) & 0x07070707u;
+        const uint32_t rv = __builtin_amdgcn_alignbyte(*(const uint32_t *)(rp + i + 4), *(const uint32_t *)(rp + i), sh) >> 2;
+        uint32_t x = (rd ^ rv) | ((rd | rv) & 0x04040404u);
+        x = (x | (x >> 1) | (x >> 2)) & 0x01010101u;
+        // bytes u with i + u in (lo, hi): from byte lo - i + 1, below byte hi - i
+        auto between = [&](int lo, int hi) {
+            const int a = lo + 1 - i, b = hi - i;
+            const uint32_t ma_ = a <= 0 ? ~0u : a >= 4 ? 0u : ~0u << (8 * a);
+            const uint32_t mb_ = b >= 4 ? ~0u : b <= 0 ? 0u : ~0u >> (8 * (4 - b));
+            return ma_ & mb_;
+        };
+        c1 += __builtin_popcount(x & between(x0, x1));
+        if (nm == 3) c2 += __builtin_popcount(x & between(x1, xl));
+    }
+    const int d = kl > kb ? kl - kb : kb - kl;
+    const int gI = oeI + exI * (d - 1), gD = oeD + exD * (d - 1);
+    const int gc = gI < gD ? gI : gD;
+    bool fail = es[0] + es[1] - ma * c1 >= gc;
+    if (nm == 3)
+        fail = fail || es[1] + es[2] - ma * c2 >= gc || es[0] + es[1] + es[2] - ma * (c1 + c2) >= gc;
+    return __builtin_amdgcn_ballot_w64(other && fail) == 0;
+}
+
 template <int LOCAL>
 __device__ bool dp_ungapped(const XView &X, int m, int lane, int gmin, int hb, int &best, int &bi,
-                            int &bl, int &low)
+                            int &bl, int &low, int oeI, int exI, int oeD, int exD)
 {
     const uint32_t *tab = X.tab;
     const uint8_t *refw = X.refw, *rdc = X.rdc;
@@ -954,8 +1037,10 @@ __device__ bool dp_ungapped(const XView &X, int m, int lane, int gmin, int hb, i
     // or S <= ma * (m - nm).  Lane L compares rows 4L .. 4L+3 (and 256 on),
     // one LDS word of read codes against one of reference codes (the window
     // of lane XCENTER is word-aligned). ----
+    // (local, <= 3 non-matches: ungapped_wide decides where Gb does not)
+    int nm = 0;
+    uint32_t xm0 = 0, xm1 = 0;
     {
-        int nm = 0;
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             const int i = 4 * lane + 256 * r;
@@ -966,11 +1051,14 @@ __device__ bool dp_ungapped(const XView &X, int m, int lane, int gmin, int hb, i
                 x = (x | (x >> 1) | (x >> 2)) & 0x01010101u;
                 if (m - i < 4) x &= (1u << (8 * (m - i))) - 1u;   // rows past the read
                 nm += __builtin_popcount(x);
+                if (r == 0) xm0 = x;
+                else xm1 = x;
             }
         }
         nm = wave_sum(nm);
-        if ((LOCAL ? ma * (m - nm) : -nm) <= gb_max) return false;
     }
+    const bool wide = LOCAL && nm <= 3;
+    if ((LOCAL ? ma * (m - nm) : -nm) <= gb_max && !wide) return false;
     // ---- exact ungapped recurrence on band lane kb: rows 8*lane .. 8*lane+7 ----
     const int r0 = 8 * lane;
     int s[8];
@@ -1021,7 +1109,8 @@ __device__ bool dp_ungapped(const XView &X, int m, int lane, int gmin, int hb, i
         istar = last;
     }
     // (A)
-    if (!(S > gb_max)) return false;
+    const bool crude = S > gb_max;
+    if (!crude && !wide) return false;
     if (LOCAL && S <= 0) return false;
     // (B): non-matches per diagonal, read bytes rdc[i..i+3] against ref bytes
     // refw[i+kl .. i+kl+3] (codes * 4), 16 rows per step with every LDS read
@@ -1079,7 +1168,9 @@ __device__ bool dp_ungapped(const XView &X, int m, int lane, int gmin, int hb, i
         const int r = r0 + u;
         if (r >= lo && r <= istar && r >= GBAR && H[u] < ma * (r + 1) - gmin) bad = true;
     }
-    if (__builtin_amdgcn_ballot_w64(bad) != 0) return false;
+    if (!crude || __builtin_amdgcn_ballot_w64(bad) != 0) {
+        if (!wide || !ungapped_wide<LOCAL>(X, m, lane, hb, nm, xm0, xm1, oeI, exI, oeD, exD)) return false;
+    }
     best = S;
     bi = istar;
     bl = kb;
@@ -1828,7 +1919,8 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         wave_sync();
         int best = 0, bi = 0, bl = 0, low = -1;
         const bool fast = it.m > 2 * GBAR + 8 && it.m <= 512 &&
-                          dp_ungapped<LOCAL>(X, it.m, lane, gmin, it.hb, best, bi, bl, low);
+                          dp_ungapped<LOCAL>(X, it.m, lane, gmin, it.hb, best, bi, bl, low, A.oeI, A.exI,
+                                            A.oeD, A.exD);
         n_fast += fast;
         if (at(1) < n_work) cur = to_item(sid1, cd1, m1, roff1);
         if (at(2) < n_work) {

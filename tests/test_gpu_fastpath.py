@@ -1,7 +1,7 @@
 """The exact ungapped fast path of k_dp (mh_map.hip dp_ungapped) against the
 CPU oracle's full banded DP (og_mapper.c dp_extend): reads built to sit on
-both sides of every bound the fast path relies on -- 0/1/2 mismatches at
-every quality band and at the read ends, local clips, Ns, reference ends,
+both sides of every bound the fast path relies on -- 0/1/2/3 mismatches at
+every quality band and at the read ends, adjacent or a few rows apart, local clips, Ns, reference ends,
 tandem repeats (other diagonals with few mismatches), indels, short and long
 reads.  The launch must take both branches (fast path and full DP) and agree
 with the oracle bit for bit."""
@@ -71,6 +71,29 @@ def _cases():
                 if len(dele) == m:
                     add(dele, q)                                   # deletion
             add(_revcomp(base), q)                          # reverse strand
+    # two or three non-matches on the seeded diagonal (local mode takes these
+    # on the fast path when no other diagonal of the band matches the read
+    # across the span between them well enough to pay for a gap): spread,
+    # adjacent, a few rows apart, at the read ends, with an N, at low and
+    # high quality, and inside tandem repeats (diagonals 3 and 8 away match
+    # every row between the non-matches)
+    for m in (251, 150, 300):
+        st = int(rng.integers(0, len(POL) - m + 1))
+        base = POL[st:st + m]
+        for qc in ('#', '5', 'I'):
+            q = qc * m
+            for at in ((m // 4, m // 2, 3 * m // 4), (m // 2, m // 2 + 1), (m // 2, m // 2 + 2),
+                       (m // 2, m // 2 + 3, m // 2 + 6), (40, 44, 48), (1, m - 2), (0, 4, m - 1),
+                       (m // 3, m // 3 + 4), (60, 70), (60, 61, 62)):
+                add(mutate(base, list(at)), q)
+            nb = mutate(base, [m // 3, 2 * m // 3])
+            add(nb[:m // 2] + 'N' + nb[m // 2 + 1:], q)
+    for m in (251, 120):
+        rep = refs[1]
+        for st in (8, 330, 420):
+            for at in ((m // 2, m // 2 + 5), (m // 3, m // 2, 2 * m // 3), (10, 12), (m // 2, m // 2 + 9)):
+                for qc in ('#', 'I'):
+                    add(mutate(rep[st:st + m], list(at)), qc * m)
     # reference-end overhangs and tandem-repeat reads
     for m in (251, 120):
         add(POL[:m - 30].rjust(m, 'A'), 'G' * m)
