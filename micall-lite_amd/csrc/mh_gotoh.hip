@@ -55,6 +55,7 @@ constexpr int G_HUGE = 1 << 29;
 enum { GA = 1, GB = 2, GC = 4, GD = 8, GE_ = 16, GF = 32, GG = 64 };
 constexpr int GOTOH_THREADS = 1024;        // k_gotoh_tb
 constexpr int GBLK = 32;                   // boundary columns published / awaited at a time
+constexpr int BBLK = 16;                   // the same in k_gotoh_bwd (5 register arrays of it)
 constexpr uint32_t GOOB = 0x80000000u;     // a buffer offset past every plane (planes < 2 GiB)
 // traceback window: TBD anti-diagonals x TBR rows (a window twice as deep
 // in diagonals, for the mostly diagonal paths, measured no faster: the walk
@@ -535,17 +536,17 @@ __global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
     int mine = 0;        // final abc of (i, j + 1): this lane, one step ago
     int dnp = 0;         // final abc of (i + 1, j + 1): the lane below, two steps ago
     int pub = 0;         // lanes 0..31: lane 0's final abc at the block's steps (last step in lane 0)
-    int cx[GBLK], sx[GBLK], nx[GBLK], nsx[GBLK], ox[GBLK];
+    int cx[BBLK], sx[BBLK], nx[BBLK], nsx[BBLK], ox[BBLK];
     // lane q: the plane base of the diagonal of step t0 + q
     auto bases = [&](int t0b) {
         const int64_t sd = (int64_t)s0 - t0b - lane;
         const int64_t sc = sd < 0 ? 0 : sd;
         return (int)(doff_of(sc, m + 1, n + 1) - (sc - (n + 1) > 0 ? sc - (n + 1) : 0));
     };
-    // the plane bytes and lane 63's side bits of steps t0b .. t0b + GBLK - 1
+    // the plane bytes and lane 63's side bits of steps t0b .. t0b + BBLK - 1
     // (a lane off the grid reads some other byte or 0: it only feeds garbage)
     auto load_block = [&](int t0b, int vb, int *dst, int *dsts) {
-        unroll<GBLK>([&](auto qc) {
+        unroll<BBLK>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             dst[q] = __builtin_amdgcn_raw_buffer_load_b8(rbits, plane_off, __builtin_amdgcn_readlane(vb, q), 0);
             dsts[q] = __builtin_amdgcn_raw_buffer_load_b8(rside, side_off + (uint32_t)t0b + q, 0, 0);
@@ -553,22 +554,22 @@ __global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
     };
     int vb = bases(0);
     load_block(0, vb, cx, sx);
-    for (int t0 = 0; t0 <= n + 63; t0 += GBLK) {
-        stamp(S, 1, u, t0 / GBLK, 0);
+    for (int t0 = 0; t0 <= n + 63; t0 += BBLK) {
+        stamp(S, 1, u, t0 / BBLK, 0);
         // the strip below's first row for this block (lane 63's cells below),
         // tagged with the strip below's tag
         int d = 0;
         if (consume && t0 <= n) {
             const int want = (k + 1) % 0xFFFFFF + 1;
-            d = poll_block(under + t0, lane, lane < GBLK && t0 + lane < W1,
+            d = poll_block(under + t0, lane, lane < BBLK && t0 + lane < W1,
                            [&](int w) { return (w >> 8) == want; }, (int *)flags, S.wait_ticks) & 0xFF;
         }
-        if (lane < GBLK) bw[lane] = d;
+        if (lane < BBLK) bw[lane] = d;
 #pragma unroll
-        for (int q = 0; q < GBLK; ++q) asm volatile("; touch %0 %1" : "+v"(cx[q]), "+v"(sx[q]));
-        stamp(S, 1, u, t0 / GBLK, 1);
-        const int vbn = bases(t0 + GBLK);
-        load_block(t0 + GBLK, vbn, nx, nsx);
+        for (int q = 0; q < BBLK; ++q) asm volatile("; touch %0 %1" : "+v"(cx[q]), "+v"(sx[q]));
+        stamp(S, 1, u, t0 / BBLK, 1);
+        const int vbn = bases(t0 + BBLK);
+        load_block(t0 + BBLK, vbn, nx, nsx);
         const int j0 = n + 63 - lane - t0;
         auto step = [&](auto edgec, auto tlc, int q) {
             constexpr bool EDGE = decltype(edgec)::value, TL = decltype(tlc)::value;
@@ -596,24 +597,24 @@ __global__ __launch_bounds__(64) void k_gotoh_bwd(GotohStrips S)
         };
         constexpr std::true_type Y{};
         constexpr std::false_type N{};
-        const bool edge = t0 < 64 || t0 + GBLK - 1 > n;
+        const bool edge = t0 < 64 || t0 + BBLK - 1 > n;
         if (tl) {
-            if (edge) unroll<GBLK>([&](auto qc) { step(Y, Y, decltype(qc)::value); });
-            else unroll<GBLK>([&](auto qc) { step(N, Y, decltype(qc)::value); });
+            if (edge) unroll<BBLK>([&](auto qc) { step(Y, Y, decltype(qc)::value); });
+            else unroll<BBLK>([&](auto qc) { step(N, Y, decltype(qc)::value); });
         } else {
-            if (edge) unroll<GBLK>([&](auto qc) { step(Y, N, decltype(qc)::value); });
-            else unroll<GBLK>([&](auto qc) { step(N, N, decltype(qc)::value); });
+            if (edge) unroll<BBLK>([&](auto qc) { step(Y, N, decltype(qc)::value); });
+            else unroll<BBLK>([&](auto qc) { step(N, N, decltype(qc)::value); });
         }
         // the block's final bytes; the strip's first row (lane 0) to the strip above
-        unroll<GBLK>([&](auto qc) {
+        unroll<BBLK>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             const int j = j0 - q;
             const uint32_t off = (!edge || (uint32_t)j <= (uint32_t)n) ? plane_off : GOOB;
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ox[q], rbits, off, __builtin_amdgcn_readlane(vb, q), 0);
         });
-        const int tp = t0 + (GBLK - 1 - lane) - 63;
-        if (produce && lane < GBLK && tp >= 0 && tp <= n) dev_store(mytop + tp, tagk | pub);
-        unroll<GBLK>([&](auto qc) {
+        const int tp = t0 + (BBLK - 1 - lane) - 63;
+        if (produce && lane < BBLK && tp >= 0 && tp <= n) dev_store(mytop + tp, tagk | pub);
+        unroll<BBLK>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             cx[q] = nx[q];
             sx[q] = nsx[q];
@@ -1203,7 +1204,7 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     if (stamp_path && *stamp_path) {
         int nmx = 0;
         for (int t = 0; t < count; ++t) nmx = std::max(nmx, ns[t]);
-        S.stamp_blocks = (nmx + 64) / GBLK + 2;
+        S.stamp_blocks = (nmx + 64) / BBLK + 2;   // the smaller of the two passes' blocks
         MH_HIP(hipMalloc(&S.stamps, sizeof(unsigned long long) * 4 * strips * S.stamp_blocks));
         MH_HIP(hipMemsetAsync(S.stamps, 0, sizeof(unsigned long long) * 4 * strips * S.stamp_blocks, st));
     }
@@ -1221,7 +1222,7 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     }
     prof_end(c, pf);
     const int pb = prof_begin(c, "k_gotoh_bwd");
-    hipLaunchKernelGGL(k_gotoh_bwd, dim3((unsigned)strips), dim3(64), sizeof(int) * GBLK, st, S);
+    hipLaunchKernelGGL(k_gotoh_bwd, dim3((unsigned)strips), dim3(64), sizeof(int) * BBLK, st, S);
     prof_end(c, pb);
     const int pg = prof_begin(c, "k_gotoh");
     hipLaunchKernelGGL(k_gotoh_tb, dim3((unsigned)count), dim3(GOTOH_THREADS), TB_LDS, st,
