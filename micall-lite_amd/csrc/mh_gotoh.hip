@@ -43,6 +43,7 @@
 #include <algorithm>
 #include <mutex>
 #include <type_traits>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -942,12 +943,28 @@ __global__ __launch_bounds__(64) void k_lev(LevBatch B)
 
 static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// Per alignment: an "io" block (codes, strings, output strings, result: what
-// crosses PCIe) and a "work" block (diagonal buffers, last row / column and
-// the three tie planes, zeroed on the device).
-static size_t gotoh_in_bytes(int m, int n, int L)     // codes, text, score profile (uploaded)
+// Uploaded "in" blocks, one per distinct sequence (a filter batch aligns K
+// consensuses against the same K seeds: K + K blocks, not 2 K^2): seq1's
+// codes and text; seq2's codes, text and score profile.  Per alignment an
+// "out" block (output strings, result: what is fetched) and a "work" block
+// (diagonal buffers, last row / column and the three tie planes, zeroed on
+// the device).
+static size_t gotoh_in1_bytes(int m) { return align16(m + 8) + align16(m + 1); }
+static size_t gotoh_in2_bytes(int n, int L) { return align16(n + 8) + align16(n + 1) + (size_t)L * prof_width(n); }
+
+// distinct pointers of ptr[0 .. count) in first-seen order: idx[t] = the
+// distinct index of ptr[t]; returns the distinct pointers
+static std::vector<const char *> distinct_ptrs(int count, const char *const *ptr, std::vector<int> &idx)
 {
-    return align16(m + 8) + align16(n + 8) + align16(m + 1) + align16(n + 1) + (size_t)L * prof_width(n);
+    std::vector<const char *> uniq;
+    std::unordered_map<const char *, int> at;
+    idx.resize((size_t)count);
+    for (int t = 0; t < count; ++t) {
+        auto it = at.emplace(ptr[t], (int)uniq.size());
+        if (it.second) uniq.push_back(ptr[t]);
+        idx[(size_t)t] = it.first->second;
+    }
+    return uniq;
 }
 
 static size_t gotoh_out_bytes(int m, int n)            // aligned strings, result (fetched)
@@ -971,11 +988,12 @@ static void gotoh_par(int count, const std::function<void(int)> &fn)
     for (auto &x : th) x.join();
 }
 
+// the zeroed work block (without the tie planes, which k_gotoh_fwd writes
+// in full -- every cell (i <= m, j <= n) -- before anything reads them)
 static size_t gotoh_work_bytes(int m, int n)
 {
     const size_t strips = (size_t)(m + 1 + 63) / 64;
-    return align16(sizeof(int) * (m + 2)) + align16(sizeof(int) * (n + 2)) +
-           align16((size_t)(m + 2) * (n + 2)) + align16(8 * strips * (n + 1)) +
+    return align16(sizeof(int) * (m + 2)) + align16(sizeof(int) * (n + 2)) + align16(8 * strips * (n + 1)) +
            align16(sizeof(int) * strips * (n + 1)) + align16(strips * (n + 1)) + 16;
 }
 
@@ -1004,31 +1022,57 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     if (mat_max > 127) { set_error("mh_gotoh_align: scores outside -127..127"); return -3; }
     if (gop < 0 || gep < 0 || gop > (1 << 16) || gep > (1 << 16)) { set_error("mh_gotoh_align: bad gap penalties"); return -3; }
     std::vector<int> ms(count), ns(count), nt(count, 0), lstr(count, 0);
-    std::vector<size_t> io(count + 1, 0), oo(count + 1, 0), work(count + 1, 0);
+    std::vector<size_t> oo(count + 1, 0), work(count + 1, 0), planes(count + 1, 0);
     for (int t = 0; t < count; ++t)
         if (!s1[t] || !s2[t] || (lev ? !lev_text[t] : !out1[t] || !out2[t])) {
             set_error("mh_gotoh_align: null argument");
             return -3;
         }
-    // lengths and the alphabet check of every alignment on host threads; the
-    // first offending character (by alignment, then position) is reported
-    std::vector<int> badc(count, -1);
-    gotoh_par(count, [&](int t) {
-        ms[t] = (int)strlen(s1[t]);
-        ns[t] = (int)strlen(s2[t]);
-        if (lev) nt[t] = (int)strlen(lev_text[t]);
-        for (int i = 0; i < ms[t] && badc[t] < 0; ++i)
-            if (code[(unsigned char)s1[t][i]] < 0) badc[t] = (unsigned char)s1[t][i];
-        for (int j = 0; j < ns[t] && badc[t] < 0; ++j)
-            if (code[(unsigned char)s2[t][j]] < 0) badc[t] = (unsigned char)s2[t][j];
+    // the distinct sequences (by pointer): lengths and the alphabet check of
+    // each on host threads; the first offending character (by alignment,
+    // then position) is reported
+    std::vector<int> i1, i2, i3;
+    const std::vector<const char *> u1 = distinct_ptrs(count, s1, i1), u2 = distinct_ptrs(count, s2, i2);
+    const std::vector<const char *> u3 = lev ? distinct_ptrs(count, lev_text, i3) : std::vector<const char *>();
+    const int n1 = (int)u1.size(), n2 = (int)u2.size(), n3 = (int)u3.size();
+    std::vector<int> len1(n1), len2(n2), len3(n3), bad1(n1, -1), bad2(n2, -1);
+    gotoh_par(n1 + n2 + n3, [&](int x) {
+        if (x < n1) {
+            const char *p = u1[x];
+            len1[x] = (int)strlen(p);
+            for (int i = 0; i < len1[x] && bad1[x] < 0; ++i)
+                if (code[(unsigned char)p[i]] < 0) bad1[x] = (unsigned char)p[i];
+        } else if (x < n1 + n2) {
+            const int y = x - n1;
+            const char *p = u2[y];
+            len2[y] = (int)strlen(p);
+            for (int j = 0; j < len2[y] && bad2[y] < 0; ++j)
+                if (code[(unsigned char)p[j]] < 0) bad2[y] = (unsigned char)p[j];
+        } else {
+            len3[x - n1 - n2] = (int)strlen(u3[x - n1 - n2]);
+        }
     });
+    std::vector<int> badc(count, -1);
+    for (int t = 0; t < count; ++t) {
+        ms[t] = len1[i1[t]];
+        ns[t] = len2[i2[t]];
+        if (lev) nt[t] = len3[i3[t]];
+        badc[t] = bad1[i1[t]] >= 0 ? bad1[i1[t]] : bad2[i2[t]];
+    }
+    // in blocks: [distinct seq1][distinct seq2][distinct texts]
+    std::vector<size_t> io1(n1 + 1, 0), io2(n2 + 1, 0), io3(n3 + 1, 0);
+    for (int x = 0; x < n1; ++x) io1[x + 1] = io1[x] + gotoh_in1_bytes(len1[x]);
+    io2[0] = io1[n1];
+    for (int y = 0; y < n2; ++y) io2[y + 1] = io2[y] + gotoh_in2_bytes(len2[y], L);
+    io3[0] = io2[n2];
+    for (int z = 0; z < n3; ++z) io3[z + 1] = io3[z] + align16((size_t)len3[z] + 16);
+    const size_t io_total = io3[n3];
     for (int t = 0; t < count; ++t) {
         if (ms[t] == 0 || ns[t] == 0 || (!lev && cap[t] < ms[t] + ns[t] + 1)) {
             set_error("mh_gotoh_align: bad arguments (alignment %d)", t);
             return -3;
         }
         if (badc[t] >= 0) { set_error("mh_gotoh_align: '%c' not in alphabet", badc[t]); return -3; }
-        io[t + 1] = io[t] + gotoh_in_bytes(ms[t], ns[t], L) + (lev ? align16((size_t)nt[t] + 16) : 0);
         oo[t + 1] = oo[t] + gotoh_out_bytes(ms[t], ns[t]);
         // boundary cells carry R and P in 26 bits (k_gotoh_fwd rp_pack)
         if ((int64_t)(ms[t] + ns[t] + 2) * (mat_max + gop + gep + 1) >= ((int64_t)1 << 24)) {
@@ -1044,6 +1088,7 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
         work[t + 1] = work[t] + gotoh_work_bytes(ms[t], ns[t]) +
                       (lev ? align16((size_t)ms[t] + 64) + align16(sizeof(int) * (size_t)(lstr[t] - 1) * nt[t]) + 16
                            : 0);
+        planes[t + 1] = planes[t] + align16((size_t)(ms[t] + 2) * (ns[t] + 2));
     }
     // strips in ticket order, the longest remaining critical path first:
     // strip q of an alignment (q-th in its pass's dependency order) still has
@@ -1095,12 +1140,13 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
                                     align16((size_t)16 * count)
                               : 0;
     // device buffer: [in blocks][out blocks][matrix][arguments][strip table, tickets][edit distances][work blocks]
-    const size_t off_out = io[count];
+    // [tie planes]
+    const size_t off_out = io_total;
     const size_t off_mat = off_out + oo[count], off_args = off_mat + sz_mat, off_first = off_args + sz_args,
-                 off_lev = off_first + sz_first, off_work = off_lev + sz_lev;
+                 off_lev = off_first + sz_first, off_work = off_lev + sz_lev, off_planes = off_work + work[count];
     const size_t off_lut = off_lev + align16(sizeof(LevArgs) * count), off_ltick = off_lut + 256,
                  off_lctr = off_ltick + align16(sizeof(int2) * ltick.size()), off_lres = off_lctr + 16;
-    const size_t total = off_work + work[count] + 256;
+    const size_t total = off_planes + planes[count] + 256;
     std::lock_guard<std::mutex> guard(c.gotoh_mutex);   // the scratch is per context
     if (c.gotoh_cap < total) {
         hipFree(c.gotoh_buf);
@@ -1110,45 +1156,69 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
         c.gotoh_cap = total;
     }
     char *d = c.gotoh_buf;
-    // host images of the in blocks (uploaded) and the out blocks (fetched),
-    // each alignment's part built by one host thread
-    std::unique_ptr<char[]> img(new char[io[count] + 16]);
+    hipStream_t st = c.stream;
+    // the device zeroes the work and out areas while the host builds the images
+    // (the tie planes are not zeroed: 16 GB at C4-all size; a test poisons
+    // them instead, MH_GOTOH_POISON_PLANES=1)
+    MH_HIP(hipMemsetAsync(d + off_work, 0, work[count], st));
+    if (const char *pz = getenv("MH_GOTOH_POISON_PLANES"); pz && *pz == '1')
+        MH_HIP(hipMemsetAsync(d + off_planes, 0xA5, planes[count], st));
+    MH_HIP(hipMemsetAsync(d + off_first, 0, sz_first, st));
+    MH_HIP(hipMemsetAsync(d + off_out, 0, oo[count], st));
+    // host images of the in blocks (uploaded) and the out blocks (fetched):
+    // each distinct sequence's block, then each alignment's arguments, built
+    // on host threads
+    std::unique_ptr<char[]> img(new char[io_total + 16]);
     std::unique_ptr<char[]> oimg(new char[oo[count] + 16]);
+    gotoh_par(n1 + n2 + n3, [&](int x) {
+        if (x < n1) {   // seq1: codes, text
+            const int m = len1[x];
+            const char *p = u1[x];
+            char *b = &img[io1[x]];
+            memset(b, 0, io1[x + 1] - io1[x]);
+            for (int i = 0; i < m; ++i) b[i] = (char)code[(unsigned char)p[i]];
+            memcpy(b + align16(m + 8), p, m);
+        } else if (x < n1 + n2) {   // seq2: codes, text, the score profile (prof_width)
+            const int y = x - n1, n = len2[y];
+            const char *p = u2[y];
+            char *b = &img[io2[y]];
+            memset(b, 0, io2[y + 1] - io2[y]);
+            for (int j = 0; j < n; ++j) b[j] = (char)code[(unsigned char)p[j]];
+            memcpy(b + align16(n + 8), p, n);
+            const int PW = prof_width(n);
+            int8_t *prof = (int8_t *)(b + align16(n + 8) + align16(n + 1));
+            for (int cc = 0; cc < L; ++cc) {
+                int8_t *row = prof + (size_t)cc * PW;
+                for (int j = 1; j <= n; ++j) row[PROF_PAD + j] = (int8_t)matrix[cc * L + code[(unsigned char)p[j - 1]]];
+            }
+        } else {   // the edit distance's text, reversed
+            const int z = x - n1 - n2, nx = len3[z];
+            const char *p = u3[z];
+            char *b = &img[io3[z]];
+            memset(b, 0, io3[z + 1] - io3[z]);
+            for (int j = 0; j < nx; ++j) b[j] = p[nx - 1 - j];
+        }
+    });
     std::vector<GotohArgs> args(count);
     std::vector<LevArgs> largs(lev ? count : 0);
     gotoh_par(count, [&](int t) {
         const int m = ms[t], n = ns[t];
-        size_t o = io[t], q = off_out + oo[t], w = off_work + work[t];
-        memset(&img[o], 0, io[t + 1] - io[t]);
-        auto take_io = [&](size_t sz) { const size_t at = o; o += align16(sz); return at; };
+        size_t q = off_out + oo[t], w = off_work + work[t];
         auto take_out = [&](size_t sz) { const size_t at = q; q += align16(sz); return at; };
         auto take_w = [&](size_t sz) { char *at = d + w; w += align16(sz); return at; };
         GotohArgs &A = args[t];
-        const size_t oa = take_io(m + 8), ob = take_io(n + 8), o1 = take_io(m + 1),
-                     o2 = take_io(n + 1), oprof = take_io((size_t)L * prof_width(n));
+        const size_t oa = io1[i1[t]], o1 = oa + align16(m + 8);
+        const size_t ob = io2[i2[t]], o2 = ob + align16(n + 8), oprof = o2 + align16(n + 1);
         const size_t oo1 = take_out(m + n + 1), oo2 = take_out(m + n + 1), ores = take_out(64);
         A.lastcol = (int *)take_w(sizeof(int) * (m + 2));
         A.lastrow = (int *)take_w(sizeof(int) * (n + 2));
-        const size_t cells = (size_t)(m + 2) * (n + 2);
-        A.bits = (uint8_t *)take_w(cells);
+        A.bits = (uint8_t *)(d + off_planes + planes[t]);
         const size_t strips = (size_t)(m + 1 + 63) / 64;
         A.brow1 = (unsigned long long *)take_w(8 * strips * (n + 1));
         A.brow2 = (int *)take_w(sizeof(int) * strips * (n + 1));
         A.rowde = (uint8_t *)take_w(strips * (n + 1));
         A.flags = (int *)take_w(16);
-        for (int i = 0; i < m; ++i) img[oa + i] = (char)code[(unsigned char)s1[t][i]];
-        for (int j = 0; j < n; ++j) img[ob + j] = (char)code[(unsigned char)s2[t][j]];
-        {   // the score profile (prof_width)
-            const int PW = prof_width(n);
-            for (int cc = 0; cc < L; ++cc) {
-                int8_t *row = (int8_t *)&img[oprof + (size_t)cc * PW];
-                for (int j = 1; j <= n; ++j)
-                    row[PROF_PAD + j] = (int8_t)matrix[cc * L + code[(unsigned char)s2[t][j - 1]]];
-            }
-        }
         A.prof = (const int8_t *)(d + oprof);
-        memcpy(&img[o1], s1[t], m);
-        memcpy(&img[o2], s2[t], n);
         A.a = (const int8_t *)(d + oa);
         A.b = (const int8_t *)(d + ob);
         A.s1 = d + o1;
@@ -1161,8 +1231,7 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
         if (lev) {
             LevArgs &E = largs[t];
             const int nx = nt[t];
-            const size_t otx = take_io((size_t)nx + 16);
-            for (int j = 0; j < nx; ++j) img[otx + j] = lev_text[t][nx - 1 - j];
+            const size_t otx = io3[i3[t]];
             E.o1 = A.out1;
             E.o2 = A.out2;
             E.result = A.result;
@@ -1174,11 +1243,7 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
             E.res = (int *)(d + off_lres + (size_t)16 * t);
         }
     });
-    hipStream_t st = c.stream;
-    MH_HIP(hipMemsetAsync(d + off_work, 0, work[count], st));
-    MH_HIP(hipMemsetAsync(d + off_first, 0, sz_first, st));
-    MH_HIP(hipMemsetAsync(d + off_out, 0, oo[count], st));
-    MH_HIP(hipMemcpyAsync(d, img.get(), io[count], hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(d, img.get(), io_total, hipMemcpyHostToDevice, st));
     MH_HIP(hipMemcpyAsync(d + off_mat, matrix, sizeof(int) * L * L, hipMemcpyHostToDevice, st));
     MH_HIP(hipMemcpyAsync(d + off_args, args.data(), sizeof(GotohArgs) * count,
                           hipMemcpyHostToDevice, st));

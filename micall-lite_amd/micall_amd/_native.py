@@ -1135,8 +1135,9 @@ class Context:
         n = len(pairs)
         if n == 0:
             return []
-        s1 = (ctypes.c_char_p * n)(*[a.encode() for a, _ in pairs])
-        s2 = (ctypes.c_char_p * n)(*[b.encode() for _, b in pairs])
+        enc = _encoder()
+        s1 = (ctypes.c_char_p * n)(*[enc(a) for a, _ in pairs])
+        s2 = (ctypes.c_char_p * n)(*[enc(b) for _, b in pairs])
         caps = np.array([len(a) + len(b) + 1 for a, b in pairs], dtype=np.int32)
         o1 = [ctypes.create_string_buffer(int(c)) for c in caps]
         o2 = [ctypes.create_string_buffer(int(c)) for c in caps]
@@ -1166,9 +1167,10 @@ class Context:
         n = len(triples)
         if n == 0:
             return []
-        s1 = (ctypes.c_char_p * n)(*[a.encode() for a, _, _ in triples])
-        s2 = (ctypes.c_char_p * n)(*[b.encode() for _, b, _ in triples])
-        tx = (ctypes.c_char_p * n)(*[c.encode() for _, _, c in triples])
+        enc = _encoder()
+        s1 = (ctypes.c_char_p * n)(*[enc(a) for a, _, _ in triples])
+        s2 = (ctypes.c_char_p * n)(*[enc(b) for _, b, _ in triples])
+        tx = (ctypes.c_char_p * n)(*[enc(c) for _, _, c in triples])
         dist = np.zeros(n, dtype=np.int32)
         score = np.zeros(n, dtype=np.int32)
         status = np.zeros(n, dtype=np.int32)
@@ -1188,6 +1190,20 @@ class Context:
             else:
                 out.append(int(dist[t]))
         return out
+
+
+def _encoder():
+    """str -> bytes, one bytes object per distinct string of a batch, so the
+    library sees one pointer per distinct sequence (mh_gotoh_align_batch
+    uploads each distinct sequence once)."""
+    seen = {}
+
+    def enc(x):
+        b = seen.get(x)
+        if b is None:
+            b = seen[x] = x.encode()
+        return b
+    return enc
 
 
 def _plain_fd(handle):

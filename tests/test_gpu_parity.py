@@ -483,6 +483,18 @@ def test_gotoh_distance_batch_no_nongap_column(ctx):
     assert got[1] == _filter_distance_oracle(POL[:80], POL[10:60], POL[10:60], 'ACGT-', mat)
 
 
+def test_gotoh_planes_need_no_zeroing(ctx, golden_dir, monkeypatch):
+    """The tie planes are not zeroed between batches (k_gotoh_fwd writes
+    every cell of the grid before anything reads it): with them poisoned
+    first (MH_GOTOH_POISON_PLANES=1) the golden batch, the long-profile
+    batches and the distance batch still equal the oracle."""
+    monkeypatch.setenv('MH_GOTOH_POISON_PLANES', '1')
+    test_gotoh_batch_vs_golden(ctx, golden_dir)
+    test_gotoh_profile_in_global_memory(ctx, True)
+    test_gotoh_profile_in_global_memory(ctx, False)
+    test_gotoh_distance_batch(ctx)
+
+
 @pytest.mark.parametrize('is_global', [True, False])
 def test_gotoh_long_seq1_global_memory_variant(ctx, is_global):
     """seq1 too long for the rolling diagonals in LDS (k_gotoh<false>: they
