@@ -700,11 +700,16 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh_tb(const GotohArgs *bat
             while (i > 0 && j > 0) {
                 const int t = s0 - (i + j), r = i0 - i, c = j0 - j;
                 if (t >= TBD || r >= TBR || c >= TBD) break;
+                // the cell's bits and both characters in one LDS round trip
                 const uint8_t x = win[t * TBR + r];
-                if (x & GA) { r1[len] = wc1[r]; r2[len] = '-'; --i; }
-                else if (x & GB) { r1[len] = '-'; r2[len] = wc2[c]; --j; }
-                else if (x & GC) { r1[len] = wc1[r]; r2[len] = wc2[c]; --i; --j; }
-                else { status = -1; break; }
+                int ch1 = wc1[r], ch2 = wc2[c];
+                asm volatile("" : "+v"(ch1), "+v"(ch2));   // loaded here, not after the test
+                if (!(x & (GA | GB | GC))) { status = -1; break; }
+                const bool up = x & GA, left = !up && (x & GB);
+                r1[len] = left ? '-' : (char)ch1;
+                r2[len] = up ? '-' : (char)ch2;
+                i -= left ? 0 : 1;
+                j -= up ? 0 : 1;
                 ++len;
             }
             tb_ii = i; tb_jj = j; tb_len = len; tb_status = status;
