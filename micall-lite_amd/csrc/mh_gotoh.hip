@@ -26,6 +26,10 @@
 //                f(i,j+1) are never read again (each cell reads its own d/f
 //                before its upper/left neighbour runs) and are dropped
 //   k_gotoh_tb   traceback (:316-438) by one thread over LDS windows.
+//   k_lev_prep / k_lev  (the consensus-distance filter only, remap.py:249-251)
+//                the relevant seed cut from the traceback's output and its
+//                edit distance to the relevant consensus, bit-parallel, in
+//                strips of 64 pattern blocks (see the section below).
 // The planes are stored anti-diagonal-major over the (m+2) x (n+2) grid
 // (doff[s] = first byte of diagonal s, cells by row i), so a step's plane
 // bytes are consecutive; they are written and read through buffer
