@@ -318,6 +318,13 @@ int mh_pileup_fetch(mh_ctx *ctx, int32_t *dense, uint8_t *nflag, uint8_t *dflag,
  * fetching only the references that received pairs keeps a pileup over many
  * seeds from copying every seed's counters. */
 int mh_pileup_fetch_ref(mh_ctx *ctx, int ref, int32_t *dense, uint8_t *nflag, uint8_t *dflag);
+/* The counter rows of n_sel references in one call (one stream
+ * synchronisation): dense / nflag / dflag are the whole (n_refs x cap [x 4])
+ * arrays, and reference refs[k]'s rows 0 .. max_pos - 1 are written (its
+ * positions 1 .. max_pos; past its last counted position every row is zero,
+ * and those rows are left as the caller zeroed them). */
+int mh_pileup_fetch_refs(mh_ctx *ctx, int n_sel, const int32_t *refs, int32_t *dense, uint8_t *nflag,
+                         uint8_t *dflag);
 /* Sparse tokens (base + insertion with len % 3 == 0), aggregated over the
  * pileup: n_events (mh_pileup_dims) distinct (ref, pos, token) entries in
  * (ref, pos, token) order, each with the number of merged pairs that voted

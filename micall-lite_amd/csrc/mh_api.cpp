@@ -2700,6 +2700,35 @@ int mh_pileup_fetch_ref(mh_ctx *ctx, int ref, int32_t *dense, uint8_t *nflag, ui
     return fetch_parts(*c, parts, 3);
 }
 
+int mh_pileup_fetch_refs(mh_ctx *ctx, int n_sel, const int32_t *refs, int32_t *dense, uint8_t *nflag,
+                         uint8_t *dflag)
+{
+    if (!ctx || n_sel < 0 || (n_sel > 0 && (!refs || !dense || !nflag || !dflag))) return -3;
+    CtxEx *c = X(ctx);
+    PileState &P = c->pile;
+    if (!P.dense) { set_error("no pileup (call mh_pileup)"); return -3; }
+    MH_HIP(hipSetDevice(c->device));
+    // each reference's last counted position (landed behind mh_pileup, else fetched)
+    std::vector<int32_t> mx((size_t)std::max(P.n_refs, 1));
+    if (P.land_ok && P.land)
+        std::memcpy(mx.data(), P.land + 16 * (size_t)P.n_refs, sizeof(int32_t) * (size_t)P.n_refs);
+    else
+        MH_HIP(copy_sync(*c, mx.data(), P.max_pos, sizeof(int32_t) * (size_t)P.n_refs, hipMemcpyDeviceToHost));
+    std::vector<FetchPart> parts;
+    parts.reserve(3 * (size_t)n_sel);
+    for (int k = 0; k < n_sel; ++k) {
+        const int r = refs[k];
+        if (r < 0 || r >= P.n_refs) { set_error("mh_pileup_fetch_refs: ref %d out of range", r); return -3; }
+        const int64_t rows = std::min<int64_t>(P.cap, std::max(mx[(size_t)r], 0));
+        if (rows == 0) continue;
+        const int64_t base = (int64_t)r * P.cap;
+        parts.push_back({P.dense + 4 * base, sizeof(int32_t) * 4 * (size_t)rows, dense + 4 * base});
+        parts.push_back({P.nflag + base, (size_t)rows, nflag + base});
+        parts.push_back({P.dflag + base, (size_t)rows, dflag + base});
+    }
+    return parts.empty() ? 0 : fetch_parts(*c, parts.data(), (int)parts.size());
+}
+
 int mh_pileup_events(mh_ctx *ctx, int32_t *ref, int32_t *pos, int32_t *tok_off, int32_t *tok_len,
                      int64_t *count, char *pool)
 {

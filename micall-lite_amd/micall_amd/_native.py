@@ -98,6 +98,7 @@ def _declare(L):
         'mh_pileup_dims': ([_P, ctypes.POINTER(ctypes.c_int), _I32P, _I64P, _I64P], ctypes.c_int),
         'mh_pileup_fetch': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
         'mh_pileup_fetch_ref': ([_P, ctypes.c_int, _P, _P, _P], ctypes.c_int),
+        'mh_pileup_fetch_refs': ([_P, ctypes.c_int, _P, _P, _P, _P], ctypes.c_int),
         'mh_pileup_events': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
         'mh_pileup_exchange_bytes': ([_P, ctypes.c_int, _I64P, _I64P, _I64P], ctypes.c_int),
         'mh_pileup_export': ([_P, ctypes.c_int, _P, ctypes.c_int64, _P, _P, _P], ctypes.c_int),
@@ -1033,10 +1034,10 @@ class Context:
         # pairs (np.zeros leaves the other rows as untouched zero pages)
         check(lib().mh_pileup_fetch(self.h, None, None, None, _ptr(rc), _ptr(fu), _ptr(mp)),
               'mh_pileup_fetch')
-        for r in range(n):
-            if fu[r] >= 0 or mp[r] > 0:
-                check(lib().mh_pileup_fetch_ref(self.h, r, _ptr(dense[r]), _ptr(nflag[r]),
-                                                _ptr(dflag[r])), 'mh_pileup_fetch_ref')
+        sel = np.flatnonzero((fu[:n] >= 0) | (mp[:n] > 0)).astype(np.int32)
+        if len(sel):   # their rows up to their last counted position, one call
+            check(lib().mh_pileup_fetch_refs(self.h, len(sel), _ptr(sel), _ptr(dense), _ptr(nflag),
+                                             _ptr(dflag)), 'mh_pileup_fetch_refs')
         eref = np.zeros(max(ne, 1), dtype=np.int32)
         epos = np.zeros(max(ne, 1), dtype=np.int32)
         eoff = np.zeros(max(ne, 1), dtype=np.int32)

@@ -20,6 +20,8 @@ from collections import Counter
 import numpy as np
 
 BASE_CODES = np.frombuffer(b'ACGT', dtype=np.uint8)
+BASE_INDEX = np.full(256, 255, dtype=np.int64)   # 'A' 'C' 'G' 'T' -> 0..3, else 255
+BASE_INDEX[BASE_CODES] = np.arange(4)
 DASH = ord('-')
 
 # micall/alignment/models/HYPHY_NUC.csv, the model of remap.py:33
@@ -44,9 +46,28 @@ class Pileup:
         self.first_unit = fetched['first_unit']
         self.max_pos = fetched['max_pos']
         self.cap = fetched['cap']
-        self.events = {}
+        # insertion-token events per reference as parallel lists (pos, token,
+        # count); the {ref: {pos: Counter}} view is built only when asked for
+        self._ev = {}
         for r, pos, tok, count in fetched['events']:
-            self.events.setdefault(r, {}).setdefault(pos, Counter())[tok] += count
+            g = self._ev.get(r)
+            if g is None:
+                g = self._ev[r] = ([], [], [])
+            g[0].append(pos)
+            g[1].append(tok)
+            g[2].append(count)
+        self._events = None
+
+    @property
+    def events(self):
+        """{ref: {pos: Counter(token -> merged pairs)}}."""
+        if self._events is None:
+            self._events = {}
+            for r, (ps, ts, cs) in self._ev.items():
+                d = self._events[r] = {}
+                for pos, tok, count in zip(ps, ts, cs):
+                    d.setdefault(pos, Counter())[tok] += count
+        return self._events
 
     def refs_with_reads(self, rank=None):
         """Reference indices that received a merged pair, in refmap order:
@@ -74,8 +95,10 @@ class Pileup:
         df[:n] = self.dflag[r, :n] != 0
         return d, nf, df
 
-    def counter_at(self, r, pos, seed):
-        """The reference's pos_nucs[pos] Counter (for positions with events)."""
+    def counter_at(self, r, pos, seed, events=None):
+        """The reference's pos_nucs[pos] Counter (for positions with events);
+        `events`: that position's (token, count) pairs, if the caller has
+        them (else they come from the events view)."""
         c = Counter()
         if seed and pos <= len(seed):
             c[seed[pos - 1]] = 0
@@ -88,11 +111,15 @@ class Pileup:
                 c['N'] = -1
             if self.dflag[r, pos - 1]:
                 c['-'] = -2
-        c.update(self.events.get(r, {}).get(pos, {}))
+        if events is None:
+            c.update(self.events.get(r, {}).get(pos, {}))
+        else:
+            for token, count in events:
+                c[token] += count
         return c
 
     def has_positive(self, r):
-        return bool(self.dense[r].max() > 0) or bool(self.events.get(r))
+        return bool(self.dense[r].max() > 0) or r in self._ev
 
     def tokens(self, r, seed):
         """Top token per position 1..end-1 (remap.py:318-321), one byte each
@@ -120,31 +147,125 @@ class Pileup:
                 fill[:k] = np.frombuffer(seed[:k].encode('latin-1'), dtype=np.uint8)
             tok[~positive] = fill[~positive]
         longer = {}
-        ev = self.events.get(r, {})
-        positions = [pos for pos in ev if pos <= length]
-        if positions:
-            # the counter rows of every position with tokens in one gather
-            # (counter_at's Counter, built from plain lists)
-            idx = np.asarray(positions, dtype=np.int64) - 1
-            rows, nfs, dfs = d[idx].tolist(), nf[idx].tolist(), df[idx].tolist()
-            nseed = len(seed) if seed else 0
-            for pos, row, n_flag, d_flag in zip(positions, rows, nfs, dfs):
-                c = {seed[pos - 1]: 0} if pos <= nseed else {}   # a plain dict: Counter's
-                for k, v in enumerate(row):                     # update is slow Python
-                    if v:
-                        base = 'ACGT'[k]
-                        c[base] = c.get(base, 0) + v
-                if n_flag:
-                    c['N'] = -1
-                if d_flag:
-                    c['-'] = -2
-                for token, count in ev[pos].items():
-                    c[token] = c.get(token, 0) + count
-                t = find_top_token(c)
-                tok[pos - 1] = ord(t[0]) if t else 0
-                if t and len(t) > 1:
-                    longer[pos - 1] = t
+        if r in self._ev:
+            # a few events: one Counter per position; many: vectorised (its
+            # fixed cost, ~0.2 ms of numpy calls, pays from a few hundred)
+            if len(self._ev[r][0]) < 256:
+                self._event_tokens_loop(r, seed, length, d, nf, df, tok, longer)
+            else:
+                self._event_tokens(r, seed, length, d, nf, df, tok, longer)
         return tok, longer
+
+    def _event_tokens_loop(self, r, seed, length, d, nf, df, tok, longer):
+        """The positions holding insertion tokens, one Counter each
+        (counter_at's, built from plain lists)."""
+        ev = {}
+        for pos, t, k in zip(*self._ev[r]):
+            if pos <= length:
+                e = ev.setdefault(pos, {})
+                e[t] = e.get(t, 0) + k
+        if not ev:
+            return
+        positions = list(ev)
+        idx = np.asarray(positions, dtype=np.int64) - 1
+        rows, nfs, dfs = d[idx].tolist(), nf[idx].tolist(), df[idx].tolist()
+        nseed = len(seed) if seed else 0
+        for pos, row, n_flag, d_flag in zip(positions, rows, nfs, dfs):
+            c = {seed[pos - 1]: 0} if pos <= nseed else {}
+            for k, v in enumerate(row):
+                if v:
+                    base = 'ACGT'[k]
+                    c[base] = c.get(base, 0) + v
+            if n_flag:
+                c['N'] = -1
+            if d_flag:
+                c['-'] = -2
+            for token, count in ev[pos].items():
+                c[token] = c.get(token, 0) + count
+            t = find_top_token(c)
+            tok[pos - 1] = ord(t[0]) if t else 0
+            if t and len(t) > 1:
+                longer[pos - 1] = t
+
+    def _event_tokens(self, r, seed, length, d, nf, df, tok, longer):
+        """find_top_token (remap.py:892-902) at the positions holding
+        insertion tokens, vectorised: the best event token per position
+        (most pairs, then the smallest string) against the best base-like
+        entry (a base with pairs or the seed's prefill, else 'N' -1, else
+        '-' -2).  Positions with a one-character token (which adds to a base's
+        count) or a seed character other than A/C/G/T take the per-position
+        Counter instead."""
+        ps, ts, cs = self._ev[r]
+        pos = np.asarray(ps, dtype=np.int64)
+        cnt = np.asarray(cs, dtype=np.int64)
+        keep = pos <= length
+        if not keep.all():
+            sel = np.flatnonzero(keep)
+            pos, cnt, ts = pos[sel], cnt[sel], [ts[k] for k in sel.tolist()]
+        if len(pos) == 0:
+            return
+        toks = np.array(ts)
+        nseed = len(seed) if seed else 0
+        slow = set()
+        # one entry per (pos, token), counts summed (the device's are
+        # already distinct; a hand-built pileup may repeat one)
+        # (the device hands them over in (pos, token) order: no sort then)
+        if len(pos) > 1 and not ((pos[1:] > pos[:-1]) | ((pos[1:] == pos[:-1]) & (toks[1:] >= toks[:-1]))).all():
+            o2 = np.lexsort((toks, pos))
+            pos, toks, cnt = pos[o2], toks[o2], cnt[o2]
+        new = np.r_[True, (pos[1:] != pos[:-1]) | (toks[1:] != toks[:-1])]
+        if not new.all():
+            starts = np.flatnonzero(new)
+            pos, toks, cnt = pos[starts], toks[starts], np.add.reduceat(cnt, starts)
+        # per position (a run of equal pos), the best token: the most pairs,
+        # then the smallest string -- the first index reaching the run's max,
+        # tokens being sorted within the run
+        starts = np.flatnonzero(np.r_[True, pos[1:] != pos[:-1]])
+        run = np.repeat(np.arange(len(starts)), np.diff(np.r_[starts, len(pos)]))
+        gmax = np.maximum.reduceat(cnt, starts)
+        at = np.where(cnt == gmax[run], np.arange(len(pos)), len(pos))
+        best = np.minimum.reduceat(at, starts)
+        upos = pos[starts]
+        # token lengths from the code points (a str array pads with 0)
+        tlen = (toks.view(np.uint32).reshape(len(toks), -1) != 0).sum(axis=1)
+        short = tlen < 2
+        if short.any():
+            slow.update(pos[short].tolist())
+        sb = np.full(len(upos), 255, dtype=np.int64)   # the seed's base at the position
+        if nseed:
+            ins = upos <= nseed
+            sc = np.frombuffer(seed.encode('latin-1'), dtype=np.uint8)
+            sb[ins] = BASE_INDEX[sc[upos[ins] - 1]]
+            odd = ins & (sb == 255)
+            if odd.any():
+                slow.update(upos[odd].tolist())
+        ecnt, etok = cnt[best], toks[best]
+        idx = upos - 1
+        rows = d[idx]                       # (k, 4) counts A C G T
+        present = (rows > 0) | (sb[:, None] == np.arange(4)[None, :])
+        vals = np.where(present, rows, np.iinfo(np.int64).min)
+        bk = np.argmax(vals, axis=1)        # ties: the first of A < C < G < T
+        has_base = present.any(axis=1)
+        bcnt = np.where(has_base, vals[np.arange(len(upos)), bk], 0)
+        nfl, dfl = nf[idx], df[idx]
+        # no base-like entry: 'N' (-1) beats '-' (-2); neither: the event wins
+        bcnt = np.where(has_base, bcnt, np.where(nfl, -1, np.where(dfl, -2, np.iinfo(np.int64).min)))
+        btok = np.where(has_base, np.array(list('ACGT'))[bk], np.where(nfl, 'N', np.where(dfl, '-', '')))
+        ev_wins = (ecnt > bcnt) | ((ecnt == bcnt) & (etok < btok))
+        win = np.where(ev_wins, etok, btok)
+        # first characters as code points ('' -> 0), the longer tokens by index
+        tok[idx] = win.astype('<U1').view(np.uint32)
+        multi = np.flatnonzero(np.where(ev_wins, tlen[best], 1) > 1)
+        for k, t in zip(multi.tolist(), win[multi].tolist()):
+            longer[int(idx[k])] = t
+        for p in slow:
+            at = np.flatnonzero(pos == p)
+            c = self.counter_at(r, p, seed, events=zip(toks[at].tolist(), cnt[at].tolist()))
+            t = find_top_token(c)
+            tok[p - 1] = ord(t[0]) if t else 0
+            longer.pop(p - 1, None)
+            if t and len(t) > 1:
+                longer[p - 1] = t
 
     def position_sums(self, r, seed, length):
         """sum(counts[pos].values()) for pos 1..length (remap.py:236-238)."""

@@ -79,6 +79,56 @@ def test_tokens_and_assembly_match_the_loop(rs, seed_len):
     assert _assemble(tok, longer) == _assemble_loop(want)
 
 
+@pytest.mark.parametrize('rs', range(20))
+def test_event_positions_match_the_counter(rs):
+    """Positions with insertion tokens (resolved vectorised in
+    Pileup._event_tokens) against counter_at + find_top_token: many tokens
+    per position with tied counts, tokens tying the best base both ways
+    ('AC' < 'C', 'A' < 'AC'), positions with no base at all (only 'N' / '-'
+    flags, or nothing), one-character tokens, repeated (pos, token) entries,
+    seeds with N / R / Y, and tokens past the reference's end."""
+    rng = np.random.default_rng(100 + rs)
+    length, cap = 120, 130
+    dense = np.zeros((1, cap, 4), dtype=np.int32)
+    nflag = np.zeros((1, cap), dtype=np.uint8)
+    dflag = np.zeros((1, cap), dtype=np.uint8)
+    for p in range(length):
+        k = int(rng.integers(0, 5))
+        if k < 3:
+            dense[0, p] = rng.integers(0, 4, size=4)
+        elif k == 3:
+            nflag[0, p] = rng.integers(0, 2)
+            dflag[0, p] = rng.integers(0, 2)
+    events = []
+    for p in rng.choice(np.arange(1, length + 6), size=40, replace=False):
+        for _ in range(int(rng.integers(1, 5))):
+            n = int(rng.choice([1, 2, 3, 4]))
+            tok = ''.join(rng.choice(list('ACGT'), size=n))
+            events.append((0, int(p), tok, int(rng.integers(1, 5))))
+    if events and rs % 3 == 0:
+        events.append(events[0])            # a repeated (pos, token)
+    if rs % 2:
+        events.sort(key=lambda e: (e[1], e[2]))   # the device's (pos, token) order
+    seed = ''.join(rng.choice(list('ACGTNRY'), size=int(rng.integers(0, 140)))) or None
+    fetched = dict(dense=dense, nflag=nflag, dflag=dflag, read_counts=np.array([5]),
+                   first_unit=np.array([0]), max_pos=np.array([length]), cap=cap, events=events)
+    pile = Pileup(fetched, ['r'])
+    want = _tokens_per_position(pile, 0, seed)
+    for vectorised in (False, True):
+        # tokens() for the positions without events, then each event path
+        # over the event positions
+        tok = pile.tokens(0, seed)[0].copy()
+        longer = {}
+        end = len(tok)
+        d, nf, df = pile._slice(0, end)
+        run = pile._event_tokens if vectorised else pile._event_tokens_loop
+        run(0, seed, end, d, nf, df, tok, longer)
+        got = [None if b == 0 else chr(b) for b in tok]
+        for i, t in longer.items():
+            got[i] = t
+        assert got == want, vectorised
+
+
 def test_assembly_edge_cases():
     def run(tokens):
         tok = np.array([0 if t is None else ord(t[0]) for t in tokens], dtype=np.uint8)
