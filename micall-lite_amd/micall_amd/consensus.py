@@ -149,8 +149,8 @@ class Pileup:
         longer = {}
         if r in self._ev:
             # a few events: one Counter per position; many: vectorised (its
-            # fixed cost, ~0.2 ms of numpy calls, pays from a few hundred)
-            if len(self._ev[r][0]) < 256:
+            # fixed cost, ~0.1 ms of numpy calls, pays from ~150 events)
+            if len(self._ev[r][0]) < 160:
                 self._event_tokens_loop(r, seed, length, d, nf, df, tok, longer)
             else:
                 self._event_tokens(r, seed, length, d, nf, df, tok, longer)
