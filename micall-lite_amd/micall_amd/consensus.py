@@ -85,7 +85,10 @@ class Pileup:
         return c
 
     def _slice(self, r, length):
-        """dense, nflag, dflag for positions 1..length (zero past cap)."""
+        """dense, nflag, dflag for positions 1..length (zero past cap):
+        views of the fetched rows when they reach that far."""
+        if length <= self.cap:
+            return self.dense[r, :length], self.nflag[r, :length] != 0, self.dflag[r, :length] != 0
         n = min(length, self.cap)
         d = np.zeros((length, 4), dtype=np.int64)
         nf = np.zeros(length, dtype=bool)
