@@ -104,39 +104,55 @@ def host_cpus():
             'share_threads': share, 'cgroup_cpu_quota': quota}
 
 
-def cpu_baseline(reads, quals):
-    """The CPU oracle's step (C restatement: og_map + og_rows_from_alns +
-    og_pileup_mt, OpenMP over read pairs; O(reference length) consensus in
-    Python) on a bounded sample of the same workload -- the first pairs of
-    the bench's own input -- on every host core (sched_getaffinity) and again
-    on the box's CPU share (OMP_NUM_THREADS).  The reads are packed before
-    the clock starts, so the timed region holds no per-read Python: the
-    device-resident step's CPU equivalent.  Returns (baseline dict, the
-    oracle's records and consensus of the last run for the parity leg)."""
+def _oracle_step(reads, quals, paired, threads, iterations=1, forced=False):
+    """One run of the CPU oracle's step (cpu_pipeline.timed_step) on the
+    given units: (seconds, the prepared reads with .result)."""
     import cpu_pipeline
     from micall_amd import projects
     cfg = projects.load_default()
     seed_set = cfg.seed_sequences()
     groups = {k: cfg.getSeedGroup(k) for k in seed_set}
-    sample_pairs = reads.shape[0] // 2
-    prep = cpu_pipeline.Prepared.from_arrays(reads, quals, True)
+    prep = cpu_pipeline.Prepared.from_arrays(reads, quals, paired)
+    _, secs = cpu_pipeline.timed_step(seed_set, cfg.all_region_sequences(), groups, prep, threads,
+                                      max_iterations=iterations,
+                                      min_iterations=iterations if forced else None)
+    return secs, prep
+
+
+def cpu_baseline(reads, quals, paired=True, iterations=1, forced=False, workload='2x251 pol'):
+    """The CPU oracle's step (C restatement: og_map + og_rows_from_alns +
+    og_pileup_mt, OpenMP over read pairs; O(reference length) consensus in
+    Python; the consensus-distance filter's K x K og_gotoh_align +
+    og_levenshtein on host threads) on a bounded sample of the same workload
+    -- the first units of the bench's own input -- on every host core
+    (sched_getaffinity) and again on the box's CPU share (OMP_NUM_THREADS).
+    The reads are packed before the clock starts, so the timed region holds
+    no per-read Python: the device-resident step's CPU equivalent.  Returns
+    (baseline dict, the oracle's records and consensus of the last run for
+    the parity leg)."""
+    units = reads.shape[0] // 2 if paired else reads.shape[0]
+    per_unit = 2 if paired else 1
     cpus = host_cpus()
     runs = {}
+    prep = None
     for threads in sorted({cpus['sched_getaffinity'], cpus['share_threads']}, reverse=True):
-        _, secs = cpu_pipeline.timed_step(seed_set, cfg.all_region_sequences(), groups, prep, threads)
+        secs, prep = _oracle_step(reads, quals, paired, threads, iterations, forced)
         runs[threads] = secs
     allc, share = cpus['sched_getaffinity'], cpus['share_threads']
     best = min(runs, key=runs.get)   # the faster of the two is the baseline
-    return {'value': round(2 * sample_pairs / runs[best], 1), 'unit': 'reads/s', 'cores': best,
+    passes = len(prep.result['passes'])
+    return {'value': round(per_unit * units / runs[best], 1), 'unit': 'reads/s', 'cores': best,
             'kind': 'port', 'host_cpus': cpus,
-            'runs': {str(t): {'seconds': round(s, 3), 'value': round(2 * sample_pairs / s, 1)}
+            'runs': {str(t): {'seconds': round(s, 3), 'value': round(per_unit * units / s, 1)}
                      for t, s in sorted(runs.items())},
-            'sample': 'the first {} pairs of the bench input: prelim e2e pass over '
-                      '74 seeds + 1 local remap pass + 2 pileups/consensus, oracle C restatement '
-                      '(og_map, og_pileup_mt) with OpenMP over pairs, timed on all {} host cores '
-                      '({:.1f} s) and on the {}-thread CPU share ({:.1f} s); value is the faster; '
-                      'reads packed before timing'.format(
-                          sample_pairs, allc, runs[allc], share, runs[share])}, prep.result
+            'sample': 'the first {} {} of the bench input ({}): prelim e2e pass over 74 seeds + '
+                      '{} local remap pass(es) with pileup, consensus and the consensus-distance '
+                      'filter, oracle C restatement (og_map, og_pileup_mt, og_gotoh_align, '
+                      'og_levenshtein) with OpenMP / threads over units, timed on all {} host '
+                      'cores ({:.1f} s) and on the {}-thread CPU share ({:.1f} s); value is the '
+                      'faster; reads packed before timing'.format(
+                          units, 'pairs' if paired else 'reads', workload, passes, allc, runs[allc],
+                          share, runs[share])}, prep.result
 
 
 def record_mismatches(dev, ref):
@@ -152,7 +168,8 @@ def record_mismatches(dev, ref):
     return np.flatnonzero(~same)
 
 
-def parity_check(ctx, pipe, sample, paired, baseline_result=None, device_index=0):
+def parity_check(ctx, pipe, sample, paired, baseline_result=None, device_index=0, iterations=1,
+                 forced=False):
     """Parity at configuration size (untimed, after the timed steps): the
     device's alignment records of the bench's own run for its first units
     against the CPU oracle's (og_map) on the same reads, byte for byte.
@@ -163,10 +180,12 @@ def parity_check(ctx, pipe, sample, paired, baseline_result=None, device_index=0
                (what every step's prelim pass computes);
       remap    the last step's --local pass, against the consensus set it
                mapped to (pipe.mapped_to), vs og_map against the same set;
-      consensus  (with the CPU baseline's run of the same sample) the
-               sample alone through the device pipeline on a new context:
-               its prelim consensus and final consensus against the oracle
-               step's (cpu_pipeline.timed_step).
+      consensus  the sample alone through the device pipeline on a new
+               context, with the bench's iteration settings: its prelim
+               consensus, every pass's kept set after the consensus-distance
+               filter, and the final consensus against the oracle step's
+               (cpu_pipeline.timed_step; the CPU baseline's run of the same
+               sample when there was one, else one untimed run here).
 
     Consumers of these records in the reference: remap.py:474-541 (seed
     selection and the consensus), prelim_map.py:134-151 (prelim.csv)."""
@@ -204,18 +223,33 @@ def parity_check(ctx, pipe, sample, paired, baseline_result=None, device_index=0
     out['prelim'] = {'record_mismatches': int(len(bad)), 'first_mismatches': bad[:8].tolist(),
                      'mapped_reads': int(((ref['flag'] & 4) == 0).sum())}
     del dev, ref
+    if baseline_result is None:
+        t1 = time.perf_counter()
+        baseline_result = _oracle_step(reads, quals, paired, threads, iterations, forced)[1].result
+        out['oracle_step_seconds'] = round(time.perf_counter() - t1, 2)
     if baseline_result is not None:
         c2 = _native.Context(device_index)
         try:
             c2.reads_load_fixed(reads, quals, paired)
             p2 = RemapPipeline(c2)
-            final, _counts, _unm = p2.run(float(n), max_iterations=1)
+            units = n // 2 if paired else n
+            final, _counts, _unm = p2.run(2.0 * units, max_iterations=iterations,
+                                          min_iterations=iterations if forced else None)
+            cpu_passes = baseline_result.get('passes', [])
+            first = p2.first_mapped_to or {}
             out['consensus'] = {
-                'prelim_equal': p2.mapped_to == baseline_result['prelim_conseqs'] and
-                list(p2.mapped_to or {}) == baseline_result['remap_names'],
+                'prelim_equal': (first == baseline_result['prelim_conseqs'] and
+                                 list(first) == list(baseline_result['prelim_conseqs'])),
+                'passes': len(p2.log),
+                'passes_equal': (len(p2.log) == len(cpu_passes) and
+                                 all(sorted(a['conseqs']) == b['kept'] for a, b in zip(p2.log, cpu_passes))),
+                'kept_per_pass': [sorted(a['conseqs']) for a in p2.log],
+                'unfiltered_per_pass': [b['unfiltered'] for b in cpu_passes],
                 'final_equal': final == baseline_result['conseqs'],
                 'references': sorted(final)}
-            if out['consensus']['prelim_equal'] and baseline_result['remap'] is not None:
+            if (out['consensus']['prelim_equal'] and out['consensus']['passes_equal'] and
+                    list(p2.mapped_to or {}) == baseline_result['remap_names'] and
+                    baseline_result['remap'] is not None):
                 bad = record_mismatches(c2.fetch(), baseline_result['remap'])
                 out['consensus']['sample_remap_record_mismatches'] = int(len(bad))
         finally:
@@ -223,10 +257,56 @@ def parity_check(ctx, pipe, sample, paired, baseline_result=None, device_index=0
     out['record_mismatches'] = out['prelim']['record_mismatches'] + \
         out.get('remap', {}).get('record_mismatches', 0)
     out['pairs_checked'] = out['units_checked'] if paired else None
-    out['consensus_equal'] = (out['consensus']['prelim_equal'] and out['consensus']['final_equal']
-                              if 'consensus' in out else None)
+    out['consensus_equal'] = (out['consensus']['prelim_equal'] and out['consensus']['passes_equal'] and
+                              out['consensus']['final_equal'] if 'consensus' in out else None)
     out['seconds'] = round(time.perf_counter() - t0, 2)
     out['oracle_threads'] = threads
+    return out
+
+
+def parity_full(ctx, pipe, reads, quals, paired, chunk_units, log=sys.stderr):
+    """Whole-input parity (untimed): every record of every mapping pass of
+    the last step -- the prelim end-to-end pass over the 74 seeds and each
+    --local pass against the consensus set it mapped to (pipe.pass_refs) --
+    against og_map on the same reads, in chunks of chunk_units units so the
+    oracle's buffers stay bounded (records depend only on their read pair
+    and the references).  Each pass is mapped again on the device over the
+    whole resident input (the step's own computation, deterministic) and
+    fetched chunk by chunk.  Reference loop: remap.py:544-606."""
+    import cpu_pipeline
+    import oracle
+    from micall_amd import _native
+    threads = host_cpus()['share_threads']
+    per = 2 if paired else 1
+    n = reads.shape[0]
+    step = chunk_units * per
+    passes = [('prelim', oracle.E2E, dict(pipe.seed_set))] + \
+             [('remap-%d' % (i + 1), oracle.LOCAL, refs) for i, refs in enumerate(pipe.pass_refs)]
+    out = {'units_checked': n // per, 'unit': 'pairs' if paired else 'reads', 'chunk_units': chunk_units,
+           'oracle_threads': threads, 'passes': []}
+    t0 = time.perf_counter()
+    for name, mode, refs in passes:
+        names = list(refs)
+        ctx.index_build(names, [refs[k] for k in names], oracle.seed_len(mode))
+        ctx.map(pipe._params(_native.E2E if mode == oracle.E2E else _native.LOCAL))
+        bad_total, first_bad, mapped = 0, [], 0
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            dev = ctx.fetch(a, b - a)
+            ref = cpu_pipeline.map_arrays([refs[k] for k in names], mode, reads[a:b], quals[a:b], paired,
+                                          threads)
+            bad = record_mismatches(dev, ref)
+            bad_total += len(bad)
+            first_bad += (bad[:4] + a).tolist() if len(first_bad) < 8 else []
+            mapped += int(((ref['flag'] & 4) == 0).sum())
+            del dev, ref
+            print('parity_full {} reads {}..{}: {} mismatches ({:.0f} s)'.format(
+                name, a, b, len(bad), time.perf_counter() - t0), file=log, flush=True)
+        out['passes'].append({'pass': name, 'references': len(names), 'reads': n,
+                              'record_mismatches': int(bad_total), 'first_mismatches': first_bad[:8],
+                              'mapped_reads': mapped})
+    out['record_mismatches'] = sum(p['record_mismatches'] for p in out['passes'])
+    out['seconds'] = round(time.perf_counter() - t0, 1)
     return out
 
 
@@ -564,19 +644,42 @@ def end_to_end(n_pairs, workdir, single_member=False, job=None):
     return out
 
 
-def latest_profile(*parts):
-    """The newest committed round's copy of a profile summary
-    (profiles/rNN/...), or None."""
+KERNEL_SOURCES = ('micall-lite_amd/csrc/mh_map.hip', 'micall-lite_amd/csrc/mh_pileup.hip',
+                  'micall-lite_amd/csrc/mh_internal.h', 'micall-lite_amd/csrc/Makefile')
+
+
+def kernel_source_sha():
+    """Fingerprint of the mapping / pileup kernels' sources (the files the
+    committed PMC and SQ summaries were measured on must hash the same)."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(REPO, rel), 'rb') as f:
+            h.update(rel.encode() + b'\0' + f.read())
+    return h.hexdigest()[:16]
+
+
+def matching_profile(name):
+    """The committed profile summary `name` (profiles/rNN/c2*/name, newest
+    round first) that was measured on these kernel sources
+    (kernel_source_sha), or None: a summary of another build is never
+    divided by this run's launch times."""
     base = os.path.join(REPO, 'profiles')
     try:
         rounds = sorted((d for d in os.listdir(base) if len(d) == 3 and d[0] == 'r' and d[1:].isdigit()),
                         reverse=True)
     except OSError:
         return None
+    sha = kernel_source_sha()
     for d in rounds:
-        path = os.path.join(base, d, *parts)
-        if os.path.exists(path):
-            return path
+        for sub in sorted((x for x in os.listdir(os.path.join(base, d)) if x.startswith('c2')), reverse=True):
+            path = os.path.join(base, d, sub, name)
+            try:
+                with open(path) as f:
+                    if json.load(f).get('kernel_source_sha') == sha:
+                        return path
+            except (OSError, ValueError):
+                continue
     return None
 
 
@@ -584,9 +687,10 @@ def read_pmc_traffic(kernel, pairs, stage='remap'):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC
     summary of this stage (separate --pmc passes, FETCH_SIZE doubled per the
     gfx950 rule; profiles/collect_pmc_stages.sh), when it was measured on the
-    same per-GPU pair count."""
+    same per-GPU pair count; the remap stage's summary must also carry these
+    kernel sources' fingerprint (matching_profile)."""
     if stage == 'remap':
-        path = latest_profile('c2', 'pmc_traffic.json')
+        path = matching_profile('pmc_traffic.json')
         if path is None:
             return None
     else:
@@ -608,11 +712,11 @@ VALU_ISSUE_CYCLES = 2      # MI355X_MICROARCH.md: a wave64 VALU instruction issu
 def read_valu_issue(kernel, pairs, avg_launch_ms):
     """Issue-side roofline of `kernel` (it is bound by integer VALU issue and
     its dependency chain, not HBM): VALU wave-instructions per launch from the
-    committed SQ_INSTS_VALU pass (profiles/rNN/c2/sq_issue.json, the newest; same
-    per-GPU pair count; the mate-rescue DP launch, the one after k_rescue, is
+    committed SQ_INSTS_VALU pass (profiles/rNN/c2*/sq_issue.json measured on
+    these kernel sources, matching_profile; same per-GPU pair count; the mate-rescue DP launch, the one after k_rescue, is
     left out), over this run's average launch time, against 1024 SIMDs x the
     measured clock / VALU_ISSUE_CYCLES."""
-    path = latest_profile('c2', 'sq_issue.json')
+    path = matching_profile('sq_issue.json')
     if path is None:
         return None
     try:
@@ -966,6 +1070,75 @@ def bench_aln2counts(args):
     print(json.dumps(out))
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(args):
+    """`bench.py --gpus N` (N > 1) without a launcher: start N ranks with
+    torch.distributed.run as a CHILD process (never exec: nothing here has
+    touched the GPU, and nothing will), relay rank 0's one JSON line and exit
+    with the child's status.  The line is refused (exit 3) unless it reports
+    the N ranks asked for (n_gpus and config.dist_world).  Other output of the
+    ranks goes to stderr as it comes, so a long run shows progress."""
+    import subprocess
+    if args.stage not in ('remap', 'chain'):
+        sys.exit('bench.py: --stage {} runs on one GPU; --gpus {} needs the remap or chain '
+                 'stage'.format(args.stage, args.gpus))
+    backend = os.environ.get('MICALL_BENCH_BACKEND', 'nccl')
+    if backend == 'nccl':
+        import torch
+        ndev = torch.cuda.device_count()     # counts devices without initialising HIP
+        if ndev < args.gpus:
+            sys.exit('bench.py: --gpus {} but this node has {} GPU(s)'.format(args.gpus, ndev))
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(args.gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    lines = []
+    for ln in proc.stdout:
+        if ln.startswith('{"metric"'):
+            lines.append(ln.strip())
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc != 0:
+        sys.exit(rc)
+    if len(lines) != 1:
+        sys.exit('bench.py: expected one JSON line from rank 0, got {}'.format(len(lines)))
+    d = json.loads(lines[0])
+    if d.get('n_gpus') != args.gpus or d.get('config', {}).get('dist_world') != args.gpus:
+        print('bench.py: refusing a line for {} rank(s) (dist_world {}) under --gpus {}'.format(
+            d.get('n_gpus'), d.get('config', {}).get('dist_world'), args.gpus), file=sys.stderr)
+        sys.exit(3)
+    print(lines[0], flush=True)
+    return 0
+
+
+def _backend_name(world, backend):
+    """The process group's backend as torch.distributed reports it (None on
+    one rank, which runs no group)."""
+    import torch.distributed as dist
+    if world == 1 or not dist.is_initialized():
+        return None
+    return dist.get_backend()
+
+
+def _rank_devices(world, device):
+    """Every rank's device index, in rank order (rank 0's view)."""
+    import torch.distributed as dist
+    if world == 1:
+        return [device.index]
+    out = [None] * world
+    dist.all_gather_object(out, device.index)
+    return out
+
+
 def _init_job(args):
     """torch.distributed for a leg run under torchrun (WORLD_SIZE > 1): the
     device of this rank (RCCL), or device LOCAL_RANK % devices with
@@ -977,7 +1150,9 @@ def _init_job(args):
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
-        print('warning: --gpus {} but WORLD_SIZE {}'.format(args.gpus, world), file=sys.stderr)
+        # a line for a world other than the one asked for would be read as
+        # an N-GPU figure it is not
+        sys.exit('bench.py: --gpus {} but WORLD_SIZE {}: refusing to run'.format(args.gpus, world))
     backend = os.environ.get('MICALL_BENCH_BACKEND', 'nccl')
     ndev = torch.cuda.device_count()
     device = torch.device('cuda', local if backend == 'nccl' else local % max(ndev, 1))
@@ -1007,6 +1182,7 @@ def bench_chain(args):
     import random
     import torch.distributed as dist
     world, rank, device, backend = _init_job(args)
+    devices = _rank_devices(world, device)
     from micall_amd import (aln2counts, censor_fastq, prelim_map, remap, sam2aln, session, sharded_io,
                             synth)
     job = Job()
@@ -1128,7 +1304,9 @@ def bench_chain(args):
                        'pairs': args.pairs * world, 'pairs_per_gpu': args.pairs, 'bad_cycles': len(bad),
                        'parallelism': 'dp{}{}'.format(world, '' if world == 1 else ' ({}; every rank runs '
                                                        'the chain on the shared files)'.format(
-                                                           'RCCL' if backend == 'nccl' else backend))},
+                                                           'RCCL' if backend == 'nccl' else backend)),
+                       'dist_world': world, 'dist_backend': _backend_name(world, backend),
+                       'rank_devices': devices},
             'reported_run': 'median of {} runs by total time (the slowest rank\'s per stage)'.format(len(runs)),
             'stages_s': {k: round(v, 3) for k, v in med['stages'].items()},
             'all_runs_s': [round(r['total'], 3) for r in runs],
@@ -1201,6 +1379,9 @@ def main():
     ap.add_argument('--cpu-e2e-sample', type=int, default=20000,
                     help='pairs for the CPU end-to-end baseline (file to file)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--parity-full', type=int, default=0, metavar='CHUNK',
+                    help='after timing, check every record of every pass of the last step over '
+                         'the whole input against og_map in chunks of CHUNK units (C3: 1000000)')
     ap.add_argument('--no-parity', action='store_true',
                     help='skip the parity leg (device records of the first --cpu-sample units '
                          'against the CPU oracle, after timing)')
@@ -1217,6 +1398,8 @@ def main():
                          '(SURVEY.md 8(f)) over the remap.csv of one C2 pass; censor: the '
                          'stage before (FASTQ censor of the C2 reads) plus the FASTQ ingest')
     args = ap.parse_args()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        return _self_launch(args)
     if args.stage == 'sam2aln':
         return bench_sam2aln(args)
     if args.stage == 'aln2counts':
@@ -1232,6 +1415,7 @@ def main():
     from micall_amd.pipeline import RemapPipeline, Shard
 
     world, rank, device, backend = _init_job(args)
+    devices = _rank_devices(world, device)
 
     ctx = _native.Context(device.index)
     paired = not args.unpaired
@@ -1245,6 +1429,7 @@ def main():
         k = min(args.cpu_sample if world == 1 else min(args.cpu_sample, 20000), args.pairs)
         k *= 2 if paired else 1
         sample = (reads[:k].copy(), quals[:k].copy())
+    full_input = (reads, quals) if args.parity_full and rank == 0 else None
     del reads, quals
     shard = Shard(rank, world, read_base=rank * (1 if args.unpaired else 2) * args.pairs, device=device) if world > 1 else None
     pipe = RemapPipeline(ctx, shard=shard)
@@ -1319,12 +1504,20 @@ def main():
     parity = None
     if rank == 0:
         cpu = cpu_result = None
-        if (world == 1 and not args.no_cpu_baseline and paired and L == READ_LEN and
-                args.genomes == 'pol' and sample is not None):
-            cpu, cpu_result = cpu_baseline(*sample)
+        if world == 1 and not args.no_cpu_baseline and sample is not None:
+            cpu, cpu_result = cpu_baseline(*sample, paired=paired, iterations=args.iterations,
+                                           forced=args.force_iterations,
+                                           workload='{}x{} {}'.format(2 if paired else 1, L, args.genomes))
         if sample is not None and not args.no_parity:
-            parity = parity_check(ctx, pipe, sample, paired, cpu_result, device.index)
+            parity = parity_check(ctx, pipe, sample, paired, cpu_result, device.index,
+                                  iterations=args.iterations, forced=args.force_iterations)
             del cpu_result
+        if full_input is not None:
+            parity_whole = parity_full(ctx, pipe, full_input[0], full_input[1], paired, args.parity_full)
+            if parity is None:
+                parity = {}
+            parity['whole_input'] = parity_whole
+            full_input = None
         if cpu is not None:
             cpu['device_resident_vs_cpu'] = round(value / cpu['value'], 1)
         out = {
@@ -1351,7 +1544,9 @@ def main():
                        'parallelism': ('dp1 (one GPU, no collective)' if world == 1 else
                                        'dp{} (read-pair shards, {} all-reduce of pileup '
                                        'counters)'.format(world, 'RCCL' if backend == 'nccl'
-                                                          else backend))},
+                                                          else backend)),
+                       'dist_world': world, 'dist_backend': _backend_name(world, backend),
+                       'rank_devices': devices},
             'roofline': {'kernel': dom, 'bound': 'hbm', 'achieved': round(achieved, 3),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 6),

@@ -613,6 +613,42 @@ int mh_gotoh_distance_batch(mh_ctx *ctx, int count, const char *const *seq1,
 int mh_profile(mh_ctx *ctx, int enable);
 int mh_profile_get(mh_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 
+/* Diagnostics (tests only; no reference counterpart): for n caller-given
+ * extensions items[4t..4t+3] = (read index, strand, ref, centre diagonal) of
+ * the loaded reads against the built index, run both k_dp paths on the same
+ * staged tables: out[8t..8t+7] = (fast path taken, its best score, row, band
+ * lane; the band half; the full banded DP's best score, row, band lane).
+ * Whenever the fast path is taken its cell must equal the full DP's. */
+int mh_probe_extend(mh_ctx *ctx, const mh_params *par, int n, const int32_t *items, int32_t *out);
+
+/* Host side of counts_to_conseqs (remap.py:309-333 with find_top_token
+ * :892-902 and the seed prefill :195-197) for one reference's fetched
+ * pileup rows, positions 1..length (rows past `rows` count as empty): tok[i]
+ * = the top base-like token of position i+1 -- the first of A < C < G < T
+ * with the largest positive count, else the seed's character (count 0),
+ * else 'N' (-1), else '-' (-2), else 0 (no token).  Insertion tokens are
+ * merged in by the caller.  *any_positive: some row holds a positive count.
+ * Replaces the reference's per-position Counter walk. */
+int mh_top_tokens(int32_t length, int32_t rows, const int32_t *dense, const uint8_t *nflag,
+                  const uint8_t *dflag, const char *seed, int32_t seed_len, uint8_t *tok,
+                  int32_t *any_positive);
+
+/* counts_to_conseqs (remap.py:309-333, find_top_token :892-902, seed
+ * prefill :195-197) for n_sel references of a fetched pileup in one call
+ * (host code): reference k is row rows_of[k] of dense ([rows][cap][4]
+ * int32) / nflag / dflag ([rows][cap] bytes), positions 1..lengths[k], its
+ * seed seeds[k] (seed_lens[k] bytes, may be 0); the insertion tokens are
+ * n_ev events (row, pos, token = pool[off .. off+len), merged pairs).  Per
+ * position the top of the reference's Counter, then the deletion-run rule;
+ * consensus k is out[out_off[k] .. out_off[k+1]) and present[k] = 0 when no
+ * count is positive (no consensus).  out_cap >= sum(lengths) + sum(ev_len)
+ * always suffices.  Returns -2 when out_cap is too small. */
+int mh_conseqs_build(int n_sel, const int32_t *rows_of, const int32_t *lengths, const char *const *seeds,
+                     const int32_t *seed_lens, int32_t cap, const int32_t *dense, const uint8_t *nflag,
+                     const uint8_t *dflag, int64_t n_ev, const int32_t *ev_row, const int32_t *ev_pos,
+                     const int64_t *ev_off, const int32_t *ev_len, const int64_t *ev_cnt, const char *pool,
+                     char *out, int64_t out_cap, int64_t *out_off, int32_t *present);
+
 /* Unit-cost edit distance (Levenshtein.distance, remap.py:251). */
 int mh_levenshtein(const char *a, const char *b);
 /* out[t] = mh_levenshtein(a[t], b[t]) for count pairs, on host threads. */

@@ -194,6 +194,9 @@ struct CtxEx : Ctx {
     HostReads host;
     // index cache: large (fixed seed-set) indexes are kept by content signature
     std::vector<DevIndex> cache;
+    // the reference bytes of each cache entry (every sequence and its NUL, in
+    // order): a signature hit is used only when they compare equal
+    std::vector<std::string> cache_text;
     std::vector<Rec> rec_cache;
     std::vector<int32_t> csv_rows_info;   // per prelim.csv row: name id, flag, max M run, ref
     std::vector<int32_t> csv_present;     // compact ref id -> index into the @SQ list
@@ -868,11 +871,26 @@ int mh_index_build(mh_ctx *ctx, int n_refs, const char *const *seqs, int seedlen
     MH_HIP(hipStreamSynchronize(c->stream));
     int64_t total = 0;
     for (int r = 0; r < n_refs; ++r) total += (int64_t)std::strlen(seqs[r]);
-    const uint64_t sig = signature(n_refs, seqs, seedlen);
+    // MH_INDEX_FORCE_COLLISION=1 (tests): every reference set gets the same
+    // signature, so only the content comparison tells two sets apart
+    const char *force = getenv("MH_INDEX_FORCE_COLLISION");
+    const uint64_t sig = force && *force == '1' ? 0x5eedull : signature(n_refs, seqs, seedlen);
     const bool cacheable = total > 65536;
     c->index = DevIndex{};   // cache entries and c->small own their buffers
-    for (auto &ix : c->cache) {
-        if (ix.sig == sig && ix.n_refs == n_refs && ix.seedlen == seedlen) {
+    for (size_t e = 0; e < c->cache.size(); ++e) {
+        const DevIndex &ix = c->cache[e];
+        if (ix.sig != sig || ix.n_refs != n_refs || ix.seedlen != seedlen) continue;
+        // a 64-bit hash can collide: compare the bytes (~0.6 MB memcmp for
+        // the 74 seeds, well under a millisecond)
+        const std::string &t = c->cache_text[e];
+        bool same = t.size() == (size_t)(total + n_refs);
+        size_t at = 0;
+        for (int r = 0; same && r < n_refs; ++r) {
+            const size_t len = std::strlen(seqs[r]);
+            same = std::memcmp(t.data() + at, seqs[r], len + 1) == 0;
+            at += len + 1;
+        }
+        if (same) {
             c->index = ix;
             return 0;
         }
@@ -886,8 +904,16 @@ int mh_index_build(mh_ctx *ctx, int n_refs, const char *const *seqs, int seedlen
     DevIndex ix;
     if (int st = build_index(ix, n_refs, seqs, seedlen)) { free_index(ix); return st; }
     ix.sig = sig;
-    if (c->cache.size() >= 2) { free_index(c->cache.front()); c->cache.erase(c->cache.begin()); }
+    if (c->cache.size() >= 2) {
+        free_index(c->cache.front());
+        c->cache.erase(c->cache.begin());
+        c->cache_text.erase(c->cache_text.begin());
+    }
+    std::string text;
+    text.reserve((size_t)(total + n_refs));
+    for (int r = 0; r < n_refs; ++r) text.append(seqs[r], std::strlen(seqs[r]) + 1);
     c->cache.push_back(ix);
+    c->cache_text.push_back(std::move(text));
     c->index = ix;
     return 0;
 }
@@ -1213,6 +1239,15 @@ int mh_map(mh_ctx *ctx, const mh_params *par)
     c->fmt_valid = false;
     c->fmt_chunks.clear();
     return st;
+}
+
+int mh_probe_extend(mh_ctx *ctx, const mh_params *par, int n, const int32_t *items, int32_t *out)
+{
+    if (!ctx || !par || n < 0 || (n > 0 && (!items || !out))) return -3;
+    CtxEx *c = X(ctx);
+    MH_HIP(hipSetDevice(c->device));
+    if (int st = prepare_len_tab(*c, *par)) return st;
+    return run_probe_ext(*c, *par, n, items, out);
 }
 
 int mh_profile(mh_ctx *ctx, int enable)
@@ -2781,6 +2816,189 @@ int mh_gotoh_distance_batch(mh_ctx *ctx, int count, const char *const *seq1, con
     MH_HIP(hipSetDevice(c->device));
     return run_gotoh_distance_batch(*c, count, seq1, seq2, text, gop, gep, is_global, alphabet, matrix,
                                     dist, score, status);
+}
+
+int mh_top_tokens(int32_t length, int32_t rows, const int32_t *dense, const uint8_t *nflag,
+                  const uint8_t *dflag, const char *seed, int32_t seed_len, uint8_t *tok,
+                  int32_t *any_positive)
+{
+    if (length < 0 || rows < 0 || (rows > 0 && (!dense || !nflag || !dflag)) || (length > 0 && !tok) ||
+        seed_len < 0 || (seed_len > 0 && !seed))
+        return -3;
+    // branch-free (the counts are data: a branch per position mispredicts)
+    // and in two passes the compiler vectorises: the fill of each position
+    // (seed prefill 0 > 'N' -1 > '-' -2 > none), then the counted bases
+    const int32_t n = std::min(length, rows);
+    const int32_t ns = std::min(seed_len, length);
+    std::memcpy(tok, seed, (size_t)std::max(ns, 0));
+    for (int32_t i = ns; i < n; ++i) {
+        const uint8_t nf = nflag[i] != 0, df = dflag[i] != 0;
+        tok[i] = (uint8_t)(nf * 'N' + (1 - nf) * df * '-');
+    }
+    for (int32_t i = std::max(ns, n); i < length; ++i) tok[i] = 0;
+    int positive = 0;
+    {
+        const int32_t *__restrict__ dd = dense;
+        uint8_t *__restrict__ tt = tok;
+        for (int32_t i = 0; i < n; ++i) {
+            const int32_t c0 = dd[4 * i], c1 = dd[4 * i + 1], c2 = dd[4 * i + 2], c3 = dd[4 * i + 3];
+            const int32_t top = std::max(std::max(c0, c1), std::max(c2, c3));
+            // a positive count wins; ties go to the first of A < C < G < T
+            // the first index holding top, as arithmetic (a compare chain
+            // becomes branches that mispredict on count data)
+            const uint32_t n0 = c0 != top, n1 = n0 & (c1 != top), n2 = n1 & (c2 != top);
+            const uint32_t t = (uint32_t)(0x54474341u >> (8 * (n0 + n1 + n2))) & 0xffu;   // "ACGT"
+            const uint32_t pos = top > 0;
+            tt[i] = (uint8_t)((t & (0u - pos)) | (tt[i] & (pos - 1u)));
+            positive |= (int)pos;
+        }
+    }
+    for (int32_t i = n; i < rows && !positive; ++i) {
+        const int32_t *d = dense + 4 * (size_t)i;
+        positive = d[0] > 0 || d[1] > 0 || d[2] > 0 || d[3] > 0;
+    }
+    if (any_positive) *any_positive = positive;
+    return 0;
+}
+
+// counts_to_conseqs (remap.py:309-333) for many references at once: per
+// position the reference's Counter -- the seed's character at 0, the counted
+// bases, 'N' := -1, '-' := -2, then every insertion token's pairs added --
+// its top token (find_top_token, :892-902: the most pairs, ties to the
+// smallest string), and the deletion-run rule of the assembly.
+int mh_conseqs_build(int n_sel, const int32_t *rows_of, const int32_t *lengths, const char *const *seeds,
+                     const int32_t *seed_lens, int32_t cap, const int32_t *dense, const uint8_t *nflag,
+                     const uint8_t *dflag, int64_t n_ev, const int32_t *ev_row, const int32_t *ev_pos,
+                     const int64_t *ev_off, const int32_t *ev_len, const int64_t *ev_cnt, const char *pool,
+                     char *out, int64_t out_cap, int64_t *out_off, int32_t *present)
+{
+    if (n_sel < 0 || n_ev < 0 || cap < 0 || !out_off || !present ||
+        (n_sel > 0 && (!rows_of || !lengths || !seeds || !seed_lens || !out)) ||
+        (n_ev > 0 && (!ev_row || !ev_pos || !ev_off || !ev_len || !ev_cnt || !pool)) ||
+        (cap > 0 && n_sel > 0 && (!dense || !nflag || !dflag))) {
+        set_error("mh_conseqs_build: bad arguments");
+        return -3;
+    }
+    for (int k = 0; k < n_sel; ++k)
+        if (lengths[k] < 0 || seed_lens[k] < 0 || (seed_lens[k] > 0 && !seeds[k]) || rows_of[k] < 0) {
+            set_error("mh_conseqs_build: bad reference %d", k);
+            return -3;
+        }
+    // events grouped by (row, pos), tokens in order
+    std::vector<int64_t> ev((size_t)n_ev);
+    for (int64_t e = 0; e < n_ev; ++e) ev[(size_t)e] = e;
+    std::sort(ev.begin(), ev.end(), [&](int64_t a, int64_t b) {
+        if (ev_row[a] != ev_row[b]) return ev_row[a] < ev_row[b];
+        return ev_pos[a] < ev_pos[b];
+    });
+    std::vector<std::string> texts((size_t)n_sel);
+
+    // one reference: its consensus into texts[k], present[k]
+    auto build_one = [&](int k, std::vector<uint8_t> &tok) {
+        const int32_t row = rows_of[k], length = lengths[k], slen = seed_lens[k];
+        const char *seed = slen > 0 ? seeds[k] : "";
+        const int32_t rows = std::min(length, cap);
+        const int32_t *d = dense + (size_t)row * cap * 4;
+        const uint8_t *nf = nflag + (size_t)row * cap, *df = dflag + (size_t)row * cap;
+        if (tok.size() < (size_t)std::max(length, 1)) tok.resize((size_t)std::max(length, 1));
+        int32_t pos_any = 0;
+        mh_top_tokens(length, rows, d, nf, df, seed, std::min(slen, length), tok.data(), &pos_any);
+        auto lo = std::lower_bound(ev.begin(), ev.end(), row, [&](int64_t e, int32_t r) { return ev_row[e] < r; });
+        auto hi = std::upper_bound(ev.begin(), ev.end(), row, [&](int32_t r, int64_t e) { return r < ev_row[e]; });
+        present[k] = pos_any || lo != hi;
+        // positions with events: the whole Counter (longer tokens kept aside)
+        std::vector<std::pair<int32_t, std::string>> longer;   // (0-based position, token)
+        for (auto it = lo; it != hi;) {
+            const int32_t pos = ev_pos[*it];
+            auto jt = it;
+            while (jt != hi && ev_pos[*jt] == pos) ++jt;
+            if (pos >= 1 && pos <= length) {
+                std::vector<std::pair<std::string, int64_t>> c;   // insertion order irrelevant to the top
+                auto add = [&](const std::string &t, int64_t v, bool assign) {
+                    for (auto &x : c) if (x.first == t) { x.second = assign ? v : x.second + v; return; }
+                    c.emplace_back(t, v);
+                };
+                const int32_t i = pos - 1;
+                if (pos <= slen) add(std::string(1, seed[i]), 0, false);
+                if (i < rows) {
+                    static const char B[4] = {'A', 'C', 'G', 'T'};
+                    for (int b = 0; b < 4; ++b) if (d[4 * (size_t)i + b]) add(std::string(1, B[b]), d[4 * (size_t)i + b], false);
+                    if (nf[i]) add("N", -1, true);
+                    if (df[i]) add("-", -2, true);
+                }
+                for (auto e = it; e != jt; ++e)
+                    add(std::string(pool + ev_off[*e], (size_t)ev_len[*e]), ev_cnt[*e], false);
+                const std::pair<std::string, int64_t> *top = nullptr;
+                for (auto &x : c)
+                    if (!top || x.second > top->second || (x.second == top->second && x.first < top->first)) top = &x;
+                tok[(size_t)i] = top && !top->first.empty() ? (uint8_t)top->first[0] : 0;
+                if (top && top->first.size() > 1) longer.emplace_back(i, top->first);
+            }
+            it = jt;
+        }
+        std::sort(longer.begin(), longer.end());
+        if (!present[k]) return;
+        // assembly: a missing token writes 'N' at once, a '-' opens or grows
+        // the deletion, any other token first writes the open deletion when
+        // its length is not a multiple of 3; a trailing deletion is dropped.
+        // At most one byte per position plus the longer tokens' extra bytes.
+        size_t need = (size_t)length;
+        for (auto &x : longer) need += x.second.size() - 1;
+        std::string &text = texts[(size_t)k];
+        text.resize(need);
+        char *o = &text[0], *o0 = o;
+        const uint8_t *t = tok.data();
+        size_t li = 0;
+        int32_t dels = 0;
+        for (int32_t i = 0; i < length;) {
+            // a span of plain tokens (no 0, no '-', no longer token) is copied
+            // as it is: the common case, one byte per position
+            const int32_t stop = li < longer.size() ? longer[li].first : length;
+            int32_t j = i;
+            while (j < stop && t[j] != 0 && t[j] != '-') ++j;
+            if (j > i) {
+                if (dels) {
+                    if (dels % 3 != 0) { std::memset(o, '-', (size_t)dels); o += dels; }
+                    dels = 0;
+                }
+                std::memcpy(o, t + i, (size_t)(j - i));
+                o += j - i;
+                i = j;
+                continue;
+            }
+            const uint8_t c = t[i];
+            if (c == 0) { *o++ = 'N'; ++i; continue; }
+            const bool is_longer = li < longer.size() && longer[li].first == i;
+            if (c == '-' && !is_longer) { ++dels; ++i; continue; }
+            if (dels) {
+                if (dels % 3 != 0) { std::memset(o, '-', (size_t)dels); o += dels; }
+                dels = 0;
+            }
+            const std::string &x = longer[li++].second;   // (is_longer here)
+            std::memcpy(o, x.data(), x.size());
+            o += x.size();
+            ++i;
+        }
+        text.resize((size_t)(o - o0));
+    };
+
+    // one thread: ~3.5 ns per position (C4-all's ~0.7 M positions in ~2.5
+    // ms); threads measured slower (their start-up and the texts' first
+    // touch outweigh the work)
+    {
+        std::vector<uint8_t> tok;
+        for (int k = 0; k < n_sel; ++k) build_one(k, tok);
+    }
+    int64_t at = 0;
+    out_off[0] = 0;
+    for (int k = 0; k < n_sel; ++k) {
+        const std::string &text = texts[(size_t)k];
+        if (at + (int64_t)text.size() > out_cap) { set_error("mh_conseqs_build: output capacity"); return -2; }
+        std::memcpy(out + at, text.data(), text.size());
+        at += (int64_t)text.size();
+        out_off[k + 1] = at;
+    }
+    return 0;
 }
 
 int mh_levenshtein_batch(int count, const char *const *a, const char *const *b, int *out)

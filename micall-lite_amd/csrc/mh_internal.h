@@ -222,6 +222,7 @@ struct PileState {
 hipError_t launch_pack_reads(DevReads &r, const uint8_t *d_seq, const uint8_t *d_qual,
                              const int64_t *d_src_off, hipStream_t s);
 int run_map(struct Ctx &c, const mh_params &par);
+int run_probe_ext(struct Ctx &c, const mh_params &par, int n, const int32_t *items, int32_t *out);
 // the per-reference tallies of the last mapping pass on the host (one copy
 // per pass); nullptr on a copy error
 const int64_t *map_stats_host(struct Ctx &c);

@@ -940,26 +940,101 @@ __device__ __forceinline__ void half_max64(long long v, int lane, long long &k0,
 // (tests/test_gpu_parity.py runs both and compares them with the oracle,
 // og_mapper.c:dp_extend).
 // ---------------------------------------------------------------------------
-// Local mode, up to three non-matches on the seeded diagonal (rows x_t,
-// each scoring s_t): the crude bound Gb prices a gapped path as matching
-// every row, and fails as soon as two non-matches cost more than one gap.
-// A gapped path P over rows [a, b] scores at most the seeded diagonal's sum
-// over [a, b] (<= S, and <= U(r, kb) when P ends at (r, kb)) plus, per row it
-// spends off that diagonal, e(i) = ma - s(i, kb) at a non-match row and at
-// most 0 elsewhere (a row on another diagonal scores <= ma; an inserted row
-// 0 before its gap's extension, which the gap's cost holds), minus its gaps.
-// With two or more gaps P gains at most G = sum(ma - s_t) - 2 gmin; with one
-// gap its off-diagonal rows are one interval at an end of [a, b] on one
-// diagonal k (plus the inserted rows of the gap), costing the gap
-// oe + ex (|k - kb| - 1) at least, and a row of the interval where k does
-// not match the read loses ma there (e <= 0 - ma, or 0 - ma inserted).
-// The interval's best sum starts and ends at non-match rows, so it is
-// enough that for every other live diagonal k and every run x_j .. x_l
-// (j < l) of the non-match rows,
-//     sum_{t=j..l} (ma - s_t) - ma * (non-matches of k strictly inside, x_t
-//     excluded) < the gap's cost to k,
-// and G < 2 gmin.  Then no gapped cell reaches its diagonal's ungapped
-// value, so (A) and (C) hold without Gb.  One wave, lane = diagonal as (B).
+// Local mode, up to three non-matches on the seeded diagonal kb (rows x_t,
+// each scoring s_t, e_t = ma - s_t): the crude bound Gb prices a gapped path
+// as matching every row, and fails as soon as two non-matches cost more than
+// one gap.  Against kb, a path P over rows [a, b] gains per row s_P(i) -
+// s(i, kb): at most e_t at a non-match row x_t, and -ma or less at any other
+// row where P's diagonal does not match the read or P inserts the row (kb
+// matches there, P scores <= 0); kb's own sum over [a, b] is <= S (and <=
+// U(r, kb) when P ends at (r, kb)).  So P beats kb only by covering a run
+// x_j .. x_l (j < l) of the non-match rows (one e_t < gmin never pays a
+// gap), and then gains at most
+//     sum_{t=j..l} e_t - ma * (penalty rows strictly inside, x_t excluded)
+//                      - (its gaps).
+// Two or more gaps: G = sum e_t - 2 gmin < 0 is required.  One gap, three
+// shapes (the band lanes are diagonals; a gap of d lanes costs at least
+// gc(d) = min(oeI + exI (d-1), oeD + exD (d-1)) >= gmin):
+//  (i)  kb, then one other diagonal k (or k, then kb): the rows of the run
+//       off kb are one interval at an end, all of them on k or inserted, so
+//       the penalty is at least c_k = k's non-matches in the whole run; it
+//       is enough that sum e - ma c_k < gc(|k - kb|) for every live k;
+//  (ii) k1, then k2, both off kb (k1 covering the run up to a row c, k2
+//       after, any inserted rows between are penalty rows too): the penalty
+//       is at least P_k1(c) + Q_k2(c), k1's non-matches in (x_j, c] and k2's
+//       in (c, x_l).  With R = sum e - gmin and n = floor(R / ma) + 1, P can
+//       only gain if some c has P_k1(c) <= n - 1 and Q_k2(c) <= n - 1, i.e.
+//       c < f_k1 (the row of k1's n-th non-match from x_j, or x_l) and
+//       c >= g_k2 (the row of k2's n-th from x_l, or x_j); it is enough that
+//       min over lanes of g < max over lanes of f never holds (k1 = k2 is
+//       let in: only more conservative).
+// One wave, lane = diagonal as in (B).  Each run is scanned word by word from
+// both ends and the scans stop as soon as every other live lane has met its
+// count (n non-matches), which is a few words on ordinary sequence; a
+// low-complexity stretch (every diagonal matching long stretches) scans the
+// whole run or fails.
+
+// offset (0 .. 3) of the k-th (1-based) set row of a per-row mask (one bit per
+// byte), from the low end
+__device__ __forceinline__ int sel_row(uint32_t x, int k)
+{
+    uint32_t b = (x | x >> 7 | x >> 14 | x >> 21) & 0xFu;
+    if (k > 1) b &= b - 1;
+    if (k > 2) b &= b - 1;
+    if (k > 3) b &= b - 1;
+    return __builtin_ctz(b);
+}
+
+// bytes u of the word at row i with i + u in (lo, hi)
+__device__ __forceinline__ uint32_t rows_between(int i, int lo, int hi)
+{
+    const int a = lo + 1 - i, b = hi - i;
+    const uint32_t ma_ = a <= 0 ? ~0u : a >= 4 ? 0u : ~0u << (8 * a);
+    const uint32_t mb_ = b >= 4 ? ~0u : b <= 0 ? 0u : ~0u >> (8 * (4 - b));
+    return ma_ & mb_;
+}
+
+// this lane's non-match rows at rows i .. i+3 of its diagonal (one bit per byte)
+__device__ __forceinline__ uint32_t nonmatch_word(const uint8_t *rdc, const uint8_t *rp, uint32_t sh, int i)
+{
+    const uint32_t rd = *(const uint32_t *)(rdc + i) & 0x07070707u;
+    const uint32_t rv = __builtin_amdgcn_alignbyte(*(const uint32_t *)(rp + i + 4), *(const uint32_t *)(rp + i), sh) >> 2;
+    uint32_t x = (rd ^ rv) | ((rd | rv) & 0x04040404u);
+    return (x | (x >> 1) | (x >> 2)) & 0x01010101u;
+}
+
+// One run (lo, hi) of a lane's diagonal, row ex (a non-match row of kb inside
+// the run, or -1) left out.  Forward: cnt = the lane's non-matches counted
+// (all of the run's unless every other lane had reached n first), f = the row
+// of its n-th (hi if none).  Backward: g = the row of its n-th from hi (lo if
+// none).  Live lanes only; the loops end together.
+__device__ __forceinline__ void scan_run(const uint8_t *rdc, const uint8_t *rp, uint32_t sh, bool other,
+                                         int lo, int hi, int ex, int n, int &cnt, int &f, int &g)
+{
+    const uint32_t exm = ex >= 0 ? ~(1u << (8 * (ex & 3))) : ~0u;
+    const int exw = ex & ~3;
+    cnt = 0;
+    f = hi;
+    for (int i = (lo + 1) & ~3; i < hi; i += 4) {
+        uint32_t x = nonmatch_word(rdc, rp, sh, i) & rows_between(i, lo, hi);
+        if (i == exw) x &= exm;
+        const int p = __builtin_popcount(x);
+        if (cnt < n && cnt + p >= n) f = i + sel_row(x, n - cnt);
+        cnt += p;
+        if (__builtin_amdgcn_ballot_w64(other && cnt < n) == 0) break;
+    }
+    int c = 0;
+    g = lo;
+    for (int i = (hi - 1) & ~3; i + 3 > lo; i -= 4) {
+        uint32_t x = nonmatch_word(rdc, rp, sh, i) & rows_between(i, lo, hi);
+        if (i == exw) x &= exm;
+        const int p = __builtin_popcount(x);
+        if (c < n && c + p >= n) g = i + sel_row(x, p - (n - c) + 1);
+        c += p;
+        if (__builtin_amdgcn_ballot_w64(other && c < n) == 0) break;
+    }
+}
+
 template <int LOCAL>
 __device__ bool ungapped_wide(const XView &X, int m, int lane, int hb, int nm, uint32_t xm0, uint32_t xm1,
                               int oeI, int exI, int oeD, int exD)
@@ -991,35 +1066,36 @@ __device__ bool ungapped_wide(const XView &X, int m, int lane, int hb, int nm, u
     }
     if (G >= 2 * gmin) return false;
     if (nm <= 1) return true;   // one gap already costs more than the one non-match
-    const int x0 = xs[0], x1 = xs[1], xl = xs[nm - 1];
-    // this lane's diagonal: its non-matches in (x0, x1) and (x1, x2)
+    // this lane's diagonal
     const int kl = lane - 16;
     const bool other = kl >= XCENTER - hb && kl <= XCENTER + hb && kl != kb;
     const int kr = other ? kl : 0;
     const uint8_t *rp = refw + (kr & ~3);
     const uint32_t sh = (uint32_t)(kr & 3);
-    int c1 = 0, c2 = 0;
-    for (int i = (x0 + 1) & ~3; i < xl; i += 4) {
-        const uint32_t rd = *(const uint32_t *)(rdc + i) & 0x07070707u;
-        const uint32_t rv = __builtin_amdgcn_alignbyte(*(const uint32_t *)(rp + i + 4), *(const uint32_t *)(rp + i), sh) >> 2;
-        uint32_t x = (rd ^ rv) | ((rd | rv) & 0x04040404u);
-        x = (x | (x >> 1) | (x >> 2)) & 0x01010101u;
-        // bytes u with i + u in (lo, hi): from byte lo - i + 1, below byte hi - i
-        auto between = [&](int lo, int hi) {
-            const int a = lo + 1 - i, b = hi - i;
-            const uint32_t ma_ = a <= 0 ? ~0u : a >= 4 ? 0u : ~0u << (8 * a);
-            const uint32_t mb_ = b >= 4 ? ~0u : b <= 0 ? 0u : ~0u >> (8 * (4 - b));
-            return ma_ & mb_;
-        };
-        c1 += __builtin_popcount(x & between(x0, x1));
-        if (nm == 3) c2 += __builtin_popcount(x & between(x1, xl));
-    }
     const int d = kl > kb ? kl - kb : kb - kl;
     const int gI = oeI + exI * (d - 1), gD = oeD + exD * (d - 1);
     const int gc = gI < gD ? gI : gD;
-    bool fail = es[0] + es[1] - ma * c1 >= gc;
-    if (nm == 3)
-        fail = fail || es[1] + es[2] - ma * c2 >= gc || es[0] + es[1] + es[2] - ma * (c1 + c2) >= gc;
+    // the runs: (x0, x1), and with three non-matches (x1, x2) and (x0, x2)
+    // without x1
+    bool fail = false;
+    const int nruns = nm == 3 ? 3 : 1;
+    for (int r = 0; r < nruns; ++r) {
+        const int lo = r == 1 ? xs[1] : xs[0];
+        const int hi = r == 0 ? xs[1] : xs[2];
+        const int ex = r == 2 ? xs[1] : -1;
+        const int esum = r == 0 ? es[0] + es[1] : r == 1 ? es[1] + es[2] : G;
+        const int R = esum - gmin;
+        if (R < 0) continue;                 // gc >= gmin: no shape can gain
+        const int n = R / ma + 1;
+        int cnt, f, g;
+        scan_run(rdc, rp, sh, other, lo, hi, ex, n, cnt, f, g);
+        // (i): esum - ma * c_k < gc, with cnt = c_k or cnt >= n
+        if (esum - ma * cnt >= gc) fail = true;
+        // (ii)
+        const int gminl = wave_min(other ? g : INT32_MAX);
+        const int fmaxl = wave_max(other ? f : INT32_MIN);
+        if (gminl < fmaxl) return false;
+    }
     return __builtin_amdgcn_ballot_w64(other && fail) == 0;
 }
 
@@ -2600,6 +2676,96 @@ const int64_t *map_stats_host(Ctx &c)
         M.stats_host_valid = true;
     }
     return M.stats_host.data();
+}
+
+// ---------------------------------------------------------------------------
+// Diagnostics: k_probe_ext runs, for caller-given (read, strand, ref, centre)
+// extensions, both the exact ungapped fast path (dp_ungapped) and the full
+// banded DP (dp_pair) on the same staged tables, one wave per extension, and
+// writes [fast, best, row, lane] of the fast path (zeros when it declines),
+// the band half, and [best, row, lane] of the full DP.  Whenever the fast path accepts, the
+// full DP must find the same best cell (tests/test_gpu_fastpath.py feeds it
+// adversarial low-complexity windows).  Not on any product path.
+// ---------------------------------------------------------------------------
+template <int LOCAL>
+__global__ __launch_bounds__(64) void k_probe_ext(DpArgs A, const int32_t *items, int32_t *out, int n)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int e = blockIdx.x;
+    if (e >= n) return;
+    uint32_t *bits = (uint32_t *)smem;
+    unsigned char *xbase = smem + (size_t)32 * A.rows_pad;
+    const XView X0 = xview(xbase, A.rows_pad, 0);
+    const int gmin = A.oeI < A.oeD ? A.oeI : A.oeD;
+    const int r = items[4 * e];
+    XItem it;
+    it.sid = 0;
+    it.m = A.R.len[r];
+    it.roff = A.R.off[r];
+    it.strand = items[4 * e + 1];
+    it.ref = items[4 * e + 2];
+    it.d0 = items[4 * e + 3] - XCENTER;
+    it.reflen = A.I.ref_len[it.ref];
+    it.gref = A.I.ref_off[it.ref];
+    it.hb = A.len_tab[3 * (MAXLEN + 1) + it.m];
+    stage_ext<LOCAL>(A, it, X0, lane);
+    wave_sync();
+    int best = 0, bi = 0, bl = 0, low = -1;
+    const bool fast = it.m > 2 * GBAR + 8 && it.m <= 512 &&
+                      dp_ungapped<LOCAL>(X0, it.m, lane, gmin, it.hb, best, bi, bl, low, A.oeI, A.exI,
+                                        A.oeD, A.exD);
+    wave_sync();
+    int b0, i0, l0, b1, i1, l1;
+    dp_pair<LOCAL>(A, X0, X0, it.m, it.m, it.hb, it.hb, bits, lane, b0, i0, l0, b1, i1, l1);
+    if (lane == 0) {
+        int32_t *o = out + 8 * e;
+        o[0] = fast;
+        o[1] = fast ? best : 0;
+        o[2] = fast ? bi : 0;
+        o[3] = fast ? bl : 0;
+        o[4] = it.hb;
+        o[5] = b0;
+        o[6] = i0;
+        o[7] = l0;
+    }
+}
+
+int run_probe_ext(Ctx &c, const mh_params &par, int n, const int32_t *items, int32_t *out)
+{
+    if (c.index.n_refs <= 0 || c.reads.n <= 0 || n < 0) { set_error("mh_probe_extend: no index / reads"); return -3; }
+    if (par.mode != MH_E2E && par.mode != MH_LOCAL) { set_error("mh_probe_extend: bad mode"); return -3; }
+    if (c.len_tab == nullptr || c.len_tab_key != len_tab_key(par)) { set_error("mh_probe_extend: length tables"); return -3; }
+    // every item checked on the host before the launch: read, strand, ref
+    for (int e = 0; e < n; ++e) {
+        if (items[4 * e] < 0 || items[4 * e] >= c.reads.n || (items[4 * e + 1] & ~1) ||
+            items[4 * e + 2] < 0 || items[4 * e + 2] >= c.index.n_refs) {
+            set_error("mh_probe_extend: item %d out of range", e);
+            return -3;
+        }
+    }
+    if (n == 0) return 0;
+    const int rows_pad = ((c.reads.max_len + 7) / 8) * 8;
+    const int lds = 32 * rows_pad + 2 * xview_bytes(rows_pad);
+    if (lds > 160 * 1024) { set_error("mh_probe_extend: reads too long"); return -3; }
+    hipStream_t s = c.stream;
+    int32_t *d_items = nullptr, *d_out = nullptr;
+    MH_HIP(hipMalloc(&d_items, sizeof(int32_t) * 4 * (size_t)n));
+    MH_HIP(hipMalloc(&d_out, sizeof(int32_t) * 8 * (size_t)n));
+    MH_HIP(hipMemcpyAsync(d_items, items, sizeof(int32_t) * 4 * (size_t)n, hipMemcpyHostToDevice, s));
+    DpArgs da{c.reads, c.index, c.len_tab, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+              nullptr, nullptr, nullptr, 0, rows_pad, lds,
+              par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext, par.rdg_ext};
+    const void *kf = par.mode == MH_LOCAL ? (const void *)k_probe_ext<1> : (const void *)k_probe_ext<0>;
+    MH_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    if (par.mode == MH_LOCAL) hipLaunchKernelGGL((k_probe_ext<1>), dim3(n), dim3(64), lds, s, da, d_items, d_out, n);
+    else hipLaunchKernelGGL((k_probe_ext<0>), dim3(n), dim3(64), lds, s, da, d_items, d_out, n);
+    MH_HIP(hipGetLastError());
+    MH_HIP(hipMemcpyAsync(out, d_out, sizeof(int32_t) * 8 * (size_t)n, hipMemcpyDeviceToHost, s));
+    MH_HIP(hipStreamSynchronize(s));
+    hipFree(d_items);
+    hipFree(d_out);
+    return 0;
 }
 
 int run_map(Ctx &c, const mh_params &par)

@@ -68,6 +68,12 @@ def _declare(L):
         'mh_reads_count': ([_P, _I64P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         'mh_reads_set_names': ([_P, ctypes.c_int64, ctypes.POINTER(ctypes.c_char_p)], ctypes.c_int),
         'mh_map': ([_P, ctypes.POINTER(Params)], ctypes.c_int),
+        'mh_probe_extend': ([_P, ctypes.POINTER(Params), ctypes.c_int, _P, _P], ctypes.c_int),
+        'mh_conseqs_build': ([ctypes.c_int, _P, _P, _P, _P, ctypes.c_int32, _P, _P, _P, ctypes.c_int64,
+                              _P, _P, _P, _P, _P, ctypes.c_char_p, _P, ctypes.c_int64, _P, _P],
+                             ctypes.c_int),
+        'mh_top_tokens': ([ctypes.c_int32, ctypes.c_int32, _P, _P, _P, ctypes.c_char_p, ctypes.c_int32, _P,
+                           _P], ctypes.c_int),
         'mh_alns_fetch': ([_P, ctypes.c_int64, ctypes.c_int64, _P], ctypes.c_int),
         'mh_map_counts': ([_P, _P, _P, _P, _P, _P, _I64P, _I64P, _I64P], ctypes.c_int),
         'mh_map_stats': ([_P, _P], ctypes.c_int),
@@ -243,6 +249,48 @@ def check(status, what):
     if status == -1:
         raise RuntimeError(msg or 'Traceback failed, try local alignment')
     raise NativeError('{} failed ({}): {}'.format(what, status, msg))
+
+
+def top_tokens(length, rows, dense, nflag, dflag, seed, tok):
+    """mh_top_tokens: tok[:length] = the top base-like token of each
+    position (host code of the library; dense (>= rows, 4) int32, flags
+    uint8, seed bytes); returns whether any row holds a positive count."""
+    pos = ctypes.c_int32()
+    check(lib().mh_top_tokens(length, rows, _ptr(dense), _ptr(nflag), _ptr(dflag), seed, len(seed),
+                              _ptr(tok), ctypes.byref(pos)), 'mh_top_tokens')
+    return bool(pos.value)
+
+
+def conseqs_build(rows_of, lengths, seeds, dense, nflag, dflag, ev_row, ev_pos, ev_tok, ev_cnt):
+    """mh_conseqs_build: [(consensus bytes, present)] per selected row.
+    dense (n, cap, 4) int32, flags (n, cap) uint8, all C-contiguous; seeds
+    bytes per selected row; events as parallel sequences (row, pos, token
+    str, merged pairs)."""
+    n = len(rows_of)
+    cap = dense.shape[1] if dense.ndim == 3 else 0
+    rows_of = np.ascontiguousarray(rows_of, dtype=np.int32)
+    lengths = np.ascontiguousarray(lengths, dtype=np.int32)
+    seed_bufs = [ctypes.create_string_buffer(sd, len(sd) + 1) for sd in seeds]
+    seed_ptrs = (ctypes.c_char_p * max(n, 1))(*[ctypes.cast(b, ctypes.c_char_p) for b in seed_bufs])
+    seed_lens = np.ascontiguousarray([len(sd) for sd in seeds], dtype=np.int32)
+    pool = ''.join(ev_tok).encode('latin-1')
+    ev_len = np.ascontiguousarray([len(t) for t in ev_tok], dtype=np.int32)
+    ev_off = np.zeros(max(len(ev_tok), 1), dtype=np.int64)
+    if len(ev_tok):
+        ev_off[1:len(ev_tok)] = np.cumsum(ev_len)[:-1]
+    ev_row = np.ascontiguousarray(ev_row, dtype=np.int32)
+    ev_pos = np.ascontiguousarray(ev_pos, dtype=np.int32)
+    ev_cnt = np.ascontiguousarray(ev_cnt, dtype=np.int64)
+    out_cap = int(lengths.sum()) + int(ev_len.sum()) + 1
+    out = np.zeros(out_cap, dtype=np.uint8)
+    off = np.zeros(n + 1, dtype=np.int64)
+    present = np.zeros(max(n, 1), dtype=np.int32)
+    check(lib().mh_conseqs_build(n, _ptr(rows_of), _ptr(lengths), seed_ptrs, _ptr(seed_lens), cap,
+                                 _ptr(dense), _ptr(nflag), _ptr(dflag), len(ev_tok), _ptr(ev_row),
+                                 _ptr(ev_pos), _ptr(ev_off), _ptr(ev_len), _ptr(ev_cnt), pool,
+                                 _ptr(out), out_cap, _ptr(off), _ptr(present)), 'mh_conseqs_build')
+    raw = out.tobytes()
+    return [(raw[off[k]:off[k + 1]], bool(present[k])) for k in range(n)]
 
 
 def device_count():
@@ -860,6 +908,17 @@ class Context:
         out = np.zeros(5, dtype=np.int64)
         check(lib().mh_map_stats(self.h, _ptr(out)), 'mh_map_stats')
         return tuple(int(x) for x in out)
+
+    def probe_extend(self, par, items):
+        """Diagnostics: items = (n, 4) int32 (read, strand, ref, centre) of
+        the loaded reads and built index; returns (n, 8) int32 rows (fast
+        path taken, its score, row, lane; band half; the full DP's score,
+        row, lane) -- mh_probe_extend."""
+        items = np.ascontiguousarray(items, dtype=np.int32).reshape(-1, 4)
+        out = np.zeros((max(len(items), 1), 8), dtype=np.int32)
+        check(lib().mh_probe_extend(self.h, ctypes.byref(par), len(items), _ptr(items), _ptr(out)),
+              'mh_probe_extend')
+        return out[:len(items)]
 
     def test_set_capacities(self, cigar_pool_words=0, pileup_events=0, pileup_event_bytes=0,
                             token_bytes=0):

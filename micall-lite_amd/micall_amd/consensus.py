@@ -19,6 +19,8 @@ from collections import Counter
 
 import numpy as np
 
+from . import _native
+
 BASE_CODES = np.frombuffer(b'ACGT', dtype=np.uint8)
 BASE_INDEX = np.full(256, 255, dtype=np.int64)   # 'A' 'C' 'G' 'T' -> 0..3, else 255
 BASE_INDEX[BASE_CODES] = np.arange(4)
@@ -121,36 +123,56 @@ class Pileup:
                 c[token] += count
         return c
 
+    def native_arrays(self):
+        """dense (n, cap, 4) int32 and the flags (n, cap) uint8, contiguous
+        (converted once when a pileup arrives in another dtype)."""
+        if getattr(self, '_native', None) is None:
+            d, nf, df = self.dense, self.nflag, self.dflag
+            if d.dtype != np.int32 or not d.flags.c_contiguous:
+                d = np.ascontiguousarray(d, dtype=np.int32)
+            if nf.dtype != np.uint8 or not nf.flags.c_contiguous:
+                nf = np.ascontiguousarray(nf != 0, dtype=np.uint8)
+            if df.dtype != np.uint8 or not df.flags.c_contiguous:
+                df = np.ascontiguousarray(df != 0, dtype=np.uint8)
+            self._native = (d, nf, df)
+        return self._native
+
+    def _rows(self, r):
+        """The reference's fetched counter rows as the native call takes
+        them: (cap, 4) int32 counts and uint8 flags, contiguous."""
+        d, nf, df = self.dense[r], self.nflag[r], self.dflag[r]
+        if d.dtype != np.int32 or not d.flags.c_contiguous:
+            d = np.ascontiguousarray(d, dtype=np.int32)
+        if nf.dtype != np.uint8 or not nf.flags.c_contiguous:
+            nf = np.ascontiguousarray(nf != 0, dtype=np.uint8)
+        if df.dtype != np.uint8 or not df.flags.c_contiguous:
+            df = np.ascontiguousarray(df != 0, dtype=np.uint8)
+        return d, nf, df
+
     def has_positive(self, r):
-        return bool(self.dense[r].max() > 0) or r in self._ev
+        if r in self._ev:
+            return True
+        rd, rnf, rdf = self._rows(r)
+        return _native.top_tokens(0, len(rd), rd, rnf, rdf, b'', np.zeros(1, dtype=np.uint8))
 
     def tokens(self, r, seed):
         """Top token per position 1..end-1 (remap.py:318-321), one byte each
         (0: no token), and {index: token} for the positions whose top token
-        is longer than one character (a base with its insertion)."""
+        is longer than one character (a base with its insertion).  The
+        base-like entries (counts, seed prefill, 'N', '-') are ranked by the
+        library's host code (mh_top_tokens, one pass over the rows); the
+        insertion tokens are merged in here."""
         end = max(int(self.max_pos[r]), len(seed) if seed else 0) + 1
         length = end - 1
-        d, nf, df = self._slice(r, length)
-        tok = np.zeros(length, dtype=np.uint8)
-        if length:
-            # column-wise: numpy's reductions over a 4-wide axis cost a
-            # per-row overhead (0.13 ms for 3 kb)
-            c0, c1, c2, c3 = d[:, 0], d[:, 1], d[:, 2], d[:, 3]
-            top = np.maximum(np.maximum(c0, c1), np.maximum(c2, c3))
-            positive = top > 0
-            # a positive count wins; ties go to the first of A<C<G<T
-            first = np.where(c0 == top, 0, np.where(c1 == top, 1, np.where(c2 == top, 2, 3)))
-            tok[positive] = BASE_CODES[first[positive]]
-            # otherwise: seed prefill (0) > 'N' (-1) > '-' (-2) > nothing
-            fill = np.zeros(length, dtype=np.uint8)
-            fill[df] = DASH
-            fill[nf] = ord('N')
-            if seed:
-                k = min(len(seed), length)
-                fill[:k] = np.frombuffer(seed[:k].encode('latin-1'), dtype=np.uint8)
-            tok[~positive] = fill[~positive]
+        tok = np.zeros(max(length, 1), dtype=np.uint8)
+        rd, rnf, rdf = self._rows(r)
+        sb = seed.encode('latin-1') if seed else b''
+        # (no count lies past max_pos: positive over 1..length is over the row)
+        self.last_positive = _native.top_tokens(length, min(length, self.cap), rd, rnf, rdf, sb, tok)
+        tok = tok[:length]
         longer = {}
         if r in self._ev:
+            d, nf, df = self._slice(r, length)
             # a few events: one Counter per position; many: vectorised (its
             # fixed cost, ~0.1 ms of numpy calls, pays from ~150 events)
             if len(self._ev[r][0]) < 160:
@@ -329,14 +351,44 @@ def _assemble(tok, longer):
 
 
 def counts_to_conseqs(pile, order, seeds=None):
-    """{rname: consensus} in refmap order (remap.py:309-333)."""
+    """{rname: consensus} in refmap order (remap.py:309-333): every
+    reference in one call of the library's host code (mh_conseqs_build: the
+    top token of each position's Counter, insertion tokens merged, then the
+    deletion-run rule).  counts_to_conseqs_py is the same in Python (the
+    tests hold the two equal)."""
+    order = list(order)
+    if not order:
+        return {}
+    dense, nflag, dflag = pile.native_arrays()
+    lengths, seed_bytes = [], []
+    for r in order:
+        seed = seeds.get(pile.refnames[r]) if seeds else None
+        lengths.append(max(int(pile.max_pos[r]), len(seed) if seed else 0))
+        seed_bytes.append(seed.encode('latin-1') if seed else b'')
+    ev_row, ev_pos, ev_tok, ev_cnt = [], [], [], []
+    for r in order:
+        g = pile._ev.get(r)
+        if g:
+            ev_row.extend([r] * len(g[0]))
+            ev_pos.extend(g[0])
+            ev_tok.extend(g[1])
+            ev_cnt.extend(g[2])
+    built = _native.conseqs_build(order, lengths, seed_bytes, dense, nflag, dflag, ev_row, ev_pos, ev_tok,
+                                  ev_cnt)
+    return {pile.refnames[r]: text.decode('latin-1') for r, (text, present) in zip(order, built) if present}
+
+
+def counts_to_conseqs_py(pile, order, seeds=None):
+    """counts_to_conseqs in Python (numpy per reference; the tests' second
+    implementation)."""
     conseqs = {}
     for r in order:
         name = pile.refnames[r]
         seed = seeds.get(name) if seeds else None
-        if not pile.has_positive(r):
+        tok, longer = pile.tokens(r, seed)
+        if not (pile.last_positive or r in pile._ev):
             continue
-        conseqs[name] = _assemble(*pile.tokens(r, seed))
+        conseqs[name] = _assemble(tok, longer)
     return conseqs
 
 

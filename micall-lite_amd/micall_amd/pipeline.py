@@ -248,6 +248,8 @@ class RemapPipeline:
         self.callback = callback
         self.raw_count = None
         self.log = []
+        self.first_mapped_to = None
+        self.pass_refs = []
 
     # ---- plumbing --------------------------------------------------------
     def _params(self, mode):
@@ -402,12 +404,15 @@ class RemapPipeline:
         new_counts = Counter()
         unmapped_count = raw_count
         self.mapped_to = None
+        self.first_mapped_to = dict(conseqs)   # the prelim consensus set the first pass maps to
+        self.pass_refs = []                     # every pass's consensus set, in pass order
         while conseqs:
             if self.callback:
                 self.callback(message='... remap iteration %d' % n_remaps, progress=0)
             if before_pass is not None:
                 before_pass()
             self.mapped_to = mapped_to = conseqs
+            self.pass_refs.append(dict(conseqs))
             new_counts, unmapped_count = self.map_to_reference(conseqs)
             if after_pass is not None:
                 after_pass()

@@ -190,18 +190,30 @@ def _open_members(sh, sources):
             got = t.cpu().numpy()
             for j, k in enumerate(live):
                 windows[k] = got[j * win:(j + 1) * win].tobytes()
+        # Whatever goes wrong on this rank, rank r + 1 is blocked in recv
+        # until a window arrives: a failed tail (any exception, not only the
+        # library's) is sent on as zeros and marked unresolved, so the CRC
+        # agreement below fails on every rank and the file is decoded whole.
         tails = []
         for k in live:
             try:
                 tail = fqs[k].member_tail(windows[k])
-            except _native.NativeError:
+                if tail is not None:
+                    tail = np.asarray(tail, dtype=np.uint8).reshape(-1)
+            except Exception:   # noqa: BLE001 -- the chain must not stall
                 tail = None
-            if tail is None:          # sent on anyway (the chain must not stall); the CRC check fails
+            if tail is None or len(tail) != win:
                 resolved[k] = False
                 tail = np.zeros(win, dtype=np.uint8)
             tails.append(tail)
         if r + 1 < W:
-            dist.send(torch.from_numpy(np.concatenate(tails)).to(dev), dst=r + 1)
+            try:
+                msg = np.concatenate(tails)
+            except Exception:   # noqa: BLE001
+                for k in live:
+                    resolved[k] = False
+                msg = np.zeros(win * len(live), dtype=np.uint8)
+            dist.send(torch.from_numpy(msg).to(dev), dst=r + 1)
 
     def finish(k):
         if k not in resolved or not resolved[k]:

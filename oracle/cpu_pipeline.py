@@ -243,9 +243,111 @@ def _pileup_fast(prep, alns, recs, n_refs, ref_lens, nthreads, q=20):
     return dense, rc, fu, mp, ev, ne.value, pool.raw, cap
 
 
-def timed_step(seed_set, all_seeds, seed_groups, prep, nthreads, count_threshold=10):
+def _position_sums(pile, r, length):
+    """sum(counts[pos].values()) for pos 1..length of reference r of an
+    og_pileup result (remap.py:236-237): the base counts, -1 where an N was
+    seen, -2 where a deletion was, and every insertion token's count; the
+    seed prefill adds 0."""
+    dense, _rc, _fu, _mp, ev, ne, _pool, cap = pile
+    d = np.asarray(dense).reshape(-1, cap, 6)[r, :length].astype(np.int64)
+    s = d[:, 0] + d[:, 1] + d[:, 2] + d[:, 3] - (d[:, 4] != 0) - 2 * (d[:, 5] != 0)
+    if ne:
+        e = np.frombuffer(ev, dtype=np.int32, count=4 * ne).reshape(ne, 4)
+        pos = e[(e[:, 0] == r) & (e[:, 1] >= 1) & (e[:, 1] <= length), 1]
+        np.add.at(s, pos - 1, 1)
+    return s
+
+
+def distance_filter(names, all_seeds, pile, order, new_conseqs, filter_coverage, nthreads,
+                    distance_report=None):
+    """The consensus-distance filter of remap.sam_to_conseqs (remap.py:228-268,
+    extract_relevant_seed :129-138) on the oracle's pileup: for every
+    consensus (name order), its positions whose counts sum to at least
+    filter_coverage; og_gotoh_align of each seed (name order) against them,
+    global, gop 15 / gep 3, HYPHY_NUC (remap.py:33, :248); the seed's part
+    under the consensus; og_levenshtein (C, so 30 kb strings take seconds).
+    A consensus stays when its own seed is no farther than the nearest other;
+    if none stays, the reference with the most merged pairs (ties: first
+    counted) does.  The K x K alignments run on nthreads host threads
+    (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from cpu_e2e import HYPHY_NUC
+    if len(new_conseqs) < 2:
+        return new_conseqs
+    matrix, alphabet = HYPHY_NUC
+    index = {names[r]: r for r in order}
+    conseq_names = sorted(new_conseqs)
+    relevant = {}
+    for name in conseq_names:
+        conseq = new_conseqs[name]
+        keep = _position_sums(pile, index[name], len(conseq)) >= filter_coverage
+        rel = ''.join(c for c, k in zip(conseq, keep) if k)
+        if rel:
+            relevant[name] = rel
+    jobs = [(name, seed_name) for name in conseq_names if name in relevant for seed_name in conseq_names]
+
+    def one(job):
+        name, seed_name = job
+        a_seed, a_conseq, _ = oracle.gotoh_align(oracle.clean_sequence(all_seeds[seed_name], alphabet),
+                                                 oracle.clean_sequence(relevant[name], alphabet),
+                                                 15, 3, True, alphabet, matrix)
+        return oracle.levenshtein(oracle.extract_relevant_seed(a_conseq, a_seed), relevant[name])
+
+    # longest alignments first, so the pool ends together
+    by_size = sorted(range(len(jobs)), key=lambda j: -len(all_seeds[jobs[j][1]]) * len(relevant[jobs[j][0]]))
+    dists = [None] * len(jobs)
+    with ThreadPoolExecutor(max(1, nthreads)) as pool:
+        for j, d in zip(by_size, pool.map(lambda j: one(jobs[j]), by_size)):
+            dists[j] = d
+    filtered = {}
+    for name in conseq_names:
+        if name not in relevant:
+            continue
+        seed_dist = other_dist = other_seed = None
+        for (n2, seed_name), d in zip(jobs, dists):
+            if n2 != name:
+                continue
+            if seed_name == name:
+                seed_dist = d
+            elif other_dist is None or d < other_dist:
+                other_seed, other_dist = seed_name, d
+        if seed_dist <= other_dist:
+            filtered[name] = new_conseqs[name]
+        if distance_report is not None:
+            distance_report[name] = dict(seed_dist=seed_dist, other_dist=other_dist, other_seed=other_seed)
+    if not filtered:
+        rc = pile[1]
+        counts = Counter()
+        for r in order:
+            counts[names[r]] = int(rc[r])
+        best_ref = counts.most_common(1)[0][0]
+        filtered[best_ref] = new_conseqs[best_ref]
+    return filtered
+
+
+def converged(old_names, new_names, new_counts, map_counts, raw_count, n_remaps):
+    """remap.py:591-603: with the consensus names unchanged, stop when no
+    reference gained mapped lines, or more than 95 % of raw_count mapped, or
+    after MAX_REMAPS passes."""
+    from cpu_e2e import MAX_REMAPS, MIN_MAPPING_EFFICIENCY
+    if new_names != old_names:
+        return False
+    if all(n <= map_counts[name] for name, n in new_counts.items()):
+        return True
+    if sum(new_counts.values()) / float(raw_count) > MIN_MAPPING_EFFICIENCY:
+        return True
+    return n_remaps >= MAX_REMAPS
+
+
+def timed_step(seed_set, all_seeds, seed_groups, prep, nthreads, count_threshold=10,
+               max_iterations=1, min_iterations=None):
     """run_step on prepared reads: prelim e2e pass over every seed, seed
-    selection, prelim consensus, one --local pass, pileup and consensus.
+    selection, prelim consensus, then remap()'s loop (remap.py:544-606):
+    --local pass against the consensus set, pileup, consensus, the
+    consensus-distance filter (filter_coverage = count_threshold / 2,
+    remap.py:576-581), stopping rules -- capped at max_iterations passes,
+    and with the rules held off for min_iterations (bench configs only, as
+    RemapPipeline.iterate).  raw_count = 2 x units (remap.py:457).
     Returns (conseqs, seconds); only this function's body is timed."""
     _declare_fast(oracle.lib())
     t0 = time.perf_counter()
@@ -271,17 +373,40 @@ def timed_step(seed_set, all_seeds, seed_groups, prep, nthreads, count_threshold
     pile = _pileup_fast(prep, prep.alns, recs, len(names), [len(seed_set[k]) for k in names], nthreads)
     order = sorted((r for r in range(len(names)) if pile[2][r] >= 0), key=lambda r: first[names[r]])
     conseqs = {k: v for k, v in _conseqs(names, all_seeds, pile, order).items() if k in seed_counts}
+    map_counts = {k: seed_counts[k] for k in conseqs}
     prelim_conseqs, cn, recs2 = dict(conseqs), [], None
-    if conseqs:
+    raw_count = 2.0 * (prep.n // 2 if prep.paired else prep.n)
+    passes = []
+    n_remaps = 0
+    while conseqs:
+        mapped_to = conseqs
         cn = list(conseqs)
         ix2 = oracle.Index([conseqs[k] for k in cn], 20)
         recs2 = _map_fast(prep, ix2, oracle.LOCAL, nthreads, prep.alns2)
+        r2 = recs2['sam_ref']
+        ok = (r2 >= 0) & ((recs2['flag'] & 4) == 0)
+        per_ref = np.bincount(r2[ok], minlength=len(cn))
+        firstm = {r: int(np.argmax(ok & (r2 == r))) for r in np.flatnonzero(per_ref)}
+        new_counts = Counter()
+        for r in sorted(firstm, key=firstm.get):
+            new_counts[cn[r]] = int(per_ref[r])
         pile2 = _pileup_fast(prep, prep.alns2, recs2, len(cn), [len(conseqs[k]) for k in cn], nthreads)
         order2 = sorted((r for r in range(len(cn)) if pile2[2][r] >= 0), key=lambda r: pile2[2][r])
-        conseqs = _conseqs(cn, all_seeds, pile2, order2)
+        new = _conseqs(cn, all_seeds, pile2, order2)
+        conseqs = distance_filter(cn, all_seeds, pile2, order2, new, count_threshold / 2, nthreads)
+        n_remaps += 1
+        passes.append(dict(names=cn, new_counts=dict(new_counts), unfiltered=sorted(new),
+                           kept=sorted(conseqs)))
+        if max_iterations is not None and n_remaps >= max_iterations:
+            break
+        forced = min_iterations is not None and n_remaps < min_iterations
+        if not forced and converged(set(mapped_to), set(conseqs), new_counts, map_counts, raw_count,
+                                    n_remaps):
+            break
+        map_counts = dict(new_counts)
     secs = time.perf_counter() - t0
     prep.result = dict(prelim=recs, prelim_names=names, prelim_conseqs=prelim_conseqs,
-                       remap=recs2, remap_names=cn, conseqs=conseqs)
+                       remap=recs2, remap_names=cn, conseqs=conseqs, passes=passes)
     return conseqs, secs
 
 

@@ -50,24 +50,30 @@ int og_gotoh_align(const char *s1, const char *s2, int gop, int gep, int is_glob
     for (int k = 0; k < 256; ++k) code[k] = -1;
     for (int k = 0; k < L; ++k) code[(unsigned char)alphabet[k]] = k;
 
+    /* The costs are kept two rows at a time (rows i-1 and i of R and P, row
+     * i of Q) plus R's last column: the traceback reads R only there and on
+     * the last row.  The bit matrix is the one full (m+2)x(n+2) array, one
+     * byte per cell, so a 30 kb x 30 kb alignment (C4-all's SARS-CoV-2
+     * consensus against its seed) needs 0.9 GB instead of 12. */
     const size_t W = (size_t)n + 1, BW = (size_t)n + 2;
-    const size_t cells = (size_t)(m + 1) * W;
     int *a = malloc(sizeof(int) * (size_t)m), *b = malloc(sizeof(int) * (size_t)n);
-    int *R = malloc(sizeof(int) * cells), *P = malloc(sizeof(int) * cells),
-        *Q = malloc(sizeof(int) * cells);
+    int *R0 = malloc(sizeof(int) * W), *R1 = malloc(sizeof(int) * W),
+        *P0 = malloc(sizeof(int) * W), *P1 = malloc(sizeof(int) * W),
+        *Q = malloc(sizeof(int) * W), *Rcol = malloc(sizeof(int) * ((size_t)m + 1));
     uint8_t *bt = calloc((size_t)(m + 2) * BW, 1);
     char *r1 = malloc((size_t)m + n + 1), *r2 = malloc((size_t)m + n + 1);
     int status = 0;
-    if (!a || !b || !R || !P || !Q || !bt || !r1 || !r2) { status = -2; goto done; }
+    if (!a || !b || !R0 || !R1 || !P0 || !P1 || !Q || !Rcol || !bt || !r1 || !r2) { status = -2; goto done; }
 
     for (int i = 0; i < m; ++i) if ((a[i] = code[(unsigned char)s1[i]]) < 0) { status = -3; goto done; }
     for (int j = 0; j < n; ++j) if ((b[j] = code[(unsigned char)s2[j]]) < 0) { status = -3; goto done; }
 
-#define IX(i, j) ((size_t)(i) * W + (size_t)(j))
 #define BX(i, j) ((size_t)(i) * BW + (size_t)(j))
     const int u = gep, v = gop;
 
-    /* ---- cost assignment (row-major, same visiting order as :142-143) ---- */
+    /* ---- cost assignment (row-major, same visiting order as :142-143);
+     * Rp/Pp: row i-1, Rc/Pc: row i ---- */
+    int *Rp = R0, *Rc = R1, *Pp = P0, *Pc = P1;
     for (int i = 0; i <= m; ++i) {
         for (int j = 0; j <= n; ++j) {
             int p, q, r;
@@ -75,7 +81,7 @@ int og_gotoh_align(const char *s1, const char *s2, int gop, int gep, int is_glob
             if (i == 0) {
                 p = OG_INF;
             } else {
-                const int pu = P[IX(i - 1, j)], ru = R[IX(i - 1, j)];
+                const int pu = Pp[j], ru = Rp[j];
                 p = u + imin(pu, ru + v);
                 if (pu != OG_INF && p == pu + u) bt[BX(i - 1, j)] |= BIT_D;
                 if (p == ru + v + u) bt[BX(i - 1, j)] |= BIT_E;
@@ -84,7 +90,7 @@ int og_gotoh_align(const char *s1, const char *s2, int gop, int gep, int is_glob
             if (j == 0) {
                 q = OG_INF;
             } else {
-                const int ql = Q[IX(i, j - 1)], rl = R[IX(i, j - 1)];
+                const int ql = Q[j - 1], rl = Rc[j - 1];
                 q = u + imin(ql, rl + v);
                 if (ql != OG_INF && q == ql + u) bt[BX(i, j - 1)] |= BIT_F;
                 if (q == rl + v + u) bt[BX(i, j - 1)] |= BIT_G;
@@ -95,15 +101,19 @@ int og_gotoh_align(const char *s1, const char *s2, int gop, int gep, int is_glob
             } else if (i == 0 || j == 0) {
                 r = is_global ? imin(p, q) : 0; /* borders: v+u*k global, 0 ends-free */
             } else {
-                dg = R[IX(i - 1, j - 1)] - matrix[a[i - 1] * L + b[j - 1]];
+                dg = Rp[j - 1] - matrix[a[i - 1] * L + b[j - 1]];
                 r = imin(imin(dg, p), q);
             }
-            P[IX(i, j)] = p; Q[IX(i, j)] = q; R[IX(i, j)] = r;
+            Pc[j] = p; Q[j] = q; Rc[j] = r;
             if (r == p) bt[BX(i, j)] |= BIT_A;
             if (r == q) bt[BX(i, j)] |= BIT_B;
             if (i > 0 && j > 0 && r == dg) bt[BX(i, j)] |= BIT_C;
         }
+        Rcol[i] = Rc[n];
+        int *t = Rp; Rp = Rc; Rc = t;
+        t = Pp; Pp = Pc; Pc = t;
     }
+    const int *Rlast = Rp;   /* row m after the final swap */
 
     /* ---- boundary bits of the (m+2)x(n+2) bit matrix (:117-131) ---- */
     if (!is_global) {
@@ -145,10 +155,10 @@ int og_gotoh_align(const char *s1, const char *s2, int gop, int gep, int is_glob
 
     /* ---- traceback (:316-438) ---- */
     {
-        int ii = m, jj = n, best = R[IX(m, n)];
+        int ii = m, jj = n, best = Rlast[n];
         if (!is_global) {
-            for (int i = 0; i <= m; ++i) if (R[IX(i, n)] < best) { best = R[IX(i, n)]; ii = i; jj = n; }
-            for (int j = 0; j <= n; ++j) if (R[IX(m, j)] < best) { best = R[IX(m, j)]; ii = m; jj = j; }
+            for (int i = 0; i <= m; ++i) if (Rcol[i] < best) { best = Rcol[i]; ii = i; jj = n; }
+            for (int j = 0; j <= n; ++j) if (Rlast[j] < best) { best = Rlast[j]; ii = m; jj = j; }
         }
         int len = 0; /* built back to front in r1/r2 */
         if (ii < m) for (int k = m - 1; k >= ii; --k) { r1[len] = s1[k]; r2[len] = '-'; ++len; }
@@ -167,10 +177,10 @@ int og_gotoh_align(const char *s1, const char *s2, int gop, int gep, int is_glob
         out1[len] = out2[len] = '\0';
         *score = -best;
     }
-#undef IX
 #undef BX
 done:
-    free(a); free(b); free(R); free(P); free(Q); free(bt); free(r1); free(r2);
+    free(a); free(b); free(R0); free(R1); free(P0); free(P1); free(Q); free(Rcol); free(bt);
+    free(r1); free(r2);
     return status;
 }
 

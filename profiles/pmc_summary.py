@@ -50,7 +50,16 @@ def main(fetch_csv, write_csv, pairs, out):
                       'hbm_bytes_per_launch': int(round((2 * fk + wk) * 1024))}
     with open(out, 'w') as f:
         json.dump({'pairs': int(pairs), 'rule': '(2*FETCH_SIZE + WRITE_SIZE) * 1024',
-                   'kernels': kernels}, f, indent=1)
+                   'kernel_source_sha': _source_sha(), 'kernels': kernels}, f, indent=1)
+
+
+def _source_sha():
+    """bench.kernel_source_sha() of the tree the passes were collected from
+    (bench.py only uses a summary whose fingerprint matches its own)."""
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_source_sha
+    return kernel_source_sha()
 
 
 if __name__ == '__main__':

@@ -48,7 +48,16 @@ def main(path, out, *kernels):
     with open(out, 'w') as f:
         json.dump({'note': 'rocprofv3 --pmc SQ_* pass (profiles/collect_r02.sh); counters are '
                            'chip totals per dispatch; see profiles/sq_summary.py',
-                   'dispatches': res}, f, indent=1)
+                   'kernel_source_sha': _source_sha(), 'dispatches': res}, f, indent=1)
+
+
+def _source_sha():
+    """bench.kernel_source_sha() of the tree the passes were collected from
+    (bench.py only uses a summary whose fingerprint matches its own)."""
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_source_sha
+    return kernel_source_sha()
 
 
 if __name__ == '__main__':

@@ -139,3 +139,69 @@ def test_assembly_edge_cases():
                    ['-', '-', 'T', '-', '-', '-', '-', 'G', '-']):
         got, want = run(tokens)
         assert got == want, tokens
+
+
+def _random_pileup(rng, n_refs, cap):
+    dense = np.zeros((n_refs, cap, 4), dtype=np.int32)
+    nflag = np.zeros((n_refs, cap), dtype=np.uint8)
+    dflag = np.zeros((n_refs, cap), dtype=np.uint8)
+    max_pos = np.zeros(n_refs, dtype=np.int32)
+    events = []
+    for r in range(n_refs):
+        kind = int(rng.integers(0, 5))
+        if kind == 0:
+            continue                                     # nothing counted: no consensus
+        length = int(rng.integers(5, cap - 5))
+        max_pos[r] = length
+        k = rng.integers(0, 6, size=length)
+        dense[r, :length][k <= 1] = rng.integers(0, 4, size=(int((k <= 1).sum()), 4))
+        nflag[r, :length][k == 2] = 1
+        dflag[r, :length][(k == 3) | ((k == 2) & (rng.random(length) < 0.5))] = 1
+        for _ in range(int(rng.integers(0, 4))):         # deletion runs of 1..7
+            a = int(rng.integers(0, max(1, length - 8)))
+            n = int(rng.integers(1, 8))
+            dense[r, a:a + n] = 0
+            nflag[r, a:a + n] = 0
+            dflag[r, a:a + n] = 1
+        if kind == 4:                                    # only sentinels and events
+            dense[r] = 0
+        for p in rng.choice(np.arange(1, length + 1), size=min(length, int(rng.integers(0, 12))),
+                            replace=False):
+            for _ in range(int(rng.integers(1, 4))):
+                n = int(rng.choice([1, 2, 4, 7]))
+                tok = ''.join(rng.choice(list('ACGT'), size=n))
+                events.append((r, int(p), tok, int(rng.integers(1, 4))))
+    return dict(dense=dense, nflag=nflag, dflag=dflag, read_counts=rng.integers(1, 9, size=n_refs),
+                first_unit=np.arange(n_refs), max_pos=max_pos, cap=cap, events=events)
+
+
+@pytest.mark.parametrize('rs', range(30))
+def test_native_counts_to_conseqs_matches_the_counter(rs):
+    """consensus.counts_to_conseqs (the library's mh_conseqs_build, every
+    reference in one call) against the per-position Counter + find_top_token
+    + token-by-token assembly (remap.py:309-333), and against
+    counts_to_conseqs_py: several references, some with nothing counted or
+    only sentinels and insertion tokens, seeds shorter and longer than the
+    counted span (with N / R / Y), one-character and long tokens, ties."""
+    from micall_amd.consensus import counts_to_conseqs, counts_to_conseqs_py
+    rng = np.random.default_rng(500 + rs)
+    n_refs, cap = 6, 90
+    fetched = _random_pileup(rng, n_refs, cap)
+    names = ['r%d' % r for r in range(n_refs)]
+    seeds = {}
+    for r in range(n_refs):
+        if rng.random() < 0.7:
+            seeds[names[r]] = ''.join(rng.choice(list('ACGTNRY'), size=int(rng.integers(1, cap + 20))))
+    pile = Pileup(fetched, names)
+    order = list(range(n_refs))
+    want = {}
+    for r in order:
+        seed = seeds.get(names[r])
+        toks = _tokens_per_position(pile, r, seed)
+        positive = (pile.dense[r] > 0).any() or any(e[0] == r for e in fetched['events'])
+        if positive:
+            want[names[r]] = _assemble_loop(toks)
+    got = counts_to_conseqs(pile, order, seeds=seeds)
+    assert got == want
+    assert list(got) == list(want)
+    assert counts_to_conseqs_py(pile, order, seeds=seeds) == want

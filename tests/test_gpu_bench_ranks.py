@@ -22,11 +22,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _bench(args, timeout=400):
+def _bench(args, timeout=400, launcher=True):
     env = dict(os.environ, MICALL_BENCH_BACKEND='gloo')
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
-           os.path.join(REPO, 'bench.py'), '--gpus', '2'] + args
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK'):
+        env.pop(k, None)
+    pre = ([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+            '--master-addr', '127.0.0.1', '--master-port', str(_free_port())] if launcher
+           else [sys.executable])
+    cmd = pre + [os.path.join(REPO, 'bench.py'), '--gpus', '2'] + args
     out = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=timeout)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith('{"metric"')]
@@ -74,3 +77,19 @@ def test_bench_chain_two_ranks_gloo():
     for stage in ('censor', 'prelim_map', 'remap'):
         w = io[stage]['written_bytes']
         assert min(w) > 0 and max(w) <= 0.75 * sum(w), (stage, w)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_gpus_2_launches_its_own_ranks():
+    """Plain `bench.py --gpus 2` (no torchrun around it, as the driver may
+    call it): bench.py starts the two ranks itself as a child
+    torch.distributed.run and relays rank 0's line, which reports the world
+    the process group really had."""
+    pairs = 10000
+    d = _bench(['--pairs', str(pairs), '--steps', '1', '--warmup', '1', '--no-cpu-baseline',
+                '--no-e2e'], launcher=False)
+    assert d['n_gpus'] == 2
+    c = d['config']
+    assert c['dist_world'] == 2 and c['dist_backend'] == 'gloo' and len(c['rank_devices']) == 2, c
+    assert sum(d['result']['mapped_lines'].values()) == 2 * 2 * pairs

@@ -132,3 +132,146 @@ def test_fast_path_equals_oracle_full_dp(mode):
             n = ref[i]['n_cigar']
             assert np.array_equal(got[i]['cigar'][:n], ref[i]['cigar'][:n]), (
                 name, i, _native.cigar_text(got[i]), _native.cigar_text(ref[i]))
+
+
+def _low_complexity_reference(rng):
+    """Homopolymer runs, di- and trinucleotide repeats and short random
+    stretches: many diagonals of a band match the read over long stretches,
+    so a one-gap path between two diagonals that are both off the seeded one
+    can beat the seeded diagonal's two or three non-matches."""
+    parts, prev = [], ''
+    while sum(map(len, parts)) < 3000:
+        kind = int(rng.integers(0, 5))
+        if kind <= 1:
+            b = 'ACGT'[int(rng.integers(0, 4))]
+            while b == prev:
+                b = 'ACGT'[int(rng.integers(0, 4))]
+            parts.append(b * int(rng.integers(6, 70)))
+            prev = b
+        elif kind == 2:
+            unit = ['AC', 'AT', 'GT', 'CG', 'AG'][int(rng.integers(0, 5))]
+            parts.append(unit * int(rng.integers(5, 30)))
+            prev = ''
+        elif kind == 3:
+            unit = ['AAC', 'GGT', 'ACT', 'TTG'][int(rng.integers(0, 4))]
+            parts.append(unit * int(rng.integers(4, 20)))
+            prev = ''
+        else:
+            parts.append(''.join('ACGT'[x] for x in rng.integers(0, 4, int(rng.integers(4, 20)))))
+            prev = ''
+    return ''.join(parts)
+
+
+def _low_complexity_cases():
+    rng = np.random.default_rng(2029)
+    ref = _low_complexity_reference(rng)
+    seqs, quals = [], []
+    for _ in range(6000):
+        m = int(rng.choice([251, 150, 300]))
+        st = int(rng.integers(0, len(ref) - m - 8))
+        s = list(ref[st:st + m + 8])
+        # one or two small indels (a run one or two bases shorter or longer):
+        # the read then sits on two or three diagonals of the band
+        for _ in range(int(rng.integers(0, 3))):
+            p = int(rng.integers(10, m - 10))
+            n = int(rng.integers(1, 3))
+            if rng.integers(0, 2):
+                del s[p:p + n]
+            else:
+                s[p:p] = [s[p]] * n
+        s = s[:m]
+        # two or three substitutions (non-matches of the seeded diagonal)
+        for p in rng.choice(m, size=int(rng.integers(0, 4)), replace=False):
+            s[p] = 'ACGT'[('ACGT'.index(s[p]) + 1 + int(rng.integers(0, 3))) % 4]
+        seq = ''.join(s)
+        if rng.integers(0, 4) == 0:
+            seq = _revcomp(seq)
+        qc = 'I' if rng.integers(0, 3) else 'G'
+        seqs.append(seq)
+        quals.append(qc * m)
+    return [ref, POL], seqs, quals
+
+
+def test_fast_path_low_complexity_equals_oracle():
+    """Local mode over low-complexity reference: every fast-path decision must
+    agree with the full DP (og_mapper.c dp_extend), including the one-gap
+    paths between two diagonals that are both off the seeded one."""
+    refs, seqs, quals = _low_complexity_cases()
+    mode = oracle.LOCAL
+    ix = oracle.Index(refs, oracle.seed_len(mode))
+    ref = np.frombuffer(bytes(oracle.map_reads(ix, oracle.params(mode), seqs, quals, False)),
+                        dtype=_native.ALN_DTYPE)[:len(seqs)]
+    ctx = _native.Context(0)
+    try:
+        got, st = _gpu(ctx, refs, mode, seqs, quals)
+    finally:
+        ctx.close()
+    assert 0 < st[3] < st[1], st
+    def same(a, b):
+        n = int(b['n_cigar'])
+        return (all(a[f] == b[f] for f in _native.ALN_FIELDS)
+                and np.array_equal(a['cigar'][:n], b['cigar'][:n]))
+    bad = [i for i in range(len(ref)) if not same(got[i], ref[i])]
+    assert not bad, [(i, _native.cigar_text(got[i]), int(got[i]['score']), _native.cigar_text(ref[i]),
+                      int(ref[i]['score'])) for i in bad[:5]]
+
+
+def _periodic_pieces(rng, n):
+    """A reference stretch of periodic pieces (period 1 to 4, random units
+    and lengths): diagonals a period apart match the read along a whole
+    piece."""
+    out = []
+    while len(out) < n:
+        per = int(rng.integers(1, 5))
+        unit = rng.integers(0, 4, per)
+        out.extend(np.resize(unit, int(rng.integers(8, 90))).tolist())
+    return np.array(out[:n], dtype=np.int64)
+
+
+def _two_diagonal_cases(n_cases, seed):
+    """Reads that sit exactly on one diagonal up to a row c and on another
+    after it (one gap, 1 to 12 lanes apart), over periodic reference pieces,
+    with up to one substitution: a centre between or beside the two (probed
+    at every offset of the band) sees only two or three non-matches on its
+    own diagonal while the best path is the two-diagonal one -- the shape
+    ADVICE r05 found the ungapped fast path's bound missing."""
+    rng = np.random.default_rng(seed)
+    refs, reads, quals, items = [], [], [], []
+    for t in range(n_cases):
+        m = int(rng.choice([251, 150, 300]))
+        g = _periodic_pieces(rng, m + 80)
+        p = 40
+        s1, s2 = 0, 0
+        while s1 == s2:
+            s1, s2 = (int(x) for x in rng.integers(-6, 7, 2))
+        c = int(rng.integers(20, m - 20))
+        rows = np.arange(m)
+        r = np.where(rows <= c, g[p + rows + s1], g[p + rows + s2])
+        if rng.integers(0, 2):
+            x = int(rng.integers(0, m))
+            r[x] = (r[x] + 1 + int(rng.integers(0, 3))) % 4
+        refs.append(''.join('ACGT'[v] for v in g))
+        reads.append(''.join('ACGT'[v] for v in r))
+        quals.append(('I' if rng.integers(0, 3) else '5') * m)
+        for d in range(-8, 9):
+            items.append((t, 0, t, p + d))
+    return refs, reads, quals, np.array(items, dtype=np.int32)
+
+
+@pytest.mark.parametrize('seed', [5, 6])
+def test_fast_path_cell_equals_full_dp_two_diagonals(seed):
+    """mh_probe_extend: for every probed extension the fast path accepts,
+    the full banded DP on the same staged tables must find the same best
+    cell (score, row, band lane).  The probe runs both k_dp paths."""
+    refs, reads, quals, items = _two_diagonal_cases(4000, seed)
+    ctx = _native.Context(0)
+    try:
+        ctx.index_build(['t%d' % i for i in range(len(refs))], refs, oracle.seed_len(oracle.LOCAL))
+        ctx.reads_load(reads, quals, False)
+        out = ctx.probe_extend(_native.params(oracle.LOCAL), items)
+    finally:
+        ctx.close()
+    fast = out[:, 0] == 1
+    assert fast.sum() > 0.05 * len(out), fast.sum()
+    bad = np.flatnonzero(fast & np.any(out[:, 1:4] != out[:, 5:8], axis=1))
+    assert len(bad) == 0, [(int(i), items[i].tolist(), out[i].tolist()) for i in bad[:5]]

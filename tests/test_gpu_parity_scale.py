@@ -1,7 +1,8 @@
 """GPU parity at configuration scale: 100k read pairs (or unpaired reads) of
 each read shape the BASELINE configs use, through the device pipeline, every
 alignment record compared byte for byte with the CPU oracle's (og_map) on
-the same reads, and the consensus compared with the oracle step's
+the same reads, and the consensus -- after the consensus-distance filter
+when there are several -- compared with the oracle step's
 (oracle/cpu_pipeline.timed_step).
 
     pol_2x251        C2 / C3: 2x251 HIV-1 pol pairs
@@ -108,8 +109,11 @@ def test_records_and_consensus_at_scale(ctx, which, read_len, paired):
     res = prep.result
     assert mapped_to == res['prelim_conseqs']
     assert list(mapped_to) == res['remap_names']
-    if len(mapped_to) < 2:
-        # one consensus: no distance filter on either side
-        assert final == cpu_final
+    # the final consensus after the consensus-distance filter (remap.py:228-
+    # 268): the device's Gotoh + Levenshtein batch against the oracle's
+    # og_gotoh_align + og_levenshtein, same kept set, same strings
+    assert sorted(final) == res['passes'][0]['kept']
+    assert final == cpu_final
     if which == 'hiv':
         assert len(mapped_to) >= 3, sorted(mapped_to)
+        assert len(res['passes'][0]['unfiltered']) >= 3    # the filter ran on >= 3 consensuses

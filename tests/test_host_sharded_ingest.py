@@ -127,6 +127,12 @@ def _worker(rank, world, port, d, case, strict):
         # first copy window bytes that are still symbolic
         os.environ['MH_PINFLATE_SPAN_MIN'] = str(1 << 20)
     dist.init_process_group('gloo', rank=rank, world_size=world)
+    if case == 'big_tail_fail' and rank == 0:
+        # any exception while resolving rank 0's tail (not only the
+        # library's NativeError): rank 1 must still get its window
+        def boom(self, window):
+            raise MemoryError('injected')
+        _native.Fastq.member_tail = boom
     try:
         paths, recs = _make_case(d, case) if rank == 0 else (None, None)
         dist.barrier()
@@ -458,3 +464,13 @@ def test_member_scan_near_range_ends(tmp_path):
     single = tmp_path / 'one.gz'
     single.write_bytes(gzip.compress(data, 1))
     assert not any(_native.Fastq.scan_part(str(single), -1, r, 3)[2] for r in range(3))
+
+
+@pytest.mark.timeout(300)
+def test_member_tail_failure_does_not_stall_the_chain(tmp_path):
+    """an exception other than NativeError in rank 0's
+    member_tail used to skip the send, leaving rank 1 in recv forever.  Now
+    the window goes on as zeros marked unresolved, the CRC agreement fails on
+    every rank and every rank falls back to reading the files whole."""
+    res = _run(tmp_path, 2, 'big_tail_fail')
+    assert all(r[0] for r in res) or all(r[3] == MODES['whole'] for r in res), res
