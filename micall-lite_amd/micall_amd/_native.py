@@ -1075,7 +1075,10 @@ class Context:
         rl = np.ascontiguousarray(ref_lens, dtype=np.int32)
         check(lib().mh_pileup(self.h, source, q_cutoff, len(rl), _ptr(rl)), 'mh_pileup')
 
-    def pileup_fetch(self):
+    def pileup_fetch(self, only=None):
+        """The last pileup: every reference's scalars, the counter rows of
+        those that received pairs (of `only`'s among them, when given),
+        the insertion tokens."""
         n = ctypes.c_int()
         cap = ctypes.c_int32()
         ne = ctypes.c_int64()
@@ -1094,6 +1097,8 @@ class Context:
         check(lib().mh_pileup_fetch(self.h, None, None, None, _ptr(rc), _ptr(fu), _ptr(mp)),
               'mh_pileup_fetch')
         sel = np.flatnonzero((fu[:n] >= 0) | (mp[:n] > 0)).astype(np.int32)
+        if only is not None:
+            sel = np.intersect1d(sel, np.asarray(only, dtype=np.int32)).astype(np.int32)
         if len(sel):   # their rows up to their last counted position, one call
             check(lib().mh_pileup_fetch_refs(self.h, len(sel), _ptr(sel), _ptr(dense), _ptr(nflag),
                                              _ptr(dflag)), 'mh_pileup_fetch_refs')

@@ -269,12 +269,14 @@ class RemapPipeline:
             c['unmapped'], c['star'] = (int(x) for x in sh.sum_i64([c['unmapped'], c['star']]))
         return c
 
-    def _pileup(self, ref_lens):
+    def _pileup(self, ref_lens, only=None):
+        """Pileup of the last pass; `only` (reference indices): the counter
+        rows of just these are fetched (the scalars of all)."""
         self.ctx.pileup(0, CONSENSUS_Q_CUTOFF, ref_lens)
         if self.shard is not None:
             unit_base = self.shard.read_base // 2 if self.ctx.reads_count()[1] else self.shard.read_base
             return self.shard.pileup(self.ctx, unit_base)
-        return self.ctx.pileup_fetch()
+        return self.ctx.pileup_fetch(only=only)
 
     # ---- prelim_map ------------------------------------------------------
     def prelim(self):
@@ -316,10 +318,15 @@ class RemapPipeline:
         """build_conseqs on the prelim alignments, then keep the seed-group
         winners (remap.py:531-541)."""
         names = self.prelim_names
-        fetched = self._pileup([len(self.seed_set[n]) for n in names])
+        # only the seed-group winners' consensuses are kept: only their
+        # counter rows are fetched and only theirs built, in refmap order
+        # (the order of the kept ones is the same either way)
+        winners = [r for r, n in enumerate(names) if n in seed_counts]
+        fetched = self._pileup([len(self.seed_set[n]) for n in names], only=winners)
         pile = Pileup(fetched, names)
         rank = self.prelim_stats['first_row']
-        order = pile.refs_with_reads(rank=np.where(rank < 0, np.iinfo(np.int64).max, rank))
+        order = [r for r in pile.refs_with_reads(rank=np.where(rank < 0, np.iinfo(np.int64).max, rank))
+                 if names[r] in seed_counts]
         conseqs = counts_to_conseqs(pile, order, seeds=self.seeds)
         new_conseqs, map_counts = {}, {}
         for rname, conseq in conseqs.items():
