@@ -272,6 +272,35 @@ def test_fast_path_cell_equals_full_dp_two_diagonals(seed):
     finally:
         ctx.close()
     fast = out[:, 0] == 1
-    assert fast.sum() > 0.05 * len(out), fast.sum()
+    assert fast.sum() > 100, fast.sum()   # (B) declines most: periodic pieces
     bad = np.flatnonzero(fast & np.any(out[:, 1:4] != out[:, 5:8], axis=1))
     assert len(bad) == 0, [(int(i), items[i].tolist(), out[i].tolist()) for i in bad[:5]]
+
+
+def test_fast_path_round5_counterexamples():
+    """Extensions on which round 5's fast path (restated in
+    profiles/diag/fastpath_search.py) accepted the seeded diagonal's cell
+    while the full banded DP finds a better one on a path between two other
+    diagonals (tests/golden/fastpath_two_diagonal.json, found by that
+    search).  Through mh_probe_extend: the full DP must find the fixture's
+    cell, and the fast path must decline or agree with it."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(__file__), 'golden', 'fastpath_two_diagonal.json')
+    with open(path) as f:
+        cases = json.load(f)['cases']
+    assert len(cases) >= 10
+    ctx = _native.Context(0)
+    try:
+        ctx.index_build(['t%d' % i for i in range(len(cases))], [c['ref'] for c in cases],
+                        oracle.seed_len(oracle.LOCAL))
+        ctx.reads_load([c['read'] for c in cases], [c['qual'] for c in cases], False)
+        items = np.array([(t, 0, t, c['centre']) for t, c in enumerate(cases)], dtype=np.int32)
+        out = ctx.probe_extend(_native.params(oracle.LOCAL), items)
+    finally:
+        ctx.close()
+    for t, c in enumerate(cases):
+        full = c['full']
+        # the full DP's cell: score, row, band lane (lane 16 = the centre)
+        assert out[t, 5:8].tolist() == [full[0], full[1], full[2] - 15 + 16], (t, out[t].tolist(), full)
+        assert out[t, 0] == 0 or out[t, 1:4].tolist() == out[t, 5:8].tolist(), (t, out[t].tolist())
