@@ -261,11 +261,12 @@ def top_tokens(length, rows, dense, nflag, dflag, seed, tok):
     return bool(pos.value)
 
 
-def conseqs_build(rows_of, lengths, seeds, dense, nflag, dflag, ev_row, ev_pos, ev_tok, ev_cnt):
+def conseqs_build(rows_of, lengths, seeds, dense, nflag, dflag, ev_row, ev_pos, ev_off, ev_len, ev_cnt,
+                  pool):
     """mh_conseqs_build: [(consensus bytes, present)] per selected row.
     dense (n, cap, 4) int32, flags (n, cap) uint8, all C-contiguous; seeds
-    bytes per selected row; events as parallel sequences (row, pos, token
-    str, merged pairs)."""
+    bytes per selected row; events as arrays (row, pos, token offset and
+    length in `pool`, merged pairs)."""
     n = len(rows_of)
     cap = dense.shape[1] if dense.ndim == 3 else 0
     rows_of = np.ascontiguousarray(rows_of, dtype=np.int32)
@@ -273,21 +274,19 @@ def conseqs_build(rows_of, lengths, seeds, dense, nflag, dflag, ev_row, ev_pos, 
     seed_bufs = [ctypes.create_string_buffer(sd, len(sd) + 1) for sd in seeds]
     seed_ptrs = (ctypes.c_char_p * max(n, 1))(*[ctypes.cast(b, ctypes.c_char_p) for b in seed_bufs])
     seed_lens = np.ascontiguousarray([len(sd) for sd in seeds], dtype=np.int32)
-    pool = ''.join(ev_tok).encode('latin-1')
-    ev_len = np.ascontiguousarray([len(t) for t in ev_tok], dtype=np.int32)
-    ev_off = np.zeros(max(len(ev_tok), 1), dtype=np.int64)
-    if len(ev_tok):
-        ev_off[1:len(ev_tok)] = np.cumsum(ev_len)[:-1]
+    n_ev = len(ev_row)
     ev_row = np.ascontiguousarray(ev_row, dtype=np.int32)
     ev_pos = np.ascontiguousarray(ev_pos, dtype=np.int32)
+    ev_off = np.ascontiguousarray(ev_off, dtype=np.int64)
+    ev_len = np.ascontiguousarray(ev_len, dtype=np.int32)
     ev_cnt = np.ascontiguousarray(ev_cnt, dtype=np.int64)
     out_cap = int(lengths.sum()) + int(ev_len.sum()) + 1
     out = np.zeros(out_cap, dtype=np.uint8)
     off = np.zeros(n + 1, dtype=np.int64)
     present = np.zeros(max(n, 1), dtype=np.int32)
     check(lib().mh_conseqs_build(n, _ptr(rows_of), _ptr(lengths), seed_ptrs, _ptr(seed_lens), cap,
-                                 _ptr(dense), _ptr(nflag), _ptr(dflag), len(ev_tok), _ptr(ev_row),
-                                 _ptr(ev_pos), _ptr(ev_off), _ptr(ev_len), _ptr(ev_cnt), pool,
+                                 _ptr(dense), _ptr(nflag), _ptr(dflag), n_ev, _ptr(ev_row),
+                                 _ptr(ev_pos), _ptr(ev_off), _ptr(ev_len), _ptr(ev_cnt), bytes(pool) or b'\0',
                                  _ptr(out), out_cap, _ptr(off), _ptr(present)), 'mh_conseqs_build')
     raw = out.tobytes()
     return [(raw[off[k]:off[k + 1]], bool(present[k])) for k in range(n)]
@@ -1075,10 +1074,11 @@ class Context:
         rl = np.ascontiguousarray(ref_lens, dtype=np.int32)
         check(lib().mh_pileup(self.h, source, q_cutoff, len(rl), _ptr(rl)), 'mh_pileup')
 
-    def pileup_fetch(self, only=None):
+    def pileup_fetch(self, only=None, events=True):
         """The last pileup: every reference's scalars, the counter rows of
         those that received pairs (of `only`'s among them, when given),
-        the insertion tokens."""
+        the insertion tokens as arrays (`ev_raw`) and, with events=True, as
+        (ref, pos, token, merged pairs) tuples too."""
         n = ctypes.c_int()
         cap = ctypes.c_int32()
         ne = ctypes.c_int64()
@@ -1110,14 +1110,19 @@ class Context:
         pool = ctypes.create_string_buffer(max(nb, 1))
         check(lib().mh_pileup_events(self.h, _ptr(eref), _ptr(epos), _ptr(eoff), _ptr(elen),
                                      _ptr(ecnt), pool), 'mh_pileup_events')
-        raw = pool.raw
-        # (ref, pos, token, number of merged pairs with that token); the
-        # arrays as lists first (a numpy scalar per field costs ~100 ns)
-        events = [(r, p, raw[o:o + ln].decode(), k) for r, p, o, ln, k in
-                  zip(eref[:ne].tolist(), epos[:ne].tolist(), eoff[:ne].tolist(), elen[:ne].tolist(),
-                      ecnt[:ne].tolist())]
-        return dict(dense=dense[:n], nflag=nflag[:n], dflag=dflag[:n], read_counts=rc[:n],
-                    first_unit=fu[:n], max_pos=mp[:n], events=events, cap=cap)
+        raw = pool.raw[:max(nb, 0)]
+        out = dict(dense=dense[:n], nflag=nflag[:n], dflag=dflag[:n], read_counts=rc[:n],
+                   first_unit=fu[:n], max_pos=mp[:n], cap=cap,
+                   ev_raw=dict(ref=eref[:ne].astype(np.int64), pos=epos[:ne].astype(np.int64),
+                               off=eoff[:ne].astype(np.int64), len=elen[:ne].astype(np.int64),
+                               count=ecnt[:ne], pool=raw))
+        if events:
+            # (ref, pos, token, number of merged pairs with that token); the
+            # arrays as lists first (a numpy scalar per field costs ~100 ns)
+            out['events'] = [(r, p, raw[o:o + ln].decode(), k) for r, p, o, ln, k in
+                             zip(eref[:ne].tolist(), epos[:ne].tolist(), eoff[:ne].tolist(),
+                                 elen[:ne].tolist(), ecnt[:ne].tolist())]
+        return out
 
     def pileup_scalars(self):
         """read_counts, first_unit, max_pos of the last pileup (n_refs each)."""

@@ -48,17 +48,58 @@ class Pileup:
         self.first_unit = fetched['first_unit']
         self.max_pos = fetched['max_pos']
         self.cap = fetched['cap']
-        # insertion-token events per reference as parallel lists (pos, token,
-        # count); the {ref: {pos: Counter}} view is built only when asked for
-        self._ev = {}
-        for r, pos, tok, count in fetched['events']:
-            g = self._ev.get(r)
-            if g is None:
-                g = self._ev[r] = ([], [], [])
-            g[0].append(pos)
-            g[1].append(tok)
-            g[2].append(count)
+        # insertion-token events as arrays (ref, pos, token offset / length in
+        # a byte pool, merged pairs): the library's fetch hands them over this
+        # way (ev_raw); a pileup built elsewhere gives (ref, pos, token,
+        # count) tuples, packed here.  The per-reference lists and the
+        # {ref: {pos: Counter}} view are built only when asked for.
+        raw = fetched.get('ev_raw')
+        if raw is None:
+            evs = fetched.get('events') or []
+            toks = [t for _r, _p, t, _n in evs]
+            lens = np.array([len(t) for t in toks], dtype=np.int64)
+            offs = np.zeros(len(toks), dtype=np.int64)
+            if len(toks) > 1:
+                offs[1:] = np.cumsum(lens)[:-1]
+            raw = dict(ref=np.array([e[0] for e in evs], dtype=np.int64),
+                       pos=np.array([e[1] for e in evs], dtype=np.int64), off=offs, len=lens,
+                       count=np.array([e[3] for e in evs], dtype=np.int64),
+                       pool=''.join(toks).encode('latin-1'))
+        self._raw = raw
+        self._ev_refs = set(np.unique(raw['ref']).tolist()) if len(raw['ref']) else set()
+        self._ev_lists = None
         self._events = None
+
+    def has_events(self, r):
+        return r in self._ev_refs
+
+    @property
+    def _ev(self):
+        """{ref: ([pos], [token], [count])} (the Python paths' view)."""
+        if self._ev_lists is None:
+            raw = self._raw
+            pool = raw['pool']
+            d = {}
+            for r, pos, o, ln, k in zip(raw['ref'].tolist(), raw['pos'].tolist(), raw['off'].tolist(),
+                                        raw['len'].tolist(), raw['count'].tolist()):
+                g = d.get(r)
+                if g is None:
+                    g = d[r] = ([], [], [])
+                g[0].append(pos)
+                g[1].append(pool[o:o + ln].decode('latin-1'))
+                g[2].append(k)
+            self._ev_lists = d
+        return self._ev_lists
+
+    def ev_arrays(self, refs):
+        """The events of references `refs` as arrays (ref, pos, offset,
+        length, count) and the byte pool they index."""
+        raw = self._raw
+        if not len(raw['ref']):
+            e = np.zeros(0, dtype=np.int64)
+            return e, e, e, e, e, raw['pool']
+        sel = np.isin(raw['ref'], np.asarray(list(refs), dtype=np.int64))
+        return raw['ref'][sel], raw['pos'][sel], raw['off'][sel], raw['len'][sel], raw['count'][sel], raw['pool']
 
     @property
     def events(self):
@@ -150,7 +191,7 @@ class Pileup:
         return d, nf, df
 
     def has_positive(self, r):
-        if r in self._ev:
+        if self.has_events(r):
             return True
         rd, rnf, rdf = self._rows(r)
         return _native.top_tokens(0, len(rd), rd, rnf, rdf, b'', np.zeros(1, dtype=np.uint8))
@@ -171,7 +212,7 @@ class Pileup:
         self.last_positive = _native.top_tokens(length, min(length, self.cap), rd, rnf, rdf, sb, tok)
         tok = tok[:length]
         longer = {}
-        if r in self._ev:
+        if self.has_events(r):
             d, nf, df = self._slice(r, length)
             # a few events: one Counter per position; many: vectorised (its
             # fixed cost, ~0.1 ms of numpy calls, pays from ~150 events)
@@ -296,9 +337,10 @@ class Pileup:
         """sum(counts[pos].values()) for pos 1..length (remap.py:236-238)."""
         d, nf, df = self._slice(r, length)
         s = d[:, 0] + d[:, 1] + d[:, 2] + d[:, 3] - nf.astype(np.int64) - 2 * df.astype(np.int64)
-        for pos, c in self.events.get(r, {}).items():
-            if pos <= length:
-                s[pos - 1] += sum(c.values())
+        if self.has_events(r):
+            _r, pos, _o, _l, cnt, _p = self.ev_arrays([r])
+            keep = (pos >= 1) & (pos <= length)
+            np.add.at(s, pos[keep] - 1, cnt[keep])
         return s
 
 
@@ -365,16 +407,7 @@ def counts_to_conseqs(pile, order, seeds=None):
         seed = seeds.get(pile.refnames[r]) if seeds else None
         lengths.append(max(int(pile.max_pos[r]), len(seed) if seed else 0))
         seed_bytes.append(seed.encode('latin-1') if seed else b'')
-    ev_row, ev_pos, ev_tok, ev_cnt = [], [], [], []
-    for r in order:
-        g = pile._ev.get(r)
-        if g:
-            ev_row.extend([r] * len(g[0]))
-            ev_pos.extend(g[0])
-            ev_tok.extend(g[1])
-            ev_cnt.extend(g[2])
-    built = _native.conseqs_build(order, lengths, seed_bytes, dense, nflag, dflag, ev_row, ev_pos, ev_tok,
-                                  ev_cnt)
+    built = _native.conseqs_build(order, lengths, seed_bytes, dense, nflag, dflag, *pile.ev_arrays(order))
     return {pile.refnames[r]: text.decode('latin-1') for r, (text, present) in zip(order, built) if present}
 
 
@@ -386,7 +419,7 @@ def counts_to_conseqs_py(pile, order, seeds=None):
         name = pile.refnames[r]
         seed = seeds.get(name) if seeds else None
         tok, longer = pile.tokens(r, seed)
-        if not (pile.last_positive or r in pile._ev):
+        if not (pile.last_positive or pile.has_events(r)):
             continue
         conseqs[name] = _assemble(tok, longer)
     return conseqs

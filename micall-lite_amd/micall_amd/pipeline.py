@@ -183,10 +183,11 @@ class Shard:
             torch.cuda.synchronize(dev)
             ctx.pileup_events_import(sizes[:, 0], sizes[:, 1], ev_all.data_ptr(), 4 * n_max,
                                      pool_all.data_ptr(), b_max)
-            return ctx.pileup_fetch()
+            return ctx.pileup_fetch(events=False)
         # CPU collective (tests): the same exchange over host copies
         fetched = reduce_fetched_host(self, ctx.pileup_fetch(), unit_base)
         fetched['events'] = self._gather_events(fetched['events'])
+        fetched.pop('ev_raw', None)   # this rank's events only: Pileup packs the gathered ones
         return fetched
 
     def _gather_events(self, events):
@@ -276,7 +277,7 @@ class RemapPipeline:
         if self.shard is not None:
             unit_base = self.shard.read_base // 2 if self.ctx.reads_count()[1] else self.shard.read_base
             return self.shard.pileup(self.ctx, unit_base)
-        return self.ctx.pileup_fetch(only=only)
+        return self.ctx.pileup_fetch(only=only, events=False)
 
     # ---- prelim_map ------------------------------------------------------
     def prelim(self):
