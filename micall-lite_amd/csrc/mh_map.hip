@@ -800,6 +800,52 @@ __device__ __forceinline__ void dp_row_gap(uint32_t tbv, int rc, int &Hp, int &E
     Ep = E;
 }
 
+// dp_row_gap with the traceback bits software-pipelined: the row's four
+// sign differences are left in pd and pushed into acc during the next row's
+// deletion scan (between its dependent DPP steps, where the wave would
+// otherwise wait out the DPP hazards); the caller pushes the last row's.
+// The bits land in acc in the same order as dp_row_gap's.
+template <int LOCAL, bool HAVE>
+__device__ __forceinline__ void dp_row_gap_pipe(uint32_t tbv, int rc, int &Hp, int &Ep,
+                                                uint32_t &bestKey, int ci, const DpConst &K,
+                                                uint32_t &acc, int (&pd)[4])
+{
+    const int nib = (int)__builtin_amdgcn_ubfe(tbv, (uint32_t)rc, 4);
+    const int Hd = LOCAL ? Hp + nib - 8 : Hp + nib;
+    const int hc = Hp + K.dIE;
+    const int q = imax(Ep, hc);
+    const int E = dppz<DPP_WAVE_SHL1>(q) + K.mexI;
+    const int de = hc - Ep;
+    int H1 = imax(Hd, E);
+    if (LOCAL) H1 = imax(H1, K.floor);
+    int x = H1;
+    x = imax(x, dppz<DPP_ROW_SHR1>(x));
+    if (HAVE) acc = push_sign(acc, pd[0]);
+    x = imax(x, dppz<DPP_ROW_SHR2>(x));
+    if (HAVE) acc = push_sign(acc, pd[1]);
+    x = imax(x, dppz<DPP_ROW_SHR4>(x));
+    if (HAVE) acc = push_sign(acc, pd[2]);
+    x = imax(x, dppz<DPP_ROW_SHR8>(x));
+    if (HAVE) acc = push_sign(acc, pd[3]);
+    asm volatile("s_nop 1\n\t"
+                 "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+                 "s_nop 1"
+                 : "+v"(x));
+    const int P = x;
+    const int F = dppz<DPP_WAVE_SHR1>(P) + K.cF;
+    const int H = imax(H1, F);
+    pd[0] = de;
+    pd[1] = H1 - P;
+    pd[2] = Hd - H;
+    pd[3] = E - H;
+    if (LOCAL) {
+        const uint32_t key = ((uint32_t)H << 10) | (uint32_t)ci;   // ci < 1024
+        bestKey = bestKey > key ? bestKey : key;
+    }
+    Hp = H;
+    Ep = E;
+}
+
 // A row outside the gap window (first / last GBAR rows): no E, no F.  Its
 // nibble is 0: a local cell at H == 0 is a stop the traceback sees from H.
 template <int LOCAL>
@@ -1512,9 +1558,15 @@ __device__ void dp_pair(const DpArgs &A, const XView &X0, const XView &X1, int m
         }
         uint32_t acc = 0;
         if (i0 >= GBAR && i0 + 8 <= mlo - GBAR) {
+            int pd[4];
+            dp_row_gap_pipe<LOCAL, false>(tbv[0], rcv[0], Hp, Ep, bestKey, 1023 - i0, K, acc, pd);
 #pragma unroll
-            for (int t = 0; t < 8; ++t)
-                dp_row_gap<LOCAL>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K, acc);
+            for (int t = 1; t < 8; ++t)
+                dp_row_gap_pipe<LOCAL, true>(tbv[t], rcv[t], Hp, Ep, bestKey, 1023 - (i0 + t), K, acc, pd);
+            acc = push_sign(acc, pd[0]);
+            acc = push_sign(acc, pd[1]);
+            acc = push_sign(acc, pd[2]);
+            acc = push_sign(acc, pd[3]);
         } else if (m0 == m1) {
             // both halves end on the same row: a row's gap window is the same
             // on every lane (wave-uniform branches), rows past the read are
