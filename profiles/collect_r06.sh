@@ -13,7 +13,7 @@
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
 WHAT=${1:?config}
-O=$R/gpurun_out/r06/$WHAT
+O=$R/gpurun_out/r06/${OUTNAME:-$WHAT}
 mkdir -p $O
 cd $R
 first() { ls $1/*$2 $1/*/*$2 2>/dev/null | head -1; }
