@@ -260,7 +260,13 @@ __device__ __forceinline__ T poll_block(const T *p, int lane, bool has, Tag tagg
 // column of seq2 (mat[c][b[j - 1]] at c * PW + PROF_PAD + j; zero outside
 // 1..n), so a lane at column j reads its score at a fixed per-lane base + t.
 constexpr int PROF_PAD = 128;                       // >= 64 columns before 1 and 96 after n
-constexpr size_t GPROF_LDS_MAX = 64 * 1024;         // profiles up to this stay in LDS
+// Profiles up to this stay in LDS.  A larger one costs residency (one
+// 64-lane strip per workgroup: a 48 KiB profile leaves 3 strips per CU), and
+// the profile streamed from global memory one block ahead is then faster:
+// C4-all's pairs without SARS-CoV-2 (HCV seeds, 48 KiB profiles) 25 -> 12 ms
+// of k_gotoh_fwd, HIV-only pairs (<= 15 KiB) equal either way
+// (profiles/r06/diag/profile_lds.txt).
+constexpr size_t GPROF_LDS_MAX = 16 * 1024;
 __host__ __device__ inline int prof_width(int n) { return (int)gotoh_al16((size_t)n + 2 * PROF_PAD); }
 
 // unrolled calls f(integral_constant<int, Q>) for Q = 0 .. N - 1
@@ -699,24 +705,59 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh_tb(const GotohArgs *bat
             wc2[x] = j0 - 1 - x >= 0 ? A.s2[j0 - 1 - x] : 0;
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (threadIdx.x < 64) {
+            // Wave 0 walks by runs: a cell's move is up (GA), else left (GB),
+            // else diagonal (GC), and a run of one move is found in one LDS
+            // round trip: lane l reads the l-th cell of the run that each of
+            // the three moves would make from the current cell (its l = 0 cell
+            // is the current one for all three) and both characters; the
+            // current cell's move picks the run, and a ballot its length (the
+            // first lane whose cell moves otherwise, or the window's, the
+            // grid's or the wave's end).  The lanes write the run's output
+            // characters together.
+            const int lane = threadIdx.x;
             int i = i0, j = j0, len = tb_len, status = 0;
             while (i > 0 && j > 0) {
                 const int t = s0 - (i + j), r = i0 - i, c = j0 - j;
                 if (t >= TBD || r >= TBR || c >= TBD) break;
-                // the cell's bits and both characters in one LDS round trip
-                const uint8_t x = win[t * TBR + r];
-                int ch1 = wc1[r], ch2 = wc2[c];
-                asm volatile("" : "+v"(ch1), "+v"(ch2));   // loaded here, not after the test
+                // cells available to each run from here (the current one included)
+                const int nd = min(min((TBD - 1 - t) / 2, TBR - 1 - r), min(TBD - 1 - c, min(i, j) - 1)) + 1;
+                const int nu = min(min(TBD - 1 - t, TBR - 1 - r), i - 1) + 1;
+                const int nl = min(min(TBD - 1 - t, TBD - 1 - c), j - 1) + 1;
+                const uint8_t xd = lane < nd ? win[(t + 2 * lane) * TBR + r + lane] : 0;
+                const uint8_t xu = lane < nu ? win[(t + lane) * TBR + r + lane] : 0;
+                const uint8_t xl = lane < nl ? win[(t + lane) * TBR + r] : 0;
+                const int ch1 = r + lane < TBR ? wc1[r + lane] : 0;
+                const int ch2 = c + lane < TBD ? wc2[c + lane] : 0;
+                const int x = __builtin_amdgcn_readfirstlane((int)xd);
                 if (!(x & (GA | GB | GC))) { status = -1; break; }
                 const bool up = x & GA, left = !up && (x & GB);
-                r1[len] = left ? '-' : (char)ch1;
-                r2[len] = up ? '-' : (char)ch2;
-                i -= left ? 0 : 1;
-                j -= up ? 0 : 1;
-                ++len;
+                int run;
+                if (up) {
+                    const uint64_t stop = __builtin_amdgcn_ballot_w64(lane >= min(nu, 64) || !(xu & GA));
+                    run = (int)__builtin_ctzll(stop | (1ull << 63));
+                    run = run < 1 ? 1 : run;
+                    if (lane < run) { r1[len + lane] = (char)ch1; r2[len + lane] = '-'; }
+                    i -= run;
+                } else if (left) {
+                    const uint64_t stop =
+                        __builtin_amdgcn_ballot_w64(lane >= min(nl, 64) || (xl & GA) || !(xl & GB));
+                    run = (int)__builtin_ctzll(stop | (1ull << 63));
+                    run = run < 1 ? 1 : run;
+                    if (lane < run) { r1[len + lane] = '-'; r2[len + lane] = (char)ch2; }
+                    j -= run;
+                } else {
+                    const uint64_t stop =
+                        __builtin_amdgcn_ballot_w64(lane >= min(nd, 64) || (xd & (GA | GB)) || !(xd & GC));
+                    run = (int)__builtin_ctzll(stop | (1ull << 63));
+                    run = run < 1 ? 1 : run;
+                    if (lane < run) { r1[len + lane] = (char)ch1; r2[len + lane] = (char)ch2; }
+                    i -= run;
+                    j -= run;
+                }
+                len += run;
             }
-            tb_ii = i; tb_jj = j; tb_len = len; tb_status = status;
+            if (lane == 0) { tb_ii = i; tb_jj = j; tb_len = len; tb_status = status; }
         }
         __syncthreads();
     }
@@ -1286,7 +1327,10 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
     int nmax = 0;
     for (int t = 0; t < count; ++t) nmax = std::max(nmax, ns[t]);
     const size_t prof_bytes = (size_t)L * prof_width(nmax);
-    if (prof_bytes <= GPROF_LDS_MAX) {
+    // MH_GOTOH_PROF_LDS_MAX (diagnostics): another limit for the LDS profile
+    size_t lds_max = GPROF_LDS_MAX;
+    if (const char *e = getenv("MH_GOTOH_PROF_LDS_MAX"); e && *e) lds_max = (size_t)strtoull(e, nullptr, 10);
+    if (prof_bytes <= lds_max) {
         const size_t lds_fwd = sizeof(int2) * GBLK + prof_bytes;
         MH_HIP(hipFuncSetAttribute((const void *)k_gotoh_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_fwd));
