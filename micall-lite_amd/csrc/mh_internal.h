@@ -103,15 +103,22 @@ struct Slot {
 
 // In HBM a slot is split in two arrays: the 16-B key that pairing, mate
 // rescue and the best-candidate choice compare (a read's MAXCAND keys are
-// one 64-B line), and the 32-B statistics only the chosen candidate's
-// record copies.
+// one 64-B line), and the 16-B statistics only the chosen candidate's
+// record copies.  Memory requests are 128-B lines
+// (profiles/r06/diag/fetch_calib.json), so the statistics are packed to put
+// a pair's two reads (2 x MAXCAND x 16 B) in one line: k_pair reads one line
+// of them per pair, not two.  NM = XM + XG is not stored.
 struct alignas(16) SlotKey {
     int32_t rs;      // ref << 1 | strand; -1 when the extension found no alignment
     int32_t pos, end, score;
 };
 struct alignas(16) SlotInfo {
-    int32_t xm, xo, xg, nm, n_cigar, cig_off, maxm, pad;
+    int32_t cig_off;
+    uint32_t xm_xo;   // xm | xo << 16 (both below 2^16: reads <= MAXLEN, ops <= MH_MAXOPS)
+    uint32_t xg_nc;   // xg | n_cigar << 16
+    int32_t maxm;
 };
+static_assert(sizeof(SlotInfo) == 16, "a read's MAXCAND statistics fill half a 128-B line");
 
 // Final per-read SAM record (mh_aln without the inline CIGAR).
 struct Rec {

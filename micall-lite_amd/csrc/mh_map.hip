@@ -1932,7 +1932,8 @@ __device__ void post_ext(const DpArgs &A, const XItem &it, const XView &X, int b
     }
     if (lane == 0) {
         A.skey[it.sid] = SlotKey{out.valid ? (out.ref << 1 | out.strand) : -1, out.pos, out.end, out.score};
-        A.sinfo[it.sid] = SlotInfo{out.xm, out.xo, out.xg, out.nm, out.n_cigar, out.cig_off, out.maxm, 0};
+        A.sinfo[it.sid] = SlotInfo{out.cig_off, (uint32_t)out.xm | (uint32_t)out.xo << 16,
+                                   (uint32_t)out.xg | (uint32_t)out.n_cigar << 16, out.maxm};
     }
     wave_sync();
 }
@@ -2436,8 +2437,9 @@ __device__ __forceinline__ void fill_aligned(const PairArgs &A, Rec &o, const Ma
     o.secbest = has ? sec : I32MIN;
     o.mapq = mapq_v2(A.local, A.local ? 2 * m : 0, A.len_tab[(MAXLEN + 1) + m], a.score, has, sec);
     const SlotInfo f = A.sinfo[mv.base + chosen];
-    o.xm = f.xm; o.xo = f.xo; o.xg = f.xg; o.nm = f.nm;
-    o.n_cigar = f.n_cigar;
+    o.xm = (int)(f.xm_xo & 0xffffu); o.xo = (int)(f.xm_xo >> 16);
+    o.xg = (int)(f.xg_nc & 0xffffu); o.nm = o.xm + o.xg;
+    o.n_cigar = (int)(f.xg_nc >> 16);
     o.cig_off = f.cig_off;
     o.maxm = f.maxm;
     o.sam_ref = o.ref;
