@@ -376,14 +376,17 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
         ent.reserve(n);
         for (auto &v : per) { ent.insert(ent.end(), v.begin(), v.end()); std::vector<E>().swap(v); }
     }
-    // (key, ref, pos) order: the entries come in (ref, pos) order, so a stable
-    // sort by key alone gives it with a cheaper comparison
-    auto less = [](const E &a, const E &b) { return a.key < b.key; };
-    {   // stable-sorted in parallel chunks, then merged pairwise (stable)
+    // (key, ref, pos) order, a total order (no two entries share ref and
+    // pos), so an unstable sort gives it (std::stable_sort's buffer cost
+    // ~0.1 ms per consensus index of a few thousand entries)
+    auto less = [](const E &a, const E &b) {
+        return a.key != b.key ? a.key < b.key : a.ref != b.ref ? a.ref < b.ref : a.pos < b.pos;
+    };
+    {   // sorted in parallel chunks, then merged pairwise
         const int ns = ent.size() < 65536 ? 1 : s2a_threads();
         std::vector<size_t> b((size_t)ns + 1);
         for (int t = 0; t <= ns; ++t) b[(size_t)t] = ent.size() * (size_t)t / (size_t)ns;
-        par_for(ns, [&](int t) { std::stable_sort(ent.begin() + b[(size_t)t], ent.begin() + b[(size_t)t + 1], less); });
+        par_for(ns, [&](int t) { std::sort(ent.begin() + b[(size_t)t], ent.begin() + b[(size_t)t + 1], less); });
         for (int w = 1; w < ns; w *= 2) {
             std::vector<std::pair<int, int>> jobs;
             for (int t = 0; t + w < ns; t += 2 * w) jobs.push_back({t, std::min(t + 2 * w, ns)});
@@ -398,17 +401,15 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     for (size_t i = 0; i < ent.size(); ++i) if (i == 0 || ent[i].key != ent[i - 1].key) ++nkeys;
     uint64_t cap = 1024;
     while (cap < 2 * nkeys) cap <<= 1;
-    std::vector<uint64_t> hkey(cap, HEMPTY);
-    std::vector<uint32_t> hstart(cap, 0), hcount(cap, 0);
+    // one 16-B entry per slot: key (two words, EMPTY = ~0), start, count
+    std::vector<uint4> hent(cap, make_uint4(~0u, ~0u, 0u, 0u));
     std::vector<int2> hits(ent.size() ? ent.size() : 1);
     for (size_t i = 0; i < ent.size();) {
         size_t j = i + 1;
         while (j < ent.size() && ent[j].key == ent[i].key) ++j;
         uint64_t h = hash_key(ent[i].key) & (cap - 1);
-        while (hkey[h] != HEMPTY) h = (h + 1) & (cap - 1);
-        hkey[h] = ent[i].key;
-        hstart[h] = (uint32_t)i;
-        hcount[h] = (uint32_t)(j - i);
+        while (((uint64_t)hent[h].x | ((uint64_t)hent[h].y << 32)) != HEMPTY) h = (h + 1) & (cap - 1);
+        hent[h] = make_uint4((uint32_t)ent[i].key, (uint32_t)(ent[i].key >> 32), (uint32_t)i, (uint32_t)(j - i));
         i = j;
     }
     for (size_t i = 0; i < ent.size(); ++i) hits[i] = make_int2(ent[i].ref, ent[i].pos);
@@ -430,17 +431,17 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
         cplane[2 * (j >> 5)] |= (c & 1u) << (j & 31);
         cplane[2 * (j >> 5) + 1] |= (c >> 1) << (j & 31);
     }
-    // one blob: codes, ref_off, ref_len, hkey, hstart, hcount, hits, code2,
-    // ncode, cplane (256-B aligned parts), staged on the host and uploaded with one copy
+    // one blob: codes, ref_off, ref_len, hent, hits, code2, ncode, cplane
+    // (256-B aligned parts), staged on the host and uploaded with one copy
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t sz[10] = {codes.size(), sizeof(int64_t) * (size_t)n_refs, sizeof(int32_t) * (size_t)n_refs,
-                          sizeof(uint64_t) * cap, sizeof(uint32_t) * cap, sizeof(uint32_t) * cap,
-                          sizeof(int2) * hits.size(), sizeof(uint32_t) * code2.size(),
-                          sizeof(uint32_t) * ncode.size(), sizeof(uint32_t) * cplane.size()};
-    const void *src[10] = {codes.data(), ref_off.data(), ref_len.data(), hkey.data(), hstart.data(),
-                           hcount.data(), hits.data(), code2.data(), ncode.data(), cplane.data()};
-    size_t at[10], total = 0;
-    for (int x = 0; x < 10; ++x) { at[x] = total; total += al(sz[x]); }
+    constexpr int NP = 8;
+    const size_t sz[NP] = {codes.size(), sizeof(int64_t) * (size_t)n_refs, sizeof(int32_t) * (size_t)n_refs,
+                           sizeof(uint4) * cap, sizeof(int2) * hits.size(), sizeof(uint32_t) * code2.size(),
+                           sizeof(uint32_t) * ncode.size(), sizeof(uint32_t) * cplane.size()};
+    const void *src[NP] = {codes.data(), ref_off.data(), ref_len.data(), hent.data(), hits.data(),
+                           code2.data(), ncode.data(), cplane.data()};
+    size_t at[NP], total = 0;
+    for (int x = 0; x < NP; ++x) { at[x] = total; total += al(sz[x]); }
     if ((int64_t)total > ix.cap_blob) {   // (re)allocate only when it does not fit
         hipFree(ix.blob);
         ix.blob = nullptr;
@@ -450,19 +451,17 @@ static int build_index(DevIndex &ix, int n_refs, const char *const *seqs, int se
     }
     mark("planes+alloc");
     std::vector<uint8_t> stage(total);
-    for (int x = 0; x < 10; ++x) if (sz[x]) std::memcpy(stage.data() + at[x], src[x], sz[x]);
+    for (int x = 0; x < NP; ++x) if (sz[x]) std::memcpy(stage.data() + at[x], src[x], sz[x]);
     mark("stage");
     uint8_t *d = (uint8_t *)ix.blob;
     ix.codes = d + at[0];
     ix.ref_off = (int64_t *)(d + at[1]);
     ix.ref_len = (int32_t *)(d + at[2]);
-    ix.hkey = (uint64_t *)(d + at[3]);
-    ix.hstart = (uint32_t *)(d + at[4]);
-    ix.hcount = (uint32_t *)(d + at[5]);
-    ix.hits = (int2 *)(d + at[6]);
-    ix.code2 = (uint32_t *)(d + at[7]);
-    ix.ncode = (uint32_t *)(d + at[8]);
-    ix.cplane = (uint32_t *)(d + at[9]);
+    ix.hent = (uint4 *)(d + at[3]);
+    ix.hits = (int2 *)(d + at[4]);
+    ix.code2 = (uint32_t *)(d + at[5]);
+    ix.ncode = (uint32_t *)(d + at[6]);
+    ix.cplane = (uint32_t *)(d + at[7]);
     // callers synchronise the context stream first (mh_index_build)
     MH_HIP(hipMemcpy(ix.blob, stage.data(), total, hipMemcpyHostToDevice));
     mark("upload");

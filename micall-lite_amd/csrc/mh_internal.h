@@ -66,9 +66,10 @@ struct DevIndex {
     uint32_t *cplane = nullptr;    // bit planes, 32 bases per word: [2k] low code bits, [2k+1] high
     int64_t *ref_off = nullptr;
     int32_t *ref_len = nullptr;
-    uint64_t *hkey = nullptr;      // open addressing, EMPTY = ~0
-    uint32_t *hstart = nullptr;
-    uint32_t *hcount = nullptr;
+    // open addressing: one 16-B entry per slot, (key low, key high, start,
+    // count) with key EMPTY = ~0, so a probe that finds its key has the hits'
+    // range in the same load (one dependent round trip less per seed)
+    uint4 *hent = nullptr;
     uint64_t hmask = 0;
     int2 *hits = nullptr;          // (ref, pos) sorted per key
     uint64_t sig = 0;              // content signature (cache key)

@@ -515,25 +515,27 @@ __device__ int seed_read(const SeedArgs &A, int64_t r, const SeedPre &P, int lan
     int cnt = 0;
     uint32_t start = 0;
     // the first probe of every seed, then the next read's loads, then the
-    // rest of the probe chains
+    // rest of the probe chains (an entry holds its key and its hits' range)
     const bool probe = t < ns && wnm == 0;
-    uint64_t key = 0, h = 0, k = HEMPTY;
+    uint64_t key = 0, h = 0;
+    uint4 e = make_uint4(~0u, ~0u, 0u, 0u);
     if (probe) {
         key = s ? revcomp_key(wkey, SL) : wkey;
         h = hash_key(key) & A.I.hmask;
-        k = A.I.hkey[h];
+        e = A.I.hent[h];
     }
     fetch_next();
     if (probe) {
         for (;;) {
+            const uint64_t k = (uint64_t)e.x | ((uint64_t)e.y << 32);
             if (k == HEMPTY) break;
             if (k == key) {
-                start = A.I.hstart[h];
-                cnt = (int)A.I.hcount[h];
+                start = e.z;
+                cnt = (int)e.w;
                 break;
             }
             h = (h + 1) & A.I.hmask;
-            k = A.I.hkey[h];
+            e = A.I.hent[h];
         }
         if (cnt > MAXHITS_SEED) cnt = 0;
     }
@@ -2826,7 +2828,7 @@ int run_map(Ctx &c, const mh_params &par)
 {
     c.map.stats_host_valid = false;
     c.map.stats_pin_ready = false;
-    if (c.index.n_refs <= 0 || c.index.hkey == nullptr) {
+    if (c.index.n_refs <= 0 || c.index.hent == nullptr) {
         set_error("mh_map: no reference index (call mh_index_build first)");
         return -3;
     }
