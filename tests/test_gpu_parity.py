@@ -433,6 +433,34 @@ def test_gotoh_profile_in_global_memory(ctx, is_global):
         assert g == oracle.gotoh_align(a, b, 15, 3, is_global, alpha, mat)
 
 
+@pytest.mark.parametrize('is_global', [True, False])
+def test_gotoh_traceback_runs(ctx, is_global):
+    """k_gotoh_tb walks by runs of one move (a ballot over the next 64
+    cells of each move): paths with long diagonal runs, insertions and
+    deletions of 1-300 bases (runs longer than the wave and than the
+    128 x 128 window), gaps right at the ends, alternating short gaps, and
+    ties (repeats) -- every aligned pair equal to the oracle's, global and
+    local."""
+    rng = np.random.default_rng(41)
+    mat, alpha = [5, -4, -4, -4, 0, -4, 5, -4, -4, 0, -4, -4, 5, -4, 0, -4, -4, -4, 5, 0,
+                  0, 0, 0, 0, 0], 'ACGT?'
+    rand = lambda k: ''.join(rng.choice(list('ACGT'), size=k))
+    base = POL[:2400]
+    pairs = [
+        (base, base[:700] + base[770:]),                     # a 70-base deletion
+        (base, base[:500] + rand(130) + base[500:]),         # a 130-base insertion
+        (base, base[:900] + base[1200:]),                    # 300 bases: past the window
+        (base, rand(200) + base + rand(150)),                # end gaps, both sides
+        (base[300:] , base),                                 # seq1 starts inside seq2
+        (base, ''.join(base[i:i + 40] + ('' if i % 80 else rand(2)) for i in range(0, 2400, 40))),
+        (('ACGTTGCA' * 150)[:1100], ('ACGTTGCA' * 160)[3:1203]),   # repeats: ties
+        (base[:64], base[:64]), (base[:65], base[1:64]),     # one run of exactly the wave
+    ]
+    got = ctx.gotoh_align_many(pairs, 15, 3, is_global, alpha, mat)
+    for (a, b), g in zip(pairs, got):
+        assert g == oracle.gotoh_align(a, b, 15, 3, is_global, alpha, mat), (len(a), len(b))
+
+
 def _filter_distance_oracle(seq1, seq2, text, alpha, mat):
     from micall_amd.consensus import extract_relevant_seed
     a_seed, a_conseq, _ = oracle.gotoh_align(seq1, seq2, 15, 3, True, alpha, mat)
