@@ -25,7 +25,8 @@
 //                above through its first row; its writes to d(i+1,j) and
 //                f(i,j+1) are never read again (each cell reads its own d/f
 //                before its upper/left neighbour runs) and are dropped
-//   k_gotoh_tb   traceback (:316-438) by one thread over LDS windows.
+//   k_gotoh_tb   traceback (:316-438) over LDS windows, one wave walking
+//                runs of one move (a ballot per run).
 //   k_lev_prep / k_lev  (the consensus-distance filter only, remap.py:249-251)
 //                the relevant seed cut from the traceback's output and its
 //                edit distance to the relevant consensus, bit-parallel, in
@@ -646,7 +647,7 @@ __global__ __launch_bounds__(GOTOH_THREADS) void k_gotoh_tb(const GotohArgs *bat
     // stages a TBD x TBR window of abc (diagonals s0 .. s0-TBD+1, rows
     // ii .. ii-TBR+1 of the current cell (ii, jj), which holds every cell the
     // path can reach before it leaves the window) and the TBR / TBD characters of
-    // each sequence before ii / jj into LDS; thread 0 walks the window and
+    // each sequence before ii / jj into LDS; wave 0 walks the window and
     // writes the output characters; repeat.  The gap runs at both ends are
     // written by the whole block.
     uint8_t *win = gsm;
