@@ -306,6 +306,14 @@ int mh_rows_info(mh_ctx *ctx, int32_t *out4, int32_t *present, char *unknown, si
  * counters (positions 1..ref_lens[r] + MH_PILEUP_SLACK). */
 #define MH_PILEUP_SLACK 2048
 int mh_pileup(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *ref_lens);
+/* mh_pileup counting only the references sel[0 .. n_sel) (n_sel < 0: all):
+ * the units mapped to any other are skipped and its counters, read count
+ * and positions stay empty.  The prelim pass builds only the seed-group
+ * winners' consensuses (remap.py:531-541 keeps those of build_conseqs'
+ * output), so their pileup alone is needed; every reference is counted
+ * independently of the others, so theirs are the same. */
+int mh_pileup_only(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *ref_lens, int n_sel,
+                   const int32_t *sel);
 /* dense: n_refs x cap x 4 int32 counts of A,C,G,T at positions 1..cap;
  * nflag/dflag: n_refs x cap bytes ('N' seen -> count -1, '-' seen -> -2);
  * read_counts: merged pairs per ref; first_unit: first merged unit index

@@ -2553,9 +2553,25 @@ extern "C" int mh_reads_fastq_lines(mh_ctx *ctx, int64_t *lines1)
 
 int mh_pileup(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *ref_lens)
 {
-    if (!ctx || n_refs < 0 || (n_refs > 0 && !ref_lens) || (source != 0 && source != 1)) return -3;
+    return mh_pileup_only(ctx, source, q_cutoff, n_refs, ref_lens, -1, nullptr);
+}
+
+int mh_pileup_only(mh_ctx *ctx, int source, int q_cutoff, int n_refs, const int32_t *ref_lens, int n_sel,
+                   const int32_t *sel)
+{
+    if (!ctx || n_refs < 0 || (n_refs > 0 && !ref_lens) || (source != 0 && source != 1) ||
+        (n_sel > 0 && !sel))
+        return -3;
     CtxEx *c = X(ctx);
     MH_HIP(hipSetDevice(c->device));
+    c->pile.only.clear();
+    if (n_sel >= 0) {
+        c->pile.only.assign((size_t)n_refs, 0);
+        for (int k = 0; k < n_sel; ++k) {
+            if (sel[k] < 0 || sel[k] >= n_refs) { set_error("mh_pileup_only: reference %d out of range", sel[k]); return -3; }
+            c->pile.only[(size_t)sel[k]] = 1;
+        }
+    }
     int32_t cap = 1;
     for (int r = 0; r < n_refs; ++r) cap = std::max(cap, ref_lens[r] + MH_PILEUP_SLACK);
     c->pile.n_refs = n_refs;

@@ -202,9 +202,12 @@ struct PileState {
     size_t land_cap = 0;
     bool land_ok = false;
     std::vector<int32_t> ref_lens;  // host copy (sizes the LDS window)
+    // references this pileup counts (mh_pileup_only; empty: all): the units
+    // of any other are skipped and its counters stay zero
+    std::vector<uint8_t> only;
     int32_t *sel = nullptr;         // references of a multi-GPU exchange
     int sel_cap = 0;
-    int32_t *win_map = nullptr;     // k_pileup: per reference (LDS window word offset or -1, positions)
+    int32_t *win_map = nullptr;     // k_pileup: per reference (LDS window word offset, -1 none, -2 skipped; positions)
     int win_map_cap = 0;
     char *ins_scratch = nullptr;    // per-wave merged-insertion scratch of k_pileup
     int64_t ins_scratch_bytes = 0;

@@ -352,6 +352,8 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
             if (lane == 0) atomicExch(&A.ev_ctr[3], 1ull);
             continue;
         }
+        // a reference this pileup does not count (mh_pileup_only)
+        if (__builtin_amdgcn_readfirstlane(wmap[2 * ref]) == -2) continue;
 
         // ---- apply_cigar: op offsets by a lane-parallel prefix scan, then
         // expand each mate into reference coordinates lane-parallel ----
@@ -926,8 +928,11 @@ static int pile_geometry(Ctx &c, int source, int64_t n_units, PileGeometry &g)
     std::vector<int> order((size_t)NR);
     for (int r = 0; r < NR; ++r) order[(size_t)r] = r;
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return hits[(size_t)x] > hits[(size_t)y]; });
+    // references outside mh_pileup_only's set: skipped (-2), no window
+    const bool some = P.only.size() == (size_t)NR;
+    for (int r = 0; r < NR && some; ++r) if (!P.only[(size_t)r]) hits[(size_t)r] = 0;
     g.win_map.assign(2 * (size_t)NR, 0);
-    for (int r = 0; r < NR; ++r) g.win_map[2 * (size_t)r] = -1;
+    for (int r = 0; r < NR; ++r) g.win_map[2 * (size_t)r] = some && !P.only[(size_t)r] ? -2 : -1;
     int64_t words = 0;
     for (int r : order) {
         if (hits[(size_t)r] <= 0) break;

@@ -101,6 +101,7 @@ def _declare(L):
         'mh_rows_info': ([_P, _P, _P, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
         'mh_reads_fastq_lines': ([_P, _I64P], ctypes.c_int),
         'mh_pileup': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),
+        'mh_pileup_only': ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, _P], ctypes.c_int),
         'mh_pileup_dims': ([_P, ctypes.POINTER(ctypes.c_int), _I32P, _I64P, _I64P], ctypes.c_int),
         'mh_pileup_fetch': ([_P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
         'mh_pileup_fetch_ref': ([_P, ctypes.c_int, _P, _P, _P], ctypes.c_int),
@@ -1070,9 +1071,16 @@ class Context:
         check(lib().mh_reads_fastq_lines(self.h, ctypes.byref(n)), 'mh_reads_fastq_lines')
         return n.value
 
-    def pileup(self, source, q_cutoff, ref_lens):
+    def pileup(self, source, q_cutoff, ref_lens, only=None):
+        """Pile up the last mapping pass (source 0) or the loaded rows (1);
+        `only` (reference indices): count just these (mh_pileup_only)."""
         rl = np.ascontiguousarray(ref_lens, dtype=np.int32)
-        check(lib().mh_pileup(self.h, source, q_cutoff, len(rl), _ptr(rl)), 'mh_pileup')
+        if only is None:
+            check(lib().mh_pileup(self.h, source, q_cutoff, len(rl), _ptr(rl)), 'mh_pileup')
+        else:
+            sel = np.ascontiguousarray(list(only), dtype=np.int32)
+            check(lib().mh_pileup_only(self.h, source, q_cutoff, len(rl), _ptr(rl), len(sel), _ptr(sel)),
+                  'mh_pileup_only')
 
     def pileup_fetch(self, only=None, events=True):
         """The last pileup: every reference's scalars, the counter rows of

@@ -271,9 +271,9 @@ class RemapPipeline:
         return c
 
     def _pileup(self, ref_lens, only=None):
-        """Pileup of the last pass; `only` (reference indices): the counter
-        rows of just these are fetched (the scalars of all)."""
-        self.ctx.pileup(0, CONSENSUS_Q_CUTOFF, ref_lens)
+        """Pileup of the last pass; `only` (reference indices): just these
+        are counted (mh_pileup_only) and their counter rows fetched."""
+        self.ctx.pileup(0, CONSENSUS_Q_CUTOFF, ref_lens, only=only)
         if self.shard is not None:
             unit_base = self.shard.read_base // 2 if self.ctx.reads_count()[1] else self.shard.read_base
             return self.shard.pileup(self.ctx, unit_base)

@@ -1,0 +1,16 @@
+#!/bin/bash
+# mh_pileup_only (the prelim pileup counts the seed-group winners only):
+# pileup / consensus tests, then the C4-all and C4 lines
+set -e -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r06/only
+mkdir -p $O
+cd $R
+timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+    tests/test_gpu_parity.py tests/test_gpu_parity_scale.py tests/test_gpu_e2e.py tests/test_gpu_shard.py \
+    tests/test_gpu_bench_parity.py tests/test_gpu_chain.py > $O/tests.log 2>&1
+echo tests ok
+timeout -k 10 900 python3 bench.py --genomes all --pairs 5000000 --steps 3 --warmup 1 --no-e2e > $O/c4all.json 2> $O/c4all.err
+echo c4all ok
+timeout -k 10 600 python3 bench.py --genomes hiv --pairs 5000000 --steps 3 --warmup 1 --no-e2e > $O/c4.json 2> $O/c4.err
+echo c4 ok

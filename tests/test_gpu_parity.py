@@ -257,6 +257,35 @@ def _gpu_pileup_as_refmap(ctx, refnames, reflens, q_cutoff, source=0):
     return refmap, counts
 
 
+def test_pileup_only_selected_references(ctx):
+    """mh_pileup_only: pairs over three references (pol, env, gag, with
+    insertions), piled up in full and with only pol and gag counted: the
+    counted references' counters, flags, scalars and insertion tokens are
+    the full pileup's, env's stay empty."""
+    env, gag = SEEDS['HIV1B-env-seed'], SEEDS['HIV1B-gag-seed']
+    names, seqs, quals = _reads(1500, 29, genomes={'HIV1B-pol-seed': POL, 'HIV1B-env-seed': env,
+                                                   'HIV1B-gag-seed': gag}, indel_rate=0.01)
+    refs = ['HIV1B-pol-seed', 'HIV1B-env-seed', 'HIV1B-gag-seed']
+    ctx.index_build(refs, [POL, env, gag], 20)
+    ctx.reads_load(seqs, quals, True)
+    ctx.map(_native.params(oracle.LOCAL))
+    lens = [len(POL), len(env), len(gag)]
+    ctx.pileup(0, 20, lens)
+    full = ctx.pileup_fetch()
+    ctx.pileup(0, 20, lens, only=[0, 2])
+    part = ctx.pileup_fetch()
+    assert full['read_counts'][1] > 0
+    for r in (0, 2):
+        for k in ('dense', 'nflag', 'dflag'):
+            assert np.array_equal(part[k][r], full[k][r]), (r, k)
+        for k in ('read_counts', 'first_unit', 'max_pos'):
+            assert part[k][r] == full[k][r], (r, k)
+    assert part['read_counts'][1] == 0 and part['first_unit'][1] < 0 and part['max_pos'][1] == 0
+    assert not part['dense'][1].any() and not part['nflag'][1].any() and not part['dflag'][1].any()
+    assert sorted(e for e in part['events'] if e[0] != 1) == sorted(e for e in full['events'] if e[0] != 1)
+    assert not [e for e in part['events'] if e[0] == 1]
+
+
 @pytest.mark.parametrize('mode,q', [(oracle.LOCAL, 20), (oracle.E2E, 20), (oracle.LOCAL, 0)])
 def test_pileup_vs_oracle(ctx, mode, q):
     names, seqs, quals = _reads(2000, 23, indel_rate=0.01)
