@@ -1048,9 +1048,20 @@ static size_t gotoh_work_bytes(int m, int n)
            align16(sizeof(int) * strips * (n + 1)) + align16(strips * (n + 1)) + 16;
 }
 
-// Retained scratch above this is released after the call (one very long
-// alignment must not pin device memory for the rest of the session).
-constexpr size_t GOTOH_KEEP_BYTES = (size_t)1 << 30;
+// Retained scratch above an eighth of the device's memory (36 GB of an
+// MI355X's 288) is released after the call: one very long alignment must not
+// pin device memory for the rest of the session, but a batch the size of
+// C4-all's filter (16 GB of tie planes) keeps its buffer -- allocating it
+// afresh cost 0.4 s per call on a box's first processes (fresh VRAM pages)
+static size_t gotoh_keep_bytes()
+{
+    static const size_t keep = [] {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess || tot == 0) return (size_t)1 << 30;
+        return std::max((size_t)1 << 30, tot / 8);
+    }();
+    return keep;
+}
 
 // lev_text non-null: the filter's edit distances instead of the aligned
 // strings (out1 / out2 / cap unused): lev_dist[t] = the distance between
@@ -1409,7 +1420,7 @@ static int gotoh_batch_once(Ctx &c, int count, const char *const *s1, const char
         for (int k = 0; k < len; ++k) { out1[t][k] = t1[len - 1 - k]; out2[t][k] = t2[len - 1 - k]; }
         out1[t][len] = out2[t][len] = '\0';
     }
-    if (c.gotoh_cap > GOTOH_KEEP_BYTES) {
+    if (c.gotoh_cap > gotoh_keep_bytes()) {
         hipFree(c.gotoh_buf);
         c.gotoh_buf = nullptr;
         c.gotoh_cap = 0;

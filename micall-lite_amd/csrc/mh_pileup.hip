@@ -280,8 +280,10 @@ __device__ __forceinline__ int wave_max_all(int v)
 }
 
 // 6 waves per SIMD: at most 80 VGPRs, so 24 waves stay resident per CU
-// (pile_geometry); k_pileup<0> keeps 2 VGPRs in scratch (12 B per lane)
-template <int SRC>
+// (pile_geometry); k_pileup<0> keeps 2 VGPRs in scratch (12 B per lane).
+// SKIP: some references are not counted (mh_pileup_only); a separate
+// instance, so the full pileup pays no per-unit LDS read or SGPR for it
+template <int SRC, bool SKIP>
 __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -353,7 +355,7 @@ __global__ __launch_bounds__(1024, 6) void k_pileup(PileArgs A)
             continue;
         }
         // a reference this pileup does not count (mh_pileup_only)
-        if (__builtin_amdgcn_readfirstlane(wmap[2 * ref]) == -2) continue;
+        if (SKIP && __builtin_amdgcn_readfirstlane(wmap[2 * ref]) == -2) continue;
 
         // ---- apply_cigar: op offsets by a lane-parallel prefix scan, then
         // expand each mate into reference coordinates lane-parallel ----
@@ -954,7 +956,9 @@ static int pile_geometry(Ctx &c, int source, int64_t n_units, PileGeometry &g)
     auto hit = P.shapes.find(key);
     if (hit == P.shapes.end()) {
         if (!c.n_cu) MH_HIP(hipDeviceGetAttribute(&c.n_cu, hipDeviceAttributeMultiprocessorCount, c.device));
-        const void *kern = source == 0 ? (const void *)k_pileup<0> : (const void *)k_pileup<1>;
+        // the skipping instances have the same resources (the occupancy
+        // query of the full ones stands for them)
+        const void *kern = source == 0 ? (const void *)k_pileup<0, false> : (const void *)k_pileup<1, false>;
         MH_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, PU_LDS));
         int best_w = 0, best_wpb = 1, best_nb = 1;
         for (int wpb = 16; wpb >= 1; --wpb) {
@@ -1049,13 +1053,13 @@ int run_pileup(Ctx &c, int source, int q_cutoff)
         A.ins_scratch = P.ins_scratch;
         if (n_units > 0) {
             const int pk = prof_begin(c, "k_pileup");
-            if (source == 0) {
-                MH_HIP(hipFuncSetAttribute((const void *)k_pileup<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds));
-                hipLaunchKernelGGL(k_pileup<0>, dim3((unsigned)geo.blocks), dim3(64 * geo.wpb), geo.lds, s, A);
-            } else {
-                MH_HIP(hipFuncSetAttribute((const void *)k_pileup<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds));
-                hipLaunchKernelGGL(k_pileup<1>, dim3((unsigned)geo.blocks), dim3(64 * geo.wpb), geo.lds, s, A);
-            }
+            const bool skip = P.only.size() == (size_t)P.n_refs &&
+                              std::find(P.only.begin(), P.only.end(), (uint8_t)0) != P.only.end();
+            const void *kern = source == 0 ? (skip ? (const void *)k_pileup<0, true> : (const void *)k_pileup<0, false>)
+                                           : (skip ? (const void *)k_pileup<1, true> : (const void *)k_pileup<1, false>);
+            MH_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds));
+            void *kargs[] = {&A};
+            MH_HIP(hipLaunchKernel(kern, dim3((unsigned)geo.blocks), dim3(64 * geo.wpb), kargs, geo.lds, s));
             prof_end(c, pk);
             MH_HIP(hipGetLastError());
         }
