@@ -128,17 +128,28 @@ struct Rec {
     int32_t cig_off, maxm;   // cigar offset in the pool; longest M run
 };
 
+// slot id (read * MAXCAND + candidate) -> its index in the candidate-major
+// slot planes of stride `plane`
+__host__ __device__ inline int64_t slot_at(int32_t sid, int64_t plane)
+{
+    const uint32_t u = (uint32_t)sid;
+    return (int64_t)(u % MAXCAND) * plane + (int64_t)(u / MAXCAND);
+}
+
 struct MapState {
     int64_t n_reads = 0;
     int n_refs = 0;
     mh_params par{};
-    Cand *cand = nullptr;        // n_reads * MAXCAND
+    Cand *cand = nullptr;        // MAXCAND planes of cap_reads, like the slots
     int32_t *n_cand = nullptr;   // n_reads
     int32_t *yf = nullptr;       // n_reads
     int32_t *work = nullptr;     // slot ids to extend
     int32_t *rwork = nullptr;    // slot ids of mate-rescue candidates (one per pair at most)
-    SlotKey *skey = nullptr;     // n_reads * MAXCAND
-    SlotInfo *sinfo = nullptr;   // n_reads * MAXCAND
+    // the extension slots, candidate-major: slot id r * MAXCAND + c lives at
+    // c * cap_reads + r (slot_at), so a pass where most reads have one
+    // candidate reads one plane of keys and statistics, not every line
+    SlotKey *skey = nullptr;     // MAXCAND planes of cap_reads
+    SlotInfo *sinfo = nullptr;   // MAXCAND planes of cap_reads
     uint32_t *pool = nullptr;    // CIGAR ops of all slots
     int64_t pool_cap = 0;
     unsigned long long *pool_used = nullptr;  // words claimed (demand; may exceed pool_cap)

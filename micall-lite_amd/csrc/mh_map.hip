@@ -295,6 +295,7 @@ struct SeedArgs {
     int32_t *yf;
     int32_t *work;
     int32_t *counters;
+    int64_t plane;           // slot planes' stride (slot_at)
 };
 
 __device__ __forceinline__ bool cand_before(const Cand &x, const Cand &y)
@@ -420,7 +421,7 @@ __device__ int cluster_lanes(const SeedArgs &A, int64_t r, int lane, uint64_t v,
         }
     }
     if (lane == 0) {
-        for (int c = 0; c < nc; ++c) A.cand[r * MAXCAND + c] = best[c];
+        for (int c = 0; c < nc; ++c) A.cand[(int64_t)c * A.plane + r] = best[c];
         A.n_cand[r] = nc;
     }
     wave_sync();
@@ -609,7 +610,7 @@ __device__ int seed_read(const SeedArgs &A, int64_t r, const SeedPre &P, int lan
             }
             h0 = h1;
         }
-        for (int c = 0; c < nc; ++c) A.cand[r * MAXCAND + c] = best[c];
+        for (int c = 0; c < nc; ++c) A.cand[(int64_t)c * A.plane + r] = best[c];
         A.n_cand[r] = nc;
     }
     wave_sync();
@@ -685,6 +686,7 @@ struct DpArgs {
     int rows_pad;             // per-wave LDS row capacity (multiple of 8)
     int wave_lds;             // bytes of LDS per wave
     int oeI, exI, oeD, exD;
+    int64_t plane;            // slot planes' stride (slot_at)
 };
 
 __device__ __forceinline__ int mm_pen(int qchar)
@@ -1933,8 +1935,9 @@ __device__ void post_ext(const DpArgs &A, const XItem &it, const XView &X, int b
         }
     }
     if (lane == 0) {
-        A.skey[it.sid] = SlotKey{out.valid ? (out.ref << 1 | out.strand) : -1, out.pos, out.end, out.score};
-        A.sinfo[it.sid] = SlotInfo{out.cig_off, (uint32_t)out.xm | (uint32_t)out.xo << 16,
+        const int64_t at = slot_at(it.sid, A.plane);
+        A.skey[at] = SlotKey{out.valid ? (out.ref << 1 | out.strand) : -1, out.pos, out.end, out.score};
+        A.sinfo[at] = SlotInfo{out.cig_off, (uint32_t)out.xm | (uint32_t)out.xo << 16,
                                    (uint32_t)out.xg | (uint32_t)out.n_cigar << 16, out.maxm};
     }
     wave_sync();
@@ -2024,12 +2027,12 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
     };
     if (w < n_work) {
         const int sid = ldc(&A.work[w]);
-        cur = to_item(sid, ldc_cand(&A.cand[sid]), ldc(&A.R.len[sid / MAXCAND]),
+        cur = to_item(sid, ldc_cand(&A.cand[slot_at(sid, A.plane)]), ldc(&A.R.len[sid / MAXCAND]),
                       ldc(&A.R.off[sid / MAXCAND]));
     }
     if (at(1) < n_work) {
         sid1 = ldc(&A.work[at(1)]);
-        cd1 = ldc_cand(&A.cand[sid1]);
+        cd1 = ldc_cand(&A.cand[slot_at(sid1, A.plane)]);
         m1 = ldc(&A.R.len[sid1 / MAXCAND]);
         roff1 = ldc(&A.R.off[sid1 / MAXCAND]);
     }
@@ -2056,7 +2059,7 @@ __global__ __launch_bounds__(256) void k_dp(DpArgs A)
         if (at(1) < n_work) cur = to_item(sid1, cd1, m1, roff1);
         if (at(2) < n_work) {
             sid1 = sid2;
-            cd1 = ldc_cand(&A.cand[sid2]);
+            cd1 = ldc_cand(&A.cand[slot_at(sid2, A.plane)]);
             m1 = ldc(&A.R.len[sid2 / MAXCAND]);
             roff1 = ldc(&A.R.off[sid2 / MAXCAND]);
         }
@@ -2117,6 +2120,7 @@ struct RescueArgs {
     int32_t *work;        // rescue work list (slot ids)
     int32_t *counter;     // [0] rescue work items
     int maxins;
+    int64_t plane;        // slot planes' stride (slot_at)
 };
 
 // diagonals per staged reference window (the -X window of C2 has ~950)
@@ -2134,11 +2138,11 @@ __device__ __forceinline__ uint32_t compact16(uint32_t x)
     return (x | (x >> 8)) & 0x0000ffffu;
 }
 
-__device__ __forceinline__ int best_slot(const SlotKey *sl, int n)
+__device__ __forceinline__ int best_slot(const SlotKey *skey, int64_t r, int n, int64_t plane)
 {
     int best = -1, bs = 0;
     for (int c = 0; c < n; ++c) {
-        const SlotKey k = sl[c];
+        const SlotKey k = skey[(int64_t)c * plane + r];
         if (k.rs >= 0 && (best < 0 || k.score > bs)) { best = c; bs = k.score; }
     }
     return best;
@@ -2170,12 +2174,12 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
         int64_t t_off = 0, r_off = 0;   // the mate's and the reference's (loaded lane-parallel here)
         if (u < units) {
             const int64_t r1 = 2 * u, r2 = r1 + 1;
-            const int b1 = best_slot(A.skey + r1 * MAXCAND, A.n_cand[r1]);
-            const int b2 = best_slot(A.skey + r2 * MAXCAND, A.n_cand[r2]);
+            const int b1 = best_slot(A.skey, r1, A.n_cand[r1], A.plane);
+            const int b2 = best_slot(A.skey, r2, A.n_cand[r2], A.plane);
             if ((b1 >= 0) != (b2 >= 0)) {
                 const int64_t an = b1 >= 0 ? r1 : r2, tg = b1 >= 0 ? r2 : r1;
                 if (A.yf[tg] == 0 && A.R.len[tg] > 0) {
-                    const SlotKey s = A.skey[an * MAXCAND + (b1 >= 0 ? b1 : b2)];
+                    const SlotKey s = A.skey[(int64_t)(b1 >= 0 ? b1 : b2) * A.plane + an];
                     need = 1;
                     tgt_mate = b1 >= 0 ? 1 : 0;
                     a_ref = s.rs >> 1; a_strand = s.rs & 1; a_pos = s.pos; a_end = s.end;
@@ -2323,7 +2327,7 @@ __global__ __launch_bounds__(256) void k_rescue(RescueArgs A)
             const int mmax = wave_max(bestM);
             const int dsel = wave_min(bestM == mmax ? bestd : INT32_MAX);
             if (lane == 0) {
-                A.cand[tg * MAXCAND] = Cand{s, ref, dsel, 0};
+                A.cand[tg] = Cand{s, ref, dsel, 0};   // candidate 0: plane 0
                 A.n_cand[tg] = 1;
                 sh_items[wv][n_items] = (int32_t)(tg * MAXCAND);
             }
@@ -2390,6 +2394,7 @@ struct PairArgs {
     int local;
     int maxins;
     int paired;
+    int64_t plane;       // slot planes' stride (slot_at)
 };
 
 // A read's candidates: its keys in registers (one 16-B load each, the
@@ -2397,7 +2402,7 @@ struct PairArgs {
 // n_cand as rs = -1.
 struct MateView {
     SlotKey k[MAXCAND];
-    int64_t base;    // slot id of candidate 0
+    int64_t base;    // the read (candidate c at c * plane + base)
     int best;
     SlotKey bk;      // k[best] (copied when chosen: a run-time index into k would
                      // put the view in scratch memory)
@@ -2405,13 +2410,13 @@ struct MateView {
 
 __device__ __forceinline__ void load_mate(const PairArgs &A, int64_t r, MateView &mv)
 {
-    mv.base = r * MAXCAND;
+    mv.base = r;
     const int n = A.n_cand[r];
     mv.best = -1;
     mv.bk = SlotKey{-1, 0, 0, 0};
 #pragma unroll
     for (int c = 0; c < MAXCAND; ++c) {
-        mv.k[c] = c < n ? A.skey[mv.base + c] : SlotKey{-1, 0, 0, 0};
+        mv.k[c] = c < n ? A.skey[(int64_t)c * A.plane + r] : SlotKey{-1, 0, 0, 0};
         if (mv.k[c].rs >= 0 && (mv.best < 0 || mv.k[c].score > mv.bk.score)) { mv.best = c; mv.bk = mv.k[c]; }
     }
 }
@@ -2438,7 +2443,7 @@ __device__ __forceinline__ void fill_aligned(const PairArgs &A, Rec &o, const Ma
     }
     o.secbest = has ? sec : I32MIN;
     o.mapq = mapq_v2(A.local, A.local ? 2 * m : 0, A.len_tab[(MAXLEN + 1) + m], a.score, has, sec);
-    const SlotInfo f = A.sinfo[mv.base + chosen];
+    const SlotInfo f = A.sinfo[(int64_t)chosen * A.plane + mv.base];
     o.xm = (int)(f.xm_xo & 0xffffu); o.xo = (int)(f.xm_xo >> 16);
     o.xg = (int)(f.xg_nc & 0xffffu); o.nm = o.xm + o.xg;
     o.n_cigar = (int)(f.xg_nc >> 16);
@@ -2855,7 +2860,7 @@ int run_map(Ctx &c, const mh_params &par)
         // seeds, candidates and the work list; run again by a retry, since
         // k_rescue replaces the candidates of the mates it rescues
         auto launch_seed = [&]() -> int {
-            SeedArgs sa{c.reads, c.index, par.mode, c.len_tab, M.cand, M.n_cand, M.yf, M.work, M.counters};
+            SeedArgs sa{c.reads, c.index, par.mode, c.len_tab, M.cand, M.n_cand, M.yf, M.work, M.counters, M.cap_reads};
             int64_t blocks = ((n + SEED_CHUNK - 1) / SEED_CHUNK + 3) / 4;
             if (blocks > 1 << 16) blocks = 1 << 16;
             const int pk = prof_begin(c, "k_seed");
@@ -2883,7 +2888,7 @@ int run_map(Ctx &c, const mh_params &par)
             DpArgs da{c.reads, c.index, c.len_tab, M.cand, work, count, M.skey, M.sinfo, M.pool,
                       M.pool_used, M.counters + 1, queue, M.pool_cap, rows_pad, wave_lds,
                       par.rfg_open + par.rfg_ext, par.rfg_ext, par.rdg_open + par.rdg_ext,
-                      par.rdg_ext};
+                      par.rdg_ext, M.cap_reads};
             const int round = rows_pad <= 256 ? 256 : rows_pad <= 320 ? 320 : 0;
             const void *kf =
                 par.mode == MH_LOCAL
@@ -2925,7 +2930,7 @@ int run_map(Ctx &c, const mh_params &par)
         };
         const int64_t units = c.reads.paired ? n / 2 : n;
         PairArgs pa{c.reads, c.len_tab, M.skey, M.sinfo, M.n_cand, M.yf, M.pool, M.rec, M.ref_stats,
-                    M.n_refs, par.mode == MH_LOCAL, par.maxins, c.reads.paired};
+                    M.n_refs, par.mode == MH_LOCAL, par.maxins, c.reads.paired, M.cap_reads};
         int64_t pblocks = (units + 255) / 256;
         if (pblocks > 1 << 16) pblocks = 1 << 16;
         if (pblocks < 1) pblocks = 1;
@@ -2942,7 +2947,7 @@ int run_map(Ctx &c, const mh_params &par)
             if (int st = launch_dp(M.work, M.counters, M.counters + 5, n * 2, "k_dp")) return st;
             if (c.reads.paired && units > 0) {
                 RescueArgs ra{c.reads, c.index, M.skey, M.n_cand, M.yf, M.cand, M.rwork,
-                              M.counters + 4, par.maxins};
+                              M.counters + 4, par.maxins, M.cap_reads};
                 int64_t rblocks = (units + 255) / 256;
                 if (rblocks > 4096) rblocks = 4096;
                 const int pr = prof_begin(c, "k_rescue");
