@@ -2,7 +2,7 @@
 # the round's last build: the whole GPU suite, smoke, the default bench line
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r06/final
+O=$R/gpurun_out/r06/${OUTNAME:-final}
 mkdir -p $O
 cd $R
 timeout -k 10 1200 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/gpu_suite.log 2>&1

@@ -3,7 +3,7 @@
 # parity leg; its whole-input check is profiles/r06/c3/parity_full.json)
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r06/refresh
+O=$R/gpurun_out/r06/${OUTNAME:-refresh}
 mkdir -p $O
 cd $R
 timeout -k 10 600 python3 bench.py --genomes hiv --pairs 5000000 --steps 3 --warmup 1 --no-e2e > $O/c4.json 2> $O/c4.err
