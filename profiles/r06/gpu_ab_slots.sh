@@ -8,7 +8,7 @@ O=gpurun_out/r06/${ABNAME:-abslots}
 mkdir -p $O
 V=$PWD/_v6/base/libmicall_hip.so
 for r in 1 2 3; do
-  for which in base slots; do
+  for which in base ${BNAME:-slots}; do
     if [ $which = base ]; then L=$V; else L=$PWD/micall-lite_amd/micall_amd/libmicall_hip.so; fi
     timeout -k 10 300 env MICALL_HIP_LIB=$L python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e --no-parity \
         > $O/$which.$r.json 2>/dev/null || exit 1
