@@ -386,6 +386,21 @@ __device__ __forceinline__ uint64_t bitonic_lanes(uint64_t v, int lane, int N)
 __device__ int cluster_lanes(const SeedArgs &A, int64_t r, int lane, uint64_t v, int total,
                              Cand *best)
 {
+    // every hit the same (strand, reference, diagonal) -- a read without an
+    // indel against a reference it maps to once: one cluster of one run,
+    // the candidate the sort and the walk below would give
+    {
+        const uint64_t v0 = readlane64(v, 0);
+        if (__builtin_amdgcn_ballot_w64(lane < total && v != v0) == 0) {
+            if (lane == 0) {
+                A.cand[r] = Cand{(int)(v0 >> 62), (int)((v0 >> 32) & 0x3fffffff),
+                                 (int)(uint32_t)v0 - (1 << 30), total};   // candidate 0: plane 0
+                A.n_cand[r] = 1;
+            }
+            wave_sync();
+            return 1;
+        }
+    }
     int N = 2;
     while (N < total) N <<= 1;
     v = bitonic_lanes(v, lane, N);
