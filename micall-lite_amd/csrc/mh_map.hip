@@ -403,7 +403,13 @@ __device__ int cluster_lanes(const SeedArgs &A, int64_t r, int lane, uint64_t v,
     }
     int N = 2;
     while (N < total) N <<= 1;
-    v = bitonic_lanes(v, lane, N);
+    {
+        // hits arrive in seed order, already sorted when the read's diagonal
+        // only grows along it (a deletion): the sort is then the identity
+        const uint64_t qv = ((uint64_t)(uint32_t)dpp<DPP_WAVE_SHR1>(0, (int)(v >> 32)) << 32) |
+                            (uint32_t)dpp<DPP_WAVE_SHR1>(0, (int)(uint32_t)v);   // lane - 1's hit
+        if (__builtin_amdgcn_ballot_w64(lane > 0 && lane < total && v < qv) != 0) v = bitonic_lanes(v, lane, N);
+    }
     const uint64_t pv = ((uint64_t)(uint32_t)dpp<DPP_WAVE_SHR1>(0, (int)(v >> 32)) << 32) |
                         (uint32_t)dpp<DPP_WAVE_SHR1>(0, (int)(uint32_t)v);   // lane - 1's hit
     const bool valid = lane < total;
